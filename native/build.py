@@ -1,0 +1,177 @@
+"""Builds every native component of the framework in-tree.
+
+Targets (outputs land in ``gpushare_scheduler_extender_amd/_native/``):
+
+* ``engine``  – C++17 ledger/JSON engine + pybind11 module ``_engine``.
+* ``mxdev``   – C++17 amdsmi device library + pybind11 module ``_mxdev``
+                (amdsmi is dlopen'ed with RTLD_DEEPBIND at run time so the
+                module also loads on hosts without a GPU and never binds to the
+                ROCm-SMI copy bundled inside the torch wheel).
+* ``kernels`` – HIP/CDNA4 kernels for gfx950 (``libgsx_kernels.so``): CU probe,
+                HBM touch/verify, bf16 MFMA GEMM workload, CU-masked streams.
+* ``tools``   – standalone HIP executables (``gsx-cuprobe``).
+* ``asan``    – host-only sanitizer build of the engine unit test.
+
+Usage: ``python native/build.py [targets...] [--force] [-v]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+NATIVE = ROOT / "native"
+OUT = ROOT / "gpushare_scheduler_extender_amd" / "_native"
+OBJ = ROOT / "build" / "obj"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("GSX_OFFLOAD_ARCH", "gfx950")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-fvisibility=hidden"]
+
+
+def _pybind_includes() -> list[str]:
+    import pybind11  # noqa: PLC0415
+
+    return ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
+
+
+def _newer(out: Path, deps: list[Path]) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print("+", " ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"native build failed: {' '.join(cmd[:3])} ... (exit {r.returncode})")
+
+
+def _compile_objs(srcs: list[Path], compiler: str, flags: list[str], tag: str, force: bool, verbose: bool,
+                  headers: list[Path]) -> list[Path]:
+    OBJ.mkdir(parents=True, exist_ok=True)
+    jobs = []
+    objs = []
+    for s in srcs:
+        o = OBJ / f"{tag}_{s.stem}.o"
+        objs.append(o)
+        if force or _newer(o, [s, *headers]):
+            jobs.append([compiler, *flags, "-c", str(s), "-o", str(o)])
+    if jobs:
+        with cf.ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
+            list(ex.map(lambda c: _run(c, verbose), jobs))
+    return objs
+
+
+def build_engine(force: bool = False, verbose: bool = False) -> Path:
+    src = NATIVE / "engine"
+    srcs = sorted(src.glob("*.cc"))
+    srcs = [s for s in srcs if s.name != "engine_test.cc"]
+    headers = sorted(src.glob("*.h"))
+    out = OUT / f"_engine{EXT}"
+    flags = [*CXXFLAGS, *_pybind_includes(), "-I" + str(src)]
+    objs = _compile_objs(srcs, "g++", flags, "engine", force, verbose, headers)
+    if force or _newer(out, objs):
+        OUT.mkdir(parents=True, exist_ok=True)
+        _run(["g++", "-shared", "-o", str(out), *map(str, objs)], verbose)
+    return out
+
+
+def build_mxdev(force: bool = False, verbose: bool = False) -> Path:
+    src = NATIVE / "mxdev"
+    srcs = sorted(src.glob("*.cc"))
+    srcs = [s for s in srcs if not s.name.endswith("_test.cc")]
+    headers = sorted(src.glob("*.h"))
+    out = OUT / f"_mxdev{EXT}"
+    flags = [*CXXFLAGS, *_pybind_includes(), "-I" + str(src), "-I" + str(ROCM / "include"),
+             "-I" + str(NATIVE / "engine")]
+    objs = _compile_objs(srcs, "g++", flags, "mxdev", force, verbose, headers)
+    eng = [OBJ / "engine_json.o"]
+    if force or _newer(out, objs + eng):
+        OUT.mkdir(parents=True, exist_ok=True)
+        _run(["g++", "-shared", "-o", str(out), *map(str, objs), *map(str, eng), "-ldl"], verbose)
+    return out
+
+
+def _hipcc() -> str:
+    h = ROCM / "bin" / "hipcc"
+    return str(h) if h.exists() else (shutil.which("hipcc") or "hipcc")
+
+
+def build_kernels(force: bool = False, verbose: bool = False) -> Path:
+    src = NATIVE / "kernels"
+    srcs = sorted(src.glob("*.hip"))
+    srcs = [s for s in srcs if not s.stem.startswith("tool_")]
+    headers = sorted(src.glob("*.h"))
+    out = OUT / "libgsx_kernels.so"
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I" + str(src),
+             "-munsafe-fp-atomics"]
+    objs = _compile_objs(srcs, _hipcc(), flags, "kern", force, verbose, headers)
+    if force or _newer(out, objs):
+        OUT.mkdir(parents=True, exist_ok=True)
+        _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out), *map(str, objs)], verbose)
+    return out
+
+
+def build_tools(force: bool = False, verbose: bool = False) -> list[Path]:
+    src = NATIVE / "kernels"
+    outs = []
+    for s in sorted(src.glob("tool_*.hip")):
+        out = OUT / ("gsx-" + s.stem[len("tool_"):])
+        deps = [s, *sorted(src.glob("*.h")), *sorted(src.glob("*.hip"))]
+        if force or _newer(out, deps):
+            OUT.mkdir(parents=True, exist_ok=True)
+            others = [str(x) for x in sorted(src.glob("*.hip")) if not x.stem.startswith("tool_")]
+            _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-I" + str(src), str(s), *others,
+                  "-o", str(out)], verbose)
+        outs.append(out)
+    return outs
+
+
+def build_asan(force: bool = False, verbose: bool = False) -> Path:
+    """Host-only ASan/UBSan build of the engine's C++ unit test."""
+    src = NATIVE / "engine"
+    out = ROOT / "build" / "engine_test_asan"
+    srcs = [s for s in sorted(src.glob("*.cc")) if s.name != "bindings.cc"]
+    if force or _newer(out, srcs + sorted(src.glob("*.h"))):
+        out.parent.mkdir(parents=True, exist_ok=True)
+        _run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+              "-I" + str(src), *map(str, srcs), "-o", str(out)], verbose)
+    return out
+
+
+TARGETS = {
+    "engine": build_engine,
+    "mxdev": build_mxdev,
+    "kernels": build_kernels,
+    "tools": build_tools,
+    "asan": build_asan,
+}
+DEFAULT = ["engine", "mxdev", "kernels", "tools"]
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("targets", nargs="*", default=DEFAULT)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    for t in a.targets:
+        r = TARGETS[t](force=a.force, verbose=a.verbose)
+        print(f"[native] {t}: {r}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,298 @@
+// pybind11 bindings for the native ledger engine (module `_engine`).
+//
+// The Python control plane (asyncio I/O) owns no scheduling state: every
+// filter/bind decision and all accounting happen here, behind one mutex.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "ledger.h"
+#include "quantity.h"
+
+namespace py = pybind11;
+using namespace gsx;
+
+namespace {
+
+Profile profile_from(const py::dict& d) {
+  Profile p;
+  auto get = [&](const char* k, std::string* dst) {
+    if (d.contains(k)) *dst = d[k].cast<std::string>();
+  };
+  get("resource", &p.resource);
+  get("count", &p.count);
+  get("annotation_idx", &p.a_idx);
+  get("annotation_pod", &p.a_pod);
+  get("annotation_dev", &p.a_dev);
+  get("annotation_assigned", &p.a_assigned);
+  get("annotation_assume_time", &p.a_assume);
+  get("annotation_node_devices", &p.a_node_devs);
+  return p;
+}
+
+std::string_view view_of(const py::bytes& b) {
+  char* buf;
+  Py_ssize_t len;
+  if (PyBytes_AsStringAndSize(b.ptr(), &buf, &len) != 0) throw py::error_already_set();
+  return std::string_view(buf, static_cast<size_t>(len));
+}
+
+bool parse_pod_bytes(const py::bytes& b, const Profile& p, PodView* out, std::string* err) {
+  json::Doc d;
+  if (!d.parse(view_of(b), err)) return false;
+  // accept either a bare pod or a watch event {"type":..,"object":pod}
+  uint32_t root = 0;
+  int64_t obj = d.find(0, "object");
+  if (obj >= 0 && d.find(0, "type") >= 0) root = static_cast<uint32_t>(obj);
+  if (!parse_pod(d, root, p, out)) {
+    *err = "not a pod object";
+    return false;
+  }
+  return true;
+}
+
+bool parse_node_bytes(const py::bytes& b, const Profile& p, NodeView* out, std::string* err) {
+  json::Doc d;
+  if (!d.parse(view_of(b), err)) return false;
+  uint32_t root = 0;
+  int64_t obj = d.find(0, "object");
+  if (obj >= 0 && d.find(0, "type") >= 0) root = static_cast<uint32_t>(obj);
+  if (!parse_node(d, root, p, out)) {
+    *err = "not a node object";
+    return false;
+  }
+  return true;
+}
+
+class Engine {
+ public:
+  explicit Engine(const py::dict& profile) : l_(profile_from(profile)) {}
+
+  py::dict profile() const {
+    const Profile& p = l_.profile();
+    py::dict d;
+    d["resource"] = p.resource;
+    d["count"] = p.count;
+    d["annotation_idx"] = p.a_idx;
+    d["annotation_pod"] = p.a_pod;
+    d["annotation_dev"] = p.a_dev;
+    d["annotation_assigned"] = p.a_assigned;
+    d["annotation_assume_time"] = p.a_assume;
+    d["annotation_node_devices"] = p.a_node_devs;
+    return d;
+  }
+
+  bool upsert_node(const std::string& name, int64_t total, int64_t count, std::vector<int64_t> devs,
+                   const std::string& address) {
+    NodeView nv;
+    nv.name = name;
+    nv.total = total;
+    nv.count = count;
+    nv.dev_totals = std::move(devs);
+    nv.address = address;
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.upsert_node(nv);
+  }
+
+  py::tuple upsert_node_json(const py::bytes& b) {
+    NodeView nv;
+    std::string err;
+    if (!parse_node_bytes(b, l_.profile(), &nv, &err)) throw py::value_error(err);
+    bool rebuilt;
+    {
+      std::lock_guard<std::mutex> g(l_.mu());
+      rebuilt = l_.upsert_node(nv);
+    }
+    return py::make_tuple(nv.name, rebuilt);
+  }
+
+  bool remove_node(const std::string& name) {
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.remove_node(name);
+  }
+
+  bool has_node(const std::string& name) {
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.has_node(name);
+  }
+
+  py::tuple node_info(const std::string& name) {
+    std::lock_guard<std::mutex> g(l_.mu());
+    const NodeState* n = l_.node(name);
+    if (!n) return py::make_tuple();
+    return py::make_tuple(n->total, n->count, n->address);
+  }
+
+  int upsert_pod(const PodView& v) {
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.upsert_pod(v);
+  }
+
+  bool remove_pod(const std::string& uid) {
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.remove_pod(uid);
+  }
+
+  bool known(const std::string& uid) {
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.known(uid);
+  }
+
+  int check(const std::string& node, int64_t req) {
+    std::lock_guard<std::mutex> g(l_.mu());
+    return static_cast<int>(l_.check(node, req));
+  }
+
+  py::bytes filter(const py::bytes& body) {
+    std::string_view v = view_of(body);
+    std::string out;
+    {
+      py::gil_scoped_release rel;
+      std::lock_guard<std::mutex> g(l_.mu());
+      out = filter_body(l_, v);
+    }
+    return py::bytes(out);
+  }
+
+  py::tuple assume(const std::string& uid, const std::string& ns, const std::string& name,
+                   const std::string& node, int64_t req) {
+    int64_t dev_total = -1;
+    std::lock_guard<std::mutex> g(l_.mu());
+    int64_t dev = l_.assume(uid, ns, name, node, req, &dev_total);
+    return py::make_tuple(dev, dev_total);
+  }
+
+  void finish_bind(const std::string& uid, bool ok, double ttl) {
+    std::lock_guard<std::mutex> g(l_.mu());
+    l_.finish_bind(uid, ok, ttl);
+  }
+
+  int gc() {
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.gc();
+  }
+
+  py::tuple inspect(const std::string& node) {
+    bool found;
+    std::string s;
+    {
+      std::lock_guard<std::mutex> g(l_.mu());
+      s = l_.inspect_json(node, &found);
+    }
+    return py::make_tuple(py::bytes(s), found);
+  }
+
+  std::vector<std::pair<int64_t, int64_t>> node_devices(const std::string& node) {
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.node_devices(node);
+  }
+
+  std::vector<std::string> node_names() {
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.node_names();
+  }
+
+  py::dict stats() {
+    Stats s;
+    size_t pods;
+    {
+      std::lock_guard<std::mutex> g(l_.mu());
+      s = l_.stats();
+      pods = l_.pod_count();
+    }
+    py::dict d;
+    d["filter_calls"] = s.filter_calls;
+    d["filter_nodes_ok"] = s.filter_nodes_ok;
+    d["filter_nodes_failed"] = s.filter_nodes_failed;
+    d["assume_ok"] = s.assume_ok;
+    d["assume_fail"] = s.assume_fail;
+    d["bind_ok"] = s.bind_ok;
+    d["bind_fail"] = s.bind_fail;
+    d["expired"] = s.expired;
+    d["overcommit_events"] = s.overcommit_events;
+    d["pod_upserts"] = s.pod_upserts;
+    d["pod_removes"] = s.pod_removes;
+    d["pods"] = pods;
+    return d;
+  }
+
+  PodView parse_pod(const py::bytes& b) {
+    PodView v;
+    std::string err;
+    if (!parse_pod_bytes(b, l_.profile(), &v, &err)) throw py::value_error(err);
+    return v;
+  }
+
+ private:
+  Ledger l_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_engine, m) {
+  m.doc() = "gpushare MI355X native ledger engine";
+
+  py::class_<PodView>(m, "PodView")
+      .def(py::init<>())
+      .def_readwrite("uid", &PodView::uid)
+      .def_readwrite("name", &PodView::name)
+      .def_readwrite("namespace", &PodView::ns)
+      .def_readwrite("node", &PodView::node)
+      .def_readwrite("phase", &PodView::phase)
+      .def_readwrite("resource_version", &PodView::rv)
+      .def_readwrite("deleting", &PodView::deleting)
+      .def_readwrite("request", &PodView::request)
+      .def_readwrite("dev_idx", &PodView::dev_idx)
+      .def_readwrite("annot_mem", &PodView::annot_mem)
+      .def_readwrite("has_annot_mem", &PodView::has_annot_mem)
+      .def_readwrite("annot_dev_total", &PodView::annot_dev_total)
+      .def_readwrite("assigned", &PodView::assigned)
+      .def_readwrite("assume_time", &PodView::assume_time)
+      .def_readwrite("cu_mask", &PodView::cu_mask)
+      .def_property_readonly("terminal", &PodView::terminal)
+      .def_property_readonly("complete", &PodView::complete)
+      .def_property_readonly("assigned_non_terminated", &PodView::assigned_non_terminated)
+      .def("__repr__", [](const PodView& v) {
+        return "<PodView " + v.ns + "/" + v.name + " uid=" + v.uid + " node=" + v.node +
+               " req=" + std::to_string(v.request) + " idx=" + std::to_string(v.dev_idx) + ">";
+      });
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<const py::dict&>(), py::arg("profile") = py::dict())
+      .def("profile", &Engine::profile)
+      .def("upsert_node", &Engine::upsert_node, py::arg("name"), py::arg("total"), py::arg("count"),
+           py::arg("dev_totals") = std::vector<int64_t>(), py::arg("address") = std::string())
+      .def("upsert_node_json", &Engine::upsert_node_json)
+      .def("remove_node", &Engine::remove_node)
+      .def("has_node", &Engine::has_node)
+      .def("node_info", &Engine::node_info)
+      .def("upsert_pod", &Engine::upsert_pod)
+      .def("remove_pod", &Engine::remove_pod)
+      .def("known", &Engine::known)
+      .def("check", &Engine::check)
+      .def("filter", &Engine::filter)
+      .def("assume", &Engine::assume)
+      .def("finish_bind", &Engine::finish_bind, py::arg("uid"), py::arg("ok"), py::arg("ttl") = 30.0)
+      .def("gc", &Engine::gc)
+      .def("inspect", &Engine::inspect, py::arg("node") = std::string())
+      .def("node_devices", &Engine::node_devices)
+      .def("node_names", &Engine::node_names)
+      .def("stats", &Engine::stats)
+      .def("parse_pod", &Engine::parse_pod);
+
+  m.def("parse_quantity", [](const std::string& s) {
+    int64_t v;
+    if (!parse_quantity(s, &v)) throw py::value_error("quantities must match the regular expression");
+    return v;
+  });
+  m.def("json_quote", [](const std::string& s) {
+    std::string o;
+    json::append_quoted(&o, s);
+    return o;
+  });
+  m.def("json_validate", [](const py::bytes& b) {
+    json::Doc d;
+    std::string err;
+    bool ok = d.parse(view_of(b), &err);
+    return py::make_tuple(ok, err, static_cast<int64_t>(d.size()));
+  });
+}

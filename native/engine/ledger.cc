@@ -1,0 +1,489 @@
+#include "ledger.h"
+
+#include <algorithm>
+#include <cstdio>
+
+namespace gsx {
+
+// ---------------------------------------------------------------- accounting
+
+void Ledger::account(PodRec& r) {
+  if (r.accounted) return;
+  if (r.dev < 0 || r.terminal) return;
+  auto it = nodes_.find(r.node);
+  if (it == nodes_.end()) return;
+  NodeState& n = it->second;
+  if (r.dev >= static_cast<int64_t>(n.devs.size())) return;
+  DevState& d = n.devs[static_cast<size_t>(r.dev)];
+  d.used += r.mem;
+  d.npods += 1;
+  if (d.used > d.total) stats_.overcommit_events++;
+  r.accounted = true;
+}
+
+void Ledger::unaccount(PodRec& r) {
+  if (!r.accounted) return;
+  auto it = nodes_.find(r.node);
+  r.accounted = false;
+  if (it == nodes_.end()) return;
+  NodeState& n = it->second;
+  if (r.dev < 0 || r.dev >= static_cast<int64_t>(n.devs.size())) return;
+  DevState& d = n.devs[static_cast<size_t>(r.dev)];
+  d.used -= r.mem;
+  d.npods -= 1;
+}
+
+void Ledger::rebuild(NodeState& n) {
+  // nodeinfo.go:29-45: count devices, total/count each (homogeneous); the
+  // per-device annotation, when it matches the count, is exact.
+  n.devs.assign(static_cast<size_t>(n.count > 0 ? n.count : 0), DevState{});
+  bool use_override = static_cast<int64_t>(n.dev_totals_override.size()) == n.count && n.count > 0;
+  for (int64_t i = 0; i < n.count; ++i) {
+    n.devs[static_cast<size_t>(i)].total =
+        use_override ? n.dev_totals_override[static_cast<size_t>(i)] : (n.total / n.count);
+  }
+  for (const auto& uid : n.pods) {
+    auto pit = pods_.find(uid);
+    if (pit == pods_.end()) continue;
+    pit->second.accounted = false;
+    account(pit->second);
+  }
+}
+
+bool Ledger::upsert_node(const NodeView& nv) {
+  auto it = nodes_.find(nv.name);
+  if (it == nodes_.end()) {
+    NodeState n;
+    n.name = nv.name;
+    n.address = nv.address;
+    n.total = nv.total;
+    n.count = nv.count;
+    n.dev_totals_override = nv.dev_totals;
+    // adopt pods that arrived before their node
+    for (auto& kv : pods_) {
+      if (kv.second.node == nv.name) n.pods.insert(kv.first);
+    }
+    auto res = nodes_.emplace(nv.name, std::move(n));
+    rebuild(res.first->second);
+    return true;
+  }
+  NodeState& n = it->second;
+  n.address = nv.address;
+  if (n.total == nv.total && n.count == nv.count && n.dev_totals_override == nv.dev_totals) return false;
+  n.total = nv.total;
+  n.count = nv.count;
+  n.dev_totals_override = nv.dev_totals;
+  rebuild(n);
+  return true;
+}
+
+bool Ledger::remove_node(const std::string& name) {
+  auto it = nodes_.find(name);
+  if (it == nodes_.end()) return false;
+  for (const auto& uid : it->second.pods) {
+    auto pit = pods_.find(uid);
+    if (pit != pods_.end()) pit->second.accounted = false;
+  }
+  nodes_.erase(it);
+  return true;
+}
+
+bool Ledger::has_node(const std::string& name) const { return nodes_.count(name) != 0; }
+
+// ---------------------------------------------------------------- pods
+
+void Ledger::erase_pod(std::unordered_map<std::string, PodRec>::iterator it) {
+  unaccount(it->second);
+  auto nit = nodes_.find(it->second.node);
+  if (nit != nodes_.end()) nit->second.pods.erase(it->first);
+  pods_.erase(it);
+}
+
+int Ledger::upsert_pod(const PodView& v) {
+  stats_.pod_upserts++;
+  auto it = pods_.find(v.uid);
+  if (v.node.empty()) {
+    // cache.go:91-95 skips unscheduled pods.  An assumed reservation stays:
+    // this is the annotation write racing ahead of the Binding.
+    if (it != pods_.end() && it->second.assumed) return it->second.dev >= 0 ? 1 : 0;
+    return 0;
+  }
+  if (it != pods_.end()) {
+    PodRec& r = it->second;
+    unaccount(r);
+    if (r.node != v.node) {
+      auto oit = nodes_.find(r.node);
+      if (oit != nodes_.end()) oit->second.pods.erase(r.uid);
+      r.node = v.node;
+      auto nit = nodes_.find(r.node);
+      if (nit != nodes_.end()) nit->second.pods.insert(r.uid);
+    }
+    r.ns = v.ns;
+    r.name = v.name;
+    r.request = v.request;
+    r.terminal = v.terminal();
+    r.deleting = v.deleting;
+    if (v.dev_idx >= 0) {
+      r.dev = v.dev_idx;
+      r.mem = v.annot_mem;
+      r.assumed = false;  // observed with annotations: reservation confirmed
+    } else if (!r.assumed) {
+      r.dev = -1;
+    }
+    account(r);
+    return r.dev >= 0 ? 1 : 0;
+  }
+  if (v.dev_idx < 0) return 0;  // nodeinfo.go:89-110 only adds pods with an idx
+  PodRec r;
+  r.uid = v.uid;
+  r.ns = v.ns;
+  r.name = v.name;
+  r.node = v.node;
+  r.dev = v.dev_idx;
+  r.mem = v.annot_mem;
+  r.request = v.request;
+  r.terminal = v.terminal();
+  r.deleting = v.deleting;
+  auto res = pods_.emplace(v.uid, std::move(r));
+  auto nit = nodes_.find(v.node);
+  if (nit != nodes_.end()) nit->second.pods.insert(v.uid);
+  account(res.first->second);
+  return 1;
+}
+
+bool Ledger::remove_pod(const std::string& uid) {
+  auto it = pods_.find(uid);
+  if (it == pods_.end()) return false;
+  stats_.pod_removes++;
+  erase_pod(it);
+  return true;
+}
+
+bool Ledger::known(const std::string& uid) const { return pods_.count(uid) != 0; }
+
+// ---------------------------------------------------------------- verbs
+
+Check Ledger::check(const std::string& node, int64_t req) const {
+  auto it = nodes_.find(node);
+  if (it == nodes_.end()) return Check::NodeNotFound;
+  const NodeState& n = it->second;
+  if (!n.gpushare()) return Check::NotGPUShare;
+  for (const DevState& d : n.devs) {
+    if (d.total - d.used >= req) return Check::Ok;
+  }
+  return Check::Insufficient;
+}
+
+int64_t Ledger::assume(const std::string& uid, const std::string& ns, const std::string& name,
+                       const std::string& node, int64_t req, int64_t* dev_total) {
+  auto nit = nodes_.find(node);
+  if (nit == nodes_.end()) {
+    stats_.assume_fail++;
+    return -2;
+  }
+  NodeState& n = nit->second;
+  if (!n.gpushare()) {
+    stats_.assume_fail++;
+    return -3;
+  }
+  auto pit = pods_.find(uid);
+  if (pit != pods_.end()) {
+    PodRec& r = pit->second;
+    if (r.assumed && !r.bound) {
+      stats_.assume_fail++;
+      return -4;
+    }
+    if (r.node == node && r.dev >= 0 && r.dev < static_cast<int64_t>(n.devs.size()) && !r.terminal) {
+      // idempotent re-bind of an already placed pod: keep its record as is
+      if (dev_total) *dev_total = n.devs[static_cast<size_t>(r.dev)].total;
+      stats_.assume_ok++;
+      return r.dev;
+    }
+    erase_pod(pit);
+  }
+  // best fit: smallest free >= req, lowest index on ties (nodeinfo.go:219-232)
+  int64_t cand = -1;
+  int64_t cand_free = 0;
+  for (size_t i = 0; i < n.devs.size(); ++i) {
+    int64_t free = n.devs[i].total - n.devs[i].used;
+    if (free >= req && (cand < 0 || free < cand_free)) {
+      cand = static_cast<int64_t>(i);
+      cand_free = free;
+    }
+  }
+  if (cand < 0 || req <= 0) {
+    // nodeinfo.go:218: a pod with no gpu-mem request is never placed
+    stats_.assume_fail++;
+    return -1;
+  }
+  PodRec r;
+  r.uid = uid;
+  r.ns = ns;
+  r.name = name;
+  r.node = node;
+  r.dev = cand;
+  r.mem = req;
+  r.request = req;
+  r.assumed = true;
+  r.assumed_at = now_s();
+  auto res = pods_.emplace(uid, std::move(r));
+  n.pods.insert(uid);
+  account(res.first->second);
+  if (dev_total) *dev_total = n.devs[static_cast<size_t>(cand)].total;
+  stats_.assume_ok++;
+  return cand;
+}
+
+void Ledger::finish_bind(const std::string& uid, bool ok, double ttl_s) {
+  auto it = pods_.find(uid);
+  if (it == pods_.end()) return;
+  if (!ok) {
+    stats_.bind_fail++;
+    if (it->second.assumed) erase_pod(it);
+    return;
+  }
+  stats_.bind_ok++;
+  it->second.bound = true;
+  it->second.deadline = now_s() + ttl_s;
+}
+
+int Ledger::gc() {
+  double now = now_s();
+  int n = 0;
+  for (auto it = pods_.begin(); it != pods_.end();) {
+    const PodRec& r = it->second;
+    // bound but never observed by the informer within ttl, or a bind that
+    // never finished (crashed coroutine) after 10 minutes.
+    bool expire = r.assumed && ((r.bound && r.deadline < now) || (!r.bound && now - r.assumed_at > 600.0));
+    if (expire) {
+      auto cur = it++;
+      erase_pod(cur);
+      ++n;
+    } else {
+      ++it;
+    }
+  }
+  stats_.expired += static_cast<uint64_t>(n);
+  return n;
+}
+
+// ---------------------------------------------------------------- inspect
+
+std::vector<std::pair<int64_t, int64_t>> Ledger::node_devices(const std::string& node) const {
+  std::vector<std::pair<int64_t, int64_t>> out;
+  auto it = nodes_.find(node);
+  if (it == nodes_.end()) return out;
+  for (const DevState& d : it->second.devs) out.emplace_back(d.total, d.used);
+  return out;
+}
+
+std::vector<std::string> Ledger::node_names() const {
+  std::vector<std::string> out;
+  out.reserve(nodes_.size());
+  for (const auto& kv : nodes_) out.push_back(kv.first);
+  return out;
+}
+
+namespace {
+void append_int(std::string* o, int64_t v) {
+  char buf[32];
+  int n = std::snprintf(buf, sizeof(buf), "%lld", static_cast<long long>(v));
+  o->append(buf, static_cast<size_t>(n));
+}
+}  // namespace
+
+std::string Ledger::inspect_json(const std::string& node, bool* found) const {
+  // Schema of pkg/scheduler/gpushare-inspect.go:14-38 (lowercase tags).
+  std::string o;
+  o.reserve(256);
+  o.append("{\"nodes\":[");
+  bool first_node = true;
+  *found = true;
+  auto emit = [&](const NodeState& n) {
+    if (!first_node) o.push_back(',');
+    first_node = false;
+    // per-device pod lists, sorted for determinism
+    std::vector<std::vector<const PodRec*>> per(n.devs.size());
+    for (const auto& uid : n.pods) {
+      auto pit = pods_.find(uid);
+      if (pit == pods_.end()) continue;
+      const PodRec& r = pit->second;
+      if (r.dev < 0 || r.dev >= static_cast<int64_t>(n.devs.size())) continue;
+      if (r.deleting || r.terminal) continue;  // AssignedNonTerminatedPod
+      per[static_cast<size_t>(r.dev)].push_back(&r);
+    }
+    int64_t used_total = 0;
+    for (const DevState& d : n.devs) used_total += d.used;
+    o.append("{\"name\":");
+    json::append_quoted(&o, n.name);
+    o.append(",\"totalGPU\":");
+    append_int(&o, n.total);
+    o.append(",\"usedGPU\":");
+    append_int(&o, used_total);
+    o.append(",\"devs\":[");
+    for (size_t i = 0; i < n.devs.size(); ++i) {
+      if (i) o.push_back(',');
+      o.append("{\"id\":");
+      append_int(&o, static_cast<int64_t>(i));
+      o.append(",\"totalGPU\":");
+      append_int(&o, n.devs[i].total);
+      o.append(",\"usedGPU\":");
+      append_int(&o, n.devs[i].used);
+      o.append(",\"pods\":[");
+      auto& lst = per[i];
+      std::sort(lst.begin(), lst.end(), [](const PodRec* a, const PodRec* b) {
+        return a->ns != b->ns ? a->ns < b->ns : a->name < b->name;
+      });
+      for (size_t k = 0; k < lst.size(); ++k) {
+        if (k) o.push_back(',');
+        o.append("{\"name\":");
+        json::append_quoted(&o, lst[k]->name);
+        o.append(",\"namespace\":");
+        json::append_quoted(&o, lst[k]->ns);
+        o.append(",\"usedGPU\":");
+        append_int(&o, lst[k]->request);
+        o.push_back('}');
+      }
+      o.append("]}");
+    }
+    o.append("]}");
+  };
+  std::string err;
+  if (node.empty()) {
+    for (const auto& kv : nodes_) emit(kv.second);
+  } else {
+    auto it = nodes_.find(node);
+    if (it == nodes_.end()) {
+      *found = false;
+      err = "node \"" + node + "\" not found";
+    } else {
+      emit(it->second);
+    }
+  }
+  o.push_back(']');
+  if (!err.empty()) {
+    o.append(",\"error\":");
+    json::append_quoted(&o, err);
+  }
+  o.push_back('}');
+  return o;
+}
+
+// ---------------------------------------------------------------- filter verb
+
+std::string filter_body(Ledger& l, std::string_view body) {
+  l.mutable_stats().filter_calls++;
+  json::Doc d;
+  std::string err;
+  auto error_result = [](const std::string& e) {
+    std::string o("{\"Nodes\":null,\"NodeNames\":null,\"FailedNodes\":null,\"Error\":");
+    json::append_quoted(&o, e);
+    o.push_back('}');
+    return o;
+  };
+  if (!d.parse(body, &err)) return error_result(err);
+  if (d.at(0).type != json::T::Object) {
+    return error_result("json: cannot unmarshal value into Go value of type api.ExtenderArgs");
+  }
+  int64_t pod = d.find(0, "Pod", true);
+  if (pod < 0 || d.at(static_cast<uint32_t>(pod)).type != json::T::Object) {
+    return error_result("ExtenderArgs.Pod is required");
+  }
+  const Profile& p = l.profile();
+  int64_t req = pod_limits_sum(d, static_cast<uint32_t>(pod), p.resource);
+
+  // Candidate nodes: NodeNames (nodeCacheCapable) or Nodes.items.
+  struct Cand {
+    std::string name;
+    int64_t item = -1;  // tape index of the v1.Node when given as NodeList
+  };
+  std::vector<Cand> cands;
+  bool by_names = false, by_nodes = false;
+  int64_t names = d.find(0, "NodeNames", true);
+  if (names >= 0 && d.at(static_cast<uint32_t>(names)).type == json::T::Array) {
+    by_names = true;
+    uint32_t end = d.at(static_cast<uint32_t>(names)).skip;
+    for (uint32_t i = static_cast<uint32_t>(names) + 1; i < end; i = d.next(i)) {
+      cands.push_back(Cand{d.str(i), -1});
+    }
+  }
+  int64_t nodes = d.find(0, "Nodes", true);
+  if (!by_names && nodes >= 0 && d.at(static_cast<uint32_t>(nodes)).type == json::T::Object) {
+    int64_t items = d.find(static_cast<uint32_t>(nodes), "items");
+    if (items >= 0 && d.at(static_cast<uint32_t>(items)).type == json::T::Array) {
+      by_nodes = true;
+      uint32_t end = d.at(static_cast<uint32_t>(items)).skip;
+      for (uint32_t i = static_cast<uint32_t>(items) + 1; i < end; i = d.next(i)) {
+        std::string nm;
+        int64_t m = d.path(i, {"metadata", "name"});
+        if (m >= 0) nm = d.str(static_cast<uint32_t>(m));
+        cands.push_back(Cand{nm, static_cast<int64_t>(i)});
+      }
+    }
+  }
+
+  std::vector<const Cand*> ok;
+  std::vector<std::pair<std::string, std::string>> failed;
+  ok.reserve(cands.size());
+  for (const Cand& c : cands) {
+    Check r = l.check(c.name, req);
+    switch (r) {
+      case Check::Ok:
+        ok.push_back(&c);
+        break;
+      case Check::NodeNotFound:
+        failed.emplace_back(c.name, "node \"" + c.name + "\" not found");
+        break;
+      case Check::NotGPUShare:
+        failed.emplace_back(c.name, "The node " + c.name + " is not for GPU share, need skip");
+        break;
+      case Check::Insufficient:
+        failed.emplace_back(c.name, "Insufficient GPU Memory in one device");
+        break;
+    }
+  }
+  l.mutable_stats().filter_nodes_ok += ok.size();
+  l.mutable_stats().filter_nodes_failed += failed.size();
+  // Go marshals map keys sorted; duplicates collapse (last wins).
+  std::stable_sort(failed.begin(), failed.end(),
+                   [](const auto& a, const auto& b) { return a.first < b.first; });
+
+  std::string o;
+  o.reserve(64 + 24 * cands.size());
+  o.append("{\"Nodes\":");
+  if (by_nodes) {
+    o.append("{\"metadata\":{},\"items\":[");
+    for (size_t i = 0; i < ok.size(); ++i) {
+      if (i) o.push_back(',');
+      o.append(d.raw(static_cast<uint32_t>(ok[i]->item)));
+    }
+    o.append("]}");
+  } else {
+    o.append("null");
+  }
+  o.append(",\"NodeNames\":");
+  if (by_names || by_nodes) {
+    o.push_back('[');
+    for (size_t i = 0; i < ok.size(); ++i) {
+      if (i) o.push_back(',');
+      json::append_quoted(&o, ok[i]->name);
+    }
+    o.push_back(']');
+  } else {
+    o.append("[]");
+  }
+  o.append(",\"FailedNodes\":{");
+  bool first = true;
+  for (size_t i = 0; i < failed.size(); ++i) {
+    if (i + 1 < failed.size() && failed[i + 1].first == failed[i].first) continue;
+    if (!first) o.push_back(',');
+    first = false;
+    json::append_quoted(&o, failed[i].first);
+    o.push_back(':');
+    json::append_quoted(&o, failed[i].second);
+  }
+  o.append("},\"Error\":\"\"}");
+  return o;
+}
+
+}  // namespace gsx

@@ -1,0 +1,133 @@
+// GPU-share ledger: node -> device -> pod accounting and the binpack policy.
+//
+// Reference: pkg/cache/{cache,nodeinfo,deviceinfo}.go.  Same observable
+// policy (single-device fit in filter, best-fit with lowest-index ties in
+// bind, used memory = sum of the pods' SHARED_GPU_MEM_POD annotations,
+// Succeeded/Failed pods not counted), re-designed for throughput:
+//   * per-device used counters are maintained incrementally (the reference
+//     re-parses every pod annotation on every query, deviceinfo.go:41-54);
+//   * signed arithmetic, no uint underflow on over-commit (nodeinfo.go:260);
+//   * bind reserves memory up front ("assume"), so concurrent binds on one
+//     node need no lock held across apiserver round-trips (nodeinfo.go:141);
+//   * capacity / device-count changes rebuild the node (cache.go:144-157
+//     only rebuilt on the non-gpushare -> gpushare transition);
+//   * heterogeneous per-device totals via a node annotation.
+#pragma once
+
+#include <chrono>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "model.h"
+
+namespace gsx {
+
+enum class Check : int { Ok = 0, NodeNotFound = 1, NotGPUShare = 2, Insufficient = 3 };
+
+struct PodRec {
+  std::string uid, ns, name, node;
+  int64_t dev = -1;      // device index on node (-1: not placed)
+  int64_t mem = 0;       // accounted memory (annotation POD / assumed request)
+  int64_t request = 0;   // container-limit sum (inspect "usedGPU" per pod)
+  bool terminal = false; // Succeeded/Failed -> not counted
+  bool deleting = false;
+  bool assumed = false;  // reserved by bind, not yet observed with annotations
+  bool bound = false;    // bind round-trips finished successfully
+  double assumed_at = 0;
+  double deadline = 0;   // expiry of an assumed+bound reservation
+  bool accounted = false;
+};
+
+struct DevState {
+  int64_t total = 0;
+  int64_t used = 0;
+  int64_t npods = 0;
+};
+
+struct NodeState {
+  std::string name;
+  std::string address;
+  int64_t total = 0;  // node capacity
+  int64_t count = 0;
+  std::vector<int64_t> dev_totals_override;
+  std::vector<DevState> devs;
+  std::unordered_set<std::string> pods;  // uids whose rec.node == name
+  bool gpushare() const { return total > 0 && count > 0; }
+};
+
+struct Stats {
+  uint64_t filter_calls = 0, filter_nodes_ok = 0, filter_nodes_failed = 0;
+  uint64_t assume_ok = 0, assume_fail = 0, bind_ok = 0, bind_fail = 0;
+  uint64_t expired = 0, overcommit_events = 0, pod_upserts = 0, pod_removes = 0;
+};
+
+class Ledger {
+ public:
+  explicit Ledger(Profile p) : profile_(std::move(p)) {}
+  const Profile& profile() const { return profile_; }
+
+  // ---- nodes (informer-driven) ----
+  // Returns true when the device layout was (re)built.
+  bool upsert_node(const NodeView& nv);
+  bool remove_node(const std::string& name);
+  bool has_node(const std::string& name) const;
+
+  // ---- pods (informer-driven; cache.go:89-127) ----
+  // Returns 1 if the pod is (now) accounted to a device, 0 if skipped
+  // (no nodeName / no valid device index).
+  int upsert_pod(const PodView& v);
+  bool remove_pod(const std::string& uid);
+  bool known(const std::string& uid) const;
+
+  // ---- scheduling verbs ----
+  Check check(const std::string& node, int64_t req) const;  // nodeinfo.go:113-137
+  // Reserve a device for a pod being bound (best fit, nodeinfo.go:209-252).
+  // Returns device index >= 0, or -1 insufficient, -2 node not found,
+  // -3 node not gpushare, -4 bind already in flight for this uid.
+  int64_t assume(const std::string& uid, const std::string& ns, const std::string& name,
+                 const std::string& node, int64_t req, int64_t* dev_total);
+  void finish_bind(const std::string& uid, bool ok, double ttl_s);
+  int gc();  // expire stale reservations
+
+  // ---- observation ----
+  std::string inspect_json(const std::string& node, bool* found) const;
+  std::vector<std::pair<int64_t, int64_t>> node_devices(const std::string& node) const;
+  std::vector<std::string> node_names() const;
+  Stats stats() const { return stats_; }
+  Stats& mutable_stats() { return stats_; }
+  size_t pod_count() const { return pods_.size(); }
+  const NodeState* node(const std::string& name) const {
+    auto it = nodes_.find(name);
+    return it == nodes_.end() ? nullptr : &it->second;
+  }
+
+  static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+
+  std::mutex& mu() { return mu_; }
+
+ private:
+  void account(PodRec& r);
+  void unaccount(PodRec& r);
+  void rebuild(NodeState& n);
+  void erase_pod(std::unordered_map<std::string, PodRec>::iterator it);
+
+  Profile profile_;
+  std::map<std::string, NodeState> nodes_;  // ordered: deterministic inspect
+  std::unordered_map<std::string, PodRec> pods_;
+  Stats stats_;
+  mutable std::mutex mu_;
+};
+
+// Full filter verb on a raw ExtenderArgs body; returns the
+// ExtenderFilterResult JSON with the reference's Go field names
+// (vendor/k8s.io/kubernetes/pkg/scheduler/api/types.go:273-284).
+std::string filter_body(Ledger& l, std::string_view body);
+
+}  // namespace gsx
