@@ -1,0 +1,89 @@
+"""Process entry for the scheduler extender (``cmd/main.go`` equivalent).
+
+Environment (same names as the reference, ``cmd/main.go:23,92-98`` and
+``config/gpushare-schd-extender.yaml:93-98``):
+
+* ``PORT``        listen port (default 39999)
+* ``KUBECONFIG``  kubeconfig path; in-cluster service account otherwise
+* ``THREADNESS``  controller workers (honoured; the reference ignored it)
+* ``LOG_LEVEL``   debug|info|warning|error (set by the reference's yaml, never read)
+
+Ours: ``GSX_PROFILE`` (shared-gpu|aliyun), ``GSX_BIND_MODE`` (binding|update),
+``GSX_KUBE_QPS`` / ``GSX_KUBE_BURST`` (client-go defaults 5/10 cap the
+reference at ~2.5 binds/s), ``GSX_APISERVER`` (explicit apiserver URL).
+Every variable has a flag of the same meaning.  SIGINT/SIGTERM shut down
+gracefully; a second signal exits at once (``pkg/utils/signals/signal.go``).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import signal
+import sys
+
+from ..k8s.client import KubeClient, KubeConfig
+from ..models.profile import get_profile
+from .server import ExtenderRunner, ExtenderServer
+
+
+def parse_args(argv=None):
+    env = os.environ
+    ap = argparse.ArgumentParser(prog="gpushare-schd-extender", description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--host", default=env.get("HOST", "0.0.0.0"))
+    ap.add_argument("--port", type=int, default=int(env.get("PORT", "39999")))
+    ap.add_argument("--kubeconfig", default=env.get("KUBECONFIG"))
+    ap.add_argument("--apiserver", default=env.get("GSX_APISERVER"))
+    ap.add_argument("--threadness", type=int, default=int(env.get("THREADNESS", "1") or 1))
+    ap.add_argument("--log-level", default=env.get("LOG_LEVEL", "info"))
+    ap.add_argument("--profile", default=env.get("GSX_PROFILE", "shared-gpu"))
+    ap.add_argument("--bind-mode", default=env.get("GSX_BIND_MODE", "binding"), choices=["binding", "update"])
+    ap.add_argument("--kube-qps", type=float, default=float(env.get("GSX_KUBE_QPS", "0")))
+    ap.add_argument("--kube-burst", type=int, default=int(env.get("GSX_KUBE_BURST", "1000")))
+    ap.add_argument("--resync", type=float, default=float(env.get("GSX_RESYNC", "30")))
+    ap.add_argument("--reservation-ttl", type=float, default=float(env.get("GSX_RESERVATION_TTL", "60")))
+    ap.add_argument("--port-file", default="", help="write the bound port to this file once serving")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    a = parse_args(argv)
+    logging.basicConfig(level=getattr(logging, a.log_level.upper(), logging.INFO),
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    log = logging.getLogger("gsx.main")
+
+    async def run():
+        cfg = KubeConfig.auto(a.kubeconfig, a.apiserver)
+        client = KubeClient(cfg, qps=a.kube_qps, burst=a.kube_burst)
+        srv = ExtenderServer(client, get_profile(a.profile), workers=a.threadness, bind_mode=a.bind_mode,
+                             reservation_ttl=a.reservation_ttl, resync_period=a.resync)
+        runner = await ExtenderRunner(srv, a.host, a.port).start()
+        if a.port_file:
+            with open(a.port_file + ".tmp", "w") as f:
+                f.write(str(runner.port))
+            os.replace(a.port_file + ".tmp", a.port_file)
+        log.info("gpushare extender %s listening on %s:%d (profile=%s bind=%s)", "0.1.0", a.host, runner.port,
+                 a.profile, a.bind_mode)
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        hits = {"n": 0}
+
+        def on_sig():
+            hits["n"] += 1
+            if hits["n"] > 1:
+                os._exit(1)
+            stop.set()
+        for s in (signal.SIGINT, signal.SIGTERM):
+            loop.add_signal_handler(s, on_sig)
+        await stop.wait()
+        await runner.stop()
+        await client.close()
+
+    asyncio.run(run())
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

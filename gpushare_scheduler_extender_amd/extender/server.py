@@ -1,0 +1,287 @@
+"""kube-scheduler extender HTTP service: filter / bind / inspect / version / pprof / metrics.
+
+Route table and status-code contract of ``pkg/routes/routes.go:18-182``:
+
+=======================================  =========================================================
+``POST /gpushare-scheduler/filter``      ExtenderArgs -> ExtenderFilterResult, **always 200**
+                                         (``routes.go:58-99``); decided entirely in the native
+                                         engine (``native/engine/ledger.cc: filter_body``)
+``POST /gpushare-scheduler/bind``        ExtenderBindingArgs -> ExtenderBindingResult,
+                                         **500 iff Error != ""** (``routes.go:101-148``)
+``GET  /gpushare-scheduler/inspect``     all nodes (``pkg/scheduler/inspect.go``)
+``GET  /gpushare-scheduler/inspect/:n``  one node; unknown node -> ``error`` field (the
+                                         reference dereferences nil, ``inspect.go:19-24``)
+``GET  /version``                        ``0.1.0`` (``routes.go:27-30,150-156``)
+``GET  /debug/pprof/*``                  see :mod:`.pprof`
+``GET  /metrics``, ``GET /healthz``       ours
+=======================================  =========================================================
+
+Bind (``pkg/scheduler/gpushare-bind.go`` + ``pkg/cache/nodeinfo.go:139-206``)
+is re-designed for throughput while keeping its observable result (same
+annotations, same best-fit device, same error strings):
+
+1. the pod comes from the informer (lister); a UID mismatch triggers one live
+   GET and the reference's UID error (``gpushare-bind.go:44-65``);
+2. the native ledger *reserves* the best-fit device (``assume``) under its
+   mutex for microseconds, instead of holding a node write lock across the
+   apiserver round trips (``nodeinfo.go:141-142``), so binds to one node run
+   concurrently and a concurrent filter already sees the reservation;
+3. ``bind_mode="binding"`` (default) writes annotations and ``nodeName`` in
+   one ``pods/binding`` POST whose annotations kube-apiserver copies onto the
+   pod; ``bind_mode="update"`` reproduces the reference's two calls
+   (annotate, then bind) with its retry-once-on-conflict
+   (``nodeinfo.go:150-189``), detecting conflicts by HTTP 409;
+4. failure releases the reservation; success keeps it until the informer
+   observes the annotated pod (then the annotations are the record).
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import logging
+import time
+
+from aiohttp import web
+
+from ..core.controller import Controller
+from ..core.engine import new_engine
+from ..k8s.client import ApiError, KubeClient
+from ..models import pod as podutil
+from ..models import wire
+from ..models.profile import NamingProfile, SHARED_GPU
+from ..utils.metrics import Metrics
+from .pprof import add_pprof
+
+log = logging.getLogger("gsx.extender")
+
+VERSION = "0.1.0"
+API_PREFIX = "/gpushare-scheduler"
+
+
+class BindError(Exception):
+    pass
+
+
+class ExtenderServer:
+    def __init__(self, client: KubeClient, profile: NamingProfile = SHARED_GPU, *, workers: int = 1,
+                 bind_mode: str = "binding", reservation_ttl: float = 60.0, resync_period: float = 30.0,
+                 emit_events: bool = True):
+        if bind_mode not in ("binding", "update"):
+            raise ValueError("bind_mode must be 'binding' or 'update'")
+        self.client = client
+        self.profile = profile
+        self.engine = new_engine(profile)
+        self.metrics = Metrics(self.engine)
+        self.controller = Controller(client, self.engine, profile, workers=workers, resync_period=resync_period,
+                                     metrics=self.metrics)
+        self.bind_mode = bind_mode
+        self.reservation_ttl = reservation_ttl
+        self.emit_events = emit_events
+        self.app = self._make_app()
+        self._gc_task: asyncio.Task | None = None
+        self._bg: set[asyncio.Task] = set()
+
+    # ------------------------------------------------------------ lifecycle
+    async def start(self):
+        await self.controller.start()
+        self._gc_task = asyncio.get_running_loop().create_task(self._gc_loop())
+
+    async def stop(self):
+        if self._gc_task:
+            self._gc_task.cancel()
+        await self.controller.stop()
+
+    async def _gc_loop(self):
+        while True:
+            await asyncio.sleep(min(5.0, max(0.05, self.reservation_ttl / 4)))
+            n = self.engine.gc()
+            if n:
+                log.warning("expired %d unconfirmed bind reservations", n)
+
+    # ------------------------------------------------------------ verbs
+    def filter(self, body: bytes) -> bytes:
+        """predicate.go:15-39 + gpushare-predicate.go:13-40, in C++."""
+        return self.engine.filter(body)
+
+    async def _get_pod(self, name: str, ns: str, uid: str) -> dict:
+        """gpushare-bind.go:44-65."""
+        pod = self.controller.pods.get_by(name, ns)
+        if pod is not None and (pod.get("metadata") or {}).get("uid") == uid:
+            return pod
+        t0 = time.perf_counter()
+        try:
+            pod = await self.client.get("pods", name, ns)
+        except ApiError as e:
+            raise BindError(e.message or str(e)) from e
+        finally:
+            self.metrics.api_latency.labels("get_pod").observe(time.perf_counter() - t0)
+        puid = (pod.get("metadata") or {}).get("uid")
+        if puid != uid:
+            raise BindError(f"The pod {name} in ns {ns}'s uid is {puid}, and it's not equal with expected {uid}")
+        return pod
+
+    async def bind(self, args: wire.ExtenderBindingArgs) -> str:
+        """Returns "" on success or the error string of ExtenderBindingResult."""
+        name, ns, uid, node = args.pod_name, args.pod_namespace, args.pod_uid, args.node
+        try:
+            pod = await self._get_pod(name, ns, uid)
+        except BindError as e:
+            self.metrics.bind_results.labels("pod_lookup_failed").inc()
+            return str(e)
+        req = podutil.gpu_mem_request(pod, self.profile)
+        dev, dev_total = self.engine.assume(uid, ns, name, node, req)
+        if dev < 0:
+            self.metrics.bind_results.labels("no_device").inc()
+            if dev == -2:
+                msg = f'node "{node}" not found'
+            elif dev == -3:
+                msg = f"The node {node} is not for GPU share, need skip"
+            elif dev == -4:
+                msg = f"bind of pod {name} in ns {ns} is already in progress"
+            else:
+                msg = f"The node {node} can't place the pod {name} in ns {ns}"  # nodeinfo.go:170
+            self._event(pod, "FailedBinding", msg)
+            return msg
+        ann = podutil.bind_annotations(self.profile, dev, dev_total, req)
+        t0 = time.perf_counter()
+        try:
+            if self.bind_mode == "binding":
+                await self._bind_with_annotations(pod, node, ann)
+            else:
+                await self._update_then_bind(pod, node, ann)
+        except (ApiError, BindError, OSError, asyncio.TimeoutError) as e:
+            self.engine.finish_bind(uid, False, 0.0)
+            self.metrics.bind_results.labels("api_error").inc()
+            msg = e.message if isinstance(e, ApiError) and e.message else str(e)
+            self._event(pod, "FailedBinding", msg)
+            return msg
+        finally:
+            self.metrics.api_latency.labels("bind").observe(time.perf_counter() - t0)
+        self.engine.finish_bind(uid, True, self.reservation_ttl)
+        self.metrics.bind_results.labels("ok").inc()
+        return ""
+
+    async def _bind_with_annotations(self, pod: dict, node: str, ann: dict, retries: int = 2):
+        md = pod["metadata"]
+        for attempt in range(retries + 1):
+            try:
+                await self.client.bind_pod(md["namespace"], md["name"], node, md.get("uid"), ann)
+                return
+            except ApiError as e:
+                # only a transient (injected / storage) conflict is retried; an
+                # "already assigned" conflict is final
+                if e.conflict and "already assigned" not in e.message and attempt < retries:
+                    continue
+                raise
+
+    async def _update_then_bind(self, pod: dict, node: str, ann: dict):
+        """nodeinfo.go:145-189: annotate (retry once on conflict with a fresh GET), then bind."""
+        md = pod["metadata"]
+        new = podutil.with_annotations(pod, ann)
+        try:
+            await self.client.replace("pods", new)
+        except ApiError as e:
+            if not e.conflict:
+                raise
+            fresh = await self.client.get("pods", md["name"], md["namespace"])
+            await self.client.replace("pods", podutil.with_annotations(fresh, ann))
+        await self.client.bind_pod(md["namespace"], md["name"], node, md.get("uid"))
+
+    def _event(self, pod: dict, reason: str, msg: str):
+        if not self.emit_events:
+            return
+        ns = (pod.get("metadata") or {}).get("namespace", "default")
+
+        async def go():
+            try:
+                await self.client.create_event(ns, {"kind": "Pod", **pod}, reason, msg, "Warning")
+            except Exception as e:  # noqa: BLE001 - events are best effort
+                log.debug("event emit failed: %r", e)
+        t = asyncio.get_running_loop().create_task(go())
+        self._bg.add(t)
+        t.add_done_callback(self._bg.discard)
+
+    # ------------------------------------------------------------ HTTP
+    def _make_app(self) -> web.Application:
+        app = web.Application(client_max_size=64 * 1024 * 1024)
+        r = app.router
+        r.add_post(API_PREFIX + "/filter", self.h_filter)
+        r.add_post(API_PREFIX + "/bind", self.h_bind)
+        r.add_get(API_PREFIX + "/inspect", self.h_inspect)
+        r.add_get(API_PREFIX + "/inspect/", self.h_inspect)
+        r.add_get(API_PREFIX + "/inspect/{nodename}", self.h_inspect)
+        r.add_get("/version", self.h_version)
+        r.add_get("/metrics", self.h_metrics)
+        r.add_get("/healthz", self.h_healthz)
+        add_pprof(app)
+        return app
+
+    async def h_filter(self, request: web.Request):
+        t0 = time.perf_counter()
+        body = await request.read()
+        out = self.filter(body)
+        self.metrics.latency.labels("filter").observe(time.perf_counter() - t0)
+        self.metrics.requests.labels("filter", "200").inc()
+        return web.Response(body=out, content_type="application/json")
+
+    async def h_bind(self, request: web.Request):
+        t0 = time.perf_counter()
+        body = await request.read()
+        try:
+            args = wire.ExtenderBindingArgs.decode(body)
+            err = await self.bind(args)
+        except wire.WireError as e:
+            err = str(e)
+        status = 500 if err else 200
+        self.metrics.latency.labels("bind").observe(time.perf_counter() - t0)
+        self.metrics.requests.labels("bind", str(status)).inc()
+        return web.Response(body=wire.binding_result(err), status=status, content_type="application/json")
+
+    async def h_inspect(self, request: web.Request):
+        node = request.match_info.get("nodename", "")
+        body, _found = self.engine.inspect(node)
+        self.metrics.requests.labels("inspect", "200").inc()
+        return web.Response(body=body, content_type="application/json")
+
+    async def h_version(self, request):
+        return web.Response(text=VERSION)
+
+    async def h_healthz(self, request):
+        ok = self.controller.pods.synced.is_set() and self.controller.nodes.synced.is_set()
+        return web.Response(text="ok" if ok else "not synced", status=200 if ok else 503)
+
+    async def h_metrics(self, request):
+        return web.Response(body=self.metrics.render(), content_type="text/plain")
+
+
+class ExtenderRunner:
+    """Serve an :class:`ExtenderServer` on host:port (port 0 = ephemeral)."""
+
+    def __init__(self, server: ExtenderServer, host: str = "127.0.0.1", port: int = 0):
+        self.server = server
+        self.host = host
+        self.port = port
+        self._runner: web.AppRunner | None = None
+
+    @property
+    def url(self) -> str:
+        return f"http://{self.host}:{self.port}"
+
+    async def start(self) -> "ExtenderRunner":
+        await self.server.start()
+        self._runner = web.AppRunner(self.server.app, access_log=None, handle_signals=False, shutdown_timeout=1.0)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, self.host, self.port, backlog=1024, reuse_address=True)
+        await site.start()
+        if self.port == 0:
+            self.port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+        return self
+
+    async def stop(self):
+        if self._runner:
+            await self._runner.cleanup()
+        await self.server.stop()
+
+
+def dumps(o) -> bytes:
+    return json.dumps(o, separators=(",", ":")).encode()

@@ -1,0 +1,646 @@
+"""In-process fake kube-apiserver (pods, nodes, bindings, events) over real HTTP.
+
+The reference was only ever validated by hand on a live cluster;
+this stands in for that cluster in tests and in ``bench.py``.  It speaks the
+subset of the core/v1 REST API the scheduler extender, the controller, the
+device plugin and the CLI use, with the semantics they rely on:
+
+* LIST + chunk-streamed WATCH with ``resourceVersion`` (one global counter, as
+  etcd gives kube-apiserver), ``410 Gone`` for compacted versions, field
+  selectors ``spec.nodeName`` / ``metadata.name`` and equality label selectors;
+* optimistic concurrency on PUT / PATCH: ``409 Conflict`` with the exact
+  message client-go produces, which the reference matches by string
+  (``pkg/cache/nodeinfo.go:14-16,150-168``);
+* ``POST pods/{name}/binding`` sets ``spec.nodeName`` once and merges the
+  Binding's ``metadata.annotations`` into the pod, as kube-apiserver's
+  ``setPodHostAndAnnotations`` does (this is what lets our bind verb annotate
+  and bind in one round trip instead of the reference's PUT + POST,
+  ``pkg/cache/nodeinfo.go:150-189``);
+* JSON merge patch and strategic-merge-patch (treated as merge patch, which is
+  exact for the metadata/annotation/status patches used here);
+* graceful pod deletion (``deletionTimestamp`` first, object removed after the
+  grace period) and immediate deletion;
+* fault injection: conflict / error rates, latency and watch drops
+  (``POST /fake/faults``), which the reference never had.
+
+Run standalone with ``python -m gpushare_scheduler_extender_amd.k8s.fakeapi``.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import collections
+import copy
+import json
+import logging
+import random
+import time
+import uuid
+from datetime import datetime, timezone
+
+from aiohttp import web
+
+log = logging.getLogger("gsx.fakeapi")
+
+CONFLICT_MSG = ("Operation cannot be fulfilled on {res} \"{name}\": the object has been modified; "
+                "please apply your changes to the latest version and try again")
+
+
+def _now_iso() -> str:
+    return datetime.now(timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
+
+
+def status_body(code: int, reason: str, message: str, details: dict | None = None) -> dict:
+    b = {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Failure", "message": message,
+         "reason": reason, "code": code}
+    if details:
+        b["details"] = details
+    return b
+
+
+def merge_patch(target, patch):
+    """RFC 7386 JSON merge patch."""
+    if not isinstance(patch, dict):
+        return copy.deepcopy(patch)
+    if not isinstance(target, dict):
+        target = {}
+    out = dict(target)
+    for k, v in patch.items():
+        if v is None:
+            out.pop(k, None)
+        else:
+            out[k] = merge_patch(out.get(k), v)
+    return out
+
+
+def _label_match(obj: dict, selector: str) -> bool:
+    if not selector:
+        return True
+    labels = (obj.get("metadata") or {}).get("labels") or {}
+    for term in selector.split(","):
+        term = term.strip()
+        if not term:
+            continue
+        if "!=" in term:
+            k, v = term.split("!=", 1)
+            if labels.get(k.strip()) == v.strip():
+                return False
+        elif "=" in term:
+            k, v = term.split("=", 1)
+            k = k.strip().rstrip("=")
+            if labels.get(k) != v.strip():
+                return False
+        elif term.startswith("!"):
+            if term[1:] in labels:
+                return False
+        elif term not in labels:
+            return False
+    return True
+
+
+def _field_value(obj: dict, path: str):
+    cur = obj
+    for p in path.split("."):
+        if not isinstance(cur, dict):
+            return ""
+        cur = cur.get(p)
+    return "" if cur is None else cur
+
+
+def _field_match(obj: dict, selector: str) -> bool:
+    if not selector:
+        return True
+    for term in selector.split(","):
+        term = term.strip()
+        if not term:
+            continue
+        if "!=" in term:
+            k, v = term.split("!=", 1)
+            if str(_field_value(obj, k.strip())) == v.strip():
+                return False
+        else:
+            k, v = term.split("=", 1)
+            k = k.strip().rstrip("=")
+            if str(_field_value(obj, k)) != v.strip():
+                return False
+    return True
+
+
+class _Watcher:
+    __slots__ = ("kind", "ns", "fsel", "lsel", "queue", "closed")
+
+    def __init__(self, kind, ns, fsel, lsel):
+        self.kind = kind
+        self.ns = ns
+        self.fsel = fsel
+        self.lsel = lsel
+        self.queue: asyncio.Queue = asyncio.Queue()
+        self.closed = False
+
+    def wants(self, obj: dict) -> bool:
+        if self.ns and (obj.get("metadata") or {}).get("namespace") != self.ns:
+            return False
+        return _field_match(obj, self.fsel) and _label_match(obj, self.lsel)
+
+
+class Faults:
+    def __init__(self):
+        self.conflict_rate = 0.0  # extra 409s on pod PUT/PATCH/binding
+        self.error_rate = 0.0  # 500s on mutating pod calls
+        self.latency_ms = 0.0  # added to every non-watch request
+        self.drop_watch_after = 0  # close watch streams after this many events (0 = never)
+        self.seed = 0
+        self.rng = random.Random(0)
+
+    def update(self, d: dict):
+        for k in ("conflict_rate", "error_rate", "latency_ms", "drop_watch_after"):
+            if k in d:
+                setattr(self, k, type(getattr(self, k))(d[k]))
+        if "seed" in d:
+            self.seed = int(d["seed"])
+            self.rng = random.Random(self.seed)
+
+    def as_dict(self):
+        return {"conflict_rate": self.conflict_rate, "error_rate": self.error_rate,
+                "latency_ms": self.latency_ms, "drop_watch_after": self.drop_watch_after}
+
+
+class FakeApiServer:
+    """State + aiohttp application.  All mutation happens on the event loop thread."""
+
+    KINDS = ("pods", "nodes", "events")
+
+    def __init__(self, history: int = 200000):
+        self.rv = 0
+        self.store: dict[str, dict[tuple[str, str], dict]] = {k: {} for k in self.KINDS}
+        self.history: collections.deque = collections.deque(maxlen=history)  # (rv, kind, type, bytes, obj)
+        self.oldest_rv = 0
+        self.watchers: list[_Watcher] = []
+        self.faults = Faults()
+        self.counts = collections.Counter()
+        self._grace_tasks: set[asyncio.Task] = set()
+        self.app = self._make_app()
+
+    # ------------------------------------------------------------ state
+    def _bump(self) -> str:
+        self.rv += 1
+        return str(self.rv)
+
+    def _emit(self, kind: str, etype: str, obj: dict):
+        rv = int(obj["metadata"]["resourceVersion"])
+        line = json.dumps({"type": etype, "object": obj}, separators=(",", ":")).encode() + b"\n"
+        if len(self.history) == self.history.maxlen:
+            self.oldest_rv = self.history[0][0]
+        self.history.append((rv, kind, etype, line, obj))
+        for w in self.watchers:
+            if w.kind == kind and not w.closed and w.wants(obj):
+                w.queue.put_nowait(line)
+
+    def create(self, kind: str, obj: dict, ns: str | None = None) -> dict:
+        obj = copy.deepcopy(obj)
+        md = obj.setdefault("metadata", {})
+        if ns is not None and kind != "nodes":
+            md["namespace"] = ns
+        if kind != "nodes":
+            md.setdefault("namespace", "default")
+        if not md.get("name"):
+            if md.get("generateName"):
+                md["name"] = md["generateName"] + uuid.uuid4().hex[:5]
+            else:
+                raise web.HTTPUnprocessableEntity(
+                    text=json.dumps(status_body(422, "Invalid", "metadata.name: Required value")),
+                    content_type="application/json")
+        key = (md.get("namespace", ""), md["name"])
+        if key in self.store[kind]:
+            raise web.HTTPConflict(
+                text=json.dumps(status_body(409, "AlreadyExists", f'{kind} "{md["name"]}" already exists')),
+                content_type="application/json")
+        md.setdefault("uid", str(uuid.uuid4()))
+        md.setdefault("creationTimestamp", _now_iso())
+        if kind == "pods":
+            obj.setdefault("status", {}).setdefault("phase", "Pending")
+            obj.setdefault("spec", {})
+        md["resourceVersion"] = self._bump()
+        self.store[kind][key] = obj
+        self._emit(kind, "ADDED", obj)
+        return obj
+
+    def _get(self, kind: str, ns: str, name: str) -> dict:
+        o = self.store[kind].get((ns if kind != "nodes" else "", name))
+        if o is None:
+            raise web.HTTPNotFound(text=json.dumps(status_body(404, "NotFound", f'{kind} "{name}" not found',
+                                                               {"name": name, "kind": kind})),
+                                   content_type="application/json")
+        return o
+
+    def _conflict(self, kind: str, name: str):
+        return web.HTTPConflict(text=json.dumps(status_body(409, "Conflict", CONFLICT_MSG.format(res=kind, name=name),
+                                                            {"name": name, "kind": kind})),
+                                content_type="application/json")
+
+    def replace(self, kind: str, ns: str, name: str, obj: dict, subresource: str = "") -> dict:
+        cur = self._get(kind, ns, name)
+        want_rv = (obj.get("metadata") or {}).get("resourceVersion")
+        if want_rv and want_rv != cur["metadata"]["resourceVersion"]:
+            raise self._conflict(kind, name)
+        if kind == "pods" and self.faults.conflict_rate and self.faults.rng.random() < self.faults.conflict_rate:
+            self.counts["injected_conflict"] += 1
+            raise self._conflict(kind, name)
+        new = copy.deepcopy(obj)
+        md = new.setdefault("metadata", {})
+        # immutable / server-owned fields
+        for f in ("uid", "creationTimestamp", "namespace", "name", "deletionTimestamp"):
+            if f in cur["metadata"]:
+                md[f] = cur["metadata"][f]
+        if subresource == "status":
+            merged = copy.deepcopy(cur)
+            merged["status"] = new.get("status", {})
+            new = merged
+        elif kind == "pods":
+            # spec.nodeName is only settable through the binding subresource
+            old_node = (cur.get("spec") or {}).get("nodeName")
+            if old_node:
+                new.setdefault("spec", {})["nodeName"] = old_node
+            else:
+                (new.get("spec") or {}).pop("nodeName", None)
+            new["status"] = cur.get("status", {})
+        new["metadata"]["resourceVersion"] = self._bump()
+        self.store[kind][(ns if kind != "nodes" else "", name)] = new
+        self._emit(kind, "MODIFIED", new)
+        return new
+
+    def patch(self, kind: str, ns: str, name: str, patch: dict, subresource: str = "") -> dict:
+        cur = self._get(kind, ns, name)
+        want_rv = ((patch or {}).get("metadata") or {}).get("resourceVersion")
+        if want_rv and want_rv != cur["metadata"]["resourceVersion"]:
+            raise self._conflict(kind, name)
+        if kind == "pods" and self.faults.conflict_rate and self.faults.rng.random() < self.faults.conflict_rate:
+            self.counts["injected_conflict"] += 1
+            raise self._conflict(kind, name)
+        if subresource == "status":
+            patch = {"status": (patch or {}).get("status", {})}
+        elif kind == "pods":
+            patch = dict(patch or {})
+            spec = patch.get("spec")
+            if isinstance(spec, dict) and "nodeName" in spec:
+                spec = dict(spec)
+                spec.pop("nodeName")
+                patch["spec"] = spec
+            if subresource == "":
+                patch.pop("status", None)
+        new = merge_patch(cur, patch)
+        for f in ("uid", "creationTimestamp", "namespace", "name", "deletionTimestamp"):
+            if f in cur["metadata"]:
+                new["metadata"][f] = cur["metadata"][f]
+        new["metadata"]["resourceVersion"] = self._bump()
+        self.store[kind][(ns if kind != "nodes" else "", name)] = new
+        self._emit(kind, "MODIFIED", new)
+        return new
+
+    def bind(self, ns: str, name: str, binding: dict) -> None:
+        cur = self._get("pods", ns, name)
+        bmd = binding.get("metadata") or {}
+        if bmd.get("uid") and bmd["uid"] != cur["metadata"]["uid"]:
+            raise web.HTTPConflict(text=json.dumps(status_body(
+                409, "Conflict", f'Precondition failed: UID in precondition: {bmd["uid"]}, '
+                                 f'UID in object meta: {cur["metadata"]["uid"]}')), content_type="application/json")
+        if self.faults.conflict_rate and self.faults.rng.random() < self.faults.conflict_rate:
+            self.counts["injected_conflict"] += 1
+            raise self._conflict("pods", name)
+        if (cur.get("spec") or {}).get("nodeName"):
+            raise web.HTTPConflict(text=json.dumps(status_body(
+                409, "Conflict", f'pod {name} is already assigned to node "{cur["spec"]["nodeName"]}"')),
+                content_type="application/json")
+        if cur["metadata"].get("deletionTimestamp"):
+            raise web.HTTPConflict(text=json.dumps(status_body(409, "Conflict", f"pod {name} is being deleted")),
+                                   content_type="application/json")
+        target = (binding.get("target") or {}).get("name", "")
+        if not target:
+            raise web.HTTPUnprocessableEntity(text=json.dumps(status_body(422, "Invalid", "target.name: Required value")),
+                                              content_type="application/json")
+        new = copy.deepcopy(cur)
+        new.setdefault("spec", {})["nodeName"] = target
+        ann = bmd.get("annotations") or {}
+        if ann:
+            new["metadata"].setdefault("annotations", {}).update(ann)
+        conds = new.setdefault("status", {}).setdefault("conditions", [])
+        conds.append({"type": "PodScheduled", "status": "True", "lastTransitionTime": _now_iso()})
+        new["metadata"]["resourceVersion"] = self._bump()
+        self.store["pods"][(ns, name)] = new
+        self._emit("pods", "MODIFIED", new)
+
+    def delete(self, kind: str, ns: str, name: str, grace: float | None = None) -> dict:
+        cur = self._get(kind, ns, name)
+        key = (ns if kind != "nodes" else "", name)
+        if kind == "pods" and grace and grace > 0 and (cur.get("spec") or {}).get("nodeName"):
+            if cur["metadata"].get("deletionTimestamp"):
+                return cur
+            new = copy.deepcopy(cur)
+            new["metadata"]["deletionTimestamp"] = _now_iso()
+            new["metadata"]["deletionGracePeriodSeconds"] = int(grace)
+            new["metadata"]["resourceVersion"] = self._bump()
+            self.store[kind][key] = new
+            self._emit(kind, "MODIFIED", new)
+            loop = asyncio.get_running_loop()
+            t = loop.create_task(self._finalize_later(kind, ns, name, new["metadata"]["uid"], grace))
+            self._grace_tasks.add(t)
+            t.add_done_callback(self._grace_tasks.discard)
+            return new
+        del self.store[kind][key]
+        gone = copy.deepcopy(cur)
+        gone["metadata"]["resourceVersion"] = self._bump()
+        self._emit(kind, "DELETED", gone)
+        return gone
+
+    async def _finalize_later(self, kind, ns, name, uid, grace):
+        await asyncio.sleep(grace)
+        cur = self.store[kind].get((ns, name))
+        if cur is not None and cur["metadata"]["uid"] == uid:
+            self.delete(kind, ns, name, None)
+
+    def list(self, kind: str, ns: str = "", fsel: str = "", lsel: str = "") -> list[dict]:
+        out = []
+        for (ons, _), o in self.store[kind].items():
+            if ns and ons != ns:
+                continue
+            if _field_match(o, fsel) and _label_match(o, lsel):
+                out.append(o)
+        return out
+
+    # ------------------------------------------------------------ HTTP
+    def _make_app(self) -> web.Application:
+        app = web.Application(middlewares=[self._mw], client_max_size=64 * 1024 * 1024)
+        r = app.router
+        r.add_get("/version", self.h_version)
+        r.add_get("/healthz", self.h_healthz)
+        r.add_get("/api", self.h_api)
+        for kind in ("pods", "events"):
+            r.add_get(f"/api/v1/{kind}", self._mk_list(kind))
+            r.add_get(f"/api/v1/namespaces/{{ns}}/{kind}", self._mk_list(kind))
+            r.add_post(f"/api/v1/namespaces/{{ns}}/{kind}", self._mk_create(kind))
+            r.add_get(f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", self._mk_get(kind))
+            r.add_put(f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", self._mk_put(kind, ""))
+            r.add_patch(f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", self._mk_patch(kind, ""))
+            r.add_delete(f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", self._mk_delete(kind))
+        r.add_put("/api/v1/namespaces/{ns}/pods/{name}/status", self._mk_put("pods", "status"))
+        r.add_patch("/api/v1/namespaces/{ns}/pods/{name}/status", self._mk_patch("pods", "status"))
+        r.add_post("/api/v1/namespaces/{ns}/pods/{name}/binding", self.h_binding)
+        r.add_post("/api/v1/namespaces/{ns}/bindings", self.h_bindings)
+        r.add_get("/api/v1/nodes", self._mk_list("nodes"))
+        r.add_post("/api/v1/nodes", self._mk_create("nodes"))
+        r.add_get("/api/v1/nodes/{name}", self._mk_get("nodes"))
+        r.add_put("/api/v1/nodes/{name}", self._mk_put("nodes", ""))
+        r.add_patch("/api/v1/nodes/{name}", self._mk_patch("nodes", ""))
+        r.add_put("/api/v1/nodes/{name}/status", self._mk_put("nodes", "status"))
+        r.add_patch("/api/v1/nodes/{name}/status", self._mk_patch("nodes", "status"))
+        r.add_delete("/api/v1/nodes/{name}", self._mk_delete("nodes"))
+        r.add_get("/fake/faults", self.h_faults_get)
+        r.add_post("/fake/faults", self.h_faults)
+        r.add_get("/fake/stats", self.h_stats)
+        return app
+
+    @web.middleware
+    async def _mw(self, request: web.Request, handler):
+        self.counts[request.method] += 1
+        if self.faults.latency_ms and request.query.get("watch") not in ("1", "true"):
+            await asyncio.sleep(self.faults.latency_ms / 1000.0)
+        return await handler(request)
+
+    @staticmethod
+    def _json(obj, status=200) -> web.Response:
+        return web.Response(body=json.dumps(obj, separators=(",", ":")).encode(), status=status,
+                            content_type="application/json")
+
+    async def h_version(self, request):
+        return self._json({"major": "1", "minor": "30", "gitVersion": "v1.30.0-gsx-fake", "platform": "linux/amd64"})
+
+    async def h_healthz(self, request):
+        return web.Response(text="ok")
+
+    async def h_api(self, request):
+        return self._json({"kind": "APIVersions", "versions": ["v1"]})
+
+    async def h_faults_get(self, request):
+        return self._json(self.faults.as_dict())
+
+    async def h_faults(self, request):
+        self.faults.update(await request.json())
+        return self._json(self.faults.as_dict())
+
+    async def h_stats(self, request):
+        return self._json({"rv": self.rv, "counts": dict(self.counts), "watchers": len(self.watchers),
+                           **{k: len(v) for k, v in self.store.items()}})
+
+    def _maybe_error(self):
+        if self.faults.error_rate and self.faults.rng.random() < self.faults.error_rate:
+            self.counts["injected_error"] += 1
+            raise web.HTTPInternalServerError(text=json.dumps(status_body(500, "InternalError", "injected fault")),
+                                              content_type="application/json")
+
+    def _mk_list(self, kind):
+        async def h(request: web.Request):
+            q = request.query
+            ns = request.match_info.get("ns", "")
+            fsel = q.get("fieldSelector", "")
+            lsel = q.get("labelSelector", "")
+            if q.get("watch") in ("1", "true"):
+                return await self._watch(request, kind, ns, fsel, lsel, q.get("resourceVersion", ""))
+            items = self.list(kind, ns, fsel, lsel)
+            body = {"kind": {"pods": "PodList", "nodes": "NodeList", "events": "EventList"}[kind],
+                    "apiVersion": "v1", "metadata": {"resourceVersion": str(self.rv)}, "items": items}
+            return self._json(body)
+        return h
+
+    async def _watch(self, request, kind, ns, fsel, lsel, rv_s):
+        w = _Watcher(kind, ns, fsel, lsel)
+        # replay history after rv (or 410 if compacted)
+        backlog = []
+        if rv_s not in ("", "0"):
+            try:
+                rv = int(rv_s)
+            except ValueError:
+                rv = 0
+            if self.oldest_rv and rv < self.oldest_rv:
+                resp = web.StreamResponse(headers={"Content-Type": "application/json"})
+                await resp.prepare(request)
+                err = {"type": "ERROR", "object": status_body(
+                    410, "Expired", f"too old resource version: {rv} ({self.oldest_rv})")}
+                await resp.write(json.dumps(err).encode() + b"\n")
+                return resp
+            for (erv, k, _et, line, obj) in self.history:
+                if erv > rv and k == kind and w.wants(obj):
+                    backlog.append(line)
+        else:
+            for o in self.list(kind, ns, fsel, lsel):
+                backlog.append(json.dumps({"type": "ADDED", "object": o}, separators=(",", ":")).encode() + b"\n")
+        self.watchers.append(w)
+        resp = web.StreamResponse(headers={"Content-Type": "application/json", "Transfer-Encoding": "chunked"})
+        try:
+            await resp.prepare(request)
+            sent = 0
+            if backlog:
+                await resp.write(b"".join(backlog))
+                sent += len(backlog)
+            timeout = float(request.query.get("timeoutSeconds", "0") or 0) or None
+            deadline = time.monotonic() + timeout if timeout else None
+            while True:
+                rem = None if deadline is None else deadline - time.monotonic()
+                if rem is not None and rem <= 0:
+                    break
+                try:
+                    line = await asyncio.wait_for(w.queue.get(), 1.0 if rem is None else min(rem, 1.0))
+                except asyncio.TimeoutError:
+                    tr = request.transport
+                    if tr is None or tr.is_closing():
+                        break  # client went away (aiohttp does not cancel the handler)
+                    continue
+                if not line:
+                    break  # server shutdown sentinel
+                lines = [line]
+                while not w.queue.empty():
+                    lines.append(w.queue.get_nowait())
+                await resp.write(b"".join(lines))
+                sent += len(lines)
+                if self.faults.drop_watch_after and sent >= self.faults.drop_watch_after:
+                    self.counts["watch_dropped"] += 1
+                    break
+        except (ConnectionResetError, asyncio.CancelledError):
+            pass
+        finally:
+            w.closed = True
+            try:
+                self.watchers.remove(w)
+            except ValueError:
+                pass
+        return resp
+
+    def _mk_create(self, kind):
+        async def h(request):
+            body = await request.json()
+            if kind == "pods":
+                self._maybe_error()
+            obj = self.create(kind, body, request.match_info.get("ns"))
+            return self._json(obj, 201)
+        return h
+
+    def _mk_get(self, kind):
+        async def h(request):
+            return self._json(self._get(kind, request.match_info.get("ns", ""), request.match_info["name"]))
+        return h
+
+    def _mk_put(self, kind, sub):
+        async def h(request):
+            body = await request.json()
+            if kind == "pods":
+                self._maybe_error()
+            obj = self.replace(kind, request.match_info.get("ns", ""), request.match_info["name"], body, sub)
+            return self._json(obj)
+        return h
+
+    def _mk_patch(self, kind, sub):
+        async def h(request):
+            ct = request.headers.get("Content-Type", "")
+            body = await request.json()
+            if "json-patch+json" in ct:
+                return self._json(status_body(415, "UnsupportedMediaType", "json-patch not supported"), 415)
+            if kind == "pods":
+                self._maybe_error()
+            obj = self.patch(kind, request.match_info.get("ns", ""), request.match_info["name"], body, sub)
+            return self._json(obj)
+        return h
+
+    def _mk_delete(self, kind):
+        async def h(request):
+            grace = None
+            if "gracePeriodSeconds" in request.query:
+                grace = float(request.query["gracePeriodSeconds"])
+            elif request.can_read_body:
+                try:
+                    b = await request.json()
+                    if isinstance(b, dict) and b.get("gracePeriodSeconds") is not None:
+                        grace = float(b["gracePeriodSeconds"])
+                except ValueError:
+                    pass
+            obj = self.delete(kind, request.match_info.get("ns", ""), request.match_info["name"], grace)
+            return self._json(obj)
+        return h
+
+    async def h_binding(self, request):
+        body = await request.json()
+        self._maybe_error()
+        self.bind(request.match_info["ns"], request.match_info["name"], body)
+        return self._json({"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201}, 201)
+
+    async def h_bindings(self, request):
+        body = await request.json()
+        self._maybe_error()
+        self.bind(request.match_info["ns"], (body.get("metadata") or {}).get("name", ""), body)
+        return self._json({"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201}, 201)
+
+
+class FakeApiServerRunner:
+    """Start/stop helper on the current event loop (tests) or a dedicated thread/process."""
+
+    def __init__(self, server: FakeApiServer | None = None, host: str = "127.0.0.1", port: int = 0):
+        self.server = server or FakeApiServer()
+        self.host = host
+        self.port = port
+        self._runner: web.AppRunner | None = None
+
+    @property
+    def url(self) -> str:
+        return f"http://{self.host}:{self.port}"
+
+    async def start(self) -> "FakeApiServerRunner":
+        self._runner = web.AppRunner(self.server.app, access_log=None, handle_signals=False, shutdown_timeout=1.0)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, self.host, self.port, backlog=1024, reuse_address=True)
+        await site.start()
+        if self.port == 0:
+            self.port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+        return self
+
+    async def stop(self):
+        for w in list(self.server.watchers):
+            w.closed = True
+            w.queue.put_nowait(b"")
+        if self._runner:
+            await self._runner.cleanup()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="fake kube-apiserver for gpushare tests/bench")
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--port-file", default="", help="write the bound port here once listening")
+    ap.add_argument("--seed-json", default="", help="JSON file with {'nodes':[...],'pods':[...]} to preload")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.WARNING)
+
+    async def run():
+        srv = FakeApiServer()
+        if a.seed_json:
+            with open(a.seed_json) as f:
+                seed = json.load(f)
+            for n in seed.get("nodes", []):
+                srv.create("nodes", n)
+            for p in seed.get("pods", []):
+                srv.create("pods", p)
+        r = await FakeApiServerRunner(srv, a.host, a.port).start()
+        if a.port_file:
+            with open(a.port_file + ".tmp", "w") as f:
+                f.write(str(r.port))
+            import os  # noqa: PLC0415
+
+            os.replace(a.port_file + ".tmp", a.port_file)
+        print(f"fake-apiserver listening on {r.url}", flush=True)
+        await asyncio.Event().wait()
+
+    try:
+        asyncio.run(run())
+    except KeyboardInterrupt:
+        pass
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,64 @@
+"""Prometheus metrics for the extender and the device plugin.
+
+The reference exports none (beego log files + /inspect only).
+Here: request counters and latency histograms per verb, apiserver round-trip
+latency, bind outcomes, and ledger gauges (per-device used / total gpu-mem,
+binpack utilisation) that are computed at scrape time from the native ledger.
+"""
+from __future__ import annotations
+
+from prometheus_client import CollectorRegistry, Counter, Histogram, generate_latest
+from prometheus_client.core import GaugeMetricFamily
+
+LAT_BUCKETS = (0.0001, 0.00025, 0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0)
+
+
+class _LedgerCollector:
+    def __init__(self, engine):
+        self.engine = engine
+
+    def collect(self):
+        used = GaugeMetricFamily("gpushare_device_used_gpu_mem", "gpu-mem accounted on a device",
+                                 labels=["node", "device"])
+        total = GaugeMetricFamily("gpushare_device_total_gpu_mem", "gpu-mem capacity of a device",
+                                  labels=["node", "device"])
+        util = GaugeMetricFamily("gpushare_binpack_utilization", "sum(used)/sum(total) over gpushare nodes")
+        pods = GaugeMetricFamily("gpushare_ledger_pods", "pods tracked by the ledger")
+        su = st = 0
+        for n in self.engine.node_names():
+            for i, (t, u) in enumerate(self.engine.node_devices(n)):
+                used.add_metric([n, str(i)], u)
+                total.add_metric([n, str(i)], t)
+                su += u
+                st += t
+        util.add_metric([], (su / st) if st else 0.0)
+        s = self.engine.stats()
+        pods.add_metric([], s["pods"])
+        yield used
+        yield total
+        yield util
+        yield pods
+        for k in ("filter_calls", "assume_ok", "assume_fail", "bind_ok", "bind_fail", "expired",
+                  "overcommit_events", "pod_upserts", "pod_removes"):
+            g = GaugeMetricFamily(f"gpushare_engine_{k}", f"native engine counter {k}")
+            g.add_metric([], s[k])
+            yield g
+
+
+class Metrics:
+    def __init__(self, engine=None, prefix: str = "gpushare"):
+        self.registry = CollectorRegistry(auto_describe=True)
+        self.requests = Counter(f"{prefix}_http_requests", "extender HTTP requests", ["verb", "code"],
+                                registry=self.registry)
+        self.latency = Histogram(f"{prefix}_verb_latency_seconds", "extender verb latency", ["verb"],
+                                 buckets=LAT_BUCKETS, registry=self.registry)
+        self.api_latency = Histogram(f"{prefix}_apiserver_latency_seconds", "apiserver round-trip latency",
+                                     ["call"], buckets=LAT_BUCKETS, registry=self.registry)
+        self.bind_results = Counter(f"{prefix}_bind_results", "bind outcomes", ["result"], registry=self.registry)
+        self.allocate_results = Counter(f"{prefix}_allocate_results", "device-plugin Allocate outcomes",
+                                        ["result"], registry=self.registry)
+        if engine is not None:
+            self.registry.register(_LedgerCollector(engine))
+
+    def render(self) -> bytes:
+        return generate_latest(self.registry)

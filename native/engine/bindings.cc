@@ -137,6 +137,25 @@ class Engine {
     return l_.known(uid);
   }
 
+  py::tuple pod_state(const std::string& uid) {
+    int64_t dev;
+    int st;
+    {
+      std::lock_guard<std::mutex> g(l_.mu());
+      st = l_.pod_state(uid, &dev);
+    }
+    return py::make_tuple(st, dev);
+  }
+
+  // Upsert straight from a raw pod / watch-event JSON (informer fast path).
+  int upsert_pod_json(const py::bytes& b) {
+    PodView v;
+    std::string err;
+    if (!parse_pod_bytes(b, l_.profile(), &v, &err)) throw py::value_error(err);
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.upsert_pod(v);
+  }
+
   int check(const std::string& node, int64_t req) {
     std::lock_guard<std::mutex> g(l_.mu());
     return static_cast<int>(l_.check(node, req));
@@ -268,6 +287,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("upsert_pod", &Engine::upsert_pod)
       .def("remove_pod", &Engine::remove_pod)
       .def("known", &Engine::known)
+      .def("pod_state", &Engine::pod_state)
+      .def("upsert_pod_json", &Engine::upsert_pod_json)
       .def("check", &Engine::check)
       .def("filter", &Engine::filter)
       .def("assume", &Engine::assume)

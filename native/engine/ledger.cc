@@ -161,6 +161,16 @@ bool Ledger::remove_pod(const std::string& uid) {
 
 bool Ledger::known(const std::string& uid) const { return pods_.count(uid) != 0; }
 
+int Ledger::pod_state(const std::string& uid, int64_t* dev) const {
+  auto it = pods_.find(uid);
+  if (it == pods_.end()) {
+    *dev = -1;
+    return 0;
+  }
+  *dev = it->second.dev;
+  return it->second.assumed ? 2 : 1;
+}
+
 // ---------------------------------------------------------------- verbs
 
 Check Ledger::check(const std::string& node, int64_t req) const {

@@ -83,6 +83,10 @@ class Ledger {
   int upsert_pod(const PodView& v);
   bool remove_pod(const std::string& uid);
   bool known(const std::string& uid) const;
+  // 0 unknown, 1 accounted from annotations, 2 assumed (bind reservation not
+  // yet confirmed by the informer).  The controller uses it to decide whether
+  // an update event must be synced (pkg/gpushare/controller.go:257-305).
+  int pod_state(const std::string& uid, int64_t* dev) const;
 
   // ---- scheduling verbs ----
   Check check(const std::string& node, int64_t req) const;  // nodeinfo.go:113-137
