@@ -1,0 +1,351 @@
+#!/usr/bin/env python3
+"""Headline benchmark: pods bound/s, p50/p99 bind latency and gpu-mem binpack utilisation on N x MI355X.
+
+BASELINE.json metric/config: "8xMI355X: 32 pods x 64 GiB, binpack-first
+placement across all 8 devices" (1 GPU: 4 pods x 64 GiB on the single 288 GB
+device).  One rank per GPU (torchrun); per-GPU work is fixed (weak scaling):
+every step is one *wave* of ``pods_per_gpu x N`` pods of ``pod_gib`` GiB
+(``aliyun.com/gpu-mem``, the BASELINE naming) through the whole stack:
+
+  rank 0 (before touching the GPU) starts the fake kube-apiserver and the
+  scheduler extender as child processes, registers one node whose
+  ``gpu-mem``/``gpu-count`` come from the ranks' real MI355X HBM sizes, and
+  runs the kube-scheduler simulator (aggregate fit -> extender filter ->
+  async extender bind);  every rank runs a node agent for its own GPU:
+  Allocate (ASSIGNED=true, env, /dev nodes) -> the pod's slice of a real HBM
+  arena is stamped by a HIP kernel and every co-resident pod's stamps are
+  verified -> pod Running.  When all pods of the wave run, utilisation is
+  read from the extender's /inspect and from bytes resident in HBM; then the
+  wave is deleted and the step ends when the extender's ledger is empty.
+
+Timed region: exactly K steps bracketed by barrier + torch.cuda.synchronize()
+on both sides; the max over ranks is reported.  ``value`` = pods bound per
+second over the whole job (all GPUs).  Synthetic pods; no cluster, no real
+kubelet (there is none in this environment) — see SURVEY.md §4.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import statistics
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_BINDS_PER_S = 2.5  # derived reference ceiling (client-go QPS 5 / 2 calls per bind)
+NODE = "mi355x-node-0"
+
+
+class LoopThread:
+    """An asyncio loop in a daemon thread; the main thread keeps torch.distributed."""
+
+    def __init__(self):
+        self.loop = asyncio.new_event_loop()
+        self.t = threading.Thread(target=self.loop.run_forever, daemon=True, name="gsx-loop")
+        self.t.start()
+
+    def run(self, coro, timeout: float | None = None):
+        return asyncio.run_coroutine_threadsafe(coro, self.loop).result(timeout)
+
+    def stop(self):
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self.t.join(5)
+
+
+def pct(xs, q):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    k = min(len(xs) - 1, max(0, int(round(q / 100.0 * (len(xs) - 1)))))
+    return xs[k]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pods-per-gpu", type=int, default=4)
+    ap.add_argument("--pod-gib", type=int, default=64)
+    ap.add_argument("--profile", default="aliyun")
+    ap.add_argument("--bind-mode", default="binding", choices=["binding", "update"])
+    ap.add_argument("--devices", default="auto", help="auto|hip|amdsmi|fake (fake: no GPU, CPU plumbing only)")
+    ap.add_argument("--stamp-stride", type=int, default=1 << 20)
+    ap.add_argument("--json-out", default="")
+    ap.add_argument("--inproc", action="store_true",
+                    help="run apiserver + extender in this process (no child processes; used under rocprofv3)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run --nproc-per-node N")
+        a.gpus = world
+
+    # ---- rank 0 starts its child processes BEFORE anything initialises the GPU
+    children = []
+    api_url = ext_url = ""
+    lt = LoopThread()
+    inproc = []
+    if rank == 0 and a.inproc:
+        from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
+        from gpushare_scheduler_extender_amd.k8s.client import KubeClient as _KC
+        from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+        from gpushare_scheduler_extender_amd.models.profile import get_profile as _gp
+
+        api_r = lt.run(FakeApiServerRunner().start())
+        ext_r = lt.run(ExtenderRunner(ExtenderServer(_KC(api_r.url), _gp(a.profile), bind_mode=a.bind_mode)).start())
+        inproc = [ext_r, api_r]
+        api_url, ext_url = api_r.url, ext_r.url
+    elif rank == 0:
+        from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver, start_extender
+
+        api = start_apiserver()
+        children.append(api)
+        ext = start_extender(api.url, profile=a.profile, bind_mode=a.bind_mode)
+        children.append(ext)
+        api_url, ext_url = api.url, ext.url
+
+    import torch
+    import torch.distributed as dist
+
+    from gpushare_scheduler_extender_amd.deviceplugin.agent import NodeAgent
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import UNITS, discover
+    from gpushare_scheduler_extender_amd.deviceplugin.runtime import HbmArenaRuntime, LedgerRuntime
+    from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+    from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
+    from gpushare_scheduler_extender_amd.models.profile import get_profile
+    from gpushare_scheduler_extender_amd.sim.scheduler import SchedulerSim
+
+    profile = get_profile(a.profile)
+    use_gpu = a.devices != "fake" and torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl" if use_gpu else "gloo")
+        ctl = dist.new_group(backend="gloo")
+    else:
+        ctl = None
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if use_gpu:
+            torch.cuda.synchronize()
+
+    def bcast(obj):
+        if world == 1:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=0, group=ctl)
+        return box[0]
+
+    def gather(obj):
+        if world == 1:
+            return [obj]
+        out = [None] * world
+        dist.all_gather_object(out, obj, group=ctl)
+        return out
+
+    api_url, ext_url = bcast((api_url, ext_url))
+
+    # ---- this rank's GPU
+    backend, devs = discover("fake" if not use_gpu else a.devices)
+    if use_gpu:
+        mine = [d for d in devs if d.index == local_rank]
+        if not mine:
+            raise SystemExit(f"rank {rank}: GPU {local_rank} not found ({backend})")
+        dev = mine[0]
+    else:
+        dev = devs[local_rank % len(devs)]
+        dev.index = local_rank
+    dev.index = local_rank
+    unit = "GiB"
+    pod_bytes = a.pod_gib * UNITS[unit]
+    all_devs = gather(dev.to_dict())
+
+    arena = a.pods_per_gpu * pod_bytes
+    runtime = (HbmArenaRuntime({local_rank: arena}, stamp_stride=a.stamp_stride) if use_gpu
+               else LedgerRuntime({local_rank: arena}))
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import Device
+
+    agent_client = KubeClient(api_url)
+
+    async def setup_node():
+        c = KubeClient(api_url)
+        totals = [Device(**d).units(unit) for d in all_devs]
+        node = make_node(NODE, sum(totals), len(totals), profile=profile, device_totals=totals)
+        node["metadata"].setdefault("labels", {})["gpushare"] = "true"
+        await c.create("nodes", node)
+        await c.close()
+        return totals
+
+    totals = lt.run(setup_node()) if rank == 0 else None
+    totals = bcast(totals)
+    agent = NodeAgent(agent_client, NODE, [dev], profile, runtime, unit=unit, verify_each=True,
+                      mount_mode="isolated")
+    lt.run(agent.start())
+
+    sim = client = None
+    if rank == 0:
+        client = KubeClient(api_url)
+        sim = SchedulerSim(KubeClient(api_url), ext_url, profile, max_inflight_binds=256)
+        lt.run(sim.start())
+        # wait until the extender has seen the node
+        import urllib.request
+
+        for _ in range(2000):
+            with urllib.request.urlopen(ext_url + "/gpushare-scheduler/inspect") as r:
+                if json.loads(r.read()).get("nodes"):
+                    break
+            time.sleep(0.005)
+    barrier()
+
+    n_pods = a.pods_per_gpu * world
+    step_stats = []
+
+    async def wave(step: int):
+        import aiohttp
+
+        keys = [f"default/w{step}-p{i}" for i in range(n_pods)]
+        t0 = time.perf_counter()
+        await asyncio.gather(*(client.create("pods", make_pod(k.split("/")[1], a.pod_gib, profile=profile))
+                               for k in keys))
+        await sim.wait_bound(keys, 120)
+        t_bound = time.perf_counter()
+        # every pod admitted on its GPU and Running
+        while True:
+            ph = [((sim.pods.get(k) or {}).get("status") or {}).get("phase") for k in keys]
+            if all(p == "Running" for p in ph):
+                break
+            if any(p == "Failed" for p in ph):
+                raise RuntimeError(f"pod admission failed: {[k for k, p in zip(keys, ph) if p == 'Failed']}")
+            if time.perf_counter() - t0 > 120:
+                raise TimeoutError(f"pods not running: {ph}")
+            await asyncio.sleep(0.0005)
+        t_run = time.perf_counter()
+        async with aiohttp.ClientSession() as s:
+            async with s.get(ext_url + "/gpushare-scheduler/inspect") as r:
+                insp = json.loads(await r.read())
+        used = sum(n["usedGPU"] for n in insp["nodes"])
+        total = sum(n["totalGPU"] for n in insp["nodes"])
+        per_dev = [d["usedGPU"] for n in insp["nodes"] for d in n["devs"]]
+        # teardown: delete the wave, the step ends when the ledger is empty again
+        await asyncio.gather(*(client.delete("pods", k.split("/")[1], "default") for k in keys))
+        async with aiohttp.ClientSession() as s:
+            while True:
+                async with s.get(ext_url + "/gpushare-scheduler/inspect") as r:
+                    insp2 = json.loads(await r.read())
+                if sum(n["usedGPU"] for n in insp2["nodes"]) == 0:
+                    break
+                await asyncio.sleep(0.0005)
+        t_end = time.perf_counter()
+        tm = [sim.stats.timings[k] for k in keys]
+        res = {"bind_latency": [t.bound - t.seen for t in tm], "bind_rtt": [t.bind_rtt for t in tm],
+               "filter_rtt": [t.filter_rtt for t in tm], "used": used, "total": total, "per_dev": per_dev,
+               "t_bound": t_bound - t0, "t_run": t_run - t0, "t_total": t_end - t0, "attempts": [t.attempts for t in tm]}
+        sim.forget(keys)
+        return res
+
+    t_start = None
+    for step in range(a.warmup + a.steps):
+        if step == a.warmup:
+            barrier()
+            t_start = time.perf_counter()
+        if rank == 0:
+            r = lt.run(wave(step), timeout=600)
+            if step >= a.warmup:
+                step_stats.append(r)
+        if world > 1:
+            dist.barrier(group=ctl)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if use_gpu else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    bad = runtime.verify() if use_gpu else 0
+    agent_stats = gather({"admitted": agent.admitted, "failed": agent.failed, "bad_stamps": agent.bad_stamps + bad,
+                          "admit_p50_ms": (pct(agent.latency, 50) or 0) * 1e3,
+                          "hbm_total": dev.total_bytes, "arena": arena})
+
+    if rank == 0:
+        pods_total = n_pods * a.steps
+        value = pods_total / elapsed
+        lat = [x for s in step_stats for x in s["bind_latency"]]
+        rtt = [x for s in step_stats for x in s["bind_rtt"]]
+        frtt = [x for s in step_stats for x in s["filter_rtt"]]
+        util = statistics.mean(s["used"] / s["total"] for s in step_stats) if step_stats else 0.0
+        hbm_total = sum(x["hbm_total"] for x in agent_stats)
+        hbm_resident = n_pods * pod_bytes
+        out = {
+            "metric": "pods bound/sec",
+            "value": round(value, 3),
+            "unit": "pods/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1e3 * elapsed / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_BINDS_PER_S, 2),
+            "dtype": "bf16",
+            "data": "synthetic pods (random-init ledger, fake kube-apiserver); HBM slices on real MI355X" if use_gpu
+                    else "synthetic pods; fake devices (no GPU)",
+            "config": {"model": f"gpushare extender+device plugin: {a.pods_per_gpu} pods/GPU x {a.pod_gib} GiB "
+                                f"({profile.resource}), binpack", "global_batch": n_pods, "seq_len": 0,
+                       "parallelism": f"{world} GPU(s) advertised on 1 node, 1 node-agent rank per GPU",
+                       "bind_mode": a.bind_mode, "device_backend": backend},
+            "p50_bind_latency_ms": round(1e3 * pct(lat, 50), 3),
+            "p99_bind_latency_ms": round(1e3 * pct(lat, 99), 3),
+            "p50_bind_rtt_ms": round(1e3 * pct(rtt, 50), 3),
+            "p50_filter_rtt_ms": round(1e3 * pct(frtt, 50), 3),
+            "binpack_util_pct": round(100 * util, 2),
+            "per_device_used_gib": step_stats[-1]["per_dev"] if step_stats else [],
+            "device_gpu_mem_gib": totals,
+            "hbm_resident_pct": round(100 * hbm_resident / hbm_total, 2) if hbm_total else None,
+            "wave_ms": {"bound": round(1e3 * statistics.mean(s["t_bound"] for s in step_stats), 3),
+                        "running": round(1e3 * statistics.mean(s["t_run"] for s in step_stats), 3),
+                        "total": round(1e3 * statistics.mean(s["t_total"] for s in step_stats), 3)},
+            "bind_retries": sum(sum(s["attempts"]) - len(s["attempts"]) for s in step_stats),
+            "agents": agent_stats,
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+
+    # ---- teardown
+    try:
+        lt.run(agent.stop(), 30)
+        lt.run(agent_client.close(), 30)
+        if rank == 0:
+            lt.run(sim.stop(), 30)
+            lt.run(sim.client.close(), 30)
+            lt.run(client.close(), 30)
+            for r in inproc:
+                lt.run(r.stop(), 30)
+    finally:
+        runtime.close()
+        lt.stop()
+        for c in children:
+            c.stop()
+        if world > 1:
+            dist.barrier(group=ctl)
+            dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,181 @@
+"""Node agent: kubelet + device-plugin + container-runtime stand-in for one node (or some of its GPUs).
+
+Where there is no kubelet (tests, the simulator, ``bench.py``), this drives
+the same Allocate logic the gRPC device plugin serves to kubelet
+(:mod:`.allocator`), then "starts" the pod through a runtime
+(:mod:`.runtime`) and reports it Running — the tail of the reference's
+sequence diagram (``docs/designs/sequence.jpg``): bound pod -> Allocate ->
+``ASSIGNED=true`` -> container env -> pod runs on the chosen GPU.
+
+It watches only pods bound to its node (``fieldSelector=spec.nodeName``) and,
+with ``devices`` set, only those whose ``*_IDX`` annotation names one of its
+GPUs, so one agent per GPU (one per rank in ``bench.py``) can share a node.
+A pod that completes or is deleted is stopped and its slice (and CU
+partition) released.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import time
+
+from ..k8s.client import ApiError, KubeClient
+from ..k8s.informer import Handler, Informer, obj_key
+from ..models import pod as podutil
+from ..models.profile import NamingProfile
+from .allocator import CU_COUNT_ANNOTATION, CUPartitioner, assigned_patch, build_response, pick_pod
+from .devices import UNITS, Device
+from .runtime import AdmissionError
+
+log = logging.getLogger("gsx.agent")
+
+
+class NodeAgent:
+    def __init__(self, client: KubeClient, node: str, devices: list[Device], profile: NamingProfile, runtime, *,
+                 unit: str = "GiB", verify_each: bool = True, mount_mode: str = "isolated", report_status: bool = True,
+                 workers: int = 8):
+        self.client = client
+        self.node = node
+        self.devices = {d.index: d for d in devices}
+        self.profile = profile
+        self.runtime = runtime
+        self.unit_bytes = UNITS[unit]
+        self.verify_each = verify_each
+        self.mount_mode = mount_mode
+        self.report_status = report_status
+        self.cus = {d.index: CUPartitioner(d.cu_count, d.xcc_count) for d in devices}
+        self.pods = Informer(client, "pods", field_selector=f"spec.nodeName={node}")
+        self.running: dict[str, str] = {}  # uid -> pod key
+        self.inflight: set[str] = set()
+        self.allocations: dict[str, dict] = {}  # uid -> container env of the last Allocate
+        self.admitted = 0
+        self.failed = 0
+        self.bad_stamps = 0
+        self.latency: list[float] = []  # bound-observed -> Running
+        self._bg: set[asyncio.Task] = set()
+        self.queue: asyncio.Queue = asyncio.Queue()
+        self.queued: set[str] = set()
+        self.seen: dict[str, float] = {}
+        self.workers = workers
+        self.pods.add_handler(Handler(self._on_pod, lambda o, n, r: self._on_pod(n, r), self._on_delete))
+
+    def _mine(self, pod: dict) -> bool:
+        return podutil.gpu_id_from_annotation(pod, self.profile) in self.devices
+
+    def _on_pod(self, pod: dict, raw):
+        uid = podutil.meta(pod).get("uid", "")
+        if podutil.is_complete(pod):
+            self._stop(uid)
+            return
+        if not podutil.is_gpushare_pod(pod, self.profile) or not self._mine(pod):
+            return
+        ann = podutil.annotations(pod)
+        if (ann.get(self.profile.annotation_assigned) == "false" and uid not in self.inflight
+                and uid not in self.running and uid not in self.queued):
+            self.queued.add(uid)
+            self.seen.setdefault(uid, time.perf_counter())
+            self.queue.put_nowait(obj_key(pod))
+
+    def _on_delete(self, pod: dict, raw):
+        self._stop(podutil.meta(pod).get("uid", ""))
+
+    def _stop(self, uid: str):
+        if uid in self.running:
+            self.running.pop(uid, None)
+            self.runtime.stop(uid)
+            for p in self.cus.values():
+                p.release(uid)
+
+    async def _worker(self):
+        while True:
+            key = await self.queue.get()
+            pod = self.pods.get(key)
+            if pod is None:
+                continue
+            self.queued.discard(podutil.meta(pod).get("uid", ""))
+            await self._admit(key)
+
+    async def _admit(self, key: str):
+        """One kubelet Allocate for the container(s) of the pod behind ``key``."""
+        pod = self.pods.get(key)
+        uid = podutil.meta(pod).get("uid", "") if pod else ""
+        try:
+            if pod is None or uid in self.running or uid in self.inflight:
+                return
+            units = podutil.gpu_mem_request(pod, self.profile)
+            # kubelet's Allocate(N ids): pick the pod exactly as the device plugin does —
+            # earliest ASSUME_TIME among unassigned pods of that size (not yet claimed here)
+            busy = self.inflight | set(self.running)
+            chosen = pick_pod([p for p in self.pods.list()
+                               if podutil.meta(p).get("uid") not in busy and self._mine(p)],
+                              self.node, units, self.profile)
+            if chosen is None:
+                return
+            cuid = podutil.meta(chosen).get("uid", "")
+            if cuid != uid:
+                # an earlier same-size pod wins this Allocate; ours is served by the next one
+                self.queued.add(uid)
+                self.queue.put_nowait(key)
+                key, pod, uid = obj_key(chosen), chosen, cuid
+            self.inflight.add(uid)
+            t0 = self.seen.get(uid, time.perf_counter())
+            dev_idx = podutil.gpu_id_from_annotation(pod, self.profile)
+            device = self.devices[dev_idx]
+            cus = None
+            want_cus = podutil.annotations(pod).get(CU_COUNT_ANNOTATION)
+            if want_cus:
+                cus = self.cus[dev_idx].allocate(uid, int(want_cus))
+            alloc = build_response(pod, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
+            try:
+                await self.client.patch("pods", podutil.meta(pod)["name"], assigned_patch(pod, self.profile,
+                                        alloc.annotations), podutil.meta(pod)["namespace"])
+            except ApiError as e:
+                if e.conflict:  # stale copy: retry from the informer's latest version
+                    if cus:
+                        self.cus[dev_idx].release(uid)
+                    if uid not in self.queued:
+                        self.queued.add(uid)
+                        asyncio.get_running_loop().call_later(0.001, self.queue.put_nowait, key)
+                    return
+                raise
+            self.allocations[uid] = alloc.envs
+            try:
+                self.runtime.start(uid, dev_idx, units * self.unit_bytes, cus)
+                if self.verify_each:
+                    bad = self.runtime.verify()
+                    if bad:
+                        self.bad_stamps += bad
+                        raise AdmissionError(f"{bad} bad HBM stamps after admitting {key}")
+            except AdmissionError as e:
+                self.failed += 1
+                log.error("admission of %s on GPU %d failed: %s", key, dev_idx, e)
+                self.runtime.stop(uid)
+                if self.report_status:
+                    await self.client.patch("pods", podutil.meta(pod)["name"],
+                                            {"status": {"phase": "Failed", "reason": "UnexpectedAdmissionError",
+                                                        "message": str(e)}},
+                                            podutil.meta(pod)["namespace"], sub="status")
+                return
+            self.running[uid] = key
+            self.admitted += 1
+            if self.report_status:
+                await self.client.patch("pods", podutil.meta(pod)["name"], {"status": {"phase": "Running"}},
+                                        podutil.meta(pod)["namespace"], sub="status")
+            self.latency.append(time.perf_counter() - t0)
+            self.seen.pop(uid, None)
+        except Exception as e:  # noqa: BLE001
+            log.exception("admit %s: %r", key, e)
+        finally:
+            self.inflight.discard(uid)
+
+    async def start(self):
+        await self.pods.start()
+        await self.pods.wait_synced(30)
+        for i in range(self.workers):
+            t = asyncio.get_running_loop().create_task(self._worker(), name=f"agent-{self.node}-{i}")
+            self._bg.add(t)
+
+    async def stop(self):
+        for t in list(self._bg):
+            t.cancel()
+        await self.pods.stop()

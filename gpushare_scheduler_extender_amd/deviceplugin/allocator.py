@@ -1,0 +1,173 @@
+"""Device-plugin Allocate logic (kubelet -> plugin -> pod), shared by the gRPC plugin and the node agent.
+
+Behaviour reconstructed from ``docs/designs/designs.md:93-103`` and
+``docs/designs/sequence.jpg`` (the plugin itself is not in the reference tree,
+SURVEY.md §2.8):
+
+1. kubelet asks for N fake device IDs (N = gpu-mem units of the container);
+2. the plugin lists this node's Pending gpushare pods whose ``ASSIGNED``
+   annotation is ``false``, ordered by ``ASSUME_TIME`` (earliest first), and
+   takes the first whose request equals N;
+3. it flips ``ASSIGNED`` to ``true`` (with a resourceVersion precondition, so
+   two Allocates can never claim the same pod) — the commit point;
+4. it returns the container's environment and device nodes.
+
+MI355X-specific response: ``/dev/kfd`` + the chosen GPU's
+``/dev/dri/renderD*`` / ``card*`` nodes, ``HIP_VISIBLE_DEVICES`` /
+``ROCR_VISIBLE_DEVICES`` (0 inside the container when only that GPU's nodes
+are mounted, the host index otherwise), the ``*_IDX/_DEV/_POD/_CONTAINER``
+variables the sample workload reads (``samples/docker/run.sh:3-6``), a memory
+fraction for ``torch.cuda.set_per_process_memory_fraction``, and — optional —
+a per-pod CU partition (``HSA_CU_MASK`` + ``GSX_CU_MASK``), the stand-in for
+the reference's "integrate Nvidia MPS" roadmap item (``README.md:77``).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+from ..models import pod as podutil
+from ..models.profile import POD_ASSIGN_TIME_ANNOTATION, POD_CU_MASK_ANNOTATION, NamingProfile
+from .devices import Device
+
+CU_COUNT_ANNOTATION = "gpushare.amd.com/cu-count"  # pod asks for a CU partition of this size
+
+
+@dataclass
+class ContainerAllocation:
+    envs: dict[str, str]
+    devices: list[dict]  # {container_path, host_path, permissions}
+    annotations: dict[str, str] = field(default_factory=dict)
+    mounts: list[dict] = field(default_factory=list)
+
+
+class AllocateError(Exception):
+    pass
+
+
+def candidate_pods(pods: list[dict], node: str, profile: NamingProfile) -> list[dict]:
+    """Pending gpushare pods on ``node`` not yet assigned, earliest ASSUME_TIME first."""
+    out = []
+    for p in pods:
+        if podutil.node_name(p) != node or podutil.phase(p) not in ("Pending", ""):
+            continue
+        if podutil.is_complete(p) or not podutil.is_gpushare_pod(p, profile):
+            continue
+        ann = podutil.annotations(p)
+        if ann.get(profile.annotation_assigned) != "false":
+            continue
+        if podutil.gpu_id_from_annotation(p, profile) < 0:
+            continue
+        out.append(p)
+    out.sort(key=lambda p: (podutil.assume_time(p, profile), podutil.meta(p).get("creationTimestamp", ""),
+                            podutil.pod_key(p)))
+    return out
+
+
+def pick_pod(pods: list[dict], node: str, units: int, profile: NamingProfile) -> dict | None:
+    for p in candidate_pods(pods, node, profile):
+        if podutil.gpu_mem_request(p, profile) == units:
+            return p
+    return None
+
+
+class CUPartitioner:
+    """Per-device ledger of compute units handed to pods as CU masks.
+
+    A partition is spread evenly over the XCDs (CU ``c`` of a 256-CU MI355X is
+    logical CU ``c``; ROCr stripes logical CUs over XCDs/SEs, so contiguous
+    ranges in *per-XCD* order keep each pod's work on every L2 slice).  The
+    bitmap words are what ``hipExtStreamCreateWithCUMask`` and ``HSA_CU_MASK``
+    take.
+    """
+
+    def __init__(self, cu_count: int = 256, xcc_count: int = 8):
+        self.cu_count = cu_count
+        self.xcc_count = max(1, xcc_count)
+        self.owner: list[str | None] = [None] * cu_count
+
+    def _order(self) -> list[int]:
+        per = self.cu_count // self.xcc_count
+        # round-robin over XCDs: xcc0 cu0, xcc1 cu0, ... (logical ids are xcc-major blocks of `per`)
+        return [x * per + i for i in range(per) for x in range(self.xcc_count)]
+
+    def allocate(self, uid: str, n: int) -> list[int]:
+        if n <= 0 or n > self.cu_count:
+            raise AllocateError(f"invalid CU partition size {n}")
+        mine = [c for c, o in enumerate(self.owner) if o == uid]
+        if mine:
+            return mine
+        free = [c for c in self._order() if self.owner[c] is None]
+        if len(free) < n:
+            raise AllocateError(f"only {len(free)} CUs free, {n} requested")
+        got = sorted(free[:n])
+        for c in got:
+            self.owner[c] = uid
+        return got
+
+    def release(self, uid: str) -> int:
+        n = 0
+        for c, o in enumerate(self.owner):
+            if o == uid:
+                self.owner[c] = None
+                n += 1
+        return n
+
+    def free_count(self) -> int:
+        return sum(1 for o in self.owner if o is None)
+
+    @staticmethod
+    def words(cus: list[int], cu_count: int = 256) -> list[int]:
+        w = [0] * ((cu_count + 31) // 32)
+        for c in cus:
+            w[c // 32] |= 1 << (c % 32)
+        return w
+
+    @staticmethod
+    def ranges(cus: list[int]) -> str:
+        """``0-7,32-39`` — the list syntax of ROCr's HSA_CU_MASK."""
+        cus = sorted(cus)
+        out = []
+        i = 0
+        while i < len(cus):
+            j = i
+            while j + 1 < len(cus) and cus[j + 1] == cus[j] + 1:
+                j += 1
+            out.append(f"{cus[i]}" if i == j else f"{cus[i]}-{cus[j]}")
+            i = j + 1
+        return ",".join(out)
+
+
+def build_response(pod: dict, device: Device, container_units: int, profile: NamingProfile, *,
+                   mount_mode: str = "isolated", cus: list[int] | None = None) -> ContainerAllocation:
+    """Env + device nodes for one container of ``pod`` on ``device``."""
+    idx = device.index
+    dev_total = int(podutil.annotations(pod).get(profile.annotation_dev, "0") or 0)
+    pod_mem = podutil.gpu_mem_request(pod, profile)
+    visible = "0" if mount_mode == "isolated" else str(idx)
+    envs = {
+        "HIP_VISIBLE_DEVICES": visible,
+        "ROCR_VISIBLE_DEVICES": visible,
+        profile.annotation_idx: str(idx),
+        profile.annotation_dev: str(dev_total),
+        profile.annotation_pod: str(pod_mem),
+        profile.env_container: str(container_units),
+        "GSX_GPU_MEM_FRACTION": f"{(container_units / dev_total) if dev_total else 0.0:.6f}",
+        "GSX_GPU_BDF": device.bdf,
+    }
+    ann = {}
+    if cus:
+        envs["GSX_CU_MASK"] = ",".join(f"0x{w:08x}" for w in CUPartitioner.words(cus, device.cu_count))
+        envs["HSA_CU_MASK"] = f"{visible}:{CUPartitioner.ranges(cus)}"
+        ann[POD_CU_MASK_ANNOTATION] = envs["GSX_CU_MASK"]
+    nodes = device.device_nodes() if mount_mode == "isolated" else []
+    devs = [{"container_path": p, "host_path": p, "permissions": "rw"} for p in nodes]
+    return ContainerAllocation(envs=envs, devices=devs, annotations=ann)
+
+
+def assigned_patch(pod: dict, profile: NamingProfile, extra: dict | None = None) -> dict:
+    """Merge patch flipping ASSIGNED to true, guarded by the pod's resourceVersion."""
+    ann = {profile.annotation_assigned: "true", POD_ASSIGN_TIME_ANNOTATION: str(time.time_ns())}
+    if extra:
+        ann.update(extra)
+    return {"metadata": {"resourceVersion": podutil.meta(pod).get("resourceVersion"), "annotations": ann}}

@@ -1,0 +1,139 @@
+"""Pod "container runtimes" for the node agent: where an admitted pod's gpu-mem physically lives.
+
+kubelet + the container runtime start a pod's containers after the device
+plugin's Allocate; here (no kubelet) the node agent does it through a
+runtime:
+
+* :class:`HbmArenaRuntime` — the MI355X path.  Each device holds one HBM
+  arena sized to what the node advertises; an admitted pod gets a 2 MiB
+  aligned slice (first fit), the slice is stamped with the pod's tag by a HIP
+  kernel and every resident pod's stamps are verified after each admission.
+  A binpack decision that overcommits a device, or two pods sharing bytes,
+  shows up as a failed admission or as bad stamps — on real HBM;
+* :class:`LedgerRuntime` — the same slice accounting without a GPU
+  (CPU tests, simulator).
+"""
+from __future__ import annotations
+
+import hashlib
+import threading
+
+ALIGN = 2 << 20
+
+
+class AdmissionError(Exception):
+    pass
+
+
+class _Slices:
+    """First-fit allocator of aligned [offset, offset+size) slices in one arena."""
+
+    def __init__(self, capacity: int):
+        self.capacity = capacity
+        self.used: dict[str, tuple[int, int]] = {}
+
+    def alloc(self, uid: str, size: int) -> int:
+        if uid in self.used:
+            return self.used[uid][0]
+        size = (size + ALIGN - 1) // ALIGN * ALIGN
+        pos = 0
+        for off, sz in sorted(self.used.values()):
+            if off - pos >= size:
+                break
+            pos = max(pos, off + sz)
+        if pos + size > self.capacity:
+            raise AdmissionError(f"arena exhausted: need {size} B at {pos}, capacity {self.capacity}")
+        self.used[uid] = (pos, size)
+        return pos
+
+    def free(self, uid: str) -> tuple[int, int] | None:
+        return self.used.pop(uid, None)
+
+    def bytes_used(self) -> int:
+        return sum(sz for _, sz in self.used.values())
+
+
+def pod_tag(uid: str) -> int:
+    return int.from_bytes(hashlib.blake2b(uid.encode(), digest_size=8).digest(), "little") | 1
+
+
+class LedgerRuntime:
+    def __init__(self, capacities: dict[int, int]):
+        self.slices = {d: _Slices(c) for d, c in capacities.items()}
+        self.where: dict[str, int] = {}
+        self.lock = threading.Lock()
+
+    def start(self, uid: str, dev: int, nbytes: int, cus: list[int] | None = None) -> int:
+        with self.lock:
+            if dev not in self.slices:
+                raise AdmissionError(f"device {dev} not managed here")
+            off = self.slices[dev].alloc(uid, nbytes)
+            self.where[uid] = dev
+            return off
+
+    def stop(self, uid: str) -> bool:
+        with self.lock:
+            dev = self.where.pop(uid, None)
+            if dev is None:
+                return False
+            self.slices[dev].free(uid)
+            return True
+
+    def verify(self) -> int:
+        return 0
+
+    def resident_bytes(self, dev: int) -> int:
+        return self.slices[dev].bytes_used()
+
+    def close(self):
+        pass
+
+
+class HbmArenaRuntime(LedgerRuntime):
+    def __init__(self, capacities: dict[int, int], stamp_stride: int = 1 << 20, scrub_on_exit: bool = False):
+        super().__init__(capacities)
+        from ..ops import hip  # noqa: PLC0415
+
+        self.hip = hip
+        self.stride = stamp_stride
+        self.scrub = scrub_on_exit
+        self.arena = {d: hip.DeviceBuffer(d, c) for d, c in capacities.items()}
+        self.stream = {d: hip.Stream(d) for d in capacities}
+        self.stamps = 0
+        self.verified = 0
+
+    def start(self, uid: str, dev: int, nbytes: int, cus: list[int] | None = None) -> int:
+        off = super().start(uid, dev, nbytes, cus)
+        size = self.slices[dev].used[uid][1]
+        self.hip.hbm_stamp(self.stream[dev], self.arena[dev].addr(off), size, self.stride, pod_tag(uid))
+        self.stamps += 1
+        return off
+
+    def stop(self, uid: str) -> bool:
+        with self.lock:
+            dev = self.where.get(uid)
+            sl = self.slices[dev].used.get(uid) if dev is not None else None
+        if sl is not None and self.scrub:
+            self.hip.hbm_fill(self.stream[dev], self.arena[dev].addr(sl[0]), sl[1], 0)
+        return super().stop(uid)
+
+    def verify(self) -> int:
+        """Verify every resident pod's stamps; returns the number of bad stamps."""
+        bad = 0
+        with self.lock:
+            items = [(uid, dev, self.slices[dev].used[uid]) for uid, dev in self.where.items()]
+        for uid, dev, (off, size) in items:
+            bad += self.hip.hbm_verify(self.stream[dev], self.arena[dev].addr(off), size, self.stride, pod_tag(uid))
+            self.verified += 1
+        return bad
+
+    def sync(self):
+        for s in self.stream.values():
+            s.sync()
+
+    def close(self):
+        for s in self.stream.values():
+            s.sync()
+            s.destroy()
+        for a in self.arena.values():
+            a.free()

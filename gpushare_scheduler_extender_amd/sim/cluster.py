@@ -1,0 +1,77 @@
+"""Process-level harness: run the fake apiserver and the extender as child processes.
+
+kube-apiserver and the extender are separate processes in a real cluster
+(``config/gpushare-schd-extender.yaml``); the benchmark keeps them separate
+too, so the extender's event loop is not shared with the load generator.
+Children are started with ``subprocess.Popen`` (fork+exec happens in the
+child; callers start them before touching the GPU).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+
+
+def _wait_port(path: str, proc: subprocess.Popen, timeout: float = 60.0) -> int:
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        if os.path.exists(path):
+            with open(path) as f:
+                s = f.read().strip()
+            if s:
+                return int(s)
+        if proc.poll() is not None:
+            raise RuntimeError(f"child exited with {proc.returncode} before listening")
+        time.sleep(0.02)
+    raise TimeoutError(f"child did not publish a port in {path}")
+
+
+class ChildProc:
+    def __init__(self, args: list[str], name: str, env: dict | None = None):
+        self.tmp = tempfile.mkdtemp(prefix=f"gsx-{name}-")
+        self.port_file = os.path.join(self.tmp, "port")
+        self.log_path = os.path.join(self.tmp, "log")
+        e = dict(os.environ)
+        e["PYTHONPATH"] = str(ROOT) + os.pathsep + e.get("PYTHONPATH", "")
+        e.setdefault("GSX_AUTOBUILD", "0")
+        if env:
+            e.update(env)
+        self.log = open(self.log_path, "w")
+        self.proc = subprocess.Popen([sys.executable, *args, "--port-file", self.port_file], stdout=self.log,
+                                     stderr=subprocess.STDOUT, env=e, cwd=str(ROOT))
+        self.port = _wait_port(self.port_file, self.proc)
+        self.url = f"http://127.0.0.1:{self.port}"
+
+    def tail(self, n: int = 40) -> str:
+        try:
+            with open(self.log_path) as f:
+                return "".join(f.readlines()[-n:])
+        except OSError:
+            return ""
+
+    def stop(self):
+        if self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(5)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait(5)
+        self.log.close()
+
+
+def start_apiserver() -> ChildProc:
+    return ChildProc(["-m", "gpushare_scheduler_extender_amd.k8s.fakeapi", "--port", "0"], "apiserver")
+
+
+def start_extender(apiserver: str, profile: str = "shared-gpu", bind_mode: str = "binding", threadness: int = 1,
+                   log_level: str = "warning") -> ChildProc:
+    return ChildProc(["-m", "gpushare_scheduler_extender_amd.extender", "--host", "127.0.0.1", "--port", "0",
+                      "--apiserver", apiserver, "--profile", profile, "--bind-mode", bind_mode,
+                      "--threadness", str(threadness), "--log-level", log_level], "extender")

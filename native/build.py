@@ -158,7 +158,7 @@ TARGETS = {
     "tools": build_tools,
     "asan": build_asan,
 }
-DEFAULT = ["engine", "mxdev", "kernels", "tools"]
+DEFAULT = ["engine", "kernels"]
 
 
 def main(argv: list[str] | None = None) -> int:

@@ -1,0 +1,397 @@
+// MI355X (gfx950 / CDNA4) kernels of the GPU-share stack.  See gsx_kernels.h.
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "gsx_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(hipError_t e, const char* what) {
+  char buf[256];
+  std::snprintf(buf, sizeof(buf), "%s: %s (%d)", what, hipGetErrorString(e), static_cast<int>(e));
+  g_err = buf;
+  return static_cast<int>(e);
+}
+
+int fail_arg(const char* what) {
+  g_err = what;
+  return static_cast<int>(hipErrorInvalidValue);
+}
+
+#define GSX_CHECK(call)                       \
+  do {                                        \
+    hipError_t _e = (call);                   \
+    if (_e != hipSuccess) return fail(_e, #call); \
+  } while (0)
+
+// ------------------------------------------------------------------ CU probe
+
+__global__ __launch_bounds__(64) void cuprobe_kernel(uint32_t* out, int spin) {
+  uint32_t hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  // keep the workgroup resident for a while so the dispatcher spreads the
+  // grid over every CU the queue's mask allows
+  float x = static_cast<float>(threadIdx.x);
+  for (int i = 0; i < spin; ++i) x = __builtin_fmaf(x, 1.0000001f, 0.5f);
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = hw;
+    out[2 * blockIdx.x + 1] = xcc | (x == -1.0f ? 0x80000000u : 0u);
+  }
+}
+
+// ------------------------------------------------------------------ HBM stamp / verify / fill
+
+struct Stamp {
+  uint64_t tag;
+  uint64_t off;
+};
+
+__global__ __launch_bounds__(256) void stamp_kernel(char* base, uint64_t n, uint64_t stride, uint64_t tag) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    Stamp s{tag, i * stride};
+    *reinterpret_cast<Stamp*>(base + i * stride) = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void verify_kernel(const char* base, uint64_t n, uint64_t stride, uint64_t tag,
+                                                     unsigned long long* bad) {
+  uint32_t mine = 0;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    Stamp s = *reinterpret_cast<const Stamp*>(base + i * stride);
+    mine += (s.tag != tag || s.off != i * stride) ? 1u : 0u;
+  }
+  // wave64 reduction, one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+  if ((threadIdx.x & 63) == 0 && mine) atomicAdd(bad, static_cast<unsigned long long>(mine));
+}
+
+__global__ __launch_bounds__(256) void fill_kernel(uint4* p, uint64_t n16, uint32_t pat) {
+  uint4 v = make_uint4(pat, pat, pat, pat);
+  uint64_t i = blockIdx.x * 256ull + threadIdx.x;
+  const uint64_t step = gridDim.x * 256ull;
+  // 4 independent 16-B stores in flight per lane
+  for (; i + 3 * step < n16; i += 4 * step) {
+    p[i] = v;
+    p[i + step] = v;
+    p[i + 2 * step] = v;
+    p[i + 3 * step] = v;
+  }
+  for (; i < n16; i += step) p[i] = v;
+}
+
+// ------------------------------------------------------------------ bf16 MFMA GEMM (C = A * B^T)
+//
+// 128x128x64 tile, 256 threads = 4 waves in 2x2, each wave 64x64 of C as a
+// 4x4 grid of v_mfma_f32_16x16x32_bf16 tiles.  Operands are register-staged
+// into a double-buffered, XOR-swizzled LDS image (one __shared__ array):
+// 16-B chunk c of row r lives at slot c ^ ((r >> 1) & 7), which spreads the
+// 16 rows one ds_read_b128 lane group touches over all sixteen 16-B slots of
+// two 256-B bank rows.  One barrier per K-tile: tile k+1 is fetched into
+// registers before the MFMAs on tile k and written to the other buffer after.
+// Workgroup ids are remapped so consecutive output tiles share an XCD's L2
+// (bijective for any grid size).
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE_BYTES = BM * BK * 2;  // 16 KiB per operand per buffer
+
+__device__ __forceinline__ uint32_t swz(int row, int chunk) {
+  return static_cast<uint32_t>(row * (BK * 2) + ((chunk ^ ((row >> 1) & 7)) << 4));
+}
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return static_cast<uint16_t>((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(const uint16_t* __restrict__ A,
+                                                              const uint16_t* __restrict__ B,
+                                                              uint16_t* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char lds[4 * TILE_BYTES];  // [buf][A|B]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+
+  // XCD-aware bijective remap of the workgroup id
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int ntn = N / BN;
+  const int tm = wg / ntn, tn = wg % ntn;
+  const int row0 = tm * BM, col0 = tn * BN;
+
+  const uint16_t* Ab = A + static_cast<size_t>(row0) * K;
+  const uint16_t* Bb = B + static_cast<size_t>(col0) * K;
+
+  uint4 ra[4], rb[4];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int id = tid + i * 256;
+      int rr = id >> 3, ch = id & 7;
+      ra[i] = *reinterpret_cast<const uint4*>(Ab + static_cast<size_t>(rr) * K + kt * BK + ch * 8);
+      rb[i] = *reinterpret_cast<const uint4*>(Bb + static_cast<size_t>(rr) * K + kt * BK + ch * 8);
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* la = lds + buf * 2 * TILE_BYTES;
+    char* lb = la + TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int id = tid + i * 256;
+      int rr = id >> 3, ch = id & 7;
+      *reinterpret_cast<uint4*>(la + swz(rr, ch)) = ra[i];
+      *reinterpret_cast<uint4*>(lb + swz(rr, ch)) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const char* la = lds + buf * 2 * TILE_BYTES;
+    const char* lb = la + TILE_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[4], bfr[4];
+      const int ch = kk * 4 + fq;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) af[m] = *reinterpret_cast<const bf16x8*>(la + swz(wr * 64 + m * 16 + fr, ch));
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bfr[n] = *reinterpret_cast<const bf16x8*>(lb + swz(wc * 64 + n * 16 + fr, ch));
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+    }
+    if (kt + 1 < nk) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  // epilogue: C/D map of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + j
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int rr = row0 + wr * 64 + m * 16 + fq * 4 + j;
+        int cc = col0 + wc * 64 + n * 16 + fr;
+        C[static_cast<size_t>(rr) * N + cc] = f2bf(acc[m][n][j]);
+      }
+}
+
+std::mutex g_mu;
+unsigned long long* g_counter[64] = {nullptr};
+
+hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+int grid_for(uint64_t n, int per_block, int max_blocks) {
+  uint64_t g = (n + per_block - 1) / per_block;
+  if (g > static_cast<uint64_t>(max_blocks)) g = max_blocks;
+  return g < 1 ? 1 : static_cast<int>(g);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gsx_last_error(void) { return g_err.c_str(); }
+
+int gsx_device_count(int* n) {
+  GSX_CHECK(hipGetDeviceCount(n));
+  return 0;
+}
+
+int gsx_device_info(int dev, gsx_devinfo* out) {
+  hipDeviceProp_t p;
+  GSX_CHECK(hipGetDeviceProperties(&p, dev));
+  std::memset(out, 0, sizeof(*out));
+  std::snprintf(out->name, sizeof(out->name), "%s", p.name);
+  std::snprintf(out->arch, sizeof(out->arch), "%s", p.gcnArchName);
+  GSX_CHECK(hipDeviceGetPCIBusId(out->pci_bus_id, sizeof(out->pci_bus_id), dev));
+  out->total_mem = p.totalGlobalMem;
+  out->cu_count = p.multiProcessorCount;
+  out->clock_khz = p.clockRate;
+  out->wave_size = p.warpSize;
+  out->lds_per_block = p.sharedMemPerBlock;
+  return 0;
+}
+
+int gsx_mem_info(int dev, uint64_t* free_b, uint64_t* total_b) {
+  GSX_CHECK(hipSetDevice(dev));
+  size_t f = 0, t = 0;
+  GSX_CHECK(hipMemGetInfo(&f, &t));
+  *free_b = f;
+  *total_b = t;
+  return 0;
+}
+
+int gsx_synchronize(int dev) {
+  GSX_CHECK(hipSetDevice(dev));
+  GSX_CHECK(hipDeviceSynchronize());
+  return 0;
+}
+
+int gsx_stream_create(int dev, const uint32_t* cu_mask, int mask_words, void** stream) {
+  GSX_CHECK(hipSetDevice(dev));
+  hipStream_t s;
+  if (mask_words > 0) {
+    GSX_CHECK(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask_words), cu_mask));
+  } else {
+    GSX_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  }
+  *stream = s;
+  return 0;
+}
+
+int gsx_stream_get_mask(void* stream, uint32_t* cu_mask, int mask_words) {
+  GSX_CHECK(hipExtStreamGetCUMask(S(stream), static_cast<uint32_t>(mask_words), cu_mask));
+  return 0;
+}
+
+int gsx_stream_destroy(void* stream) {
+  GSX_CHECK(hipStreamDestroy(S(stream)));
+  return 0;
+}
+
+int gsx_stream_sync(void* stream) {
+  GSX_CHECK(hipStreamSynchronize(S(stream)));
+  return 0;
+}
+
+int gsx_malloc(int dev, uint64_t bytes, void** ptr) {
+  GSX_CHECK(hipSetDevice(dev));
+  GSX_CHECK(hipMalloc(ptr, bytes));
+  return 0;
+}
+
+int gsx_free(void* ptr) {
+  GSX_CHECK(hipFree(ptr));
+  return 0;
+}
+
+int gsx_memcpy_d2h(void* dst, const void* src, uint64_t bytes) {
+  GSX_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int gsx_memcpy_h2d(void* dst, const void* src, uint64_t bytes) {
+  GSX_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int gsx_cuprobe(void* stream, int blocks, int spin, uint32_t* out_host) {
+  if (blocks <= 0 || blocks > (1 << 20) || spin < 0) return fail_arg("gsx_cuprobe: bad blocks/spin");
+  uint32_t* d = nullptr;
+  GSX_CHECK(hipMallocAsync(reinterpret_cast<void**>(&d), sizeof(uint32_t) * 2 * blocks, S(stream)));
+  hipLaunchKernelGGL(cuprobe_kernel, dim3(blocks), dim3(64), 0, S(stream), d, spin);
+  GSX_CHECK(hipGetLastError());
+  GSX_CHECK(hipMemcpyAsync(out_host, d, sizeof(uint32_t) * 2 * blocks, hipMemcpyDeviceToHost, S(stream)));
+  GSX_CHECK(hipFreeAsync(d, S(stream)));
+  GSX_CHECK(hipStreamSynchronize(S(stream)));
+  return 0;
+}
+
+int gsx_hbm_stamp(void* stream, void* base, uint64_t bytes, uint64_t stride, uint64_t tag) {
+  if (!base || stride < sizeof(Stamp) || stride % 16) return fail_arg("gsx_hbm_stamp: stride must be >=16, %16");
+  if (reinterpret_cast<uintptr_t>(base) % 16) return fail_arg("gsx_hbm_stamp: base not 16-B aligned");
+  uint64_t n = bytes / stride;
+  if (!n) return 0;
+  hipLaunchKernelGGL(stamp_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, S(stream), static_cast<char*>(base),
+                     n, stride, tag);
+  GSX_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gsx_hbm_verify(void* stream, const void* base, uint64_t bytes, uint64_t stride, uint64_t tag, uint64_t* bad) {
+  if (!base || stride < sizeof(Stamp) || stride % 16) return fail_arg("gsx_hbm_verify: stride must be >=16, %16");
+  if (reinterpret_cast<uintptr_t>(base) % 16) return fail_arg("gsx_hbm_verify: base not 16-B aligned");
+  uint64_t n = bytes / stride;
+  *bad = 0;
+  if (!n) return 0;
+  int dev = 0;
+  GSX_CHECK(hipGetDevice(&dev));
+  unsigned long long* ctr;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (dev < 0 || dev >= 64) return fail_arg("gsx_hbm_verify: device index");
+    if (!g_counter[dev]) GSX_CHECK(hipMalloc(reinterpret_cast<void**>(&g_counter[dev]), 64));
+    ctr = g_counter[dev];
+  }
+  GSX_CHECK(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), S(stream)));
+  hipLaunchKernelGGL(verify_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, S(stream),
+                     static_cast<const char*>(base), n, stride, tag, ctr);
+  GSX_CHECK(hipGetLastError());
+  unsigned long long h = 0;
+  GSX_CHECK(hipMemcpyAsync(&h, ctr, sizeof(h), hipMemcpyDeviceToHost, S(stream)));
+  GSX_CHECK(hipStreamSynchronize(S(stream)));
+  *bad = h;
+  return 0;
+}
+
+int gsx_hbm_fill(void* stream, void* base, uint64_t bytes, uint32_t pattern) {
+  if (!base || bytes % 16 || reinterpret_cast<uintptr_t>(base) % 16) return fail_arg("gsx_hbm_fill: need 16-B multiple");
+  uint64_t n16 = bytes / 16;
+  if (!n16) return 0;
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n16, 256 * 4, 256 * 16)), dim3(256), 0, S(stream),
+                     static_cast<uint4*>(base), n16, pattern);
+  GSX_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gsx_gemm_bf16_nt(void* stream, const void* A, const void* B, void* C, int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK)
+    return fail_arg("gsx_gemm_bf16_nt: need M%128==0, N%128==0, K%64==0");
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) % 16)
+    return fail_arg("gsx_gemm_bf16_nt: operands must be 16-B aligned");
+  int tiles = (M / BM) * (N / BN);
+  hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3(tiles), dim3(256), 0, S(stream), static_cast<const uint16_t*>(A),
+                     static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N, K);
+  GSX_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gsx_event_time_gemm(void* stream, const void* A, const void* B, void* C, int M, int N, int K, int iters,
+                        float* ms) {
+  hipEvent_t e0, e1;
+  GSX_CHECK(hipEventCreate(&e0));
+  GSX_CHECK(hipEventCreate(&e1));
+  GSX_CHECK(hipEventRecord(e0, S(stream)));
+  for (int i = 0; i < iters; ++i) {
+    int rc = gsx_gemm_bf16_nt(stream, A, B, C, M, N, K);
+    if (rc) return rc;
+  }
+  GSX_CHECK(hipEventRecord(e1, S(stream)));
+  GSX_CHECK(hipEventSynchronize(e1));
+  GSX_CHECK(hipEventElapsedTime(ms, e0, e1));
+  GSX_CHECK(hipEventDestroy(e0));
+  GSX_CHECK(hipEventDestroy(e1));
+  return 0;
+}
+
+}  // extern "C"

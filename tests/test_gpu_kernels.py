@@ -1,0 +1,161 @@
+"""HIP/CDNA4 kernels on a real MI355X (run with ``-m gpu`` on the GPU box).
+
+Numerics are checked against plain PyTorch fp32 references; the CU probe and
+HBM stamp tests check the isolation/placement properties the device plugin
+relies on.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hip():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a GPU")
+    from gpushare_scheduler_extender_amd.ops import hip as h
+
+    assert h.SO.exists()
+    return h
+
+
+def test_device_info_is_mi355x(hip):
+    info = hip.device_info(0)
+    assert info["arch"].startswith("gfx950"), info
+    assert info["cu_count"] == 256
+    free, total = hip.mem_info(0)
+    assert total > 250 * 10**9 and free <= total
+
+
+def test_hbm_stamp_verify_and_overlap_detection(hip):
+    s = hip.Stream(0)
+    buf = hip.DeviceBuffer(0, 256 << 20)
+    half = 128 << 20
+    hip.hbm_stamp(s, buf.addr(0), half, 1 << 16, 111)
+    hip.hbm_stamp(s, buf.addr(half), half, 1 << 16, 222)
+    assert hip.hbm_verify(s, buf.addr(0), half, 1 << 16, 111) == 0
+    assert hip.hbm_verify(s, buf.addr(half), half, 1 << 16, 222) == 0
+    # a third "pod" placed over the second half of pod 111 corrupts exactly its stamps
+    hip.hbm_stamp(s, buf.addr(half // 2), half // 2, 1 << 16, 333)
+    assert hip.hbm_verify(s, buf.addr(0), half, 1 << 16, 111) == (half // 2) // (1 << 16)
+    buf.free()
+    s.destroy()
+
+
+def test_hbm_fill_pattern_and_bandwidth(hip):
+    s = hip.Stream(0)
+    n = 4 << 30
+    t = torch.empty(n // 4, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    hip.hbm_fill(s, t.data_ptr(), 4096, 0x1234ABCD)
+    s.sync()
+    assert (t[:1024] == 0x1234ABCD).all()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    hip.hbm_fill(s, t.data_ptr(), n, 7)
+    s.sync()
+    ev0.record()
+    for _ in range(5):
+        hip.hbm_fill(s, t.data_ptr(), n, 7)
+    s.sync()
+    ev1.record()
+    torch.cuda.synchronize()
+    # events are on the default stream, our stream was synced in between: wall time via python instead
+    import time
+    t0 = time.perf_counter()
+    for _ in range(5):
+        hip.hbm_fill(s, t.data_ptr(), n, 9)
+    s.sync()
+    dt = time.perf_counter() - t0
+    bw = 5 * n / dt / 1e12
+    print(f"hbm fill {bw:.2f} TB/s")
+    assert int(t[-1].item()) == 9
+    assert bw > 2.0  # write roofline ~5-6 TB/s on MI355X; a broken kernel is far below
+
+
+@pytest.mark.parametrize("m,n,k", [(128, 128, 64), (256, 384, 192), (1024, 512, 1024)])
+def test_gemm_bf16_matches_fp32_reference(hip, m, n, k):
+    torch.manual_seed(m + n + k)
+    a = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(n, k, device="cuda", dtype=torch.bfloat16)
+    c = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+    s = hip.Stream(0)
+    torch.cuda.synchronize()
+    hip.gemm_bf16_nt(s, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k)
+    s.sync()
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(c.float(), ref, atol=0.05 * (k ** 0.5), rtol=1e-2)
+    s.destroy()
+
+
+def test_gemm_asymmetric_identity(hip):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    m = 128
+    a = torch.eye(m, device="cuda", dtype=torch.bfloat16)
+    b = (torch.arange(128 * 128, device="cuda", dtype=torch.float32).reshape(128, 128) % 97).to(torch.bfloat16)
+    c = torch.empty(m, 128, device="cuda", dtype=torch.bfloat16)
+    s = hip.Stream(0)
+    torch.cuda.synchronize()
+    hip.gemm_bf16_nt(s, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, 128, 128)
+    s.sync()
+    torch.testing.assert_close(c.float(), b.float().t(), atol=0, rtol=0)
+    s.destroy()
+
+
+def test_gemm_rejects_bad_shapes(hip):
+    s = hip.Stream(0)
+    with pytest.raises(hip.HipError):
+        hip.gemm_bf16_nt(s, 0, 0, 0, 100, 128, 64)
+    s.destroy()
+
+
+def test_cuprobe_full_and_masked(hip):
+    s = hip.Stream(0)
+    full = hip.physical_cus(hip.cuprobe(s, 8192, 20000))
+    s.destroy()
+    print("distinct CUs unmasked:", len(full))
+    assert len(full) >= 200
+    words = hip.mask_words(range(0, 64))
+    m = hip.Stream(0, words)
+    assert m.mask(8)[:2] == [0xFFFFFFFF, 0xFFFFFFFF]
+    part = hip.physical_cus(hip.cuprobe(m, 8192, 20000))
+    m.destroy()
+    print("distinct CUs with a 64-CU mask:", len(part))
+    assert 0 < len(part) <= 64
+
+
+def test_hsa_cu_mask_env_limits_process():
+    """The device plugin's HSA_CU_MASK env restricts a whole process (checked in a child)."""
+    code = ("from gpushare_scheduler_extender_amd.ops import hip;"
+            "s=hip.Stream(0);print(len(hip.physical_cus(hip.cuprobe(s,8192,20000))))")
+    env = dict(os.environ, HSA_CU_MASK="0:0-31")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr
+    n = int(r.stdout.strip().splitlines()[-1])
+    print("distinct CUs under HSA_CU_MASK=0:0-31:", n)
+    assert n <= 32
+
+
+def test_arena_runtime_admits_four_64gib_pods():
+    """BASELINE config 2: 4 x 64 GiB pods co-resident on one MI355X, stamps verified."""
+    from gpushare_scheduler_extender_amd.deviceplugin.runtime import HbmArenaRuntime, AdmissionError
+
+    gib = 1 << 30
+    rt = HbmArenaRuntime({0: 256 * gib})
+    try:
+        for i in range(4):
+            rt.start(f"pod-{i}", 0, 64 * gib)
+        assert rt.verify() == 0
+        with pytest.raises(AdmissionError):
+            rt.start("pod-5", 0, 1 * gib)
+        rt.stop("pod-1")
+        rt.start("pod-6", 0, 64 * gib)
+        assert rt.verify() == 0
+    finally:
+        rt.close()
