@@ -97,10 +97,9 @@ def build_mxdev(force: bool = False, verbose: bool = False) -> Path:
     flags = [*CXXFLAGS, *_pybind_includes(), "-I" + str(src), "-I" + str(ROCM / "include"),
              "-I" + str(NATIVE / "engine")]
     objs = _compile_objs(srcs, "g++", flags, "mxdev", force, verbose, headers)
-    eng = [OBJ / "engine_json.o"]
-    if force or _newer(out, objs + eng):
+    if force or _newer(out, objs):
         OUT.mkdir(parents=True, exist_ok=True)
-        _run(["g++", "-shared", "-o", str(out), *map(str, objs), *map(str, eng), "-ldl"], verbose)
+        _run(["g++", "-shared", "-o", str(out), *map(str, objs), "-ldl"], verbose)
     return out
 
 
@@ -158,7 +157,7 @@ TARGETS = {
     "tools": build_tools,
     "asan": build_asan,
 }
-DEFAULT = ["engine", "kernels"]
+DEFAULT = ["engine", "mxdev", "kernels"]
 
 
 def main(argv: list[str] | None = None) -> int:

@@ -1,0 +1,70 @@
+// mxdev: MI355X device discovery / health / topology over amdsmi.
+//
+// Replaces the NVML (cgo) layer of the upstream gpushare device plugin
+// (docs/designs/designs.md:57-61): per-GPU VRAM total for the gpu-mem
+// capacity, BDF / UUID / render+card minors for the /dev nodes handed to
+// containers, KFD ids, compute/memory partition mode, RAS/ECC counters and
+// reset / fault events for device health, and xGMI link types between GPUs.
+//
+// libamd_smi is dlopen()ed at run time with RTLD_DEEPBIND|RTLD_LOCAL, so the
+// module loads on CPU-only hosts (the driver's build check), and the symbols
+// never bind to the ROCm-SMI copy bundled inside the torch wheel.  A "fake"
+// backend (e.g. "8x288GB") serves CPU tests with the same record layout.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mxdev {
+
+struct DeviceRec {
+  int index = 0;           // HIP enumeration order
+  std::string name;        // market name
+  std::string arch = "gfx950";
+  std::string bdf;         // dddd:bb:dd.f
+  std::string uuid;
+  uint64_t total_bytes = 0;  // VRAM total
+  uint64_t used_bytes = 0;
+  int cu_count = 0;
+  int xcc_count = 8;
+  int render_minor = -1;
+  int card_minor = -1;
+  int64_t kfd_id = -1;
+  int hsa_id = -1;
+  std::string partition = "SPX";
+  std::string memory_partition;
+  bool healthy = true;
+  uint64_t ecc_uncorrectable = 0;
+  uint64_t ecc_correctable = 0;
+  int numa_node = -1;
+  std::vector<std::string> link_types;  // per peer index: XGMI / PCIE / SELF / UNKNOWN
+};
+
+struct Event {
+  int index;        // device index
+  int type;         // amdsmi_evt_notification_type_t
+  std::string name; // VMFAULT / THERMAL_THROTTLE / GPU_PRE_RESET / GPU_POST_RESET / ...
+  std::string message;
+};
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual std::string name() const = 0;
+  virtual bool enumerate(std::vector<DeviceRec>* out, std::string* err) = 0;
+  // refresh health counters of one device (ECC); false on error
+  virtual bool health(int index, DeviceRec* rec, std::string* err) = 0;
+  // start listening for reset / fault events on every device
+  virtual bool watch_events(std::string* err) = 0;
+  // wait up to timeout_ms for events
+  virtual std::vector<Event> poll_events(int timeout_ms) = 0;
+};
+
+// "amdsmi", "fake:<spec>", or "auto" (amdsmi, error if unavailable).
+Backend* make_backend(const std::string& kind, std::string* err);
+
+// Parse "NxSIZE{GB,GiB,MiB,MB}" into fake device records.
+bool fake_spec(const std::string& spec, std::vector<DeviceRec>* out, std::string* err);
+
+}  // namespace mxdev
