@@ -1,0 +1,65 @@
+"""``python -m gpushare_scheduler_extender_amd.deviceplugin`` — the node DaemonSet process.
+
+Deployed on nodes labelled ``gpushare=true`` (``docs/install.md:69-79``; see
+``deploy/device-plugin-ds.yaml``).  ``NODE_NAME`` comes from the downward API.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import signal
+import sys
+
+from ..k8s.client import KubeClient, KubeConfig
+from ..models.profile import get_profile
+from . import api
+from .devices import discover
+from .plugin import GpuSharePlugin
+
+
+def main(argv=None) -> int:
+    env = os.environ
+    ap = argparse.ArgumentParser(prog="gpushare-device-plugin-amd")
+    ap.add_argument("--node", default=env.get("NODE_NAME", ""))
+    ap.add_argument("--kubeconfig", default=env.get("KUBECONFIG"))
+    ap.add_argument("--apiserver", default=env.get("GSX_APISERVER"))
+    ap.add_argument("--profile", default=env.get("GSX_PROFILE", "shared-gpu"))
+    ap.add_argument("--unit", default=env.get("GSX_MEMORY_UNIT", "GiB"), choices=["GiB", "MiB", "GB"])
+    ap.add_argument("--backend", default=env.get("GSX_DEVICE_BACKEND", "auto"), choices=["auto", "amdsmi", "hip", "fake"])
+    ap.add_argument("--socket-dir", default=env.get("GSX_SOCKET_DIR", api.DEVICE_PLUGIN_PATH))
+    ap.add_argument("--mount-mode", default=env.get("GSX_MOUNT_MODE", "isolated"), choices=["isolated", "all"])
+    ap.add_argument("--reserve-gib", type=float, default=float(env.get("GSX_RESERVE_GIB", "0")),
+                    help="HBM per GPU withheld from sharing (driver / runtime overhead)")
+    ap.add_argument("--health-interval", type=float, default=float(env.get("GSX_HEALTH_INTERVAL", "10")))
+    ap.add_argument("--log-level", default=env.get("LOG_LEVEL", "info"))
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=getattr(logging, a.log_level.upper(), logging.INFO),
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    if not a.node:
+        ap.error("--node / NODE_NAME is required")
+
+    async def run():
+        backend, devs = discover(a.backend)
+        logging.getLogger("gsx.main").info("%d GPU(s) via %s: %s", len(devs), backend,
+                                           ", ".join(f"{d.index}:{d.bdf}:{d.total_bytes >> 30}GiB" for d in devs))
+        client = KubeClient(KubeConfig.auto(a.kubeconfig, a.apiserver))
+        plugin = GpuSharePlugin(client, a.node, devs, get_profile(a.profile), unit=a.unit, socket_dir=a.socket_dir,
+                                mount_mode=a.mount_mode, health_backend="amdsmi" if backend == "amdsmi" else None,
+                                health_interval=a.health_interval, reserve_bytes=int(a.reserve_gib * (1 << 30)))
+        await plugin.start()
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for s in (signal.SIGINT, signal.SIGTERM):
+            loop.add_signal_handler(s, stop.set)
+        await stop.wait()
+        await plugin.stop()
+        await client.close()
+
+    asyncio.run(run())
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

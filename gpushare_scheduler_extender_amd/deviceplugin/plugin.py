@@ -1,0 +1,417 @@
+"""GPU-share device plugin for kubelet (``v1beta1`` gRPC over a unix socket).
+
+The companion the reference depends on but does not ship (SURVEY.md §2.8;
+``docs/designs/designs.md:57-61,93-103``; ``docs/install.md:58-67``),
+re-built for MI355X:
+
+* **inventory** from amdsmi (``_mxdev``) or HIP, not NVML; per-device HBM in
+  GiB units (MiB would be ~2.4 M fake IDs for 8 x 288 GB);
+* **ListAndWatch** advertises ``<resource>`` as one fake device ID per unit
+  per GPU, with NUMA topology, and re-sends with ``Unhealthy`` IDs when a
+  GPU's uncorrectable-ECC count rises or amdsmi reports a reset / VM fault;
+* the plugin also publishes ``<count>`` (GPU count) in node capacity and the
+  per-device totals annotation the extender's ledger prefers over
+  ``capacity / count`` (``pkg/cache/nodeinfo.go:34``);
+* **GetPreferredAllocation** steers kubelet's fake-ID choice onto the GPU the
+  extender picked, so kubelet's own per-ID accounting matches the annotation;
+* **Allocate** = :mod:`.allocator` (earliest ``ASSUME_TIME`` pod of that
+  size, ``ASSIGNED=true`` under a resourceVersion precondition, env +
+  ``/dev/kfd`` + render node + optional CU partition);
+* re-registers when kubelet restarts (its socket is re-created).
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import time
+
+import grpc
+
+from ..k8s.client import ApiError, KubeClient
+from ..models import pod as podutil
+from ..models.profile import NODE_DEVICE_INFO_ANNOTATION, NODE_DEVICE_MEMORY_ANNOTATION, NamingProfile
+from . import api
+from .allocator import CU_COUNT_ANNOTATION, AllocateError, CUPartitioner, assigned_patch, build_response, candidate_pods
+from .devices import UNITS, Device
+
+log = logging.getLogger("gsx.deviceplugin")
+
+ID_SEP = "-_-"
+
+
+def fake_ids(dev: Device, units: int) -> list[str]:
+    base = dev.uuid or dev.bdf or f"gpu{dev.index}"
+    return [f"{base}{ID_SEP}{k}" for k in range(units)]
+
+
+class GpuSharePlugin:
+    def __init__(self, client: KubeClient, node: str, devices: list[Device], profile: NamingProfile, *,
+                 unit: str = "GiB", socket_dir: str = api.DEVICE_PLUGIN_PATH, endpoint: str = "gpushare-amd.sock",
+                 mount_mode: str = "isolated", health_backend: str | None = None, health_interval: float = 10.0,
+                 reserve_bytes: int = 0):
+        self.client = client
+        self.node = node
+        self.devices = {d.index: d for d in devices}
+        self.profile = profile
+        self.unit = unit
+        self.socket_dir = socket_dir
+        self.endpoint = endpoint
+        self.mount_mode = mount_mode
+        self.health_backend = health_backend
+        self.health_interval = health_interval
+        self.units = {d.index: d.units(unit, reserve_bytes) for d in devices}
+        self.ids = {d.index: fake_ids(d, self.units[d.index]) for d in devices}
+        self.id_owner = {i: d for d, ids in self.ids.items() for i in ids}
+        self.cus = {d.index: CUPartitioner(d.cu_count, d.xcc_count) for d in devices}
+        self.partial: dict[str, list[int]] = {}  # pod uid -> container requests not yet allocated
+        self._changed = asyncio.Event()
+        self._version = 0
+        self._server: grpc.aio.Server | None = None
+        self._tasks: list[asyncio.Task] = []
+        self.allocations = 0
+        self.stats = {"allocate_ok": 0, "allocate_fail": 0, "preferred": 0, "registrations": 0}
+
+    # ------------------------------------------------------------ paths
+    @property
+    def socket_path(self) -> str:
+        return os.path.join(self.socket_dir, self.endpoint)
+
+    @property
+    def kubelet_socket(self) -> str:
+        return os.path.join(self.socket_dir, api.KUBELET_SOCKET)
+
+    # ------------------------------------------------------------ device list
+    def device_list(self) -> list:
+        out = []
+        for idx, ids in self.ids.items():
+            d = self.devices[idx]
+            health = api.HEALTHY if d.healthy else api.UNHEALTHY
+            topo = api.TopologyInfo(nodes=[api.NUMANode(ID=d.numa_node)]) if d.numa_node >= 0 else None
+            for i in ids:
+                dev = api.Device(ID=i, health=health)
+                if topo is not None:
+                    dev.topology.CopyFrom(topo)
+                out.append(dev)
+        return out
+
+    def set_health(self, index: int, healthy: bool, why: str = ""):
+        d = self.devices.get(index)
+        if d is None or d.healthy == healthy:
+            return
+        d.healthy = healthy
+        log.warning("GPU %d (%s) is now %s %s", index, d.bdf, "Healthy" if healthy else "Unhealthy", why)
+        self._version += 1
+        self._changed.set()
+
+    # ------------------------------------------------------------ gRPC handlers
+    async def GetDevicePluginOptions(self, request, context):
+        return api.DevicePluginOptions(pre_start_required=False, get_preferred_allocation_available=True)
+
+    async def ListAndWatch(self, request, context):
+        seen = -1
+        while True:
+            if seen != self._version:
+                seen = self._version
+                yield api.ListAndWatchResponse(devices=self.device_list())
+            self._changed.clear()
+            try:
+                await asyncio.wait_for(self._changed.wait(), 5.0)
+            except asyncio.TimeoutError:
+                pass
+
+    async def _pods_on_node(self) -> list[dict]:
+        lst = await self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
+        return lst.get("items") or []
+
+    def _match(self, pods: list[dict], units: int) -> tuple[dict | None, bool]:
+        """(pod, whole_pod) for a request of ``units``: whole pods first, then one container of a multi-container pod."""
+        cands = candidate_pods(pods, self.node, self.profile)
+        for p in cands:
+            if podutil.gpu_mem_request(p, self.profile) == units:
+                return p, True
+        for p in pods:  # second container of a pod whose first container was already allocated
+            uid = podutil.meta(p).get("uid", "")
+            if units in self.partial.get(uid, []):
+                return p, False
+        for p in cands:
+            reqs = [podutil.container_limit(c, self.profile.resource) for c in (p.get("spec") or {}).get("containers", [])]
+            if units in reqs:
+                return p, False
+        return None, False
+
+    async def GetPreferredAllocation(self, request, context):
+        resp = api.PreferredAllocationResponse()
+        pods = await self._pods_on_node()
+        for creq in request.container_requests:
+            size = creq.allocation_size
+            pod, _ = self._match(pods, size)
+            want_dev = podutil.gpu_id_from_annotation(pod, self.profile) if pod else -1
+            avail = list(creq.available_deviceIDs)
+            chosen = list(creq.must_include_deviceIDs)
+            pref = [i for i in avail if i not in chosen and self.id_owner.get(i) == want_dev]
+            rest = [i for i in avail if i not in chosen and i not in pref]
+            for i in pref + rest:
+                if len(chosen) >= size:
+                    break
+                chosen.append(i)
+            resp.container_responses.add(deviceIDs=chosen[:size])
+            self.stats["preferred"] += 1
+        return resp
+
+    async def Allocate(self, request, context):
+        resp = api.AllocateResponse()
+        try:
+            pods = await self._pods_on_node()
+            for creq in request.container_requests:
+                units = len(creq.devices_ids)
+                pod, whole = self._match(pods, units)
+                if pod is None:
+                    raise AllocateError(f"no pending pod on {self.node} requests {units} {self.profile.resource} "
+                                        f"with {self.profile.annotation_assigned}=false")
+                uid = podutil.meta(pod).get("uid", "")
+                dev_idx = podutil.gpu_id_from_annotation(pod, self.profile)
+                device = self.devices.get(dev_idx)
+                if device is None:
+                    raise AllocateError(f"pod {podutil.pod_key(pod)} annotated with GPU {dev_idx}, not on this node")
+                cus = None
+                want = podutil.annotations(pod).get(CU_COUNT_ANNOTATION)
+                if want:
+                    cus = self.cus[dev_idx].allocate(uid, int(want))
+                alloc = build_response(pod, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
+                if uid not in self.partial:
+                    # first (or only) container: commit point ASSIGNED=true
+                    try:
+                        await self.client.patch("pods", podutil.meta(pod)["name"],
+                                                assigned_patch(pod, self.profile, alloc.annotations),
+                                                podutil.meta(pod)["namespace"])
+                    except ApiError as e:
+                        raise AllocateError(f"marking {podutil.pod_key(pod)} assigned failed: {e}") from e
+                    if not whole:
+                        reqs = [podutil.container_limit(c, self.profile.resource)
+                                for c in (pod.get("spec") or {}).get("containers", [])]
+                        reqs.remove(units)
+                        self.partial[uid] = [r for r in reqs if r > 0]
+                else:
+                    self.partial[uid].remove(units)
+                    if not self.partial[uid]:
+                        del self.partial[uid]
+                c = resp.container_responses.add()
+                for k, v in alloc.envs.items():
+                    c.envs[k] = v
+                for k, v in alloc.annotations.items():
+                    c.annotations[k] = v
+                for dspec in alloc.devices:
+                    c.devices.add(**dspec)
+            self.stats["allocate_ok"] += 1
+            return resp
+        except AllocateError as e:
+            self.stats["allocate_fail"] += 1
+            log.error("Allocate failed: %s", e)
+            await context.abort(grpc.StatusCode.FAILED_PRECONDITION, str(e))
+
+    async def PreStartContainer(self, request, context):
+        return api.PreStartContainerResponse()
+
+    # ------------------------------------------------------------ server / registration
+    def _handlers(self):
+        methods = {}
+        for meth, (inp, out, stream) in api.SERVICES["DevicePlugin"].items():
+            ic, oc, _ = api.io_types("DevicePlugin", meth)
+            fn = getattr(self, meth)
+            if stream:
+                methods[meth] = grpc.unary_stream_rpc_method_handler(fn, request_deserializer=ic.FromString,
+                                                                     response_serializer=oc.SerializeToString)
+            else:
+                methods[meth] = grpc.unary_unary_rpc_method_handler(fn, request_deserializer=ic.FromString,
+                                                                    response_serializer=oc.SerializeToString)
+        return grpc.method_handlers_generic_handler(f"{api.PKG}.DevicePlugin", methods)
+
+    async def serve(self):
+        os.makedirs(self.socket_dir, exist_ok=True)
+        try:
+            os.unlink(self.socket_path)
+        except FileNotFoundError:
+            pass
+        self._server = grpc.aio.server()
+        self._server.add_generic_rpc_handlers((self._handlers(),))
+        self._server.add_insecure_port(f"unix://{self.socket_path}")
+        await self._server.start()
+
+    async def register(self, timeout: float = 10.0):
+        async with grpc.aio.insecure_channel(f"unix://{self.kubelet_socket}") as ch:
+            ic, oc, _ = api.io_types("Registration", "Register")
+            call = ch.unary_unary(api.method_path("Registration", "Register"), request_serializer=ic.SerializeToString,
+                                  response_deserializer=oc.FromString)
+            await call(api.RegisterRequest(version=api.VERSION, endpoint=self.endpoint,
+                                           resource_name=self.profile.resource,
+                                           options=api.DevicePluginOptions(get_preferred_allocation_available=True)),
+                       timeout=timeout)
+        self.stats["registrations"] += 1
+        log.info("registered %s with kubelet at %s", self.profile.resource, self.kubelet_socket)
+
+    async def publish_node(self):
+        """gpu-count capacity + per-device totals / inventory annotations (what kubelet does not publish)."""
+        import json  # noqa: PLC0415
+
+        totals = [self.units[i] for i in sorted(self.units)]
+        inv = [{"index": d.index, "bdf": d.bdf, "uuid": d.uuid, "units": self.units[d.index],
+                "cu": d.cu_count, "partition": d.partition, "render": d.render_minor}
+               for d in sorted(self.devices.values(), key=lambda d: d.index)]
+        await self.client.patch("nodes", self.node, {"metadata": {"annotations": {
+            NODE_DEVICE_MEMORY_ANNOTATION: ",".join(str(t) for t in totals),
+            NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv, separators=(",", ":"))}}})
+        await self.client.patch("nodes", self.node, {"status": {"capacity": {
+            self.profile.count: str(len(self.devices))}}}, sub="status")
+
+    async def _watch_kubelet(self):
+        """Re-register when kubelet restarts (it deletes and re-creates its socket)."""
+        last = None
+        while True:
+            try:
+                st = os.stat(self.kubelet_socket)
+                ident = (st.st_ino, st.st_ctime)
+                if last is not None and ident != last:
+                    log.info("kubelet restarted; re-registering")
+                    await self.serve()
+                    await self.register()
+                last = ident
+            except FileNotFoundError:
+                last = None
+            except Exception as e:  # noqa: BLE001
+                log.warning("re-register failed: %r", e)
+            await asyncio.sleep(1.0)
+
+    async def _health_loop(self):
+        from ..ops import mxdev  # noqa: PLC0415
+
+        while True:
+            for idx in list(self.devices):
+                try:
+                    h = await asyncio.get_running_loop().run_in_executor(None, mxdev.health, idx,
+                                                                         self.health_backend)
+                    self.set_health(idx, bool(h["healthy"]), f"(ecc uncorrectable={h['ecc_uncorrectable']})")
+                except Exception as e:  # noqa: BLE001
+                    log.debug("health of GPU %d: %r", idx, e)
+            await asyncio.sleep(self.health_interval)
+
+    async def _event_loop(self):
+        from ..ops import mxdev  # noqa: PLC0415
+
+        sess = mxdev.session(self.health_backend)
+        try:
+            sess.watch_events()
+        except Exception as e:  # noqa: BLE001
+            log.info("amdsmi events unavailable: %r", e)
+            return
+        loop = asyncio.get_running_loop()
+        while True:
+            evs = await loop.run_in_executor(None, sess.poll_events, 1000)
+            for ev in evs:
+                if ev["name"] in ("GPU_PRE_RESET", "VMFAULT"):
+                    self.set_health(ev["index"], False, f"({ev['name']}: {ev['message']})")
+                elif ev["name"] == "GPU_POST_RESET":
+                    self.set_health(ev["index"], True, "(post reset)")
+
+    async def start(self, register: bool = True, publish: bool = True):
+        await self.serve()
+        if publish:
+            try:
+                await self.publish_node()
+            except ApiError as e:
+                log.warning("publishing node info failed: %s", e)
+        if register:
+            await self.register()
+            self._tasks.append(asyncio.get_running_loop().create_task(self._watch_kubelet()))
+        if self.health_backend:
+            self._tasks.append(asyncio.get_running_loop().create_task(self._health_loop()))
+            self._tasks.append(asyncio.get_running_loop().create_task(self._event_loop()))
+
+    async def stop(self):
+        for t in self._tasks:
+            t.cancel()
+        if self._server is not None:
+            await self._server.stop(0.5)
+        try:
+            os.unlink(self.socket_path)
+        except FileNotFoundError:
+            pass
+
+
+class PluginClient:
+    """What kubelet does with a plugin (used by the fake kubelet in tests and by `gsx-plugin-probe`)."""
+
+    def __init__(self, socket_path: str):
+        self.channel = grpc.aio.insecure_channel(f"unix://{socket_path}")
+
+    def _call(self, meth: str):
+        ic, oc, stream = api.io_types("DevicePlugin", meth)
+        path = api.method_path("DevicePlugin", meth)
+        if stream:
+            return self.channel.unary_stream(path, request_serializer=ic.SerializeToString,
+                                             response_deserializer=oc.FromString)
+        return self.channel.unary_unary(path, request_serializer=ic.SerializeToString,
+                                        response_deserializer=oc.FromString)
+
+    async def options(self):
+        return await self._call("GetDevicePluginOptions")(api.Empty())
+
+    def list_and_watch(self):
+        return self._call("ListAndWatch")(api.Empty())
+
+    async def preferred(self, available: list[str], size: int, must: list[str] | None = None):
+        req = api.PreferredAllocationRequest()
+        req.container_requests.add(available_deviceIDs=available, must_include_deviceIDs=must or [],
+                                   allocation_size=size)
+        return await self._call("GetPreferredAllocation")(req)
+
+    async def allocate(self, ids_per_container: list[list[str]]):
+        req = api.AllocateRequest()
+        for ids in ids_per_container:
+            req.container_requests.add(devices_ids=ids)
+        return await self._call("Allocate")(req)
+
+    async def close(self):
+        await self.channel.close()
+
+
+class FakeKubelet:
+    """Registration server on ``<dir>/kubelet.sock`` that records plugin registrations."""
+
+    def __init__(self, socket_dir: str):
+        self.socket_dir = socket_dir
+        self.registrations: list = []
+        self.registered = asyncio.Event()
+        self._server: grpc.aio.Server | None = None
+
+    async def Register(self, request, context):
+        self.registrations.append(request)
+        self.registered.set()
+        return api.Empty()
+
+    async def start(self):
+        os.makedirs(self.socket_dir, exist_ok=True)
+        path = os.path.join(self.socket_dir, api.KUBELET_SOCKET)
+        try:
+            os.unlink(path)
+        except FileNotFoundError:
+            pass
+        ic, oc, _ = api.io_types("Registration", "Register")
+        h = grpc.method_handlers_generic_handler(f"{api.PKG}.Registration", {
+            "Register": grpc.unary_unary_rpc_method_handler(self.Register, request_deserializer=ic.FromString,
+                                                            response_serializer=oc.SerializeToString)})
+        self._server = grpc.aio.server()
+        self._server.add_generic_rpc_handlers((h,))
+        self._server.add_insecure_port(f"unix://{path}")
+        await self._server.start()
+
+    async def stop(self):
+        if self._server is not None:
+            await self._server.stop(0.2)
+
+
+def now_ns() -> int:
+    return time.time_ns()
+
+
+UNIT_BYTES = UNITS

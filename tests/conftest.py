@@ -20,5 +20,5 @@ def _native_built():
     """Build the native extensions in-tree once per session (no-op when up to date)."""
     from gpushare_scheduler_extender_amd.utils.build import build_native
 
-    build_native(["engine"])
+    build_native(["engine", "mxdev"])
     yield

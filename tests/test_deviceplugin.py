@@ -1,0 +1,259 @@
+"""Device plugin: kubelet gRPC API against a fake kubelet + fake apiserver; Allocate semantics; CU partitions."""
+import asyncio
+import json
+import tempfile
+
+import pytest
+
+from gpushare_scheduler_extender_amd.deviceplugin import api
+from gpushare_scheduler_extender_amd.deviceplugin.allocator import (CU_COUNT_ANNOTATION, CUPartitioner, build_response,
+                                                                   candidate_pods, pick_pod)
+from gpushare_scheduler_extender_amd.deviceplugin.agent import NodeAgent
+from gpushare_scheduler_extender_amd.deviceplugin.devices import Device, discover, fake_devices
+from gpushare_scheduler_extender_amd.deviceplugin.plugin import FakeKubelet, GpuSharePlugin, PluginClient, fake_ids
+from gpushare_scheduler_extender_amd.deviceplugin.runtime import AdmissionError, LedgerRuntime
+from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
+from gpushare_scheduler_extender_amd.models.profile import ALIYUN, SHARED_GPU
+
+P = SHARED_GPU
+GIB = 1 << 30
+
+
+def bound_pod(name, mem, node="n1", dev=0, assume=1, assigned="false", dev_total=268, **kw):
+    ann = {P.annotation_idx: str(dev), P.annotation_pod: str(mem if not isinstance(mem, list) else sum(mem)),
+           P.annotation_dev: str(dev_total), P.annotation_assigned: assigned, P.annotation_assume_time: str(assume)}
+    ann.update(kw.pop("annotations", {}))
+    return make_pod(name, mem, node=node, annotations=ann, **kw)
+
+
+# ---------------------------------------------------------------- allocator (pure)
+
+def test_candidate_order_and_pick_by_size():
+    pods = [bound_pod("late", 8, assume=30), bound_pod("early", 8, assume=10), bound_pod("other", 4, assume=5),
+            bound_pod("done", 8, assume=1, assigned="true"), bound_pod("elsewhere", 8, node="n2", assume=1),
+            bound_pod("running", 8, assume=2, phase="Running")]
+    assert [p["metadata"]["name"] for p in candidate_pods(pods, "n1", P)] == ["other", "early", "late"]
+    assert pick_pod(pods, "n1", 8, P)["metadata"]["name"] == "early"
+    assert pick_pod(pods, "n1", 4, P)["metadata"]["name"] == "other"
+    assert pick_pod(pods, "n1", 3, P) is None
+
+
+def test_build_response_env_and_devices():
+    dev = fake_devices("8x288GB")[3]
+    pod = bound_pod("p", 64, dev=3, dev_total=268)
+    r = build_response(pod, dev, 64, P)
+    assert r.envs["HIP_VISIBLE_DEVICES"] == "0" and r.envs["ROCR_VISIBLE_DEVICES"] == "0"
+    assert r.envs["SHARED_GPU_MEM_IDX"] == "3" and r.envs["SHARED_GPU_MEM_DEV"] == "268"
+    assert r.envs["SHARED_GPU_MEM_CONTAINER"] == "64" and r.envs["SHARED_GPU_MEM_POD"] == "64"
+    assert abs(float(r.envs["GSX_GPU_MEM_FRACTION"]) - 64 / 268) < 1e-6
+    paths = [d["host_path"] for d in r.devices]
+    assert paths == ["/dev/kfd", f"/dev/dri/renderD{128 + 24}", "/dev/dri/card4"]
+    r2 = build_response(pod, dev, 64, P, mount_mode="all")
+    assert r2.envs["HIP_VISIBLE_DEVICES"] == "3" and r2.devices == []
+    r3 = build_response(bound_pod("q", 8, dev=0), dev, 8, ALIYUN)
+    assert "ALIYUN_COM_GPU_MEM_CONTAINER" in r3.envs
+
+
+def test_cu_partitioner_spreads_over_xcds_and_releases():
+    cp = CUPartitioner(256, 8)
+    a = cp.allocate("a", 64)
+    assert len(a) == 64 and len({c // 32 for c in a}) == 8  # 8 CUs on each of the 8 XCDs
+    b = cp.allocate("b", 64)
+    assert not set(a) & set(b)
+    assert cp.allocate("a", 64) == a  # idempotent
+    cp.allocate("c", 64)
+    cp.allocate("d", 64)
+    with pytest.raises(Exception):
+        cp.allocate("e", 1)
+    assert cp.release("b") == 64 and cp.free_count() == 64
+    assert CUPartitioner.ranges([0, 1, 2, 5, 7, 8]) == "0-2,5,7-8"
+    w = CUPartitioner.words(list(range(32, 40)))
+    assert w[1] == 0xFF and w[0] == 0
+
+
+def test_build_response_cu_mask_env():
+    dev = fake_devices("1x288GB")[0]
+    r = build_response(bound_pod("p", 8), dev, 8, P, cus=[0, 1, 2, 3, 32, 33])
+    assert r.envs["HSA_CU_MASK"] == "0:0-3,32-33"
+    assert r.envs["GSX_CU_MASK"].startswith("0x0000000f,0x00000003")
+
+
+def test_fake_devices_and_discover(monkeypatch):
+    devs = fake_devices("4x288GB")
+    assert [d.units("GiB") for d in devs] == [268] * 4
+    monkeypatch.setenv("GSX_FAKE_DEVICES", "2x64GiB")
+    backend, d2 = discover()
+    assert backend == "fake" and [d.units("GiB") for d in d2] == [64, 64]
+
+
+def test_native_mxdev_fake_backend_matches_python():
+    from gpushare_scheduler_extender_amd.ops import mxdev
+
+    recs = mxdev.enumerate_devices("fake:8x288GB")
+    assert len(recs) == 8
+    devs = [Device(**r) for r in recs]
+    py = fake_devices("8x288GB")
+    assert [(d.bdf, d.total_bytes, d.render_minor) for d in devs] == [(d.bdf, d.total_bytes, d.render_minor) for d in py]
+    assert devs[0].links[1] == "XGMI" and devs[0].links[0] == "SELF"
+    with pytest.raises(RuntimeError):
+        mxdev.native().Session("fake:nonsense")
+
+
+def test_runtime_slices_first_fit():
+    rt = LedgerRuntime({0: 256 * GIB})
+    offs = [rt.start(f"p{i}", 0, 64 * GIB) for i in range(4)]
+    assert offs == [0, 64 * GIB, 128 * GIB, 192 * GIB]
+    with pytest.raises(AdmissionError):
+        rt.start("p5", 0, GIB)
+    rt.stop("p1")
+    assert rt.start("p6", 0, 32 * GIB) == 64 * GIB
+    assert rt.resident_bytes(0) == 224 * GIB
+
+
+# ---------------------------------------------------------------- gRPC plugin with fake kubelet
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+def test_plugin_register_listandwatch_allocate():
+    async def go():
+        api_srv = await FakeApiServerRunner().start()
+        client = KubeClient(api_srv.url)
+        d = tempfile.mkdtemp(prefix="gsx-dp-")
+        kubelet = FakeKubelet(d)
+        await kubelet.start()
+        devs = fake_devices("2x16GiB")
+        await client.create("nodes", make_node("n1", 32, 0))
+        plugin = GpuSharePlugin(client, "n1", devs, P, socket_dir=d)
+        await plugin.start()
+        try:
+            await asyncio.wait_for(kubelet.registered.wait(), 5)
+            reg = kubelet.registrations[0]
+            assert reg.resource_name == "shared-gpu/gpu-mem" and reg.version == "v1beta1"
+            assert reg.endpoint == "gpushare-amd.sock" and reg.options.get_preferred_allocation_available
+            node = await client.get("nodes", "n1")
+            assert node["status"]["capacity"]["shared-gpu/gpu-count"] == "2"
+            assert node["metadata"]["annotations"]["gpushare.amd.com/device-memory"] == "16,16"
+            pc = PluginClient(plugin.socket_path)
+            stream = pc.list_and_watch()
+            first = await stream.read()
+            assert len(first.devices) == 32 and all(x.health == "Healthy" for x in first.devices)
+            # two bound pods of 8 on GPU1; the earlier ASSUME_TIME wins the first Allocate
+            await client.create("pods", bound_pod("b", 8, dev=1, assume=20, dev_total=16))
+            await client.create("pods", bound_pod("a", 8, dev=1, assume=10, dev_total=16))
+            ids = fake_ids(devs[0], 16) + fake_ids(devs[1], 16)
+            pref = await pc.preferred(ids, 8)
+            assert all(i in plugin.ids[1] for i in pref.container_responses[0].deviceIDs)
+            r = await pc.allocate([list(pref.container_responses[0].deviceIDs)])
+            env = dict(r.container_responses[0].envs)
+            assert env["SHARED_GPU_MEM_IDX"] == "1" and env["SHARED_GPU_MEM_CONTAINER"] == "8"
+            assert [x.host_path for x in r.container_responses[0].devices][0] == "/dev/kfd"
+            a = await client.get("pods", "a", "default")
+            b = await client.get("pods", "b", "default")
+            assert a["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
+            assert b["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "false"
+            await pc.allocate([ids[:8]])
+            b = await client.get("pods", "b", "default")
+            assert b["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
+            # nothing left to match
+            with pytest.raises(Exception) as ei:
+                await pc.allocate([ids[:8]])
+            assert "no pending pod" in str(ei.value)
+            # health change re-sends the list with Unhealthy IDs of GPU0
+            plugin.set_health(0, False, "test")
+            nxt = await asyncio.wait_for(stream.read(), 5)
+            bad = [x.ID for x in nxt.devices if x.health == "Unhealthy"]
+            assert sorted(bad) == sorted(plugin.ids[0])
+            stream.cancel()
+            await pc.close()
+        finally:
+            await plugin.stop()
+            await kubelet.stop()
+            await client.close()
+            await api_srv.stop()
+    run(go())
+
+
+def test_plugin_multi_container_pod_and_cu_partition():
+    async def go():
+        api_srv = await FakeApiServerRunner().start()
+        client = KubeClient(api_srv.url)
+        d = tempfile.mkdtemp(prefix="gsx-dp-")
+        devs = fake_devices("1x64GiB")
+        await client.create("nodes", make_node("n1", 64, 1))
+        plugin = GpuSharePlugin(client, "n1", devs, P, socket_dir=d)
+        await plugin.start(register=False)
+        try:
+            pc = PluginClient(plugin.socket_path)
+            await client.create("pods", bound_pod("mc", [10, 20], dev=0, dev_total=64,
+                                                  annotations={CU_COUNT_ANNOTATION: "64"}))
+            ids = plugin.ids[0]
+            r1 = await pc.allocate([ids[:20]])
+            r2 = await pc.allocate([ids[20:30]])
+            e1, e2 = dict(r1.container_responses[0].envs), dict(r2.container_responses[0].envs)
+            assert e1["SHARED_GPU_MEM_CONTAINER"] == "20" and e2["SHARED_GPU_MEM_CONTAINER"] == "10"
+            assert e1["HSA_CU_MASK"] == e2["HSA_CU_MASK"] and e1["HSA_CU_MASK"].startswith("0:")
+            p = await client.get("pods", "mc", "default")
+            assert p["metadata"]["annotations"]["gpushare.amd.com/cu-mask"] == e1["GSX_CU_MASK"]
+            await pc.close()
+        finally:
+            await plugin.stop()
+            await client.close()
+            await api_srv.stop()
+    run(go())
+
+
+def test_node_agent_admits_and_releases():
+    async def go():
+        api_srv = await FakeApiServerRunner().start()
+        client = KubeClient(api_srv.url)
+        devs = fake_devices("2x16GiB")
+        rt = LedgerRuntime({0: 16 * GIB, 1: 16 * GIB})
+        agent = NodeAgent(client, "n1", devs, P, rt)
+        await agent.start()
+        try:
+            for i, dev in enumerate([0, 0, 1]):
+                await client.create("pods", bound_pod(f"p{i}", 8, dev=dev, assume=i, dev_total=16))
+            for _ in range(400):
+                if agent.admitted == 3:
+                    break
+                await asyncio.sleep(0.01)
+            assert agent.admitted == 3 and rt.resident_bytes(0) == 16 * GIB and rt.resident_bytes(1) == 8 * GIB
+            p = await client.get("pods", "p0", "default")
+            assert p["status"]["phase"] == "Running"
+            assert p["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
+            await client.delete("pods", "p1", "default")
+            for _ in range(400):
+                if rt.resident_bytes(0) == 8 * GIB:
+                    break
+                await asyncio.sleep(0.01)
+            assert rt.resident_bytes(0) == 8 * GIB
+            # an over-committed pod (the ledger would never do this) is refused at admission
+            await client.create("pods", bound_pod("big", 12, dev=0, assume=9, dev_total=16))
+            for _ in range(400):
+                if agent.failed:
+                    break
+                await asyncio.sleep(0.01)
+            assert agent.failed == 1
+            big = await client.get("pods", "big", "default")
+            assert big["status"]["phase"] == "Failed"
+        finally:
+            await agent.stop()
+            await client.close()
+            await api_srv.stop()
+    run(go())
+
+
+def test_api_messages_roundtrip():
+    r = api.ContainerAllocateResponse()
+    r.envs["HIP_VISIBLE_DEVICES"] = "0"
+    r.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
+    b = r.SerializeToString()
+    assert api.ContainerAllocateResponse.FromString(b).envs["HIP_VISIBLE_DEVICES"] == "0"
+    # field numbers match the upstream proto: envs=1 (map), devices=3
+    assert b[0] == 0x0A and b"\x1a" in b
+    assert api.method_path("DevicePlugin", "Allocate") == "/v1beta1.DevicePlugin/Allocate"
+    assert json.dumps(list(api.SERVICES["DevicePlugin"]))
