@@ -57,6 +57,22 @@ class LoopThread:
         self.t.join(5)
 
 
+def _cpu_times(children) -> dict:
+    """user+sys CPU seconds of this process and the child servers (where the control plane spends time)."""
+    import resource
+
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    out = {"rank0": ru.ru_utime + ru.ru_stime}
+    for c in children:
+        try:
+            with open(f"/proc/{c.proc.pid}/stat") as f:
+                parts = f.read().rsplit(")", 1)[1].split()
+            out[c.name] = (int(parts[11]) + int(parts[12])) / os.sysconf("SC_CLK_TCK")
+        except (OSError, AttributeError, IndexError):
+            pass
+    return out
+
+
 def pct(xs, q):
     if not xs:
         return None
@@ -262,6 +278,7 @@ def main():
         if step == a.warmup:
             barrier()
             t_start = time.perf_counter()
+            cpu0 = _cpu_times(children)
         if rank == 0:
             r = lt.run(wave(step), timeout=600)
             if step >= a.warmup:
@@ -270,6 +287,7 @@ def main():
             dist.barrier(group=ctl)
     barrier()
     elapsed = time.perf_counter() - t_start
+    cpu1 = _cpu_times(children)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if use_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -320,6 +338,7 @@ def main():
                         "total": round(1e3 * statistics.mean(s["t_total"] for s in step_stats), 3)},
             "bind_retries": sum(sum(s["attempts"]) - len(s["attempts"]) for s in step_stats),
             "agents": agent_stats,
+            "cpu_s": {k: round(cpu1[k] - cpu0.get(k, 0.0), 3) for k in cpu1},
         }
         line = json.dumps(out)
         print(line, flush=True)

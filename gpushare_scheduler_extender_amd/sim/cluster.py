@@ -34,6 +34,7 @@ def _wait_port(path: str, proc: subprocess.Popen, timeout: float = 60.0) -> int:
 
 class ChildProc:
     def __init__(self, args: list[str], name: str, env: dict | None = None):
+        self.name = name
         self.tmp = tempfile.mkdtemp(prefix=f"gsx-{name}-")
         self.port_file = os.path.join(self.tmp, "port")
         self.log_path = os.path.join(self.tmp, "log")
