@@ -44,6 +44,10 @@ def parse_args(argv=None):
     ap.add_argument("--kube-burst", type=int, default=int(env.get("GSX_KUBE_BURST", "1000")))
     ap.add_argument("--resync", type=float, default=float(env.get("GSX_RESYNC", "30")))
     ap.add_argument("--reservation-ttl", type=float, default=float(env.get("GSX_RESERVATION_TTL", "60")))
+    ap.add_argument("--native-http", type=int, default=int(env.get("GSX_NATIVE_HTTP", "1")),
+                    help="1: C++ front end serves filter/bind/inspect (default); 0: aiohttp only")
+    ap.add_argument("--http-threads", type=int, default=int(env.get("GSX_HTTP_THREADS", "2")))
+    ap.add_argument("--bind-threads", type=int, default=int(env.get("GSX_BIND_THREADS", "16")))
     ap.add_argument("--port-file", default="", help="write the bound port to this file once serving")
     return ap.parse_args(argv)
 
@@ -59,7 +63,8 @@ def main(argv=None) -> int:
         client = KubeClient(cfg, qps=a.kube_qps, burst=a.kube_burst)
         srv = ExtenderServer(client, get_profile(a.profile), workers=a.threadness, bind_mode=a.bind_mode,
                              reservation_ttl=a.reservation_ttl, resync_period=a.resync)
-        runner = await ExtenderRunner(srv, a.host, a.port).start()
+        runner = await ExtenderRunner(srv, a.host, a.port, native=bool(a.native_http), http_threads=a.http_threads,
+                                      pool_threads=a.bind_threads).start()
         if a.port_file:
             with open(a.port_file + ".tmp", "w") as f:
                 f.write(str(runner.port))

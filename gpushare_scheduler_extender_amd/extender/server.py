@@ -80,6 +80,7 @@ class ExtenderServer:
         self.app = self._make_app()
         self._gc_task: asyncio.Task | None = None
         self._bg: set[asyncio.Task] = set()
+        self.native_server = False
 
     # ------------------------------------------------------------ lifecycle
     async def start(self):
@@ -255,13 +256,26 @@ class ExtenderServer:
 
 
 class ExtenderRunner:
-    """Serve an :class:`ExtenderServer` on host:port (port 0 = ephemeral)."""
+    """Serve an :class:`ExtenderServer` on host:port (port 0 = ephemeral).
 
-    def __init__(self, server: ExtenderServer, host: str = "127.0.0.1", port: int = 0):
+    ``native=True`` (default) puts the C++ front end (``native/engine/server.cc``)
+    on the public port: filter / bind / inspect / version never touch Python;
+    every other route is proxied to the aiohttp app on a loopback port.
+    ``native=False`` serves everything from aiohttp (reference-equivalent path,
+    used to A/B the native one).
+    """
+
+    def __init__(self, server: ExtenderServer, host: str = "127.0.0.1", port: int = 0, *, native: bool = True,
+                 http_threads: int = 2, pool_threads: int = 16):
         self.server = server
         self.host = host
         self.port = port
+        self.native = native
+        self.http_threads = http_threads
+        self.pool_threads = pool_threads
+        self.internal_port = 0
         self._runner: web.AppRunner | None = None
+        self._drain: asyncio.Task | None = None
 
     @property
     def url(self) -> str:
@@ -271,13 +285,39 @@ class ExtenderRunner:
         await self.server.start()
         self._runner = web.AppRunner(self.server.app, access_log=None, handle_signals=False, shutdown_timeout=1.0)
         await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port, backlog=1024, reuse_address=True)
-        await site.start()
-        if self.port == 0:
-            self.port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+        if self.native:
+            site = web.TCPSite(self._runner, "127.0.0.1", 0, backlog=1024, reuse_address=True)
+            await site.start()
+            self.internal_port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+            cfg = self.server.client.config
+            api = {"server": cfg.server, "token": cfg.token or "", "ca_file": cfg.ca_file or "",
+                   "cert_file": cfg.cert_file or "", "key_file": cfg.key_file or "", "insecure": bool(cfg.insecure)}
+            native_bind = self.server.bind_mode == "binding" and self.server.client.limiter.qps <= 0
+            self.port = self.server.engine.serve(self.host, self.port, self.http_threads, self.pool_threads,
+                                                 self.internal_port, native_bind, self.server.reservation_ttl, api)
+            self.server.native_server = True
+            self._drain = asyncio.get_running_loop().create_task(self._drain_failures())
+        else:
+            site = web.TCPSite(self._runner, self.host, self.port, backlog=1024, reuse_address=True)
+            await site.start()
+            if self.port == 0:
+                self.port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
         return self
 
+    async def _drain_failures(self):
+        """Native bind failures -> Warning events + metrics (the C++ path does not call Python)."""
+        while True:
+            await asyncio.sleep(0.2)
+            for f in self.server.engine.drain_bind_failures():
+                self.server.metrics.bind_results.labels("native_fail").inc()
+                pod = {"kind": "Pod", "metadata": {"name": f["name"], "namespace": f["namespace"], "uid": f["uid"]}}
+                self.server._event(pod, "FailedBinding", f["message"])  # noqa: SLF001
+
     async def stop(self):
+        if self._drain:
+            self._drain.cancel()
+        if self.native:
+            await asyncio.get_running_loop().run_in_executor(None, self.server.engine.stop_server)
         if self._runner:
             await self._runner.cleanup()
         await self.server.stop()

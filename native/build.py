@@ -84,7 +84,7 @@ def build_engine(force: bool = False, verbose: bool = False) -> Path:
     objs = _compile_objs(srcs, "g++", flags, "engine", force, verbose, headers)
     if force or _newer(out, objs):
         OUT.mkdir(parents=True, exist_ok=True)
-        _run(["g++", "-shared", "-o", str(out), *map(str, objs)], verbose)
+        _run(["g++", "-shared", "-o", str(out), *map(str, objs), "-lssl", "-lcrypto", "-lpthread"], verbose)
     return out
 
 
@@ -146,7 +146,7 @@ def build_asan(force: bool = False, verbose: bool = False) -> Path:
     if force or _newer(out, srcs + sorted(src.glob("*.h"))):
         out.parent.mkdir(parents=True, exist_ok=True)
         _run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
-              "-I" + str(src), *map(str, srcs), "-o", str(out)], verbose)
+              "-I" + str(src), *map(str, srcs), "-o", str(out), "-lssl", "-lcrypto", "-lpthread"], verbose)
     return out
 
 

@@ -1,0 +1,277 @@
+#include "apiclient.h"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
+#include <sys/socket.h>
+#include <sys/time.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+
+namespace gsx {
+
+namespace {
+
+std::string ssl_err() {
+  unsigned long e = ERR_get_error();
+  char buf[256];
+  ERR_error_string_n(e, buf, sizeof(buf));
+  return buf;
+}
+
+bool is_ip(const std::string& h) {
+  unsigned char b[16];
+  return inet_pton(AF_INET, h.c_str(), b) == 1 || inet_pton(AF_INET6, h.c_str(), b) == 1;
+}
+
+}  // namespace
+
+ApiClient::ApiClient(ApiConfig cfg) : cfg_(std::move(cfg)) {
+  if (!http::parse_url(cfg_.server, &url_)) {
+    init_err_ = "bad apiserver url: " + cfg_.server;
+    return;
+  }
+  if (url_.tls) {
+    ctx_ = SSL_CTX_new(TLS_client_method());
+    if (!ctx_) {
+      init_err_ = "SSL_CTX_new: " + ssl_err();
+      return;
+    }
+    SSL_CTX_set_min_proto_version(ctx_, TLS1_2_VERSION);
+    if (cfg_.insecure) {
+      SSL_CTX_set_verify(ctx_, SSL_VERIFY_NONE, nullptr);
+    } else {
+      SSL_CTX_set_verify(ctx_, SSL_VERIFY_PEER, nullptr);
+      int r = cfg_.ca_file.empty() ? SSL_CTX_set_default_verify_paths(ctx_)
+                                   : SSL_CTX_load_verify_locations(ctx_, cfg_.ca_file.c_str(), nullptr);
+      if (r != 1) {
+        init_err_ = "loading CA: " + ssl_err();
+        return;
+      }
+    }
+    if (!cfg_.cert_file.empty() && !cfg_.key_file.empty()) {
+      if (SSL_CTX_use_certificate_chain_file(ctx_, cfg_.cert_file.c_str()) != 1 ||
+          SSL_CTX_use_PrivateKey_file(ctx_, cfg_.key_file.c_str(), SSL_FILETYPE_PEM) != 1) {
+        init_err_ = "loading client cert: " + ssl_err();
+        return;
+      }
+    }
+  }
+  ok_ = true;
+}
+
+ApiClient::~ApiClient() {
+  std::lock_guard<std::mutex> g(mu_);
+  for (Conn* c : idle_) {
+    close_conn(c);
+    delete c;
+  }
+  idle_.clear();
+  if (ctx_) SSL_CTX_free(ctx_);
+}
+
+void ApiClient::close_conn(Conn* c) {
+  if (c->ssl) {
+    SSL_shutdown(c->ssl);
+    SSL_free(c->ssl);
+    c->ssl = nullptr;
+  }
+  if (c->fd >= 0) ::close(c->fd);
+  c->fd = -1;
+}
+
+ApiClient::Conn* ApiClient::acquire(std::string* err) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!idle_.empty()) {
+      Conn* c = idle_.back();
+      idle_.pop_back();
+      return c;
+    }
+  }
+  addrinfo hints;
+  std::memset(&hints, 0, sizeof(hints));
+  hints.ai_socktype = SOCK_STREAM;
+  hints.ai_family = AF_UNSPEC;
+  addrinfo* res = nullptr;
+  std::string port = std::to_string(url_.port);
+  int gr = getaddrinfo(url_.host.c_str(), port.c_str(), &hints, &res);
+  if (gr != 0) {
+    *err = std::string("resolve ") + url_.host + ": " + gai_strerror(gr);
+    return nullptr;
+  }
+  int fd = -1;
+  for (addrinfo* a = res; a; a = a->ai_next) {
+    fd = ::socket(a->ai_family, a->ai_socktype | SOCK_CLOEXEC, a->ai_protocol);
+    if (fd < 0) continue;
+    timeval tv;
+    tv.tv_sec = static_cast<long>(cfg_.timeout_s);
+    tv.tv_usec = static_cast<long>((cfg_.timeout_s - static_cast<double>(tv.tv_sec)) * 1e6);
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    if (::connect(fd, a->ai_addr, a->ai_addrlen) == 0) break;
+    ::close(fd);
+    fd = -1;
+  }
+  freeaddrinfo(res);
+  if (fd < 0) {
+    *err = "connect " + cfg_.server + ": " + std::strerror(errno);
+    return nullptr;
+  }
+  Conn* c = new Conn();
+  c->fd = fd;
+  if (url_.tls) {
+    c->ssl = SSL_new(ctx_);
+    SSL_set_fd(c->ssl, fd);
+    SSL_set_tlsext_host_name(c->ssl, url_.host.c_str());
+    if (!cfg_.insecure) {
+      X509_VERIFY_PARAM* p = SSL_get0_param(c->ssl);
+      if (is_ip(url_.host)) {
+        X509_VERIFY_PARAM_set1_ip_asc(p, url_.host.c_str());
+      } else {
+        X509_VERIFY_PARAM_set1_host(p, url_.host.c_str(), 0);
+      }
+    }
+    if (SSL_connect(c->ssl) != 1) {
+      *err = "TLS handshake with " + cfg_.server + ": " + ssl_err();
+      close_conn(c);
+      delete c;
+      return nullptr;
+    }
+  }
+  ++reconnects_;
+  return c;
+}
+
+void ApiClient::release(Conn* c, bool reuse) {
+  if (!reuse) {
+    close_conn(c);
+    delete c;
+    return;
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  if (idle_.size() >= 64) {
+    close_conn(c);
+    delete c;
+    return;
+  }
+  idle_.push_back(c);
+}
+
+bool ApiClient::send_all(Conn* c, const std::string& data) {
+  size_t off = 0;
+  while (off < data.size()) {
+    long w;
+    if (c->ssl) {
+      w = SSL_write(c->ssl, data.data() + off, static_cast<int>(data.size() - off));
+      if (w <= 0) return false;
+    } else {
+      w = ::send(c->fd, data.data() + off, data.size() - off, MSG_NOSIGNAL);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        return false;
+      }
+    }
+    off += static_cast<size_t>(w);
+  }
+  return true;
+}
+
+long ApiClient::recv_some(Conn* c, char* buf, size_t n) {
+  if (c->ssl) {
+    int r = SSL_read(c->ssl, buf, static_cast<int>(n));
+    return r > 0 ? r : (SSL_get_error(c->ssl, r) == SSL_ERROR_ZERO_RETURN ? 0 : -1);
+  }
+  while (true) {
+    long r = ::recv(c->fd, buf, n, 0);
+    if (r < 0 && errno == EINTR) continue;
+    return r;
+  }
+}
+
+bool ApiClient::request(const std::string& method, const std::string& path, const std::string& body,
+                        const char* content_type, int* status, std::string* resp, std::string* err,
+                        std::string* resp_content_type) {
+  if (!ok_) {
+    *err = init_err_;
+    return false;
+  }
+  std::string req;
+  req.reserve(256 + body.size());
+  req.append(method).append(" ").append(url_.prefix).append(path).append(" HTTP/1.1\r\nHost: ");
+  req.append(url_.host);
+  if ((url_.tls && url_.port != 443) || (!url_.tls && url_.port != 80)) req.append(":").append(std::to_string(url_.port));
+  req.append("\r\nUser-Agent: ").append(cfg_.user_agent);
+  req.append("\r\nAccept: application/json\r\n");
+  if (!cfg_.token.empty()) req.append("Authorization: Bearer ").append(cfg_.token).append("\r\n");
+  if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
+    req.append("Content-Type: ").append(content_type ? content_type : "application/json").append("\r\n");
+    req.append("Content-Length: ").append(std::to_string(body.size())).append("\r\n");
+  }
+  req.append("\r\n").append(body);
+
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    Conn* c = acquire(err);
+    if (!c) return false;
+    bool fresh_fail = false;
+    if (!send_all(c, req)) {
+      release(c, false);
+      if (attempt == 0) continue;  // stale keep-alive connection: retry once on a new one
+      *err = "send to apiserver failed";
+      return false;
+    }
+    http::Message m;
+    std::string perr;
+    char buf[16384];
+    c->rbuf.clear();
+    while (true) {
+      long got = http::parse(c->rbuf.data(), c->rbuf.size(), false, &m, &perr, false);
+      if (got > 0) break;
+      if (got < 0) {
+        release(c, false);
+        *err = "bad response from apiserver: " + perr;
+        return false;
+      }
+      long r = recv_some(c, buf, sizeof(buf));
+      if (r == 0) {
+        long got2 = http::parse(c->rbuf.data(), c->rbuf.size(), false, &m, &perr, true);
+        if (got2 > 0) break;
+        fresh_fail = c->rbuf.empty();
+        break;
+      }
+      if (r < 0) {
+        fresh_fail = c->rbuf.empty();
+        break;
+      }
+      c->rbuf.append(buf, static_cast<size_t>(r));
+    }
+    if (m.status == 0) {
+      release(c, false);
+      if (fresh_fail && attempt == 0) continue;
+      *err = "apiserver closed the connection";
+      return false;
+    }
+    ++requests_;
+    *status = m.status;
+    if (resp_content_type) {
+      const std::string* ct = m.header("content-type");
+      *resp_content_type = ct ? *ct : std::string();
+    }
+    *resp = std::move(m.body);
+    release(c, m.keep_alive && !m.body_until_close);
+    return true;
+  }
+  *err = "apiserver request failed";
+  return false;
+}
+
+}  // namespace gsx

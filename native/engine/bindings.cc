@@ -5,8 +5,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <memory>
+
 #include "ledger.h"
 #include "quantity.h"
+#include "server.h"
 
 namespace py = pybind11;
 using namespace gsx;
@@ -234,6 +237,100 @@ class Engine {
     return d;
   }
 
+  // ---- native HTTP front end (server.h) ----
+  int serve(const std::string& host, int port, int threads, int pool_threads, int fallback_port, bool native_bind,
+            double ttl, const py::dict& api) {
+    if (srv_) throw std::runtime_error("native server already running");
+    ServerConfig cfg;
+    cfg.host = host;
+    cfg.port = port;
+    cfg.threads = threads;
+    cfg.pool_threads = pool_threads;
+    cfg.fallback_port = fallback_port;
+    cfg.native_bind = native_bind;
+    cfg.reservation_ttl = ttl;
+    auto get = [&](const char* k, std::string* dst) {
+      if (api.contains(k) && !api[k].is_none()) *dst = api[k].cast<std::string>();
+    };
+    get("server", &cfg.api.server);
+    get("token", &cfg.api.token);
+    get("ca_file", &cfg.api.ca_file);
+    get("cert_file", &cfg.api.cert_file);
+    get("key_file", &cfg.api.key_file);
+    if (api.contains("insecure")) cfg.api.insecure = api["insecure"].cast<bool>();
+    if (cfg.api.server.empty()) cfg.native_bind = false;
+    srv_.reset(new NativeServer(&l_, cfg));
+    std::string err;
+    int p = srv_->start(&err);
+    if (p < 0) {
+      srv_.reset();
+      throw std::runtime_error(err);
+    }
+    return p;
+  }
+
+  void stop_server() {
+    if (srv_) {
+      py::gil_scoped_release rel;
+      srv_->stop();
+    }
+    srv_.reset();
+  }
+
+  py::dict server_stats() {
+    py::dict d;
+    if (!srv_) return d;
+    const ServerStats& s = srv_->stats();
+    d["requests"] = s.requests.load();
+    d["filters"] = s.filters.load();
+    d["binds"] = s.binds.load();
+    d["bind_ok"] = s.bind_ok.load();
+    d["bind_fail"] = s.bind_fail.load();
+    d["proxied"] = s.proxied.load();
+    d["bad_requests"] = s.bad_requests.load();
+    d["inspects"] = s.inspects.load();
+    d["connections"] = s.connections.load();
+    d["api_calls"] = s.api_calls.load();
+    d["conflicts_retried"] = s.conflicts_retried.load();
+    auto hist = [](const LatencyHist& h) {
+      py::dict o;
+      py::list bounds, counts;
+      for (int i = 0; i < LatencyHist::kBuckets; ++i) bounds.append(LatencyHist::kBounds[i]);
+      for (int i = 0; i <= LatencyHist::kBuckets; ++i) counts.append(h.counts[i].load());
+      o["bounds"] = bounds;
+      o["counts"] = counts;
+      o["n"] = h.n.load();
+      o["sum"] = static_cast<double>(h.sum_ns.load()) / 1e9;
+      return o;
+    };
+    d["filter_latency"] = hist(s.filter_lat);
+    d["bind_latency"] = hist(s.bind_lat);
+    d["api_latency"] = hist(s.api_lat);
+    return d;
+  }
+
+  py::list drain_bind_failures() {
+    py::list out;
+    if (!srv_) return out;
+    for (auto& f : srv_->drain_failures()) {
+      py::dict d;
+      d["namespace"] = f.ns;
+      d["name"] = f.name;
+      d["uid"] = f.uid;
+      d["node"] = f.node;
+      d["message"] = f.message;
+      out.append(d);
+    }
+    return out;
+  }
+
+  size_t pending_count() {
+    std::lock_guard<std::mutex> g(l_.mu());
+    return l_.pending_count();
+  }
+
+  ~Engine() { stop_server(); }
+
   PodView parse_pod(const py::bytes& b) {
     PodView v;
     std::string err;
@@ -243,6 +340,7 @@ class Engine {
 
  private:
   Ledger l_;
+  std::unique_ptr<NativeServer> srv_;  // declared after l_: destroyed (stopped) first
 };
 
 }  // namespace
@@ -298,7 +396,14 @@ PYBIND11_MODULE(_engine, m) {
       .def("node_devices", &Engine::node_devices)
       .def("node_names", &Engine::node_names)
       .def("stats", &Engine::stats)
-      .def("parse_pod", &Engine::parse_pod);
+      .def("parse_pod", &Engine::parse_pod)
+      .def("serve", &Engine::serve, py::arg("host"), py::arg("port"), py::arg("threads") = 2,
+           py::arg("pool_threads") = 16, py::arg("fallback_port") = 0, py::arg("native_bind") = true,
+           py::arg("ttl") = 60.0, py::arg("api") = py::dict())
+      .def("stop_server", &Engine::stop_server)
+      .def("server_stats", &Engine::server_stats)
+      .def("drain_bind_failures", &Engine::drain_bind_failures)
+      .def("pending_count", &Engine::pending_count);
 
   m.def("parse_quantity", [](const std::string& s) {
     int64_t v;

@@ -1,0 +1,273 @@
+#include "http.h"
+
+#include <cctype>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+namespace gsx {
+namespace http {
+
+namespace {
+
+std::string lower(std::string_view s) {
+  std::string o(s);
+  for (char& c : o) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  return o;
+}
+
+std::string_view trim(std::string_view s) {
+  while (!s.empty() && (s.front() == ' ' || s.front() == '\t')) s.remove_prefix(1);
+  while (!s.empty() && (s.back() == ' ' || s.back() == '\t' || s.back() == '\r')) s.remove_suffix(1);
+  return s;
+}
+
+bool contains_token(std::string_view v, std::string_view tok) {
+  // comma-separated, case-insensitive
+  size_t i = 0;
+  while (i <= v.size()) {
+    size_t j = v.find(',', i);
+    if (j == std::string_view::npos) j = v.size();
+    std::string_view t = trim(v.substr(i, j - i));
+    if (t.size() == tok.size()) {
+      bool eq = true;
+      for (size_t k = 0; k < t.size(); ++k) {
+        if (std::tolower(static_cast<unsigned char>(t[k])) != std::tolower(static_cast<unsigned char>(tok[k]))) {
+          eq = false;
+          break;
+        }
+      }
+      if (eq) return true;
+    }
+    i = j + 1;
+  }
+  return false;
+}
+
+}  // namespace
+
+const std::string* Message::header(std::string_view name) const {
+  for (const auto& h : headers) {
+    if (h.first == name) return &h.second;
+  }
+  return nullptr;
+}
+
+std::string_view Message::path() const {
+  std::string_view t(target);
+  size_t q = t.find('?');
+  return q == std::string_view::npos ? t : t.substr(0, q);
+}
+
+long parse(const char* buf, size_t n, bool is_request, Message* out, std::string* err, bool eof, size_t max_body) {
+  std::string_view s(buf, n);
+  size_t hend = s.find("\r\n\r\n");
+  if (hend == std::string_view::npos) {
+    if (n > (64u << 10)) {
+      *err = "header too large";
+      return -1;
+    }
+    return 0;
+  }
+  *out = Message();
+  std::string_view head = s.substr(0, hend);
+  size_t le = head.find("\r\n");
+  std::string_view start = head.substr(0, le);
+  // start line
+  if (is_request) {
+    size_t a = start.find(' ');
+    size_t b = a == std::string_view::npos ? a : start.find(' ', a + 1);
+    if (a == std::string_view::npos || b == std::string_view::npos) {
+      *err = "bad request line";
+      return -1;
+    }
+    out->method = std::string(start.substr(0, a));
+    out->target = std::string(start.substr(a + 1, b - a - 1));
+    std::string_view ver = start.substr(b + 1);
+    if (ver.size() != 8 || ver.substr(0, 5) != "HTTP/") {
+      *err = "bad http version";
+      return -1;
+    }
+    out->minor_version = ver[7] - '0';
+  } else {
+    if (start.size() < 12 || start.substr(0, 5) != "HTTP/") {
+      *err = "bad status line";
+      return -1;
+    }
+    out->minor_version = start[7] - '0';
+    out->status = std::atoi(std::string(start.substr(9, 3)).c_str());
+    out->reason = start.size() > 13 ? std::string(start.substr(13)) : std::string();
+  }
+  // headers
+  size_t pos = le == std::string_view::npos ? head.size() : le + 2;
+  long content_length = -1;
+  bool chunked = false;
+  bool conn_close = false, conn_keep = false;
+  while (pos < head.size()) {
+    size_t e = head.find("\r\n", pos);
+    if (e == std::string_view::npos) e = head.size();
+    std::string_view line = head.substr(pos, e - pos);
+    size_t c = line.find(':');
+    if (c == std::string_view::npos) {
+      *err = "bad header line";
+      return -1;
+    }
+    std::string name = lower(trim(line.substr(0, c)));
+    std::string_view val = trim(line.substr(c + 1));
+    if (name == "content-length") {
+      char* endp = nullptr;
+      std::string v(val);
+      long cl = std::strtol(v.c_str(), &endp, 10);
+      if (!endp || *endp || cl < 0) {
+        *err = "bad content-length";
+        return -1;
+      }
+      content_length = cl;
+    } else if (name == "transfer-encoding") {
+      chunked = contains_token(val, "chunked");
+    } else if (name == "connection") {
+      conn_close = contains_token(val, "close");
+      conn_keep = contains_token(val, "keep-alive");
+    }
+    out->headers.emplace_back(std::move(name), std::string(val));
+    pos = e + 2;
+  }
+  out->keep_alive = out->minor_version >= 1 ? !conn_close : conn_keep;
+  size_t body_start = hend + 4;
+  if (chunked) {
+    size_t p = body_start;
+    std::string body;
+    while (true) {
+      size_t e = s.find("\r\n", p);
+      if (e == std::string_view::npos) return 0;
+      std::string szs(s.substr(p, e - p));
+      size_t semi = szs.find(';');
+      if (semi != std::string::npos) szs.resize(semi);
+      char* endp = nullptr;
+      unsigned long sz = std::strtoul(szs.c_str(), &endp, 16);
+      if (endp == szs.c_str()) {
+        *err = "bad chunk size";
+        return -1;
+      }
+      p = e + 2;
+      if (sz == 0) {
+        // trailers until empty line
+        while (true) {
+          size_t e2 = s.find("\r\n", p);
+          if (e2 == std::string_view::npos) return 0;
+          if (e2 == p) {
+            p += 2;
+            break;
+          }
+          p = e2 + 2;
+        }
+        out->body = std::move(body);
+        return static_cast<long>(p);
+      }
+      if (body.size() + sz > max_body) {
+        *err = "body too large";
+        return -1;
+      }
+      if (n < p + sz + 2) return 0;
+      body.append(buf + p, sz);
+      p += sz + 2;
+    }
+  }
+  if (content_length >= 0) {
+    if (static_cast<size_t>(content_length) > max_body) {
+      *err = "body too large";
+      return -1;
+    }
+    if (n < body_start + static_cast<size_t>(content_length)) return 0;
+    out->body.assign(buf + body_start, static_cast<size_t>(content_length));
+    return static_cast<long>(body_start + static_cast<size_t>(content_length));
+  }
+  if (is_request || out->status == 204 || out->status == 304 || (out->status >= 100 && out->status < 200)) {
+    return static_cast<long>(body_start);
+  }
+  // response delimited by connection close
+  out->body_until_close = true;
+  out->keep_alive = false;
+  if (!eof) return 0;
+  out->body.assign(buf + body_start, n - body_start);
+  return static_cast<long>(n);
+}
+
+const char* reason_phrase(int status) {
+  switch (status) {
+    case 200: return "OK";
+    case 201: return "Created";
+    case 204: return "No Content";
+    case 400: return "Bad Request";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 409: return "Conflict";
+    case 413: return "Payload Too Large";
+    case 500: return "Internal Server Error";
+    case 502: return "Bad Gateway";
+    case 503: return "Service Unavailable";
+    default: return "Status";
+  }
+}
+
+std::string response(int status, std::string_view content_type, std::string_view body, bool keep_alive,
+                     std::string_view extra_headers) {
+  std::string o;
+  o.reserve(160 + body.size());
+  char line[96];
+  int k = std::snprintf(line, sizeof(line), "HTTP/1.1 %d %s\r\n", status, reason_phrase(status));
+  o.append(line, static_cast<size_t>(k));
+  if (!content_type.empty()) {
+    o.append("Content-Type: ");
+    o.append(content_type);
+    o.append("\r\n");
+  }
+  k = std::snprintf(line, sizeof(line), "Content-Length: %zu\r\n", body.size());
+  o.append(line, static_cast<size_t>(k));
+  if (!keep_alive) o.append("Connection: close\r\n");
+  o.append(extra_headers);
+  o.append("\r\n");
+  o.append(body);
+  return o;
+}
+
+bool parse_url(const std::string& s, Url* out) {
+  *out = Url();
+  std::string rest;
+  if (s.rfind("https://", 0) == 0) {
+    out->tls = true;
+    out->port = 443;
+    rest = s.substr(8);
+  } else if (s.rfind("http://", 0) == 0) {
+    rest = s.substr(7);
+  } else {
+    return false;
+  }
+  size_t slash = rest.find('/');
+  std::string hostport = rest.substr(0, slash);
+  if (slash != std::string::npos) {
+    out->prefix = rest.substr(slash);
+    while (!out->prefix.empty() && out->prefix.back() == '/') out->prefix.pop_back();
+  }
+  if (!hostport.empty() && hostport[0] == '[') {
+    size_t rb = hostport.find(']');
+    if (rb == std::string::npos) return false;
+    out->host = hostport.substr(1, rb - 1);
+    if (rb + 1 < hostport.size()) {
+      if (hostport[rb + 1] != ':') return false;
+      out->port = std::atoi(hostport.c_str() + rb + 2);
+    }
+  } else {
+    size_t c = hostport.rfind(':');
+    if (c != std::string::npos) {
+      out->host = hostport.substr(0, c);
+      out->port = std::atoi(hostport.c_str() + c + 1);
+    } else {
+      out->host = hostport;
+    }
+  }
+  return !out->host.empty() && out->port > 0 && out->port < 65536;
+}
+
+}  // namespace http
+}  // namespace gsx

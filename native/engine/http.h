@@ -1,0 +1,59 @@
+// Minimal HTTP/1.1 message parsing / serialisation for the native extender
+// server and its apiserver client.
+//
+// The reference serves kube-scheduler with Go's net/http
+// (pkg/routes/routes.go, cmd/main.go:128) and talks to kube-apiserver with
+// client-go.  The native equivalents only need: request/response start lines,
+// headers, Content-Length and chunked bodies, keep-alive.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <string_view>
+#include <utility>
+#include <vector>
+
+namespace gsx {
+namespace http {
+
+struct Message {
+  // request
+  std::string method;
+  std::string target;  // path + optional ?query
+  // response
+  int status = 0;
+  std::string reason;
+  // both
+  int minor_version = 1;
+  std::vector<std::pair<std::string, std::string>> headers;  // names lower-cased
+  std::string body;
+  bool keep_alive = true;
+  bool body_until_close = false;  // response without length: read to EOF
+
+  const std::string* header(std::string_view lower_name) const;
+  std::string_view path() const;  // target without query
+};
+
+// Parse one complete message from buf[0..n).  Returns the number of bytes
+// consumed (> 0), 0 if more input is needed, -1 on a malformed message.
+// `eof` tells the parser the peer closed (completes read-to-close bodies).
+long parse(const char* buf, size_t n, bool is_request, Message* out, std::string* err, bool eof = false,
+           size_t max_body = 64u << 20);
+
+// Serialise a response.
+std::string response(int status, std::string_view content_type, std::string_view body, bool keep_alive,
+                     std::string_view extra_headers = {});
+
+const char* reason_phrase(int status);
+
+// scheme://host[:port][/prefix] -> parts.  Returns false if malformed.
+struct Url {
+  bool tls = false;
+  std::string host;  // without brackets
+  int port = 80;
+  std::string prefix;  // path prefix without trailing slash
+};
+bool parse_url(const std::string& s, Url* out);
+
+}  // namespace http
+}  // namespace gsx

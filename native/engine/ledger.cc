@@ -379,6 +379,40 @@ std::string Ledger::inspect_json(const std::string& node, bool* found) const {
   return o;
 }
 
+// ---------------------------------------------------------------- pending pods
+
+void Ledger::remember_pending(const std::string& uid, PendingPod p) {
+  auto it = pending_.find(uid);
+  if (it != pending_.end()) {
+    it->second = std::move(p);
+    return;
+  }
+  constexpr size_t kMax = 65536;
+  while (pending_.size() >= kMax && !pending_order_.empty()) {
+    pending_.erase(pending_order_.front());
+    pending_order_.pop_front();
+  }
+  pending_.emplace(uid, std::move(p));
+  pending_order_.push_back(uid);
+  if (pending_order_.size() > 2 * kMax) {
+    // drop ids already forgotten so the order queue stays bounded
+    std::deque<std::string> keep;
+    for (auto& u : pending_order_) {
+      if (pending_.count(u)) keep.push_back(u);
+    }
+    pending_order_.swap(keep);
+  }
+}
+
+bool Ledger::pending(const std::string& uid, PendingPod* out) const {
+  auto it = pending_.find(uid);
+  if (it == pending_.end()) return false;
+  *out = it->second;
+  return true;
+}
+
+void Ledger::forget_pending(const std::string& uid) { pending_.erase(uid); }
+
 // ---------------------------------------------------------------- filter verb
 
 std::string filter_body(Ledger& l, std::string_view body) {
@@ -401,6 +435,18 @@ std::string filter_body(Ledger& l, std::string_view body) {
   }
   const Profile& p = l.profile();
   int64_t req = pod_limits_sum(d, static_cast<uint32_t>(pod), p.resource);
+  {
+    int64_t u = d.path(static_cast<uint32_t>(pod), {"metadata", "uid"});
+    if (u >= 0 && d.at(static_cast<uint32_t>(u)).type == json::T::String) {
+      Ledger::PendingPod pp;
+      int64_t nm = d.path(static_cast<uint32_t>(pod), {"metadata", "name"});
+      int64_t ns = d.path(static_cast<uint32_t>(pod), {"metadata", "namespace"});
+      if (nm >= 0) pp.name = d.str(static_cast<uint32_t>(nm));
+      pp.ns = ns >= 0 ? d.str(static_cast<uint32_t>(ns)) : std::string("default");
+      pp.req = req;
+      l.remember_pending(d.str(static_cast<uint32_t>(u)), std::move(pp));
+    }
+  }
 
   // Candidate nodes: NodeNames (nodeCacheCapable) or Nodes.items.
   struct Cand {

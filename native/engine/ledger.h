@@ -21,6 +21,7 @@
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
+#include <deque>
 #include <vector>
 
 #include "model.h"
@@ -116,6 +117,18 @@ class Ledger {
 
   std::mutex& mu() { return mu_; }
 
+  // ---- pods seen by the filter verb (native bind fast path) ----
+  // The filter request carries the whole v1.Pod; remembering (uid -> ns,
+  // name, request) lets the native bind skip the lister lookup.  Bounded FIFO.
+  struct PendingPod {
+    std::string ns, name;
+    int64_t req = 0;
+  };
+  void remember_pending(const std::string& uid, PendingPod p);
+  bool pending(const std::string& uid, PendingPod* out) const;
+  void forget_pending(const std::string& uid);
+  size_t pending_count() const { return pending_.size(); }
+
  private:
   void account(PodRec& r);
   void unaccount(PodRec& r);
@@ -127,6 +140,8 @@ class Ledger {
   std::unordered_map<std::string, PodRec> pods_;
   Stats stats_;
   mutable std::mutex mu_;
+  std::unordered_map<std::string, PendingPod> pending_;
+  std::deque<std::string> pending_order_;
 };
 
 // Full filter verb on a raw ExtenderArgs body; returns the

@@ -1,0 +1,616 @@
+#include "server.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+
+#include "json.h"
+
+namespace gsx {
+
+const double LatencyHist::kBounds[LatencyHist::kBuckets] = {0.0001, 0.00025, 0.0005, 0.001, 0.0025,
+                                                             0.005,  0.01,    0.025,  0.05,  0.1,
+                                                             0.25,   0.5,     1.0,    2.5,   5.0};
+
+void LatencyHist::observe(double s) {
+  int i = 0;
+  while (i < kBuckets && s > kBounds[i]) ++i;
+  counts[i].fetch_add(1, std::memory_order_relaxed);
+  n.fetch_add(1, std::memory_order_relaxed);
+  sum_ns.fetch_add(static_cast<uint64_t>(s * 1e9), std::memory_order_relaxed);
+}
+
+namespace {
+
+constexpr uint64_t kListenId = 1;
+constexpr uint64_t kEventId = 2;
+constexpr const char* kPrefix = "/gpushare-scheduler";
+constexpr const char* kVersion = "0.1.0";
+
+double mono() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int64_t unix_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
+
+std::string error_body(const std::string& msg) {
+  std::string o("{\"Error\":");
+  json::append_quoted(&o, msg);
+  o.push_back('}');
+  return o;
+}
+
+// Go-style lookup of a string member of the ExtenderBindingArgs object.
+bool arg_str(const json::Doc& d, const char* key, std::string* out) {
+  int64_t i = d.find(0, key, true);
+  if (i < 0) {
+    out->clear();
+    return true;
+  }
+  const json::Val& v = d.at(static_cast<uint32_t>(i));
+  if (v.type == json::T::Null) {
+    out->clear();
+    return true;
+  }
+  if (v.type != json::T::String) return false;
+  *out = d.str(static_cast<uint32_t>(i));
+  return true;
+}
+
+std::string status_message(const std::string& body, int status) {
+  json::Doc d;
+  std::string e;
+  if (!body.empty() && d.parse(body, &e) && d.at(0).type == json::T::Object) {
+    int64_t m = d.find(0, "message");
+    if (m >= 0 && d.at(static_cast<uint32_t>(m)).type == json::T::String) return d.str(static_cast<uint32_t>(m));
+  }
+  return "apiserver returned HTTP " + std::to_string(status);
+}
+
+std::string url_escape_path(const std::string& s) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string o;
+  for (unsigned char c : s) {
+    if (std::isalnum(c) || c == '-' || c == '.' || c == '_' || c == '~') {
+      o.push_back(static_cast<char>(c));
+    } else {
+      o.push_back('%');
+      o.push_back(hex[c >> 4]);
+      o.push_back(hex[c & 15]);
+    }
+  }
+  return o;
+}
+
+}  // namespace
+
+struct NativeServer::Conn {
+  int fd = -1;
+  uint64_t id = 0;
+  std::string in;
+  std::string out;
+  size_t out_off = 0;
+  bool busy = false;
+  bool close_after = false;
+  bool want_write = false;
+};
+
+struct NativeServer::Loop {
+  int ep = -1;
+  int lfd = -1;
+  int efd = -1;
+  uint64_t next_id = 16;
+  std::unordered_map<uint64_t, Conn*> conns;
+  std::mutex cmu;
+  std::deque<std::tuple<uint64_t, std::string, bool>> done;
+};
+
+NativeServer::NativeServer(Ledger* ledger, ServerConfig cfg) : l_(ledger), cfg_(std::move(cfg)) {}
+
+NativeServer::~NativeServer() { stop(); }
+
+int NativeServer::start(std::string* err) {
+  if (cfg_.threads < 1) cfg_.threads = 1;
+  if (cfg_.pool_threads < 1) cfg_.pool_threads = 1;
+  if (cfg_.native_bind) {
+    api_.reset(new ApiClient(cfg_.api));
+    if (!api_->ok()) {
+      *err = "apiserver client: " + api_->init_error();
+      return -1;
+    }
+  }
+  if (cfg_.fallback_port > 0) {
+    ApiConfig fc;
+    fc.server = "http://127.0.0.1:" + std::to_string(cfg_.fallback_port);
+    fc.timeout_s = 120.0;
+    fallback_.reset(new ApiClient(fc));
+  }
+  int port = cfg_.port;
+  for (int i = 0; i < cfg_.threads; ++i) {
+    std::unique_ptr<Loop> lp(new Loop());
+    addrinfo hints;
+    std::memset(&hints, 0, sizeof(hints));
+    hints.ai_family = AF_UNSPEC;
+    hints.ai_socktype = SOCK_STREAM;
+    hints.ai_flags = AI_PASSIVE | AI_NUMERICHOST;
+    addrinfo* res = nullptr;
+    std::string ps = std::to_string(port);
+    int gr = getaddrinfo(cfg_.host.empty() ? nullptr : cfg_.host.c_str(), ps.c_str(), &hints, &res);
+    if (gr != 0) {
+      *err = std::string("listen address ") + cfg_.host + ": " + gai_strerror(gr);
+      return -1;
+    }
+    int fd = ::socket(res->ai_family, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    setsockopt(fd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one));
+    if (::bind(fd, res->ai_addr, res->ai_addrlen) != 0 || ::listen(fd, 1024) != 0) {
+      *err = std::string("bind/listen on port ") + ps + ": " + std::strerror(errno);
+      freeaddrinfo(res);
+      ::close(fd);
+      return -1;
+    }
+    freeaddrinfo(res);
+    if (port == 0) {
+      sockaddr_storage ss;
+      socklen_t sl = sizeof(ss);
+      getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &sl);
+      port = ss.ss_family == AF_INET6 ? ntohs(reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port)
+                                      : ntohs(reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
+    }
+    set_nonblock(fd);
+    lp->lfd = fd;
+    lp->ep = epoll_create1(EPOLL_CLOEXEC);
+    lp->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    epoll_event ev;
+    ev.events = EPOLLIN;
+    ev.data.u64 = kListenId;
+    epoll_ctl(lp->ep, EPOLL_CTL_ADD, lp->lfd, &ev);
+    ev.data.u64 = kEventId;
+    epoll_ctl(lp->ep, EPOLL_CTL_ADD, lp->efd, &ev);
+    loops_.push_back(std::move(lp));
+  }
+  port_ = port;
+  for (auto& lp : loops_) loop_threads_.emplace_back([this, p = lp.get()] { run_loop(p); });
+  for (int i = 0; i < cfg_.pool_threads; ++i) pool_threads_.emplace_back([this] { pool_main(); });
+  return port_;
+}
+
+void NativeServer::stop() {
+  if (stop_.exchange(true)) return;
+  for (auto& lp : loops_) {
+    uint64_t one = 1;
+    if (write(lp->efd, &one, sizeof(one)) < 0) {
+    }
+  }
+  jcv_.notify_all();
+  for (auto& t : loop_threads_) t.join();
+  for (auto& t : pool_threads_) t.join();
+  loop_threads_.clear();
+  pool_threads_.clear();
+  for (auto& lp : loops_) {
+    for (auto& kv : lp->conns) {
+      ::close(kv.second->fd);
+      delete kv.second;
+    }
+    lp->conns.clear();
+    ::close(lp->lfd);
+    ::close(lp->efd);
+    ::close(lp->ep);
+  }
+  loops_.clear();
+}
+
+std::vector<BindFailure> NativeServer::drain_failures() {
+  std::lock_guard<std::mutex> g(fmu_);
+  std::vector<BindFailure> out;
+  out.swap(failures_);
+  return out;
+}
+
+void NativeServer::record_failure(BindFailure f) {
+  std::lock_guard<std::mutex> g(fmu_);
+  if (failures_.size() < 4096) failures_.push_back(std::move(f));
+}
+
+// ------------------------------------------------------------------ event loop
+
+void NativeServer::run_loop(Loop* lp) {
+  epoll_event evs[128];
+  while (!stop_.load()) {
+    int n = epoll_wait(lp->ep, evs, 128, 500);
+    for (int i = 0; i < n; ++i) {
+      uint64_t id = evs[i].data.u64;
+      if (id == kListenId) {
+        while (true) {
+          int cfd = accept4(lp->lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          if (cfd < 0) break;
+          int one = 1;
+          setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+          Conn* c = new Conn();
+          c->fd = cfd;
+          c->id = lp->next_id++;
+          lp->conns[c->id] = c;
+          epoll_event ev;
+          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.data.u64 = c->id;
+          epoll_ctl(lp->ep, EPOLL_CTL_ADD, cfd, &ev);
+          stats_.connections.fetch_add(1, std::memory_order_relaxed);
+        }
+      } else if (id == kEventId) {
+        uint64_t v;
+        while (read(lp->efd, &v, sizeof(v)) > 0) {
+        }
+        drain_completions(lp);
+      } else {
+        auto it = lp->conns.find(id);
+        if (it == lp->conns.end()) continue;
+        Conn* c = it->second;
+        if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
+          close_conn(lp, c);
+          continue;
+        }
+        if (evs[i].events & EPOLLOUT) {
+          flush(lp, c);
+          if (lp->conns.find(id) == lp->conns.end()) continue;
+        }
+        if (evs[i].events & (EPOLLIN | EPOLLRDHUP)) on_readable(lp, c);
+      }
+    }
+  }
+}
+
+void NativeServer::on_readable(Loop* lp, Conn* c) {
+  char buf[65536];
+  bool eof = false;
+  while (true) {
+    ssize_t r = ::recv(c->fd, buf, sizeof(buf), 0);
+    if (r > 0) {
+      c->in.append(buf, static_cast<size_t>(r));
+      if (c->in.size() > cfg_.max_body + (64u << 10)) {
+        close_conn(lp, c);
+        return;
+      }
+      continue;
+    }
+    if (r == 0) eof = true;
+    break;  // EAGAIN or error
+  }
+  uint64_t id = c->id;
+  process(lp, c);
+  if (eof && lp->conns.count(id)) {
+    Conn* cc = lp->conns[id];
+    if (!cc->busy && cc->out_off >= cc->out.size()) {
+      close_conn(lp, cc);
+    } else {
+      cc->close_after = true;
+    }
+  }
+}
+
+void NativeServer::process(Loop* lp, Conn* c) {
+  uint64_t id = c->id;
+  while (!c->busy && !c->in.empty()) {
+    http::Message req;
+    std::string perr;
+    long used = http::parse(c->in.data(), c->in.size(), true, &req, &perr, false, cfg_.max_body);
+    if (used == 0) return;
+    if (used < 0) {
+      stats_.bad_requests.fetch_add(1, std::memory_order_relaxed);
+      respond(lp, c, http::response(400, "text/plain", perr, false), false);
+      return;
+    }
+    c->in.erase(0, static_cast<size_t>(used));
+    stats_.requests.fetch_add(1, std::memory_order_relaxed);
+    dispatch(lp, c, req);
+    if (!lp->conns.count(id)) return;
+  }
+}
+
+void NativeServer::respond(Loop* lp, Conn* c, std::string resp, bool keep_alive) {
+  c->out.append(resp);
+  if (!keep_alive) c->close_after = true;
+  flush(lp, c);
+}
+
+void NativeServer::flush(Loop* lp, Conn* c) {
+  while (c->out_off < c->out.size()) {
+    ssize_t w = ::send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+    if (w > 0) {
+      c->out_off += static_cast<size_t>(w);
+      continue;
+    }
+    if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+      if (!c->want_write) {
+        epoll_event ev;
+        ev.events = EPOLLIN | EPOLLRDHUP | EPOLLOUT;
+        ev.data.u64 = c->id;
+        epoll_ctl(lp->ep, EPOLL_CTL_MOD, c->fd, &ev);
+        c->want_write = true;
+      }
+      return;
+    }
+    close_conn(lp, c);
+    return;
+  }
+  c->out.clear();
+  c->out_off = 0;
+  if (c->want_write) {
+    epoll_event ev;
+    ev.events = EPOLLIN | EPOLLRDHUP;
+    ev.data.u64 = c->id;
+    epoll_ctl(lp->ep, EPOLL_CTL_MOD, c->fd, &ev);
+    c->want_write = false;
+  }
+  if (c->close_after && !c->busy) close_conn(lp, c);
+}
+
+void NativeServer::close_conn(Loop* lp, Conn* c) {
+  epoll_ctl(lp->ep, EPOLL_CTL_DEL, c->fd, nullptr);
+  ::close(c->fd);
+  lp->conns.erase(c->id);
+  delete c;
+}
+
+void NativeServer::complete(Loop* lp, uint64_t conn_id, std::string resp, bool keep_alive) {
+  {
+    std::lock_guard<std::mutex> g(lp->cmu);
+    lp->done.emplace_back(conn_id, std::move(resp), keep_alive);
+  }
+  uint64_t one = 1;
+  if (write(lp->efd, &one, sizeof(one)) < 0) {
+  }
+}
+
+void NativeServer::drain_completions(Loop* lp) {
+  std::deque<std::tuple<uint64_t, std::string, bool>> done;
+  {
+    std::lock_guard<std::mutex> g(lp->cmu);
+    done.swap(lp->done);
+  }
+  for (auto& t : done) {
+    auto it = lp->conns.find(std::get<0>(t));
+    if (it == lp->conns.end()) continue;  // client went away meanwhile
+    Conn* c = it->second;
+    c->busy = false;
+    uint64_t id = c->id;
+    respond(lp, c, std::move(std::get<1>(t)), std::get<2>(t));
+    if (lp->conns.count(id)) process(lp, c);
+  }
+}
+
+// ------------------------------------------------------------------ routing
+
+void NativeServer::dispatch(Loop* lp, Conn* c, http::Message& req) {
+  double t0 = mono();
+  std::string_view path = req.path();
+  const bool ka = req.keep_alive;
+  const std::string pre(kPrefix);
+  if (req.method == "POST" && path == pre + "/filter") {
+    stats_.filters.fetch_add(1, std::memory_order_relaxed);
+    std::string out;
+    {
+      std::lock_guard<std::mutex> g(l_->mu());
+      out = filter_body(*l_, req.body);
+    }
+    stats_.filter_lat.observe(mono() - t0);
+    respond(lp, c, http::response(200, "application/json", out, ka), ka);
+    return;
+  }
+  if (req.method == "POST" && path == pre + "/bind") {
+    stats_.binds.fetch_add(1, std::memory_order_relaxed);
+    c->busy = true;
+    submit(Job{lp, c->id, 0, std::move(req), t0});
+    return;
+  }
+  if (req.method == "GET" && (path == pre + "/inspect" || path == pre + "/inspect/" ||
+                              path.substr(0, pre.size() + 9) == pre + "/inspect/")) {
+    std::string node;
+    if (path.size() > pre.size() + 9) node = std::string(path.substr(pre.size() + 9));
+    stats_.inspects.fetch_add(1, std::memory_order_relaxed);
+    std::string out;
+    bool found;
+    {
+      std::lock_guard<std::mutex> g(l_->mu());
+      out = l_->inspect_json(node, &found);
+    }
+    respond(lp, c, http::response(200, "application/json", out, ka), ka);
+    return;
+  }
+  if (req.method == "GET" && path == "/version") {
+    respond(lp, c, http::response(200, "text/plain; charset=utf-8", kVersion, ka), ka);
+    return;
+  }
+  if (fallback_) {
+    c->busy = true;
+    submit(Job{lp, c->id, 1, std::move(req), t0});
+    return;
+  }
+  respond(lp, c, http::response(404, "text/plain", "404 page not found\n", ka), ka);
+}
+
+void NativeServer::submit(Job j) {
+  {
+    std::lock_guard<std::mutex> g(jmu_);
+    jobs_.push_back(std::move(j));
+  }
+  jcv_.notify_one();
+}
+
+void NativeServer::pool_main() {
+  while (true) {
+    Job j;
+    {
+      std::unique_lock<std::mutex> g(jmu_);
+      jcv_.wait(g, [this] { return stop_.load() || !jobs_.empty(); });
+      if (stop_.load() && jobs_.empty()) return;
+      j = std::move(jobs_.front());
+      jobs_.pop_front();
+    }
+    std::string resp;
+    const bool ka = j.req.keep_alive;
+    if (j.kind == 0) {
+      bool fallback = false;
+      resp = do_bind(j.req, &fallback);
+      if (fallback) {
+        resp = do_proxy(j.req);
+      }
+      stats_.bind_lat.observe(mono() - j.t0);
+    } else {
+      resp = do_proxy(j.req);
+    }
+    complete(j.loop, j.conn_id, std::move(resp), ka);
+  }
+}
+
+std::string NativeServer::bind_error_response(const std::string& msg) const {
+  return http::response(500, "application/json", error_body(msg), true);
+}
+
+std::string NativeServer::do_proxy(const http::Message& req) {
+  stats_.proxied.fetch_add(1, std::memory_order_relaxed);
+  if (!fallback_) return http::response(404, "text/plain", "404 page not found\n", true);
+  const std::string* ct = req.header("content-type");
+  int status = 0;
+  std::string body, err, rct;
+  if (!fallback_->request(req.method, req.target, req.body, ct ? ct->c_str() : "application/json", &status, &body,
+                          &err, &rct)) {
+    return http::response(502, "text/plain", "fallback: " + err, true);
+  }
+  return http::response(status, rct, body, true);
+}
+
+// Native bind: reserve on the ledger, then one POST pods/{name}/binding whose
+// metadata.annotations carry the allocation record (pkg/utils/pod.go:192-206).
+std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
+  *fallback = false;
+  if (!cfg_.native_bind || !api_) {
+    *fallback = true;
+    return {};
+  }
+  json::Doc d;
+  std::string perr;
+  if (!d.parse(req.body, &perr)) return bind_error_response(perr);
+  if (d.at(0).type != json::T::Object) {
+    return bind_error_response("json: cannot unmarshal value into Go value of type api.ExtenderBindingArgs");
+  }
+  std::string name, ns, uid, node;
+  if (!arg_str(d, "PodName", &name) || !arg_str(d, "PodNamespace", &ns) || !arg_str(d, "PodUID", &uid) ||
+      !arg_str(d, "Node", &node)) {
+    *fallback = true;  // let the Python decoder produce Go's exact type error
+    return {};
+  }
+  Ledger::PendingPod pp;
+  int64_t dev, dev_total = -1;
+  const Profile& prof = l_->profile();
+  {
+    std::lock_guard<std::mutex> g(l_->mu());
+    if (!l_->pending(uid, &pp) || pp.name != name || pp.ns != ns) {
+      *fallback = true;  // never filtered here (e.g. restart between filter and bind): slow path
+      return {};
+    }
+    dev = l_->assume(uid, ns, name, node, pp.req, &dev_total);
+  }
+  if (dev < 0) {
+    std::string msg;
+    if (dev == -2) {
+      msg = "node \"" + node + "\" not found";
+    } else if (dev == -3) {
+      msg = "The node " + node + " is not for GPU share, need skip";
+    } else if (dev == -4) {
+      msg = "bind of pod " + name + " in ns " + ns + " is already in progress";
+    } else {
+      msg = "The node " + node + " can't place the pod " + name + " in ns " + ns;  // nodeinfo.go:170
+    }
+    stats_.bind_fail.fetch_add(1, std::memory_order_relaxed);
+    record_failure(BindFailure{ns, name, uid, node, msg});
+    return bind_error_response(msg);
+  }
+  // Binding object with the annotations kube-apiserver copies onto the pod
+  std::string b;
+  b.reserve(512);
+  b.append("{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":");
+  json::append_quoted(&b, name);
+  b.append(",\"namespace\":");
+  json::append_quoted(&b, ns);
+  b.append(",\"uid\":");
+  json::append_quoted(&b, uid);
+  b.append(",\"annotations\":{");
+  auto kv = [&](const std::string& k, const std::string& v, bool last) {
+    json::append_quoted(&b, k);
+    b.push_back(':');
+    json::append_quoted(&b, v);
+    if (!last) b.push_back(',');
+  };
+  kv(prof.a_idx, std::to_string(dev), false);
+  kv(prof.a_dev, std::to_string(dev_total), false);
+  kv(prof.a_pod, std::to_string(pp.req), false);
+  kv(prof.a_assigned, "false", false);
+  kv(prof.a_assume, std::to_string(unix_ns()), true);
+  b.append("}},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":");
+  json::append_quoted(&b, node);
+  b.append("}}");
+  const std::string path = "/api/v1/namespaces/" + url_escape_path(ns) + "/pods/" + url_escape_path(name) + "/binding";
+  std::string msg;
+  bool ok = false;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    int status = 0;
+    std::string body, err;
+    double t0 = mono();
+    stats_.api_calls.fetch_add(1, std::memory_order_relaxed);
+    bool sent = api_->request("POST", path, b, "application/json", &status, &body, &err);
+    stats_.api_lat.observe(mono() - t0);
+    if (!sent) {
+      msg = err;
+      break;
+    }
+    if (status == 200 || status == 201) {
+      ok = true;
+      break;
+    }
+    msg = status_message(body, status);
+    if (status == 409 && msg.find("Precondition failed") != std::string::npos) {
+      // UID mismatch: release and let the slow path produce the reference's
+      // exact error (gpushare-bind.go:44-65 does a live GET).
+      std::lock_guard<std::mutex> g(l_->mu());
+      l_->finish_bind(uid, false, 0.0);
+      *fallback = true;
+      return {};
+    }
+    if (status == 409 && msg.find("already assigned") == std::string::npos && attempt < 2) {
+      stats_.conflicts_retried.fetch_add(1, std::memory_order_relaxed);
+      continue;
+    }
+    if (status >= 500 && attempt < 2) continue;
+    break;
+  }
+  {
+    std::lock_guard<std::mutex> g(l_->mu());
+    l_->finish_bind(uid, ok, cfg_.reservation_ttl);
+    if (ok) l_->forget_pending(uid);
+  }
+  if (!ok) {
+    stats_.bind_fail.fetch_add(1, std::memory_order_relaxed);
+    record_failure(BindFailure{ns, name, uid, node, msg});
+    return bind_error_response(msg);
+  }
+  stats_.bind_ok.fetch_add(1, std::memory_order_relaxed);
+  return http::response(200, "application/json", "{\"Error\":\"\"}", true);
+}
+
+}  // namespace gsx

@@ -1,0 +1,132 @@
+// Native HTTP front end of the scheduler extender.
+//
+// The reference extender is a Go net/http server (cmd/main.go:119-128,
+// pkg/routes/routes.go).  Here the hot verbs are served entirely in C++:
+//
+//   POST /gpushare-scheduler/filter   native ledger check (no GIL)
+//   POST /gpushare-scheduler/bind     native reserve + one apiserver
+//                                     POST pods/{name}/binding carrying the
+//                                     allocation annotations (bind pool)
+//   GET  /gpushare-scheduler/inspect  native
+//   GET  /version                     native
+//
+// Anything else (/metrics, /debug/pprof/*, /healthz, and binds the native
+// path cannot decide: pod never filtered here, "update" bind mode, UID
+// precondition failures) is proxied to the Python aiohttp app on a loopback
+// port, so the observable API is one server.
+//
+// Design: N event-loop threads, each with its own SO_REUSEPORT listening
+// socket and epoll set (the kernel spreads connections); blocking work (the
+// apiserver round trip, proxying) runs on a small thread pool and completes
+// back to the owning loop through an eventfd.  One request per connection is
+// in flight at a time, so responses stay ordered.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "apiclient.h"
+#include "http.h"
+#include "ledger.h"
+
+namespace gsx {
+
+struct ServerConfig {
+  std::string host = "0.0.0.0";
+  int port = 0;
+  int threads = 2;
+  int pool_threads = 16;
+  int fallback_port = 0;      // Python app on 127.0.0.1 (0: none)
+  bool native_bind = true;
+  double reservation_ttl = 60.0;
+  ApiConfig api;
+  size_t max_body = 64u << 20;
+};
+
+struct BindFailure {
+  std::string ns, name, uid, node, message;
+};
+
+struct LatencyHist {
+  static constexpr int kBuckets = 15;
+  static const double kBounds[kBuckets];
+  std::atomic<uint64_t> counts[kBuckets + 1];
+  std::atomic<uint64_t> n{0};
+  std::atomic<uint64_t> sum_ns{0};
+  LatencyHist() {
+    for (auto& c : counts) c.store(0);
+  }
+  void observe(double seconds);
+};
+
+struct ServerStats {
+  std::atomic<uint64_t> requests{0}, filters{0}, binds{0}, bind_ok{0}, bind_fail{0}, proxied{0}, bad_requests{0},
+      inspects{0}, connections{0}, api_calls{0}, conflicts_retried{0};
+  LatencyHist filter_lat, bind_lat, api_lat;
+};
+
+class NativeServer {
+ public:
+  NativeServer(Ledger* ledger, ServerConfig cfg);
+  ~NativeServer();
+  // Binds and starts the loops; returns the bound port (> 0) or -1 with *err.
+  int start(std::string* err);
+  void stop();
+  int port() const { return port_; }
+  const ServerStats& stats() const { return stats_; }
+  std::vector<BindFailure> drain_failures();
+
+ private:
+  struct Loop;
+  struct Conn;
+  struct Job {
+    Loop* loop;
+    uint64_t conn_id;
+    int kind;  // 0 bind, 1 proxy
+    http::Message req;
+    double t0;
+  };
+
+  void run_loop(Loop* lp);
+  void on_readable(Loop* lp, Conn* c);
+  void process(Loop* lp, Conn* c);
+  void dispatch(Loop* lp, Conn* c, http::Message& req);
+  void respond(Loop* lp, Conn* c, std::string resp, bool keep_alive);
+  void flush(Loop* lp, Conn* c);
+  void close_conn(Loop* lp, Conn* c);
+  void complete(Loop* lp, uint64_t conn_id, std::string resp, bool keep_alive);
+  void drain_completions(Loop* lp);
+  void pool_main();
+  void submit(Job j);
+  std::string do_bind(const http::Message& req, bool* fallback);
+  std::string do_proxy(const http::Message& req);
+  std::string bind_error_response(const std::string& msg) const;
+  void record_failure(BindFailure f);
+
+  Ledger* l_;
+  ServerConfig cfg_;
+  int port_ = -1;
+  std::atomic<bool> stop_{false};
+  std::vector<std::unique_ptr<Loop>> loops_;
+  std::vector<std::thread> loop_threads_;
+  std::vector<std::thread> pool_threads_;
+  std::mutex jmu_;
+  std::condition_variable jcv_;
+  std::deque<Job> jobs_;
+  std::unique_ptr<ApiClient> api_;
+  std::unique_ptr<ApiClient> fallback_;
+  std::mutex fmu_;
+  std::vector<BindFailure> failures_;
+  ServerStats stats_;
+};
+
+}  // namespace gsx

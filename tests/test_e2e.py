@@ -18,6 +18,17 @@ from gpushare_scheduler_extender_amd.models.profile import ALIYUN, SHARED_GPU
 from gpushare_scheduler_extender_amd.sim.scheduler import SchedulerSim
 
 
+NATIVE = {"on": True}
+
+
+@pytest.fixture(autouse=True, params=["native-http", "aiohttp"])
+def _frontend(request):
+    """Every end-to-end test runs against the C++ front end and against the pure-aiohttp one."""
+    NATIVE["on"] = request.param == "native-http"
+    yield
+    NATIVE["on"] = True
+
+
 class Cluster:
     def __init__(self, profile=SHARED_GPU, bind_mode="binding", **ext_kw):
         self.profile = profile
@@ -28,7 +39,8 @@ class Cluster:
         self.api = await FakeApiServerRunner().start()
         self.client = KubeClient(self.api.url)
         self.ext = await ExtenderRunner(ExtenderServer(KubeClient(self.api.url), self.profile,
-                                                       bind_mode=self.bind_mode, **self.ext_kw)).start()
+                                                       bind_mode=self.bind_mode, **self.ext_kw),
+                                        native=NATIVE["on"]).start()
         self.sim = None
         self.http = aiohttp.ClientSession()
         return self
