@@ -93,6 +93,8 @@ def parse():
     ap.add_argument("--devices", default="auto", help="auto|hip|amdsmi|fake (fake: no GPU, CPU plumbing only)")
     ap.add_argument("--stamp-stride", type=int, default=1 << 20)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--agent", default="rank", choices=["node", "rank"],
+                    help="rank: one device-plugin agent per GPU rank (default); node: one node-agent process driving a runtime shim per GPU rank")
     ap.add_argument("--inproc", action="store_true",
                     help="run apiserver + extender in this process (no child processes; used under rocprofv3)")
     return ap.parse_args()
@@ -124,12 +126,15 @@ def main():
         inproc = [ext_r, api_r]
         api_url, ext_url = api_r.url, ext_r.url
     elif rank == 0:
-        from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver, start_extender
+        from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver, start_extender, start_node_agent
 
         api = start_apiserver()
         children.append(api)
         ext = start_extender(api.url, profile=a.profile, bind_mode=a.bind_mode)
         children.append(ext)
+        if a.agent == "node":
+            # the node's device plugin / kubelet stand-in: one process for all GPUs of the node, like a DaemonSet
+            children.append(start_node_agent(api.url, NODE, profile=a.profile))
         api_url, ext_url = api.url, ext.url
 
     import torch
@@ -137,7 +142,7 @@ def main():
 
     from gpushare_scheduler_extender_amd.deviceplugin.agent import NodeAgent
     from gpushare_scheduler_extender_amd.deviceplugin.devices import UNITS, discover
-    from gpushare_scheduler_extender_amd.deviceplugin.runtime import HbmArenaRuntime, LedgerRuntime
+    from gpushare_scheduler_extender_amd.deviceplugin.runtime import HbmArenaRuntime, LedgerRuntime, RuntimeShim
     from gpushare_scheduler_extender_amd.k8s.client import KubeClient
     from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
     from gpushare_scheduler_extender_amd.models.profile import get_profile
@@ -188,19 +193,30 @@ def main():
     dev.index = local_rank
     unit = "GiB"
     pod_bytes = a.pod_gib * UNITS[unit]
-    all_devs = gather(dev.to_dict())
-
     arena = a.pods_per_gpu * pod_bytes
     runtime = (HbmArenaRuntime({local_rank: arena}, stamp_stride=a.stamp_stride) if use_gpu
                else LedgerRuntime({local_rank: arena}))
+    # this GPU's runtime endpoint (CRI-runtime role): the node agent starts pods on it over HTTP
+    shim = RuntimeShim(runtime)
+    shim_url = lt.run(shim.start("127.0.0.1", 0))
+    all_devs = gather((dev.to_dict(), shim_url))
     from gpushare_scheduler_extender_amd.deviceplugin.devices import Device
+    from gpushare_scheduler_extender_amd.models.profile import (NODE_DEVICE_INFO_ANNOTATION,
+                                                                NODE_RUNTIME_ENDPOINTS_ANNOTATION)
 
     agent_client = KubeClient(api_url)
 
     async def setup_node():
         c = KubeClient(api_url)
-        totals = [Device(**d).units(unit) for d in all_devs]
-        node = make_node(NODE, sum(totals), len(totals), profile=profile, device_totals=totals)
+        devs_ = [Device(**d) for d, _ in all_devs]
+        totals = [d.units(unit) for d in devs_]
+        inv = [{"index": d.index, "bdf": d.bdf, "uuid": d.uuid, "units": d.units(unit), "total_bytes": d.total_bytes,
+                "cu": d.cu_count, "render": d.render_minor, "card": d.card_minor, "partition": d.partition}
+               for d in devs_]
+        node = make_node(NODE, sum(totals), len(totals), profile=profile, device_totals=totals,
+                         annotations={NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv),
+                                      NODE_RUNTIME_ENDPOINTS_ANNOTATION: json.dumps(
+                                          {str(d.index): u for d, (_, u) in zip(devs_, all_devs)})})
         node["metadata"].setdefault("labels", {})["gpushare"] = "true"
         await c.create("nodes", node)
         await c.close()
@@ -208,9 +224,12 @@ def main():
 
     totals = lt.run(setup_node()) if rank == 0 else None
     totals = bcast(totals)
-    agent = NodeAgent(agent_client, NODE, [dev], profile, runtime, unit=unit, verify_each=True,
-                      mount_mode="isolated")
-    lt.run(agent.start())
+    agent = None
+    if a.agent == "rank":
+        # one agent per GPU rank (each watches the node's pods; heavier on the apiserver)
+        agent = NodeAgent(agent_client, NODE, [dev], profile, runtime, unit=unit, verify_each=True,
+                          mount_mode="isolated")
+        lt.run(agent.start())
 
     sim = client = None
     if rank == 0:
@@ -294,9 +313,13 @@ def main():
         elapsed = float(t.item())
 
     bad = runtime.verify() if use_gpu else 0
-    agent_stats = gather({"admitted": agent.admitted, "failed": agent.failed, "bad_stamps": agent.bad_stamps + bad,
-                          "admit_p50_ms": (pct(agent.latency, 50) or 0) * 1e3,
-                          "hbm_total": dev.total_bytes, "arena": arena})
+    if agent is not None:
+        mine = {"admitted": agent.admitted, "failed": agent.failed, "bad_stamps": agent.bad_stamps + bad,
+                "admit_p50_ms": round((pct(agent.latency, 50) or 0) * 1e3, 3)}
+    else:
+        mine = {"admitted": shim.admitted, "failed": shim.failed, "bad_stamps": shim.bad + bad}
+    mine.update({"gpu": local_rank, "hbm_total": dev.total_bytes, "arena": arena})
+    agent_stats = gather(mine)
 
     if rank == 0:
         pods_total = n_pods * a.steps
@@ -323,7 +346,8 @@ def main():
                     else "synthetic pods; fake devices (no GPU)",
             "config": {"model": f"gpushare extender+device plugin: {a.pods_per_gpu} pods/GPU x {a.pod_gib} GiB "
                                 f"({profile.resource}), binpack", "global_batch": n_pods, "seq_len": 0,
-                       "parallelism": f"{world} GPU(s) advertised on 1 node, 1 node-agent rank per GPU",
+                       "parallelism": f"{world} GPU(s) advertised on 1 node; 1 rank (HBM runtime) per GPU; "
+                                      f"agent={a.agent}",
                        "bind_mode": a.bind_mode, "device_backend": backend},
             "p50_bind_latency_ms": round(1e3 * pct(lat, 50), 3),
             "p99_bind_latency_ms": round(1e3 * pct(lat, 99), 3),
@@ -348,8 +372,10 @@ def main():
 
     # ---- teardown
     try:
-        lt.run(agent.stop(), 30)
+        if agent is not None:
+            lt.run(agent.stop(), 30)
         lt.run(agent_client.close(), 30)
+        lt.run(shim.stop(), 30)
         if rank == 0:
             lt.run(sim.stop(), 30)
             lt.run(sim.client.close(), 30)

@@ -25,7 +25,7 @@ from ..models import pod as podutil
 from ..models.profile import NamingProfile
 from .allocator import CU_COUNT_ANNOTATION, CUPartitioner, assigned_patch, build_response, pick_pod
 from .devices import UNITS, Device
-from .runtime import AdmissionError
+from .runtime import AdmissionError, admit_local
 
 log = logging.getLogger("gsx.agent")
 
@@ -82,9 +82,24 @@ class NodeAgent:
     def _stop(self, uid: str):
         if uid in self.running:
             self.running.pop(uid, None)
-            self.runtime.stop(uid)
+            self._release(uid)
             for p in self.cus.values():
                 p.release(uid)
+
+    def _release(self, uid: str):
+        rel = getattr(self.runtime, "release", None)
+        if rel is None:
+            self.runtime.stop(uid)
+            return
+        t = asyncio.get_running_loop().create_task(rel(uid))
+        self._bg.add(t)
+        t.add_done_callback(self._bg.discard)
+
+    async def _admit_runtime(self, uid: str, dev: int, nbytes: int, cus) -> int:
+        adm = getattr(self.runtime, "admit", None)
+        if adm is not None:
+            return await adm(uid, dev, nbytes, cus, self.verify_each)
+        return admit_local(self.runtime, uid, dev, nbytes, cus, self.verify_each)
 
     async def _worker(self):
         while True:
@@ -140,16 +155,14 @@ class NodeAgent:
                 raise
             self.allocations[uid] = alloc.envs
             try:
-                self.runtime.start(uid, dev_idx, units * self.unit_bytes, cus)
-                if self.verify_each:
-                    bad = self.runtime.verify()
-                    if bad:
-                        self.bad_stamps += bad
-                        raise AdmissionError(f"{bad} bad HBM stamps after admitting {key}")
+                bad = await self._admit_runtime(uid, dev_idx, units * self.unit_bytes, cus)
+                if bad:
+                    self.bad_stamps += bad
+                    raise AdmissionError(f"{bad} bad HBM stamps after admitting {key}")
             except AdmissionError as e:
                 self.failed += 1
                 log.error("admission of %s on GPU %d failed: %s", key, dev_idx, e)
-                self.runtime.stop(uid)
+                self._release(uid) if getattr(self.runtime, "release", None) else self.runtime.stop(uid)
                 if self.report_status:
                     await self.client.patch("pods", podutil.meta(pod)["name"],
                                             {"status": {"phase": "Failed", "reason": "UnexpectedAdmissionError",
@@ -179,3 +192,82 @@ class NodeAgent:
         for t in list(self._bg):
             t.cancel()
         await self.pods.stop()
+
+
+async def node_devices_and_endpoints(client: KubeClient, node: str, timeout: float = 60.0):
+    """Wait for the node's device inventory + runtime endpoints annotations; return (devices, endpoints)."""
+    import json  # noqa: PLC0415
+
+    from ..models.profile import NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION  # noqa: PLC0415
+
+    deadline = time.monotonic() + timeout
+    while True:
+        try:
+            n = await client.get("nodes", node)
+            ann = podutil.annotations(n)
+            inv = json.loads(ann.get(NODE_DEVICE_INFO_ANNOTATION, "[]"))
+            eps = {int(k): v for k, v in json.loads(ann.get(NODE_RUNTIME_ENDPOINTS_ANNOTATION, "{}")).items()}
+            if inv and all(d["index"] in eps for d in inv):
+                devs = [Device(index=d["index"], bdf=d.get("bdf", ""), uuid=d.get("uuid", ""),
+                               total_bytes=int(d.get("total_bytes", d.get("units", 0) * UNITS["GiB"])),
+                               cu_count=int(d.get("cu", 256)), render_minor=int(d.get("render", -1)),
+                               card_minor=int(d.get("card", -1)), partition=d.get("partition", "SPX"))
+                        for d in inv]
+                return devs, eps
+        except ApiError:
+            pass
+        if time.monotonic() > deadline:
+            raise TimeoutError(f"node {node} never published devices + runtime endpoints")
+        await asyncio.sleep(0.05)
+
+
+def main(argv=None) -> int:
+    """``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``: one node agent driving remote GPU runtimes."""
+    import argparse  # noqa: PLC0415
+    import os  # noqa: PLC0415
+    import signal  # noqa: PLC0415
+
+    from ..k8s.client import KubeConfig  # noqa: PLC0415
+    from ..models.profile import get_profile  # noqa: PLC0415
+    from .runtime import RemoteRuntime  # noqa: PLC0415
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--node", required=True)
+    ap.add_argument("--apiserver", default=os.environ.get("GSX_APISERVER"))
+    ap.add_argument("--kubeconfig", default=os.environ.get("KUBECONFIG"))
+    ap.add_argument("--profile", default="shared-gpu")
+    ap.add_argument("--unit", default="GiB")
+    ap.add_argument("--workers", type=int, default=32)
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--port-file", default="")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.WARNING)
+
+    async def run():
+        client = KubeClient(KubeConfig.auto(a.kubeconfig, a.apiserver))
+        if a.port_file:  # no listening port; signal readiness for the process harness
+            with open(a.port_file + ".tmp", "w") as f:
+                f.write("1")
+            os.replace(a.port_file + ".tmp", a.port_file)
+        devs, eps = await node_devices_and_endpoints(client, a.node, timeout=600)
+        rt = RemoteRuntime(eps)
+        agent = NodeAgent(client, a.node, devs, get_profile(a.profile), rt, unit=a.unit,
+                          verify_each=not a.no_verify, workers=a.workers)
+        await agent.start()
+        stop = asyncio.Event()
+        loop = asyncio.get_running_loop()
+        for s in (signal.SIGINT, signal.SIGTERM):
+            loop.add_signal_handler(s, stop.set)
+        await stop.wait()
+        await agent.stop()
+        await rt.close()
+        await client.close()
+
+    asyncio.run(run())
+    return 0
+
+
+if __name__ == "__main__":
+    import sys  # noqa: PLC0415
+
+    sys.exit(main())

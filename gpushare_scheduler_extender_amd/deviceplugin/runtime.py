@@ -137,3 +137,102 @@ class HbmArenaRuntime(LedgerRuntime):
             s.destroy()
         for a in self.arena.values():
             a.free()
+
+
+# ---------------------------------------------------------------- admission API used by the node agent
+
+def admit_local(rt: LedgerRuntime, uid: str, dev: int, nbytes: int, cus=None, verify: bool = True) -> int:
+    """Start a pod on a local runtime and (optionally) verify every resident slice; returns bad stamps."""
+    rt.start(uid, dev, nbytes, cus)
+    return rt.verify() if verify else 0
+
+
+class RuntimeShim:
+    """Per-GPU runtime endpoint (the CRI-runtime role): the node agent starts / stops pods through it.
+
+    ``POST /v1/pods/{uid}`` ``{"dev", "bytes", "cus", "verify"}`` -> ``{"bad"}`` (409 on admission failure),
+    ``DELETE /v1/pods/{uid}``, ``GET /v1/stats``.  In ``bench.py`` every rank serves one for its GPU, so the
+    HIP work for a pod runs in the process that owns that GPU.
+    """
+
+    def __init__(self, runtime: LedgerRuntime):
+        from ..k8s.fasthttp import Server  # noqa: PLC0415
+
+        self.runtime = runtime
+        self.server = Server()
+        self.server.route("POST", "/v1/pods/{uid}", self.h_start)
+        self.server.route("DELETE", "/v1/pods/{uid}", self.h_stop)
+        self.server.route("GET", "/v1/stats", self.h_stats)
+        self.admitted = 0
+        self.failed = 0
+        self.bad = 0
+        self.port = 0
+
+    def h_start(self, request):
+        from ..k8s.fasthttp import Response  # noqa: PLC0415
+
+        b = request.json()
+        uid = request.match_info["uid"]
+        try:
+            bad = admit_local(self.runtime, uid, int(b["dev"]), int(b["bytes"]), b.get("cus"),
+                              bool(b.get("verify", True)))
+        except AdmissionError as e:
+            self.failed += 1
+            return Response.json({"error": str(e)}, 409)
+        self.admitted += 1
+        self.bad += bad
+        return Response.json({"bad": bad})
+
+    def h_stop(self, request):
+        from ..k8s.fasthttp import Response  # noqa: PLC0415
+
+        ok = self.runtime.stop(request.match_info["uid"])
+        return Response(b"", 200 if ok else 404)
+
+    def h_stats(self, request):
+        from ..k8s.fasthttp import Response  # noqa: PLC0415
+
+        return Response.json({"admitted": self.admitted, "failed": self.failed, "bad": self.bad})
+
+    async def start(self, host: str = "127.0.0.1", port: int = 0) -> str:
+        self.port = await self.server.start(host, port)
+        return f"http://{host}:{self.port}"
+
+    async def stop(self):
+        await self.server.stop()
+
+
+class RemoteRuntime:
+    """Node-agent side of :class:`RuntimeShim`: device index -> shim URL."""
+
+    def __init__(self, endpoints: dict[int, str]):
+        from ..k8s.fasthttp import Client  # noqa: PLC0415
+
+        self.endpoints = dict(endpoints)
+        self.clients = {d: Client(u, timeout=60.0) for d, u in self.endpoints.items()}
+        self.where: dict[str, int] = {}
+
+    async def admit(self, uid: str, dev: int, nbytes: int, cus=None, verify: bool = True) -> int:
+        import json  # noqa: PLC0415
+
+        c = self.clients.get(dev)
+        if c is None:
+            raise AdmissionError(f"no runtime endpoint for GPU {dev}")
+        r = await c.request("POST", f"/v1/pods/{uid}", json.dumps({"dev": dev, "bytes": nbytes, "cus": cus,
+                                                                    "verify": verify}).encode())
+        body = r.json() or {}
+        if r.status != 200:
+            raise AdmissionError(body.get("error", f"runtime HTTP {r.status}"))
+        self.where[uid] = dev
+        return int(body.get("bad", 0))
+
+    async def release(self, uid: str) -> bool:
+        dev = self.where.pop(uid, None)
+        if dev is None or dev not in self.clients:
+            return False
+        r = await self.clients[dev].request("DELETE", f"/v1/pods/{uid}")
+        return r.status == 200
+
+    async def close(self):
+        for c in self.clients.values():
+            await c.close()

@@ -3,7 +3,8 @@
 Replaces the reference's client-go usage (``cmd/main.go:67-86``,
 ``pkg/gpushare/controller.go``, ``pkg/cache/nodeinfo.go:150-189``).  There is
 no ``kubernetes`` Python package in this image, and the extender needs only a
-handful of core/v1 verbs, so this is a small hand-written client on aiohttp:
+handful of core/v1 verbs, so this is a small hand-written client on
+:mod:`.fasthttp` (raw asyncio streams, keep-alive pool):
 
 * config from ``KUBECONFIG`` (token / client-cert / CA / insecure), the
   in-cluster service account, or an explicit base URL (fake apiserver);
@@ -29,7 +30,8 @@ from dataclasses import dataclass, field
 from typing import AsyncIterator
 from urllib.parse import quote, urlencode
 
-import aiohttp
+from .fasthttp import Client
+
 import yaml
 
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
@@ -195,26 +197,23 @@ class KubeClient:
         self.config = KubeConfig.from_url(config) if isinstance(config, str) else config
         self.limiter = RateLimiter(qps, burst)
         self.user_agent = user_agent
-        self._connector_limit = connector_limit
-        self._session: aiohttp.ClientSession | None = None
+        self._limit = connector_limit
+        self._http: Client | None = None
         self.calls = 0
 
-    async def _sess(self) -> aiohttp.ClientSession:
-        if self._session is None or self._session.closed:
-            headers = {"User-Agent": self.user_agent, "Accept": "application/json", **self.config.extra_headers}
+    def _client(self) -> Client:
+        if self._http is None or self._http.closed:
+            headers = {"User-Agent": self.user_agent, **self.config.extra_headers}
             if self.config.token:
                 headers["Authorization"] = f"Bearer {self.config.token}"
-            conn = aiohttp.TCPConnector(limit=self._connector_limit, ssl=self.config.ssl_context(),
-                                        ttl_dns_cache=300)
-            self._session = aiohttp.ClientSession(headers=headers, connector=conn,
-                                                  timeout=aiohttp.ClientTimeout(total=None, sock_connect=10),
-                                                  json_serialize=lambda o: json.dumps(o, separators=(",", ":")))
-        return self._session
+            self._http = Client(self.config.server, ssl_context=self.config.ssl_context(), headers=headers,
+                                limit=self._limit)
+        return self._http
 
     async def close(self):
-        if self._session is not None:
-            await self._session.close()
-            self._session = None
+        if self._http is not None:
+            await self._http.close()
+            self._http = None
 
     async def __aenter__(self):
         return self
@@ -222,31 +221,32 @@ class KubeClient:
     async def __aexit__(self, *exc):
         await self.close()
 
+    @staticmethod
+    def _raise(status: int, raw: bytes):
+        try:
+            st = json.loads(raw)
+            if not isinstance(st, dict):
+                st = {"message": str(st)}
+        except ValueError:
+            st = {"message": raw.decode(errors="replace")}
+        raise ApiError(status, st.get("reason", ""), st.get("message", ""), st)
+
     async def request(self, method: str, path: str, *, params: dict | None = None, body=None,
                       content_type: str = "application/json", timeout: float | None = 30.0):
-        await self.limiter.acquire()
-        s = await self._sess()
-        url = self.config.server + path
+        if self.limiter.qps > 0:
+            await self.limiter.acquire()
         if params:
-            url += "?" + urlencode(params)
+            path += "?" + urlencode(params)
         data = None
-        headers = {}
         if body is not None:
-            data = body if isinstance(body, (bytes, str)) else json.dumps(body, separators=(",", ":"))
-            headers["Content-Type"] = content_type
+            data = body if isinstance(body, bytes) else (body.encode() if isinstance(body, str) else
+                                                          json.dumps(body, separators=(",", ":")).encode())
         self.calls += 1
-        async with s.request(method, url, data=data, headers=headers,
-                             timeout=aiohttp.ClientTimeout(total=timeout)) as r:
-            raw = await r.read()
-            if r.status >= 400:
-                try:
-                    st = json.loads(raw)
-                except ValueError:
-                    st = {"message": raw.decode(errors="replace")}
-                raise ApiError(r.status, st.get("reason", ""), st.get("message", ""), st)
-            if not raw:
-                return None
-            return json.loads(raw)
+        r = await self._client().request(method, path, data, content_type if data is not None else None,
+                                         timeout=timeout)
+        if r.status >= 400:
+            self._raise(r.status, r.body)
+        return json.loads(r.body) if r.body else None
 
     # ------------------------------------------------------------ verbs
     async def get(self, kind: str, name: str, ns: str | None = None) -> dict:
@@ -322,21 +322,16 @@ class KubeClient:
             params["labelSelector"] = label_selector
         if timeout_seconds:
             params["timeoutSeconds"] = str(timeout_seconds)
-        await self.limiter.acquire()
-        s = await self._sess()
-        url = self.config.server + _ns_path(kind, ns) + "?" + urlencode(params)
+        if self.limiter.qps > 0:
+            await self.limiter.acquire()
         self.calls += 1
-        async with s.get(url, timeout=aiohttp.ClientTimeout(total=None, sock_read=None)) as r:
-            if r.status >= 400:
-                raw = await r.read()
-                try:
-                    st = json.loads(raw)
-                except ValueError:
-                    st = {}
-                raise ApiError(r.status, st.get("reason", ""), st.get("message", ""), st)
+        status, hdrs, chunks, close = await self._client().stream("GET", _ns_path(kind, ns) + "?" + urlencode(params))
+        try:
+            if status >= 400:
+                self._raise(status, b"".join([c async for c in chunks]))
             buf = b""
-            async for chunk in r.content.iter_any():
-                buf += chunk
+            async for chunk in chunks:
+                buf = buf + chunk if buf else chunk
                 while True:
                     i = buf.find(b"\n")
                     if i < 0:
@@ -349,3 +344,5 @@ class KubeClient:
                         o = ev.get("object") or {}
                         raise ApiError(int(o.get("code", 500)), o.get("reason", ""), o.get("message", ""), o)
                     yield (ev, line) if raw else ev
+        finally:
+            close()

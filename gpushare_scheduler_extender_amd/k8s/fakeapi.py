@@ -30,7 +30,6 @@ from __future__ import annotations
 import argparse
 import asyncio
 import collections
-import copy
 import json
 import logging
 import random
@@ -38,7 +37,7 @@ import time
 import uuid
 from datetime import datetime, timezone
 
-from aiohttp import web
+from .fasthttp import HTTPError, Request, Response, Server, Stream
 
 log = logging.getLogger("gsx.fakeapi")
 
@@ -61,7 +60,7 @@ def status_body(code: int, reason: str, message: str, details: dict | None = Non
 def merge_patch(target, patch):
     """RFC 7386 JSON merge patch."""
     if not isinstance(patch, dict):
-        return copy.deepcopy(patch)
+        return patch  # values come fresh from the request body; stored objects are never mutated
     if not isinstance(target, dict):
         target = {}
     out = dict(target)
@@ -197,8 +196,9 @@ class FakeApiServer:
                 w.queue.put_nowait(line)
 
     def create(self, kind: str, obj: dict, ns: str | None = None) -> dict:
-        obj = copy.deepcopy(obj)
-        md = obj.setdefault("metadata", {})
+        # copy-on-write: stored objects are immutable once emitted (watch history shares them)
+        obj = dict(obj)
+        md = obj["metadata"] = dict(obj.get("metadata") or {})
         if ns is not None and kind != "nodes":
             md["namespace"] = ns
         if kind != "nodes":
@@ -207,18 +207,15 @@ class FakeApiServer:
             if md.get("generateName"):
                 md["name"] = md["generateName"] + uuid.uuid4().hex[:5]
             else:
-                raise web.HTTPUnprocessableEntity(
-                    text=json.dumps(status_body(422, "Invalid", "metadata.name: Required value")),
-                    content_type="application/json")
+                raise HTTPError(422, status_body(422, "Invalid", "metadata.name: Required value"))
         key = (md.get("namespace", ""), md["name"])
         if key in self.store[kind]:
-            raise web.HTTPConflict(
-                text=json.dumps(status_body(409, "AlreadyExists", f'{kind} "{md["name"]}" already exists')),
-                content_type="application/json")
+            raise HTTPError(409, status_body(409, "AlreadyExists", f'{kind} "{md["name"]}" already exists'))
         md.setdefault("uid", str(uuid.uuid4()))
         md.setdefault("creationTimestamp", _now_iso())
         if kind == "pods":
-            obj.setdefault("status", {}).setdefault("phase", "Pending")
+            obj["status"] = dict(obj.get("status") or {})
+            obj["status"].setdefault("phase", "Pending")
             obj.setdefault("spec", {})
         md["resourceVersion"] = self._bump()
         self.store[kind][key] = obj
@@ -228,15 +225,13 @@ class FakeApiServer:
     def _get(self, kind: str, ns: str, name: str) -> dict:
         o = self.store[kind].get((ns if kind != "nodes" else "", name))
         if o is None:
-            raise web.HTTPNotFound(text=json.dumps(status_body(404, "NotFound", f'{kind} "{name}" not found',
-                                                               {"name": name, "kind": kind})),
-                                   content_type="application/json")
+            raise HTTPError(404, status_body(404, "NotFound", f'{kind} "{name}" not found',
+                                                               {"name": name, "kind": kind}))
         return o
 
     def _conflict(self, kind: str, name: str):
-        return web.HTTPConflict(text=json.dumps(status_body(409, "Conflict", CONFLICT_MSG.format(res=kind, name=name),
-                                                            {"name": name, "kind": kind})),
-                                content_type="application/json")
+        return HTTPError(409, status_body(409, "Conflict", CONFLICT_MSG.format(res=kind, name=name),
+                                                            {"name": name, "kind": kind}))
 
     def replace(self, kind: str, ns: str, name: str, obj: dict, subresource: str = "") -> dict:
         cur = self._get(kind, ns, name)
@@ -246,23 +241,25 @@ class FakeApiServer:
         if kind == "pods" and self.faults.conflict_rate and self.faults.rng.random() < self.faults.conflict_rate:
             self.counts["injected_conflict"] += 1
             raise self._conflict(kind, name)
-        new = copy.deepcopy(obj)
-        md = new.setdefault("metadata", {})
+        new = dict(obj)
+        md = new["metadata"] = dict(obj.get("metadata") or {})
         # immutable / server-owned fields
         for f in ("uid", "creationTimestamp", "namespace", "name", "deletionTimestamp"):
             if f in cur["metadata"]:
                 md[f] = cur["metadata"][f]
         if subresource == "status":
-            merged = copy.deepcopy(cur)
+            merged = dict(cur)
+            merged["metadata"] = dict(cur["metadata"])
             merged["status"] = new.get("status", {})
             new = merged
         elif kind == "pods":
             # spec.nodeName is only settable through the binding subresource
             old_node = (cur.get("spec") or {}).get("nodeName")
+            spec = new["spec"] = dict(new.get("spec") or {})
             if old_node:
-                new.setdefault("spec", {})["nodeName"] = old_node
+                spec["nodeName"] = old_node
             else:
-                (new.get("spec") or {}).pop("nodeName", None)
+                spec.pop("nodeName", None)
             new["status"] = cur.get("status", {})
         new["metadata"]["resourceVersion"] = self._bump()
         self.store[kind][(ns if kind != "nodes" else "", name)] = new
@@ -289,6 +286,7 @@ class FakeApiServer:
             if subresource == "":
                 patch.pop("status", None)
         new = merge_patch(cur, patch)
+        new["metadata"] = dict(new["metadata"])
         for f in ("uid", "creationTimestamp", "namespace", "name", "deletionTimestamp"):
             if f in cur["metadata"]:
                 new["metadata"][f] = cur["metadata"][f]
@@ -301,30 +299,30 @@ class FakeApiServer:
         cur = self._get("pods", ns, name)
         bmd = binding.get("metadata") or {}
         if bmd.get("uid") and bmd["uid"] != cur["metadata"]["uid"]:
-            raise web.HTTPConflict(text=json.dumps(status_body(
+            raise HTTPError(409, status_body(
                 409, "Conflict", f'Precondition failed: UID in precondition: {bmd["uid"]}, '
-                                 f'UID in object meta: {cur["metadata"]["uid"]}')), content_type="application/json")
+                                 f'UID in object meta: {cur["metadata"]["uid"]}'))
         if self.faults.conflict_rate and self.faults.rng.random() < self.faults.conflict_rate:
             self.counts["injected_conflict"] += 1
             raise self._conflict("pods", name)
         if (cur.get("spec") or {}).get("nodeName"):
-            raise web.HTTPConflict(text=json.dumps(status_body(
-                409, "Conflict", f'pod {name} is already assigned to node "{cur["spec"]["nodeName"]}"')),
-                content_type="application/json")
+            raise HTTPError(409, status_body(
+                409, "Conflict", f'pod {name} is already assigned to node "{cur["spec"]["nodeName"]}"'))
         if cur["metadata"].get("deletionTimestamp"):
-            raise web.HTTPConflict(text=json.dumps(status_body(409, "Conflict", f"pod {name} is being deleted")),
-                                   content_type="application/json")
+            raise HTTPError(409, status_body(409, "Conflict", f"pod {name} is being deleted"))
         target = (binding.get("target") or {}).get("name", "")
         if not target:
-            raise web.HTTPUnprocessableEntity(text=json.dumps(status_body(422, "Invalid", "target.name: Required value")),
-                                              content_type="application/json")
-        new = copy.deepcopy(cur)
-        new.setdefault("spec", {})["nodeName"] = target
+            raise HTTPError(422, status_body(422, "Invalid", "target.name: Required value"))
+        new = dict(cur)
+        new["spec"] = dict(cur.get("spec") or {})
+        new["spec"]["nodeName"] = target
+        new["metadata"] = dict(cur["metadata"])
         ann = bmd.get("annotations") or {}
         if ann:
-            new["metadata"].setdefault("annotations", {}).update(ann)
-        conds = new.setdefault("status", {}).setdefault("conditions", [])
-        conds.append({"type": "PodScheduled", "status": "True", "lastTransitionTime": _now_iso()})
+            new["metadata"]["annotations"] = {**(cur["metadata"].get("annotations") or {}), **ann}
+        st = new["status"] = dict(cur.get("status") or {})
+        st["conditions"] = list(st.get("conditions") or []) + [
+            {"type": "PodScheduled", "status": "True", "lastTransitionTime": _now_iso()}]
         new["metadata"]["resourceVersion"] = self._bump()
         self.store["pods"][(ns, name)] = new
         self._emit("pods", "MODIFIED", new)
@@ -335,7 +333,8 @@ class FakeApiServer:
         if kind == "pods" and grace and grace > 0 and (cur.get("spec") or {}).get("nodeName"):
             if cur["metadata"].get("deletionTimestamp"):
                 return cur
-            new = copy.deepcopy(cur)
+            new = dict(cur)
+            new["metadata"] = dict(cur["metadata"])
             new["metadata"]["deletionTimestamp"] = _now_iso()
             new["metadata"]["deletionGracePeriodSeconds"] = int(grace)
             new["metadata"]["resourceVersion"] = self._bump()
@@ -347,7 +346,8 @@ class FakeApiServer:
             t.add_done_callback(self._grace_tasks.discard)
             return new
         del self.store[kind][key]
-        gone = copy.deepcopy(cur)
+        gone = dict(cur)
+        gone["metadata"] = dict(cur["metadata"])
         gone["metadata"]["resourceVersion"] = self._bump()
         self._emit(kind, "DELETED", gone)
         return gone
@@ -368,92 +368,99 @@ class FakeApiServer:
         return out
 
     # ------------------------------------------------------------ HTTP
-    def _make_app(self) -> web.Application:
-        app = web.Application(middlewares=[self._mw], client_max_size=64 * 1024 * 1024)
-        r = app.router
-        r.add_get("/version", self.h_version)
-        r.add_get("/healthz", self.h_healthz)
-        r.add_get("/api", self.h_api)
+    def _make_app(self) -> Server:
+        srv = Server()
+        r = srv.route
+        w = self._wrap
+        r("GET", "/version", w(self.h_version))
+        r("GET", "/healthz", w(self.h_healthz))
+        r("GET", "/api", w(self.h_api))
         for kind in ("pods", "events"):
-            r.add_get(f"/api/v1/{kind}", self._mk_list(kind))
-            r.add_get(f"/api/v1/namespaces/{{ns}}/{kind}", self._mk_list(kind))
-            r.add_post(f"/api/v1/namespaces/{{ns}}/{kind}", self._mk_create(kind))
-            r.add_get(f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", self._mk_get(kind))
-            r.add_put(f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", self._mk_put(kind, ""))
-            r.add_patch(f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", self._mk_patch(kind, ""))
-            r.add_delete(f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", self._mk_delete(kind))
-        r.add_put("/api/v1/namespaces/{ns}/pods/{name}/status", self._mk_put("pods", "status"))
-        r.add_patch("/api/v1/namespaces/{ns}/pods/{name}/status", self._mk_patch("pods", "status"))
-        r.add_post("/api/v1/namespaces/{ns}/pods/{name}/binding", self.h_binding)
-        r.add_post("/api/v1/namespaces/{ns}/bindings", self.h_bindings)
-        r.add_get("/api/v1/nodes", self._mk_list("nodes"))
-        r.add_post("/api/v1/nodes", self._mk_create("nodes"))
-        r.add_get("/api/v1/nodes/{name}", self._mk_get("nodes"))
-        r.add_put("/api/v1/nodes/{name}", self._mk_put("nodes", ""))
-        r.add_patch("/api/v1/nodes/{name}", self._mk_patch("nodes", ""))
-        r.add_put("/api/v1/nodes/{name}/status", self._mk_put("nodes", "status"))
-        r.add_patch("/api/v1/nodes/{name}/status", self._mk_patch("nodes", "status"))
-        r.add_delete("/api/v1/nodes/{name}", self._mk_delete("nodes"))
-        r.add_get("/fake/faults", self.h_faults_get)
-        r.add_post("/fake/faults", self.h_faults)
-        r.add_get("/fake/stats", self.h_stats)
-        return app
+            r("GET", f"/api/v1/{kind}", w(self._mk_list(kind)))
+            r("GET", f"/api/v1/namespaces/{{ns}}/{kind}", w(self._mk_list(kind)))
+            r("POST", f"/api/v1/namespaces/{{ns}}/{kind}", w(self._mk_create(kind)))
+            r("DELETE", f"/api/v1/namespaces/{{ns}}/{kind}", w(self._mk_delete_collection(kind)))
+            r("GET", f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", w(self._mk_get(kind)))
+            r("PUT", f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", w(self._mk_put(kind, "")))
+            r("PATCH", f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", w(self._mk_patch(kind, "")))
+            r("DELETE", f"/api/v1/namespaces/{{ns}}/{kind}/{{name}}", w(self._mk_delete(kind)))
+        r("PUT", "/api/v1/namespaces/{ns}/pods/{name}/status", w(self._mk_put("pods", "status")))
+        r("PATCH", "/api/v1/namespaces/{ns}/pods/{name}/status", w(self._mk_patch("pods", "status")))
+        r("POST", "/api/v1/namespaces/{ns}/pods/{name}/binding", w(self.h_binding))
+        r("POST", "/api/v1/namespaces/{ns}/bindings", w(self.h_bindings))
+        r("GET", "/api/v1/nodes", w(self._mk_list("nodes")))
+        r("POST", "/api/v1/nodes", w(self._mk_create("nodes")))
+        r("GET", "/api/v1/nodes/{name}", w(self._mk_get("nodes")))
+        r("PUT", "/api/v1/nodes/{name}", w(self._mk_put("nodes", "")))
+        r("PATCH", "/api/v1/nodes/{name}", w(self._mk_patch("nodes", "")))
+        r("PUT", "/api/v1/nodes/{name}/status", w(self._mk_put("nodes", "status")))
+        r("PATCH", "/api/v1/nodes/{name}/status", w(self._mk_patch("nodes", "status")))
+        r("DELETE", "/api/v1/nodes/{name}", w(self._mk_delete("nodes")))
+        r("GET", "/fake/faults", w(self.h_faults_get))
+        r("POST", "/fake/faults", w(self.h_faults))
+        r("GET", "/fake/stats", w(self.h_stats))
+        return srv
 
-    @web.middleware
-    async def _mw(self, request: web.Request, handler):
-        self.counts[request.method] += 1
-        if self.faults.latency_ms and request.query.get("watch") not in ("1", "true"):
+    def _wrap(self, handler):
+        """Request accounting + injected latency (what an aiohttp middleware did)."""
+        async def slow(request):
             await asyncio.sleep(self.faults.latency_ms / 1000.0)
-        return await handler(request)
+            return await handler(request) if asyncio.iscoroutinefunction(handler) else handler(request)
+
+        def h(request):
+            self.counts[request.method] += 1
+            if self.faults.latency_ms and request.query.get("watch") not in ("1", "true"):
+                return slow(request)
+            return handler(request)
+        return h
 
     @staticmethod
-    def _json(obj, status=200) -> web.Response:
-        return web.Response(body=json.dumps(obj, separators=(",", ":")).encode(), status=status,
-                            content_type="application/json")
+    def _json(obj, status=200) -> Response:
+        return Response(json.dumps(obj, separators=(",", ":")).encode(), status)
 
-    async def h_version(self, request):
+    def h_version(self, request):
         return self._json({"major": "1", "minor": "30", "gitVersion": "v1.30.0-gsx-fake", "platform": "linux/amd64"})
 
-    async def h_healthz(self, request):
-        return web.Response(text="ok")
+    def h_healthz(self, request):
+        return Response(b"ok", 200, "text/plain")
 
-    async def h_api(self, request):
+    def h_api(self, request):
         return self._json({"kind": "APIVersions", "versions": ["v1"]})
 
-    async def h_faults_get(self, request):
+    def h_faults_get(self, request):
         return self._json(self.faults.as_dict())
 
-    async def h_faults(self, request):
-        self.faults.update(await request.json())
+    def h_faults(self, request):
+        self.faults.update(request.json() or {})
         return self._json(self.faults.as_dict())
 
-    async def h_stats(self, request):
+    def h_stats(self, request):
         return self._json({"rv": self.rv, "counts": dict(self.counts), "watchers": len(self.watchers),
                            **{k: len(v) for k, v in self.store.items()}})
 
     def _maybe_error(self):
         if self.faults.error_rate and self.faults.rng.random() < self.faults.error_rate:
             self.counts["injected_error"] += 1
-            raise web.HTTPInternalServerError(text=json.dumps(status_body(500, "InternalError", "injected fault")),
-                                              content_type="application/json")
+            raise HTTPError(500, status_body(500, "InternalError", "injected fault"))
 
     def _mk_list(self, kind):
-        async def h(request: web.Request):
+        lists = {"pods": "PodList", "nodes": "NodeList", "events": "EventList"}
+
+        def h(request: Request):
             q = request.query
             ns = request.match_info.get("ns", "")
             fsel = q.get("fieldSelector", "")
             lsel = q.get("labelSelector", "")
             if q.get("watch") in ("1", "true"):
-                return await self._watch(request, kind, ns, fsel, lsel, q.get("resourceVersion", ""))
+                return self._watch(request, kind, ns, fsel, lsel, q.get("resourceVersion", ""))
             items = self.list(kind, ns, fsel, lsel)
-            body = {"kind": {"pods": "PodList", "nodes": "NodeList", "events": "EventList"}[kind],
-                    "apiVersion": "v1", "metadata": {"resourceVersion": str(self.rv)}, "items": items}
-            return self._json(body)
+            return self._json({"kind": lists[kind], "apiVersion": "v1",
+                               "metadata": {"resourceVersion": str(self.rv)}, "items": items})
         return h
 
     async def _watch(self, request, kind, ns, fsel, lsel, rv_s):
         w = _Watcher(kind, ns, fsel, lsel)
-        # replay history after rv (or 410 if compacted)
+        out = Stream(request.transport)
         backlog = []
         if rv_s not in ("", "0"):
             try:
@@ -461,12 +468,10 @@ class FakeApiServer:
             except ValueError:
                 rv = 0
             if self.oldest_rv and rv < self.oldest_rv:
-                resp = web.StreamResponse(headers={"Content-Type": "application/json"})
-                await resp.prepare(request)
                 err = {"type": "ERROR", "object": status_body(
                     410, "Expired", f"too old resource version: {rv} ({self.oldest_rv})")}
-                await resp.write(json.dumps(err).encode() + b"\n")
-                return resp
+                out.write(json.dumps(err).encode() + b"\n")
+                return out
             for (erv, k, _et, line, obj) in self.history:
                 if erv > rv and k == kind and w.wants(obj):
                     backlog.append(line)
@@ -474,12 +479,11 @@ class FakeApiServer:
             for o in self.list(kind, ns, fsel, lsel):
                 backlog.append(json.dumps({"type": "ADDED", "object": o}, separators=(",", ":")).encode() + b"\n")
         self.watchers.append(w)
-        resp = web.StreamResponse(headers={"Content-Type": "application/json", "Transfer-Encoding": "chunked"})
         try:
-            await resp.prepare(request)
+            out.start()
             sent = 0
             if backlog:
-                await resp.write(b"".join(backlog))
+                out.write(b"".join(backlog))
                 sent += len(backlog)
             timeout = float(request.query.get("timeoutSeconds", "0") or 0) or None
             deadline = time.monotonic() + timeout if timeout else None
@@ -490,122 +494,128 @@ class FakeApiServer:
                 try:
                     line = await asyncio.wait_for(w.queue.get(), 1.0 if rem is None else min(rem, 1.0))
                 except asyncio.TimeoutError:
-                    tr = request.transport
-                    if tr is None or tr.is_closing():
-                        break  # client went away (aiohttp does not cancel the handler)
+                    if request.closed:
+                        break  # client went away
                     continue
                 if not line:
                     break  # server shutdown sentinel
                 lines = [line]
                 while not w.queue.empty():
                     lines.append(w.queue.get_nowait())
-                await resp.write(b"".join(lines))
+                if out.closed:
+                    break
+                out.write(b"".join(lines))
                 sent += len(lines)
                 if self.faults.drop_watch_after and sent >= self.faults.drop_watch_after:
                     self.counts["watch_dropped"] += 1
                     break
-        except (ConnectionResetError, asyncio.CancelledError):
-            pass
         finally:
             w.closed = True
             try:
                 self.watchers.remove(w)
             except ValueError:
                 pass
-        return resp
+        return out
 
     def _mk_create(self, kind):
-        async def h(request):
-            body = await request.json()
+        def h(request):
+            body = request.json()
             if kind == "pods":
                 self._maybe_error()
-            obj = self.create(kind, body, request.match_info.get("ns"))
-            return self._json(obj, 201)
+            return self._json(self.create(kind, body, request.match_info.get("ns")), 201)
         return h
 
     def _mk_get(self, kind):
-        async def h(request):
+        def h(request):
             return self._json(self._get(kind, request.match_info.get("ns", ""), request.match_info["name"]))
         return h
 
     def _mk_put(self, kind, sub):
-        async def h(request):
-            body = await request.json()
+        def h(request):
+            body = request.json()
             if kind == "pods":
                 self._maybe_error()
-            obj = self.replace(kind, request.match_info.get("ns", ""), request.match_info["name"], body, sub)
-            return self._json(obj)
+            return self._json(self.replace(kind, request.match_info.get("ns", ""), request.match_info["name"], body,
+                                           sub))
         return h
 
     def _mk_patch(self, kind, sub):
-        async def h(request):
-            ct = request.headers.get("Content-Type", "")
-            body = await request.json()
+        def h(request):
+            ct = request.headers.get("content-type", "")
             if "json-patch+json" in ct:
                 return self._json(status_body(415, "UnsupportedMediaType", "json-patch not supported"), 415)
+            body = request.json()
             if kind == "pods":
                 self._maybe_error()
-            obj = self.patch(kind, request.match_info.get("ns", ""), request.match_info["name"], body, sub)
-            return self._json(obj)
+            return self._json(self.patch(kind, request.match_info.get("ns", ""), request.match_info["name"], body,
+                                         sub))
         return h
+
+    @staticmethod
+    def _grace(request):
+        if "gracePeriodSeconds" in request.query:
+            return float(request.query["gracePeriodSeconds"])
+        if request.body:
+            try:
+                b = request.json()
+                if isinstance(b, dict) and b.get("gracePeriodSeconds") is not None:
+                    return float(b["gracePeriodSeconds"])
+            except ValueError:
+                pass
+        return None
 
     def _mk_delete(self, kind):
-        async def h(request):
-            grace = None
-            if "gracePeriodSeconds" in request.query:
-                grace = float(request.query["gracePeriodSeconds"])
-            elif request.can_read_body:
-                try:
-                    b = await request.json()
-                    if isinstance(b, dict) and b.get("gracePeriodSeconds") is not None:
-                        grace = float(b["gracePeriodSeconds"])
-                except ValueError:
-                    pass
-            obj = self.delete(kind, request.match_info.get("ns", ""), request.match_info["name"], grace)
+        def h(request):
+            obj = self.delete(kind, request.match_info.get("ns", ""), request.match_info["name"], self._grace(request))
             return self._json(obj)
         return h
 
-    async def h_binding(self, request):
-        body = await request.json()
+    def _mk_delete_collection(self, kind):
+        """DELETE /api/v1/namespaces/{ns}/pods?labelSelector=... (kubectl delete pods -l ...)."""
+        def h(request):
+            ns = request.match_info.get("ns", "")
+            q = request.query
+            grace = self._grace(request)
+            items = [self.delete(kind, ns, o["metadata"]["name"], grace)
+                     for o in self.list(kind, ns, q.get("fieldSelector", ""), q.get("labelSelector", ""))]
+            return self._json({"kind": "PodList", "apiVersion": "v1", "metadata": {}, "items": items})
+        return h
+
+    def h_binding(self, request):
+        body = request.json()
         self._maybe_error()
         self.bind(request.match_info["ns"], request.match_info["name"], body)
         return self._json({"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201}, 201)
 
-    async def h_bindings(self, request):
-        body = await request.json()
+    def h_bindings(self, request):
+        body = request.json()
         self._maybe_error()
         self.bind(request.match_info["ns"], (body.get("metadata") or {}).get("name", ""), body)
         return self._json({"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201}, 201)
 
 
 class FakeApiServerRunner:
-    """Start/stop helper on the current event loop (tests) or a dedicated thread/process."""
+    """Start/stop helper on the current event loop (tests) or in its own process (``main``)."""
 
     def __init__(self, server: FakeApiServer | None = None, host: str = "127.0.0.1", port: int = 0):
         self.server = server or FakeApiServer()
         self.host = host
         self.port = port
-        self._runner: web.AppRunner | None = None
 
     @property
     def url(self) -> str:
         return f"http://{self.host}:{self.port}"
 
     async def start(self) -> "FakeApiServerRunner":
-        self._runner = web.AppRunner(self.server.app, access_log=None, handle_signals=False, shutdown_timeout=1.0)
-        await self._runner.setup()
-        site = web.TCPSite(self._runner, self.host, self.port, backlog=1024, reuse_address=True)
-        await site.start()
-        if self.port == 0:
-            self.port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
+        self.port = await self.server.app.start(self.host, self.port)
         return self
 
     async def stop(self):
         for w in list(self.server.watchers):
             w.closed = True
             w.queue.put_nowait(b"")
-        if self._runner:
-            await self._runner.cleanup()
+        await asyncio.sleep(0)
+        await self.server.app.stop()
 
 
 def main(argv=None):

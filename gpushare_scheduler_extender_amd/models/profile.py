@@ -15,6 +15,7 @@ NODE_DEVICE_MEMORY_ANNOTATION = "gpushare.amd.com/device-memory"  # "268,268,...
 NODE_DEVICE_INFO_ANNOTATION = "gpushare.amd.com/devices"  # JSON device inventory from the plugin
 POD_CU_MASK_ANNOTATION = "gpushare.amd.com/cu-mask"  # per-pod CU partition (isolation)
 POD_ASSIGN_TIME_ANNOTATION = "gpushare.amd.com/assign-time"
+NODE_RUNTIME_ENDPOINTS_ANNOTATION = "gpushare.amd.com/runtime-endpoints"  # JSON {gpu index: runtime shim URL}
 
 
 @dataclass(frozen=True)

@@ -57,6 +57,8 @@ class ChildProc:
             return ""
 
     def stop(self):
+        import shutil  # noqa: PLC0415
+
         if self.proc.poll() is None:
             self.proc.terminate()
             try:
@@ -65,6 +67,8 @@ class ChildProc:
                 self.proc.kill()
                 self.proc.wait(5)
         self.log.close()
+        if os.environ.get("GSX_KEEP_LOGS") != "1":
+            shutil.rmtree(self.tmp, ignore_errors=True)
 
 
 def start_apiserver() -> ChildProc:
@@ -76,3 +80,8 @@ def start_extender(apiserver: str, profile: str = "shared-gpu", bind_mode: str =
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.extender", "--host", "127.0.0.1", "--port", "0",
                       "--apiserver", apiserver, "--profile", profile, "--bind-mode", bind_mode,
                       "--threadness", str(threadness), "--log-level", log_level], "extender")
+
+
+def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", workers: int = 32) -> ChildProc:
+    return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
+                      apiserver, "--profile", profile, "--workers", str(workers)], "node-agent")

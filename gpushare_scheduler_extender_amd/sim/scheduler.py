@@ -26,9 +26,8 @@ import logging
 import time
 from dataclasses import dataclass, field
 
-import aiohttp
-
 from ..k8s.client import KubeClient
+from ..k8s.fasthttp import Client
 from ..k8s.informer import Handler, Informer, obj_key
 from ..models import pod as podutil
 from ..models import wire
@@ -79,7 +78,7 @@ class SchedulerSim:
         self.stats = SimStats()
         self._assumed: dict[str, tuple[str, int]] = {}  # pod key -> (node, request)
         self._queued: set[str] = set()
-        self._http: aiohttp.ClientSession | None = None
+        self._http: Client | None = None
         self._http_limit = http_limit
         self._tasks: list[asyncio.Task] = []
         self._bg: set[asyncio.Task] = set()
@@ -141,9 +140,9 @@ class SchedulerSim:
         return min(names, key=lambda nm: (free(nm), nm))
 
     # ------------------------------------------------------------ cycles
-    async def _sess(self) -> aiohttp.ClientSession:
+    def _sess(self) -> Client:
         if self._http is None:
-            self._http = aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=self._http_limit))
+            self._http = Client(self.url, limit=self._http_limit, timeout=60.0)
         return self._http
 
     async def _schedule_one(self, key: str):
@@ -165,11 +164,9 @@ class SchedulerSim:
                 body = wire.filter_args(pod, [n["metadata"]["name"] for n in cands])
             else:
                 body = wire.filter_args(pod, nodes=cands)
-            s = await self._sess()
             t0 = time.perf_counter()
-            async with s.post(self.url + "/filter", data=body,
-                              headers={"Content-Type": "application/json"}) as r:
-                res = wire.ExtenderFilterResult.decode(await r.read())
+            r = await self._sess().request("POST", "/filter", body)
+            res = wire.ExtenderFilterResult.decode(r.body)
             tm.filter_rtt = time.perf_counter() - t0
             self.stats.filter_calls += 1
             if res.error:
@@ -197,12 +194,9 @@ class SchedulerSim:
         try:
             md = pod["metadata"]
             args = wire.ExtenderBindingArgs(md["name"], md.get("namespace", "default"), md.get("uid", ""), node)
-            s = await self._sess()
             t0 = time.perf_counter()
-            async with s.post(self.url + "/bind", data=args.encode(),
-                              headers={"Content-Type": "application/json"}) as r:
-                body = await r.read()
-                status = r.status
+            r = await self._sess().request("POST", "/bind", args.encode())
+            body, status = r.body, r.status
             tm.bind_rtt = time.perf_counter() - t0
             err = json.loads(body).get("Error", "") if body else f"HTTP {status}"
             if status != 200 or err:
