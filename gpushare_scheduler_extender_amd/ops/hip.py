@@ -220,3 +220,21 @@ def time_gemm(stream: Stream, a: int, b: int, c: int, m: int, n: int, k: int, it
     _ck(lib().gsx_event_time_gemm(stream.handle, ctypes.c_void_p(a), ctypes.c_void_p(b), ctypes.c_void_p(c),
                                   m, n, k, iters, ctypes.byref(ms)), "time_gemm")
     return ms.value
+
+
+class Slice(ctypes.Structure):
+    _fields_ = [("addr", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("tag", ctypes.c_uint64)]
+
+
+def hbm_admit(stream: Stream, slices: list[tuple[int, int, int]], stamp_idx: int, stride: int) -> int:
+    """Stamp slice ``stamp_idx`` (or none with -1) and verify all ``(addr, bytes, tag)`` slices in one launch."""
+    L = lib()
+    if not getattr(L, "_admit_sig", False):
+        L.gsx_hbm_admit.argtypes = [ctypes.c_void_p, ctypes.POINTER(Slice), ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+        L.gsx_hbm_admit.restype = ctypes.c_int
+        L._admit_sig = True
+    arr = (Slice * max(1, len(slices)))(*[Slice(a, b, t & 0xFFFFFFFFFFFFFFFF) for a, b, t in slices])
+    bad = ctypes.c_uint64(0)
+    _ck(L.gsx_hbm_admit(stream.handle, arr, len(slices), stamp_idx, stride, ctypes.byref(bad)), "hbm_admit")
+    return bad.value

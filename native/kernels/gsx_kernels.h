@@ -64,6 +64,17 @@ int gsx_cuprobe(void* stream, int blocks, int spin, uint32_t* out_host);
 // [base, base+bytes).  verify returns the number of bad stamps in *bad.
 int gsx_hbm_stamp(void* stream, void* base, uint64_t bytes, uint64_t stride, uint64_t tag);
 int gsx_hbm_verify(void* stream, const void* base, uint64_t bytes, uint64_t stride, uint64_t tag, uint64_t* bad);
+// Batched pod admission: optionally stamp slice `stamp_idx` (-1: none), then
+// verify every slice in ONE launch; *bad = total bad stamps.  The bad-stamp
+// counter lives in pinned host memory, so there is no memset / copy kernel
+// and exactly one stream sync per call.
+typedef struct {
+  uint64_t addr;
+  uint64_t bytes;
+  uint64_t tag;
+} gsx_slice;
+int gsx_hbm_admit(void* stream, const gsx_slice* slices, int n, int stamp_idx, uint64_t stride, uint64_t* bad);
+
 // Fill [base, base+bytes) with a 32-bit pattern (bytes % 16 == 0).
 int gsx_hbm_fill(void* stream, void* base, uint64_t bytes, uint32_t pattern);
 

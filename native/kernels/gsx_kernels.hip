@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -71,6 +72,26 @@ __global__ __launch_bounds__(256) void verify_kernel(const char* base, uint64_t 
   // wave64 reduction, one atomic per wave
   for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
   if ((threadIdx.x & 63) == 0 && mine) atomicAdd(bad, static_cast<unsigned long long>(mine));
+}
+
+constexpr int kMaxSlices = 32;
+struct SliceTable {
+  gsx_slice s[kMaxSlices];
+  int n;
+};
+
+// grid.y = slice; each block strides over that slice's stamps
+__global__ __launch_bounds__(256) void verify_slices_kernel(SliceTable t, uint64_t stride, unsigned long long* bad) {
+  const gsx_slice sl = t.s[blockIdx.y];
+  const uint64_t n = sl.bytes / stride;
+  const char* base = reinterpret_cast<const char*>(sl.addr);
+  uint32_t mine = 0;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    Stamp st = *reinterpret_cast<const Stamp*>(base + i * stride);
+    mine += (st.tag != sl.tag || st.off != i * stride) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+  if ((threadIdx.x & 63) == 0 && mine) atomicAdd_system(bad, static_cast<unsigned long long>(mine));
 }
 
 __global__ __launch_bounds__(256) void fill_kernel(uint4* p, uint64_t n16, uint32_t pat) {
@@ -207,6 +228,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(const uint16_t* __
 
 std::mutex g_mu;
 unsigned long long* g_counter[64] = {nullptr};
+unsigned long long* g_host_counter[64] = {nullptr};  // pinned, device-visible
 
 hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -351,6 +373,50 @@ int gsx_hbm_verify(void* stream, const void* base, uint64_t bytes, uint64_t stri
   GSX_CHECK(hipMemcpyAsync(&h, ctr, sizeof(h), hipMemcpyDeviceToHost, S(stream)));
   GSX_CHECK(hipStreamSynchronize(S(stream)));
   *bad = h;
+  return 0;
+}
+
+int gsx_hbm_admit(void* stream, const gsx_slice* slices, int n, int stamp_idx, uint64_t stride, uint64_t* bad) {
+  *bad = 0;
+  if (n < 0 || stride < sizeof(Stamp) || stride % 16) return fail_arg("gsx_hbm_admit: bad n/stride");
+  for (int i = 0; i < n; ++i) {
+    if (!slices[i].addr || slices[i].addr % 16) return fail_arg("gsx_hbm_admit: slice base not 16-B aligned");
+  }
+  if (stamp_idx >= n) return fail_arg("gsx_hbm_admit: stamp_idx out of range");
+  if (stamp_idx >= 0) {
+    const gsx_slice& s0 = slices[stamp_idx];
+    uint64_t ns = s0.bytes / stride;
+    if (ns) {
+      hipLaunchKernelGGL(stamp_kernel, dim3(grid_for(ns, 256, 8192)), dim3(256), 0, S(stream),
+                         reinterpret_cast<char*>(s0.addr), ns, stride, s0.tag);
+      GSX_CHECK(hipGetLastError());
+    }
+  }
+  if (n == 0) return 0;
+  int dev = 0;
+  GSX_CHECK(hipGetDevice(&dev));
+  unsigned long long* hc;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (dev < 0 || dev >= 64) return fail_arg("gsx_hbm_admit: device index");
+    if (!g_host_counter[dev]) {
+      GSX_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g_host_counter[dev]), 64, hipHostMallocCoherent));
+    }
+    hc = g_host_counter[dev];
+  }
+  __atomic_store_n(hc, 0ull, __ATOMIC_SEQ_CST);
+  uint64_t maxn = 0;
+  for (int i = 0; i < n; ++i) maxn = std::max<uint64_t>(maxn, slices[i].bytes / stride);
+  const int gx = grid_for(maxn, 256, 64);
+  for (int base = 0; base < n; base += kMaxSlices) {
+    SliceTable t;
+    t.n = std::min(kMaxSlices, n - base);
+    for (int i = 0; i < t.n; ++i) t.s[i] = slices[base + i];
+    hipLaunchKernelGGL(verify_slices_kernel, dim3(gx, t.n), dim3(256), 0, S(stream), t, stride, hc);
+    GSX_CHECK(hipGetLastError());
+  }
+  GSX_CHECK(hipStreamSynchronize(S(stream)));
+  *bad = __atomic_load_n(hc, __ATOMIC_SEQ_CST);
   return 0;
 }
 

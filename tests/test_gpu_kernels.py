@@ -48,6 +48,26 @@ def test_hbm_stamp_verify_and_overlap_detection(hip):
     s.destroy()
 
 
+def test_hbm_admit_batched_stamp_and_verify(hip):
+    s = hip.Stream(0)
+    buf = hip.DeviceBuffer(0, 64 << 20)
+    mib16, st = 16 << 20, 1 << 16
+    a = (buf.addr(0), mib16, 11)
+    b = (buf.addr(mib16), mib16, 22)
+    assert hip.hbm_admit(s, [a], 0, st) == 0
+    assert hip.hbm_admit(s, [a, b], 1, st) == 0
+    # a pod wrongly placed over the second half of a and the first half of b
+    c = (buf.addr(mib16 // 2), mib16, 33)
+    assert hip.hbm_admit(s, [a, b, c], 2, st) == 2 * (mib16 // 2) // st
+    assert hip.hbm_admit(s, [c], -1, st) == 0
+    # more slices than one launch's table (32): chunked launches
+    many = [(buf.addr(i * (1 << 20)), 1 << 20, 100 + i) for i in range(40)]
+    for i in range(40):
+        assert hip.hbm_admit(s, many[: i + 1], i, st) == 0
+    buf.free()
+    s.destroy()
+
+
 def test_hbm_fill_pattern_and_bandwidth(hip):
     s = hip.Stream(0)
     n = 4 << 30

@@ -1,0 +1,294 @@
+"""k8s layer: fake apiserver semantics, lean HTTP stack, client/kubeconfig, informer recovery, work queue."""
+import asyncio
+import base64
+import json
+import os
+import socket
+import tempfile
+
+import pytest
+import yaml
+
+from gpushare_scheduler_extender_amd.k8s.client import ApiError, KubeClient, KubeConfig, RateLimiter
+from gpushare_scheduler_extender_amd.k8s.fakeapi import CONFLICT_MSG, FakeApiServer, FakeApiServerRunner, merge_patch
+from gpushare_scheduler_extender_amd.k8s.fasthttp import Client, Response, Server
+from gpushare_scheduler_extender_amd.k8s.informer import Handler, Informer
+from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
+from gpushare_scheduler_extender_amd.parallel.workqueue import (BucketLimiter, ItemExponentialBackoff, ShutDown,
+                                                                WorkQueue)
+
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+async def _api(history=200000):
+    r = await FakeApiServerRunner(FakeApiServer(history=history)).start()
+    return r, KubeClient(r.url)
+
+
+# ---------------------------------------------------------------- fake apiserver semantics
+
+def test_optimistic_concurrency_exact_message_and_patch():
+    async def go():
+        r, c = await _api()
+        try:
+            p = await c.create("pods", make_pod("a", 2))
+            stale = dict(p)
+            p2 = await c.patch("pods", "a", {"metadata": {"annotations": {"x": "1"}}}, "default")
+            assert p2["metadata"]["resourceVersion"] != p["metadata"]["resourceVersion"]
+            with pytest.raises(ApiError) as ei:
+                await c.replace("pods", stale)
+            assert ei.value.conflict
+            # the exact string the reference compares against (pkg/cache/nodeinfo.go:14-16)
+            assert ei.value.message == CONFLICT_MSG.format(res="pods", name="a")
+            assert "the object has been modified; please apply your changes to the latest version" in ei.value.message
+            with pytest.raises(ApiError) as ei:
+                await c.patch("pods", "a", {"metadata": {"resourceVersion": "1", "labels": {"a": "b"}}}, "default")
+            assert ei.value.status == 409
+            # merge patch deletes with null and never touches spec.nodeName / status on the main resource
+            p3 = await c.patch("pods", "a", {"metadata": {"annotations": {"x": None, "y": "2"}},
+                                             "spec": {"nodeName": "evil"}, "status": {"phase": "Running"}}, "default")
+            assert p3["metadata"]["annotations"] == {"y": "2"}
+            assert "nodeName" not in p3["spec"] and p3["status"]["phase"] == "Pending"
+        finally:
+            await c.close()
+            await r.stop()
+    run(go())
+
+
+def test_binding_copies_annotations_once():
+    async def go():
+        r, c = await _api()
+        try:
+            p = await c.create("pods", make_pod("a", 2, annotations={"keep": "me"}))
+            await c.bind_pod("default", "a", "n1", p["metadata"]["uid"], {"IDX": "3"})
+            got = await c.get("pods", "a", "default")
+            assert got["spec"]["nodeName"] == "n1"
+            assert got["metadata"]["annotations"] == {"keep": "me", "IDX": "3"}
+            assert got["status"]["conditions"][-1]["type"] == "PodScheduled"
+            with pytest.raises(ApiError) as ei:
+                await c.bind_pod("default", "a", "n2")
+            assert ei.value.conflict and "already assigned" in ei.value.message
+            q = await c.create("pods", make_pod("b", 2))
+            with pytest.raises(ApiError) as ei:
+                await c.bind_pod("default", "b", "n1", "wrong-uid")
+            assert "Precondition failed" in ei.value.message
+            assert q["metadata"]["uid"]
+        finally:
+            await c.close()
+            await r.stop()
+    run(go())
+
+
+def test_selectors_graceful_delete_and_deletecollection():
+    async def go():
+        r, c = await _api()
+        try:
+            await c.create("pods", make_pod("a", 1, node="n1", labels={"wave": "1"}))
+            await c.create("pods", make_pod("b", 1, node="n2", labels={"wave": "1"}))
+            await c.create("pods", make_pod("c", 1, labels={"wave": "2"}))
+            lst = await c.list("pods", field_selector="spec.nodeName=n1")
+            assert [p["metadata"]["name"] for p in lst["items"]] == ["a"]
+            lst = await c.list("pods", "default", label_selector="wave=1")
+            assert sorted(p["metadata"]["name"] for p in lst["items"]) == ["a", "b"]
+            lst = await c.list("pods", label_selector="wave!=1")
+            assert [p["metadata"]["name"] for p in lst["items"]] == ["c"]
+            d = await c.delete("pods", "a", "default", grace_seconds=1)
+            assert d["metadata"]["deletionTimestamp"]
+            assert (await c.get("pods", "a", "default"))["metadata"]["deletionTimestamp"]
+            await asyncio.sleep(1.2)
+            with pytest.raises(ApiError) as ei:
+                await c.get("pods", "a", "default")
+            assert ei.value.not_found
+            out = await c.request("DELETE", "/api/v1/namespaces/default/pods", params={"labelSelector": "wave=1"})
+            assert [p["metadata"]["name"] for p in out["items"]] == ["b"]
+            assert [p["metadata"]["name"] for p in (await c.list("pods"))["items"]] == ["c"]
+        finally:
+            await c.close()
+            await r.stop()
+    run(go())
+
+
+def test_watch_from_compacted_version_is_410():
+    async def go():
+        r, c = await _api(history=3)
+        try:
+            for i in range(6):
+                await c.create("pods", make_pod(f"p{i}", 1))
+            with pytest.raises(ApiError) as ei:
+                async for _ev in c.watch("pods", resource_version="1"):
+                    pass
+            assert ei.value.gone and ei.value.reason == "Expired"
+            got = []
+            async for ev in c.watch("pods", resource_version="5", timeout_seconds=1):
+                got.append(ev["object"]["metadata"]["name"])
+            assert got == ["p5"]
+        finally:
+            await c.close()
+            await r.stop()
+    run(go())
+
+
+def test_merge_patch_rfc7386():
+    assert merge_patch({"a": 1, "b": {"c": 2, "d": 3}}, {"b": {"c": None, "e": 4}, "f": [1]}) == \
+        {"a": 1, "b": {"d": 3, "e": 4}, "f": [1]}
+    assert merge_patch({"a": 1}, {"a": {"b": 1}}) == {"a": {"b": 1}}
+
+
+# ---------------------------------------------------------------- informer recovery
+
+def test_informer_rewatch_after_drop_and_relist_after_410():
+    async def go():
+        r, c = await _api(history=5)
+        inf = Informer(KubeClient(r.url), "pods")
+        seen = {"add": 0, "upd": 0, "del": 0}
+        inf.add_handler(Handler(lambda o, raw: seen.__setitem__("add", seen["add"] + 1),
+                                lambda o, n, raw: seen.__setitem__("upd", seen["upd"] + 1),
+                                lambda o, raw: seen.__setitem__("del", seen["del"] + 1)))
+        try:
+            await inf.start()
+            await inf.wait_synced(5)
+            r.server.faults.update({"drop_watch_after": 2})
+            for i in range(6):
+                await c.create("pods", make_pod(f"p{i}", 1))
+            for _ in range(400):
+                if len(inf.store) == 6:
+                    break
+                await asyncio.sleep(0.01)
+            assert len(inf.store) == 6 and inf.rewatches >= 1
+            # compacted history: a watch from an old resourceVersion gets 410 -> re-list
+            r.server.faults.update({"drop_watch_after": 0})
+            inf.last_rv = "1"
+            for t in inf._tasks:  # noqa: SLF001 - force the reconnect path
+                t.cancel()
+            inf._tasks.clear()  # noqa: SLF001
+            await inf.start()
+            await c.delete("pods", "p0", "default")
+            for _ in range(400):
+                if "default/p0" not in inf.store and inf.relists >= 2:
+                    break
+                await asyncio.sleep(0.01)
+            assert "default/p0" not in inf.store and inf.relists >= 2
+            assert seen["add"] == 6 and seen["del"] >= 1
+        finally:
+            await inf.stop()
+            await inf.client.close()
+            await c.close()
+            await r.stop()
+    run(go())
+
+
+# ---------------------------------------------------------------- lean HTTP stack
+
+def test_fasthttp_pipelining_chunked_body_and_keepalive():
+    async def go():
+        srv = Server()
+        srv.route("POST", "/echo/{x}", lambda req: Response.json({"x": req.match_info["x"], "n": len(req.body),
+                                                                  "q": req.query.get("a", "")}))
+
+        async def slow(req):
+            await asyncio.sleep(0.01)
+            return Response(b"slow", 200, "text/plain")
+        srv.route("GET", "/slow", slow)
+        port = await srv.start()
+        # two pipelined requests, the first slow: responses must come back in order
+        rd, wr = await asyncio.open_connection("127.0.0.1", port)
+        wr.write(b"GET /slow HTTP/1.1\r\nHost: x\r\n\r\n"
+                 b"POST /echo/7?a=b HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabc\r\n2\r\nde\r\n0\r\n\r\n")
+        data = b""
+        while data.count(b"HTTP/1.1 200") < 2 or not data.endswith(b"}"):
+            data += await asyncio.wait_for(rd.read(4096), 2)
+        assert data.index(b"slow") < data.index(b'"x":"7"')
+        assert b'"n":5' in data and b'"q":"b"' in data
+        wr.close()
+        cli = Client(f"http://127.0.0.1:{port}")
+        for i in range(5):
+            resp = await cli.request("POST", f"/echo/{i}", b"{}")
+            assert resp.status == 200 and resp.json()["x"] == str(i)
+        assert len(cli.idle) == 1  # one keep-alive connection reused
+        resp = await cli.request("GET", "/nope")
+        assert resp.status == 404
+        await cli.close()
+        await srv.stop()
+    run(go())
+
+
+# ---------------------------------------------------------------- config / client
+
+def test_kubeconfig_parsing_token_and_embedded_certs(tmp_path):
+    ca = base64.b64encode(b"-----BEGIN CERTIFICATE-----\nX\n-----END CERTIFICATE-----\n").decode()
+    kc = {"apiVersion": "v1", "kind": "Config", "current-context": "ctx",
+          "clusters": [{"name": "c", "cluster": {"server": "https://10.0.0.1:6443/", "certificate-authority-data": ca}}],
+          "users": [{"name": "u", "user": {"token": "abc"}}, {"name": "v", "user": {"username": "x", "password": "y"}}],
+          "contexts": [{"name": "ctx", "context": {"cluster": "c", "user": "u"}},
+                       {"name": "basic", "context": {"cluster": "c", "user": "v"}}]}
+    p = tmp_path / "kc.yaml"
+    p.write_text(yaml.safe_dump(kc))
+    cfg = KubeConfig.from_kubeconfig(str(p))
+    assert cfg.server == "https://10.0.0.1:6443" and cfg.token == "abc"
+    assert open(cfg.ca_file, "rb").read().startswith(b"-----BEGIN CERTIFICATE-----")
+    cfg2 = KubeConfig.from_kubeconfig(str(p), "basic")
+    assert cfg2.extra_headers["Authorization"] == "Basic " + base64.b64encode(b"x:y").decode()
+    assert KubeConfig.auto(server="http://h:1").server == "http://h:1"
+
+
+def test_rate_limiter_token_bucket():
+    async def go():
+        lim = RateLimiter(qps=100, burst=2)
+        loop = asyncio.get_running_loop()
+        t0 = loop.time()
+        for _ in range(6):
+            await lim.acquire()
+        dt = loop.time() - t0
+        assert 0.03 <= dt < 0.5  # 2 burst + 4 at 100 qps ~= 40 ms
+    run(go())
+
+
+# ---------------------------------------------------------------- work queue
+
+def test_workqueue_dedup_and_processing_semantics():
+    async def go():
+        q = WorkQueue()
+        q.add("a")
+        q.add("a")
+        q.add("b")
+        assert len(q) == 2
+        a = await q.get()
+        q.add("a")  # re-added while processing: not handed out twice
+        b = await q.get()
+        assert (a, b) == ("a", "b") and len(q) == 0
+        q.done("a")
+        assert len(q) == 1  # replayed on done
+        assert await q.get() == "a"
+        q.done("a")
+        q.done("b")
+        assert q.idle()
+        await q.shutdown()
+        with pytest.raises(ShutDown):
+            await q.get()
+    run(go())
+
+
+def test_rate_limiters():
+    ex = ItemExponentialBackoff(0.005, 1.0)
+    assert [ex.when("x") for _ in range(4)] == [0.005, 0.01, 0.02, 0.04]
+    assert ex.num_requeues("x") == 4
+    ex.forget("x")
+    assert ex.when("x") == 0.005
+    for _ in range(20):
+        ex.when("y")
+    assert ex.when("y") == 1.0
+    b = BucketLimiter(qps=10, burst=2)
+    assert b.when("a") == 0 and b.when("a") == 0 and b.when("a") > 0
+
+
+def test_rate_limited_requeue_delivers_later():
+    async def go():
+        q = WorkQueue()
+        q.add_rate_limited("x")
+        assert len(q) == 0
+        item = await asyncio.wait_for(q.get(), 1)
+        assert item == "x"
+        await q.shutdown()
+    run(go())

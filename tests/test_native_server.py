@@ -1,0 +1,164 @@
+"""C++ front end of the extender (native/engine/server.cc): HTTP edge cases, concurrency, fallback routing."""
+import asyncio
+import json
+import socket
+import threading
+
+from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
+from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
+from gpushare_scheduler_extender_amd.models import wire
+
+
+async def _stack():
+    api = await FakeApiServerRunner().start()
+    c = KubeClient(api.url)
+    await c.create("nodes", make_node("n", 8 * 100, 8))
+    ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=True, http_threads=2).start()
+    for _ in range(200):
+        if ext.server.engine.has_node("n"):
+            break
+        await asyncio.sleep(0.01)
+    return api, c, ext
+
+
+async def _teardown(api, c, ext):
+    await ext.stop()
+    await ext.server.client.close()
+    await c.close()
+    await api.stop()
+
+
+def _raw(port, payload: bytes, expect_responses: int) -> bytes:
+    s = socket.create_connection(("127.0.0.1", port), timeout=5)
+    s.sendall(payload)
+    data = b""
+    while data.count(b"HTTP/1.1 ") < expect_responses or not data.rstrip().endswith(b"}"):
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    s.close()
+    return data
+
+
+def test_pipelined_and_chunked_requests():
+    async def go():
+        api, c, ext = await _stack()
+        try:
+            body = wire.filter_args(make_pod("p", 50), ["n"])
+            one = (b"POST /gpushare-scheduler/filter HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n" % len(body)) + body
+            chunked = (b"POST /gpushare-scheduler/filter HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n" +
+                       b"%x\r\n" % 10 + body[:10] + b"\r\n" + b"%x\r\n" % (len(body) - 10) + body[10:] + b"\r\n0\r\n\r\n")
+            loop = asyncio.get_running_loop()
+            data = await loop.run_in_executor(None, _raw, ext.port, one + chunked + one, 3)
+            assert data.count(b'"NodeNames":["n"]') == 3
+            # garbage request line -> 400 and close
+            bad = await loop.run_in_executor(None, _raw, ext.port, b"NOPE\r\n\r\n", 1)
+            assert bad.startswith(b"HTTP/1.1 400")
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())
+
+
+def test_concurrent_filters_from_threads_and_stats():
+    async def go():
+        api, c, ext = await _stack()
+        try:
+            body = wire.filter_args(make_pod("p", 10), ["n", "ghost"])
+            req = (b"POST /gpushare-scheduler/filter HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n" % len(body)) + body
+            errs = []
+
+            def worker():
+                try:
+                    s = socket.create_connection(("127.0.0.1", ext.port), timeout=5)
+                    for _ in range(50):
+                        s.sendall(req)
+                        data = b""
+                        while not data.endswith(b'"Error":""}'):
+                            data += s.recv(65536)
+                        assert b'"NodeNames":["n"]' in data
+                    s.close()
+                except Exception as e:  # noqa: BLE001
+                    errs.append(e)
+            ts = [threading.Thread(target=worker) for _ in range(8)]
+            loop = asyncio.get_running_loop()
+            await loop.run_in_executor(None, lambda: ([t.start() for t in ts], [t.join() for t in ts]))
+            assert not errs, errs
+            st = ext.server.engine.server_stats()
+            assert st["filters"] >= 400 and st["filter_latency"]["n"] >= 400
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())
+
+
+def test_native_bind_fast_path_and_python_fallback():
+    async def go():
+        api, c, ext = await _stack()
+        try:
+            import aiohttp
+
+            eng = ext.server.engine
+            p1 = await c.create("pods", make_pod("fast", 30))
+            p2 = await c.create("pods", make_pod("slow", 20))
+            for _ in range(200):
+                if ext.server.controller.pods.get("default/slow"):
+                    break
+                await asyncio.sleep(0.01)
+            async with aiohttp.ClientSession() as s:
+                # filter first: the pod is remembered natively, bind never touches Python
+                async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(p1, ["n"])) as r:
+                    assert json.loads(await r.read())["NodeNames"] == ["n"]
+                before = eng.server_stats()["proxied"]
+                async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
+                        "fast", "default", p1["metadata"]["uid"], "n").encode()) as r:
+                    assert r.status == 200 and json.loads(await r.read()) == {"Error": ""}
+                assert eng.server_stats()["proxied"] == before
+                # never filtered here -> the Python slow path binds it (proxied)
+                async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
+                        "slow", "default", p2["metadata"]["uid"], "n").encode()) as r:
+                    assert r.status == 200, await r.read()
+                assert eng.server_stats()["proxied"] == before + 1
+                # non-native routes are served through the proxy
+                async with s.get(ext.url + "/metrics") as r:
+                    text = await r.text()
+                    assert r.status == 200 and "gpushare_binpack_utilization" in text
+                async with s.get(ext.url + "/healthz") as r:
+                    assert r.status == 200
+            fast = await c.get("pods", "fast", "default")
+            slow = await c.get("pods", "slow", "default")
+            assert fast["spec"]["nodeName"] == "n" and slow["spec"]["nodeName"] == "n"
+            # best fit: both land on device 0 (30 + 20 <= 100)
+            assert fast["metadata"]["annotations"]["SHARED_GPU_MEM_IDX"] == "0"
+            assert slow["metadata"]["annotations"]["SHARED_GPU_MEM_IDX"] == "0"
+            assert eng.node_devices("n")[0] == (100, 50)
+            assert eng.server_stats()["bind_ok"] == 1
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())
+
+
+def test_native_bind_failure_becomes_event():
+    async def go():
+        api, c, ext = await _stack()
+        try:
+            import aiohttp
+
+            p = await c.create("pods", make_pod("huge", 500))
+            async with aiohttp.ClientSession() as s:
+                async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(p, ["n"])) as r:
+                    assert json.loads(await r.read())["FailedNodes"] == {"n": "Insufficient GPU Memory in one device"}
+                async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
+                        "huge", "default", p["metadata"]["uid"], "n").encode()) as r:
+                    assert r.status == 500
+                    assert json.loads(await r.read())["Error"] == "The node n can't place the pod huge in ns default"
+            for _ in range(100):
+                evs = (await c.list("events", "default"))["items"]
+                if evs:
+                    break
+                await asyncio.sleep(0.05)
+            assert evs and evs[0]["reason"] == "FailedBinding" and evs[0]["type"] == "Warning"
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())
