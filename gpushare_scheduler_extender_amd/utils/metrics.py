@@ -8,7 +8,7 @@ binpack utilisation) that are computed at scrape time from the native ledger.
 from __future__ import annotations
 
 from prometheus_client import CollectorRegistry, Counter, Histogram, generate_latest
-from prometheus_client.core import GaugeMetricFamily
+from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, HistogramMetricFamily
 
 LAT_BUCKETS = (0.0001, 0.00025, 0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0)
 
@@ -43,6 +43,23 @@ class _LedgerCollector:
             g = GaugeMetricFamily(f"gpushare_engine_{k}", f"native engine counter {k}")
             g.add_metric([], s[k])
             yield g
+        # C++ front end (native/engine/server.cc): request counters + latency histograms
+        ns = self.engine.server_stats() if hasattr(self.engine, "server_stats") else {}
+        if ns:
+            for k in ("requests", "filters", "binds", "bind_ok", "bind_fail", "proxied", "bad_requests", "inspects",
+                      "connections", "api_calls", "conflicts_retried"):
+                c = CounterMetricFamily(f"gpushare_native_{k}", f"native HTTP front end: {k}")
+                c.add_metric([], ns[k])
+                yield c
+            for k in ("filter_latency", "bind_latency", "api_latency"):
+                h = ns[k]
+                cum, buckets = 0, []
+                for le, cnt in zip(h["bounds"], h["counts"]):
+                    cum += cnt
+                    buckets.append((repr(le), cum))
+                buckets.append(("+Inf", cum + h["counts"][-1]))
+                yield HistogramMetricFamily(f"gpushare_native_{k}_seconds", f"native {k.replace('_', ' ')}",
+                                            buckets=buckets, sum_value=h["sum"])
 
 
 class Metrics:
