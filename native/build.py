@@ -150,12 +150,25 @@ def build_asan(force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
+def build_tsan(force: bool = False, verbose: bool = False) -> Path:
+    """Host-only ThreadSanitizer build of the same test (epoll loops + bind pool + ledger mutex)."""
+    src = NATIVE / "engine"
+    out = ROOT / "build" / "engine_test_tsan"
+    srcs = [s for s in sorted(src.glob("*.cc")) if s.name != "bindings.cc"]
+    if force or _newer(out, srcs + sorted(src.glob("*.h"))):
+        out.parent.mkdir(parents=True, exist_ok=True)
+        _run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=thread", "-fno-omit-frame-pointer",
+              "-I" + str(src), *map(str, srcs), "-o", str(out), "-lssl", "-lcrypto", "-lpthread"], verbose)
+    return out
+
+
 TARGETS = {
     "engine": build_engine,
     "mxdev": build_mxdev,
     "kernels": build_kernels,
     "tools": build_tools,
     "asan": build_asan,
+    "tsan": build_tsan,
 }
 DEFAULT = ["engine", "mxdev", "kernels"]
 

@@ -1,0 +1,277 @@
+// Host-side unit + stress test of the native engine, built with sanitizers:
+//   ASan+UBSan: python native/build.py asan   -> build/engine_test_asan
+//   TSan:       python native/build.py tsan   -> build/engine_test_tsan
+// (the reference had no race detection at all; its cache had
+// two data races.)  The stress part runs the epoll front end with 8 client
+// threads doing filter + bind against a tiny in-process "apiserver".
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cassert>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <memory>
+#include <vector>
+
+#include "http.h"
+#include "json.h"
+#include "ledger.h"
+#include "model.h"
+#include "quantity.h"
+#include "server.h"
+
+using namespace gsx;
+
+static int g_fail = 0;
+#define CHECK(c)                                                   \
+  do {                                                             \
+    if (!(c)) {                                                    \
+      std::fprintf(stderr, "%s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #c); \
+      ++g_fail;                                                    \
+    }                                                              \
+  } while (0)
+
+static void test_json() {
+  json::Doc d;
+  std::string err;
+  CHECK(d.parse(R"({"Pod":{"metadata":{"name":"a\u00e9","uid":"u1"}},"nodenames":["n1","n2"]})", &err));
+  CHECK(d.find(0, "pod", true) >= 0);
+  CHECK(d.find(0, "pod", false) < 0);
+  int64_t nn = d.find(0, "NodeNames", true);
+  CHECK(nn >= 0 && d.at(static_cast<uint32_t>(nn)).count == 2);
+  int64_t nm = d.path(static_cast<uint32_t>(d.find(0, "Pod")), {"metadata", "name"});
+  CHECK(nm >= 0 && d.str(static_cast<uint32_t>(nm)) == "a\xc3\xa9");
+  json::Doc bad;
+  CHECK(!bad.parse("{\"a\":", &err) && err == "unexpected end of JSON input");
+  CHECK(!bad.parse("[1,]", &err));
+  std::string q;
+  json::append_quoted(&q, "<&>\"\n");
+  CHECK(q == "\"\\u003c\\u0026\\u003e\\\"\\n\"");
+}
+
+static void test_quantity() {
+  int64_t v;
+  CHECK(parse_quantity("64Gi", &v) && v == (int64_t(64) << 30));
+  CHECK(parse_quantity("1.5", &v) && v == 2);
+  CHECK(parse_quantity("500m", &v) && v == 1);
+  CHECK(parse_quantity("1e3", &v) && v == 1000);
+  CHECK(!parse_quantity("1Kib", &v));
+  CHECK(parse_atoi("-12", &v) && v == -12);
+  CHECK(!parse_atoi(" 1", &v));
+}
+
+static std::string pod_json(const std::string& name, const std::string& uid, int mem) {
+  return "{\"metadata\":{\"name\":\"" + name + "\",\"namespace\":\"default\",\"uid\":\"" + uid +
+         "\"},\"spec\":{\"containers\":[{\"name\":\"c\",\"resources\":{\"limits\":{\"shared-gpu/gpu-mem\":\"" +
+         std::to_string(mem) + "\"}}}]},\"status\":{\"phase\":\"Pending\"}}";
+}
+
+static void test_ledger() {
+  Ledger l{Profile()};
+  NodeView nv;
+  nv.name = "n";
+  nv.total = 4 * 16276;
+  nv.count = 4;
+  l.upsert_node(nv);
+  // design doc bind example: free {12207, 8138, 4069, 16276}, request 8138 -> GPU1
+  const int64_t used[3] = {16276 - 12207, 16276 - 8138, 16276 - 4069};
+  for (int i = 0; i < 3; ++i) {
+    PodView v;
+    v.uid = "x" + std::to_string(i);
+    v.name = v.uid;
+    v.ns = "default";
+    v.node = "n";
+    v.dev_idx = i;
+    v.annot_mem = used[i];
+    v.phase = "Running";
+    CHECK(l.upsert_pod(v) == 1);
+  }
+  int64_t total = 0;
+  CHECK(l.assume("u", "default", "p", "n", 8138, &total) == 1 && total == 16276);
+  CHECK(l.assume("u", "default", "p", "n", 8138, &total) == -4);  // in flight
+  l.finish_bind("u", false, 0);
+  CHECK(l.node_devices("n")[1].second == 8138);
+  CHECK(l.check("n", 16276) == Check::Ok);
+  CHECK(l.check("n", 16277) == Check::Insufficient);
+  CHECK(l.check("zz", 1) == Check::NodeNotFound);
+  std::string body = "{\"Pod\":" + pod_json("q", "uq", 16276) + ",\"NodeNames\":[\"n\",\"zz\"]}";
+  std::string out = filter_body(l, body);
+  CHECK(out.find("\"NodeNames\":[\"n\"]") != std::string::npos);
+  CHECK(out.find("\"zz\":\"node \\\"zz\\\" not found\"") != std::string::npos);
+  Ledger::PendingPod pp;
+  CHECK(l.pending("uq", &pp) && pp.req == 16276 && pp.name == "q");
+}
+
+static void test_http() {
+  http::Message m;
+  std::string err;
+  std::string two = "POST /a?x=1 HTTP/1.1\r\nHost: h\r\nContent-Length: 3\r\n\r\nabcGET /b HTTP/1.1\r\n\r\n";
+  long n = http::parse(two.data(), two.size(), true, &m, &err);
+  CHECK(n > 0 && m.method == "POST" && m.path() == "/a" && m.body == "abc" && m.keep_alive);
+  long n2 = http::parse(two.data() + n, two.size() - static_cast<size_t>(n), true, &m, &err);
+  CHECK(n2 > 0 && m.method == "GET" && m.body.empty());
+  std::string ch = "HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabc\r\n2\r\nde\r\n0\r\n\r\n";
+  CHECK(http::parse(ch.data(), ch.size() - 3, false, &m, &err) == 0);  // incomplete
+  CHECK(http::parse(ch.data(), ch.size(), false, &m, &err) == static_cast<long>(ch.size()) && m.body == "abcde");
+  std::string close = "HTTP/1.0 200 OK\r\n\r\nxyz";
+  CHECK(http::parse(close.data(), close.size(), false, &m, &err) == 0);
+  CHECK(http::parse(close.data(), close.size(), false, &m, &err, true) > 0 && m.body == "xyz" && !m.keep_alive);
+  http::Url u;
+  CHECK(http::parse_url("https://[::1]:6443/pre/", &u) && u.tls && u.host == "::1" && u.port == 6443 &&
+        u.prefix == "/pre");
+}
+
+// ---------------------------------------------------------------- stress
+
+static int listen_any(int* port) {
+  int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  int one = 1;
+  setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in a;
+  std::memset(&a, 0, sizeof(a));
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  ::bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a));
+  ::listen(fd, 128);
+  socklen_t sl = sizeof(a);
+  getsockname(fd, reinterpret_cast<sockaddr*>(&a), &sl);
+  *port = ntohs(a.sin_port);
+  return fd;
+}
+
+// minimal "kube-apiserver": answers every request with 201 Created, keep-alive
+static void fake_apiserver(int lfd, std::atomic<bool>* stop, std::atomic<int>* bindings) {
+  std::vector<std::thread> conns;
+  while (!stop->load()) {
+    int c = ::accept(lfd, nullptr, nullptr);
+    if (c < 0) break;
+    conns.emplace_back([c, bindings] {
+      std::string buf;
+      char tmp[8192];
+      while (true) {
+        http::Message m;
+        std::string err;
+        long n = http::parse(buf.data(), buf.size(), true, &m, &err);
+        if (n > 0) {
+          buf.erase(0, static_cast<size_t>(n));
+          if (m.path().find("/binding") != std::string_view::npos) bindings->fetch_add(1);
+          std::string r = http::response(201, "application/json", "{\"kind\":\"Status\",\"code\":201}", true);
+          if (::send(c, r.data(), r.size(), MSG_NOSIGNAL) < 0) break;
+          continue;
+        }
+        if (n < 0) break;
+        ssize_t got = ::recv(c, tmp, sizeof(tmp), 0);
+        if (got <= 0) break;
+        buf.append(tmp, static_cast<size_t>(got));
+      }
+      ::close(c);
+    });
+  }
+  for (auto& t : conns) t.join();
+}
+
+static std::string roundtrip(int fd, const std::string& req) {
+  if (::send(fd, req.data(), req.size(), MSG_NOSIGNAL) < 0) return {};
+  std::string buf;
+  char tmp[8192];
+  while (true) {
+    http::Message m;
+    std::string err;
+    if (http::parse(buf.data(), buf.size(), false, &m, &err) > 0) return std::to_string(m.status) + " " + m.body;
+    ssize_t got = ::recv(fd, tmp, sizeof(tmp), 0);
+    if (got <= 0) return {};
+    buf.append(tmp, static_cast<size_t>(got));
+  }
+}
+
+static void test_server_stress() {
+  int aport = 0;
+  int alfd = listen_any(&aport);
+  std::atomic<bool> stop{false};
+  std::atomic<int> bindings{0};
+  std::thread api(fake_apiserver, alfd, &stop, &bindings);
+
+  Ledger l{Profile()};
+  NodeView nv;
+  nv.name = "n";
+  nv.total = 8 * 1000;
+  nv.count = 8;
+  l.upsert_node(nv);
+  ServerConfig cfg;
+  cfg.host = "127.0.0.1";
+  cfg.threads = 3;
+  cfg.pool_threads = 6;
+  cfg.api.server = "http://127.0.0.1:" + std::to_string(aport);
+  std::unique_ptr<NativeServer> srv(new NativeServer(&l, cfg));
+  std::string err;
+  int port = srv->start(&err);
+  CHECK(port > 0);
+  const int kThreads = 8, kPods = 40;
+  std::atomic<int> ok{0}, failed{0};
+  std::vector<std::thread> cs;
+  for (int t = 0; t < kThreads; ++t) {
+    cs.emplace_back([&, t] {
+      int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+      sockaddr_in a;
+      std::memset(&a, 0, sizeof(a));
+      a.sin_family = AF_INET;
+      a.sin_port = htons(static_cast<uint16_t>(port));
+      a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+      if (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) {
+        failed.fetch_add(kPods);
+        return;
+      }
+      for (int i = 0; i < kPods; ++i) {
+        std::string uid = "u" + std::to_string(t) + "-" + std::to_string(i);
+        std::string name = "p" + std::to_string(t) + "-" + std::to_string(i);
+        std::string fb = "{\"Pod\":" + pod_json(name, uid, 25) + ",\"NodeNames\":[\"n\"]}";
+        std::string r1 = roundtrip(fd, "POST /gpushare-scheduler/filter HTTP/1.1\r\nContent-Length: " +
+                                           std::to_string(fb.size()) + "\r\n\r\n" + fb);
+        std::string bb = "{\"PodName\":\"" + name + "\",\"PodNamespace\":\"default\",\"PodUID\":\"" + uid +
+                         "\",\"Node\":\"n\"}";
+        std::string r2 = roundtrip(fd, "POST /gpushare-scheduler/bind HTTP/1.1\r\nContent-Length: " +
+                                           std::to_string(bb.size()) + "\r\n\r\n" + bb);
+        if (r2.rfind("200 ", 0) == 0) {
+          ok.fetch_add(1);
+        } else {
+          failed.fetch_add(1);
+        }
+        (void)r1;
+      }
+      ::close(fd);
+    });
+  }
+  for (auto& t : cs) t.join();
+  // 8 devices x 1000 / 25 = 320 slots for 320 pods: every bind fits exactly once
+  CHECK(ok.load() == kThreads * kPods);
+  CHECK(failed.load() == 0);
+  CHECK(bindings.load() == kThreads * kPods);
+  {
+    std::lock_guard<std::mutex> g(l.mu());
+    for (auto& d : l.node_devices("n")) CHECK(d.second == 1000);
+  }
+  srv.reset();  // stops the loops and closes the keep-alive apiserver connections
+  stop.store(true);
+  ::shutdown(alfd, SHUT_RDWR);
+  ::close(alfd);
+  api.join();
+}
+
+int main() {
+  test_json();
+  test_quantity();
+  test_ledger();
+  test_http();
+  test_server_stress();
+  if (g_fail) {
+    std::fprintf(stderr, "%d check(s) failed\n", g_fail);
+    return 1;
+  }
+  std::printf("engine_test: all checks passed\n");
+  return 0;
+}
