@@ -52,6 +52,7 @@ class Controller:
         self._raw: dict[str, bytes] = {}  # key -> raw JSON of the latest event (native parse fast path)
         self._tasks: list[asyncio.Task] = []
         self.synced_pods = 0
+        self.overcommitted: list = []
         self.sync_errors = 0
         self.pods.add_handler(Handler(self._on_pod_add, self._on_pod_update, self._on_pod_delete,
                                       filter_fn=self._is_gpushare_pod))
@@ -128,6 +129,14 @@ class Controller:
                 self.engine.upsert_pod_json(dumps(pod))
                 n += 1
         log.info("build_cache: recovered %d pods from annotations", n)
+        # consistency check: the reference's uint arithmetic would have wrapped here
+        self.overcommitted = []
+        for node in self.engine.node_names():
+            for i, (total, used) in enumerate(self.engine.node_devices(node)):
+                if used > total:
+                    self.overcommitted.append((node, i, used, total))
+                    log.warning("node %s GPU %d is over-committed after recovery: %d > %d (annotations disagree "
+                                "with capacity); it accepts no new pods until it drains", node, i, used, total)
         return n
 
     async def _worker(self):

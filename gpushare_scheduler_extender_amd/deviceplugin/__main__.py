@@ -14,6 +14,7 @@ import sys
 
 from ..k8s.client import KubeClient, KubeConfig
 from ..models.profile import get_profile
+from ..utils.logsetup import setup_logging
 from . import api
 from .devices import discover
 from .plugin import GpuSharePlugin
@@ -34,9 +35,9 @@ def main(argv=None) -> int:
                     help="HBM per GPU withheld from sharing (driver / runtime overhead)")
     ap.add_argument("--health-interval", type=float, default=float(env.get("GSX_HEALTH_INTERVAL", "10")))
     ap.add_argument("--log-level", default=env.get("LOG_LEVEL", "info"))
+    ap.add_argument("--log-dir", default=env.get("GSX_LOG_DIR", ""))
     a = ap.parse_args(argv)
-    logging.basicConfig(level=getattr(logging, a.log_level.upper(), logging.INFO),
-                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    setup_logging(a.log_level, a.log_dir or None, "gpushare-device-plugin")
     if not a.node:
         ap.error("--node / NODE_NAME is required")
 

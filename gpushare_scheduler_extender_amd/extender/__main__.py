@@ -25,6 +25,7 @@ import sys
 
 from ..k8s.client import KubeClient, KubeConfig
 from ..models.profile import get_profile
+from ..utils.logsetup import setup_logging
 from .server import ExtenderRunner, ExtenderServer
 
 
@@ -38,6 +39,8 @@ def parse_args(argv=None):
     ap.add_argument("--apiserver", default=env.get("GSX_APISERVER"))
     ap.add_argument("--threadness", type=int, default=int(env.get("THREADNESS", "1") or 1))
     ap.add_argument("--log-level", default=env.get("LOG_LEVEL", "info"))
+    ap.add_argument("--log-dir", default=env.get("GSX_LOG_DIR", ""),
+                    help="also write per-level rotating log files here (the reference used /var/log/device-plugin)")
     ap.add_argument("--profile", default=env.get("GSX_PROFILE", "shared-gpu"))
     ap.add_argument("--bind-mode", default=env.get("GSX_BIND_MODE", "binding"), choices=["binding", "update"])
     ap.add_argument("--kube-qps", type=float, default=float(env.get("GSX_KUBE_QPS", "0")))
@@ -54,8 +57,7 @@ def parse_args(argv=None):
 
 def main(argv=None) -> int:
     a = parse_args(argv)
-    logging.basicConfig(level=getattr(logging, a.log_level.upper(), logging.INFO),
-                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    setup_logging(a.log_level, a.log_dir or None, "gpushare-schd-extender")
     log = logging.getLogger("gsx.main")
 
     async def run():

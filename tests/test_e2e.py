@@ -248,3 +248,23 @@ def test_fragmentation_guard_end_to_end():
             st, body = await c.post("/gpushare-scheduler/filter", wire.filter_args(big, ["n"]))
             assert json.loads(body)["FailedNodes"] == {"n": "Insufficient GPU Memory in one device"}
     run(go())
+
+
+def test_recovery_consistency_check_flags_overcommit():
+    """Annotations that over-commit a device (e.g. capacity shrank) are reported, not wrapped (nodeinfo.go:260)."""
+    async def go():
+        async with Cluster() as c:
+            await c.client.create("nodes", make_node("n", 10, 1))
+            for nm in ("a", "b"):
+                await c.client.create("pods", make_pod(nm, 8, node="n", phase="Running", annotations={
+                    "SHARED_GPU_MEM_IDX": "0", "SHARED_GPU_MEM_POD": "8"}))
+            srv2 = ExtenderServer(KubeClient(c.api.url), SHARED_GPU)
+            await srv2.start()
+            try:
+                assert srv2.controller.overcommitted == [("n", 0, 16, 10)]
+                st, body = await c.post("/gpushare-scheduler/filter", wire.filter_args(make_pod("p", 1), ["n"]))
+                assert json.loads(body)["NodeNames"] == []
+            finally:
+                await srv2.stop()
+                await srv2.client.close()
+    run(go())
