@@ -93,8 +93,8 @@ def parse():
     ap.add_argument("--devices", default="auto", help="auto|hip|amdsmi|fake (fake: no GPU, CPU plumbing only)")
     ap.add_argument("--stamp-stride", type=int, default=1 << 20)
     ap.add_argument("--json-out", default="")
-    ap.add_argument("--agent", default="rank", choices=["node", "rank"],
-                    help="rank: one device-plugin agent per GPU rank (default); node: one node-agent process driving a runtime shim per GPU rank")
+    ap.add_argument("--agent", default="node", choices=["node", "rank"],
+                    help="node: one node-agent process (the node's device plugin) driving a runtime shim per GPU rank (default); rank: one agent per GPU rank")
     ap.add_argument("--inproc", action="store_true",
                     help="run apiserver + extender in this process (no child processes; used under rocprofv3)")
     return ap.parse_args()
@@ -249,41 +249,50 @@ def main():
     n_pods = a.pods_per_gpu * world
     step_stats = []
 
-    async def wave(step: int):
-        import aiohttp
+    ext_http = {}
 
-        keys = [f"default/w{step}-p{i}" for i in range(n_pods)]
+    async def inspect_used():
+        if "c" not in ext_http:
+            from gpushare_scheduler_extender_amd.k8s.fasthttp import Client
+
+            ext_http["c"] = Client(ext_url)
+        r = await ext_http["c"].request("GET", "/gpushare-scheduler/inspect")
+        return json.loads(r.body)
+
+    async def wave(step: int):
+        names = [f"w{step}-p{i}" for i in range(n_pods)]
+        keys = [f"default/{nm}" for nm in names]
+        label = {"gsx-wave": str(step)}
         t0 = time.perf_counter()
-        await asyncio.gather(*(client.create("pods", make_pod(k.split("/")[1], a.pod_gib, profile=profile))
-                               for k in keys))
+        await asyncio.gather(*(client.create("pods", make_pod(nm, a.pod_gib, profile=profile, labels=label))
+                               for nm in names))
         await sim.wait_bound(keys, 120)
         t_bound = time.perf_counter()
-        # every pod admitted on its GPU and Running
-        while True:
-            ph = [((sim.pods.get(k) or {}).get("status") or {}).get("phase") for k in keys]
-            if all(p == "Running" for p in ph):
-                break
+
+        def phases():
+            return [((sim.pods.get(k) or {}).get("status") or {}).get("phase") for k in keys]
+
+        # every pod admitted on its GPU and Running (event-driven on the scheduler's pod informer)
+        def all_running():
+            ph = phases()
             if any(p == "Failed" for p in ph):
                 raise RuntimeError(f"pod admission failed: {[k for k, p in zip(keys, ph) if p == 'Failed']}")
-            if time.perf_counter() - t0 > 120:
-                raise TimeoutError(f"pods not running: {ph}")
-            await asyncio.sleep(0.0005)
+            return all(p == "Running" for p in ph)
+        await sim.wait_for(all_running, 120)
         t_run = time.perf_counter()
-        async with aiohttp.ClientSession() as s:
-            async with s.get(ext_url + "/gpushare-scheduler/inspect") as r:
-                insp = json.loads(await r.read())
+        insp = await inspect_used()
         used = sum(n["usedGPU"] for n in insp["nodes"])
         total = sum(n["totalGPU"] for n in insp["nodes"])
         per_dev = [d["usedGPU"] for n in insp["nodes"] for d in n["devs"]]
-        # teardown: delete the wave, the step ends when the ledger is empty again
-        await asyncio.gather(*(client.delete("pods", k.split("/")[1], "default") for k in keys))
-        async with aiohttp.ClientSession() as s:
-            while True:
-                async with s.get(ext_url + "/gpushare-scheduler/inspect") as r:
-                    insp2 = json.loads(await r.read())
-                if sum(n["usedGPU"] for n in insp2["nodes"]) == 0:
-                    break
-                await asyncio.sleep(0.0005)
+        # teardown: one DeleteCollection for the wave; the step ends when the extender's ledger is empty
+        await client.request("DELETE", "/api/v1/namespaces/default/pods", params={"labelSelector": f"gsx-wave={step}"})
+        while True:
+            insp2 = await inspect_used()
+            if sum(n["usedGPU"] for n in insp2["nodes"]) == 0:
+                break
+            if time.perf_counter() - t0 > 120:
+                raise TimeoutError("ledger did not drain")
+            await asyncio.sleep(0.0003)
         t_end = time.perf_counter()
         tm = [sim.stats.timings[k] for k in keys]
         res = {"bind_latency": [t.bound - t.seen for t in tm], "bind_rtt": [t.bind_rtt for t in tm],
@@ -380,6 +389,8 @@ def main():
             lt.run(sim.stop(), 30)
             lt.run(sim.client.close(), 30)
             lt.run(client.close(), 30)
+            if "c" in ext_http:
+                lt.run(ext_http["c"].close(), 30)
             for r in inproc:
                 lt.run(r.stop(), 30)
     finally:

@@ -27,6 +27,8 @@ def parse_quantity(s) -> int:
         return max(_INT64_MIN, min(_INT64_MAX, s))
     if isinstance(s, float):
         s = repr(s)
+    if isinstance(s, str) and s.isdigit() and s.isascii():  # fast path: plain integers ("64")
+        return min(_INT64_MAX, int(s))
     m = _RE.match(str(s))
     if not m:
         raise ValueError(f"quantities must match the regular expression: {s!r}")

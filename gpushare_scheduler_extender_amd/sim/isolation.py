@@ -10,7 +10,12 @@ exact environment the device plugin's Allocate produces, in four scenarios:
 * ``shared``        4 pods co-resident, no partition (time-sliced, unisolated);
 * ``partitioned``   4 pods co-resident, 64 CUs each via the stream CU mask;
 * ``env``           4 pods co-resident, 64 CUs each via ``HSA_CU_MASK`` only
-                    (process-wide; applies to torch's own queues too).
+                    (process-wide; applies to torch's own queues too);
+* ``solo64``        one pod alone inside a 64-CU partition (what a partition is worth);
+* ``noisy`` / ``noisy-partitioned``  pod 0 runs a small (latency-bound) GEMM
+                    next to 3 pods running large GEMMs, without / with
+                    partitions: pod 0's throughput relative to ``solo`` / ``solo64``
+                    is the interference the partition removes.
 
 Reported per scenario: per-pod TFLOP/s, aggregate, and fairness (min/max).
 Run: ``python -m gpushare_scheduler_extender_amd.sim.isolation --seconds 8``.
@@ -45,10 +50,11 @@ def pod_envs(n_pods: int, cus_each: int, gpu_total_gib: int, pod_gib: int, with_
     return envs
 
 
-def run_pods(envs: list[dict], seconds: float, kernel: str, size: int, mask_mode: str) -> list[dict]:
+def run_pods(envs: list[dict], seconds: float, kernel: str, size, mask_mode: str) -> list[dict]:
     start_at = time.time() + 20.0  # time for every process to import torch and warm up
     procs = []
-    for e in envs:
+    sizes = size if isinstance(size, list) else [size] * len(envs)
+    for e, sz in zip(envs, sizes):
         env = dict(os.environ)
         env.update({k: v for k, v in e.items() if k not in ("GSX_CU_MASK", "HSA_CU_MASK")})
         if mask_mode in ("stream", "both") and "GSX_CU_MASK" in e:
@@ -61,7 +67,7 @@ def run_pods(envs: list[dict], seconds: float, kernel: str, size: int, mask_mode
         env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
         cmd = [sys.executable, "-m", "gpushare_scheduler_extender_amd.sim.workload", "--total",
                e["SHARED_GPU_MEM_DEV"], "--allocated", e["SHARED_GPU_MEM_CONTAINER"], "--kernel", kernel,
-               "--size", str(size), "--seconds", str(seconds), "--json"]
+               "--size", str(sz), "--seconds", str(seconds), "--json"]
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                                       cwd=str(ROOT)))
     out = []
@@ -88,7 +94,8 @@ def main(argv=None) -> int:
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--kernel", default="gsx", choices=["gsx", "torch"])
     ap.add_argument("--size", type=int, default=8192)
-    ap.add_argument("--scenarios", default="solo,shared,partitioned,env")
+    ap.add_argument("--small-size", type=int, default=2048)
+    ap.add_argument("--scenarios", default="solo,shared,partitioned,env,solo-small,solo64,noisy,noisy-partitioned")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args(argv)
     results = []
@@ -102,6 +109,17 @@ def main(argv=None) -> int:
         elif sc == "partitioned":
             envs = pod_envs(a.pods, a.cus, a.gpu_gib, a.pod_gib, True)
             res = run_pods(envs, a.seconds, a.kernel, a.size, "stream")
+        elif sc == "solo64":
+            envs = pod_envs(1, a.cus, a.gpu_gib, a.pod_gib, True)
+            res = run_pods(envs, a.seconds, a.kernel, a.small_size, "stream")
+        elif sc == "solo-small":
+            envs = pod_envs(1, a.cus, a.gpu_gib, a.pod_gib, False)
+            res = run_pods(envs, a.seconds, a.kernel, a.small_size, "none")
+        elif sc in ("noisy", "noisy-partitioned"):
+            masked = sc == "noisy-partitioned"
+            envs = pod_envs(a.pods, a.cus, a.gpu_gib, a.pod_gib, masked)
+            sizes = [a.small_size] + [a.size] * (a.pods - 1)
+            res = run_pods(envs, a.seconds, a.kernel, sizes, "stream" if masked else "none")
         elif sc == "env":
             envs = pod_envs(a.pods, a.cus, a.gpu_gib, a.pod_gib, True)
             res = run_pods(envs, a.seconds, "torch" if a.kernel == "gsx" else a.kernel, a.size, "env")

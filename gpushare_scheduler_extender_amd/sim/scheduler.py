@@ -76,13 +76,17 @@ class SchedulerSim:
         self.queue: asyncio.Queue = asyncio.Queue()
         self.bind_sem = asyncio.Semaphore(max_inflight_binds)
         self.stats = SimStats()
-        self._assumed: dict[str, tuple[str, int]] = {}  # pod key -> (node, request)
+        self._assumed: dict[str, tuple[str, int]] = {}  # pod key -> (node, request), bind in flight
+        self._placed: dict[str, tuple[str, int]] = {}  # pod key -> (node, request), observed bound & live
+        self._used: dict[str, int] = collections.defaultdict(int)  # node -> placed + assumed requests
+        self._req: dict[str, int] = {}  # pod uid -> gpu-mem request (pod specs are immutable)
         self._queued: set[str] = set()
         self._http: Client | None = None
         self._http_limit = http_limit
         self._tasks: list[asyncio.Task] = []
         self._bg: set[asyncio.Task] = set()
         self.bound_event = asyncio.Event()
+        self.changed = asyncio.Event()  # set on every pod event (event-driven waits)
         self.pods.add_handler(Handler(self._on_pod, lambda o, n, r: self._on_pod(n, r), self._on_pod_delete))
 
     # ------------------------------------------------------------ pod intake
@@ -91,8 +95,42 @@ class SchedulerSim:
                                                                            "default-scheduler") == self.scheduler_name
                 and not podutil.is_complete(pod))
 
+    def _request(self, pod: dict) -> int:
+        uid = (pod.get("metadata") or {}).get("uid", "")
+        r = self._req.get(uid)
+        if r is None:
+            r = self._req[uid] = podutil.gpu_mem_request(pod, self.profile)
+        return r
+
+    def _account(self, key: str, pod: dict | None):
+        """Incremental NodeResourcesFit bookkeeping (the scheduler cache's view of node usage)."""
+        old = self._placed.pop(key, None)
+        if old is not None:
+            self._used[old[0]] -= old[1]
+        if pod is None:
+            return
+        n = podutil.node_name(pod)
+        if n and not podutil.is_terminal(pod):
+            req = self._request(pod)
+            self._placed[key] = (n, req)
+            self._used[n] += req
+            a = self._assumed.pop(key, None)  # now observed: stop counting the assumption
+            if a is not None:
+                self._used[a[0]] -= a[1]
+
+    def _assume(self, key: str, node: str, req: int):
+        self._assumed[key] = (node, req)
+        self._used[node] += req
+
+    def _unassume(self, key: str):
+        a = self._assumed.pop(key, None)
+        if a is not None:
+            self._used[a[0]] -= a[1]
+
     def _on_pod(self, pod: dict, raw):
         key = obj_key(pod)
+        self._account(key, pod)
+        self.changed.set()
         if self._pending(pod) and key not in self._queued and key not in self._assumed:
             self._queued.add(key)
             t = self.stats.timings.get(key)
@@ -102,20 +140,14 @@ class SchedulerSim:
 
     def _on_pod_delete(self, pod: dict, raw):
         key = obj_key(pod)
-        self._assumed.pop(key, None)
+        self._account(key, None)
+        self.changed.set()
+        self._unassume(key)
+        self._req.pop((pod.get("metadata") or {}).get("uid", ""), None)
 
     # ------------------------------------------------------------ aggregate fit (NodeResourcesFit)
     def _node_used(self) -> dict[str, int]:
-        used: dict[str, int] = collections.defaultdict(int)
-        for p in self.pods.list():
-            n = podutil.node_name(p)
-            if n and not podutil.is_terminal(p):
-                used[n] += podutil.gpu_mem_request(p, self.profile)
-        for key, (n, req) in self._assumed.items():
-            p = self.pods.get(key)
-            if p is None or not podutil.node_name(p):
-                used[n] += req
-        return used
+        return self._used
 
     def _prefilter(self, req: int) -> list[dict]:
         used = self._node_used()
@@ -152,7 +184,7 @@ class SchedulerSim:
             return
         tm = self.stats.timings.setdefault(key, PodTiming(key, seen=time.perf_counter()))
         tm.attempts += 1
-        req = podutil.gpu_mem_request(pod, self.profile)
+        req = self._request(pod)
         cands = self._prefilter(req)
         if not cands:
             self.stats.unschedulable += 1
@@ -183,7 +215,7 @@ class SchedulerSim:
             return
         node = self._pick(names, req)
         tm.filtered = time.perf_counter()
-        self._assumed[key] = (node, req)
+        self._assume(key, node, req)
         self.stats.scheduled += 1
         await self.bind_sem.acquire()
         t = asyncio.get_running_loop().create_task(self._bind(key, pod, node, tm))
@@ -202,7 +234,7 @@ class SchedulerSim:
             if status != 200 or err:
                 self.stats.bind_errors += 1
                 tm.error = err
-                self._assumed.pop(key, None)
+                self._unassume(key)
                 self._retry_later(key)
                 return
             tm.bound = time.perf_counter()
@@ -213,7 +245,7 @@ class SchedulerSim:
         except Exception as e:  # noqa: BLE001
             self.stats.bind_errors += 1
             tm.error = repr(e)
-            self._assumed.pop(key, None)
+            self._unassume(key)
             self._retry_later(key)
         finally:
             self.bind_sem.release()
@@ -259,7 +291,19 @@ class SchedulerSim:
     def forget(self, keys):
         for k in keys:
             self.stats.timings.pop(k, None)
-            self._assumed.pop(k, None)
+
+    async def wait_for(self, cond, timeout: float = 30.0):
+        """Wait until ``cond()`` holds, re-checking on every pod event the informer delivers."""
+        deadline = time.perf_counter() + timeout
+        while not cond():
+            rem = deadline - time.perf_counter()
+            if rem <= 0:
+                raise TimeoutError("condition not reached")
+            self.changed.clear()
+            try:
+                await asyncio.wait_for(self.changed.wait(), min(rem, 0.05))
+            except asyncio.TimeoutError:
+                pass
 
     async def wait_bound(self, keys: list[str], timeout: float = 30.0):
         deadline = time.perf_counter() + timeout
