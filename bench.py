@@ -102,6 +102,8 @@ def parse():
 
 def main():
     a = parse()
+    if a.inproc:
+        a.agent = "rank"  # no child processes at all: the agents run in-process too
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
