@@ -208,6 +208,7 @@ class ExtenderServer:
         r = app.router
         r.add_post(API_PREFIX + "/filter", self.h_filter)
         r.add_post(API_PREFIX + "/bind", self.h_bind)
+        r.add_post(API_PREFIX + "/prioritize", self.h_prioritize)
         r.add_get(API_PREFIX + "/inspect", self.h_inspect)
         r.add_get(API_PREFIX + "/inspect/", self.h_inspect)
         r.add_get(API_PREFIX + "/inspect/{nodename}", self.h_inspect)
@@ -224,6 +225,12 @@ class ExtenderServer:
         self.metrics.latency.labels("filter").observe(time.perf_counter() - t0)
         self.metrics.requests.labels("filter", "200").inc()
         return web.Response(body=out, content_type="application/json")
+
+    async def h_prioritize(self, request: web.Request):
+        """Ours (the reference has no prioritize verb): binpack-first node scores, HostPriorityList."""
+        body = await request.read()
+        self.metrics.requests.labels("prioritize", "200").inc()
+        return web.Response(body=self.engine.prioritize(body), content_type="application/json")
 
     async def h_bind(self, request: web.Request):
         t0 = time.perf_counter()

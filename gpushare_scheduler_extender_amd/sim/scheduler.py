@@ -63,13 +63,14 @@ class SchedulerSim:
     def __init__(self, client: KubeClient, extender_url: str, profile: NamingProfile, *,
                  scheduler_name: str = "default-scheduler", node_cache_capable: bool = True,
                  node_policy: str = "binpack", max_inflight_binds: int = 64, retry_backoff: float = 0.05,
-                 http_limit: int = 128, namespace: str | None = None):
+                 http_limit: int = 128, namespace: str | None = None, use_prioritize: bool = False):
         self.client = client
         self.url = extender_url.rstrip("/") + "/gpushare-scheduler"
         self.profile = profile
         self.scheduler_name = scheduler_name
         self.node_cache_capable = node_cache_capable
         self.node_policy = node_policy
+        self.use_prioritize = use_prioritize  # call the extender's prioritize verb when >1 node passes
         self.retry_backoff = retry_backoff
         self.pods = Informer(client, "pods", namespace=namespace)
         self.nodes = Informer(client, "nodes")
@@ -213,7 +214,12 @@ class SchedulerSim:
             tm.error = "extender filtered all nodes"
             self._retry_later(key)
             return
-        node = self._pick(names, req)
+        if self.use_prioritize and len(names) > 1:
+            r = await self._sess().request("POST", "/prioritize", wire.filter_args(pod, names))
+            scores = {h["Host"]: h["Score"] for h in json.loads(r.body)}
+            node = max(names, key=lambda nm: (scores.get(nm, 0), [-ord(ch) for ch in nm]))
+        else:
+            node = self._pick(names, req)
         tm.filtered = time.perf_counter()
         self._assume(key, node, req)
         self.stats.scheduled += 1

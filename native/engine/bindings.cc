@@ -175,6 +175,17 @@ class Engine {
     return py::bytes(out);
   }
 
+  py::bytes prioritize(const py::bytes& body) {
+    std::string_view v = view_of(body);
+    std::string out;
+    {
+      py::gil_scoped_release rel;
+      std::lock_guard<std::mutex> g(l_.mu());
+      out = prioritize_body(l_, v);
+    }
+    return py::bytes(out);
+  }
+
   py::tuple assume(const std::string& uid, const std::string& ns, const std::string& name,
                    const std::string& node, int64_t req) {
     int64_t dev_total = -1;
@@ -389,6 +400,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("upsert_pod_json", &Engine::upsert_pod_json)
       .def("check", &Engine::check)
       .def("filter", &Engine::filter)
+      .def("prioritize", &Engine::prioritize)
       .def("assume", &Engine::assume)
       .def("finish_bind", &Engine::finish_bind, py::arg("uid"), py::arg("ok"), py::arg("ttl") = 30.0)
       .def("gc", &Engine::gc)

@@ -543,3 +543,68 @@ std::string filter_body(Ledger& l, std::string_view body) {
 }
 
 }  // namespace gsx
+
+namespace gsx {
+
+// ---------------------------------------------------------------- prioritize verb (ours)
+//
+// The reference registers only filter + bind (config/scheduler-policy-config.json:7-8),
+// so kube-scheduler spreads gpushare pods across nodes by its default scores
+// and binpacking happens only inside a node.  This verb scores every node by
+// how tightly the pod would fit its best-fit device: 10 = exact fit, 0 = does
+// not fit / empty device of a node that has a partly used one elsewhere, so
+// "binpack-first" also holds across nodes.  Wire format: HostPriorityList
+// [{"Host": name, "Score": 0..10}] (kube-scheduler extender API).
+std::string prioritize_body(Ledger& l, std::string_view body) {
+  json::Doc d;
+  std::string err;
+  if (!d.parse(body, &err) || d.at(0).type != json::T::Object) return "[]";
+  int64_t pod = d.find(0, "Pod", true);
+  if (pod < 0 || d.at(static_cast<uint32_t>(pod)).type != json::T::Object) return "[]";
+  int64_t req = pod_limits_sum(d, static_cast<uint32_t>(pod), l.profile().resource);
+  std::vector<std::string> names;
+  int64_t nn = d.find(0, "NodeNames", true);
+  if (nn >= 0 && d.at(static_cast<uint32_t>(nn)).type == json::T::Array) {
+    uint32_t end = d.at(static_cast<uint32_t>(nn)).skip;
+    for (uint32_t i = static_cast<uint32_t>(nn) + 1; i < end; i = d.next(i)) names.push_back(d.str(i));
+  } else {
+    int64_t nodes = d.find(0, "Nodes", true);
+    if (nodes >= 0 && d.at(static_cast<uint32_t>(nodes)).type == json::T::Object) {
+      int64_t items = d.find(static_cast<uint32_t>(nodes), "items");
+      if (items >= 0 && d.at(static_cast<uint32_t>(items)).type == json::T::Array) {
+        uint32_t end = d.at(static_cast<uint32_t>(items)).skip;
+        for (uint32_t i = static_cast<uint32_t>(items) + 1; i < end; i = d.next(i)) {
+          int64_t m = d.path(i, {"metadata", "name"});
+          names.push_back(m >= 0 ? d.str(static_cast<uint32_t>(m)) : std::string());
+        }
+      }
+    }
+  }
+  std::string o("[");
+  for (size_t k = 0; k < names.size(); ++k) {
+    int64_t score = 0;
+    const NodeState* n = l.node(names[k]);
+    if (n && n->gpushare() && req > 0) {
+      int64_t best = -1, best_total = 1;
+      for (const DevState& dv : n->devs) {
+        int64_t left = dv.total - dv.used - req;
+        if (left >= 0 && (best < 0 || left < best)) {
+          best = left;
+          best_total = dv.total > 0 ? dv.total : 1;
+        }
+      }
+      if (best >= 0) score = 10 - (10 * best + best_total - 1) / best_total;  // ceil: only an exact fit scores 10
+      if (score < 0) score = 0;
+    }
+    if (k) o.push_back(',');
+    o.append("{\"Host\":");
+    json::append_quoted(&o, names[k]);
+    o.append(",\"Score\":");
+    o.append(std::to_string(score));
+    o.push_back('}');
+  }
+  o.push_back(']');
+  return o;
+}
+
+}  // namespace gsx

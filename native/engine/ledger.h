@@ -149,4 +149,7 @@ class Ledger {
 // (vendor/k8s.io/kubernetes/pkg/scheduler/api/types.go:273-284).
 std::string filter_body(Ledger& l, std::string_view body);
 
+// Prioritize verb: HostPriorityList scoring nodes by best-fit tightness (0..10).
+std::string prioritize_body(Ledger& l, std::string_view body);
+
 }  // namespace gsx

@@ -412,6 +412,15 @@ void NativeServer::dispatch(Loop* lp, Conn* c, http::Message& req) {
     respond(lp, c, http::response(200, "application/json", out, ka), ka);
     return;
   }
+  if (req.method == "POST" && path == pre + "/prioritize") {
+    std::string out;
+    {
+      std::lock_guard<std::mutex> g(l_->mu());
+      out = prioritize_body(*l_, req.body);
+    }
+    respond(lp, c, http::response(200, "application/json", out, ka), ka);
+    return;
+  }
   if (req.method == "POST" && path == pre + "/bind") {
     stats_.binds.fetch_add(1, std::memory_order_relaxed);
     c->busy = true;

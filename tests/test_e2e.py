@@ -268,3 +268,23 @@ def test_recovery_consistency_check_flags_overcommit():
                 await srv2.stop()
                 await srv2.client.close()
     run(go())
+
+
+def test_prioritize_packs_nodes_before_spreading():
+    """With the prioritize verb the scheduler fills the partly used node first (binpack across nodes)."""
+    async def go():
+        async with Cluster() as c:
+            for n in ("n1", "n2", "n3"):
+                await c.client.create("nodes", make_node(n, 100, 1))
+            await c.start_sim(use_prioritize=True, node_policy="spread")
+            keys = []
+            for i in range(6):
+                await c.client.create("pods", make_pod(f"p{i}", 30))
+                keys.append(f"default/p{i}")
+                await c.sim.wait_bound([keys[-1]], 10)
+            nodes = [c.sim.stats.timings[k].node for k in keys]
+            # 3 pods of 30 fit one 100-unit device: the first node fills before the next is opened
+            assert nodes[:3] == [nodes[0]] * 3 and nodes[3:] == [nodes[3]] * 3 and nodes[0] != nodes[3]
+            st, body = await c.post("/gpushare-scheduler/prioritize", wire.filter_args(make_pod("q", 10), ["n1", "n2", "n3"]))
+            assert st == 200 and len(json.loads(body)) == 3
+    run(go())

@@ -396,3 +396,20 @@ def test_engine_matches_reference_model(counts, ops):
             for req in (1, 50, 100):
                 ok = json.loads(eng.filter(wire.filter_args(make_pod("q", req), [name])))["NodeNames"] == [name]
                 assert ok == rn2.fits(req)
+
+
+# ---------------------------------------------------------------- prioritize verb (ours)
+
+def test_prioritize_binpack_first_across_nodes():
+    eng = new_engine()
+    eng.upsert_node("tight", 100, 1)
+    eng.upsert_node("loose", 100, 1)
+    eng.upsert_node("full", 100, 1)
+    eng.upsert_node("cpu", 0, 0)
+    _load(eng, _annotated("a", "tight", 0, 70))
+    _load(eng, _annotated("b", "full", 0, 95))
+    out = json.loads(eng.prioritize(wire.filter_args(make_pod("p", 30), ["tight", "loose", "full", "cpu", "ghost"])))
+    scores = {h["Host"]: h["Score"] for h in out}
+    assert scores == {"tight": 10, "loose": 3, "full": 0, "cpu": 0, "ghost": 0}
+    assert list(out[0]) == ["Host", "Score"]
+    assert json.loads(eng.prioritize(b"junk")) == []
