@@ -51,6 +51,10 @@ def parse_args(argv=None):
                     help="1: C++ front end serves filter/bind/inspect (default); 0: aiohttp only")
     ap.add_argument("--http-threads", type=int, default=int(env.get("GSX_HTTP_THREADS", "2")))
     ap.add_argument("--bind-threads", type=int, default=int(env.get("GSX_BIND_THREADS", "16")))
+    ap.add_argument("--leader-elect", type=int, default=int(env.get("GSX_LEADER_ELECT", "0")),
+                    help="1: run as an HA replica; only the holder of the Lease binds (reference: single replica)")
+    ap.add_argument("--lease-name", default=env.get("GSX_LEASE_NAME", "gpushare-schd-extender"))
+    ap.add_argument("--lease-namespace", default=env.get("POD_NAMESPACE", "kube-system"))
     ap.add_argument("--port-file", default="", help="write the bound port to this file once serving")
     return ap.parse_args(argv)
 
@@ -64,7 +68,9 @@ def main(argv=None) -> int:
         cfg = KubeConfig.auto(a.kubeconfig, a.apiserver)
         client = KubeClient(cfg, qps=a.kube_qps, burst=a.kube_burst)
         srv = ExtenderServer(client, get_profile(a.profile), workers=a.threadness, bind_mode=a.bind_mode,
-                             reservation_ttl=a.reservation_ttl, resync_period=a.resync)
+                             reservation_ttl=a.reservation_ttl, resync_period=a.resync,
+                             leader_elect=bool(a.leader_elect), lease_name=a.lease_name,
+                             lease_namespace=a.lease_namespace)
         runner = await ExtenderRunner(srv, a.host, a.port, native=bool(a.native_http), http_threads=a.http_threads,
                                       pool_threads=a.bind_threads).start()
         if a.port_file:

@@ -65,7 +65,9 @@ class BindError(Exception):
 class ExtenderServer:
     def __init__(self, client: KubeClient, profile: NamingProfile = SHARED_GPU, *, workers: int = 1,
                  bind_mode: str = "binding", reservation_ttl: float = 60.0, resync_period: float = 30.0,
-                 emit_events: bool = True):
+                 emit_events: bool = True, leader_elect: bool = False, lease_name: str = "gpushare-schd-extender",
+                 lease_namespace: str = "kube-system", lease_duration: float = 15.0, renew_deadline: float = 10.0,
+                 retry_period: float = 2.0):
         if bind_mode not in ("binding", "update"):
             raise ValueError("bind_mode must be 'binding' or 'update'")
         self.client = client
@@ -81,13 +83,35 @@ class ExtenderServer:
         self._gc_task: asyncio.Task | None = None
         self._bg: set[asyncio.Task] = set()
         self.native_server = False
+        self.elector = None
+        if leader_elect:
+            from ..k8s.leader import LeaderElector  # noqa: PLC0415
+
+            self.elector = LeaderElector(client, lease_name, lease_namespace, lease_duration=lease_duration,
+                                         renew_deadline=renew_deadline, retry_period=retry_period,
+                                         on_started=self._became_leader, on_stopped=self._lost_leadership)
+            self.engine.set_binds_enabled(False)  # standby until the Lease is ours
+
+    @property
+    def is_leader(self) -> bool:
+        return self.elector is None or self.elector.is_leader
+
+    def _became_leader(self):
+        self.engine.set_binds_enabled(True)
+
+    def _lost_leadership(self):
+        self.engine.set_binds_enabled(False)
 
     # ------------------------------------------------------------ lifecycle
     async def start(self):
         await self.controller.start()
         self._gc_task = asyncio.get_running_loop().create_task(self._gc_loop())
+        if self.elector is not None:
+            await self.elector.start()  # informers + ledger are warm before we can win
 
     async def stop(self):
+        if self.elector is not None:
+            await self.elector.stop()
         if self._gc_task:
             self._gc_task.cancel()
         await self.controller.stop()
@@ -124,6 +148,9 @@ class ExtenderServer:
     async def bind(self, args: wire.ExtenderBindingArgs) -> str:
         """Returns "" on success or the error string of ExtenderBindingResult."""
         name, ns, uid, node = args.pod_name, args.pod_namespace, args.pod_uid, args.node
+        if not self.is_leader:
+            self.metrics.bind_results.labels("standby").inc()
+            return "this extender replica is not the leader"
         try:
             pod = await self._get_pod(name, ns, uid)
         except BindError as e:
@@ -256,6 +283,8 @@ class ExtenderServer:
 
     async def h_healthz(self, request):
         ok = self.controller.pods.synced.is_set() and self.controller.nodes.synced.is_set()
+        if ok and not self.is_leader:
+            return web.Response(text="standby (not the leader)", status=503)
         return web.Response(text="ok" if ok else "not synced", status=200 if ok else 503)
 
     async def h_metrics(self, request):

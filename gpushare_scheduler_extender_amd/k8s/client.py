@@ -178,7 +178,9 @@ class KubeConfig:
 
 
 def _ns_path(kind: str, ns: str | None, name: str | None = None, sub: str | None = None) -> str:
-    if kind == "nodes":
+    if kind == "leases":
+        p = f"/apis/coordination.k8s.io/v1/namespaces/{quote(ns or 'default', safe='')}/leases"
+    elif kind == "nodes":
         p = "/api/v1/nodes"
     elif ns:
         p = f"/api/v1/namespaces/{quote(ns, safe='')}/{kind}"

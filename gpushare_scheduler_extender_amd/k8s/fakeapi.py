@@ -167,7 +167,7 @@ class Faults:
 class FakeApiServer:
     """State + aiohttp application.  All mutation happens on the event loop thread."""
 
-    KINDS = ("pods", "nodes", "events")
+    KINDS = ("pods", "nodes", "events", "leases")
 
     def __init__(self, history: int = 200000):
         self.rv = 0
@@ -396,6 +396,12 @@ class FakeApiServer:
         r("PUT", "/api/v1/nodes/{name}/status", w(self._mk_put("nodes", "status")))
         r("PATCH", "/api/v1/nodes/{name}/status", w(self._mk_patch("nodes", "status")))
         r("DELETE", "/api/v1/nodes/{name}", w(self._mk_delete("nodes")))
+        lease = "/apis/coordination.k8s.io/v1/namespaces/{ns}/leases"
+        r("GET", lease, w(self._mk_list("leases")))
+        r("POST", lease, w(self._mk_create("leases")))
+        r("GET", lease + "/{name}", w(self._mk_get("leases")))
+        r("PUT", lease + "/{name}", w(self._mk_put("leases", "")))
+        r("DELETE", lease + "/{name}", w(self._mk_delete("leases")))
         r("GET", "/fake/faults", w(self.h_faults_get))
         r("POST", "/fake/faults", w(self.h_faults))
         r("GET", "/fake/stats", w(self.h_stats))
@@ -444,7 +450,7 @@ class FakeApiServer:
             raise HTTPError(500, status_body(500, "InternalError", "injected fault"))
 
     def _mk_list(self, kind):
-        lists = {"pods": "PodList", "nodes": "NodeList", "events": "EventList"}
+        lists = {"pods": "PodList", "nodes": "NodeList", "events": "EventList", "leases": "LeaseList"}
 
         def h(request: Request):
             q = request.query

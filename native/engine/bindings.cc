@@ -271,6 +271,7 @@ class Engine {
     if (api.contains("insecure")) cfg.api.insecure = api["insecure"].cast<bool>();
     if (cfg.api.server.empty()) cfg.native_bind = false;
     srv_.reset(new NativeServer(&l_, cfg));
+    srv_->set_binds_enabled(binds_enabled_);
     std::string err;
     int p = srv_->start(&err);
     if (p < 0) {
@@ -320,6 +321,11 @@ class Engine {
     return d;
   }
 
+  void set_binds_enabled(bool on) {
+    binds_enabled_ = on;
+    if (srv_) srv_->set_binds_enabled(on);
+  }
+
   py::list drain_bind_failures() {
     py::list out;
     if (!srv_) return out;
@@ -352,6 +358,7 @@ class Engine {
  private:
   Ledger l_;
   std::unique_ptr<NativeServer> srv_;  // declared after l_: destroyed (stopped) first
+  bool binds_enabled_ = true;
 };
 
 }  // namespace
@@ -415,6 +422,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("stop_server", &Engine::stop_server)
       .def("server_stats", &Engine::server_stats)
       .def("drain_bind_failures", &Engine::drain_bind_failures)
+      .def("set_binds_enabled", &Engine::set_binds_enabled)
       .def("pending_count", &Engine::pending_count);
 
   m.def("parse_quantity", [](const std::string& s) {

@@ -508,6 +508,9 @@ std::string NativeServer::do_proxy(const http::Message& req) {
 // metadata.annotations carry the allocation record (pkg/utils/pod.go:192-206).
 std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
   *fallback = false;
+  if (!binds_enabled_.load()) {
+    return bind_error_response("this extender replica is not the leader");
+  }
   if (!cfg_.native_bind || !api_) {
     *fallback = true;
     return {};

@@ -84,6 +84,9 @@ class NativeServer {
   int port() const { return port_; }
   const ServerStats& stats() const { return stats_; }
   std::vector<BindFailure> drain_failures();
+  // HA standby: a replica that does not hold the leader Lease refuses binds.
+  void set_binds_enabled(bool on) { binds_enabled_.store(on); }
+  bool binds_enabled() const { return binds_enabled_.load(); }
 
  private:
   struct Loop;
@@ -116,6 +119,7 @@ class NativeServer {
   ServerConfig cfg_;
   int port_ = -1;
   std::atomic<bool> stop_{false};
+  std::atomic<bool> binds_enabled_{true};
   std::vector<std::unique_ptr<Loop>> loops_;
   std::vector<std::thread> loop_threads_;
   std::vector<std::thread> pool_threads_;

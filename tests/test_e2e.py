@@ -288,3 +288,43 @@ def test_prioritize_packs_nodes_before_spreading():
             st, body = await c.post("/gpushare-scheduler/prioritize", wire.filter_args(make_pod("q", 10), ["n1", "n2", "n3"]))
             assert st == 200 and len(json.loads(body)) == 3
     run(go())
+
+
+def test_leader_election_failover():
+    """HA (reference roadmap): two hot replicas, only the Lease holder binds; the standby takes over on loss."""
+    async def go():
+        async with Cluster() as c:
+            await c.client.create("nodes", make_node("n", 100, 1))
+            kw = dict(leader_elect=True, lease_namespace="default", lease_duration=0.6, renew_deadline=0.4,
+                      retry_period=0.05)
+            a = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, **kw),
+                                     native=NATIVE["on"]).start()
+            await asyncio.sleep(0.2)
+            b = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, **kw),
+                                     native=NATIVE["on"]).start()
+            try:
+                await c.settle(lambda: a.server.is_leader, 3)
+                await asyncio.sleep(0.3)
+                assert not b.server.is_leader
+                async with c.http.get(b.url + "/healthz") as r:
+                    assert r.status == 503 and "standby" in await r.text()
+                p = await c.client.create("pods", make_pod("x", 10))
+                args = wire.ExtenderBindingArgs("x", "default", p["metadata"]["uid"], "n").encode()
+                await c.settle(lambda: b.server.controller.pods.get("default/x") is not None)
+                async with c.http.post(b.url + "/gpushare-scheduler/bind", data=args) as r:
+                    assert r.status == 500 and "not the leader" in json.loads(await r.read())["Error"]
+                # the leader goes away (Lease released on stop); the standby takes over and binds
+                await a.stop()
+                await a.server.client.close()
+                await c.settle(lambda: b.server.is_leader, 5)
+                async with c.http.get(b.url + "/healthz") as r:
+                    assert r.status == 200
+                async with c.http.post(b.url + "/gpushare-scheduler/bind", data=args) as r:
+                    assert r.status == 200, await r.read()
+                lease = await c.client.get("leases", "gpushare-schd-extender", "default")
+                assert lease["spec"]["holderIdentity"] == b.server.elector.identity
+                assert lease["spec"]["leaseTransitions"] >= 1
+            finally:
+                await b.stop()
+                await b.server.client.close()
+    run(go())
