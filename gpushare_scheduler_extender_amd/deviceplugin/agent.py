@@ -23,7 +23,7 @@ from ..k8s.client import ApiError, KubeClient
 from ..k8s.informer import Handler, Informer, obj_key
 from ..models import pod as podutil
 from ..models.profile import NamingProfile
-from .allocator import CU_COUNT_ANNOTATION, CUPartitioner, assigned_patch, build_response, pick_pod
+from .allocator import CU_COUNT_ANNOTATION, CUPartitioner, assigned_patch, build_response
 from .devices import UNITS, Device
 from .runtime import AdmissionError, admit_local
 
@@ -56,6 +56,9 @@ class NodeAgent:
         self.queue: asyncio.Queue = asyncio.Queue()
         self.queued: set[str] = set()
         self.seen: dict[str, float] = {}
+        # Allocate candidates (pending, ASSIGNED=false, one of our GPUs): uid -> (assume_time, key, units);
+        # kept incrementally so an Allocate is O(candidates) instead of a scan + sort of every pod on the node
+        self._cands: dict[str, tuple[int, str, int]] = {}
         self.workers = workers
         self.pods.add_handler(Handler(self._on_pod, lambda o, n, r: self._on_pod(n, r), self._on_delete))
 
@@ -65,11 +68,18 @@ class NodeAgent:
     def _on_pod(self, pod: dict, raw):
         uid = podutil.meta(pod).get("uid", "")
         if podutil.is_complete(pod):
+            self._cands.pop(uid, None)
             self._stop(uid)
             return
         if not podutil.is_gpushare_pod(pod, self.profile) or not self._mine(pod):
+            self._cands.pop(uid, None)
             return
         ann = podutil.annotations(pod)
+        if ann.get(self.profile.annotation_assigned) == "false" and podutil.phase(pod) in ("Pending", ""):
+            self._cands[uid] = (podutil.assume_time(pod, self.profile), obj_key(pod),
+                                podutil.gpu_mem_request(pod, self.profile))
+        else:
+            self._cands.pop(uid, None)
         if (ann.get(self.profile.annotation_assigned) == "false" and uid not in self.inflight
                 and uid not in self.running and uid not in self.queued):
             self.queued.add(uid)
@@ -77,7 +87,9 @@ class NodeAgent:
             self.queue.put_nowait(obj_key(pod))
 
     def _on_delete(self, pod: dict, raw):
-        self._stop(podutil.meta(pod).get("uid", ""))
+        uid = podutil.meta(pod).get("uid", "")
+        self._cands.pop(uid, None)
+        self._stop(uid)
 
     def _stop(self, uid: str):
         if uid in self.running:
@@ -120,10 +132,12 @@ class NodeAgent:
             units = podutil.gpu_mem_request(pod, self.profile)
             # kubelet's Allocate(N ids): pick the pod exactly as the device plugin does —
             # earliest ASSUME_TIME among unassigned pods of that size (not yet claimed here)
-            busy = self.inflight | set(self.running)
-            chosen = pick_pod([p for p in self.pods.list()
-                               if podutil.meta(p).get("uid") not in busy and self._mine(p)],
-                              self.node, units, self.profile)
+            best = None
+            for cu, (at, ck, cu_units) in self._cands.items():
+                if cu_units == units and cu not in self.inflight and cu not in self.running:
+                    if best is None or (at, ck) < best[0]:
+                        best = ((at, ck), cu)
+            chosen = self.pods.get(best[0][1]) if best is not None else None
             if chosen is None:
                 return
             cuid = podutil.meta(chosen).get("uid", "")

@@ -178,6 +178,7 @@ class FakeApiServer:
         self.faults = Faults()
         self.counts = collections.Counter()
         self._grace_tasks: set[asyncio.Task] = set()
+        self._last: tuple | None = None
         self.app = self._make_app()
 
     # ------------------------------------------------------------ state
@@ -187,7 +188,9 @@ class FakeApiServer:
 
     def _emit(self, kind: str, etype: str, obj: dict):
         rv = int(obj["metadata"]["resourceVersion"])
-        line = json.dumps({"type": etype, "object": obj}, separators=(",", ":")).encode() + b"\n"
+        ob = json.dumps(obj, separators=(",", ":")).encode()
+        line = b'{"type":"' + etype.encode() + b'","object":' + ob + b"}\n"
+        self._last = (obj, ob)  # the write's HTTP response reuses this serialisation
         if len(self.history) == self.history.maxlen:
             self.oldest_rv = self.history[0][0]
         self.history.append((rv, kind, etype, line, obj))
@@ -420,8 +423,10 @@ class FakeApiServer:
             return handler(request)
         return h
 
-    @staticmethod
-    def _json(obj, status=200) -> Response:
+    def _json(self, obj, status=200) -> Response:
+        last = self._last
+        if last is not None and last[0] is obj:
+            return Response(last[1], status)
         return Response(json.dumps(obj, separators=(",", ":")).encode(), status)
 
     def h_version(self, request):
