@@ -238,3 +238,26 @@ def hbm_admit(stream: Stream, slices: list[tuple[int, int, int]], stamp_idx: int
     bad = ctypes.c_uint64(0)
     _ck(L.gsx_hbm_admit(stream.handle, arr, len(slices), stamp_idx, stride, ctypes.byref(bad)), "hbm_admit")
     return bad.value
+
+
+GEMM_CFGS = {0: "128x128/4w", 1: "256x128/8w", 2: "128x256/8w", 3: "256x256/8w", 4: "128x128/4w-nogroup"}
+
+
+def gemm_bf16_nt_cfg(stream: Stream, a: int, b: int, c: int, m: int, n: int, k: int, cfg: int):
+    """Launch one tile configuration of the templated GEMM (native/kernels/gemm.hip)."""
+    L = lib()
+    if not getattr(L, "_cfg_sig", False):
+        L.gsx_gemm_bf16_nt_launch_cfg.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 4
+        L.gsx_gemm_bf16_nt_launch_cfg.restype = ctypes.c_int
+        L.gsx_gemm_cfg_tile.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+        L.gsx_gemm_cfg_tile.restype = ctypes.c_int
+        L._cfg_sig = True
+    bm, bn = ctypes.c_int(0), ctypes.c_int(0)
+    if L.gsx_gemm_cfg_tile(cfg, ctypes.byref(bm), ctypes.byref(bn)) != 0:
+        raise HipError(f"unknown GEMM config {cfg}")
+    if m % bm.value or n % bn.value or k % 64:
+        raise HipError(f"GEMM config {cfg} needs M%{bm.value}==0, N%{bn.value}==0, K%64==0")
+    rc = L.gsx_gemm_bf16_nt_launch_cfg(stream.handle, ctypes.c_void_p(a), ctypes.c_void_p(b), ctypes.c_void_p(c),
+                                       m, n, k, cfg)
+    if rc != 0:
+        raise HipError(f"gemm cfg {cfg}: hip error {rc}")

@@ -1,0 +1,192 @@
+// bf16 MFMA GEMM family for the pod workload: C[M][N] = A[M][K] * B[N][K]^T (bf16 in/out, fp32 accumulate).
+//
+// One template, several tile shapes (BM x BN with WM x WN waves, BK = 64),
+// selected at launch.  Structure per K-tile (see gsx_kernels.hip for the
+// 128x128 original and the reasoning):
+//   * global -> LDS with global_load_lds (16 B/lane), lane-linear LDS image,
+//     XOR swizzle folded into the per-lane *global* source address;
+//   * two LDS buffers: tile k+1 in flight while the MFMAs consume tile k;
+//     one barrier per K-tile;
+//   * v_mfma_f32_16x16x32_bf16, each wave owns a (BM/WM) x (BN/WN) C tile;
+//   * s_setprio around the MFMA burst so the partner wave's loads issue;
+//   * grouped, XCD-aware tile order (GROUP_M tile-rows per group; workgroup
+//     ids remapped bijectively so one XCD's blocks share A/B panels in L2);
+//   * epilogue through LDS: 16-B coalesced row stores.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace gsxgemm {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef const void __attribute__((address_space(1)))* gptr_t;
+typedef void __attribute__((address_space(3)))* lptr_t;
+
+constexpr int BK = 64;
+
+__device__ __forceinline__ uint32_t swz(int row, int chunk) {
+  return static_cast<uint32_t>(row * (BK * 2) + ((chunk ^ ((row >> 1) & 7)) << 4));
+}
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return static_cast<uint16_t>((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<uint16_t>(u >> 16);
+}
+
+template <int BM, int BN, int WM, int WN, int GROUP_M>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(const uint16_t* __restrict__ A,
+                                                           const uint16_t* __restrict__ B,
+                                                           uint16_t* __restrict__ C, int M, int N, int K) {
+  constexpr int NW = WM * WN;
+  constexpr int TA = BM * BK * 2, TB = BN * BK * 2;  // bytes per operand tile
+  constexpr int MR = BM / WM / 16, NR = BN / WN / 16;
+  constexpr int RA = TA / 1024 / NW, RB = TB / 1024 / NW;  // glds rounds per wave (1 KiB each)
+  static_assert(RA >= 1 && RB >= 1 && TA % (1024 * NW) == 0 && TB % (1024 * NW) == 0, "tile/wave mismatch");
+  constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
+  static_assert(NW * WTM * WTN * 2 <= 2 * (TA + TB), "epilogue staging must fit in LDS");
+  extern __shared__ __attribute__((aligned(16))) char lds[];  // [buf][A|B], reused by the epilogue
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+
+  // XCD-aware bijective remap, then grouped tile order
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int ntm = M / BM, ntn = N / BN;
+  const int per_group = GROUP_M * ntn;
+  const int g = wg / per_group;
+  const int first_m = g * GROUP_M;
+  const int gm = (ntm - first_m) < GROUP_M ? (ntm - first_m) : GROUP_M;
+  const int tm = first_m + (wg % per_group) % gm;
+  const int tn = (wg % per_group) / gm;
+  const int row0 = tm * BM, col0 = tn * BN;
+
+  int offA[RA], offB[RB];
+#pragma unroll
+  for (int i = 0; i < RA; ++i) {
+    const int p = (i * NW + wid) * 64 + lane;
+    const int rr = p >> 3, slot = p & 7;
+    offA[i] = rr * K + ((slot ^ ((rr >> 1) & 7)) * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < RB; ++i) {
+    const int p = (i * NW + wid) * 64 + lane;
+    const int rr = p >> 3, slot = p & 7;
+    offB[i] = rr * K + ((slot ^ ((rr >> 1) & 7)) * 8);
+  }
+  const uint16_t* Ab = A + static_cast<size_t>(row0) * K;
+  const uint16_t* Bb = B + static_cast<size_t>(col0) * K;
+
+  auto stage = [&](int kt, int buf) {
+    char* la = lds + buf * (TA + TB);
+    char* lb = la + TA;
+#pragma unroll
+    for (int i = 0; i < RA; ++i)
+      __builtin_amdgcn_global_load_lds((gptr_t)(Ab + offA[i] + kt * BK), (lptr_t)(la + (i * NW + wid) * 1024), 16,
+                                       0, 0);
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+      __builtin_amdgcn_global_load_lds((gptr_t)(Bb + offB[i] + kt * BK), (lptr_t)(lb + (i * NW + wid) * 1024), 16,
+                                       0, 0);
+  };
+
+  f32x4 acc[MR][NR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int n = 0; n < NR; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  stage(0, 0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
+    const char* la = lds + buf * (TA + TB);
+    const char* lb = la + TA;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int ch = kk * 4 + fq;
+      bf16x8 bfr[NR];
+#pragma unroll
+      for (int n = 0; n < NR; ++n) bfr[n] = *reinterpret_cast<const bf16x8*>(lb + swz(wc * WTN + n * 16 + fr, ch));
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(la + swz(wr * WTM + m * 16 + fr, ch));
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int n = 0; n < NR; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[n], acc[m][n], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    __syncthreads();
+  }
+  // epilogue through LDS (wave-private region): bf16 tile, then 16-B row stores
+  uint16_t* ct = reinterpret_cast<uint16_t*>(lds + wid * (WTM * WTN * 2));
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int n = 0; n < NR; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ct[(m * 16 + fq * 4 + j) * WTN + n * 16 + fr] = f2bf(acc[m][n][j]);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  constexpr int LPR = WTN / 8;   // lanes per row (16 B each)
+  constexpr int RPI = 64 / LPR;  // rows per store instruction
+#pragma unroll
+  for (int i = 0; i < WTM / RPI; ++i) {
+    const int rr = i * RPI + lane / LPR, cc = (lane % LPR) * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(ct + rr * WTN + cc);
+    *reinterpret_cast<uint4*>(C + static_cast<size_t>(row0 + wr * WTM + rr) * N + col0 + wc * WTN + cc) = v;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int GM>
+hipError_t launch(hipStream_t s, const void* A, const void* B, void* C, int M, int N, int K) {
+  constexpr int lds = 2 * (BM + BN) * BK * 2;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_kernel<BM, BN, WM, WN, GM>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int tiles = (M / BM) * (N / BN);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, GM>), dim3(tiles), dim3(WM * WN * 64), lds, s,
+                     static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
+                     N, K);
+  return hipGetLastError();
+}
+
+}  // namespace gsxgemm
+
+// Tile configurations (index -> BM x BN, waves).  Exposed for benchmarking.
+extern "C" int gsx_gemm_cfg_tile(int cfg, int* bm, int* bn) {
+  static const int t[][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}, {128, 128}};
+  if (cfg < 0 || cfg > 4) return -1;
+  *bm = t[cfg][0];
+  *bn = t[cfg][1];
+  return 0;
+}
+
+extern "C" int gsx_gemm_bf16_nt_launch_cfg(void* stream, const void* A, const void* B, void* C, int M, int N, int K,
+                                           int cfg) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (cfg) {
+    case 0: return static_cast<int>(gsxgemm::launch<128, 128, 2, 2, 8>(s, A, B, C, M, N, K));
+    case 1: return static_cast<int>(gsxgemm::launch<256, 128, 4, 2, 4>(s, A, B, C, M, N, K));
+    case 2: return static_cast<int>(gsxgemm::launch<128, 256, 2, 4, 8>(s, A, B, C, M, N, K));
+    case 3: return static_cast<int>(gsxgemm::launch<256, 256, 2, 4, 4>(s, A, B, C, M, N, K));
+    case 4: return static_cast<int>(gsxgemm::launch<128, 128, 2, 2, 1>(s, A, B, C, M, N, K));
+    default: return static_cast<int>(hipErrorInvalidValue);
+  }
+}

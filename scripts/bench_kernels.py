@@ -35,8 +35,28 @@ def gemm(size_list, iters=20):
         tms = e0.elapsed_time(e1) / iters
         ref = 2 * m * n * k / tms / 1e9
         err = (c.float() - (a.float() @ b.float().t())).abs().max().item()
-        out.append({"m": m, "n": n, "k": k, "gsx_tflops": round(ours, 1), "torch_tflops": round(ref, 1),
-                    "gsx_ms": round(ms, 4), "max_abs_err": round(err, 4)})
+        row = {"m": m, "n": n, "k": k, "gsx_tflops": round(ours, 1), "torch_tflops": round(ref, 1),
+               "gsx_ms": round(ms, 4), "max_abs_err": round(err, 4)}
+        ts = torch.cuda.ExternalStream(s.ptr)
+        for cfg, name in hip.GEMM_CFGS.items():
+            try:
+                hip.gemm_bf16_nt_cfg(s, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, cfg)
+            except hip.HipError:
+                continue
+            s.sync()
+            e = (c.float() - (a.float() @ b.float().t())).abs().max().item()
+            torch.cuda.synchronize()
+            with torch.cuda.stream(ts):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(ts)
+                for _ in range(iters):
+                    hip.gemm_bf16_nt_cfg(s, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, cfg)
+                e1.record(ts)
+            e1.synchronize()
+            cms = e0.elapsed_time(e1) / iters
+            row[f"cfg{cfg}_{name}_tflops"] = round(2 * m * n * k / cms / 1e9, 1)
+            row[f"cfg{cfg}_err"] = round(e, 4)
+        out.append(row)
         del a, b, c
     s.destroy()
     return out

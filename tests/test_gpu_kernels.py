@@ -179,3 +179,25 @@ def test_arena_runtime_admits_four_64gib_pods():
         assert rt.verify() == 0
     finally:
         rt.close()
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+def test_gemm_tile_configs_match_fp32_reference(hip, cfg):
+    m, n, k = 512, 512, 256
+    torch.manual_seed(cfg)
+    a = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(n, k, device="cuda", dtype=torch.bfloat16)
+    c = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+    s = hip.Stream(0)
+    torch.cuda.synchronize()
+    hip.gemm_bf16_nt_cfg(s, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, cfg)
+    s.sync()
+    torch.testing.assert_close(c.float(), a.float() @ b.float().t(), atol=0.05 * (k ** 0.5), rtol=1e-2)
+    # asymmetric identity check: C = I * B^T must be exact
+    eye = torch.eye(m, k, device="cuda", dtype=torch.bfloat16)
+    bb = (torch.arange(n * k, device="cuda", dtype=torch.float32).reshape(n, k) % 61).to(torch.bfloat16)
+    torch.cuda.synchronize()
+    hip.gemm_bf16_nt_cfg(s, eye.data_ptr(), bb.data_ptr(), c.data_ptr(), m, n, k, cfg)
+    s.sync()
+    torch.testing.assert_close(c.float()[:, :], (eye.float() @ bb.float().t()), atol=0, rtol=0)
+    s.destroy()
