@@ -79,7 +79,8 @@ int gsx_hbm_admit(void* stream, const gsx_slice* slices, int n, int stamp_idx, u
 int gsx_hbm_fill(void* stream, void* base, uint64_t bytes, uint32_t pattern);
 
 // C[M][N] (bf16) = A[M][K] (bf16, row-major) * B[N][K]^T (bf16, row-major).
-// Requires M % 128 == 0, N % 128 == 0, K % 64 == 0.
+// Requires M % 128 == 0, N % 128 == 0, K % 64 == 0.  Dispatches to the best
+// tile of the templated family in gemm.hip (256x256 when M, N % 256 == 0).
 int gsx_gemm_bf16_nt(void* stream, const void* A, const void* B, void* C, int M, int N, int K);
 
 // elapsed milliseconds of running `fn` on stream via hip events (for benches)

@@ -10,6 +10,9 @@
 
 #include "gsx_kernels.h"
 
+extern "C" int gsx_gemm_bf16_nt_launch_cfg(void* stream, const void* A, const void* B, void* C, int M, int N, int K,
+                                           int cfg);
+
 namespace {
 
 thread_local std::string g_err;
@@ -108,138 +111,9 @@ __global__ __launch_bounds__(256) void fill_kernel(uint4* p, uint64_t n16, uint3
   for (; i < n16; i += step) p[i] = v;
 }
 
-// ------------------------------------------------------------------ bf16 MFMA GEMM (C = A * B^T)
-//
-// 128x128x64 tile, 256 threads = 4 waves in 2x2, each wave 64x64 of C as a
-// 4x4 grid of v_mfma_f32_16x16x32_bf16 tiles (K = 32 per MFMA, 2 per K-tile).
-//
-// Staging: global -> LDS with global_load_lds (16 B per lane, no VGPR round
-// trip).  The LDS image of a 128x64 bf16 operand tile is lane-linear per wave
-// instruction (the instruction writes wave-uniform base + lane*16), so the XOR
-// swizzle is applied on the *global source* address: linear LDS slot s of row r
-// holds logical 16-B chunk s ^ ((r >> 1) & 7).  A ds_read_b128 lane group then
-// touches 16 rows spread over all sixteen 16-B slots of two 256-B bank rows.
-// Two LDS buffers: tile k+1 is in flight while the MFMAs consume tile k; one
-// barrier per K-tile (its implicit vmcnt(0) retires the prefetch).
-//
-// Epilogue: accumulators -> bf16 -> LDS (per-wave 64x64 tile) -> 16-B coalesced
-// row stores, instead of 2-byte scattered stores from the MFMA C layout.
-// Workgroup ids are remapped so neighbouring output tiles share an XCD's L2
-// (bijective for any grid size).
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int TILE_BYTES = BM * BK * 2;  // 16 KiB per operand per buffer
-
-__device__ __forceinline__ uint32_t swz(int row, int chunk) {
-  return static_cast<uint32_t>(row * (BK * 2) + ((chunk ^ ((row >> 1) & 7)) << 4));
-}
-
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return static_cast<uint16_t>((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<uint16_t>(u >> 16);
-}
-
-typedef const void __attribute__((address_space(1)))* gptr_t;
-typedef void __attribute__((address_space(3)))* lptr_t;
-
-__global__ __launch_bounds__(256, 2) void gemm_bf16_nt_kernel(const uint16_t* __restrict__ A,
-                                                              const uint16_t* __restrict__ B,
-                                                              uint16_t* __restrict__ C, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char lds[4 * TILE_BYTES];  // [buf][A|B], reused by the epilogue
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-
-  // XCD-aware bijective remap of the workgroup id
-  const int nwg = gridDim.x;
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7;
-  const int q = nwg >> 3, r = nwg & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-  const int ntn = N / BN;
-  const int tm = wg / ntn, tn = wg % ntn;
-  const int row0 = tm * BM, col0 = tn * BN;
-
-  // per-lane global source offsets (elements) of this wave's 4 glds rounds, swizzle folded in
-  int src_off[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int p = (i * 4 + wid) * 64 + lane;  // linear 16-B slot index in the 16 KiB tile
-    const int rr = p >> 3, slot = p & 7;
-    const int chunk = slot ^ ((rr >> 1) & 7);
-    src_off[i] = rr * K + chunk * 8;
-  }
-  const uint16_t* Ab = A + static_cast<size_t>(row0) * K;
-  const uint16_t* Bb = B + static_cast<size_t>(col0) * K;
-
-  auto stage = [&](int kt, int buf) {
-    char* la = lds + buf * 2 * TILE_BYTES;
-    char* lb = la + TILE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int wofs = (i * 4 + wid) * 1024;  // wave-uniform LDS base of this round
-      __builtin_amdgcn_global_load_lds((gptr_t)(Ab + src_off[i] + kt * BK),
-                                       (lptr_t)(la + wofs), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gptr_t)(Bb + src_off[i] + kt * BK),
-                                       (lptr_t)(lb + wofs), 16, 0, 0);
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BK;
-  stage(0, 0);
-  __syncthreads();
-  const int fr = lane & 15, fq = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
-    const char* la = lds + buf * 2 * TILE_BYTES;
-    const char* lb = la + TILE_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 af[4], bfr[4];
-      const int ch = kk * 4 + fq;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) af[m] = *reinterpret_cast<const bf16x8*>(la + swz(wr * 64 + m * 16 + fr, ch));
-#pragma unroll
-      for (int n = 0; n < 4; ++n) bfr[n] = *reinterpret_cast<const bf16x8*>(lb + swz(wc * 64 + n * 16 + fr, ch));
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
-    }
-    __syncthreads();
-  }
-  // epilogue through LDS: wave tile 64x64 bf16 = 8 KiB at lds + wid * 8 KiB (row stride 128 B)
-  // C/D map of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + j
-  uint16_t* ct = reinterpret_cast<uint16_t*>(lds + wid * 8192);
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ct[(m * 16 + fq * 4 + j) * 64 + n * 16 + fr] = f2bf(acc[m][n][j]);
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed (wave-private region)
-  __builtin_amdgcn_wave_barrier();
-  // 64 rows x 128 B: each lane stores 16 B; 8 lanes per row, 8 rows per instruction, 8 instructions
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int rr = i * 8 + (lane >> 3), cc = (lane & 7) * 8;
-    const uint4 v = *reinterpret_cast<const uint4*>(ct + rr * 64 + cc);
-    *reinterpret_cast<uint4*>(C + static_cast<size_t>(row0 + wr * 64 + rr) * N + col0 + wc * 64 + cc) = v;
-  }
-}
+// ------------------------------------------------------------------ bf16 MFMA GEMM
+// The kernels live in gemm.hip (templated tile family); gsx_gemm_bf16_nt
+// picks the measured-best tile for the shape (profiles/r01_kernels.json).
 
 std::mutex g_mu;
 unsigned long long* g_counter[64] = {nullptr};
@@ -446,14 +320,14 @@ int gsx_hbm_fill(void* stream, void* base, uint64_t bytes, uint32_t pattern) {
 }
 
 int gsx_gemm_bf16_nt(void* stream, const void* A, const void* B, void* C, int M, int N, int K) {
-  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK)
+  if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % 64)
     return fail_arg("gsx_gemm_bf16_nt: need M%128==0, N%128==0, K%64==0");
-  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) % 16)
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) | reinterpret_cast<uintptr_t>(C)) % 16)
     return fail_arg("gsx_gemm_bf16_nt: operands must be 16-B aligned");
-  int tiles = (M / BM) * (N / BN);
-  hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3(tiles), dim3(256), 0, S(stream), static_cast<const uint16_t*>(A),
-                     static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M, N, K);
-  GSX_CHECK(hipGetLastError());
+  // 256x256 / 8 waves: 1.09-1.22 PFLOP/s on MI355X at 4k-16k; 128x128 grouped otherwise
+  const int cfg = (M % 256 == 0 && N % 256 == 0) ? 3 : 0;
+  int rc = gsx_gemm_bf16_nt_launch_cfg(stream, A, B, C, M, N, K, cfg);
+  if (rc != 0) return fail(static_cast<hipError_t>(rc), "gemm launch");
   return 0;
 }
 
