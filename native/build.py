@@ -170,7 +170,7 @@ TARGETS = {
     "asan": build_asan,
     "tsan": build_tsan,
 }
-DEFAULT = ["engine", "mxdev", "kernels"]
+DEFAULT = ["engine", "mxdev", "kernels", "tools"]
 
 
 def main(argv: list[str] | None = None) -> int:
