@@ -150,6 +150,209 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_kernel(const uint16_t* __re
   }
 }
 
+// ---------------------------------------------------------------------------
+// Phased 256x256 kernel: the prefetch stays in flight across barriers.
+//
+// The kernel above ends every K-tile with __syncthreads(), which hipcc lowers
+// to `s_waitcnt vmcnt(0); s_barrier`: the next tile's loads are drained every
+// 64 K, and at one 512-thread block per CU nothing hides that.  Here a K-tile
+// is four phases; each phase MFMAs one quadrant of the wave's 128x64 C tile
+// (16 MFMAs) and issues one *half-tile* (16 KiB: 128 rows x 64 k of A or B)
+// two K-tiles ahead.  Waits are counted (`vmcnt(8)` = four half-tiles may stay
+// in flight), barriers are raw s_barrier, and the two wave groups (wr = 0/1,
+// one of each per SIMD) run one barrier apart so that one wave's ds_reads
+// overlap the other's MFMAs.
+//
+// Half-tiles (LDS regions of 16 KiB, [buffer = tile & 1][half]):
+//   0: A rows {0-63, 128-191}  1: A rows {64-127, 192-255}   (m-half of each wave row)
+//   2: B cols {wc*64 + 0..31}  3: B cols {wc*64 + 32..63}     (n-half of each wave col)
+// Per K-tile phases (reads -> MFMA quadrant, and what is staged):
+//   p0: read A0,B2 -> (m0,n0)   stage tile t+1 half 3
+//   p1: read B3    -> (m0,n1)   stage tile t+1 half 1
+//   p2: read A1    -> (m1,n1)   stage tile t+2 half 0
+//   p3: -          -> (m1,n0)   stage tile t+2 half 2
+// Every half is restaged >= 2 phases after its last read (WAR across the
+// staggered groups) and waited for (vmcnt(8) before the first barrier of the
+// phase) one phase before it is read (RAW).  Tiles past the end are clamped to
+// the last tile so the counts stay uniform; those loads land in dead buffers.
+// ---------------------------------------------------------------------------
+constexpr int PH_HALF = 128 * BK * 2;  // 16 KiB
+
+__device__ __forceinline__ void ph_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int GROUP_M>
+__global__ __launch_bounds__(512) void gemm_phased_kernel(const uint16_t* __restrict__ A,
+                                                         const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
+                                                         int M, int N, int K) {
+  constexpr int BM = 256, BN = 256, WTM = 128, WTN = 64;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int ntm = M / BM, ntn = N / BN;
+  const int per_group = GROUP_M * ntn;
+  const int g = wg / per_group;
+  const int first_m = g * GROUP_M;
+  const int gm = (ntm - first_m) < GROUP_M ? (ntm - first_m) : GROUP_M;
+  const int tm = first_m + (wg % per_group) % gm;
+  const int tn = (wg % per_group) / gm;
+  const uint16_t* Ab = A + static_cast<size_t>(tm * BM) * K;
+  const uint16_t* Bb = B + static_cast<size_t>(tn * BN) * K;
+
+  // per-lane source offsets of the two 8-KiB rounds of each half
+  int off[4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = (i * 8 + wid) * 64 + lane;
+    const int lr = p >> 3, slot = p & 7;
+    const int sw = (slot ^ ((lr >> 1) & 7)) * 8;
+    off[0][i] = ((lr >> 6) * 128 + (lr & 63)) * K + sw;
+    off[1][i] = ((lr >> 6) * 128 + 64 + (lr & 63)) * K + sw;
+    off[2][i] = ((lr >> 5) * 64 + (lr & 31)) * K + sw;
+    off[3][i] = ((lr >> 5) * 64 + 32 + (lr & 31)) * K + sw;
+  }
+  const int nk = K / BK;
+  auto stage = [&](int tile, int half) {
+    const int kt = tile < nk ? tile : nk - 1;
+    const uint16_t* src = (half < 2 ? Ab : Bb) + kt * BK;
+    char* dst = lds + ((tile & 1) * 4 + half) * PH_HALF + wid * 1024;
+    __builtin_amdgcn_global_load_lds((gptr_t)(src + off[half][0]), (lptr_t)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gptr_t)(src + off[half][1]), (lptr_t)(dst + 8 * 1024), 16, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 af[4][2], bf[2][2][2];  // A: [m][kk]; B: [nh][n][kk]
+
+  auto read_a = [&](const char* base, int mh) {
+    const char* h = base + mh * PH_HALF;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        af[m][kk] = *reinterpret_cast<const bf16x8*>(h + swz(wr * 64 + m * 16 + fr, kk * 4 + fq));
+  };
+  auto read_b = [&](const char* base, int nh) {
+    const char* h = base + (2 + nh) * PH_HALF;
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bf[nh][n][kk] = *reinterpret_cast<const bf16x8*>(h + swz(wc * 32 + n * 16 + fr, kk * 4 + fq));
+  };
+  auto mma = [&](int mh, int nh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[mh * 4 + m][nh * 2 + n] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], bf[nh][n][kk], acc[mh * 4 + m][nh * 2 + n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: what the steady state has issued before tile 0, phase 0
+  stage(0, 0);
+  stage(0, 2);
+  stage(0, 3);
+  stage(0, 1);
+  stage(1, 0);
+  stage(1, 2);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  ph_barrier();
+  if (wr == 1) ph_barrier();  // stagger the groups by one barrier
+
+  for (int t = 0; t < nk; ++t) {
+    const char* base = lds + (t & 1) * 4 * PH_HALF;
+    // p0
+    read_a(base, 0);
+    read_b(base, 0);
+    stage(t + 1, 3);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    ph_barrier();
+    mma(0, 0);
+    ph_barrier();
+    // p1
+    read_b(base, 1);
+    stage(t + 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    ph_barrier();
+    mma(0, 1);
+    ph_barrier();
+    // p2
+    read_a(base, 1);
+    stage(t + 2, 0);
+    ph_barrier();
+    mma(1, 1);
+    ph_barrier();
+    // p3
+    stage(t + 2, 2);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    ph_barrier();
+    mma(1, 0);
+    ph_barrier();
+  }
+  if (wr == 0) ph_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ph_barrier();
+
+  uint16_t* ct = reinterpret_cast<uint16_t*>(lds + wid * (WTM * WTN * 2));
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ct[(m * 16 + fq * 4 + j) * WTN + n * 16 + fr] = f2bf(acc[m][n][j]);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  constexpr int LPR = WTN / 8, RPI = 64 / LPR;
+  const int row0 = tm * BM + wr * WTM, col0 = tn * BN + wc * WTN;
+#pragma unroll
+  for (int i = 0; i < WTM / RPI; ++i) {
+    const int rr = i * RPI + lane / LPR, cc = (lane % LPR) * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(ct + rr * WTN + cc);
+    *reinterpret_cast<uint4*>(C + static_cast<size_t>(row0 + rr) * N + col0 + cc) = v;
+  }
+}
+
+template <int GM>
+hipError_t launch_phased(hipStream_t s, const void* A, const void* B, void* C, int M, int N, int K) {
+  constexpr int lds = 8 * PH_HALF;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_phased_kernel<GM>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  if (M % 256 || N % 256 || K % BK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_phased_kernel<GM>), dim3((M / 256) * (N / 256)), dim3(512), lds, s,
+                     static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
+                     N, K);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int WM, int WN, int GM>
 hipError_t launch(hipStream_t s, const void* A, const void* B, void* C, int M, int N, int K) {
   constexpr int lds = 2 * (BM + BN) * BK * 2;
@@ -171,8 +374,8 @@ hipError_t launch(hipStream_t s, const void* A, const void* B, void* C, int M, i
 
 // Tile configurations (index -> BM x BN, waves).  Exposed for benchmarking.
 extern "C" int gsx_gemm_cfg_tile(int cfg, int* bm, int* bn) {
-  static const int t[][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}, {128, 128}};
-  if (cfg < 0 || cfg > 4) return -1;
+  static const int t[][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}, {128, 128}, {256, 256}, {256, 256}};
+  if (cfg < 0 || cfg > 6) return -1;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
   return 0;
@@ -187,6 +390,8 @@ extern "C" int gsx_gemm_bf16_nt_launch_cfg(void* stream, const void* A, const vo
     case 2: return static_cast<int>(gsxgemm::launch<128, 256, 2, 4, 8>(s, A, B, C, M, N, K));
     case 3: return static_cast<int>(gsxgemm::launch<256, 256, 2, 4, 4>(s, A, B, C, M, N, K));
     case 4: return static_cast<int>(gsxgemm::launch<128, 128, 2, 2, 1>(s, A, B, C, M, N, K));
+    case 5: return static_cast<int>(gsxgemm::launch_phased<4>(s, A, B, C, M, N, K));
+    case 6: return static_cast<int>(gsxgemm::launch_phased<8>(s, A, B, C, M, N, K));
     default: return static_cast<int>(hipErrorInvalidValue);
   }
 }

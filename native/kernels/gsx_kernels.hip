@@ -324,8 +324,9 @@ int gsx_gemm_bf16_nt(void* stream, const void* A, const void* B, void* C, int M,
     return fail_arg("gsx_gemm_bf16_nt: need M%128==0, N%128==0, K%64==0");
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B) | reinterpret_cast<uintptr_t>(C)) % 16)
     return fail_arg("gsx_gemm_bf16_nt: operands must be 16-B aligned");
-  // 256x256 / 8 waves: 1.09-1.22 PFLOP/s on MI355X at 4k-16k; 128x128 grouped otherwise
-  const int cfg = (M % 256 == 0 && N % 256 == 0) ? 3 : 0;
+  // phased 256x256 / 8 waves (prefetch in flight across barriers): 1.39-1.46 PFLOP/s on MI355X at
+  // 4k-16k (the __syncthreads 256x256 tile: 1.12-1.21); 128x128 grouped otherwise
+  const int cfg = (M % 256 == 0 && N % 256 == 0) ? 5 : 0;
   int rc = gsx_gemm_bf16_nt_launch_cfg(stream, A, B, C, M, N, K, cfg);
   if (rc != 0) return fail(static_cast<hipError_t>(rc), "gemm launch");
   return 0;

@@ -181,7 +181,7 @@ def test_arena_runtime_admits_four_64gib_pods():
         rt.close()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 def test_gemm_tile_configs_match_fp32_reference(hip, cfg):
     m, n, k = 512, 512, 256
     torch.manual_seed(cfg)
@@ -200,4 +200,42 @@ def test_gemm_tile_configs_match_fp32_reference(hip, cfg):
     hip.gemm_bf16_nt_cfg(s, eye.data_ptr(), bb.data_ptr(), c.data_ptr(), m, n, k, cfg)
     s.sync()
     torch.testing.assert_close(c.float()[:, :], (eye.float() @ bb.float().t()), atol=0, rtol=0)
+    s.destroy()
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 64), (768, 1280, 320), (2048, 512, 4096)])
+def test_gemm_phased_edge_shapes(hip, m, n, k):
+    """Phased kernel: one K-tile (clamped prefetch), odd tile counts, long K (many buffer reuses)."""
+    torch.manual_seed(k)
+    a = torch.randn(m, k, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(n, k, device="cuda", dtype=torch.bfloat16)
+    ref = a.float() @ b.float().t()
+    s = hip.Stream(0)
+    for cfg in (5, 6):
+        c = torch.full((m, n), float("nan"), device="cuda", dtype=torch.bfloat16)
+        torch.cuda.synchronize()
+        hip.gemm_bf16_nt_cfg(s, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, cfg)
+        s.sync()
+        torch.testing.assert_close(c.float(), ref, atol=0.05 * (k ** 0.5), rtol=1e-2)
+    s.destroy()
+
+
+def test_gemm_phased_is_deterministic(hip):
+    """Race screen for the counted-vmcnt schedule: 30 back-to-back runs must be bit-identical."""
+    m, n, k = 4096, 4096, 1024
+    torch.manual_seed(7)
+    a = torch.rand(m, k, device="cuda", dtype=torch.bfloat16) * 2 - 1
+    b = torch.rand(n, k, device="cuda", dtype=torch.bfloat16) * 2 - 1
+    s = hip.Stream(0)
+    for cfg in (5, 6):
+        c0 = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+        c = torch.empty_like(c0)
+        torch.cuda.synchronize()
+        hip.gemm_bf16_nt_cfg(s, a.data_ptr(), b.data_ptr(), c0.data_ptr(), m, n, k, cfg)
+        s.sync()
+        for _ in range(30):
+            hip.gemm_bf16_nt_cfg(s, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, cfg)
+            s.sync()
+            assert torch.equal(c, c0)
+        torch.testing.assert_close(c0.float(), a.float() @ b.float().t(), atol=0.05 * (k ** 0.5), rtol=1e-2)
     s.destroy()
