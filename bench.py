@@ -246,6 +246,9 @@ def main():
                 if json.loads(r.read()).get("nodes"):
                     break
             time.sleep(0.005)
+    from gpushare_scheduler_extender_amd.utils.gctune import tune
+
+    tune()
     barrier()
 
     n_pods = a.pods_per_gpu * world
@@ -288,6 +291,8 @@ def main():
         per_dev = [d["usedGPU"] for n in insp["nodes"] for d in n["devs"]]
         # teardown: one DeleteCollection for the wave; the step ends when the extender's ledger is empty
         await client.request("DELETE", "/api/v1/namespaces/default/pods", params={"labelSelector": f"gsx-wave={step}"})
+        # event-driven until the scheduler's informer saw every delete, then poll the ledger (usually empty by then)
+        await sim.wait_for(lambda: all(sim.pods.get(k) is None for k in keys), 120)
         while True:
             insp2 = await inspect_used()
             if sum(n["usedGPU"] for n in insp2["nodes"]) == 0:
@@ -303,6 +308,12 @@ def main():
         sim.forget(keys)
         return res
 
+    prof = None
+    if rank == 0 and os.environ.get("GSX_CPROFILE_DIR"):
+        import cProfile  # the scheduler simulator + load generator run on the loop thread
+
+        prof = cProfile.Profile()
+        lt.loop.call_soon_threadsafe(prof.enable)
     t_start = None
     for step in range(a.warmup + a.steps):
         if step == a.warmup:
@@ -313,11 +324,18 @@ def main():
             r = lt.run(wave(step), timeout=600)
             if step >= a.warmup:
                 step_stats.append(r)
-        if world > 1:
+        elif step < a.warmup:
+            dist.barrier(group=ctl)  # warmup waves in lockstep; timed waves are driven by rank 0 alone
+        if rank == 0 and world > 1 and step < a.warmup:
             dist.barrier(group=ctl)
     barrier()
     elapsed = time.perf_counter() - t_start
     cpu1 = _cpu_times(children)
+    if prof is not None:
+        lt.run(asyncio.sleep(0))
+        lt.loop.call_soon_threadsafe(prof.disable)
+        lt.run(asyncio.sleep(0))
+        prof.dump_stats(os.path.join(os.environ["GSX_CPROFILE_DIR"], "rank0-loop.prof"))
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if use_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -268,6 +268,9 @@ def main(argv=None) -> int:
         agent = NodeAgent(client, a.node, devs, get_profile(a.profile), rt, unit=a.unit,
                           verify_each=not a.no_verify, workers=a.workers)
         await agent.start()
+        from ..utils.gctune import tune  # noqa: PLC0415
+
+        tune()
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()
         for s in (signal.SIGINT, signal.SIGTERM):

@@ -85,6 +85,7 @@ class CUPartitioner:
         self.cu_count = cu_count
         self.xcc_count = max(1, xcc_count)
         self.owner: list[str | None] = [None] * cu_count
+        self._held: dict[str, list[int]] = {}
 
     def _order(self) -> list[int]:
         per = self.cu_count // self.xcc_count
@@ -94,24 +95,25 @@ class CUPartitioner:
     def allocate(self, uid: str, n: int) -> list[int]:
         if n <= 0 or n > self.cu_count:
             raise AllocateError(f"invalid CU partition size {n}")
-        mine = [c for c, o in enumerate(self.owner) if o == uid]
+        mine = self._held.get(uid)
         if mine:
-            return mine
+            return list(mine)
         free = [c for c in self._order() if self.owner[c] is None]
         if len(free) < n:
             raise AllocateError(f"only {len(free)} CUs free, {n} requested")
         got = sorted(free[:n])
         for c in got:
             self.owner[c] = uid
-        return got
+        self._held[uid] = got
+        return list(got)
 
     def release(self, uid: str) -> int:
-        n = 0
-        for c, o in enumerate(self.owner):
-            if o == uid:
-                self.owner[c] = None
-                n += 1
-        return n
+        got = self._held.pop(uid, None)
+        if not got:
+            return 0
+        for c in got:
+            self.owner[c] = None
+        return len(got)
 
     def free_count(self) -> int:
         return sum(1 for o in self.owner if o is None)

@@ -79,6 +79,9 @@ def main(argv=None) -> int:
             os.replace(a.port_file + ".tmp", a.port_file)
         log.info("gpushare extender %s listening on %s:%d (profile=%s bind=%s)", "0.1.0", a.host, runner.port,
                  a.profile, a.bind_mode)
+        from ..utils.gctune import tune  # noqa: PLC0415
+
+        tune()
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()
         hits = {"n": 0}

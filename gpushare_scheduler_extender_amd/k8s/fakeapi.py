@@ -126,15 +126,58 @@ def _field_match(obj: dict, selector: str) -> bool:
 
 
 class _Watcher:
-    __slots__ = ("kind", "ns", "fsel", "lsel", "queue", "closed")
+    """One watch stream.  Events are pushed, not pulled: ``push`` buffers the
+    line and schedules one ``flush`` per event-loop iteration, so a burst of
+    writes (a DeleteCollection, 32 creates) goes out as one chunk and no
+    coroutine wakes per event."""
+
+    __slots__ = ("kind", "ns", "fsel", "lsel", "closed", "pending", "scheduled", "out", "done", "sent", "drop_after",
+                 "on_drop")
 
     def __init__(self, kind, ns, fsel, lsel):
         self.kind = kind
         self.ns = ns
         self.fsel = fsel
         self.lsel = lsel
-        self.queue: asyncio.Queue = asyncio.Queue()
         self.closed = False
+        self.pending: list[bytes] = []
+        self.scheduled = False
+        self.out = None  # Stream once the backlog is written
+        self.done: asyncio.Future = asyncio.get_running_loop().create_future()
+        self.sent = 0
+        self.drop_after = 0
+        self.on_drop = None
+
+    def push(self, line: bytes):
+        self.pending.append(line)
+        if not self.scheduled and self.out is not None:
+            self.scheduled = True
+            asyncio.get_running_loop().call_soon(self.flush)
+
+    def go_live(self, out):
+        self.out = out
+        if self.pending:
+            self.flush()
+
+    def flush(self):
+        self.scheduled = False
+        if self.closed or self.out is None or not self.pending:
+            return
+        if self.out.closed:
+            self.finish()
+            return
+        lines, self.pending = self.pending, []
+        self.out.write(b"".join(lines))
+        self.sent += len(lines)
+        if self.drop_after and self.sent >= self.drop_after:
+            if self.on_drop:
+                self.on_drop()
+            self.finish()
+
+    def finish(self):
+        self.closed = True
+        if not self.done.done():
+            self.done.set_result(None)
 
     def wants(self, obj: dict) -> bool:
         if self.ns and (obj.get("metadata") or {}).get("namespace") != self.ns:
@@ -196,7 +239,7 @@ class FakeApiServer:
         self.history.append((rv, kind, etype, line, obj))
         for w in self.watchers:
             if w.kind == kind and not w.closed and w.wants(obj):
-                w.queue.put_nowait(line)
+                w.push(line)
 
     def create(self, kind: str, obj: dict, ns: str | None = None) -> dict:
         # copy-on-write: stored objects are immutable once emitted (watch history shares them)
@@ -492,34 +535,20 @@ class FakeApiServer:
         self.watchers.append(w)
         try:
             out.start()
-            sent = 0
-            if backlog:
-                out.write(b"".join(backlog))
-                sent += len(backlog)
+            w.drop_after = self.faults.drop_watch_after
+            w.on_drop = lambda: self.counts.__setitem__("watch_dropped", self.counts["watch_dropped"] + 1)
+            w.pending[:0] = backlog
+            w.go_live(out)
             timeout = float(request.query.get("timeoutSeconds", "0") or 0) or None
             deadline = time.monotonic() + timeout if timeout else None
-            while True:
+            while not w.closed:
                 rem = None if deadline is None else deadline - time.monotonic()
                 if rem is not None and rem <= 0:
                     break
-                try:
-                    line = await asyncio.wait_for(w.queue.get(), 1.0 if rem is None else min(rem, 1.0))
-                except asyncio.TimeoutError:
-                    if request.closed:
-                        break  # client went away
-                    continue
-                if not line:
-                    break  # server shutdown sentinel
-                lines = [line]
-                while not w.queue.empty():
-                    lines.append(w.queue.get_nowait())
-                if out.closed:
-                    break
-                out.write(b"".join(lines))
-                sent += len(lines)
-                if self.faults.drop_watch_after and sent >= self.faults.drop_watch_after:
-                    self.counts["watch_dropped"] += 1
-                    break
+                # events are pushed by _emit; this only watches for the end of the stream
+                await asyncio.wait([w.done], timeout=1.0 if rem is None else min(rem, 1.0))
+                if request.closed or out.closed:
+                    break  # client went away
         finally:
             w.closed = True
             try:
@@ -623,8 +652,7 @@ class FakeApiServerRunner:
 
     async def stop(self):
         for w in list(self.server.watchers):
-            w.closed = True
-            w.queue.put_nowait(b"")
+            w.finish()
         await asyncio.sleep(0)
         await self.server.app.stop()
 
@@ -655,6 +683,9 @@ def main(argv=None):
 
             os.replace(a.port_file + ".tmp", a.port_file)
         print(f"fake-apiserver listening on {r.url}", flush=True)
+        from ..utils.gctune import tune  # noqa: PLC0415
+
+        tune()
         await asyncio.Event().wait()
 
     try:

@@ -421,17 +421,34 @@ class Client:
                       headers: dict | None = None, timeout: float | None = -1.0) -> ClientResponse:
         data = self._req_bytes(method, path, body, content_type, headers)
         tmo = self.timeout if timeout == -1.0 else timeout
+        # one timer that cancels this task (asyncio.wait_for would wrap every read in a new task)
+        timer = fired = None
+        if tmo:
+            task = asyncio.current_task()
+            fired = []
+
+            def _expire():
+                fired.append(True)
+                task.cancel()
+            timer = asyncio.get_running_loop().call_later(tmo, _expire)
+        try:
+            return await self._request(method, path, data)
+        except asyncio.CancelledError:
+            if fired:
+                raise asyncio.TimeoutError(f"{method} {path}: no response in {tmo}s") from None
+            raise
+        finally:
+            if timer is not None:
+                timer.cancel()
+
+    async def _request(self, method: str, path: str, data: bytes) -> "ClientResponse":
         for attempt in range(2):
             reused = bool(self.idle)
             c = self.idle.pop() if reused else await self._open()
             try:
                 c.writer.write(data)
-                if tmo:
-                    status, hdrs = await asyncio.wait_for(_read_head(c.reader), tmo)
-                    rbody, reusable = await asyncio.wait_for(_read_body(c.reader, hdrs), tmo)
-                else:
-                    status, hdrs = await _read_head(c.reader)
-                    rbody, reusable = await _read_body(c.reader, hdrs)
+                status, hdrs = await _read_head(c.reader)
+                rbody, reusable = await _read_body(c.reader, hdrs)
             except (asyncio.IncompleteReadError, ConnectionError, OSError) as e:
                 c.close()
                 if reused and attempt == 0:

@@ -44,6 +44,10 @@ class ChildProc:
         if env:
             e.update(env)
         self.log = open(self.log_path, "w")
+        prof = os.environ.get("GSX_CPROFILE_DIR")
+        if prof and args[0] == "-m":  # profile the child (see utils/profrun.py)
+            os.makedirs(prof, exist_ok=True)
+            args = ["-m", "gpushare_scheduler_extender_amd.utils.profrun", os.path.join(prof, f"{name}.prof"), *args[1:]]
         self.proc = subprocess.Popen([sys.executable, *args, "--port-file", self.port_file], stdout=self.log,
                                      stderr=subprocess.STDOUT, env=e, cwd=str(ROOT))
         self.port = _wait_port(self.port_file, self.proc)

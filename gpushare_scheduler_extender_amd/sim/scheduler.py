@@ -86,8 +86,7 @@ class SchedulerSim:
         self._http_limit = http_limit
         self._tasks: list[asyncio.Task] = []
         self._bg: set[asyncio.Task] = set()
-        self.bound_event = asyncio.Event()
-        self.changed = asyncio.Event()  # set on every pod event (event-driven waits)
+        self._waiters: list[asyncio.Future] = []  # woken on every pod event and every bind (event-driven waits)
         self.pods.add_handler(Handler(self._on_pod, lambda o, n, r: self._on_pod(n, r), self._on_pod_delete))
 
     # ------------------------------------------------------------ pod intake
@@ -131,7 +130,7 @@ class SchedulerSim:
     def _on_pod(self, pod: dict, raw):
         key = obj_key(pod)
         self._account(key, pod)
-        self.changed.set()
+        self._notify()
         if self._pending(pod) and key not in self._queued and key not in self._assumed:
             self._queued.add(key)
             t = self.stats.timings.get(key)
@@ -142,7 +141,7 @@ class SchedulerSim:
     def _on_pod_delete(self, pod: dict, raw):
         key = obj_key(pod)
         self._account(key, None)
-        self.changed.set()
+        self._notify()
         self._unassume(key)
         self._req.pop((pod.get("metadata") or {}).get("uid", ""), None)
 
@@ -247,7 +246,7 @@ class SchedulerSim:
             tm.node = node
             tm.error = ""
             self.stats.bound += 1
-            self.bound_event.set()
+            self._notify()
         except Exception as e:  # noqa: BLE001
             self.stats.bind_errors += 1
             tm.error = repr(e)
@@ -298,6 +297,23 @@ class SchedulerSim:
         for k in keys:
             self.stats.timings.pop(k, None)
 
+    def _notify(self):
+        ws, self._waiters = self._waiters, []
+        for f in ws:
+            if not f.done():
+                f.set_result(None)
+
+    async def _changed(self, timeout: float):
+        """Sleep until the next pod event / bind or ``timeout`` (a bare future: no task per wait)."""
+        loop = asyncio.get_running_loop()
+        f = loop.create_future()
+        self._waiters.append(f)
+        h = loop.call_later(timeout, lambda: f.done() or f.set_result(None))
+        try:
+            await f
+        finally:
+            h.cancel()
+
     async def wait_for(self, cond, timeout: float = 30.0):
         """Wait until ``cond()`` holds, re-checking on every pod event the informer delivers."""
         deadline = time.perf_counter() + timeout
@@ -305,11 +321,7 @@ class SchedulerSim:
             rem = deadline - time.perf_counter()
             if rem <= 0:
                 raise TimeoutError("condition not reached")
-            self.changed.clear()
-            try:
-                await asyncio.wait_for(self.changed.wait(), min(rem, 0.05))
-            except asyncio.TimeoutError:
-                pass
+            await self._changed(min(rem, 0.05))
 
     async def wait_bound(self, keys: list[str], timeout: float = 30.0):
         deadline = time.perf_counter() + timeout
@@ -321,8 +333,4 @@ class SchedulerSim:
             if time.perf_counter() > deadline:
                 raise TimeoutError(f"{len(pending)} pods not bound, e.g. {sorted(pending)[:3]}: "
                                    f"{[self.stats.timings.get(k).error if self.stats.timings.get(k) else '?' for k in sorted(pending)[:3]]}")
-            self.bound_event.clear()
-            try:
-                await asyncio.wait_for(self.bound_event.wait(), 0.05)
-            except asyncio.TimeoutError:
-                pass
+            await self._changed(0.05)
