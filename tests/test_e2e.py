@@ -295,7 +295,7 @@ def test_leader_election_failover():
     async def go():
         async with Cluster() as c:
             await c.client.create("nodes", make_node("n", 100, 1))
-            kw = dict(leader_elect=True, lease_namespace="default", lease_duration=0.6, renew_deadline=0.4,
+            kw = dict(leader_elect=True, lease_namespace="default", lease_duration=2.0, renew_deadline=1.2,
                       retry_period=0.05)
             a = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, **kw),
                                      native=NATIVE["on"]).start()
