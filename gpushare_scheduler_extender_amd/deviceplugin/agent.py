@@ -41,7 +41,8 @@ class NodeAgent:
         self.runtime = runtime
         self.unit_bytes = UNITS[unit]
         self.verify_each = verify_each
-        self.mount_mode = mount_mode
+        # a host-process launcher cannot hide device nodes: it needs host GPU indices in *_VISIBLE_DEVICES
+        self.mount_mode = getattr(runtime, "mount_mode", mount_mode)
         self.report_status = report_status
         self.cus = {d.index: CUPartitioner(d.cu_count, d.xcc_count) for d in devices}
         self.pods = Informer(client, "pods", field_selector=f"spec.nodeName={node}")
@@ -110,6 +111,8 @@ class NodeAgent:
     async def _admit_runtime(self, uid: str, dev: int, nbytes: int, cus) -> int:
         adm = getattr(self.runtime, "admit", None)
         if adm is not None:
+            if getattr(self.runtime, "wants_envs", False):  # a launcher: give it the Allocate container env
+                return await adm(uid, dev, nbytes, cus, self.verify_each, envs=self.allocations.get(uid))
             return await adm(uid, dev, nbytes, cus, self.verify_each)
         return admit_local(self.runtime, uid, dev, nbytes, cus, self.verify_each)
 

@@ -257,3 +257,75 @@ class RemoteRuntime:
     async def close(self):
         for c in self.clients.values():
             await c.close()
+
+
+class ProcessRuntime:
+    """Container-runtime stand-in that runs each admitted pod's command as a child process.
+
+    The child gets exactly the container environment the device plugin's
+    Allocate returned (``HIP_VISIBLE_DEVICES``/``ROCR_VISIBLE_DEVICES``,
+    ``SHARED_GPU_MEM_*``, ``HSA_CU_MASK``/``GSX_CU_MASK``) on top of this
+    process's environment — the "Allocate output applied by a launcher" of
+    SURVEY.md §7.3 slice B.  Children are started with fork+exec in the child
+    (``asyncio.create_subprocess_exec``), never by replacing this process.
+    """
+
+    wants_envs = True
+    mount_mode = "all"  # children run on the host and see every GPU: HIP_VISIBLE_DEVICES = host index
+
+    def __init__(self, command: list[str], extra_env: dict | None = None, cwd: str | None = None):
+        self.command = list(command)
+        self.extra_env = dict(extra_env or {})
+        self.cwd = cwd
+        self.procs: dict = {}
+        self.envs: dict[str, dict] = {}
+        self.admitted = 0
+        self.failed = 0
+        self.bad = 0
+
+    async def admit(self, uid: str, dev: int, nbytes: int, cus=None, verify: bool = True,
+                    envs: dict | None = None) -> int:
+        import asyncio  # noqa: PLC0415
+        import os  # noqa: PLC0415
+
+        env = dict(os.environ)
+        env.update(self.extra_env)
+        env.update(envs or {})
+        try:
+            proc = await asyncio.create_subprocess_exec(*self.command, env=env, cwd=self.cwd,
+                                                        stdout=asyncio.subprocess.PIPE,
+                                                        stderr=asyncio.subprocess.PIPE)
+        except OSError as e:
+            self.failed += 1
+            raise AdmissionError(f"cannot start container: {e}") from e
+        self.procs[uid] = proc
+        self.envs[uid] = dict(envs or {})
+        self.admitted += 1
+        return 0
+
+    async def wait(self, uid: str, timeout: float) -> tuple[int, str, str]:
+        import asyncio  # noqa: PLC0415
+
+        proc = self.procs[uid]
+        so, se = await asyncio.wait_for(proc.communicate(), timeout)
+        return proc.returncode, so.decode(errors="replace"), se.decode(errors="replace")
+
+    async def release(self, uid: str) -> bool:
+        proc = self.procs.pop(uid, None)
+        if proc is None:
+            return False
+        if proc.returncode is None:
+            proc.terminate()
+            try:
+                await proc.wait()
+            except Exception:  # noqa: BLE001
+                pass
+        return True
+
+    def verify(self) -> int:
+        return 0
+
+    def close(self):
+        for p in self.procs.values():
+            if p.returncode is None:
+                p.kill()

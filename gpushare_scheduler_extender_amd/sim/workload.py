@@ -28,7 +28,8 @@ def parse_mask(s: str) -> list[int]:
 
 
 def run(total: float, allocated: float, *, kernel: str = "gsx", size: int = 8192, seconds: float = 0.0,
-        iters: int = 0, report_every: float = 5.0, touch: bool = False, quiet: bool = False) -> dict:
+        iters: int = 0, report_every: float = 5.0, touch: bool = False, quiet: bool = False,
+        probe_limit: bool = False) -> dict:
     import torch
 
     dev = torch.device("cuda", 0)
@@ -99,7 +100,17 @@ def run(total: float, allocated: float, *, kernel: str = "gsx", size: int = 8192
             break
     el = time.perf_counter() - t0
     out = {"tflops": done * flops / el / 1e12, "iters": done, "seconds": el, "fraction": frac,
-           "cu_mask": os.environ.get("GSX_CU_MASK", ""), "kernel": kernel, "size": size}
+           "cu_mask": os.environ.get("GSX_CU_MASK", ""), "kernel": kernel, "size": size,
+           "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES", ""),
+           "device_total_bytes": torch.cuda.get_device_properties(dev).total_memory}
+    if probe_limit and allocated:
+        # the share is a ceiling: one more share-sized tensor must be refused by the caching allocator
+        try:
+            extra = torch.empty(int(allocated * (1 << 30)) // 2, dtype=torch.bfloat16, device=dev)
+            del extra
+            out["limit_enforced"] = False
+        except torch.cuda.OutOfMemoryError:
+            out["limit_enforced"] = True
     del hold
     if hip_stream is not None:
         hip_stream.destroy()
@@ -116,9 +127,10 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=0)
     ap.add_argument("--touch", action="store_true")
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--probe-limit", action="store_true", help="check that the memory share is enforced")
     a = ap.parse_args(argv)
     res = run(a.total, a.allocated, kernel=a.kernel, size=a.size, seconds=a.seconds, iters=a.iters, touch=a.touch,
-              quiet=a.json)
+              quiet=a.json, probe_limit=a.probe_limit)
     print(json.dumps(res) if a.json else res, flush=True)
     return 0
 

@@ -353,6 +353,156 @@ hipError_t launch_phased(hipStream_t s, const void* A, const void* B, void* C, i
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// 4-wave 256x256 kernel: one wave per SIMD, 128x128 C per wave.
+//
+// rocprofv3 on the 8-wave kernels showed 1.57x the LDS instructions of
+// hipBLASLt's 256x256 kernel: a 128x64 wave tile re-reads A once per 64
+// columns.  A 128x128 wave tile halves that (LDS bytes per FLOP 0.75x), at
+// the price of 256 fp32 accumulators per lane — AGPRs, which gfx950 has when
+// a wave owns its SIMD (waves_per_eu = 1, 512 registers per lane).
+//
+// With no partner wave on the SIMD, latency is hidden inside the wave: the
+// K loop runs in k32 sub-steps, and the fragments of sub-step s+1 (16
+// ds_read_b128) are issued before the 64 MFMAs of sub-step s (register
+// double buffer).  LDS holds two K-tiles (2 x 64 KiB); tile t+2 is staged
+// into tile t's buffer as soon as every wave has read it, and waited for
+// with a counted vmcnt(16) (one tile of loads stays in flight) one sub-step
+// before it is read.  Past-the-end tiles are clamped (dead buffers).
+// ---------------------------------------------------------------------------
+template <int GROUP_M>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(
+    const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C, int M, int N, int K) {
+  constexpr int BM = 256, BN = 256, WT = 128;
+  constexpr int TILE = 256 * BK * 2;  // 32 KiB per operand per K-tile
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int ntm = M / BM, ntn = N / BN;
+  const int per_group = GROUP_M * ntn;
+  const int g = wg / per_group;
+  const int first_m = g * GROUP_M;
+  const int gm = (ntm - first_m) < GROUP_M ? (ntm - first_m) : GROUP_M;
+  const int tm = first_m + (wg % per_group) % gm;
+  const int tn = (wg % per_group) / gm;
+  const uint16_t* Ab = A + static_cast<size_t>(tm * BM) * K;
+  const uint16_t* Bb = B + static_cast<size_t>(tn * BN) * K;
+
+  int off[8];  // 8 rounds of 4 KiB (256 lanes x 16 B) cover one 256-row operand tile
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int p = (i * 4 + wid) * 64 + lane;
+    const int row = p >> 3, slot = p & 7;
+    off[i] = row * K + (slot ^ ((row >> 1) & 7)) * 8;
+  }
+  const int nk = K / BK;
+  auto stage = [&](int tile) {
+    const int kt = tile < nk ? tile : nk - 1;
+    char* la = lds + (tile & 1) * 2 * TILE;
+    char* lb = la + TILE;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      __builtin_amdgcn_global_load_lds((gptr_t)(Ab + off[i] + kt * BK), (lptr_t)(la + (i * 4 + wid) * 1024), 16, 0,
+                                       0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      __builtin_amdgcn_global_load_lds((gptr_t)(Bb + off[i] + kt * BK), (lptr_t)(lb + (i * 4 + wid) * 1024), 16, 0,
+                                       0);
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 af[2][8], bfr[2][8];
+  auto read = [&](int set, int tile, int kk) {
+    const char* la = lds + (tile & 1) * 2 * TILE;
+    const char* lb = la + TILE;
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      af[set][m] = *reinterpret_cast<const bf16x8*>(la + swz(wr * WT + m * 16 + fr, kk * 4 + fq));
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+      bfr[set][n] = *reinterpret_cast<const bf16x8*>(lb + swz(wc * WT + n * 16 + fr, kk * 4 + fq));
+  };
+  auto mma = [&](int set) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 8; ++n)
+        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[set][m], bfr[set][n], acc[m][n], 0, 0, 0);
+  };
+
+  stage(0);
+  stage(1);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  ph_barrier();
+  read(0, 0, 0);
+  for (int t = 0; t < nk; ++t) {
+    // sub-step (t, k 0..31): fragments of (t, k 32..63) in flight under the MFMAs
+    read(1, t, 1);
+    mma(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ph_barrier();  // every wave is done with tile t's buffer
+    stage(t + 2);
+    // sub-step (t, k 32..63): tile t+1 must have landed (tile t+2's 16 loads stay in flight)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    ph_barrier();
+    if (t + 1 < nk) read(0, t + 1, 0);
+    mma(1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ph_barrier();
+
+  // epilogue: wave-private 128x128 bf16 staging (32 KiB per wave), 16-B row stores
+  uint16_t* ct = reinterpret_cast<uint16_t*>(lds + wid * (WT * WT * 2));
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 8; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ct[(m * 16 + fq * 4 + j) * WT + n * 16 + fr] = f2bf(acc[m][n][j]);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  constexpr int LPR = WT / 8, RPI = 64 / LPR;
+  const int row0 = tm * BM + wr * WT, col0 = tn * BN + wc * WT;
+#pragma unroll
+  for (int i = 0; i < WT / RPI; ++i) {
+    const int rr = i * RPI + lane / LPR, cc = (lane % LPR) * 8;
+    const uint4 v = *reinterpret_cast<const uint4*>(ct + rr * WT + cc);
+    *reinterpret_cast<uint4*>(C + static_cast<size_t>(row0 + rr) * N + col0 + cc) = v;
+  }
+}
+
+template <int GM>
+hipError_t launch_w4(hipStream_t s, const void* A, const void* B, void* C, int M, int N, int K) {
+  constexpr int lds = 4 * 256 * BK * 2;  // 128 KiB
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_w4_kernel<GM>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  if (M % 256 || N % 256 || K % BK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_w4_kernel<GM>), dim3((M / 256) * (N / 256)), dim3(256), lds, s,
+                     static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
+                     N, K);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int WM, int WN, int GM>
 hipError_t launch(hipStream_t s, const void* A, const void* B, void* C, int M, int N, int K) {
   constexpr int lds = 2 * (BM + BN) * BK * 2;
@@ -374,8 +524,9 @@ hipError_t launch(hipStream_t s, const void* A, const void* B, void* C, int M, i
 
 // Tile configurations (index -> BM x BN, waves).  Exposed for benchmarking.
 extern "C" int gsx_gemm_cfg_tile(int cfg, int* bm, int* bn) {
-  static const int t[][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}, {128, 128}, {256, 256}, {256, 256}};
-  if (cfg < 0 || cfg > 6) return -1;
+  static const int t[][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}, {128, 128},
+                             {256, 256}, {256, 256}, {256, 256}, {256, 256}};
+  if (cfg < 0 || cfg > 8) return -1;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
   return 0;
@@ -392,6 +543,8 @@ extern "C" int gsx_gemm_bf16_nt_launch_cfg(void* stream, const void* A, const vo
     case 4: return static_cast<int>(gsxgemm::launch<128, 128, 2, 2, 1>(s, A, B, C, M, N, K));
     case 5: return static_cast<int>(gsxgemm::launch_phased<4>(s, A, B, C, M, N, K));
     case 6: return static_cast<int>(gsxgemm::launch_phased<8>(s, A, B, C, M, N, K));
+    case 7: return static_cast<int>(gsxgemm::launch_w4<4>(s, A, B, C, M, N, K));
+    case 8: return static_cast<int>(gsxgemm::launch_w4<8>(s, A, B, C, M, N, K));
     default: return static_cast<int>(hipErrorInvalidValue);
   }
 }

@@ -257,3 +257,66 @@ def test_api_messages_roundtrip():
     assert b[0] == 0x0A and b"\x1a" in b
     assert api.method_path("DevicePlugin", "Allocate") == "/v1beta1.DevicePlugin/Allocate"
     assert json.dumps(list(api.SERVICES["DevicePlugin"]))
+
+
+def test_process_runtime_starts_container_with_allocate_env():
+    """Slice B plumbing on CPU: bind -> Allocate -> the launcher runs the container with Allocate's env."""
+    import asyncio
+    import sys as _sys
+
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
+    from gpushare_scheduler_extender_amd.deviceplugin.runtime import ProcessRuntime
+    from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
+    from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+    from gpushare_scheduler_extender_amd.sim.scheduler import SchedulerSim
+
+    code = "import json,os;print(json.dumps({k:v for k,v in os.environ.items() if k.startswith(('SHARED_','HIP_','ROCR_'))}))"
+
+    async def go():
+        api = await FakeApiServerRunner().start()
+        client = KubeClient(api.url)
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), P), native=True).start()
+        devs = fake_devices("2x288GB")
+        rt = ProcessRuntime([_sys.executable, "-c", code])
+        agent = NodeAgent(KubeClient(api.url), "n1", devs, P, rt, unit="GiB")
+        sim = SchedulerSim(KubeClient(api.url), ext.url, P)
+        try:
+            totals = [d.units("GiB") for d in devs]
+            await client.create("nodes", make_node("n1", sum(totals), 2, device_totals=totals))
+            await agent.start()
+            await sim.start()
+            await client.create("pods", make_pod("b1", 200))
+            await client.create("pods", make_pod("b2", 200))
+            await sim.wait_bound(["default/b1", "default/b2"], 20)
+            for _ in range(2000):
+                if len(rt.procs) == 2:
+                    break
+                await asyncio.sleep(0.005)
+            outs = {}
+            for uid in list(rt.procs):
+                rc, so, _se = await rt.wait(uid, 60)
+                assert rc == 0
+                outs[uid] = json.loads(so.strip().splitlines()[-1])
+            pods = {p["metadata"]["uid"]: p for p in (await client.list("pods"))["items"]}
+            return outs, pods
+        finally:
+            await sim.stop()
+            await sim.client.close()
+            await agent.stop()
+            await agent.client.close()
+            rt.close()
+            await ext.stop()
+            await ext.server.client.close()
+            await client.close()
+            await api.stop()
+
+    outs, pods = asyncio.run(go())
+    assert len(outs) == 2
+    used = set()
+    for uid, env in outs.items():
+        ann = pods[uid]["metadata"]["annotations"]
+        assert ann[P.annotation_assigned] == "true"
+        assert env["HIP_VISIBLE_DEVICES"] == ann[P.annotation_idx] == env["SHARED_GPU_MEM_IDX"]
+        assert env["SHARED_GPU_MEM_CONTAINER"] == "200"
+        used.add(env["HIP_VISIBLE_DEVICES"])
+    assert used == {"0", "1"}  # 200 + 200 GiB cannot share one 288 GB device
