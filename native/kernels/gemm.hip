@@ -369,6 +369,13 @@ hipError_t launch_phased(hipStream_t s, const void* A, const void* B, void* C, i
 // into tile t's buffer as soon as every wave has read it, and waited for
 // with a counted vmcnt(16) (one tile of loads stays in flight) one sub-step
 // before it is read.  Past-the-end tiles are clamped (dead buffers).
+//
+// Measured (MI355X, random bf16, profiles/r01_rocprof_bench_gemm.md): LDS
+// instructions drop to hipBLASLt's level (18.0M vs 16.8M at 8192^3; the
+// 8-wave kernels issue 26.4M), but the kernel runs at 1.04-1.18 PFLOP/s, below
+// the phased 8-wave kernel (1.41-1.47): hipcc (ROCm 7.2) keeps 256
+// accumulators in AGPRs only with v_accvgpr_mov copies and s_nops between the
+// MFMAs of the inner loop.  Kept as an ablation; not dispatched by default.
 // ---------------------------------------------------------------------------
 template <int GROUP_M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(
@@ -460,7 +467,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // sub-step (t, k 32..63): tile t+1 must have landed (tile t+2's 16 loads stay in flight)
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     ph_barrier();
-    if (t + 1 < nk) read(0, t + 1, 0);
+    read(0, t + 1, 0);  // unconditional (no phi copies); the last one reads a dead buffer, never used
     mma(1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
