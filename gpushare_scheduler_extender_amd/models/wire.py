@@ -68,6 +68,30 @@ def binding_result(error: str = "") -> bytes:
     return json.dumps({"Error": error}, separators=(",", ":")).encode()
 
 
+def watch_object_bytes(line: bytes | None) -> bytes | None:
+    """The ``object`` of a watch event line ``{"type":"...","object":{...}}``, without re-encoding.
+
+    Returns None unless the line has exactly that shape (what kube-apiserver and
+    the fake apiserver emit); callers fall back to ``json.dumps``.
+    """
+    if not line or not line.startswith(b'{"type":"'):
+        return None
+    i = line.find(b'","object":', 9)
+    if i < 0:
+        return None
+    end = len(line.rstrip())
+    if end < 1 or line[end - 1:end] != b"}":
+        return None
+    obj = line[i + 11:end - 1]
+    return obj if obj[:1] == b"{" and obj[-1:] == b"}" else None
+
+
+def filter_args_raw(pod_json: bytes, node_names: list[str]) -> bytes:
+    """:func:`filter_args` for a pod already serialised (NodeNames form)."""
+    names = json.dumps(node_names, separators=(",", ":")).encode()
+    return b'{"Pod":' + pod_json + b',"Nodes":null,"NodeNames":' + names + b"}"
+
+
 def filter_args(pod: dict, node_names: list[str] | None = None, nodes: list[dict] | None = None) -> bytes:
     """ExtenderArgs as kube-scheduler sends it (nodeCacheCapable -> NodeNames)."""
     d = {"Pod": pod, "Nodes": None, "NodeNames": node_names}

@@ -82,6 +82,7 @@ class SchedulerSim:
         self._used: dict[str, int] = collections.defaultdict(int)  # node -> placed + assumed requests
         self._req: dict[str, int] = {}  # pod uid -> gpu-mem request (pod specs are immutable)
         self._queued: set[str] = set()
+        self._pod_json: dict[str, bytes] = {}  # pending pod -> its bytes from the watch event (no re-encode)
         self._http: Client | None = None
         self._http_limit = http_limit
         self._tasks: list[asyncio.Task] = []
@@ -132,17 +133,31 @@ class SchedulerSim:
         self._account(key, pod)
         self._notify()
         if self._pending(pod) and key not in self._queued and key not in self._assumed:
+            ob = wire.watch_object_bytes(raw)
+            if ob is not None:
+                self._pod_json[key] = ob
+            else:
+                self._pod_json.pop(key, None)
             self._queued.add(key)
             t = self.stats.timings.get(key)
             if t is None:
                 self.stats.timings[key] = PodTiming(key, seen=time.perf_counter())
             self.queue.put_nowait(key)
 
+    @staticmethod
+    def _rv_of(ob: bytes) -> str | None:
+        i = ob.find(b'"resourceVersion":"')
+        if i < 0:
+            return None
+        j = ob.find(b'"', i + 19)
+        return ob[i + 19:j].decode() if j > 0 else None
+
     def _on_pod_delete(self, pod: dict, raw):
         key = obj_key(pod)
         self._account(key, None)
         self._notify()
         self._unassume(key)
+        self._pod_json.pop(key, None)
         self._req.pop((pod.get("metadata") or {}).get("uid", ""), None)
 
     # ------------------------------------------------------------ aggregate fit (NodeResourcesFit)
@@ -192,7 +207,11 @@ class SchedulerSim:
             self._retry_later(key)
             return
         if req > 0:
-            if self.node_cache_capable:
+            ob = self._pod_json.pop(key, None)
+            if self.node_cache_capable and ob is not None and (pod.get("metadata") or {}).get(
+                    "resourceVersion") == self._rv_of(ob):
+                body = wire.filter_args_raw(ob, [n["metadata"]["name"] for n in cands])
+            elif self.node_cache_capable:
                 body = wire.filter_args(pod, [n["metadata"]["name"] for n in cands])
             else:
                 body = wire.filter_args(pod, nodes=cands)
