@@ -128,12 +128,15 @@ def main():
         inproc = [ext_r, api_r]
         api_url, ext_url = api_r.url, ext_r.url
     elif rank == 0:
-        from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver, start_extender, start_node_agent
+        from gpushare_scheduler_extender_amd.sim.cluster import (start_apiserver, start_extender, start_node_agent,
+                                                                 start_scheduler)
 
         api = start_apiserver()
         children.append(api)
         ext = start_extender(api.url, profile=a.profile, bind_mode=a.bind_mode)
         children.append(ext)
+        # kube-scheduler stand-in: its own process, like the real one (serial scheduling cycle)
+        children.append(start_scheduler(api.url, ext.url, profile=a.profile))
         if a.agent == "node":
             # the node's device plugin / kubelet stand-in: one process for all GPUs of the node, like a DaemonSet
             children.append(start_node_agent(api.url, NODE, profile=a.profile))
@@ -233,11 +236,20 @@ def main():
                           mount_mode="isolated")
         lt.run(agent.start())
 
-    sim = client = None
+    sim = client = tracker = sched_http = None
     if rank == 0:
+        from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as _HttpClient
+        from gpushare_scheduler_extender_amd.sim.tracker import PodTracker
+
         client = KubeClient(api_url)
-        sim = SchedulerSim(KubeClient(api_url), ext_url, profile, max_inflight_binds=256)
-        lt.run(sim.start())
+        if a.inproc:
+            sim = SchedulerSim(KubeClient(api_url), ext_url, profile, max_inflight_binds=256)
+            lt.run(sim.start())
+        else:
+            sched_http = _HttpClient(next(c.url for c in children if c.name == "scheduler"))
+        # the wave driver's own view of the wave's pods (bound / Running / gone), event-driven
+        tracker = PodTracker(KubeClient(api_url), "default", label_selector="gsx-wave")
+        lt.run(tracker.start())
         # wait until the extender has seen the node
         import urllib.request
 
@@ -271,11 +283,12 @@ def main():
         t0 = time.perf_counter()
         await asyncio.gather(*(client.create("pods", make_pod(nm, a.pod_gib, profile=profile, labels=label))
                                for nm in names))
-        await sim.wait_bound(keys, 120)
+        await tracker.wait_for(lambda: all(((tracker.get(k) or {}).get("spec") or {}).get("nodeName") for k in keys),
+                               120)
         t_bound = time.perf_counter()
 
         def phases():
-            return [((sim.pods.get(k) or {}).get("status") or {}).get("phase") for k in keys]
+            return [((tracker.get(k) or {}).get("status") or {}).get("phase") for k in keys]
 
         # every pod admitted on its GPU and Running (event-driven on the scheduler's pod informer)
         def all_running():
@@ -283,7 +296,7 @@ def main():
             if any(p == "Failed" for p in ph):
                 raise RuntimeError(f"pod admission failed: {[k for k, p in zip(keys, ph) if p == 'Failed']}")
             return all(p == "Running" for p in ph)
-        await sim.wait_for(all_running, 120)
+        await tracker.wait_for(all_running, 120)
         t_run = time.perf_counter()
         insp = await inspect_used()
         used = sum(n["usedGPU"] for n in insp["nodes"])
@@ -292,7 +305,7 @@ def main():
         # teardown: one DeleteCollection for the wave; the step ends when the extender's ledger is empty
         await client.request("DELETE", "/api/v1/namespaces/default/pods", params={"labelSelector": f"gsx-wave={step}"})
         # event-driven until the scheduler's informer saw every delete, then poll the ledger (usually empty by then)
-        await sim.wait_for(lambda: all(sim.pods.get(k) is None for k in keys), 120)
+        await tracker.wait_for(lambda: all(tracker.get(k) is None for k in keys), 120)
         while True:
             insp2 = await inspect_used()
             if sum(n["usedGPU"] for n in insp2["nodes"]) == 0:
@@ -301,12 +314,20 @@ def main():
                 raise TimeoutError("ledger did not drain")
             await asyncio.sleep(0.0003)
         t_end = time.perf_counter()
-        tm = [sim.stats.timings[k] for k in keys]
-        res = {"bind_latency": [t.bound - t.seen for t in tm], "bind_rtt": [t.bind_rtt for t in tm],
-               "filter_rtt": [t.filter_rtt for t in tm], "used": used, "total": total, "per_dev": per_dev,
-               "t_bound": t_bound - t0, "t_run": t_run - t0, "t_total": t_end - t0, "attempts": [t.attempts for t in tm]}
-        sim.forget(keys)
-        return res
+        # per-pod scheduler timings are collected after the timed region (fetch_timings)
+        return {"keys": keys, "used": used, "total": total, "per_dev": per_dev,
+                "t_bound": t_bound - t0, "t_run": t_run - t0, "t_total": t_end - t0}
+
+    async def fetch_timings(keys):
+        if sim is not None:
+            tm = [vars(sim.stats.timings[k]) for k in keys]
+            sim.forget(keys)
+            return tm
+        # the scheduler process's per-pod timings (its own clock; only differences are used)
+        body = json.dumps(keys).encode()
+        got = json.loads((await sched_http.request("POST", "/v1/timings", body)).body)
+        await sched_http.request("POST", "/v1/forget", body)
+        return [got[k] for k in keys]
 
     prof = None
     if rank == 0 and os.environ.get("GSX_CPROFILE_DIR"):
@@ -351,6 +372,10 @@ def main():
     agent_stats = gather(mine)
 
     if rank == 0:
+        for s in step_stats:
+            tm = lt.run(fetch_timings(s["keys"]), 60)
+            s.update({"bind_latency": [t["bound"] - t["seen"] for t in tm], "bind_rtt": [t["bind_rtt"] for t in tm],
+                      "filter_rtt": [t["filter_rtt"] for t in tm], "attempts": [t["attempts"] for t in tm]})
         pods_total = n_pods * a.steps
         value = pods_total / elapsed
         lat = [x for s in step_stats for x in s["bind_latency"]]
@@ -406,8 +431,13 @@ def main():
         lt.run(agent_client.close(), 30)
         lt.run(shim.stop(), 30)
         if rank == 0:
-            lt.run(sim.stop(), 30)
-            lt.run(sim.client.close(), 30)
+            if sim is not None:
+                lt.run(sim.stop(), 30)
+                lt.run(sim.client.close(), 30)
+            lt.run(tracker.stop(), 30)
+            lt.run(tracker.pods.client.close(), 30)
+            if sched_http is not None:
+                lt.run(sched_http.close(), 30)
             lt.run(client.close(), 30)
             if "c" in ext_http:
                 lt.run(ext_http["c"].close(), 30)

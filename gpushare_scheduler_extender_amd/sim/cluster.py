@@ -89,3 +89,9 @@ def start_extender(apiserver: str, profile: str = "shared-gpu", bind_mode: str =
 def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", workers: int = 32) -> ChildProc:
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
                       apiserver, "--profile", profile, "--workers", str(workers)], "node-agent")
+
+
+def start_scheduler(apiserver: str, extender: str, profile: str = "shared-gpu", max_inflight_binds: int = 256) -> ChildProc:
+    """kube-scheduler stand-in (``python -m gpushare_scheduler_extender_amd.sim``) with a timings endpoint."""
+    return ChildProc(["-m", "gpushare_scheduler_extender_amd.sim", "--apiserver", apiserver, "--extender", extender,
+                      "--profile", profile, "--max-inflight-binds", str(max_inflight_binds)], "scheduler")
