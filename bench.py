@@ -84,8 +84,8 @@ def pct(xs, q):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--pods-per-gpu", type=int, default=4)
     ap.add_argument("--pod-gib", type=int, default=64)
     ap.add_argument("--profile", default="aliyun")
