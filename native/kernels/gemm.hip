@@ -375,9 +375,14 @@ hipError_t launch_phased(hipStream_t s, const void* A, const void* B, void* C, i
 // 8-wave kernels issue 26.4M), but the kernel runs at 1.04-1.18 PFLOP/s, below
 // the phased 8-wave kernel (1.41-1.47): hipcc (ROCm 7.2) keeps 256
 // accumulators in AGPRs only with v_accvgpr_mov copies and s_nops between the
-// MFMAs of the inner loop.  Kept as an ablation; not dispatched by default.
+// MFMAs of the inner loop.  With the MFMAs in inline asm ("+a" pins the
+// accumulators, ASM=true) the loop is clean — 8 MFMAs, 16 prefetch ds_reads,
+// 56 MFMAs per sub-step, no copies — and reaches 1.11-1.22 PFLOP/s: with one
+// wave per SIMD nothing fills the MFMA pipe across the two barriers per
+// K-tile, which the staggered 8-wave kernel hides.  Kept as ablations; not
+// dispatched by default.
 // ---------------------------------------------------------------------------
-template <int GROUP_M>
+template <int GROUP_M, bool ASM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_w4_kernel(
     const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, uint16_t* __restrict__ C, int M, int N, int K) {
   constexpr int BM = 256, BN = 256, WT = 128;
@@ -444,12 +449,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int n = 0; n < 8; ++n)
       bfr[set][n] = *reinterpret_cast<const bf16x8*>(lb + swz(wc * WT + n * 16 + fr, kk * 4 + fq));
   };
-  auto mma = [&](int set) {
+  // 64 MFMAs of one k32 sub-step; `prefetch` (the next sub-step's ds_reads) is issued after the
+  // first row of 8, so the wait for this sub-step's fragments never covers the prefetch
+  auto mma = [&](int set, int pf_tile, int pf_kk) {
 #pragma unroll
     for (int m = 0; m < 8; ++m)
 #pragma unroll
-      for (int n = 0; n < 8; ++n)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[set][m], bfr[set][n], acc[m][n], 0, 0, 0);
+      for (int n = 0; n < 8; ++n) {
+        if (m == 1 && n == 0) {
+          __builtin_amdgcn_sched_barrier(0);
+          read(set ^ 1, pf_tile, pf_kk);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (ASM) {
+          // accumulator pinned to AGPRs ("+a"): no accumulator copies between the MFMAs
+          asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[m][n]) : "v"(af[set][m]), "v"(bfr[set][n]));
+        } else {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[set][m], bfr[set][n], acc[m][n], 0, 0, 0);
+        }
+      }
   };
 
   stage(0);
@@ -459,18 +477,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   read(0, 0, 0);
   for (int t = 0; t < nk; ++t) {
     // sub-step (t, k 0..31): fragments of (t, k 32..63) in flight under the MFMAs
-    read(1, t, 1);
-    mma(0);
+    mma(0, t, 1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ph_barrier();  // every wave is done with tile t's buffer
     stage(t + 2);
     // sub-step (t, k 32..63): tile t+1 must have landed (tile t+2's 16 loads stay in flight)
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     ph_barrier();
-    read(0, t + 1, 0);  // unconditional (no phi copies); the last one reads a dead buffer, never used
-    mma(1);
+    // unconditional (no phi copies); the last one reads a dead buffer, never used
+    mma(1, t + 1, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (ASM) {
+    // the compiler cannot see the asm MFMAs: cover the MFMA-write -> VALU-read (v_accvgpr_read) hazard
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  }
   ph_barrier();
 
   // epilogue: wave-private 128x128 bf16 staging (32 KiB per wave), 16-B row stores
@@ -493,18 +514,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
-template <int GM>
+template <int GM, bool ASM>
 hipError_t launch_w4(hipStream_t s, const void* A, const void* B, void* C, int M, int N, int K) {
   constexpr int lds = 4 * 256 * BK * 2;  // 128 KiB
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_w4_kernel<GM>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_w4_kernel<GM, ASM>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
   if (M % 256 || N % 256 || K % BK) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_w4_kernel<GM>), dim3((M / 256) * (N / 256)), dim3(256), lds, s,
+  hipLaunchKernelGGL((gemm_w4_kernel<GM, ASM>), dim3((M / 256) * (N / 256)), dim3(256), lds, s,
                      static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
                      N, K);
   return hipGetLastError();
@@ -532,8 +553,8 @@ hipError_t launch(hipStream_t s, const void* A, const void* B, void* C, int M, i
 // Tile configurations (index -> BM x BN, waves).  Exposed for benchmarking.
 extern "C" int gsx_gemm_cfg_tile(int cfg, int* bm, int* bn) {
   static const int t[][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}, {128, 128},
-                             {256, 256}, {256, 256}, {256, 256}, {256, 256}};
-  if (cfg < 0 || cfg > 8) return -1;
+                             {256, 256}, {256, 256}, {256, 256}, {256, 256}, {256, 256}};
+  if (cfg < 0 || cfg > 9) return -1;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
   return 0;
@@ -550,8 +571,9 @@ extern "C" int gsx_gemm_bf16_nt_launch_cfg(void* stream, const void* A, const vo
     case 4: return static_cast<int>(gsxgemm::launch<128, 128, 2, 2, 1>(s, A, B, C, M, N, K));
     case 5: return static_cast<int>(gsxgemm::launch_phased<4>(s, A, B, C, M, N, K));
     case 6: return static_cast<int>(gsxgemm::launch_phased<8>(s, A, B, C, M, N, K));
-    case 7: return static_cast<int>(gsxgemm::launch_w4<4>(s, A, B, C, M, N, K));
-    case 8: return static_cast<int>(gsxgemm::launch_w4<8>(s, A, B, C, M, N, K));
+    case 7: return static_cast<int>(gsxgemm::launch_w4<4, false>(s, A, B, C, M, N, K));
+    case 8: return static_cast<int>(gsxgemm::launch_w4<8, false>(s, A, B, C, M, N, K));
+    case 9: return static_cast<int>(gsxgemm::launch_w4<4, true>(s, A, B, C, M, N, K));
     default: return static_cast<int>(hipErrorInvalidValue);
   }
 }
