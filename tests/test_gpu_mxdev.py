@@ -1,0 +1,75 @@
+"""The native amdsmi layer (``native/mxdev``) on a real MI355X.
+
+amdsmi enumeration, VRAM totals, BDF and render node, health counters and link
+types are checked against what HIP reports for the same GPU — the inventory the
+device plugin advertises to kubelet and publishes on the node.  HIP is queried in
+a child process so this process only ever talks to amdsmi.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _hip_view() -> list[dict]:
+    code = ("import json;from gpushare_scheduler_extender_amd.ops import hip;"
+            "out=[];"
+            "[out.append(dict(hip.device_info(i), total=hip.mem_info(i)[1])) for i in range(hip.device_count())];"
+            "print(json.dumps(out))")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, cwd=ROOT,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def test_amdsmi_inventory_matches_hip():
+    from gpushare_scheduler_extender_amd.ops import mxdev
+
+    s = mxdev.session("amdsmi")
+    assert s.backend == "amdsmi"
+    devs = s.devices()
+    hip = _hip_view()
+    assert len(devs) >= 1 and len(devs) == len(hip), (devs, hip)
+    by_bdf = {h["pci_bus_id"].lower(): h for h in hip}
+    for d in devs:
+        print(json.dumps({k: v for k, v in d.items() if k != "links"}))
+        assert d["arch"].startswith("gfx950"), d
+        assert d["cu_count"] == 256 and d["xcc_count"] == 8, d
+        h = by_bdf.get(d["bdf"].lower())
+        assert h is not None, (d["bdf"], list(by_bdf))
+        # amdsmi VRAM total vs hipMemGetInfo total: same device memory (hip may hold back a little)
+        assert abs(d["total_bytes"] - h["total"]) <= 0.02 * d["total_bytes"], (d["total_bytes"], h["total"])
+        assert d["total_bytes"] > 250 * 10**9
+        assert d["render_minor"] >= 128 and os.path.exists(f"/dev/dri/renderD{d['render_minor']}"), d
+        assert d["partition"] in ("SPX", "DPX", "QPX", "CPX", "UNKNOWN", ""), d
+        assert d["links"].get(d["index"]) in ("SELF", None), d["links"]
+
+
+def test_amdsmi_health_counters_readable():
+    from gpushare_scheduler_extender_amd.ops import mxdev
+
+    s = mxdev.session("amdsmi")
+    for d in s.devices():
+        h = s.health(d["index"])
+        print(d["index"], h)
+        assert h["healthy"] is True
+        assert h["ecc_uncorrectable"] >= 0 and h["ecc_correctable"] >= 0
+
+
+def test_device_plugin_advertises_real_inventory():
+    """What ListAndWatch would advertise for this node: gpu-mem in GiB, one fake ID per GiB per GPU."""
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import discover
+    from gpushare_scheduler_extender_amd.deviceplugin.plugin import fake_ids
+
+    backend, devs = discover("amdsmi")
+    assert backend == "amdsmi"
+    per_dev = {d.index: fake_ids(d, d.units("GiB")) for d in devs}
+    ids = [i for v in per_dev.values() for i in v]
+    assert len(set(ids)) == len(ids)  # kubelet needs unique device IDs across the node
+    assert all(len(v) >= 256 for v in per_dev.values()), {k: len(v) for k, v in per_dev.items()}
