@@ -95,6 +95,12 @@ def parse():
     ap.add_argument("--json-out", default="")
     ap.add_argument("--agent", default="node", choices=["node", "rank"],
                     help="node: one node-agent process (the node's device plugin) driving a runtime shim per GPU rank (default); rank: one agent per GPU rank")
+    ap.add_argument("--scheduler", default="native", choices=["native", "python"],
+                    help="kube-scheduler stand-in: compiled gsx-schedsim (default) or the asyncio simulator")
+    ap.add_argument("--apiserver", default="native", choices=["native", "python"],
+                    help="fake kube-apiserver: gsx-fakeapi (default) or the asyncio one")
+    ap.add_argument("--node-agent", default="native", choices=["native", "python"],
+                    help="node agent (kubelet + device-plugin Allocate stand-in): gsx-nodeagent (default) or asyncio")
     ap.add_argument("--inproc", action="store_true",
                     help="run apiserver + extender in this process (no child processes; used under rocprofv3)")
     return ap.parse_args()
@@ -131,15 +137,15 @@ def main():
         from gpushare_scheduler_extender_amd.sim.cluster import (start_apiserver, start_extender, start_node_agent,
                                                                  start_scheduler)
 
-        api = start_apiserver()
+        api = start_apiserver(native=a.apiserver == "native")
         children.append(api)
         ext = start_extender(api.url, profile=a.profile, bind_mode=a.bind_mode)
         children.append(ext)
         # kube-scheduler stand-in: its own process, like the real one (serial scheduling cycle)
-        children.append(start_scheduler(api.url, ext.url, profile=a.profile))
+        children.append(start_scheduler(api.url, ext.url, profile=a.profile, native=a.scheduler == "native"))
         if a.agent == "node":
             # the node's device plugin / kubelet stand-in: one process for all GPUs of the node, like a DaemonSet
-            children.append(start_node_agent(api.url, NODE, profile=a.profile))
+            children.append(start_node_agent(api.url, NODE, profile=a.profile, native=a.node_agent == "native"))
         api_url, ext_url = api.url, ext.url
 
     import torch
@@ -238,26 +244,31 @@ def main():
 
     sim = client = tracker = sched_http = None
     if rank == 0:
+        from gpushare_scheduler_extender_amd.core.engine import native as _native_engine
         from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as _HttpClient
-        from gpushare_scheduler_extender_amd.sim.tracker import PodTracker
 
+        E = _native_engine()
         client = KubeClient(api_url)
         if a.inproc:
             sim = SchedulerSim(KubeClient(api_url), ext_url, profile, max_inflight_binds=256)
             lt.run(sim.start())
         else:
             sched_http = _HttpClient(next(c.url for c in children if c.name == "scheduler"))
-        # the wave driver's own view of the wave's pods (bound / Running / gone), event-driven
-        tracker = PodTracker(KubeClient(api_url), "default", label_selector="gsx-wave")
-        lt.run(tracker.start())
+        # the wave driver (load generator) is native: a reflector over the wave's pods that answers
+        # "all bound / Running / gone?" and a keep-alive batch client for the creates (native/engine/tracker.cc)
+        tracker = E.PodTracker({"server": api_url}, "default", "gsx-wave")
+        tracker.start(60)
+        api_batch = E.BatchClient({"server": api_url})
+        ext_batch = E.BatchClient({"server": ext_url})
         # wait until the extender has seen the node
-        import urllib.request
-
         for _ in range(2000):
-            with urllib.request.urlopen(ext_url + "/gpushare-scheduler/inspect") as r:
-                if json.loads(r.read()).get("nodes"):
-                    break
+            st, body = ext_batch.run([("GET", "/gpushare-scheduler/inspect", b"")], 1)[0]
+            if st == 200 and json.loads(body).get("nodes"):
+                break
             time.sleep(0.005)
+        pod_tmpl = make_pod("__NAME__", a.pod_gib, profile=profile, labels={"gsx-wave": "__STEP__"})
+        del pod_tmpl["metadata"]["uid"]  # the apiserver assigns one per pod
+        pod_tmpl = json.dumps(pod_tmpl, separators=(",", ":"))
     from gpushare_scheduler_extender_amd.utils.gctune import tune
 
     tune()
@@ -266,53 +277,47 @@ def main():
     n_pods = a.pods_per_gpu * world
     step_stats = []
 
-    ext_http = {}
+    def inspect_used():
+        st, body = ext_batch.run([("GET", "/gpushare-scheduler/inspect", b"")], 1)[0]
+        if st != 200:
+            raise RuntimeError(f"inspect failed: {st} {body[:200]!r}")
+        return json.loads(body)
 
-    async def inspect_used():
-        if "c" not in ext_http:
-            from gpushare_scheduler_extender_amd.k8s.fasthttp import Client
-
-            ext_http["c"] = Client(ext_url)
-        r = await ext_http["c"].request("GET", "/gpushare-scheduler/inspect")
-        return json.loads(r.body)
-
-    async def wave(step: int):
+    def wave(step: int):
         names = [f"w{step}-p{i}" for i in range(n_pods)]
         keys = [f"default/{nm}" for nm in names]
-        label = {"gsx-wave": str(step)}
         t0 = time.perf_counter()
-        await asyncio.gather(*(client.create("pods", make_pod(nm, a.pod_gib, profile=profile, labels=label))
-                               for nm in names))
-        await tracker.wait_for(lambda: all(((tracker.get(k) or {}).get("spec") or {}).get("nodeName") for k in keys),
-                               120)
+        body = pod_tmpl.replace("__STEP__", str(step))
+        res = api_batch.run([("POST", "/api/v1/namespaces/default/pods", body.replace("__NAME__", nm).encode())
+                             for nm in names], min(16, n_pods))
+        bad = [(st, b[:200]) for st, b in res if st != 201]
+        if bad:
+            raise RuntimeError(f"pod create failed: {bad[:3]}")
+        err = tracker.wait(keys, E.TRACK_BOUND, 120)
+        if err:
+            raise RuntimeError(err)
         t_bound = time.perf_counter()
-
-        def phases():
-            return [((tracker.get(k) or {}).get("status") or {}).get("phase") for k in keys]
-
-        # every pod admitted on its GPU and Running (event-driven on the scheduler's pod informer)
-        def all_running():
-            ph = phases()
-            if any(p == "Failed" for p in ph):
-                raise RuntimeError(f"pod admission failed: {[k for k, p in zip(keys, ph) if p == 'Failed']}")
-            return all(p == "Running" for p in ph)
-        await tracker.wait_for(all_running, 120)
+        # every pod admitted on its GPU and Running (a Failed admission aborts the run)
+        err = tracker.wait(keys, E.TRACK_RUNNING, 120)
+        if err:
+            raise RuntimeError(f"pod admission failed: {err}")
         t_run = time.perf_counter()
-        insp = await inspect_used()
+        insp = inspect_used()
         used = sum(n["usedGPU"] for n in insp["nodes"])
         total = sum(n["totalGPU"] for n in insp["nodes"])
         per_dev = [d["usedGPU"] for n in insp["nodes"] for d in n["devs"]]
         # teardown: one DeleteCollection for the wave; the step ends when the extender's ledger is empty
-        await client.request("DELETE", "/api/v1/namespaces/default/pods", params={"labelSelector": f"gsx-wave={step}"})
-        # event-driven until the scheduler's informer saw every delete, then poll the ledger (usually empty by then)
-        await tracker.wait_for(lambda: all(tracker.get(k) is None for k in keys), 120)
-        while True:
-            insp2 = await inspect_used()
-            if sum(n["usedGPU"] for n in insp2["nodes"]) == 0:
-                break
+        st, b = api_batch.run([("DELETE", f"/api/v1/namespaces/default/pods?labelSelector=gsx-wave%3D{step}", b"")],
+                              1)[0]
+        if st != 200:
+            raise RuntimeError(f"delete collection failed: {st} {b[:200]!r}")
+        err = tracker.wait(keys, E.TRACK_GONE, 120)
+        if err:
+            raise RuntimeError(err)
+        while sum(n["usedGPU"] for n in inspect_used()["nodes"]) != 0:
             if time.perf_counter() - t0 > 120:
                 raise TimeoutError("ledger did not drain")
-            await asyncio.sleep(0.0003)
+            time.sleep(0.0002)
         t_end = time.perf_counter()
         # per-pod scheduler timings are collected after the timed region (fetch_timings)
         return {"keys": keys, "used": used, "total": total, "per_dev": per_dev,
@@ -342,7 +347,7 @@ def main():
             t_start = time.perf_counter()
             cpu0 = _cpu_times(children)
         if rank == 0:
-            r = lt.run(wave(step), timeout=600)
+            r = wave(step)
             if step >= a.warmup:
                 step_stats.append(r)
         elif step < a.warmup:
@@ -434,13 +439,10 @@ def main():
             if sim is not None:
                 lt.run(sim.stop(), 30)
                 lt.run(sim.client.close(), 30)
-            lt.run(tracker.stop(), 30)
-            lt.run(tracker.pods.client.close(), 30)
+            tracker.stop()
             if sched_http is not None:
                 lt.run(sched_http.close(), 30)
             lt.run(client.close(), 30)
-            if "c" in ext_http:
-                lt.run(ext_http["c"].close(), 30)
             for r in inproc:
                 lt.run(r.stop(), 30)
     finally:

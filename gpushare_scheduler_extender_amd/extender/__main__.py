@@ -49,6 +49,8 @@ def parse_args(argv=None):
     ap.add_argument("--reservation-ttl", type=float, default=float(env.get("GSX_RESERVATION_TTL", "60")))
     ap.add_argument("--native-http", type=int, default=int(env.get("GSX_NATIVE_HTTP", "1")),
                     help="1: C++ front end serves filter/bind/inspect (default); 0: aiohttp only")
+    ap.add_argument("--native-controller", type=int, default=int(env.get("GSX_NATIVE_CONTROLLER", "1")),
+                    help="1: pod/node informers + controller in C++ (default); 0: asyncio controller")
     ap.add_argument("--http-threads", type=int, default=int(env.get("GSX_HTTP_THREADS", "2")))
     ap.add_argument("--bind-threads", type=int, default=int(env.get("GSX_BIND_THREADS", "16")))
     ap.add_argument("--leader-elect", type=int, default=int(env.get("GSX_LEADER_ELECT", "0")),
@@ -70,7 +72,7 @@ def main(argv=None) -> int:
         srv = ExtenderServer(client, get_profile(a.profile), workers=a.threadness, bind_mode=a.bind_mode,
                              reservation_ttl=a.reservation_ttl, resync_period=a.resync,
                              leader_elect=bool(a.leader_elect), lease_name=a.lease_name,
-                             lease_namespace=a.lease_namespace)
+                             lease_namespace=a.lease_namespace, native_controller=bool(a.native_controller))
         runner = await ExtenderRunner(srv, a.host, a.port, native=bool(a.native_http), http_threads=a.http_threads,
                                       pool_threads=a.bind_threads).start()
         if a.port_file:

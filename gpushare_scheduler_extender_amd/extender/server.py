@@ -43,7 +43,7 @@ import time
 
 from aiohttp import web
 
-from ..core.controller import Controller
+from ..core.controller import Controller, NativeController, api_dict
 from ..core.engine import new_engine
 from ..k8s.client import ApiError, KubeClient
 from ..models import pod as podutil
@@ -67,15 +67,18 @@ class ExtenderServer:
                  bind_mode: str = "binding", reservation_ttl: float = 60.0, resync_period: float = 30.0,
                  emit_events: bool = True, leader_elect: bool = False, lease_name: str = "gpushare-schd-extender",
                  lease_namespace: str = "kube-system", lease_duration: float = 15.0, renew_deadline: float = 10.0,
-                 retry_period: float = 2.0):
+                 retry_period: float = 2.0, native_controller: bool = True):
         if bind_mode not in ("binding", "update"):
             raise ValueError("bind_mode must be 'binding' or 'update'")
         self.client = client
         self.profile = profile
         self.engine = new_engine(profile)
         self.metrics = Metrics(self.engine)
-        self.controller = Controller(client, self.engine, profile, workers=workers, resync_period=resync_period,
-                                     metrics=self.metrics)
+        if native_controller:
+            self.controller = NativeController(client, self.engine, profile, resync_period=resync_period)
+        else:
+            self.controller = Controller(client, self.engine, profile, workers=workers, resync_period=resync_period,
+                                         metrics=self.metrics)
         self.bind_mode = bind_mode
         self.reservation_ttl = reservation_ttl
         self.emit_events = emit_events
@@ -130,7 +133,7 @@ class ExtenderServer:
 
     async def _get_pod(self, name: str, ns: str, uid: str) -> dict:
         """gpushare-bind.go:44-65."""
-        pod = self.controller.pods.get_by(name, ns)
+        pod = self.controller.get_pod(name, ns)
         if pod is not None and (pod.get("metadata") or {}).get("uid") == uid:
             return pod
         t0 = time.perf_counter()
@@ -282,7 +285,7 @@ class ExtenderServer:
         return web.Response(text=VERSION)
 
     async def h_healthz(self, request):
-        ok = self.controller.pods.synced.is_set() and self.controller.nodes.synced.is_set()
+        ok = self.controller.is_synced()
         if ok and not self.is_leader:
             return web.Response(text="standby (not the leader)", status=503)
         return web.Response(text="ok" if ok else "not synced", status=200 if ok else 503)
@@ -325,9 +328,7 @@ class ExtenderRunner:
             site = web.TCPSite(self._runner, "127.0.0.1", 0, backlog=1024, reuse_address=True)
             await site.start()
             self.internal_port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
-            cfg = self.server.client.config
-            api = {"server": cfg.server, "token": cfg.token or "", "ca_file": cfg.ca_file or "",
-                   "cert_file": cfg.cert_file or "", "key_file": cfg.key_file or "", "insecure": bool(cfg.insecure)}
+            api = api_dict(self.server.client.config)
             native_bind = self.server.bind_mode == "binding" and self.server.client.limiter.qps <= 0
             self.port = self.server.engine.serve(self.host, self.port, self.http_threads, self.pool_threads,
                                                  self.internal_port, native_bind, self.server.reservation_ttl, api)

@@ -191,11 +191,13 @@ class Faults:
         self.error_rate = 0.0  # 500s on mutating pod calls
         self.latency_ms = 0.0  # added to every non-watch request
         self.drop_watch_after = 0  # close watch streams after this many events (0 = never)
+        self.expire_watches = 0  # the next N watch requests get 410 Gone (history compacted)
+        self.hold_watches = False  # new watch requests wait until this is cleared
         self.seed = 0
         self.rng = random.Random(0)
 
     def update(self, d: dict):
-        for k in ("conflict_rate", "error_rate", "latency_ms", "drop_watch_after"):
+        for k in ("conflict_rate", "error_rate", "latency_ms", "drop_watch_after", "expire_watches", "hold_watches"):
             if k in d:
                 setattr(self, k, type(getattr(self, k))(d[k]))
         if "seed" in d:
@@ -204,7 +206,8 @@ class Faults:
 
     def as_dict(self):
         return {"conflict_rate": self.conflict_rate, "error_rate": self.error_rate,
-                "latency_ms": self.latency_ms, "drop_watch_after": self.drop_watch_after}
+                "latency_ms": self.latency_ms, "drop_watch_after": self.drop_watch_after,
+                "expire_watches": self.expire_watches, "hold_watches": self.hold_watches}
 
 
 class FakeApiServer:
@@ -485,7 +488,11 @@ class FakeApiServer:
         return self._json(self.faults.as_dict())
 
     def h_faults(self, request):
-        self.faults.update(request.json() or {})
+        d = request.json() or {}
+        self.faults.update(d)
+        if d.get("drop_watches_now"):  # one-shot: end every open watch stream
+            for w in list(self.watchers):
+                w.finish()
         return self._json(self.faults.as_dict())
 
     def h_stats(self, request):
@@ -515,6 +522,14 @@ class FakeApiServer:
     async def _watch(self, request, kind, ns, fsel, lsel, rv_s):
         w = _Watcher(kind, ns, fsel, lsel)
         out = Stream(request.transport)
+        while self.faults.hold_watches:
+            await asyncio.sleep(0.005)
+        if self.faults.expire_watches > 0:
+            self.faults.expire_watches -= 1
+            self.counts["watch_expired"] += 1
+            err = {"type": "ERROR", "object": status_body(410, "Expired", "too old resource version (injected)")}
+            out.write(json.dumps(err).encode() + b"\n")
+            return out
         backlog = []
         if rv_s not in ("", "0"):
             try:

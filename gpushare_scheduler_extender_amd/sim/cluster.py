@@ -48,7 +48,9 @@ class ChildProc:
         if prof and args[0] == "-m":  # profile the child (see utils/profrun.py)
             os.makedirs(prof, exist_ok=True)
             args = ["-m", "gpushare_scheduler_extender_amd.utils.profrun", os.path.join(prof, f"{name}.prof"), *args[1:]]
-        self.proc = subprocess.Popen([sys.executable, *args, "--port-file", self.port_file], stdout=self.log,
+        # "-m module ..." runs under this interpreter; anything else is a native executable
+        argv = [sys.executable, *args] if args[0] == "-m" else list(args)
+        self.proc = subprocess.Popen([*argv, "--port-file", self.port_file], stdout=self.log,
                                      stderr=subprocess.STDOUT, env=e, cwd=str(ROOT))
         self.port = _wait_port(self.port_file, self.proc)
         self.url = f"http://127.0.0.1:{self.port}"
@@ -75,7 +77,15 @@ class ChildProc:
             shutil.rmtree(self.tmp, ignore_errors=True)
 
 
-def start_apiserver() -> ChildProc:
+FAKEAPI = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-fakeapi"
+
+
+def start_apiserver(native: bool = True, history: int = 200000) -> ChildProc:
+    """Fake kube-apiserver: the compiled ``gsx-fakeapi`` (native/fakeapi) or ``python -m ...k8s.fakeapi``."""
+    if native:
+        if not FAKEAPI.exists():
+            raise FileNotFoundError(f"{FAKEAPI} missing; run `python native/build.py fakeapi`")
+        return ChildProc([str(FAKEAPI), "--port", "0", "--history", str(history)], "apiserver")
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.k8s.fakeapi", "--port", "0"], "apiserver")
 
 
@@ -86,12 +96,40 @@ def start_extender(apiserver: str, profile: str = "shared-gpu", bind_mode: str =
                       "--threadness", str(threadness), "--log-level", log_level], "extender")
 
 
-def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", workers: int = 32) -> ChildProc:
+NODEAGENT = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-nodeagent"
+
+
+def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", workers: int = 32,
+                     native: bool = True) -> ChildProc:
+    """kubelet + device-plugin Allocate + runtime stand-in for ``node``.
+
+    ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent);
+    otherwise ``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``.
+    """
+    if native:
+        if not NODEAGENT.exists():
+            raise FileNotFoundError(f"{NODEAGENT} missing; run `python native/build.py nodeagent`")
+        return ChildProc([str(NODEAGENT), "--node", node, "--apiserver", apiserver, "--profile", profile,
+                          "--workers", str(min(workers, 64))], "node-agent")
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
                       apiserver, "--profile", profile, "--workers", str(workers)], "node-agent")
 
 
-def start_scheduler(apiserver: str, extender: str, profile: str = "shared-gpu", max_inflight_binds: int = 256) -> ChildProc:
-    """kube-scheduler stand-in (``python -m gpushare_scheduler_extender_amd.sim``) with a timings endpoint."""
+SCHEDSIM = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-schedsim"
+
+
+def start_scheduler(apiserver: str, extender: str, profile: str = "shared-gpu", max_inflight_binds: int = 256,
+                    native: bool = True) -> ChildProc:
+    """kube-scheduler stand-in with a timings endpoint.
+
+    ``native=True``: the compiled ``gsx-schedsim`` (native/schedsim, built by
+    ``native/build.py``); otherwise ``python -m gpushare_scheduler_extender_amd.sim``.
+    Both serve the same ``/v1/timings``, ``/v1/forget`` and ``/v1/stats``.
+    """
+    if native:
+        if not SCHEDSIM.exists():
+            raise FileNotFoundError(f"{SCHEDSIM} missing; run `python native/build.py schedsim`")
+        return ChildProc([str(SCHEDSIM), "--apiserver", apiserver, "--extender", extender, "--profile", profile,
+                          "--bind-threads", str(min(64, max_inflight_binds))], "scheduler")
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.sim", "--apiserver", apiserver, "--extender", extender,
                       "--profile", profile, "--max-inflight-binds", str(max_inflight_binds)], "scheduler")

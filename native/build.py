@@ -2,7 +2,10 @@
 
 Targets (outputs land in ``gpushare_scheduler_extender_amd/_native/``):
 
-* ``engine``  – C++17 ledger/JSON engine + pybind11 module ``_engine``.
+* ``engine``  – C++17 ledger/JSON engine, reflectors + controller, pybind11 module ``_engine``.
+* ``schedsim`` – ``gsx-schedsim``, the compiled kube-scheduler stand-in used by the benchmark.
+* ``nodeagent`` – ``gsx-nodeagent``, the compiled kubelet / device-plugin Allocate / runtime stand-in.
+* ``fakeapi`` – ``gsx-fakeapi``, the compiled fake kube-apiserver.
 * ``mxdev``   – C++17 amdsmi device library + pybind11 module ``_mxdev``
                 (amdsmi is dlopen'ed with RTLD_DEEPBIND at run time so the
                 module also loads on hosts without a GPU and never binds to the
@@ -88,6 +91,36 @@ def build_engine(force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
+def _build_native_tool(name: str, srcdir: str, force: bool, verbose: bool) -> Path:
+    """A standalone executable from ``native/<srcdir>/*.cc`` linked with the engine's objects."""
+    src = NATIVE / "engine"
+    eng = [s for s in sorted(src.glob("*.cc")) if s.name not in ("bindings.cc", "engine_test.cc")]
+    headers = sorted(src.glob("*.h"))
+    flags = [*CXXFLAGS, "-I" + str(src)]
+    objs = _compile_objs(eng, "g++", flags, "tool", force, verbose, headers)
+    objs += _compile_objs(sorted((NATIVE / srcdir).glob("*.cc")), "g++", flags, srcdir, force, verbose, headers)
+    out = OUT / name
+    if force or _newer(out, objs):
+        OUT.mkdir(parents=True, exist_ok=True)
+        _run(["g++", "-o", str(out), *map(str, objs), "-lssl", "-lcrypto", "-lpthread"], verbose)
+    return out
+
+
+def build_schedsim(force: bool = False, verbose: bool = False) -> Path:
+    """``gsx-schedsim``: the compiled kube-scheduler stand-in (reflectors + serial cycle + bind pool)."""
+    return _build_native_tool("gsx-schedsim", "schedsim", force, verbose)
+
+
+def build_nodeagent(force: bool = False, verbose: bool = False) -> Path:
+    """``gsx-nodeagent``: the compiled kubelet + device-plugin Allocate + runtime stand-in for one node."""
+    return _build_native_tool("gsx-nodeagent", "nodeagent", force, verbose)
+
+
+def build_fakeapi(force: bool = False, verbose: bool = False) -> Path:
+    """``gsx-fakeapi``: the compiled fake kube-apiserver (same REST subset as k8s/fakeapi.py)."""
+    return _build_native_tool("gsx-fakeapi", "fakeapi", force, verbose)
+
+
 def build_mxdev(force: bool = False, verbose: bool = False) -> Path:
     src = NATIVE / "mxdev"
     srcs = sorted(src.glob("*.cc"))
@@ -164,13 +197,16 @@ def build_tsan(force: bool = False, verbose: bool = False) -> Path:
 
 TARGETS = {
     "engine": build_engine,
+    "schedsim": build_schedsim,
+    "nodeagent": build_nodeagent,
+    "fakeapi": build_fakeapi,
     "mxdev": build_mxdev,
     "kernels": build_kernels,
     "tools": build_tools,
     "asan": build_asan,
     "tsan": build_tsan,
 }
-DEFAULT = ["engine", "mxdev", "kernels", "tools"]
+DEFAULT = ["engine", "schedsim", "nodeagent", "fakeapi", "mxdev", "kernels", "tools"]
 
 
 def main(argv: list[str] | None = None) -> int:

@@ -14,6 +14,7 @@
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 
 namespace gsx {
 
@@ -96,6 +97,10 @@ ApiClient::Conn* ApiClient::acquire(std::string* err) {
       return c;
     }
   }
+  return connect_new(err);
+}
+
+ApiClient::Conn* ApiClient::connect_new(std::string* err) {
   addrinfo hints;
   std::memset(&hints, 0, sizeof(hints));
   hints.ai_socktype = SOCK_STREAM;
@@ -198,6 +203,126 @@ long ApiClient::recv_some(Conn* c, char* buf, size_t n) {
   }
 }
 
+std::string ApiClient::request_head(const std::string& method, const std::string& path, size_t body_len,
+                                    const char* content_type, bool has_body) const {
+  std::string req;
+  req.reserve(256 + body_len);
+  req.append(method).append(" ").append(url_.prefix).append(path).append(" HTTP/1.1\r\nHost: ");
+  req.append(url_.host);
+  if ((url_.tls && url_.port != 443) || (!url_.tls && url_.port != 80)) req.append(":").append(std::to_string(url_.port));
+  req.append("\r\nUser-Agent: ").append(cfg_.user_agent);
+  req.append("\r\nAccept: application/json\r\n");
+  if (!cfg_.token.empty()) req.append("Authorization: Bearer ").append(cfg_.token).append("\r\n");
+  if (has_body) {
+    req.append("Content-Type: ").append(content_type ? content_type : "application/json").append("\r\n");
+    req.append("Content-Length: ").append(std::to_string(body_len)).append("\r\n");
+  }
+  req.append("\r\n");
+  return req;
+}
+
+void StreamHandle::abort() {
+  aborted.store(true);
+  int fd_ = fd.load();
+  if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
+}
+
+bool ApiClient::stream(const std::string& path, int* status, std::string* error_body,
+                       const std::function<bool(std::string_view)>& on_data, std::string* err, StreamHandle* h,
+                       double idle_timeout_s) {
+  if (!ok_) {
+    *err = init_err_;
+    return false;
+  }
+  if (h->aborted.load()) return true;
+  Conn* c = connect_new(err);
+  if (!c) return false;
+  struct Closer {
+    ApiClient* self;
+    Conn* c;
+    StreamHandle* h;
+    ~Closer() {
+      h->fd.store(-1);
+      self->close_conn(c);
+      delete c;
+    }
+  } closer{this, c, h};
+  h->fd.store(c->fd);
+  if (h->aborted.load()) return true;  // abort raced with the connect
+  timeval tv;
+  tv.tv_sec = static_cast<long>(idle_timeout_s);
+  tv.tv_usec = 0;
+  setsockopt(c->fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  if (!send_all(c, request_head("GET", path, 0, nullptr, false))) {
+    if (h->aborted.load()) return true;
+    *err = "send to apiserver failed";
+    return false;
+  }
+  ++requests_;
+  char buf[65536];
+  std::string head;
+  http::Message m;
+  long content_length = -1;
+  bool chunked = false;
+  long hl = 0;
+  while (true) {
+    long r = recv_some(c, buf, sizeof(buf));
+    if (r <= 0) {
+      if (h->aborted.load()) return true;
+      *err = r == 0 ? "apiserver closed the watch before responding" : "watch read failed";
+      return false;
+    }
+    head.append(buf, static_cast<size_t>(r));
+    std::string perr;
+    hl = http::parse_head(head.data(), head.size(), false, &m, &perr, &content_length, &chunked);
+    if (hl < 0) {
+      *err = "bad watch response: " + perr;
+      return false;
+    }
+    if (hl > 0) break;
+  }
+  *status = m.status;
+  const bool is_err = m.status >= 400;
+  http::Dechunker dech;
+  bool stop = false;
+  long long left = content_length;  // -1: until close (when not chunked)
+  auto emit = [&](std::string_view piece) {
+    if (stop || piece.empty()) return;
+    if (is_err) {
+      error_body->append(piece);
+    } else if (!on_data(piece)) {
+      stop = true;
+    }
+  };
+  auto consume = [&](const char* p, size_t n) -> int {
+    if (chunked) return dech.feed(p, n, emit);
+    if (left >= 0) {
+      size_t take = static_cast<size_t>(std::min<long long>(left, static_cast<long long>(n)));
+      emit(std::string_view(p, take));
+      left -= static_cast<long long>(take);
+      return left == 0 ? 1 : 0;
+    }
+    emit(std::string_view(p, n));
+    return 0;
+  };
+  int st = consume(head.data() + hl, head.size() - static_cast<size_t>(hl));
+  while (st == 0 && !stop) {
+    long r = recv_some(c, buf, sizeof(buf));
+    if (r == 0) break;  // server closed: end of stream
+    if (r < 0) {
+      if (h->aborted.load()) return true;
+      *err = "watch read failed";
+      return false;
+    }
+    st = consume(buf, static_cast<size_t>(r));
+  }
+  if (st < 0) {
+    *err = "bad chunked framing in watch stream";
+    return false;
+  }
+  return true;
+}
+
 bool ApiClient::request(const std::string& method, const std::string& path, const std::string& body,
                         const char* content_type, int* status, std::string* resp, std::string* err,
                         std::string* resp_content_type) {
@@ -205,19 +330,9 @@ bool ApiClient::request(const std::string& method, const std::string& path, cons
     *err = init_err_;
     return false;
   }
-  std::string req;
-  req.reserve(256 + body.size());
-  req.append(method).append(" ").append(url_.prefix).append(path).append(" HTTP/1.1\r\nHost: ");
-  req.append(url_.host);
-  if ((url_.tls && url_.port != 443) || (!url_.tls && url_.port != 80)) req.append(":").append(std::to_string(url_.port));
-  req.append("\r\nUser-Agent: ").append(cfg_.user_agent);
-  req.append("\r\nAccept: application/json\r\n");
-  if (!cfg_.token.empty()) req.append("Authorization: Bearer ").append(cfg_.token).append("\r\n");
-  if (!body.empty() || method == "POST" || method == "PUT" || method == "PATCH") {
-    req.append("Content-Type: ").append(content_type ? content_type : "application/json").append("\r\n");
-    req.append("Content-Length: ").append(std::to_string(body.size())).append("\r\n");
-  }
-  req.append("\r\n").append(body);
+  std::string req = request_head(method, path, body.size(), content_type,
+                                 !body.empty() || method == "POST" || method == "PUT" || method == "PATCH");
+  req.append(body);
 
   for (int attempt = 0; attempt < 2; ++attempt) {
     Conn* c = acquire(err);

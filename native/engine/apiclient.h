@@ -6,6 +6,8 @@
 #pragma once
 
 #include <atomic>
+#include <functional>
+#include <string_view>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -27,6 +29,13 @@ struct ApiConfig {
   std::string user_agent = "gpushare-schd-extender-amd/0.1.0 (native)";
 };
 
+// Lets another thread end a running ApiClient::stream() (shuts the socket).
+struct StreamHandle {
+  std::atomic<int> fd{-1};
+  std::atomic<bool> aborted{false};
+  void abort();
+};
+
 class ApiClient {
  public:
   explicit ApiClient(ApiConfig cfg);
@@ -40,6 +49,16 @@ class ApiClient {
                const char* content_type, int* status, std::string* resp, std::string* err,
                std::string* resp_content_type = nullptr);
 
+  // Streams one GET on a dedicated connection (watch).  Decoded body bytes
+  // (chunked or length / close delimited) go to on_data; returning false
+  // from it ends the stream.  For HTTP status >= 400 the body is collected
+  // into *error_body instead.  Returns false on transport errors (*err set);
+  // a stream that ends cleanly (server timeout, abort) returns true.
+  // idle_timeout_s bounds a silent connection.
+  bool stream(const std::string& path, int* status, std::string* error_body,
+              const std::function<bool(std::string_view)>& on_data, std::string* err, StreamHandle* h,
+              double idle_timeout_s);
+
   uint64_t requests() const { return requests_; }
   uint64_t reconnects() const { return reconnects_; }
 
@@ -50,6 +69,9 @@ class ApiClient {
     std::string rbuf;
   };
   Conn* acquire(std::string* err);
+  Conn* connect_new(std::string* err);
+  std::string request_head(const std::string& method, const std::string& path, size_t body_len,
+                           const char* content_type, bool has_body) const;
   void release(Conn* c, bool reuse);
   void close_conn(Conn* c);
   bool send_all(Conn* c, const std::string& data);

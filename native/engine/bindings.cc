@@ -9,7 +9,9 @@
 
 #include "ledger.h"
 #include "quantity.h"
+#include "controller.h"
 #include "server.h"
+#include "tracker.h"
 
 namespace py = pybind11;
 using namespace gsx;
@@ -64,6 +66,20 @@ bool parse_node_bytes(const py::bytes& b, const Profile& p, NodeView* out, std::
     return false;
   }
   return true;
+}
+
+ApiConfig api_from(const py::dict& api) {
+  ApiConfig c;
+  auto get = [&](const char* k, std::string* dst) {
+    if (api.contains(k) && !api[k].is_none()) *dst = api[k].cast<std::string>();
+  };
+  get("server", &c.server);
+  get("token", &c.token);
+  get("ca_file", &c.ca_file);
+  get("cert_file", &c.cert_file);
+  get("key_file", &c.key_file);
+  if (api.contains("insecure")) c.insecure = api["insecure"].cast<bool>();
+  return c;
 }
 
 class Engine {
@@ -260,15 +276,7 @@ class Engine {
     cfg.fallback_port = fallback_port;
     cfg.native_bind = native_bind;
     cfg.reservation_ttl = ttl;
-    auto get = [&](const char* k, std::string* dst) {
-      if (api.contains(k) && !api[k].is_none()) *dst = api[k].cast<std::string>();
-    };
-    get("server", &cfg.api.server);
-    get("token", &cfg.api.token);
-    get("ca_file", &cfg.api.ca_file);
-    get("cert_file", &cfg.api.cert_file);
-    get("key_file", &cfg.api.key_file);
-    if (api.contains("insecure")) cfg.api.insecure = api["insecure"].cast<bool>();
+    cfg.api = api_from(api);
     if (cfg.api.server.empty()) cfg.native_bind = false;
     srv_.reset(new NativeServer(&l_, cfg));
     srv_->set_binds_enabled(binds_enabled_);
@@ -279,6 +287,75 @@ class Engine {
       throw std::runtime_error(err);
     }
     return p;
+  }
+
+  // ---- native controller (controller.h): reflectors -> ledger ----
+  void start_controller(const py::dict& api, double resync_s, double sync_timeout_s, int watch_timeout_s) {
+    if (ctl_) throw std::runtime_error("native controller already running");
+    ControllerConfig cfg;
+    cfg.api = api_from(api);
+    cfg.resync_s = resync_s;
+    cfg.watch_timeout_s = watch_timeout_s;
+    ctl_.reset(new Controller(&l_, cfg));
+    std::string err;
+    bool ok;
+    {
+      py::gil_scoped_release rel;
+      ok = ctl_->start(sync_timeout_s, &err);
+    }
+    if (!ok) {
+      {
+        py::gil_scoped_release rel;
+        ctl_->stop();
+      }
+      ctl_.reset();
+      throw std::runtime_error(err);
+    }
+  }
+
+  void stop_controller() {
+    if (ctl_) {
+      py::gil_scoped_release rel;
+      ctl_->stop();
+    }
+    ctl_.reset();
+  }
+
+  bool controller_synced() const { return ctl_ && ctl_->synced(); }
+
+  py::object controller_get_pod(const std::string& key) {
+    std::string raw;
+    if (!ctl_ || !ctl_->get_pod(key, &raw)) return py::none();
+    return py::bytes(raw);
+  }
+
+  py::list controller_overcommitted() {
+    py::list out;
+    if (!ctl_) return out;
+    for (auto& t : ctl_->overcommitted()) {
+      out.append(py::make_tuple(std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)));
+    }
+    return out;
+  }
+
+  py::dict controller_stats() {
+    py::dict d;
+    if (!ctl_) return d;
+    ControllerStats s = ctl_->stats();
+    d["pod_events"] = s.pod_events;
+    d["node_events"] = s.node_events;
+    d["syncs"] = s.syncs;
+    d["removes"] = s.removes;
+    d["upserts"] = s.upserts;
+    d["pod_lists"] = s.pod_lists;
+    d["node_lists"] = s.node_lists;
+    d["pod_rewatches"] = s.pod_watches;
+    d["node_rewatches"] = s.node_watches;
+    d["watch_errors"] = s.watch_errors;
+    d["resyncs"] = s.resyncs;
+    d["recovered"] = s.recovered;
+    d["last_error"] = ctl_->last_error();
+    return d;
   }
 
   void stop_server() {
@@ -346,7 +423,10 @@ class Engine {
     return l_.pending_count();
   }
 
-  ~Engine() { stop_server(); }
+  ~Engine() {
+    stop_server();
+    stop_controller();
+  }
 
   PodView parse_pod(const py::bytes& b) {
     PodView v;
@@ -358,7 +438,61 @@ class Engine {
  private:
   Ledger l_;
   std::unique_ptr<NativeServer> srv_;  // declared after l_: destroyed (stopped) first
+  std::unique_ptr<Controller> ctl_;
   bool binds_enabled_ = true;
+};
+
+}  // namespace
+
+namespace {
+
+// Benchmark wave-driver helpers (tracker.h); blocking calls drop the GIL.
+class PyPodTracker {
+ public:
+  PyPodTracker(const py::dict& api, const std::string& ns, const std::string& label_selector)
+      : t_(api_from(api), ns, label_selector) {}
+  void start(double timeout) {
+    std::string err;
+    bool ok;
+    {
+      py::gil_scoped_release rel;
+      ok = t_.start(timeout, &err);
+    }
+    if (!ok) throw std::runtime_error(err);
+  }
+  void stop() {
+    py::gil_scoped_release rel;
+    t_.stop();
+  }
+  std::string wait(const std::vector<std::string>& keys, int cond, double timeout) {
+    py::gil_scoped_release rel;
+    return t_.wait(keys, cond, timeout);
+  }
+  size_t size() const { return t_.size(); }
+
+ private:
+  PodTracker t_;
+};
+
+class PyBatchClient {
+ public:
+  explicit PyBatchClient(const py::dict& api) : c_(api_from(api)) {}
+  py::list run(const std::vector<std::tuple<std::string, std::string, py::bytes>>& reqs, int concurrency) {
+    std::vector<std::tuple<std::string, std::string, std::string>> rq;
+    rq.reserve(reqs.size());
+    for (const auto& r : reqs) rq.emplace_back(std::get<0>(r), std::get<1>(r), std::string(std::get<2>(r)));
+    std::vector<std::pair<int, std::string>> out;
+    {
+      py::gil_scoped_release rel;
+      out = c_.run(rq, concurrency);
+    }
+    py::list l;
+    for (auto& o : out) l.append(py::make_tuple(o.first, py::bytes(o.second)));
+    return l;
+  }
+
+ private:
+  BatchClient c_;
 };
 
 }  // namespace
@@ -420,10 +554,31 @@ PYBIND11_MODULE(_engine, m) {
            py::arg("pool_threads") = 16, py::arg("fallback_port") = 0, py::arg("native_bind") = true,
            py::arg("ttl") = 60.0, py::arg("api") = py::dict())
       .def("stop_server", &Engine::stop_server)
+      .def("start_controller", &Engine::start_controller, py::arg("api"), py::arg("resync") = 30.0,
+           py::arg("sync_timeout") = 60.0, py::arg("watch_timeout") = 300)
+      .def("stop_controller", &Engine::stop_controller)
+      .def("controller_synced", &Engine::controller_synced)
+      .def("controller_get_pod", &Engine::controller_get_pod)
+      .def("controller_overcommitted", &Engine::controller_overcommitted)
+      .def("controller_stats", &Engine::controller_stats)
       .def("server_stats", &Engine::server_stats)
       .def("drain_bind_failures", &Engine::drain_bind_failures)
       .def("set_binds_enabled", &Engine::set_binds_enabled)
       .def("pending_count", &Engine::pending_count);
+
+  py::class_<PyPodTracker>(m, "PodTracker")
+      .def(py::init<const py::dict&, const std::string&, const std::string&>(), py::arg("api"),
+           py::arg("namespace") = std::string(), py::arg("label_selector") = std::string())
+      .def("start", &PyPodTracker::start, py::arg("timeout") = 30.0)
+      .def("stop", &PyPodTracker::stop)
+      .def("wait", &PyPodTracker::wait, py::arg("keys"), py::arg("cond"), py::arg("timeout") = 120.0)
+      .def("size", &PyPodTracker::size);
+  m.attr("TRACK_BOUND") = static_cast<int>(PodTracker::Bound);
+  m.attr("TRACK_RUNNING") = static_cast<int>(PodTracker::Running);
+  m.attr("TRACK_GONE") = static_cast<int>(PodTracker::Gone);
+  py::class_<PyBatchClient>(m, "BatchClient")
+      .def(py::init<const py::dict&>())
+      .def("run", &PyBatchClient::run, py::arg("requests"), py::arg("concurrency") = 8);
 
   m.def("parse_quantity", [](const std::string& s) {
     int64_t v;

@@ -1,0 +1,47 @@
+// Small blocking HTTP/1.1 server for low-rate control endpoints of the native
+// tools (scheduler simulator timings / stats).  One thread per connection,
+// keep-alive, request handler called serially per connection.  The extender's
+// own hot verbs are served by NativeServer (server.h), not by this.
+#pragma once
+
+#include <atomic>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "http.h"
+
+namespace gsx {
+
+class CtlServer {
+ public:
+  // Handler: request -> (status, content type, body).
+  struct Reply {
+    int status = 200;
+    std::string content_type = "application/json";
+    std::string body;
+  };
+  using Handler = std::function<Reply(const http::Message&)>;
+
+  explicit CtlServer(Handler h) : h_(std::move(h)) {}
+  ~CtlServer() { stop(); }
+  // Returns the bound port or -1 (*err).
+  int start(const std::string& host, int port, std::string* err);
+  void stop();
+
+ private:
+  void accept_loop();
+  void serve_conn(int fd);
+
+  Handler h_;
+  int lfd_ = -1;
+  std::atomic<bool> stop_{false};
+  std::thread acc_;
+  std::mutex mu_;
+  std::vector<int> conns_;
+  std::vector<std::thread> threads_;
+};
+
+}  // namespace gsx

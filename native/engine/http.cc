@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 
 namespace gsx {
 namespace http {
@@ -59,7 +60,8 @@ std::string_view Message::path() const {
   return q == std::string_view::npos ? t : t.substr(0, q);
 }
 
-long parse(const char* buf, size_t n, bool is_request, Message* out, std::string* err, bool eof, size_t max_body) {
+long parse_head(const char* buf, size_t n, bool is_request, Message* out, std::string* err, long* content_length,
+                bool* chunked) {
   std::string_view s(buf, n);
   size_t hend = s.find("\r\n\r\n");
   if (hend == std::string_view::npos) {
@@ -100,8 +102,8 @@ long parse(const char* buf, size_t n, bool is_request, Message* out, std::string
   }
   // headers
   size_t pos = le == std::string_view::npos ? head.size() : le + 2;
-  long content_length = -1;
-  bool chunked = false;
+  *content_length = -1;
+  *chunked = false;
   bool conn_close = false, conn_keep = false;
   while (pos < head.size()) {
     size_t e = head.find("\r\n", pos);
@@ -122,9 +124,9 @@ long parse(const char* buf, size_t n, bool is_request, Message* out, std::string
         *err = "bad content-length";
         return -1;
       }
-      content_length = cl;
+      *content_length = cl;
     } else if (name == "transfer-encoding") {
-      chunked = contains_token(val, "chunked");
+      *chunked = contains_token(val, "chunked");
     } else if (name == "connection") {
       conn_close = contains_token(val, "close");
       conn_keep = contains_token(val, "keep-alive");
@@ -133,7 +135,16 @@ long parse(const char* buf, size_t n, bool is_request, Message* out, std::string
     pos = e + 2;
   }
   out->keep_alive = out->minor_version >= 1 ? !conn_close : conn_keep;
-  size_t body_start = hend + 4;
+  return static_cast<long>(hend + 4);
+}
+
+long parse(const char* buf, size_t n, bool is_request, Message* out, std::string* err, bool eof, size_t max_body) {
+  std::string_view s(buf, n);
+  long content_length = -1;
+  bool chunked = false;
+  long hl = parse_head(buf, n, is_request, out, err, &content_length, &chunked);
+  if (hl <= 0) return hl;
+  size_t body_start = static_cast<size_t>(hl);
   if (chunked) {
     size_t p = body_start;
     std::string body;
@@ -191,6 +202,68 @@ long parse(const char* buf, size_t n, bool is_request, Message* out, std::string
   if (!eof) return 0;
   out->body.assign(buf + body_start, n - body_start);
   return static_cast<long>(n);
+}
+
+
+int Dechunker::feed(const char* data, size_t n, const std::function<void(std::string_view)>& out) {
+  size_t i = 0;
+  while (i < n) {
+    switch (state_) {
+      case State::Size: {
+        char c = data[i++];
+        if (c == '\n') {
+          // size line complete (ignore extensions after ';')
+          size_t semi = line_.find(';');
+          if (semi != std::string::npos) line_.resize(semi);
+          while (!line_.empty() && (line_.back() == '\r' || line_.back() == ' ')) line_.pop_back();
+          if (line_.empty()) return -1;
+          char* endp = nullptr;
+          unsigned long long sz = std::strtoull(line_.c_str(), &endp, 16);
+          if (endp == line_.c_str() || *endp) return -1;
+          line_.clear();
+          remaining_ = sz;
+          state_ = sz == 0 ? State::Trailer : State::Data;
+        } else {
+          if (line_.size() > 64) return -1;
+          line_.push_back(c);
+        }
+        break;
+      }
+      case State::Data: {
+        size_t take = static_cast<size_t>(std::min<unsigned long long>(remaining_, n - i));
+        out(std::string_view(data + i, take));
+        i += take;
+        remaining_ -= take;
+        if (remaining_ == 0) state_ = State::DataEnd;
+        break;
+      }
+      case State::DataEnd: {
+        char c = data[i++];
+        if (c == '\n') {
+          state_ = State::Size;
+        } else if (c != '\r') {
+          return -1;
+        }
+        break;
+      }
+      case State::Trailer: {
+        char c = data[i++];
+        if (c == '\n') {
+          if (line_.empty() || line_ == "\r") {
+            state_ = State::Done;
+            return 1;
+          }
+          line_.clear();
+        } else {
+          line_.push_back(c);
+        }
+        break;
+      }
+      case State::Done:
+        return 1;
+    }
+  }
+  return state_ == State::Done ? 1 : 0;
 }
 
 const char* reason_phrase(int status) {

@@ -8,6 +8,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <string_view>
 #include <utility>
@@ -39,6 +40,27 @@ struct Message {
 // `eof` tells the parser the peer closed (completes read-to-close bodies).
 long parse(const char* buf, size_t n, bool is_request, Message* out, std::string* err, bool eof = false,
            size_t max_body = 64u << 20);
+
+// Parse only the start line + headers.  Returns the head length (> 0), 0 if
+// more input is needed, -1 if malformed.  *content_length = -1 when absent.
+long parse_head(const char* buf, size_t n, bool is_request, Message* out, std::string* err, long* content_length,
+                bool* chunked);
+
+// Incremental Transfer-Encoding: chunked decoder for streamed bodies (watch
+// responses).  feed() passes decoded bytes to `out`; returns 1 once the
+// terminating chunk (and trailers) were consumed, 0 if more input is needed,
+// -1 on malformed framing.
+class Dechunker {
+ public:
+  int feed(const char* data, size_t n, const std::function<void(std::string_view)>& out);
+  bool done() const { return state_ == State::Done; }
+
+ private:
+  enum class State { Size, Data, DataEnd, Trailer, Done };
+  State state_ = State::Size;
+  std::string line_;
+  unsigned long long remaining_ = 0;
+};
 
 // Serialise a response.
 std::string response(int status, std::string_view content_type, std::string_view body, bool keep_alive,

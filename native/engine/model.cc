@@ -48,6 +48,21 @@ int64_t pod_limits_sum(const json::Doc& d, uint32_t pod, const std::string& name
   return total;
 }
 
+Profile profile_by_name(const std::string& name) {
+  Profile p;
+  if (name == "aliyun") {
+    p.resource = "aliyun.com/gpu-mem";
+    p.count = "aliyun.com/gpu-count";
+    p.a_idx = "ALIYUN_COM_GPU_MEM_IDX";
+    p.a_pod = "ALIYUN_COM_GPU_MEM_POD";
+    p.a_dev = "ALIYUN_COM_GPU_MEM_DEV";
+    p.a_assigned = "ALIYUN_COM_GPU_MEM_ASSIGNED";
+    p.a_assume = "ALIYUN_COM_GPU_MEM_ASSUME_TIME";
+    p.env_container = "ALIYUN_COM_GPU_MEM_CONTAINER";
+  }
+  return p;
+}
+
 bool parse_pod(const json::Doc& d, uint32_t pod, const Profile& p, PodView* out) {
   if (pod >= d.size() || d.at(pod).type != json::T::Object) return false;
   int64_t meta = d.find(pod, "metadata");

@@ -28,7 +28,12 @@ struct Profile {
   // ("268,268,...") so heterogeneous / partitioned devices are exact instead
   // of capacity/count integer division (reference pkg/cache/nodeinfo.go:34).
   std::string a_node_devs = "gpushare.amd.com/device-memory";
+  // container env with the container's share (samples/docker/run.sh:3-6)
+  std::string env_container = "SHARED_GPU_MEM_CONTAINER";
 };
+
+// "shared-gpu" (default, pkg/utils/const.go) or "aliyun" (docs/designs/bind.jpg).
+Profile profile_by_name(const std::string& name);
 
 struct PodView {
   std::string uid, name, ns, node, phase, rv;

@@ -1,0 +1,1194 @@
+// gsx-fakeapi: fake kube-apiserver in C++ (pods, nodes, events, leases,
+// bindings) -- the compiled counterpart of k8s/fakeapi.py with the same REST
+// subset and semantics, for benchmarks where the asyncio one would be the
+// bottleneck (a real kube-apiserver is compiled Go in front of etcd):
+//
+//   * LIST + chunked WATCH with resourceVersion (one global counter, as etcd
+//     gives kube-apiserver), 410 Gone for compacted history, field selectors
+//     (dotted paths, = / !=) and label selectors (=, !=, exists, !exists);
+//   * optimistic concurrency on PUT / PATCH (409 with client-go's exact
+//     message, pkg/cache/nodeinfo.go:14-16), server-owned metadata;
+//   * POST pods/<name>/binding sets spec.nodeName once and merges the
+//     Binding's annotations into the pod (kube-apiserver's
+//     setPodHostAndAnnotations), plus a PodScheduled condition;
+//   * JSON merge patch (strategic merge patch treated as merge patch),
+//     graceful pod deletion, DeleteCollection with selectors;
+//   * fault injection (POST /fake/faults): conflict_rate, error_rate,
+//     latency_ms, drop_watch_after, expire_watches, hold_watches,
+//     drop_watches_now; GET /fake/stats.
+//
+// One epoll thread owns all state (like the etcd-serialised apiserver); watch
+// events produced while handling a batch of requests go out as one chunk per
+// watcher per loop iteration.
+//
+//   gsx-fakeapi [--host 127.0.0.1] [--port 0] [--port-file F] [--history N]
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <deque>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <random>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "http.h"
+#include "jdom.h"
+#include "json.h"
+
+using namespace gsx;
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+std::string now_iso() {
+  time_t t = time(nullptr);
+  struct tm tmv;
+  gmtime_r(&t, &tmv);
+  char b[32];
+  strftime(b, sizeof(b), "%Y-%m-%dT%H:%M:%SZ", &tmv);
+  return b;
+}
+
+std::mt19937_64& rng() {
+  static std::mt19937_64 r(std::random_device{}());
+  return r;
+}
+
+std::string uuid4() {
+  uint64_t a = rng()(), b = rng()();
+  a = (a & 0xffffffffffff0fffull) | 0x0000000000004000ull;
+  b = (b & 0x3fffffffffffffffull) | 0x8000000000000000ull;
+  char s[40];
+  std::snprintf(s, sizeof(s), "%08x-%04x-%04x-%04x-%012llx", static_cast<unsigned>(a >> 32),
+                static_cast<unsigned>((a >> 16) & 0xffff), static_cast<unsigned>(a & 0xffff),
+                static_cast<unsigned>(b >> 48), static_cast<unsigned long long>(b & 0xffffffffffffull));
+  return s;
+}
+
+std::string url_unescape(std::string_view s) {
+  std::string o;
+  o.reserve(s.size());
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size()) {
+      o.push_back(static_cast<char>(std::strtol(std::string(s.substr(i + 1, 2)).c_str(), nullptr, 16)));
+      i += 2;
+    } else if (s[i] == '+') {
+      o.push_back(' ');
+    } else {
+      o.push_back(s[i]);
+    }
+  }
+  return o;
+}
+
+std::map<std::string, std::string> parse_query(std::string_view target) {
+  std::map<std::string, std::string> q;
+  size_t qm = target.find('?');
+  if (qm == std::string_view::npos) return q;
+  std::string_view s = target.substr(qm + 1);
+  size_t i = 0;
+  while (i <= s.size()) {
+    size_t j = s.find('&', i);
+    if (j == std::string_view::npos) j = s.size();
+    std::string_view kv = s.substr(i, j - i);
+    size_t eq = kv.find('=');
+    if (!kv.empty()) {
+      q[url_unescape(kv.substr(0, eq))] = eq == std::string_view::npos ? "" : url_unescape(kv.substr(eq + 1));
+    }
+    i = j + 1;
+  }
+  return q;
+}
+
+std::vector<std::string> split(std::string_view s, char c) {
+  std::vector<std::string> out;
+  size_t i = 0;
+  while (i <= s.size()) {
+    size_t j = s.find(c, i);
+    if (j == std::string_view::npos) j = s.size();
+    out.emplace_back(s.substr(i, j - i));
+    i = j + 1;
+  }
+  return out;
+}
+
+std::string trim(std::string s) {
+  while (!s.empty() && s.back() == ' ') s.pop_back();
+  size_t i = 0;
+  while (i < s.size() && s[i] == ' ') ++i;
+  return s.substr(i);
+}
+
+bool label_match(const jd::Value& obj, const std::string& sel) {
+  if (sel.empty()) return true;
+  const jd::Value* md = obj.get("metadata");
+  const jd::Value* labels = md ? md->get("labels") : nullptr;
+  auto lab = [&](const std::string& k) -> const jd::Value* { return labels ? labels->get(k) : nullptr; };
+  for (std::string term : split(sel, ',')) {
+    term = trim(term);
+    if (term.empty()) continue;
+    size_t ne = term.find("!=");
+    if (ne != std::string::npos) {
+      const jd::Value* v = lab(trim(term.substr(0, ne)));
+      if (v && v->is_str() && v->s == trim(term.substr(ne + 2))) return false;
+      continue;
+    }
+    size_t eq = term.find('=');
+    if (eq != std::string::npos) {
+      std::string k = trim(term.substr(0, eq));
+      std::string val = term.substr(eq + 1);
+      if (!val.empty() && val[0] == '=') val.erase(0, 1);  // "=="
+      const jd::Value* v = lab(k);
+      if (!v || !v->is_str() || v->s != trim(val)) return false;
+      continue;
+    }
+    if (term[0] == '!') {
+      if (lab(term.substr(1))) return false;
+    } else if (!lab(term)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+bool field_match(const jd::Value& obj, const std::string& sel) {
+  if (sel.empty()) return true;
+  for (std::string term : split(sel, ',')) {
+    term = trim(term);
+    if (term.empty()) continue;
+    size_t ne = term.find("!=");
+    if (ne != std::string::npos) {
+      const jd::Value* v = obj.at_path(trim(term.substr(0, ne)));
+      if ((v ? v->scalar_text() : std::string()) == trim(term.substr(ne + 2))) return false;
+      continue;
+    }
+    size_t eq = term.find('=');
+    if (eq == std::string::npos) return false;
+    std::string k = trim(term.substr(0, eq));
+    std::string val = term.substr(eq + 1);
+    if (!val.empty() && val[0] == '=') val.erase(0, 1);
+    const jd::Value* v = obj.at_path(k);
+    if ((v ? v->scalar_text() : std::string()) != trim(val)) return false;
+  }
+  return true;
+}
+
+std::string status_body(int code, const std::string& reason, const std::string& message, const std::string& name = "",
+                        const std::string& kind = "") {
+  std::string o = "{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"metadata\":{},\"status\":\"Failure\",\"message\":";
+  json::append_quoted(&o, message);
+  o.append(",\"reason\":");
+  json::append_quoted(&o, reason);
+  o.append(",\"code\":").append(std::to_string(code));
+  if (!name.empty()) {
+    o.append(",\"details\":{\"name\":");
+    json::append_quoted(&o, name);
+    o.append(",\"kind\":");
+    json::append_quoted(&o, kind);
+    o.push_back('}');
+  }
+  o.push_back('}');
+  return o;
+}
+
+struct HttpError {
+  int code;
+  std::string body;
+};
+
+HttpError conflict(const std::string& kind, const std::string& name) {
+  return {409, status_body(409, "Conflict",
+                           "Operation cannot be fulfilled on " + kind + " \"" + name +
+                               "\": the object has been modified; please apply your changes to the latest version and "
+                               "try again",
+                           name, kind)};
+}
+
+HttpError not_found(const std::string& kind, const std::string& name) {
+  return {404, status_body(404, "NotFound", kind + " \"" + name + "\" not found", name, kind)};
+}
+
+// A stored object: immutable once stored (writes replace the pointer), with
+// its serialisation cached for GET / LIST / watch / write responses.
+struct Obj {
+  jd::Value v;
+  std::string json;
+  std::string ns, name;
+};
+using ObjP = std::shared_ptr<const Obj>;
+
+ObjP make_obj(jd::Value v) {
+  auto o = std::make_shared<Obj>();
+  const jd::Value* md = v.get("metadata");
+  if (md) {
+    o->ns = md->str_or("namespace");
+    o->name = md->str_or("name");
+  }
+  o->v = std::move(v);
+  o->json = jd::dump(o->v);
+  return o;
+}
+
+struct Event {
+  int64_t rv;
+  std::string kind;
+  std::shared_ptr<const std::string> line;
+  ObjP obj;
+};
+
+struct Watcher;
+
+struct Conn {
+  int fd = -1;
+  uint64_t id = 0;
+  std::string rbuf, wbuf;
+  bool want_close = false;
+  bool busy = false;           // a delayed response is pending
+  Watcher* watch = nullptr;    // streaming
+  bool epollout = false;
+};
+
+struct Watcher {
+  uint64_t conn_id;
+  std::string kind, ns, fsel, lsel;
+  std::string pending;
+  uint64_t sent = 0, drop_after = 0;
+  double deadline = 0;  // 0: none
+  bool closed = false;
+};
+
+struct Faults {
+  double conflict_rate = 0, error_rate = 0, latency_ms = 0;
+  int64_t drop_watch_after = 0, expire_watches = 0;
+  bool hold_watches = false;
+  std::string json() const {
+    char b[320];
+    std::snprintf(b, sizeof(b),
+                  "{\"conflict_rate\":%g,\"error_rate\":%g,\"latency_ms\":%g,\"drop_watch_after\":%lld,"
+                  "\"expire_watches\":%lld,\"hold_watches\":%s}",
+                  conflict_rate, error_rate, latency_ms, (long long)drop_watch_after, (long long)expire_watches,
+                  hold_watches ? "true" : "false");
+    return b;
+  }
+};
+
+struct Reply {
+  int status = 200;
+  std::string body;
+  const char* ct = "application/json";
+};
+
+class Server {
+ public:
+  explicit Server(size_t history) : history_max_(history) {
+    for (const char* k : {"pods", "nodes", "events", "leases"}) store_[k];
+  }
+
+  int listen_on(const std::string& host, int port, std::string* err) {
+    lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    int one = 1;
+    setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in a;
+    std::memset(&a, 0, sizeof(a));
+    a.sin_family = AF_INET;
+    a.sin_port = htons(static_cast<uint16_t>(port));
+    inet_pton(AF_INET, host.c_str(), &a.sin_addr);
+    if (::bind(lfd_, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || ::listen(lfd_, 1024) != 0) {
+      *err = std::string("bind/listen: ") + std::strerror(errno);
+      return -1;
+    }
+    socklen_t len = sizeof(a);
+    getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &len);
+    ep_ = epoll_create1(EPOLL_CLOEXEC);
+    epoll_event ev;
+    ev.events = EPOLLIN;
+    ev.data.u64 = 0;
+    epoll_ctl(ep_, EPOLL_CTL_ADD, lfd_, &ev);
+    return ntohs(a.sin_port);
+  }
+
+  void run(volatile sig_atomic_t* stop) {
+    std::vector<epoll_event> evs(256);
+    while (!*stop) {
+      int timeout = next_timeout_ms();
+      int n = epoll_wait(ep_, evs.data(), static_cast<int>(evs.size()), timeout);
+      for (int i = 0; i < n; ++i) {
+        uint64_t id = evs[i].data.u64;
+        if (id == 0) {
+          accept_all();
+          continue;
+        }
+        auto it = conns_.find(id);
+        if (it == conns_.end()) continue;
+        Conn* c = it->second.get();
+        if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
+          close_conn(c);
+          continue;
+        }
+        if (evs[i].events & EPOLLIN) on_readable(c);
+        if (conns_.count(id) && (evs[i].events & EPOLLOUT)) flush_conn(c);
+      }
+      run_timers();
+      flush_watchers();
+    }
+  }
+
+ private:
+  // ---------------------------------------------------------------- connections
+  void accept_all() {
+    while (true) {
+      int fd = ::accept4(lfd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+      if (fd < 0) return;
+      int one = 1;
+      setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+      auto c = std::make_unique<Conn>();
+      c->fd = fd;
+      c->id = ++next_id_;
+      epoll_event ev;
+      ev.events = EPOLLIN | EPOLLRDHUP;
+      ev.data.u64 = c->id;
+      epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &ev);
+      conns_[c->id] = std::move(c);
+    }
+  }
+
+  void close_conn(Conn* c) {
+    if (c->watch) {
+      c->watch->closed = true;
+      c->watch = nullptr;
+    }
+    epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
+    ::close(c->fd);
+    conns_.erase(c->id);
+  }
+
+  void on_readable(Conn* c) {
+    char buf[65536];
+    while (true) {
+      long r = ::recv(c->fd, buf, sizeof(buf), 0);
+      if (r > 0) {
+        c->rbuf.append(buf, static_cast<size_t>(r));
+        continue;
+      }
+      if (r == 0) {
+        close_conn(c);
+        return;
+      }
+      if (errno == EINTR) continue;
+      break;  // EAGAIN
+    }
+    process(c);
+  }
+
+  void process(Conn* c) {
+    uint64_t id = c->id;
+    while (!c->busy && !c->watch && !c->rbuf.empty()) {
+      http::Message req;
+      std::string perr;
+      long got = http::parse(c->rbuf.data(), c->rbuf.size(), true, &req, &perr);
+      if (got == 0) return;
+      if (got < 0) {
+        respond(c, Reply{400, status_body(400, "BadRequest", perr)}, false);
+        return;
+      }
+      c->rbuf.erase(0, static_cast<size_t>(got));
+      counts_[req.method]++;
+      bool is_watch = false;
+      {
+        auto q = parse_query(req.target);
+        auto w = q.find("watch");
+        is_watch = w != q.end() && (w->second == "1" || w->second == "true");
+      }
+      if (faults_.latency_ms > 0 && !is_watch) {
+        c->busy = true;
+        delayed_.push_back({now_s() + faults_.latency_ms / 1000.0, id, std::move(req)});
+        return;
+      }
+      handle(c, req);
+      if (!conns_.count(id)) return;
+    }
+  }
+
+  void handle(Conn* c, http::Message& req) {
+    Reply rep;
+    try {
+      if (!route(c, req, &rep)) return;  // became a watch stream (or is held)
+    } catch (const HttpError& e) {
+      rep.status = e.code;
+      rep.body = e.body;
+    }
+    respond(c, rep, req.keep_alive);
+  }
+
+  void respond(Conn* c, const Reply& r, bool keep_alive) {
+    c->wbuf.append(http::response(r.status, r.ct, r.body, keep_alive));
+    if (!keep_alive) c->want_close = true;
+    flush_conn(c);
+  }
+
+  void flush_conn(Conn* c) {
+    while (!c->wbuf.empty()) {
+      long w = ::send(c->fd, c->wbuf.data(), c->wbuf.size(), MSG_NOSIGNAL);
+      if (w > 0) {
+        c->wbuf.erase(0, static_cast<size_t>(w));
+        continue;
+      }
+      if (w < 0 && errno == EINTR) continue;
+      if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        if (!c->epollout) {
+          epoll_event ev;
+          ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
+          ev.data.u64 = c->id;
+          epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
+          c->epollout = true;
+        }
+        return;
+      }
+      close_conn(c);
+      return;
+    }
+    if (c->epollout) {
+      epoll_event ev;
+      ev.events = EPOLLIN | EPOLLRDHUP;
+      ev.data.u64 = c->id;
+      epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
+      c->epollout = false;
+    }
+    if (c->want_close) close_conn(c);
+  }
+
+  // ---------------------------------------------------------------- timers
+  int next_timeout_ms() {
+    double next = now_s() + 1.0;
+    for (auto& d : delayed_) next = std::min(next, d.due);
+    for (auto& g : graces_) next = std::min(next, g.due);
+    for (auto& w : watchers_) {
+      if (w->deadline > 0) next = std::min(next, w->deadline);
+    }
+    if (!held_.empty()) next = std::min(next, now_s() + 0.005);
+    double ms = (next - now_s()) * 1000.0;
+    return ms <= 0 ? 0 : static_cast<int>(ms) + 1;
+  }
+
+  void run_timers() {
+    double now = now_s();
+    if (!delayed_.empty()) {
+      std::vector<Delayed> due;
+      for (auto it = delayed_.begin(); it != delayed_.end();) {
+        if (it->due <= now) {
+          due.push_back(std::move(*it));
+          it = delayed_.erase(it);
+        } else {
+          ++it;
+        }
+      }
+      for (auto& d : due) {
+        auto it = conns_.find(d.conn);
+        if (it == conns_.end()) continue;
+        Conn* c = it->second.get();
+        c->busy = false;
+        handle(c, d.req);
+        if (conns_.count(d.conn)) process(c);
+      }
+    }
+    if (!graces_.empty()) {
+      std::vector<Grace> due;
+      for (auto it = graces_.begin(); it != graces_.end();) {
+        if (it->due <= now) {
+          due.push_back(*it);
+          it = graces_.erase(it);
+        } else {
+          ++it;
+        }
+      }
+      for (auto& g : due) {
+        auto& m = store_[g.kind];
+        auto it = m.find({g.ns, g.name});
+        if (it != m.end()) {
+          const jd::Value* md = it->second->v.get("metadata");
+          if (md && md->str_or("uid") == g.uid) do_delete(g.kind, g.ns, g.name, -1);
+        }
+      }
+    }
+    for (auto& w : watchers_) {
+      if (!w->closed && w->deadline > 0 && w->deadline <= now) end_watch(w.get());
+    }
+    if (!held_.empty() && !faults_.hold_watches) {
+      auto held = std::move(held_);
+      held_.clear();
+      for (auto& h : held) {
+        auto it = conns_.find(h.conn);
+        if (it == conns_.end()) continue;
+        Conn* c = it->second.get();
+        c->busy = false;
+        handle(c, h.req);
+        if (conns_.count(h.conn)) process(c);
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- watch
+  void emit(const std::string& kind, const char* etype, const ObjP& o) {
+    const jd::Value* md = o->v.get("metadata");
+    int64_t rv = md ? std::atoll(md->str_or("resourceVersion").c_str()) : 0;
+    auto line = std::make_shared<std::string>();
+    line->reserve(o->json.size() + 32);
+    line->append("{\"type\":\"").append(etype).append("\",\"object\":").append(o->json).append("}\n");
+    if (history_.size() >= history_max_) {
+      oldest_rv_ = history_.front().rv;  // watches from before this are told 410 Gone
+      history_.pop_front();
+    }
+    history_.push_back(Event{rv, kind, line, o});
+    for (auto& w : watchers_) {
+      if (!w->closed && w->kind == kind && wants(*w, *o)) w->pending.append(*line);
+    }
+  }
+
+  bool wants(const Watcher& w, const Obj& o) const {
+    if (!w.ns.empty() && o.ns != w.ns) return false;
+    return field_match(o.v, w.fsel) && label_match(o.v, w.lsel);
+  }
+
+  void flush_watchers() {
+    for (auto& w : watchers_) {
+      if (w->closed || w->pending.empty()) continue;
+      auto it = conns_.find(w->conn_id);
+      if (it == conns_.end()) {
+        w->closed = true;
+        continue;
+      }
+      Conn* c = it->second.get();
+      // one chunk per loop iteration; count events for drop_watch_after
+      size_t events = static_cast<size_t>(std::count(w->pending.begin(), w->pending.end(), '\n'));
+      char hdr[32];
+      std::snprintf(hdr, sizeof(hdr), "%zx\r\n", w->pending.size());
+      c->wbuf.append(hdr).append(w->pending).append("\r\n");
+      w->pending.clear();
+      w->sent += events;
+      if (w->drop_after && w->sent >= w->drop_after) {
+        counts_["watch_dropped"]++;
+        end_watch(w.get());
+        continue;
+      }
+      flush_conn(c);
+    }
+    watchers_.erase(std::remove_if(watchers_.begin(), watchers_.end(), [](const std::unique_ptr<Watcher>& w) {
+                      return w->closed;
+                    }),
+                    watchers_.end());
+  }
+
+  void end_watch(Watcher* w) {
+    if (w->closed) return;
+    w->closed = true;
+    auto it = conns_.find(w->conn_id);
+    if (it == conns_.end()) return;
+    Conn* c = it->second.get();
+    c->watch = nullptr;
+    if (!w->pending.empty()) {
+      char hdr[32];
+      std::snprintf(hdr, sizeof(hdr), "%zx\r\n", w->pending.size());
+      c->wbuf.append(hdr).append(w->pending).append("\r\n");
+    }
+    c->wbuf.append("0\r\n\r\n");
+    c->want_close = true;
+    flush_conn(c);
+  }
+
+  // Returns false when the request became a (held) watch stream.
+  bool start_watch(Conn* c, const http::Message& req, const std::string& kind, const std::string& ns,
+                   const std::map<std::string, std::string>& q) {
+    if (faults_.hold_watches) {
+      c->busy = true;
+      held_.push_back({c->id, req});
+      return false;
+    }
+    std::string head = "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n";
+    auto get = [&](const char* k) {
+      auto it = q.find(k);
+      return it == q.end() ? std::string() : it->second;
+    };
+    if (faults_.expire_watches > 0) {
+      faults_.expire_watches--;
+      counts_["watch_expired"]++;
+      std::string line = "{\"type\":\"ERROR\",\"object\":" +
+                         status_body(410, "Expired", "too old resource version (injected)") + "}\n";
+      char hdr[32];
+      std::snprintf(hdr, sizeof(hdr), "%zx\r\n", line.size());
+      c->wbuf.append(head).append(hdr).append(line).append("\r\n0\r\n\r\n");
+      c->want_close = true;
+      flush_conn(c);
+      return false;
+    }
+    auto w = std::make_unique<Watcher>();
+    w->conn_id = c->id;
+    w->kind = kind;
+    w->ns = ns;
+    w->fsel = get("fieldSelector");
+    w->lsel = get("labelSelector");
+    w->drop_after = static_cast<uint64_t>(std::max<int64_t>(0, faults_.drop_watch_after));
+    std::string to = get("timeoutSeconds");
+    if (!to.empty() && std::atof(to.c_str()) > 0) w->deadline = now_s() + std::atof(to.c_str());
+    std::string rvs = get("resourceVersion");
+    if (!rvs.empty() && rvs != "0") {
+      int64_t rv = std::atoll(rvs.c_str());
+      if (oldest_rv_ && rv < oldest_rv_) {
+        std::string line = "{\"type\":\"ERROR\",\"object\":" +
+                           status_body(410, "Expired", "too old resource version: " + std::to_string(rv) + " (" +
+                                                           std::to_string(oldest_rv_) + ")") +
+                           "}\n";
+        char hdr[32];
+        std::snprintf(hdr, sizeof(hdr), "%zx\r\n", line.size());
+        c->wbuf.append(head).append(hdr).append(line).append("\r\n0\r\n\r\n");
+        c->want_close = true;
+        flush_conn(c);
+        return false;
+      }
+      // backlog: history after rv (binary search: history is rv-ordered)
+      auto it = std::upper_bound(history_.begin(), history_.end(), rv,
+                                 [](int64_t v, const Event& e) { return v < e.rv; });
+      for (; it != history_.end(); ++it) {
+        if (it->kind == kind && wants(*w, *it->obj)) w->pending.append(*it->line);
+      }
+    } else {
+      for (auto& kv : store_[kind]) {
+        if (wants(*w, *kv.second)) {
+          w->pending.append("{\"type\":\"ADDED\",\"object\":").append(kv.second->json).append("}\n");
+        }
+      }
+    }
+    c->wbuf.append(head);
+    c->watch = w.get();
+    watchers_.push_back(std::move(w));
+    flush_conn(c);
+    return false;
+  }
+
+  // ---------------------------------------------------------------- store
+  using Key = std::pair<std::string, std::string>;
+  std::string bump() { return std::to_string(++rv_); }
+
+  ObjP get_obj(const std::string& kind, const std::string& ns, const std::string& name) {
+    auto& m = store_[kind];
+    auto it = m.find({kind == "nodes" ? std::string() : ns, name});
+    if (it == m.end()) throw not_found(kind, name);
+    return it->second;
+  }
+
+  void maybe_error() {
+    if (faults_.error_rate > 0 && std::uniform_real_distribution<double>(0, 1)(rng()) < faults_.error_rate) {
+      counts_["injected_error"]++;
+      throw HttpError{500, status_body(500, "InternalError", "injected fault")};
+    }
+  }
+
+  bool injected_conflict() {
+    if (faults_.conflict_rate > 0 && std::uniform_real_distribution<double>(0, 1)(rng()) < faults_.conflict_rate) {
+      counts_["injected_conflict"]++;
+      return true;
+    }
+    return false;
+  }
+
+  ObjP do_create(const std::string& kind, jd::Value obj, const std::string& ns) {
+    jd::Value& md = obj.member("metadata");
+    if (kind != "nodes") {
+      if (!ns.empty()) md.set("namespace", jd::Value::string(ns));
+      if (!md.get("namespace")) md.set("namespace", jd::Value::string("default"));
+    }
+    std::string name = md.str_or("name");
+    if (name.empty()) {
+      std::string gen = md.str_or("generateName");
+      if (gen.empty()) throw HttpError{422, status_body(422, "Invalid", "metadata.name: Required value")};
+      name = gen + uuid4().substr(0, 5);
+      md.set("name", jd::Value::string(name));
+    }
+    Key key{kind == "nodes" ? std::string() : md.str_or("namespace"), name};
+    auto& m = store_[kind];
+    if (m.count(key)) throw HttpError{409, status_body(409, "AlreadyExists", kind + " \"" + name + "\" already exists")};
+    if (md.str_or("uid").empty()) md.set("uid", jd::Value::string(uuid4()));
+    if (!md.get("creationTimestamp")) md.set("creationTimestamp", jd::Value::string(now_iso()));
+    if (kind == "pods") {
+      jd::Value& st = obj.member("status");
+      if (!st.get("phase")) st.set("phase", jd::Value::string("Pending"));
+      obj.member("spec");
+    }
+    md.set("resourceVersion", jd::Value::string(bump()));
+    ObjP o = make_obj(std::move(obj));
+    m[key] = o;
+    emit(kind, "ADDED", o);
+    return o;
+  }
+
+  static void keep_server_fields(const jd::Value& cur_md, jd::Value* md) {
+    for (const char* f : {"uid", "creationTimestamp", "namespace", "name", "deletionTimestamp"}) {
+      const jd::Value* v = cur_md.get(f);
+      if (v) md->set(f, *v);
+    }
+  }
+
+  ObjP do_replace(const std::string& kind, const std::string& ns, const std::string& name, jd::Value obj,
+                  const std::string& sub) {
+    ObjP cur = get_obj(kind, ns, name);
+    const jd::Value& cmd = *cur->v.get("metadata");
+    const jd::Value* omd = obj.get("metadata");
+    std::string want = omd ? omd->str_or("resourceVersion") : std::string();
+    if (!want.empty() && want != cmd.str_or("resourceVersion")) throw conflict(kind, name);
+    if (kind == "pods" && injected_conflict()) throw conflict(kind, name);
+    jd::Value nv;
+    if (sub == "status") {
+      nv = cur->v;
+      const jd::Value* st = obj.get("status");
+      nv.set("status", st ? *st : jd::Value::object());
+    } else {
+      nv = std::move(obj);
+      jd::Value& md = nv.member("metadata");
+      keep_server_fields(cmd, &md);
+      if (kind == "pods") {
+        const jd::Value* cs = cur->v.get("spec");
+        const jd::Value* on = cs ? cs->get("nodeName") : nullptr;
+        jd::Value& spec = nv.member("spec");
+        if (on && on->is_str() && !on->s.empty()) {
+          spec.set("nodeName", *on);
+        } else {
+          spec.erase("nodeName");
+        }
+        const jd::Value* cst = cur->v.get("status");
+        nv.set("status", cst ? *cst : jd::Value::object());
+      }
+    }
+    nv.member("metadata").set("resourceVersion", jd::Value::string(bump()));
+    ObjP o = make_obj(std::move(nv));
+    store_[kind][{kind == "nodes" ? std::string() : ns, name}] = o;
+    emit(kind, "MODIFIED", o);
+    return o;
+  }
+
+  ObjP do_patch(const std::string& kind, const std::string& ns, const std::string& name, jd::Value patch,
+                const std::string& sub) {
+    ObjP cur = get_obj(kind, ns, name);
+    const jd::Value& cmd = *cur->v.get("metadata");
+    const jd::Value* pmd = patch.get("metadata");
+    std::string want = pmd ? pmd->str_or("resourceVersion") : std::string();
+    if (!want.empty() && want != cmd.str_or("resourceVersion")) throw conflict(kind, name);
+    if (kind == "pods" && injected_conflict()) throw conflict(kind, name);
+    if (sub == "status") {
+      jd::Value p = jd::Value::object();
+      const jd::Value* st = patch.get("status");
+      p.set("status", st ? *st : jd::Value::object());
+      patch = std::move(p);
+    } else if (kind == "pods") {
+      jd::Value* spec = patch.get("spec");
+      if (spec && spec->is_obj()) spec->erase("nodeName");
+      if (sub.empty()) patch.erase("status");
+    }
+    jd::Value nv = cur->v;
+    jd::merge_patch(&nv, patch);
+    jd::Value& md = nv.member("metadata");
+    keep_server_fields(cmd, &md);
+    md.set("resourceVersion", jd::Value::string(bump()));
+    ObjP o = make_obj(std::move(nv));
+    store_[kind][{kind == "nodes" ? std::string() : ns, name}] = o;
+    emit(kind, "MODIFIED", o);
+    return o;
+  }
+
+  void do_bind(const std::string& ns, const std::string& name, const jd::Value& binding) {
+    ObjP cur = get_obj("pods", ns, name);
+    const jd::Value& cmd = *cur->v.get("metadata");
+    const jd::Value* bmd = binding.get("metadata");
+    std::string buid = bmd ? bmd->str_or("uid") : std::string();
+    if (!buid.empty() && buid != cmd.str_or("uid")) {
+      throw HttpError{409, status_body(409, "Conflict", "Precondition failed: UID in precondition: " + buid +
+                                                            ", UID in object meta: " + cmd.str_or("uid"))};
+    }
+    if (injected_conflict()) throw conflict("pods", name);
+    const jd::Value* cs = cur->v.get("spec");
+    std::string cur_node = cs ? cs->str_or("nodeName") : std::string();
+    if (!cur_node.empty()) {
+      throw HttpError{409, status_body(409, "Conflict", "pod " + name + " is already assigned to node \"" + cur_node + "\"")};
+    }
+    if (cmd.get("deletionTimestamp") && !cmd.get("deletionTimestamp")->is_null()) {
+      throw HttpError{409, status_body(409, "Conflict", "pod " + name + " is being deleted")};
+    }
+    const jd::Value* tgt = binding.get("target");
+    std::string target = tgt ? tgt->str_or("name") : std::string();
+    if (target.empty()) throw HttpError{422, status_body(422, "Invalid", "target.name: Required value")};
+    jd::Value nv = cur->v;
+    nv.member("spec").set("nodeName", jd::Value::string(target));
+    const jd::Value* ann = bmd ? bmd->get("annotations") : nullptr;
+    if (ann && ann->is_obj() && !ann->o.empty()) {
+      jd::Value& a = nv.member("metadata").member("annotations");
+      for (const auto& m : ann->o) a.set(m.first, m.second);
+    }
+    jd::Value& st = nv.member("status");
+    jd::Value* conds = st.get("conditions");
+    if (!conds || conds->k != jd::Value::Arr) {
+      st.set("conditions", jd::Value::array());
+      conds = st.get("conditions");
+    }
+    jd::Value c = jd::Value::object();
+    c.set("type", jd::Value::string("PodScheduled"));
+    c.set("status", jd::Value::string("True"));
+    c.set("lastTransitionTime", jd::Value::string(now_iso()));
+    conds->a.push_back(std::move(c));
+    nv.member("metadata").set("resourceVersion", jd::Value::string(bump()));
+    ObjP o = make_obj(std::move(nv));
+    store_["pods"][{ns, name}] = o;
+    emit("pods", "MODIFIED", o);
+  }
+
+  ObjP do_delete(const std::string& kind, const std::string& ns, const std::string& name, double grace) {
+    ObjP cur = get_obj(kind, ns, name);
+    Key key{kind == "nodes" ? std::string() : ns, name};
+    const jd::Value* cs = cur->v.get("spec");
+    if (kind == "pods" && grace > 0 && cs && !cs->str_or("nodeName").empty()) {
+      const jd::Value& cmd = *cur->v.get("metadata");
+      const jd::Value* dt = cmd.get("deletionTimestamp");
+      if (dt && !dt->is_null()) return cur;
+      jd::Value nv = cur->v;
+      jd::Value& md = nv.member("metadata");
+      md.set("deletionTimestamp", jd::Value::string(now_iso()));
+      md.set("deletionGracePeriodSeconds", jd::Value::number(static_cast<int64_t>(grace)));
+      md.set("resourceVersion", jd::Value::string(bump()));
+      ObjP o = make_obj(std::move(nv));
+      store_[kind][key] = o;
+      emit(kind, "MODIFIED", o);
+      graces_.push_back(Grace{now_s() + grace, kind, ns, name, cmd.str_or("uid")});
+      return o;
+    }
+    store_[kind].erase(key);
+    jd::Value gone = cur->v;
+    gone.member("metadata").set("resourceVersion", jd::Value::string(bump()));
+    ObjP o = make_obj(std::move(gone));
+    emit(kind, "DELETED", o);
+    return o;
+  }
+
+  // ---------------------------------------------------------------- routing
+  static jd::Value body_json(const http::Message& req) {
+    jd::Value v;
+    std::string err;
+    if (req.body.empty()) return jd::Value::object();
+    if (!jd::parse(req.body, &v, &err)) throw HttpError{400, status_body(400, "BadRequest", "invalid JSON: " + err)};
+    return v;
+  }
+
+  static double grace_of(const http::Message& req, const std::map<std::string, std::string>& q) {
+    auto it = q.find("gracePeriodSeconds");
+    if (it != q.end()) return std::atof(it->second.c_str());
+    if (!req.body.empty()) {
+      jd::Value v;
+      std::string err;
+      if (jd::parse(req.body, &v, &err)) {
+        const jd::Value* g = v.get("gracePeriodSeconds");
+        if (g && g->k == jd::Value::Num) return std::atof(g->s.c_str());
+      }
+    }
+    return -1;
+  }
+
+  std::string list_json(const std::string& kind, const std::string& ns, const std::string& fsel,
+                        const std::string& lsel) {
+    static const std::map<std::string, std::string> lists = {
+        {"pods", "PodList"}, {"nodes", "NodeList"}, {"events", "EventList"}, {"leases", "LeaseList"}};
+    std::string o = "{\"kind\":\"" + lists.at(kind) + "\",\"apiVersion\":\"v1\",\"metadata\":{\"resourceVersion\":\"" +
+                    std::to_string(rv_) + "\"},\"items\":[";
+    bool first = true;
+    for (auto& kv : store_[kind]) {
+      if (!ns.empty() && kv.second->ns != ns) continue;
+      if (!field_match(kv.second->v, fsel) || !label_match(kv.second->v, lsel)) continue;
+      if (!first) o.push_back(',');
+      first = false;
+      o.append(kv.second->json);
+    }
+    o.append("]}");
+    return o;
+  }
+
+  // Collection routes: (kind, ns) for "/api/v1/<kind>", "/api/v1/namespaces/<ns>/<kind>",
+  // "/apis/coordination.k8s.io/v1/namespaces/<ns>/leases"; item routes add name and subresource.
+  bool route(Conn* c, http::Message& req, Reply* rep) {
+    std::string path(req.path());
+    auto q = parse_query(req.target);
+    const std::string& m = req.method;
+    if (path == "/version") {
+      rep->body = "{\"major\":\"1\",\"minor\":\"30\",\"gitVersion\":\"v1.30.0-gsx-fake-native\",\"platform\":\"linux/amd64\"}";
+      return true;
+    }
+    if (path == "/healthz") {
+      rep->body = "ok";
+      rep->ct = "text/plain";
+      return true;
+    }
+    if (path == "/api") {
+      rep->body = "{\"kind\":\"APIVersions\",\"versions\":[\"v1\"]}";
+      return true;
+    }
+    if (path == "/fake/faults") {
+      if (m == "POST") {
+        jd::Value b = body_json(req);
+        auto num = [&](const char* k, double* dst) {
+          const jd::Value* v = b.get(k);
+          if (v && v->k == jd::Value::Num) *dst = std::atof(v->s.c_str());
+        };
+        auto inum = [&](const char* k, int64_t* dst) {
+          const jd::Value* v = b.get(k);
+          if (v && v->k == jd::Value::Num) *dst = std::atoll(v->s.c_str());
+        };
+        num("conflict_rate", &faults_.conflict_rate);
+        num("error_rate", &faults_.error_rate);
+        num("latency_ms", &faults_.latency_ms);
+        inum("drop_watch_after", &faults_.drop_watch_after);
+        inum("expire_watches", &faults_.expire_watches);
+        const jd::Value* h = b.get("hold_watches");
+        if (h && h->k == jd::Value::Bool) faults_.hold_watches = h->b;
+        const jd::Value* seed = b.get("seed");
+        if (seed && seed->k == jd::Value::Num) rng().seed(static_cast<uint64_t>(std::atoll(seed->s.c_str())));
+        const jd::Value* drop = b.get("drop_watches_now");
+        if (drop && drop->k == jd::Value::Bool && drop->b) {
+          for (auto& w : watchers_) end_watch(w.get());
+        }
+      }
+      rep->body = faults_.json();
+      return true;
+    }
+    if (path == "/fake/stats") {
+      std::string o = "{\"rv\":" + std::to_string(rv_) + ",\"native\":true,\"counts\":{";
+      bool first = true;
+      for (auto& kv : counts_) {
+        if (!first) o.push_back(',');
+        first = false;
+        json::append_quoted(&o, kv.first);
+        o.append(":").append(std::to_string(kv.second));
+      }
+      size_t live = 0;
+      for (auto& w : watchers_) live += w->closed ? 0 : 1;
+      o.append("},\"watchers\":").append(std::to_string(live));
+      for (auto& kv : store_) o.append(",\"" + kv.first + "\":" + std::to_string(kv.second.size()));
+      o.push_back('}');
+      rep->body = o;
+      return true;
+    }
+    std::vector<std::string> seg = split(path, '/');  // "", "api", "v1", ...
+    std::string kind, ns, name, sub;
+    bool coll = false;
+    if (seg.size() >= 4 && seg[1] == "api" && seg[2] == "v1") {
+      if (seg[3] == "namespaces" && seg.size() >= 6) {
+        ns = seg[4];
+        kind = seg[5];
+        if (seg.size() == 6) {
+          coll = true;
+        } else {
+          name = seg[6];
+          if (seg.size() == 8) sub = seg[7];
+          if (seg.size() > 8) throw HttpError{404, status_body(404, "NotFound", "the server could not find the requested resource")};
+        }
+        if (kind == "bindings" && coll && m == "POST") {
+          jd::Value b = body_json(req);
+          maybe_error();
+          const jd::Value* bmd = b.get("metadata");
+          do_bind(ns, bmd ? bmd->str_or("name") : std::string(), b);
+          rep->status = 201;
+          rep->body = "{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"metadata\":{},\"status\":\"Success\",\"code\":201}";
+          return true;
+        }
+      } else if (seg.size() == 4) {
+        kind = seg[3];
+        coll = true;
+      } else if (seg[3] == "nodes") {
+        kind = "nodes";
+        name = seg[4];
+        if (seg.size() == 6) sub = seg[5];
+      }
+    } else if (seg.size() >= 7 && seg[1] == "apis" && seg[2] == "coordination.k8s.io" && seg[3] == "v1" &&
+               seg[4] == "namespaces" && seg[6] == "leases") {
+      ns = seg[5];
+      kind = "leases";
+      if (seg.size() == 7) {
+        coll = true;
+      } else {
+        name = seg[7];
+      }
+    }
+    if (!store_.count(kind) || (kind == "nodes" && !ns.empty())) {
+      throw HttpError{404, status_body(404, "NotFound", "the server could not find the requested resource")};
+    }
+    if (coll) {
+      if (m == "GET") {
+        auto w = q.find("watch");
+        if (w != q.end() && (w->second == "1" || w->second == "true")) return start_watch(c, req, kind, ns, q);
+        rep->body = list_json(kind, ns, q.count("fieldSelector") ? q["fieldSelector"] : "",
+                              q.count("labelSelector") ? q["labelSelector"] : "");
+        return true;
+      }
+      if (m == "POST") {
+        jd::Value b = body_json(req);
+        if (kind == "pods") maybe_error();
+        rep->status = 201;
+        rep->body = do_create(kind, std::move(b), ns)->json;
+        return true;
+      }
+      if (m == "DELETE" && kind != "nodes") {
+        double grace = grace_of(req, q);
+        std::string fsel = q.count("fieldSelector") ? q["fieldSelector"] : "";
+        std::string lsel = q.count("labelSelector") ? q["labelSelector"] : "";
+        std::vector<std::string> names;
+        for (auto& kv : store_[kind]) {
+          if (!ns.empty() && kv.second->ns != ns) continue;
+          if (field_match(kv.second->v, fsel) && label_match(kv.second->v, lsel)) names.push_back(kv.second->name);
+        }
+        std::string o = "{\"kind\":\"PodList\",\"apiVersion\":\"v1\",\"metadata\":{},\"items\":[";
+        for (size_t i = 0; i < names.size(); ++i) {
+          if (i) o.push_back(',');
+          o.append(do_delete(kind, ns, names[i], grace)->json);
+        }
+        o.append("]}");
+        rep->body = o;
+        return true;
+      }
+      throw HttpError{405, status_body(405, "MethodNotAllowed", "method not allowed")};
+    }
+    if (sub == "binding" && kind == "pods" && m == "POST") {
+      jd::Value b = body_json(req);
+      maybe_error();
+      do_bind(ns, name, b);
+      rep->status = 201;
+      rep->body = "{\"kind\":\"Status\",\"apiVersion\":\"v1\",\"metadata\":{},\"status\":\"Success\",\"code\":201}";
+      return true;
+    }
+    if (!sub.empty() && sub != "status") {
+      throw HttpError{404, status_body(404, "NotFound", "the server could not find the requested resource")};
+    }
+    if (m == "GET" && sub.empty()) {
+      rep->body = get_obj(kind, ns, name)->json;
+      return true;
+    }
+    if (m == "PUT") {
+      jd::Value b = body_json(req);
+      if (kind == "pods") maybe_error();
+      rep->body = do_replace(kind, ns, name, std::move(b), sub)->json;
+      return true;
+    }
+    if (m == "PATCH") {
+      const std::string* ct = req.header("content-type");
+      if (ct && ct->find("json-patch+json") != std::string::npos) {
+        rep->status = 415;
+        rep->body = status_body(415, "UnsupportedMediaType", "json-patch not supported");
+        return true;
+      }
+      jd::Value b = body_json(req);
+      if (kind == "pods") maybe_error();
+      rep->body = do_patch(kind, ns, name, std::move(b), sub)->json;
+      return true;
+    }
+    if (m == "DELETE" && sub.empty()) {
+      rep->body = do_delete(kind, ns, name, grace_of(req, q))->json;
+      return true;
+    }
+    throw HttpError{405, status_body(405, "MethodNotAllowed", "method not allowed")};
+  }
+
+  struct Delayed {
+    double due;
+    uint64_t conn;
+    http::Message req;
+  };
+  struct Held {
+    uint64_t conn;
+    http::Message req;
+  };
+  struct Grace {
+    double due;
+    std::string kind, ns, name, uid;
+  };
+
+  size_t history_max_;
+  int lfd_ = -1, ep_ = -1;
+  uint64_t next_id_ = 0;
+  std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns_;
+  std::vector<std::unique_ptr<Watcher>> watchers_;
+  std::map<std::string, std::map<Key, ObjP>> store_;
+  std::deque<Event> history_;
+  int64_t rv_ = 0, oldest_rv_ = 0;
+  Faults faults_;
+  std::map<std::string, uint64_t> counts_;
+  std::vector<Delayed> delayed_;
+  std::vector<Held> held_;
+  std::vector<Grace> graces_;
+};
+
+volatile sig_atomic_t g_stop = 0;
+void on_sig(int) { g_stop = 1; }
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string host = "127.0.0.1", port_file;
+  int port = 0;
+  size_t history = 200000;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "missing value for %s\n", a.c_str());
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--host") host = val();
+    else if (a == "--port") port = std::atoi(val().c_str());
+    else if (a == "--port-file") port_file = val();
+    else if (a == "--history") history = static_cast<size_t>(std::max(1, std::atoi(val().c_str())));
+    else if (a == "-h" || a == "--help") {
+      std::printf("usage: gsx-fakeapi [--host H] [--port P] [--port-file F] [--history N]\n");
+      return 0;
+    } else {
+      std::fprintf(stderr, "unknown argument %s\n", a.c_str());
+      return 2;
+    }
+  }
+  signal(SIGPIPE, SIG_IGN);
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof(sa));
+  sa.sa_handler = on_sig;
+  sigaction(SIGTERM, &sa, nullptr);
+  sigaction(SIGINT, &sa, nullptr);
+  Server srv(history);
+  std::string err;
+  int bound = srv.listen_on(host, port, &err);
+  if (bound < 0) {
+    std::fprintf(stderr, "gsx-fakeapi: %s\n", err.c_str());
+    return 1;
+  }
+  if (!port_file.empty()) {
+    std::string tmp = port_file + ".tmp";
+    {
+      std::ofstream f(tmp);
+      f << bound;
+    }
+    std::rename(tmp.c_str(), port_file.c_str());
+  }
+  std::printf("fake-apiserver (native) listening on http://%s:%d\n", host.c_str(), bound);
+  std::fflush(stdout);
+  srv.run(&g_stop);
+  return 0;
+}

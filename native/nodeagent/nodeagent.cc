@@ -1,0 +1,725 @@
+// gsx-nodeagent: kubelet + device-plugin + container-runtime stand-in for one
+// node, in C++ (the compiled counterpart of deviceplugin/agent.py).
+//
+// Where there is no kubelet (bench.py on the GPU box, simulators), this drives
+// the device plugin's Allocate logic for every pod bound to the node and
+// starts the pod on its GPU's runtime endpoint -- the tail of the reference's
+// sequence diagram (docs/designs/sequence.jpg, docs/designs/designs.md:93-103):
+//
+//   bound pod, ASSIGNED=false ──► Allocate(N ids): the earliest-ASSUME_TIME
+//   unassigned pod of that size on this node ──► PATCH ASSIGNED=true with a
+//   resourceVersion precondition (the commit point; 409 -> retry) ──► container
+//   env (HIP_VISIBLE_DEVICES, *_IDX/_DEV/_POD/_CONTAINER, memory fraction,
+//   optional CU partition) ──► POST <runtime>/v1/pods/<uid>: the pod's slice of
+//   the GPU's HBM arena is stamped by a HIP kernel and every resident slice is
+//   verified ──► PATCH status Running.
+//   completed / deleted pod ──► DELETE <runtime>/v1/pods/<uid>, CUs released.
+//
+// Devices and runtime endpoints come from the node's annotations
+// (gpushare.amd.com/devices, gpushare.amd.com/runtime-endpoints), written by
+// the device plugin / the benchmark.  Control endpoints:
+//   GET /v1/stats, GET /v1/allocations/<uid> (container env of the Allocate).
+//
+//   gsx-nodeagent --apiserver URL --node NAME [--profile P] [--unit GiB]
+//                 [--workers N] [--no-verify] [--port-file F]
+#include <signal.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "apiclient.h"
+#include "ctlserver.h"
+#include "informer.h"
+#include "json.h"
+#include "model.h"
+#include "quantity.h"
+
+using namespace gsx;
+
+namespace {
+
+const char* kDevInfoAnn = "gpushare.amd.com/devices";
+const char* kEndpointsAnn = "gpushare.amd.com/runtime-endpoints";
+const char* kCuCountAnn = "gpushare.amd.com/cu-count";
+const char* kCuMaskAnn = "gpushare.amd.com/cu-mask";
+const char* kAssignTimeAnn = "gpushare.amd.com/assign-time";
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int64_t unix_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+struct Device {
+  int index = 0;
+  std::string bdf;
+  int cu = 256, xcc = 8;
+  int render = -1, card = -1;
+  std::string endpoint;
+};
+
+// Per-device CU ledger (deviceplugin/allocator.py CUPartitioner): partitions
+// are spread round-robin over the XCDs so each pod keeps every L2 slice.
+class CuPartitioner {
+ public:
+  CuPartitioner(int cu = 256, int xcc = 8) : cu_(cu), xcc_(std::max(1, xcc)), owner_(static_cast<size_t>(cu)) {}
+  bool allocate(const std::string& uid, int n, std::vector<int>* out, std::string* err) {
+    auto h = held_.find(uid);
+    if (h != held_.end()) {
+      *out = h->second;
+      return true;
+    }
+    if (n <= 0 || n > cu_) {
+      *err = "invalid CU partition size " + std::to_string(n);
+      return false;
+    }
+    int per = cu_ / xcc_;
+    std::vector<int> got;
+    for (int i = 0; i < per && static_cast<int>(got.size()) < n; ++i) {
+      for (int x = 0; x < xcc_ && static_cast<int>(got.size()) < n; ++x) {
+        int c = x * per + i;
+        if (owner_[static_cast<size_t>(c)].empty()) got.push_back(c);
+      }
+    }
+    if (static_cast<int>(got.size()) < n) {
+      *err = "only " + std::to_string(got.size()) + " CUs free, " + std::to_string(n) + " requested";
+      return false;
+    }
+    std::sort(got.begin(), got.end());
+    for (int c : got) owner_[static_cast<size_t>(c)] = uid;
+    held_[uid] = got;
+    *out = got;
+    return true;
+  }
+  void release(const std::string& uid) {
+    auto h = held_.find(uid);
+    if (h == held_.end()) return;
+    for (int c : h->second) owner_[static_cast<size_t>(c)].clear();
+    held_.erase(h);
+  }
+  int cu_count() const { return cu_; }
+
+ private:
+  int cu_, xcc_;
+  std::vector<std::string> owner_;
+  std::unordered_map<std::string, std::vector<int>> held_;
+};
+
+std::string cu_words(const std::vector<int>& cus, int cu_count) {
+  std::vector<uint32_t> w(static_cast<size_t>((cu_count + 31) / 32), 0);
+  for (int c : cus) w[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
+  std::string o;
+  char b[16];
+  for (size_t i = 0; i < w.size(); ++i) {
+    std::snprintf(b, sizeof(b), "%s0x%08x", i ? "," : "", w[i]);
+    o.append(b);
+  }
+  return o;
+}
+
+std::string cu_ranges(const std::vector<int>& cus) {
+  std::string o;
+  size_t i = 0;
+  while (i < cus.size()) {
+    size_t j = i;
+    while (j + 1 < cus.size() && cus[j + 1] == cus[j] + 1) ++j;
+    if (!o.empty()) o.push_back(',');
+    o.append(std::to_string(cus[i]));
+    if (j > i) o.append("-").append(std::to_string(cus[j]));
+    i = j + 1;
+  }
+  return o;
+}
+
+struct AgentPod {
+  std::string uid, ns, name, rv, phase;
+  int64_t dev_idx = -1, request = 0, assume_time = -1, dev_total = 0;
+  int assigned = -1;
+  bool complete = false;
+  int cu_count = 0;
+};
+
+struct Cand {
+  int64_t assume_time;
+  std::string key;
+  int64_t units;
+};
+
+class Agent {
+ public:
+  Agent(ApiConfig api, std::string node, Profile p, int64_t unit_bytes, int workers, bool verify)
+      : api_cfg_(api), node_(std::move(node)), p_(std::move(p)), unit_(unit_bytes), nworkers_(workers),
+        verify_(verify), api_(api) {}
+
+  bool load_devices(double timeout_s, std::string* err) {
+    double deadline = now_s() + timeout_s;
+    while (true) {
+      int status = 0;
+      std::string body, e;
+      if (api_.request("GET", "/api/v1/nodes/" + node_, std::string(), nullptr, &status, &body, &e) && status == 200) {
+        json::Doc d;
+        std::string perr;
+        if (d.parse(body, &perr)) {
+          int64_t an = d.path(0, {"metadata", "annotations"});
+          int64_t inv = an >= 0 ? d.find(static_cast<uint32_t>(an), kDevInfoAnn) : -1;
+          int64_t eps = an >= 0 ? d.find(static_cast<uint32_t>(an), kEndpointsAnn) : -1;
+          if (inv >= 0 && eps >= 0 && parse_devices(d.str(static_cast<uint32_t>(inv)), d.str(static_cast<uint32_t>(eps))))
+            return true;
+        }
+      }
+      if (now_s() > deadline) {
+        *err = "node " + node_ + " never published devices + runtime endpoints";
+        return false;
+      }
+      ::usleep(50000);
+    }
+  }
+
+  bool start(std::string* err) {
+    ReflectorConfig rc;
+    rc.path = "/api/v1/pods";
+    rc.field_selector = "spec.nodeName=" + node_;
+    ReflectorHandler h;
+    h.on_list = [this](const json::Doc& d, const std::vector<uint32_t>& items) {
+      std::lock_guard<std::mutex> g(mu_);
+      std::unordered_set<std::string> seen;
+      for (uint32_t i : items) seen.insert(on_pod_locked(d, i));
+      std::vector<std::string> gone;
+      for (auto& kv : pods_) {
+        if (!seen.count(kv.first)) gone.push_back(kv.first);
+      }
+      for (auto& k : gone) on_delete_locked(k);
+      wake_locked();
+    };
+    h.on_event = [this](Ev ev, const json::Doc& d, uint32_t obj) {
+      std::lock_guard<std::mutex> g(mu_);
+      if (ev == Ev::Deleted) {
+        PodView v;
+        parse_pod(d, obj, p_, &v);
+        on_delete_locked(v.ns + "/" + v.name);
+      } else {
+        on_pod_locked(d, obj);
+      }
+      wake_locked();
+    };
+    pods_r_ = std::make_unique<Reflector>(api_cfg_, rc, h);
+    pods_r_->start();
+    if (!pods_r_->wait_synced(60)) {
+      *err = "pod informer did not sync: " + pods_r_->last_error();
+      return false;
+    }
+    for (int i = 0; i < nworkers_; ++i) workers_.emplace_back([this] { worker(); });
+    return true;
+  }
+
+  void stop() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+    if (pods_r_) pods_r_->stop();
+  }
+
+  CtlServer::Reply handle(const http::Message& req) {
+    CtlServer::Reply rep;
+    std::string_view path = req.path();
+    std::lock_guard<std::mutex> g(mu_);
+    if (req.method == "GET" && path == "/v1/stats") {
+      std::vector<double> lat = latency_;
+      std::sort(lat.begin(), lat.end());
+      double p50 = lat.empty() ? 0 : lat[lat.size() / 2];
+      char b[256];
+      std::snprintf(b, sizeof(b),
+                    "{\"admitted\":%llu,\"failed\":%llu,\"bad_stamps\":%llu,\"conflicts\":%llu,\"running\":%zu,"
+                    "\"admit_p50_ms\":%.3f,\"native\":true}",
+                    (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
+                    (unsigned long long)conflicts_, running_.size(), p50 * 1e3);
+      rep.body = b;
+      return rep;
+    }
+    const std::string_view pre = "/v1/allocations/";
+    if (req.method == "GET" && path.substr(0, pre.size()) == pre) {
+      auto it = allocations_.find(std::string(path.substr(pre.size())));
+      if (it == allocations_.end()) {
+        rep.status = 404;
+        rep.body = "{}";
+      } else {
+        rep.body = it->second;
+      }
+      return rep;
+    }
+    rep.status = 404;
+    rep.body = "{\"error\":\"not found\"}";
+    return rep;
+  }
+
+ private:
+  bool parse_devices(const std::string& inv, const std::string& eps) {
+    json::Doc di, de;
+    std::string e;
+    if (!di.parse(inv, &e) || !de.parse(eps, &e)) return false;
+    if (di.at(0).type != json::T::Array || de.at(0).type != json::T::Object) return false;
+    std::map<int, Device> devs;
+    uint32_t end = di.at(0).skip;
+    for (uint32_t i = 1; i < end; i = di.next(i)) {
+      if (di.at(i).type != json::T::Object) continue;
+      Device d;
+      int64_t v;
+      auto geti = [&](const char* k, int* dst) {
+        int64_t x = di.find(i, k);
+        if (x >= 0 && di.as_int(static_cast<uint32_t>(x), &v)) *dst = static_cast<int>(v);
+      };
+      geti("index", &d.index);
+      geti("cu", &d.cu);
+      geti("xcc", &d.xcc);
+      geti("render", &d.render);
+      geti("card", &d.card);
+      int64_t b = di.find(i, "bdf");
+      if (b >= 0) d.bdf = di.str(static_cast<uint32_t>(b));
+      int64_t ep = de.find(0, std::to_string(d.index));
+      if (ep < 0) return false;  // every GPU needs its runtime endpoint
+      d.endpoint = de.str(static_cast<uint32_t>(ep));
+      devs[d.index] = d;
+    }
+    if (devs.empty()) return false;
+    for (auto& kv : devs) {
+      cus_.emplace(kv.first, CuPartitioner(kv.second.cu, kv.second.xcc));
+      ApiConfig rc;
+      rc.server = kv.second.endpoint;
+      rc.timeout_s = 60;
+      runtimes_.emplace(kv.first, std::make_unique<ApiClient>(rc));
+    }
+    devices_ = std::move(devs);
+    return true;
+  }
+
+  // ---------------------------------------------------------------- informer handlers (agent.py _on_pod)
+  std::string on_pod_locked(const json::Doc& d, uint32_t obj) {
+    PodView v;
+    parse_pod(d, obj, p_, &v);
+    std::string key = v.ns + "/" + v.name;
+    AgentPod& ap = pods_[key];
+    ap.uid = v.uid;
+    ap.ns = v.ns;
+    ap.name = v.name;
+    ap.rv = v.rv;
+    ap.phase = v.phase;
+    ap.dev_idx = v.dev_idx;
+    ap.request = v.request;
+    ap.assume_time = v.assume_time;
+    ap.assigned = v.assigned;
+    ap.dev_total = v.annot_dev_total;
+    ap.complete = v.complete();
+    ap.cu_count = 0;
+    int64_t an = d.path(obj, {"metadata", "annotations"});
+    if (an >= 0) {
+      int64_t c = d.find(static_cast<uint32_t>(an), kCuCountAnn);
+      if (c >= 0) ap.cu_count = std::atoi(d.str(static_cast<uint32_t>(c)).c_str());
+    }
+    const std::string& uid = ap.uid;
+    if (ap.complete) {
+      cands_.erase(uid);
+      stop_pod_locked(uid);
+      return key;
+    }
+    if (ap.request <= 0 || !devices_.count(static_cast<int>(ap.dev_idx))) {
+      cands_.erase(uid);
+      return key;
+    }
+    if (ap.assigned == 0 && (ap.phase == "Pending" || ap.phase.empty())) {
+      cands_[uid] = Cand{ap.assume_time, key, ap.request};
+    } else {
+      cands_.erase(uid);
+    }
+    if (ap.assigned == 0 && !inflight_.count(uid) && !running_.count(uid) && !queued_.count(uid)) {
+      queued_.insert(uid);
+      seen_.emplace(uid, now_s());
+      queue_.push_back(key);
+      ++added_;
+    }
+    return key;
+  }
+
+  void on_delete_locked(const std::string& key) {
+    auto it = pods_.find(key);
+    if (it == pods_.end()) return;
+    std::string uid = it->second.uid;
+    pods_.erase(it);
+    cands_.erase(uid);
+    stop_pod_locked(uid);
+  }
+
+  void stop_pod_locked(const std::string& uid) {
+    auto r = running_.find(uid);
+    if (r == running_.end()) return;
+    int dev = r->second;
+    running_.erase(r);
+    for (auto& kv : cus_) kv.second.release(uid);
+    allocations_.erase(uid);
+    releases_.push_back({uid, dev});
+    ++added_;
+  }
+
+  // One worker per new work item (an event that queued nothing wakes nobody).
+  void wake_locked() {
+    for (; added_ > 0; --added_) cv_.notify_one();
+  }
+
+  // ---------------------------------------------------------------- admission (agent.py _admit)
+  void worker() {
+    std::unique_lock<std::mutex> lk(mu_);
+    while (true) {
+      double now = now_s();
+      for (auto it = delayed_.begin(); it != delayed_.end();) {
+        if (it->first <= now) {
+          queue_.push_back(it->second);
+          it = delayed_.erase(it);
+        } else {
+          ++it;
+        }
+      }
+      if (stop_) return;
+      if (!releases_.empty()) {
+        auto rel = releases_.front();
+        releases_.pop_front();
+        lk.unlock();
+        runtime_call(rel.second, "DELETE", "/v1/pods/" + rel.first, std::string(), nullptr);
+        lk.lock();
+        continue;
+      }
+      if (queue_.empty()) {
+        double wait = 0.05;
+        for (auto& dl : delayed_) wait = std::min(wait, std::max(0.0, dl.first - now));
+        cv_.wait_for(lk, std::chrono::duration<double>(wait));
+        continue;
+      }
+      std::string key = std::move(queue_.front());
+      queue_.pop_front();
+      auto pit = pods_.find(key);
+      if (pit == pods_.end()) continue;
+      queued_.erase(pit->second.uid);
+      admit_locked(key, lk);
+    }
+  }
+
+  std::string build_envs_locked(const AgentPod& pod, const Device& dev, const std::vector<int>& cus) {
+    // deviceplugin/allocator.py build_response, mount_mode "isolated": only this GPU's nodes are mounted
+    const std::string visible = "0";
+    char frac[32];
+    std::snprintf(frac, sizeof(frac), "%.6f",
+                  pod.dev_total > 0 ? static_cast<double>(pod.request) / static_cast<double>(pod.dev_total) : 0.0);
+    std::vector<std::pair<std::string, std::string>> env = {
+        {"HIP_VISIBLE_DEVICES", visible},
+        {"ROCR_VISIBLE_DEVICES", visible},
+        {p_.a_idx, std::to_string(dev.index)},
+        {p_.a_dev, std::to_string(pod.dev_total > 0 ? pod.dev_total : 0)},
+        {p_.a_pod, std::to_string(pod.request)},
+        {p_.env_container, std::to_string(pod.request)},
+        {"GSX_GPU_MEM_FRACTION", frac},
+        {"GSX_GPU_BDF", dev.bdf},
+    };
+    if (!cus.empty()) {
+      env.emplace_back("GSX_CU_MASK", cu_words(cus, dev.cu));
+      env.emplace_back("HSA_CU_MASK", visible + ":" + cu_ranges(cus));
+    }
+    std::string o = "{\"envs\":{";
+    for (size_t i = 0; i < env.size(); ++i) {
+      if (i) o.push_back(',');
+      json::append_quoted(&o, env[i].first);
+      o.push_back(':');
+      json::append_quoted(&o, env[i].second);
+    }
+    o.append("},\"devices\":[");
+    std::vector<std::string> nodes = {"/dev/kfd"};
+    if (dev.render >= 0) nodes.push_back("/dev/dri/renderD" + std::to_string(dev.render));
+    if (dev.card >= 0) nodes.push_back("/dev/dri/card" + std::to_string(dev.card));
+    for (size_t i = 0; i < nodes.size(); ++i) {
+      if (i) o.push_back(',');
+      o.append("{\"container_path\":");
+      json::append_quoted(&o, nodes[i]);
+      o.append(",\"host_path\":");
+      json::append_quoted(&o, nodes[i]);
+      o.append(",\"permissions\":\"rw\"}");
+    }
+    o.append("]}");
+    return o;
+  }
+
+  void admit_locked(std::string key, std::unique_lock<std::mutex>& lk) {
+    auto pit = pods_.find(key);
+    if (pit == pods_.end()) return;
+    std::string uid = pit->second.uid;
+    if (running_.count(uid) || inflight_.count(uid)) return;
+    int64_t units = pit->second.request;
+    // kubelet's Allocate(N ids): the earliest-ASSUME_TIME unassigned pod of that size
+    const Cand* best = nullptr;
+    std::string best_uid;
+    for (auto& kv : cands_) {
+      if (kv.second.units != units || inflight_.count(kv.first) || running_.count(kv.first)) continue;
+      if (!best || kv.second.assume_time < best->assume_time ||
+          (kv.second.assume_time == best->assume_time && kv.second.key < best->key)) {
+        best = &kv.second;
+        best_uid = kv.first;
+      }
+    }
+    if (!best) return;
+    auto cit = pods_.find(best->key);
+    if (cit == pods_.end()) return;
+    if (best_uid != uid) {
+      // an earlier same-size pod wins this Allocate; ours is served by the next one
+      queued_.insert(uid);
+      queue_.push_back(key);
+      ++added_;
+      wake_locked();
+      key = best->key;
+      uid = best_uid;
+    }
+    AgentPod pod = cit->second;
+    inflight_.insert(uid);
+    double t0 = seen_.count(uid) ? seen_[uid] : now_s();
+    int dev_idx = static_cast<int>(pod.dev_idx);
+    const Device dev = devices_.at(dev_idx);
+    std::vector<int> cus;
+    if (pod.cu_count > 0) {
+      std::string e;
+      if (!cus_.at(dev_idx).allocate(uid, pod.cu_count, &cus, &e)) {
+        std::fprintf(stderr, "[gsx-nodeagent] %s: %s\n", key.c_str(), e.c_str());
+        inflight_.erase(uid);
+        return;
+      }
+    }
+    std::string envs = build_envs_locked(pod, dev, cus);
+    lk.unlock();
+
+    // commit point: ASSIGNED=true guarded by the resourceVersion we decided on
+    std::string patch = "{\"metadata\":{\"resourceVersion\":";
+    json::append_quoted(&patch, pod.rv);
+    patch.append(",\"annotations\":{");
+    json::append_quoted(&patch, p_.a_assigned);
+    patch.append(":\"true\",");
+    json::append_quoted(&patch, kAssignTimeAnn);
+    patch.append(":\"").append(std::to_string(unix_ns())).append("\"");
+    if (!cus.empty()) {
+      patch.push_back(',');
+      json::append_quoted(&patch, kCuMaskAnn);
+      patch.push_back(':');
+      json::append_quoted(&patch, cu_words(cus, dev.cu));
+    }
+    patch.append("}}}");
+    std::string path = "/api/v1/namespaces/" + pod.ns + "/pods/" + pod.name;
+    int status = 0;
+    std::string resp, err;
+    bool ok = api_.request("PATCH", path, patch, "application/merge-patch+json", &status, &resp, &err);
+    if (!ok || status >= 300) {
+      lk.lock();
+      if (!cus.empty()) cus_.at(dev_idx).release(uid);
+      inflight_.erase(uid);
+      if (ok && status == 409) {
+        conflicts_++;  // stale copy: retry from the informer's latest version
+        if (!queued_.count(uid)) {
+          queued_.insert(uid);
+          delayed_.push_back({now_s() + 0.001, key});
+        }
+      } else {
+        std::fprintf(stderr, "[gsx-nodeagent] ASSIGNED patch of %s failed: %s %d %s\n", key.c_str(), err.c_str(),
+                     status, resp.substr(0, 200).c_str());
+      }
+      return;
+    }
+    // start the pod on its GPU's runtime: slice stamped + every resident slice verified
+    std::string body = "{\"dev\":" + std::to_string(dev_idx) + ",\"bytes\":" + std::to_string(pod.request * unit_) +
+                       ",\"cus\":";
+    if (cus.empty()) {
+      body.append("null");
+    } else {
+      body.push_back('[');
+      for (size_t i = 0; i < cus.size(); ++i) {
+        if (i) body.push_back(',');
+        body.append(std::to_string(cus[i]));
+      }
+      body.push_back(']');
+    }
+    body.append(",\"verify\":").append(verify_ ? "true" : "false").append("}");
+    std::string rresp;
+    int rst = runtime_call(dev_idx, "POST", "/v1/pods/" + uid, body, &rresp);
+    int64_t bad = 0;
+    std::string why;
+    if (rst != 200) {
+      why = "runtime HTTP " + std::to_string(rst) + ": " + rresp.substr(0, 200);
+    } else {
+      json::Doc d;
+      std::string perr;
+      if (d.parse(rresp, &perr)) {
+        int64_t b = d.find(0, "bad");
+        if (b >= 0) d.as_int(static_cast<uint32_t>(b), &bad);
+      }
+      if (bad) why = std::to_string(bad) + " bad HBM stamps after admitting " + key;
+    }
+    if (!why.empty()) {
+      lk.lock();
+      failed_++;
+      bad_ += static_cast<uint64_t>(bad);
+      if (!cus.empty()) cus_.at(dev_idx).release(uid);
+      inflight_.erase(uid);
+      lk.unlock();
+      if (rst == 200) runtime_call(dev_idx, "DELETE", "/v1/pods/" + uid, std::string(), nullptr);
+      std::fprintf(stderr, "[gsx-nodeagent] admission of %s on GPU %d failed: %s\n", key.c_str(), dev_idx, why.c_str());
+      std::string st = "{\"status\":{\"phase\":\"Failed\",\"reason\":\"UnexpectedAdmissionError\",\"message\":";
+      json::append_quoted(&st, why);
+      st.append("}}");
+      api_.request("PATCH", path + "/status", st, "application/merge-patch+json", &status, &resp, &err);
+      lk.lock();
+      return;
+    }
+    lk.lock();
+    running_[uid] = dev_idx;
+    allocations_[uid] = envs;
+    admitted_++;
+    lk.unlock();
+    api_.request("PATCH", path + "/status", "{\"status\":{\"phase\":\"Running\"}}", "application/merge-patch+json",
+                 &status, &resp, &err);
+    lk.lock();
+    latency_.push_back(now_s() - t0);
+    if (latency_.size() > 100000) latency_.erase(latency_.begin(), latency_.begin() + 50000);
+    seen_.erase(uid);
+    inflight_.erase(uid);
+    // deleted while we were admitting: release now
+    auto pk = pods_.find(key);
+    if (pk == pods_.end() || pk->second.uid != uid || pk->second.complete) stop_pod_locked(uid);
+    wake_locked();
+  }
+
+  int runtime_call(int dev, const char* method, const std::string& path, const std::string& body, std::string* out) {
+    auto it = runtimes_.find(dev);
+    if (it == runtimes_.end()) return -1;
+    int status = 0;
+    std::string resp, err;
+    if (!it->second->request(method, path, body, "application/json", &status, &resp, &err)) return -1;
+    if (out) *out = std::move(resp);
+    return status;
+  }
+
+  ApiConfig api_cfg_;
+  std::string node_;
+  Profile p_;
+  int64_t unit_;
+  int nworkers_;
+  bool verify_;
+  ApiClient api_;
+  std::map<int, Device> devices_;
+  std::map<int, CuPartitioner> cus_;
+  std::map<int, std::unique_ptr<ApiClient>> runtimes_;
+  std::unique_ptr<Reflector> pods_r_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+  std::unordered_map<std::string, AgentPod> pods_;
+  std::unordered_map<std::string, Cand> cands_;
+  std::unordered_map<std::string, int> running_;
+  std::unordered_set<std::string> inflight_, queued_;
+  std::unordered_map<std::string, double> seen_;
+  std::unordered_map<std::string, std::string> allocations_;
+  std::deque<std::string> queue_;
+  std::vector<std::pair<double, std::string>> delayed_;
+  std::deque<std::pair<std::string, int>> releases_;
+  std::vector<double> latency_;
+  uint64_t admitted_ = 0, failed_ = 0, bad_ = 0, conflicts_ = 0;
+  int added_ = 0;  // work items queued since the last wake_locked()
+  std::vector<std::thread> workers_;
+};
+
+volatile sig_atomic_t g_stop = 0;
+void on_sig(int) { g_stop = 1; }
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string apiserver, node, profile = "shared-gpu", unit = "GiB", port_file, host = "127.0.0.1";
+  int workers = 16, port = 0;
+  bool verify = true;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&](const char* name) -> std::string {
+      if (i + 1 >= argc) {
+        std::fprintf(stderr, "missing value for %s\n", name);
+        std::exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--apiserver") apiserver = val("--apiserver");
+    else if (a == "--node") node = val("--node");
+    else if (a == "--profile") profile = val("--profile");
+    else if (a == "--unit") unit = val("--unit");
+    else if (a == "--workers") workers = std::max(1, std::min(128, std::atoi(val("--workers").c_str())));
+    else if (a == "--no-verify") verify = false;
+    else if (a == "--port") port = std::atoi(val("--port").c_str());
+    else if (a == "--port-file") port_file = val("--port-file");
+    else if (a == "-h" || a == "--help") {
+      std::printf("usage: gsx-nodeagent --apiserver URL --node NAME [--profile P] [--unit GiB|MiB] [--workers N]\n"
+                  "                     [--no-verify] [--port P] [--port-file F]\n");
+      return 0;
+    } else {
+      std::fprintf(stderr, "unknown argument %s\n", a.c_str());
+      return 2;
+    }
+  }
+  if (apiserver.empty() || node.empty()) {
+    std::fprintf(stderr, "--apiserver and --node are required\n");
+    return 2;
+  }
+  int64_t unit_bytes = unit == "MiB" ? (1ll << 20) : unit == "GB" ? 1000000000ll : unit == "MB" ? 1000000ll : (1ll << 30);
+  signal(SIGPIPE, SIG_IGN);
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof(sa));
+  sa.sa_handler = on_sig;
+  sigaction(SIGTERM, &sa, nullptr);
+  sigaction(SIGINT, &sa, nullptr);
+  ApiConfig api;
+  api.server = apiserver;
+  Agent agent(api, node, profile_by_name(profile), unit_bytes, workers, verify);
+  std::string err;
+  CtlServer srv([&](const http::Message& m) { return agent.handle(m); });
+  int bound = srv.start(host, port, &err);
+  if (bound < 0) {
+    std::fprintf(stderr, "gsx-nodeagent: %s\n", err.c_str());
+    return 1;
+  }
+  // readiness for the process harness: published before waiting for the node's inventory
+  if (!port_file.empty()) {
+    std::string tmp = port_file + ".tmp";
+    {
+      std::ofstream f(tmp);
+      f << bound;
+    }
+    std::rename(tmp.c_str(), port_file.c_str());
+  }
+  if (!agent.load_devices(600, &err) || !agent.start(&err)) {
+    std::fprintf(stderr, "gsx-nodeagent: %s\n", err.c_str());
+    srv.stop();
+    return 1;
+  }
+  while (!g_stop) ::usleep(20000);
+  srv.stop();
+  agent.stop();
+  return 0;
+}

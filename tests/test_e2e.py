@@ -23,7 +23,7 @@ NATIVE = {"on": True}
 
 @pytest.fixture(autouse=True, params=["native-http", "aiohttp"])
 def _frontend(request):
-    """Every end-to-end test runs against the C++ front end and against the pure-aiohttp one."""
+    """Every end-to-end test runs twice: C++ front end + C++ controller, and aiohttp + asyncio controller."""
     NATIVE["on"] = request.param == "native-http"
     yield
     NATIVE["on"] = True
@@ -38,8 +38,9 @@ class Cluster:
     async def __aenter__(self):
         self.api = await FakeApiServerRunner().start()
         self.client = KubeClient(self.api.url)
+        kw = {"native_controller": NATIVE["on"], **self.ext_kw}
         self.ext = await ExtenderRunner(ExtenderServer(KubeClient(self.api.url), self.profile,
-                                                       bind_mode=self.bind_mode, **self.ext_kw),
+                                                       bind_mode=self.bind_mode, **kw),
                                         native=NATIVE["on"]).start()
         self.sim = None
         self.http = aiohttp.ClientSession()
@@ -156,7 +157,7 @@ def test_bind_modes_and_cant_place(mode):
             for nm, m in (("a", 8), ("b", 8), ("c", 8)):
                 await c.client.create("pods", make_pod(nm, m, uid=f"u-{nm}"))
             eng = c.ext.server.engine
-            await c.settle(lambda: eng.has_node("n") and c.ext.server.controller.pods.get("default/c") is not None)
+            await c.settle(lambda: eng.has_node("n") and c.ext.server.controller.get_pod("c", "default") is not None)
             for nm in ("a", "b"):
                 st, body = await c.post("/gpushare-scheduler/bind",
                                         wire.ExtenderBindingArgs(nm, "default", f"u-{nm}", "n").encode())
@@ -176,7 +177,7 @@ def test_bind_conflict_retry_and_release_on_error():
             await c.client.create("nodes", make_node("n", 10, 1))
             await c.client.create("pods", make_pod("a", 6, uid="ua"))
             eng = c.ext.server.engine
-            await c.settle(lambda: eng.has_node("n") and c.ext.server.controller.pods.get("default/a") is not None)
+            await c.settle(lambda: eng.has_node("n") and c.ext.server.controller.get_pod("a", "default") is not None)
             c.api.server.faults.update({"error_rate": 1.0})
             st, body = await c.post("/gpushare-scheduler/bind", wire.ExtenderBindingArgs("a", "default", "ua", "n").encode())
             assert st == 500
@@ -198,7 +199,7 @@ def test_pod_lifecycle_frees_memory_and_restart_recovery():
             eng = c.ext.server.engine
             await c.settle(lambda: eng.node_devices("n") == [(10, 6)])
             # a second extender started now rebuilds the ledger from annotations (cache.go:49-74)
-            srv2 = ExtenderServer(KubeClient(c.api.url), SHARED_GPU)
+            srv2 = ExtenderServer(KubeClient(c.api.url), SHARED_GPU, native_controller=NATIVE["on"])
             await srv2.start()
             assert srv2.engine.node_devices("n") == [(10, 6)]
             await srv2.stop()
@@ -258,7 +259,7 @@ def test_recovery_consistency_check_flags_overcommit():
             for nm in ("a", "b"):
                 await c.client.create("pods", make_pod(nm, 8, node="n", phase="Running", annotations={
                     "SHARED_GPU_MEM_IDX": "0", "SHARED_GPU_MEM_POD": "8"}))
-            srv2 = ExtenderServer(KubeClient(c.api.url), SHARED_GPU)
+            srv2 = ExtenderServer(KubeClient(c.api.url), SHARED_GPU, native_controller=NATIVE["on"])
             await srv2.start()
             try:
                 assert srv2.controller.overcommitted == [("n", 0, 16, 10)]
@@ -297,10 +298,10 @@ def test_leader_election_failover():
             await c.client.create("nodes", make_node("n", 100, 1))
             kw = dict(leader_elect=True, lease_namespace="default", lease_duration=2.0, renew_deadline=1.2,
                       retry_period=0.05)
-            a = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, **kw),
+            a = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, native_controller=NATIVE["on"], **kw),
                                      native=NATIVE["on"]).start()
             await asyncio.sleep(0.2)
-            b = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, **kw),
+            b = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, native_controller=NATIVE["on"], **kw),
                                      native=NATIVE["on"]).start()
             try:
                 await c.settle(lambda: a.server.is_leader, 3)
@@ -310,7 +311,7 @@ def test_leader_election_failover():
                     assert r.status == 503 and "standby" in await r.text()
                 p = await c.client.create("pods", make_pod("x", 10))
                 args = wire.ExtenderBindingArgs("x", "default", p["metadata"]["uid"], "n").encode()
-                await c.settle(lambda: b.server.controller.pods.get("default/x") is not None)
+                await c.settle(lambda: b.server.controller.get_pod("x", "default") is not None)
                 async with c.http.post(b.url + "/gpushare-scheduler/bind", data=args) as r:
                     assert r.status == 500 and "not the leader" in json.loads(await r.read())["Error"]
                 # the leader goes away (Lease released on stop); the standby takes over and binds

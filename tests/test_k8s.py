@@ -22,16 +22,34 @@ def run(coro):
     return asyncio.run(coro)
 
 
-async def _api(history=200000):
-    r = await FakeApiServerRunner(FakeApiServer(history=history)).start()
+class _NativeApi:
+    """gsx-fakeapi (native/fakeapi) as a child process, with the runner interface the tests use."""
+
+    def __init__(self, history):
+        from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver
+
+        self.proc = start_apiserver(native=True, history=history)
+        self.url = self.proc.url
+
+    async def stop(self):
+        self.proc.stop()
+
+
+async def _api(history=200000, impl="python"):
+    """The asyncio fake apiserver in-process, or the compiled one (same REST semantics)."""
+    r = _NativeApi(history) if impl == "native" else await FakeApiServerRunner(FakeApiServer(history=history)).start()
     return r, KubeClient(r.url)
+
+
+IMPLS = pytest.mark.parametrize("impl", ["python", "native"])
 
 
 # ---------------------------------------------------------------- fake apiserver semantics
 
-def test_optimistic_concurrency_exact_message_and_patch():
+@IMPLS
+def test_optimistic_concurrency_exact_message_and_patch(impl):
     async def go():
-        r, c = await _api()
+        r, c = await _api(impl=impl)
         try:
             p = await c.create("pods", make_pod("a", 2))
             stale = dict(p)
@@ -57,9 +75,10 @@ def test_optimistic_concurrency_exact_message_and_patch():
     run(go())
 
 
-def test_binding_copies_annotations_once():
+@IMPLS
+def test_binding_copies_annotations_once(impl):
     async def go():
-        r, c = await _api()
+        r, c = await _api(impl=impl)
         try:
             p = await c.create("pods", make_pod("a", 2, annotations={"keep": "me"}))
             await c.bind_pod("default", "a", "n1", p["metadata"]["uid"], {"IDX": "3"})
@@ -81,9 +100,10 @@ def test_binding_copies_annotations_once():
     run(go())
 
 
-def test_selectors_graceful_delete_and_deletecollection():
+@IMPLS
+def test_selectors_graceful_delete_and_deletecollection(impl):
     async def go():
-        r, c = await _api()
+        r, c = await _api(impl=impl)
         try:
             await c.create("pods", make_pod("a", 1, node="n1", labels={"wave": "1"}))
             await c.create("pods", make_pod("b", 1, node="n2", labels={"wave": "1"}))
@@ -110,9 +130,10 @@ def test_selectors_graceful_delete_and_deletecollection():
     run(go())
 
 
-def test_watch_from_compacted_version_is_410():
+@IMPLS
+def test_watch_from_compacted_version_is_410(impl):
     async def go():
-        r, c = await _api(history=3)
+        r, c = await _api(impl=impl, history=3)
         try:
             for i in range(6):
                 await c.create("pods", make_pod(f"p{i}", 1))

@@ -1,0 +1,165 @@
+"""Native (C++) controller: reflectors -> ledger (native/engine/{informer,controller}.cc).
+
+Checks the reference's controller semantics (pkg/gpushare/controller.go:174-305,
+pkg/cache/cache.go:49-127) on the C++ path against the fake kube-apiserver:
+filter transitions, bind-reservation confirmation, lifecycle removal, BuildCache
+recovery, watch drops (re-watch from the last resourceVersion) and 410 Gone
+(re-list + diff, deletes that happened while not watching).
+"""
+import asyncio
+
+from gpushare_scheduler_extender_amd.core.controller import NativeController
+from gpushare_scheduler_extender_amd.core.engine import new_engine
+from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServer, FakeApiServerRunner
+from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
+from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+
+P = SHARED_GPU
+
+
+def run(coro):
+    return asyncio.run(coro)
+
+
+async def settle(cond, timeout=5.0):
+    for _ in range(int(timeout / 0.005)):
+        if cond():
+            return
+        await asyncio.sleep(0.005)
+    raise TimeoutError("condition not reached")
+
+
+def annotated(name, mem, dev, node="n", **kw):
+    p = make_pod(name, mem, profile=P, node=node, **kw)
+    p["metadata"]["annotations"] = {P.annotation_idx: str(dev), P.annotation_pod: str(mem),
+                                    P.annotation_dev: "16", P.annotation_assigned: "false"}
+    return p
+
+
+class Env:
+    def __init__(self, history=200000):
+        self.history = history
+
+    async def __aenter__(self):
+        self.api = await FakeApiServerRunner(FakeApiServer(history=self.history)).start()
+        self.c = KubeClient(self.api.url)
+        self.eng = new_engine(P)
+        self.ctl = None
+        return self
+
+    async def start(self):
+        self.ctl = NativeController(KubeClient(self.api.url), self.eng, P, resync_period=0.2)
+        await self.ctl.start(10)
+        return self.ctl
+
+    async def __aexit__(self, *exc):
+        if self.ctl:
+            await self.ctl.stop()
+            await self.ctl.client.close()
+        await self.c.close()
+        await self.api.stop()
+
+    def used(self, node="n"):
+        return [u for _t, u in self.eng.node_devices(node)]
+
+
+def test_native_controller_lifecycle_and_filter_transitions():
+    async def go():
+        async with Env() as e:
+            await e.c.create("nodes", make_node("n", 32, 2, profile=P))
+            await e.start()
+            assert e.eng.has_node("n") and e.ctl.is_synced()
+            # annotated, bound pod -> accounted on its device
+            await e.c.create("pods", annotated("a", 8, 1))
+            await settle(lambda: e.used() == [0, 8])
+            assert e.ctl.get_pod("a", "default")["metadata"]["name"] == "a"
+            # a pod that does not request gpu-mem never enters the ledger nor the lister
+            await e.c.create("pods", make_pod("plain", 0, profile=P, node="n"))
+            # device index rewritten -> re-accounted
+            pod = await e.c.get("pods", "a", "default")
+            pod["metadata"]["annotations"][P.annotation_idx] = "0"
+            await e.c.replace("pods", pod)
+            await settle(lambda: e.used() == [8, 0])
+            # Succeeded -> removed (IsCompletePod)
+            pod = await e.c.get("pods", "a", "default")
+            pod["status"] = {"phase": "Succeeded"}
+            await e.c.request("PUT", "/api/v1/namespaces/default/pods/a/status", body=pod)
+            await settle(lambda: e.used() == [0, 0])
+            # delete of an accounted pod frees memory
+            await e.c.create("pods", annotated("b", 4, 0))
+            await settle(lambda: e.used() == [4, 0])
+            await e.c.delete("pods", "b", "default")
+            await settle(lambda: e.used() == [0, 0] and e.ctl.get_pod("b", "default") is None)
+            assert e.ctl.get_pod("plain", "default") is None
+            # node capacity change rebuilds the device layout
+            node = await e.c.get("nodes", "n")
+            node["status"]["capacity"][P.resource] = "48"
+            node["status"]["capacity"][P.count] = "3"
+            await e.c.replace("nodes", node)
+            await settle(lambda: [t for t, _u in e.eng.node_devices("n")] == [16, 16, 16])
+            await e.c.delete("nodes", "n")
+            await settle(lambda: not e.eng.has_node("n"))
+            st = e.ctl.stats()
+            assert st["pod_events"] >= 6 and st["node_events"] >= 2 and st["removes"] >= 2
+    run(go())
+
+
+def test_native_controller_confirms_bind_reservation():
+    async def go():
+        async with Env() as e:
+            await e.c.create("nodes", make_node("n", 32, 2, profile=P))
+            await e.c.create("pods", make_pod("x", 8, profile=P))
+            await e.start()
+            pod = await e.c.get("pods", "x", "default")
+            uid = pod["metadata"]["uid"]
+            dev, _total = e.eng.assume(uid, "default", "x", "n", 8)
+            e.eng.finish_bind(uid, True, 60.0)
+            assert e.eng.pod_state(uid)[0] == 2  # assumed
+            ann = {P.annotation_idx: str(dev), P.annotation_pod: "8", P.annotation_dev: "16",
+                   P.annotation_assigned: "false", P.annotation_assume_time: "1"}
+            await e.c.bind_pod("default", "x", "n", uid, ann)
+            await settle(lambda: e.eng.pod_state(uid)[0] == 1)  # observed with annotations: confirmed
+            assert e.used() == [8, 0]
+    run(go())
+
+
+def test_native_controller_build_cache_recovery_and_overcommit():
+    async def go():
+        async with Env() as e:
+            await e.c.create("nodes", make_node("n", 20, 2, profile=P))  # 10 per device
+            await e.c.create("pods", annotated("a", 6, 0))
+            await e.c.create("pods", annotated("b", 10, 0))  # 16 > 10: over-committed
+            await e.c.create("pods", annotated("c", 3, 1))
+            await e.start()
+            assert e.used() == [16, 3]
+            assert e.ctl.overcommitted == [("n", 0, 16, 10)]
+            assert e.ctl.stats()["recovered"] == 3
+            assert e.eng.check("n", 7) == 0 and e.eng.check("n", 8) == 3  # device 1: 7 free; device 0 never wraps
+    run(go())
+
+
+def test_native_controller_rewatch_and_relist_after_410():
+    async def go():
+        async with Env() as e:
+            await e.c.create("nodes", make_node("n", 32, 2, profile=P))
+            await e.start()
+            # dropped streams: the reflector re-watches from its last resourceVersion, nothing is lost
+            e.api.server.faults.update({"drop_watch_after": 2})
+            for i in range(6):
+                await e.c.create("pods", annotated(f"p{i}", 1, i % 2))
+            await settle(lambda: e.used() == [3, 3])
+            assert e.ctl.stats()["pod_rewatches"] >= 2
+            # while no watch is open the pod is deleted; the next watches are told 410 -> LIST + diff
+            assert e.ctl.stats()["pod_lists"] == 1
+            await e.c.request("POST", "/fake/faults", body={"drop_watch_after": 0, "hold_watches": True,
+                                                            "drop_watches_now": True})
+            await asyncio.sleep(0.1)
+            await e.c.delete("pods", "p0", "default")
+            await e.c.request("POST", "/fake/faults", body={"expire_watches": 2, "hold_watches": False})
+            await settle(lambda: e.used() == [2, 3] and e.ctl.stats()["pod_lists"] == 2)
+            assert e.ctl.get_pod("p0", "default") is None
+            # and it keeps watching afterwards
+            await e.c.create("pods", annotated("late", 2, 1))
+            await settle(lambda: e.used() == [2, 5])
+    run(go())

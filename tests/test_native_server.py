@@ -103,7 +103,7 @@ def test_native_bind_fast_path_and_python_fallback():
             p1 = await c.create("pods", make_pod("fast", 30))
             p2 = await c.create("pods", make_pod("slow", 20))
             for _ in range(200):
-                if ext.server.controller.pods.get("default/slow"):
+                if ext.server.controller.get_pod("slow", "default"):
                     break
                 await asyncio.sleep(0.01)
             async with aiohttp.ClientSession() as s:
