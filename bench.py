@@ -73,6 +73,15 @@ def _cpu_times(children) -> dict:
     return out
 
 
+def _cgroup_cpu() -> dict:
+    """cgroup v2 cpu.stat (usage / throttling) of this container, {} where unavailable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f if ln.strip())}
+    except (OSError, ValueError):
+        return {}
+
+
 def pct(xs, q):
     if not xs:
         return None
@@ -107,6 +116,10 @@ def parse():
 
 
 def main():
+    import signal
+
+    # torchrun stops the other ranks with SIGTERM when one fails: exit through atexit so child servers stop too
+    signal.signal(signal.SIGTERM, lambda *_: sys.exit(143))
     a = parse()
     if a.inproc:
         a.agent = "rank"  # no child processes at all: the agents run in-process too
@@ -159,6 +172,8 @@ def main():
     from gpushare_scheduler_extender_amd.models.profile import get_profile
     from gpushare_scheduler_extender_amd.sim.scheduler import SchedulerSim
 
+    # ranks do no CPU tensor work: one intra-op thread each, so 8 ranks never burst past a container's CPU quota
+    torch.set_num_threads(1)
     profile = get_profile(a.profile)
     use_gpu = a.devices != "fake" and torch.cuda.is_available()
     if use_gpu:
@@ -346,6 +361,7 @@ def main():
             barrier()
             t_start = time.perf_counter()
             cpu0 = _cpu_times(children)
+            cg0 = _cgroup_cpu()
         if rank == 0:
             r = wave(step)
             if step >= a.warmup:
@@ -354,9 +370,14 @@ def main():
             dist.barrier(group=ctl)  # warmup waves in lockstep; timed waves are driven by rank 0 alone
         if rank == 0 and world > 1 and step < a.warmup:
             dist.barrier(group=ctl)
+    if world > 1:
+        # ranks > 0 wait for rank 0's timed waves in a blocking gloo barrier (no CPU / GPU-sync spinning),
+        # then everyone leaves through the barrier + synchronize bracket
+        dist.barrier(group=ctl)
     barrier()
     elapsed = time.perf_counter() - t_start
     cpu1 = _cpu_times(children)
+    cg1 = _cgroup_cpu()
     if prof is not None:
         lt.run(asyncio.sleep(0))
         lt.loop.call_soon_threadsafe(prof.disable)
@@ -375,6 +396,16 @@ def main():
         mine = {"admitted": shim.admitted, "failed": shim.failed, "bad_stamps": shim.bad + bad}
     mine.update({"gpu": local_rank, "hbm_total": dev.total_bytes, "arena": arena})
     agent_stats = gather(mine)
+    node_agent_stats = None
+    if rank == 0 and a.agent == "node" and a.node_agent == "native":
+        na = next(c for c in children if c.name == "node-agent")
+        st, body = E.BatchClient({"server": na.url}).run([("GET", "/v1/stats", b"")], 1)[0]
+        node_agent_stats = json.loads(body) if st == 200 else {"error": st}
+    apiserver_stats = None
+    if rank == 0 and not a.inproc:
+        st, body = api_batch.run([("GET", "/fake/stats", b"")], 1)[0]
+        apiserver_stats = json.loads(body) if st == 200 else {"error": st}
+        apiserver_stats.pop("counts", None)
 
     if rank == 0:
         for s in step_stats:
@@ -419,9 +450,20 @@ def main():
             "wave_ms": {"bound": round(1e3 * statistics.mean(s["t_bound"] for s in step_stats), 3),
                         "running": round(1e3 * statistics.mean(s["t_run"] for s in step_stats), 3),
                         "total": round(1e3 * statistics.mean(s["t_total"] for s in step_stats), 3)},
+            "wave_ms_p50": {k: round(1e3 * pct([s[t] for s in step_stats], 50), 3)
+                            for k, t in (("bound", "t_bound"), ("running", "t_run"), ("total", "t_total"))},
+            "wave_ms_max": {k: round(1e3 * max(s[t] for s in step_stats), 3)
+                            for k, t in (("bound", "t_bound"), ("running", "t_run"), ("total", "t_total"))},
             "bind_retries": sum(sum(s["attempts"]) - len(s["attempts"]) for s in step_stats),
             "agents": agent_stats,
+            "node_agent": node_agent_stats,
+            "apiserver": apiserver_stats,
             "cpu_s": {k: round(cpu1[k] - cpu0.get(k, 0.0), 3) for k in cpu1},
+            # CPU-quota throttling of the container during the timed region (cgroup v2), if any
+            "cgroup_timed": {"usage_ms": round((cg1.get("usage_usec", 0) - cg0.get("usage_usec", 0)) / 1e3, 1),
+                             "nr_throttled": cg1.get("nr_throttled", 0) - cg0.get("nr_throttled", 0),
+                             "throttled_ms": round((cg1.get("throttled_usec", 0) - cg0.get("throttled_usec", 0)) / 1e3,
+                                                   1)} if cg1 else None,
         }
         line = json.dumps(out)
         print(line, flush=True)

@@ -8,6 +8,7 @@ child; callers start them before touching the GPU).
 """
 from __future__ import annotations
 
+import atexit
 import os
 import subprocess
 import sys
@@ -32,6 +33,19 @@ def _wait_port(path: str, proc: subprocess.Popen, timeout: float = 60.0) -> int:
     raise TimeoutError(f"child did not publish a port in {path}")
 
 
+_LIVE: set = set()
+
+
+@atexit.register
+def _stop_all():
+    """Children never outlive their parent, also when it fails before its own teardown."""
+    for c in list(_LIVE):
+        try:
+            c.stop()
+        except Exception:  # noqa: BLE001 - best effort at exit
+            pass
+
+
 class ChildProc:
     def __init__(self, args: list[str], name: str, env: dict | None = None):
         self.name = name
@@ -52,6 +66,7 @@ class ChildProc:
         argv = [sys.executable, *args] if args[0] == "-m" else list(args)
         self.proc = subprocess.Popen([*argv, "--port-file", self.port_file], stdout=self.log,
                                      stderr=subprocess.STDOUT, env=e, cwd=str(ROOT))
+        _LIVE.add(self)
         self.port = _wait_port(self.port_file, self.proc)
         self.url = f"http://127.0.0.1:{self.port}"
 
@@ -65,6 +80,7 @@ class ChildProc:
     def stop(self):
         import shutil  # noqa: PLC0415
 
+        _LIVE.discard(self)
         if self.proc.poll() is None:
             self.proc.terminate()
             try:
@@ -110,7 +126,7 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
         if not NODEAGENT.exists():
             raise FileNotFoundError(f"{NODEAGENT} missing; run `python native/build.py nodeagent`")
         return ChildProc([str(NODEAGENT), "--node", node, "--apiserver", apiserver, "--profile", profile,
-                          "--workers", str(min(workers, 64))], "node-agent")
+                          "--workers", str(min(workers, 16))], "node-agent")
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
                       apiserver, "--profile", profile, "--workers", str(workers)], "node-agent")
 
@@ -130,6 +146,6 @@ def start_scheduler(apiserver: str, extender: str, profile: str = "shared-gpu", 
         if not SCHEDSIM.exists():
             raise FileNotFoundError(f"{SCHEDSIM} missing; run `python native/build.py schedsim`")
         return ChildProc([str(SCHEDSIM), "--apiserver", apiserver, "--extender", extender, "--profile", profile,
-                          "--bind-threads", str(min(64, max_inflight_binds))], "scheduler")
+                          "--bind-threads", str(min(16, max_inflight_binds))], "scheduler")
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.sim", "--apiserver", apiserver, "--extender", extender,
                       "--profile", profile, "--max-inflight-binds", str(max_inflight_binds)], "scheduler")

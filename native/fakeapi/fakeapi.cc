@@ -330,6 +330,7 @@ class Server {
     while (!*stop) {
       int timeout = next_timeout_ms();
       int n = epoll_wait(ep_, evs.data(), static_cast<int>(evs.size()), timeout);
+      double t_iter = now_s();
       for (int i = 0; i < n; ++i) {
         uint64_t id = evs[i].data.u64;
         if (id == 0) {
@@ -348,6 +349,7 @@ class Server {
       }
       run_timers();
       flush_watchers();
+      max_iter_ = std::max(max_iter_, now_s() - t_iter);
     }
   }
 
@@ -982,7 +984,10 @@ class Server {
       }
       size_t live = 0;
       for (auto& w : watchers_) live += w->closed ? 0 : 1;
-      o.append("},\"watchers\":").append(std::to_string(live));
+      char mx[64];
+      std::snprintf(mx, sizeof(mx), "},\"max_iter_ms\":%.3f", max_iter_ * 1e3);
+      o.append(mx);
+      o.append(",\"watchers\":").append(std::to_string(live));
       for (auto& kv : store_) o.append(",\"" + kv.first + "\":" + std::to_string(kv.second.size()));
       o.push_back('}');
       rep->body = o;
@@ -1122,6 +1127,7 @@ class Server {
   };
 
   size_t history_max_;
+  double max_iter_ = 0;  // longest event-loop iteration (request handling + fan-out), seconds
   int lfd_ = -1, ep_ = -1;
   uint64_t next_id_ = 0;
   std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns_;

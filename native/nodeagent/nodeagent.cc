@@ -248,12 +248,15 @@ class Agent {
       std::vector<double> lat = latency_;
       std::sort(lat.begin(), lat.end());
       double p50 = lat.empty() ? 0 : lat[lat.size() / 2];
-      char b[256];
+      char b[512];
       std::snprintf(b, sizeof(b),
                     "{\"admitted\":%llu,\"failed\":%llu,\"bad_stamps\":%llu,\"conflicts\":%llu,\"running\":%zu,"
-                    "\"admit_p50_ms\":%.3f,\"native\":true}",
+                    "\"admit_p50_ms\":%.3f,\"admit_max_ms\":%.3f,\"max_ms\":{\"queue\":%.3f,\"assign_patch\":%.3f,"
+                    "\"runtime\":%.3f,\"running_patch\":%.3f},\"api_connects\":%llu,\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
-                    (unsigned long long)conflicts_, running_.size(), p50 * 1e3);
+                    (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
+                    max_queue_ * 1e3, max_patch_ * 1e3, max_runtime_ * 1e3, max_status_ * 1e3,
+                    (unsigned long long)api_.reconnects());
       rep.body = b;
       return rep;
     }
@@ -529,7 +532,9 @@ class Agent {
     std::string path = "/api/v1/namespaces/" + pod.ns + "/pods/" + pod.name;
     int status = 0;
     std::string resp, err;
+    double tp0 = now_s();
     bool ok = api_.request("PATCH", path, patch, "application/merge-patch+json", &status, &resp, &err);
+    double tp1 = now_s();
     if (!ok || status >= 300) {
       lk.lock();
       if (!cus.empty()) cus_.at(dev_idx).release(uid);
@@ -562,6 +567,7 @@ class Agent {
     body.append(",\"verify\":").append(verify_ ? "true" : "false").append("}");
     std::string rresp;
     int rst = runtime_call(dev_idx, "POST", "/v1/pods/" + uid, body, &rresp);
+    double tp2 = now_s();
     int64_t bad = 0;
     std::string why;
     if (rst != 200) {
@@ -598,7 +604,12 @@ class Agent {
     lk.unlock();
     api_.request("PATCH", path + "/status", "{\"status\":{\"phase\":\"Running\"}}", "application/merge-patch+json",
                  &status, &resp, &err);
+    double tp3 = now_s();
     lk.lock();
+    max_patch_ = std::max(max_patch_, tp1 - tp0);
+    max_runtime_ = std::max(max_runtime_, tp2 - tp1);
+    max_status_ = std::max(max_status_, tp3 - tp2);
+    max_queue_ = std::max(max_queue_, tp0 - t0);
     latency_.push_back(now_s() - t0);
     if (latency_.size() > 100000) latency_.erase(latency_.begin(), latency_.begin() + 50000);
     seen_.erase(uid);
@@ -645,6 +656,8 @@ class Agent {
   std::vector<double> latency_;
   uint64_t admitted_ = 0, failed_ = 0, bad_ = 0, conflicts_ = 0;
   int added_ = 0;  // work items queued since the last wake_locked()
+  // worst case per admission step (seconds): queue wait, ASSIGNED patch, runtime admit, Running patch
+  double max_queue_ = 0, max_patch_ = 0, max_runtime_ = 0, max_status_ = 0;
   std::vector<std::thread> workers_;
 };
 
