@@ -73,6 +73,51 @@ def _cpu_times(children) -> dict:
     return out
 
 
+class NativeRuntime:
+    """One GPU's pod runtime endpoint served from C++ (``_engine.PodRuntime``) with the rank's HBM arena."""
+
+    def __init__(self, dev: int, arena_bytes: int, use_gpu: bool, stride: int):
+        from gpushare_scheduler_extender_amd.core.engine import native
+
+        self.buf = self.stream = None
+        if use_gpu:
+            from gpushare_scheduler_extender_amd.ops import hip
+
+            self.buf = hip.DeviceBuffer(dev, arena_bytes)
+            self.stream = hip.Stream(dev)
+            self.rt = native().PodRuntime(dev, arena_bytes, self.buf.addr(0), self.stream.ptr, stride,
+                                          hip.lib()._name)
+        else:
+            self.rt = native().PodRuntime(dev, arena_bytes)
+        self.url = f"http://127.0.0.1:{self.rt.serve('127.0.0.1', 0)}"
+
+    @property
+    def admitted(self):
+        return self.rt.stats()["admitted"]
+
+    @property
+    def failed(self):
+        return self.rt.stats()["failed"]
+
+    @property
+    def bad(self):
+        return self.rt.stats()["bad"]
+
+    def verify(self) -> int:
+        return self.rt.verify()
+
+    def stop(self):
+        self.rt.stop()
+
+    def close(self):
+        self.rt.stop()
+        if self.stream is not None:
+            self.stream.sync()
+            self.stream.destroy()
+        if self.buf is not None:
+            self.buf.free()
+
+
 def _cgroup_cpu() -> dict:
     """cgroup v2 cpu.stat (usage / throttling) of this container, {} where unavailable."""
     try:
@@ -220,11 +265,16 @@ def main():
     unit = "GiB"
     pod_bytes = a.pod_gib * UNITS[unit]
     arena = a.pods_per_gpu * pod_bytes
-    runtime = (HbmArenaRuntime({local_rank: arena}, stamp_stride=a.stamp_stride) if use_gpu
-               else LedgerRuntime({local_rank: arena}))
     # this GPU's runtime endpoint (CRI-runtime role): the node agent starts pods on it over HTTP
-    shim = RuntimeShim(runtime)
-    shim_url = lt.run(shim.start("127.0.0.1", 0))
+    if a.agent == "node":
+        # native (native/engine/podruntime.cc): request threads carve the slice and run the HIP admission
+        runtime = shim = NativeRuntime(local_rank, arena, use_gpu, a.stamp_stride)
+        shim_url = shim.url
+    else:
+        runtime = (HbmArenaRuntime({local_rank: arena}, stamp_stride=a.stamp_stride) if use_gpu
+                   else LedgerRuntime({local_rank: arena}))
+        shim = RuntimeShim(runtime)
+        shim_url = lt.run(shim.start("127.0.0.1", 0))
     all_devs = gather((dev.to_dict(), shim_url))
     from gpushare_scheduler_extender_amd.deviceplugin.devices import Device
     from gpushare_scheduler_extender_amd.models.profile import (NODE_DEVICE_INFO_ANNOTATION,
@@ -476,7 +526,10 @@ def main():
         if agent is not None:
             lt.run(agent.stop(), 30)
         lt.run(agent_client.close(), 30)
-        lt.run(shim.stop(), 30)
+        if isinstance(shim, NativeRuntime):
+            shim.stop()
+        else:
+            lt.run(shim.stop(), 30)
         if rank == 0:
             if sim is not None:
                 lt.run(sim.stop(), 30)

@@ -87,7 +87,7 @@ def build_engine(force: bool = False, verbose: bool = False) -> Path:
     objs = _compile_objs(srcs, "g++", flags, "engine", force, verbose, headers)
     if force or _newer(out, objs):
         OUT.mkdir(parents=True, exist_ok=True)
-        _run(["g++", "-shared", "-o", str(out), *map(str, objs), "-lssl", "-lcrypto", "-lpthread"], verbose)
+        _run(["g++", "-shared", "-o", str(out), *map(str, objs), "-lssl", "-lcrypto", "-lpthread", "-ldl"], verbose)
     return out
 
 
@@ -102,7 +102,7 @@ def _build_native_tool(name: str, srcdir: str, force: bool, verbose: bool) -> Pa
     out = OUT / name
     if force or _newer(out, objs):
         OUT.mkdir(parents=True, exist_ok=True)
-        _run(["g++", "-o", str(out), *map(str, objs), "-lssl", "-lcrypto", "-lpthread"], verbose)
+        _run(["g++", "-o", str(out), *map(str, objs), "-lssl", "-lcrypto", "-lpthread", "-ldl"], verbose)
     return out
 
 
@@ -179,7 +179,7 @@ def build_asan(force: bool = False, verbose: bool = False) -> Path:
     if force or _newer(out, srcs + sorted(src.glob("*.h"))):
         out.parent.mkdir(parents=True, exist_ok=True)
         _run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
-              "-I" + str(src), *map(str, srcs), "-o", str(out), "-lssl", "-lcrypto", "-lpthread"], verbose)
+              "-I" + str(src), *map(str, srcs), "-o", str(out), "-lssl", "-lcrypto", "-lpthread", "-ldl"], verbose)
     return out
 
 
@@ -191,7 +191,7 @@ def build_tsan(force: bool = False, verbose: bool = False) -> Path:
     if force or _newer(out, srcs + sorted(src.glob("*.h"))):
         out.parent.mkdir(parents=True, exist_ok=True)
         _run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=thread", "-fno-omit-frame-pointer",
-              "-I" + str(src), *map(str, srcs), "-o", str(out), "-lssl", "-lcrypto", "-lpthread"], verbose)
+              "-I" + str(src), *map(str, srcs), "-o", str(out), "-lssl", "-lcrypto", "-lpthread", "-ldl"], verbose)
     return out
 
 

@@ -12,6 +12,7 @@
 #include "controller.h"
 #include "server.h"
 #include "tracker.h"
+#include "podruntime.h"
 
 namespace py = pybind11;
 using namespace gsx;
@@ -495,6 +496,66 @@ class PyBatchClient {
   BatchClient c_;
 };
 
+class PyPodRuntime {
+ public:
+  PyPodRuntime(int dev, uint64_t arena_bytes, uint64_t arena_addr, uint64_t stream, uint64_t stride,
+               const std::string& kernels_lib) {
+    PodRuntimeConfig c;
+    c.dev = dev;
+    c.arena_bytes = arena_bytes;
+    c.arena_addr = arena_addr;
+    c.stream = reinterpret_cast<void*>(stream);
+    c.stride = stride;
+    c.kernels_lib = kernels_lib;
+    r_ = std::make_unique<PodRuntime>(c);
+    std::string err;
+    if (!r_->init(&err)) throw std::runtime_error(err);
+  }
+  int serve(const std::string& host, int port) {
+    std::string err;
+    int p = r_->serve(host, port, &err);
+    if (p < 0) throw std::runtime_error(err);
+    return p;
+  }
+  void stop() {
+    py::gil_scoped_release rel;
+    r_->stop();
+  }
+  int64_t admit(const std::string& uid, uint64_t bytes, bool verify) {
+    std::string err;
+    int64_t bad;
+    {
+      py::gil_scoped_release rel;
+      bad = r_->admit(uid, bytes, verify, &err);
+    }
+    if (bad < 0) throw std::runtime_error(err);
+    return bad;
+  }
+  bool release(const std::string& uid) { return r_->release(uid); }
+  int64_t verify() {
+    std::string err;
+    int64_t bad;
+    {
+      py::gil_scoped_release rel;
+      bad = r_->verify_all(&err);
+    }
+    if (bad < 0) throw std::runtime_error(err);
+    return bad;
+  }
+  py::dict stats() const {
+    py::dict d;
+    d["admitted"] = r_->admitted();
+    d["failed"] = r_->failed();
+    d["bad"] = r_->bad();
+    d["resident"] = r_->resident();
+    d["resident_bytes"] = r_->resident_bytes();
+    return d;
+  }
+
+ private:
+  std::unique_ptr<PodRuntime> r_;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_engine, m) {
@@ -579,6 +640,17 @@ PYBIND11_MODULE(_engine, m) {
   py::class_<PyBatchClient>(m, "BatchClient")
       .def(py::init<const py::dict&>())
       .def("run", &PyBatchClient::run, py::arg("requests"), py::arg("concurrency") = 8);
+
+  py::class_<PyPodRuntime>(m, "PodRuntime")
+      .def(py::init<int, uint64_t, uint64_t, uint64_t, uint64_t, const std::string&>(), py::arg("dev"),
+           py::arg("arena_bytes"), py::arg("arena_addr") = 0, py::arg("stream") = 0, py::arg("stride") = 1 << 20,
+           py::arg("kernels_lib") = std::string())
+      .def("serve", &PyPodRuntime::serve, py::arg("host") = "127.0.0.1", py::arg("port") = 0)
+      .def("stop", &PyPodRuntime::stop)
+      .def("admit", &PyPodRuntime::admit, py::arg("uid"), py::arg("bytes"), py::arg("verify") = true)
+      .def("release", &PyPodRuntime::release)
+      .def("verify", &PyPodRuntime::verify)
+      .def("stats", &PyPodRuntime::stats);
 
   m.def("parse_quantity", [](const std::string& s) {
     int64_t v;

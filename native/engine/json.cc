@@ -455,17 +455,32 @@ bool unescape(std::string_view s, std::string* out) {
   return true;
 }
 
+namespace {
+// 1 for bytes Go's encoding/json (HTML-safe) copies verbatim.
+struct SafeTable {
+  bool t[256];
+  SafeTable() {
+    for (int c = 0; c < 256; ++c) t[c] = c >= 0x20 && c < 0x80 && c != '"' && c != '\\' && c != '<' && c != '>' && c != '&';
+  }
+};
+const SafeTable kSafe;
+}  // namespace
+
 void append_quoted(std::string* out, std::string_view s) {
   static const char* hex = "0123456789abcdef";
   out->push_back('"');
   size_t i = 0;
-  while (i < s.size()) {
-    unsigned char c = static_cast<unsigned char>(s[i]);
-    if (c >= 0x20 && c != '"' && c != '\\' && c != '<' && c != '>' && c != '&' && c < 0x80) {
-      out->push_back(char(c));
-      ++i;
-      continue;
+  const size_t n = s.size();
+  while (i < n) {
+    // bulk-copy the run of bytes that need no escaping
+    size_t j = i;
+    while (j < n && kSafe.t[static_cast<unsigned char>(s[j])]) ++j;
+    if (j > i) {
+      out->append(s.data() + i, j - i);
+      i = j;
+      if (i == n) break;
     }
+    unsigned char c = static_cast<unsigned char>(s[i]);
     if (c < 0x80) {
       switch (c) {
         case '"': out->append("\\\""); break;
@@ -482,7 +497,7 @@ void append_quoted(std::string* out, std::string_view s) {
       continue;
     }
     // U+2028 / U+2029 are E2 80 A8 / E2 80 A9
-    if (c == 0xE2 && i + 2 < s.size() && static_cast<unsigned char>(s[i + 1]) == 0x80 &&
+    if (c == 0xE2 && i + 2 < n && static_cast<unsigned char>(s[i + 1]) == 0x80 &&
         (static_cast<unsigned char>(s[i + 2]) == 0xA8 || static_cast<unsigned char>(s[i + 2]) == 0xA9)) {
       out->append(static_cast<unsigned char>(s[i + 2]) == 0xA8 ? "\\u2028" : "\\u2029");
       i += 3;

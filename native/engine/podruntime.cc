@@ -1,0 +1,202 @@
+#include "podruntime.h"
+
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#include "json.h"
+
+namespace gsx {
+
+namespace {
+
+constexpr uint64_t kAlign = 2ull << 20;
+
+// Per-pod stamp tag: FNV-1a of the uid, odd (never 0 = "unstamped").
+uint64_t tag_of(const std::string& uid) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : uid) {
+    h ^= c;
+    h *= 1099511628211ull;
+  }
+  return h | 1;
+}
+
+// layout of gsx_slice in gsx_kernels.h
+struct GsxSlice {
+  uint64_t addr, bytes, tag;
+};
+
+}  // namespace
+
+PodRuntime::PodRuntime(PodRuntimeConfig cfg) : cfg_(std::move(cfg)) {}
+
+PodRuntime::~PodRuntime() {
+  stop();
+  if (lib_) dlclose(lib_);
+}
+
+bool PodRuntime::init(std::string* err) {
+  if (!cfg_.arena_addr) return true;  // accounting only
+  lib_ = dlopen(cfg_.kernels_lib.c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (!lib_) {
+    *err = std::string("dlopen ") + cfg_.kernels_lib + ": " + dlerror();
+    return false;
+  }
+  set_device_ = reinterpret_cast<int (*)(int)>(dlsym(lib_, "gsx_set_device"));
+  admit_ = reinterpret_cast<int (*)(void*, const void*, int, int, uint64_t, uint64_t*)>(dlsym(lib_, "gsx_hbm_admit"));
+  last_error_ = reinterpret_cast<const char* (*)()>(dlsym(lib_, "gsx_last_error"));
+  if (!set_device_ || !admit_ || !last_error_) {
+    *err = "libgsx_kernels.so lacks gsx_set_device / gsx_hbm_admit";
+    return false;
+  }
+  if (!cfg_.stream || cfg_.stride < 16 || cfg_.stride % 16) {
+    *err = "pod runtime needs a stream and a 16-B multiple stamp stride";
+    return false;
+  }
+  return true;
+}
+
+int PodRuntime::serve(const std::string& host, int port, std::string* err) {
+  srv_ = std::make_unique<CtlServer>([this](const http::Message& m) { return handle(m); });
+  return srv_->start(host, port, err);
+}
+
+void PodRuntime::stop() {
+  if (srv_) srv_->stop();
+}
+
+uint64_t PodRuntime::resident_bytes() const {
+  std::lock_guard<std::mutex> g(mu_);
+  uint64_t b = 0;
+  for (auto& kv : slices_) b += kv.second.size;
+  return b;
+}
+
+size_t PodRuntime::resident() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return slices_.size();
+}
+
+// Stamp `uid`'s slice (if given) and verify every resident slice; mu_ held.
+int64_t PodRuntime::run_admit(int stamp, const std::string& uid, bool verify, std::string* err) {
+  if (!cfg_.arena_addr) return 0;
+  std::vector<GsxSlice> sl;
+  sl.reserve(slices_.size());
+  int idx = -1;
+  for (auto& kv : slices_) {
+    if (stamp && kv.first == uid) idx = static_cast<int>(sl.size());
+    sl.push_back(GsxSlice{cfg_.arena_addr + kv.second.off, kv.second.size, kv.second.tag});
+  }
+  if (stamp && !verify) {  // stamp only: pass just the new slice
+    GsxSlice one = sl[static_cast<size_t>(idx)];
+    sl.assign(1, one);
+    idx = 0;
+  }
+  uint64_t bad = 0;
+  int rc = set_device_(cfg_.dev);
+  if (rc == 0) rc = admit_(cfg_.stream, sl.data(), static_cast<int>(sl.size()), idx, cfg_.stride, &bad);
+  if (rc != 0) {
+    *err = std::string("gsx_hbm_admit: ") + last_error_();
+    return -1;
+  }
+  return (stamp && !verify) ? 0 : static_cast<int64_t>(bad);
+}
+
+int64_t PodRuntime::admit(const std::string& uid, uint64_t bytes, bool verify, std::string* err) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (slices_.count(uid)) return run_admit(0, uid, verify, err) < 0 ? -1 : 0;  // idempotent
+  uint64_t size = (bytes + kAlign - 1) / kAlign * kAlign;
+  // first fit over the offset-ordered slices
+  std::vector<std::pair<uint64_t, uint64_t>> used;
+  used.reserve(slices_.size());
+  for (auto& kv : slices_) used.emplace_back(kv.second.off, kv.second.size);
+  std::sort(used.begin(), used.end());
+  uint64_t pos = 0;
+  for (auto& u : used) {
+    if (u.first >= pos + size) break;
+    pos = std::max(pos, u.first + u.second);
+  }
+  if (pos + size > cfg_.arena_bytes) {
+    failed_++;
+    *err = "arena exhausted: need " + std::to_string(size) + " B at " + std::to_string(pos) + ", capacity " +
+           std::to_string(cfg_.arena_bytes);
+    return -1;
+  }
+  slices_[uid] = Slice{pos, size, tag_of(uid)};
+  int64_t bad = run_admit(1, uid, verify, err);
+  if (bad < 0) {
+    slices_.erase(uid);
+    failed_++;
+    return -1;
+  }
+  admitted_++;
+  bad_ += static_cast<uint64_t>(bad);
+  return bad;
+}
+
+bool PodRuntime::release(const std::string& uid) {
+  std::lock_guard<std::mutex> g(mu_);
+  return slices_.erase(uid) > 0;
+}
+
+int64_t PodRuntime::verify_all(std::string* err) {
+  std::lock_guard<std::mutex> g(mu_);
+  return run_admit(0, std::string(), true, err);
+}
+
+CtlServer::Reply PodRuntime::handle(const http::Message& m) {
+  CtlServer::Reply rep;
+  std::string_view path = m.path();
+  const std::string_view pre = "/v1/pods/";
+  if (path.substr(0, pre.size()) == pre && path.size() > pre.size()) {
+    std::string uid(path.substr(pre.size()));
+    if (m.method == "POST") {
+      json::Doc d;
+      std::string err;
+      int64_t bytes = 0;
+      bool verify = true;
+      if (d.parse(m.body, &err)) {
+        int64_t b = d.find(0, "bytes");
+        if (b >= 0) d.as_int(static_cast<uint32_t>(b), &bytes);
+        int64_t v = d.find(0, "verify");
+        if (v >= 0) verify = d.at(static_cast<uint32_t>(v)).type != json::T::False;
+      }
+      if (bytes <= 0) {
+        rep.status = 400;
+        rep.body = "{\"error\":\"bytes must be > 0\"}";
+        return rep;
+      }
+      int64_t bad = admit(uid, static_cast<uint64_t>(bytes), verify, &err);
+      if (bad < 0) {
+        rep.status = 409;
+        rep.body = "{\"error\":";
+        json::append_quoted(&rep.body, err);
+        rep.body.push_back('}');
+        return rep;
+      }
+      rep.body = "{\"bad\":" + std::to_string(bad) + "}";
+      return rep;
+    }
+    if (m.method == "DELETE") {
+      rep.status = release(uid) ? 200 : 404;
+      return rep;
+    }
+  }
+  if (m.method == "GET" && path == "/v1/stats") {
+    std::lock_guard<std::mutex> g(mu_);
+    char b[256];
+    std::snprintf(b, sizeof(b), "{\"admitted\":%llu,\"failed\":%llu,\"bad\":%llu,\"resident\":%zu,\"native\":true}",
+                  (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
+                  slices_.size());
+    rep.body = b;
+    return rep;
+  }
+  rep.status = 404;
+  rep.body = "{\"error\":\"not found\"}";
+  return rep;
+}
+
+}  // namespace gsx

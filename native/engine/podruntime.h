@@ -1,0 +1,70 @@
+// Per-GPU pod runtime endpoint in C++ (the CRI-runtime role of the node):
+// the node agent starts / stops pods on a GPU through it.  Counterpart of
+// deviceplugin/runtime.py (HbmArenaRuntime + RuntimeShim) without Python on
+// the admission path: the request thread carves the pod's 2 MiB-aligned slice
+// out of the GPU's HBM arena (first fit), stamps it and verifies every
+// resident slice with ONE call into libgsx_kernels.so (gsx_hbm_admit: two
+// kernel launches, one stream sync), and answers.
+//
+//   POST   /v1/pods/<uid>  {"dev","bytes","cus","verify"} -> {"bad": n} | 409 {"error"}
+//   DELETE /v1/pods/<uid>
+//   GET    /v1/stats
+//
+// With arena_addr == 0 (no GPU) only the slice accounting runs.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "ctlserver.h"
+
+namespace gsx {
+
+struct PodRuntimeConfig {
+  int dev = 0;
+  uint64_t arena_bytes = 0;
+  uint64_t arena_addr = 0;  // device pointer of the arena (0: accounting only)
+  void* stream = nullptr;   // hipStream_t for the admission kernels
+  uint64_t stride = 1 << 20;
+  std::string kernels_lib;  // path of libgsx_kernels.so (already loaded by the process)
+};
+
+class PodRuntime {
+ public:
+  explicit PodRuntime(PodRuntimeConfig cfg);
+  ~PodRuntime();
+  bool init(std::string* err);  // resolves the kernel entry points
+  int serve(const std::string& host, int port, std::string* err);
+  void stop();
+  // Admission without HTTP (tests): returns bad stamps, -1 with *err on failure.
+  int64_t admit(const std::string& uid, uint64_t bytes, bool verify, std::string* err);
+  bool release(const std::string& uid);
+  int64_t verify_all(std::string* err);
+  uint64_t admitted() const { return admitted_; }
+  uint64_t failed() const { return failed_; }
+  uint64_t bad() const { return bad_; }
+  uint64_t resident_bytes() const;
+  size_t resident() const;
+
+ private:
+  struct Slice {
+    uint64_t off, size, tag;
+  };
+  CtlServer::Reply handle(const http::Message& m);
+  int64_t run_admit(int stamp_idx_uid_known, const std::string& uid, bool verify, std::string* err);
+
+  PodRuntimeConfig cfg_;
+  mutable std::mutex mu_;
+  std::map<std::string, Slice> slices_;  // uid -> slice
+  uint64_t admitted_ = 0, failed_ = 0, bad_ = 0;
+  std::unique_ptr<CtlServer> srv_;
+  void* lib_ = nullptr;
+  int (*set_device_)(int) = nullptr;
+  int (*admit_)(void*, const void*, int, int, uint64_t, uint64_t*) = nullptr;
+  const char* (*last_error_)() = nullptr;
+};
+
+}  // namespace gsx

@@ -286,6 +286,7 @@ void NativeServer::on_readable(Loop* lp, Conn* c) {
         close_conn(lp, c);
         return;
       }
+      if (static_cast<size_t>(r) < sizeof(buf)) break;  // drained; level-triggered epoll reports more input
       continue;
     }
     if (r == 0) eof = true;

@@ -137,59 +137,77 @@ std::string trim(std::string s) {
   return s.substr(i);
 }
 
-bool label_match(const jd::Value& obj, const std::string& sel) {
-  if (sel.empty()) return true;
-  const jd::Value* md = obj.get("metadata");
-  const jd::Value* labels = md ? md->get("labels") : nullptr;
-  auto lab = [&](const std::string& k) -> const jd::Value* { return labels ? labels->get(k) : nullptr; };
-  for (std::string term : split(sel, ',')) {
-    term = trim(term);
-    if (term.empty()) continue;
-    size_t ne = term.find("!=");
-    if (ne != std::string::npos) {
-      const jd::Value* v = lab(trim(term.substr(0, ne)));
-      if (v && v->is_str() && v->s == trim(term.substr(ne + 2))) return false;
-      continue;
-    }
-    size_t eq = term.find('=');
-    if (eq != std::string::npos) {
-      std::string k = trim(term.substr(0, eq));
-      std::string val = term.substr(eq + 1);
-      if (!val.empty() && val[0] == '=') val.erase(0, 1);  // "=="
-      const jd::Value* v = lab(k);
-      if (!v || !v->is_str() || v->s != trim(val)) return false;
-      continue;
-    }
-    if (term[0] == '!') {
-      if (lab(term.substr(1))) return false;
-    } else if (!lab(term)) {
-      return false;
-    }
-  }
-  return true;
-}
+// A parsed label / field selector ("a=b,c!=d,e,!f"), matched many times per
+// watch stream without re-splitting the string.
+struct Selector {
+  enum Op { Eq, Ne, Exists, NotExists };
+  struct Term {
+    std::string key, val;
+    Op op;
+  };
+  std::vector<Term> terms;
+  bool field = false;  // field selector: dotted paths, no existence terms
 
-bool field_match(const jd::Value& obj, const std::string& sel) {
-  if (sel.empty()) return true;
-  for (std::string term : split(sel, ',')) {
-    term = trim(term);
-    if (term.empty()) continue;
-    size_t ne = term.find("!=");
-    if (ne != std::string::npos) {
-      const jd::Value* v = obj.at_path(trim(term.substr(0, ne)));
-      if ((v ? v->scalar_text() : std::string()) == trim(term.substr(ne + 2))) return false;
-      continue;
+  static Selector parse(const std::string& sel, bool field) {
+    Selector out;
+    out.field = field;
+    for (std::string term : split(sel, ',')) {
+      term = trim(term);
+      if (term.empty()) continue;
+      Term t;
+      size_t ne = term.find("!=");
+      size_t eq = term.find('=');
+      if (ne != std::string::npos) {
+        t = {trim(term.substr(0, ne)), trim(term.substr(ne + 2)), Ne};
+      } else if (eq != std::string::npos) {
+        std::string val = term.substr(eq + 1);
+        if (!val.empty() && val[0] == '=') val.erase(0, 1);  // "=="
+        t = {trim(term.substr(0, eq)), trim(val), Eq};
+      } else if (field) {
+        t = {term, std::string(), Eq};  // malformed field term: never matches a non-empty value
+      } else if (term[0] == '!') {
+        t = {term.substr(1), std::string(), NotExists};
+      } else {
+        t = {term, std::string(), Exists};
+      }
+      out.terms.push_back(std::move(t));
     }
-    size_t eq = term.find('=');
-    if (eq == std::string::npos) return false;
-    std::string k = trim(term.substr(0, eq));
-    std::string val = term.substr(eq + 1);
-    if (!val.empty() && val[0] == '=') val.erase(0, 1);
-    const jd::Value* v = obj.at_path(k);
-    if ((v ? v->scalar_text() : std::string()) != trim(val)) return false;
+    return out;
   }
-  return true;
-}
+
+  bool matches(const jd::Value& obj) const {
+    if (terms.empty()) return true;
+    const jd::Value* labels = nullptr;
+    if (!field) {
+      const jd::Value* md = obj.get("metadata");
+      labels = md ? md->get("labels") : nullptr;
+    }
+    for (const Term& t : terms) {
+      if (field) {
+        const jd::Value* v = obj.at_path(t.key);
+        bool same = (v ? v->scalar_text() : std::string()) == t.val;
+        if ((t.op == Eq) != same) return false;
+        continue;
+      }
+      const jd::Value* v = labels ? labels->get(t.key) : nullptr;
+      switch (t.op) {
+        case Eq:
+          if (!v || !v->is_str() || v->s != t.val) return false;
+          break;
+        case Ne:
+          if (v && v->is_str() && v->s == t.val) return false;
+          break;
+        case Exists:
+          if (!v) return false;
+          break;
+        case NotExists:
+          if (v) return false;
+          break;
+      }
+    }
+    return true;
+  }
+};
 
 std::string status_body(int code, const std::string& reason, const std::string& message, const std::string& name = "",
                         const std::string& kind = "") {
@@ -268,7 +286,8 @@ struct Conn {
 
 struct Watcher {
   uint64_t conn_id;
-  std::string kind, ns, fsel, lsel;
+  std::string kind, ns;
+  Selector fsel, lsel;
   std::string pending;
   uint64_t sent = 0, drop_after = 0;
   double deadline = 0;  // 0: none
@@ -388,6 +407,7 @@ class Server {
       long r = ::recv(c->fd, buf, sizeof(buf), 0);
       if (r > 0) {
         c->rbuf.append(buf, static_cast<size_t>(r));
+        if (static_cast<size_t>(r) < sizeof(buf)) break;  // drained (level-triggered epoll wakes us for more)
         continue;
       }
       if (r == 0) {
@@ -566,7 +586,7 @@ class Server {
 
   bool wants(const Watcher& w, const Obj& o) const {
     if (!w.ns.empty() && o.ns != w.ns) return false;
-    return field_match(o.v, w.fsel) && label_match(o.v, w.lsel);
+    return w.fsel.matches(o.v) && w.lsel.matches(o.v);
   }
 
   void flush_watchers() {
@@ -644,8 +664,8 @@ class Server {
     w->conn_id = c->id;
     w->kind = kind;
     w->ns = ns;
-    w->fsel = get("fieldSelector");
-    w->lsel = get("labelSelector");
+    w->fsel = Selector::parse(get("fieldSelector"), true);
+    w->lsel = Selector::parse(get("labelSelector"), false);
     w->drop_after = static_cast<uint64_t>(std::max<int64_t>(0, faults_.drop_watch_after));
     std::string to = get("timeoutSeconds");
     if (!to.empty() && std::atof(to.c_str()) > 0) w->deadline = now_s() + std::atof(to.c_str());
@@ -915,9 +935,10 @@ class Server {
     std::string o = "{\"kind\":\"" + lists.at(kind) + "\",\"apiVersion\":\"v1\",\"metadata\":{\"resourceVersion\":\"" +
                     std::to_string(rv_) + "\"},\"items\":[";
     bool first = true;
+    Selector fs = Selector::parse(fsel, true), ls = Selector::parse(lsel, false);
     for (auto& kv : store_[kind]) {
       if (!ns.empty() && kv.second->ns != ns) continue;
-      if (!field_match(kv.second->v, fsel) || !label_match(kv.second->v, lsel)) continue;
+      if (!fs.matches(kv.second->v) || !ls.matches(kv.second->v)) continue;
       if (!first) o.push_back(',');
       first = false;
       o.append(kv.second->json);
@@ -1057,9 +1078,10 @@ class Server {
         std::string fsel = q.count("fieldSelector") ? q["fieldSelector"] : "";
         std::string lsel = q.count("labelSelector") ? q["labelSelector"] : "";
         std::vector<std::string> names;
+        Selector fs = Selector::parse(fsel, true), ls = Selector::parse(lsel, false);
         for (auto& kv : store_[kind]) {
           if (!ns.empty() && kv.second->ns != ns) continue;
-          if (field_match(kv.second->v, fsel) && label_match(kv.second->v, lsel)) names.push_back(kv.second->name);
+          if (fs.matches(kv.second->v) && ls.matches(kv.second->v)) names.push_back(kv.second->name);
         }
         std::string o = "{\"kind\":\"PodList\",\"apiVersion\":\"v1\",\"metadata\":{},\"items\":[";
         for (size_t i = 0; i < names.size(); ++i) {

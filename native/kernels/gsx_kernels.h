@@ -42,6 +42,8 @@ int gsx_device_count(int* n);
 int gsx_device_info(int dev, gsx_devinfo* out);
 int gsx_mem_info(int dev, uint64_t* free_b, uint64_t* total_b);
 int gsx_synchronize(int dev);
+// Make `dev` current on the calling thread (native runtime threads launch admission kernels).
+int gsx_set_device(int dev);
 
 // streams (mask_words == 0: plain stream)
 int gsx_stream_create(int dev, const uint32_t* cu_mask, int mask_words, void** stream);

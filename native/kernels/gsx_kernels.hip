@@ -162,6 +162,11 @@ int gsx_mem_info(int dev, uint64_t* free_b, uint64_t* total_b) {
   return 0;
 }
 
+int gsx_set_device(int dev) {
+  GSX_CHECK(hipSetDevice(dev));
+  return 0;
+}
+
 int gsx_synchronize(int dev) {
   GSX_CHECK(hipSetDevice(dev));
   GSX_CHECK(hipDeviceSynchronize());
