@@ -54,6 +54,7 @@ class NodeAgent:
         self.bad_stamps = 0
         self.latency: list[float] = []  # bound-observed -> Running
         self._bg: set[asyncio.Task] = set()
+        self._releasing: set[asyncio.Task] = set()
         self.queue: asyncio.Queue = asyncio.Queue()
         self.queued: set[str] = set()
         self.seen: dict[str, float] = {}
@@ -106,9 +107,15 @@ class NodeAgent:
             return
         t = asyncio.get_running_loop().create_task(rel(uid))
         self._bg.add(t)
+        self._releasing.add(t)
         t.add_done_callback(self._bg.discard)
+        t.add_done_callback(self._releasing.discard)
 
     async def _admit_runtime(self, uid: str, dev: int, nbytes: int, cus) -> int:
+        # a container runtime tears down before it starts: releases already decided (e.g. the previous
+        # wave, whose device the extender has just freed) reach the runtime before this slice is carved
+        if self._releasing:
+            await asyncio.gather(*list(self._releasing), return_exceptions=True)
         adm = getattr(self.runtime, "admit", None)
         if adm is not None:
             if getattr(self.runtime, "wants_envs", False):  # a launcher: give it the Allocate container env

@@ -96,12 +96,17 @@ class ChildProc:
 FAKEAPI = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-fakeapi"
 
 
-def start_apiserver(native: bool = True, history: int = 200000) -> ChildProc:
-    """Fake kube-apiserver: the compiled ``gsx-fakeapi`` (native/fakeapi) or ``python -m ...k8s.fakeapi``."""
+def start_apiserver(native: bool = True, history: int = 200000, threads: int | None = None) -> ChildProc:
+    """Fake kube-apiserver: the compiled ``gsx-fakeapi`` (native/fakeapi) or ``python -m ...k8s.fakeapi``.
+
+    ``threads``: event loops of the native server (default ``GSX_FAKEAPI_THREADS`` or 1).
+    """
     if native:
         if not FAKEAPI.exists():
             raise FileNotFoundError(f"{FAKEAPI} missing; run `python native/build.py fakeapi`")
-        return ChildProc([str(FAKEAPI), "--port", "0", "--history", str(history)], "apiserver")
+        threads = threads or int(os.environ.get("GSX_FAKEAPI_THREADS", "1"))
+        return ChildProc([str(FAKEAPI), "--port", "0", "--history", str(history), "--threads", str(threads)],
+                         "apiserver")
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.k8s.fakeapi", "--port", "0"], "apiserver")
 
 

@@ -17,21 +17,37 @@
 //     latency_ms, drop_watch_after, expire_watches, hold_watches,
 //     drop_watches_now; GET /fake/stats.
 //
-// One epoll thread owns all state (like the etcd-serialised apiserver); watch
-// events produced while handling a batch of requests go out as one chunk per
-// watcher per loop iteration.
+// Concurrency (a real kube-apiserver serves requests on many cores in front of
+// one etcd revision counter): N epoll loops, each with its own SO_REUSEPORT
+// listener and the connections it accepted.  A loop parses requests and JSON
+// bodies and sends responses and watch chunks without any lock; the object
+// store, the revision counter, the watch history and the watcher registry sit
+// behind one state mutex, held only while a request mutates or reads them.
+// Watch events are appended under that mutex to the watcher's buffer in
+// revision order and sent by the loop that owns the watch connection (woken
+// through its eventfd), one chunk per watcher per loop iteration.
 //
-//   gsx-fakeapi [--host 127.0.0.1] [--port 0] [--port-file F] [--history N]
+// Default 1 loop.  Measured on the MI355X box (bench.py, fake devices, N=8:
+// 32 pods per wave, ~5 writes per pod): 4 loops were slower (10.7k vs 13.6k
+// pods/s) -- each write is still serialised under the mutex, its hold time
+// doubled once objects bounce between cores, and an event produced on one loop
+// for a watch owned by another costs a wakeup hop on the wave's critical path.
+// More loops pay off for many independent clients, not for one latency-bound
+// chain of dependent writes.  GET /fake/stats reports lock wait / hold times.
+//
+//   gsx-fakeapi [--host 127.0.0.1] [--port 0] [--port-file F] [--history N] [--threads N]
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <signal.h>
 #include <sys/epoll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -41,8 +57,10 @@
 #include <fstream>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -273,26 +291,63 @@ struct Event {
 };
 
 struct Watcher;
+struct Loop;
 
+// A client connection; touched only by the loop that accepted it.
 struct Conn {
   int fd = -1;
   uint64_t id = 0;
   std::string rbuf, wbuf;
   bool want_close = false;
-  bool busy = false;           // a delayed response is pending
-  Watcher* watch = nullptr;    // streaming
+  bool busy = false;                // a delayed response is pending
+  std::shared_ptr<Watcher> watch;   // streaming
   bool epollout = false;
 };
 
+// A watch stream.  `pending`, `dirty`, `closed` and `end_requested` are guarded
+// by the state mutex; the rest is fixed at creation or owned by `owner`.
 struct Watcher {
   uint64_t conn_id;
+  Loop* owner = nullptr;
   std::string kind, ns;
   Selector fsel, lsel;
   std::string pending;
   uint64_t sent = 0, drop_after = 0;
   double deadline = 0;  // 0: none
-  bool closed = false;
+  std::atomic<bool> closed{false};  // written under the state mutex, read anywhere
+  bool dirty = false;          // queued on owner->dirty
+  bool end_requested = false;  // another loop asked the owner to end it
 };
+
+struct Delayed {
+  double due;
+  uint64_t conn;
+  http::Message req;
+};
+
+struct Held {
+  uint64_t conn;
+  http::Message req;
+};
+
+// One event loop: its listener, eventfd and connections (owner-only), plus
+// the watchers with events to send (`dirty`, `signaled`: state mutex).
+struct Loop {
+  int idx = 0;
+  int ep = -1, lfd = -1, efd = -1;
+  std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns;
+  std::vector<std::shared_ptr<Watcher>> mine;  // watches on this loop's connections
+  std::vector<Delayed> delayed;
+  std::vector<Held> held;
+  std::vector<std::shared_ptr<Watcher>> dirty;
+  bool signaled = false;
+  std::atomic<bool> has_dirty{false};  // `dirty` is non-empty (checked before taking the mutex)
+  // owner-written, read by /fake/stats
+  std::atomic<uint64_t> busy_ns{0}, max_iter_ns{0}, flush_ns{0}, flushes{0};
+  std::thread th;
+};
+
+thread_local Loop* tl_loop = nullptr;
 
 struct Faults {
   double conflict_rate = 0, error_rate = 0, latency_ms = 0;
@@ -315,93 +370,175 @@ struct Reply {
   const char* ct = "application/json";
 };
 
+class Server;
+
+// The state mutex with wait / hold accounting for /fake/stats.
+struct LockStats {
+  std::atomic<uint64_t> n{0}, wait_ns{0}, max_wait_ns{0}, hold_ns{0}, max_hold_ns{0};
+};
+
+inline uint64_t mono_ns() {
+  return static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+
+inline void atomic_max(std::atomic<uint64_t>& a, uint64_t v) {
+  uint64_t cur = a.load(std::memory_order_relaxed);
+  while (v > cur && !a.compare_exchange_weak(cur, v, std::memory_order_relaxed)) {
+  }
+}
+
+class StateLock {
+ public:
+  StateLock(std::mutex& m, LockStats& st) : m_(m), st_(st) {
+    uint64_t t0 = mono_ns();
+    m_.lock();
+    t1_ = mono_ns();
+    st_.n.fetch_add(1, std::memory_order_relaxed);
+    st_.wait_ns.fetch_add(t1_ - t0, std::memory_order_relaxed);
+    atomic_max(st_.max_wait_ns, t1_ - t0);
+  }
+  ~StateLock() {
+    uint64_t h = mono_ns() - t1_;
+    m_.unlock();
+    st_.hold_ns.fetch_add(h, std::memory_order_relaxed);
+    atomic_max(st_.max_hold_ns, h);
+  }
+  StateLock(const StateLock&) = delete;
+  StateLock& operator=(const StateLock&) = delete;
+
+ private:
+  std::mutex& m_;
+  LockStats& st_;
+  uint64_t t1_ = 0;
+};
+
 class Server {
  public:
-  explicit Server(size_t history) : history_max_(history) {
+  Server(size_t history, int threads) : history_max_(history), nloops_(std::max(1, std::min(64, threads))) {
     for (const char* k : {"pods", "nodes", "events", "leases"}) store_[k];
   }
 
+  // One SO_REUSEPORT listener per loop on the same port (the first picks it when `port` is 0).
   int listen_on(const std::string& host, int port, std::string* err) {
-    lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
-    int one = 1;
-    setsockopt(lfd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-    sockaddr_in a;
-    std::memset(&a, 0, sizeof(a));
-    a.sin_family = AF_INET;
-    a.sin_port = htons(static_cast<uint16_t>(port));
-    inet_pton(AF_INET, host.c_str(), &a.sin_addr);
-    if (::bind(lfd_, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || ::listen(lfd_, 1024) != 0) {
-      *err = std::string("bind/listen: ") + std::strerror(errno);
-      return -1;
+    for (int i = 0; i < nloops_; ++i) {
+      auto L = std::make_unique<Loop>();
+      L->idx = i;
+      L->lfd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+      int one = 1;
+      setsockopt(L->lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+      setsockopt(L->lfd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one));
+      sockaddr_in a;
+      std::memset(&a, 0, sizeof(a));
+      a.sin_family = AF_INET;
+      a.sin_port = htons(static_cast<uint16_t>(port));
+      inet_pton(AF_INET, host.c_str(), &a.sin_addr);
+      if (::bind(L->lfd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || ::listen(L->lfd, 1024) != 0) {
+        *err = std::string("bind/listen: ") + std::strerror(errno);
+        return -1;
+      }
+      socklen_t len = sizeof(a);
+      getsockname(L->lfd, reinterpret_cast<sockaddr*>(&a), &len);
+      port = ntohs(a.sin_port);
+      L->ep = epoll_create1(EPOLL_CLOEXEC);
+      L->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+      epoll_event ev;
+      ev.events = EPOLLIN;
+      ev.data.u64 = kListenId;
+      epoll_ctl(L->ep, EPOLL_CTL_ADD, L->lfd, &ev);
+      ev.data.u64 = kWakeId;
+      epoll_ctl(L->ep, EPOLL_CTL_ADD, L->efd, &ev);
+      loops_.push_back(std::move(L));
     }
-    socklen_t len = sizeof(a);
-    getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &len);
-    ep_ = epoll_create1(EPOLL_CLOEXEC);
-    epoll_event ev;
-    ev.events = EPOLLIN;
-    ev.data.u64 = 0;
-    epoll_ctl(ep_, EPOLL_CTL_ADD, lfd_, &ev);
-    return ntohs(a.sin_port);
+    return port;
   }
 
   void run(volatile sig_atomic_t* stop) {
-    std::vector<epoll_event> evs(256);
-    while (!*stop) {
-      int timeout = next_timeout_ms();
-      int n = epoll_wait(ep_, evs.data(), static_cast<int>(evs.size()), timeout);
-      double t_iter = now_s();
-      for (int i = 0; i < n; ++i) {
-        uint64_t id = evs[i].data.u64;
-        if (id == 0) {
-          accept_all();
-          continue;
-        }
-        auto it = conns_.find(id);
-        if (it == conns_.end()) continue;
-        Conn* c = it->second.get();
-        if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
-          close_conn(c);
-          continue;
-        }
-        if (evs[i].events & EPOLLIN) on_readable(c);
-        if (conns_.count(id) && (evs[i].events & EPOLLOUT)) flush_conn(c);
-      }
-      run_timers();
-      flush_watchers();
-      max_iter_ = std::max(max_iter_, now_s() - t_iter);
+    for (size_t i = 1; i < loops_.size(); ++i) {
+      Loop* L = loops_[i].get();
+      L->th = std::thread([this, L, stop] { loop_main(L, stop); });
     }
+    loop_main(loops_[0].get(), stop);
+    for (size_t i = 1; i < loops_.size(); ++i) loops_[i]->th.join();
   }
 
  private:
+  static constexpr uint64_t kListenId = 0, kWakeId = 1;
+
+  void loop_main(Loop* L, volatile sig_atomic_t* stop) {
+    tl_loop = L;
+    std::vector<epoll_event> evs(256);
+    while (!*stop) {
+      int timeout = next_timeout_ms(L);
+      int n = epoll_wait(L->ep, evs.data(), static_cast<int>(evs.size()), timeout);
+      double t_iter = now_s();
+      for (int i = 0; i < n; ++i) {
+        uint64_t id = evs[i].data.u64;
+        if (id == kListenId) {
+          accept_all(L);
+          continue;
+        }
+        if (id == kWakeId) {
+          uint64_t v;
+          while (::read(L->efd, &v, sizeof(v)) > 0) {
+          }
+          continue;
+        }
+        auto it = L->conns.find(id);
+        if (it == L->conns.end()) continue;
+        Conn* c = it->second.get();
+        if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
+          close_conn(L, c);
+          continue;
+        }
+        if (evs[i].events & EPOLLIN) on_readable(L, c);
+        if (L->conns.count(id) && (evs[i].events & EPOLLOUT)) flush_conn(L, c);
+      }
+      run_timers(L);
+      double t_flush = now_s();
+      if (flush_watchers(L)) {
+        L->flushes.fetch_add(1, std::memory_order_relaxed);
+        L->flush_ns.fetch_add(static_cast<uint64_t>((now_s() - t_flush) * 1e9), std::memory_order_relaxed);
+      }
+      uint64_t iter_ns = static_cast<uint64_t>((now_s() - t_iter) * 1e9);
+      L->busy_ns.fetch_add(iter_ns, std::memory_order_relaxed);  // loop time outside epoll_wait
+      atomic_max(L->max_iter_ns, iter_ns);
+    }
+    // leave every connection of this loop closed
+    std::vector<Conn*> all;
+    for (auto& kv : L->conns) all.push_back(kv.second.get());
+    for (Conn* c : all) close_conn(L, c);
+  }
+
   // ---------------------------------------------------------------- connections
-  void accept_all() {
+  void accept_all(Loop* L) {
     while (true) {
-      int fd = ::accept4(lfd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+      int fd = ::accept4(L->lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
       if (fd < 0) return;
       int one = 1;
       setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
       auto c = std::make_unique<Conn>();
       c->fd = fd;
-      c->id = ++next_id_;
+      c->id = next_id_.fetch_add(1) + 2;  // 0 / 1: listener / eventfd
       epoll_event ev;
       ev.events = EPOLLIN | EPOLLRDHUP;
       ev.data.u64 = c->id;
-      epoll_ctl(ep_, EPOLL_CTL_ADD, fd, &ev);
-      conns_[c->id] = std::move(c);
+      epoll_ctl(L->ep, EPOLL_CTL_ADD, fd, &ev);
+      L->conns[c->id] = std::move(c);
     }
   }
 
-  void close_conn(Conn* c) {
+  void close_conn(Loop* L, Conn* c) {
     if (c->watch) {
+      StateLock g(smu_, lstats_);
       c->watch->closed = true;
-      c->watch = nullptr;
     }
-    epoll_ctl(ep_, EPOLL_CTL_DEL, c->fd, nullptr);
+    epoll_ctl(L->ep, EPOLL_CTL_DEL, c->fd, nullptr);
     ::close(c->fd);
-    conns_.erase(c->id);
+    L->conns.erase(c->id);
   }
 
-  void on_readable(Conn* c) {
+  void on_readable(Loop* L, Conn* c) {
     char buf[65536];
     while (true) {
       long r = ::recv(c->fd, buf, sizeof(buf), 0);
@@ -411,16 +548,16 @@ class Server {
         continue;
       }
       if (r == 0) {
-        close_conn(c);
+        close_conn(L, c);
         return;
       }
       if (errno == EINTR) continue;
       break;  // EAGAIN
     }
-    process(c);
+    process(L, c);
   }
 
-  void process(Conn* c) {
+  void process(Loop* L, Conn* c) {
     uint64_t id = c->id;
     while (!c->busy && !c->watch && !c->rbuf.empty()) {
       http::Message req;
@@ -428,45 +565,92 @@ class Server {
       long got = http::parse(c->rbuf.data(), c->rbuf.size(), true, &req, &perr);
       if (got == 0) return;
       if (got < 0) {
-        respond(c, Reply{400, status_body(400, "BadRequest", perr)}, false);
+        respond(L, c, Reply{400, status_body(400, "BadRequest", perr)}, false);
         return;
       }
       c->rbuf.erase(0, static_cast<size_t>(got));
-      counts_[req.method]++;
-      bool is_watch = false;
-      {
-        auto q = parse_query(req.target);
-        auto w = q.find("watch");
-        is_watch = w != q.end() && (w->second == "1" || w->second == "true");
-      }
-      if (faults_.latency_ms > 0 && !is_watch) {
+      handle(L, c, req, true);
+      if (!L->conns.count(id)) return;
+    }
+  }
+
+  // A request body parsed outside the state mutex (JSON decoding is the costly part of a write).
+  struct Body {
+    bool ok = true;
+    jd::Value v;
+    std::string err;
+  };
+
+  static jd::Value take_body(Body& b) {
+    if (!b.ok) throw HttpError{400, status_body(400, "BadRequest", "invalid JSON: " + b.err)};
+    return std::move(b.v);
+  }
+
+  // `fresh`: the request has not been through the injected-latency queue yet.
+  void handle(Loop* L, Conn* c, http::Message& req, bool fresh) {
+    bool is_watch = false;
+    {
+      auto q = parse_query(req.target);
+      auto w = q.find("watch");
+      is_watch = w != q.end() && (w->second == "1" || w->second == "true");
+    }
+    Body body;
+    if (!req.body.empty() && (req.method == "POST" || req.method == "PUT" || req.method == "PATCH")) {
+      body.ok = jd::parse(req.body, &body.v, &body.err);
+    } else {
+      body.v = jd::Value::object();
+    }
+    std::string cls = route_class(req);
+    Reply rep;
+    bool reply = true;
+    {
+      StateLock g(smu_, lstats_);
+      if (fresh) counts_[req.method]++;
+      if (fresh && faults_.latency_ms > 0 && !is_watch) {
         c->busy = true;
-        delayed_.push_back({now_s() + faults_.latency_ms / 1000.0, id, std::move(req)});
+        L->delayed.push_back({now_s() + faults_.latency_ms / 1000.0, c->id, std::move(req)});
         return;
       }
-      handle(c, req);
-      if (!conns_.count(id)) return;
+      double t0 = now_s();
+      RouteTime& rt = route_time_[cls];
+      rt.n++;
+      try {
+        reply = route(L, c, req, body, &rep);  // false: became a watch stream (or is held)
+      } catch (const HttpError& e) {
+        rep.status = e.code;
+        rep.body = e.body;
+      }
+      rt.s += now_s() - t0;
+    }
+    if (reply) {
+      respond(L, c, rep, req.keep_alive);
+    } else if (!c->wbuf.empty() || c->want_close) {
+      flush_conn(L, c);
     }
   }
 
-  void handle(Conn* c, http::Message& req) {
-    Reply rep;
-    try {
-      if (!route(c, req, &rep)) return;  // became a watch stream (or is held)
-    } catch (const HttpError& e) {
-      rep.status = e.code;
-      rep.body = e.body;
+  // "METHOD kind[/sub]" (names and namespaces dropped) for the per-route time table of /fake/stats.
+  static std::string route_class(const http::Message& req) {
+    std::vector<std::string> seg = split(std::string(req.path()), '/');
+    std::string k;
+    if (seg.size() >= 4 && seg[1] == "api" && seg[2] == "v1") {
+      size_t at = seg[3] == "namespaces" && seg.size() >= 6 ? 5 : 3;
+      k = seg[at];
+      if (seg.size() == at + 3) k += "/" + seg[at + 2];
+      if (seg.size() == at + 1 && req.target.find("watch=") != std::string::npos) k += "?watch";
+    } else {
+      k = std::string(req.path());
     }
-    respond(c, rep, req.keep_alive);
+    return req.method + " " + k;
   }
 
-  void respond(Conn* c, const Reply& r, bool keep_alive) {
+  void respond(Loop* L, Conn* c, const Reply& r, bool keep_alive) {
     c->wbuf.append(http::response(r.status, r.ct, r.body, keep_alive));
     if (!keep_alive) c->want_close = true;
-    flush_conn(c);
+    flush_conn(L, c);
   }
 
-  void flush_conn(Conn* c) {
+  void flush_conn(Loop* L, Conn* c) {
     while (!c->wbuf.empty()) {
       long w = ::send(c->fd, c->wbuf.data(), c->wbuf.size(), MSG_NOSIGNAL);
       if (w > 0) {
@@ -479,95 +663,130 @@ class Server {
           epoll_event ev;
           ev.events = EPOLLIN | EPOLLOUT | EPOLLRDHUP;
           ev.data.u64 = c->id;
-          epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
+          epoll_ctl(L->ep, EPOLL_CTL_MOD, c->fd, &ev);
           c->epollout = true;
         }
         return;
       }
-      close_conn(c);
+      close_conn(L, c);
       return;
     }
     if (c->epollout) {
       epoll_event ev;
       ev.events = EPOLLIN | EPOLLRDHUP;
       ev.data.u64 = c->id;
-      epoll_ctl(ep_, EPOLL_CTL_MOD, c->fd, &ev);
+      epoll_ctl(L->ep, EPOLL_CTL_MOD, c->fd, &ev);
       c->epollout = false;
     }
-    if (c->want_close) close_conn(c);
+    if (c->want_close) close_conn(L, c);
+  }
+
+  void wake(Loop* L) {
+    uint64_t one = 1;
+    ssize_t r = ::write(L->efd, &one, sizeof(one));
+    (void)r;
   }
 
   // ---------------------------------------------------------------- timers
-  int next_timeout_ms() {
-    double next = now_s() + 1.0;
-    for (auto& d : delayed_) next = std::min(next, d.due);
-    for (auto& g : graces_) next = std::min(next, g.due);
-    for (auto& w : watchers_) {
+  int next_timeout_ms(Loop* L) {
+    double now = now_s();
+    double next = now + 1.0;
+    for (auto& d : L->delayed) next = std::min(next, d.due);
+    for (auto& w : L->mine) {
       if (w->deadline > 0) next = std::min(next, w->deadline);
     }
-    if (!held_.empty()) next = std::min(next, now_s() + 0.005);
-    double ms = (next - now_s()) * 1000.0;
+    if (!L->held.empty()) next = std::min(next, now + 0.005);
+    if (L->idx == 0 && ngraces_.load() > 0) {
+      StateLock g(smu_, lstats_);
+      for (auto& gr : graces_) next = std::min(next, gr.due);
+    }
+    double ms = (next - now) * 1000.0;
     return ms <= 0 ? 0 : static_cast<int>(ms) + 1;
   }
 
-  void run_timers() {
+  void run_timers(Loop* L) {
     double now = now_s();
-    if (!delayed_.empty()) {
+    if (!L->delayed.empty()) {
       std::vector<Delayed> due;
-      for (auto it = delayed_.begin(); it != delayed_.end();) {
+      for (auto it = L->delayed.begin(); it != L->delayed.end();) {
         if (it->due <= now) {
           due.push_back(std::move(*it));
-          it = delayed_.erase(it);
+          it = L->delayed.erase(it);
         } else {
           ++it;
         }
       }
       for (auto& d : due) {
-        auto it = conns_.find(d.conn);
-        if (it == conns_.end()) continue;
+        auto it = L->conns.find(d.conn);
+        if (it == L->conns.end()) continue;
         Conn* c = it->second.get();
         c->busy = false;
-        handle(c, d.req);
-        if (conns_.count(d.conn)) process(c);
+        handle(L, c, d.req, false);
+        if (L->conns.count(d.conn)) process(L, c);
       }
     }
-    if (!graces_.empty()) {
-      std::vector<Grace> due;
-      for (auto it = graces_.begin(); it != graces_.end();) {
-        if (it->due <= now) {
-          due.push_back(*it);
-          it = graces_.erase(it);
+    if (L->idx == 0 && ngraces_.load() > 0) {
+      StateLock g(smu_, lstats_);
+      if (!graces_.empty()) {
+        std::vector<Grace> due;
+        for (auto it = graces_.begin(); it != graces_.end();) {
+          if (it->due <= now) {
+            due.push_back(*it);
+            it = graces_.erase(it);
+          } else {
+            ++it;
+          }
+        }
+        ngraces_.store(static_cast<int>(graces_.size()));
+        for (auto& gr : due) {
+          auto& m = store_[gr.kind];
+          auto it = m.find({gr.ns, gr.name});
+          if (it != m.end()) {
+            const jd::Value* md = it->second->v.get("metadata");
+            if (md && md->str_or("uid") == gr.uid) do_delete(gr.kind, gr.ns, gr.name, -1);
+          }
+        }
+      }
+    }
+    if (!L->mine.empty()) {
+      // prune closed watches and end the expired ones (timeoutSeconds)
+      std::vector<std::shared_ptr<Watcher>> expired, keep;
+      for (auto& w : L->mine) {
+        if (w->closed) continue;
+        if (w->deadline > 0 && w->deadline <= now) {
+          expired.push_back(w);
         } else {
-          ++it;
+          keep.push_back(w);
         }
       }
-      for (auto& g : due) {
-        auto& m = store_[g.kind];
-        auto it = m.find({g.ns, g.name});
-        if (it != m.end()) {
-          const jd::Value* md = it->second->v.get("metadata");
-          if (md && md->str_or("uid") == g.uid) do_delete(g.kind, g.ns, g.name, -1);
-        }
+      L->mine.swap(keep);
+      for (auto& w : expired) end_watch(L, w);
+    }
+    if (!L->held.empty()) {
+      bool hold;
+      {
+        StateLock g(smu_, lstats_);
+        hold = faults_.hold_watches;
       }
-    }
-    for (auto& w : watchers_) {
-      if (!w->closed && w->deadline > 0 && w->deadline <= now) end_watch(w.get());
-    }
-    if (!held_.empty() && !faults_.hold_watches) {
-      auto held = std::move(held_);
-      held_.clear();
-      for (auto& h : held) {
-        auto it = conns_.find(h.conn);
-        if (it == conns_.end()) continue;
-        Conn* c = it->second.get();
-        c->busy = false;
-        handle(c, h.req);
-        if (conns_.count(h.conn)) process(c);
+      if (!hold) {
+        auto held = std::move(L->held);
+        L->held.clear();
+        for (auto& h : held) {
+          auto it = L->conns.find(h.conn);
+          if (it == L->conns.end()) continue;
+          Conn* c = it->second.get();
+          c->busy = false;
+          handle(L, c, h.req, false);
+          if (L->conns.count(h.conn)) process(L, c);
+        }
       }
     }
   }
 
   // ---------------------------------------------------------------- watch
+  // State mutex held: append the event to every matching watcher and queue the
+  // watcher on its owner loop (woken unless it is the calling loop, which
+  // flushes at the end of its iteration).
   void emit(const std::string& kind, const char* etype, const ObjP& o) {
     const jd::Value* md = o->v.get("metadata");
     int64_t rv = md ? std::atoll(md->str_or("resourceVersion").c_str()) : 0;
@@ -580,7 +799,22 @@ class Server {
     }
     history_.push_back(Event{rv, kind, line, o});
     for (auto& w : watchers_) {
-      if (!w->closed && w->kind == kind && wants(*w, *o)) w->pending.append(*line);
+      if (!w->closed && w->kind == kind && wants(*w, *o)) {
+        w->pending.append(*line);
+        mark_dirty_locked(w);
+      }
+    }
+  }
+
+  void mark_dirty_locked(const std::shared_ptr<Watcher>& w) {
+    if (w->dirty) return;
+    w->dirty = true;
+    Loop* L = w->owner;
+    L->dirty.push_back(w);
+    L->has_dirty.store(true);
+    if (L != tl_loop && !L->signaled) {
+      L->signaled = true;
+      wake(L);
     }
   }
 
@@ -589,58 +823,92 @@ class Server {
     return w.fsel.matches(o.v) && w.lsel.matches(o.v);
   }
 
-  void flush_watchers() {
-    for (auto& w : watchers_) {
-      if (w->closed || w->pending.empty()) continue;
-      auto it = conns_.find(w->conn_id);
-      if (it == conns_.end()) {
-        w->closed = true;
+  // Send what this loop's dirty watchers accumulated: buffers are taken under the
+  // state mutex, the socket writes happen outside it.
+  // Returns whether there was anything to send.
+  bool flush_watchers(Loop* L) {
+    struct Out {
+      std::shared_ptr<Watcher> w;
+      std::string data;
+      bool end;
+    };
+    std::vector<Out> outs;
+    if (!L->has_dirty.exchange(false)) return false;
+    {
+      StateLock g(smu_, lstats_);
+      L->signaled = false;
+      if (L->dirty.empty()) return false;
+      for (auto& w : L->dirty) {
+        w->dirty = false;
+        if (w->closed) continue;
+        Out o{w, std::move(w->pending), w->end_requested};
+        w->pending.clear();
+        // one chunk per loop iteration; count events for drop_watch_after
+        w->sent += static_cast<uint64_t>(std::count(o.data.begin(), o.data.end(), '\n'));
+        if (w->drop_after && w->sent >= w->drop_after) {
+          counts_["watch_dropped"]++;
+          o.end = true;
+        }
+        outs.push_back(std::move(o));
+      }
+      L->dirty.clear();
+      watchers_.erase(std::remove_if(watchers_.begin(), watchers_.end(),
+                                     [](const std::shared_ptr<Watcher>& w) { return w->closed.load(); }),
+                      watchers_.end());
+    }
+    for (auto& o : outs) {
+      auto it = L->conns.find(o.w->conn_id);
+      if (it == L->conns.end()) {
+        StateLock g(smu_, lstats_);
+        o.w->closed = true;
         continue;
       }
       Conn* c = it->second.get();
-      // one chunk per loop iteration; count events for drop_watch_after
-      size_t events = static_cast<size_t>(std::count(w->pending.begin(), w->pending.end(), '\n'));
-      char hdr[32];
-      std::snprintf(hdr, sizeof(hdr), "%zx\r\n", w->pending.size());
-      c->wbuf.append(hdr).append(w->pending).append("\r\n");
-      w->pending.clear();
-      w->sent += events;
-      if (w->drop_after && w->sent >= w->drop_after) {
-        counts_["watch_dropped"]++;
-        end_watch(w.get());
+      if (!o.data.empty()) {
+        char hdr[32];
+        std::snprintf(hdr, sizeof(hdr), "%zx\r\n", o.data.size());
+        c->wbuf.append(hdr).append(o.data).append("\r\n");
+      }
+      if (o.end) {
+        end_watch(L, o.w);
         continue;
       }
-      flush_conn(c);
+      flush_conn(L, c);
     }
-    watchers_.erase(std::remove_if(watchers_.begin(), watchers_.end(), [](const std::unique_ptr<Watcher>& w) {
-                      return w->closed;
-                    }),
-                    watchers_.end());
+    return true;
   }
 
-  void end_watch(Watcher* w) {
-    if (w->closed) return;
-    w->closed = true;
-    auto it = conns_.find(w->conn_id);
-    if (it == conns_.end()) return;
+  // Owner loop only: send what is pending, the terminating chunk, and close.
+  void end_watch(Loop* L, const std::shared_ptr<Watcher>& w) {
+    std::string rest;
+    {
+      StateLock g(smu_, lstats_);
+      if (w->closed) return;
+      w->closed = true;
+      rest = std::move(w->pending);
+      w->pending.clear();
+    }
+    auto it = L->conns.find(w->conn_id);
+    if (it == L->conns.end()) return;
     Conn* c = it->second.get();
     c->watch = nullptr;
-    if (!w->pending.empty()) {
+    if (!rest.empty()) {
       char hdr[32];
-      std::snprintf(hdr, sizeof(hdr), "%zx\r\n", w->pending.size());
-      c->wbuf.append(hdr).append(w->pending).append("\r\n");
+      std::snprintf(hdr, sizeof(hdr), "%zx\r\n", rest.size());
+      c->wbuf.append(hdr).append(rest).append("\r\n");
     }
     c->wbuf.append("0\r\n\r\n");
     c->want_close = true;
-    flush_conn(c);
+    flush_conn(L, c);
   }
 
-  // Returns false when the request became a (held) watch stream.
-  bool start_watch(Conn* c, const http::Message& req, const std::string& kind, const std::string& ns,
+  // State mutex held (called from route).  Returns false: the request became a
+  // (held) watch stream; the caller flushes what was queued on the connection.
+  bool start_watch(Loop* L, Conn* c, const http::Message& req, const std::string& kind, const std::string& ns,
                    const std::map<std::string, std::string>& q) {
     if (faults_.hold_watches) {
       c->busy = true;
-      held_.push_back({c->id, req});
+      L->held.push_back({c->id, req});
       return false;
     }
     std::string head = "HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n";
@@ -657,11 +925,11 @@ class Server {
       std::snprintf(hdr, sizeof(hdr), "%zx\r\n", line.size());
       c->wbuf.append(head).append(hdr).append(line).append("\r\n0\r\n\r\n");
       c->want_close = true;
-      flush_conn(c);
       return false;
     }
-    auto w = std::make_unique<Watcher>();
+    auto w = std::make_shared<Watcher>();
     w->conn_id = c->id;
+    w->owner = L;
     w->kind = kind;
     w->ns = ns;
     w->fsel = Selector::parse(get("fieldSelector"), true);
@@ -681,7 +949,6 @@ class Server {
         std::snprintf(hdr, sizeof(hdr), "%zx\r\n", line.size());
         c->wbuf.append(head).append(hdr).append(line).append("\r\n0\r\n\r\n");
         c->want_close = true;
-        flush_conn(c);
         return false;
       }
       // backlog: history after rv (binary search: history is rv-ordered)
@@ -698,9 +965,10 @@ class Server {
       }
     }
     c->wbuf.append(head);
-    c->watch = w.get();
-    watchers_.push_back(std::move(w));
-    flush_conn(c);
+    c->watch = w;
+    L->mine.push_back(w);
+    watchers_.push_back(w);
+    if (!w->pending.empty()) mark_dirty_locked(w);
     return false;
   }
 
@@ -895,6 +1163,8 @@ class Server {
       store_[kind][key] = o;
       emit(kind, "MODIFIED", o);
       graces_.push_back(Grace{now_s() + grace, kind, ns, name, cmd.str_or("uid")});
+      ngraces_.store(static_cast<int>(graces_.size()));
+      if (tl_loop != loops_[0].get()) wake(loops_[0].get());  // loop 0 runs the grace timers
       return o;
     }
     store_[kind].erase(key);
@@ -906,14 +1176,6 @@ class Server {
   }
 
   // ---------------------------------------------------------------- routing
-  static jd::Value body_json(const http::Message& req) {
-    jd::Value v;
-    std::string err;
-    if (req.body.empty()) return jd::Value::object();
-    if (!jd::parse(req.body, &v, &err)) throw HttpError{400, status_body(400, "BadRequest", "invalid JSON: " + err)};
-    return v;
-  }
-
   static double grace_of(const http::Message& req, const std::map<std::string, std::string>& q) {
     auto it = q.find("gracePeriodSeconds");
     if (it != q.end()) return std::atof(it->second.c_str());
@@ -949,7 +1211,7 @@ class Server {
 
   // Collection routes: (kind, ns) for "/api/v1/<kind>", "/api/v1/namespaces/<ns>/<kind>",
   // "/apis/coordination.k8s.io/v1/namespaces/<ns>/leases"; item routes add name and subresource.
-  bool route(Conn* c, http::Message& req, Reply* rep) {
+  bool route(Loop* L, Conn* c, http::Message& req, Body& body, Reply* rep) {
     std::string path(req.path());
     auto q = parse_query(req.target);
     const std::string& m = req.method;
@@ -968,7 +1230,7 @@ class Server {
     }
     if (path == "/fake/faults") {
       if (m == "POST") {
-        jd::Value b = body_json(req);
+        jd::Value b = take_body(body);
         auto num = [&](const char* k, double* dst) {
           const jd::Value* v = b.get(k);
           if (v && v->k == jd::Value::Num) *dst = std::atof(v->s.c_str());
@@ -988,7 +1250,11 @@ class Server {
         if (seed && seed->k == jd::Value::Num) rng().seed(static_cast<uint64_t>(std::atoll(seed->s.c_str())));
         const jd::Value* drop = b.get("drop_watches_now");
         if (drop && drop->k == jd::Value::Bool && drop->b) {
-          for (auto& w : watchers_) end_watch(w.get());
+          for (auto& w : watchers_) {  // each owner loop ends its own watches
+            if (w->closed) continue;
+            w->end_requested = true;
+            mark_dirty_locked(w);
+          }
         }
       }
       rep->body = faults_.json();
@@ -1005,9 +1271,35 @@ class Server {
       }
       size_t live = 0;
       for (auto& w : watchers_) live += w->closed ? 0 : 1;
-      char mx[64];
-      std::snprintf(mx, sizeof(mx), "},\"max_iter_ms\":%.3f", max_iter_ * 1e3);
+      char mx[96];
+      uint64_t busy = 0, mxi = 0, fl = 0, fln = 0;
+      for (auto& lp : loops_) {
+        busy += lp->busy_ns.load();
+        mxi = std::max<uint64_t>(mxi, lp->max_iter_ns.load());
+        fl += lp->flush_ns.load();
+        fln += lp->flushes.load();
+      }
+      char lk[256];
+      std::snprintf(lk, sizeof(lk),
+                    "},\"lock\":{\"n\":%llu,\"wait_ms\":%.3f,\"max_wait_ms\":%.3f,\"hold_ms\":%.3f,\"max_hold_ms\":%.3f}",
+                    (unsigned long long)lstats_.n.load(), lstats_.wait_ns.load() / 1e6, lstats_.max_wait_ns.load() / 1e6,
+                    lstats_.hold_ns.load() / 1e6, lstats_.max_hold_ns.load() / 1e6);
+      o.append(lk);
+      std::snprintf(mx, sizeof(mx), ",\"max_iter_ms\":%.3f,\"busy_ms\":%.3f,\"loops\":%zu,\"route_ms\":{", mxi / 1e6,
+                    busy / 1e6, loops_.size());
       o.append(mx);
+      first = true;
+      std::snprintf(mx, sizeof(mx), "\"watch-flush\":[%llu,%.3f]", (unsigned long long)fln, fl / 1e6);
+      o.append(mx);
+      first = false;
+      for (auto& kv : route_time_) {
+        if (!first) o.push_back(',');
+        first = false;
+        json::append_quoted(&o, kv.first);
+        std::snprintf(mx, sizeof(mx), ":[%llu,%.3f]", (unsigned long long)kv.second.n, kv.second.s * 1e3);
+        o.append(mx);
+      }
+      o.push_back('}');
       o.append(",\"watchers\":").append(std::to_string(live));
       for (auto& kv : store_) o.append(",\"" + kv.first + "\":" + std::to_string(kv.second.size()));
       o.push_back('}');
@@ -1029,7 +1321,7 @@ class Server {
           if (seg.size() > 8) throw HttpError{404, status_body(404, "NotFound", "the server could not find the requested resource")};
         }
         if (kind == "bindings" && coll && m == "POST") {
-          jd::Value b = body_json(req);
+          jd::Value b = take_body(body);
           maybe_error();
           const jd::Value* bmd = b.get("metadata");
           do_bind(ns, bmd ? bmd->str_or("name") : std::string(), b);
@@ -1061,13 +1353,13 @@ class Server {
     if (coll) {
       if (m == "GET") {
         auto w = q.find("watch");
-        if (w != q.end() && (w->second == "1" || w->second == "true")) return start_watch(c, req, kind, ns, q);
+        if (w != q.end() && (w->second == "1" || w->second == "true")) return start_watch(L, c, req, kind, ns, q);
         rep->body = list_json(kind, ns, q.count("fieldSelector") ? q["fieldSelector"] : "",
                               q.count("labelSelector") ? q["labelSelector"] : "");
         return true;
       }
       if (m == "POST") {
-        jd::Value b = body_json(req);
+        jd::Value b = take_body(body);
         if (kind == "pods") maybe_error();
         rep->status = 201;
         rep->body = do_create(kind, std::move(b), ns)->json;
@@ -1095,7 +1387,7 @@ class Server {
       throw HttpError{405, status_body(405, "MethodNotAllowed", "method not allowed")};
     }
     if (sub == "binding" && kind == "pods" && m == "POST") {
-      jd::Value b = body_json(req);
+      jd::Value b = take_body(body);
       maybe_error();
       do_bind(ns, name, b);
       rep->status = 201;
@@ -1110,7 +1402,7 @@ class Server {
       return true;
     }
     if (m == "PUT") {
-      jd::Value b = body_json(req);
+      jd::Value b = take_body(body);
       if (kind == "pods") maybe_error();
       rep->body = do_replace(kind, ns, name, std::move(b), sub)->json;
       return true;
@@ -1122,7 +1414,7 @@ class Server {
         rep->body = status_body(415, "UnsupportedMediaType", "json-patch not supported");
         return true;
       }
-      jd::Value b = body_json(req);
+      jd::Value b = take_body(body);
       if (kind == "pods") maybe_error();
       rep->body = do_patch(kind, ns, name, std::move(b), sub)->json;
       return true;
@@ -1134,33 +1426,30 @@ class Server {
     throw HttpError{405, status_body(405, "MethodNotAllowed", "method not allowed")};
   }
 
-  struct Delayed {
-    double due;
-    uint64_t conn;
-    http::Message req;
-  };
-  struct Held {
-    uint64_t conn;
-    http::Message req;
-  };
   struct Grace {
     double due;
     std::string kind, ns, name, uid;
   };
 
+  struct RouteTime {
+    uint64_t n = 0;
+    double s = 0;
+  };
+
   size_t history_max_;
-  double max_iter_ = 0;  // longest event-loop iteration (request handling + fan-out), seconds
-  int lfd_ = -1, ep_ = -1;
-  uint64_t next_id_ = 0;
-  std::unordered_map<uint64_t, std::unique_ptr<Conn>> conns_;
-  std::vector<std::unique_ptr<Watcher>> watchers_;
+  std::map<std::string, RouteTime> route_time_;
+  int nloops_;
+  std::vector<std::unique_ptr<Loop>> loops_;
+  LockStats lstats_;
+  std::atomic<int> ngraces_{0};  // graces_.size(), readable without the mutex
+  std::mutex smu_;  // the state below: store, revision, history, watchers, faults, counters, graces
+  std::atomic<uint64_t> next_id_{0};
+  std::vector<std::shared_ptr<Watcher>> watchers_;
   std::map<std::string, std::map<Key, ObjP>> store_;
   std::deque<Event> history_;
   int64_t rv_ = 0, oldest_rv_ = 0;
   Faults faults_;
   std::map<std::string, uint64_t> counts_;
-  std::vector<Delayed> delayed_;
-  std::vector<Held> held_;
   std::vector<Grace> graces_;
 };
 
@@ -1173,6 +1462,7 @@ int main(int argc, char** argv) {
   std::string host = "127.0.0.1", port_file;
   int port = 0;
   size_t history = 200000;
+  int threads = 1;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&]() -> std::string {
@@ -1186,8 +1476,9 @@ int main(int argc, char** argv) {
     else if (a == "--port") port = std::atoi(val().c_str());
     else if (a == "--port-file") port_file = val();
     else if (a == "--history") history = static_cast<size_t>(std::max(1, std::atoi(val().c_str())));
+    else if (a == "--threads") threads = std::atoi(val().c_str());
     else if (a == "-h" || a == "--help") {
-      std::printf("usage: gsx-fakeapi [--host H] [--port P] [--port-file F] [--history N]\n");
+      std::printf("usage: gsx-fakeapi [--host H] [--port P] [--port-file F] [--history N] [--threads N]\n");
       return 0;
     } else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -1200,7 +1491,7 @@ int main(int argc, char** argv) {
   sa.sa_handler = on_sig;
   sigaction(SIGTERM, &sa, nullptr);
   sigaction(SIGINT, &sa, nullptr);
-  Server srv(history);
+  Server srv(history, threads);
   std::string err;
   int bound = srv.listen_on(host, port, &err);
   if (bound < 0) {

@@ -301,7 +301,9 @@ int gsx_hbm_admit(void* stream, const gsx_slice* slices, int n, int stamp_idx, u
   __atomic_store_n(hc, 0ull, __ATOMIC_SEQ_CST);
   uint64_t maxn = 0;
   for (int i = 0; i < n; ++i) maxn = std::max<uint64_t>(maxn, slices[i].bytes / stride);
-  const int gx = grid_for(maxn, 256, 64);
+  // one stamp per lane up to 1024 blocks per slice: the reads are 1 MiB apart (a DRAM page each), so the
+  // kernel is latency-bound and every extra serial iteration per lane costs a full HBM round trip
+  const int gx = grid_for(maxn, 256, 1024);
   for (int base = 0; base < n; base += kMaxSlices) {
     SliceTable t;
     t.n = std::min(kMaxSlices, n - base);

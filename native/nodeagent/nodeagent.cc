@@ -405,9 +405,7 @@ class Agent {
       if (!releases_.empty()) {
         auto rel = releases_.front();
         releases_.pop_front();
-        lk.unlock();
-        runtime_call(rel.second, "DELETE", "/v1/pods/" + rel.first, std::string(), nullptr);
-        lk.lock();
+        release_one(rel, lk);
         continue;
       }
       if (queue_.empty()) {
@@ -551,8 +549,14 @@ class Agent {
       }
       return;
     }
+    // a container runtime tears down before it starts: every release already decided for this GPU
+    // reaches the runtime before this pod's slice is carved (the next wave's pods may be bound the
+    // moment the extender's ledger frees the device, while another worker is still releasing)
+    lk.lock();
+    drain_releases_locked(dev_idx, lk);
+    lk.unlock();
     // start the pod on its GPU's runtime: slice stamped + every resident slice verified
-    std::string body = "{\"dev\":" + std::to_string(dev_idx) + ",\"bytes\":" + std::to_string(pod.request * unit_) +
+    std::string body ="{\"dev\":" + std::to_string(dev_idx) + ",\"bytes\":" + std::to_string(pod.request * unit_) +
                        ",\"cus\":";
     if (cus.empty()) {
       body.append("null");
@@ -620,6 +624,31 @@ class Agent {
     wake_locked();
   }
 
+  // DELETE a pod's slice on its runtime; mu_ held on entry and exit, dropped around the call.
+  void release_one(const std::pair<std::string, int>& rel, std::unique_lock<std::mutex>& lk) {
+    releasing_[rel.second]++;
+    lk.unlock();
+    runtime_call(rel.second, "DELETE", "/v1/pods/" + rel.first, std::string(), nullptr);
+    lk.lock();
+    if (--releasing_[rel.second] == 0) cv_.notify_all();
+  }
+
+  // Run this GPU's queued releases on the calling worker and wait for the ones other workers have in
+  // flight (they never wait on anything, so this cannot deadlock); mu_ held.
+  void drain_releases_locked(int dev, std::unique_lock<std::mutex>& lk) {
+    while (true) {
+      auto it = std::find_if(releases_.begin(), releases_.end(), [dev](const auto& r) { return r.second == dev; });
+      if (it != releases_.end()) {
+        auto rel = *it;
+        releases_.erase(it);
+        release_one(rel, lk);
+        continue;
+      }
+      if (releasing_[dev] == 0 || stop_) return;
+      cv_.wait(lk);
+    }
+  }
+
   int runtime_call(int dev, const char* method, const std::string& path, const std::string& body, std::string* out) {
     auto it = runtimes_.find(dev);
     if (it == runtimes_.end()) return -1;
@@ -653,6 +682,7 @@ class Agent {
   std::deque<std::string> queue_;
   std::vector<std::pair<double, std::string>> delayed_;
   std::deque<std::pair<std::string, int>> releases_;
+  std::map<int, int> releasing_;  // per GPU: DELETEs in flight on some worker
   std::vector<double> latency_;
   uint64_t admitted_ = 0, failed_ = 0, bad_ = 0, conflicts_ = 0;
   int added_ = 0;  // work items queued since the last wake_locked()

@@ -25,10 +25,10 @@ def run(coro):
 class _NativeApi:
     """gsx-fakeapi (native/fakeapi) as a child process, with the runner interface the tests use."""
 
-    def __init__(self, history):
+    def __init__(self, history, threads=1):
         from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver
 
-        self.proc = start_apiserver(native=True, history=history)
+        self.proc = start_apiserver(native=True, history=history, threads=threads)
         self.url = self.proc.url
 
     async def stop(self):
@@ -37,11 +37,15 @@ class _NativeApi:
 
 async def _api(history=200000, impl="python"):
     """The asyncio fake apiserver in-process, or the compiled one (same REST semantics)."""
-    r = _NativeApi(history) if impl == "native" else await FakeApiServerRunner(FakeApiServer(history=history)).start()
+    if impl.startswith("native"):
+        r = _NativeApi(history, threads=4 if impl == "native-mt" else 1)
+    else:
+        r = await FakeApiServerRunner(FakeApiServer(history=history)).start()
     return r, KubeClient(r.url)
 
 
-IMPLS = pytest.mark.parametrize("impl", ["python", "native"])
+# native-mt: the compiled server with 4 event loops sharing the store (watch events cross loops)
+IMPLS = pytest.mark.parametrize("impl", ["python", "native", "native-mt"])
 
 
 # ---------------------------------------------------------------- fake apiserver semantics
@@ -147,6 +151,44 @@ def test_watch_from_compacted_version_is_410(impl):
             assert got == ["p5"]
         finally:
             await c.close()
+            await r.stop()
+    run(go())
+
+
+@pytest.mark.parametrize("impl", ["native", "native-mt"])
+def test_concurrent_writers_watch_in_revision_order(impl):
+    """Many connections writing at once: every watcher sees every event exactly once, in resourceVersion order."""
+    async def go():
+        r, c = await _api(impl=impl)
+        watchers = [KubeClient(r.url) for _ in range(3)]
+        writers = [KubeClient(r.url) for _ in range(8)]
+        try:
+            seen = [[] for _ in watchers]
+
+            async def watch(i):
+                async for ev in watchers[i].watch("pods", resource_version="0", timeout_seconds=3):
+                    seen[i].append((int(ev["object"]["metadata"]["resourceVersion"]), ev["type"],
+                                    ev["object"]["metadata"]["name"]))
+                    if len(seen[i]) == 8 * 10 * 2:
+                        return
+
+            tasks = [asyncio.create_task(watch(i)) for i in range(len(watchers))]
+            await asyncio.sleep(0.2)
+
+            async def write(w, k):
+                for j in range(10):
+                    await w.create("pods", make_pod(f"c{k}-{j}", 1))
+                    await w.patch("pods", f"c{k}-{j}", {"metadata": {"labels": {"x": "1"}}}, "default")
+
+            await asyncio.gather(*(write(w, k) for k, w in enumerate(writers)))
+            await asyncio.wait_for(asyncio.gather(*tasks), 10)
+            for got in seen:
+                rvs = [rv for rv, _, _ in got]
+                assert len(got) == 160 and rvs == sorted(rvs) and len(set(rvs)) == 160
+                assert sum(1 for _, t, _ in got if t == "ADDED") == 80
+        finally:
+            for x in watchers + writers + [c]:
+                await x.close()
             await r.stop()
     run(go())
 
