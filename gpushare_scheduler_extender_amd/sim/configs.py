@@ -1,0 +1,344 @@
+"""The five BASELINE.json configurations, end to end through the whole stack.
+
+    python -m gpushare_scheduler_extender_amd.sim.configs [--gpu] [--json-out F] [--only 1,4]
+
+Every configuration starts the same processes as ``bench.py`` (fake kube-apiserver, the extender, the
+kube-scheduler stand-in and the node agent as child processes; a pod runtime endpoint per GPU in this
+process), registers one node, creates pods and checks where they land:
+
+1. kind-style plumbing: one fake 16 GiB device, 2 pods x 2 GiB (reference ``shared-gpu`` naming) ->
+   both bound to device 0 and admitted (``samples/1.yaml``, ``docs/designs/designs.md:88``);
+2. 1 x MI355X: 4 pods x 64 GiB (``aliyun.com/gpu-mem``) on the single 288 GB device -> 4 co-resident;
+3. 8 x MI355X: 32 pods x 64 GiB on 8 devices -> binpack-first, 4 per device;
+4. fragmentation guard: 8 devices each holding a 200 GiB pod (68 GiB free each, 544 GiB free on the
+   node), then 100 / 200 / 50 GiB requests: the 100 and 200 GiB pods pass kube-scheduler's aggregate
+   fit but the extender filters the node ("Insufficient GPU Memory in one device",
+   ``pkg/scheduler/gpushare-predicate.go:29``) and they stay Pending; the 50 GiB pod is placed;
+5. CU-mask isolation (MPS stand-in): 4 pods x 64 GiB with ``gpushare.amd.com/cu-count: 64`` on one
+   device -> disjoint 64-CU partitions, 8 CUs on each of the 8 XCDs.  With ``--gpu`` each pod's
+   partition is also checked on the MI355X: a CU-masked stream runs the CU probe kernel and the
+   hardware CU ids it records must be 64 per pod and disjoint across pods.
+
+``--gpu``: device sizes come from the real MI355X (devices beyond the box's GPUs are fakes of the
+same size) and configs 2 and 5 use a real HBM arena on GPU 0 (each pod's slice stamped and every
+resident slice verified by the admission kernel).  Without it everything is CPU-only.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import sys
+import time
+
+from ..k8s.client import KubeClient
+from ..k8s.fasthttp import Client as HttpClient
+from ..k8s.objects import make_node, make_pod
+from ..models.profile import (ALIYUN, NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION, SHARED_GPU,
+                              NamingProfile)
+from .cluster import start_apiserver, start_extender, start_node_agent, start_scheduler
+
+GIB = 1 << 30
+NODE = "mi355x-node-0"
+CU_COUNT_ANNOTATION = "gpushare.amd.com/cu-count"
+
+
+class Runtimes:
+    """One pod runtime endpoint per device (native ``_engine.PodRuntime``): accounting only, or GPU 0's HBM arena."""
+
+    def __init__(self, n: int, unit_bytes: int, gib_per_dev: int, gpu: bool):
+        from ..core.engine import native
+
+        E = native()
+        self.rts, self.urls, self.bufs, self.streams = [], [], [], []
+        for i in range(n):
+            arena = gib_per_dev * unit_bytes
+            if gpu and i == 0:
+                from ..ops import hip
+
+                buf = hip.DeviceBuffer(0, arena)
+                st = hip.Stream(0)
+                rt = E.PodRuntime(0, arena, buf.addr(0), st.ptr, 1 << 20, hip.lib()._name)
+                self.bufs.append(buf)
+                self.streams.append(st)
+            else:
+                rt = E.PodRuntime(i, arena)
+            self.rts.append(rt)
+            self.urls.append(f"http://127.0.0.1:{rt.serve('127.0.0.1', 0)}")
+
+    def stats(self) -> list[dict]:
+        return [rt.stats() for rt in self.rts]
+
+    def verify(self) -> int:
+        return sum(rt.verify() for rt in self.rts)
+
+    def close(self):
+        for rt in self.rts:
+            rt.stop()
+        for s in self.streams:
+            s.sync()
+            s.destroy()
+        for b in self.bufs:
+            b.free()
+
+
+class Cluster:
+    """apiserver + extender + scheduler + node agent (child processes) and one node with ``len(totals)`` devices."""
+
+    def __init__(self, profile: NamingProfile, totals: list[int], gpu: bool, cu_count: int = 256):
+        self.profile = profile
+        self.totals = totals
+        self.children = []
+        self.api = start_apiserver()
+        self.children.append(self.api)
+        self.ext = start_extender(self.api.url, profile=profile.name)
+        self.children.append(self.ext)
+        self.children.append(start_scheduler(self.api.url, self.ext.url, profile=profile.name))
+        self.children.append(start_node_agent(self.api.url, NODE, profile=profile.name))
+        self.rt = Runtimes(len(totals), GIB, max(totals), gpu)
+        self.cu_count = cu_count
+
+    async def start(self):
+        self.c = KubeClient(self.api.url)
+        inv = [{"index": i, "bdf": f"0000:{0x10 + i:02x}:00.0", "uuid": f"gpu-{i}", "units": t, "total_bytes": t * GIB,
+                "cu": self.cu_count, "render": 128 + i, "card": i, "partition": "SPX"} for i, t in enumerate(self.totals)]
+        node = make_node(NODE, sum(self.totals), len(self.totals), profile=self.profile, device_totals=self.totals,
+                         annotations={NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv),
+                                      NODE_RUNTIME_ENDPOINTS_ANNOTATION: json.dumps(
+                                          {str(i): u for i, u in enumerate(self.rt.urls)})},
+                         labels={"gpushare": "true"})
+        await self.c.create("nodes", node)
+        self.ext_http = HttpClient(self.ext.url)
+        self.agent_http = HttpClient(next(ch.url for ch in self.children if ch.name == "node-agent"))
+        for _ in range(2000):  # the extender has seen the node
+            if (await self.inspect()).get("nodes"):
+                return
+            await asyncio.sleep(0.005)
+        raise TimeoutError("extender never saw the node")
+
+    async def inspect(self) -> dict:
+        r = await self.ext_http.request("GET", "/gpushare-scheduler/inspect")
+        return json.loads(r.body)
+
+    async def filter(self, pod: dict) -> dict:
+        body = json.dumps({"Pod": pod, "Nodes": None, "NodeNames": [NODE]}).encode()
+        r = await self.ext_http.request("POST", "/gpushare-scheduler/filter", body)
+        return json.loads(r.body)
+
+    async def allocation(self, uid: str) -> dict:
+        r = await self.agent_http.request("GET", f"/v1/allocations/{uid}")
+        return json.loads(r.body) if r.status == 200 else {}
+
+    async def create(self, name: str, gib: int, annotations: dict | None = None) -> dict:
+        pod = make_pod(name, gib, profile=self.profile, annotations=annotations)
+        del pod["metadata"]["uid"]
+        return await self.c.create("pods", pod)
+
+    async def wait(self, names: list[str], phase: str = "Running", timeout: float = 30.0) -> dict[str, dict]:
+        deadline = time.monotonic() + timeout
+        while True:
+            pods = {p["metadata"]["name"]: p for p in (await self.c.list("pods", "default"))["items"]}
+            got = {n: pods[n] for n in names if n in pods and pods[n].get("status", {}).get("phase") == phase}
+            if len(got) == len(names):
+                return got
+            failed = [n for n in names if n in pods and pods[n].get("status", {}).get("phase") == "Failed"]
+            if failed or time.monotonic() > deadline:
+                raise RuntimeError(f"pods not {phase}: {sorted(set(names) - set(got))}; failed: {failed}")
+            await asyncio.sleep(0.01)
+
+    async def pending_after(self, names: list[str], seconds: float) -> list[str]:
+        """Names still unbound after ``seconds`` (the scheduler keeps retrying them)."""
+        await asyncio.sleep(seconds)
+        pods = {p["metadata"]["name"]: p for p in (await self.c.list("pods", "default"))["items"]}
+        return [n for n in names if not pods[n].get("spec", {}).get("nodeName")]
+
+    def device_of(self, pod: dict) -> int:
+        return int(pod["metadata"]["annotations"][self.profile.annotation_idx])
+
+    async def close(self):
+        await self.c.close()
+        await self.ext_http.close()
+        await self.agent_http.close()
+        self.rt.close()
+        for ch in reversed(self.children):
+            ch.stop()
+
+
+def _gpu_gib() -> int:
+    from ..ops import hip
+
+    return hip.mem_info(0)[1] // GIB
+
+
+async def config1(gpu: bool) -> dict:
+    cl = Cluster(SHARED_GPU, [16], gpu=False)
+    try:
+        await cl.start()
+        for i in range(2):
+            await cl.create(f"binpack-{i}", 2)
+        pods = await cl.wait([f"binpack-{i}" for i in range(2)])
+        devs = sorted(cl.device_of(p) for p in pods.values())
+        insp = await cl.inspect()
+        ok = devs == [0, 0] and insp["nodes"][0]["usedGPU"] == 4
+        return {"ok": ok, "devices": devs, "inspect_used": insp["nodes"][0]["usedGPU"],
+                "inspect_total": insp["nodes"][0]["totalGPU"]}
+    finally:
+        await cl.close()
+
+
+async def config2(gpu: bool) -> dict:
+    total = _gpu_gib() if gpu else 268
+    cl = Cluster(ALIYUN, [total], gpu=gpu)
+    try:
+        await cl.start()
+        t0 = time.perf_counter()
+        for i in range(4):
+            await cl.create(f"p64-{i}", 64)
+        pods = await cl.wait([f"p64-{i}" for i in range(4)])
+        dt = time.perf_counter() - t0
+        insp = await cl.inspect()
+        used = insp["nodes"][0]["usedGPU"]
+        bad = cl.rt.verify() if gpu else 0
+        st = cl.rt.stats()[0]
+        ok = sorted(cl.device_of(p) for p in pods.values()) == [0] * 4 and used == 256 and bad == 0
+        return {"ok": ok, "device_gib": total, "used_gib": used, "util_pct": round(100 * used / total, 2),
+                "resident_slices": st.get("resident"), "bad_stamps": bad, "hbm_arena": gpu, "seconds": round(dt, 4)}
+    finally:
+        await cl.close()
+
+
+async def config3(gpu: bool) -> dict:
+    per = _gpu_gib() if gpu else 268
+    cl = Cluster(ALIYUN, [per] * 8, gpu=False)
+    try:
+        await cl.start()
+        t0 = time.perf_counter()
+        await asyncio.gather(*(cl.create(f"p64-{i}", 64) for i in range(32)))
+        pods = await cl.wait([f"p64-{i}" for i in range(32)])
+        dt = time.perf_counter() - t0
+        per_dev = [0] * 8
+        for p in pods.values():
+            per_dev[cl.device_of(p)] += 64
+        insp = await cl.inspect()
+        used = insp["nodes"][0]["usedGPU"]
+        ok = per_dev == [256] * 8 and used == 256 * 8
+        return {"ok": ok, "per_device_gib": per_dev, "device_gib": per, "util_pct": round(100 * used / (8 * per), 2),
+                "seconds": round(dt, 4)}
+    finally:
+        await cl.close()
+
+
+async def config4(gpu: bool) -> dict:
+    per = _gpu_gib() if gpu else 268
+    cl = Cluster(ALIYUN, [per] * 8, gpu=False)
+    try:
+        await cl.start()
+        for i in range(8):
+            await cl.create(f"big-{i}", 200)
+        big = await cl.wait([f"big-{i}" for i in range(8)])
+        placed = sorted(cl.device_of(p) for p in big.values())
+        free_dev = per - 200
+        free_node = 8 * free_dev
+        out = {"device_gib": per, "fill": "8 x 200 GiB", "placed_devices": placed, "free_per_device_gib": free_dev,
+               "free_on_node_gib": free_node, "requests": []}
+        ok = placed == list(range(8))
+        for name, gib in (("req-100", 100), ("req-200", 200), ("req-50", 50)):
+            pod = make_pod(name, gib, profile=ALIYUN)
+            f = await cl.filter(pod)
+            await cl.create(name, gib)
+            fits_aggregate = gib <= free_node
+            rec = {"request_gib": gib, "fits_node_aggregate": fits_aggregate, "extender_nodes": f["NodeNames"],
+                   "failed_reason": (f.get("FailedNodes") or {}).get(NODE, "")}
+            if gib <= free_dev:
+                p = (await cl.wait([name]))[name]
+                rec["placed_device"] = cl.device_of(p)
+                ok = ok and f["NodeNames"] == [NODE]
+            else:
+                rec["pending_after_0.5s"] = bool(await cl.pending_after([name], 0.5))
+                ok = ok and fits_aggregate and f["NodeNames"] == [] and \
+                    rec["failed_reason"] == "Insufficient GPU Memory in one device" and rec["pending_after_0.5s"]
+            out["requests"].append(rec)
+        out["ok"] = ok
+        return out
+    finally:
+        await cl.close()
+
+
+async def config5(gpu: bool) -> dict:
+    total = _gpu_gib() if gpu else 268
+    cl = Cluster(ALIYUN, [total], gpu=gpu)
+    try:
+        await cl.start()
+        for i in range(4):
+            await cl.create(f"cu-{i}", 64, annotations={CU_COUNT_ANNOTATION: "64"})
+        pods = await cl.wait([f"cu-{i}" for i in range(4)])
+        parts = []
+        for name in sorted(pods):
+            env = (await cl.allocation(pods[name]["metadata"]["uid"])).get("envs", {})
+            words = [int(w, 16) for w in env.get("GSX_CU_MASK", "").split(",") if w]
+            cus = [32 * wi + b for wi, w in enumerate(words) for b in range(32) if w >> b & 1]
+            parts.append({"pod": name, "HSA_CU_MASK": env.get("HSA_CU_MASK", ""), "cus": cus})
+        sets = [set(p["cus"]) for p in parts]
+        disjoint = all(not (sets[i] & sets[j]) for i in range(4) for j in range(i + 1, 4))
+        per_xcd = [sorted({c // 32 for c in s}) for s in sets]
+        ok = disjoint and all(len(s) == 64 for s in sets) and all(x == list(range(8)) for x in per_xcd)
+        out = {"device_gib": total, "partitions": [{"pod": p["pod"], "HSA_CU_MASK": p["HSA_CU_MASK"],
+                                                   "n_cus": len(p["cus"])} for p in parts],
+               "disjoint": disjoint, "xcds_per_pod": [len(x) for x in per_xcd]}
+        if gpu:
+            from ..ops import hip
+
+            hw = []
+            for p in parts:
+                s = hip.Stream(0, hip.mask_words(p["cus"]))
+                hw.append(hip.physical_cus(hip.cuprobe(s, 8192, 20000)))
+                s.destroy()
+            hw_disjoint = all(not (hw[i] & hw[j]) for i in range(4) for j in range(i + 1, 4))
+            out["probe_cus_per_pod"] = [len(h) for h in hw]
+            out["probe_disjoint"] = hw_disjoint
+            # physical XCDs each partition landed on (the partitioner intends 8 CUs on each of the 8)
+            out["probe_xcds_per_pod"] = [len({t[0] for t in h}) for h in hw]
+            out["probe_cus_per_xcd"] = [sorted(sum(1 for t in h if t[0] == x) for x in {t[0] for t in h}) for h in hw]
+            ok = ok and hw_disjoint and all(len(h) == 64 for h in hw)
+        out["ok"] = ok
+        return out
+    finally:
+        await cl.close()
+
+
+CONFIGS = {
+    1: ("kind cluster + fake device plugin: 2 pods binpack onto one fake device", config1),
+    2: ("1xMI355X: 4 pods x 64 GiB binpacked onto the single 288 GB device", config2),
+    3: ("8xMI355X: 32 pods x 64 GiB, binpack-first across all 8 devices", config3),
+    4: ("fragmentation guard: 200/100/50 GiB requests that fit the node total but no single device", config4),
+    5: ("CU-mask isolation: 4 pods co-resident on one MI355X with per-pod CU partitions", config5),
+}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpu", action="store_true", help="real MI355X sizes, HBM arena and CU probe (needs a GPU)")
+    ap.add_argument("--only", default="", help="comma-separated config numbers")
+    ap.add_argument("--json-out", default="")
+    a = ap.parse_args(argv)
+    which = [int(x) for x in a.only.split(",") if x] or sorted(CONFIGS)
+    report = {}
+    for k in which:
+        desc, fn = CONFIGS[k]
+        t0 = time.perf_counter()
+        try:
+            res = asyncio.run(fn(a.gpu))
+        except Exception as e:  # noqa: BLE001 - reported per config
+            res = {"ok": False, "error": f"{type(e).__name__}: {e}"}
+        res["wall_s"] = round(time.perf_counter() - t0, 3)
+        report[str(k)] = {"config": desc, **res}
+        print(f"[{'PASS' if res['ok'] else 'FAIL'}] {k}. {desc}: "
+              f"{json.dumps({x: y for x, y in res.items() if x not in ('ok', 'requests', 'partitions')})}", flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            json.dump(report, f, indent=1)
+    return 0 if all(v["ok"] for v in report.values()) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
