@@ -55,6 +55,7 @@ class NodeAgent:
         self.latency: list[float] = []  # bound-observed -> Running
         self._bg: set[asyncio.Task] = set()
         self._releasing: set[asyncio.Task] = set()
+        self._assign_retries: dict[str, int] = {}
         self.queue: asyncio.Queue = asyncio.Queue()
         self.queued: set[str] = set()
         self.seen: dict[str, float] = {}
@@ -168,15 +169,19 @@ class NodeAgent:
             try:
                 await self.client.patch("pods", podutil.meta(pod)["name"], assigned_patch(pod, self.profile,
                                         alloc.annotations), podutil.meta(pod)["namespace"])
-            except ApiError as e:
-                if e.conflict:  # stale copy: retry from the informer's latest version
-                    if cus:
-                        self.cus[dev_idx].release(uid)
-                    if uid not in self.queued:
-                        self.queued.add(uid)
-                        asyncio.get_running_loop().call_later(0.001, self.queue.put_nowait, key)
-                    return
-                raise
+            except (ApiError, OSError) as e:
+                # 409: stale copy, retry from the informer's latest version; 5xx / transport: retry with
+                # capped backoff (as kubelet does); other 4xx: give up
+                if isinstance(e, ApiError) and not (e.conflict or e.status >= 500):
+                    raise
+                if cus:
+                    self.cus[dev_idx].release(uid)
+                if uid not in self.queued:
+                    n = self._assign_retries[uid] = self._assign_retries.get(uid, 0) + 1
+                    self.queued.add(uid)
+                    asyncio.get_running_loop().call_later(min(0.2, 0.001 * 2 ** min(n, 8)), self.queue.put_nowait,
+                                                          key)
+                return
             self.allocations[uid] = alloc.envs
             try:
                 bad = await self._admit_runtime(uid, dev_idx, units * self.unit_bytes, cus)
@@ -188,22 +193,34 @@ class NodeAgent:
                 log.error("admission of %s on GPU %d failed: %s", key, dev_idx, e)
                 self._release(uid) if getattr(self.runtime, "release", None) else self.runtime.stop(uid)
                 if self.report_status:
-                    await self.client.patch("pods", podutil.meta(pod)["name"],
-                                            {"status": {"phase": "Failed", "reason": "UnexpectedAdmissionError",
-                                                        "message": str(e)}},
-                                            podutil.meta(pod)["namespace"], sub="status")
+                    await self._patch_status(pod, {"phase": "Failed", "reason": "UnexpectedAdmissionError",
+                                                   "message": str(e)})
                 return
             self.running[uid] = key
             self.admitted += 1
+            self._assign_retries.pop(uid, None)
             if self.report_status:
-                await self.client.patch("pods", podutil.meta(pod)["name"], {"status": {"phase": "Running"}},
-                                        podutil.meta(pod)["namespace"], sub="status")
+                await self._patch_status(pod, {"phase": "Running"})
             self.latency.append(time.perf_counter() - t0)
             self.seen.pop(uid, None)
         except Exception as e:  # noqa: BLE001
             log.exception("admit %s: %r", key, e)
         finally:
             self.inflight.discard(uid)
+
+    async def _patch_status(self, pod: dict, status: dict):
+        """kubelet's status manager: retried on 409 / 5xx / transport errors with capped backoff; 404 ends it."""
+        md = podutil.meta(pod)
+        for attempt in range(50):
+            try:
+                await self.client.patch("pods", md["name"], {"status": status}, md["namespace"], sub="status")
+                return
+            except ApiError as e:
+                if e.not_found or not (e.conflict or e.status >= 500):
+                    return
+            except OSError:
+                pass
+            await asyncio.sleep(min(0.1, 0.0005 * 2 ** min(attempt, 8)))
 
     async def start(self):
         await self.pods.start()

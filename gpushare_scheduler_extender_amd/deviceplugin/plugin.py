@@ -45,6 +45,8 @@ def fake_ids(dev: Device, units: int) -> list[str]:
     return [f"{base}{ID_SEP}{k}" for k in range(units)]
 
 
+ALLOCATE_ATTEMPTS = 8  # per container request: transient apiserver failures retried with capped backoff
+
 class GpuSharePlugin:
     def __init__(self, client: KubeClient, node: str, devices: list[Device], profile: NamingProfile, *,
                  unit: str = "GiB", socket_dir: str = api.DEVICE_PLUGIN_PATH, endpoint: str = "gpushare-amd.sock",
@@ -67,10 +69,12 @@ class GpuSharePlugin:
         self.partial: dict[str, list[int]] = {}  # pod uid -> container requests not yet allocated
         self._changed = asyncio.Event()
         self._version = 0
+        self._stopped = False
         self._server: grpc.aio.Server | None = None
         self._tasks: list[asyncio.Task] = []
         self.allocations = 0
-        self.stats = {"allocate_ok": 0, "allocate_fail": 0, "preferred": 0, "registrations": 0}
+        self.stats = {"allocate_ok": 0, "allocate_fail": 0, "allocate_retries": 0, "preferred": 0,
+                      "registrations": 0}
 
     # ------------------------------------------------------------ paths
     @property
@@ -110,7 +114,9 @@ class GpuSharePlugin:
 
     async def ListAndWatch(self, request, context):
         seen = -1
-        while True:
+        # the flag also ends the stream: before Python 3.12 asyncio.wait_for may swallow the cancellation
+        # that grpc delivers when kubelet goes away
+        while not self._stopped:
             if seen != self._version:
                 seen = self._version
                 yield api.ListAndWatchResponse(devices=self.device_list())
@@ -159,34 +165,55 @@ class GpuSharePlugin:
             self.stats["preferred"] += 1
         return resp
 
+    async def _claim(self, pods: list[dict], units: int) -> tuple:
+        """Match one container request to its pod; for the pod's first container commit ASSIGNED=true.
+
+        A 409 (the pod changed since our LIST) or an apiserver 5xx / transport error is retried from a
+        fresh LIST with capped backoff: failing Allocate makes kubelet reject the pod
+        (UnexpectedAdmissionError) over a transient apiserver hiccup.  Returns (pod, whole, alloc, pods)."""
+        for attempt in range(ALLOCATE_ATTEMPTS):
+            pod, whole = self._match(pods, units)
+            if pod is None:
+                raise AllocateError(f"no pending pod on {self.node} requests {units} {self.profile.resource} "
+                                    f"with {self.profile.annotation_assigned}=false")
+            uid = podutil.meta(pod).get("uid", "")
+            dev_idx = podutil.gpu_id_from_annotation(pod, self.profile)
+            device = self.devices.get(dev_idx)
+            if device is None:
+                raise AllocateError(f"pod {podutil.pod_key(pod)} annotated with GPU {dev_idx}, not on this node")
+            cus = None
+            want = podutil.annotations(pod).get(CU_COUNT_ANNOTATION)
+            if want:
+                cus = self.cus[dev_idx].allocate(uid, int(want))
+            alloc = build_response(pod, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
+            if uid in self.partial:  # a later container of a pod whose first container committed
+                return pod, whole, alloc, pods
+            try:
+                # first (or only) container: commit point ASSIGNED=true
+                await self.client.patch("pods", podutil.meta(pod)["name"],
+                                        assigned_patch(pod, self.profile, alloc.annotations),
+                                        podutil.meta(pod)["namespace"])
+                return pod, whole, alloc, pods
+            except (ApiError, OSError) as e:
+                if cus:
+                    self.cus[dev_idx].release(uid)
+                transient = not isinstance(e, ApiError) or e.conflict or e.status >= 500
+                if not transient or attempt == ALLOCATE_ATTEMPTS - 1:
+                    raise AllocateError(f"marking {podutil.pod_key(pod)} assigned failed: {e}") from e
+                self.stats["allocate_retries"] += 1
+                await asyncio.sleep(min(0.2, 0.005 * 2 ** attempt))
+                pods = await self._pods_on_node()
+        raise AllocateError("unreachable")
+
     async def Allocate(self, request, context):
         resp = api.AllocateResponse()
         try:
             pods = await self._pods_on_node()
             for creq in request.container_requests:
                 units = len(creq.devices_ids)
-                pod, whole = self._match(pods, units)
-                if pod is None:
-                    raise AllocateError(f"no pending pod on {self.node} requests {units} {self.profile.resource} "
-                                        f"with {self.profile.annotation_assigned}=false")
+                pod, whole, alloc, pods = await self._claim(pods, units)
                 uid = podutil.meta(pod).get("uid", "")
-                dev_idx = podutil.gpu_id_from_annotation(pod, self.profile)
-                device = self.devices.get(dev_idx)
-                if device is None:
-                    raise AllocateError(f"pod {podutil.pod_key(pod)} annotated with GPU {dev_idx}, not on this node")
-                cus = None
-                want = podutil.annotations(pod).get(CU_COUNT_ANNOTATION)
-                if want:
-                    cus = self.cus[dev_idx].allocate(uid, int(want))
-                alloc = build_response(pod, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
                 if uid not in self.partial:
-                    # first (or only) container: commit point ASSIGNED=true
-                    try:
-                        await self.client.patch("pods", podutil.meta(pod)["name"],
-                                                assigned_patch(pod, self.profile, alloc.annotations),
-                                                podutil.meta(pod)["namespace"])
-                    except ApiError as e:
-                        raise AllocateError(f"marking {podutil.pod_key(pod)} assigned failed: {e}") from e
                     if not whole:
                         reqs = [podutil.container_limit(c, self.profile.resource)
                                 for c in (pod.get("spec") or {}).get("containers", [])]
@@ -328,6 +355,8 @@ class GpuSharePlugin:
             self._tasks.append(asyncio.get_running_loop().create_task(self._event_loop()))
 
     async def stop(self):
+        self._stopped = True
+        self._changed.set()
         for t in self._tasks:
             t.cancel()
         if self._server is not None:

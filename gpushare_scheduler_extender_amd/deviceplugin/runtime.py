@@ -6,7 +6,10 @@ runtime:
 
 * :class:`HbmArenaRuntime` — the MI355X path.  Each device holds one HBM
   arena sized to what the node advertises; an admitted pod gets a 2 MiB
-  aligned slice (first fit), the slice is stamped with the pod's tag by a HIP
+  aligned slice — extents taken first-fit from the arena's holes, so a pod
+  that fits the device's free bytes is admitted even when the arena is
+  fragmented (the extender accounts a device as one number, like HBM behind
+  the GPU's page tables) — the slice is stamped with the pod's tag by a HIP
   kernel and every resident pod's stamps are verified after each admission.
   A binpack decision that overcommits a device, or two pods sharing bytes,
   shows up as a failed admission or as bad stamps — on real HBM;
@@ -26,31 +29,33 @@ class AdmissionError(Exception):
 
 
 class _Slices:
-    """First-fit allocator of aligned [offset, offset+size) slices in one arena."""
+    """Aligned slices of one arena, each a list of (offset, size) extents taken first-fit from the holes."""
 
     def __init__(self, capacity: int):
         self.capacity = capacity
-        self.used: dict[str, tuple[int, int]] = {}
+        self.used: dict[str, list[tuple[int, int]]] = {}
 
-    def alloc(self, uid: str, size: int) -> int:
+    def alloc(self, uid: str, size: int) -> list[tuple[int, int]]:
         if uid in self.used:
-            return self.used[uid][0]
+            return self.used[uid]
         size = (size + ALIGN - 1) // ALIGN * ALIGN
-        pos = 0
-        for off, sz in sorted(self.used.values()):
-            if off - pos >= size:
-                break
+        ext, pos, need = [], 0, size
+        for off, sz in sorted(e for x in self.used.values() for e in x) + [(self.capacity, 0)]:
+            if need and off > pos:
+                n = min(need, off - pos)
+                ext.append((pos, n))
+                need -= n
             pos = max(pos, off + sz)
-        if pos + size > self.capacity:
-            raise AdmissionError(f"arena exhausted: need {size} B at {pos}, capacity {self.capacity}")
-        self.used[uid] = (pos, size)
-        return pos
+        if need:
+            raise AdmissionError(f"arena exhausted: need {size} B, {size - need} free of {self.capacity}")
+        self.used[uid] = ext
+        return ext
 
-    def free(self, uid: str) -> tuple[int, int] | None:
+    def free(self, uid: str) -> list[tuple[int, int]] | None:
         return self.used.pop(uid, None)
 
     def bytes_used(self) -> int:
-        return sum(sz for _, sz in self.used.values())
+        return sum(sz for x in self.used.values() for _, sz in x)
 
 
 def pod_tag(uid: str) -> int:
@@ -64,12 +69,13 @@ class LedgerRuntime:
         self.lock = threading.Lock()
 
     def start(self, uid: str, dev: int, nbytes: int, cus: list[int] | None = None) -> int:
+        """Carve the pod's slice; returns the offset of its first extent."""
         with self.lock:
             if dev not in self.slices:
                 raise AdmissionError(f"device {dev} not managed here")
-            off = self.slices[dev].alloc(uid, nbytes)
+            ext = self.slices[dev].alloc(uid, nbytes)
             self.where[uid] = dev
-            return off
+            return ext[0][0]
 
     def stop(self, uid: str) -> bool:
         with self.lock:
@@ -104,44 +110,42 @@ class HbmArenaRuntime(LedgerRuntime):
 
     def start(self, uid: str, dev: int, nbytes: int, cus: list[int] | None = None) -> int:
         off = super().start(uid, dev, nbytes, cus)
-        size = self.slices[dev].used[uid][1]
-        self.hip.hbm_stamp(self.stream[dev], self.arena[dev].addr(off), size, self.stride, pod_tag(uid))
+        for o, size in self.slices[dev].used[uid]:
+            self.hip.hbm_stamp(self.stream[dev], self.arena[dev].addr(o), size, self.stride, pod_tag(uid))
         self.stamps += 1
         return off
 
     def stop(self, uid: str) -> bool:
         with self.lock:
             dev = self.where.get(uid)
-            sl = self.slices[dev].used.get(uid) if dev is not None else None
-        if sl is not None and self.scrub:
-            self.hip.hbm_fill(self.stream[dev], self.arena[dev].addr(sl[0]), sl[1], 0)
+            ext = self.slices[dev].used.get(uid) if dev is not None else None
+        if ext is not None and self.scrub:
+            for o, size in ext:
+                self.hip.hbm_fill(self.stream[dev], self.arena[dev].addr(o), size, 0)
         return super().stop(uid)
 
     def admit_sync(self, uid: str, dev: int, nbytes: int, cus=None, verify: bool = True) -> int:
         """Carve the slice, stamp it and verify every resident slice of the GPU: 2 launches, 1 sync."""
-        off = LedgerRuntime.start(self, uid, dev, nbytes, cus)
+        LedgerRuntime.start(self, uid, dev, nbytes, cus)
         with self.lock:
-            items = [(u, self.slices[dev].used[u]) for u, d in self.where.items() if d == dev]
-        sl = [(self.arena[dev].addr(o), sz, pod_tag(u)) for u, (o, sz) in items]
-        idx = next(i for i, (u, _) in enumerate(items) if u == uid)
-        if not verify:
-            sl, idx = [sl[idx]], 0
-            self.hip.hbm_admit(self.stream[dev], sl, 0, self.stride)
-            self.stamps += 1
-            return 0
-        bad = self.hip.hbm_admit(self.stream[dev], sl, idx, self.stride)
+            used = self.slices[dev].used
+            mine = [(self.arena[dev].addr(o), sz, pod_tag(uid)) for o, sz in used[uid]]
+            others = [(self.arena[dev].addr(o), sz, pod_tag(u)) for u, d in self.where.items() if d == dev and u != uid
+                      for o, sz in used[u]] if verify else []
+        bad = self.hip.hbm_admit_n(self.stream[dev], mine + others, len(mine), self.stride)
         self.stamps += 1
-        self.verified += len(sl)
-        del off
-        return bad
+        self.verified += len(mine) + len(others)
+        return bad if verify else 0
 
     def verify(self) -> int:
         """Verify every resident pod's stamps; returns the number of bad stamps."""
         bad = 0
         with self.lock:
-            items = [(uid, dev, self.slices[dev].used[uid]) for uid, dev in self.where.items()]
-        for uid, dev, (off, size) in items:
-            bad += self.hip.hbm_verify(self.stream[dev], self.arena[dev].addr(off), size, self.stride, pod_tag(uid))
+            items = [(uid, dev, list(self.slices[dev].used[uid])) for uid, dev in self.where.items()]
+        for uid, dev, ext in items:
+            for off, size in ext:
+                bad += self.hip.hbm_verify(self.stream[dev], self.arena[dev].addr(off), size, self.stride,
+                                           pod_tag(uid))
             self.verified += 1
         return bad
 

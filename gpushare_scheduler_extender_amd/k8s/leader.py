@@ -54,6 +54,7 @@ class LeaderElector:
         self._observed_at = 0.0
         self._last_renew = 0.0
         self._task: asyncio.Task | None = None
+        self._stopping = False
 
     def _lease_obj(self, cur: dict | None) -> dict:
         now = _micro_time()
@@ -101,7 +102,10 @@ class LeaderElector:
         return True
 
     async def _run(self):
-        while True:
+        # The flag, not only the cancel, ends the loop: before Python 3.12 asyncio.wait_for returns the
+        # inner result and swallows a cancellation that lands just as the inner call completes, and a
+        # loop that relied on CancelledError alone would renew forever (stop() would never return).
+        while not self._stopping:
             try:
                 ok = await asyncio.wait_for(self.try_acquire_or_renew(), self.renew_deadline)
             except (ApiError, OSError, ConnectionError, asyncio.TimeoutError) as e:
@@ -124,6 +128,7 @@ class LeaderElector:
         self._task = asyncio.get_running_loop().create_task(self._run(), name=f"leader-{self.name}")
 
     async def stop(self, release: bool = True):
+        self._stopping = True
         if self._task:
             self._task.cancel()
             try:

@@ -240,6 +240,22 @@ def hbm_admit(stream: Stream, slices: list[tuple[int, int, int]], stamp_idx: int
     return bad.value
 
 
+def hbm_admit_n(stream: Stream, slices: list[tuple[int, int, int]], n_stamp: int, stride: int,
+                verify: bool = True) -> int:
+    """Stamp the first ``n_stamp`` ``(addr, bytes, tag)`` extents, then verify all of them; one stream sync."""
+    L = lib()
+    if not getattr(L, "_admit_n_sig", False):
+        L.gsx_hbm_admit_n.argtypes = [ctypes.c_void_p, ctypes.POINTER(Slice), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+        L.gsx_hbm_admit_n.restype = ctypes.c_int
+        L._admit_n_sig = True
+    arr = (Slice * max(1, len(slices)))(*[Slice(a, b, t & 0xFFFFFFFFFFFFFFFF) for a, b, t in slices])
+    bad = ctypes.c_uint64(0)
+    _ck(L.gsx_hbm_admit_n(stream.handle, arr, len(slices), n_stamp, int(verify), stride, ctypes.byref(bad)),
+        "hbm_admit_n")
+    return bad.value
+
+
 GEMM_CFGS = {0: "128x128/4w", 1: "256x128/8w", 2: "128x256/8w", 3: "256x256/8w", 4: "128x128/4w-nogroup",
              5: "256x256/8w-phased-g4", 6: "256x256/8w-phased-g8", 7: "256x256/4w-agpr-g4", 8: "256x256/4w-agpr-g8",
              9: "256x256/4w-asm-agpr-g4"}

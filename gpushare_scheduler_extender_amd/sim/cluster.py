@@ -111,8 +111,8 @@ def start_apiserver(native: bool = True, history: int = 200000, threads: int | N
 
 
 def start_extender(apiserver: str, profile: str = "shared-gpu", bind_mode: str = "binding", threadness: int = 1,
-                   log_level: str = "warning") -> ChildProc:
-    return ChildProc(["-m", "gpushare_scheduler_extender_amd.extender", "--host", "127.0.0.1", "--port", "0",
+                   log_level: str = "warning", port: int = 0) -> ChildProc:
+    return ChildProc(["-m", "gpushare_scheduler_extender_amd.extender", "--host", "127.0.0.1", "--port", str(port),
                       "--apiserver", apiserver, "--profile", profile, "--bind-mode", bind_mode,
                       "--threadness", str(threadness), "--log-level", log_level], "extender")
 

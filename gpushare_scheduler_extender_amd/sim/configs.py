@@ -85,7 +85,8 @@ class Runtimes:
 class Cluster:
     """apiserver + extender + scheduler + node agent (child processes) and one node with ``len(totals)`` devices."""
 
-    def __init__(self, profile: NamingProfile, totals: list[int], gpu: bool, cu_count: int = 256):
+    def __init__(self, profile: NamingProfile, totals: list[int], gpu: bool, cu_count: int = 256,
+                 native: bool = True):
         self.profile = profile
         self.totals = totals
         self.children = []
@@ -93,8 +94,9 @@ class Cluster:
         self.children.append(self.api)
         self.ext = start_extender(self.api.url, profile=profile.name)
         self.children.append(self.ext)
-        self.children.append(start_scheduler(self.api.url, self.ext.url, profile=profile.name))
-        self.children.append(start_node_agent(self.api.url, NODE, profile=profile.name))
+        # native: compiled kube-scheduler / node-agent stand-ins; otherwise the asyncio ones
+        self.children.append(start_scheduler(self.api.url, self.ext.url, profile=profile.name, native=native))
+        self.children.append(start_node_agent(self.api.url, NODE, profile=profile.name, native=native))
         self.rt = Runtimes(len(totals), GIB, max(totals), gpu)
         self.cu_count = cu_count
 
@@ -151,6 +153,19 @@ class Cluster:
         await asyncio.sleep(seconds)
         pods = {p["metadata"]["name"]: p for p in (await self.c.list("pods", "default"))["items"]}
         return [n for n in names if not pods[n].get("spec", {}).get("nodeName")]
+
+    def kill_extender(self):
+        """SIGKILL the extender: no graceful shutdown, its in-memory ledger is gone."""
+        self.ext.proc.kill()
+        self.ext.proc.wait(5)
+
+    def restart_extender(self):
+        """A new extender process on the same port (kube-scheduler keeps its urlPrefix); it rebuilds its
+        ledger from the pod annotations before serving (BuildCache, pkg/cache/cache.go:49-74)."""
+        old = self.ext
+        old.stop()
+        self.ext = start_extender(self.api.url, profile=self.profile.name, port=old.port)
+        self.children[self.children.index(old)] = self.ext
 
     def device_of(self, pod: dict) -> int:
         return int(pod["metadata"]["annotations"][self.profile.annotation_idx])

@@ -46,10 +46,11 @@ bool PodRuntime::init(std::string* err) {
     return false;
   }
   set_device_ = reinterpret_cast<int (*)(int)>(dlsym(lib_, "gsx_set_device"));
-  admit_ = reinterpret_cast<int (*)(void*, const void*, int, int, uint64_t, uint64_t*)>(dlsym(lib_, "gsx_hbm_admit"));
+  admit_n_ = reinterpret_cast<int (*)(void*, const void*, int, int, int, uint64_t, uint64_t*)>(
+      dlsym(lib_, "gsx_hbm_admit_n"));
   last_error_ = reinterpret_cast<const char* (*)()>(dlsym(lib_, "gsx_last_error"));
-  if (!set_device_ || !admit_ || !last_error_) {
-    *err = "libgsx_kernels.so lacks gsx_set_device / gsx_hbm_admit";
+  if (!set_device_ || !admit_n_ || !last_error_) {
+    *err = "libgsx_kernels.so lacks gsx_set_device / gsx_hbm_admit_n";
     return false;
   }
   if (!cfg_.stream || cfg_.stride < 16 || cfg_.stride % 16) {
@@ -80,53 +81,61 @@ size_t PodRuntime::resident() const {
   return slices_.size();
 }
 
-// Stamp `uid`'s slice (if given) and verify every resident slice; mu_ held.
-int64_t PodRuntime::run_admit(int stamp, const std::string& uid, bool verify, std::string* err) {
+int64_t PodRuntime::run_admit(bool stamp, const std::string& uid, bool verify, std::string* err) {
   if (!cfg_.arena_addr) return 0;
   std::vector<GsxSlice> sl;
-  sl.reserve(slices_.size());
-  int idx = -1;
-  for (auto& kv : slices_) {
-    if (stamp && kv.first == uid) idx = static_cast<int>(sl.size());
-    sl.push_back(GsxSlice{cfg_.arena_addr + kv.second.off, kv.second.size, kv.second.tag});
+  auto add = [&](const Slice& s) {
+    for (auto& e : s.ext) sl.push_back(GsxSlice{cfg_.arena_addr + e.first, e.second, s.tag});
+  };
+  auto mine = slices_.find(uid);
+  if (mine != slices_.end()) add(mine->second);  // the new pod's extents first: they are the ones stamped
+  const int n_stamp = stamp ? static_cast<int>(sl.size()) : 0;
+  if (verify) {
+    for (auto& kv : slices_) {
+      if (kv.first != uid) add(kv.second);
+    }
   }
-  if (stamp && !verify) {  // stamp only: pass just the new slice
-    GsxSlice one = sl[static_cast<size_t>(idx)];
-    sl.assign(1, one);
-    idx = 0;
-  }
+  if (sl.empty()) return 0;
   uint64_t bad = 0;
   int rc = set_device_(cfg_.dev);
-  if (rc == 0) rc = admit_(cfg_.stream, sl.data(), static_cast<int>(sl.size()), idx, cfg_.stride, &bad);
+  if (rc == 0) rc = admit_n_(cfg_.stream, sl.data(), static_cast<int>(sl.size()), n_stamp, 1, cfg_.stride, &bad);
   if (rc != 0) {
-    *err = std::string("gsx_hbm_admit: ") + last_error_();
+    *err = std::string("gsx_hbm_admit_n: ") + last_error_();
     return -1;
   }
-  return (stamp && !verify) ? 0 : static_cast<int64_t>(bad);
+  return static_cast<int64_t>(bad);
 }
 
 int64_t PodRuntime::admit(const std::string& uid, uint64_t bytes, bool verify, std::string* err) {
   std::lock_guard<std::mutex> g(mu_);
-  if (slices_.count(uid)) return run_admit(0, uid, verify, err) < 0 ? -1 : 0;  // idempotent
+  if (slices_.count(uid)) return run_admit(false, uid, verify, err) < 0 ? -1 : 0;  // idempotent
   uint64_t size = (bytes + kAlign - 1) / kAlign * kAlign;
-  // first fit over the offset-ordered slices
+  // extents from the arena's holes in offset order (first fit; one extent unless fragmented)
   std::vector<std::pair<uint64_t, uint64_t>> used;
-  used.reserve(slices_.size());
-  for (auto& kv : slices_) used.emplace_back(kv.second.off, kv.second.size);
+  for (auto& kv : slices_) used.insert(used.end(), kv.second.ext.begin(), kv.second.ext.end());
   std::sort(used.begin(), used.end());
-  uint64_t pos = 0;
+  Slice s{{}, size, tag_of(uid)};
+  uint64_t pos = 0, need = size;
+  auto take = [&](uint64_t end) {
+    if (need && end > pos) {
+      uint64_t n = std::min(need, end - pos);
+      s.ext.emplace_back(pos, n);
+      need -= n;
+    }
+  };
   for (auto& u : used) {
-    if (u.first >= pos + size) break;
+    take(u.first);
     pos = std::max(pos, u.first + u.second);
   }
-  if (pos + size > cfg_.arena_bytes) {
+  take(cfg_.arena_bytes);
+  if (need) {
     failed_++;
-    *err = "arena exhausted: need " + std::to_string(size) + " B at " + std::to_string(pos) + ", capacity " +
+    *err = "arena exhausted: need " + std::to_string(size) + " B, " + std::to_string(size - need) + " free of " +
            std::to_string(cfg_.arena_bytes);
     return -1;
   }
-  slices_[uid] = Slice{pos, size, tag_of(uid)};
-  int64_t bad = run_admit(1, uid, verify, err);
+  slices_[uid] = std::move(s);
+  int64_t bad = run_admit(true, uid, verify, err);
   if (bad < 0) {
     slices_.erase(uid);
     failed_++;
@@ -144,7 +153,7 @@ bool PodRuntime::release(const std::string& uid) {
 
 int64_t PodRuntime::verify_all(std::string* err) {
   std::lock_guard<std::mutex> g(mu_);
-  return run_admit(0, std::string(), true, err);
+  return run_admit(false, std::string(), true, err);
 }
 
 CtlServer::Reply PodRuntime::handle(const http::Message& m) {

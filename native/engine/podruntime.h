@@ -2,9 +2,12 @@
 // the node agent starts / stops pods on a GPU through it.  Counterpart of
 // deviceplugin/runtime.py (HbmArenaRuntime + RuntimeShim) without Python on
 // the admission path: the request thread carves the pod's 2 MiB-aligned slice
-// out of the GPU's HBM arena (first fit), stamps it and verifies every
-// resident slice with ONE call into libgsx_kernels.so (gsx_hbm_admit: two
-// kernel launches, one stream sync), and answers.
+// out of the GPU's HBM arena, stamps it and verifies every resident slice with
+// ONE call into libgsx_kernels.so (gsx_hbm_admit_n: two kernel launches, one
+// stream sync), and answers.  A slice is a list of extents taken first-fit
+// from the arena's holes: the extender accounts a device's memory as one
+// number (like HBM behind the GPU's page tables), so a pod that fits the
+// device's free bytes must be admitted even when no single hole is big enough.
 //
 //   POST   /v1/pods/<uid>  {"dev","bytes","cus","verify"} -> {"bad": n} | 409 {"error"}
 //   DELETE /v1/pods/<uid>
@@ -18,6 +21,8 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "ctlserver.h"
 
@@ -51,10 +56,13 @@ class PodRuntime {
 
  private:
   struct Slice {
-    uint64_t off, size, tag;
+    std::vector<std::pair<uint64_t, uint64_t>> ext;  // (offset, bytes), offset-ordered
+    uint64_t size, tag;
   };
   CtlServer::Reply handle(const http::Message& m);
-  int64_t run_admit(int stamp_idx_uid_known, const std::string& uid, bool verify, std::string* err);
+  // Stamp `uid`'s extents (if `stamp`) and verify the resident slices (all of them, or only `uid`'s when
+  // !verify); mu_ held.  Returns bad stamps, -1 with *err.
+  int64_t run_admit(bool stamp, const std::string& uid, bool verify, std::string* err);
 
   PodRuntimeConfig cfg_;
   mutable std::mutex mu_;
@@ -63,7 +71,7 @@ class PodRuntime {
   std::unique_ptr<CtlServer> srv_;
   void* lib_ = nullptr;
   int (*set_device_)(int) = nullptr;
-  int (*admit_)(void*, const void*, int, int, uint64_t, uint64_t*) = nullptr;
+  int (*admit_n_)(void*, const void*, int, int, int, uint64_t, uint64_t*) = nullptr;
   const char* (*last_error_)() = nullptr;
 };
 

@@ -76,6 +76,11 @@ typedef struct {
   uint64_t tag;
 } gsx_slice;
 int gsx_hbm_admit(void* stream, const gsx_slice* slices, int n, int stamp_idx, uint64_t stride, uint64_t* bad);
+// Admission of a pod made of several extents (its slice is not contiguous when the arena is
+// fragmented): stamp slices[0, n_stamp) in one launch, then (verify != 0) verify all n slices;
+// one stream sync.
+int gsx_hbm_admit_n(void* stream, const gsx_slice* slices, int n, int n_stamp, int verify, uint64_t stride,
+                    uint64_t* bad);
 
 // Fill [base, base+bytes) with a 32-bit pattern (bytes % 16 == 0).
 int gsx_hbm_fill(void* stream, void* base, uint64_t bytes, uint32_t pattern);

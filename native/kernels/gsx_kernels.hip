@@ -97,6 +97,16 @@ __global__ __launch_bounds__(256) void verify_slices_kernel(SliceTable t, uint64
   if ((threadIdx.x & 63) == 0 && mine) atomicAdd_system(bad, static_cast<unsigned long long>(mine));
 }
 
+// grid.y = slice; each block strides over that slice's stamp positions
+__global__ __launch_bounds__(256) void stamp_slices_kernel(SliceTable t, uint64_t stride) {
+  const gsx_slice sl = t.s[blockIdx.y];
+  const uint64_t n = sl.bytes / stride;
+  char* base = reinterpret_cast<char*>(sl.addr);
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    *reinterpret_cast<Stamp*>(base + i * stride) = Stamp{sl.tag, i * stride};
+  }
+}
+
 __global__ __launch_bounds__(256) void fill_kernel(uint4* p, uint64_t n16, uint32_t pat) {
   uint4 v = make_uint4(pat, pat, pat, pat);
   uint64_t i = blockIdx.x * 256ull + threadIdx.x;
@@ -301,13 +311,64 @@ int gsx_hbm_admit(void* stream, const gsx_slice* slices, int n, int stamp_idx, u
   __atomic_store_n(hc, 0ull, __ATOMIC_SEQ_CST);
   uint64_t maxn = 0;
   for (int i = 0; i < n; ++i) maxn = std::max<uint64_t>(maxn, slices[i].bytes / stride);
-  // one stamp per lane up to 1024 blocks per slice: the reads are 1 MiB apart (a DRAM page each), so the
-  // kernel is latency-bound and every extra serial iteration per lane costs a full HBM round trip
+  // one stamp per lane (up to 1024 blocks per slice).  Measured on MI355X: verifying 4 x 64 GiB at a
+  // 1 MiB stride takes ~12 us with 64 or with 1024 blocks per slice -- every read opens its own DRAM page
+  // and TLB entry, so translation, not per-lane latency, bounds it (profiles/r01_session7_gpu.md)
   const int gx = grid_for(maxn, 256, 1024);
   for (int base = 0; base < n; base += kMaxSlices) {
     SliceTable t;
     t.n = std::min(kMaxSlices, n - base);
     for (int i = 0; i < t.n; ++i) t.s[i] = slices[base + i];
+    hipLaunchKernelGGL(verify_slices_kernel, dim3(gx, t.n), dim3(256), 0, S(stream), t, stride, hc);
+    GSX_CHECK(hipGetLastError());
+  }
+  GSX_CHECK(hipStreamSynchronize(S(stream)));
+  *bad = __atomic_load_n(hc, __ATOMIC_SEQ_CST);
+  return 0;
+}
+
+int gsx_hbm_admit_n(void* stream, const gsx_slice* slices, int n, int n_stamp, int verify, uint64_t stride,
+                    uint64_t* bad) {
+  *bad = 0;
+  if (n < 0 || n_stamp < 0 || n_stamp > n || stride < sizeof(Stamp) || stride % 16)
+    return fail_arg("gsx_hbm_admit_n: bad n/n_stamp/stride");
+  for (int i = 0; i < n; ++i) {
+    if (!slices[i].addr || slices[i].addr % 16) return fail_arg("gsx_hbm_admit_n: slice base not 16-B aligned");
+  }
+  auto table_grid = [&](int from, int count, SliceTable* t) {
+    t->n = count;
+    uint64_t maxn = 0;
+    for (int i = 0; i < count; ++i) {
+      t->s[i] = slices[from + i];
+      maxn = std::max<uint64_t>(maxn, slices[from + i].bytes / stride);
+    }
+    return grid_for(maxn, 256, 1024);
+  };
+  for (int base = 0; base < n_stamp; base += kMaxSlices) {
+    SliceTable t;
+    const int gx = table_grid(base, std::min(kMaxSlices, n_stamp - base), &t);
+    hipLaunchKernelGGL(stamp_slices_kernel, dim3(gx, t.n), dim3(256), 0, S(stream), t, stride);
+    GSX_CHECK(hipGetLastError());
+  }
+  if (!verify || n == 0) {
+    GSX_CHECK(hipStreamSynchronize(S(stream)));
+    return 0;
+  }
+  int dev = 0;
+  GSX_CHECK(hipGetDevice(&dev));
+  unsigned long long* hc;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (dev < 0 || dev >= 64) return fail_arg("gsx_hbm_admit_n: device index");
+    if (!g_host_counter[dev]) {
+      GSX_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g_host_counter[dev]), 64, hipHostMallocCoherent));
+    }
+    hc = g_host_counter[dev];
+  }
+  __atomic_store_n(hc, 0ull, __ATOMIC_SEQ_CST);
+  for (int base = 0; base < n; base += kMaxSlices) {
+    SliceTable t;
+    const int gx = table_grid(base, std::min(kMaxSlices, n - base), &t);
     hipLaunchKernelGGL(verify_slices_kernel, dim3(gx, t.n), dim3(256), 0, S(stream), t, stride, hc);
     GSX_CHECK(hipGetLastError());
   }

@@ -26,6 +26,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -235,6 +236,7 @@ class Agent {
       std::lock_guard<std::mutex> g(mu_);
       stop_ = true;
     }
+    stop_flag_.store(true);
     cv_.notify_all();
     for (auto& t : workers_) t.join();
     if (pods_r_) pods_r_->stop();
@@ -252,11 +254,12 @@ class Agent {
       std::snprintf(b, sizeof(b),
                     "{\"admitted\":%llu,\"failed\":%llu,\"bad_stamps\":%llu,\"conflicts\":%llu,\"running\":%zu,"
                     "\"admit_p50_ms\":%.3f,\"admit_max_ms\":%.3f,\"max_ms\":{\"queue\":%.3f,\"assign_patch\":%.3f,"
-                    "\"runtime\":%.3f,\"running_patch\":%.3f},\"api_connects\":%llu,\"native\":true}",
+                    "\"runtime\":%.3f,\"running_patch\":%.3f},\"status_retries\":%llu,\"api_connects\":%llu,"
+                    "\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
                     (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
                     max_queue_ * 1e3, max_patch_ * 1e3, max_runtime_ * 1e3, max_status_ * 1e3,
-                    (unsigned long long)api_.reconnects());
+                    (unsigned long long)status_retries_.load(), (unsigned long long)api_.reconnects());
       rep.body = b;
       return rep;
     }
@@ -537,13 +540,17 @@ class Agent {
       lk.lock();
       if (!cus.empty()) cus_.at(dev_idx).release(uid);
       inflight_.erase(uid);
-      if (ok && status == 409) {
-        conflicts_++;  // stale copy: retry from the informer's latest version
-        if (!queued_.count(uid)) {
-          queued_.insert(uid);
-          delayed_.push_back({now_s() + 0.001, key});
-        }
-      } else {
+      // 409: stale copy, retry from the informer's latest version; 5xx / transport: the apiserver is
+      // unhealthy, retry with backoff (kubelet retries Allocate-time failures the same way); 4xx: give up
+      const bool retry = !ok || status == 409 || status >= 500;
+      if (ok && status == 409) conflicts_++;
+      if (retry && !queued_.count(uid)) {
+        int& n = assign_retries_[uid];
+        n++;
+        queued_.insert(uid);
+        delayed_.push_back({now_s() + std::min(0.2, 0.001 * (1 << std::min(n, 8))), key});
+      }
+      if (!retry || (ok && status >= 500)) {
         std::fprintf(stderr, "[gsx-nodeagent] ASSIGNED patch of %s failed: %s %d %s\n", key.c_str(), err.c_str(),
                      status, resp.substr(0, 200).c_str());
       }
@@ -597,7 +604,7 @@ class Agent {
       std::string st = "{\"status\":{\"phase\":\"Failed\",\"reason\":\"UnexpectedAdmissionError\",\"message\":";
       json::append_quoted(&st, why);
       st.append("}}");
-      api_.request("PATCH", path + "/status", st, "application/merge-patch+json", &status, &resp, &err);
+      patch_status(path, st);
       lk.lock();
       return;
     }
@@ -606,8 +613,7 @@ class Agent {
     allocations_[uid] = envs;
     admitted_++;
     lk.unlock();
-    api_.request("PATCH", path + "/status", "{\"status\":{\"phase\":\"Running\"}}", "application/merge-patch+json",
-                 &status, &resp, &err);
+    patch_status(path, "{\"status\":{\"phase\":\"Running\"}}");
     double tp3 = now_s();
     lk.lock();
     max_patch_ = std::max(max_patch_, tp1 - tp0);
@@ -618,10 +624,24 @@ class Agent {
     if (latency_.size() > 100000) latency_.erase(latency_.begin(), latency_.begin() + 50000);
     seen_.erase(uid);
     inflight_.erase(uid);
+    assign_retries_.erase(uid);
     // deleted while we were admitting: release now
     auto pk = pods_.find(key);
     if (pk == pods_.end() || pk->second.uid != uid || pk->second.complete) stop_pod_locked(uid);
     wake_locked();
+  }
+
+  // kubelet's status manager: a pod status update is retried until the apiserver takes it (409 / 5xx /
+  // transport errors), with capped backoff; 404 (pod gone) ends it.  mu_ not held.
+  void patch_status(const std::string& path, const std::string& body) {
+    for (int attempt = 0; attempt < 50 && !stop_flag_.load(); ++attempt) {
+      int status = 0;
+      std::string resp, err;
+      bool ok = api_.request("PATCH", path + "/status", body, "application/merge-patch+json", &status, &resp, &err);
+      if (ok && (status < 300 || status == 404 || (status >= 400 && status < 500 && status != 409))) return;
+      status_retries_.fetch_add(1);
+      std::this_thread::sleep_for(std::chrono::microseconds(std::min(100000, 500 << std::min(attempt, 8))));
+    }
   }
 
   // DELETE a pod's slice on its runtime; mu_ held on entry and exit, dropped around the call.
@@ -683,6 +703,9 @@ class Agent {
   std::vector<std::pair<double, std::string>> delayed_;
   std::deque<std::pair<std::string, int>> releases_;
   std::map<int, int> releasing_;  // per GPU: DELETEs in flight on some worker
+  std::unordered_map<std::string, int> assign_retries_;  // per pod: ASSIGNED patch attempts (backoff)
+  std::atomic<uint64_t> status_retries_{0};
+  std::atomic<bool> stop_flag_{false};
   std::vector<double> latency_;
   uint64_t admitted_ = 0, failed_ = 0, bad_ = 0, conflicts_ = 0;
   int added_ = 0;  // work items queued since the last wake_locked()

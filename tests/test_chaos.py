@@ -1,0 +1,131 @@
+"""Whole-stack fault injection: the fake apiserver answers 409 / 500 at random, drops watch streams and
+expires watch resourceVersions while pods of mixed sizes are created and deleted; afterwards every
+surviving pod must be bound, admitted and Running, no device over-committed, and the extender's ledger
+equal to what the pod annotations record (the reference's durable state, pkg/utils/pod.go:192-206)."""
+import asyncio
+import json
+import random
+import time
+
+import pytest
+
+from gpushare_scheduler_extender_amd.k8s.client import ApiError
+from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as HttpClient
+from gpushare_scheduler_extender_amd.models.profile import ALIYUN
+from gpushare_scheduler_extender_amd.sim.configs import NODE, Cluster
+
+
+async def _retry(fn, *a, tries=50, **kw):
+    for i in range(tries):
+        try:
+            return await fn(*a, **kw)
+        except ApiError as e:
+            if e.status == 409 and "already exists" in str(e):
+                return None
+            if e.status not in (409, 500) or i == tries - 1:
+                raise
+            await asyncio.sleep(0.002)
+
+
+@pytest.mark.parametrize("seed,impl", [(7, "native"), (11, "native"), (23, "native"), (7, "python")])
+def test_chaos_whole_stack_converges_without_overcommit(seed, impl):
+    async def go():
+        rnd = random.Random(seed)
+        cl = Cluster(ALIYUN, [96] * 4, gpu=False, native=impl == "native")
+        try:
+            await cl.start()
+            api = HttpClient(cl.api.url)
+            faults = {"conflict_rate": 0.15, "error_rate": 0.1, "drop_watch_after": 40, "expire_watches": 2,
+                      "seed": seed}
+            await api.request("POST", "/fake/faults", json.dumps(faults).encode())
+            sizes = [8, 16, 24, 32]
+            live, deleted = {}, set()
+            for wave in range(4):
+                names = [f"c{wave}-{i}" for i in range(10)]
+                for n in names:
+                    live[n] = rnd.choice(sizes)
+                    await _retry(cl.create, n, live[n])
+                await asyncio.sleep(0.05)
+                for n in rnd.sample(sorted(live), 4):  # delete some, bound or not
+                    await _retry(cl.c.delete, "pods", n, "default")
+                    deleted.add(n)
+                    live.pop(n)
+            await api.request("POST", "/fake/faults", json.dumps({"conflict_rate": 0, "error_rate": 0,
+                                                                  "drop_watch_after": 0}).encode())
+            # capacity 4 x 96 GiB: whatever fits is bound and Running; the rest stays Pending (never Failed)
+            deadline = time.monotonic() + 30
+            while True:
+                pods = {p["metadata"]["name"]: p for p in (await cl.c.list("pods", "default"))["items"]}
+                assert set(pods) == set(live), (sorted(set(pods) ^ set(live)))
+                bound = {n: p for n, p in pods.items() if p["spec"].get("nodeName")}
+                running = [n for n, p in bound.items() if p["status"].get("phase") == "Running"]
+                failed = [n for n, p in pods.items() if p["status"].get("phase") == "Failed"]
+                assert not failed, (failed, [ch.tail(20) for ch in cl.children if ch.name == "node-agent"])
+                used = [0] * 4
+                for p in bound.values():
+                    used[cl.device_of(p)] += int(p["metadata"]["annotations"][ALIYUN.annotation_pod])
+                assert all(u <= 96 for u in used), used
+                pending = [live[n] for n in live if n not in bound]
+                free = [96 - u for u in used]
+                settled = len(running) == len(bound) and all(s > max(free) for s in pending)
+                insp = await cl.inspect()
+                ledger = [d["usedGPU"] for d in insp["nodes"][0]["devs"]]
+                if settled and ledger == used:
+                    break
+                assert time.monotonic() < deadline, {"used": used, "ledger": ledger, "pending": pending,
+                                                     "running": len(running), "bound": len(bound)}
+                await asyncio.sleep(0.05)
+            st = json.loads((await api.request("GET", "/fake/stats")).body)
+            assert st["counts"].get("injected_conflict", 0) > 0 and st["counts"].get("injected_error", 0) > 0
+            await api.close()
+        finally:
+            await cl.close()
+    asyncio.run(go())
+
+
+async def _settled(cl, names, timeout=30.0):
+    """All ``names`` bound and Running; returns per-device GiB from the annotations of the bound pods once
+    the extender's ledger reports exactly that."""
+    deadline = time.monotonic() + timeout
+    while True:
+        pods = {p["metadata"]["name"]: p for p in (await cl.c.list("pods", "default"))["items"]}
+        ok = all(n in pods and pods[n]["status"].get("phase") == "Running" for n in names)
+        used = [0] * len(cl.totals)
+        for p in pods.values():
+            if p["spec"].get("nodeName"):
+                used[cl.device_of(p)] += int(p["metadata"]["annotations"][ALIYUN.annotation_pod])
+        try:
+            ledger = [d["usedGPU"] for d in (await cl.inspect())["nodes"][0]["devs"]]
+        except (OSError, ValueError, KeyError, IndexError):
+            ledger = None
+        if ok and ledger == used:
+            return used
+        assert time.monotonic() < deadline, {"used": used, "ledger": ledger}
+        await asyncio.sleep(0.05)
+
+
+def test_extender_crash_restart_rebuilds_ledger_from_annotations():
+    """Checkpoint / resume: the durable state is the pod annotations (pkg/utils/pod.go:192-206).  The
+    extender is SIGKILLed with pods placed, more pods arrive while it is down (kube-scheduler's filter and
+    bind calls fail and are retried), a new process on the same port rebuilds the ledger from the
+    annotations and placement resumes without over-committing a device."""
+    async def go():
+        cl = Cluster(ALIYUN, [96] * 4, gpu=False)
+        try:
+            await cl.start()
+            first = [f"a{i}" for i in range(8)]
+            for n in first:
+                await cl.create(n, 24)
+            assert await _settled(cl, first) == [96, 96, 0, 0]  # binpack: best fit fills a device first
+            cl.kill_extender()
+            second = [f"b{i}" for i in range(6)]
+            for n in second:
+                await cl.create(n, 16)
+            await asyncio.sleep(0.3)
+            pods = {p["metadata"]["name"]: p for p in (await cl.c.list("pods", "default"))["items"]}
+            assert not any(pods[n]["spec"].get("nodeName") for n in second)  # nothing binds without it
+            cl.restart_extender()
+            assert await _settled(cl, first + second) == [96, 96, 96, 0]
+        finally:
+            await cl.close()
+    asyncio.run(go())

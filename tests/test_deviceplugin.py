@@ -112,6 +112,37 @@ def test_runtime_slices_first_fit():
     assert rt.resident_bytes(0) == 224 * GIB
 
 
+def test_runtime_slices_span_holes_when_fragmented():
+    """The extender admits by free bytes per device; a fragmented arena must still hold the pod (extents)."""
+    rt = LedgerRuntime({0: 96 * GIB})
+    for n in ("a", "b", "c"):
+        rt.start(n, 0, 32 * GIB)
+    rt.stop("a")
+    rt.stop("c")
+    assert rt.start("d", 0, 48 * GIB) == 0
+    assert rt.slices[0].used["d"] == [(0, 32 * GIB), (64 * GIB, 16 * GIB)]
+    assert rt.resident_bytes(0) == 80 * GIB
+    with pytest.raises(AdmissionError):
+        rt.start("e", 0, 20 * GIB)
+    rt.stop("b")
+    assert rt.start("e", 0, 20 * GIB) == 32 * GIB and rt.resident_bytes(0) == 68 * GIB
+
+
+def test_native_pod_runtime_extents_match_python():
+    """_engine.PodRuntime (accounting only) carves the same extents: a fragmented device still admits."""
+    from gpushare_scheduler_extender_amd.core.engine import native
+
+    rt = native().PodRuntime(0, 96 * GIB)
+    for n in ("a", "b", "c"):
+        assert rt.admit(n, 32 * GIB, True) == 0
+    rt.release("a")
+    rt.release("c")
+    assert rt.admit("d", 48 * GIB, True) == 0
+    assert rt.stats()["resident_bytes"] == 80 * GIB
+    with pytest.raises(RuntimeError, match="arena exhausted"):
+        rt.admit("e", 20 * GIB, True)
+
+
 # ---------------------------------------------------------------- gRPC plugin with fake kubelet
 
 def run(coro):
@@ -168,6 +199,43 @@ def test_plugin_register_listandwatch_allocate():
             bad = [x.ID for x in nxt.devices if x.health == "Unhealthy"]
             assert sorted(bad) == sorted(plugin.ids[0])
             stream.cancel()
+            await pc.close()
+        finally:
+            await plugin.stop()
+            await kubelet.stop()
+            await client.close()
+            await api_srv.stop()
+    run(go())
+
+
+def test_plugin_allocate_retries_conflicts_and_apiserver_errors():
+    """kubelet's Allocate must not fail over transient apiserver trouble: 409s and 500s on the ASSIGNED patch
+    are retried from a fresh LIST; every pod still ends up ASSIGNED=true exactly once."""
+    async def go():
+        api_srv = await FakeApiServerRunner().start()
+        client = KubeClient(api_srv.url)
+        d = tempfile.mkdtemp(prefix="gsx-dp-")
+        kubelet = FakeKubelet(d)
+        await kubelet.start()
+        devs = fake_devices("2x16GiB")
+        await client.create("nodes", make_node("n1", 32, 0))
+        plugin = GpuSharePlugin(client, "n1", devs, P, socket_dir=d)
+        await plugin.start()
+        try:
+            await asyncio.wait_for(kubelet.registered.wait(), 5)
+            pc = PluginClient(plugin.socket_path)
+            for i in range(4):
+                await client.create("pods", bound_pod(f"p{i}", 4, dev=0, assume=10 + i, dev_total=16))
+            api_srv.server.faults.update({"conflict_rate": 0.25, "error_rate": 0.25, "seed": 5})
+            ids = fake_ids(devs[0], 16)
+            for i in range(4):
+                r = await pc.allocate([ids[4 * i: 4 * i + 4]])
+                assert dict(r.container_responses[0].envs)["SHARED_GPU_MEM_IDX"] == "0"
+            api_srv.server.faults.update({"conflict_rate": 0, "error_rate": 0})
+            for i in range(4):
+                p = await client.get("pods", f"p{i}", "default")
+                assert p["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
+            assert plugin.stats["allocate_retries"] > 0 and plugin.stats["allocate_fail"] == 0
             await pc.close()
         finally:
             await plugin.stop()

@@ -68,6 +68,28 @@ def test_hbm_admit_batched_stamp_and_verify(hip):
     s.destroy()
 
 
+def test_hbm_admit_n_multi_extent_pods(hip):
+    """A pod whose slice is two extents (fragmented arena): both stamped in one launch, every slice verified."""
+    s = hip.Stream(0)
+    buf = hip.DeviceBuffer(0, 64 << 20)
+    mib8, st = 8 << 20, 1 << 16
+    a = (buf.addr(0), mib8, 11)
+    b = (buf.addr(2 * mib8), mib8, 22)
+    assert hip.hbm_admit_n(s, [a, b], 2, st) == 0  # two pods stamped at once
+    # pod 33 lives in the holes around b: [8, 16) MiB and [24, 40) MiB
+    c = [(buf.addr(mib8), mib8, 33), (buf.addr(3 * mib8), 2 * mib8, 33)]
+    assert hip.hbm_admit_n(s, c + [a, b], 2, st) == 0
+    # stamp-only admission (verify off) does not report, the next full verify does
+    d = [(buf.addr(mib8 + mib8 // 2), mib8, 44)]  # wrongly over the second half of c[0] and first half of b
+    assert hip.hbm_admit_n(s, d, 1, st, verify=False) == 0
+    assert hip.hbm_admit_n(s, c + [a, b], 0, st) == 2 * (mib8 // 2) // st
+    # more extents than one launch's table (32)
+    many = [(buf.addr(i * (1 << 20)), 1 << 20, 500) for i in range(40)]
+    assert hip.hbm_admit_n(s, many, 40, st) == 0
+    buf.free()
+    s.destroy()
+
+
 def test_hbm_fill_pattern_and_bandwidth(hip):
     s = hip.Stream(0)
     n = 4 << 30

@@ -145,7 +145,8 @@ def test_native_controller_rewatch_and_relist_after_410():
             await e.c.create("nodes", make_node("n", 32, 2, profile=P))
             await e.start()
             # dropped streams: the reflector re-watches from its last resourceVersion, nothing is lost
-            e.api.server.faults.update({"drop_watch_after": 2})
+            # (the open stream is ended too: drop_watch_after applies to streams started after it is set)
+            await e.c.request("POST", "/fake/faults", body={"drop_watch_after": 2, "drop_watches_now": True})
             for i in range(6):
                 await e.c.create("pods", annotated(f"p{i}", 1, i % 2))
             await settle(lambda: e.used() == [3, 3])
