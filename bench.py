@@ -138,8 +138,10 @@ def pct(xs, q):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    # a 1-GPU wave takes ~0.6 ms: 300 steps keep the timed region >= ~0.2 s (at 50 steps the same binaries
+    # read 5.0k-7.0k pods/s run to run on one box, scripts/gpu_ab.sh)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--pods-per-gpu", type=int, default=4)
     ap.add_argument("--pod-gib", type=int, default=64)
     ap.add_argument("--profile", default="aliyun")
@@ -371,12 +373,16 @@ def main():
         used = sum(n["usedGPU"] for n in insp["nodes"])
         total = sum(n["totalGPU"] for n in insp["nodes"])
         per_dev = [d["usedGPU"] for n in insp["nodes"] for d in n["devs"]]
-        # teardown: one DeleteCollection for the wave (its 200 means the pods are gone from the apiserver);
-        # the step ends when the extender's ledger is empty, i.e. its informer has seen every deletion
+        # teardown: one DeleteCollection for the wave; the step ends when the extender's ledger is empty.
+        # The wait is event-driven first (the wave driver's informer sees the deletions about when the
+        # extender's does); polling /inspect straight away would pay a sleep quantum per poll instead.
         st, b = api_batch.run([("DELETE", f"/api/v1/namespaces/default/pods?labelSelector=gsx-wave%3D{step}", b"")],
                               1)[0]
         if st != 200:
             raise RuntimeError(f"delete collection failed: {st} {b[:200]!r}")
+        err = tracker.wait(keys, E.TRACK_GONE, 120)
+        if err:
+            raise RuntimeError(err)
         while sum(n["usedGPU"] for n in inspect_used()["nodes"]) != 0:
             if time.perf_counter() - t0 > 120:
                 raise TimeoutError("ledger did not drain")
