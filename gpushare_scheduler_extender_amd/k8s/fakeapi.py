@@ -193,6 +193,7 @@ class Faults:
         self.drop_watch_after = 0  # close watch streams after this many events (0 = never)
         self.expire_watches = 0  # the next N watch requests get 410 Gone (history compacted)
         self.hold_watches = False  # new watch requests wait until this is cleared
+        self.slow_bindings: dict[str, float] = {}  # pod name -> ms a binding of it takes
         self.seed = 0
         self.rng = random.Random(0)
 
@@ -200,6 +201,8 @@ class Faults:
         for k in ("conflict_rate", "error_rate", "latency_ms", "drop_watch_after", "expire_watches", "hold_watches"):
             if k in d:
                 setattr(self, k, type(getattr(self, k))(d[k]))
+        if "slow_bindings" in d:
+            self.slow_bindings = {str(k): float(v) for k, v in (d["slow_bindings"] or {}).items()}
         if "seed" in d:
             self.seed = int(d["seed"])
             self.rng = random.Random(self.seed)
@@ -222,6 +225,7 @@ class FakeApiServer:
         self.oldest_rv = 0
         self.watchers: list[_Watcher] = []
         self.faults = Faults()
+        self.binding_log: list[str] = []  # pod names in binding commit order
         self.counts = collections.Counter()
         self._grace_tasks: set[asyncio.Task] = set()
         self._last: tuple | None = None
@@ -638,8 +642,18 @@ class FakeApiServer:
 
     def h_binding(self, request):
         body = request.json()
+        delay = self.faults.slow_bindings.get(request.match_info["name"], 0.0)
+        if delay:
+            async def later():
+                await asyncio.sleep(delay / 1000.0)
+                return self._do_binding(request, body)
+            return later()
+        return self._do_binding(request, body)
+
+    def _do_binding(self, request, body):
         self._maybe_error()
         self.bind(request.match_info["ns"], request.match_info["name"], body)
+        self.binding_log.append(request.match_info["name"])
         return self._json({"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Success", "code": 201}, 201)
 
     def h_bindings(self, request):

@@ -374,6 +374,7 @@ class Engine {
     d["requests"] = s.requests.load();
     d["filters"] = s.filters.load();
     d["binds"] = s.binds.load();
+    d["bind_order_waits"] = s.bind_order_waits.load();
     d["bind_ok"] = s.bind_ok.load();
     d["bind_fail"] = s.bind_fail.load();
     d["proxied"] = s.proxied.load();

@@ -529,7 +529,8 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
     return {};
   }
   Ledger::PendingPod pp;
-  int64_t dev, dev_total = -1;
+  int64_t dev, dev_total = -1, assume_ns = 0;
+  uint64_t seq = 0;
   const Profile& prof = l_->profile();
   {
     std::lock_guard<std::mutex> g(l_->mu());
@@ -538,6 +539,14 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
       return {};
     }
     dev = l_->assume(uid, ns, name, node, pp.req, &dev_total);
+    if (dev >= 0) {
+      // ASSUME_TIME and the ordering sequence are taken in assume order, under the ledger mutex
+      std::lock_guard<std::mutex> o(order_mu_);
+      assume_ns = std::max(unix_ns(), last_assume_ns_ + 1);
+      last_assume_ns_ = assume_ns;
+      seq = ++order_seq_;
+      inflight_.push_back(InflightBind{node, pp.req, dev, seq});
+    }
   }
   if (dev < 0) {
     std::string msg;
@@ -574,11 +583,41 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
   kv(prof.a_dev, std::to_string(dev_total), false);
   kv(prof.a_pod, std::to_string(pp.req), false);
   kv(prof.a_assigned, "false", false);
-  kv(prof.a_assume, std::to_string(unix_ns()), true);
+  kv(prof.a_assume, std::to_string(assume_ns), true);
   b.append("}},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":");
   json::append_quoted(&b, node);
   b.append("}}");
   const std::string path = "/api/v1/namespaces/" + url_escape_path(ns) + "/pods/" + url_escape_path(name) + "/binding";
+  // kubelet admits a node's pods in the order their bindings land, and the device plugin gives a request
+  // of N units to the earliest-ASSUME_TIME unassigned pod of that size (docs/designs/designs.md:93-103).
+  // Two equal-size pods headed for different GPUs of one node must therefore land in ASSUME_TIME order,
+  // or each container is started with the other's GPU.  The reference got this from its node lock held
+  // across the API calls (pkg/cache/nodeinfo.go:141-189); here only such a pair waits, everything else
+  // (other nodes, other sizes, the same GPU) binds concurrently.
+  {
+    std::unique_lock<std::mutex> o(order_mu_);
+    auto blocked = [&] {
+      for (const auto& f : inflight_) {
+        if (f.seq < seq && f.node == node && f.size == pp.req && f.dev != dev) return true;
+      }
+      return false;
+    };
+    if (blocked()) {
+      stats_.bind_order_waits.fetch_add(1, std::memory_order_relaxed);
+      order_cv_.wait(o, [&] { return !blocked() || stop_.load(); });
+    }
+  }
+  struct Done {  // leave the in-flight set however the bind ends
+    NativeServer* s;
+    uint64_t seq;
+    ~Done() {
+      {
+        std::lock_guard<std::mutex> o(s->order_mu_);
+        s->inflight_.remove_if([this](const InflightBind& f) { return f.seq == seq; });
+      }
+      s->order_cv_.notify_all();
+    }
+  } done{this, seq};
   std::string msg;
   bool ok = false;
   for (int attempt = 0; attempt < 3; ++attempt) {

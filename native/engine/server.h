@@ -27,6 +27,7 @@
 #include <cstdint>
 #include <deque>
 #include <functional>
+#include <list>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -70,7 +71,7 @@ struct LatencyHist {
 
 struct ServerStats {
   std::atomic<uint64_t> requests{0}, filters{0}, binds{0}, bind_ok{0}, bind_fail{0}, proxied{0}, bad_requests{0},
-      inspects{0}, connections{0}, api_calls{0}, conflicts_retried{0};
+      inspects{0}, connections{0}, api_calls{0}, conflicts_retried{0}, bind_order_waits{0};
   LatencyHist filter_lat, bind_lat, api_lat;
 };
 
@@ -131,6 +132,18 @@ class NativeServer {
   std::mutex fmu_;
   std::vector<BindFailure> failures_;
   ServerStats stats_;
+  // Binds in flight (see do_bind: equal-size pods bound to one node on different GPUs reach the
+  // apiserver in ASSUME_TIME order).  order_mu_ nests inside the ledger mutex, never around it.
+  struct InflightBind {
+    std::string node;
+    int64_t size, dev;
+    uint64_t seq;
+  };
+  std::mutex order_mu_;
+  std::condition_variable order_cv_;
+  std::list<InflightBind> inflight_;
+  uint64_t order_seq_ = 0;
+  int64_t last_assume_ns_ = 0;
 };
 
 }  // namespace gsx

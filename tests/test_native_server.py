@@ -4,6 +4,8 @@ import json
 import socket
 import threading
 
+import pytest
+
 from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient
 from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
@@ -159,6 +161,55 @@ def test_native_bind_failure_becomes_event():
                     break
                 await asyncio.sleep(0.05)
             assert evs and evs[0]["reason"] == "FailedBinding" and evs[0]["type"] == "Warning"
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())
+
+
+@pytest.mark.parametrize("native", [True, False], ids=["native-bind", "python-bind"])
+def test_equal_size_binds_for_different_gpus_land_in_assume_order(native):
+    """kubelet admits pods in binding order and the device plugin serves a request of N units with the
+    earliest-ASSUME_TIME pod of that size: two equal-size pods bound to different GPUs of one node must
+    commit in ASSUME_TIME order even when the first binding is slow; other binds do not wait."""
+    async def go():
+        import aiohttp
+
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 2 * 16, 2))
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=native, http_threads=2).start()
+        try:
+            pods = {}
+            for name, mem in (("a", 10), ("b", 10), ("x", 6), ("y", 5)):
+                pods[name] = await c.create("pods", make_pod(name, mem))
+            for _ in range(300):
+                if ext.server.engine.has_node("n") and ext.server.controller.get_pod("y", "default"):
+                    break
+                await asyncio.sleep(0.01)
+            async with aiohttp.ClientSession() as s:
+                async def bind(name):
+                    p = pods[name]
+                    async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(p, ["n"])) as r:
+                        assert json.loads(await r.read())["NodeNames"] == ["n"]
+                    async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
+                            name, "default", p["metadata"]["uid"], "n").encode()) as r:
+                        assert r.status == 200, await r.read()
+
+                # a (10 GiB) -> GPU0, b (10 GiB) -> GPU1; a's binding takes 300 ms: b must wait for it
+                api.server.faults.slow_bindings = {"a": 300.0, "x": 300.0}
+                ta = asyncio.create_task(bind("a"))
+                await asyncio.sleep(0.05)
+                await asyncio.gather(ta, bind("b"))
+                # x (6 GiB) -> GPU0, y (5 GiB) -> GPU1: different sizes, y does not wait for slow x
+                tx = asyncio.create_task(bind("x"))
+                await asyncio.sleep(0.05)
+                await asyncio.gather(tx, bind("y"))
+            assert api.server.binding_log == ["a", "b", "y", "x"]
+            got = {n: (await c.get("pods", n, "default"))["metadata"]["annotations"] for n in pods}
+            assert [got[n]["SHARED_GPU_MEM_IDX"] for n in ("a", "b", "x", "y")] == ["0", "1", "0", "1"]
+            assert int(got["a"]["SHARED_GPU_MEM_ASSUME_TIME"]) < int(got["b"]["SHARED_GPU_MEM_ASSUME_TIME"])
+            if native:
+                assert ext.server.engine.server_stats()["bind_order_waits"] == 1
         finally:
             await _teardown(api, c, ext)
     asyncio.run(go())
