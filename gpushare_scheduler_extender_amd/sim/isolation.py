@@ -10,7 +10,8 @@ exact environment the device plugin's Allocate produces, in four scenarios:
 * ``shared``        4 pods co-resident, no partition (time-sliced, unisolated);
 * ``partitioned``   4 pods co-resident, 64 CUs each via the stream CU mask;
 * ``env``           4 pods co-resident, 64 CUs each via ``HSA_CU_MASK`` only
-                    (process-wide; applies to torch's own queues too);
+                    (process-wide; applies to torch's own queues too), hipBLASLt GEMM;
+* ``env-gsx``       the same with the libgsx_kernels GEMM (stream mask vs process mask, same kernel);
 * ``solo64``        one pod alone inside a 64-CU partition (what a partition is worth);
 * ``noisy`` / ``noisy-partitioned``  pod 0 runs a small (latency-bound) GEMM
                     next to 3 pods running large GEMMs, without / with
@@ -95,7 +96,8 @@ def main(argv=None) -> int:
     ap.add_argument("--kernel", default="gsx", choices=["gsx", "torch"])
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--small-size", type=int, default=2048)
-    ap.add_argument("--scenarios", default="solo,shared,partitioned,env,solo-small,solo64,noisy,noisy-partitioned")
+    ap.add_argument("--scenarios",
+                    default="solo,shared,partitioned,env,env-gsx,solo-small,solo64,noisy,noisy-partitioned")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args(argv)
     results = []
@@ -123,6 +125,9 @@ def main(argv=None) -> int:
         elif sc == "env":
             envs = pod_envs(a.pods, a.cus, a.gpu_gib, a.pod_gib, True)
             res = run_pods(envs, a.seconds, "torch" if a.kernel == "gsx" else a.kernel, a.size, "env")
+        elif sc == "env-gsx":
+            envs = pod_envs(a.pods, a.cus, a.gpu_gib, a.pod_gib, True)
+            res = run_pods(envs, a.seconds, a.kernel, a.size, "env")
         else:
             raise SystemExit(f"unknown scenario {sc}")
         s = summarize(sc, res)
