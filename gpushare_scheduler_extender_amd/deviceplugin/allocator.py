@@ -147,6 +147,10 @@ def build_response(pod: dict, device: Device, container_units: int, profile: Nam
     dev_total = int(podutil.annotations(pod).get(profile.annotation_dev, "0") or 0)
     pod_mem = podutil.gpu_mem_request(pod, profile)
     visible = "0" if mount_mode == "isolated" else str(idx)
+    frac = (container_units / dev_total) if dev_total else 0.0
+    if device.share_bytes and device.total_bytes > device.share_bytes:
+        # a partition that shares its HBM pool sees the whole pool as device memory: scale to the pool
+        frac *= device.share_bytes / device.total_bytes
     envs = {
         "HIP_VISIBLE_DEVICES": visible,
         "ROCR_VISIBLE_DEVICES": visible,
@@ -154,7 +158,7 @@ def build_response(pod: dict, device: Device, container_units: int, profile: Nam
         profile.annotation_dev: str(dev_total),
         profile.annotation_pod: str(pod_mem),
         profile.env_container: str(container_units),
-        "GSX_GPU_MEM_FRACTION": f"{(container_units / dev_total) if dev_total else 0.0:.6f}",
+        "GSX_GPU_MEM_FRACTION": f"{frac:.6f}",
         "GSX_GPU_BDF": device.bdf,
     }
     ann = {}

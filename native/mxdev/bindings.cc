@@ -25,6 +25,9 @@ py::dict to_dict(const mxdev::DeviceRec& r) {
   d["card_minor"] = r.card_minor;
   d["kfd_id"] = r.kfd_id;
   d["partition"] = r.partition;
+  d["memory_partition"] = r.memory_partition;
+  d["partition_id"] = r.partition_id;
+  d["pool"] = r.pool;
   d["healthy"] = r.healthy;
   d["numa_node"] = r.numa_node;
   py::dict links;

@@ -194,7 +194,10 @@ class AmdSmi : public Backend {
       if (api_.kfd) {
         amdsmi_kfd_info_t k;
         std::memset(&k, 0, sizeof(k));
-        if (api_.kfd(p, &k) == AMDSMI_STATUS_SUCCESS && k.kfd_id != ~0ull) r.kfd_id = static_cast<int64_t>(k.kfd_id);
+        if (api_.kfd(p, &k) == AMDSMI_STATUS_SUCCESS) {
+          if (k.kfd_id != ~0ull) r.kfd_id = static_cast<int64_t>(k.kfd_id);
+          if (k.current_partition_id != 0xFFFFFFFFu) r.partition_id = static_cast<int>(k.current_partition_id);
+        }
       }
       if (api_.cpart) {
         char buf[64] = {0};
@@ -204,6 +207,9 @@ class AmdSmi : public Backend {
         char buf[64] = {0};
         if (api_.mpart(p, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) r.memory_partition = buf;
       }
+      r.xcc_count = xcds_for_partition(r.partition);
+      // partitions of one GPU differ only in the PCI function number
+      r.pool = r.bdf.size() > 2 ? r.bdf.substr(0, r.bdf.size() - 2) : r.bdf;
       if (api_.numa) {
         uint32_t nn = 0;
         if (api_.numa(p, &nn) == AMDSMI_STATUS_SUCCESS) r.numa_node = static_cast<int>(nn);
@@ -356,8 +362,18 @@ class Fake : public Backend {
 
 }  // namespace
 
+int partitions_for_mode(const std::string& mode) {
+  if (mode == "CPX") return 8;
+  if (mode == "QPX") return 4;
+  if (mode == "DPX") return 2;
+  return 1;  // SPX / unknown
+}
+
+int xcds_for_partition(const std::string& mode) { return 8 / partitions_for_mode(mode); }
+
 bool fake_spec(const std::string& spec, std::vector<DeviceRec>* out, std::string* err) {
-  static const std::regex re(R"(^(\d+)x(\d+(?:\.\d+)?)(GB|GiB|MiB|MB)$)");
+  static const std::regex re(
+      R"(^(\d+)x(\d+(?:\.\d+)?)(GB|GiB|MiB|MB)(?::(SPX|DPX|QPX|CPX))?(?::NPS(1|2|4|8))?$)");
   std::smatch m;
   if (!std::regex_match(spec, m, re)) {
     *err = "fake spec must look like 8x288GB, got '" + spec + "'";
@@ -371,24 +387,46 @@ bool fake_spec(const std::string& spec, std::vector<DeviceRec>* out, std::string
     *err = "fake device count out of range";
     return false;
   }
+  const std::string mode = m[4].matched ? m[4].str() : "SPX";
+  const int nps = m[5].matched ? std::stoi(m[5].str()) : 1;
+  const int parts = partitions_for_mode(mode);
+  if (nps > parts) {
+    *err = "NPS" + std::to_string(nps) + " needs at least as many compute partitions (" + mode + ")";
+    return false;
+  }
+  const int total = n * parts;
+  if (total > 64) {
+    *err = "fake logical device count out of range";
+    return false;
+  }
   out->clear();
-  for (int i = 0; i < n; ++i) {
-    DeviceRec r;
-    r.index = i;
-    r.name = "AMD Instinct MI355X";
-    char bdf[32];
-    std::snprintf(bdf, sizeof(bdf), "0000:%02x:00.0", 0x05 + 0x10 * i);
-    r.bdf = bdf;
-    r.uuid = "fake-" + std::to_string(i);
-    r.total_bytes = static_cast<uint64_t>(std::llround(size * mult));
-    r.cu_count = 256;
-    r.render_minor = 128 + 8 * i;
-    r.card_minor = i + 1;
-    r.kfd_id = i;
-    r.hsa_id = i + 1;
-    r.link_types.assign(static_cast<size_t>(n), "XGMI");
-    r.link_types[static_cast<size_t>(i)] = "SELF";
-    out->push_back(r);
+  // each logical device reports the VRAM of its memory pool (the whole GPU in NPS1)
+  const uint64_t pool_bytes = static_cast<uint64_t>(std::llround(size * mult)) / static_cast<uint64_t>(nps);
+  for (int g = 0; g < n; ++g) {
+    for (int p = 0; p < parts; ++p) {
+      const int i = g * parts + p;
+      DeviceRec r;
+      r.index = i;
+      r.name = "AMD Instinct MI355X";
+      char bdf[32];
+      std::snprintf(bdf, sizeof(bdf), "0000:%02x:00.%d", 0x05 + 0x10 * g, p);
+      r.bdf = bdf;
+      r.pool = r.bdf.substr(0, r.bdf.size() - 2);
+      r.uuid = "fake-" + std::to_string(i);
+      r.total_bytes = pool_bytes;
+      r.cu_count = 256 / parts;
+      r.xcc_count = 8 / parts;
+      r.partition = mode;
+      r.memory_partition = "NPS" + std::to_string(nps);
+      r.partition_id = p;
+      r.render_minor = parts == 1 ? 128 + 8 * i : 128 + i;
+      r.card_minor = i + 1;
+      r.kfd_id = i;
+      r.hsa_id = i + 1;
+      r.link_types.assign(static_cast<size_t>(total), "XGMI");
+      r.link_types[static_cast<size_t>(i)] = "SELF";
+      out->push_back(r);
+    }
   }
   return true;
 }

@@ -33,7 +33,9 @@ struct DeviceRec {
   int64_t kfd_id = -1;
   int hsa_id = -1;
   std::string partition = "SPX";
-  std::string memory_partition;
+  std::string memory_partition;  // NPS1 / NPS2 / NPS4 / NPS8 (memory pools per physical GPU)
+  int partition_id = 0;          // compute-partition index on its physical GPU (KFD current_partition_id)
+  std::string pool;              // physical GPU key (BDF without the function): partitions of one GPU share it
   bool healthy = true;
   uint64_t ecc_uncorrectable = 0;
   uint64_t ecc_correctable = 0;
@@ -64,7 +66,14 @@ class Backend {
 // "amdsmi", "fake:<spec>", or "auto" (amdsmi, error if unavailable).
 Backend* make_backend(const std::string& kind, std::string* err);
 
-// Parse "NxSIZE{GB,GiB,MiB,MB}" into fake device records.
+// Parse "NxSIZE{GB,GiB,MiB,MB}[:SPX|DPX|QPX|CPX[:NPS1|NPS2|NPS4|NPS8]]" into fake device records.
+// With a compute-partition mode every physical GPU appears as 1/2/4/8 logical devices (function number =
+// partition id), each reporting the VRAM of the memory pool it sits in, as KFD does.
+// XCDs per logical device on MI355X (8 XCDs per physical GPU) for a compute-partition mode.
+int xcds_for_partition(const std::string& mode);
+// Logical devices per physical GPU for a compute-partition mode.
+int partitions_for_mode(const std::string& mode);
+
 bool fake_spec(const std::string& spec, std::vector<DeviceRec>* out, std::string* err);
 
 }  // namespace mxdev

@@ -101,6 +101,65 @@ def test_native_mxdev_fake_backend_matches_python():
         mxdev.native().Session("fake:nonsense")
 
 
+@pytest.mark.parametrize("spec", ["2x288GB:CPX:NPS1", "2x288GB:CPX:NPS2", "1x288GB:DPX", "1x288GB:QPX:NPS4"])
+def test_native_mxdev_partition_spec_matches_python(spec):
+    from gpushare_scheduler_extender_amd.ops import mxdev
+
+    nat = [Device(**r) for r in mxdev.enumerate_devices("fake:" + spec)]
+    py = fake_devices(spec)
+    key = lambda d: (d.index, d.bdf, d.pool, d.total_bytes, d.cu_count, d.xcc_count, d.partition,  # noqa: E731
+                     d.memory_partition, d.partition_id, d.render_minor)
+    assert [key(d) for d in nat] == [key(d) for d in py]
+    with pytest.raises(RuntimeError):
+        mxdev.native().Session("fake:1x288GB:SPX:NPS2")  # more memory pools than compute partitions
+
+
+def test_memory_pools_split_shared_hbm(monkeypatch):
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import apply_memory_pools
+
+    # CPX / NPS1: 8 partitions per GPU, each reporting the whole 288 GB pool
+    devs = apply_memory_pools(fake_devices("2x288GB:CPX:NPS1"))
+    assert len(devs) == 16 and all(d.total_bytes == 288 * 10**9 for d in devs)
+    assert all(d.cu_count == 32 and d.xcc_count == 1 for d in devs)
+    assert sum(d.usable_bytes for d in devs) == 2 * 288 * 10**9  # the pool is advertised once
+    assert {d.usable_bytes for d in devs} == {36 * 10**9}
+    # CPX / NPS2: two 144 GB pools per GPU, four partitions each
+    d2 = apply_memory_pools(fake_devices("1x288GB:CPX:NPS2"))
+    assert sum(d.usable_bytes for d in d2) == 288 * 10**9 and {d.usable_bytes for d in d2} == {36 * 10**9}
+    # QPX / NPS4: one pool per partition, nothing to split; SPX untouched
+    assert all(d.share_bytes == 0 for d in apply_memory_pools(fake_devices("1x288GB:QPX:NPS4")))
+    assert all(d.share_bytes == 0 for d in apply_memory_pools(fake_devices("8x288GB")))
+    # uneven pool: the remainder goes to the lowest partition ids
+    odd = fake_devices("1x288GB:DPX")
+    for d in odd:
+        d.total_bytes = 101
+    assert [d.usable_bytes for d in apply_memory_pools(odd)] == [51, 50]
+    # off: raw totals (a driver that already reports per-partition VRAM)
+    assert all(d.share_bytes == 0 for d in apply_memory_pools(fake_devices("1x288GB:CPX"), "off"))
+    monkeypatch.setenv("GSX_FAKE_DEVICES", "1x288GB:CPX:NPS1")
+    _, d3 = discover()
+    assert sum(d.units("GiB") for d in d3) == 8 * (36 * 10**9 // 2**30)
+
+
+def test_partitioned_device_plugin_advertises_pool_once_and_scales_fraction():
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import apply_memory_pools
+
+    devs = apply_memory_pools(fake_devices("1x288GB:CPX:NPS1"))
+    plugin = GpuSharePlugin(None, "n1", devs, P)
+    assert sum(plugin.units.values()) == 8 * 33 and len(plugin.device_list()) == 8 * 33
+    dev = devs[5]
+    r = build_response(bound_pod("p", 16, dev=5, dev_total=33), dev, 16, P)
+    # the partition's process sees the whole 288 GB pool: 16 of its 33 GiB is 16/33 * 36/288 of that
+    assert abs(float(r.envs["GSX_GPU_MEM_FRACTION"]) - (16 / 33) * (36 / 288)) < 1e-6
+    assert r.envs["SHARED_GPU_MEM_DEV"] == "33"
+    # CU masks stay inside the partition's one XCD
+    cp = CUPartitioner(dev.cu_count, dev.xcc_count)
+    a = cp.allocate("a", 16)
+    assert len(a) == 16 and all(0 <= c < 32 for c in a)
+    with pytest.raises(Exception):
+        cp.allocate("b", 17)
+
+
 def test_runtime_slices_first_fit():
     rt = LedgerRuntime({0: 256 * GIB})
     offs = [rt.start(f"p{i}", 0, 64 * GIB) for i in range(4)]

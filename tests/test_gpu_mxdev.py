@@ -49,6 +49,26 @@ def test_amdsmi_inventory_matches_hip():
         assert d["render_minor"] >= 128 and os.path.exists(f"/dev/dri/renderD{d['render_minor']}"), d
         assert d["partition"] in ("SPX", "DPX", "QPX", "CPX", "UNKNOWN", ""), d
         assert d["links"].get(d["index"]) in ("SELF", None), d["links"]
+        assert d["pool"] and d["bdf"].startswith(d["pool"]), d
+        print("memory partition:", d["memory_partition"], "partition id:", d["partition_id"])
+
+
+def test_amdsmi_discover_memory_pools():
+    """Logical devices of one physical GPU advertise its HBM once (SPX on the box: one device per pool)."""
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import discover
+
+    backend, devs = discover("amdsmi")
+    assert backend == "amdsmi"
+    pools = {}
+    for d in devs:
+        pools.setdefault(d.pool, []).append(d)
+    for members in pools.values():
+        if len(members) == 1:
+            assert members[0].share_bytes == 0 and members[0].usable_bytes == members[0].total_bytes
+        else:  # a partitioned GPU: the shares never add up to more than the GPU's memory
+            nps = members[0].memory_partition
+            n_pools = int(nps[3:]) if nps.startswith("NPS") else 1
+            assert sum(d.usable_bytes for d in members) <= n_pools * max(d.total_bytes for d in members)
 
 
 def test_amdsmi_health_counters_readable():
