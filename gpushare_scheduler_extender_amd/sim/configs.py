@@ -1,4 +1,4 @@
-"""The five BASELINE.json configurations, end to end through the whole stack.
+"""The five BASELINE.json configurations (plus hardware partitions), end to end through the whole stack.
 
     python -m gpushare_scheduler_extender_amd.sim.configs [--gpu] [--json-out F] [--only 1,4]
 
@@ -17,7 +17,11 @@ process), registers one node, creates pods and checks where they land:
 5. CU-mask isolation (MPS stand-in): 4 pods x 64 GiB with ``gpushare.amd.com/cu-count: 64`` on one
    device -> disjoint 64-CU partitions, 8 CUs on each of the 8 XCDs.  With ``--gpu`` each pod's
    partition is also checked on the MI355X: a CU-masked stream runs the CU probe kernel and the
-   hardware CU ids it records must be 64 per pod and disjoint across pods.
+   hardware CU ids it records must be 64 per pod and disjoint across pods;
+6. hardware partitions (CPX / NPS1): one MI355X as 8 logical devices sharing one HBM pool.  Each
+   advertises its share of the pool (``deviceplugin/devices.py: apply_memory_pools``), not the whole
+   pool 8 times; a 64 GiB request that fits the node but no partition is filtered; 8 x 32 GiB pods
+   land one per partition.
 
 ``--gpu``: device sizes come from the real MI355X (devices beyond the box's GPUs are fakes of the
 same size) and configs 2 and 5 use a real HBM arena on GPU 0 (each pod's slice stamped and every
@@ -86,7 +90,7 @@ class Cluster:
     """apiserver + extender + scheduler + node agent (child processes) and one node with ``len(totals)`` devices."""
 
     def __init__(self, profile: NamingProfile, totals: list[int], gpu: bool, cu_count: int = 256,
-                 native: bool = True):
+                 native: bool = True, partition: str = "SPX"):
         self.profile = profile
         self.totals = totals
         self.children = []
@@ -99,11 +103,12 @@ class Cluster:
         self.children.append(start_node_agent(self.api.url, NODE, profile=profile.name, native=native))
         self.rt = Runtimes(len(totals), GIB, max(totals), gpu)
         self.cu_count = cu_count
+        self.partition = partition
 
     async def start(self):
         self.c = KubeClient(self.api.url)
         inv = [{"index": i, "bdf": f"0000:{0x10 + i:02x}:00.0", "uuid": f"gpu-{i}", "units": t, "total_bytes": t * GIB,
-                "cu": self.cu_count, "render": 128 + i, "card": i, "partition": "SPX"} for i, t in enumerate(self.totals)]
+                "cu": self.cu_count, "render": 128 + i, "card": i, "partition": self.partition} for i, t in enumerate(self.totals)]
         node = make_node(NODE, sum(self.totals), len(self.totals), profile=self.profile, device_totals=self.totals,
                          annotations={NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv),
                                       NODE_RUNTIME_ENDPOINTS_ANNOTATION: json.dumps(
@@ -321,12 +326,40 @@ async def config5(gpu: bool) -> dict:
         await cl.close()
 
 
+async def config6(gpu: bool) -> dict:
+    from ..deviceplugin.devices import apply_memory_pools, fake_devices
+
+    total = _gpu_gib() if gpu else 268
+    devs = apply_memory_pools(fake_devices(f"1x{total}GiB:CPX:NPS1"), "auto")
+    shares = [d.units("GiB") for d in devs]
+    raw = [d.total_bytes // GIB for d in devs]
+    cl = Cluster(ALIYUN, shares, gpu=False, cu_count=devs[0].cu_count, partition="CPX")
+    try:
+        await cl.start()
+        f = await cl.filter(make_pod("req-64", 64, profile=ALIYUN))
+        reason = (f.get("FailedNodes") or {}).get(NODE, "")
+        names = [f"cpx-{i}" for i in range(8)]
+        await asyncio.gather(*(cl.create(n, 32) for n in names))
+        pods = await cl.wait(names)
+        placed = sorted(cl.device_of(p) for p in pods.values())
+        insp = await cl.inspect()
+        used, node_total = insp["nodes"][0]["usedGPU"], insp["nodes"][0]["totalGPU"]
+        ok = (len(devs) == 8 and sum(shares) <= total and f["NodeNames"] == []
+              and reason == "Insufficient GPU Memory in one device" and placed == list(range(8)) and used == 256)
+        return {"ok": ok, "gpu_gib": total, "logical_devices": len(devs), "reported_gib_per_partition": raw[0],
+                "advertised_gib_per_partition": shares, "node_gpu_mem": node_total, "cus_per_partition": devs[0].cu_count,
+                "req64_filtered": reason, "placed_devices": placed, "used_gib": used}
+    finally:
+        await cl.close()
+
+
 CONFIGS = {
     1: ("kind cluster + fake device plugin: 2 pods binpack onto one fake device", config1),
     2: ("1xMI355X: 4 pods x 64 GiB binpacked onto the single 288 GB device", config2),
     3: ("8xMI355X: 32 pods x 64 GiB, binpack-first across all 8 devices", config3),
     4: ("fragmentation guard: 200/100/50 GiB requests that fit the node total but no single device", config4),
     5: ("CU-mask isolation: 4 pods co-resident on one MI355X with per-pod CU partitions", config5),
+    6: ("hardware partitions: one MI355X in CPX/NPS1 as 8 logical devices sharing one HBM pool", config6),
 }
 
 
