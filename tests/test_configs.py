@@ -1,4 +1,4 @@
-"""BASELINE.json configurations 1-5 through the whole stack (sim/configs.py): CPU plumbing and, on MI355X,
+"""BASELINE.json configurations 1-5 and the hardware-partition scenario (6) through the whole stack (sim/configs.py): CPU plumbing and, on MI355X,
 real device sizes, the HBM arena and hardware-verified CU partitions."""
 import pytest
 
