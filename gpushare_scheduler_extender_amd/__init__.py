@@ -9,7 +9,7 @@ bnulwh/gpushare-scheduler-extender:
 * ``deviceplugin`` kubelet device plugin (v1beta1 gRPC) handing out /dev/kfd + /dev/dri render nodes
 * ``ops``          amdsmi device library, HIP/CDNA4 kernels (CU probe, HBM touch, MFMA GEMM), CU masks
 * ``models``       wire types, naming profiles, pod/node accessors, quantities
-* ``parallel``     workqueue / rate limiting / keyed locks / multi-rank coordination
+* ``parallel``     client-go-style rate-limited work queue (dedup, per-item backoff, bucket limiter)
 * ``sim``          kube-scheduler protocol simulator used by tests and bench.py
 * ``cli``          ``kubectl inspect gpushare`` equivalent
 """

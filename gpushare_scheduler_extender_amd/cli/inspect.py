@@ -1,6 +1,8 @@
 """``kubectl inspect gpushare`` equivalent (the upstream CLI ships with the device plugin, not the reference).
 
-Output format from ``docs/userguide.md:9-19`` and ``demo1.jpg`` / ``demo2.jpg``:
+Two output styles, both reproduced byte for byte (Go ``text/tabwriter``, padding 2):
+
+* ``userguide`` (``docs/userguide.md:9-19``; default for GiB)::
 
     NAME     IPADDRESS     GPU0(Allocated/Total)  GPU Memory(GiB)
     node-a   192.168.0.71  6/15                   6/15
@@ -8,7 +10,18 @@ Output format from ``docs/userguide.md:9-19`` and ``demo1.jpg`` / ``demo2.jpg``:
     Allocated/Total GPU Memory In Cluster:
     9/30 (30%)
 
-``-d`` prints one block per node with a row per pod and a column per GPU.
+* ``demo`` (``demo1.jpg``; default for MiB)::
+
+    NAME  IPADDRESS  GPU0(Request MiB/Total MiB)  GPU1(Request MiB/Total MiB)  GPU Memory
+    ...
+
+``-d`` prints the ``demo2.jpg`` layout: a ``NAME:`` / ``IPADDRESS:`` block per
+node, then one table holding ``NAME NAMESPACE GPU<i>(Request <unit>)``, a row
+per pod, ``Allocated GPU Memory In Node <n>:  x (p%)`` and ``Total GPU Memory
+In Node <n>:  y`` (one tabwriter block, so the node lines set the first
+column's width, as in the screenshot), the dashed rule, and after all nodes
+``Allocated/Total GPU Memory In Cluster:  a/t (p%)``.
+
 Data comes from the apiserver (nodes + pods, like the upstream plugin) or,
 with ``--extender URL``, from the extender's ``/gpushare-scheduler/inspect``.
 Install as ``kubectl-inspect-gpushare`` on PATH to get the kubectl plugin
@@ -25,7 +38,8 @@ from dataclasses import dataclass, field
 from ..models import pod as podutil
 from ..models.profile import NamingProfile, get_profile
 
-DASH = "-" * 78
+DASH = "-" * 78  # docs/userguide.md:14
+DEMO_DASH = "-" * 95  # demo1.jpg / demo2.jpg rule
 
 
 @dataclass
@@ -101,9 +115,20 @@ def views_from_inspect(doc: dict, addresses: dict[str, str] | None = None) -> li
     return out
 
 
-def render_summary(views: list[NodeView], unit: str = "GiB") -> str:
+def default_style(unit: str) -> str:
+    return "demo" if unit == "MiB" else "userguide"
+
+
+def render_summary(views: list[NodeView], unit: str = "GiB", style: str | None = None) -> str:
+    style = style or default_style(unit)
     ndev = max((len(v.totals) for v in views), default=0)
-    header = ["NAME", "IPADDRESS"] + [f"GPU{i}(Allocated/Total)" for i in range(ndev)] + [f"GPU Memory({unit})"]
+    if style == "demo":  # demo1.jpg
+        header = (["NAME", "IPADDRESS"] + [f"GPU{i}(Request {unit}/Total {unit})" for i in range(ndev)]
+                  + ["GPU Memory"])
+        dash = DEMO_DASH
+    else:  # docs/userguide.md:11
+        header = ["NAME", "IPADDRESS"] + [f"GPU{i}(Allocated/Total)" for i in range(ndev)] + [f"GPU Memory({unit})"]
+        dash = DASH
     rows = [header]
     for v in views:
         cells = [v.name, v.address]
@@ -113,25 +138,29 @@ def render_summary(views: list[NodeView], unit: str = "GiB") -> str:
         rows.append(cells)
     a = sum(v.allocated for v in views)
     t = sum(v.total for v in views)
-    return "\n".join([tabwrite(rows), DASH, "Allocated/Total GPU Memory In Cluster:", f"{a}/{t} ({pct(a, t)}%)"]) + "\n"
+    return "\n".join([tabwrite(rows), dash, "Allocated/Total GPU Memory In Cluster:", f"{a}/{t} ({pct(a, t)}%)"]) + "\n"
 
 
 def render_details(views: list[NodeView], unit: str = "GiB") -> str:
-    blocks = []
+    """``demo2.jpg``: per-node block, then the cluster line two blank lines below the last rule."""
+    out = []
     for v in views:
-        lines = [tabwrite([["NAME:", v.name], ["IPADDRESS:", v.address]]), ""]
-        rows = [["NAME", "NAMESPACE"] + [f"GPU{i}(Allocated)" for i in range(len(v.totals))]]
+        out.append("")
+        out.append(tabwrite([["NAME:", v.name], ["IPADDRESS:", v.address]]))
+        out.append("")
+        ndev = len(v.totals)
+        # one tabwriter block: pod rows and the two node lines share column widths (tab-terminated cells)
+        rows = [["NAME", "NAMESPACE"] + [f"GPU{i}(Request {unit})" for i in range(ndev)] + [""]]
         for name, ns, dev, mem in sorted(v.pods, key=lambda x: (x[1], x[0])):
-            rows.append([name, ns] + [str(mem) if i == dev else "0" for i in range(len(v.totals))])
-        lines.append(tabwrite(rows))
-        lines.append(tabwrite([["Allocated :", f"{v.allocated} ({pct(v.allocated, v.total)}%)"],
-                               ["Total :", f"{v.total}"]]))
-        lines.append(DASH)
-        blocks.append("\n".join(lines))
+            rows.append([name, ns] + [str(mem) if i == dev else "0" for i in range(ndev)] + [""])
+        rows.append([f"Allocated GPU Memory In Node {v.name}:", f"{v.allocated} ({pct(v.allocated, v.total)}%)", ""])
+        rows.append([f"Total GPU Memory In Node {v.name}:", f"{v.total}", ""])
+        out.append(tabwrite(rows))
+        out.append(DEMO_DASH)
     a = sum(v.allocated for v in views)
     t = sum(v.total for v in views)
-    blocks.append(f"\nAllocated/Total GPU Memory In Cluster:  {a}/{t} ({pct(a, t)}%)")
-    return "\n".join(blocks) + "\n"
+    out += ["", "", tabwrite([["Allocated/Total GPU Memory In Cluster:", f"{a}/{t} ({pct(a, t)}%)", ""]])]
+    return "\n".join(out) + "\n"
 
 
 async def collect(args) -> list[NodeView]:
@@ -165,6 +194,8 @@ def main(argv=None) -> int:
     ap.add_argument("-d", "--details", action="store_true")
     ap.add_argument("--profile", default="shared-gpu")
     ap.add_argument("--unit", default="GiB")
+    ap.add_argument("--style", default=None, choices=["userguide", "demo"],
+                    help="summary header: docs/userguide.md (default for GiB) or demo1.jpg (default for MiB)")
     ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("--apiserver", default=None)
     ap.add_argument("--extender", default=None, help="read the extender's /gpushare-scheduler/inspect instead")
@@ -176,7 +207,7 @@ def main(argv=None) -> int:
     elif a.details:
         sys.stdout.write(render_details(views, a.unit))
     else:
-        sys.stdout.write(render_summary(views, a.unit))
+        sys.stdout.write(render_summary(views, a.unit, a.style))
     return 0
 
 

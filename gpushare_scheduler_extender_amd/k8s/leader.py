@@ -15,6 +15,13 @@ renewing, measured on the *local* clock from when we last saw the record
 change (clock skew between replicas does not matter).  A leader that cannot
 renew within ``renew_deadline`` steps down.  All writes use the Lease's
 resourceVersion, so two candidates can never both win.
+
+Step-down is bounded like client-go's shared ``RenewDeadline`` context: a
+renewal counts from the moment its attempt *started*, every attempt by the
+leader is cut off at ``last_renew + renew_deadline`` (a hanging apiserver
+call cannot stretch it), and the retry sleep never runs past that deadline.
+So the old leader stops binding within ``renew_deadline`` of its last good
+renewal, before a standby can take over (``lease_duration`` > ``renew_deadline``).
 """
 from __future__ import annotations
 
@@ -70,6 +77,7 @@ class LeaderElector:
         return {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease", "metadata": md, "spec": spec}
 
     async def try_acquire_or_renew(self) -> bool:
+        t0 = time.monotonic()  # a successful write happened after this: the conservative renewal time
         try:
             cur = await self.client.get("leases", self.name, self.namespace)
         except ApiError as e:
@@ -81,7 +89,7 @@ class LeaderElector:
                 if e2.status == 409:
                     return False
                 raise
-            self._last_renew = time.monotonic()
+            self._last_renew = t0
             return True
         spec = cur.get("spec") or {}
         holder = spec.get("holderIdentity") or ""
@@ -98,16 +106,32 @@ class LeaderElector:
             if e.conflict:
                 return False
             raise
-        self._last_renew = now
+        self._last_renew = t0
         return True
+
+    def _deadline_left(self) -> float:
+        return self._last_renew + self.renew_deadline - time.monotonic()
+
+    def _step_down(self):
+        if self.is_leader:
+            self.is_leader = False
+            log.warning("%s lost leadership of %s/%s", self.identity, self.namespace, self.name)
+            if self.on_stopped:
+                self.on_stopped()
 
     async def _run(self):
         # The flag, not only the cancel, ends the loop: before Python 3.12 asyncio.wait_for returns the
         # inner result and swallows a cancellation that lands just as the inner call completes, and a
         # loop that relied on CancelledError alone would renew forever (stop() would never return).
         while not self._stopping:
+            timeout = self.renew_deadline
+            if self.is_leader:
+                timeout = self._deadline_left()
+                if timeout <= 0:
+                    self._step_down()
+                    timeout = self.renew_deadline
             try:
-                ok = await asyncio.wait_for(self.try_acquire_or_renew(), self.renew_deadline)
+                ok = await asyncio.wait_for(self.try_acquire_or_renew(), timeout)
             except (ApiError, OSError, ConnectionError, asyncio.TimeoutError) as e:
                 log.warning("lease %s/%s: %r", self.namespace, self.name, e)
                 ok = False
@@ -117,12 +141,12 @@ class LeaderElector:
                 log.info("%s became leader of %s/%s", self.identity, self.namespace, self.name)
                 if self.on_started:
                     self.on_started()
-            elif not ok and self.is_leader and time.monotonic() - self._last_renew > self.renew_deadline:
-                self.is_leader = False
-                log.warning("%s lost leadership of %s/%s", self.identity, self.namespace, self.name)
-                if self.on_stopped:
-                    self.on_stopped()
-            await asyncio.sleep(self.retry_period)
+            elif not ok and self.is_leader and self._deadline_left() <= 0:
+                self._step_down()
+            sleep = self.retry_period
+            if self.is_leader:
+                sleep = max(0.0, min(sleep, self._deadline_left()))
+            await asyncio.sleep(sleep)
 
     async def start(self):
         self._task = asyncio.get_running_loop().create_task(self._run(), name=f"leader-{self.name}")

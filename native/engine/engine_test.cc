@@ -121,6 +121,24 @@ static void test_http() {
   std::string close = "HTTP/1.0 200 OK\r\n\r\nxyz";
   CHECK(http::parse(close.data(), close.size(), false, &m, &err) == 0);
   CHECK(http::parse(close.data(), close.size(), false, &m, &err, true) > 0 && m.body == "xyz" && !m.keep_alive);
+  // hostile chunk sizes: a size that would wrap body.size() + sz, a signed size, garbage
+  const char* hostile[] = {"5\r\nhello\r\nfffffffffffffffb\r\n", "5\r\nhello\r\n-1\r\n", "0x5\r\nhello\r\n0\r\n\r\n",
+                           "ffffffffffffffffff\r\n", "\r\n", "4 4\r\nabcd\r\n0\r\n\r\n"};
+  for (const char* b : hostile) {
+    std::string req = std::string("POST /f HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n") + b;
+    CHECK(http::parse(req.data(), req.size(), true, &m, &err, false, 1 << 20) == -1);
+  }
+  std::string big = "POST /f HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nhello\r\n100000\r\n";
+  CHECK(http::parse(big.data(), big.size(), true, &m, &err, false, 1 << 20) == -1 && err == "body too large");
+  std::string okc = "POST /f HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n5;ext=1\r\nhello\r\nA\r\n0123456789\r\n0\r\n\r\n";
+  CHECK(http::parse(okc.data(), okc.size(), true, &m, &err, false, 1 << 20) == static_cast<long>(okc.size()) &&
+        m.body == "hello0123456789");
+  size_t sz = 0;
+  CHECK(!http::parse_chunk_size("fffffffffffffffb", size_t(-1) / 2, &sz));
+  CHECK(http::parse_chunk_size("7fffffffffffffff", size_t(-1) / 2, &sz) && sz == size_t(-1) / 2);
+  CHECK(!http::parse_chunk_size("+5", 100, &sz) && !http::parse_chunk_size("", 100, &sz));
+  http::Dechunker dc;
+  CHECK(dc.feed("-1\r\n", 4, [](std::string_view) {}) == -1);
   http::Url u;
   CHECK(http::parse_url("https://[::1]:6443/pre/", &u) && u.tls && u.host == "::1" && u.port == 6443 &&
         u.prefix == "/pre");

@@ -47,6 +47,28 @@ bool contains_token(std::string_view v, std::string_view tok) {
 
 }  // namespace
 
+bool parse_chunk_size(std::string_view hex, size_t limit, size_t* out) {
+  // 1*HEXDIG only: no sign, no "0x", no whitespace; anything above `limit` is refused before it can wrap
+  if (hex.empty() || hex.size() > 16) return false;
+  size_t v = 0;
+  for (char c : hex) {
+    int d;
+    if (c >= '0' && c <= '9') {
+      d = c - '0';
+    } else if (c >= 'a' && c <= 'f') {
+      d = c - 'a' + 10;
+    } else if (c >= 'A' && c <= 'F') {
+      d = c - 'A' + 10;
+    } else {
+      return false;
+    }
+    if (static_cast<size_t>(d) > limit || v > (limit - static_cast<size_t>(d)) / 16) return false;
+    v = v * 16 + static_cast<size_t>(d);
+  }
+  *out = v;
+  return true;
+}
+
 const std::string* Message::header(std::string_view name) const {
   for (const auto& h : headers) {
     if (h.first == name) return &h.second;
@@ -151,12 +173,12 @@ long parse(const char* buf, size_t n, bool is_request, Message* out, std::string
     while (true) {
       size_t e = s.find("\r\n", p);
       if (e == std::string_view::npos) return 0;
-      std::string szs(s.substr(p, e - p));
+      std::string_view szs = s.substr(p, e - p);
       size_t semi = szs.find(';');
-      if (semi != std::string::npos) szs.resize(semi);
-      char* endp = nullptr;
-      unsigned long sz = std::strtoul(szs.c_str(), &endp, 16);
-      if (endp == szs.c_str()) {
+      if (semi != std::string_view::npos) szs = szs.substr(0, semi);
+      szs = trim(szs);
+      size_t sz = 0;
+      if (!parse_chunk_size(szs, max_body, &sz)) {
         *err = "bad chunk size";
         return -1;
       }
@@ -175,11 +197,12 @@ long parse(const char* buf, size_t n, bool is_request, Message* out, std::string
         out->body = std::move(body);
         return static_cast<long>(p);
       }
-      if (body.size() + sz > max_body) {
+      // invariant body.size() <= max_body and sz <= max_body: no subtraction or sum below can wrap
+      if (sz > max_body - body.size()) {
         *err = "body too large";
         return -1;
       }
-      if (n < p + sz + 2) return 0;
+      if (p > n || n - p < sz + 2) return 0;
       body.append(buf + p, sz);
       p += sz + 2;
     }
@@ -216,10 +239,8 @@ int Dechunker::feed(const char* data, size_t n, const std::function<void(std::st
           size_t semi = line_.find(';');
           if (semi != std::string::npos) line_.resize(semi);
           while (!line_.empty() && (line_.back() == '\r' || line_.back() == ' ')) line_.pop_back();
-          if (line_.empty()) return -1;
-          char* endp = nullptr;
-          unsigned long long sz = std::strtoull(line_.c_str(), &endp, 16);
-          if (endp == line_.c_str() || *endp) return -1;
+          size_t sz = 0;
+          if (!parse_chunk_size(line_, size_t{1} << 40, &sz)) return -1;
           line_.clear();
           remaining_ = sz;
           state_ = sz == 0 ? State::Trailer : State::Data;

@@ -46,6 +46,11 @@ long parse(const char* buf, size_t n, bool is_request, Message* out, std::string
 long parse_head(const char* buf, size_t n, bool is_request, Message* out, std::string* err, long* content_length,
                 bool* chunked);
 
+// A chunk-size token (1*HEXDIG, extensions already stripped) no larger than
+// `limit`.  Rejects signs, prefixes, empty and over-long input, and any value
+// above `limit` before it can wrap.
+bool parse_chunk_size(std::string_view hex, size_t limit, size_t* out);
+
 // Incremental Transfer-Encoding: chunked decoder for streamed bodies (watch
 // responses).  feed() passes decoded bytes to `out`; returns 1 once the
 // terminating chunk (and trailers) were consumed, 0 if more input is needed,

@@ -293,7 +293,7 @@ void NativeServer::on_readable(Loop* lp, Conn* c) {
     break;  // EAGAIN or error
   }
   uint64_t id = c->id;
-  process(lp, c);
+  safe_process(lp, c);
   if (eof && lp->conns.count(id)) {
     Conn* cc = lp->conns[id];
     if (!cc->busy && cc->out_off >= cc->out.size()) {
@@ -301,6 +301,19 @@ void NativeServer::on_readable(Loop* lp, Conn* c) {
     } else {
       cc->close_after = true;
     }
+  }
+}
+
+void NativeServer::safe_process(Loop* lp, Conn* c) {
+  uint64_t id = c->id;
+  try {
+    process(lp, c);
+  } catch (const std::exception& e) {
+    // one malformed or hostile request must never take the loop thread (and the extender) down
+    stats_.bad_requests.fetch_add(1, std::memory_order_relaxed);
+    std::fprintf(stderr, "[gsx-engine] request dropped: %s\n", e.what());
+    auto it = lp->conns.find(id);
+    if (it != lp->conns.end()) close_conn(lp, it->second);
   }
 }
 
@@ -391,7 +404,7 @@ void NativeServer::drain_completions(Loop* lp) {
     c->busy = false;
     uint64_t id = c->id;
     respond(lp, c, std::move(std::get<1>(t)), std::get<2>(t));
-    if (lp->conns.count(id)) process(lp, c);
+    if (lp->conns.count(id)) safe_process(lp, c);
   }
 }
 

@@ -103,6 +103,7 @@ class NativeServer {
   void run_loop(Loop* lp);
   void on_readable(Loop* lp, Conn* c);
   void process(Loop* lp, Conn* c);
+  void safe_process(Loop* lp, Conn* c);  // process() that closes only this connection on an exception
   void dispatch(Loop* lp, Conn* c, http::Message& req);
   void respond(Loop* lp, Conn* c, std::string resp, bool keep_alive);
   void flush(Loop* lp, Conn* c);

@@ -355,3 +355,80 @@ def test_rate_limited_requeue_delivers_later():
         assert item == "x"
         await q.shutdown()
     run(go())
+
+
+class _StallingClient:
+    """A KubeClient stand-in whose Lease calls fail fast once, then hang, once ``stall`` is set."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        self.stall = False
+        self.fast_failures = 0
+        self._never = asyncio.Event()
+
+    async def _gate(self):
+        if self.stall:
+            if self.fast_failures:
+                self.fast_failures -= 1
+                raise OSError("connection reset")
+            await self._never.wait()
+
+    async def get(self, *a, **kw):
+        await self._gate()
+        return await self.inner.get(*a, **kw)
+
+    async def create(self, *a, **kw):
+        await self._gate()
+        return await self.inner.create(*a, **kw)
+
+    async def replace(self, *a, **kw):
+        await self._gate()
+        return await self.inner.replace(*a, **kw)
+
+
+def test_leader_steps_down_before_standby_can_acquire():
+    """A fast failure followed by a hanging renew must not keep the old leader in office past renew_deadline:
+    it stops (no more binds) before the standby can acquire the Lease, so two ledgers never bind at once."""
+    from gpushare_scheduler_extender_amd.k8s.leader import LeaderElector
+
+    async def go():
+        api = await FakeApiServerRunner().start()
+        ca, cb = KubeClient(api.url), KubeClient(api.url)
+        sa = _StallingClient(ca)
+        t = {}
+        loop = asyncio.get_running_loop()
+        kw = dict(namespace="default", lease_duration=1.5, renew_deadline=1.0, retry_period=0.4)
+        a = LeaderElector(sa, identity="a", on_stopped=lambda: t.setdefault("a_stop", loop.time()), **kw)
+        b = LeaderElector(cb, identity="b", on_started=lambda: t.setdefault("b_start", loop.time()), **kw)
+        try:
+            await a.start()
+            for _ in range(100):
+                if a.is_leader:
+                    break
+                await asyncio.sleep(0.02)
+            assert a.is_leader
+            await b.start()
+            await asyncio.sleep(0.5)
+            assert not b.is_leader
+            sa.fast_failures = 1
+            sa.stall = True
+            t_stall = loop.time()
+            for _ in range(400):
+                if "b_start" in t:
+                    break
+                await asyncio.sleep(0.01)
+            assert "a_stop" in t and "b_start" in t, t
+            assert t["a_stop"] < t["b_start"], t
+            # bounded by renew_deadline from a's last successful renewal (which was before the stall)
+            assert t["a_stop"] - t_stall <= kw["renew_deadline"] + 0.15, t["a_stop"] - t_stall
+            assert not a.is_leader and b.is_leader
+        finally:
+            sa.stall = False
+            a._stopping = True
+            if a._task:
+                a._task.cancel()
+            await b.stop()
+            await ca.close()
+            await cb.close()
+            await api.stop()
+    asyncio.run(go())

@@ -64,6 +64,26 @@ def test_pipelined_and_chunked_requests():
     asyncio.run(go())
 
 
+def test_hostile_chunk_sizes_do_not_stop_the_server():
+    """a chunk size that wraps ``body.size() + sz`` used to abort the extender process."""
+    async def go():
+        api, c, ext = await _stack()
+        try:
+            loop = asyncio.get_running_loop()
+            head = b"POST /gpushare-scheduler/filter HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+            for tail in (b"5\r\nhello\r\nfffffffffffffffb\r\n", b"5\r\nhello\r\n-1\r\n", b"ffffffffffffffffffff\r\n"):
+                r = await loop.run_in_executor(None, _raw, ext.port, head + tail, 1)
+                assert r.startswith(b"HTTP/1.1 400"), r[:80]
+            # the server is still up and answers a normal filter
+            body = wire.filter_args(make_pod("p", 50), ["n"])
+            one = (b"POST /gpushare-scheduler/filter HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n" % len(body)) + body
+            data = await loop.run_in_executor(None, _raw, ext.port, one, 1)
+            assert b'"NodeNames":["n"]' in data
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())
+
+
 def test_concurrent_filters_from_threads_and_stats():
     async def go():
         api, c, ext = await _stack()
