@@ -289,7 +289,8 @@ def main():
         devs_ = [Device(**d) for d, _ in all_devs]
         totals = [d.units(unit) for d in devs_]
         inv = [{"index": d.index, "bdf": d.bdf, "uuid": d.uuid, "units": d.units(unit), "total_bytes": d.total_bytes,
-                "cu": d.cu_count, "render": d.render_minor, "card": d.card_minor, "partition": d.partition}
+                "share_bytes": d.share_bytes, "cu": d.cu_count, "xcc": d.xcc_count, "render": d.render_minor,
+                "card": d.card_minor, "partition": d.partition}
                for d in devs_]
         node = make_node(NODE, sum(totals), len(totals), profile=profile, device_totals=totals,
                          annotations={NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv),

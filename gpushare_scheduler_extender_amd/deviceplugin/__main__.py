@@ -34,6 +34,9 @@ def main(argv=None) -> int:
     ap.add_argument("--reserve-gib", type=float, default=float(env.get("GSX_RESERVE_GIB", "0")),
                     help="HBM per GPU withheld from sharing (driver / runtime overhead)")
     ap.add_argument("--health-interval", type=float, default=float(env.get("GSX_HEALTH_INTERVAL", "10")))
+    ap.add_argument("--debug-port", type=int, default=int(env.get("GSX_DEBUG_PORT", "0")),
+                    help="serve /healthz, /metrics and /debug/state on this port (0: off)")
+    ap.add_argument("--debug-host", default=env.get("GSX_DEBUG_HOST", "127.0.0.1"))
     ap.add_argument("--log-level", default=env.get("LOG_LEVEL", "info"))
     ap.add_argument("--log-dir", default=env.get("GSX_LOG_DIR", ""))
     a = ap.parse_args(argv)
@@ -50,6 +53,9 @@ def main(argv=None) -> int:
                                 mount_mode=a.mount_mode, health_backend="amdsmi" if backend == "amdsmi" else None,
                                 health_interval=a.health_interval, reserve_bytes=int(a.reserve_gib * (1 << 30)))
         await plugin.start()
+        if a.debug_port:
+            port = await plugin.serve_debug(a.debug_host, a.debug_port)
+            logging.getLogger("gsx.main").info("debug endpoints on %s:%d", a.debug_host, port)
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()
         for s in (signal.SIGINT, signal.SIGTERM):

@@ -1,17 +1,31 @@
-"""Node agent: kubelet + device-plugin + container-runtime stand-in for one node (or some of its GPUs).
+"""Node agent: the kubelet + container-runtime stand-in for one node (or some of its GPUs).
 
-Where there is no kubelet (tests, the simulator, ``bench.py``), this drives
-the same Allocate logic the gRPC device plugin serves to kubelet
-(:mod:`.allocator`), then "starts" the pod through a runtime
-(:mod:`.runtime`) and reports it Running — the tail of the reference's
-sequence diagram (``docs/designs/sequence.jpg``): bound pod -> Allocate ->
-``ASSIGNED=true`` -> container env -> pod runs on the chosen GPU.
+Where there is no kubelet (tests, the simulator, ``bench.py``), this plays
+kubelet against the *shipped* device plugin — the tail of the reference's
+sequence diagram (``docs/designs/sequence.jpg``): pod bound to the node ->
+kubelet admission -> device plugin ``Allocate`` -> ``ASSIGNED=true`` ->
+container env -> the pod runs on the chosen GPU.
 
-It watches only pods bound to its node (``fieldSelector=spec.nodeName``) and,
-with ``devices`` set, only those whose ``*_IDX`` annotation names one of its
-GPUs, so one agent per GPU (one per rank in ``bench.py``) can share a node.
-A pod that completes or is deleted is stopped and its slice (and CU
-partition) released.
+* Which pod an Allocate belongs to is decided by the plugin alone
+  (:meth:`GpuSharePlugin.allocate_container` over :mod:`.state`); the agent
+  has no matching logic of its own.  ``plugin_socket`` set: the agent is a
+  gRPC client of a running plugin, exactly as kubelet's device manager is
+  (ListAndWatch for the IDs, GetPreferredAllocation to pick IDs, Allocate);
+  otherwise it calls an in-process :class:`GpuSharePlugin` that shares its
+  pod informer.
+* Admission is serial, in the order pods are seen (kubelet's
+  ``HandlePodAdditions``); starting containers and reporting status run on
+  ``workers`` tasks (kubelet's per-pod workers).
+* If the plugin matched a different pod than the one being admitted (two
+  pending pods of one size), the allocation goes to the pod the plugin
+  committed — the ``gpushare.amd.com/pod`` container annotation names it —
+  and the admitted pod waits for the next Allocate (``stats["mismatch"]``).
+* A pod that completes or is deleted is stopped and its slice released; the
+  plugin's own informer releases its CU partition.
+
+With ``devices`` set to a subset of the node's GPUs, only pods whose
+``*_IDX`` annotation names one of them are admitted, so one agent per GPU
+(one per rank in ``bench.py --agent rank``) can share a node.
 """
 from __future__ import annotations
 
@@ -23,17 +37,25 @@ from ..k8s.client import ApiError, KubeClient
 from ..k8s.informer import Handler, Informer, obj_key
 from ..models import pod as podutil
 from ..models.profile import NamingProfile
-from .allocator import CU_COUNT_ANNOTATION, CUPartitioner, assigned_patch, build_response
+from .allocator import AllocateError
 from .devices import UNITS, Device
+from .plugin import POD_ANNOTATION, GpuSharePlugin, PluginClient
 from .runtime import AdmissionError, admit_local
 
 log = logging.getLogger("gsx.agent")
 
 
+class _Alloc:
+    """What kubelet keeps from one container's Allocate response."""
+
+    def __init__(self, uid: str, key: str, dev: int, envs: dict, cus: list[int] | None, ids: list[str]):
+        self.uid, self.key, self.dev, self.envs, self.cus, self.ids = uid, key, dev, envs, cus, ids
+
+
 class NodeAgent:
     def __init__(self, client: KubeClient, node: str, devices: list[Device], profile: NamingProfile, runtime, *,
                  unit: str = "GiB", verify_each: bool = True, mount_mode: str = "isolated", report_status: bool = True,
-                 workers: int = 8):
+                 workers: int = 8, plugin: GpuSharePlugin | None = None, plugin_socket: str | None = None):
         self.client = client
         self.node = node
         self.devices = {d.index: d for d in devices}
@@ -44,62 +66,58 @@ class NodeAgent:
         # a host-process launcher cannot hide device nodes: it needs host GPU indices in *_VISIBLE_DEVICES
         self.mount_mode = getattr(runtime, "mount_mode", mount_mode)
         self.report_status = report_status
-        self.cus = {d.index: CUPartitioner(d.cu_count, d.xcc_count) for d in devices}
         self.pods = Informer(client, "pods", field_selector=f"spec.nodeName={node}")
+        self.pclient = PluginClient(plugin_socket) if plugin_socket else None
+        self._own_plugin = plugin is None and plugin_socket is None
+        if self._own_plugin:
+            plugin = GpuSharePlugin(client, node, devices, profile, unit=unit, mount_mode=self.mount_mode,
+                                    informer=self.pods)
+        self.plugin = plugin
         self.running: dict[str, str] = {}  # uid -> pod key
-        self.inflight: set[str] = set()
         self.allocations: dict[str, dict] = {}  # uid -> container env of the last Allocate
         self.admitted = 0
         self.failed = 0
         self.bad_stamps = 0
         self.latency: list[float] = []  # bound-observed -> Running
+        self.stats = {"allocate_calls": 0, "allocate_errors": 0, "mismatch": 0, "allocate_ms_max": 0.0}
         self._bg: set[asyncio.Task] = set()
         self._releasing: set[asyncio.Task] = set()
-        self._assign_retries: dict[str, int] = {}
-        self.queue: asyncio.Queue = asyncio.Queue()
+        self.admit_q: asyncio.Queue = asyncio.Queue()
+        self.start_q: asyncio.Queue = asyncio.Queue()
         self.queued: set[str] = set()
+        self.claimed: set[str] = set()  # uids whose allocation is done (starting or running)
         self.seen: dict[str, float] = {}
-        # Allocate candidates (pending, ASSIGNED=false, one of our GPUs): uid -> (assume_time, key, units);
-        # kept incrementally so an Allocate is O(candidates) instead of a scan + sort of every pod on the node
-        self._cands: dict[str, tuple[int, str, int]] = {}
         self.workers = workers
+        # kubelet's device-ID accounting (gRPC mode): all plugin IDs, and the ones each pod holds
+        self.all_ids: list[str] = []
+        self.used_ids: dict[str, list[str]] = {}
         self.pods.add_handler(Handler(self._on_pod, lambda o, n, r: self._on_pod(n, r), self._on_delete))
 
+    # ------------------------------------------------------------ pod watch (kubelet's pod config source)
     def _mine(self, pod: dict) -> bool:
         return podutil.gpu_id_from_annotation(pod, self.profile) in self.devices
 
     def _on_pod(self, pod: dict, raw):
         uid = podutil.meta(pod).get("uid", "")
         if podutil.is_complete(pod):
-            self._cands.pop(uid, None)
             self._stop(uid)
             return
         if not podutil.is_gpushare_pod(pod, self.profile) or not self._mine(pod):
-            self._cands.pop(uid, None)
             return
-        ann = podutil.annotations(pod)
-        if ann.get(self.profile.annotation_assigned) == "false" and podutil.phase(pod) in ("Pending", ""):
-            self._cands[uid] = (podutil.assume_time(pod, self.profile), obj_key(pod),
-                                podutil.gpu_mem_request(pod, self.profile))
-        else:
-            self._cands.pop(uid, None)
-        if (ann.get(self.profile.annotation_assigned) == "false" and uid not in self.inflight
-                and uid not in self.running and uid not in self.queued):
+        if (podutil.annotations(pod).get(self.profile.annotation_assigned) == "false" and uid not in self.claimed
+                and uid not in self.queued and podutil.phase(pod) in ("Pending", "")):
             self.queued.add(uid)
             self.seen.setdefault(uid, time.perf_counter())
-            self.queue.put_nowait(obj_key(pod))
+            self.admit_q.put_nowait(obj_key(pod))
 
     def _on_delete(self, pod: dict, raw):
-        uid = podutil.meta(pod).get("uid", "")
-        self._cands.pop(uid, None)
-        self._stop(uid)
+        self._stop(podutil.meta(pod).get("uid", ""))
 
     def _stop(self, uid: str):
-        if uid in self.running:
-            self.running.pop(uid, None)
+        self.claimed.discard(uid)
+        self.used_ids.pop(uid, None)
+        if self.running.pop(uid, None) is not None:
             self._release(uid)
-            for p in self.cus.values():
-                p.release(uid)
 
     def _release(self, uid: str):
         rel = getattr(self.runtime, "release", None)
@@ -112,6 +130,92 @@ class NodeAgent:
         t.add_done_callback(self._bg.discard)
         t.add_done_callback(self._releasing.discard)
 
+    # ------------------------------------------------------------ device plugin calls (kubelet's device manager)
+    async def _allocate_grpc(self, uid: str, units: int) -> _Alloc:
+        free = sorted(set(self.all_ids) - {i for ids in self.used_ids.values() for i in ids})
+        if len(free) < units:
+            raise AllocateError(f"kubelet: {units} {self.profile.resource} requested, {len(free)} IDs free")
+        pref = await self.pclient.preferred(free, units)
+        ids = list(pref.container_responses[0].deviceIDs)
+        r = (await self.pclient.allocate([ids])).container_responses[0]
+        who = r.annotations.get(POD_ANNOTATION, "")
+        envs = dict(r.envs)
+        cus = None
+        if envs.get("GSX_CU_MASK"):
+            from .state import parse_cu_mask  # noqa: PLC0415
+
+            cus = parse_cu_mask(envs["GSX_CU_MASK"])
+        key, _, cuid = who.rpartition("/")
+        return _Alloc(cuid or uid, key, int(envs.get(self.profile.annotation_idx, "-1")), envs, cus, ids)
+
+    async def _allocate_inproc(self, units: int) -> _Alloc:
+        rec, alloc = await self.plugin.allocate_container(units)
+        cus = None
+        if alloc.envs.get("GSX_CU_MASK"):
+            from .state import parse_cu_mask  # noqa: PLC0415
+
+            cus = parse_cu_mask(alloc.envs["GSX_CU_MASK"])
+        return _Alloc(rec.uid, rec.key, rec.dev, alloc.envs, cus, [])
+
+    async def _allocate(self, uid: str, units: int) -> _Alloc:
+        t0 = time.perf_counter()
+        self.stats["allocate_calls"] += 1
+        try:
+            if self.pclient is not None:
+                return await self._allocate_grpc(uid, units)
+            return await self._allocate_inproc(units)
+        finally:
+            self.stats["allocate_ms_max"] = max(self.stats["allocate_ms_max"], 1e3 * (time.perf_counter() - t0))
+
+    # ------------------------------------------------------------ admission (serial, like kubelet)
+    async def _admission_worker(self):
+        while True:
+            key = await self.admit_q.get()
+            pod = self.pods.get(key)
+            if pod is None:
+                continue
+            uid = podutil.meta(pod).get("uid", "")
+            self.queued.discard(uid)
+            if uid in self.claimed or podutil.is_complete(pod):
+                continue
+            try:
+                await self._admit(key, pod, uid)
+            except Exception as e:  # noqa: BLE001
+                log.exception("admit %s: %r", key, e)
+
+    async def _admit(self, key: str, pod: dict, uid: str):
+        conts = [podutil.container_limit(c, self.profile.resource) for c in (pod.get("spec") or {}).get("containers") or []]
+        allocs: list[_Alloc] = []
+        try:
+            for units in (u for u in conts if u > 0):
+                allocs.append(await self._allocate(uid, units))
+        except (AllocateError, ApiError, OSError, Exception) as e:  # noqa: BLE001 - grpc errors included
+            self.stats["allocate_errors"] += 1
+            # a pod another Allocate already served, or one that went away meanwhile, needs nothing
+            cur = self.pods.get(key)
+            if cur is None or podutil.is_complete(cur) or podutil.meta(cur).get("uid") in self.claimed:
+                return
+            self.failed += 1
+            log.error("Allocate for %s failed: %s", key, e)
+            if self.report_status:
+                await self._patch_status(cur, {"phase": "Failed", "reason": "UnexpectedAdmissionError",
+                                               "message": f"Allocate failed: {e}"})
+            return
+        got = allocs[0]
+        if got.uid != uid:
+            # the plugin committed an earlier pod of this size: that pod starts with this allocation, ours
+            # is served by the next Allocate
+            self.stats["mismatch"] += 1
+            self.queued.add(uid)
+            self.admit_q.put_nowait(key)
+            key = got.key or key
+        self.claimed.add(got.uid)
+        if allocs[0].ids:
+            self.used_ids[got.uid] = [i for a in allocs for i in a.ids]
+        self.allocations[got.uid] = got.envs
+        self.start_q.put_nowait((got.uid, key, allocs))
+
+    # ------------------------------------------------------------ container start (per-pod workers)
     async def _admit_runtime(self, uid: str, dev: int, nbytes: int, cus) -> int:
         # a container runtime tears down before it starts: releases already decided (e.g. the previous
         # wave, whose device the extender has just freed) reach the runtime before this slice is carved
@@ -124,89 +228,42 @@ class NodeAgent:
             return await adm(uid, dev, nbytes, cus, self.verify_each)
         return admit_local(self.runtime, uid, dev, nbytes, cus, self.verify_each)
 
-    async def _worker(self):
+    async def _start_worker(self):
         while True:
-            key = await self.queue.get()
-            pod = self.pods.get(key)
-            if pod is None:
-                continue
-            self.queued.discard(podutil.meta(pod).get("uid", ""))
-            await self._admit(key)
+            uid, key, allocs = await self.start_q.get()
+            try:
+                await self._start(uid, key, allocs)
+            except Exception as e:  # noqa: BLE001
+                log.exception("start %s: %r", key, e)
 
-    async def _admit(self, key: str):
-        """One kubelet Allocate for the container(s) of the pod behind ``key``."""
+    async def _start(self, uid: str, key: str, allocs: list[_Alloc]):
+        if uid not in self.claimed:
+            return  # deleted while waiting to start
         pod = self.pods.get(key)
-        uid = podutil.meta(pod).get("uid", "") if pod else ""
+        t0 = self.seen.pop(uid, time.perf_counter())
+        dev = allocs[0].dev
+        units = sum(int(a.envs.get(self.profile.env_container, "0") or 0) for a in allocs)
         try:
-            if pod is None or uid in self.running or uid in self.inflight:
-                return
-            units = podutil.gpu_mem_request(pod, self.profile)
-            # kubelet's Allocate(N ids): pick the pod exactly as the device plugin does —
-            # earliest ASSUME_TIME among unassigned pods of that size (not yet claimed here)
-            best = None
-            for cu, (at, ck, cu_units) in self._cands.items():
-                if cu_units == units and cu not in self.inflight and cu not in self.running:
-                    if best is None or (at, ck) < best[0]:
-                        best = ((at, ck), cu)
-            chosen = self.pods.get(best[0][1]) if best is not None else None
-            if chosen is None:
-                return
-            cuid = podutil.meta(chosen).get("uid", "")
-            if cuid != uid:
-                # an earlier same-size pod wins this Allocate; ours is served by the next one
-                self.queued.add(uid)
-                self.queue.put_nowait(key)
-                key, pod, uid = obj_key(chosen), chosen, cuid
-            self.inflight.add(uid)
-            t0 = self.seen.get(uid, time.perf_counter())
-            dev_idx = podutil.gpu_id_from_annotation(pod, self.profile)
-            device = self.devices[dev_idx]
-            cus = None
-            want_cus = podutil.annotations(pod).get(CU_COUNT_ANNOTATION)
-            if want_cus:
-                cus = self.cus[dev_idx].allocate(uid, int(want_cus))
-            alloc = build_response(pod, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
-            try:
-                await self.client.patch("pods", podutil.meta(pod)["name"], assigned_patch(pod, self.profile,
-                                        alloc.annotations), podutil.meta(pod)["namespace"])
-            except (ApiError, OSError) as e:
-                # 409: stale copy, retry from the informer's latest version; 5xx / transport: retry with
-                # capped backoff (as kubelet does); other 4xx: give up
-                if isinstance(e, ApiError) and not (e.conflict or e.status >= 500):
-                    raise
-                if cus:
-                    self.cus[dev_idx].release(uid)
-                if uid not in self.queued:
-                    n = self._assign_retries[uid] = self._assign_retries.get(uid, 0) + 1
-                    self.queued.add(uid)
-                    asyncio.get_running_loop().call_later(min(0.2, 0.001 * 2 ** min(n, 8)), self.queue.put_nowait,
-                                                          key)
-                return
-            self.allocations[uid] = alloc.envs
-            try:
-                bad = await self._admit_runtime(uid, dev_idx, units * self.unit_bytes, cus)
-                if bad:
-                    self.bad_stamps += bad
-                    raise AdmissionError(f"{bad} bad HBM stamps after admitting {key}")
-            except AdmissionError as e:
-                self.failed += 1
-                log.error("admission of %s on GPU %d failed: %s", key, dev_idx, e)
-                self._release(uid) if getattr(self.runtime, "release", None) else self.runtime.stop(uid)
-                if self.report_status:
-                    await self._patch_status(pod, {"phase": "Failed", "reason": "UnexpectedAdmissionError",
-                                                   "message": str(e)})
-                return
-            self.running[uid] = key
-            self.admitted += 1
-            self._assign_retries.pop(uid, None)
-            if self.report_status:
-                await self._patch_status(pod, {"phase": "Running"})
-            self.latency.append(time.perf_counter() - t0)
-            self.seen.pop(uid, None)
-        except Exception as e:  # noqa: BLE001
-            log.exception("admit %s: %r", key, e)
-        finally:
-            self.inflight.discard(uid)
+            bad = await self._admit_runtime(uid, dev, units * self.unit_bytes, allocs[0].cus)
+            if bad:
+                self.bad_stamps += bad
+                raise AdmissionError(f"{bad} bad HBM stamps after admitting {key}")
+        except AdmissionError as e:
+            self.failed += 1
+            log.error("admission of %s on GPU %d failed: %s", key, dev, e)
+            self._release(uid) if getattr(self.runtime, "release", None) else self.runtime.stop(uid)
+            if self.report_status and pod is not None:
+                await self._patch_status(pod, {"phase": "Failed", "reason": "UnexpectedAdmissionError",
+                                               "message": str(e)})
+            return
+        if uid not in self.claimed:  # deleted while starting: tear down what we just started
+            self._release(uid)
+            return
+        self.running[uid] = key
+        self.admitted += 1
+        if self.report_status and pod is not None:
+            await self._patch_status(pod, {"phase": "Running"})
+        self.latency.append(time.perf_counter() - t0)
 
     async def _patch_status(self, pod: dict, status: dict):
         """kubelet's status manager: retried on 409 / 5xx / transport errors with capped backoff; 404 ends it."""
@@ -222,16 +279,29 @@ class NodeAgent:
                 pass
             await asyncio.sleep(min(0.1, 0.0005 * 2 ** min(attempt, 8)))
 
+    # ------------------------------------------------------------ lifecycle
     async def start(self):
+        loop = asyncio.get_running_loop()
+        if self.pclient is not None:
+            stream = self.pclient.list_and_watch()
+            first = await asyncio.wait_for(stream.read(), 30)
+            self.all_ids = [d.ID for d in first.devices if d.health == "Healthy"]
+            stream.cancel()
         await self.pods.start()
         await self.pods.wait_synced(30)
+        if self._own_plugin:
+            await self.plugin.start(register=False, publish=False, serve=False)
+        self._bg.add(loop.create_task(self._admission_worker(), name=f"kubelet-admit-{self.node}"))
         for i in range(self.workers):
-            t = asyncio.get_running_loop().create_task(self._worker(), name=f"agent-{self.node}-{i}")
-            self._bg.add(t)
+            self._bg.add(loop.create_task(self._start_worker(), name=f"kubelet-pod-{self.node}-{i}"))
 
     async def stop(self):
         for t in list(self._bg):
             t.cancel()
+        if self._own_plugin:
+            await self.plugin.stop()
+        if self.pclient is not None:
+            await self.pclient.close()
         await self.pods.stop()
 
 
@@ -251,7 +321,9 @@ async def node_devices_and_endpoints(client: KubeClient, node: str, timeout: flo
             if inv and all(d["index"] in eps for d in inv):
                 devs = [Device(index=d["index"], bdf=d.get("bdf", ""), uuid=d.get("uuid", ""),
                                total_bytes=int(d.get("total_bytes", d.get("units", 0) * UNITS["GiB"])),
-                               cu_count=int(d.get("cu", 256)), render_minor=int(d.get("render", -1)),
+                               share_bytes=int(d.get("share_bytes", 0)),
+                               cu_count=int(d.get("cu", 256)), xcc_count=int(d.get("xcc", 8)),
+                               render_minor=int(d.get("render", -1)),
                                card_minor=int(d.get("card", -1)), partition=d.get("partition", "SPX"))
                         for d in inv]
                 return devs, eps
@@ -262,11 +334,54 @@ async def node_devices_and_endpoints(client: KubeClient, node: str, timeout: flo
         await asyncio.sleep(0.05)
 
 
+async def serve_stats(box: dict, host: str = "127.0.0.1", port: int = 0):
+    """``GET /v1/stats`` and ``GET /v1/allocations/<uid>`` (the native node agent serves the same) for the
+    agent in ``box["agent"]`` (503 until it is there: the port is published before the node exists)."""
+    import json  # noqa: PLC0415
+
+    from aiohttp import web  # noqa: PLC0415
+
+    async def stats(_):
+        agent = box.get("agent")
+        if agent is None:
+            return web.Response(status=503, text="{}", content_type="application/json")
+        lat = sorted(agent.latency)
+        body = {"admitted": agent.admitted, "failed": agent.failed, "bad_stamps": agent.bad_stamps,
+                "running": len(agent.running), "admit_p50_ms": round(1e3 * lat[len(lat) // 2], 3) if lat else 0.0,
+                "admit_max_ms": round(1e3 * lat[-1], 3) if lat else 0.0, **agent.stats, "native": False,
+                "plugin": "grpc" if agent.pclient is not None else "inproc"}
+        if agent.plugin is not None:
+            body["plugin_stats"] = dict(agent.plugin.stats)
+        return web.Response(text=json.dumps(body), content_type="application/json")
+
+    async def allocation(request):
+        agent = box.get("agent")
+        env = agent.allocations.get(request.match_info["uid"]) if agent is not None else None
+        if env is None:
+            return web.Response(status=404, text="{}", content_type="application/json")
+        return web.Response(text=json.dumps({"envs": env}), content_type="application/json")
+
+    app = web.Application()
+    app.router.add_get("/v1/stats", stats)
+    app.router.add_get("/v1/allocations/{uid}", allocation)
+    runner = web.AppRunner(app, access_log=None)
+    await runner.setup()
+    site = web.TCPSite(runner, host, port)
+    await site.start()
+    return runner, site._server.sockets[0].getsockname()[1]
+
+
 def main(argv=None) -> int:
-    """``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``: one node agent driving remote GPU runtimes."""
+    """``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``: kubelet stand-in for one node.
+
+    ``--plugin grpc`` (default): the shipped :class:`GpuSharePlugin` is served on a unix socket in this process
+    (devices from the node's inventory annotation) and driven over gRPC like kubelet drives it;
+    ``--plugin inproc``: the same plugin called directly.
+    """
     import argparse  # noqa: PLC0415
     import os  # noqa: PLC0415
     import signal  # noqa: PLC0415
+    import tempfile  # noqa: PLC0415
 
     from ..k8s.client import KubeConfig  # noqa: PLC0415
     from ..models.profile import get_profile  # noqa: PLC0415
@@ -279,6 +394,8 @@ def main(argv=None) -> int:
     ap.add_argument("--profile", default="shared-gpu")
     ap.add_argument("--unit", default="GiB")
     ap.add_argument("--workers", type=int, default=32)
+    ap.add_argument("--plugin", default="grpc", choices=["grpc", "inproc"])
+    ap.add_argument("--socket-dir", default="")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--port-file", default="")
     a = ap.parse_args(argv)
@@ -286,15 +403,29 @@ def main(argv=None) -> int:
 
     async def run():
         client = KubeClient(KubeConfig.auto(a.kubeconfig, a.apiserver))
-        if a.port_file:  # no listening port; signal readiness for the process harness
+        box: dict = {}
+        runner, port = await serve_stats(box)
+        if a.port_file:  # published before the node exists: the harness starts us first
             with open(a.port_file + ".tmp", "w") as f:
-                f.write("1")
+                f.write(str(port))
             os.replace(a.port_file + ".tmp", a.port_file)
         devs, eps = await node_devices_and_endpoints(client, a.node, timeout=600)
         rt = RemoteRuntime(eps)
-        agent = NodeAgent(client, a.node, devs, get_profile(a.profile), rt, unit=a.unit,
-                          verify_each=not a.no_verify, workers=a.workers)
+        profile = get_profile(a.profile)
+        plugin = None
+        if a.plugin == "grpc":
+            plugin = GpuSharePlugin(KubeClient(KubeConfig.auto(a.kubeconfig, a.apiserver)), a.node, devs, profile,
+                                    unit=a.unit, socket_dir=a.socket_dir or tempfile.mkdtemp(prefix="gsx-dp-"))
+            await plugin.start(register=False, publish=False)
+            agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
+                              workers=a.workers, plugin_socket=plugin.socket_path)
+        else:
+            agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
+                              workers=a.workers)
         await agent.start()
+        if plugin is not None:
+            agent.plugin = plugin  # for /v1/stats
+        box["agent"] = agent
         from ..utils.gctune import tune  # noqa: PLC0415
 
         tune()
@@ -304,6 +435,10 @@ def main(argv=None) -> int:
             loop.add_signal_handler(s, stop.set)
         await stop.wait()
         await agent.stop()
+        if plugin is not None:
+            await plugin.stop()
+            await plugin.client.close()
+        await runner.cleanup()
         await rt.close()
         await client.close()
 

@@ -1,4 +1,7 @@
-"""Device-plugin Allocate logic (kubelet -> plugin -> pod), shared by the gRPC plugin and the node agent.
+"""Device-plugin Allocate building blocks: the container response, the ASSIGNED patch, CU partitions.
+
+Which pod an Allocate belongs to is decided by :mod:`.state` (one implementation, used by the
+gRPC plugin and the kubelet stand-in alike).
 
 Behaviour reconstructed from ``docs/designs/designs.md:93-103`` and
 ``docs/designs/sequence.jpg`` (the plugin itself is not in the reference tree,
@@ -45,32 +48,6 @@ class AllocateError(Exception):
     pass
 
 
-def candidate_pods(pods: list[dict], node: str, profile: NamingProfile) -> list[dict]:
-    """Pending gpushare pods on ``node`` not yet assigned, earliest ASSUME_TIME first."""
-    out = []
-    for p in pods:
-        if podutil.node_name(p) != node or podutil.phase(p) not in ("Pending", ""):
-            continue
-        if podutil.is_complete(p) or not podutil.is_gpushare_pod(p, profile):
-            continue
-        ann = podutil.annotations(p)
-        if ann.get(profile.annotation_assigned) != "false":
-            continue
-        if podutil.gpu_id_from_annotation(p, profile) < 0:
-            continue
-        out.append(p)
-    out.sort(key=lambda p: (podutil.assume_time(p, profile), podutil.meta(p).get("creationTimestamp", ""),
-                            podutil.pod_key(p)))
-    return out
-
-
-def pick_pod(pods: list[dict], node: str, units: int, profile: NamingProfile) -> dict | None:
-    for p in candidate_pods(pods, node, profile):
-        if podutil.gpu_mem_request(p, profile) == units:
-            return p
-    return None
-
-
 class CUPartitioner:
     """Per-device ledger of compute units handed to pods as CU masks.
 
@@ -114,6 +91,28 @@ class CUPartitioner:
         for c in got:
             self.owner[c] = None
         return len(got)
+
+    def adopt(self, uid: str, cus: list[int]) -> list[int]:
+        """Record an existing partition (rebuilt from a pod's cu-mask annotation); returns the CUs that
+        another pod already owned (left with their owner)."""
+        clash, got = [], []
+        for c in sorted(set(cus)):
+            if not 0 <= c < self.cu_count:
+                continue
+            if self.owner[c] is not None and self.owner[c] != uid:
+                clash.append(c)
+                continue
+            self.owner[c] = uid
+            got.append(c)
+        if got:
+            self._held[uid] = sorted(set(self._held.get(uid, [])) | set(got))
+        return clash
+
+    def holds(self, uid: str) -> bool:
+        return uid in self._held
+
+    def held(self) -> dict[str, list[int]]:
+        return {u: list(c) for u, c in self._held.items()}
 
     def free_count(self) -> int:
         return sum(1 for o in self.owner if o is None)

@@ -14,10 +14,16 @@ re-built for MI355X:
   ``capacity / count`` (``pkg/cache/nodeinfo.go:34``);
 * **GetPreferredAllocation** steers kubelet's fake-ID choice onto the GPU the
   extender picked, so kubelet's own per-ID accounting matches the annotation;
-* **Allocate** = :mod:`.allocator` (earliest ``ASSUME_TIME`` pod of that
-  size, ``ASSIGNED=true`` under a resourceVersion precondition, env +
-  ``/dev/kfd`` + render node + optional CU partition);
-* re-registers when kubelet restarts (its socket is re-created).
+* **Allocate** matches the container to a pod through :mod:`.state` (earliest
+  ``ASSUME_TIME`` pod of that size), commits ``ASSIGNED=true`` under a
+  resourceVersion precondition and answers env + ``/dev/kfd`` + render node +
+  optional CU partition (:mod:`.allocator`);
+* a **pod informer** on ``spec.nodeName=<node>`` keeps that state current: CU
+  partitions and multi-container progress are released when a pod completes
+  or is deleted, and rebuilt from the ``gpushare.amd.com/cu-mask`` /
+  ``ASSIGNED`` annotations when the plugin starts, before it serves;
+* re-registers when kubelet restarts (its socket is re-created);
+* optional debug port: ``/healthz``, ``/metrics``, ``/debug/state``.
 """
 from __future__ import annotations
 
@@ -32,8 +38,10 @@ from ..k8s.client import ApiError, KubeClient
 from ..models import pod as podutil
 from ..models.profile import NODE_DEVICE_INFO_ANNOTATION, NODE_DEVICE_MEMORY_ANNOTATION, NamingProfile
 from . import api
-from .allocator import CU_COUNT_ANNOTATION, AllocateError, CUPartitioner, assigned_patch, build_response, candidate_pods
+from ..k8s.informer import Handler, Informer
+from .allocator import AllocateError, ContainerAllocation, assigned_patch, build_response
 from .devices import UNITS, Device
+from .state import AllocationState, PodRec
 
 log = logging.getLogger("gsx.deviceplugin")
 
@@ -46,12 +54,13 @@ def fake_ids(dev: Device, units: int) -> list[str]:
 
 
 ALLOCATE_ATTEMPTS = 8  # per container request: transient apiserver failures retried with capped backoff
+POD_ANNOTATION = "gpushare.amd.com/pod"  # container annotation: the pod this Allocate was matched to
 
 class GpuSharePlugin:
     def __init__(self, client: KubeClient, node: str, devices: list[Device], profile: NamingProfile, *,
                  unit: str = "GiB", socket_dir: str = api.DEVICE_PLUGIN_PATH, endpoint: str = "gpushare-amd.sock",
                  mount_mode: str = "isolated", health_backend: str | None = None, health_interval: float = 10.0,
-                 reserve_bytes: int = 0):
+                 reserve_bytes: int = 0, informer: Informer | None = None):
         self.client = client
         self.node = node
         self.devices = {d.index: d for d in devices}
@@ -65,8 +74,13 @@ class GpuSharePlugin:
         self.units = {d.index: d.units(unit, reserve_bytes) for d in devices}
         self.ids = {d.index: fake_ids(d, self.units[d.index]) for d in devices}
         self.id_owner = {i: d for d, ids in self.ids.items() for i in ids}
-        self.cus = {d.index: CUPartitioner(d.cu_count, d.xcc_count) for d in devices}
-        self.partial: dict[str, list[int]] = {}  # pod uid -> container requests not yet allocated
+        self.state = AllocationState(node, self.devices, profile)
+        # a kubelet stand-in in the same process may share its pod informer (one watch per node)
+        self._own_informer = informer is None
+        self.pods = informer or Informer(client, "pods", field_selector=f"spec.nodeName={node}")
+        self.pods.add_handler(Handler(lambda o, raw: self.state.observe(o),
+                                      lambda old, new, raw: self.state.observe(new),
+                                      lambda o, raw: self.state.forget(o)))
         self._changed = asyncio.Event()
         self._version = 0
         self._stopped = False
@@ -74,7 +88,8 @@ class GpuSharePlugin:
         self._tasks: list[asyncio.Task] = []
         self.allocations = 0
         self.stats = {"allocate_ok": 0, "allocate_fail": 0, "allocate_retries": 0, "preferred": 0,
-                      "registrations": 0}
+                      "registrations": 0, "refreshes": 0}
+        self._debug = None
 
     # ------------------------------------------------------------ paths
     @property
@@ -126,33 +141,23 @@ class GpuSharePlugin:
             except asyncio.TimeoutError:
                 pass
 
-    async def _pods_on_node(self) -> list[dict]:
+    async def refresh(self):
+        """A fresh LIST of this node's pods into the state (the informer may lag an Allocate by a moment)."""
         lst = await self.client.list("pods", field_selector=f"spec.nodeName={self.node}")
-        return lst.get("items") or []
-
-    def _match(self, pods: list[dict], units: int) -> tuple[dict | None, bool]:
-        """(pod, whole_pod) for a request of ``units``: whole pods first, then one container of a multi-container pod."""
-        cands = candidate_pods(pods, self.node, self.profile)
-        for p in cands:
-            if podutil.gpu_mem_request(p, self.profile) == units:
-                return p, True
-        for p in pods:  # second container of a pod whose first container was already allocated
-            uid = podutil.meta(p).get("uid", "")
-            if units in self.partial.get(uid, []):
-                return p, False
-        for p in cands:
-            reqs = [podutil.container_limit(c, self.profile.resource) for c in (p.get("spec") or {}).get("containers", [])]
-            if units in reqs:
-                return p, False
-        return None, False
+        self.state.resync(lst.get("items") or [])
+        self.stats["refreshes"] += 1
 
     async def GetPreferredAllocation(self, request, context):
         resp = api.PreferredAllocationResponse()
-        pods = await self._pods_on_node()
         for creq in request.container_requests:
             size = creq.allocation_size
-            pod, _ = self._match(pods, size)
-            want_dev = podutil.gpu_id_from_annotation(pod, self.profile) if pod else -1
+            want_dev = self.state.preferred_device(size)
+            if want_dev < 0:
+                try:
+                    await self.refresh()
+                except (ApiError, OSError) as e:
+                    log.warning("GetPreferredAllocation refresh: %s", e)
+                want_dev = self.state.preferred_device(size)
             avail = list(creq.available_deviceIDs)
             chosen = list(creq.must_include_deviceIDs)
             pref = [i for i in avail if i not in chosen and self.id_owner.get(i) == want_dev]
@@ -165,74 +170,75 @@ class GpuSharePlugin:
             self.stats["preferred"] += 1
         return resp
 
-    async def _claim(self, pods: list[dict], units: int) -> tuple:
-        """Match one container request to its pod; for the pod's first container commit ASSIGNED=true.
+    async def allocate_container(self, units: int) -> tuple[PodRec, ContainerAllocation]:
+        """Match one container request of ``units`` to its pod and build its allocation.
 
-        A 409 (the pod changed since our LIST) or an apiserver 5xx / transport error is retried from a
-        fresh LIST with capped backoff: failing Allocate makes kubelet reject the pod
-        (UnexpectedAdmissionError) over a transient apiserver hiccup.  Returns (pod, whole, alloc, pods)."""
+        For the pod's first container this commits ``ASSIGNED=true`` (with the pod's resourceVersion as a
+        precondition, so two Allocates never claim one pod).  A 409 (the pod changed since we saw it) or an
+        apiserver 5xx / transport error is retried from fresh state with capped backoff: failing Allocate makes
+        kubelet reject the pod (UnexpectedAdmissionError) over a transient apiserver hiccup."""
+        refreshed = False
         for attempt in range(ALLOCATE_ATTEMPTS):
-            pod, whole = self._match(pods, units)
-            if pod is None:
+            rec, whole = self.state.match(units)
+            if rec is None and not refreshed:
+                await self.refresh()
+                refreshed = True
+                rec, whole = self.state.match(units)
+            if rec is None:
                 raise AllocateError(f"no pending pod on {self.node} requests {units} {self.profile.resource} "
                                     f"with {self.profile.annotation_assigned}=false")
-            uid = podutil.meta(pod).get("uid", "")
-            dev_idx = podutil.gpu_id_from_annotation(pod, self.profile)
-            device = self.devices.get(dev_idx)
+            device = self.devices.get(rec.dev)
             if device is None:
-                raise AllocateError(f"pod {podutil.pod_key(pod)} annotated with GPU {dev_idx}, not on this node")
-            cus = None
-            want = podutil.annotations(pod).get(CU_COUNT_ANNOTATION)
-            if want:
-                cus = self.cus[dev_idx].allocate(uid, int(want))
-            alloc = build_response(pod, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
-            if uid in self.partial:  # a later container of a pod whose first container committed
-                return pod, whole, alloc, pods
+                raise AllocateError(f"pod {rec.key} annotated with GPU {rec.dev}, not on this node")
+            cp = self.state.cus.get(rec.dev)
+            had_cus = cp is not None and cp.holds(rec.uid)
+            if rec.assigned == "true":  # a later container of a pod whose first container committed
+                cus = self.state.claim_cus(rec)
+                alloc = build_response(rec.obj, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
+                self.state.later_container_allocated(rec, units)
+                return rec, alloc
+            self.state.inflight.add(rec.uid)
             try:
-                # first (or only) container: commit point ASSIGNED=true
-                await self.client.patch("pods", podutil.meta(pod)["name"],
-                                        assigned_patch(pod, self.profile, alloc.annotations),
-                                        podutil.meta(pod)["namespace"])
-                return pod, whole, alloc, pods
-            except (ApiError, OSError) as e:
-                if cus:
-                    self.cus[dev_idx].release(uid)
-                transient = not isinstance(e, ApiError) or e.conflict or e.status >= 500
-                if not transient or attempt == ALLOCATE_ATTEMPTS - 1:
-                    raise AllocateError(f"marking {podutil.pod_key(pod)} assigned failed: {e}") from e
-                self.stats["allocate_retries"] += 1
-                await asyncio.sleep(min(0.2, 0.005 * 2 ** attempt))
-                pods = await self._pods_on_node()
+                cus = self.state.claim_cus(rec)
+                alloc = build_response(rec.obj, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
+                try:
+                    pod = await self.client.patch("pods", rec.name, assigned_patch(rec.obj, self.profile,
+                                                                                    alloc.annotations),
+                                                  rec.namespace)
+                except (ApiError, OSError) as e:
+                    if cus and not had_cus:
+                        cp.release(rec.uid)
+                    transient = not isinstance(e, ApiError) or e.conflict or e.status >= 500
+                    if not transient or attempt == ALLOCATE_ATTEMPTS - 1:
+                        raise AllocateError(f"marking {rec.key} assigned failed: {e}") from e
+                    self.stats["allocate_retries"] += 1
+                    await asyncio.sleep(min(0.2, 0.005 * 2 ** attempt))
+                    await self.refresh()
+                    refreshed = True
+                    continue
+            finally:
+                self.state.inflight.discard(rec.uid)
+            self.state.observe(pod)
+            self.state.first_container_committed(rec, units, whole)
+            return rec, alloc
         raise AllocateError("unreachable")
 
     async def Allocate(self, request, context):
         resp = api.AllocateResponse()
         try:
-            pods = await self._pods_on_node()
             for creq in request.container_requests:
-                units = len(creq.devices_ids)
-                pod, whole, alloc, pods = await self._claim(pods, units)
-                uid = podutil.meta(pod).get("uid", "")
-                if uid not in self.partial:
-                    if not whole:
-                        reqs = [podutil.container_limit(c, self.profile.resource)
-                                for c in (pod.get("spec") or {}).get("containers", [])]
-                        reqs.remove(units)
-                        self.partial[uid] = [r for r in reqs if r > 0]
-                else:
-                    self.partial[uid].remove(units)
-                    if not self.partial[uid]:
-                        del self.partial[uid]
+                rec, alloc = await self.allocate_container(len(creq.devices_ids))
                 c = resp.container_responses.add()
                 for k, v in alloc.envs.items():
                     c.envs[k] = v
                 for k, v in alloc.annotations.items():
                     c.annotations[k] = v
+                c.annotations[POD_ANNOTATION] = f"{rec.key}/{rec.uid}"
                 for dspec in alloc.devices:
                     c.devices.add(**dspec)
             self.stats["allocate_ok"] += 1
             return resp
-        except AllocateError as e:
+        except (AllocateError, ApiError, OSError) as e:
             self.stats["allocate_fail"] += 1
             log.error("Allocate failed: %s", e)
             await context.abort(grpc.StatusCode.FAILED_PRECONDITION, str(e))
@@ -283,13 +289,71 @@ class GpuSharePlugin:
 
         totals = [self.units[i] for i in sorted(self.units)]
         inv = [{"index": d.index, "bdf": d.bdf, "uuid": d.uuid, "units": self.units[d.index],
-                "cu": d.cu_count, "partition": d.partition, "render": d.render_minor}
+                "total_bytes": d.total_bytes, "share_bytes": d.share_bytes, "cu": d.cu_count, "xcc": d.xcc_count,
+                "partition": d.partition, "render": d.render_minor, "card": d.card_minor}
                for d in sorted(self.devices.values(), key=lambda d: d.index)]
         await self.client.patch("nodes", self.node, {"metadata": {"annotations": {
             NODE_DEVICE_MEMORY_ANNOTATION: ",".join(str(t) for t in totals),
             NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv, separators=(",", ":"))}}})
         await self.client.patch("nodes", self.node, {"status": {"capacity": {
             self.profile.count: str(len(self.devices))}}}, sub="status")
+
+    def healthy(self) -> tuple[bool, str]:
+        if self._stopped:
+            return False, "stopped"
+        if not self.pods.synced.is_set():
+            return False, "pod informer not synced"
+        if self._server is None:
+            return False, "gRPC server not started"
+        return True, "ok"
+
+    def debug_state(self) -> dict:
+        return {"node": self.node, "resource": self.profile.resource, "unit": self.unit,
+                "devices": [{"index": d.index, "bdf": d.bdf, "healthy": d.healthy, "units": self.units[d.index],
+                             "cu": d.cu_count, "partition": d.partition} for d in self.devices.values()],
+                "informer": {"synced": self.pods.synced.is_set(), "relists": self.pods.relists,
+                             "rewatches": self.pods.rewatches, "events": self.pods.events},
+                "stats": dict(self.stats), **self.state.snapshot()}
+
+    def metrics_text(self) -> str:
+        lines = []
+        for k, v in sorted(self.stats.items()):
+            lines += [f"# TYPE gpushare_plugin_{k}_total counter", f"gpushare_plugin_{k}_total {v}"]
+        for k, v in sorted(self.state.stats.items()):
+            lines += [f"# TYPE gpushare_plugin_state_{k}_total counter", f"gpushare_plugin_state_{k}_total {v}"]
+        lines.append("# TYPE gpushare_plugin_device_healthy gauge")
+        lines += [f'gpushare_plugin_device_healthy{{device="{d.index}"}} {int(d.healthy)}' for d in self.devices.values()]
+        lines.append("# TYPE gpushare_plugin_cu_free gauge")
+        lines += [f'gpushare_plugin_cu_free{{device="{i}"}} {cp.free_count()}' for i, cp in self.state.cus.items()]
+        lines.append("# TYPE gpushare_plugin_allocate_candidates gauge")
+        lines.append(f"gpushare_plugin_allocate_candidates {len(self.state.candidates())}")
+        return "\n".join(lines) + "\n"
+
+    async def serve_debug(self, host: str, port: int) -> int:
+        """``/healthz``, ``/metrics`` (Prometheus text) and ``/debug/state`` (JSON) for problem determination."""
+        import json  # noqa: PLC0415
+
+        from aiohttp import web  # noqa: PLC0415
+
+        async def healthz(_):
+            ok, why = self.healthy()
+            return web.Response(status=200 if ok else 503, text=why)
+
+        async def metrics(_):
+            return web.Response(text=self.metrics_text(), content_type="text/plain")
+
+        async def state(_):
+            return web.Response(text=json.dumps(self.debug_state(), indent=1), content_type="application/json")
+
+        app = web.Application()
+        app.router.add_get("/healthz", healthz)
+        app.router.add_get("/metrics", metrics)
+        app.router.add_get("/debug/state", state)
+        self._debug = web.AppRunner(app, access_log=None)
+        await self._debug.setup()
+        site = web.TCPSite(self._debug, host, port)
+        await site.start()
+        return site._server.sockets[0].getsockname()[1]
 
     async def _watch_kubelet(self):
         """Re-register when kubelet restarts (it deletes and re-creates its socket)."""
@@ -340,7 +404,17 @@ class GpuSharePlugin:
                 elif ev["name"] == "GPU_POST_RESET":
                     self.set_health(ev["index"], True, "(post reset)")
 
-    async def start(self, register: bool = True, publish: bool = True):
+    async def start(self, register: bool = True, publish: bool = True, serve: bool = True,
+                    sync_timeout: float = 30.0):
+        # state first: CU partitions of running pods are rebuilt before the first Allocate can be served
+        if self._own_informer:
+            await self.pods.start()
+        try:
+            await self.pods.wait_synced(sync_timeout)
+        except asyncio.TimeoutError:
+            log.warning("pod informer of %s not synced after %.0fs; Allocate will LIST", self.node, sync_timeout)
+        if not serve:
+            return
         await self.serve()
         if publish:
             try:
@@ -359,6 +433,11 @@ class GpuSharePlugin:
         self._changed.set()
         for t in self._tasks:
             t.cancel()
+        if self._own_informer:
+            await self.pods.stop()
+        if self._debug is not None:
+            await self._debug.cleanup()
+            self._debug = None
         if self._server is not None:
             await self._server.stop(0.5)
         try:

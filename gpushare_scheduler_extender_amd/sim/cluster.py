@@ -121,11 +121,12 @@ NODEAGENT = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-nodeagen
 
 
 def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", workers: int = 32,
-                     native: bool = True) -> ChildProc:
+                     native: bool = True, plugin: str = "grpc") -> ChildProc:
     """kubelet + device-plugin Allocate + runtime stand-in for ``node``.
 
-    ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent);
-    otherwise ``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``.
+    ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent, its own Allocate matching);
+    otherwise ``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``: a kubelet stand-in driving
+    the shipped device plugin, over its unix socket (``plugin="grpc"``) or in-process (``"inproc"``).
     """
     if native:
         if not NODEAGENT.exists():
@@ -133,7 +134,7 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
         return ChildProc([str(NODEAGENT), "--node", node, "--apiserver", apiserver, "--profile", profile,
                           "--workers", str(min(workers, 16))], "node-agent")
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
-                      apiserver, "--profile", profile, "--workers", str(workers)], "node-agent")
+                      apiserver, "--profile", profile, "--workers", str(workers), "--plugin", plugin], "node-agent")
 
 
 SCHEDSIM = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-schedsim"

@@ -23,9 +23,14 @@ process), registers one node, creates pods and checks where they land:
    pool 8 times; a 64 GiB request that fits the node but no partition is filtered; 8 x 32 GiB pods
    land one per partition.
 
-``--gpu``: device sizes come from the real MI355X (devices beyond the box's GPUs are fakes of the
-same size) and configs 2 and 5 use a real HBM arena on GPU 0 (each pod's slice stamped and every
-resident slice verified by the admission kernel).  Without it everything is CPU-only.
+``--gpu``: device sizes come from the real MI355X and configs 2 and 5 use a real HBM arena on GPU 0
+(each pod's slice stamped and every resident slice verified by the admission kernel).  Configs 3 and
+4 use one real HBM arena per GPU when 8 GPUs are visible (an 8 x MI355X node); with fewer, the
+devices beyond the box's GPUs are fakes of the same size.  Without ``--gpu`` everything is CPU-only.
+
+``--agent``: who plays kubelet + device plugin.  ``plugin`` (default): the kubelet stand-in
+(``deviceplugin/agent.py``) drives the shipped gRPC :class:`GpuSharePlugin` over its unix socket;
+``inproc``: the same plugin called in-process; ``native``: the compiled ``gsx-nodeagent``.
 """
 from __future__ import annotations
 
@@ -38,31 +43,35 @@ import time
 from ..k8s.client import KubeClient
 from ..k8s.fasthttp import Client as HttpClient
 from ..k8s.objects import make_node, make_pod
-from ..models.profile import (ALIYUN, NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION, SHARED_GPU,
-                              NamingProfile)
+from ..models.profile import (ALIYUN, NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION,
+                              POD_CU_MASK_ANNOTATION, SHARED_GPU, NamingProfile)
 from .cluster import start_apiserver, start_extender, start_node_agent, start_scheduler
 
 GIB = 1 << 30
 NODE = "mi355x-node-0"
 CU_COUNT_ANNOTATION = "gpushare.amd.com/cu-count"
+AGENT = {"kind": "plugin"}  # --agent: plugin | inproc | native
 
 
 class Runtimes:
     """One pod runtime endpoint per device (native ``_engine.PodRuntime``): accounting only, or GPU 0's HBM arena."""
 
-    def __init__(self, n: int, unit_bytes: int, gib_per_dev: int, gpu: bool):
+    def __init__(self, n: int, unit_bytes: int, gib_per_dev: int, gpu: bool | int):
+        """``gpu``: False, True (GPU 0 backs device 0) or the number of leading devices backed by real GPUs."""
         from ..core.engine import native
 
         E = native()
+        n_real = int(gpu)
         self.rts, self.urls, self.bufs, self.streams = [], [], [], []
+        self.real = n_real
         for i in range(n):
             arena = gib_per_dev * unit_bytes
-            if gpu and i == 0:
+            if i < n_real:
                 from ..ops import hip
 
-                buf = hip.DeviceBuffer(0, arena)
-                st = hip.Stream(0)
-                rt = E.PodRuntime(0, arena, buf.addr(0), st.ptr, 1 << 20, hip.lib()._name)
+                buf = hip.DeviceBuffer(i, arena)
+                st = hip.Stream(i)
+                rt = E.PodRuntime(i, arena, buf.addr(0), st.ptr, 1 << 20, hip.lib()._name)
                 self.bufs.append(buf)
                 self.streams.append(st)
             else:
@@ -89,8 +98,9 @@ class Runtimes:
 class Cluster:
     """apiserver + extender + scheduler + node agent (child processes) and one node with ``len(totals)`` devices."""
 
-    def __init__(self, profile: NamingProfile, totals: list[int], gpu: bool, cu_count: int = 256,
-                 native: bool = True, partition: str = "SPX"):
+    def __init__(self, profile: NamingProfile, totals: list[int], gpu: bool | int, cu_count: int = 256,
+                 native: bool = True, partition: str = "SPX", xcc_count: int = 8, agent: str | None = None,
+                 pool_gib: int = 0):
         self.profile = profile
         self.totals = totals
         self.children = []
@@ -100,15 +110,22 @@ class Cluster:
         self.children.append(self.ext)
         # native: compiled kube-scheduler / node-agent stand-ins; otherwise the asyncio ones
         self.children.append(start_scheduler(self.api.url, self.ext.url, profile=profile.name, native=native))
-        self.children.append(start_node_agent(self.api.url, NODE, profile=profile.name, native=native))
+        self.agent_kind = agent or AGENT["kind"]
+        self.children.append(start_node_agent(self.api.url, NODE, profile=profile.name,
+                                              native=self.agent_kind == "native",
+                                              plugin="inproc" if self.agent_kind == "inproc" else "grpc"))
         self.rt = Runtimes(len(totals), GIB, max(totals), gpu)
         self.cu_count = cu_count
+        self.xcc_count = xcc_count
         self.partition = partition
+        self.pool_gib = pool_gib  # partitions sharing one HBM pool: each reports the pool, owns a share
 
     async def start(self):
         self.c = KubeClient(self.api.url)
-        inv = [{"index": i, "bdf": f"0000:{0x10 + i:02x}:00.0", "uuid": f"gpu-{i}", "units": t, "total_bytes": t * GIB,
-                "cu": self.cu_count, "render": 128 + i, "card": i, "partition": self.partition} for i, t in enumerate(self.totals)]
+        inv = [{"index": i, "bdf": f"0000:{0x10 + i:02x}:00.0", "uuid": f"gpu-{i}", "units": t,
+                "total_bytes": (self.pool_gib or t) * GIB, "share_bytes": t * GIB if self.pool_gib else 0,
+                "cu": self.cu_count, "xcc": self.xcc_count, "render": 128 + i, "card": i, "partition": self.partition}
+               for i, t in enumerate(self.totals)]
         node = make_node(NODE, sum(self.totals), len(self.totals), profile=self.profile, device_totals=self.totals,
                          annotations={NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv),
                                       NODE_RUNTIME_ENDPOINTS_ANNOTATION: json.dumps(
@@ -190,6 +207,15 @@ def _gpu_gib() -> int:
     return hip.mem_info(0)[1] // GIB
 
 
+def _real_gpus(gpu: bool, want: int) -> int:
+    """How many of ``want`` devices real GPUs back: all of them on a node with that many, else none."""
+    if not gpu:
+        return 0
+    import torch
+
+    return want if torch.cuda.device_count() >= want else 0
+
+
 async def config1(gpu: bool) -> dict:
     cl = Cluster(SHARED_GPU, [16], gpu=False)
     try:
@@ -229,7 +255,8 @@ async def config2(gpu: bool) -> dict:
 
 async def config3(gpu: bool) -> dict:
     per = _gpu_gib() if gpu else 268
-    cl = Cluster(ALIYUN, [per] * 8, gpu=False)
+    real = _real_gpus(gpu, 8)
+    cl = Cluster(ALIYUN, [per] * 8, gpu=real)
     try:
         await cl.start()
         t0 = time.perf_counter()
@@ -241,16 +268,21 @@ async def config3(gpu: bool) -> dict:
             per_dev[cl.device_of(p)] += 64
         insp = await cl.inspect()
         used = insp["nodes"][0]["usedGPU"]
-        ok = per_dev == [256] * 8 and used == 256 * 8
+        bad = cl.rt.verify() if real else 0
+        resident = [st.get("resident") for st in cl.rt.stats()]
+        ok = per_dev == [256] * 8 and used == 256 * 8 and bad == 0
+        if real:  # 32 x 64 GiB co-resident in 8 real HBM arenas, 4 slices each
+            ok = ok and resident == [4] * 8
         return {"ok": ok, "per_device_gib": per_dev, "device_gib": per, "util_pct": round(100 * used / (8 * per), 2),
-                "seconds": round(dt, 4)}
+                "real_gpus": real, "resident_slices": resident, "bad_stamps": bad, "seconds": round(dt, 4)}
     finally:
         await cl.close()
 
 
 async def config4(gpu: bool) -> dict:
     per = _gpu_gib() if gpu else 268
-    cl = Cluster(ALIYUN, [per] * 8, gpu=False)
+    real = _real_gpus(gpu, 8)
+    cl = Cluster(ALIYUN, [per] * 8, gpu=real)
     try:
         await cl.start()
         for i in range(8):
@@ -260,7 +292,7 @@ async def config4(gpu: bool) -> dict:
         free_dev = per - 200
         free_node = 8 * free_dev
         out = {"device_gib": per, "fill": "8 x 200 GiB", "placed_devices": placed, "free_per_device_gib": free_dev,
-               "free_on_node_gib": free_node, "requests": []}
+               "free_on_node_gib": free_node, "real_gpus": real, "requests": []}
         ok = placed == list(range(8))
         for name, gib in (("req-100", 100), ("req-200", 200), ("req-50", 50)):
             pod = make_pod(name, gib, profile=ALIYUN)
@@ -278,6 +310,9 @@ async def config4(gpu: bool) -> dict:
                 ok = ok and fits_aggregate and f["NodeNames"] == [] and \
                     rec["failed_reason"] == "Insufficient GPU Memory in one device" and rec["pending_after_0.5s"]
             out["requests"].append(rec)
+        if real:
+            out["bad_stamps"] = cl.rt.verify()
+            ok = ok and out["bad_stamps"] == 0
         out["ok"] = ok
         return out
     finally:
@@ -292,18 +327,20 @@ async def config5(gpu: bool) -> dict:
         for i in range(4):
             await cl.create(f"cu-{i}", 64, annotations={CU_COUNT_ANNOTATION: "64"})
         pods = await cl.wait([f"cu-{i}" for i in range(4)])
+        from ..deviceplugin.allocator import CUPartitioner
+        from ..deviceplugin.state import parse_cu_mask
+
         parts = []
         for name in sorted(pods):
-            env = (await cl.allocation(pods[name]["metadata"]["uid"])).get("envs", {})
-            words = [int(w, 16) for w in env.get("GSX_CU_MASK", "").split(",") if w]
-            cus = [32 * wi + b for wi, w in enumerate(words) for b in range(32) if w >> b & 1]
-            parts.append({"pod": name, "HSA_CU_MASK": env.get("HSA_CU_MASK", ""), "cus": cus})
+            # the partition the device plugin committed with ASSIGNED=true (and handed to the container)
+            cus = parse_cu_mask(pods[name]["metadata"]["annotations"].get(POD_CU_MASK_ANNOTATION, ""))
+            parts.append({"pod": name, "HSA_CU_MASK": f"0:{CUPartitioner.ranges(cus)}", "cus": cus})
         sets = [set(p["cus"]) for p in parts]
         disjoint = all(not (sets[i] & sets[j]) for i in range(4) for j in range(i + 1, 4))
         per_xcd = [sorted({c // 32 for c in s}) for s in sets]
         ok = disjoint and all(len(s) == 64 for s in sets) and all(x == list(range(8)) for x in per_xcd)
-        out = {"device_gib": total, "partitions": [{"pod": p["pod"], "HSA_CU_MASK": p["HSA_CU_MASK"],
-                                                   "n_cus": len(p["cus"])} for p in parts],
+        out = {"device_gib": total, "agent": cl.agent_kind,
+               "partitions": [{"pod": p["pod"], "HSA_CU_MASK": p["HSA_CU_MASK"], "n_cus": len(p["cus"])} for p in parts],
                "disjoint": disjoint, "xcds_per_pod": [len(x) for x in per_xcd]}
         if gpu:
             from ..ops import hip
@@ -333,7 +370,8 @@ async def config6(gpu: bool) -> dict:
     devs = apply_memory_pools(fake_devices(f"1x{total}GiB:CPX:NPS1"), "auto")
     shares = [d.units("GiB") for d in devs]
     raw = [d.total_bytes // GIB for d in devs]
-    cl = Cluster(ALIYUN, shares, gpu=False, cu_count=devs[0].cu_count, partition="CPX")
+    cl = Cluster(ALIYUN, shares, gpu=False, cu_count=devs[0].cu_count, xcc_count=devs[0].xcc_count, partition="CPX",
+                 pool_gib=total)
     try:
         await cl.start()
         f = await cl.filter(make_pod("req-64", 64, profile=ALIYUN))
@@ -344,11 +382,17 @@ async def config6(gpu: bool) -> dict:
         placed = sorted(cl.device_of(p) for p in pods.values())
         insp = await cl.inspect()
         used, node_total = insp["nodes"][0]["usedGPU"], insp["nodes"][0]["totalGPU"]
+        # the container's memory fraction is of the pool its partition sees, not of the partition
+        env = (await cl.allocation(pods[names[0]]["metadata"]["uid"])).get("envs", {})
+        frac = float(env.get("GSX_GPU_MEM_FRACTION", "nan"))
+        want = 32 / shares[0] * (shares[0] / total)
         ok = (len(devs) == 8 and sum(shares) <= total and f["NodeNames"] == []
-              and reason == "Insufficient GPU Memory in one device" and placed == list(range(8)) and used == 256)
+              and reason == "Insufficient GPU Memory in one device" and placed == list(range(8)) and used == 256
+              and abs(frac - want) < 1e-4)
         return {"ok": ok, "gpu_gib": total, "logical_devices": len(devs), "reported_gib_per_partition": raw[0],
                 "advertised_gib_per_partition": shares, "node_gpu_mem": node_total, "cus_per_partition": devs[0].cu_count,
-                "req64_filtered": reason, "placed_devices": placed, "used_gib": used}
+                "req64_filtered": reason, "placed_devices": placed, "used_gib": used, "mem_fraction": frac,
+                "mem_fraction_expected": round(want, 6)}
     finally:
         await cl.close()
 
@@ -367,8 +411,12 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpu", action="store_true", help="real MI355X sizes, HBM arena and CU probe (needs a GPU)")
     ap.add_argument("--only", default="", help="comma-separated config numbers")
+    ap.add_argument("--agent", default="plugin", choices=["plugin", "inproc", "native"],
+                    help="kubelet + device plugin: the shipped gRPC plugin driven over its socket (default), "
+                         "the same in-process, or the compiled gsx-nodeagent")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args(argv)
+    AGENT["kind"] = a.agent
     which = [int(x) for x in a.only.split(",") if x] or sorted(CONFIGS)
     report = {}
     for k in which:

@@ -74,6 +74,9 @@ struct Device {
   std::string bdf;
   int cu = 256, xcc = 8;
   int render = -1, card = -1;
+  // a partition sharing one HBM pool (CPX/NPS1): its process sees the whole pool, so the memory
+  // fraction is scaled by share/total (deviceplugin/allocator.py build_response)
+  int64_t total_bytes = 0, share_bytes = 0;
   std::string endpoint;
 };
 
@@ -116,6 +119,26 @@ class CuPartitioner {
     for (int c : h->second) owner_[static_cast<size_t>(c)].clear();
     held_.erase(h);
   }
+  // An existing partition (a pod's cu-mask annotation, e.g. after a restart); CUs another pod owns stay
+  // with it.  Returns how many clashed (deviceplugin/allocator.py CUPartitioner.adopt).
+  int adopt(const std::string& uid, const std::vector<int>& cus) {
+    int clash = 0;
+    std::vector<int>& mine = held_[uid];
+    for (int c : cus) {
+      if (c < 0 || c >= cu_) continue;
+      std::string& o = owner_[static_cast<size_t>(c)];
+      if (!o.empty() && o != uid) {
+        ++clash;
+        continue;
+      }
+      if (o.empty()) mine.push_back(c);
+      o = uid;
+    }
+    std::sort(mine.begin(), mine.end());
+    if (mine.empty()) held_.erase(uid);
+    return clash;
+  }
+  bool holds(const std::string& uid) const { return held_.count(uid) != 0; }
   int cu_count() const { return cu_; }
 
  private:
@@ -134,6 +157,23 @@ std::string cu_words(const std::vector<int>& cus, int cu_count) {
     o.append(b);
   }
   return o;
+}
+
+std::vector<int> parse_cu_words(const std::string& words) {
+  std::vector<int> out;
+  size_t i = 0;
+  int wi = 0;
+  while (i < words.size()) {
+    size_t j = words.find(',', i);
+    if (j == std::string::npos) j = words.size();
+    unsigned long v = std::strtoul(words.substr(i, j - i).c_str(), nullptr, 16);
+    for (int b = 0; b < 32; ++b) {
+      if (v >> b & 1ul) out.push_back(32 * wi + b);
+    }
+    ++wi;
+    i = j + 1;
+  }
+  return out;
 }
 
 std::string cu_ranges(const std::vector<int>& cus) {
@@ -156,6 +196,7 @@ struct AgentPod {
   int assigned = -1;
   bool complete = false;
   int cu_count = 0;
+  std::string cu_mask;
 };
 
 struct Cand {
@@ -300,6 +341,10 @@ class Agent {
       geti("xcc", &d.xcc);
       geti("render", &d.render);
       geti("card", &d.card);
+      int64_t tb = di.find(i, "total_bytes");
+      if (tb >= 0) di.as_int(static_cast<uint32_t>(tb), &d.total_bytes);
+      int64_t sb = di.find(i, "share_bytes");
+      if (sb >= 0) di.as_int(static_cast<uint32_t>(sb), &d.share_bytes);
       int64_t b = di.find(i, "bdf");
       if (b >= 0) d.bdf = di.str(static_cast<uint32_t>(b));
       int64_t ep = de.find(0, std::to_string(d.index));
@@ -337,20 +382,32 @@ class Agent {
     ap.dev_total = v.annot_dev_total;
     ap.complete = v.complete();
     ap.cu_count = 0;
+    ap.cu_mask.clear();
     int64_t an = d.path(obj, {"metadata", "annotations"});
     if (an >= 0) {
       int64_t c = d.find(static_cast<uint32_t>(an), kCuCountAnn);
       if (c >= 0) ap.cu_count = std::atoi(d.str(static_cast<uint32_t>(c)).c_str());
+      int64_t m = d.find(static_cast<uint32_t>(an), kCuMaskAnn);
+      if (m >= 0) ap.cu_mask = d.str(static_cast<uint32_t>(m));
     }
     const std::string& uid = ap.uid;
     if (ap.complete) {
       cands_.erase(uid);
       stop_pod_locked(uid);
+      release_cus_locked(uid);  // also for pods this agent did not start (e.g. before a restart)
       return key;
     }
     if (ap.request <= 0 || !devices_.count(static_cast<int>(ap.dev_idx))) {
       cands_.erase(uid);
       return key;
+    }
+    // an assigned pod owns the partition recorded on it: rebuilt after a restart, never handed out twice
+    if (ap.assigned == 1 && !ap.cu_mask.empty()) {
+      auto cp = cus_.find(static_cast<int>(ap.dev_idx));
+      if (cp != cus_.end() && !cp->second.holds(uid)) {
+        int clash = cp->second.adopt(uid, parse_cu_words(ap.cu_mask));
+        if (clash) std::fprintf(stderr, "[gsx-nodeagent] %s: %d CU(s) already owned\n", key.c_str(), clash);
+      }
     }
     if (ap.assigned == 0 && (ap.phase == "Pending" || ap.phase.empty())) {
       cands_[uid] = Cand{ap.assume_time, key, ap.request};
@@ -373,6 +430,12 @@ class Agent {
     pods_.erase(it);
     cands_.erase(uid);
     stop_pod_locked(uid);
+    release_cus_locked(uid);
+  }
+
+  void release_cus_locked(const std::string& uid) {
+    if (inflight_.count(uid)) return;  // the admitting worker owns it until its patch resolves
+    for (auto& kv : cus_) kv.second.release(uid);
   }
 
   void stop_pod_locked(const std::string& uid) {
@@ -430,8 +493,11 @@ class Agent {
     // deviceplugin/allocator.py build_response, mount_mode "isolated": only this GPU's nodes are mounted
     const std::string visible = "0";
     char frac[32];
-    std::snprintf(frac, sizeof(frac), "%.6f",
-                  pod.dev_total > 0 ? static_cast<double>(pod.request) / static_cast<double>(pod.dev_total) : 0.0);
+    double f = pod.dev_total > 0 ? static_cast<double>(pod.request) / static_cast<double>(pod.dev_total) : 0.0;
+    if (dev.share_bytes > 0 && dev.total_bytes > dev.share_bytes) {
+      f *= static_cast<double>(dev.share_bytes) / static_cast<double>(dev.total_bytes);
+    }
+    std::snprintf(frac, sizeof(frac), "%.6f", f);
     std::vector<std::pair<std::string, std::string>> env = {
         {"HIP_VISIBLE_DEVICES", visible},
         {"ROCR_VISIBLE_DEVICES", visible},

@@ -6,12 +6,12 @@ import tempfile
 import pytest
 
 from gpushare_scheduler_extender_amd.deviceplugin import api
-from gpushare_scheduler_extender_amd.deviceplugin.allocator import (CU_COUNT_ANNOTATION, CUPartitioner, build_response,
-                                                                   candidate_pods, pick_pod)
+from gpushare_scheduler_extender_amd.deviceplugin.allocator import CU_COUNT_ANNOTATION, CUPartitioner, build_response
 from gpushare_scheduler_extender_amd.deviceplugin.agent import NodeAgent
 from gpushare_scheduler_extender_amd.deviceplugin.devices import Device, discover, fake_devices
 from gpushare_scheduler_extender_amd.deviceplugin.plugin import FakeKubelet, GpuSharePlugin, PluginClient, fake_ids
 from gpushare_scheduler_extender_amd.deviceplugin.runtime import AdmissionError, LedgerRuntime
+from gpushare_scheduler_extender_amd.deviceplugin.state import AllocationState
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient
 from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
 from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
@@ -30,14 +30,68 @@ def bound_pod(name, mem, node="n1", dev=0, assume=1, assigned="false", dev_total
 
 # ---------------------------------------------------------------- allocator (pure)
 
+def _state(spec="2x16GiB"):
+    return AllocationState("n1", {d.index: d for d in fake_devices(spec)}, P)
+
+
 def test_candidate_order_and_pick_by_size():
+    st = _state()
     pods = [bound_pod("late", 8, assume=30), bound_pod("early", 8, assume=10), bound_pod("other", 4, assume=5),
             bound_pod("done", 8, assume=1, assigned="true"), bound_pod("elsewhere", 8, node="n2", assume=1),
-            bound_pod("running", 8, assume=2, phase="Running")]
-    assert [p["metadata"]["name"] for p in candidate_pods(pods, "n1", P)] == ["other", "early", "late"]
-    assert pick_pod(pods, "n1", 8, P)["metadata"]["name"] == "early"
-    assert pick_pod(pods, "n1", 4, P)["metadata"]["name"] == "other"
-    assert pick_pod(pods, "n1", 3, P) is None
+            bound_pod("running", 8, assume=2, phase="Running"), bound_pod("gpu7", 8, dev=7, assume=0)]
+    st.resync(pods)
+    assert [r.name for r in st.candidates()] == ["other", "early", "late"]
+    assert st.match(8)[0].name == "early"
+    assert st.match(4)[0].name == "other"
+    assert st.match(3) == (None, False)
+    st.inflight.add(st.match(8)[0].uid)  # a claim in flight is never matched twice
+    assert st.match(8)[0].name == "late"
+
+
+def test_state_releases_cus_and_partial_on_completion_and_delete():
+    st = _state("1x64GiB")
+    a = bound_pod("a", 16, annotations={CU_COUNT_ANNOTATION: "64"})
+    mc = bound_pod("mc", [8, 4], assume=2)
+    st.resync([a, mc])
+    rec, whole = st.match(16)
+    assert rec.name == "a" and whole and len(st.claim_cus(rec)) == 64 and st.cus[0].free_count() == 192
+    rec2, whole2 = st.match(8)
+    assert rec2.name == "mc" and not whole2
+    st.first_container_committed(rec2, 8, whole2)
+    assert st.partial[rec2.uid] == [4]
+    # a completes (Succeeded): its CUs come back; mc is deleted: its partial entry goes
+    st.observe(bound_pod("a", 16, phase="Succeeded", uid=rec.uid, annotations={CU_COUNT_ANNOTATION: "64"}))
+    assert st.cus[0].free_count() == 256 and st.stats["cu_released"] == 64
+    st.forget(mc)
+    assert not st.partial and not st.pods
+
+
+def test_state_rebuilds_cu_ownership_from_annotations():
+    """After a plugin restart the running pods' partitions are taken from their cu-mask annotations."""
+    from gpushare_scheduler_extender_amd.models.profile import POD_CU_MASK_ANNOTATION
+
+    first = _state("1x64GiB")
+    run = []
+    for i in range(3):
+        p = bound_pod(f"r{i}", 8, assume=i, annotations={CU_COUNT_ANNOTATION: "64"})
+        first.observe(p)
+        rec, _ = first.match(8)
+        words = build_response(p, first.devices[0], 8, P, cus=first.claim_cus(rec)).envs["GSX_CU_MASK"]
+        run.append(bound_pod(f"r{i}", 8, assume=i, assigned="true", phase="Running", uid=rec.uid,
+                             annotations={CU_COUNT_ANNOTATION: "64", POD_CU_MASK_ANNOTATION: words}))
+        first.observe(run[-1])
+    fresh = _state("1x64GiB")
+    new = bound_pod("new", 8, assume=9, annotations={CU_COUNT_ANNOTATION: "64"})
+    fresh.resync(run + [new])
+    assert fresh.cus[0].free_count() == 64 and fresh.stats["cu_adopted"] == 3
+    rec, _ = fresh.match(8)
+    got = set(fresh.claim_cus(rec))
+    held = {c for u, cs in fresh.cus[0].held().items() if u != rec.uid for c in cs}
+    assert len(got) == 64 and not got & held
+    # a pending ASSIGNED=true multi-container pod: progress unknown after restart, all sizes accepted
+    mc = bound_pod("mc", [8, 4], assume=3, assigned="true")
+    fresh.observe(mc)
+    assert sorted(fresh.partial[mc["metadata"]["uid"]]) == [4, 8]
 
 
 def test_build_response_env_and_devices():
@@ -447,3 +501,137 @@ def test_process_runtime_starts_container_with_allocate_env():
         assert env["SHARED_GPU_MEM_CONTAINER"] == "200"
         used.add(env["HIP_VISIBLE_DEVICES"])
     assert used == {"0", "1"}  # 200 + 200 GiB cannot share one 288 GB device
+
+
+# ---------------------------------------------------------------- plugin lifecycle
+
+class _PluginStack:
+    """fake apiserver + the shipped gRPC plugin + the kubelet stand-in talking to it over its unix socket."""
+
+    def __init__(self, spec="1x268GiB"):
+        self.spec = spec
+
+    async def __aenter__(self):
+        self.api = await FakeApiServerRunner().start()
+        self.client = KubeClient(self.api.url)
+        self.dir = tempfile.mkdtemp(prefix="gsx-dp-")
+        self.devs = fake_devices(self.spec)
+        totals = [d.units("GiB") for d in self.devs]
+        await self.client.create("nodes", make_node("n1", sum(totals), len(totals), device_totals=totals))
+        self.plugin = await self.start_plugin()
+        self.rt = LedgerRuntime({d.index: d.units("GiB") * GIB for d in self.devs})
+        self.agent = NodeAgent(KubeClient(self.api.url), "n1", self.devs, P, self.rt,
+                               plugin_socket=self.plugin.socket_path)
+        await self.agent.start()
+        return self
+
+    async def start_plugin(self):
+        plugin = GpuSharePlugin(KubeClient(self.api.url), "n1", self.devs, P, socket_dir=self.dir)
+        await plugin.start(register=False)
+        return plugin
+
+    async def restart_plugin(self):
+        await self.plugin.stop()
+        await self.plugin.client.close()
+        self.plugin = await self.start_plugin()  # same socket path: the kubelet stand-in reconnects
+
+    async def wait(self, pred, timeout=10.0):
+        for _ in range(int(timeout / 0.01)):
+            if pred():
+                return
+            await asyncio.sleep(0.01)
+        raise TimeoutError("condition not reached")
+
+    async def phase(self, name):
+        return (await self.client.get("pods", name, "default"))["status"].get("phase")
+
+    async def wait_phase(self, name, phase="Running", timeout=10.0):
+        for _ in range(int(timeout / 0.01)):
+            if await self.phase(name) == phase:
+                return await self.client.get("pods", name, "default")
+            await asyncio.sleep(0.01)
+        raise TimeoutError(f"{name} not {phase}: {await self.phase(name)}")
+
+    async def __aexit__(self, *exc):
+        await self.agent.stop()
+        await self.agent.client.close()
+        await self.plugin.stop()
+        await self.plugin.client.close()
+        await self.client.close()
+        await self.api.stop()
+
+
+def _cus_of(pod):
+    from gpushare_scheduler_extender_amd.deviceplugin.state import parse_cu_mask
+    from gpushare_scheduler_extender_amd.models.profile import POD_CU_MASK_ANNOTATION
+
+    return set(parse_cu_mask(pod["metadata"]["annotations"][POD_CU_MASK_ANNOTATION]))
+
+
+def test_cu_partitions_are_released_when_pods_go_away():
+    """Done-criterion (a): 64-CU pods keep allocating across deletes; before the fix the fifth failed forever."""
+    async def go():
+        async with _PluginStack() as s:
+            cu = {CU_COUNT_ANNOTATION: "64"}
+            for i in range(4):
+                await s.client.create("pods", bound_pod(f"p{i}", 16, assume=i, annotations=cu))
+            pods = [await s.wait_phase(f"p{i}") for i in range(4)]
+            sets = [_cus_of(p) for p in pods]
+            assert all(len(x) == 64 for x in sets) and len(set().union(*sets)) == 256
+            assert s.plugin.state.cus[0].free_count() == 0
+            # the node's CUs are all taken: a fifth partition needs a pod to go away first
+            await s.client.delete("pods", "p1", "default")
+            await s.wait(lambda: s.plugin.state.cus[0].free_count() == 64)
+            await s.client.create("pods", bound_pod("p4", 16, assume=4, annotations=cu))
+            p4 = await s.wait_phase("p4")
+            assert _cus_of(p4) == sets[1]
+            # five sequential pods, each deleted before the next: all allocate
+            for i in (0, 2, 3, 4):
+                await s.client.delete("pods", f"p{i}", "default")
+            await s.wait(lambda: s.plugin.state.cus[0].free_count() == 256)
+            for i in range(5):
+                await s.client.create("pods", bound_pod(f"s{i}", 16, assume=10 + i, annotations=cu))
+                assert len(_cus_of(await s.wait_phase(f"s{i}"))) == 64
+                await s.client.delete("pods", f"s{i}", "default")
+            await s.wait(lambda: s.plugin.state.cus[0].free_count() == 256 and not s.plugin.state.pods)
+            assert s.plugin.stats["allocate_fail"] == 0 and s.agent.failed == 0
+            # a Succeeded pod (not deleted) also gives its partition back
+            await s.client.create("pods", bound_pod("job", 16, assume=30, annotations=cu))
+            await s.wait_phase("job")
+            await s.client.patch("pods", "job", {"status": {"phase": "Succeeded"}}, "default", sub="status")
+            await s.wait(lambda: s.plugin.state.cus[0].free_count() == 256)
+    run(go())
+
+
+def test_plugin_restart_rebuilds_partitions_from_annotations():
+    """Done-criterion (b): after a restart the new pod's CU mask is disjoint from every running pod's."""
+    async def go():
+        async with _PluginStack() as s:
+            cu = {CU_COUNT_ANNOTATION: "64"}
+            for i in range(3):
+                await s.client.create("pods", bound_pod(f"r{i}", 16, assume=i, annotations=cu))
+            running = [_cus_of(await s.wait_phase(f"r{i}")) for i in range(3)]
+            await s.restart_plugin()
+            assert s.plugin.state.cus[0].free_count() == 64  # rebuilt before serving
+            assert s.plugin.state.stats["cu_adopted"] == 3
+            await s.client.create("pods", bound_pod("new", 16, assume=9, annotations=cu))
+            new = _cus_of(await s.wait_phase("new"))
+            assert len(new) == 64 and all(not new & r for r in running)
+            # and a fifth partition does not exist until one goes away
+            await s.client.create("pods", bound_pod("extra", 16, assume=10, annotations=cu))
+            await s.wait_phase("extra", "Failed")
+            assert s.plugin.stats["allocate_fail"] >= 1
+    run(go())
+
+
+def test_multi_container_progress_survives_restart_and_is_released():
+    async def go():
+        async with _PluginStack() as s:
+            await s.client.create("pods", bound_pod("mc", [10, 20], assume=1))
+            await s.wait_phase("mc")
+            env = s.agent.allocations[(await s.client.get("pods", "mc", "default"))["metadata"]["uid"]]
+            assert env["SHARED_GPU_MEM_POD"] == "30"
+            assert not s.plugin.state.partial  # both containers allocated, pod Running
+            await s.client.delete("pods", "mc", "default")
+            await s.wait(lambda: not s.plugin.state.pods)
+    run(go())
