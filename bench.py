@@ -21,7 +21,21 @@ every step is one *wave* of ``pods_per_gpu x N`` pods of ``pod_gib`` GiB
 Timed region: exactly K steps bracketed by barrier + torch.cuda.synchronize()
 on both sides; the max over ranks is reported.  ``value`` = pods bound per
 second over the whole job (all GPUs).  Synthetic pods; no cluster, no real
-kubelet (there is none in this environment) — see SURVEY.md §4.
+kubelet (there is none in this environment) — see SURVEY.md §4.  ``dtype`` is
+"n/a": the timed region does no floating-point work (the GPU work is the HIP
+stamp / verify of each pod's HBM slice).
+
+Stability: every control-plane process is pinned to its own physical core
+(``--pin``, utils/cpuset.py) and the per-wave distribution is reported next to
+``value`` (``wave_pods_per_s``: p50 and IQR).
+
+After the timed region rank 0 runs ``latency_sweep`` (extra keys, not part of
+``value``): the same waves with the fake kube-apiserver answering every
+non-watch request after 0 / 1 / 2 / 5 ms, for ``--bind-mode binding`` (one
+``pods/binding`` POST per pod) and ``update`` (the reference's PUT + POST), and
+``reference_client``: ``update`` mode behind client-go's default token bucket
+(QPS 5, burst 10 — what the reference runs with, ``cmd/main.go:76-82``) next to
+``binding`` mode behind the same bucket: the same-condition comparison.
 """
 from __future__ import annotations
 
@@ -135,6 +149,89 @@ def pct(xs, q):
     return xs[k]
 
 
+def wave_dist(xs) -> dict:
+    if not xs:
+        return {}
+    p25, p50, p75 = pct(xs, 25), pct(xs, 50), pct(xs, 75)
+    return {"p50": round(p50, 1), "p25": round(p25, 1), "p75": round(p75, 1),
+            "iqr_pct": round(100 * (p75 - p25) / p50, 1) if p50 else None, "n": len(xs)}
+
+
+def set_latency(api_batch, ms: float):
+    st, b = api_batch.run([("POST", "/fake/faults", json.dumps({"latency_ms": ms}).encode())], 1)[0]
+    if st != 200:
+        raise RuntimeError(f"setting apiserver latency failed: {st} {b[:200]!r}")
+
+
+SWEEP_LATENCIES_MS = (0, 1, 2, 5)
+
+
+def latency_sweep(a, children, api_url, api_batch, wave, fetch_timings, lt, n_pods, first_step, inspect_used):
+    """Waves of the headline shape with the apiserver answering after L ms, for both bind modes, and behind
+    client-go's default token bucket (QPS 5 / burst 10, the reference's client).  Rank 0 only; untimed by the
+    driver's headline.  Returns (sweep rows, reference_client rows)."""
+    from gpushare_scheduler_extender_amd.sim.cluster import start_extender
+
+    step = [first_step]
+
+    def restart_extender(mode: str, qps: float = 0.0, burst: int = 1000):
+        old = next(c for c in children if c.name == "extender")
+        old.stop()
+        new = start_extender(api_url, profile=a.profile, bind_mode=mode, port=old.port, cpus=old.cpus,
+                             kube_qps=qps, kube_burst=burst)
+        children[children.index(old)] = new
+        deadline = time.perf_counter() + 60
+        while True:  # serving and synced: the node is in its ledger
+            try:
+                if inspect_used().get("nodes"):
+                    return
+            except Exception:  # noqa: BLE001 - connection refused while it starts
+                pass
+            if time.perf_counter() > deadline:
+                raise TimeoutError("restarted extender never saw the node")
+            time.sleep(0.01)
+
+    def measure(warm: int, steps: int) -> dict:
+        for _ in range(warm):
+            wave(step[0])
+            step[0] += 1
+        rs = []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            rs.append(wave(step[0]))
+            step[0] += 1
+        dt = time.perf_counter() - t0
+        lat, rtt = [], []
+        for r in rs:
+            for t in lt.run(fetch_timings(r["keys"]), 60):
+                lat.append(t["bound"] - t["seen"])
+                rtt.append(t["bind_rtt"])
+        return {"pods_per_s": round(n_pods * steps / dt, 1),
+                "wave_ms_p50": round(1e3 * pct([r["t_total"] for r in rs], 50), 3),
+                "p50_bind_latency_ms": round(1e3 * pct(lat, 50), 3), "p99_bind_latency_ms": round(1e3 * pct(lat, 99), 3),
+                "p50_bind_rtt_ms": round(1e3 * pct(rtt, 50), 3), "pods": n_pods * steps}
+
+    rows, mode = [], a.bind_mode
+    for m in ("binding", "update"):
+        if m != mode:
+            restart_extender(m)
+            mode = m
+        for ms in SWEEP_LATENCIES_MS:
+            set_latency(api_batch, ms)
+            rows.append({"bind_mode": m, "api_latency_ms": ms, **measure(1, a.sweep_steps)})
+    set_latency(api_batch, 0)
+    # the reference's client: client-go defaults QPS 5 / burst 10 (cmd/main.go:76-82 never overrides them).
+    # The warm-up waves drain the burst, so the timed waves see the sustained rate.
+    ref = []
+    for m, calls in (("update", 2), ("binding", 1)):
+        restart_extender(m, qps=5.0, burst=10)
+        row = measure(3, 3)
+        ref.append({"bind_mode": m, "kube_qps": 5, "kube_burst": 10, "apiserver_calls_per_bind": calls,
+                    "derived_ceiling_pods_per_s": round(5.0 / calls, 2), **row})
+    restart_extender(a.bind_mode)
+    return rows, ref
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -155,8 +252,15 @@ def parse():
                     help="kube-scheduler stand-in: compiled gsx-schedsim (default) or the asyncio simulator")
     ap.add_argument("--apiserver", default="native", choices=["native", "python"],
                     help="fake kube-apiserver: gsx-fakeapi (default) or the asyncio one")
-    ap.add_argument("--node-agent", default="native", choices=["native", "python"],
-                    help="node agent (kubelet + device-plugin Allocate stand-in): gsx-nodeagent (default) or asyncio")
+    ap.add_argument("--node-agent", default="native", choices=["native", "plugin", "inproc"],
+                    help="kubelet + device plugin: gsx-nodeagent (default), or the kubelet stand-in driving the "
+                         "shipped gRPC device plugin over its unix socket (plugin) / in-process (inproc)")
+    ap.add_argument("--pin", default="auto", choices=["auto", "spread", "compact", "none"],
+                    help="CPU placement of the control-plane processes (auto = spread when there are enough cores)")
+    ap.add_argument("--api-latency-ms", type=float, default=0.0,
+                    help="fake kube-apiserver answers every non-watch request after this delay (timed region)")
+    ap.add_argument("--sweep", type=int, default=1, help="1: run the latency sweep after the timed region")
+    ap.add_argument("--sweep-steps", type=int, default=8)
     ap.add_argument("--inproc", action="store_true",
                     help="run apiserver + extender in this process (no child processes; used under rocprofv3)")
     return ap.parse_args()
@@ -178,6 +282,15 @@ def main():
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run --nproc-per-node N")
         a.gpus = world
 
+    # ---- CPU placement (the same plan on every rank: each takes its own slot)
+    from gpushare_scheduler_extender_amd.utils.cpuset import pin_self, plan
+
+    names = ["rank0", "apiserver", "extender", "scheduler", "node-agent"] + [f"rank{r}" for r in range(1, world)]
+    widths = {"extender": 2, "node-agent": 2}
+    mode = a.pin if a.pin != "auto" else "spread"
+    cpu_plan = plan(names, widths, mode)
+    pin_self(cpu_plan.get(f"rank{rank}"))
+
     # ---- rank 0 starts its child processes BEFORE anything initialises the GPU
     children = []
     api_url = ext_url = ""
@@ -197,15 +310,18 @@ def main():
         from gpushare_scheduler_extender_amd.sim.cluster import (start_apiserver, start_extender, start_node_agent,
                                                                  start_scheduler)
 
-        api = start_apiserver(native=a.apiserver == "native")
+        api = start_apiserver(native=a.apiserver == "native", cpus=cpu_plan.get("apiserver"))
         children.append(api)
-        ext = start_extender(api.url, profile=a.profile, bind_mode=a.bind_mode)
+        ext = start_extender(api.url, profile=a.profile, bind_mode=a.bind_mode, cpus=cpu_plan.get("extender"))
         children.append(ext)
         # kube-scheduler stand-in: its own process, like the real one (serial scheduling cycle)
-        children.append(start_scheduler(api.url, ext.url, profile=a.profile, native=a.scheduler == "native"))
+        children.append(start_scheduler(api.url, ext.url, profile=a.profile, native=a.scheduler == "native",
+                                        cpus=cpu_plan.get("scheduler")))
         if a.agent == "node":
             # the node's device plugin / kubelet stand-in: one process for all GPUs of the node, like a DaemonSet
-            children.append(start_node_agent(api.url, NODE, profile=a.profile, native=a.node_agent == "native"))
+            children.append(start_node_agent(api.url, NODE, profile=a.profile, native=a.node_agent == "native",
+                                             plugin="inproc" if a.node_agent == "inproc" else "grpc",
+                                             cpus=cpu_plan.get("node-agent")))
         api_url, ext_url = api.url, ext.url
 
     import torch
@@ -339,6 +455,8 @@ def main():
         pod_tmpl = json.dumps(pod_tmpl, separators=(",", ":"))
     from gpushare_scheduler_extender_amd.utils.gctune import tune
 
+    if rank == 0 and a.api_latency_ms and not a.inproc:
+        set_latency(api_batch, a.api_latency_ms)
     tune()
     barrier()
 
@@ -452,7 +570,7 @@ def main():
     mine.update({"gpu": local_rank, "hbm_total": dev.total_bytes, "arena": arena})
     agent_stats = gather(mine)
     node_agent_stats = None
-    if rank == 0 and a.agent == "node" and a.node_agent == "native":
+    if rank == 0 and a.agent == "node":
         na = next(c for c in children if c.name == "node-agent")
         st, body = E.BatchClient({"server": na.url}).run([("GET", "/v1/stats", b"")], 1)[0]
         node_agent_stats = json.loads(body) if st == 200 else {"error": st}
@@ -461,6 +579,16 @@ def main():
         st, body = api_batch.run([("GET", "/fake/stats", b"")], 1)[0]
         apiserver_stats = json.loads(body) if st == 200 else {"error": st}
         apiserver_stats.pop("counts", None)
+
+    sweep = ref_client = None
+    if rank == 0 and a.sweep and not a.inproc:
+        try:
+            sweep, ref_client = latency_sweep(a, children, api_url, api_batch, wave, fetch_timings, lt, n_pods,
+                                              a.warmup + a.steps, inspect_used)
+        except Exception as e:  # noqa: BLE001 - the sweep never costs the headline line
+            sweep = {"error": f"{type(e).__name__}: {e}"}
+    if world > 1:
+        dist.barrier(group=ctl)  # every rank's runtime endpoint stays up until rank 0's sweep is done
 
     if rank == 0:
         for s in step_stats:
@@ -486,7 +614,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_BINDS_PER_S, 2),
-            "dtype": "bf16",
+            "dtype": "n/a",
             "data": "synthetic pods (random-init ledger, fake kube-apiserver); HBM slices on real MI355X" if use_gpu
                     else "synthetic pods; fake devices (no GPU)",
             "config": {"model": f"gpushare extender+device plugin: {a.pods_per_gpu} pods/GPU x {a.pod_gib} GiB "
@@ -509,6 +637,13 @@ def main():
                             for k, t in (("bound", "t_bound"), ("running", "t_run"), ("total", "t_total"))},
             "wave_ms_max": {k: round(1e3 * max(s[t] for s in step_stats), 3)
                             for k, t in (("bound", "t_bound"), ("running", "t_run"), ("total", "t_total"))},
+            # per-wave throughput distribution: p50 and IQR next to `value` (one number from ~20 short waves is
+            # sensitive to single slow waves)
+            "wave_pods_per_s": wave_dist([n_pods / s["t_total"] for s in step_stats]),
+            "cpu_pinning": {k: v for k, v in cpu_plan.items()} or "none",
+            "api_latency_ms": a.api_latency_ms,
+            "latency_sweep": sweep,
+            "reference_client": ref_client,
             "bind_retries": sum(sum(s["attempts"]) - len(s["attempts"]) for s in step_stats),
             "agents": agent_stats,
             "node_agent": node_agent_stats,

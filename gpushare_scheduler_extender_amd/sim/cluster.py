@@ -47,8 +47,9 @@ def _stop_all():
 
 
 class ChildProc:
-    def __init__(self, args: list[str], name: str, env: dict | None = None):
+    def __init__(self, args: list[str], name: str, env: dict | None = None, cpus: list[int] | None = None):
         self.name = name
+        self.cpus = list(cpus or [])
         self.tmp = tempfile.mkdtemp(prefix=f"gsx-{name}-")
         self.port_file = os.path.join(self.tmp, "port")
         self.log_path = os.path.join(self.tmp, "log")
@@ -64,8 +65,14 @@ class ChildProc:
             args = ["-m", "gpushare_scheduler_extender_amd.utils.profrun", os.path.join(prof, f"{name}.prof"), *args[1:]]
         # "-m module ..." runs under this interpreter; anything else is a native executable
         argv = [sys.executable, *args] if args[0] == "-m" else list(args)
+        pin = None
+        if self.cpus:
+            mask = set(self.cpus)
+
+            def pin():  # in the child between fork and exec: the whole program starts pinned
+                os.sched_setaffinity(0, mask)
         self.proc = subprocess.Popen([*argv, "--port-file", self.port_file], stdout=self.log,
-                                     stderr=subprocess.STDOUT, env=e, cwd=str(ROOT))
+                                     stderr=subprocess.STDOUT, env=e, cwd=str(ROOT), preexec_fn=pin)
         _LIVE.add(self)
         self.port = _wait_port(self.port_file, self.proc)
         self.url = f"http://127.0.0.1:{self.port}"
@@ -96,7 +103,8 @@ class ChildProc:
 FAKEAPI = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-fakeapi"
 
 
-def start_apiserver(native: bool = True, history: int = 200000, threads: int | None = None) -> ChildProc:
+def start_apiserver(native: bool = True, history: int = 200000, threads: int | None = None,
+                    cpus: list[int] | None = None) -> ChildProc:
     """Fake kube-apiserver: the compiled ``gsx-fakeapi`` (native/fakeapi) or ``python -m ...k8s.fakeapi``.
 
     ``threads``: event loops of the native server (default ``GSX_FAKEAPI_THREADS`` or 1).
@@ -106,22 +114,24 @@ def start_apiserver(native: bool = True, history: int = 200000, threads: int | N
             raise FileNotFoundError(f"{FAKEAPI} missing; run `python native/build.py fakeapi`")
         threads = threads or int(os.environ.get("GSX_FAKEAPI_THREADS", "1"))
         return ChildProc([str(FAKEAPI), "--port", "0", "--history", str(history), "--threads", str(threads)],
-                         "apiserver")
-    return ChildProc(["-m", "gpushare_scheduler_extender_amd.k8s.fakeapi", "--port", "0"], "apiserver")
+                         "apiserver", cpus=cpus)
+    return ChildProc(["-m", "gpushare_scheduler_extender_amd.k8s.fakeapi", "--port", "0"], "apiserver", cpus=cpus)
 
 
 def start_extender(apiserver: str, profile: str = "shared-gpu", bind_mode: str = "binding", threadness: int = 1,
-                   log_level: str = "warning", port: int = 0) -> ChildProc:
+                   log_level: str = "warning", port: int = 0, cpus: list[int] | None = None,
+                   kube_qps: float = 0.0, kube_burst: int = 1000) -> ChildProc:
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.extender", "--host", "127.0.0.1", "--port", str(port),
                       "--apiserver", apiserver, "--profile", profile, "--bind-mode", bind_mode,
-                      "--threadness", str(threadness), "--log-level", log_level], "extender")
+                      "--threadness", str(threadness), "--log-level", log_level, "--kube-qps", str(kube_qps),
+                      "--kube-burst", str(kube_burst)], "extender", cpus=cpus)
 
 
 NODEAGENT = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-nodeagent"
 
 
 def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", workers: int = 32,
-                     native: bool = True, plugin: str = "grpc") -> ChildProc:
+                     native: bool = True, plugin: str = "grpc", cpus: list[int] | None = None) -> ChildProc:
     """kubelet + device-plugin Allocate + runtime stand-in for ``node``.
 
     ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent, its own Allocate matching);
@@ -132,16 +142,17 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
         if not NODEAGENT.exists():
             raise FileNotFoundError(f"{NODEAGENT} missing; run `python native/build.py nodeagent`")
         return ChildProc([str(NODEAGENT), "--node", node, "--apiserver", apiserver, "--profile", profile,
-                          "--workers", str(min(workers, 16))], "node-agent")
+                          "--workers", str(min(workers, 16))], "node-agent", cpus=cpus)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
-                      apiserver, "--profile", profile, "--workers", str(workers), "--plugin", plugin], "node-agent")
+                      apiserver, "--profile", profile, "--workers", str(workers), "--plugin", plugin], "node-agent",
+                     cpus=cpus)
 
 
 SCHEDSIM = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-schedsim"
 
 
 def start_scheduler(apiserver: str, extender: str, profile: str = "shared-gpu", max_inflight_binds: int = 256,
-                    native: bool = True) -> ChildProc:
+                    native: bool = True, cpus: list[int] | None = None) -> ChildProc:
     """kube-scheduler stand-in with a timings endpoint.
 
     ``native=True``: the compiled ``gsx-schedsim`` (native/schedsim, built by
@@ -152,6 +163,6 @@ def start_scheduler(apiserver: str, extender: str, profile: str = "shared-gpu", 
         if not SCHEDSIM.exists():
             raise FileNotFoundError(f"{SCHEDSIM} missing; run `python native/build.py schedsim`")
         return ChildProc([str(SCHEDSIM), "--apiserver", apiserver, "--extender", extender, "--profile", profile,
-                          "--bind-threads", str(min(16, max_inflight_binds))], "scheduler")
+                          "--bind-threads", str(min(16, max_inflight_binds))], "scheduler", cpus=cpus)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.sim", "--apiserver", apiserver, "--extender", extender,
-                      "--profile", profile, "--max-inflight-binds", str(max_inflight_binds)], "scheduler")
+                      "--profile", profile, "--max-inflight-binds", str(max_inflight_binds)], "scheduler", cpus=cpus)

@@ -47,15 +47,25 @@ def test_bench_single_process_fake_devices():
     assert d["config"]["global_batch"] == 4 and d["value"] > 0
     assert d["per_device_used_gib"] == [256] and d["binpack_util_pct"] > 90
     assert all(a["bad_stamps"] == 0 and a["failed"] == 0 for a in d["agents"])
+    assert d["dtype"] == "n/a" and d["wave_pods_per_s"]["n"] == 3
+    # latency sweep (extra keys): both bind modes at 0/1/2/5 ms; bind latency tracks the injected RTT
+    rows = {(r["bind_mode"], r["api_latency_ms"]): r for r in d["latency_sweep"]}
+    assert set(rows) == {(m, ms) for m in ("binding", "update") for ms in (0, 1, 2, 5)}
+    assert rows[("binding", 5)]["p50_bind_latency_ms"] >= 5.0
+    assert rows[("update", 5)]["p50_bind_latency_ms"] >= 10.0  # PUT + POST: two round trips
+    # the reference's client (QPS 5 / burst 10, PUT + POST) reproduces the derived 2.5 binds/s on this stack
+    ref = {r["bind_mode"]: r for r in d["reference_client"]}
+    assert 2.0 <= ref["update"]["pods_per_s"] <= 3.0
+    assert ref["binding"]["pods_per_s"] > ref["update"]["pods_per_s"]
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("agent", ["rank", "node"])
-def test_bench_two_ranks_gloo(agent):
+@pytest.mark.parametrize("agent,extra", [("rank", []), ("node", []), ("node", ["--node-agent", "plugin"])])
+def test_bench_two_ranks_gloo(agent, extra):
     port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "3",
-           "--warmup", "1", "--devices", "fake", "--agent", agent]
+           "--warmup", "1", "--devices", "fake", "--agent", agent, "--sweep", "0", *extra]
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     d = _json_line(r.stdout)
@@ -63,4 +73,20 @@ def test_bench_two_ranks_gloo(agent):
     # 4 x 64 GiB on each of the two devices: binpack fills GPU0 before GPU1 ... and both end full
     assert d["per_device_used_gib"] == [256, 256]
     assert sum(a["admitted"] for a in d["agents"]) == 8 * 4  # (warmup + steps) waves x 8 pods
+    assert all(a["bad_stamps"] == 0 for a in d["agents"])
+
+
+@pytest.mark.slow
+def test_bench_eight_ranks_gloo():
+    """The N=8 launch the driver uses on an 8 x MI355X node, rehearsed with 8 gloo ranks on fake devices."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "8", "--steps", "2",
+           "--warmup", "1", "--devices", "fake", "--agent", "node", "--sweep", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 32
+    assert d["per_device_used_gib"] == [256] * 8  # 32 x 64 GiB: 4 per device, binpack-first
+    assert sum(a["admitted"] for a in d["agents"]) == 3 * 32 or d["node_agent"]["admitted"] == 3 * 32
     assert all(a["bad_stamps"] == 0 for a in d["agents"])
