@@ -180,6 +180,13 @@ class Controller:
     def get_pod(self, name: str, ns: str | None = None) -> dict | None:
         return self.pods.get_by(name, ns)
 
+    def gc_reservations(self) -> tuple[int, bool]:
+        """Ledger GC gated on the pod informer's last LIST (see Ledger::gc); forces a re-list when needed."""
+        n, need = self.engine.gc(self.pods.last_list_start)
+        if need:
+            self.pods.request_relist()
+        return n, need
+
     def is_synced(self) -> bool:
         return self.pods.synced.is_set() and self.nodes.synced.is_set()
 
@@ -241,6 +248,9 @@ class NativeController:
 
     def stats(self) -> dict:
         return self.engine.controller_stats()
+
+    def gc_reservations(self) -> tuple[int, bool]:
+        return tuple(self.engine.controller_gc())
 
     async def wait_idle(self, timeout: float = 10.0):
         """Events are applied as they are decoded; nothing is queued."""

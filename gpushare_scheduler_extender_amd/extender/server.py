@@ -126,11 +126,15 @@ class ExtenderServer:
         await self.controller.stop()
 
     async def _gc_loop(self):
+        """Expire bind reservations the pod informer never confirmed -- but only on the evidence of a LIST
+        begun after the binding was written; a stalled watch forces a re-list instead (never over-commit)."""
         while True:
             await asyncio.sleep(min(5.0, max(0.05, self.reservation_ttl / 4)))
-            n = self.engine.gc()
+            n, relist = self.controller.gc_reservations()
             if n:
-                log.warning("expired %d unconfirmed bind reservations", n)
+                log.warning("expired %d bind reservations a fresh LIST did not confirm", n)
+            if relist:
+                log.info("bind reservations overdue: forcing a pod re-list to confirm them")
 
     # ------------------------------------------------------------ verbs
     def filter(self, body: bytes) -> bytes:

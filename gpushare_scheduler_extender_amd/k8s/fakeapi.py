@@ -193,12 +193,14 @@ class Faults:
         self.drop_watch_after = 0  # close watch streams after this many events (0 = never)
         self.expire_watches = 0  # the next N watch requests get 410 Gone (history compacted)
         self.hold_watches = False  # new watch requests wait until this is cleared
+        self.fail_lists = False  # LIST requests answer 503 (an apiserver that cannot serve reads)
         self.slow_bindings: dict[str, float] = {}  # pod name -> ms a binding of it takes
         self.seed = 0
         self.rng = random.Random(0)
 
     def update(self, d: dict):
-        for k in ("conflict_rate", "error_rate", "latency_ms", "drop_watch_after", "expire_watches", "hold_watches"):
+        for k in ("conflict_rate", "error_rate", "latency_ms", "drop_watch_after", "expire_watches", "hold_watches",
+                  "fail_lists"):
             if k in d:
                 setattr(self, k, type(getattr(self, k))(d[k]))
         if "slow_bindings" in d:
@@ -210,7 +212,8 @@ class Faults:
     def as_dict(self):
         return {"conflict_rate": self.conflict_rate, "error_rate": self.error_rate,
                 "latency_ms": self.latency_ms, "drop_watch_after": self.drop_watch_after,
-                "expire_watches": self.expire_watches, "hold_watches": self.hold_watches}
+                "expire_watches": self.expire_watches, "hold_watches": self.hold_watches,
+                "fail_lists": self.fail_lists}
 
 
 class FakeApiServer:
@@ -518,6 +521,9 @@ class FakeApiServer:
             lsel = q.get("labelSelector", "")
             if q.get("watch") in ("1", "true"):
                 return self._watch(request, kind, ns, fsel, lsel, q.get("resourceVersion", ""))
+            if self.faults.fail_lists:
+                self.counts["list_failed"] += 1
+                raise HTTPError(503, status_body(503, "ServiceUnavailable", "injected: LIST unavailable"))
             items = self.list(kind, ns, fsel, lsel)
             return self._json({"kind": lists[kind], "apiVersion": "v1",
                                "metadata": {"resourceVersion": str(self.rv)}, "items": items})

@@ -20,6 +20,7 @@ from __future__ import annotations
 import asyncio
 import json
 import logging
+import time
 from typing import Callable
 
 from .client import ApiError, KubeClient
@@ -91,6 +92,9 @@ class Informer:
         self.relists = 0
         self.rewatches = 0
         self.events = 0
+        self.last_list_start = 0.0  # time.monotonic() when the last applied LIST was sent
+        self._relist = False
+        self._watch_task: asyncio.Task | None = None
 
     # lister API
     def get(self, key: str) -> dict | None:
@@ -147,7 +151,14 @@ class Informer:
         if rv:
             self.last_rv = rv
 
+    def request_relist(self):
+        """End the current watch (also one the apiserver never answered) and LIST again."""
+        self._relist = True
+        if self._watch_task is not None and not self._watch_task.done():
+            self._watch_task.cancel()
+
     async def _list(self):
+        started = time.monotonic()
         lst = await self.client.list(self.kind, self.namespace, self.field_selector, self.label_selector)
         items = lst.get("items") or []
         new = {obj_key(o): o for o in items}
@@ -169,20 +180,36 @@ class Informer:
                     h.update(prev, o, None)
         self.last_rv = (lst.get("metadata") or {}).get("resourceVersion", "")
         self.relists += 1
+        self.last_list_start = started
+
+    async def _watch_once(self):
+        async for ev, raw in self.client.watch(self.kind, self.namespace, self.last_rv, self.field_selector,
+                                               self.label_selector, self.watch_timeout, raw=True):
+            self._dispatch(ev["type"], ev["object"], raw)
 
     async def _run(self):
         backoff = 0.05
         need_list = True
         while not self._stopped:
             try:
+                if self._relist:
+                    self._relist = False
+                    need_list = True
                 if need_list:
                     await self._list()
                     need_list = False
                     self.synced.set()
-                async for ev, raw in self.client.watch(self.kind, self.namespace, self.last_rv, self.field_selector,
-                                                       self.label_selector, self.watch_timeout, raw=True):
-                    self._dispatch(ev["type"], ev["object"], raw)
-                    backoff = 0.05
+                # the watch runs in its own task so request_relist() can end it without ending the informer
+                self._watch_task = asyncio.get_running_loop().create_task(self._watch_once())
+                try:
+                    await self._watch_task
+                except asyncio.CancelledError:
+                    if not self._relist or self._stopped:
+                        raise
+                    continue
+                finally:
+                    self._watch_task = None
+                backoff = 0.05
                 self.rewatches += 1
             except asyncio.CancelledError:
                 raise

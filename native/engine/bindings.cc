@@ -216,9 +216,27 @@ class Engine {
     l_.finish_bind(uid, ok, ttl);
   }
 
-  int gc() {
-    std::lock_guard<std::mutex> g(l_.mu());
-    return l_.gc();
+  // (expired, need_relist): see Ledger::gc; list_start is the start time of the last applied pod LIST
+  py::tuple gc(double list_start) {
+    bool need = false;
+    int n;
+    {
+      std::lock_guard<std::mutex> g(l_.mu());
+      n = l_.gc(list_start, &need);
+    }
+    return py::make_tuple(n, need);
+  }
+
+  // (expired, relist_requested) with the native controller's pod reflector as the confirming LIST source
+  py::tuple controller_gc() {
+    if (!ctl_) return gc(0.0);
+    bool need = false;
+    int n;
+    {
+      py::gil_scoped_release rel;
+      n = ctl_->gc_reservations(&need);
+    }
+    return py::make_tuple(n, need);
   }
 
   py::tuple inspect(const std::string& node) {
@@ -258,6 +276,7 @@ class Engine {
     d["bind_ok"] = s.bind_ok;
     d["bind_fail"] = s.bind_fail;
     d["expired"] = s.expired;
+    d["expiry_deferred"] = s.expiry_deferred;
     d["overcommit_events"] = s.overcommit_events;
     d["pod_upserts"] = s.pod_upserts;
     d["pod_removes"] = s.pod_removes;
@@ -606,7 +625,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("prioritize", &Engine::prioritize)
       .def("assume", &Engine::assume)
       .def("finish_bind", &Engine::finish_bind, py::arg("uid"), py::arg("ok"), py::arg("ttl") = 30.0)
-      .def("gc", &Engine::gc)
+      .def("gc", &Engine::gc, py::arg("list_start") = 0.0)
+      .def("controller_gc", &Engine::controller_gc)
       .def("inspect", &Engine::inspect, py::arg("node") = std::string())
       .def("node_devices", &Engine::node_devices)
       .def("node_names", &Engine::node_names)

@@ -16,14 +16,14 @@ Controller::Controller(Ledger* l, ControllerConfig cfg) : l_(l), cfg_(std::move(
   pr.path = "/api/v1/pods";
   pr.watch_timeout_s = cfg_.watch_timeout_s;
   ReflectorHandler ph;
-  ph.on_list = [this](const json::Doc& d, const std::vector<uint32_t>& items) { on_pod_list(d, items); };
+  ph.on_list = [this](const ListView& lv) { on_pod_list(lv); };
   ph.on_event = [this](Ev ev, const json::Doc& d, uint32_t obj) { on_pod_event(ev, d, obj); };
   pods_ = std::make_unique<Reflector>(cfg_.api, pr, ph);
   ReflectorConfig nr;
   nr.path = "/api/v1/nodes";
   nr.watch_timeout_s = cfg_.watch_timeout_s;
   ReflectorHandler nh;
-  nh.on_list = [this](const json::Doc& d, const std::vector<uint32_t>& items) { on_node_list(d, items); };
+  nh.on_list = [this](const ListView& lv) { on_node_list(lv); };
   nh.on_event = [this](Ev ev, const json::Doc& d, uint32_t obj) { on_node_event(ev, d, obj); };
   nodes_ = std::make_unique<Reflector>(cfg_.api, nr, nh);
 }
@@ -55,6 +55,22 @@ void Controller::stop() {
 }
 
 bool Controller::synced() const { return pods_->synced() && nodes_->synced(); }
+
+double Controller::pod_list_start() const { return pods_->last_list_start(); }
+
+void Controller::request_pod_relist() { pods_->request_relist(); }
+
+int Controller::gc_reservations(bool* relist_requested) {
+  bool need = false;
+  int n;
+  {
+    std::lock_guard<std::mutex> g(l_->mu());
+    n = l_->gc(pods_->last_list_start(), &need);
+  }
+  if (need) pods_->request_relist();
+  if (relist_requested) *relist_requested = need;
+  return n;
+}
 
 std::string Controller::last_error() const {
   std::string e = pods_->last_error();
@@ -196,12 +212,12 @@ void Controller::on_pod_event(Ev ev, const json::Doc& d, uint32_t obj) {
   }
 }
 
-void Controller::on_pod_list(const json::Doc& d, const std::vector<uint32_t>& items) {
+void Controller::on_pod_list(const ListView& lv) {
   std::unordered_map<std::string, Entry> fresh;
-  fresh.reserve(items.size());
-  for (uint32_t i : items) {
+  fresh.reserve(lv.size());
+  for (size_t k = 0; k < lv.size(); ++k) {
     Entry e;
-    if (!decode(d, i, &e)) continue;
+    if (!decode(lv.doc(k), lv.obj(k), &e)) continue;
     std::string key = key_of(e.v);
     fresh[key] = std::move(e);
   }
@@ -310,12 +326,12 @@ void Controller::on_node_event(Ev ev, const json::Doc& d, uint32_t obj) {
   }
 }
 
-void Controller::on_node_list(const json::Doc& d, const std::vector<uint32_t>& items) {
+void Controller::on_node_list(const ListView& lv) {
   std::unordered_set<std::string> seen;
   std::lock_guard<std::mutex> g(l_->mu());
-  for (uint32_t i : items) {
+  for (size_t k = 0; k < lv.size(); ++k) {
     NodeView nv;
-    if (!parse_node(d, i, l_->profile(), &nv)) continue;
+    if (!parse_node(lv.doc(k), lv.obj(k), l_->profile(), &nv)) continue;
     seen.insert(nv.name);
     l_->upsert_node(nv);
   }

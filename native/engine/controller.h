@@ -66,6 +66,12 @@ class Controller {
   std::vector<std::tuple<std::string, int, int64_t, int64_t>> overcommitted() const;
   ControllerStats stats() const;
   std::string last_error() const;
+  // Reservation GC gated on the pod reflector (Ledger::gc): an overdue bind reservation is dropped only
+  // once a LIST begun after its binding has been applied without confirming it; until then a re-list is
+  // forced (a stalled or unanswered watch never makes a held device look free).
+  int gc_reservations(bool* relist_requested);
+  double pod_list_start() const;
+  void request_pod_relist();
 
  private:
   struct Entry {
@@ -74,9 +80,9 @@ class Controller {
     std::string raw;     // object JSON (gpu-share pods only; lister)
   };
 
-  void on_pod_list(const json::Doc& d, const std::vector<uint32_t>& items);
+  void on_pod_list(const ListView& lv);
   void on_pod_event(Ev ev, const json::Doc& d, uint32_t obj);
-  void on_node_list(const json::Doc& d, const std::vector<uint32_t>& items);
+  void on_node_list(const ListView& lv);
   void on_node_event(Ev ev, const json::Doc& d, uint32_t obj);
   bool decode(const json::Doc& d, uint32_t obj, Entry* e) const;
   // handler semantics (called with smu_ held)

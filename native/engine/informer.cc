@@ -1,5 +1,7 @@
 #include "informer.h"
 
+#include <sys/socket.h>
+
 #include <chrono>
 #include <cstdio>
 
@@ -64,7 +66,15 @@ void Reflector::set_error(const std::string& e) {
   last_err_ = e;
 }
 
-std::string Reflector::query(bool watch) const {
+void Reflector::request_relist() {
+  relist_req_.store(true);
+  // shut the socket down without marking the handle aborted: the watch ends, the loop re-lists
+  int fd = stream_.fd.load();
+  if (fd >= 0) ::shutdown(fd, SHUT_RDWR);
+  cv_.notify_all();
+}
+
+std::string Reflector::query(bool watch, const std::string& cont) const {
   std::string q = rc_.path;
   char sep = '?';
   auto add = [&](const char* k, const std::string& v) {
@@ -75,6 +85,10 @@ std::string Reflector::query(bool watch) const {
   };
   if (!rc_.label_selector.empty()) add("labelSelector", rc_.label_selector);
   if (!rc_.field_selector.empty()) add("fieldSelector", rc_.field_selector);
+  if (!watch && rc_.list_page_size > 0) {
+    add("limit", std::to_string(rc_.list_page_size));
+    if (!cont.empty()) add("continue", cont);
+  }
   if (watch) {
     add("watch", "true");
     add("allowWatchBookmarks", "true");
@@ -90,29 +104,49 @@ std::string Reflector::query(bool watch) const {
 }
 
 bool Reflector::do_list(std::string* err) {
-  int status = 0;
-  std::string body;
-  if (!api_.request("GET", query(false), std::string(), nullptr, &status, &body, err)) return false;
-  if (status != 200) {
-    *err = "LIST " + rc_.path + ": HTTP " + std::to_string(status) + ": " + body.substr(0, 200);
-    return false;
-  }
-  json::Doc d;
-  if (!d.parse(body, err)) return false;
-  std::vector<uint32_t> items;
-  int64_t it = d.find(0, "items");
-  if (it >= 0 && d.at(static_cast<uint32_t>(it)).type == json::T::Array) {
-    uint32_t end = d.at(static_cast<uint32_t>(it)).skip;
-    for (uint32_t i = static_cast<uint32_t>(it) + 1; i < end; i = d.next(i)) {
-      if (d.at(i).type == json::T::Object) items.push_back(i);
+  const double started = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  ListView lv;
+  std::string cont, list_rv;
+  for (int page = 0;; ++page) {
+    int status = 0;
+    lv.bodies.emplace_back(new std::string());
+    std::string& body = *lv.bodies.back();
+    if (!api_.request("GET", query(false, cont), std::string(), nullptr, &status, &body, err)) return false;
+    if (status == 410 && page > 0) {
+      // the continue token outlived the apiserver's history: start the LIST over
+      *err = "LIST " + rc_.path + ": continue token expired";
+      return false;
     }
+    if (status != 200) {
+      *err = "LIST " + rc_.path + ": HTTP " + std::to_string(status) + ": " + body.substr(0, 200);
+      return false;
+    }
+    lv.pages.emplace_back();
+    json::Doc& d = lv.pages.back();
+    if (!d.parse(body, err)) return false;
+    int64_t it = d.find(0, "items");
+    if (it >= 0 && d.at(static_cast<uint32_t>(it)).type == json::T::Array) {
+      uint32_t end = d.at(static_cast<uint32_t>(it)).skip;
+      for (uint32_t i = static_cast<uint32_t>(it) + 1; i < end; i = d.next(i)) {
+        if (d.at(i).type == json::T::Object) lv.items.emplace_back(static_cast<uint32_t>(page), i);
+      }
+    }
+    // the whole LIST is consistent at the first page's resourceVersion
+    if (page == 0) {
+      int64_t rv = d.path(0, {"metadata", "resourceVersion"});
+      list_rv = rv >= 0 ? d.str(static_cast<uint32_t>(rv)) : std::string();
+    }
+    list_pages_++;
+    int64_t c = d.path(0, {"metadata", "continue"});
+    cont = c >= 0 ? d.str(static_cast<uint32_t>(c)) : std::string();
+    if (cont.empty() || rc_.list_page_size <= 0) break;
   }
-  int64_t rv = d.path(0, {"metadata", "resourceVersion"});
   {
     std::lock_guard<std::mutex> g(mu_);
-    rv_ = rv >= 0 ? d.str(static_cast<uint32_t>(rv)) : std::string();
+    rv_ = list_rv;
   }
-  if (h_.on_list) h_.on_list(d, items);
+  if (h_.on_list) h_.on_list(lv);
+  last_list_start_.store(started);
   relists_++;
   return true;
 }
@@ -202,7 +236,7 @@ int Reflector::do_watch(std::string* err) {
     return true;
   };
   double idle = rc_.watch_timeout_s > 0 ? rc_.watch_timeout_s + 60.0 : 3600.0;
-  if (!api_.stream(query(true), &status, &ebody, on_data, err, &stream_, idle)) return -1;
+  if (!api_.stream(query(true, std::string()), &status, &ebody, on_data, err, &stream_, idle)) return -1;
   if (status == 410) return 1;
   if (status >= 400) {
     *err = "WATCH " + rc_.path + ": HTTP " + std::to_string(status) + ": " + ebody.substr(0, 200);
@@ -220,11 +254,12 @@ void Reflector::run() {
   bool need_list = true;
   auto sleep_backoff = [&] {
     std::unique_lock<std::mutex> lk(mu_);
-    cv_.wait_for(lk, std::chrono::duration<double>(backoff), [this] { return stop_.load(); });
+    cv_.wait_for(lk, std::chrono::duration<double>(backoff), [this] { return stop_.load() || relist_req_.load(); });
     backoff = std::min(rc_.backoff_max_s, backoff * 2);
   };
   while (!stop_.load()) {
     std::string err;
+    if (relist_req_.exchange(false)) need_list = true;
     if (need_list) {
       if (!do_list(&err)) {
         set_error(err);
@@ -239,6 +274,7 @@ void Reflector::run() {
     }
     int r = do_watch(&err);
     if (stop_.load()) break;
+    if (relist_req_.load()) continue;  // ended on purpose: LIST next
     if (r == 1) {
       need_list = true;  // 410 Gone: history compacted past our resourceVersion
       continue;

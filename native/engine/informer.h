@@ -13,6 +13,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -30,14 +31,27 @@ struct ReflectorConfig {
   std::string label_selector, field_selector;
   int watch_timeout_s = 300;       // server-side watch timeout (then re-watch)
   double backoff_max_s = 5.0;      // reconnect backoff cap
+  // LIST in pages of this many objects (`limit` / `continue`, client-go's pager default 500); 0 = one
+  // unpaginated request.  Keeps each apiserver response (and etcd range read) bounded in a large cluster.
+  int list_page_size = 500;
+};
+
+// One complete LIST, possibly assembled from several pages.  Objects are addressed as
+// (page, tape index); the pages' bodies live as long as the view.
+struct ListView {
+  std::vector<std::unique_ptr<std::string>> bodies;
+  std::vector<json::Doc> pages;
+  std::vector<std::pair<uint32_t, uint32_t>> items;
+  size_t size() const { return items.size(); }
+  const json::Doc& doc(size_t i) const { return pages[items[i].first]; }
+  uint32_t obj(size_t i) const { return items[i].second; }
 };
 
 // Callbacks run serially on the reflector thread.
 struct ReflectorHandler {
-  // A complete LIST: `items` are tape indices of the objects in `doc`.  The
-  // owner replaces its view (and diffs it to emit deletes, like client-go's
+  // A complete LIST.  The owner replaces its view (and diffs it to emit deletes, like client-go's
   // Replace()).
-  std::function<void(const json::Doc& doc, const std::vector<uint32_t>& items)> on_list;
+  std::function<void(const ListView& list)> on_list;
   // One watch event; `obj` is the tape index of the object in `doc`.
   std::function<void(Ev type, const json::Doc& doc, uint32_t obj)> on_event;
 };
@@ -57,6 +71,12 @@ class Reflector {
   uint64_t errors() const { return errors_.load(); }
   std::string last_error() const;
   std::string resource_version() const;
+  uint64_t list_pages() const { return list_pages_.load(); }
+  // Steady-clock seconds at which the last successfully applied LIST was *sent* (0: none yet).  Any write
+  // acknowledged before this instant is reflected in that LIST.
+  double last_list_start() const { return last_list_start_.load(); }
+  // End the current watch (even one the apiserver never answered) and LIST again.
+  void request_relist();
 
  private:
   void run();
@@ -65,7 +85,7 @@ class Reflector {
   int do_watch(std::string* err);
   bool on_line(std::string_view line, int* verdict);
   void set_error(const std::string& e);
-  std::string query(bool watch) const;
+  std::string query(bool watch, const std::string& cont) const;
 
   ApiClient api_;
   ReflectorConfig rc_;
@@ -73,7 +93,9 @@ class Reflector {
   std::thread th_;
   std::atomic<bool> stop_{false};
   std::atomic<bool> synced_{false};
-  std::atomic<uint64_t> events_{0}, relists_{0}, rewatches_{0}, errors_{0};
+  std::atomic<uint64_t> events_{0}, relists_{0}, rewatches_{0}, errors_{0}, list_pages_{0};
+  std::atomic<double> last_list_start_{0.0};
+  std::atomic<bool> relist_req_{false};
   StreamHandle stream_;
   mutable std::mutex mu_;
   std::condition_variable cv_;

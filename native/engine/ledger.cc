@@ -254,17 +254,28 @@ void Ledger::finish_bind(const std::string& uid, bool ok, double ttl_s) {
   }
   stats_.bind_ok++;
   it->second.bound = true;
-  it->second.deadline = now_s() + ttl_s;
+  it->second.bound_at = now_s();
+  it->second.deadline = it->second.bound_at + ttl_s;
 }
 
-int Ledger::gc() {
+int Ledger::gc(double confirmed_list_start, bool* need_relist) {
   double now = now_s();
   int n = 0;
+  bool relist = false;
   for (auto it = pods_.begin(); it != pods_.end();) {
     const PodRec& r = it->second;
-    // bound but never observed by the informer within ttl, or a bind that
-    // never finished (crashed coroutine) after 10 minutes.
-    bool expire = r.assumed && ((r.bound && r.deadline < now) || (!r.bound && now - r.assumed_at > 600.0));
+    bool expire = false;
+    if (r.assumed && r.bound && r.deadline < now) {
+      // overdue: only a LIST begun after the binding was written can prove the binding absent
+      if (confirmed_list_start > r.bound_at) {
+        expire = true;
+      } else {
+        relist = true;
+        stats_.expiry_deferred++;
+      }
+    } else if (r.assumed && !r.bound && now - r.assumed_at > 600.0) {
+      expire = true;  // a bind that never finished (crashed worker)
+    }
     if (expire) {
       auto cur = it++;
       erase_pod(cur);
@@ -274,6 +285,7 @@ int Ledger::gc() {
     }
   }
   stats_.expired += static_cast<uint64_t>(n);
+  if (need_relist) *need_relist = relist;
   return n;
 }
 

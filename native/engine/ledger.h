@@ -40,6 +40,7 @@ struct PodRec {
   bool assumed = false;  // reserved by bind, not yet observed with annotations
   bool bound = false;    // bind round-trips finished successfully
   double assumed_at = 0;
+  double bound_at = 0;   // when the bind's apiserver write succeeded
   double deadline = 0;   // expiry of an assumed+bound reservation
   bool accounted = false;
 };
@@ -65,6 +66,7 @@ struct Stats {
   uint64_t filter_calls = 0, filter_nodes_ok = 0, filter_nodes_failed = 0;
   uint64_t assume_ok = 0, assume_fail = 0, bind_ok = 0, bind_fail = 0;
   uint64_t expired = 0, overcommit_events = 0, pod_upserts = 0, pod_removes = 0;
+  uint64_t expiry_deferred = 0;  // GC passes that kept an overdue reservation until a LIST could confirm it
 };
 
 class Ledger {
@@ -97,7 +99,12 @@ class Ledger {
   int64_t assume(const std::string& uid, const std::string& ns, const std::string& name,
                  const std::string& node, int64_t req, int64_t* dev_total);
   void finish_bind(const std::string& uid, bool ok, double ttl_s);
-  int gc();  // expire stale reservations
+  // Expire stale reservations.  A bound reservation the pod informer has not confirmed within its TTL is
+  // dropped only if a pod LIST that *started after the bind succeeded* (`confirmed_list_start`, steady-clock
+  // seconds; 0 = none) was applied without confirming it: then the apiserver really has no such binding.
+  // Otherwise -- watch stalled, apiserver unreachable -- the device stays reserved (never over-committed)
+  // and `*need_relist` is set so the caller forces a LIST.  Binds that never finished expire after 600 s.
+  int gc(double confirmed_list_start, bool* need_relist);
 
   // ---- observation ----
   std::string inspect_json(const std::string& node, bool* found) const;

@@ -23,10 +23,12 @@ PodTracker::PodTracker(const ApiConfig& cfg, const std::string& ns, const std::s
     std::string name = str_at(d, d.path(obj, {"metadata", "name"}));
     return ns_.empty() ? name : ns_ + "/" + name;
   };
-  h.on_list = [this, key_of](const json::Doc& d, const std::vector<uint32_t>& items) {
+  h.on_list = [this, key_of](const ListView& lv) {
     std::lock_guard<std::mutex> g(mu_);
     pods_.clear();
-    for (uint32_t i : items) {
+    for (size_t k = 0; k < lv.size(); ++k) {
+      const json::Doc& d = lv.doc(k);
+      uint32_t i = lv.obj(k);
       St& s = pods_[key_of(d, i)];
       s.node = str_at(d, d.path(i, {"spec", "nodeName"}));
       s.phase = str_at(d, d.path(i, {"status", "phase"}));

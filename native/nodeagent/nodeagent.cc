@@ -240,10 +240,10 @@ class Agent {
     rc.path = "/api/v1/pods";
     rc.field_selector = "spec.nodeName=" + node_;
     ReflectorHandler h;
-    h.on_list = [this](const json::Doc& d, const std::vector<uint32_t>& items) {
+    h.on_list = [this](const ListView& lv) {
       std::lock_guard<std::mutex> g(mu_);
       std::unordered_set<std::string> seen;
-      for (uint32_t i : items) seen.insert(on_pod_locked(d, i));
+      for (size_t k = 0; k < lv.size(); ++k) seen.insert(on_pod_locked(lv.doc(k), lv.obj(k)));
       std::vector<std::string> gone;
       for (auto& kv : pods_) {
         if (!seen.count(kv.first)) gone.push_back(kv.first);

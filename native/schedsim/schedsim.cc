@@ -91,10 +91,10 @@ class Sim {
     ReflectorConfig pr;
     pr.path = "/api/v1/pods";
     ReflectorHandler ph;
-    ph.on_list = [this](const json::Doc& d, const std::vector<uint32_t>& items) {
+    ph.on_list = [this](const ListView& lv) {
       std::lock_guard<std::mutex> g(mu_);
       std::unordered_set<std::string> seen;
-      for (uint32_t i : items) seen.insert(on_pod_locked(d, i));
+      for (size_t k = 0; k < lv.size(); ++k) seen.insert(on_pod_locked(lv.doc(k), lv.obj(k)));
       std::vector<std::string> gone;
       for (auto& kv : pods_) {
         if (!seen.count(kv.first)) gone.push_back(kv.first);
@@ -117,10 +117,10 @@ class Sim {
     ReflectorConfig nr;
     nr.path = "/api/v1/nodes";
     ReflectorHandler nh;
-    nh.on_list = [this](const json::Doc& d, const std::vector<uint32_t>& items) {
+    nh.on_list = [this](const ListView& lv) {
       std::lock_guard<std::mutex> g(mu_);
       nodes_.clear();
-      for (uint32_t i : items) on_node_locked(d, i);
+      for (size_t k = 0; k < lv.size(); ++k) on_node_locked(lv.doc(k), lv.obj(k));
       cv_.notify_all();
     };
     nh.on_event = [this](Ev ev, const json::Doc& d, uint32_t obj) {

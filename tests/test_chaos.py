@@ -129,3 +129,79 @@ def test_extender_crash_restart_rebuilds_ledger_from_annotations():
         finally:
             await cl.close()
     asyncio.run(go())
+
+
+@pytest.mark.parametrize("native_controller", [True, False])
+def test_reservation_gc_never_frees_a_device_behind_a_stalled_watch(native_controller):
+    """a bound reservation the informer has not confirmed within its TTL must not be dropped
+    while the pod watch is stalled and LISTs fail (the device would look free while the pod holds it); once
+    a LIST begun after the binding succeeds it decides: confirmed -> kept, absent -> expired."""
+    from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
+    from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+    from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+    from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
+    from gpushare_scheduler_extender_amd.models import wire
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+
+    async def go():
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 100, 1))
+        srv = ExtenderServer(KubeClient(api.url), SHARED_GPU, reservation_ttl=0.2, native_controller=native_controller)
+        ext = await ExtenderRunner(srv, native=True).start()
+        http = HttpClient(ext.url)
+        eng = srv.engine
+        try:
+            for _ in range(200):
+                if eng.has_node("n"):
+                    break
+                await asyncio.sleep(0.01)
+
+            async def filter_(pod):
+                r = await http.request("POST", "/gpushare-scheduler/filter", wire.filter_args(pod, ["n"]))
+                return json.loads(r.body)
+
+            async def bind(pod):
+                args = wire.ExtenderBindingArgs(pod["metadata"]["name"], "default", pod["metadata"]["uid"], "n")
+                r = await http.request("POST", "/gpushare-scheduler/bind", args.encode())
+                return r.status
+
+            # the extender's pod watch stalls (dropped, new watches never answered) and LISTs fail
+            fa = HttpClient(api.url)
+            await fa.request("POST", "/fake/faults", json.dumps({"hold_watches": True, "fail_lists": True,
+                                                                 "drop_watches_now": True}).encode())
+            await fa.close()
+            await asyncio.sleep(0.1)
+            a = await c.create("pods", make_pod("a", 60))
+            assert (await filter_(a))["NodeNames"] == ["n"]
+            assert await bind(a) == 200
+            await asyncio.sleep(1.0)  # 5 x the TTL, GC runs every 0.05 s
+            assert eng.node_devices("n") == [(100, 60)], "reservation dropped behind a stalled watch"
+            b = make_pod("b", 60)
+            assert (await filter_(b))["NodeNames"] == []  # still no room: never over-committed
+            assert eng.stats()["expired"] == 0 and eng.stats()["expiry_deferred"] > 0
+            # LISTs work again (watches still held): the forced re-list confirms the binding -> kept
+            api.server.faults.fail_lists = False
+            await asyncio.sleep(0.6)
+            assert eng.node_devices("n") == [(100, 60)] and eng.stats()["expired"] == 0
+            # a binding the apiserver no longer has (pod deleted unseen): the next LIST proves it -> expired
+            await c.delete("pods", "a", "default")
+            await asyncio.sleep(0.05)
+            p2 = await c.create("pods", make_pod("p2", 30))
+            await filter_(p2)
+            assert await bind(p2) == 200
+            await c.delete("pods", "p2", "default")
+            for _ in range(200):
+                if eng.node_devices("n") == [(100, 0)]:
+                    break
+                await asyncio.sleep(0.02)
+            assert eng.node_devices("n") == [(100, 0)]
+            assert eng.stats()["expired"] >= 1
+        finally:
+            api.server.faults.hold_watches = False
+            await http.close()
+            await ext.stop()
+            await srv.client.close()
+            await c.close()
+            await api.stop()
+    asyncio.run(go())

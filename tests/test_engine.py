@@ -1,5 +1,6 @@
 """Native engine: golden cases from the reference design doc, wire format, quirks, properties."""
 import json
+import time
 
 import pytest
 from hypothesis import given, settings, strategies as st
@@ -272,11 +273,15 @@ def test_assume_confirmed_by_informer_and_gc():
     eng.finish_bind("u1", True, 0.0)  # ttl 0: would expire immediately if unconfirmed
     pod = _annotated("a", "n", dev, 6, uid="u1")
     _load(eng, pod)  # informer observes the annotated, bound pod
-    assert eng.gc() == 0
+    assert eng.gc() == (0, False)
     assert eng.node_devices("n") == [(10, 6)]
     eng.assume("u2", "d", "b", "n", 2)
     eng.finish_bind("u2", True, 0.0)
-    assert eng.gc() == 1
+    # overdue, but no LIST since the binding was written: kept (the watch may be stalled), re-list asked for
+    assert eng.gc() == (0, True) and eng.gc(time.monotonic() - 60) == (0, True)
+    assert eng.node_devices("n") == [(10, 8)] and eng.stats()["expiry_deferred"] == 2
+    # a LIST sent after the binding that did not confirm it: the apiserver has no such binding
+    assert eng.gc(time.monotonic()) == (1, False)
     assert eng.node_devices("n") == [(10, 6)]
 
 
