@@ -272,6 +272,7 @@ class ExtenderServer:
         r.add_get("/version", self.h_version)
         r.add_get("/metrics", self.h_metrics)
         r.add_get("/healthz", self.h_healthz)
+        r.add_get("/debug/engine", self.h_debug_engine)
         add_pprof(app)
         return app
 
@@ -316,6 +317,16 @@ class ExtenderServer:
         if ok and not self.is_leader:
             return web.Response(text="standby (not the leader)", status=503)
         return web.Response(text="ok" if ok else "not synced", status=200 if ok else 503)
+
+    async def h_debug_engine(self, request):
+        """Ledger, controller (LIST pages, watch errors) and native front-end counters as JSON."""
+        out = {"ledger": self.engine.stats()}
+        st = getattr(self.controller, "stats", None)
+        if st is not None:
+            out["controller"] = st()
+        if self.native_server:
+            out["server"] = self.engine.server_stats()
+        return web.Response(text=json.dumps(out), content_type="application/json")
 
     async def h_metrics(self, request):
         return web.Response(body=self.metrics.render(), content_type="text/plain")

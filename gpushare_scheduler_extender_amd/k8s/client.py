@@ -255,7 +255,9 @@ class KubeClient:
         return await self.request("GET", _ns_path(kind, ns, name))
 
     async def list(self, kind: str, ns: str | None = None, field_selector: str = "", label_selector: str = "",
-                   resource_version: str = "") -> dict:
+                   resource_version: str = "", page_size: int = 0) -> dict:
+        """One LIST; with ``page_size`` > 0 it is fetched in pages (``limit`` / ``continue``, client-go's
+        pager) and returned assembled, at the first page's resourceVersion."""
         params = {}
         if field_selector:
             params["fieldSelector"] = field_selector
@@ -263,7 +265,18 @@ class KubeClient:
             params["labelSelector"] = label_selector
         if resource_version:
             params["resourceVersion"] = resource_version
-        return await self.request("GET", _ns_path(kind, ns), params=params, timeout=120)
+        if page_size <= 0:
+            return await self.request("GET", _ns_path(kind, ns), params=params, timeout=120)
+        params["limit"] = str(page_size)
+        out = await self.request("GET", _ns_path(kind, ns), params=params, timeout=120)
+        items = list(out.get("items") or [])
+        while (out.get("metadata") or {}).get("continue"):
+            params["continue"] = out["metadata"]["continue"]
+            out = await self.request("GET", _ns_path(kind, ns), params=params, timeout=120)
+            items.extend(out.get("items") or [])
+        first_md = dict(out.get("metadata") or {})
+        first_md.pop("continue", None)
+        return {**out, "metadata": first_md, "items": items}
 
     async def create(self, kind: str, obj: dict, ns: str | None = None) -> dict:
         ns = ns if ns is not None else (obj.get("metadata") or {}).get("namespace", "default")

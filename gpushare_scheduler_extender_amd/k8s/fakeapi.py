@@ -49,6 +49,11 @@ def _now_iso() -> str:
     return datetime.now(timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ")
 
 
+def _obj_key(o: dict) -> tuple[str, str]:
+    md = o.get("metadata") or {}
+    return md.get("namespace", "") or "", md.get("name", "")
+
+
 def status_body(code: int, reason: str, message: str, details: dict | None = None) -> dict:
     b = {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Failure", "message": message,
          "reason": reason, "code": code}
@@ -525,8 +530,20 @@ class FakeApiServer:
                 self.counts["list_failed"] += 1
                 raise HTTPError(503, status_body(503, "ServiceUnavailable", "injected: LIST unavailable"))
             items = self.list(kind, ns, fsel, lsel)
-            return self._json({"kind": lists[kind], "apiVersion": "v1",
-                               "metadata": {"resourceVersion": str(self.rv)}, "items": items})
+            md = {"resourceVersion": str(self.rv)}
+            # pagination (kube-apiserver limit / continue): key order, "<rv>:<ns>/<name>" resumes after an item
+            cont = q.get("continue", "")
+            limit = int(q.get("limit", "0") or 0)
+            if cont or limit > 0:
+                items.sort(key=_obj_key)
+            if cont:
+                rv_s, _, last = cont.partition(":")
+                md["resourceVersion"] = rv_s
+                items = [o for o in items if _obj_key(o) > tuple(last.split("/", 1))]
+            if limit > 0 and len(items) > limit:
+                items = items[:limit]
+                md["continue"] = f"{md['resourceVersion']}:{'/'.join(_obj_key(items[-1]))}"
+            return self._json({"kind": lists[kind], "apiVersion": "v1", "metadata": md, "items": items})
         return h
 
     async def _watch(self, request, kind, ns, fsel, lsel, rv_s):

@@ -75,7 +75,8 @@ class Handler:
 
 class Informer:
     def __init__(self, client: KubeClient, kind: str, namespace: str | None = None, field_selector: str = "",
-                 label_selector: str = "", resync_period: float = 0.0, watch_timeout: int = 300):
+                 label_selector: str = "", resync_period: float = 0.0, watch_timeout: int = 300,
+                 page_size: int = 500):
         self.client = client
         self.kind = kind
         self.namespace = namespace
@@ -83,6 +84,7 @@ class Informer:
         self.label_selector = label_selector
         self.resync_period = resync_period
         self.watch_timeout = watch_timeout
+        self.page_size = page_size  # LIST in pages (limit / continue); 0 = one request
         self.store: dict[str, dict] = {}
         self.handlers: list[Handler] = []
         self.last_rv = ""
@@ -159,7 +161,8 @@ class Informer:
 
     async def _list(self):
         started = time.monotonic()
-        lst = await self.client.list(self.kind, self.namespace, self.field_selector, self.label_selector)
+        lst = await self.client.list(self.kind, self.namespace, self.field_selector, self.label_selector,
+                                     page_size=self.page_size)
         items = lst.get("items") or []
         new = {obj_key(o): o for o in items}
         old = self.store

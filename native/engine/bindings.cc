@@ -372,6 +372,8 @@ class Engine {
     d["pod_rewatches"] = s.pod_watches;
     d["node_rewatches"] = s.node_watches;
     d["watch_errors"] = s.watch_errors;
+    d["pod_list_pages"] = s.pod_list_pages;
+    d["node_list_pages"] = s.node_list_pages;
     d["resyncs"] = s.resyncs;
     d["recovered"] = s.recovered;
     d["last_error"] = ctl_->last_error();

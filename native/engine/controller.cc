@@ -104,6 +104,8 @@ ControllerStats Controller::stats() const {
   s.pod_watches = pods_->rewatches();
   s.node_watches = nodes_->rewatches();
   s.watch_errors = pods_->errors() + nodes_->errors();
+  s.pod_list_pages = pods_->list_pages();
+  s.node_list_pages = nodes_->list_pages();
   return s;
 }
 

@@ -48,6 +48,7 @@ struct ControllerConfig {
 struct ControllerStats {
   uint64_t pod_events = 0, node_events = 0, syncs = 0, removes = 0, upserts = 0, resyncs = 0;
   uint64_t pod_lists = 0, node_lists = 0, pod_watches = 0, node_watches = 0, watch_errors = 0;
+  uint64_t pod_list_pages = 0, node_list_pages = 0;
   uint64_t recovered = 0;  // pods replayed by BuildCache
 };
 

@@ -1190,21 +1190,51 @@ class Server {
     return -1;
   }
 
+  // LIST, optionally paginated like kube-apiserver: `limit` caps the items of one response and
+  // metadata.continue ("<rv>:<ns>/<name>" of the last item sent) resumes after it, in key order; every
+  // page reports the first page's resourceVersion.
   std::string list_json(const std::string& kind, const std::string& ns, const std::string& fsel,
-                        const std::string& lsel) {
+                        const std::string& lsel, int64_t limit = 0, const std::string& cont = std::string()) {
     static const std::map<std::string, std::string> lists = {
         {"pods", "PodList"}, {"nodes", "NodeList"}, {"events", "EventList"}, {"leases", "LeaseList"}};
-    std::string o = "{\"kind\":\"" + lists.at(kind) + "\",\"apiVersion\":\"v1\",\"metadata\":{\"resourceVersion\":\"" +
-                    std::to_string(rv_) + "\"},\"items\":[";
-    bool first = true;
-    Selector fs = Selector::parse(fsel, true), ls = Selector::parse(lsel, false);
-    for (auto& kv : store_[kind]) {
-      if (!ns.empty() && kv.second->ns != ns) continue;
-      if (!fs.matches(kv.second->v) || !ls.matches(kv.second->v)) continue;
-      if (!first) o.push_back(',');
-      first = false;
-      o.append(kv.second->json);
+    auto& m = store_[kind];
+    auto it = m.begin();
+    std::string list_rv = std::to_string(rv_);
+    if (!cont.empty()) {
+      size_t colon = cont.find(':'), slash = cont.find('/', colon == std::string::npos ? 0 : colon);
+      if (colon == std::string::npos || slash == std::string::npos) {
+        throw HttpError{400, status_body(400, "BadRequest", "invalid continue token")};
+      }
+      list_rv = cont.substr(0, colon);
+      it = m.upper_bound(Key{cont.substr(colon + 1, slash - colon - 1), cont.substr(slash + 1)});
     }
+    std::string items;
+    bool first = true;
+    int64_t n = 0;
+    std::string next;
+    const Key* last_sent = nullptr;
+    Selector fs = Selector::parse(fsel, true), ls = Selector::parse(lsel, false);
+    for (; it != m.end(); ++it) {
+      if (!ns.empty() && it->second->ns != ns) continue;
+      if (!fs.matches(it->second->v) || !ls.matches(it->second->v)) continue;
+      if (limit > 0 && n == limit) {  // more matching items remain: continue after the last one sent
+        next = list_rv + ":" + last_sent->first + "/" + last_sent->second;
+        break;
+      }
+      if (!first) items.push_back(',');
+      first = false;
+      items.append(it->second->json);
+      last_sent = &it->first;
+      ++n;
+    }
+    std::string o = "{\"kind\":\"" + lists.at(kind) + "\",\"apiVersion\":\"v1\",\"metadata\":{\"resourceVersion\":\"" +
+                    list_rv + "\"";
+    if (!next.empty()) {
+      o.append(",\"continue\":");
+      json::append_quoted(&o, next);
+    }
+    o.append("},\"items\":[");
+    o.append(items);
     o.append("]}");
     return o;
   }
@@ -1354,8 +1384,10 @@ class Server {
       if (m == "GET") {
         auto w = q.find("watch");
         if (w != q.end() && (w->second == "1" || w->second == "true")) return start_watch(L, c, req, kind, ns, q);
+        int64_t limit = q.count("limit") ? std::atoll(q["limit"].c_str()) : 0;
         rep->body = list_json(kind, ns, q.count("fieldSelector") ? q["fieldSelector"] : "",
-                              q.count("labelSelector") ? q["labelSelector"] : "");
+                              q.count("labelSelector") ? q["labelSelector"] : "", limit,
+                              q.count("continue") ? q["continue"] : "");
         return true;
       }
       if (m == "POST") {

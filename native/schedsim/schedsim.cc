@@ -24,6 +24,13 @@
 //   gsx-schedsim --apiserver URL --extender URL [--profile shared-gpu|aliyun]
 //                [--node-policy binpack|spread|first] [--bind-threads N]
 //                [--port P] [--port-file F] [--scheduler-name S]
+//                [--nodes-to-score adaptive|all|<percent>]
+//
+// Node sampling follows kube-scheduler's numFeasibleNodesToFind: below 100
+// nodes every feasible node goes to the extender; above, the search stops once
+// max(100, N * p / 100) feasible nodes were found, with the adaptive
+// p = max(5, 50 - N / 125) percent (percentageOfNodesToScore unset), starting
+// where the previous cycle stopped (nextStartNodeIndex).
 #include <signal.h>
 #include <unistd.h>
 
@@ -86,8 +93,9 @@ int64_t quantity_at(const json::Doc& d, int64_t idx) {
 class Sim {
  public:
   Sim(ApiConfig api, ApiConfig ext, Profile p, std::string policy, std::string sched_name, int bind_threads,
-      double backoff)
-      : p_(std::move(p)), policy_(std::move(policy)), sched_(std::move(sched_name)), ext_(ext), backoff_(backoff) {
+      double backoff, double score_pct = 0)
+      : p_(std::move(p)), policy_(std::move(policy)), sched_(std::move(sched_name)), ext_(ext), backoff_(backoff),
+        score_pct_(score_pct) {
     ReflectorConfig pr;
     pr.path = "/api/v1/pods";
     ReflectorHandler ph;
@@ -342,12 +350,25 @@ class Sim {
     Timing& tm = timings_[key];
     if (tm.seen == 0) tm.seen = now_s();
     tm.attempts++;
-    // NodeResourcesFit on the aggregate (sorted by name, like the Python simulator's list order)
+    // NodeResourcesFit on the aggregate (name order, like the Python simulator's list order), stopping at
+    // kube-scheduler's numFeasibleNodesToFind from a rotating start index
     std::vector<std::string> cands;
-    for (auto& kv : nodes_) {
-      int64_t used = used_.count(kv.first) ? used_[kv.first] : 0;
-      if (pi.request == 0 || kv.second - used >= pi.request) cands.push_back(kv.first);
+    const size_t n_all = nodes_.size();
+    const size_t want = feasible_to_find(n_all);
+    if (node_order_.size() != n_all) {
+      node_order_.clear();
+      for (auto& kv : nodes_) node_order_.push_back(kv.first);
     }
+    size_t processed = 0;
+    for (size_t k = 0; k < n_all && cands.size() < want; ++k) {
+      const std::string& name = node_order_[(next_start_ + k) % n_all];
+      ++processed;
+      auto nit = nodes_.find(name);
+      if (nit == nodes_.end()) continue;
+      int64_t used = used_.count(name) ? used_[name] : 0;
+      if (pi.request == 0 || nit->second - used >= pi.request) cands.push_back(name);
+    }
+    if (n_all) next_start_ = (next_start_ + processed) % n_all;
     if (cands.empty()) {
       unschedulable_++;
       tm.error = "0 nodes available: Insufficient " + p_.resource;
@@ -418,6 +439,14 @@ class Sim {
     scheduled_++;
     jobs_.push_back(BindJob{key, pi.ns, pi.name, pi.uid, node});
     bcv_.notify_one();
+  }
+
+  size_t feasible_to_find(size_t n) const {
+    if (score_pct_ == 100 || n < 100) return n;  // all nodes (minFeasibleNodesToFind = 100)
+    double pct = score_pct_;
+    if (pct <= 0) pct = std::max(5.0, 50.0 - static_cast<double>(n) / 125.0);  // adaptive
+    size_t k = static_cast<size_t>(static_cast<double>(n) * pct / 100.0);
+    return std::max<size_t>(100, k);
   }
 
   std::string pick_locked(const std::vector<std::string>& names) {
@@ -498,6 +527,9 @@ class Sim {
   std::string policy_, sched_;
   ApiConfig ext_;
   double backoff_;
+  double score_pct_ = 0;  // percentageOfNodesToScore: 0 adaptive, 100 all
+  std::vector<std::string> node_order_;  // node names in order (rebuilt when the set changes size)
+  size_t next_start_ = 0;
   int nbind_ = 16;
   std::unique_ptr<Reflector> pods_r_, nodes_r_;
   std::unique_ptr<ApiClient> filter_api_, bind_api_;
@@ -527,7 +559,7 @@ int main(int argc, char** argv) {
   std::string apiserver, extender, profile = "shared-gpu", policy = "binpack", host = "127.0.0.1", port_file;
   std::string sched = "default-scheduler";
   int port = 0, bind_threads = 16;
-  double backoff = 0.05;
+  double backoff = 0.05, score_pct = 0;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&](const char* name) -> std::string {
@@ -547,6 +579,10 @@ int main(int argc, char** argv) {
     else if (a == "--bind-threads" || a == "--max-inflight-binds") bind_threads = std::max(1, std::min(256, std::atoi(val("--bind-threads").c_str())));
     else if (a == "--scheduler-name") sched = val("--scheduler-name");
     else if (a == "--retry-backoff") backoff = std::atof(val("--retry-backoff").c_str());
+    else if (a == "--nodes-to-score") {
+      std::string v = val("--nodes-to-score");
+      score_pct = v == "adaptive" ? 0 : v == "all" ? 100 : std::atof(v.c_str());
+    }
     else if (a == "-h" || a == "--help") {
       std::printf("usage: gsx-schedsim --apiserver URL --extender URL [--profile P] [--node-policy binpack|spread|first]\n"
                   "                    [--bind-threads N] [--port P] [--port-file F] [--scheduler-name S]\n");
@@ -572,7 +608,7 @@ int main(int argc, char** argv) {
   ext.server = extender;
   ext.timeout_s = 60;
   // bind threads beyond 64 cannot keep their own idle connection in the pool
-  Sim sim(api, ext, profile_by_name(profile), policy, sched, std::min(bind_threads, 64), backoff);
+  Sim sim(api, ext, profile_by_name(profile), policy, sched, std::min(bind_threads, 64), backoff, score_pct);
   std::string err;
   if (!sim.start(&err)) {
     std::fprintf(stderr, "gsx-schedsim: %s\n", err.c_str());

@@ -432,3 +432,40 @@ def test_leader_steps_down_before_standby_can_acquire():
             await cb.close()
             await api.stop()
     asyncio.run(go())
+
+
+@pytest.mark.parametrize("impl", ["python", "native"])
+def test_paginated_list_limit_continue(impl):
+    """kube-apiserver pagination on both fake apiservers: pages of `limit`, `continue` resumes in key order,
+    every page carries the first page's resourceVersion; the reflectors assemble complete LISTs from pages."""
+    from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver
+
+    async def go():
+        if impl == "python":
+            runner = await FakeApiServerRunner().start()
+            url, child = runner.url, None
+        else:
+            child = start_apiserver(native=True)
+            url, runner = child.url, None
+        c = KubeClient(url)
+        try:
+            for i in range(23):
+                await c.create("pods", make_pod(f"p{i:02d}", 1, namespace="a" if i % 2 else "b"))
+            names, cont, rvs = [], "", set()
+            while True:
+                q = "?limit=5" + (f"&continue={cont}" if cont else "")
+                page = await c.request("GET", "/api/v1/pods" + q)
+                assert len(page["items"]) <= 5
+                names += [(p["metadata"]["namespace"], p["metadata"]["name"]) for p in page["items"]]
+                rvs.add(page["metadata"]["resourceVersion"])
+                cont = page["metadata"].get("continue", "")
+                if not cont:
+                    break
+            assert len(names) == 23 and names == sorted(names) and len(rvs) == 1
+        finally:
+            await c.close()
+            if runner:
+                await runner.stop()
+            if child:
+                child.stop()
+    asyncio.run(go())
