@@ -286,7 +286,9 @@ def main():
     from gpushare_scheduler_extender_amd.utils.cpuset import pin_self, plan
 
     names = ["rank0", "apiserver", "extender", "scheduler", "node-agent"] + [f"rank{r}" for r in range(1, world)]
-    widths = {"extender": 2, "node-agent": 2}
+    # threads per process on the wave's critical path: rank 0 (driver + tracker + runtime endpoint), the
+    # extender (2 loops + bind pool + reflectors), schedsim (cycle + binds), node agent (reflector + workers)
+    widths = {"rank0": 2, "extender": 3, "scheduler": 2, "node-agent": 3}
     mode = a.pin if a.pin != "auto" else "spread"
     cpu_plan = plan(names, widths, mode)
     pin_self(cpu_plan.get(f"rank{rank}"))
@@ -321,7 +323,7 @@ def main():
             # the node's device plugin / kubelet stand-in: one process for all GPUs of the node, like a DaemonSet
             children.append(start_node_agent(api.url, NODE, profile=a.profile, native=a.node_agent == "native",
                                              plugin="inproc" if a.node_agent == "inproc" else "grpc",
-                                             cpus=cpu_plan.get("node-agent")))
+                                             workers=8, cpus=cpu_plan.get("node-agent")))
         api_url, ext_url = api.url, ext.url
 
     import torch

@@ -100,6 +100,15 @@ class ChildProc:
             shutil.rmtree(self.tmp, ignore_errors=True)
 
 
+def tool_path(name: str) -> Path:
+    """A compiled stand-in: ``_native/<name>``, or ``build/<name><suffix>`` when ``GSX_NATIVE_TOOLS_SUFFIX`` is set
+    (e.g. ``_tsan``: the ThreadSanitizer builds of ``native/build.py tools_tsan``, used by tests/test_sanitizers.py)."""
+    suffix = os.environ.get("GSX_NATIVE_TOOLS_SUFFIX", "")
+    if suffix:
+        return ROOT / "build" / f"{name}{suffix}"
+    return ROOT / "gpushare_scheduler_extender_amd" / "_native" / name
+
+
 FAKEAPI = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-fakeapi"
 
 
@@ -110,10 +119,11 @@ def start_apiserver(native: bool = True, history: int = 200000, threads: int | N
     ``threads``: event loops of the native server (default ``GSX_FAKEAPI_THREADS`` or 1).
     """
     if native:
-        if not FAKEAPI.exists():
-            raise FileNotFoundError(f"{FAKEAPI} missing; run `python native/build.py fakeapi`")
+        exe = tool_path("gsx-fakeapi")
+        if not exe.exists():
+            raise FileNotFoundError(f"{exe} missing; run `python native/build.py fakeapi`")
         threads = threads or int(os.environ.get("GSX_FAKEAPI_THREADS", "1"))
-        return ChildProc([str(FAKEAPI), "--port", "0", "--history", str(history), "--threads", str(threads)],
+        return ChildProc([str(exe), "--port", "0", "--history", str(history), "--threads", str(threads)],
                          "apiserver", cpus=cpus)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.k8s.fakeapi", "--port", "0"], "apiserver", cpus=cpus)
 
@@ -139,9 +149,10 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
     the shipped device plugin, over its unix socket (``plugin="grpc"``) or in-process (``"inproc"``).
     """
     if native:
-        if not NODEAGENT.exists():
-            raise FileNotFoundError(f"{NODEAGENT} missing; run `python native/build.py nodeagent`")
-        return ChildProc([str(NODEAGENT), "--node", node, "--apiserver", apiserver, "--profile", profile,
+        exe = tool_path("gsx-nodeagent")
+        if not exe.exists():
+            raise FileNotFoundError(f"{exe} missing; run `python native/build.py nodeagent`")
+        return ChildProc([str(exe), "--node", node, "--apiserver", apiserver, "--profile", profile,
                           "--workers", str(min(workers, 16))], "node-agent", cpus=cpus)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
                       apiserver, "--profile", profile, "--workers", str(workers), "--plugin", plugin], "node-agent",
@@ -152,7 +163,7 @@ SCHEDSIM = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-schedsim"
 
 
 def start_scheduler(apiserver: str, extender: str, profile: str = "shared-gpu", max_inflight_binds: int = 256,
-                    native: bool = True, cpus: list[int] | None = None) -> ChildProc:
+                    native: bool = True, cpus: list[int] | None = None, nodes_to_score: str = "") -> ChildProc:
     """kube-scheduler stand-in with a timings endpoint.
 
     ``native=True``: the compiled ``gsx-schedsim`` (native/schedsim, built by
@@ -160,9 +171,11 @@ def start_scheduler(apiserver: str, extender: str, profile: str = "shared-gpu", 
     Both serve the same ``/v1/timings``, ``/v1/forget`` and ``/v1/stats``.
     """
     if native:
-        if not SCHEDSIM.exists():
-            raise FileNotFoundError(f"{SCHEDSIM} missing; run `python native/build.py schedsim`")
-        return ChildProc([str(SCHEDSIM), "--apiserver", apiserver, "--extender", extender, "--profile", profile,
-                          "--bind-threads", str(min(16, max_inflight_binds))], "scheduler", cpus=cpus)
+        exe = tool_path("gsx-schedsim")
+        if not exe.exists():
+            raise FileNotFoundError(f"{exe} missing; run `python native/build.py schedsim`")
+        extra = ["--nodes-to-score", nodes_to_score] if nodes_to_score else []
+        return ChildProc([str(exe), "--apiserver", apiserver, "--extender", extender, "--profile", profile,
+                          "--bind-threads", str(min(16, max_inflight_binds)), *extra], "scheduler", cpus=cpus)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.sim", "--apiserver", apiserver, "--extender", extender,
                       "--profile", profile, "--max-inflight-binds", str(max_inflight_binds)], "scheduler", cpus=cpus)

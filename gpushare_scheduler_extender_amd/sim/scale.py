@@ -31,7 +31,7 @@ import time
 from ..k8s.objects import make_node, make_pod
 from ..models.profile import ALIYUN
 from ..utils.cpuset import plan
-from .cluster import ChildProc, SCHEDSIM, start_apiserver, start_extender
+from .cluster import start_apiserver, start_extender, start_scheduler
 
 GIB_PER_DEV = 268  # a 288 GB MI355X in GiB units
 DEVS = 8
@@ -184,9 +184,8 @@ def run_one(n_nodes: int, pods_per_node: int, churn_batches: int, batch: int, fi
         rss_sync = _rss_mib(ext.proc.pid)
         ctl = extender_stats(E, ext.url).get("controller", {})
         flt = filter_latency(E, ext.url, n_nodes, filter_reps)
-        sched = ChildProc([str(SCHEDSIM), "--apiserver", api.url, "--extender", ext.url, "--profile", ALIYUN.name,
-                           "--bind-threads", "16", "--nodes-to-score", "adaptive"], "scheduler",
-                          cpus=cpus.get("scheduler"))
+        sched = start_scheduler(api.url, ext.url, profile=ALIYUN.name, max_inflight_binds=16,
+                                cpus=cpus.get("scheduler"), nodes_to_score="adaptive")
         children.append(sched)
         ch = churn(E, api.url, sched.url, churn_batches, batch)
         return {"nodes": n_nodes, "devices": n_nodes * DEVS, "resident_pods": n_nodes * pods_per_node,

@@ -80,7 +80,7 @@ def _compile_objs(srcs: list[Path], compiler: str, flags: list[str], tag: str, f
 def build_engine(force: bool = False, verbose: bool = False) -> Path:
     src = NATIVE / "engine"
     srcs = sorted(src.glob("*.cc"))
-    srcs = [s for s in srcs if s.name != "engine_test.cc"]
+    srcs = [s for s in srcs if s.name not in ("engine_test.cc", "controller_test.cc")]
     headers = sorted(src.glob("*.h"))
     out = OUT / f"_engine{EXT}"
     flags = [*CXXFLAGS, *_pybind_includes(), "-I" + str(src)]
@@ -94,7 +94,7 @@ def build_engine(force: bool = False, verbose: bool = False) -> Path:
 def _build_native_tool(name: str, srcdir: str, force: bool, verbose: bool) -> Path:
     """A standalone executable from ``native/<srcdir>/*.cc`` linked with the engine's objects."""
     src = NATIVE / "engine"
-    eng = [s for s in sorted(src.glob("*.cc")) if s.name not in ("bindings.cc", "engine_test.cc")]
+    eng = [s for s in sorted(src.glob("*.cc")) if s.name not in ("bindings.cc", "engine_test.cc", "controller_test.cc")]
     headers = sorted(src.glob("*.h"))
     flags = [*CXXFLAGS, "-I" + str(src)]
     objs = _compile_objs(eng, "g++", flags, "tool", force, verbose, headers)
@@ -171,28 +171,56 @@ def build_tools(force: bool = False, verbose: bool = False) -> list[Path]:
     return outs
 
 
-def build_asan(force: bool = False, verbose: bool = False) -> Path:
-    """Host-only ASan/UBSan build of the engine's C++ unit test."""
+TEST_MAINS = ("engine_test.cc", "controller_test.cc")
+
+
+def _host_clang() -> str:
+    """ROCm's clang++: its sanitizer runtimes intercept pthread_cond_clockwait, which std::condition_variable
+    uses for steady-clock waits on this glibc; GCC 11's libtsan does not and reports false double locks."""
+    c = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / "lib" / "llvm" / "bin" / "clang++"
+    return str(c) if c.exists() else "g++"
+
+
+def _sanitized(test: str, tag: str, flags: list[str], force: bool, verbose: bool) -> Path:
+    """Host-only sanitizer build of one test main against every engine source (not the Python bindings)."""
     src = NATIVE / "engine"
-    out = ROOT / "build" / "engine_test_asan"
-    srcs = [s for s in sorted(src.glob("*.cc")) if s.name != "bindings.cc"]
+    out = ROOT / "build" / f"{test}_{tag}"
+    lib = [s for s in sorted(src.glob("*.cc")) if s.name != "bindings.cc" and s.name not in TEST_MAINS]
+    srcs = [*lib, src / f"{test}.cc"]
     if force or _newer(out, srcs + sorted(src.glob("*.h"))):
         out.parent.mkdir(parents=True, exist_ok=True)
-        _run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
-              "-I" + str(src), *map(str, srcs), "-o", str(out), "-lssl", "-lcrypto", "-lpthread", "-ldl"], verbose)
+        _run([_host_clang(), "-O1", "-g", "-std=c++17", *flags, "-fno-omit-frame-pointer", "-I" + str(src),
+              *map(str, srcs), "-o", str(out), "-lssl", "-lcrypto", "-lpthread", "-ldl"], verbose)
     return out
 
 
-def build_tsan(force: bool = False, verbose: bool = False) -> Path:
-    """Host-only ThreadSanitizer build of the same test (epoll loops + bind pool + ledger mutex)."""
+def build_asan(force: bool = False, verbose: bool = False) -> list[Path]:
+    """ASan + UBSan builds of the engine unit/stress test and the controller concurrency test."""
+    return [_sanitized(t, "asan", ["-fsanitize=address,undefined"], force, verbose)
+            for t in ("engine_test", "controller_test")]
+
+
+def build_tsan(force: bool = False, verbose: bool = False) -> list[Path]:
+    """ThreadSanitizer builds of the same tests (epoll loops, bind pool, reflectors, resync, GC, tracker)."""
+    return [_sanitized(t, "tsan", ["-fsanitize=thread"], force, verbose) for t in ("engine_test", "controller_test")]
+
+
+def build_tools_tsan(force: bool = False, verbose: bool = False) -> list[Path]:
+    """ThreadSanitizer builds of the compiled stand-ins (``build/gsx-{fakeapi,schedsim,nodeagent}_tsan``);
+    ``GSX_NATIVE_TOOLS_SUFFIX=_tsan`` makes sim/cluster.py start these instead of the optimised ones."""
     src = NATIVE / "engine"
-    out = ROOT / "build" / "engine_test_tsan"
-    srcs = [s for s in sorted(src.glob("*.cc")) if s.name != "bindings.cc"]
-    if force or _newer(out, srcs + sorted(src.glob("*.h"))):
-        out.parent.mkdir(parents=True, exist_ok=True)
-        _run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=thread", "-fno-omit-frame-pointer",
-              "-I" + str(src), *map(str, srcs), "-o", str(out), "-lssl", "-lcrypto", "-lpthread", "-ldl"], verbose)
-    return out
+    lib = [s for s in sorted(src.glob("*.cc")) if s.name != "bindings.cc" and s.name not in TEST_MAINS]
+    outs = []
+    for tool in ("fakeapi", "schedsim", "nodeagent"):
+        mains = sorted((NATIVE / tool).glob("*.cc"))
+        out = ROOT / "build" / f"gsx-{tool}_tsan"
+        if force or _newer(out, lib + mains + sorted(src.glob("*.h"))):
+            out.parent.mkdir(parents=True, exist_ok=True)
+            _run([_host_clang(), "-O1", "-g", "-std=c++17", "-fsanitize=thread", "-fno-omit-frame-pointer",
+                  "-I" + str(src), *map(str, lib + mains), "-o", str(out), "-lssl", "-lcrypto", "-lpthread", "-ldl"],
+                 verbose)
+        outs.append(out)
+    return outs
 
 
 TARGETS = {
@@ -205,6 +233,7 @@ TARGETS = {
     "tools": build_tools,
     "asan": build_asan,
     "tsan": build_tsan,
+    "tools_tsan": build_tools_tsan,
 }
 DEFAULT = ["engine", "schedsim", "nodeagent", "fakeapi", "mxdev", "kernels", "tools"]
 
