@@ -273,7 +273,7 @@ class ExtenderServer:
         r.add_get("/metrics", self.h_metrics)
         r.add_get("/healthz", self.h_healthz)
         r.add_get("/debug/engine", self.h_debug_engine)
-        add_pprof(app)
+        add_pprof(app, self.engine)
         return app
 
     async def h_filter(self, request: web.Request):

@@ -7,6 +7,7 @@
 
 #include <memory>
 
+#include "introspect.h"
 #include "ledger.h"
 #include "quantity.h"
 #include "controller.h"
@@ -109,7 +110,7 @@ class Engine {
     nv.count = count;
     nv.dev_totals = std::move(devs);
     nv.address = address;
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.upsert_node(nv);
   }
 
@@ -119,41 +120,41 @@ class Engine {
     if (!parse_node_bytes(b, l_.profile(), &nv, &err)) throw py::value_error(err);
     bool rebuilt;
     {
-      std::lock_guard<std::mutex> g(l_.mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
       rebuilt = l_.upsert_node(nv);
     }
     return py::make_tuple(nv.name, rebuilt);
   }
 
   bool remove_node(const std::string& name) {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.remove_node(name);
   }
 
   bool has_node(const std::string& name) {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.has_node(name);
   }
 
   py::tuple node_info(const std::string& name) {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     const NodeState* n = l_.node(name);
     if (!n) return py::make_tuple();
     return py::make_tuple(n->total, n->count, n->address);
   }
 
   int upsert_pod(const PodView& v) {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.upsert_pod(v);
   }
 
   bool remove_pod(const std::string& uid) {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.remove_pod(uid);
   }
 
   bool known(const std::string& uid) {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.known(uid);
   }
 
@@ -161,7 +162,7 @@ class Engine {
     int64_t dev;
     int st;
     {
-      std::lock_guard<std::mutex> g(l_.mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
       st = l_.pod_state(uid, &dev);
     }
     return py::make_tuple(st, dev);
@@ -172,12 +173,12 @@ class Engine {
     PodView v;
     std::string err;
     if (!parse_pod_bytes(b, l_.profile(), &v, &err)) throw py::value_error(err);
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.upsert_pod(v);
   }
 
   int check(const std::string& node, int64_t req) {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return static_cast<int>(l_.check(node, req));
   }
 
@@ -186,7 +187,7 @@ class Engine {
     std::string out;
     {
       py::gil_scoped_release rel;
-      std::lock_guard<std::mutex> g(l_.mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
       out = filter_body(l_, v);
     }
     return py::bytes(out);
@@ -197,7 +198,7 @@ class Engine {
     std::string out;
     {
       py::gil_scoped_release rel;
-      std::lock_guard<std::mutex> g(l_.mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
       out = prioritize_body(l_, v);
     }
     return py::bytes(out);
@@ -206,13 +207,13 @@ class Engine {
   py::tuple assume(const std::string& uid, const std::string& ns, const std::string& name,
                    const std::string& node, int64_t req) {
     int64_t dev_total = -1;
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     int64_t dev = l_.assume(uid, ns, name, node, req, &dev_total);
     return py::make_tuple(dev, dev_total);
   }
 
   void finish_bind(const std::string& uid, bool ok, double ttl) {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     l_.finish_bind(uid, ok, ttl);
   }
 
@@ -221,7 +222,7 @@ class Engine {
     bool need = false;
     int n;
     {
-      std::lock_guard<std::mutex> g(l_.mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
       n = l_.gc(list_start, &need);
     }
     return py::make_tuple(n, need);
@@ -243,19 +244,19 @@ class Engine {
     bool found;
     std::string s;
     {
-      std::lock_guard<std::mutex> g(l_.mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
       s = l_.inspect_json(node, &found);
     }
     return py::make_tuple(py::bytes(s), found);
   }
 
   std::vector<std::pair<int64_t, int64_t>> node_devices(const std::string& node) {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.node_devices(node);
   }
 
   std::vector<std::string> node_names() {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.node_names();
   }
 
@@ -263,7 +264,7 @@ class Engine {
     Stats s;
     size_t pods;
     {
-      std::lock_guard<std::mutex> g(l_.mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
       s = l_.stats();
       pods = l_.pod_count();
     }
@@ -421,6 +422,19 @@ class Engine {
     return d;
   }
 
+  // ---- introspection for /debug/pprof (introspect.h) ----
+  py::dict ledger_mutex() {
+    introspect::MutexStats m = l_.mu().stats();
+    py::dict d;
+    d["acquisitions"] = m.acquisitions;
+    d["contended"] = m.contended;
+    d["wait_s"] = m.wait_s;
+    d["max_wait_s"] = m.max_wait_s;
+    d["hold_s"] = m.hold_s;
+    d["max_hold_s"] = m.max_hold_s;
+    return d;
+  }
+
   void set_binds_enabled(bool on) {
     binds_enabled_ = on;
     if (srv_) srv_->set_binds_enabled(on);
@@ -442,7 +456,7 @@ class Engine {
   }
 
   size_t pending_count() {
-    std::lock_guard<std::mutex> g(l_.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.pending_count();
   }
 
@@ -581,6 +595,21 @@ class PyPodRuntime {
 }  // namespace
 
 PYBIND11_MODULE(_engine, m) {
+  m.def(
+      "native_stacks",
+      [](std::vector<int> tids, double timeout) {
+        std::vector<introspect::Sample> got;
+        {
+          py::gil_scoped_release rel;  // Python threads must be able to run their handlers too
+          got = introspect::capture(tids, timeout);
+        }
+        py::list out;
+        for (auto& smp : got) out.append(py::make_tuple(smp.tid, smp.comm, smp.ok, smp.frames));
+        return out;
+      },
+      py::arg("tids") = std::vector<int>(), py::arg("timeout") = 0.05,
+      "Stack samples (tid, comm, ok, frames innermost-first) of this process's threads (all when tids is empty).");
+
   m.doc() = "gpushare MI355X native ledger engine";
 
   py::class_<PodView>(m, "PodView")
@@ -646,6 +675,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("controller_overcommitted", &Engine::controller_overcommitted)
       .def("controller_stats", &Engine::controller_stats)
       .def("server_stats", &Engine::server_stats)
+      .def("ledger_mutex", &Engine::ledger_mutex)
       .def("drain_bind_failures", &Engine::drain_bind_failures)
       .def("set_binds_enabled", &Engine::set_binds_enabled)
       .def("pending_count", &Engine::pending_count);

@@ -1,4 +1,5 @@
 #include "controller.h"
+#include "introspect.h"
 
 #include <chrono>
 #include <unordered_set>
@@ -42,7 +43,10 @@ bool Controller::start(double sync_timeout_s, std::string* err) {
     *err = "pod informer did not sync: " + pods_->last_error();
     return false;
   }
-  if (cfg_.resync_s > 0 && !resync_th_.joinable()) resync_th_ = std::thread([this] { resync_loop(); });
+  if (cfg_.resync_s > 0 && !resync_th_.joinable()) resync_th_ = std::thread([this] {
+    introspect::name_thread("resync");
+    resync_loop();
+  });
   return true;
 }
 
@@ -64,7 +68,7 @@ int Controller::gc_reservations(bool* relist_requested) {
   bool need = false;
   int n;
   {
-    std::lock_guard<std::mutex> g(l_->mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
     n = l_->gc(pods_->last_list_start(), &need);
   }
   if (need) pods_->request_relist();
@@ -126,7 +130,7 @@ void Controller::sync(const std::string& key) {
     auto gone = removed_.find(key);
     if (gone != removed_.end()) {
       {
-        std::lock_guard<std::mutex> g(l_->mu());
+        std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
         l_->remove_pod(gone->second.v.uid);
       }
       stats_.removes++;
@@ -136,7 +140,7 @@ void Controller::sync(const std::string& key) {
   }
   removed_.erase(key);
   const PodView& v = it->second.v;
-  std::lock_guard<std::mutex> g(l_->mu());
+  std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
   if (v.complete()) {
     l_->remove_pod(v.uid);
     stats_.removes++;
@@ -156,7 +160,7 @@ void Controller::h_update(const Entry& old, const std::string& key) {
   int64_t dev = -1;
   int state;
   {
-    std::lock_guard<std::mutex> g(l_->mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
     state = l_->pod_state(cur.v.uid, &dev);
   }
   bool enqueue = false;
@@ -259,7 +263,7 @@ void Controller::build_cache() {
   // durable allocation record), then the informer's initial adds.
   uint64_t n = 0;
   {
-    std::lock_guard<std::mutex> g(l_->mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
     for (auto& kv : store_) {
       const PodView& v = kv.second.v;
       if (!kv.second.share || v.complete()) continue;
@@ -275,7 +279,7 @@ void Controller::build_cache() {
   // consistency check: report devices whose annotations add
   // up to more than capacity instead of wrapping (nodeinfo.go:260)
   overcommitted_.clear();
-  std::lock_guard<std::mutex> g(l_->mu());
+  std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
   for (const std::string& node : l_->node_names()) {
     auto devs = l_->node_devices(node);
     for (size_t i = 0; i < devs.size(); ++i) {
@@ -318,7 +322,7 @@ void Controller::on_node_event(Ev ev, const json::Doc& d, uint32_t obj) {
     std::lock_guard<std::mutex> g(smu_);
     stats_.node_events++;
   }
-  std::lock_guard<std::mutex> g(l_->mu());
+  std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
   if (ev == Ev::Deleted) {
     l_->remove_node(nv.name);
     listed_nodes_.erase(nv.name);
@@ -330,7 +334,7 @@ void Controller::on_node_event(Ev ev, const json::Doc& d, uint32_t obj) {
 
 void Controller::on_node_list(const ListView& lv) {
   std::unordered_set<std::string> seen;
-  std::lock_guard<std::mutex> g(l_->mu());
+  std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
   for (size_t k = 0; k < lv.size(); ++k) {
     NodeView nv;
     if (!parse_node(lv.doc(k), lv.obj(k), l_->profile(), &nv)) continue;

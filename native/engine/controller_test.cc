@@ -227,7 +227,7 @@ int main(int argc, char** argv) {
   th.emplace_back([&] {  // observers: inspect, stats, lister
     while (!stop.load()) {
       {
-        std::lock_guard<std::mutex> g(ledger.mu());
+        std::lock_guard<introspect::ProfiledMutex> g(ledger.mu());
         bool found = false;
         std::string js = ledger.inspect_json("", &found);
         CHECK(!js.empty());
@@ -269,7 +269,7 @@ int main(int argc, char** argv) {
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
   }
   {
-    std::lock_guard<std::mutex> g(ledger.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(ledger.mu());
     for (int i = 0; i < kNodes; ++i) {
       for (auto& d : ledger.node_devices("n" + std::to_string(i))) CHECK(d.second <= d.first);
     }

@@ -1,4 +1,5 @@
 #include "ctlserver.h"
+#include "introspect.h"
 
 #include <arpa/inet.h>
 #include <netinet/in.h>
@@ -36,7 +37,10 @@ int CtlServer::start(const std::string& host, int port, std::string* err) {
   }
   socklen_t len = sizeof(a);
   getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &len);
-  acc_ = std::thread([this] { accept_loop(); });
+  acc_ = std::thread([this] {
+    introspect::name_thread("ctl-accept");
+    accept_loop();
+  });
   return ntohs(a.sin_port);
 }
 
@@ -70,7 +74,10 @@ void CtlServer::accept_loop() {
       return;
     }
     conns_.push_back(fd);
-    threads_.emplace_back([this, fd] { serve_conn(fd); });
+    threads_.emplace_back([this, fd] {
+      introspect::name_thread("ctl-conn");
+      serve_conn(fd);
+    });
   }
 }
 

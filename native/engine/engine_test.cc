@@ -270,7 +270,7 @@ static void test_server_stress() {
   CHECK(failed.load() == 0);
   CHECK(bindings.load() == kThreads * kPods);
   {
-    std::lock_guard<std::mutex> g(l.mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l.mu());
     for (auto& d : l.node_devices("n")) CHECK(d.second == 1000);
   }
   srv.reset();  // stops the loops and closes the keep-alive apiserver connections

@@ -1,4 +1,5 @@
 #include "informer.h"
+#include "introspect.h"
 
 #include <sys/socket.h>
 
@@ -33,7 +34,11 @@ void Reflector::start() {
   if (th_.joinable()) return;
   stop_.store(false);
   stream_.aborted.store(false);
-  th_ = std::thread([this] { run(); });
+  th_ = std::thread([this] {
+    std::string res = rc_.path.substr(rc_.path.rfind('/') + 1);
+    introspect::name_thread("refl-" + res);
+    run();
+  });
 }
 
 void Reflector::stop() {

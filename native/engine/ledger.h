@@ -24,6 +24,7 @@
 #include <deque>
 #include <vector>
 
+#include "introspect.h"
 #include "model.h"
 
 namespace gsx {
@@ -122,7 +123,7 @@ class Ledger {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }
 
-  std::mutex& mu() { return mu_; }
+  introspect::ProfiledMutex& mu() { return mu_; }
 
   // ---- pods seen by the filter verb (native bind fast path) ----
   // The filter request carries the whole v1.Pod; remembering (uid -> ns,
@@ -146,7 +147,7 @@ class Ledger {
   std::map<std::string, NodeState> nodes_;  // ordered: deterministic inspect
   std::unordered_map<std::string, PodRec> pods_;
   Stats stats_;
-  mutable std::mutex mu_;
+  mutable introspect::ProfiledMutex mu_;  // every caller locks it; contention is exported to /debug/pprof/mutex
   std::unordered_map<std::string, PendingPod> pending_;
   std::deque<std::string> pending_order_;
 };

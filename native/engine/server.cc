@@ -1,4 +1,5 @@
 #include "server.h"
+#include "introspect.h"
 
 #include <arpa/inet.h>
 #include <fcntl.h>
@@ -186,8 +187,20 @@ int NativeServer::start(std::string* err) {
     loops_.push_back(std::move(lp));
   }
   port_ = port;
-  for (auto& lp : loops_) loop_threads_.emplace_back([this, p = lp.get()] { run_loop(p); });
-  for (int i = 0; i < cfg_.pool_threads; ++i) pool_threads_.emplace_back([this] { pool_main(); });
+  int li = 0;
+  for (auto& lp : loops_) {
+    loop_threads_.emplace_back([this, p = lp.get(), li] {
+      introspect::name_thread("http-" + std::to_string(li));
+      run_loop(p);
+    });
+    ++li;
+  }
+  for (int i = 0; i < cfg_.pool_threads; ++i) {
+    pool_threads_.emplace_back([this, i] {
+      introspect::name_thread("bind-" + std::to_string(i));
+      pool_main();
+    });
+  }
   return port_;
 }
 
@@ -419,7 +432,7 @@ void NativeServer::dispatch(Loop* lp, Conn* c, http::Message& req) {
     stats_.filters.fetch_add(1, std::memory_order_relaxed);
     std::string out;
     {
-      std::lock_guard<std::mutex> g(l_->mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
       out = filter_body(*l_, req.body);
     }
     stats_.filter_lat.observe(mono() - t0);
@@ -429,7 +442,7 @@ void NativeServer::dispatch(Loop* lp, Conn* c, http::Message& req) {
   if (req.method == "POST" && path == pre + "/prioritize") {
     std::string out;
     {
-      std::lock_guard<std::mutex> g(l_->mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
       out = prioritize_body(*l_, req.body);
     }
     respond(lp, c, http::response(200, "application/json", out, ka), ka);
@@ -449,7 +462,7 @@ void NativeServer::dispatch(Loop* lp, Conn* c, http::Message& req) {
     std::string out;
     bool found;
     {
-      std::lock_guard<std::mutex> g(l_->mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
       out = l_->inspect_json(node, &found);
     }
     respond(lp, c, http::response(200, "application/json", out, ka), ka);
@@ -546,7 +559,7 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
   uint64_t seq = 0;
   const Profile& prof = l_->profile();
   {
-    std::lock_guard<std::mutex> g(l_->mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
     if (!l_->pending(uid, &pp) || pp.name != name || pp.ns != ns) {
       *fallback = true;  // never filtered here (e.g. restart between filter and bind): slow path
       return {};
@@ -652,7 +665,7 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
     if (status == 409 && msg.find("Precondition failed") != std::string::npos) {
       // UID mismatch: release and let the slow path produce the reference's
       // exact error (gpushare-bind.go:44-65 does a live GET).
-      std::lock_guard<std::mutex> g(l_->mu());
+      std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
       l_->finish_bind(uid, false, 0.0);
       *fallback = true;
       return {};
@@ -665,7 +678,7 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
     break;
   }
   {
-    std::lock_guard<std::mutex> g(l_->mu());
+    std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
     l_->finish_bind(uid, ok, cfg_.reservation_ttl);
     if (ok) l_->forget_pending(uid);
   }

@@ -233,3 +233,53 @@ def test_equal_size_binds_for_different_gpus_land_in_assume_order(native):
         finally:
             await _teardown(api, c, ext)
     asyncio.run(go())
+
+
+def test_pprof_sees_native_threads():
+    """/debug/pprof covers the C++ threads that serve filter / bind (names, native stacks, CPU
+    time, verb latency histograms, ledger mutex profile), not only the Python loop."""
+    async def go():
+        api, c, ext = await _stack()
+        stop = threading.Event()
+        body = wire.filter_args(make_pod("p", 50), ["n"])
+        req = (b"POST /gpushare-scheduler/filter HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n" % len(body)) + body
+
+        def storm():
+            s = socket.create_connection(("127.0.0.1", ext.port), timeout=5)
+            while not stop.is_set():
+                s.sendall(req)
+                buf = b""
+                while not buf.endswith(b"}"):
+                    buf += s.recv(65536)
+            s.close()
+        ts = [threading.Thread(target=storm, daemon=True) for _ in range(3)]
+        for t in ts:
+            t.start()
+        try:
+            from aiohttp import ClientSession
+
+            async with ClientSession() as http:
+                async with http.get(ext.url + "/debug/pprof/goroutine/") as r:
+                    g = await r.text()
+                async with http.get(ext.url + "/debug/pprof/profile?seconds=1&hz=200") as r:
+                    prof = await r.text()
+                async with http.get(ext.url + "/debug/pprof/mutex") as r:
+                    mtx = await r.text()
+                async with http.get(ext.url + "/debug/pprof/threadcreate/") as r:
+                    tc = await r.text()
+        finally:
+            stop.set()
+            for t in ts:
+                t.join(5)
+            await _teardown(api, c, ext)
+        # thread names and symbolised native stacks of the epoll loops, bind pool and reflectors
+        for name in ("gsx-http-0", "gsx-bind-0", "gsx-refl-pods", "gsx-refl-nodes"):
+            assert f"[{name}] native" in g, name
+        assert "NativeServer::run_loop" in g and "Reflector::run" in g
+        # on-CPU profile of the whole process: native frames of the filter path, per-thread CPU, histograms
+        assert "# native filter_latency: n=" in prof and "# ledger mutex: acquisitions=" in prof
+        assert any(ln.startswith("#   gsx-http") for ln in prof.splitlines())
+        stacks = [ln for ln in prof.splitlines() if ln.startswith("gsx-http")]
+        assert stacks and any("NativeServer" in ln for ln in stacks)
+        assert "acquisitions=" in mtx and "native" in tc
+    asyncio.run(go())
