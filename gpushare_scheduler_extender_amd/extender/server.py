@@ -81,12 +81,6 @@ class ExtenderServer:
                                          metrics=self.metrics)
         self.bind_mode = bind_mode
         self.reservation_ttl = reservation_ttl
-        # binds in flight: (seq, node, size, device) -- equal-size pods for different GPUs of one node
-        # reach the apiserver in ASSUME_TIME order (see bind)
-        self._inflight: list[tuple[int, str, int, int]] = []
-        self._bind_seq = 0
-        self._last_assume_ns = 0
-        self._order_cv = asyncio.Condition()
         self.emit_events = emit_events
         self.app = self._make_app()
         self._gc_task: asyncio.Task | None = None
@@ -170,7 +164,8 @@ class ExtenderServer:
             self.metrics.bind_results.labels("pod_lookup_failed").inc()
             return str(e)
         req = podutil.gpu_mem_request(pod, self.profile)
-        dev, dev_total = self.engine.assume(uid, ns, name, node, req)
+        # reservation + ASSUME_TIME + entry in the bind-order set shared with the native front end
+        dev, dev_total, seq, assume_ns = self.engine.assume_ordered(uid, ns, name, node, req)
         if dev < 0:
             self.metrics.bind_results.labels("no_device").inc()
             if dev == -2:
@@ -183,23 +178,15 @@ class ExtenderServer:
                 msg = f"The node {node} can't place the pod {name} in ns {ns}"  # nodeinfo.go:170
             self._event(pod, "FailedBinding", msg)
             return msg
-        # ASSUME_TIME and the ordering sequence in assume order (no await since engine.assume)
-        self._last_assume_ns = max(time.time_ns(), self._last_assume_ns + 1)
-        ann = podutil.bind_annotations(self.profile, dev, dev_total, req, now_ns=self._last_assume_ns)
-        self._bind_seq += 1
-        entry = (self._bind_seq, node, req, dev)
-        self._inflight.append(entry)
+        ann = podutil.bind_annotations(self.profile, dev, dev_total, req, now_ns=assume_ns)
         t0 = time.perf_counter()
         try:
             # kubelet admits a node's pods in binding order and the device plugin hands a request of N
             # units to the earliest-ASSUME_TIME pod of that size: an equal-size pod for another GPU of the
-            # same node must not overtake an earlier one (the reference's node lock across the API calls,
-            # pkg/cache/nodeinfo.go:141-189, guaranteed it); other binds run concurrently
-            def blocked():
-                return any(f[0] < entry[0] and f[1] == node and f[2] == req and f[3] != dev for f in self._inflight)
-            if blocked():
-                async with self._order_cv:
-                    await self._order_cv.wait_for(lambda: not blocked())
+            # same node must not overtake an earlier one, whichever path (native or this one) binds it
+            # (the reference's node lock across the API calls, pkg/cache/nodeinfo.go:141-189)
+            if self.engine.bind_blocked(seq):
+                await asyncio.get_running_loop().run_in_executor(None, self.engine.bind_wait, seq)
             if self.bind_mode == "binding":
                 await self._bind_with_annotations(pod, node, ann)
             else:
@@ -212,9 +199,7 @@ class ExtenderServer:
             return msg
         finally:
             self.metrics.api_latency.labels("bind").observe(time.perf_counter() - t0)
-            self._inflight.remove(entry)
-            async with self._order_cv:
-                self._order_cv.notify_all()
+            self.engine.bind_leave(seq)
         self.engine.finish_bind(uid, True, self.reservation_ttl)
         self.metrics.bind_results.labels("ok").inc()
         return ""

@@ -212,6 +212,25 @@ class Engine {
     return py::make_tuple(dev, dev_total);
   }
 
+  // (dev, dev_total, seq, assume_ns): reservation + ASSUME_TIME + entry in the shared bind-order set
+  py::tuple assume_ordered(const std::string& uid, const std::string& ns, const std::string& name,
+                           const std::string& node, int64_t req) {
+    int64_t dev_total = -1, assume_ns = 0;
+    uint64_t seq = 0;
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
+    int64_t dev = l_.assume_ordered(uid, ns, name, node, req, &dev_total, &seq, &assume_ns);
+    return py::make_tuple(dev, dev_total, seq, assume_ns);
+  }
+
+  bool bind_blocked(uint64_t seq) { return l_.bind_blocked(seq); }
+
+  void bind_wait(uint64_t seq) {
+    py::gil_scoped_release rel;
+    l_.bind_wait(seq, nullptr);
+  }
+
+  void bind_leave(uint64_t seq) { l_.bind_leave(seq); }
+
   void finish_bind(const std::string& uid, bool ok, double ttl) {
     std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     l_.finish_bind(uid, ok, ttl);
@@ -657,6 +676,10 @@ PYBIND11_MODULE(_engine, m) {
       .def("assume", &Engine::assume)
       .def("finish_bind", &Engine::finish_bind, py::arg("uid"), py::arg("ok"), py::arg("ttl") = 30.0)
       .def("gc", &Engine::gc, py::arg("list_start") = 0.0)
+      .def("assume_ordered", &Engine::assume_ordered)
+      .def("bind_blocked", &Engine::bind_blocked)
+      .def("bind_wait", &Engine::bind_wait)
+      .def("bind_leave", &Engine::bind_leave)
       .def("controller_gc", &Engine::controller_gc)
       .def("inspect", &Engine::inspect, py::arg("node") = std::string())
       .def("node_devices", &Engine::node_devices)

@@ -244,6 +244,57 @@ int64_t Ledger::assume(const std::string& uid, const std::string& ns, const std:
   return cand;
 }
 
+int64_t Ledger::assume_ordered(const std::string& uid, const std::string& ns, const std::string& name,
+                               const std::string& node, int64_t req, int64_t* dev_total, uint64_t* seq,
+                               int64_t* assume_ns) {
+  int64_t dev = assume(uid, ns, name, node, req, dev_total);
+  if (dev < 0) return dev;
+  int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                    std::chrono::system_clock::now().time_since_epoch()).count();
+  std::lock_guard<std::mutex> o(order_mu_);
+  last_assume_ns_ = std::max(now, last_assume_ns_ + 1);  // strictly increasing in assume order
+  *assume_ns = last_assume_ns_;
+  *seq = ++order_seq_;
+  inflight_.push_back(InflightBind{node, req, dev, *seq});
+  return dev;
+}
+
+bool Ledger::blocked_locked(const InflightBind& me) const {
+  for (const auto& f : inflight_) {
+    if (f.seq < me.seq && f.node == me.node && f.size == me.size && f.dev != me.dev) return true;
+  }
+  return false;
+}
+
+bool Ledger::bind_blocked(uint64_t seq) {
+  std::lock_guard<std::mutex> o(order_mu_);
+  for (const auto& f : inflight_) {
+    if (f.seq == seq) return blocked_locked(f);
+  }
+  return false;
+}
+
+void Ledger::bind_wait(uint64_t seq, const std::atomic<bool>* stop) {
+  std::unique_lock<std::mutex> o(order_mu_);
+  const InflightBind* me = nullptr;
+  for (const auto& f : inflight_) {
+    if (f.seq == seq) me = &f;
+  }
+  if (!me || !blocked_locked(*me)) return;
+  order_waits_.fetch_add(1, std::memory_order_relaxed);
+  while (blocked_locked(*me) && !(stop && stop->load())) {
+    order_cv_.wait_for(o, std::chrono::milliseconds(100));
+  }
+}
+
+void Ledger::bind_leave(uint64_t seq) {
+  {
+    std::lock_guard<std::mutex> o(order_mu_);
+    inflight_.remove_if([seq](const InflightBind& f) { return f.seq == seq; });
+  }
+  order_cv_.notify_all();
+}
+
 void Ledger::finish_bind(const std::string& uid, bool ok, double ttl_s) {
   auto it = pods_.find(uid);
   if (it == pods_.end()) return;

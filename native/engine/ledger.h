@@ -15,10 +15,13 @@
 #pragma once
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
+#include <list>
 #include <map>
 #include <mutex>
 #include <string>
+#include <atomic>
 #include <unordered_map>
 #include <unordered_set>
 #include <deque>
@@ -100,6 +103,20 @@ class Ledger {
   int64_t assume(const std::string& uid, const std::string& ns, const std::string& name,
                  const std::string& node, int64_t req, int64_t* dev_total);
   void finish_bind(const std::string& uid, bool ok, double ttl_s);
+
+  // ---- bind ordering, shared by the native front end and the Python slow path ----
+  // kubelet admits a node's pods in the order their bindings land, and the device plugin gives a request
+  // of N units to the earliest-ASSUME_TIME unassigned pod of that size (docs/designs/designs.md:93-103):
+  // two equal-size pods headed for different GPUs of one node must reach the apiserver in ASSUME_TIME
+  // order.  assume_ordered() (ledger mutex held) reserves the device, stamps ASSUME_TIME and enters the
+  // in-flight set in one step; bind_wait() (ledger mutex NOT held) blocks only while an earlier
+  // equal-size bind for another GPU of that node is in flight; bind_leave() ends the entry.
+  int64_t assume_ordered(const std::string& uid, const std::string& ns, const std::string& name,
+                         const std::string& node, int64_t req, int64_t* dev_total, uint64_t* seq, int64_t* assume_ns);
+  bool bind_blocked(uint64_t seq);
+  void bind_wait(uint64_t seq, const std::atomic<bool>* stop);
+  void bind_leave(uint64_t seq);
+  uint64_t bind_order_waits() const { return order_waits_.load(); }
   // Expire stale reservations.  A bound reservation the pod informer has not confirmed within its TTL is
   // dropped only if a pod LIST that *started after the bind succeeded* (`confirmed_list_start`, steady-clock
   // seconds; 0 = none) was applied without confirming it: then the apiserver really has no such binding.
@@ -150,6 +167,19 @@ class Ledger {
   mutable introspect::ProfiledMutex mu_;  // every caller locks it; contention is exported to /debug/pprof/mutex
   std::unordered_map<std::string, PendingPod> pending_;
   std::deque<std::string> pending_order_;
+  // in-flight binds (order_mu_ nests inside the ledger mutex, never around it)
+  struct InflightBind {
+    std::string node;
+    int64_t size, dev;
+    uint64_t seq;
+  };
+  bool blocked_locked(const InflightBind& me) const;
+  std::mutex order_mu_;
+  std::condition_variable order_cv_;
+  std::list<InflightBind> inflight_;
+  uint64_t order_seq_ = 0;
+  int64_t last_assume_ns_ = 0;
+  std::atomic<uint64_t> order_waits_{0};
 };
 
 // Full filter verb on a raw ExtenderArgs body; returns the

@@ -42,11 +42,6 @@ double mono() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-int64_t unix_ns() {
-  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::system_clock::now().time_since_epoch())
-      .count();
-}
-
 void set_nonblock(int fd) { fcntl(fd, F_SETFL, fcntl(fd, F_GETFL, 0) | O_NONBLOCK); }
 
 std::string error_body(const std::string& msg) {
@@ -564,15 +559,8 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
       *fallback = true;  // never filtered here (e.g. restart between filter and bind): slow path
       return {};
     }
-    dev = l_->assume(uid, ns, name, node, pp.req, &dev_total);
-    if (dev >= 0) {
-      // ASSUME_TIME and the ordering sequence are taken in assume order, under the ledger mutex
-      std::lock_guard<std::mutex> o(order_mu_);
-      assume_ns = std::max(unix_ns(), last_assume_ns_ + 1);
-      last_assume_ns_ = assume_ns;
-      seq = ++order_seq_;
-      inflight_.push_back(InflightBind{node, pp.req, dev, seq});
-    }
+    // reservation, ASSUME_TIME and the ordering sequence in one step, shared with the Python slow path
+    dev = l_->assume_ordered(uid, ns, name, node, pp.req, &dev_total, &seq, &assume_ns);
   }
   if (dev < 0) {
     std::string msg;
@@ -620,30 +608,15 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
   // or each container is started with the other's GPU.  The reference got this from its node lock held
   // across the API calls (pkg/cache/nodeinfo.go:141-189); here only such a pair waits, everything else
   // (other nodes, other sizes, the same GPU) binds concurrently.
-  {
-    std::unique_lock<std::mutex> o(order_mu_);
-    auto blocked = [&] {
-      for (const auto& f : inflight_) {
-        if (f.seq < seq && f.node == node && f.size == pp.req && f.dev != dev) return true;
-      }
-      return false;
-    };
-    if (blocked()) {
-      stats_.bind_order_waits.fetch_add(1, std::memory_order_relaxed);
-      order_cv_.wait(o, [&] { return !blocked() || stop_.load(); });
-    }
+  if (l_->bind_blocked(seq)) {
+    stats_.bind_order_waits.fetch_add(1, std::memory_order_relaxed);
+    l_->bind_wait(seq, &stop_);
   }
   struct Done {  // leave the in-flight set however the bind ends
-    NativeServer* s;
+    Ledger* l;
     uint64_t seq;
-    ~Done() {
-      {
-        std::lock_guard<std::mutex> o(s->order_mu_);
-        s->inflight_.remove_if([this](const InflightBind& f) { return f.seq == seq; });
-      }
-      s->order_cv_.notify_all();
-    }
-  } done{this, seq};
+    ~Done() { l->bind_leave(seq); }
+  } done{l_, seq};
   std::string msg;
   bool ok = false;
   for (int attempt = 0; attempt < 3; ++attempt) {

@@ -133,18 +133,8 @@ class NativeServer {
   std::mutex fmu_;
   std::vector<BindFailure> failures_;
   ServerStats stats_;
-  // Binds in flight (see do_bind: equal-size pods bound to one node on different GPUs reach the
-  // apiserver in ASSUME_TIME order).  order_mu_ nests inside the ledger mutex, never around it.
-  struct InflightBind {
-    std::string node;
-    int64_t size, dev;
-    uint64_t seq;
-  };
-  std::mutex order_mu_;
-  std::condition_variable order_cv_;
-  std::list<InflightBind> inflight_;
-  uint64_t order_seq_ = 0;
-  int64_t last_assume_ns_ = 0;
+  // bind ordering lives in the ledger (Ledger::assume_ordered / bind_wait / bind_leave): one in-flight
+  // set for the native binds and the Python slow path alike
 };
 
 }  // namespace gsx

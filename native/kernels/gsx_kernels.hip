@@ -128,6 +128,9 @@ __global__ __launch_bounds__(256) void fill_kernel(uint4* p, uint64_t n16, uint3
 std::mutex g_mu;
 unsigned long long* g_counter[64] = {nullptr};
 unsigned long long* g_host_counter[64] = {nullptr};  // pinned, device-visible
+// One bad-stamp counter per device: its reset -> kernel launch -> readback sequence is held under the
+// device's mutex, so concurrent callers on one device (e.g. two Python threads) never mix their counts.
+std::mutex g_dev_mu[64];
 
 hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
@@ -269,6 +272,7 @@ int gsx_hbm_verify(void* stream, const void* base, uint64_t bytes, uint64_t stri
     if (!g_counter[dev]) GSX_CHECK(hipMalloc(reinterpret_cast<void**>(&g_counter[dev]), 64));
     ctr = g_counter[dev];
   }
+  std::lock_guard<std::mutex> dl(g_dev_mu[dev]);
   GSX_CHECK(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), S(stream)));
   hipLaunchKernelGGL(verify_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0, S(stream),
                      static_cast<const char*>(base), n, stride, tag, ctr);
@@ -308,6 +312,7 @@ int gsx_hbm_admit(void* stream, const gsx_slice* slices, int n, int stamp_idx, u
     }
     hc = g_host_counter[dev];
   }
+  std::lock_guard<std::mutex> dl(g_dev_mu[dev]);
   __atomic_store_n(hc, 0ull, __ATOMIC_SEQ_CST);
   uint64_t maxn = 0;
   for (int i = 0; i < n; ++i) maxn = std::max<uint64_t>(maxn, slices[i].bytes / stride);
@@ -365,6 +370,7 @@ int gsx_hbm_admit_n(void* stream, const gsx_slice* slices, int n, int n_stamp, i
     }
     hc = g_host_counter[dev];
   }
+  std::lock_guard<std::mutex> dl(g_dev_mu[dev]);
   __atomic_store_n(hc, 0ull, __ATOMIC_SEQ_CST);
   for (int base = 0; base < n; base += kMaxSlices) {
     SliceTable t;

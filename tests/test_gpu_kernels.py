@@ -168,7 +168,17 @@ def test_cuprobe_full_and_masked(hip):
     part = hip.physical_cus(hip.cuprobe(m, 8192, 20000))
     m.destroy()
     print("distinct CUs with a 64-CU mask:", len(part))
-    assert 0 < len(part) <= 64
+    # exactly the 64 CUs of the mask run work, and four disjoint masks cover four disjoint CU sets
+    assert len(part) == 64 and part <= full
+    quarters = []
+    for q in range(4):
+        ms = hip.Stream(0, hip.mask_words(range(64 * q, 64 * (q + 1))))
+        quarters.append(hip.physical_cus(hip.cuprobe(ms, 8192, 20000)))
+        ms.destroy()
+    assert [len(x) for x in quarters] == [64] * 4
+    assert all(not (quarters[i] & quarters[j]) for i in range(4) for j in range(i + 1, 4))
+    assert set().union(*quarters) == full and len(full) == 256
+    assert quarters[0] == part
 
 
 def test_hsa_cu_mask_env_limits_process():
@@ -181,7 +191,7 @@ def test_hsa_cu_mask_env_limits_process():
     assert r.returncode == 0, r.stderr
     n = int(r.stdout.strip().splitlines()[-1])
     print("distinct CUs under HSA_CU_MASK=0:0-31:", n)
-    assert n <= 32
+    assert n == 32  # the process sees exactly the 32 CUs ROCr's mask leaves it
 
 
 def test_arena_runtime_admits_four_64gib_pods():
@@ -261,3 +271,41 @@ def test_gemm_phased_is_deterministic(hip):
             assert torch.equal(c, c0)
         torch.testing.assert_close(c0.float(), a.float() @ b.float().t(), atol=0.05 * (k ** 0.5), rtol=1e-2)
     s.destroy()
+
+
+def test_hbm_verify_counts_are_per_call_under_concurrency(hip):
+    """two host threads verifying on one device must each get their own bad-stamp count (the
+    per-device counter's reset -> launch -> readback is serialised).  ctypes drops the GIL, so the calls
+    really overlap."""
+    import threading
+
+    st, mib = 1 << 16, 1 << 20
+    bufs = [hip.DeviceBuffer(0, 32 * mib) for _ in range(2)]
+    streams = [hip.Stream(0) for _ in range(2)]
+    for b, s in zip(bufs, streams):
+        hip.hbm_stamp(s, b.addr(0), 32 * mib, st, 77)
+        s.sync()
+    n = (32 * mib) // st
+    errs = []
+
+    def run(i):
+        want = 0 if i == 0 else n  # thread 1 verifies against the wrong tag: every stamp is bad
+        tag = 77 if i == 0 else 78
+        for _ in range(300):
+            got = hip.hbm_verify(streams[i], bufs[i].addr(0), 32 * mib, st, tag)
+            if got != want:
+                errs.append((i, got, want))
+                return
+            got = hip.hbm_admit(streams[i], [(bufs[i].addr(0), 32 * mib, tag)], -1, st)
+            if got != want:
+                errs.append((i, "admit", got, want))
+                return
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for b, s in zip(bufs, streams):
+        b.free()
+        s.destroy()
+    assert not errs, errs[:3]

@@ -283,3 +283,45 @@ def test_pprof_sees_native_threads():
         assert stacks and any("NativeServer" in ln for ln in stacks)
         assert "acquisitions=" in mtx and "native" in tc
     asyncio.run(go())
+
+
+def test_bind_order_spans_native_and_python_paths():
+    """one in-flight set for both bind paths.  a is bound natively (filtered here) with a slow
+    binding; b, equal-size for the other GPU, arrives on the Python slow path (never filtered by this
+    process, e.g. after a restart between filter and bind) and must still commit after a."""
+    async def go():
+        import aiohttp
+
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 2 * 16, 2))
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=True, http_threads=2).start()
+        try:
+            pa = await c.create("pods", make_pod("a", 10))
+            pb = await c.create("pods", make_pod("b", 10))
+            for _ in range(300):
+                if ext.server.engine.has_node("n") and ext.server.controller.get_pod("b", "default"):
+                    break
+                await asyncio.sleep(0.01)
+            async with aiohttp.ClientSession() as s:
+                async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(pa, ["n"])) as r:
+                    assert json.loads(await r.read())["NodeNames"] == ["n"]
+
+                async def bind(p):
+                    async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
+                            p["metadata"]["name"], "default", p["metadata"]["uid"], "n").encode()) as r:
+                        assert r.status == 200, await r.read()
+
+                api.server.faults.slow_bindings = {"a": 300.0}
+                before = ext.server.engine.server_stats()["proxied"]
+                ta = asyncio.create_task(bind(pa))
+                await asyncio.sleep(0.05)
+                await asyncio.gather(ta, bind(pb))
+                assert ext.server.engine.server_stats()["proxied"] == before + 1  # b took the Python path
+            assert api.server.binding_log == ["a", "b"]
+            got = {n: (await c.get("pods", n, "default"))["metadata"]["annotations"] for n in ("a", "b")}
+            assert [got[n]["SHARED_GPU_MEM_IDX"] for n in ("a", "b")] == ["0", "1"]
+            assert int(got["a"]["SHARED_GPU_MEM_ASSUME_TIME"]) < int(got["b"]["SHARED_GPU_MEM_ASSUME_TIME"])
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())
