@@ -29,7 +29,10 @@ Stability: every control-plane process is pinned to its own physical core
 (``--pin``, utils/cpuset.py) and the per-wave distribution is reported next to
 ``value`` (``wave_pods_per_s``: p50 and IQR).
 
-After the timed region rank 0 runs ``latency_sweep`` (extra keys, not part of
+After the timed region rank 0 runs, as extra keys outside ``value``:
+``device_plugin_path``: the same waves with kubelet + device plugin played by the shipped gRPC
+``GpuSharePlugin`` over its unix socket (the kubelet stand-in in deviceplugin/agent.py) instead of the
+compiled node agent; and ``latency_sweep`` (extra keys, not part of
 ``value``): the same waves with the fake kube-apiserver answering every
 non-watch request after 0 / 1 / 2 / 5 ms, for ``--bind-mode binding`` (one
 ``pods/binding`` POST per pod) and ``update`` (the reference's PUT + POST), and
@@ -166,50 +169,67 @@ def set_latency(api_batch, ms: float):
 SWEEP_LATENCIES_MS = (0, 1, 2, 5)
 
 
-def latency_sweep(a, children, api_url, api_batch, wave, fetch_timings, lt, n_pods, first_step, inspect_used):
+class WaveRunner:
+    """Untimed waves after the headline (same wave shape), with per-pod bind latency from the scheduler."""
+
+    def __init__(self, wave, fetch_timings, lt, n_pods, first_step):
+        self.wave, self.fetch_timings, self.lt, self.n_pods = wave, fetch_timings, lt, n_pods
+        self.step = first_step
+
+    def measure(self, warm: int, steps: int) -> dict:
+        for _ in range(warm):
+            self.wave(self.step)
+            self.step += 1
+        rs = []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            rs.append(self.wave(self.step))
+            self.step += 1
+        dt = time.perf_counter() - t0
+        lat, rtt = [], []
+        for r in rs:
+            for t in self.lt.run(self.fetch_timings(r["keys"]), 60):
+                lat.append(t["bound"] - t["seen"])
+                rtt.append(t["bind_rtt"])
+        return {"pods_per_s": round(self.n_pods * steps / dt, 1),
+                "wave_ms_p50": round(1e3 * pct([r["t_total"] for r in rs], 50), 3),
+                "wave_ms_p50_running": round(1e3 * pct([r["t_run"] for r in rs], 50), 3),
+                "p50_bind_latency_ms": round(1e3 * pct(lat, 50), 3), "p99_bind_latency_ms": round(1e3 * pct(lat, 99), 3),
+                "p50_bind_rtt_ms": round(1e3 * pct(rtt, 50), 3), "pods": self.n_pods * steps}
+
+
+def restart_child(children, name: str, start):
+    old = next(c for c in children if c.name == name)
+    old.stop()
+    new = start(old)
+    children[children.index(old)] = new
+    return new
+
+
+def wait_until(fn, timeout: float, what: str):
+    deadline = time.perf_counter() + timeout
+    while True:
+        try:
+            if fn():
+                return
+        except Exception:  # noqa: BLE001 - not up yet
+            pass
+        if time.perf_counter() > deadline:
+            raise TimeoutError(what)
+        time.sleep(0.01)
+
+
+def latency_sweep(a, children, api_url, api_batch, runner: WaveRunner, inspect_used):
     """Waves of the headline shape with the apiserver answering after L ms, for both bind modes, and behind
     client-go's default token bucket (QPS 5 / burst 10, the reference's client).  Rank 0 only; untimed by the
     driver's headline.  Returns (sweep rows, reference_client rows)."""
     from gpushare_scheduler_extender_amd.sim.cluster import start_extender
 
-    step = [first_step]
-
     def restart_extender(mode: str, qps: float = 0.0, burst: int = 1000):
-        old = next(c for c in children if c.name == "extender")
-        old.stop()
-        new = start_extender(api_url, profile=a.profile, bind_mode=mode, port=old.port, cpus=old.cpus,
-                             kube_qps=qps, kube_burst=burst)
-        children[children.index(old)] = new
-        deadline = time.perf_counter() + 60
-        while True:  # serving and synced: the node is in its ledger
-            try:
-                if inspect_used().get("nodes"):
-                    return
-            except Exception:  # noqa: BLE001 - connection refused while it starts
-                pass
-            if time.perf_counter() > deadline:
-                raise TimeoutError("restarted extender never saw the node")
-            time.sleep(0.01)
-
-    def measure(warm: int, steps: int) -> dict:
-        for _ in range(warm):
-            wave(step[0])
-            step[0] += 1
-        rs = []
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            rs.append(wave(step[0]))
-            step[0] += 1
-        dt = time.perf_counter() - t0
-        lat, rtt = [], []
-        for r in rs:
-            for t in lt.run(fetch_timings(r["keys"]), 60):
-                lat.append(t["bound"] - t["seen"])
-                rtt.append(t["bind_rtt"])
-        return {"pods_per_s": round(n_pods * steps / dt, 1),
-                "wave_ms_p50": round(1e3 * pct([r["t_total"] for r in rs], 50), 3),
-                "p50_bind_latency_ms": round(1e3 * pct(lat, 50), 3), "p99_bind_latency_ms": round(1e3 * pct(lat, 99), 3),
-                "p50_bind_rtt_ms": round(1e3 * pct(rtt, 50), 3), "pods": n_pods * steps}
+        restart_child(children, "extender", lambda old: start_extender(
+            api_url, profile=a.profile, bind_mode=mode, port=old.port, cpus=old.cpus, kube_qps=qps, kube_burst=burst))
+        # serving and synced: the node is in its ledger
+        wait_until(lambda: bool(inspect_used().get("nodes")), 60, "restarted extender never saw the node")
 
     rows, mode = [], a.bind_mode
     for m in ("binding", "update"):
@@ -218,18 +238,36 @@ def latency_sweep(a, children, api_url, api_batch, wave, fetch_timings, lt, n_po
             mode = m
         for ms in SWEEP_LATENCIES_MS:
             set_latency(api_batch, ms)
-            rows.append({"bind_mode": m, "api_latency_ms": ms, **measure(1, a.sweep_steps)})
+            rows.append({"bind_mode": m, "api_latency_ms": ms, **runner.measure(1, a.sweep_steps)})
     set_latency(api_batch, 0)
     # the reference's client: client-go defaults QPS 5 / burst 10 (cmd/main.go:76-82 never overrides them).
     # The warm-up waves drain the burst, so the timed waves see the sustained rate.
     ref = []
     for m, calls in (("update", 2), ("binding", 1)):
         restart_extender(m, qps=5.0, burst=10)
-        row = measure(3, 3)
+        row = runner.measure(3, 3)
         ref.append({"bind_mode": m, "kube_qps": 5, "kube_burst": 10, "apiserver_calls_per_bind": calls,
                     "derived_ceiling_pods_per_s": round(5.0 / calls, 2), **row})
     restart_extender(a.bind_mode)
     return rows, ref
+
+
+def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
+    """The same waves with kubelet + device plugin = the shipped gRPC GpuSharePlugin, driven over its unix socket
+    by the kubelet stand-in (serial admission, GetPreferredAllocation + Allocate per pod) instead of the
+    compiled node agent.  The plugin's own pod informer and allocation state decide every Allocate."""
+    from gpushare_scheduler_extender_amd.sim.cluster import start_node_agent
+
+    na = restart_child(children, "node-agent", lambda old: start_node_agent(
+        api_url, NODE, profile=a.profile, native=False, plugin="grpc", cpus=old.cpus))
+    client = E.BatchClient({"server": na.url})
+    wait_until(lambda: client.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 120, "plugin agent never ready")
+    row = runner.measure(2, a.sweep_steps)
+    st, body = client.run([("GET", "/v1/stats", b"")], 1)[0]
+    stats = json.loads(body) if st == 200 else {}
+    return {**row, "admit_p50_ms": stats.get("admit_p50_ms"), "allocate_calls": stats.get("allocate_calls"),
+            "allocate_errors": stats.get("allocate_errors"), "mismatch": stats.get("mismatch"),
+            "plugin_stats": stats.get("plugin_stats")}
 
 
 def parse():
@@ -257,6 +295,7 @@ def parse():
                          "shipped gRPC device plugin over its unix socket (plugin) / in-process (inproc)")
     ap.add_argument("--pin", default="auto", choices=["auto", "spread", "compact", "none"],
                     help="CPU placement of the control-plane processes (auto = spread when there are enough cores)")
+    ap.add_argument("--pin-widths", default="", help='JSON {"process": n_cpus} overriding the CPU slot widths')
     ap.add_argument("--api-latency-ms", type=float, default=0.0,
                     help="fake kube-apiserver answers every non-watch request after this delay (timed region)")
     ap.add_argument("--sweep", type=int, default=1, help="1: run the latency sweep after the timed region")
@@ -289,6 +328,8 @@ def main():
     # threads per process on the wave's critical path: rank 0 (driver + tracker + runtime endpoint), the
     # extender (2 loops + bind pool + reflectors), schedsim (cycle + binds), node agent (reflector + workers)
     widths = {"rank0": 2, "extender": 3, "scheduler": 2, "node-agent": 3}
+    if a.pin_widths:
+        widths = json.loads(a.pin_widths)
     mode = a.pin if a.pin != "auto" else "spread"
     cpu_plan = plan(names, widths, mode)
     pin_self(cpu_plan.get(f"rank{rank}"))
@@ -582,13 +623,18 @@ def main():
         apiserver_stats = json.loads(body) if st == 200 else {"error": st}
         apiserver_stats.pop("counts", None)
 
-    sweep = ref_client = None
+    sweep = ref_client = plugin_row = None
     if rank == 0 and a.sweep and not a.inproc:
+        runner = WaveRunner(wave, fetch_timings, lt, n_pods, a.warmup + a.steps)
         try:
-            sweep, ref_client = latency_sweep(a, children, api_url, api_batch, wave, fetch_timings, lt, n_pods,
-                                              a.warmup + a.steps, inspect_used)
+            sweep, ref_client = latency_sweep(a, children, api_url, api_batch, runner, inspect_used)
         except Exception as e:  # noqa: BLE001 - the sweep never costs the headline line
             sweep = {"error": f"{type(e).__name__}: {e}"}
+        if a.agent == "node" and a.node_agent == "native":
+            try:
+                plugin_row = plugin_path(a, children, api_url, runner, E)
+            except Exception as e:  # noqa: BLE001
+                plugin_row = {"error": f"{type(e).__name__}: {e}"}
     if world > 1:
         dist.barrier(group=ctl)  # every rank's runtime endpoint stays up until rank 0's sweep is done
 
@@ -646,6 +692,8 @@ def main():
             "api_latency_ms": a.api_latency_ms,
             "latency_sweep": sweep,
             "reference_client": ref_client,
+            # the shipped gRPC device plugin on the kubelet path (untimed by the headline, same waves)
+            "device_plugin_path": plugin_row,
             "bind_retries": sum(sum(s["attempts"]) - len(s["attempts"]) for s in step_stats),
             "agents": agent_stats,
             "node_agent": node_agent_stats,
