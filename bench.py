@@ -325,9 +325,10 @@ def main():
     from gpushare_scheduler_extender_amd.utils.cpuset import pin_self, plan
 
     names = ["rank0", "apiserver", "extender", "scheduler", "node-agent"] + [f"rank{r}" for r in range(1, world)]
-    # threads per process on the wave's critical path: rank 0 (driver + tracker + runtime endpoint), the
-    # extender (2 loops + bind pool + reflectors), schedsim (cycle + binds), node agent (reflector + workers)
-    widths = {"rank0": 2, "extender": 3, "scheduler": 2, "node-agent": 3}
+    # CPUs per process: the extender (2 loops + bind pool + reflectors), schedsim (cycle + bind threads) and the
+    # node agent (reflector + workers) get two; rank 0 stays on one core (a second one let its driver, tracker
+    # and runtime threads migrate: 7.5-9.4k vs 10.1k pods/s, interleaved A/B in profiles/r02_bench_stability.md)
+    widths = {"extender": 2, "scheduler": 2, "node-agent": 2}
     if a.pin_widths:
         widths = json.loads(a.pin_widths)
     mode = a.pin if a.pin != "auto" else "spread"
