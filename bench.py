@@ -365,7 +365,8 @@ def main():
             # the node's device plugin / kubelet stand-in: one process for all GPUs of the node, like a DaemonSet
             children.append(start_node_agent(api.url, NODE, profile=a.profile, native=a.node_agent == "native",
                                              plugin="inproc" if a.node_agent == "inproc" else "grpc",
-                                             workers=8, cpus=cpu_plan.get("node-agent")))
+                                             workers=min(16, max(8, 2 * a.pods_per_gpu * world)),
+                                             cpus=cpu_plan.get("node-agent")))
         api_url, ext_url = api.url, ext.url
 
     import torch

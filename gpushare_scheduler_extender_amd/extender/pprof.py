@@ -98,7 +98,22 @@ async def cmdline(request):
 
 
 async def symbol(request):
-    return _text("num_symbols: 1\n")
+    """Go's pprof symbol protocol: GET -> ``num_symbols``; POST ``0xADDR+0xADDR...`` -> ``0xADDR name`` lines
+    (native program counters of this process, symbolised from the loaded objects' symbol tables)."""
+    E = _engine_mod()
+    if request.method != "POST":
+        return _text(f"num_symbols: {1 if E is not None else 0}\n")
+    body = (await request.read()).decode(errors="replace")
+    out = []
+    for tok in body.replace("+", " ").split():
+        try:
+            pc = int(tok, 16)
+        except ValueError:
+            continue
+        name = E.native_symbol(pc) if E is not None else ""
+        if name:
+            out.append(f"{tok} {name}")
+    return _text("\n".join(out) + "\n")
 
 
 async def goroutine(request):
@@ -269,3 +284,4 @@ def add_pprof(app: web.Application, engine=None):
         r.add_get(f"/debug/pprof/{name}/", h)
         r.add_get(f"/debug/pprof/{name}", h)
     r.add_post("/debug/pprof/symbol/", symbol)
+    r.add_post("/debug/pprof/symbol", symbol)

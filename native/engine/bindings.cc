@@ -615,6 +615,9 @@ class PyPodRuntime {
 
 PYBIND11_MODULE(_engine, m) {
   m.def(
+      "native_symbol", [](uint64_t pc) { return introspect::symbol_at(static_cast<uintptr_t>(pc)); },
+      "Function name at a program counter of this process ('' when unknown).");
+  m.def(
       "native_stacks",
       [](std::vector<int> tids, double timeout) {
         std::vector<introspect::Sample> got;

@@ -189,6 +189,11 @@ bool install() {
   return true;
 }
 
+std::string symbol_at(uintptr_t pc) {
+  std::string s = symbolize(reinterpret_cast<void*>(pc + 1));  // symbolize() looks up pc - 1
+  return s.find("+0x") != std::string::npos && s.find('?') == 0 ? std::string() : s;
+}
+
 std::vector<int> thread_ids() {
   std::vector<int> out;
   DIR* d = ::opendir("/proc/self/task");

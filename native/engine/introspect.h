@@ -42,6 +42,9 @@ std::vector<Sample> capture(const std::vector<int>& tids, double timeout_s = 0.0
 // Thread ids of this process (/proc/self/task).
 std::vector<int> thread_ids();
 
+// Function name covering `pc` (ELF .symtab of the loaded objects, then dladdr); "" when unknown.
+std::string symbol_at(uintptr_t pc);
+
 struct MutexStats {
   uint64_t acquisitions = 0, contended = 0;
   double wait_s = 0, max_wait_s = 0, hold_s = 0, max_hold_s = 0;
