@@ -329,6 +329,9 @@ def main():
     # node agent (reflector + workers) get two; rank 0 stays on one core (a second one let its driver, tracker
     # and runtime threads migrate: 7.5-9.4k vs 10.1k pods/s, interleaved A/B in profiles/r02_bench_stability.md)
     widths = {"extender": 2, "scheduler": 2, "node-agent": 2}
+    # ranks > 0 idle in a gloo barrier during the timed waves while their runtime endpoint admits pods: on a
+    # single CPU the endpoint thread waited behind gloo's threads for up to 9 ms (N=4/8 rehearsal, 2 CPUs fix it)
+    widths.update({f"rank{r}": 2 for r in range(1, world)})
     if a.pin_widths:
         widths = json.loads(a.pin_widths)
     mode = a.pin if a.pin != "auto" else "spread"
