@@ -79,7 +79,8 @@ class NodeAgent:
         self.failed = 0
         self.bad_stamps = 0
         self.latency: list[float] = []  # bound-observed -> Running
-        self.stats = {"allocate_calls": 0, "allocate_errors": 0, "mismatch": 0, "allocate_ms_max": 0.0}
+        self.stats = {"allocate_calls": 0, "allocate_errors": 0, "mismatch": 0, "gone_during_allocate": 0,
+                      "allocate_ms_max": 0.0}
         self._bg: set[asyncio.Task] = set()
         self._releasing: set[asyncio.Task] = set()
         self.admit_q: asyncio.Queue = asyncio.Queue()
@@ -109,6 +110,10 @@ class NodeAgent:
             self.queued.add(uid)
             self.seen.setdefault(uid, time.perf_counter())
             self.admit_q.put_nowait(obj_key(pod))
+
+    def _alive(self, uid: str, key: str) -> bool:
+        pod = self.pods.get(key)
+        return (pod is not None and podutil.meta(pod).get("uid") == uid and not podutil.is_complete(pod))
 
     def _on_delete(self, pod: dict, raw):
         self._stop(podutil.meta(pod).get("uid", ""))
@@ -202,6 +207,14 @@ class NodeAgent:
                                                "message": f"Allocate failed: {e}"})
             return
         got = allocs[0]
+        if not self._alive(got.uid, got.key or key):
+            # the pod went away (deleted / completed) while its Allocate was in flight: kubelet's pod worker
+            # drops it; its device IDs and runtime slice are never taken (the plugin's informer frees its CUs)
+            self.stats["gone_during_allocate"] += 1
+            if got.uid != uid and self._alive(uid, key):
+                self.queued.add(uid)
+                self.admit_q.put_nowait(key)
+            return
         if got.uid != uid:
             # the plugin committed an earlier pod of this size: that pod starts with this allocation, ours
             # is served by the next Allocate
@@ -237,7 +250,8 @@ class NodeAgent:
                 log.exception("start %s: %r", key, e)
 
     async def _start(self, uid: str, key: str, allocs: list[_Alloc]):
-        if uid not in self.claimed:
+        if uid not in self.claimed or not self._alive(uid, key):
+            self._stop(uid)
             return  # deleted while waiting to start
         pod = self.pods.get(key)
         t0 = self.seen.pop(uid, time.perf_counter())
@@ -256,7 +270,9 @@ class NodeAgent:
                 await self._patch_status(pod, {"phase": "Failed", "reason": "UnexpectedAdmissionError",
                                                "message": str(e)})
             return
-        if uid not in self.claimed:  # deleted while starting: tear down what we just started
+        if uid not in self.claimed or not self._alive(uid, key):  # deleted while starting: tear it down
+            self.claimed.discard(uid)
+            self.used_ids.pop(uid, None)
             self._release(uid)
             return
         self.running[uid] = key

@@ -27,11 +27,14 @@ async def _retry(fn, *a, tries=50, **kw):
             await asyncio.sleep(0.002)
 
 
-@pytest.mark.parametrize("seed,impl", [(7, "native"), (11, "native"), (23, "native"), (7, "python")])
-def test_chaos_whole_stack_converges_without_overcommit(seed, impl):
+@pytest.mark.parametrize("seed,impl,agent", [(7, "native", "plugin"), (11, "native", "plugin"), (23, "native", "native"),
+                                             (7, "python", "plugin"), (11, "native", "native")])
+def test_chaos_whole_stack_converges_without_overcommit(seed, impl, agent):
+    """``impl``: compiled or asyncio scheduler stand-in; ``agent``: kubelet + the shipped gRPC device plugin
+    (the product path) or the compiled node agent."""
     async def go():
         rnd = random.Random(seed)
-        cl = Cluster(ALIYUN, [96] * 4, gpu=False, native=impl == "native")
+        cl = Cluster(ALIYUN, [96] * 4, gpu=False, native=impl == "native", agent=agent)
         try:
             await cl.start()
             api = HttpClient(cl.api.url)
