@@ -576,10 +576,37 @@ def main():
 
         prof = cProfile.Profile()
         lt.loop.call_soon_threadsafe(prof.enable)
+    def extender_counters():
+        # the native front end's bind counters (GET /debug/engine); diffed around the timed region
+        st, body = ext_batch.run([("GET", "/debug/engine", b"")], 1)[0]
+        srv = json.loads(body).get("server", {}) if st == 200 else {}
+        out = {k: srv.get(k, 0) for k in ("binds", "bind_ok", "bind_fail", "bind_order_waits", "bind_order_wait_s",
+                                           "api_calls", "conflicts_retried")}
+        for h in ("filter_latency", "bind_latency", "api_latency"):
+            out[h + "_n"] = (srv.get(h) or {}).get("n", 0)
+            out[h + "_s"] = (srv.get(h) or {}).get("sum", 0.0)
+        out["bind_order_wait_max_s"] = srv.get("bind_order_wait_max_s", 0.0)
+        return out
+
+    def bracket():
+        # both ends of the timed region: this rank's GPU work drained, one barrier over the gloo control group
+        # (ranks > 0 block in it -- no CPU or GPU-sync spinning -- while rank 0 drives the timed waves), then
+        # drained again.  A second, default-group barrier behind it cost 6-10 ms per run on its own (gloo,
+        # N=4/8 rehearsal), a third of the 20-wave region.
+        if use_gpu:
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier(group=ctl)
+        if use_gpu:
+            torch.cuda.synchronize()
+
+    ext0 = None
     t_start = None
     for step in range(a.warmup + a.steps):
         if step == a.warmup:
-            barrier()
+            if rank == 0:
+                ext0 = extender_counters()
+            bracket()
             t_start = time.perf_counter()
             cpu0 = _cpu_times(children)
             cg0 = _cgroup_cpu()
@@ -591,12 +618,10 @@ def main():
             dist.barrier(group=ctl)  # warmup waves in lockstep; timed waves are driven by rank 0 alone
         if rank == 0 and world > 1 and step < a.warmup:
             dist.barrier(group=ctl)
-    if world > 1:
-        # ranks > 0 wait for rank 0's timed waves in a blocking gloo barrier (no CPU / GPU-sync spinning),
-        # then everyone leaves through the barrier + synchronize bracket
-        dist.barrier(group=ctl)
-    barrier()
+    t_waves_end = time.perf_counter()
+    bracket()
     elapsed = time.perf_counter() - t_start
+    own_elapsed = elapsed
     cpu1 = _cpu_times(children)
     cg1 = _cgroup_cpu()
     if prof is not None:
@@ -622,6 +647,17 @@ def main():
         na = next(c for c in children if c.name == "node-agent")
         st, body = E.BatchClient({"server": na.url}).run([("GET", "/v1/stats", b"")], 1)[0]
         node_agent_stats = json.loads(body) if st == 200 else {"error": st}
+    extender_stats = None
+    if rank == 0:
+        ext1 = extender_counters()
+        d = {k: ext1[k] - ext0.get(k, 0) for k in ext1 if k != "bind_order_wait_max_s"}
+        extender_stats = {k: d[k] for k in ("binds", "bind_ok", "bind_fail", "bind_order_waits", "api_calls",
+                                            "conflicts_retried")}
+        extender_stats["bind_order_wait_ms"] = round(1e3 * d["bind_order_wait_s"], 3)
+        extender_stats["bind_order_wait_max_ms_run"] = round(1e3 * ext1["bind_order_wait_max_s"], 3)
+        for h in ("filter_latency", "bind_latency", "api_latency"):
+            n = d[h + "_n"]
+            extender_stats[h + "_mean_ms"] = round(1e3 * d[h + "_s"] / n, 4) if n else None
     apiserver_stats = None
     if rank == 0 and not a.inproc:
         st, body = api_batch.run([("GET", "/fake/stats", b"")], 1)[0]
@@ -693,6 +729,11 @@ def main():
             # per-wave throughput distribution: p50 and IQR next to `value` (one number from ~20 short waves is
             # sensitive to single slow waves)
             "wave_pods_per_s": wave_dist([n_pods / s["t_total"] for s in step_stats]),
+            # rank 0's view of the timed region: the waves back to back, then the closing barriers
+            "timed_region_ms": {"waves": round(1e3 * sum(s["t_total"] for s in step_stats), 3),
+                                "rank0_waves_span": round(1e3 * (t_waves_end - t_start), 3),
+                                "closing_bracket": round(1e3 * (t_start + own_elapsed - t_waves_end), 3),
+                                "max_over_ranks": round(1e3 * elapsed, 3)},
             "cpu_pinning": {k: v for k, v in cpu_plan.items()} or "none",
             "api_latency_ms": a.api_latency_ms,
             "latency_sweep": sweep,
@@ -702,6 +743,8 @@ def main():
             "bind_retries": sum(sum(s["attempts"]) - len(s["attempts"]) for s in step_stats),
             "agents": agent_stats,
             "node_agent": node_agent_stats,
+            # the extender's native front end over the timed waves (bind-order waits, apiserver round trips)
+            "extender": extender_stats,
             "apiserver": apiserver_stats,
             "cpu_s": {k: round(cpu1[k] - cpu0.get(k, 0.0), 3) for k in cpu1},
             # CPU-quota throttling of the container during the timed region (cgroup v2), if any

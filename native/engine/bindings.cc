@@ -416,6 +416,8 @@ class Engine {
     d["filters"] = s.filters.load();
     d["binds"] = s.binds.load();
     d["bind_order_waits"] = s.bind_order_waits.load();
+    d["bind_order_wait_s"] = l_.bind_order_wait_s();
+    d["bind_order_wait_max_s"] = l_.bind_order_wait_max_s();
     d["bind_ok"] = s.bind_ok.load();
     d["bind_fail"] = s.bind_fail.load();
     d["proxied"] = s.proxied.load();

@@ -276,23 +276,36 @@ bool Ledger::bind_blocked(uint64_t seq) {
 
 void Ledger::bind_wait(uint64_t seq, const std::atomic<bool>* stop) {
   std::unique_lock<std::mutex> o(order_mu_);
-  const InflightBind* me = nullptr;
-  for (const auto& f : inflight_) {
+  InflightBind* me = nullptr;
+  for (auto& f : inflight_) {
     if (f.seq == seq) me = &f;
   }
   if (!me || !blocked_locked(*me)) return;
   order_waits_.fetch_add(1, std::memory_order_relaxed);
+  auto t0 = std::chrono::steady_clock::now();
+  // a condition variable of our own: bind_leave() wakes exactly the binds it unblocks (a shared one woke
+  // every waiter of the node on every completed bind, and they queued for the extender's CPUs to re-check)
+  std::condition_variable cv;
+  me->waiter = &cv;
   while (blocked_locked(*me) && !(stop && stop->load())) {
-    order_cv_.wait_for(o, std::chrono::milliseconds(100));
+    cv.wait_for(o, std::chrono::milliseconds(100));  // timeout: notice `stop`
+  }
+  me->waiter = nullptr;  // still ours: only our own bind_leave() removes the entry
+  uint64_t ns = static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
+  order_wait_ns_.fetch_add(ns, std::memory_order_relaxed);
+  uint64_t cur = order_wait_max_ns_.load(std::memory_order_relaxed);
+  while (ns > cur && !order_wait_max_ns_.compare_exchange_weak(cur, ns, std::memory_order_relaxed)) {
   }
 }
 
 void Ledger::bind_leave(uint64_t seq) {
-  {
-    std::lock_guard<std::mutex> o(order_mu_);
-    inflight_.remove_if([seq](const InflightBind& f) { return f.seq == seq; });
+  std::lock_guard<std::mutex> o(order_mu_);
+  inflight_.remove_if([seq](const InflightBind& f) { return f.seq == seq; });
+  // notify under order_mu_: a waiter's cv lives on its stack until it has re-taken the mutex
+  for (const auto& f : inflight_) {
+    if (f.waiter && !blocked_locked(f)) f.waiter->notify_one();
   }
-  order_cv_.notify_all();
 }
 
 void Ledger::finish_bind(const std::string& uid, bool ok, double ttl_s) {

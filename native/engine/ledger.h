@@ -117,6 +117,9 @@ class Ledger {
   void bind_wait(uint64_t seq, const std::atomic<bool>* stop);
   void bind_leave(uint64_t seq);
   uint64_t bind_order_waits() const { return order_waits_.load(); }
+  // total / longest time binds spent held back by bind_wait (seconds)
+  double bind_order_wait_s() const { return static_cast<double>(order_wait_ns_.load()) * 1e-9; }
+  double bind_order_wait_max_s() const { return static_cast<double>(order_wait_max_ns_.load()) * 1e-9; }
   // Expire stale reservations.  A bound reservation the pod informer has not confirmed within its TTL is
   // dropped only if a pod LIST that *started after the bind succeeded* (`confirmed_list_start`, steady-clock
   // seconds; 0 = none) was applied without confirming it: then the apiserver really has no such binding.
@@ -172,14 +175,14 @@ class Ledger {
     std::string node;
     int64_t size, dev;
     uint64_t seq;
+    std::condition_variable* waiter = nullptr;  // set while its bind sits in bind_wait()
   };
   bool blocked_locked(const InflightBind& me) const;
   std::mutex order_mu_;
-  std::condition_variable order_cv_;
   std::list<InflightBind> inflight_;
   uint64_t order_seq_ = 0;
   int64_t last_assume_ns_ = 0;
-  std::atomic<uint64_t> order_waits_{0};
+  std::atomic<uint64_t> order_waits_{0}, order_wait_ns_{0}, order_wait_max_ns_{0};
 };
 
 // Full filter verb on a raw ExtenderArgs body; returns the
