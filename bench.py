@@ -284,6 +284,8 @@ def parse():
     ap.add_argument("--devices", default="auto", help="auto|hip|amdsmi|fake (fake: no GPU, CPU plumbing only)")
     ap.add_argument("--stamp-stride", type=int, default=1 << 20)
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--dump-timings", default="",
+                    help="write every timed pod's scheduler timeline (CLOCK_MONOTONIC, like the wave's t0) here")
     ap.add_argument("--agent", default="node", choices=["node", "rank"],
                     help="node: one node-agent process (the node's device plugin) driving a runtime shim per GPU rank (default); rank: one agent per GPU rank")
     ap.add_argument("--scheduler", default="native", choices=["native", "python"],
@@ -557,7 +559,7 @@ def main():
         t_end = time.perf_counter()
         # per-pod scheduler timings are collected after the timed region (fetch_timings)
         return {"keys": keys, "used": used, "total": total, "per_dev": per_dev,
-                "t_bound": t_bound - t0, "t_run": t_run - t0, "t_total": t_end - t0}
+                "t_bound": t_bound - t0, "t_run": t_run - t0, "t_total": t_end - t0, "t0": t0}
 
     async def fetch_timings(keys):
         if sim is not None:
@@ -682,8 +684,13 @@ def main():
     if rank == 0:
         for s in step_stats:
             tm = lt.run(fetch_timings(s["keys"]), 60)
+            s["timings"] = tm
             s.update({"bind_latency": [t["bound"] - t["seen"] for t in tm], "bind_rtt": [t["bind_rtt"] for t in tm],
                       "filter_rtt": [t["filter_rtt"] for t in tm], "attempts": [t["attempts"] for t in tm]})
+        if a.dump_timings:
+            with open(a.dump_timings, "w") as f:
+                json.dump([{"t0": s["t0"], "t_bound": s["t_bound"], "t_run": s["t_run"], "t_total": s["t_total"],
+                            "pods": s["timings"]} for s in step_stats], f)
         pods_total = n_pods * a.steps
         value = pods_total / elapsed
         lat = [x for s in step_stats for x in s["bind_latency"]]
