@@ -25,8 +25,8 @@ kubelet (there is none in this environment) — see SURVEY.md §4.  ``dtype`` is
 "n/a": the timed region does no floating-point work (the GPU work is the HIP
 stamp / verify of each pod's HBM slice).
 
-Stability: every control-plane process is pinned to its own physical core
-(``--pin``, utils/cpuset.py) and the per-wave distribution is reported next to
+Stability: every control-plane process is pinned to its own physical core, the idlest ones of the
+(shared) host as sampled at start (``--pin``, utils/cpuset.py), and the per-wave distribution is reported next to
 ``value`` (``wave_pods_per_s``: p50 and IQR).
 
 After the timed region rank 0 runs, as extra keys outside ``value``:
@@ -295,9 +295,13 @@ def parse():
     ap.add_argument("--node-agent", default="native", choices=["native", "plugin", "inproc"],
                     help="kubelet + device plugin: gsx-nodeagent (default), or the kubelet stand-in driving the "
                          "shipped gRPC device plugin over its unix socket (plugin) / in-process (inproc)")
-    ap.add_argument("--pin", default="auto", choices=["auto", "spread", "compact", "none"],
-                    help="CPU placement of the control-plane processes (auto = spread when there are enough cores)")
+    ap.add_argument("--pin", default="auto", choices=["auto", "spread", "static", "compact", "none"],
+                    help="CPU placement of the control-plane processes (auto = spread: the idlest physical cores, "
+                         "sampled at start; static: topology order without the load sample)")
     ap.add_argument("--pin-widths", default="", help='JSON {"process": n_cpus} overriding the CPU slot widths')
+    ap.add_argument("--pin-smt", type=int, default=1,
+                    help="1: a 2-CPU slot is one physical core with both SMT threads, so the N=1 plan fits one "
+                         "L3 domain (5 cores); 0: two physical cores")
     ap.add_argument("--api-latency-ms", type=float, default=0.0,
                     help="fake kube-apiserver answers every non-watch request after this delay (timed region)")
     ap.add_argument("--sweep", type=int, default=1, help="1: run the latency sweep after the timed region")
@@ -324,7 +328,7 @@ def main():
         a.gpus = world
 
     # ---- CPU placement (the same plan on every rank: each takes its own slot)
-    from gpushare_scheduler_extender_amd.utils.cpuset import pin_self, plan
+    from gpushare_scheduler_extender_amd.utils.cpuset import forget_shared_plan, pin_self, plan, shared_plan
 
     names = ["rank0", "apiserver", "extender", "scheduler", "node-agent"] + [f"rank{r}" for r in range(1, world)]
     # CPUs per process: the extender (2 loops + bind pool + reflectors), schedsim (cycle + bind threads) and the
@@ -337,7 +341,16 @@ def main():
     if a.pin_widths:
         widths = json.loads(a.pin_widths)
     mode = a.pin if a.pin != "auto" else "spread"
-    cpu_plan = plan(names, widths, mode)
+    if world > 1 and mode != "none":
+        # one plan for the whole job (the ranks' load samples would differ): keyed by the torchrun agent
+        key = f"{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}"
+        cpu_plan = shared_plan(names, widths, mode, key, smt=bool(a.pin_smt))
+        if rank == 0:
+            import atexit
+
+            atexit.register(forget_shared_plan, key)
+    else:
+        cpu_plan = plan(names, widths, mode, smt=bool(a.pin_smt))
     pin_self(cpu_plan.get(f"rank{rank}"))
 
     # ---- rank 0 starts its child processes BEFORE anything initialises the GPU

@@ -117,14 +117,16 @@ def start_apiserver(native: bool = True, history: int = 200000, threads: int | N
     """Fake kube-apiserver: the compiled ``gsx-fakeapi`` (native/fakeapi) or ``python -m ...k8s.fakeapi``.
 
     ``threads``: event loops of the native server (default ``GSX_FAKEAPI_THREADS`` or 1).
+    ``GSX_FAKEAPI_WATCH_FLUSH``: ``iteration`` (default) or ``request`` -- when watch events are pushed.
     """
     if native:
         exe = tool_path("gsx-fakeapi")
         if not exe.exists():
             raise FileNotFoundError(f"{exe} missing; run `python native/build.py fakeapi`")
         threads = threads or int(os.environ.get("GSX_FAKEAPI_THREADS", "1"))
-        return ChildProc([str(exe), "--port", "0", "--history", str(history), "--threads", str(threads)],
-                         "apiserver", cpus=cpus)
+        flush = os.environ.get("GSX_FAKEAPI_WATCH_FLUSH", "iteration")
+        return ChildProc([str(exe), "--port", "0", "--history", str(history), "--threads", str(threads),
+                          "--watch-flush", flush], "apiserver", cpus=cpus)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.k8s.fakeapi", "--port", "0"], "apiserver", cpus=cpus)
 
 

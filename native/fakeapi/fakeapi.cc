@@ -36,6 +36,7 @@
 // chain of dependent writes.  GET /fake/stats reports lock wait / hold times.
 //
 //   gsx-fakeapi [--host 127.0.0.1] [--port 0] [--port-file F] [--history N] [--threads N]
+//               [--watch-flush request|iteration]
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -415,7 +416,8 @@ class StateLock {
 
 class Server {
  public:
-  Server(size_t history, int threads) : history_max_(history), nloops_(std::max(1, std::min(64, threads))) {
+  Server(size_t history, int threads, bool flush_per_request)
+      : history_max_(history), nloops_(std::max(1, std::min(64, threads))), flush_per_request_(flush_per_request) {
     for (const char* k : {"pods", "nodes", "events", "leases"}) store_[k];
   }
 
@@ -571,6 +573,12 @@ class Server {
       c->rbuf.erase(0, static_cast<size_t>(got));
       handle(L, c, req, true);
       if (!L->conns.count(id)) return;
+      if (flush_per_request_) {
+        // push this write's watch events now, as kube-apiserver's per-watcher goroutines do, instead of at
+        // the end of the loop iteration (a burst of creates then reaches the watchers one by one)
+        flush_watchers(L);
+        if (!L->conns.count(id)) return;
+      }
     }
   }
 
@@ -1473,6 +1481,7 @@ class Server {
   int nloops_;
   std::vector<std::unique_ptr<Loop>> loops_;
   LockStats lstats_;
+  const bool flush_per_request_;  // --watch-flush request
   std::atomic<int> ngraces_{0};  // graces_.size(), readable without the mutex
   std::mutex smu_;  // the state below: store, revision, history, watchers, faults, counters, graces
   std::atomic<uint64_t> next_id_{0};
@@ -1495,6 +1504,7 @@ int main(int argc, char** argv) {
   int port = 0;
   size_t history = 200000;
   int threads = 1;
+  bool flush_per_request = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&]() -> std::string {
@@ -1509,8 +1519,16 @@ int main(int argc, char** argv) {
     else if (a == "--port-file") port_file = val();
     else if (a == "--history") history = static_cast<size_t>(std::max(1, std::atoi(val().c_str())));
     else if (a == "--threads") threads = std::atoi(val().c_str());
-    else if (a == "-h" || a == "--help") {
-      std::printf("usage: gsx-fakeapi [--host H] [--port P] [--port-file F] [--history N] [--threads N]\n");
+    else if (a == "--watch-flush") {
+      std::string m = val();
+      if (m != "request" && m != "iteration") {
+        std::fprintf(stderr, "--watch-flush: request | iteration\n");
+        return 2;
+      }
+      flush_per_request = m == "request";
+    } else if (a == "-h" || a == "--help") {
+      std::printf("usage: gsx-fakeapi [--host H] [--port P] [--port-file F] [--history N] [--threads N]\n"
+                  "                   [--watch-flush request|iteration]\n");
       return 0;
     } else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -1523,7 +1541,7 @@ int main(int argc, char** argv) {
   sa.sa_handler = on_sig;
   sigaction(SIGTERM, &sa, nullptr);
   sigaction(SIGINT, &sa, nullptr);
-  Server srv(history, threads);
+  Server srv(history, threads, flush_per_request);
   std::string err;
   int bound = srv.listen_on(host, port, &err);
   if (bound < 0) {
