@@ -64,3 +64,20 @@ def test_shared_plan_is_computed_once_per_key():
     finally:
         cpuset.forget_shared_plan(key)
     assert not os.path.exists(os.path.join(__import__("tempfile").gettempdir(), f"gsx-cpuplan-{key}.json"))
+
+
+def test_order_cores_prefers_a_domain_that_fits(monkeypatch):
+    # two L3 domains of 4 cores (CPU n and its SMT sibling n + 100); domain A has one busy core
+    dom = {c: (0,) if c < 4 else (4,) for c in range(8)}
+    monkeypatch.setattr(cpuset, "_group_key", lambda c: dom[c % 100])
+    cores = [(c, c + 100) for c in range(8)]
+    load = {c: 0.0 for core in cores for c in core}
+    load[102] = 0.5  # the sibling of CPU 2 belongs to another job
+    got = cpuset._order_cores(cores, load, need=4)
+    # domain B (4..7) holds all 4 needed cores idle: it comes first; CPU 0's core comes last
+    assert [c[0] for c in got[:4]] == [4, 5, 6, 7]
+    assert got[-1] == (0, 100)
+    assert got.index((2, 102)) > got.index((1, 101))  # busy core after the idle ones
+    # need 6: no domain fits, the one with the most idle cores comes first (B: 4 idle vs A: 2 without CPU 0)
+    got = cpuset._order_cores(cores, load, need=6)
+    assert [c[0] for c in got[:4]] == [4, 5, 6, 7]
