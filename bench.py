@@ -344,13 +344,13 @@ def main():
     if world > 1 and mode != "none":
         # one plan for the whole job (the ranks' load samples would differ): keyed by the torchrun agent
         key = f"{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}"
-        cpu_plan = shared_plan(names, widths, mode, key, smt=bool(a.pin_smt))
+        cpu_plan = shared_plan(names, widths, mode, key, smt=bool(a.pin_smt), local=5)
         if rank == 0:
             import atexit
 
             atexit.register(forget_shared_plan, key)
     else:
-        cpu_plan = plan(names, widths, mode, smt=bool(a.pin_smt))
+        cpu_plan = plan(names, widths, mode, smt=bool(a.pin_smt), local=5)
     pin_self(cpu_plan.get(f"rank{rank}"))
 
     # ---- rank 0 starts its child processes BEFORE anything initialises the GPU
@@ -622,7 +622,19 @@ def main():
             if rank == 0:
                 ext0 = extender_counters()
             bracket()
-            t_start = time.perf_counter()
+            if world > 1:
+                # rank 0 leaves the barrier up to ~1.5 ms after the others (its one core also runs the wave
+                # driver's threads), and the max over ranks would count that skew: the other ranks start their
+                # clock when rank 0's start signal arrives, so every rank's region begins at or after rank 0's
+                go = torch.zeros(1)
+                if rank == 0:
+                    t_start = time.perf_counter()
+                    dist.broadcast(go, src=0, group=ctl)
+                else:
+                    dist.broadcast(go, src=0, group=ctl)
+                    t_start = time.perf_counter()
+            else:
+                t_start = time.perf_counter()
             cpu0 = _cpu_times(children)
             cg0 = _cgroup_cpu()
         if rank == 0:

@@ -100,10 +100,11 @@ def _cores(allowed: list[int]) -> list[tuple[int, ...]]:
 def _order_cores(cores: list[tuple[int, ...]], load: dict[int, float] | None, need: int = 0) -> list[tuple[int, ...]]:
     """Best placement first.
 
-    Without ``load``: cores of the largest L3 domain first, in CPU order. With ``load``: idle cores (every
-    thread < ``IDLE`` busy) first, from the L3 domain that holds all ``need`` cores idle (the least busy such
-    domain) or else the domain with the most idle cores; busy cores last, least busy first. CPU 0's core goes
-    last either way (the kernel's housekeeping and many interrupts run there).
+    Without ``load``: cores of the largest L3 domain first, in CPU order. With ``load``: the ``need`` least
+    busy cores of the L3 domain whose ``need`` least busy cores are the least busy in total (domains with
+    fewer than ``need`` cores only when none has enough); then every other core, idle ones (every thread
+    < ``IDLE`` busy) before busy ones, least busy first. CPU 0's core goes last either way (the kernel's
+    housekeeping and many interrupts run there).
     """
     def busy(core):
         return max(load.get(c, 0.0) for c in core) if load else 0.0
@@ -114,17 +115,17 @@ def _order_cores(cores: list[tuple[int, ...]], load: dict[int, float] | None, ne
     if not load:
         ordered = [core for _, cs in sorted(groups.items(), key=lambda kv: -len(kv[1])) for core in cs]
     else:
-        idle = {k: [c for c in cs if busy(c) < IDLE and 0 not in c] for k, cs in groups.items()}
+        cand = {k: sorted((c for c in cs if 0 not in c), key=lambda c: (busy(c), c)) for k, cs in groups.items()}
 
-        def rank(k):
-            fits = len(idle[k]) >= need > 0
-            return (not fits, -len(idle[k]) if not fits else 0, sum(map(busy, groups[k])), k)
+        def score(k):
+            cs = cand[k]
+            if need and len(cs) >= need:
+                return (0, sum(busy(c) for c in cs[:need]), k)
+            return (1, -sum(1 for c in cs if busy(c) < IDLE), k)
 
-        ordered = []
-        for k in sorted(groups, key=rank):
-            ordered.extend(sorted(idle[k], key=lambda c: (busy(c), c)))
-        taken = set(ordered)
-        ordered.extend(sorted((c for c in cores if c not in taken), key=lambda c: (busy(c), c)))
+        first = cand[min(groups, key=score)][:need] if need and groups else []
+        taken = set(first)
+        ordered = first + sorted((c for c in cores if c not in taken), key=lambda c: (busy(c) >= IDLE, busy(c), c))
     return [c for c in ordered if 0 not in c] + [c for c in ordered if 0 in c]
 
 
@@ -136,7 +137,7 @@ def physical_cpus(allowed: list[int] | None = None, load: dict[int, float] | Non
 
 
 def plan(names: list[str], widths: dict[str, int] | None = None, mode: str = "spread",
-         load: dict[int, float] | None = None, smt: bool = False) -> dict[str, list[int]]:
+         load: dict[int, float] | None = None, smt: bool = False, local: int | None = None) -> dict[str, list[int]]:
     """CPU list per process name.
 
     ``spread``: each process gets ``widths[name]`` (default 1) CPUs of its own, idlest physical cores first
@@ -144,7 +145,9 @@ def plan(names: list[str], widths: dict[str, int] | None = None, mode: str = "sp
     ``compact``: all processes share the first ``max(widths)`` cores; ``none``: {} (no pinning).
     ``smt``: a slot of width w takes ceil(w / 2) physical cores with their SMT siblings, so one process's
     threads share a core's caches (width 1 leaves the sibling unused); otherwise every CPU of a slot is a
-    physical core of its own.  Falls back to {} when there are not enough CPUs.
+    physical core of its own.  ``local``: the first ``local`` names (default all) should share one L3 domain
+    (the chain of round trips); the rest go to the idlest cores anywhere.  Falls back to {} when there are not
+    enough CPUs.
     """
     if mode == "none":
         return {}
@@ -157,9 +160,10 @@ def plan(names: list[str], widths: dict[str, int] | None = None, mode: str = "sp
         w = max((widths.get(n, 1) for n in names), default=1)
         return {n: cpus[:w] for n in names}
     per = {n: max(0, widths.get(n, 1)) for n in names}  # width 0: that process is not pinned
+    near = names[:local] if local is not None else names
     if smt and all(len(c) >= 2 for c in cores):
         need = sum((w + 1) // 2 for w in per.values())
-        ordered = _order_cores(cores, load if mode == "spread" else None, need)
+        ordered = _order_cores(cores, load if mode == "spread" else None, sum((per[n] + 1) // 2 for n in near))
         if len(ordered) < need:
             return {}
         out, i = {}, 0
@@ -169,7 +173,7 @@ def plan(names: list[str], widths: dict[str, int] | None = None, mode: str = "sp
             i += k
         return out
     need = sum(per.values())
-    ordered = _order_cores(cores, load if mode == "spread" else None, need)
+    ordered = _order_cores(cores, load if mode == "spread" else None, sum(per[n] for n in near))
     cpus = [core[0] for core in ordered] + [c for core in ordered for c in core[1:]]
     if len(cpus) < need:
         return {}
@@ -181,7 +185,7 @@ def plan(names: list[str], widths: dict[str, int] | None = None, mode: str = "sp
 
 
 def shared_plan(names: list[str], widths: dict[str, int] | None, mode: str, key: str,
-                smt: bool = False) -> dict[str, list[int]]:
+                smt: bool = False, local: int | None = None) -> dict[str, list[int]]:
     """:func:`plan`, computed once per ``key`` and shared by every process that asks with that key.
 
     The ranks of one job sample the load at slightly different moments and could pick overlapping CPUs; the
@@ -198,7 +202,7 @@ def shared_plan(names: list[str], widths: dict[str, int] | None, mode: str, key:
                     return {k: list(v) for k, v in got["plan"].items()}
             except (OSError, ValueError):
                 pass
-            out = plan(names, widths, mode, smt=smt)
+            out = plan(names, widths, mode, smt=smt, local=local)
             tmp = path + f".{os.getpid()}"
             with open(tmp, "w") as f:
                 json.dump({"names": names, "widths": widths or {}, "mode": mode, "smt": smt, "plan": out}, f)

@@ -81,3 +81,14 @@ def test_order_cores_prefers_a_domain_that_fits(monkeypatch):
     # need 6: no domain fits, the one with the most idle cores comes first (B: 4 idle vs A: 2 without CPU 0)
     got = cpuset._order_cores(cores, load, need=6)
     assert [c[0] for c in got[:4]] == [4, 5, 6, 7]
+
+
+def test_order_cores_least_busy_domain_when_none_is_idle(monkeypatch):
+    monkeypatch.setattr(cpuset, "_group_key", lambda c: (8,) if c % 100 < 12 else (12,))
+    cores = [(c, c + 100) for c in range(8, 16)]
+    load = {c: 0.0 for core in cores for c in core}
+    for c in range(8, 12):
+        load[c] = 0.06  # domain A: every core a little busy
+    load[12] = 0.9  # domain B: one core taken by another job
+    assert [c[0] for c in cpuset._order_cores(cores, load, need=4)[:4]] == [8, 9, 10, 11]
+    assert [c[0] for c in cpuset._order_cores(cores, load, need=3)[:3]] == [13, 14, 15]
