@@ -30,10 +30,11 @@ import time
 from dataclasses import dataclass, field
 
 from ..models import pod as podutil
-from ..models.profile import POD_ASSIGN_TIME_ANNOTATION, POD_CU_MASK_ANNOTATION, NamingProfile
+from ..models.profile import (POD_ASSIGN_TIME_ANNOTATION, POD_CU_COUNT_ANNOTATION, POD_CU_MASK_ANNOTATION,
+                              NamingProfile)
 from .devices import Device
 
-CU_COUNT_ANNOTATION = "gpushare.amd.com/cu-count"  # pod asks for a CU partition of this size
+CU_COUNT_ANNOTATION = POD_CU_COUNT_ANNOTATION  # pod asks for a CU partition of this size
 
 
 @dataclass

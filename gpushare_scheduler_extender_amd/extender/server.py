@@ -48,7 +48,7 @@ from ..core.engine import new_engine
 from ..k8s.client import ApiError, KubeClient
 from ..models import pod as podutil
 from ..models import wire
-from ..models.profile import NamingProfile, SHARED_GPU
+from ..models.profile import POD_CU_COUNT_ANNOTATION, SHARED_GPU, NamingProfile
 from ..utils.metrics import Metrics
 from .pprof import add_pprof
 
@@ -165,7 +165,8 @@ class ExtenderServer:
             return str(e)
         req = podutil.gpu_mem_request(pod, self.profile)
         # reservation + ASSUME_TIME + entry in the bind-order set shared with the native front end
-        dev, dev_total, seq, assume_ns = self.engine.assume_ordered(uid, ns, name, node, req)
+        cu_count = ((pod.get("metadata") or {}).get("annotations") or {}).get(POD_CU_COUNT_ANNOTATION, "")
+        dev, dev_total, seq, assume_ns = self.engine.assume_ordered(uid, ns, name, node, req, str(cu_count))
         if dev < 0:
             self.metrics.bind_results.labels("no_device").inc()
             if dev == -2:

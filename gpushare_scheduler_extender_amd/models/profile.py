@@ -14,6 +14,7 @@ from dataclasses import asdict, dataclass, replace
 NODE_DEVICE_MEMORY_ANNOTATION = "gpushare.amd.com/device-memory"  # "268,268,..." per-device totals
 NODE_DEVICE_INFO_ANNOTATION = "gpushare.amd.com/devices"  # JSON device inventory from the plugin
 POD_CU_MASK_ANNOTATION = "gpushare.amd.com/cu-mask"  # per-pod CU partition (isolation)
+POD_CU_COUNT_ANNOTATION = "gpushare.amd.com/cu-count"  # the pod asks for a CU partition of this size
 POD_ASSIGN_TIME_ANNOTATION = "gpushare.amd.com/assign-time"
 NODE_RUNTIME_ENDPOINTS_ANNOTATION = "gpushare.amd.com/runtime-endpoints"  # JSON {gpu index: runtime shim URL}
 

@@ -214,11 +214,11 @@ class Engine {
 
   // (dev, dev_total, seq, assume_ns): reservation + ASSUME_TIME + entry in the shared bind-order set
   py::tuple assume_ordered(const std::string& uid, const std::string& ns, const std::string& name,
-                           const std::string& node, int64_t req) {
+                           const std::string& node, int64_t req, const std::string& cu_count) {
     int64_t dev_total = -1, assume_ns = 0;
     uint64_t seq = 0;
     std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
-    int64_t dev = l_.assume_ordered(uid, ns, name, node, req, &dev_total, &seq, &assume_ns);
+    int64_t dev = l_.assume_ordered(uid, ns, name, node, req, &dev_total, &seq, &assume_ns, cu_count);
     return py::make_tuple(dev, dev_total, seq, assume_ns);
   }
 
@@ -681,7 +681,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("assume", &Engine::assume)
       .def("finish_bind", &Engine::finish_bind, py::arg("uid"), py::arg("ok"), py::arg("ttl") = 30.0)
       .def("gc", &Engine::gc, py::arg("list_start") = 0.0)
-      .def("assume_ordered", &Engine::assume_ordered)
+      .def("assume_ordered", &Engine::assume_ordered, py::arg("uid"), py::arg("ns"), py::arg("name"),
+           py::arg("node"), py::arg("req"), py::arg("cu_count") = std::string())
       .def("bind_blocked", &Engine::bind_blocked)
       .def("bind_wait", &Engine::bind_wait)
       .def("bind_leave", &Engine::bind_leave)

@@ -246,7 +246,7 @@ int64_t Ledger::assume(const std::string& uid, const std::string& ns, const std:
 
 int64_t Ledger::assume_ordered(const std::string& uid, const std::string& ns, const std::string& name,
                                const std::string& node, int64_t req, int64_t* dev_total, uint64_t* seq,
-                               int64_t* assume_ns) {
+                               int64_t* assume_ns, const std::string& cu_count) {
   int64_t dev = assume(uid, ns, name, node, req, dev_total);
   if (dev < 0) return dev;
   int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -255,13 +255,15 @@ int64_t Ledger::assume_ordered(const std::string& uid, const std::string& ns, co
   last_assume_ns_ = std::max(now, last_assume_ns_ + 1);  // strictly increasing in assume order
   *assume_ns = last_assume_ns_;
   *seq = ++order_seq_;
-  inflight_.push_back(InflightBind{node, req, dev, *seq});
+  inflight_.push_back(InflightBind{node, req, dev, *seq, cu_count});
   return dev;
 }
 
 bool Ledger::blocked_locked(const InflightBind& me) const {
   for (const auto& f : inflight_) {
-    if (f.seq < me.seq && f.node == me.node && f.size == me.size && f.dev != me.dev) return true;
+    if (f.seq < me.seq && f.node == me.node && f.size == me.size && (f.dev != me.dev || f.cu_count != me.cu_count)) {
+      return true;
+    }
   }
   return false;
 }
@@ -520,6 +522,8 @@ std::string filter_body(Ledger& l, std::string_view body) {
       if (nm >= 0) pp.name = d.str(static_cast<uint32_t>(nm));
       pp.ns = ns >= 0 ? d.str(static_cast<uint32_t>(ns)) : std::string("default");
       pp.req = req;
+      int64_t cu = d.path(static_cast<uint32_t>(pod), {"metadata", "annotations", kCuCountAnnotation});
+      if (cu >= 0 && d.at(static_cast<uint32_t>(cu)).type == json::T::String) pp.cu_count = d.str(static_cast<uint32_t>(cu));
       l.remember_pending(d.str(static_cast<uint32_t>(u)), std::move(pp));
     }
   }

@@ -27,10 +27,15 @@
 #include <deque>
 #include <vector>
 
+#include <string_view>
+
 #include "introspect.h"
 #include "model.h"
 
 namespace gsx {
+
+// A pod's CU-partition request (deviceplugin/allocator.py CU_COUNT_ANNOTATION).
+constexpr std::string_view kCuCountAnnotation = "gpushare.amd.com/cu-count";
 
 enum class Check : int { Ok = 0, NodeNotFound = 1, NotGPUShare = 2, Insufficient = 3 };
 
@@ -110,9 +115,12 @@ class Ledger {
   // two equal-size pods headed for different GPUs of one node must reach the apiserver in ASSUME_TIME
   // order.  assume_ordered() (ledger mutex held) reserves the device, stamps ASSUME_TIME and enters the
   // in-flight set in one step; bind_wait() (ledger mutex NOT held) blocks only while an earlier
-  // equal-size bind for another GPU of that node is in flight; bind_leave() ends the entry.
+  // equal-size bind of that node is in flight whose pod is not interchangeable with this one: another GPU,
+  // or a different CU-partition request (`cu_count`, the gpushare.amd.com/cu-count annotation; the plugin
+  // would hand one pod's partition size to the other's container); bind_leave() ends the entry.
   int64_t assume_ordered(const std::string& uid, const std::string& ns, const std::string& name,
-                         const std::string& node, int64_t req, int64_t* dev_total, uint64_t* seq, int64_t* assume_ns);
+                         const std::string& node, int64_t req, int64_t* dev_total, uint64_t* seq, int64_t* assume_ns,
+                         const std::string& cu_count = std::string());
   bool bind_blocked(uint64_t seq);
   void bind_wait(uint64_t seq, const std::atomic<bool>* stop);
   void bind_leave(uint64_t seq);
@@ -151,6 +159,7 @@ class Ledger {
   struct PendingPod {
     std::string ns, name;
     int64_t req = 0;
+    std::string cu_count;  // gpushare.amd.com/cu-count annotation ("" none): part of the bind-order class
   };
   void remember_pending(const std::string& uid, PendingPod p);
   bool pending(const std::string& uid, PendingPod* out) const;
@@ -175,6 +184,7 @@ class Ledger {
     std::string node;
     int64_t size, dev;
     uint64_t seq;
+    std::string cu_count;
     std::condition_variable* waiter = nullptr;  // set while its bind sits in bind_wait()
   };
   bool blocked_locked(const InflightBind& me) const;

@@ -560,7 +560,7 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
       return {};
     }
     // reservation, ASSUME_TIME and the ordering sequence in one step, shared with the Python slow path
-    dev = l_->assume_ordered(uid, ns, name, node, pp.req, &dev_total, &seq, &assume_ns);
+    dev = l_->assume_ordered(uid, ns, name, node, pp.req, &dev_total, &seq, &assume_ns, pp.cu_count);
   }
   if (dev < 0) {
     std::string msg;

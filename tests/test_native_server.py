@@ -235,6 +235,49 @@ def test_equal_size_binds_for_different_gpus_land_in_assume_order(native):
     asyncio.run(go())
 
 
+@pytest.mark.parametrize("native", [True, False], ids=["native-bind", "python-bind"])
+def test_same_gpu_binds_with_different_cu_partitions_land_in_assume_order(native):
+    """Equal-size pods for the same GPU are interchangeable for the device plugin unless their CU-partition
+    requests differ (gpushare.amd.com/cu-count): then a swap would start one pod's container with the other's
+    partition size, so they are ordered too. Equal-size, same-class pods still bind concurrently."""
+    async def go():
+        import aiohttp
+
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 64, 1))
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=native, http_threads=2).start()
+        try:
+            cu = {"gpushare.amd.com/cu-count": "64"}
+            pods = {}
+            for name, ann in (("c", cu), ("d", None), ("e", cu), ("f", cu)):
+                pods[name] = await c.create("pods", make_pod(name, 8, annotations=ann))
+            for _ in range(300):
+                if ext.server.engine.has_node("n") and ext.server.controller.get_pod("f", "default"):
+                    break
+                await asyncio.sleep(0.01)
+            async with aiohttp.ClientSession() as s:
+                async def bind(name):
+                    p = pods[name]
+                    async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(p, ["n"])) as r:
+                        assert json.loads(await r.read())["NodeNames"] == ["n"]
+                    async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
+                            name, "default", p["metadata"]["uid"], "n").encode()) as r:
+                        assert r.status == 200, await r.read()
+
+                api.server.faults.slow_bindings = {"c": 300.0, "e": 300.0}
+                tc = asyncio.create_task(bind("c"))
+                await asyncio.sleep(0.05)
+                await asyncio.gather(tc, bind("d"))  # d has no partition request: waits for c
+                te = asyncio.create_task(bind("e"))
+                await asyncio.sleep(0.05)
+                await asyncio.gather(te, bind("f"))  # f asks for the same partition size: does not wait
+            assert api.server.binding_log == ["c", "d", "f", "e"]
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())
+
+
 def test_pprof_sees_native_threads():
     """/debug/pprof covers the C++ threads that serve filter / bind (names, native stacks, CPU
     time, verb latency histograms, ledger mutex profile), not only the Python loop."""
