@@ -621,6 +621,10 @@ def main():
         if step == a.warmup:
             if rank == 0:
                 ext0 = extender_counters()
+            # the CPU-time counters are read before the bracket: reading /proc for every child took ~0.5 ms, which
+            # sat inside the timed region (rank 0's span exceeded the sum of its waves by that much)
+            cpu0 = _cpu_times(children)
+            cg0 = _cgroup_cpu()
             bracket()
             if world > 1:
                 # rank 0 leaves the barrier up to ~1.5 ms after the others (its one core also runs the wave
@@ -635,8 +639,6 @@ def main():
                     t_start = time.perf_counter()
             else:
                 t_start = time.perf_counter()
-            cpu0 = _cpu_times(children)
-            cg0 = _cgroup_cpu()
         if rank == 0:
             r = wave(step)
             if step >= a.warmup:
