@@ -38,11 +38,20 @@ class _LedgerCollector:
         yield total
         yield util
         yield pods
-        for k in ("filter_calls", "assume_ok", "assume_fail", "bind_ok", "bind_fail", "expired",
+        for k in ("filter_calls", "assume_ok", "assume_fail", "bind_ok", "bind_fail", "expired", "expiry_deferred",
                   "overcommit_events", "pod_upserts", "pod_removes"):
             g = GaugeMetricFamily(f"gpushare_engine_{k}", f"native engine counter {k}")
             g.add_metric([], s[k])
             yield g
+        if "bind_order_waits" in s:
+            c = CounterMetricFamily("gpushare_bind_order_waits", "binds held back to keep a node's equal-size "
+                                    "bindings in ASSUME_TIME order")
+            c.add_metric([], s["bind_order_waits"])
+            yield c
+            c = CounterMetricFamily("gpushare_bind_order_wait_seconds", "time binds spent held back for ASSUME_TIME "
+                                    "order")
+            c.add_metric([], s["bind_order_wait_s"])
+            yield c
         # C++ front end (native/engine/server.cc): request counters + latency histograms
         ns = self.engine.server_stats() if hasattr(self.engine, "server_stats") else {}
         if ns:

@@ -301,6 +301,9 @@ class Engine {
     d["pod_upserts"] = s.pod_upserts;
     d["pod_removes"] = s.pod_removes;
     d["pods"] = pods;
+    // binds held back for ASSUME_TIME order, native and Python paths together
+    d["bind_order_waits"] = l_.bind_order_waits();
+    d["bind_order_wait_s"] = l_.bind_order_wait_s();
     return d;
   }
 

@@ -273,6 +273,10 @@ def test_same_gpu_binds_with_different_cu_partitions_land_in_assume_order(native
                 await asyncio.sleep(0.05)
                 await asyncio.gather(te, bind("f"))  # f asks for the same partition size: does not wait
             assert api.server.binding_log == ["c", "d", "f", "e"]
+            assert ext.server.engine.stats()["bind_order_waits"] == 1  # d, on either bind path
+            async with aiohttp.ClientSession() as s:
+                async with s.get(ext.url + "/metrics") as r:
+                    assert "gpushare_bind_order_waits_total 1.0" in await r.text()
         finally:
             await _teardown(api, c, ext)
     asyncio.run(go())
