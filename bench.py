@@ -299,6 +299,9 @@ def parse():
                     help="CPU placement of the control-plane processes (auto = spread: the idlest physical cores, "
                          "sampled at start; static: topology order without the load sample)")
     ap.add_argument("--pin-widths", default="", help='JSON {"process": n_cpus} overriding the CPU slot widths')
+    ap.add_argument("--gpu-warm-ms", type=float, default=300.0,
+                    help="run GEMMs on each rank's GPU for this long before the warmup waves (clock ramp; "
+                         "interleaved A/B after 20 s idle: 10.5-11.0k vs 8.9-10.8k pods/s, profiles/r02_pinload)")
     ap.add_argument("--pin-smt", type=int, default=1,
                     help="1: a 2-CPU slot is one physical core with both SMT threads, so the N=1 plan fits one "
                          "L3 domain (5 cores); 0: two physical cores")
@@ -521,6 +524,17 @@ def main():
     if rank == 0 and a.api_latency_ms and not a.inproc:
         set_latency(api_batch, a.api_latency_ms)
     tune()
+    if use_gpu and a.gpu_warm_ms > 0:
+        # bring this GPU out of its idle power state before the warmup waves: the admissions are ~10 us kernels,
+        # too short and too sparse to ramp the clocks themselves (a first bench on an idle box admitted at half
+        # speed: node agent p50 0.19 vs 0.10 ms)
+        x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+        t_warm = time.perf_counter() + a.gpu_warm_ms / 1e3
+        while time.perf_counter() < t_warm:
+            for _ in range(8):
+                x = (x @ x).clamp_(-1, 1)
+            torch.cuda.synchronize()
+        del x
     barrier()
 
     n_pods = a.pods_per_gpu * world
