@@ -14,7 +14,7 @@ from fractions import Fraction
 
 _BIN = {"Ki": 10, "Mi": 20, "Gi": 30, "Ti": 40, "Pi": 50, "Ei": 60}
 _DEC = {"n": -9, "u": -6, "m": -3, "": 0, "k": 3, "M": 6, "G": 9, "T": 12, "P": 15, "E": 18}
-_RE = re.compile(r"^([+-]?)(\d+\.?\d*|\.\d+)(.*)$")
+_RE = re.compile(r"^([+-]?)([0-9]+\.?[0-9]*|\.[0-9]+)(.*)$", re.S)  # ASCII digits only, like Go's parser
 _INT64_MAX = 2**63 - 1
 _INT64_MIN = -(2**63)
 
@@ -38,7 +38,7 @@ def parse_quantity(s) -> int:
         val *= 2 ** _BIN[suf]
     elif suf in _DEC:
         val *= Fraction(10) ** _DEC[suf]
-    elif suf[:1] in ("e", "E") and re.fullmatch(r"[+-]?\d+", suf[1:]):
+    elif suf[:1] in ("e", "E") and re.fullmatch(r"[+-]?[0-9]+", suf[1:]):
         val *= Fraction(10) ** int(suf[1:])
     else:
         raise ValueError(f"unknown quantity suffix in {s!r}")

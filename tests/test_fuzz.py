@@ -129,3 +129,28 @@ def test_native_front_end_survives_generated_requests():
             await c.close()
             await api.stop()
     asyncio.run(go())
+
+
+quantities = st.builds(
+    lambda sign, whole, frac, suf: sign + whole + frac + suf,
+    st.sampled_from(["", "+", "-"]),
+    st.from_regex(r"\A\d{0,22}\Z"),
+    st.sampled_from(["", "."]) | st.from_regex(r"\A\.\d{1,12}\Z"),
+    st.sampled_from(["", "Ki", "Mi", "Gi", "Ti", "Pi", "Ei", "n", "u", "m", "k", "M", "G", "T", "P", "E", "i", "K",
+                     "e", "E3", "e-3", "e+2", "e400", "e-400", "Gb", " "]) | st.from_regex(r"\A[eE][+-]?\d{1,3}\Z"))
+
+
+@settings(max_examples=1000, deadline=None)
+@given(quantities | st.text(max_size=10))
+def test_native_quantity_parser_agrees_with_python(s):
+    """native/engine/quantity.cc (filter, bind, informer) against the exact Fraction-based parser: same value
+    (ceil, saturated to int64) or both reject."""
+    from gpushare_scheduler_extender_amd.core.engine import parse_quantity as native_q
+    from gpushare_scheduler_extender_amd.models.quantity import parse_quantity as py_q
+
+    def run(f):
+        try:
+            return f(s)
+        except ValueError:
+            return "invalid"
+    assert run(native_q) == run(py_q), s
