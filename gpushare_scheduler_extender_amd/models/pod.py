@@ -70,12 +70,14 @@ def is_gpushare_pod(pod: dict, profile: NamingProfile) -> bool:
 
 
 def _atoi(v) -> int | None:
+    """Go's strconv.Atoi on a 64-bit platform: ASCII digits with an optional sign, within int64, else None."""
     if not isinstance(v, str) or not v:
         return None
     s = v[1:] if v[0] in "+-" else v
     if not s.isdigit() or not s.isascii():
         return None
-    return int(v)
+    n = int(v)
+    return n if -(2**63) <= n < 2**63 else None
 
 
 def gpu_id_from_annotation(pod: dict, profile: NamingProfile) -> int:

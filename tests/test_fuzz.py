@@ -154,3 +154,42 @@ def test_native_quantity_parser_agrees_with_python(s):
         except ValueError:
             return "invalid"
     assert run(native_q) == run(py_q), s
+
+
+atoi_like = st.one_of(st.from_regex(r"\A[+-]?\d{1,21}\Z"), st.sampled_from(["", "-", "+", "1.5", " 1", "1 ", "0x10",
+                                                                            "٣", "9223372036854775807",
+                                                                            "9223372036854775808", "-1"]),
+                      st.text(max_size=6))
+limit = st.one_of(st.integers(0, 2**40).map(str), st.sampled_from(["1Gi", "0.5", "1e3", "abc", "-4", "", "2k"]),
+                  st.integers(0, 2**40))
+
+
+@settings(max_examples=500, deadline=None)
+@given(st.lists(st.one_of(st.none(), limit), min_size=0, max_size=3), atoi_like, atoi_like, atoi_like,
+       st.sampled_from(["true", "false", "", "True"]), st.sampled_from(["Pending", "Running", "Succeeded", "Failed", ""]),
+       st.booleans(), st.sampled_from(["", "n1"]))
+def test_native_pod_view_agrees_with_python(limits, idx, mem, assume, assigned, phase, deleting, node):
+    """The native pod view (what the informer, filter and bind read) against models/pod.py, the reference's
+    pkg/utils/pod.go semantics, on generated annotations and limits."""
+    from gpushare_scheduler_extender_amd.models import pod as podutil
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU as P
+
+    ann = {P.annotation_idx: idx, P.annotation_pod: mem, P.annotation_assume_time: assume,
+           P.annotation_assigned: assigned}
+    pod = make_pod("p", [0] * max(1, len(limits)), annotations=ann, node=node, phase=phase,
+                   deletion_timestamp="2026-01-01T00:00:00Z" if deleting else None)
+    for c, lim in zip(pod["spec"]["containers"], limits):
+        lims = c.setdefault("resources", {}).setdefault("limits", {})
+        if lim is None:
+            lims.pop(P.resource, None)
+        else:
+            lims[P.resource] = lim
+    v = ENGINE.parse_pod(json.dumps(pod).encode())
+    assert v.request == podutil.gpu_mem_request(pod, P)
+    assert v.dev_idx == podutil.gpu_id_from_annotation(pod, P)
+    assert v.annot_mem == podutil.gpu_mem_from_annotation(pod, P)
+    assert v.assume_time == podutil.assume_time(pod, P)
+    assert bool(v.assigned == 1) == podutil.is_assigned(pod, P)
+    assert v.complete == podutil.is_complete(pod)
+    assert v.terminal == podutil.is_terminal(pod)
+    assert v.assigned_non_terminated == podutil.assigned_non_terminated(pod)
