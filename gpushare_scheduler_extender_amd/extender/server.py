@@ -30,7 +30,11 @@ annotations, same best-fit device, same error strings):
    one ``pods/binding`` POST whose annotations kube-apiserver copies onto the
    pod; ``bind_mode="update"`` reproduces the reference's two calls
    (annotate, then bind) with its retry-once-on-conflict
-   (``nodeinfo.go:150-189``), detecting conflicts by HTTP 409;
+   (``nodeinfo.go:150-189``), detecting conflicts by HTTP 409.  Both modes
+   run in the C++ front end (``server.cc: do_bind``; update mode writes the
+   annotations as a merge patch guarded by the resourceVersion the scheduler
+   saw); this Python path serves binds the front end did not filter, and
+   every bind when a client-side QPS limit is set;
 4. failure releases the reservation; success keeps it until the informer
    observes the annotated pod (then the annotations are the record).
 """
@@ -186,12 +190,16 @@ class ExtenderServer:
             # units to the earliest-ASSUME_TIME pod of that size: an equal-size pod for another GPU of the
             # same node must not overtake an earlier one, whichever path (native or this one) binds it
             # (the reference's node lock across the API calls, pkg/cache/nodeinfo.go:141-189)
+            if self.bind_mode == "update":
+                # the reference's first call; not ordered: a pod without spec.nodeName is no plugin candidate
+                await self._annotate(pod, ann)
             if self.engine.bind_blocked(seq):
                 await asyncio.get_running_loop().run_in_executor(None, self.engine.bind_wait, seq)
             if self.bind_mode == "binding":
                 await self._bind_with_annotations(pod, node, ann)
             else:
-                await self._update_then_bind(pod, node, ann)
+                md = pod["metadata"]
+                await self.client.bind_pod(md["namespace"], md["name"], node, md.get("uid"))
         except (ApiError, BindError, OSError, asyncio.TimeoutError) as e:
             self.engine.finish_bind(uid, False, 0.0)
             self.metrics.bind_results.labels("api_error").inc()
@@ -218,8 +226,9 @@ class ExtenderServer:
                     continue
                 raise
 
-    async def _update_then_bind(self, pod: dict, node: str, ann: dict):
-        """nodeinfo.go:145-189: annotate (retry once on conflict with a fresh GET), then bind."""
+    async def _annotate(self, pod: dict, ann: dict):
+        """nodeinfo.go:145-168: PUT the annotated pod; on a conflict retry once on a fresh GET.  The Binding
+        (nodeinfo.go:174-189) follows in :meth:`bind`, after the bind-order wait."""
         md = pod["metadata"]
         new = podutil.with_annotations(pod, ann)
         try:
@@ -229,7 +238,6 @@ class ExtenderServer:
                 raise
             fresh = await self.client.get("pods", md["name"], md["namespace"])
             await self.client.replace("pods", podutil.with_annotations(fresh, ann))
-        await self.client.bind_pod(md["namespace"], md["name"], node, md.get("uid"))
 
     def _event(self, pod: dict, reason: str, msg: str):
         if not self.emit_events:
@@ -353,9 +361,11 @@ class ExtenderRunner:
             await site.start()
             self.internal_port = site._server.sockets[0].getsockname()[1]  # noqa: SLF001
             api = api_dict(self.server.client.config)
-            native_bind = self.server.bind_mode == "binding" and self.server.client.limiter.qps <= 0
+            # a client-side QPS limit (--kube-qps) lives in the Python client: binds then take that path
+            native_bind = self.server.client.limiter.qps <= 0
             self.port = self.server.engine.serve(self.host, self.port, self.http_threads, self.pool_threads,
-                                                 self.internal_port, native_bind, self.server.reservation_ttl, api)
+                                                 self.internal_port, native_bind, self.server.reservation_ttl, api,
+                                                 update_mode=self.server.bind_mode == "update")
             self.server.native_server = True
             self._drain = asyncio.get_running_loop().create_task(self._drain_failures())
         else:

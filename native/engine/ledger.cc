@@ -524,6 +524,8 @@ std::string filter_body(Ledger& l, std::string_view body) {
       pp.req = req;
       int64_t cu = d.path(static_cast<uint32_t>(pod), {"metadata", "annotations", kCuCountAnnotation});
       if (cu >= 0 && d.at(static_cast<uint32_t>(cu)).type == json::T::String) pp.cu_count = d.str(static_cast<uint32_t>(cu));
+      int64_t rv = d.path(static_cast<uint32_t>(pod), {"metadata", "resourceVersion"});
+      if (rv >= 0 && d.at(static_cast<uint32_t>(rv)).type == json::T::String) pp.rv = d.str(static_cast<uint32_t>(rv));
       l.remember_pending(d.str(static_cast<uint32_t>(u)), std::move(pp));
     }
   }

@@ -160,6 +160,7 @@ class Ledger {
     std::string ns, name;
     int64_t req = 0;
     std::string cu_count;  // gpushare.amd.com/cu-count annotation ("" none): part of the bind-order class
+    std::string rv;        // metadata.resourceVersion the scheduler saw (update-mode precondition)
   };
   void remember_pending(const std::string& uid, PendingPod p);
   bool pending(const std::string& uid, PendingPod* out) const;

@@ -577,7 +577,73 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
     record_failure(BindFailure{ns, name, uid, node, msg});
     return bind_error_response(msg);
   }
-  // Binding object with the annotations kube-apiserver copies onto the pod
+  struct Done {  // leave the in-flight set however the bind ends
+    Ledger* l;
+    uint64_t seq;
+    ~Done() { l->bind_leave(seq); }
+  } done{l_, seq};
+  // the allocation record (pkg/utils/pod.go:192-206)
+  std::string ann;
+  ann.reserve(256);
+  auto kv = [&](const std::string& k, const std::string& v, bool last) {
+    json::append_quoted(&ann, k);
+    ann.push_back(':');
+    json::append_quoted(&ann, v);
+    if (!last) ann.push_back(',');
+  };
+  kv(prof.a_idx, std::to_string(dev), false);
+  kv(prof.a_dev, std::to_string(dev_total), false);
+  kv(prof.a_pod, std::to_string(pp.req), false);
+  kv(prof.a_assigned, "false", false);
+  kv(prof.a_assume, std::to_string(assume_ns), true);
+  const std::string pod_path = "/api/v1/namespaces/" + url_escape_path(ns) + "/pods/" + url_escape_path(name);
+  const std::string path = pod_path + "/binding";
+  std::string msg;
+  bool ok = false;
+  auto call = [&](const char* method, const std::string& target, const std::string& body, const char* ct,
+                  int* status, std::string* resp) {
+    std::string err;
+    double t0 = mono();
+    stats_.api_calls.fetch_add(1, std::memory_order_relaxed);
+    bool sent = api_->request(method, target, body, ct, status, resp, &err);
+    stats_.api_lat.observe(mono() - t0);
+    if (!sent) msg = err;
+    return sent;
+  };
+  auto fail = [&](const std::string& m) {
+    {
+      std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
+      l_->finish_bind(uid, false, cfg_.reservation_ttl);
+    }
+    stats_.bind_fail.fetch_add(1, std::memory_order_relaxed);
+    record_failure(BindFailure{ns, name, uid, node, m});
+    return bind_error_response(m);
+  };
+  if (cfg_.update_mode) {
+    // the reference's first call: write the annotations, guarded by the resourceVersion the scheduler saw;
+    // on the optimistic-lock conflict retry once on the latest version (nodeinfo.go:150-168).  Not ordered:
+    // a pod without spec.nodeName is no device-plugin candidate yet
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      std::string patch = "{\"metadata\":{";
+      if (attempt == 0 && !pp.rv.empty()) {
+        patch.append("\"resourceVersion\":");
+        json::append_quoted(&patch, pp.rv);
+        patch.push_back(',');
+      }
+      patch.append("\"annotations\":{").append(ann).append("}}}");
+      int status = 0;
+      std::string body;
+      if (!call("PATCH", pod_path, patch, "application/merge-patch+json", &status, &body)) return fail(msg);
+      if (status == 200 || status == 201) break;
+      msg = status_message(body, status);
+      if (attempt == 0 && status == 409 && msg.find("the object has been modified") != std::string::npos) {
+        stats_.conflicts_retried.fetch_add(1, std::memory_order_relaxed);
+        continue;
+      }
+      return fail(msg);
+    }
+  }
+  // Binding object; in "binding" mode it carries the annotations, which kube-apiserver copies onto the pod
   std::string b;
   b.reserve(512);
   b.append("{\"apiVersion\":\"v1\",\"kind\":\"Binding\",\"metadata\":{\"name\":");
@@ -586,22 +652,10 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
   json::append_quoted(&b, ns);
   b.append(",\"uid\":");
   json::append_quoted(&b, uid);
-  b.append(",\"annotations\":{");
-  auto kv = [&](const std::string& k, const std::string& v, bool last) {
-    json::append_quoted(&b, k);
-    b.push_back(':');
-    json::append_quoted(&b, v);
-    if (!last) b.push_back(',');
-  };
-  kv(prof.a_idx, std::to_string(dev), false);
-  kv(prof.a_dev, std::to_string(dev_total), false);
-  kv(prof.a_pod, std::to_string(pp.req), false);
-  kv(prof.a_assigned, "false", false);
-  kv(prof.a_assume, std::to_string(assume_ns), true);
-  b.append("}},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":");
+  if (!cfg_.update_mode) b.append(",\"annotations\":{").append(ann).push_back('}');
+  b.append("},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":");
   json::append_quoted(&b, node);
   b.append("}}");
-  const std::string path = "/api/v1/namespaces/" + url_escape_path(ns) + "/pods/" + url_escape_path(name) + "/binding";
   // kubelet admits a node's pods in the order their bindings land, and the device plugin gives a request
   // of N units to the earliest-ASSUME_TIME unassigned pod of that size (docs/designs/designs.md:93-103).
   // Two equal-size pods headed for different GPUs of one node must therefore land in ASSUME_TIME order,
@@ -612,24 +666,10 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
     stats_.bind_order_waits.fetch_add(1, std::memory_order_relaxed);
     l_->bind_wait(seq, &stop_);
   }
-  struct Done {  // leave the in-flight set however the bind ends
-    Ledger* l;
-    uint64_t seq;
-    ~Done() { l->bind_leave(seq); }
-  } done{l_, seq};
-  std::string msg;
-  bool ok = false;
   for (int attempt = 0; attempt < 3; ++attempt) {
     int status = 0;
-    std::string body, err;
-    double t0 = mono();
-    stats_.api_calls.fetch_add(1, std::memory_order_relaxed);
-    bool sent = api_->request("POST", path, b, "application/json", &status, &body, &err);
-    stats_.api_lat.observe(mono() - t0);
-    if (!sent) {
-      msg = err;
-      break;
-    }
+    std::string body;
+    if (!call("POST", path, b, "application/json", &status, &body)) break;
     if (status == 200 || status == 201) {
       ok = true;
       break;

@@ -48,6 +48,9 @@ struct ServerConfig {
   int pool_threads = 16;
   int fallback_port = 0;      // Python app on 127.0.0.1 (0: none)
   bool native_bind = true;
+  // bind_mode "update": the reference's two calls, annotate the pod (merge patch, resourceVersion precondition,
+  // one retry on the optimistic-lock conflict) then POST a plain Binding (pkg/cache/nodeinfo.go:145-189)
+  bool update_mode = false;
   double reservation_ttl = 60.0;
   ApiConfig api;
   size_t max_body = 64u << 20;

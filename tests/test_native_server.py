@@ -282,6 +282,54 @@ def test_same_gpu_binds_with_different_cu_partitions_land_in_assume_order(native
     asyncio.run(go())
 
 
+def test_native_update_mode_annotates_then_binds_with_one_conflict_retry():
+    """bind_mode="update" on the C++ front end: the reference's two calls (annotate, then a plain Binding,
+    pkg/cache/nodeinfo.go:145-189). The annotation write is guarded by the resourceVersion the scheduler saw.
+    On the optimistic-lock conflict it is retried once on the latest version."""
+    async def go():
+        import aiohttp
+
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 2 * 16, 2))
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), bind_mode="update"), native=True,
+                                   http_threads=2).start()
+        try:
+            pa = await c.create("pods", make_pod("a", 10))
+            pb = await c.create("pods", make_pod("b", 10))
+            for _ in range(300):
+                if ext.server.engine.has_node("n") and ext.server.controller.get_pod("b", "default"):
+                    break
+                await asyncio.sleep(0.01)
+            async with aiohttp.ClientSession() as s:
+                async def bind(p):
+                    async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(p, ["n"])) as r:
+                        assert json.loads(await r.read())["NodeNames"] == ["n"]
+                    async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
+                            p["metadata"]["name"], "default", p["metadata"]["uid"], "n").encode()) as r:
+                        assert r.status == 200, await r.read()
+
+                before = ext.server.engine.server_stats()
+                await bind(pa)
+                # b changes after the scheduler saw it: its annotation write meets a conflict, retried once
+                await c.patch("pods", "b", {"metadata": {"labels": {"touched": "1"}}}, "default")
+                await bind(pb)
+                after = ext.server.engine.server_stats()
+            assert after["proxied"] == before["proxied"]  # both bound natively
+            assert after["api_calls"] - before["api_calls"] == 5  # PATCH + POST, PATCH (409) + PATCH + POST
+            assert after["conflicts_retried"] - before["conflicts_retried"] == 1
+            for n, dev in (("a", "0"), ("b", "1")):
+                got = await c.get("pods", n, "default")
+                assert got["spec"]["nodeName"] == "n"
+                ann = got["metadata"]["annotations"]
+                assert ann["SHARED_GPU_MEM_IDX"] == dev and ann["SHARED_GPU_MEM_ASSIGNED"] == "false"
+                assert ann["SHARED_GPU_MEM_POD"] == "10" and ann["SHARED_GPU_MEM_DEV"] == "16"
+            assert (await c.get("pods", "b", "default"))["metadata"]["labels"]["touched"] == "1"
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())
+
+
 def test_pprof_sees_native_threads():
     """/debug/pprof covers the C++ threads that serve filter / bind (names, native stacks, CPU
     time, verb latency histograms, ledger mutex profile), not only the Python loop."""
