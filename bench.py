@@ -120,6 +120,10 @@ class NativeRuntime:
     def bad(self):
         return self.rt.stats()["bad"]
 
+    @property
+    def batches(self):
+        return self.rt.stats()["batches"]
+
     def verify(self) -> int:
         return self.rt.verify()
 
@@ -695,6 +699,8 @@ def main():
                 "admit_p50_ms": round((pct(agent.latency, 50) or 0) * 1e3, 3)}
     else:
         mine = {"admitted": shim.admitted, "failed": shim.failed, "bad_stamps": shim.bad + bad}
+        if isinstance(shim, NativeRuntime):
+            mine["gpu_admission_calls"] = shim.batches  # concurrent admissions share one stamp+verify+sync
     mine.update({"gpu": local_rank, "hbm_total": dev.total_bytes, "arena": arena})
     agent_stats = gather(mine)
     node_agent_stats = None

@@ -606,6 +606,7 @@ class PyPodRuntime {
   py::dict stats() const {
     py::dict d;
     d["admitted"] = r_->admitted();
+    d["batches"] = r_->batches();
     d["failed"] = r_->failed();
     d["bad"] = r_->bad();
     d["resident"] = r_->resident();

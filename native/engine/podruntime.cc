@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <set>
 #include <vector>
 
 #include "json.h"
@@ -106,9 +107,7 @@ int64_t PodRuntime::run_admit(bool stamp, const std::string& uid, bool verify, s
   return static_cast<int64_t>(bad);
 }
 
-int64_t PodRuntime::admit(const std::string& uid, uint64_t bytes, bool verify, std::string* err) {
-  std::lock_guard<std::mutex> g(mu_);
-  if (slices_.count(uid)) return run_admit(false, uid, verify, err) < 0 ? -1 : 0;  // idempotent
+bool PodRuntime::carve_locked(const std::string& uid, uint64_t bytes, std::string* err) {
   uint64_t size = (bytes + kAlign - 1) / kAlign * kAlign;
   // extents from the arena's holes in offset order (first fit; one extent unless fragmented)
   std::vector<std::pair<uint64_t, uint64_t>> used;
@@ -129,21 +128,99 @@ int64_t PodRuntime::admit(const std::string& uid, uint64_t bytes, bool verify, s
   }
   take(cfg_.arena_bytes);
   if (need) {
-    failed_++;
     *err = "arena exhausted: need " + std::to_string(size) + " B, " + std::to_string(size - need) + " free of " +
            std::to_string(cfg_.arena_bytes);
-    return -1;
+    return false;
   }
   slices_[uid] = std::move(s);
-  int64_t bad = run_admit(true, uid, verify, err);
-  if (bad < 0) {
-    slices_.erase(uid);
-    failed_++;
-    return -1;
+  return true;
+}
+
+void PodRuntime::admit_group_locked(const std::vector<Pending*>& group) {
+  std::vector<Pending*> fresh, again;
+  bool verify_all = false;
+  for (Pending* p : group) {
+    if (slices_.count(p->uid)) {
+      again.push_back(p);  // idempotent re-admission (or the same uid twice in one group)
+    } else if (!carve_locked(p->uid, p->bytes, &p->err)) {
+      failed_++;
+      p->result = -1;
+      continue;
+    } else {
+      fresh.push_back(p);
+    }
+    verify_all = verify_all || p->verify;
   }
-  admitted_++;
-  bad_ += static_cast<uint64_t>(bad);
-  return bad;
+  if (fresh.empty() && again.empty()) return;
+  // the group's new extents first (stamped), then -- if any admission asked for it -- every other resident
+  // slice, so one launch pair checks that no new stamp landed in another pod's slice
+  std::vector<GsxSlice> sl;
+  std::set<std::string> listed;
+  for (Pending* p : fresh) {
+    for (auto& e : slices_[p->uid].ext) sl.push_back(GsxSlice{cfg_.arena_addr + e.first, e.second, slices_[p->uid].tag});
+    listed.insert(p->uid);
+  }
+  const int n_stamp = static_cast<int>(sl.size());
+  for (auto& kv : slices_) {
+    if (listed.count(kv.first)) continue;
+    bool own = false;
+    for (Pending* p : again) own = own || p->uid == kv.first;
+    if (!verify_all && !own) continue;
+    for (auto& e : kv.second.ext) sl.push_back(GsxSlice{cfg_.arena_addr + e.first, e.second, kv.second.tag});
+  }
+  uint64_t bad = 0;
+  int rc = 0;
+  if (cfg_.arena_addr && !sl.empty()) {
+    rc = set_device_(cfg_.dev);
+    if (rc == 0) rc = admit_n_(cfg_.stream, sl.data(), static_cast<int>(sl.size()), n_stamp, 1, cfg_.stride, &bad);
+    batches_++;
+  }
+  if (rc != 0) {
+    std::string e = std::string("gsx_hbm_admit_n: ") + last_error_();
+    for (Pending* p : fresh) {
+      slices_.erase(p->uid);
+      failed_++;
+      p->result = -1;
+      p->err = e;
+    }
+    for (Pending* p : again) {
+      p->result = -1;
+      p->err = e;
+    }
+    return;
+  }
+  bad_ += bad;
+  for (Pending* p : fresh) {
+    admitted_++;
+    p->result = static_cast<int64_t>(bad);  // a bad stamp fails every admission of its group
+  }
+}
+
+int64_t PodRuntime::admit(const std::string& uid, uint64_t bytes, bool verify, std::string* err) {
+  Pending me{uid, bytes, verify};
+  std::unique_lock<std::mutex> q(qmu_);
+  queue_.push_back(&me);
+  while (!me.done) {
+    if (leading_) {
+      qcv_.wait(q);
+      continue;
+    }
+    // lead: admit everything queued so far as one group; admissions arriving meanwhile form the next one
+    leading_ = true;
+    std::vector<Pending*> group;
+    group.swap(queue_);
+    q.unlock();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      admit_group_locked(group);
+    }
+    q.lock();
+    for (Pending* p : group) p->done = true;
+    leading_ = false;
+    qcv_.notify_all();
+  }
+  if (me.result < 0) *err = me.err;
+  return me.result;
 }
 
 bool PodRuntime::release(const std::string& uid) {
@@ -197,9 +274,10 @@ CtlServer::Reply PodRuntime::handle(const http::Message& m) {
   if (m.method == "GET" && path == "/v1/stats") {
     std::lock_guard<std::mutex> g(mu_);
     char b[256];
-    std::snprintf(b, sizeof(b), "{\"admitted\":%llu,\"failed\":%llu,\"bad\":%llu,\"resident\":%zu,\"native\":true}",
+    std::snprintf(b, sizeof(b),
+                  "{\"admitted\":%llu,\"failed\":%llu,\"bad\":%llu,\"resident\":%zu,\"batches\":%llu,\"native\":true}",
                   (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
-                  slices_.size());
+                  slices_.size(), (unsigned long long)batches_);
     rep.body = b;
     return rep;
   }

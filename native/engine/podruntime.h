@@ -17,6 +17,7 @@
 #pragma once
 
 #include <cstdint>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -51,6 +52,7 @@ class PodRuntime {
   uint64_t admitted() const { return admitted_; }
   uint64_t failed() const { return failed_; }
   uint64_t bad() const { return bad_; }
+  uint64_t batches() const { return batches_; }  // GPU admission calls (one per group of concurrent admissions)
   uint64_t resident_bytes() const;
   size_t resident() const;
 
@@ -63,11 +65,27 @@ class PodRuntime {
   // Stamp `uid`'s extents (if `stamp`) and verify the resident slices (all of them, or only `uid`'s when
   // !verify); mu_ held.  Returns bad stamps, -1 with *err.
   int64_t run_admit(bool stamp, const std::string& uid, bool verify, std::string* err);
+  // Group commit: admissions that arrive while one is on the GPU are carved and admitted together, one
+  // stamp launch + one verify launch + one sync for the group.
+  struct Pending {
+    std::string uid;
+    uint64_t bytes;
+    bool verify;
+    bool done = false;
+    int64_t result = 0;
+    std::string err;
+  };
+  bool carve_locked(const std::string& uid, uint64_t bytes, std::string* err);  // mu_ held
+  void admit_group_locked(const std::vector<Pending*>& group);                   // mu_ held
 
   PodRuntimeConfig cfg_;
   mutable std::mutex mu_;
   std::map<std::string, Slice> slices_;  // uid -> slice
-  uint64_t admitted_ = 0, failed_ = 0, bad_ = 0;
+  uint64_t admitted_ = 0, failed_ = 0, bad_ = 0, batches_ = 0;
+  std::mutex qmu_;  // the admission queue; never held with mu_ across a GPU call
+  std::condition_variable qcv_;
+  std::vector<Pending*> queue_;
+  bool leading_ = false;  // a thread is admitting a group
   std::unique_ptr<CtlServer> srv_;
   void* lib_ = nullptr;
   int (*set_device_)(int) = nullptr;

@@ -80,3 +80,68 @@ def test_pod_runtime_hip_admission_detects_overlap():
         s.sync()
         s.destroy()
         buf.free()
+
+
+def _concurrent_admit(url, n, size):
+    import threading
+
+    go = threading.Barrier(n)
+    out = {}
+
+    def one(i):
+        go.wait()
+        out[i] = _req(url + f"/v1/pods/c{i}", "POST", {"dev": 0, "bytes": size, "verify": True})
+
+    ts = [threading.Thread(target=one, args=(i,)) for i in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    return out
+
+
+def test_pod_runtime_concurrent_admissions_group_commit():
+    """Admissions arriving together are carved and admitted as one group; every one gets its own slice."""
+    rt = native().PodRuntime(0, 64 * 4 * MiB)
+    url = f"http://127.0.0.1:{rt.serve('127.0.0.1', 0)}"
+    try:
+        out = _concurrent_admit(url, 16, 4 * MiB)
+        assert all(v == (200, b'{"bad":0}') for v in out.values()), out
+        st = json.loads(_req(url + "/v1/stats", "GET")[1])
+        assert st["admitted"] == 16 and st["resident"] == 16 and st["failed"] == 0
+        assert rt.stats()["resident_bytes"] == 16 * 4 * MiB
+        # the arena is full now: one more fails, the others are untouched
+        assert _req(url + "/v1/pods/x", "POST", {"dev": 0, "bytes": 200 * MiB})[0] == 409
+    finally:
+        rt.stop()
+
+
+@pytest.mark.gpu
+def test_pod_runtime_concurrent_admissions_on_gpu():
+    """16 concurrent admissions on the MI355X: grouped into fewer GPU calls, no bad stamp, all verified."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a GPU")
+    from gpushare_scheduler_extender_amd.ops import hip
+
+    arena = 1 << 30
+    buf = hip.DeviceBuffer(0, arena)
+    s = hip.Stream(0)
+    rt = native().PodRuntime(0, arena, buf.addr(0), s.ptr, 1 << 16, hip.lib()._name)
+    url = f"http://127.0.0.1:{rt.serve('127.0.0.1', 0)}"
+    try:
+        out = _concurrent_admit(url, 16, 32 * MiB)
+        assert all(st == 200 and json.loads(body)["bad"] == 0 for st, body in out.values()), out
+        st = json.loads(_req(url + "/v1/stats", "GET")[1])
+        assert st["admitted"] == 16 and st["resident"] == 16
+        assert 1 <= st["batches"] <= 16
+        assert rt.verify() == 0
+        # damage one slice: the next group reports it
+        hip.hbm_fill(s, buf.addr(0), 1 * MiB, 0)
+        s.sync()
+        assert rt.verify() == MiB // (1 << 16)
+    finally:
+        rt.stop()
+        s.sync()
+        s.destroy()
+        buf.free()
