@@ -291,15 +291,18 @@ class Agent {
       std::vector<double> lat = latency_;
       std::sort(lat.begin(), lat.end());
       double p50 = lat.empty() ? 0 : lat[lat.size() / 2];
-      char b[512];
+      const double n = admitted_ ? static_cast<double>(admitted_) : 1.0;
+      char b[768];
       std::snprintf(b, sizeof(b),
                     "{\"admitted\":%llu,\"failed\":%llu,\"bad_stamps\":%llu,\"conflicts\":%llu,\"running\":%zu,"
                     "\"admit_p50_ms\":%.3f,\"admit_max_ms\":%.3f,\"max_ms\":{\"queue\":%.3f,\"assign_patch\":%.3f,"
-                    "\"runtime\":%.3f,\"running_patch\":%.3f},\"status_retries\":%llu,\"api_connects\":%llu,"
+                    "\"runtime\":%.3f,\"running_patch\":%.3f},\"mean_ms\":{\"queue\":%.4f,\"assign_patch\":%.4f,"
+                    "\"runtime\":%.4f,\"running_patch\":%.4f},\"status_retries\":%llu,\"api_connects\":%llu,"
                     "\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
                     (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
-                    max_queue_ * 1e3, max_patch_ * 1e3, max_runtime_ * 1e3, max_status_ * 1e3,
+                    max_queue_ * 1e3, max_patch_ * 1e3, max_runtime_ * 1e3, max_status_ * 1e3, sum_queue_ / n * 1e3,
+                    sum_patch_ / n * 1e3, sum_runtime_ / n * 1e3, sum_status_ / n * 1e3,
                     (unsigned long long)status_retries_.load(), (unsigned long long)api_.reconnects());
       rep.body = b;
       return rep;
@@ -686,6 +689,10 @@ class Agent {
     max_runtime_ = std::max(max_runtime_, tp2 - tp1);
     max_status_ = std::max(max_status_, tp3 - tp2);
     max_queue_ = std::max(max_queue_, tp0 - t0);
+    sum_queue_ += tp0 - t0;
+    sum_patch_ += tp1 - tp0;
+    sum_runtime_ += tp2 - tp1;
+    sum_status_ += tp3 - tp2;
     latency_.push_back(now_s() - t0);
     if (latency_.size() > 100000) latency_.erase(latency_.begin(), latency_.begin() + 50000);
     seen_.erase(uid);
@@ -777,6 +784,7 @@ class Agent {
   int added_ = 0;  // work items queued since the last wake_locked()
   // worst case per admission step (seconds): queue wait, ASSIGNED patch, runtime admit, Running patch
   double max_queue_ = 0, max_patch_ = 0, max_runtime_ = 0, max_status_ = 0;
+  double sum_queue_ = 0, sum_patch_ = 0, sum_runtime_ = 0, sum_status_ = 0;  // over admitted_ pods
   std::vector<std::thread> workers_;
 };
 
