@@ -93,7 +93,7 @@ def _cpu_times(children) -> dict:
 class NativeRuntime:
     """One GPU's pod runtime endpoint served from C++ (``_engine.PodRuntime``) with the rank's HBM arena."""
 
-    def __init__(self, dev: int, arena_bytes: int, use_gpu: bool, stride: int):
+    def __init__(self, dev: int, arena_bytes: int, use_gpu: bool, stride: int, cpus: list[int] | None = None):
         from gpushare_scheduler_extender_amd.core.engine import native
 
         self.buf = self.stream = None
@@ -106,7 +106,7 @@ class NativeRuntime:
                                           hip.lib()._name)
         else:
             self.rt = native().PodRuntime(dev, arena_bytes)
-        self.url = f"http://127.0.0.1:{self.rt.serve('127.0.0.1', 0)}"
+        self.url = f"http://127.0.0.1:{self.rt.serve('127.0.0.1', 0, list(cpus or []))}"
 
     @property
     def admitted(self):
@@ -303,6 +303,9 @@ def parse():
                     help="CPU placement of the control-plane processes (auto = spread: the idlest physical cores, "
                          "sampled at start; static: topology order without the load sample)")
     ap.add_argument("--pin-widths", default="", help='JSON {"process": n_cpus} overriding the CPU slot widths')
+    ap.add_argument("--runtime-cpu", default="shared", choices=["split", "shared"],
+                    help="split: GPU 0's runtime endpoint threads get their own CPU (rank 0's SMT sibling); "
+                         "shared: they share rank 0's CPU with the wave driver")
     ap.add_argument("--gpu-warm-ms", type=float, default=300.0,
                     help="run GEMMs on each rank's GPU for this long before the warmup waves (clock ramp; "
                          "interleaved A/B after 20 s idle: 10.5-11.0k vs 8.9-10.8k pods/s, profiles/r02_pinload)")
@@ -342,6 +345,10 @@ def main():
     # node agent (reflector + workers) get two; rank 0 stays on one core (a second one let its driver, tracker
     # and runtime threads migrate: 7.5-9.4k vs 10.1k pods/s, interleaved A/B in profiles/r02_bench_stability.md)
     widths = {"extender": 2, "scheduler": 2, "node-agent": 2}
+    if a.runtime_cpu == "split":
+        # rank 0 = the wave driver + GPU 0's runtime endpoint (the CRI-runtime role): one core, the driver on
+        # one SMT thread and the endpoint's threads on the other, instead of both time-sharing one thread
+        widths["rank0"] = 2
     # ranks > 0 idle in a gloo barrier during the timed waves while their runtime endpoint admits pods: on a
     # single CPU the endpoint thread waited behind gloo's threads for up to 9 ms (N=4/8 rehearsal, 2 CPUs fix it)
     widths.update({f"rank{r}": 2 for r in range(1, world)})
@@ -358,7 +365,11 @@ def main():
             atexit.register(forget_shared_plan, key)
     else:
         cpu_plan = plan(names, widths, mode, smt=bool(a.pin_smt), local=5)
-    pin_self(cpu_plan.get(f"rank{rank}"))
+    mine_cpus = cpu_plan.get(f"rank{rank}")
+    runtime_cpus = None
+    if rank == 0 and a.runtime_cpu == "split" and mine_cpus and len(mine_cpus) >= 2:
+        mine_cpus, runtime_cpus = mine_cpus[:1], mine_cpus[1:]
+    pin_self(mine_cpus)
 
     # ---- rank 0 starts its child processes BEFORE anything initialises the GPU
     children = []
@@ -456,7 +467,7 @@ def main():
     # this GPU's runtime endpoint (CRI-runtime role): the node agent starts pods on it over HTTP
     if a.agent == "node":
         # native (native/engine/podruntime.cc): request threads carve the slice and run the HIP admission
-        runtime = shim = NativeRuntime(local_rank, arena, use_gpu, a.stamp_stride)
+        runtime = shim = NativeRuntime(local_rank, arena, use_gpu, a.stamp_stride, runtime_cpus)
         shim_url = shim.url
     else:
         runtime = (HbmArenaRuntime({local_rank: arena}, stamp_stride=a.stamp_stride) if use_gpu

@@ -572,9 +572,9 @@ class PyPodRuntime {
     std::string err;
     if (!r_->init(&err)) throw std::runtime_error(err);
   }
-  int serve(const std::string& host, int port) {
+  int serve(const std::string& host, int port, std::vector<int> cpus) {
     std::string err;
-    int p = r_->serve(host, port, &err);
+    int p = r_->serve(host, port, &err, std::move(cpus));
     if (p < 0) throw std::runtime_error(err);
     return p;
   }
@@ -732,7 +732,8 @@ PYBIND11_MODULE(_engine, m) {
       .def(py::init<int, uint64_t, uint64_t, uint64_t, uint64_t, const std::string&>(), py::arg("dev"),
            py::arg("arena_bytes"), py::arg("arena_addr") = 0, py::arg("stream") = 0, py::arg("stride") = 1 << 20,
            py::arg("kernels_lib") = std::string())
-      .def("serve", &PyPodRuntime::serve, py::arg("host") = "127.0.0.1", py::arg("port") = 0)
+      .def("serve", &PyPodRuntime::serve, py::arg("host") = "127.0.0.1", py::arg("port") = 0,
+           py::arg("cpus") = std::vector<int>())
       .def("stop", &PyPodRuntime::stop)
       .def("admit", &PyPodRuntime::admit, py::arg("uid"), py::arg("bytes"), py::arg("verify") = true)
       .def("release", &PyPodRuntime::release)

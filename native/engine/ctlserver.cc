@@ -2,6 +2,8 @@
 #include "introspect.h"
 
 #include <arpa/inet.h>
+#include <pthread.h>
+#include <sched.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
@@ -12,6 +14,16 @@
 #include <cstring>
 
 namespace gsx {
+
+void CtlServer::pin_thread() const {
+  if (cpus_.empty()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus_) {
+    if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+  }
+  pthread_setaffinity_np(pthread_self(), sizeof(set), &set);  // best effort: a CPU outside the cgroup is ignored
+}
 
 int CtlServer::start(const std::string& host, int port, std::string* err) {
   lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
@@ -39,6 +51,7 @@ int CtlServer::start(const std::string& host, int port, std::string* err) {
   getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &len);
   acc_ = std::thread([this] {
     introspect::name_thread("ctl-accept");
+    pin_thread();
     accept_loop();
   });
   return ntohs(a.sin_port);
@@ -76,6 +89,7 @@ void CtlServer::accept_loop() {
     conns_.push_back(fd);
     threads_.emplace_back([this, fd] {
       introspect::name_thread("ctl-conn");
+      pin_thread();
       serve_conn(fd);
     });
   }

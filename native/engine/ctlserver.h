@@ -29,13 +29,18 @@ class CtlServer {
   ~CtlServer() { stop(); }
   // Returns the bound port or -1 (*err).
   int start(const std::string& host, int port, std::string* err);
+  // CPUs the server's threads (acceptor, connections) run on; empty: inherit the creator's.  Before start().
+  void set_cpus(std::vector<int> cpus) { cpus_ = std::move(cpus); }
   void stop();
 
  private:
   void accept_loop();
   void serve_conn(int fd);
 
+  void pin_thread() const;
+
   Handler h_;
+  std::vector<int> cpus_;
   int lfd_ = -1;
   std::atomic<bool> stop_{false};
   std::thread acc_;

@@ -61,8 +61,9 @@ bool PodRuntime::init(std::string* err) {
   return true;
 }
 
-int PodRuntime::serve(const std::string& host, int port, std::string* err) {
+int PodRuntime::serve(const std::string& host, int port, std::string* err, std::vector<int> cpus) {
   srv_ = std::make_unique<CtlServer>([this](const http::Message& m) { return handle(m); });
+  srv_->set_cpus(std::move(cpus));
   return srv_->start(host, port, err);
 }
 

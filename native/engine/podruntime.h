@@ -43,7 +43,8 @@ class PodRuntime {
   explicit PodRuntime(PodRuntimeConfig cfg);
   ~PodRuntime();
   bool init(std::string* err);  // resolves the kernel entry points
-  int serve(const std::string& host, int port, std::string* err);
+  // `cpus`: where the endpoint's threads run (the CRI-runtime role gets a CPU of its own; empty: inherit)
+  int serve(const std::string& host, int port, std::string* err, std::vector<int> cpus = {});
   void stop();
   // Admission without HTTP (tests): returns bad stamps, -1 with *err on failure.
   int64_t admit(const std::string& uid, uint64_t bytes, bool verify, std::string* err);
