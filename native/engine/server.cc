@@ -636,7 +636,7 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
       if (!call("PATCH", pod_path, patch, "application/merge-patch+json", &status, &body)) return fail(msg);
       if (status == 200 || status == 201) break;
       msg = status_message(body, status);
-      if (attempt == 0 && status == 409 && msg.find("the object has been modified") != std::string::npos) {
+      if (attempt == 0 && status == 409) {  // a conflict is detected by status, not by message
         stats_.conflicts_retried.fetch_add(1, std::memory_order_relaxed);
         continue;
       }
