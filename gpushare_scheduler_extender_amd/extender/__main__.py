@@ -57,6 +57,9 @@ def parse_args(argv=None):
                     help="1: run as an HA replica; only the holder of the Lease binds (reference: single replica)")
     ap.add_argument("--lease-name", default=env.get("GSX_LEASE_NAME", "gpushare-schd-extender"))
     ap.add_argument("--lease-namespace", default=env.get("POD_NAMESPACE", "kube-system"))
+    ap.add_argument("--pprof", type=int, default=int(env.get("GSX_PPROF", "1")),
+                    help="1: serve /debug/pprof/* on the API port, as the reference (default); 0: off (the port is "
+                         "hostNetwork / NodePort, and profiles cost CPU)")
     ap.add_argument("--port-file", default="", help="write the bound port to this file once serving")
     return ap.parse_args(argv)
 
@@ -72,7 +75,8 @@ def main(argv=None) -> int:
         srv = ExtenderServer(client, get_profile(a.profile), workers=a.threadness, bind_mode=a.bind_mode,
                              reservation_ttl=a.reservation_ttl, resync_period=a.resync,
                              leader_elect=bool(a.leader_elect), lease_name=a.lease_name,
-                             lease_namespace=a.lease_namespace, native_controller=bool(a.native_controller))
+                             lease_namespace=a.lease_namespace, native_controller=bool(a.native_controller),
+                             pprof=bool(a.pprof))
         runner = await ExtenderRunner(srv, a.host, a.port, native=bool(a.native_http), http_threads=a.http_threads,
                                       pool_threads=a.bind_threads).start()
         if a.port_file:

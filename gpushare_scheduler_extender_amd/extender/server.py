@@ -71,7 +71,7 @@ class ExtenderServer:
                  bind_mode: str = "binding", reservation_ttl: float = 60.0, resync_period: float = 30.0,
                  emit_events: bool = True, leader_elect: bool = False, lease_name: str = "gpushare-schd-extender",
                  lease_namespace: str = "kube-system", lease_duration: float = 15.0, renew_deadline: float = 10.0,
-                 retry_period: float = 2.0, native_controller: bool = True):
+                 retry_period: float = 2.0, native_controller: bool = True, pprof: bool = True):
         if bind_mode not in ("binding", "update"):
             raise ValueError("bind_mode must be 'binding' or 'update'")
         self.client = client
@@ -86,6 +86,7 @@ class ExtenderServer:
         self.bind_mode = bind_mode
         self.reservation_ttl = reservation_ttl
         self.emit_events = emit_events
+        self.pprof = pprof
         self.app = self._make_app()
         self._gc_task: asyncio.Task | None = None
         self._bg: set[asyncio.Task] = set()
@@ -267,7 +268,8 @@ class ExtenderServer:
         r.add_get("/metrics", self.h_metrics)
         r.add_get("/healthz", self.h_healthz)
         r.add_get("/debug/engine", self.h_debug_engine)
-        add_pprof(app, self.engine)
+        if self.pprof:
+            add_pprof(app, self.engine)
         return app
 
     async def h_filter(self, request: web.Request):

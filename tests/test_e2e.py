@@ -135,6 +135,16 @@ def test_routes_version_and_status_codes():
     run(go())
 
 
+def test_pprof_can_be_turned_off():
+    async def go():
+        async with Cluster(pprof=False) as c:
+            st, _ = await c.get("/debug/pprof/")
+            assert st == 404
+            st, body = await c.get("/version")
+            assert (st, body) == (200, b"0.1.0")
+    run(go())
+
+
 def test_bind_uid_mismatch_error_string():
     async def go():
         async with Cluster() as c:
