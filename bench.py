@@ -278,7 +278,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     # a 1-GPU wave takes ~0.6 ms: 300 steps keep the timed region >= ~0.2 s (at 50 steps the same binaries
-    # read 5.0k-7.0k pods/s run to run on one box, scripts/gpu_ab.sh)
+    # read 5.0k-7.0k pods/s run to run on one box, scripts/experiments/gpu_ab.sh)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--pods-per-gpu", type=int, default=4)

@@ -7,7 +7,7 @@ Pinning each process to its own physical core keeps the chain on warm cores and 
 run-to-run spread small (``profiles/r02_bench_stability.md``).
 
 The GPU boxes are slices of a shared host: other jobs keep some CPUs busy, and their
-threads and the host's interrupts land on the low-numbered CPUs too (``scripts/cpu_probe.py``
+threads and the host's interrupts land on the low-numbered CPUs too (``scripts/experiments/cpu_probe.py``
 measured CPUs 0-7 at 0-31 % busy and ~300 interrupts/s each, with other CPUs pinned at
 100 %). A process pinned to such a CPU waits for the other job's time slice: one such
 wait cost a timed wave 14 ms. ``spread`` therefore samples per-CPU load first and

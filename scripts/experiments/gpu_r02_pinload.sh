@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r02pl}
 mkdir -p $OUT
-python scripts/cpu_probe.py 1 > $OUT/probe0.json
+python scripts/experiments/cpu_probe.py 1 > $OUT/probe0.json
 for rep in 1 2 3; do
   for m in static spread smt; do
     extra="--pin $m"; [ $m = smt ] && extra="--pin spread --pin-smt 1"
@@ -26,4 +26,4 @@ for m in spread smt; do
 import json; d=json.load(open('$OUT/n8_$m.json'))
 print('n8', '$m', d['value'], d['wave_pods_per_s']['p50'], d['wave_ms_max']['total'], d['cpu_pinning'])"
 done
-python scripts/cpu_probe.py 1 > $OUT/probe1.json
+python scripts/experiments/cpu_probe.py 1 > $OUT/probe1.json

@@ -2,7 +2,7 @@
 # One GPU-box session: GPU tests, smoke, the default 1-GPU bench, a rocprofv3 kernel-stats pass over the
 # bench (in-process control plane, no child processes under the profiler), then the N=1..8 rehearsal with
 # fake devices on the box's CPUs.  Every GPU step has its own time limit; the script stops at the first
-# failure.  Usage: scripts/gpu_session.sh [tag]
+# failure.  Usage: scripts/experiments/gpu_session.sh [tag]
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
