@@ -261,6 +261,9 @@ class GpuSharePlugin:
         return grpc.method_handlers_generic_handler(f"{api.PKG}.DevicePlugin", methods)
 
     async def serve(self):
+        if self._server is not None:  # re-serving after a kubelet restart: retire the old server first
+            await self._server.stop(0)
+            self._server = None
         os.makedirs(self.socket_dir, exist_ok=True)
         try:
             os.unlink(self.socket_path)

@@ -195,6 +195,7 @@ void PodRuntime::admit_group_locked(const std::vector<Pending*>& group) {
     admitted_++;
     p->result = static_cast<int64_t>(bad);  // a bad stamp fails every admission of its group
   }
+  for (Pending* p : again) p->result = static_cast<int64_t>(bad);  // its slice was re-verified in the launch
 }
 
 int64_t PodRuntime::admit(const std::string& uid, uint64_t bytes, bool verify, std::string* err) {

@@ -318,6 +318,48 @@ def test_plugin_register_listandwatch_allocate():
             await kubelet.stop()
             await client.close()
             await api_srv.stop()
+
+    run(go())
+
+
+def test_plugin_reregisters_after_kubelet_restart():
+    """kubelet re-creates its socket on restart: the plugin re-serves (old server retired) and registers again."""
+    async def go():
+        api_srv = await FakeApiServerRunner().start()
+        client = KubeClient(api_srv.url)
+        d = tempfile.mkdtemp(prefix="gsx-dp-")
+        kubelet = FakeKubelet(d)
+        await kubelet.start()
+        await client.create("nodes", make_node("n1", 32, 0))
+        plugin = GpuSharePlugin(client, "n1", fake_devices("2x16GiB"), P, socket_dir=d)
+        await plugin.start(publish=False)
+        kubelet2 = None
+        try:
+            await asyncio.wait_for(kubelet.registered.wait(), 5)
+            first_server = plugin._server
+            await kubelet.stop()
+            kubelet2 = FakeKubelet(d)
+            await kubelet2.start()  # new socket inode: the plugin's watcher notices within ~1 s
+            await asyncio.wait_for(kubelet2.registered.wait(), 10)
+            for _ in range(100):  # the kubelet side sees Register before the plugin's call returns
+                if plugin.stats["registrations"] == 2:
+                    break
+                await asyncio.sleep(0.01)
+            assert plugin.stats["registrations"] == 2
+            assert plugin._server is not first_server
+            pc = PluginClient(plugin.socket_path)
+            opts = await pc.options()
+            assert opts.get_preferred_allocation_available
+            first = await pc.list_and_watch().read()
+            assert len(first.devices) == 32
+            await pc.close()
+        finally:
+            await plugin.stop()
+            if kubelet2 is not None:
+                await kubelet2.stop()
+            await client.close()
+            await api_srv.stop()
+
     run(go())
 
 

@@ -68,6 +68,9 @@ def test_pod_runtime_hip_admission_detects_overlap():
         hip.hbm_fill(s, buf.addr(256 * MiB), 4 * MiB, 0)
         s.sync()
         assert rt.verify() == 4 * MiB // (1 << 16)
+        # an idempotent re-admission of p1 (kubelet retrying) re-verifies its own slice and reports the damage
+        st, body = _req(url + "/v1/pods/p1", "POST", {"dev": 0, "bytes": 256 * MiB, "verify": False})
+        assert st == 200 and json.loads(body)["bad"] == 64
         # a new admission verifies every resident slice and reports the damage
         st, body = _req(url + "/v1/pods/p3", "POST", {"dev": 0, "bytes": 128 * MiB, "verify": True})
         assert st == 200 and json.loads(body)["bad"] == 64
