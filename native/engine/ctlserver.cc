@@ -99,10 +99,11 @@ void CtlServer::serve_conn(int fd) {
   std::string buf;
   char tmp[16384];
   bool open = true;
+  http::RequestParser parser;
   while (open && !stop_.load()) {
     http::Message req;
     std::string perr;
-    long got = http::parse(buf.data(), buf.size(), true, &req, &perr);
+    long got = parser.parse(buf.data(), buf.size(), &req, &perr, 64u << 20);
     if (got < 0) break;
     if (got == 0) {
       long r = ::recv(fd, tmp, sizeof(tmp), 0);

@@ -9,6 +9,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cassert>
 #include <cstdio>
@@ -142,6 +143,86 @@ static void test_http() {
   http::Url u;
   CHECK(http::parse_url("https://[::1]:6443/pre/", &u) && u.tls && u.host == "::1" && u.port == 6443 &&
         u.prefix == "/pre");
+}
+
+// The connection parser must agree with the one-shot parser however the bytes are split across reads.
+static void test_request_parser() {
+  const std::string reqs[] = {
+      "POST /a?x=1 HTTP/1.1\r\nHost: h\r\nContent-Length: 3\r\n\r\nabc",
+      "GET /b HTTP/1.1\r\nConnection: close\r\n\r\n",
+      "POST /f HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n5;ext=1\r\nhello\r\nA\r\n0123456789\r\n0\r\nX-T: 1\r\n\r\n",
+      "POST /g HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n1\r\na\r\n1\r\nb\r\n1\r\nc\r\n0\r\n\r\n",
+  };
+  std::string stream;
+  for (const auto& r : reqs) stream += r;
+  for (size_t step : {size_t(1), size_t(2), size_t(3), size_t(7), size_t(64), stream.size()}) {
+    http::RequestParser rp;
+    std::string in;
+    std::vector<http::Message> got;
+    for (size_t off = 0; off < stream.size(); off += step) {
+      in.append(stream, off, step);
+      while (!in.empty()) {
+        http::Message m;
+        std::string err;
+        long used = rp.parse(in.data(), in.size(), &m, &err, 1 << 20);
+        CHECK(used >= 0);
+        if (used <= 0) break;
+        in.erase(0, static_cast<size_t>(used));
+        got.push_back(std::move(m));
+      }
+    }
+    CHECK(in.empty() && got.size() == 4);
+    if (got.size() != 4) continue;
+    for (size_t i = 0; i < 4; ++i) {
+      http::Message ref;
+      std::string err;
+      CHECK(http::parse(reqs[i].data(), reqs[i].size(), true, &ref, &err, false, 1 << 20) ==
+            static_cast<long>(reqs[i].size()));
+      CHECK(got[i].method == ref.method && got[i].target == ref.target && got[i].body == ref.body &&
+            got[i].keep_alive == ref.keep_alive && got[i].headers == ref.headers);
+    }
+  }
+  // the same hostile framing is refused, also when it arrives one byte at a time
+  const char* hostile[] = {"5\r\nhello\r\nfffffffffffffffb\r\n", "5\r\nhello\r\n-1\r\n", "0x5\r\nhello\r\n0\r\n\r\n",
+                           "5\r\nhello\r\n100000\r\n"};
+  for (const char* b : hostile) {
+    std::string req = std::string("POST /f HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n") + b;
+    http::RequestParser rp;
+    long r = 0;
+    http::Message m;
+    std::string err;
+    for (size_t k = 1; k <= req.size() && r == 0; ++k) r = rp.parse(req.data(), k, &m, &err, 1 << 20);
+    CHECK(r == -1);
+  }
+  // a head or a chunk-size line that never ends is cut off at 64 KiB instead of being re-scanned forever
+  {
+    http::RequestParser rp;
+    http::Message m;
+    std::string err;
+    std::string head = "GET / HTTP/1.1\r\nX: " + std::string(70000, 'a');
+    CHECK(rp.parse(head.data(), 1000, &m, &err, 1 << 20) == 0);
+    CHECK(rp.parse(head.data(), head.size(), &m, &err, 1 << 20) == -1 && err == "header too large");
+    std::string sl = "POST /f HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n" + std::string(70000, '0');
+    http::RequestParser rp2;
+    CHECK(rp2.parse(sl.data(), sl.size(), &m, &err, 1 << 20) == -1);
+  }
+  // 100k one-byte chunks trickled in 16-byte reads: linear work (this loop would be ~10^10 byte scans if every
+  // read re-parsed the buffer from the start)
+  {
+    std::string big = "POST /t HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n";
+    for (int i = 0; i < 100000; ++i) big += "1\r\nz\r\n";
+    big += "0\r\n\r\n";
+    http::RequestParser rp;
+    http::Message m;
+    std::string err;
+    long r = 0;
+    for (size_t k = 16;; k += 16) {
+      k = std::min(k, big.size());
+      r = rp.parse(big.data(), k, &m, &err, 1 << 20);
+      if (r != 0 || k == big.size()) break;
+    }
+    CHECK(r == static_cast<long>(big.size()) && m.body == std::string(100000, 'z'));
+  }
 }
 
 // ---------------------------------------------------------------- stress
@@ -285,6 +366,7 @@ int main() {
   test_quantity();
   test_ledger();
   test_http();
+  test_request_parser();
   test_server_stress();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);

@@ -227,6 +227,114 @@ long parse(const char* buf, size_t n, bool is_request, Message* out, std::string
   return static_cast<long>(n);
 }
 
+void RequestParser::reset() {
+  scanned_ = 0;
+  head_len_ = 0;
+  head_ = Message();
+  content_length_ = -1;
+  chunked_ = false;
+  cpos_ = 0;
+  body_.clear();
+}
+
+long RequestParser::parse(const char* buf, size_t n, Message* out, std::string* err, size_t max_body) {
+  constexpr size_t kMaxHead = 64u << 10;
+  std::string_view s(buf, n);
+  if (head_len_ == 0) {
+    size_t hend = s.find("\r\n\r\n", scanned_ > 3 ? scanned_ - 3 : 0);
+    if (hend == std::string_view::npos) {
+      scanned_ = n;
+      if (n > kMaxHead) {
+        *err = "header too large";
+        reset();
+        return -1;
+      }
+      return 0;
+    }
+    long hl = parse_head(buf, n, true, &head_, err, &content_length_, &chunked_);
+    if (hl <= 0) {
+      reset();
+      return -1;  // the terminator is there, so 0 cannot happen
+    }
+    head_len_ = hl;
+    cpos_ = static_cast<size_t>(hl);
+  }
+  size_t used = static_cast<size_t>(head_len_);
+  if (chunked_) {
+    size_t p = cpos_;
+    while (true) {
+      size_t e = s.find("\r\n", p);
+      if (e == std::string_view::npos) {
+        if (n - p > kMaxHead) {  // a size line (or trailers) that never ends
+          *err = "bad chunk size";
+          reset();
+          return -1;
+        }
+        return 0;
+      }
+      std::string_view szs = s.substr(p, e - p);
+      size_t semi = szs.find(';');
+      if (semi != std::string_view::npos) szs = szs.substr(0, semi);
+      szs = trim(szs);
+      size_t sz = 0;
+      if (!parse_chunk_size(szs, max_body, &sz)) {
+        *err = "bad chunk size";
+        reset();
+        return -1;
+      }
+      size_t q = e + 2;
+      if (sz == 0) {
+        while (true) {  // trailers until the empty line; resumed from the 0-size line if incomplete
+          size_t e2 = s.find("\r\n", q);
+          if (e2 == std::string_view::npos) {
+            if (n - p > kMaxHead) {
+              *err = "trailers too large";
+              reset();
+              return -1;
+            }
+            cpos_ = p;
+            return 0;
+          }
+          if (e2 == q) {
+            q += 2;
+            break;
+          }
+          q = e2 + 2;
+        }
+        used = q;
+        break;
+      }
+      if (sz > max_body - body_.size()) {  // body_.size() <= max_body, sz <= max_body: no wrap
+        *err = "body too large";
+        reset();
+        return -1;
+      }
+      if (q > n || n - q < sz + 2) {
+        cpos_ = p;  // this chunk is re-read once its data is in; the ones before stay decoded
+        return 0;
+      }
+      body_.append(buf + q, sz);
+      p = q + sz + 2;
+      cpos_ = p;
+    }
+    *out = std::move(head_);
+    out->body = std::move(body_);
+  } else if (content_length_ >= 0) {
+    if (static_cast<size_t>(content_length_) > max_body) {
+      *err = "body too large";
+      reset();
+      return -1;
+    }
+    if (n < used + static_cast<size_t>(content_length_)) return 0;
+    *out = std::move(head_);
+    out->body.assign(buf + used, static_cast<size_t>(content_length_));
+    used += static_cast<size_t>(content_length_);
+  } else {
+    *out = std::move(head_);  // a request without a body
+  }
+  reset();
+  return static_cast<long>(used);
+}
 
 int Dechunker::feed(const char* data, size_t n, const std::function<void(std::string_view)>& out) {
   size_t i = 0;

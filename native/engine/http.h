@@ -67,6 +67,27 @@ class Dechunker {
   unsigned long long remaining_ = 0;
 };
 
+// Resumable request parser for a connection's input buffer.  Same contract as
+// parse(buf, n, true, ...), but the work done on an incomplete request is kept:
+// the head search resumes where it stopped and complete chunks stay decoded, so
+// a request trickled in many small reads costs O(bytes), not O(bytes^2) (one
+// re-parse of the whole buffer per read).  `buf` must always start at the
+// current request; after a return != 0 the parser is ready for the next one.
+class RequestParser {
+ public:
+  long parse(const char* buf, size_t n, Message* out, std::string* err, size_t max_body);
+  void reset();
+
+ private:
+  size_t scanned_ = 0;  // bytes already searched for the end of the head
+  long head_len_ = 0;   // > 0 once the head is parsed
+  Message head_;
+  long content_length_ = -1;
+  bool chunked_ = false;
+  size_t cpos_ = 0;  // offset of the next chunk-size line
+  std::string body_;
+};
+
 // Serialise a response.
 std::string response(int status, std::string_view content_type, std::string_view body, bool keep_alive,
                      std::string_view extra_headers = {});

@@ -99,6 +99,7 @@ struct NativeServer::Conn {
   int fd = -1;
   uint64_t id = 0;
   std::string in;
+  http::RequestParser parser;  // resumes across reads: a trickled request is parsed once, not once per read
   std::string out;
   size_t out_off = 0;
   bool busy = false;
@@ -330,7 +331,7 @@ void NativeServer::process(Loop* lp, Conn* c) {
   while (!c->busy && !c->in.empty()) {
     http::Message req;
     std::string perr;
-    long used = http::parse(c->in.data(), c->in.size(), true, &req, &perr, false, cfg_.max_body);
+    long used = c->parser.parse(c->in.data(), c->in.size(), &req, &perr, cfg_.max_body);
     if (used == 0) return;
     if (used < 0) {
       stats_.bad_requests.fetch_add(1, std::memory_order_relaxed);

@@ -84,6 +84,42 @@ def test_hostile_chunk_sizes_do_not_stop_the_server():
     asyncio.run(go())
 
 
+def _trickle(port, payload: bytes, piece: int) -> bytes:
+    s = socket.create_connection(("127.0.0.1", port), timeout=10)
+    s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+    for i in range(0, len(payload), piece):
+        s.sendall(payload[i:i + piece])
+    data = b""
+    while not data.rstrip().endswith(b"}"):
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    s.close()
+    return data
+
+
+def test_trickled_chunked_filter_while_another_client_is_served():
+    """A filter body sent as one-byte chunks in small writes is answered, and a normal client on the same loop is
+    served meanwhile (the connection parser resumes instead of re-parsing the whole buffer on every read)."""
+    async def go():
+        api, c, ext = await _stack()
+        try:
+            loop = asyncio.get_running_loop()
+            body = wire.filter_args(make_pod("p", 50), ["n"])
+            framed = b"".join(b"1\r\n" + body[i:i + 1] + b"\r\n" for i in range(len(body))) + b"0\r\n\r\n"
+            slow = (b"POST /gpushare-scheduler/filter HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n" +
+                    framed)
+            one = (b"POST /gpushare-scheduler/filter HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n" % len(body)) + body
+            slow_f = loop.run_in_executor(None, _trickle, ext.port, slow, 7)
+            fast = await loop.run_in_executor(None, _raw, ext.port, one, 1)
+            assert b'"NodeNames":["n"]' in fast
+            assert b'"NodeNames":["n"]' in await slow_f
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())
+
+
 def test_concurrent_filters_from_threads_and_stats():
     async def go():
         api, c, ext = await _stack()
