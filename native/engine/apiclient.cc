@@ -346,10 +346,11 @@ bool ApiClient::request(const std::string& method, const std::string& path, cons
     }
     http::Message m;
     std::string perr;
-    char buf[16384];
+    char buf[65536];
     c->rbuf.clear();
+    http::MessageParser parser(false);  // a large chunked LIST page is decoded once, not re-parsed per read
     while (true) {
-      long got = http::parse(c->rbuf.data(), c->rbuf.size(), false, &m, &perr, false);
+      long got = parser.parse(c->rbuf.data(), c->rbuf.size(), &m, &perr);
       if (got > 0) break;
       if (got < 0) {
         release(c, false);
@@ -358,7 +359,7 @@ bool ApiClient::request(const std::string& method, const std::string& path, cons
       }
       long r = recv_some(c, buf, sizeof(buf));
       if (r == 0) {
-        long got2 = http::parse(c->rbuf.data(), c->rbuf.size(), false, &m, &perr, true);
+        long got2 = parser.parse(c->rbuf.data(), c->rbuf.size(), &m, &perr, 64u << 20, true);
         if (got2 > 0) break;
         fresh_fail = c->rbuf.empty();
         break;

@@ -99,7 +99,7 @@ void CtlServer::serve_conn(int fd) {
   std::string buf;
   char tmp[16384];
   bool open = true;
-  http::RequestParser parser;
+  http::MessageParser parser;
   while (open && !stop_.load()) {
     http::Message req;
     std::string perr;

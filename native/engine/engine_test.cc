@@ -156,7 +156,7 @@ static void test_request_parser() {
   std::string stream;
   for (const auto& r : reqs) stream += r;
   for (size_t step : {size_t(1), size_t(2), size_t(3), size_t(7), size_t(64), stream.size()}) {
-    http::RequestParser rp;
+    http::MessageParser rp;
     std::string in;
     std::vector<http::Message> got;
     for (size_t off = 0; off < stream.size(); off += step) {
@@ -182,12 +182,37 @@ static void test_request_parser() {
             got[i].keep_alive == ref.keep_alive && got[i].headers == ref.headers);
     }
   }
+  // responses (the apiserver client): chunked, 204 without a body, and a body delimited by the close
+  {
+    const std::string ch = "HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabc\r\n2\r\nde\r\n0\r\n\r\n";
+    const std::string nc = "HTTP/1.1 204 No Content\r\n\r\n";
+    for (size_t k = 1; k <= ch.size(); ++k) {
+      http::MessageParser rp(false);
+      http::Message m;
+      std::string err;
+      long r = rp.parse(ch.data(), k, &m, &err);
+      if (k < ch.size()) CHECK(r == 0);
+      if (k == ch.size()) CHECK(r == static_cast<long>(k) && m.status == 200 && m.body == "abcde");
+      if (k < ch.size()) {  // the rest arrives: the parser resumes from its state
+        r = rp.parse(ch.data(), ch.size(), &m, &err);
+        CHECK(r == static_cast<long>(ch.size()) && m.body == "abcde");
+      }
+    }
+    http::MessageParser rp(false);
+    http::Message m;
+    std::string err;
+    CHECK(rp.parse(nc.data(), nc.size(), &m, &err) == static_cast<long>(nc.size()) && m.status == 204);
+    const std::string cl = "HTTP/1.0 200 OK\r\n\r\nxyz";
+    CHECK(rp.parse(cl.data(), cl.size(), &m, &err) == 0);
+    CHECK(rp.parse(cl.data(), cl.size(), &m, &err, 64u << 20, true) == static_cast<long>(cl.size()) &&
+          m.body == "xyz" && m.body_until_close && !m.keep_alive);
+  }
   // the same hostile framing is refused, also when it arrives one byte at a time
   const char* hostile[] = {"5\r\nhello\r\nfffffffffffffffb\r\n", "5\r\nhello\r\n-1\r\n", "0x5\r\nhello\r\n0\r\n\r\n",
                            "5\r\nhello\r\n100000\r\n"};
   for (const char* b : hostile) {
     std::string req = std::string("POST /f HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n") + b;
-    http::RequestParser rp;
+    http::MessageParser rp;
     long r = 0;
     http::Message m;
     std::string err;
@@ -196,14 +221,14 @@ static void test_request_parser() {
   }
   // a head or a chunk-size line that never ends is cut off at 64 KiB instead of being re-scanned forever
   {
-    http::RequestParser rp;
+    http::MessageParser rp;
     http::Message m;
     std::string err;
     std::string head = "GET / HTTP/1.1\r\nX: " + std::string(70000, 'a');
     CHECK(rp.parse(head.data(), 1000, &m, &err, 1 << 20) == 0);
     CHECK(rp.parse(head.data(), head.size(), &m, &err, 1 << 20) == -1 && err == "header too large");
     std::string sl = "POST /f HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n" + std::string(70000, '0');
-    http::RequestParser rp2;
+    http::MessageParser rp2;
     CHECK(rp2.parse(sl.data(), sl.size(), &m, &err, 1 << 20) == -1);
   }
   // 100k one-byte chunks trickled in 16-byte reads: linear work (this loop would be ~10^10 byte scans if every
@@ -212,7 +237,7 @@ static void test_request_parser() {
     std::string big = "POST /t HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n";
     for (int i = 0; i < 100000; ++i) big += "1\r\nz\r\n";
     big += "0\r\n\r\n";
-    http::RequestParser rp;
+    http::MessageParser rp;
     http::Message m;
     std::string err;
     long r = 0;

@@ -227,7 +227,7 @@ long parse(const char* buf, size_t n, bool is_request, Message* out, std::string
   return static_cast<long>(n);
 }
 
-void RequestParser::reset() {
+void MessageParser::reset() {
   scanned_ = 0;
   head_len_ = 0;
   head_ = Message();
@@ -237,7 +237,7 @@ void RequestParser::reset() {
   body_.clear();
 }
 
-long RequestParser::parse(const char* buf, size_t n, Message* out, std::string* err, size_t max_body) {
+long MessageParser::parse(const char* buf, size_t n, Message* out, std::string* err, size_t max_body, bool eof) {
   constexpr size_t kMaxHead = 64u << 10;
   std::string_view s(buf, n);
   if (head_len_ == 0) {
@@ -251,7 +251,7 @@ long RequestParser::parse(const char* buf, size_t n, Message* out, std::string* 
       }
       return 0;
     }
-    long hl = parse_head(buf, n, true, &head_, err, &content_length_, &chunked_);
+    long hl = parse_head(buf, n, is_request_, &head_, err, &content_length_, &chunked_);
     if (hl <= 0) {
       reset();
       return -1;  // the terminator is there, so 0 cannot happen
@@ -329,8 +329,16 @@ long RequestParser::parse(const char* buf, size_t n, Message* out, std::string* 
     *out = std::move(head_);
     out->body.assign(buf + used, static_cast<size_t>(content_length_));
     used += static_cast<size_t>(content_length_);
+  } else if (is_request_ || head_.status == 204 || head_.status == 304 || (head_.status >= 100 && head_.status < 200)) {
+    *out = std::move(head_);  // no body
   } else {
-    *out = std::move(head_);  // a request without a body
+    // a response delimited by the connection closing
+    if (!eof) return 0;
+    *out = std::move(head_);
+    out->body_until_close = true;
+    out->keep_alive = false;
+    out->body.assign(buf + used, n - used);
+    used = n;
   }
   reset();
   return static_cast<long>(used);

@@ -67,18 +67,21 @@ class Dechunker {
   unsigned long long remaining_ = 0;
 };
 
-// Resumable request parser for a connection's input buffer.  Same contract as
-// parse(buf, n, true, ...), but the work done on an incomplete request is kept:
-// the head search resumes where it stopped and complete chunks stay decoded, so
-// a request trickled in many small reads costs O(bytes), not O(bytes^2) (one
-// re-parse of the whole buffer per read).  `buf` must always start at the
-// current request; after a return != 0 the parser is ready for the next one.
-class RequestParser {
+// Resumable parser for one connection's input buffer.  Same contract as
+// parse(), but the work done on an incomplete message is kept: the head search
+// resumes where it stopped and complete chunks stay decoded, so a message that
+// arrives in many small reads costs O(bytes), not O(bytes^2) (one re-parse of
+// the whole buffer per read).  `buf` must always start at the current message;
+// after a return != 0 the parser is ready for the next one.
+class MessageParser {
  public:
-  long parse(const char* buf, size_t n, Message* out, std::string* err, size_t max_body);
+  explicit MessageParser(bool is_request = true) : is_request_(is_request) {}
+  long parse(const char* buf, size_t n, Message* out, std::string* err, size_t max_body = 64u << 20,
+             bool eof = false);
   void reset();
 
  private:
+  bool is_request_;
   size_t scanned_ = 0;  // bytes already searched for the end of the head
   long head_len_ = 0;   // > 0 once the head is parsed
   Message head_;

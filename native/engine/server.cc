@@ -99,7 +99,7 @@ struct NativeServer::Conn {
   int fd = -1;
   uint64_t id = 0;
   std::string in;
-  http::RequestParser parser;  // resumes across reads: a trickled request is parsed once, not once per read
+  http::MessageParser parser;  // resumes across reads: a trickled request is parsed once, not once per read
   std::string out;
   size_t out_off = 0;
   bool busy = false;
