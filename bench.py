@@ -90,6 +90,22 @@ def _cpu_times(children) -> dict:
     return out
 
 
+def _rss_mib(children) -> dict:
+    """Resident set of this process and the child servers (a long run shows whether any of them grows)."""
+    out = {}
+    for name, pid in [("rank0", os.getpid())] + [(c.name, getattr(getattr(c, "proc", None), "pid", None))
+                                                 for c in children]:
+        try:
+            with open(f"/proc/{pid}/status") as f:
+                for ln in f:
+                    if ln.startswith("VmRSS:"):
+                        out[name] = round(int(ln.split()[1]) / 1024, 1)
+                        break
+        except (OSError, TypeError, ValueError):
+            pass
+    return out
+
+
 class NativeRuntime:
     """One GPU's pod runtime endpoint served from C++ (``_engine.PodRuntime``) with the rank's HBM arena."""
 
@@ -665,6 +681,7 @@ def main():
             # the CPU-time counters are read before the bracket: reading /proc for every child took ~0.5 ms, which
             # sat inside the timed region (rank 0's span exceeded the sum of its waves by that much)
             cpu0 = _cpu_times(children)
+            rss0 = _rss_mib(children)
             cg0 = _cgroup_cpu()
             bracket()
             if world > 1:
@@ -693,6 +710,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     own_elapsed = elapsed
     cpu1 = _cpu_times(children)
+    rss1 = _rss_mib(children)
     cg1 = _cgroup_cpu()
     if prof is not None:
         lt.run(asyncio.sleep(0))
@@ -824,6 +842,8 @@ def main():
             "extender": extender_stats,
             "apiserver": apiserver_stats,
             "cpu_s": {k: round(cpu1[k] - cpu0.get(k, 0.0), 3) for k in cpu1},
+            # resident memory of each process at the start and the end of the timed region
+            "rss_mib": {k: [rss0.get(k), rss1[k]] for k in rss1},
             # CPU-quota throttling of the container during the timed region (cgroup v2), if any
             "cgroup_timed": {"usage_ms": round((cg1.get("usage_usec", 0) - cg0.get("usage_usec", 0)) / 1e3, 1),
                              "nr_throttled": cg1.get("nr_throttled", 0) - cg0.get("nr_throttled", 0),
