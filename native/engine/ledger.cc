@@ -472,8 +472,9 @@ void Ledger::remember_pending(const std::string& uid, PendingPod p) {
   }
   pending_.emplace(uid, std::move(p));
   pending_order_.push_back(uid);
-  if (pending_order_.size() > 2 * kMax) {
-    // drop ids already forgotten so the order queue stays bounded
+  if (pending_order_.size() > 2 * pending_.size() + 1024) {
+    // drop ids already forgotten (bound pods) so the order queue stays proportional to the live set; each pass
+    // removes at least half the queue, so the cost is amortised O(1) per pod
     std::deque<std::string> keep;
     for (auto& u : pending_order_) {
       if (pending_.count(u)) keep.push_back(u);
