@@ -106,6 +106,14 @@ static void test_ledger() {
   CHECK(out.find("\"zz\":\"node \\\"zz\\\" not found\"") != std::string::npos);
   Ledger::PendingPod pp;
   CHECK(l.pending("uq", &pp) && pp.req == 16276 && pp.name == "q");
+  // 200k pods filtered then bound: the eviction-order queue stays proportional to the live records
+  for (int i = 0; i < 200000; ++i) {
+    std::string u = "soak-" + std::to_string(i);
+    l.remember_pending(u, pp);
+    l.forget_pending(u);
+  }
+  CHECK(l.pending_count() == 1 && l.pending_queue_len() <= 2 * l.pending_count() + 1024 + 1);
+  CHECK(l.pending("uq", &pp));
 }
 
 static void test_http() {

@@ -165,6 +165,9 @@ class Ledger {
   void remember_pending(const std::string& uid, PendingPod p);
   bool pending(const std::string& uid, PendingPod* out) const;
   void forget_pending(const std::string& uid);
+  // live filter-time records and the length of their eviction-order queue (bounded by 2x live + 1024)
+  size_t pending_count() const { return pending_.size(); }
+  size_t pending_queue_len() const { return pending_order_.size(); }
   size_t pending_count() const { return pending_.size(); }
 
  private:
