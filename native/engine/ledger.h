@@ -168,7 +168,6 @@ class Ledger {
   // live filter-time records and the length of their eviction-order queue (bounded by 2x live + 1024)
   size_t pending_count() const { return pending_.size(); }
   size_t pending_queue_len() const { return pending_order_.size(); }
-  size_t pending_count() const { return pending_.size(); }
 
  private:
   void account(PodRec& r);
