@@ -63,13 +63,14 @@ void CtlServer::stop() {
   if (acc_.joinable()) acc_.join();
   if (lfd_ >= 0) ::close(lfd_);
   lfd_ = -1;
-  std::vector<std::thread> ts;
+  std::map<uint64_t, std::thread> ts;
   {
     std::lock_guard<std::mutex> g(mu_);
     for (int fd : conns_) ::shutdown(fd, SHUT_RDWR);
     ts.swap(threads_);
+    finished_.clear();
   }
-  for (auto& t : ts) t.join();
+  for (auto& kv : ts) kv.second.join();
 }
 
 void CtlServer::accept_loop() {
@@ -81,17 +82,32 @@ void CtlServer::accept_loop() {
     }
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-    std::lock_guard<std::mutex> g(mu_);
-    if (stop_.load()) {
-      ::close(fd);
-      return;
+    std::vector<std::thread> done;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (stop_.load()) {
+        ::close(fd);
+        return;
+      }
+      // reap the threads of closed connections (a joinable thread keeps its stack until it is joined)
+      for (uint64_t id : finished_) {
+        auto it = threads_.find(id);
+        if (it == threads_.end()) continue;
+        done.push_back(std::move(it->second));
+        threads_.erase(it);
+      }
+      finished_.clear();
+      conns_.push_back(fd);
+      const uint64_t id = next_conn_++;
+      threads_.emplace(id, std::thread([this, fd, id] {
+        introspect::name_thread("ctl-conn");
+        pin_thread();
+        serve_conn(fd);
+        std::lock_guard<std::mutex> g2(mu_);
+        finished_.push_back(id);
+      }));
     }
-    conns_.push_back(fd);
-    threads_.emplace_back([this, fd] {
-      introspect::name_thread("ctl-conn");
-      pin_thread();
-      serve_conn(fd);
-    });
+    for (auto& t : done) t.join();  // returned or about to: outside the lock their epilogue needs
   }
 }
 

@@ -6,6 +6,7 @@
 
 #include <atomic>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -46,7 +47,9 @@ class CtlServer {
   std::thread acc_;
   std::mutex mu_;
   std::vector<int> conns_;
-  std::vector<std::thread> threads_;
+  std::map<uint64_t, std::thread> threads_;  // per connection; joined once finished (see accept_loop)
+  std::vector<uint64_t> finished_;            // connections whose thread has returned
+  uint64_t next_conn_ = 0;
 };
 
 }  // namespace gsx
