@@ -200,7 +200,8 @@ class Controller:
 
 def api_dict(cfg) -> dict:
     """Connection settings of a :class:`KubeConfig` for the native engine's apiserver clients."""
-    return {"server": cfg.server, "token": cfg.token or "", "ca_file": cfg.ca_file or "",
+    return {"server": cfg.server, "token": cfg.token or "", "token_file": getattr(cfg, "token_file", None) or "",
+            "token_reload_s": float(getattr(cfg, "token_reload_s", 60.0)), "ca_file": cfg.ca_file or "",
             "cert_file": cfg.cert_file or "", "key_file": cfg.key_file or "", "insecure": bool(cfg.insecure)}
 
 

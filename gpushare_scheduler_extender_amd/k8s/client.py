@@ -22,6 +22,7 @@ from __future__ import annotations
 import asyncio
 import base64
 import json
+import logging
 import os
 import ssl
 import tempfile
@@ -35,6 +36,7 @@ from .fasthttp import Client
 import yaml
 
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+log = logging.getLogger("gsx.k8s")
 
 
 class ApiError(Exception):
@@ -93,6 +95,22 @@ class KubeConfig:
     key_file: str | None = None
     insecure: bool = False
     extra_headers: dict = field(default_factory=dict)
+    # projected service-account tokens are rotated by kubelet: re-read this file (client-go does the same)
+    token_file: str | None = None
+    token_reload_s: float = 60.0
+    _token_read_at: float = field(default=0.0, repr=False)
+
+    def current_token(self) -> str | None:
+        """The bearer token, re-read from ``token_file`` at most every ``token_reload_s`` (a failed read keeps
+        the last one)."""
+        if self.token_file and time.monotonic() - self._token_read_at >= self.token_reload_s:
+            self._token_read_at = time.monotonic()
+            try:
+                with open(self.token_file) as f:
+                    self.token = f.read().strip() or self.token
+            except OSError as e:
+                log.warning("re-reading token file %s: %s", self.token_file, e)
+        return self.token
 
     @classmethod
     def from_url(cls, url: str) -> "KubeConfig":
@@ -104,11 +122,13 @@ class KubeConfig:
         port = os.environ.get("KUBERNETES_SERVICE_PORT", "443")
         if not host:
             raise RuntimeError("not running in a cluster (KUBERNETES_SERVICE_HOST unset)")
-        with open(os.path.join(SA_DIR, "token")) as f:
+        token_file = os.path.join(SA_DIR, "token")
+        with open(token_file) as f:
             token = f.read().strip()
         if ":" in host:
             host = f"[{host}]"
-        return cls(server=f"https://{host}:{port}", token=token, ca_file=os.path.join(SA_DIR, "ca.crt"))
+        return cls(server=f"https://{host}:{port}", token=token, ca_file=os.path.join(SA_DIR, "ca.crt"),
+                   token_file=token_file, _token_read_at=time.monotonic())
 
     @classmethod
     def from_kubeconfig(cls, path: str, context: str | None = None) -> "KubeConfig":
@@ -140,14 +160,17 @@ class KubeConfig:
             return None
 
         token = us.get("token")
+        token_file = None
         if not token and us.get("tokenFile"):
-            with open(us["tokenFile"]) as f:
+            token_file = us["tokenFile"] if os.path.isabs(us["tokenFile"]) else os.path.join(base, us["tokenFile"])
+            with open(token_file) as f:
                 token = f.read().strip()
         headers = {}
         if us.get("username") and us.get("password"):
             headers["Authorization"] = "Basic " + base64.b64encode(
                 f"{us['username']}:{us['password']}".encode()).decode()
-        return cls(server=cl["server"].rstrip("/"), token=token,
+        return cls(server=cl["server"].rstrip("/"), token=token, token_file=token_file,
+                   _token_read_at=time.monotonic(),
                    ca_file=_file("certificate-authority-data", "certificate-authority", cl),
                    cert_file=_file("client-certificate-data", "client-certificate", us),
                    key_file=_file("client-key-data", "client-key", us),
@@ -201,15 +224,21 @@ class KubeClient:
         self.user_agent = user_agent
         self._limit = connector_limit
         self._http: Client | None = None
+        self._sent_token: str | None = None
         self.calls = 0
 
     def _client(self) -> Client:
+        token = self.config.current_token()
         if self._http is None or self._http.closed:
             headers = {"User-Agent": self.user_agent, **self.config.extra_headers}
-            if self.config.token:
-                headers["Authorization"] = f"Bearer {self.config.token}"
+            if token:
+                headers["Authorization"] = f"Bearer {token}"
             self._http = Client(self.config.server, ssl_context=self.config.ssl_context(), headers=headers,
                                 limit=self._limit)
+            self._sent_token = token
+        elif token != self._sent_token:
+            self._http.set_header("Authorization", f"Bearer {token}")
+            self._sent_token = token
         return self._http
 
     async def close(self):

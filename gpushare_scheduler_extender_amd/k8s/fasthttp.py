@@ -392,13 +392,18 @@ class Client:
         if u.scheme == "https" and self.ssl is None:
             self.ssl = _ssl.create_default_context()
         hostport = self.host if self.port in (80, 443) else f"{self.host}:{self.port}"
-        base = {"Host": hostport, "Accept": "application/json"}
-        base.update(headers or {})
-        self._base_head = "".join(f"{k}: {v}\r\n" for k, v in base.items()).encode()
+        self._base = {"Host": hostport, "Accept": "application/json"}
+        self._base.update(headers or {})
+        self._base_head = "".join(f"{k}: {v}\r\n" for k, v in self._base.items()).encode()
         self.idle: list[_Conn] = []
         self.limit = limit
         self.timeout = timeout
         self.closed = False
+
+    def set_header(self, name: str, value: str) -> None:
+        """Replace a header sent with every request (e.g. a rotated bearer token)."""
+        self._base[name] = value
+        self._base_head = "".join(f"{k}: {v}\r\n" for k, v in self._base.items()).encode()
 
     async def _open(self) -> _Conn:
         r, w = await asyncio.open_connection(self.host, self.port, ssl=self.ssl, limit=1 << 22)

@@ -12,6 +12,9 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
+#include <fstream>
+#include <sstream>
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
@@ -203,6 +206,26 @@ long ApiClient::recv_some(Conn* c, char* buf, size_t n) {
   }
 }
 
+std::string ApiClient::bearer() const {
+  if (cfg_.token_file.empty()) return cfg_.token;
+  const double now = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  std::lock_guard<std::mutex> g(tok_mu_);
+  if (tok_at_ == 0.0 || now - tok_at_ >= cfg_.token_reload_s) {
+    tok_at_ = now;
+    std::ifstream f(cfg_.token_file);
+    std::stringstream ss;
+    if (f) ss << f.rdbuf();
+    std::string t = ss.str();
+    while (!t.empty() && (t.back() == '\n' || t.back() == '\r' || t.back() == ' ')) t.pop_back();
+    if (!t.empty()) {
+      tok_ = t;
+    } else if (tok_.empty()) {
+      tok_ = cfg_.token;  // unreadable file: keep what we were given
+    }
+  }
+  return tok_;
+}
+
 std::string ApiClient::request_head(const std::string& method, const std::string& path, size_t body_len,
                                     const char* content_type, bool has_body) const {
   std::string req;
@@ -212,7 +235,8 @@ std::string ApiClient::request_head(const std::string& method, const std::string
   if ((url_.tls && url_.port != 443) || (!url_.tls && url_.port != 80)) req.append(":").append(std::to_string(url_.port));
   req.append("\r\nUser-Agent: ").append(cfg_.user_agent);
   req.append("\r\nAccept: application/json\r\n");
-  if (!cfg_.token.empty()) req.append("Authorization: Bearer ").append(cfg_.token).append("\r\n");
+  const std::string tok = bearer();
+  if (!tok.empty()) req.append("Authorization: Bearer ").append(tok).append("\r\n");
   if (has_body) {
     req.append("Content-Type: ").append(content_type ? content_type : "application/json").append("\r\n");
     req.append("Content-Length: ").append(std::to_string(body_len)).append("\r\n");

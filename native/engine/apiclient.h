@@ -23,6 +23,8 @@ namespace gsx {
 struct ApiConfig {
   std::string server;  // http(s)://host:port
   std::string token;   // bearer token
+  std::string token_file;      // re-read every token_reload_s (kubelet rotates projected SA tokens)
+  double token_reload_s = 60.0;
   std::string ca_file, cert_file, key_file;
   bool insecure = false;
   double timeout_s = 30.0;
@@ -78,6 +80,10 @@ class ApiClient {
   long recv_some(Conn* c, char* buf, size_t n);
 
   ApiConfig cfg_;
+  std::string bearer() const;  // cfg_.token, refreshed from cfg_.token_file when it is due
+  mutable std::mutex tok_mu_;
+  mutable std::string tok_;
+  mutable double tok_at_ = 0.0;
   http::Url url_;
   SSL_CTX* ctx_ = nullptr;
   bool ok_ = false;

@@ -77,6 +77,8 @@ ApiConfig api_from(const py::dict& api) {
   };
   get("server", &c.server);
   get("token", &c.token);
+  get("token_file", &c.token_file);
+  if (api.contains("token_reload_s")) c.token_reload_s = api["token_reload_s"].cast<double>();
   get("ca_file", &c.ca_file);
   get("cert_file", &c.cert_file);
   get("key_file", &c.key_file);

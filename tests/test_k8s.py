@@ -469,3 +469,59 @@ def test_paginated_list_limit_continue(impl):
             if child:
                 child.stop()
     asyncio.run(go())
+
+
+def test_rotated_service_account_token_is_reread_by_both_clients(tmp_path):
+    """kubelet rotates projected service-account tokens in place; the asyncio client and the native apiserver
+    client both re-read the token file (client-go does too) instead of sending the first token forever."""
+    import http.server
+    import threading
+
+    from gpushare_scheduler_extender_amd.core.controller import api_dict
+    from gpushare_scheduler_extender_amd.core.engine import native
+    from gpushare_scheduler_extender_amd.k8s.client import KubeClient, KubeConfig
+
+    seen = []
+
+    class H(http.server.BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def do_GET(self):  # noqa: N802
+            seen.append(self.headers.get("Authorization"))
+            body = b'{"kind":"PodList","items":[],"metadata":{"resourceVersion":"1"}}'
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    tok = tmp_path / "token"
+    tok.write_text("first\n")
+    try:
+        cfg = KubeConfig(server=f"http://127.0.0.1:{srv.server_address[1]}", token_file=str(tok), token_reload_s=0.0)
+
+        async def py_side():
+            c = KubeClient(cfg)
+            try:
+                await c.list("pods")
+                tok.write_text("second\n")
+                await c.list("pods")
+            finally:
+                await c.close()
+
+        asyncio.run(py_side())
+        assert seen == ["Bearer first", "Bearer second"]
+        seen.clear()
+        tok.write_text("third")
+        bc = native().BatchClient(api_dict(cfg))
+        assert bc.run([("GET", "/api/v1/pods", b"")], 1)[0][0] == 200
+        tok.write_text("fourth")
+        assert bc.run([("GET", "/api/v1/pods", b"")], 1)[0][0] == 200
+        assert seen == ["Bearer third", "Bearer fourth"]
+    finally:
+        srv.shutdown()
