@@ -355,9 +355,12 @@ class KubeClient:
         return await self.create("events", ev, ns)
 
     async def watch(self, kind: str, ns: str | None = None, resource_version: str = "", field_selector: str = "",
-                    label_selector: str = "", timeout_seconds: int = 0, raw: bool = False) -> AsyncIterator:
-        """Yield watch events (dicts), or ``(event, raw_line_bytes)`` with ``raw=True``."""
-        params = {"watch": "true", "allowWatchBookmarks": "false"}
+                    label_selector: str = "", timeout_seconds: int = 0, raw: bool = False,
+                    bookmarks: bool = False) -> AsyncIterator:
+        """Yield watch events (dicts), or ``(event, raw_line_bytes)`` with ``raw=True``.  With ``bookmarks`` the
+        apiserver may also send ``BOOKMARK`` events (metadata.resourceVersion only), which keep a re-watch after a
+        timeout inside the history window instead of ending in 410 and a re-list."""
+        params = {"watch": "true", "allowWatchBookmarks": "true" if bookmarks else "false"}
         if resource_version:
             params["resourceVersion"] = resource_version
         if field_selector:
@@ -376,11 +379,12 @@ class KubeClient:
             buf = b""
             async for chunk in chunks:
                 buf = buf + chunk if buf else chunk
+                start = 0  # lines are cut from an offset: a chunk of many events is not re-copied once per event
                 while True:
-                    i = buf.find(b"\n")
+                    i = buf.find(b"\n", start)
                     if i < 0:
                         break
-                    line, buf = buf[:i], buf[i + 1:]
+                    line, start = buf[start:i], i + 1
                     if not line.strip():
                         continue
                     ev = json.loads(line)
@@ -388,5 +392,6 @@ class KubeClient:
                         o = ev.get("object") or {}
                         raise ApiError(int(o.get("code", 500)), o.get("reason", ""), o.get("message", ""), o)
                     yield (ev, line) if raw else ev
+                buf = buf[start:]
         finally:
             close()

@@ -94,6 +94,7 @@ class Informer:
         self.relists = 0
         self.rewatches = 0
         self.events = 0
+        self.bookmarks = 0
         self.last_list_start = 0.0  # time.monotonic() when the last applied LIST was sent
         self._relist = False
         self._watch_task: asyncio.Task | None = None
@@ -135,6 +136,12 @@ class Informer:
 
     # internals
     def _dispatch(self, etype: str, obj: dict, raw: bytes | None):
+        if etype == "BOOKMARK":  # progress marker: only the resourceVersion to resume from
+            self.bookmarks += 1
+            rv = (obj.get("metadata") or {}).get("resourceVersion")
+            if rv:
+                self.last_rv = rv
+            return
         key = obj_key(obj)
         self.events += 1
         if etype == "ADDED" or etype == "MODIFIED":
@@ -187,7 +194,7 @@ class Informer:
 
     async def _watch_once(self):
         async for ev, raw in self.client.watch(self.kind, self.namespace, self.last_rv, self.field_selector,
-                                               self.label_selector, self.watch_timeout, raw=True):
+                                               self.label_selector, self.watch_timeout, raw=True, bookmarks=True):
             self._dispatch(ev["type"], ev["object"], raw)
 
     async def _run(self):

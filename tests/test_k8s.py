@@ -525,3 +525,16 @@ def test_rotated_service_account_token_is_reread_by_both_clients(tmp_path):
         assert seen == ["Bearer third", "Bearer fourth"]
     finally:
         srv.shutdown()
+
+
+def test_informer_bookmark_moves_resume_version_without_events():
+    """A BOOKMARK carries only metadata.resourceVersion: the informer resumes from it and calls no handler."""
+    from gpushare_scheduler_extender_amd.k8s.informer import Handler, Informer
+
+    calls = []
+    inf = Informer(None, "pods")
+    inf.add_handler(Handler(lambda o, r: calls.append("add"), lambda a, b, r: calls.append("upd"),
+                            lambda o, r: calls.append("del")))
+    inf._dispatch("ADDED", {"metadata": {"name": "a", "namespace": "d", "resourceVersion": "5"}}, None)
+    inf._dispatch("BOOKMARK", {"kind": "Pod", "metadata": {"resourceVersion": "42"}}, None)
+    assert calls == ["add"] and inf.last_rv == "42" and inf.bookmarks == 1 and list(inf.store) == ["d/a"]
