@@ -140,7 +140,7 @@ ApiClient::Conn* ApiClient::connect_new(std::string* err) {
   if (url_.tls) {
     c->ssl = SSL_new(ctx_);
     SSL_set_fd(c->ssl, fd);
-    SSL_set_tlsext_host_name(c->ssl, url_.host.c_str());
+    if (!is_ip(url_.host)) SSL_set_tlsext_host_name(c->ssl, url_.host.c_str());  // no IP literals in SNI (RFC 6066)
     if (!cfg_.insecure) {
       X509_VERIFY_PARAM* p = SSL_get0_param(c->ssl);
       if (is_ip(url_.host)) {

@@ -538,3 +538,84 @@ def test_informer_bookmark_moves_resume_version_without_events():
     inf._dispatch("ADDED", {"metadata": {"name": "a", "namespace": "d", "resourceVersion": "5"}}, None)
     inf._dispatch("BOOKMARK", {"kind": "Pod", "metadata": {"resourceVersion": "42"}}, None)
     assert calls == ["add"] and inf.last_rv == "42" and inf.bookmarks == 1 and list(inf.store) == ["d/a"]
+
+
+def _make_pki(d):
+    """A throwaway CA and a server certificate for IP 127.0.0.1 (openssl CLI)."""
+    import shutil
+    import subprocess
+
+    if not shutil.which("openssl"):
+        pytest.skip("openssl CLI not available")
+
+    def run(*a):
+        subprocess.run(["openssl", *a], check=True, capture_output=True, cwd=d)
+
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "ca.key", "-out", "ca.crt", "-subj", "/CN=gsx-ca",
+        "-days", "1")
+    run("req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", "other.key", "-out", "other.crt", "-subj",
+        "/CN=other-ca", "-days", "1")
+    run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", "srv.key", "-out", "srv.csr", "-subj", "/CN=kubernetes")
+    (d / "ext.cnf").write_text("subjectAltName=IP:127.0.0.1,DNS:kubernetes.default.svc\n")
+    run("x509", "-req", "-in", "srv.csr", "-CA", "ca.crt", "-CAkey", "ca.key", "-CAcreateserial", "-out", "srv.crt",
+        "-days", "1", "-extfile", "ext.cnf")
+    return d / "ca.crt", d / "other.crt", d / "srv.crt", d / "srv.key"
+
+
+def test_tls_apiserver_verified_by_ca_and_ip_san(tmp_path):
+    """In-cluster traffic is HTTPS to an IP (KUBERNETES_SERVICE_HOST): both clients verify the server against the
+    CA file and the IP SAN, send the bearer token, and refuse a server the CA did not sign."""
+    import http.server
+    import ssl
+    import threading
+
+    from gpushare_scheduler_extender_amd.core.controller import api_dict
+    from gpushare_scheduler_extender_amd.core.engine import native
+    from gpushare_scheduler_extender_amd.k8s.client import KubeClient, KubeConfig
+
+    ca, other, crt, key = _make_pki(tmp_path)
+    seen = []
+
+    class H(http.server.BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def do_GET(self):  # noqa: N802
+            seen.append(self.headers.get("Authorization"))
+            body = b'{"kind":"PodList","items":[],"metadata":{"resourceVersion":"1"}}'
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+    ctx.load_cert_chain(str(crt), str(key))
+    srv.socket = ctx.wrap_socket(srv.socket, server_side=True)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    url = f"https://127.0.0.1:{srv.server_address[1]}"
+    try:
+        good = KubeConfig(server=url, token="t0k", ca_file=str(ca))
+        st, _ = native().BatchClient(api_dict(good)).run([("GET", "/api/v1/pods", b"")], 1)[0]
+        assert st == 200 and seen == ["Bearer t0k"]
+
+        async def py_side():
+            c = KubeClient(good)
+            try:
+                return await c.list("pods")
+            finally:
+                await c.close()
+
+        assert asyncio.run(py_side())["kind"] == "PodList" and len(seen) == 2
+        bad = KubeConfig(server=url, token="t0k", ca_file=str(other))
+        st, body = native().BatchClient(api_dict(bad)).run([("GET", "/api/v1/pods", b"")], 1)[0]
+        assert st != 200 and len(seen) == 2, (st, body)
+        # right CA, wrong name: "localhost" is not among the certificate's SANs
+        wrong = KubeConfig(server=f"https://localhost:{srv.server_address[1]}", token="t0k", ca_file=str(ca))
+        st, body = native().BatchClient(api_dict(wrong)).run([("GET", "/api/v1/pods", b"")], 1)[0]
+        assert st != 200 and len(seen) == 2 and b"TLS handshake" in body, (st, body)
+    finally:
+        srv.shutdown()
