@@ -559,7 +559,69 @@ def _make_pki(d):
     (d / "ext.cnf").write_text("subjectAltName=IP:127.0.0.1,DNS:kubernetes.default.svc\n")
     run("x509", "-req", "-in", "srv.csr", "-CA", "ca.crt", "-CAkey", "ca.key", "-CAcreateserial", "-out", "srv.crt",
         "-days", "1", "-extfile", "ext.cnf")
+    run("req", "-newkey", "rsa:2048", "-nodes", "-keyout", "cli.key", "-out", "cli.csr", "-subj",
+        "/CN=system:kube-scheduler")
+    run("x509", "-req", "-in", "cli.csr", "-CA", "ca.crt", "-CAkey", "ca.key", "-CAcreateserial", "-out", "cli.crt",
+        "-days", "1")
     return d / "ca.crt", d / "other.crt", d / "srv.crt", d / "srv.key"
+
+
+def test_mutual_tls_client_certificate(tmp_path):
+    """A kubeconfig with client-certificate / client-key (mTLS): the server requires a CA-signed client cert."""
+    import http.server
+    import ssl
+    import threading
+
+    from gpushare_scheduler_extender_amd.core.controller import api_dict
+    from gpushare_scheduler_extender_amd.core.engine import native
+    from gpushare_scheduler_extender_amd.k8s.client import KubeClient, KubeConfig
+
+    ca, _other, crt, key = _make_pki(tmp_path)
+    peers = []
+
+    class H(http.server.BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def do_GET(self):  # noqa: N802
+            peers.append(dict(x[0] for x in self.connection.getpeercert()["subject"])["commonName"])
+            body = b'{"kind":"PodList","items":[],"metadata":{"resourceVersion":"1"}}'
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+    ctx.load_cert_chain(str(crt), str(key))
+    ctx.load_verify_locations(str(ca))
+    ctx.verify_mode = ssl.CERT_REQUIRED
+    srv.socket = ctx.wrap_socket(srv.socket, server_side=True)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    url = f"https://127.0.0.1:{srv.server_address[1]}"
+    try:
+        cfg = KubeConfig(server=url, ca_file=str(ca), cert_file=str(tmp_path / "cli.crt"),
+                         key_file=str(tmp_path / "cli.key"))
+        st, _ = native().BatchClient(api_dict(cfg)).run([("GET", "/api/v1/pods", b"")], 1)[0]
+        assert st == 200
+
+        async def py_side():
+            c = KubeClient(cfg)
+            try:
+                return await c.list("pods")
+            finally:
+                await c.close()
+
+        assert asyncio.run(py_side())["kind"] == "PodList"
+        assert peers == ["system:kube-scheduler"] * 2
+        # without the client certificate the handshake is refused
+        anon = KubeConfig(server=url, ca_file=str(ca))
+        st, body = native().BatchClient(api_dict(anon)).run([("GET", "/api/v1/pods", b"")], 1)[0]
+        assert st != 200 and len(peers) == 2, (st, body)
+    finally:
+        srv.shutdown()
 
 
 def test_tls_apiserver_verified_by_ca_and_ip_san(tmp_path):
