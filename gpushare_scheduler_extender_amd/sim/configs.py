@@ -100,13 +100,13 @@ class Cluster:
 
     def __init__(self, profile: NamingProfile, totals: list[int], gpu: bool | int, cu_count: int = 256,
                  native: bool = True, partition: str = "SPX", xcc_count: int = 8, agent: str | None = None,
-                 pool_gib: int = 0):
+                 pool_gib: int = 0, bind_mode: str = "binding"):
         self.profile = profile
         self.totals = totals
         self.children = []
         self.api = start_apiserver()
         self.children.append(self.api)
-        self.ext = start_extender(self.api.url, profile=profile.name)
+        self.ext = start_extender(self.api.url, profile=profile.name, bind_mode=bind_mode)
         self.children.append(self.ext)
         # native: compiled kube-scheduler / node-agent stand-ins; otherwise the asyncio ones
         self.children.append(start_scheduler(self.api.url, self.ext.url, profile=profile.name, native=native))

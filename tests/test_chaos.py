@@ -27,14 +27,19 @@ async def _retry(fn, *a, tries=50, **kw):
             await asyncio.sleep(0.002)
 
 
-@pytest.mark.parametrize("seed,impl,agent", [(7, "native", "plugin"), (11, "native", "plugin"), (23, "native", "native"),
-                                             (7, "python", "plugin"), (11, "native", "native")])
-def test_chaos_whole_stack_converges_without_overcommit(seed, impl, agent):
+@pytest.mark.parametrize("seed,impl,agent,bind_mode", [(7, "native", "plugin", "binding"),
+                                                       (11, "native", "plugin", "binding"),
+                                                       (23, "native", "native", "binding"),
+                                                       (7, "python", "plugin", "binding"),
+                                                       (11, "native", "native", "binding"),
+                                                       (13, "native", "plugin", "update")])
+def test_chaos_whole_stack_converges_without_overcommit(seed, impl, agent, bind_mode):
     """``impl``: compiled or asyncio scheduler stand-in; ``agent``: kubelet + the shipped gRPC device plugin
-    (the product path) or the compiled node agent."""
+    (the product path) or the compiled node agent; ``bind_mode``: one annotated Binding, or the reference's
+    annotation write + Binding (two calls, the first guarded by resourceVersion)."""
     async def go():
         rnd = random.Random(seed)
-        cl = Cluster(ALIYUN, [96] * 4, gpu=False, native=impl == "native", agent=agent)
+        cl = Cluster(ALIYUN, [96] * 4, gpu=False, native=impl == "native", agent=agent, bind_mode=bind_mode)
         try:
             await cl.start()
             api = HttpClient(cl.api.url)
@@ -81,6 +86,12 @@ def test_chaos_whole_stack_converges_without_overcommit(seed, impl, agent):
             st = json.loads((await api.request("GET", "/fake/stats")).body)
             assert st["counts"].get("injected_conflict", 0) > 0 and st["counts"].get("injected_error", 0) > 0
             await api.close()
+            ext = HttpClient(cl.ext.url)
+            srv = json.loads((await ext.request("GET", "/debug/engine")).body)["server"]
+            await ext.close()
+            # update mode writes the annotations before each Binding: at least two apiserver calls per bind
+            assert srv["bind_ok"] > 0
+            assert (srv["api_calls"] >= 2 * srv["bind_ok"]) == (bind_mode == "update"), srv
         finally:
             await cl.close()
     asyncio.run(go())
