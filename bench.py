@@ -302,7 +302,9 @@ def parse():
     ap.add_argument("--profile", default="aliyun")
     ap.add_argument("--bind-mode", default="binding", choices=["binding", "update"])
     ap.add_argument("--devices", default="auto", help="auto|hip|amdsmi|fake (fake: no GPU, CPU plumbing only)")
-    ap.add_argument("--stamp-stride", type=int, default=1 << 20)
+    # one stamp per 2 MiB carve unit: slices are carved in 2 MiB units, so any overlap of two slices hits a stamp
+    # (1 MiB put two in each unit: verify 11.9 -> 7.2 us per admission on MI355X, profiles/r02_stride_ab/)
+    ap.add_argument("--stamp-stride", type=int, default=2 << 20)
     ap.add_argument("--json-out", default="")
     ap.add_argument("--dump-timings", default="",
                     help="write every timed pod's scheduler timeline (CLOCK_MONOTONIC, like the wave's t0) here")

@@ -96,7 +96,8 @@ class LedgerRuntime:
 
 
 class HbmArenaRuntime(LedgerRuntime):
-    def __init__(self, capacities: dict[int, int], stamp_stride: int = 1 << 20, scrub_on_exit: bool = False):
+    def __init__(self, capacities: dict[int, int], stamp_stride: int = ALIGN, scrub_on_exit: bool = False):
+        # default: one stamp per carve unit (every overlap of two slices covers at least one unit start)
         super().__init__(capacities)
         from ..ops import hip  # noqa: PLC0415
 
