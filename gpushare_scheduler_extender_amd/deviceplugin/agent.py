@@ -19,7 +19,10 @@ container env -> the pod runs on the chosen GPU.
 * If the plugin matched a different pod than the one being admitted (two
   pending pods of one size), the allocation goes to the pod the plugin
   committed — the ``gpushare.amd.com/pod`` container annotation names it —
-  and the admitted pod waits for the next Allocate (``stats["mismatch"]``).
+  and the admitted pod waits for the next Allocate.  ``stats["swapped_equivalent"]`` counts swaps between
+  pods with the same allocation (same GPU and partition request, which the extender binds unordered);
+  ``stats["mismatch"]`` counts the others, where a real kubelet would have started a container on another
+  pod's GPU (the ASSUME_TIME ordering of binds exists to keep this at 0).
 * A pod that completes or is deleted is stopped and its slice released; the
   plugin's own informer releases its CU partition.
 
@@ -37,7 +40,7 @@ from ..k8s.client import ApiError, KubeClient
 from ..k8s.informer import Handler, Informer, obj_key
 from ..models import pod as podutil
 from ..models.profile import NamingProfile
-from .allocator import AllocateError
+from .allocator import CU_COUNT_ANNOTATION, AllocateError
 from .devices import UNITS, Device
 from .plugin import POD_ANNOTATION, GpuSharePlugin, PluginClient
 from .runtime import AdmissionError, admit_local
@@ -79,11 +82,16 @@ class NodeAgent:
         self.failed = 0
         self.bad_stamps = 0
         self.latency: list[float] = []  # bound-observed -> Running
-        self.stats = {"allocate_calls": 0, "allocate_errors": 0, "mismatch": 0, "gone_during_allocate": 0,
+        self.stats = {"allocate_calls": 0, "allocate_errors": 0, "mismatch": 0, "swapped_equivalent": 0,
+                      "gone_during_allocate": 0,
                       "allocate_ms_max": 0.0}
         self._bg: set[asyncio.Task] = set()
         self._releasing: set[asyncio.Task] = set()
         self.admit_q: asyncio.Queue = asyncio.Queue()
+        # a pod whose Allocate went to another pod is admitted next, ahead of later arrivals: it was bound before
+        # them, and at the back of the queue it would push every later Allocate one pod off (a cascade a real
+        # kubelet, which never re-queues, does not have)
+        self.admit_first: list[str] = []
         self.start_q: asyncio.Queue = asyncio.Queue()
         self.queued: set[str] = set()
         self.claimed: set[str] = set()  # uids whose allocation is done (starting or running)
@@ -175,7 +183,7 @@ class NodeAgent:
     # ------------------------------------------------------------ admission (serial, like kubelet)
     async def _admission_worker(self):
         while True:
-            key = await self.admit_q.get()
+            key = self.admit_first.pop(0) if self.admit_first else await self.admit_q.get()
             pod = self.pods.get(key)
             if pod is None:
                 continue
@@ -213,14 +221,22 @@ class NodeAgent:
             self.stats["gone_during_allocate"] += 1
             if got.uid != uid and self._alive(uid, key):
                 self.queued.add(uid)
-                self.admit_q.put_nowait(key)
+                self.admit_first.append(key)
             return
         if got.uid != uid:
             # the plugin committed an earlier pod of this size: that pod starts with this allocation, ours
-            # is served by the next Allocate
-            self.stats["mismatch"] += 1
+            # is served by the next Allocate.  Harmless when both pods carry the same allocation (same GPU, same
+            # partition request: the extender leaves such binds unordered); a real kubelet would have started
+            # our container with the other pod's GPU otherwise ("mismatch")
+            want_cus = podutil.annotations(pod).get(CU_COUNT_ANNOTATION, "") or "0"
+            same = (got.dev == podutil.gpu_id_from_annotation(pod, self.profile) and
+                    str(len(got.cus or [])) == str(int(want_cus) if want_cus.isdigit() else want_cus))
+            self.stats["swapped_equivalent" if same else "mismatch"] += 1
+            if not same:
+                log.warning("Allocate for %s (GPU %s) was matched to %s: GPU %s, %d CUs", key,
+                            podutil.gpu_id_from_annotation(pod, self.profile), got.key, got.dev, len(got.cus or []))
             self.queued.add(uid)
-            self.admit_q.put_nowait(key)
+            self.admit_first.append(key)
             key = got.key or key
         self.claimed.add(got.uid)
         if allocs[0].ids:

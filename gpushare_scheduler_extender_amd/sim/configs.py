@@ -136,9 +136,17 @@ class Cluster:
         self.agent_http = HttpClient(next(ch.url for ch in self.children if ch.name == "node-agent"))
         for _ in range(2000):  # the extender has seen the node
             if (await self.inspect()).get("nodes"):
+                break
+            await asyncio.sleep(0.005)
+        else:
+            raise TimeoutError("extender never saw the node")
+        # the node agent (kubelet stand-in) watches the node's pods before any is bound: pods it first met in one
+        # LIST would be admitted in name order rather than in the order their bindings landed
+        for _ in range(6000):
+            if (await self.agent_http.request("GET", "/v1/stats")).status == 200:
                 return
             await asyncio.sleep(0.005)
-        raise TimeoutError("extender never saw the node")
+        raise TimeoutError("node agent never became ready")
 
     async def inspect(self) -> dict:
         r = await self.ext_http.request("GET", "/gpushare-scheduler/inspect")
@@ -148,6 +156,10 @@ class Cluster:
         body = json.dumps({"Pod": pod, "Nodes": None, "NodeNames": [NODE]}).encode()
         r = await self.ext_http.request("POST", "/gpushare-scheduler/filter", body)
         return json.loads(r.body)
+
+    async def agent_stats(self) -> dict:
+        r = await self.agent_http.request("GET", "/v1/stats")
+        return json.loads(r.body) if r.status == 200 else {}
 
     async def allocation(self, uid: str) -> dict:
         r = await self.agent_http.request("GET", f"/v1/allocations/{uid}")
@@ -270,11 +282,16 @@ async def config3(gpu: bool) -> dict:
         used = insp["nodes"][0]["usedGPU"]
         bad = cl.rt.verify() if real else 0
         resident = [st.get("resident") for st in cl.rt.stats()]
-        ok = per_dev == [256] * 8 and used == 256 * 8 and bad == 0
+        # 32 equal-size pods for 8 GPUs of one node: kubelet's Allocate must never be matched to a pod with another
+        # allocation (the extender keeps their binds in ASSUME_TIME order; the plugin matches on ASSUME_TIME)
+        ast = await cl.agent_stats()
+        mismatch = ast.get("mismatch", 0)
+        ok = per_dev == [256] * 8 and used == 256 * 8 and bad == 0 and mismatch == 0
         if real:  # 32 x 64 GiB co-resident in 8 real HBM arenas, 4 slices each
             ok = ok and resident == [4] * 8
         return {"ok": ok, "per_device_gib": per_dev, "device_gib": per, "util_pct": round(100 * used / (8 * per), 2),
-                "real_gpus": real, "resident_slices": resident, "bad_stamps": bad, "seconds": round(dt, 4)}
+                "real_gpus": real, "resident_slices": resident, "bad_stamps": bad, "seconds": round(dt, 4),
+                "allocate_mismatch": mismatch, "allocate_swapped_equivalent": ast.get("swapped_equivalent", 0)}
     finally:
         await cl.close()
 

@@ -269,6 +269,7 @@ class Agent {
       return false;
     }
     for (int i = 0; i < nworkers_; ++i) workers_.emplace_back([this] { worker(); });
+    ready_.store(true);
     return true;
   }
 
@@ -288,6 +289,11 @@ class Agent {
     std::string_view path = req.path();
     std::lock_guard<std::mutex> g(mu_);
     if (req.method == "GET" && path == "/v1/stats") {
+      if (!ready_.load()) {  // as the Python agent: 503 until the pod informer has synced and workers run
+        rep.status = 503;
+        rep.body = "{}";
+        return rep;
+      }
       std::vector<double> lat = latency_;
       std::sort(lat.begin(), lat.end());
       double p50 = lat.empty() ? 0 : lat[lat.size() / 2];
@@ -779,6 +785,7 @@ class Agent {
   std::unordered_map<std::string, int> assign_retries_;  // per pod: ASSIGNED patch attempts (backoff)
   std::atomic<uint64_t> status_retries_{0};
   std::atomic<bool> stop_flag_{false};
+  std::atomic<bool> ready_{false};
   std::vector<double> latency_;
   uint64_t admitted_ = 0, failed_ = 0, bad_ = 0, conflicts_ = 0;
   int added_ = 0;  // work items queued since the last wake_locked()

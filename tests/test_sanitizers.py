@@ -62,7 +62,7 @@ def test_standins_under_tsan(tmp_path):
                         "--only", "2,3,5"], capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider",
-                        "tests/test_chaos.py::test_chaos_whole_stack_converges_without_overcommit[23-native-native]"],
+                        "tests/test_chaos.py::test_chaos_whole_stack_converges_without_overcommit[23-native-native-binding]"],
                        capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout[-3000:]
     reports = sorted(glob.glob(str(logs) + "*"))
