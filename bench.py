@@ -287,6 +287,7 @@ def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
     stats = json.loads(body) if st == 200 else {}
     return {**row, "admit_p50_ms": stats.get("admit_p50_ms"), "allocate_calls": stats.get("allocate_calls"),
             "allocate_errors": stats.get("allocate_errors"), "mismatch": stats.get("mismatch"),
+            "swapped_equivalent": stats.get("swapped_equivalent"),
             "plugin_stats": stats.get("plugin_stats")}
 
 
