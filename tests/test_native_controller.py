@@ -147,9 +147,10 @@ def test_native_controller_rewatch_and_relist_after_410():
             # dropped streams: the reflector re-watches from its last resourceVersion, nothing is lost
             # (the open stream is ended too: drop_watch_after applies to streams started after it is set)
             await e.c.request("POST", "/fake/faults", body={"drop_watch_after": 2, "drop_watches_now": True})
-            for i in range(6):
+            for i in range(6):  # one at a time: each event is flushed on its own, so every 2nd ends a stream
                 await e.c.create("pods", annotated(f"p{i}", 1, i % 2))
-            await settle(lambda: e.used() == [3, 3])
+                await settle(lambda: sum(e.used()) == i + 1)
+            assert e.used() == [3, 3]
             assert e.ctl.stats()["pod_rewatches"] >= 2
             # while no watch is open the pod is deleted; the next watches are told 410 -> LIST + diff
             assert e.ctl.stats()["pod_lists"] == 1
