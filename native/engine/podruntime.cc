@@ -212,9 +212,17 @@ int64_t PodRuntime::admit(const std::string& uid, uint64_t bytes, bool verify, s
     std::vector<Pending*> group;
     group.swap(queue_);
     q.unlock();
-    {
+    try {
       std::lock_guard<std::mutex> g(mu_);
       admit_group_locked(group);
+    } catch (const std::exception& e) {
+      // the group fails, but leadership is handed back below: a throw here must not park every later admission
+      for (Pending* p : group) {
+        if (p->result >= 0 && p->err.empty()) {
+          p->result = -1;
+          p->err = std::string("admission: ") + e.what();
+        }
+      }
     }
     q.lock();
     for (Pending* p : group) p->done = true;
