@@ -496,15 +496,23 @@ void NativeServer::pool_main() {
     }
     std::string resp;
     const bool ka = j.req.keep_alive;
-    if (j.kind == 0) {
-      bool fallback = false;
-      resp = do_bind(j.req, &fallback);
-      if (fallback) {
+    try {
+      if (j.kind == 0) {
+        bool fallback = false;
+        resp = do_bind(j.req, &fallback);
+        if (fallback) {
+          resp = do_proxy(j.req);
+        }
+        stats_.bind_lat.observe(mono() - j.t0);
+      } else {
         resp = do_proxy(j.req);
       }
-      stats_.bind_lat.observe(mono() - j.t0);
-    } else {
-      resp = do_proxy(j.req);
+    } catch (const std::exception& e) {
+      // as in the loop threads: one request that throws must not terminate the extender (a pool thread has no
+      // handler above it); kube-scheduler retries a bind that answers 500
+      stats_.bad_requests.fetch_add(1, std::memory_order_relaxed);
+      std::fprintf(stderr, "[gsx-engine] %s failed: %s\n", j.kind == 0 ? "bind" : "proxied request", e.what());
+      resp = http::response(500, "application/json", error_body(std::string("internal error: ") + e.what()), true);
     }
     complete(j.loop, j.conn_id, std::move(resp), ka);
   }
