@@ -264,33 +264,40 @@ void Reflector::run() {
   };
   while (!stop_.load()) {
     std::string err;
-    if (relist_req_.exchange(false)) need_list = true;
-    if (need_list) {
-      if (!do_list(&err)) {
+    try {
+      if (relist_req_.exchange(false)) need_list = true;
+      if (need_list) {
+        if (!do_list(&err)) {
+          set_error(err);
+          sleep_backoff();
+          continue;
+        }
+        need_list = false;
+        if (!synced_.exchange(true)) {
+          std::lock_guard<std::mutex> g(mu_);
+          cv_.notify_all();
+        }
+      }
+      int r = do_watch(&err);
+      if (stop_.load()) break;
+      if (relist_req_.load()) continue;  // ended on purpose: LIST next
+      if (r == 1) {
+        need_list = true;  // 410 Gone: history compacted past our resourceVersion
+        continue;
+      }
+      if (r < 0) {
         set_error(err);
         sleep_backoff();
         continue;
       }
-      need_list = false;
-      if (!synced_.exchange(true)) {
-        std::lock_guard<std::mutex> g(mu_);
-        cv_.notify_all();
-      }
-    }
-    int r = do_watch(&err);
-    if (stop_.load()) break;
-    if (relist_req_.load()) continue;  // ended on purpose: LIST next
-    if (r == 1) {
-      need_list = true;  // 410 Gone: history compacted past our resourceVersion
-      continue;
-    }
-    if (r < 0) {
-      set_error(err);
+      backoff = 0.05;
+      rewatches_++;
+    } catch (const std::exception& e) {
+      // a handler or a decode that throws must not end the process from this thread: start over from a LIST
+      set_error(std::string("reflector: ") + e.what());
+      need_list = true;
       sleep_backoff();
-      continue;
     }
-    backoff = 0.05;
-    rewatches_++;
   }
 }
 
