@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdio>
 #include <cstring>
 
 namespace gsx {
@@ -131,7 +132,14 @@ void CtlServer::serve_conn(int fd) {
       continue;
     }
     buf.erase(0, static_cast<size_t>(got));
-    Reply rep = h_(req);
+    Reply rep;
+    try {
+      rep = h_(req);
+    } catch (const std::exception& e) {  // a connection thread has no handler above it: answer, do not terminate
+      std::fprintf(stderr, "[gsx-ctl] request failed: %s\n", e.what());
+      rep.status = 500;
+      rep.body = "{\"error\":\"internal error\"}";
+    }
     std::string out = http::response(rep.status, rep.content_type, rep.body, req.keep_alive);
     size_t off = 0;
     while (off < out.size()) {
