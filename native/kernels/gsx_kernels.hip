@@ -53,15 +53,30 @@ __global__ __launch_bounds__(64) void cuprobe_kernel(uint32_t* out, int spin) {
 
 // ------------------------------------------------------------------ HBM stamp / verify / fill
 
-struct Stamp {
+// 16-B aligned: one dwordx4 load / store per stamp.  With 8-B alignment the compiler split each access into two
+// dwordx2, and both halves of a stamp missed L2 together: two DRAM reads per stamp (rocprofv3 PMC,
+// profiles/r02_pmc_admit/)
+struct alignas(16) Stamp {
   uint64_t tag;
   uint64_t off;
 };
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));  // a stamp read as one 16-B vector
+
+typedef const __attribute__((address_space(1))) u64x2* global_stamp_ptr;  // slice addresses are device memory
+
+typedef __attribute__((address_space(1))) u64x2* global_stamp_wptr;
+
+__device__ __forceinline__ u64x2 load_stamp(const char* p) { return *(global_stamp_ptr)(p); }
+__device__ __forceinline__ void store_stamp(char* p, uint64_t tag, uint64_t off) {
+  u64x2 v;
+  v.x = tag;
+  v.y = off;
+  *(global_stamp_wptr)(p) = v;  // one global_store_dwordx4
+}
 
 __global__ __launch_bounds__(256) void stamp_kernel(char* base, uint64_t n, uint64_t stride, uint64_t tag) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
-    Stamp s{tag, i * stride};
-    *reinterpret_cast<Stamp*>(base + i * stride) = s;
+    store_stamp(base + i * stride, tag, i * stride);
   }
 }
 
@@ -69,8 +84,8 @@ __global__ __launch_bounds__(256) void verify_kernel(const char* base, uint64_t 
                                                      unsigned long long* bad) {
   uint32_t mine = 0;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
-    Stamp s = *reinterpret_cast<const Stamp*>(base + i * stride);
-    mine += (s.tag != tag || s.off != i * stride) ? 1u : 0u;
+    const u64x2 s = load_stamp(base + i * stride);
+    mine += (s.x != tag || s.y != i * stride) ? 1u : 0u;
   }
   // wave64 reduction, one atomic per wave
   for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
@@ -90,8 +105,8 @@ __global__ __launch_bounds__(256) void verify_slices_kernel(SliceTable t, uint64
   const char* base = reinterpret_cast<const char*>(sl.addr);
   uint32_t mine = 0;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
-    Stamp st = *reinterpret_cast<const Stamp*>(base + i * stride);
-    mine += (st.tag != sl.tag || st.off != i * stride) ? 1u : 0u;
+    const u64x2 st = load_stamp(base + i * stride);
+    mine += (st.x != sl.tag || st.y != i * stride) ? 1u : 0u;
   }
   for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
   if ((threadIdx.x & 63) == 0 && mine) atomicAdd_system(bad, static_cast<unsigned long long>(mine));
@@ -103,7 +118,7 @@ __global__ __launch_bounds__(256) void stamp_slices_kernel(SliceTable t, uint64_
   const uint64_t n = sl.bytes / stride;
   char* base = reinterpret_cast<char*>(sl.addr);
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
-    *reinterpret_cast<Stamp*>(base + i * stride) = Stamp{sl.tag, i * stride};
+    store_stamp(base + i * stride, sl.tag, i * stride);
   }
 }
 
