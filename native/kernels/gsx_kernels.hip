@@ -122,6 +122,30 @@ __global__ __launch_bounds__(256) void stamp_slices_kernel(SliceTable t, uint64_
   }
 }
 
+// One launch per admission: grid.y rows [0, n_stamp) stamp the new extents, the other rows verify the resident
+// ones.  Only used when the host has checked that no two extents of the table overlap, so the two kinds of block
+// touch disjoint memory and need no ordering between them; with an overlap the two-launch path runs instead, and the
+// verify launch counts the overwritten stamps.
+__global__ __launch_bounds__(256) void admit_slices_kernel(SliceTable t, int n_stamp, uint64_t stride,
+                                                           unsigned long long* bad) {
+  const gsx_slice sl = t.s[blockIdx.y];
+  const uint64_t n = sl.bytes / stride;
+  char* base = reinterpret_cast<char*>(sl.addr);
+  if (static_cast<int>(blockIdx.y) < n_stamp) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+      store_stamp(base + i * stride, sl.tag, i * stride);
+    }
+    return;  // the whole block leaves together: blockIdx.y is uniform
+  }
+  uint32_t mine = 0;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    const u64x2 st = load_stamp(base + i * stride);
+    mine += (st.x != sl.tag || st.y != i * stride) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+  if ((threadIdx.x & 63) == 0 && mine) atomicAdd_system(bad, static_cast<unsigned long long>(mine));
+}
+
 __global__ __launch_bounds__(256) void fill_kernel(uint4* p, uint64_t n16, uint32_t pat) {
   uint4 v = make_uint4(pat, pat, pat, pat);
   uint64_t i = blockIdx.x * 256ull + threadIdx.x;
@@ -364,6 +388,41 @@ int gsx_hbm_admit_n(void* stream, const gsx_slice* slices, int n, int n_stamp, i
     }
     return grid_for(maxn, 256, 1024);
   };
+  // the common case -- one table, new extents disjoint from the resident ones -- is a single launch
+  // (every pair: two new extents that overlap each other must be caught by the verify launch as well)
+  bool disjoint = verify && n > 0 && n <= kMaxSlices;
+  for (int i = 0; disjoint && i < n; ++i) {
+    for (int j = i + 1; j < n; ++j) {
+      const uint64_t a0 = slices[i].addr, a1 = a0 + slices[i].bytes;
+      const uint64_t b0 = slices[j].addr, b1 = b0 + slices[j].bytes;
+      if (a0 < b1 && b0 < a1) {
+        disjoint = false;
+        break;
+      }
+    }
+  }
+  if (disjoint) {
+    int dev = 0;
+    GSX_CHECK(hipGetDevice(&dev));
+    unsigned long long* hc;
+    {
+      std::lock_guard<std::mutex> g(g_mu);
+      if (dev < 0 || dev >= 64) return fail_arg("gsx_hbm_admit_n: device index");
+      if (!g_host_counter[dev]) {
+        GSX_CHECK(hipHostMalloc(reinterpret_cast<void**>(&g_host_counter[dev]), 64, hipHostMallocCoherent));
+      }
+      hc = g_host_counter[dev];
+    }
+    std::lock_guard<std::mutex> dl(g_dev_mu[dev]);
+    __atomic_store_n(hc, 0ull, __ATOMIC_SEQ_CST);
+    SliceTable t;
+    const int gx = table_grid(0, n, &t);
+    hipLaunchKernelGGL(admit_slices_kernel, dim3(gx, t.n), dim3(256), 0, S(stream), t, n_stamp, stride, hc);
+    GSX_CHECK(hipGetLastError());
+    GSX_CHECK(hipStreamSynchronize(S(stream)));
+    *bad = __atomic_load_n(hc, __ATOMIC_SEQ_CST);
+    return 0;
+  }
   for (int base = 0; base < n_stamp; base += kMaxSlices) {
     SliceTable t;
     const int gx = table_grid(base, std::min(kMaxSlices, n_stamp - base), &t);
