@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -388,9 +389,16 @@ int gsx_hbm_admit_n(void* stream, const gsx_slice* slices, int n, int n_stamp, i
     }
     return grid_for(maxn, 256, 1024);
   };
-  // the common case -- one table, new extents disjoint from the resident ones -- is a single launch
+  // one table, extents pairwise disjoint: stamp and verify can share one launch
   // (every pair: two new extents that overlap each other must be caught by the verify launch as well)
-  bool disjoint = verify && n > 0 && n <= kMaxSlices;
+  // opt-in (GSX_ADMIT_ONE_LAUNCH=1): it cuts GPU time per admission (6.5 vs 10.2 us) but not the wall-clock of an
+  // admission, and its kernel-time tail is longer; interleaved A/Bs of the driver's bench showed no gain
+  // (profiles/r02_fused_admit/), so two launches stay the default
+  static const bool one_launch = [] {
+    const char* e = std::getenv("GSX_ADMIT_ONE_LAUNCH");
+    return e && e[0] == '1';
+  }();
+  bool disjoint = one_launch && verify && n > 0 && n <= kMaxSlices;
   for (int i = 0; disjoint && i < n; ++i) {
     for (int j = i + 1; j < n; ++j) {
       const uint64_t a0 = slices[i].addr, a1 = a0 + slices[i].bytes;
