@@ -90,6 +90,18 @@ def test_hbm_admit_n_multi_extent_pods(hip):
     s.destroy()
 
 
+def test_hbm_admit_n_opt_in_single_launch():
+    """``GSX_ADMIT_ONE_LAUNCH=1`` is read once per process, so the check runs in a child
+    (``scripts/experiments/one_launch_check.py``): disjoint extents in one launch, an overlap in two, same counts."""
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a GPU")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GSX_ADMIT_ONE_LAUNCH="1", PYTHONPATH=repo)
+    r = subprocess.run([sys.executable, os.path.join(repo, "scripts", "experiments", "one_launch_check.py")],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=repo)
+    assert r.returncode == 0 and "one-launch ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_hbm_fill_pattern_and_bandwidth(hip):
     s = hip.Stream(0)
     n = 4 << 30
