@@ -195,7 +195,15 @@ class ExtenderServer:
                 # the reference's first call; not ordered: a pod without spec.nodeName is no plugin candidate
                 await self._annotate(pod, ann)
             if self.engine.bind_blocked(seq):
-                await asyncio.get_running_loop().run_in_executor(None, self.engine.bind_wait, seq)
+                # shielded: if this handler is cancelled (server shutdown), the finally below must not run
+                # bind_leave before the executor thread has left bind_wait (use-after-free)
+                fut = asyncio.get_running_loop().run_in_executor(None, self.engine.bind_wait, seq)
+                try:
+                    await asyncio.shield(fut)
+                except asyncio.CancelledError:
+                    self.engine.bind_leave(seq)  # wakes the waiter, which then finds its entry gone
+                    await asyncio.wait_for(asyncio.shield(fut), 5.0)
+                    raise
             if self.bind_mode == "binding":
                 await self._bind_with_annotations(pod, node, ann)
             else:

@@ -12,7 +12,9 @@ Targets (outputs land in ``gpushare_scheduler_extender_amd/_native/``):
                 ROCm-SMI copy bundled inside the torch wheel).
 * ``kernels`` – HIP/CDNA4 kernels for gfx950 (``libgsx_kernels.so``): CU probe,
                 HBM touch/verify, bf16 MFMA GEMM workload, CU-masked streams.
-* ``tools``   – standalone HIP executables (``gsx-cuprobe``).
+* ``tools``   – standalone HIP executables (``gsx-cuprobe``, ``gsx-memprobe``).
+* ``isolate`` – ``libgsx_isolate.so``, the HSA tools library that enforces a pod's CU partition and HBM share
+                inside every HIP/HSA process of the pod, plus its host-only test driver (fake HSA runtime).
 * ``asan``    – host-only sanitizer build of the engine unit test.
 
 Usage: ``python native/build.py [targets...] [--force] [-v]``.
@@ -171,6 +173,27 @@ def build_tools(force: bool = False, verbose: bool = False) -> list[Path]:
     return outs
 
 
+HSA_FLAGS = ["-DAMD_INTERNAL_BUILD", "-I" + str(ROCM / "include"), "-I" + str(ROCM / "include" / "hsa")]
+
+
+def build_isolate(force: bool = False, verbose: bool = False) -> list[Path]:
+    """``libgsx_isolate.so`` (host C++ against the HSA API-table ABI; no HIP, no device code) and
+    ``build/isolate_test`` (the library driven through a fake HSA runtime on the CPU)."""
+    src = NATIVE / "isolate"
+    lib = OUT / "libgsx_isolate.so"
+    deps = [src / "gsx_isolate.cc"]
+    if force or _newer(lib, deps):
+        OUT.mkdir(parents=True, exist_ok=True)
+        _run(["g++", *CXXFLAGS, *HSA_FLAGS, "-shared", str(src / "gsx_isolate.cc"), "-o", str(lib), "-ldl",
+              "-lpthread"], verbose)
+    test = ROOT / "build" / "isolate_test"
+    if force or _newer(test, [src / "isolate_test.cc"]):
+        test.parent.mkdir(parents=True, exist_ok=True)
+        _run(["g++", "-O1", "-g", "-std=c++17", "-Wall", *HSA_FLAGS, str(src / "isolate_test.cc"), "-o", str(test),
+              "-ldl"], verbose)
+    return [lib, test]
+
+
 TEST_MAINS = ("engine_test.cc", "controller_test.cc")
 
 
@@ -231,11 +254,12 @@ TARGETS = {
     "mxdev": build_mxdev,
     "kernels": build_kernels,
     "tools": build_tools,
+    "isolate": build_isolate,
     "asan": build_asan,
     "tsan": build_tsan,
     "tools_tsan": build_tools_tsan,
 }
-DEFAULT = ["engine", "schedsim", "nodeagent", "fakeapi", "mxdev", "kernels", "tools"]
+DEFAULT = ["engine", "schedsim", "nodeagent", "fakeapi", "mxdev", "kernels", "tools", "isolate"]
 
 
 def main(argv: list[str] | None = None) -> int:

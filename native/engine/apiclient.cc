@@ -175,13 +175,29 @@ void ApiClient::release(Conn* c, bool reuse) {
   idle_.push_back(c);
 }
 
+namespace {
+// An SSL call that failed only because a signal interrupted the underlying recv/send: the /debug/pprof stack
+// sampler signals every native thread, and on sockets with SO_RCVTIMEO/SO_SNDTIMEO the kernel never restarts
+// those calls (signal(7)), SA_RESTART or not.  A timeout (EAGAIN) is not retried.
+bool ssl_interrupted(SSL* ssl, int r, int saved_errno) {
+  int e = SSL_get_error(ssl, r);
+  return (e == SSL_ERROR_SYSCALL || e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) && saved_errno == EINTR;
+}
+}  // namespace
+
 bool ApiClient::send_all(Conn* c, const std::string& data) {
   size_t off = 0;
   while (off < data.size()) {
     long w;
     if (c->ssl) {
-      w = SSL_write(c->ssl, data.data() + off, static_cast<int>(data.size() - off));
-      if (w <= 0) return false;
+      errno = 0;
+      int r = SSL_write(c->ssl, data.data() + off, static_cast<int>(data.size() - off));
+      int err = errno;
+      if (r <= 0) {
+        if (ssl_interrupted(c->ssl, r, err)) continue;  // SSL_write must be repeated with the same arguments
+        return false;
+      }
+      w = r;
     } else {
       w = ::send(c->fd, data.data() + off, data.size() - off, MSG_NOSIGNAL);
       if (w < 0) {
@@ -196,8 +212,14 @@ bool ApiClient::send_all(Conn* c, const std::string& data) {
 
 long ApiClient::recv_some(Conn* c, char* buf, size_t n) {
   if (c->ssl) {
-    int r = SSL_read(c->ssl, buf, static_cast<int>(n));
-    return r > 0 ? r : (SSL_get_error(c->ssl, r) == SSL_ERROR_ZERO_RETURN ? 0 : -1);
+    while (true) {
+      errno = 0;
+      int r = SSL_read(c->ssl, buf, static_cast<int>(n));
+      int err = errno;
+      if (r > 0) return r;
+      if (ssl_interrupted(c->ssl, r, err)) continue;
+      return SSL_get_error(c->ssl, r) == SSL_ERROR_ZERO_RETURN ? 0 : -1;
+    }
   }
   while (true) {
     long r = ::recv(c->fd, buf, n, 0);

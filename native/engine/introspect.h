@@ -8,8 +8,10 @@
 //     gdb) so per-thread CPU time can be attributed;
 //   * capture(): a stack sample of any thread of the process.  The requester sends a real-time signal to
 //     the thread (tgkill); its handler records backtrace() into a slot; the requester symbolises outside the
-//     handler (dladdr + demangling).  Handlers are installed with SA_RESTART, so interrupted recv / send /
-//     accept calls resume; epoll_wait returns EINTR, which every loop already tolerates;
+//     handler (dladdr + demangling).  Handlers are installed with SA_RESTART, but that does NOT restart
+//     recv / send on sockets with SO_RCVTIMEO / SO_SNDTIMEO (signal(7)): those return EINTR, and every
+//     caller retries them (plain sockets and SSL_read / SSL_write alike, apiclient.cc); epoll_wait returns
+//     EINTR, which every loop already tolerates;
 //   * ProfiledMutex: the ledger's mutex, counting acquisitions, contended acquisitions, wait and hold time
 //     (the /debug/pprof/mutex and block profiles).
 #pragma once

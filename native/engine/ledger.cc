@@ -278,10 +278,15 @@ bool Ledger::bind_blocked(uint64_t seq) {
 
 void Ledger::bind_wait(uint64_t seq, const std::atomic<bool>* stop) {
   std::unique_lock<std::mutex> o(order_mu_);
-  InflightBind* me = nullptr;
-  for (auto& f : inflight_) {
-    if (f.seq == seq) me = &f;
-  }
+  // the entry is looked up by seq after every wake, never kept across one: bind_leave(seq) may run while we
+  // sleep (a cancelled Python caller's cleanup) and free it; then nobody references our cv any more
+  auto find = [this, seq]() -> InflightBind* {
+    for (auto& f : inflight_) {
+      if (f.seq == seq) return &f;
+    }
+    return nullptr;
+  };
+  InflightBind* me = find();
   if (!me || !blocked_locked(*me)) return;
   order_waits_.fetch_add(1, std::memory_order_relaxed);
   auto t0 = std::chrono::steady_clock::now();
@@ -289,10 +294,15 @@ void Ledger::bind_wait(uint64_t seq, const std::atomic<bool>* stop) {
   // every waiter of the node on every completed bind, and they queued for the extender's CPUs to re-check)
   std::condition_variable cv;
   me->waiter = &cv;
-  while (blocked_locked(*me) && !(stop && stop->load())) {
+  while (true) {
+    me = find();
+    if (me == nullptr) break;  // left while we waited: the entry (and its pointer to cv) is gone
+    if (!blocked_locked(*me) || (stop && stop->load())) {
+      me->waiter = nullptr;
+      break;
+    }
     cv.wait_for(o, std::chrono::milliseconds(100));  // timeout: notice `stop`
   }
-  me->waiter = nullptr;  // still ours: only our own bind_leave() removes the entry
   uint64_t ns = static_cast<uint64_t>(
       std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count());
   order_wait_ns_.fetch_add(ns, std::memory_order_relaxed);
@@ -303,6 +313,10 @@ void Ledger::bind_wait(uint64_t seq, const std::atomic<bool>* stop) {
 
 void Ledger::bind_leave(uint64_t seq) {
   std::lock_guard<std::mutex> o(order_mu_);
+  for (const auto& f : inflight_) {
+    // a waiter still blocked on the entry being removed (its caller gave up): wake it so it sees it is gone
+    if (f.seq == seq && f.waiter) f.waiter->notify_one();
+  }
   inflight_.remove_if([seq](const InflightBind& f) { return f.seq == seq; });
   // notify under order_mu_: a waiter's cv lives on its stack until it has re-taken the mutex
   for (const auto& f : inflight_) {

@@ -1,0 +1,213 @@
+// Host-only test of libgsx_isolate.so against a fake HSA runtime (no GPU, no ROCr).
+//
+// The test plays ROCr: it builds a CoreApiTable / AmdExtTable whose entries are fakes below, calls the
+// library's OnLoad exactly as ROCr's tools loader does, and then calls through the (now hooked) tables.
+// Checked: queues get the pod's CU mask, later set_mask calls are intersected with it, GPU-pool allocations
+// are capped at the share (CPU pools are not), pool size / available memory report the share, frees give
+// bytes back, and the ledger is shared by processes: a forked child sees the parent's bytes, and a dead
+// process's bytes stop counting.
+//
+//   isolate_test <path to libgsx_isolate.so> <scratch dir>
+#include <dlfcn.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_api_trace.h>
+#include <hsa/hsa_ext_amd.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+static int g_fail = 0;
+#define CHECK(c)                                                     \
+  do {                                                               \
+    if (!(c)) {                                                      \
+      std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      ++g_fail;                                                      \
+    }                                                                \
+  } while (0)
+
+constexpr uint64_t GPU_POOL = 1, CPU_POOL = 2, GPU_AGENT = 10, CPU_AGENT = 11;
+constexpr size_t POOL_SIZE = size_t{288} << 30;
+static std::vector<uint32_t> g_last_mask;
+static hsa_queue_t g_queue;
+
+static hsa_status_t fake_queue_create(hsa_agent_t, uint32_t, hsa_queue_type32_t, void (*)(hsa_status_t, hsa_queue_t*, void*),
+                                      void*, uint32_t, uint32_t, hsa_queue_t** q) {
+  *q = &g_queue;
+  g_last_mask.clear();
+  return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t fake_set_mask(const hsa_queue_t*, uint32_t nbits, const uint32_t* m) {
+  g_last_mask.assign(m, m + (nbits + 31) / 32);
+  return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t fake_pool_get_info(hsa_amd_memory_pool_t p, hsa_amd_memory_pool_info_t a, void* v) {
+  switch (a) {
+    case HSA_AMD_MEMORY_POOL_INFO_SEGMENT: *static_cast<hsa_amd_segment_t*>(v) = HSA_AMD_SEGMENT_GLOBAL; break;
+    case HSA_AMD_MEMORY_POOL_INFO_LOCATION:
+      *static_cast<hsa_amd_memory_pool_location_t*>(v) =
+          p.handle == GPU_POOL ? HSA_AMD_MEMORY_POOL_LOCATION_GPU : HSA_AMD_MEMORY_POOL_LOCATION_CPU;
+      break;
+    case HSA_AMD_MEMORY_POOL_INFO_SIZE: *static_cast<size_t*>(v) = POOL_SIZE; break;
+    default: return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t fake_pool_allocate(hsa_amd_memory_pool_t, size_t size, uint32_t, void** ptr) {
+  *ptr = std::malloc(16);  // a unique address stands in for the device allocation
+  return *ptr ? HSA_STATUS_SUCCESS : HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+}
+static hsa_status_t fake_pool_free(void* p) {
+  std::free(p);
+  return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t fake_agent_get_info(hsa_agent_t a, hsa_agent_info_t attr, void* v) {
+  if (attr == HSA_AGENT_INFO_DEVICE) {
+    *static_cast<hsa_device_type_t*>(v) = a.handle == GPU_AGENT ? HSA_DEVICE_TYPE_GPU : HSA_DEVICE_TYPE_CPU;
+    return HSA_STATUS_SUCCESS;
+  }
+  if (static_cast<int>(attr) == static_cast<int>(HSA_AMD_AGENT_INFO_MEMORY_AVAIL)) {
+    *static_cast<uint64_t*>(v) = POOL_SIZE;
+    return HSA_STATUS_SUCCESS;
+  }
+  return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+}
+
+static CoreApiTable core;
+static AmdExtTable amd;
+
+static hsa_status_t alloc(uint64_t pool, size_t gib, void** p) {
+  return amd.hsa_amd_memory_pool_allocate_fn(hsa_amd_memory_pool_t{pool}, gib << 30, 0, p);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) return 2;
+  std::string dir = argv[2];
+  std::string conf = dir + "/isolation.conf", ledger = dir + "/hbm.ledger";
+  FILE* f = std::fopen(conf.c_str(), "w");
+  // 32 CUs: CUs 0-7 of every other 32-CU block
+  std::fprintf(f, "# written by the device plugin\ncu_mask=0x000000ff,0x00000000,0x000000ff,0x00000000,"
+                  "0x000000ff,0x00000000,0x000000ff,0x00000000\nhbm_limit_bytes=%llu\nledger=%s\n",
+               static_cast<unsigned long long>(size_t{100} << 30), ledger.c_str());
+  std::fclose(f);
+  setenv("GSX_ISOLATION_CONFIG", conf.c_str(), 1);
+  unsetenv("HSA_TOOLS_LIB");
+
+  void* h = dlopen(argv[1], RTLD_NOW);
+  if (!h) {
+    std::fprintf(stderr, "dlopen: %s\n", dlerror());
+    return 1;
+  }
+  // the preload constructor put the library into HSA_TOOLS_LIB
+  const char* tl = std::getenv("HSA_TOOLS_LIB");
+  CHECK(tl != nullptr && std::strstr(tl, "gsx_isolate") != nullptr);
+
+  std::memset(&core, 0, sizeof core);
+  std::memset(&amd, 0, sizeof amd);
+  core.version.minor_id = sizeof(CoreApiTable);
+  amd.version.minor_id = sizeof(AmdExtTable);
+  core.hsa_queue_create_fn = fake_queue_create;
+  core.hsa_agent_get_info_fn = fake_agent_get_info;
+  amd.hsa_amd_queue_cu_set_mask_fn = fake_set_mask;
+  amd.hsa_amd_memory_pool_get_info_fn = fake_pool_get_info;
+  amd.hsa_amd_memory_pool_allocate_fn = fake_pool_allocate;
+  amd.hsa_amd_memory_pool_free_fn = fake_pool_free;
+  HsaApiTable table;
+  std::memset(&table, 0, sizeof table);
+  table.core_ = &core;
+  table.amd_ext_ = &amd;
+  auto onload = reinterpret_cast<bool (*)(HsaApiTable*, uint64_t, uint64_t, const char* const*)>(dlsym(h, "OnLoad"));
+  auto stats = reinterpret_cast<void (*)(uint64_t*)>(dlsym(h, "gsx_isolate_stats"));
+  CHECK(onload && stats);
+  CHECK(onload(&table, 3, 0, nullptr));
+  CHECK(core.hsa_queue_create_fn != fake_queue_create);
+
+  // ---- CU partition
+  hsa_queue_t* q = nullptr;
+  CHECK(core.hsa_queue_create_fn(hsa_agent_t{GPU_AGENT}, 1024, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0, &q) ==
+        HSA_STATUS_SUCCESS);
+  CHECK(g_last_mask.size() == 8 && g_last_mask[0] == 0xff && g_last_mask[1] == 0 && g_last_mask[6] == 0xff);
+  std::vector<uint32_t> all(8, 0xffffffffu);
+  // "all CUs": stays inside the partition, and succeeds (HIP fails a stream on any other status)
+  CHECK(amd.hsa_amd_queue_cu_set_mask_fn(q, 256, all.data()) == HSA_STATUS_SUCCESS);
+  CHECK(g_last_mask.size() == 8 && g_last_mask[0] == 0xff && g_last_mask[1] == 0);
+  CHECK(amd.hsa_amd_queue_cu_set_mask_fn(q, 0, nullptr) == HSA_STATUS_SUCCESS);  // reset: the partition again
+  CHECK(g_last_mask[0] == 0xff && g_last_mask[2] == 0xff);
+  std::vector<uint32_t> narrow(8, 0);
+  narrow[0] = 0x0f;  // a narrower request inside the partition is honoured as is
+  CHECK(amd.hsa_amd_queue_cu_set_mask_fn(q, 256, narrow.data()) == HSA_STATUS_SUCCESS);
+  CHECK(g_last_mask[0] == 0x0f && g_last_mask[2] == 0);
+  std::vector<uint32_t> outside(8, 0);
+  outside[1] = 0xff;  // entirely outside: keeps the partition
+  amd.hsa_amd_queue_cu_set_mask_fn(q, 256, outside.data());
+  CHECK(g_last_mask[0] == 0xff && g_last_mask[1] == 0);
+
+  // ---- HBM share
+  size_t sz = 0;
+  CHECK(amd.hsa_amd_memory_pool_get_info_fn(hsa_amd_memory_pool_t{GPU_POOL}, HSA_AMD_MEMORY_POOL_INFO_SIZE, &sz) ==
+        HSA_STATUS_SUCCESS);
+  CHECK(sz == size_t{100} << 30);
+  CHECK(amd.hsa_amd_memory_pool_get_info_fn(hsa_amd_memory_pool_t{CPU_POOL}, HSA_AMD_MEMORY_POOL_INFO_SIZE, &sz) ==
+        HSA_STATUS_SUCCESS);
+  CHECK(sz == POOL_SIZE);
+  void *a = nullptr, *b = nullptr, *c = nullptr, *big = nullptr;
+  CHECK(alloc(GPU_POOL, 60, &a) == HSA_STATUS_SUCCESS);
+  CHECK(alloc(GPU_POOL, 50, &b) == HSA_STATUS_ERROR_OUT_OF_RESOURCES);  // 110 > 100
+  CHECK(alloc(CPU_POOL, 500, &big) == HSA_STATUS_SUCCESS);             // host memory is not the share
+  uint64_t avail = 0;
+  CHECK(core.hsa_agent_get_info_fn(hsa_agent_t{GPU_AGENT}, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_MEMORY_AVAIL),
+                                   &avail) == HSA_STATUS_SUCCESS);
+  CHECK(avail == uint64_t{40} << 30);
+  CHECK(alloc(GPU_POOL, 40, &c) == HSA_STATUS_SUCCESS);  // exactly the share
+  CHECK(amd.hsa_amd_memory_pool_free_fn(c) == HSA_STATUS_SUCCESS);
+
+  // ---- the ledger is per pod: a forked child sees the parent's 60 GiB
+  pid_t pid = fork();
+  if (pid == 0) {
+    void *x = nullptr, *y = nullptr;
+    int bad = 0;
+    if (alloc(GPU_POOL, 50, &x) != HSA_STATUS_ERROR_OUT_OF_RESOURCES) bad |= 1;  // 60 + 50 > 100
+    if (alloc(GPU_POOL, 30, &y) != HSA_STATUS_SUCCESS) bad |= 2;                 // 60 + 30 fits
+    _exit(bad);  // dies holding 30 GiB: its slot stops counting with it
+  }
+  int st = 0;
+  waitpid(pid, &st, 0);
+  CHECK(WIFEXITED(st) && WEXITSTATUS(st) == 0);
+  void* d = nullptr;
+  CHECK(alloc(GPU_POOL, 40, &d) == HSA_STATUS_SUCCESS);  // the dead child's 30 GiB are not held against us
+
+  // a second, independent process of the same pod (another container: same ledger file, new process)
+  int up[2], down[2];  // child -> parent, parent -> child
+  CHECK(pipe(up) == 0 && pipe(down) == 0);
+  pid = fork();
+  if (pid == 0) {
+    // parent holds 100 of 100 now: nothing fits until it frees
+    void* x = nullptr;
+    int bad = alloc(GPU_POOL, 1, &x) == HSA_STATUS_ERROR_OUT_OF_RESOURCES ? 0 : 1;
+    char ch;
+    if (write(up[1], "r", 1) != 1) bad |= 4;
+    if (read(down[0], &ch, 1) != 1) bad |= 8;  // parent freed 40
+    if (alloc(GPU_POOL, 40, &x) != HSA_STATUS_SUCCESS) bad |= 2;
+    _exit(bad);
+  }
+  char ch;
+  CHECK(read(up[0], &ch, 1) == 1);
+  CHECK(amd.hsa_amd_memory_pool_free_fn(d) == HSA_STATUS_SUCCESS);
+  CHECK(write(down[1], "g", 1) == 1);
+  waitpid(pid, &st, 0);
+  CHECK(WIFEXITED(st) && WEXITSTATUS(st) == 0);
+
+  uint64_t sv[5];
+  stats(sv);
+  CHECK(sv[0] == 1 && sv[2] >= 1 && sv[3] == uint64_t{60} << 30 && sv[4] == 2);
+  CHECK(amd.hsa_amd_memory_pool_free_fn(a) == HSA_STATUS_SUCCESS);
+  stats(sv);
+  CHECK(sv[3] == 0);
+  amd.hsa_amd_memory_pool_free_fn(big);
+  if (g_fail == 0) std::printf("isolate_test: OK\n");
+  return g_fail ? 1 : 0;
+}

@@ -1,12 +1,12 @@
 // gsx-cuprobe: which compute units does a (CU-masked) queue actually use?
 //
-//   gsx-cuprobe [--device N] [--mask 0-63,128-191] [--blocks 8192] [--spin 20000]
+//   gsx-cuprobe [--device N] [--mask 0-63,128-191] [--blocks 8192] [--spin 20000] [--list]
 //
 // Launches the probe kernel (every workgroup records s_getreg HW_ID / XCC_ID)
 // on a stream created with hipExtStreamCreateWithCUMask (or a plain stream,
 // which still honours a process-wide HSA_CU_MASK), and prints one JSON line:
 // distinct physical CUs in total and per XCD.  Operators run it inside a pod
-// to check the partition the device plugin handed out.
+// to check the partition the device plugin handed out; --list adds every CU as [xcc,se,sh,cu].
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -40,13 +40,15 @@ static std::vector<uint32_t> parse_mask(const char* s, int cus) {
 int main(int argc, char** argv) {
   int dev = 0, blocks = 8192, spin = 20000;
   const char* mask = nullptr;
+  bool list = false;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--device") && i + 1 < argc) dev = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--mask") && i + 1 < argc) mask = argv[++i];
     else if (!std::strcmp(argv[i], "--blocks") && i + 1 < argc) blocks = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--spin") && i + 1 < argc) spin = std::atoi(argv[++i]);
+    else if (!std::strcmp(argv[i], "--list")) list = true;
     else {
-      std::fprintf(stderr, "usage: %s [--device N] [--mask LIST] [--blocks N] [--spin N]\n", argv[0]);
+      std::fprintf(stderr, "usage: %s [--device N] [--mask LIST] [--blocks N] [--spin N] [--list]\n", argv[0]);
       return 2;
     }
   }
@@ -80,7 +82,17 @@ int main(int argc, char** argv) {
               dev, info.arch, info.cu_count, mask ? mask : "", std::getenv("HSA_CU_MASK") ? std::getenv("HSA_CU_MASK") : "",
               cus.size());
   for (int x = 0; x < 8; ++x) std::printf("%s%zu", x ? "," : "", per_xcc[static_cast<size_t>(x)].size());
-  std::printf("]}\n");
+  std::printf("]");
+  if (list) {
+    std::printf(",\"cus\":[");
+    bool first = true;
+    for (const auto& t : cus) {
+      std::printf("%s[%d,%d,%d,%d]", first ? "" : ",", std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t));
+      first = false;
+    }
+    std::printf("]");
+  }
+  std::printf("}\n");
   gsx_stream_destroy(stream);
   return 0;
 }

@@ -418,3 +418,35 @@ def test_prioritize_binpack_first_across_nodes():
     assert scores == {"tight": 10, "loose": 3, "full": 0, "cpu": 0, "ghost": 0}
     assert list(out[0]) == ["Host", "Score"]
     assert json.loads(eng.prioritize(b"junk")) == []
+
+
+def test_bind_wait_returns_when_its_own_entry_is_left():
+    """a cancelled Python bind calls bind_leave(seq) while its executor thread still sits in
+    bind_wait(seq); the waiter must notice the entry is gone (no dangling pointer into the freed list node)."""
+    import threading
+
+    eng = new_engine()
+    eng.upsert_node("n", 20, 2)
+    d1, _, s1, _ = eng.assume_ordered("u1", "d", "a", "n", 10, "")
+    d2, _, s2, _ = eng.assume_ordered("u2", "d", "b", "n", 10, "")
+    assert d1 != d2 and eng.bind_blocked(s2)  # equal size, other GPU: ordered behind the first
+    done = threading.Event()
+    t = threading.Thread(target=lambda: (eng.bind_wait(s2), done.set()))
+    t.start()
+    time.sleep(0.05)
+    assert not done.is_set()
+    eng.bind_leave(s2)  # the cancelled caller's cleanup
+    assert done.wait(2.0), "bind_wait did not return after its entry was removed"
+    t.join()
+    eng.bind_leave(s1)
+    # and the normal path: a blocked bind is released by the earlier bind's completion
+    _, _, s3, _ = eng.assume_ordered("u3", "d", "c", "n", 5, "")
+    _, _, s4, _ = eng.assume_ordered("u4", "d", "e", "n", 5, "")
+    if eng.bind_blocked(s4):
+        done.clear()
+        t = threading.Thread(target=lambda: (eng.bind_wait(s4), done.set()))
+        t.start()
+        eng.bind_leave(s3)
+        assert done.wait(2.0)
+        t.join()
+    eng.bind_leave(s4)

@@ -1,0 +1,125 @@
+"""Enforced isolation on a real MI355X (VERDICT r2 "what's missing" #2): a plain HIP program that never sees
+``HSA_CU_MASK`` still runs on exactly its 64-CU partition, and allocating past its HBM share fails.
+
+Every pod environment here is produced by the device plugin's :class:`IsolationManager` for a host-process
+launcher (``HSA_TOOLS_LIB`` + ``GSX_ISOLATION_CONFIG``; in a container the same files arrive as read-only
+mounts and ``/etc/ld.so.preload``).  The programs are the compiled probes ``gsx-cuprobe`` (hardware CU id of
+every workgroup) and ``gsx-memprobe`` (hipMalloc / hipMemGetInfo), and PyTorch itself.
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+from gpushare_scheduler_extender_amd.deviceplugin.allocator import CUPartitioner
+from gpushare_scheduler_extender_amd.deviceplugin.isolation import IsolationManager
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+NATIVE = ROOT / "gpushare_scheduler_extender_amd" / "_native"
+GIB = 1 << 30
+
+
+def _env(extra: dict) -> dict:
+    env = {k: v for k, v in os.environ.items() if k not in ("HSA_CU_MASK", "GSX_CU_MASK", "HSA_TOOLS_LIB")}
+    env.update(extra)
+    return env
+
+
+def _run(cmd, env, timeout=120) -> dict:
+    r = subprocess.run([str(c) for c in cmd], env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, (cmd, r.returncode, r.stderr[-2000:])
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.fixture
+def iso(tmp_path):
+    lib = NATIVE / "libgsx_isolate.so"
+    if not lib.exists():
+        pytest.fail("libgsx_isolate.so not built: python native/build.py isolate")
+    return IsolationManager(str(tmp_path / "iso"))
+
+
+def _cus(out: dict) -> set:
+    return {tuple(c) for c in out["cus"]}
+
+
+def test_cu_partition_is_enforced_without_hsa_cu_mask(iso):
+    """Config 5 through the isolation library: four 64-CU pods, each probe process with HSA_CU_MASK unset."""
+    probe = NATIVE / "gsx-cuprobe"
+    full = _run([probe, "--list"], _env({}))
+    assert full["distinct_cus"] == 256
+    part = CUPartitioner(256, 8)
+    sets = []
+    for i in range(4):
+        cus = part.allocate(f"pod-{i}", 64)
+        _, env = iso.prepare(f"pod-{i}", cus, 256, 8 * GIB, host_process=True)
+        out = _run([probe, "--list"], _env(env))
+        assert out["hsa_cu_mask"] == ""
+        assert out["distinct_cus"] == 64, out
+        assert out["per_xcd"] == [8] * 8, out  # the partitioner's 8 CUs on each XCD
+        sets.append(_cus(out))
+    assert all(not (sets[i] & sets[j]) for i in range(4) for j in range(i + 1, 4))
+    # a stream that asks for all 256 CUs (hipExtStreamCreateWithCUMask) stays inside the partition
+    _, env0 = iso.prepare("pod-0", part.held()["pod-0"], 256, 8 * GIB, host_process=True)
+    wide = _run([probe, "--mask", "0-255", "--list"], _env(env0))
+    assert wide["distinct_cus"] == 64 and _cus(wide) == sets[0]
+    # an HSA_CU_MASK the container sets for itself cannot widen it either
+    env0b = dict(env0, HSA_CU_MASK="0:0-255")
+    assert _run([probe, "--list"], _env(env0b))["distinct_cus"] == 64
+
+
+def test_hbm_share_is_enforced_for_a_hip_program(iso):
+    probe = NATIVE / "gsx-memprobe"
+    share = 8 * GIB
+    _, env = iso.prepare("mem-0", None, 256, share, host_process=True)
+    out = _run([probe, "--alloc", f"{6 * GIB},{3 * GIB},{GIB}", "--touch"], _env(env))
+    assert out["total"] == share, out  # hipMemGetInfo reports the share as the device size
+    assert out["free"] <= share
+    assert [a["ok"] for a in out["allocs"]] == [True, False, True], out
+    assert out["allocs"][1]["err"] == "hipErrorOutOfMemory"
+    over = _run([probe, "--alloc", str(share + GIB)], _env(env))
+    assert over["allocs"][0]["ok"] is False
+    free_ = _run([probe, "--alloc", str(share + GIB)], _env({}))  # unconfined control: the whole GPU
+    assert free_["total"] > 200 * GIB and free_["allocs"][0]["ok"] is True
+
+
+def test_hbm_share_is_per_pod_across_processes(iso):
+    """Two processes of one pod share one account; a process that exits gives its bytes back."""
+    probe = NATIVE / "gsx-memprobe"
+    _, env = iso.prepare("mem-1", None, 256, 8 * GIB, host_process=True)
+    holder = subprocess.Popen([str(probe), "--alloc", str(6 * GIB), "--touch", "--hold-ms", "20000"], env=_env(env),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        first = json.loads(holder.stdout.readline())  # printed once the 6 GiB are held
+        assert first["allocs"][0]["ok"] is True
+        other = _run([probe, "--alloc", f"{3 * GIB},{GIB}"], _env(env))
+        assert [a["ok"] for a in other["allocs"]] == [False, True], other
+        assert other["total"] == 8 * GIB and other["free"] <= 2 * GIB + (64 << 20)
+    finally:
+        holder.kill()
+        holder.wait(30)
+    after = _run([probe, "--alloc", str(6 * GIB)], _env(env))
+    assert after["allocs"][0]["ok"] is True, after
+
+
+def test_pytorch_sees_and_respects_the_share(iso):
+    share = 16 * GIB
+    _, env = iso.prepare("torch-0", None, 256, share, host_process=True)
+    code = (
+        "import json,torch\n"
+        "free,total=torch.cuda.mem_get_info()\n"
+        "props=torch.cuda.get_device_properties(0).total_memory\n"
+        "x=torch.empty(8<<30,dtype=torch.uint8,device='cuda'); x.fill_(1); torch.cuda.synchronize()\n"
+        "try:\n"
+        "    y=torch.empty(12<<30,dtype=torch.uint8,device='cuda'); oom=False\n"
+        "except torch.OutOfMemoryError:\n"
+        "    oom=True\n"
+        "print(json.dumps({'free':free,'total':total,'props':props,'oom':oom,'sum':int(x[:1024].sum())}))\n")
+    out = _run([sys.executable, "-c", code], _env(env), timeout=300)
+    assert out["total"] == share and out["props"] == share, out
+    assert out["oom"] is True and out["sum"] == 1024
