@@ -87,6 +87,8 @@ class Controller:
             enqueue = True
         elif state == 1 and podutil.gpu_id_from_annotation(new, self.profile) != _dev:
             enqueue = True  # device index rewritten: re-account
+        elif state != 0 and podutil.hold_idx(new) != podutil.hold_idx(old):
+            enqueue = True  # the device plugin's reconciliation set / cleared a hold (charged on two devices)
         if enqueue:
             if raw is not None:
                 self._raw[key] = raw

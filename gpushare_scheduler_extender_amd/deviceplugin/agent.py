@@ -23,6 +23,11 @@ container env -> the pod runs on the chosen GPU.
   pods with the same allocation (same GPU and partition request, which the extender binds unordered);
   ``stats["mismatch"]`` counts the others, where a real kubelet would have started a container on another
   pod's GPU (the ASSUME_TIME ordering of binds exists to keep this at 0).
+* ``faithful=True`` plays kubelet as it is, not as the protocol would like it: the container of the pod
+  being admitted starts with whatever allocation the plugin returned (no re-routing), pods met together are
+  admitted as one batch sorted by creationTimestamp (kubelet's ``HandlePodAdditions``), and kubelet's record
+  of device IDs per container is served on the PodResources API (:mod:`.podresources`), which the plugin
+  reconciles against (:mod:`.reconcile`).  ``/v1/allocations/<uid>`` is then the container's real env.
 * A pod that completes or is deleted is stopped and its slice released; the
   plugin's own informer releases its CU partition.
 
@@ -58,7 +63,8 @@ class _Alloc:
 class NodeAgent:
     def __init__(self, client: KubeClient, node: str, devices: list[Device], profile: NamingProfile, runtime, *,
                  unit: str = "GiB", verify_each: bool = True, mount_mode: str = "isolated", report_status: bool = True,
-                 workers: int = 8, plugin: GpuSharePlugin | None = None, plugin_socket: str | None = None):
+                 workers: int = 8, plugin: GpuSharePlugin | None = None, plugin_socket: str | None = None,
+                 faithful: bool = False, batch_window: float = 0.0, podresources_socket: str | None = None):
         self.client = client
         self.node = node
         self.devices = {d.index: d for d in devices}
@@ -97,9 +103,19 @@ class NodeAgent:
         self.claimed: set[str] = set()  # uids whose allocation is done (starting or running)
         self.seen: dict[str, float] = {}
         self.workers = workers
+        self.faithful = faithful
+        self.batch_window = batch_window
+        self._held_starts: list | None = None
+        self._last_of_batch = False
         # kubelet's device-ID accounting (gRPC mode): all plugin IDs, and the ones each pod holds
         self.all_ids: list[str] = []
         self.used_ids: dict[str, list[str]] = {}
+        self.id_keys: dict[str, str] = {}  # uid -> ns/name of the pod holding used_ids[uid]
+        self.prserver = None
+        if podresources_socket:
+            from .podresources import PodResourcesServer  # noqa: PLC0415
+
+            self.prserver = PodResourcesServer(podresources_socket, self._pod_resources)
         self.pods.add_handler(Handler(self._on_pod, lambda o, n, r: self._on_pod(n, r), self._on_delete))
 
     # ------------------------------------------------------------ pod watch (kubelet's pod config source)
@@ -126,9 +142,19 @@ class NodeAgent:
     def _on_delete(self, pod: dict, raw):
         self._stop(podutil.meta(pod).get("uid", ""))
 
+    def _pod_resources(self):
+        """kubelet's podresources view: every pod holding device IDs, one container each."""
+        out = []
+        for uid, ids in self.used_ids.items():
+            key = self.id_keys.get(uid, "")
+            ns, _, name = key.partition("/")
+            out.append((ns, name, [("main", self.profile.resource, ids)]))
+        return out
+
     def _stop(self, uid: str):
         self.claimed.discard(uid)
         self.used_ids.pop(uid, None)
+        self.id_keys.pop(uid, None)
         if self.running.pop(uid, None) is not None:
             self._release(uid)
 
@@ -181,9 +207,40 @@ class NodeAgent:
             self.stats["allocate_ms_max"] = max(self.stats["allocate_ms_max"], 1e3 * (time.perf_counter() - t0))
 
     # ------------------------------------------------------------ admission (serial, like kubelet)
+    async def _next_batch(self) -> list[str]:
+        """kubelet's HandlePodAdditions: the pods it meets together, sorted by creationTimestamp."""
+        keys = [await self.admit_q.get()]
+        await asyncio.sleep(self.batch_window)
+        while not self.admit_q.empty():
+            keys.append(self.admit_q.get_nowait())
+
+        def created(k):
+            p = self.pods.get(k) or {}
+            return (podutil.meta(p).get("creationTimestamp", ""), k)
+        return sorted(keys, key=created)
+
+    def _flush_starts(self):
+        held, self._held_starts = self._held_starts, None
+        for item in held or []:
+            self.start_q.put_nowait(item)
+
     async def _admission_worker(self):
+        batch: list[str] = []
         while True:
-            key = self.admit_first.pop(0) if self.admit_first else await self.admit_q.get()
+            if self.admit_first:
+                key = self.admit_first.pop(0)
+            elif self.batch_window > 0:
+                if not batch:
+                    self._flush_starts()
+                    batch = await self._next_batch()
+                    # kubelet admits the whole batch (every Allocate) in one pass of HandlePodAdditions; its pod
+                    # workers start containers later (image pulls, runtime calls): starts wait for the batch
+                    self._held_starts = []
+                key = batch.pop(0)
+                if not batch:
+                    self._last_of_batch = True
+            else:
+                key = await self.admit_q.get()
             pod = self.pods.get(key)
             if pod is None:
                 continue
@@ -195,6 +252,10 @@ class NodeAgent:
                 await self._admit(key, pod, uid)
             except Exception as e:  # noqa: BLE001
                 log.exception("admit %s: %r", key, e)
+            finally:
+                if self._last_of_batch:
+                    self._last_of_batch = False
+                    self._flush_starts()
 
     async def _admit(self, key: str, pod: dict, uid: str):
         conts = [podutil.container_limit(c, self.profile.resource) for c in (pod.get("spec") or {}).get("containers") or []]
@@ -223,7 +284,18 @@ class NodeAgent:
                 self.queued.add(uid)
                 self.admit_first.append(key)
             return
-        if got.uid != uid:
+        if got.uid != uid and self.faithful:
+            # a real kubelet: our container starts with this allocation, whichever pod it was built for
+            want_cus = podutil.annotations(pod).get(CU_COUNT_ANNOTATION, "") or "0"
+            same = (got.dev == podutil.gpu_id_from_annotation(pod, self.profile) and
+                    str(len(got.cus or [])) == str(int(want_cus) if want_cus.isdigit() else want_cus))
+            self.stats["swapped_equivalent" if same else "mismatch"] += 1
+            if not same:
+                log.warning("kubelet starts %s (annotated GPU %s) with the allocation built for %s: GPU %s",
+                            key, podutil.gpu_id_from_annotation(pod, self.profile), got.key, got.dev)
+            got = _Alloc(uid, key, got.dev, got.envs, got.cus, got.ids)
+            allocs[0] = got
+        elif got.uid != uid:
             # the plugin committed an earlier pod of this size: that pod starts with this allocation, ours
             # is served by the next Allocate.  Harmless when both pods carry the same allocation (same GPU, same
             # partition request: the extender leaves such binds unordered); a real kubelet would have started
@@ -241,8 +313,12 @@ class NodeAgent:
         self.claimed.add(got.uid)
         if allocs[0].ids:
             self.used_ids[got.uid] = [i for a in allocs for i in a.ids]
+            self.id_keys[got.uid] = got.key or key
         self.allocations[got.uid] = got.envs
-        self.start_q.put_nowait((got.uid, key, allocs))
+        if self._held_starts is not None:
+            self._held_starts.append((got.uid, key, allocs))
+        else:
+            self.start_q.put_nowait((got.uid, key, allocs))
 
     # ------------------------------------------------------------ container start (per-pod workers)
     async def _admit_runtime(self, uid: str, dev: int, nbytes: int, cus) -> int:
@@ -314,6 +390,8 @@ class NodeAgent:
     # ------------------------------------------------------------ lifecycle
     async def start(self):
         loop = asyncio.get_running_loop()
+        if self.prserver is not None:
+            await self.prserver.start()
         if self.pclient is not None:
             stream = self.pclient.list_and_watch()
             first = await asyncio.wait_for(stream.read(), 30)
@@ -334,6 +412,8 @@ class NodeAgent:
             await self.plugin.stop()
         if self.pclient is not None:
             await self.pclient.close()
+        if self.prserver is not None:
+            await self.prserver.stop()
         await self.pods.stop()
 
 
@@ -384,6 +464,10 @@ async def serve_stats(box: dict, host: str = "127.0.0.1", port: int = 0):
                 "plugin": "grpc" if agent.pclient is not None else "inproc"}
         if agent.plugin is not None:
             body["plugin_stats"] = dict(agent.plugin.stats)
+            rc = getattr(agent.plugin, "reconciler", None)
+            if rc is not None:
+                body["reconcile"] = dict(rc.stats)
+        body["faithful"] = agent.faithful
         return web.Response(text=json.dumps(body), content_type="application/json")
 
     async def allocation(request):
@@ -429,6 +513,12 @@ def main(argv=None) -> int:
     ap.add_argument("--plugin", default="grpc", choices=["grpc", "inproc"])
     ap.add_argument("--socket-dir", default="")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--faithful", action="store_true",
+                    help="kubelet as it is: no re-routing of a mismatched Allocate, creationTimestamp-sorted batches, "
+                         "PodResources API served for the plugin's reconciliation")
+    ap.add_argument("--batch-window", type=float, default=-1.0,
+                    help="seconds kubelet collects pods into one admission batch (default 0.02 with --faithful)")
+    ap.add_argument("--no-reconcile", action="store_true", help="the plugin does not reconcile with PodResources")
     ap.add_argument("--port-file", default="")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.WARNING)
@@ -445,12 +535,18 @@ def main(argv=None) -> int:
         rt = RemoteRuntime(eps)
         profile = get_profile(a.profile)
         plugin = None
+        sock_dir = a.socket_dir or tempfile.mkdtemp(prefix="gsx-dp-")
+        prsock = os.path.join(sock_dir, "pod-resources", "kubelet.sock") if a.faithful else None
+        window = a.batch_window if a.batch_window >= 0 else (0.02 if a.faithful else 0.0)
         if a.plugin == "grpc":
             plugin = GpuSharePlugin(KubeClient(KubeConfig.auto(a.kubeconfig, a.apiserver)), a.node, devs, profile,
-                                    unit=a.unit, socket_dir=a.socket_dir or tempfile.mkdtemp(prefix="gsx-dp-"))
+                                    unit=a.unit, socket_dir=sock_dir,
+                                    podresources_socket=None if a.no_reconcile else prsock,
+                                    reconcile_interval=0.5)
             await plugin.start(register=False, publish=False)
             agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
-                              workers=a.workers, plugin_socket=plugin.socket_path)
+                              workers=a.workers, plugin_socket=plugin.socket_path, faithful=a.faithful,
+                              batch_window=window, podresources_socket=prsock)
         else:
             agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
                               workers=a.workers)

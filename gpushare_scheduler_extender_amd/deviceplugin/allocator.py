@@ -42,7 +42,8 @@ class ContainerAllocation:
     envs: dict[str, str]
     devices: list[dict]  # {container_path, host_path, permissions}
     annotations: dict[str, str] = field(default_factory=dict)
-    mounts: list[dict] = field(default_factory=list)
+    mounts: list[dict] = field(default_factory=list)  # {container_path, host_path, read_only}
+    iso: str = ""  # the isolation directory key (pod UID) its mounts point at
 
 
 class AllocateError(Exception):
@@ -108,6 +109,18 @@ class CUPartitioner:
         if got:
             self._held[uid] = sorted(set(self._held.get(uid, [])) | set(got))
         return clash
+
+    def swap_owners(self, a: str, b: str) -> None:
+        """Exchange the partitions of pods ``a`` and ``b`` (either may hold none)."""
+        pa, pb = self._held.pop(a, None), self._held.pop(b, None)
+        for c in pa or []:
+            self.owner[c] = b
+        for c in pb or []:
+            self.owner[c] = a
+        if pa:
+            self._held[b] = pa
+        if pb:
+            self._held[a] = pb
 
     def holds(self, uid: str) -> bool:
         return uid in self._held

@@ -18,6 +18,13 @@ re-built for MI355X:
   ``ASSUME_TIME`` pod of that size), commits ``ASSIGNED=true`` under a
   resourceVersion precondition and answers env + ``/dev/kfd`` + render node +
   optional CU partition (:mod:`.allocator`);
+* every Allocate is **recorded** with kubelet's device IDs and **reconciled** against kubelet's own record of
+  which pod holds them (PodResources ``List``, :mod:`.reconcile`): when kubelet gave a container the
+  allocation built for another pod of the same size, the two pods' annotations are exchanged so the durable
+  record names what each container really got (records are checkpointed next to the plugin socket);
+* **enforced isolation** (optional, :mod:`.isolation`): Allocate also mounts the per-pod config, the shared
+  HBM ledger and ``libgsx_isolate.so`` (via ``/etc/ld.so.preload``), which confine every HIP/HSA process of
+  the container to its CU partition and HBM share;
 * a **pod informer** on ``spec.nodeName=<node>`` keeps that state current: CU
   partitions and multi-container progress are released when a pod completes
   or is deleted, and rebuilt from the ``gpushare.amd.com/cu-mask`` /
@@ -41,7 +48,9 @@ from . import api
 from ..k8s.informer import Handler, Informer
 from .allocator import AllocateError, ContainerAllocation, assigned_patch, build_response
 from .devices import UNITS, Device
-from .state import AllocationState, PodRec
+from .isolation import IsolationManager
+from .podresources import PodResourcesClient
+from .state import AllocationState, AllocRecord, PodRec
 
 log = logging.getLogger("gsx.deviceplugin")
 
@@ -60,7 +69,9 @@ class GpuSharePlugin:
     def __init__(self, client: KubeClient, node: str, devices: list[Device], profile: NamingProfile, *,
                  unit: str = "GiB", socket_dir: str = api.DEVICE_PLUGIN_PATH, endpoint: str = "gpushare-amd.sock",
                  mount_mode: str = "isolated", health_backend: str | None = None, health_interval: float = 10.0,
-                 reserve_bytes: int = 0, informer: Informer | None = None):
+                 reserve_bytes: int = 0, informer: Informer | None = None,
+                 podresources_socket: str | None = None, reconcile_interval: float = 2.0,
+                 isolation: IsolationManager | None = None, checkpoint: str | None = None):
         self.client = client
         self.node = node
         self.devices = {d.index: d for d in devices}
@@ -75,6 +86,15 @@ class GpuSharePlugin:
         self.ids = {d.index: fake_ids(d, self.units[d.index]) for d in devices}
         self.id_owner = {i: d for d, ids in self.ids.items() for i in ids}
         self.state = AllocationState(node, self.devices, profile)
+        self.isolation = isolation
+        self.state.on_drop.append(self._record_dropped)
+        self.checkpoint = checkpoint if checkpoint is not None else os.path.join(socket_dir, "gsx-allocations.json")
+        self._aid = 0
+        self.reconciler = None
+        if podresources_socket:
+            from .reconcile import Reconciler  # noqa: PLC0415
+
+            self.reconciler = Reconciler(self, PodResourcesClient(podresources_socket), interval=reconcile_interval)
         # a kubelet stand-in in the same process may share its pod informer (one watch per node)
         self._own_informer = informer is None
         self.pods = informer or Informer(client, "pods", field_selector=f"spec.nodeName={node}")
@@ -170,7 +190,56 @@ class GpuSharePlugin:
             self.stats["preferred"] += 1
         return resp
 
-    async def allocate_container(self, units: int) -> tuple[PodRec, ContainerAllocation]:
+    # ------------------------------------------------------------ allocation records
+    def _next_aid(self) -> str:
+        self._aid += 1
+        return f"{time.time_ns() // 1_000_000:x}-{os.getpid():x}-{self._aid}"
+
+    def _record(self, rec: PodRec, ids, units: int, alloc: ContainerAllocation) -> AllocRecord:
+        r = self.state.record(rec, ids, units, alloc.annotations.get("gpushare.amd.com/cu-mask", rec.cu_mask),
+                              self._next_aid(), time.time())
+        r.iso = alloc.iso
+        self.persist_records()
+        return r
+
+    def _record_dropped(self, r: AllocRecord):
+        if self.isolation is not None and r.iso and not any(o.iso == r.iso for o in self.state.records.values()):
+            self.isolation.release(r.iso)
+
+    def persist_records(self):
+        """Checkpoint of the Allocate records (a restarted plugin still knows what each set of IDs was)."""
+        if not self.checkpoint:
+            return
+        import json  # noqa: PLC0415
+
+        tmp = self.checkpoint + ".tmp"
+        try:
+            with open(tmp, "w") as f:
+                json.dump({"node": self.node, "records": [r.to_dict() for r in self.state.records.values()]}, f)
+            os.replace(tmp, self.checkpoint)
+        except OSError as e:
+            log.warning("checkpoint %s: %s", self.checkpoint, e)
+
+    def load_records(self) -> int:
+        """Records of pods that are still on this node (after the informer's first sync)."""
+        import json  # noqa: PLC0415
+
+        try:
+            with open(self.checkpoint) as f:
+                data = json.load(f)
+        except (OSError, ValueError):
+            return 0
+        n = 0
+        for d in data.get("records") or []:
+            r = AllocRecord.from_dict(d)
+            if r.holder in self.state.pods:
+                self.state.records[r.aid] = r
+                if r.ids:
+                    self.state.by_ids[r.ids] = r.aid
+                n += 1
+        return n
+
+    async def allocate_container(self, units: int, ids=()) -> tuple[PodRec, ContainerAllocation]:
         """Match one container request of ``units`` to its pod and build its allocation.
 
         For the pod's first container this commits ``ASSIGNED=true`` (with the pod's resourceVersion as a
@@ -195,12 +264,15 @@ class GpuSharePlugin:
             if rec.assigned == "true":  # a later container of a pod whose first container committed
                 cus = self.state.claim_cus(rec)
                 alloc = build_response(rec.obj, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
+                self._isolate(rec, device, cus, alloc)
                 self.state.later_container_allocated(rec, units)
+                self._record(rec, ids, units, alloc)
                 return rec, alloc
             self.state.inflight.add(rec.uid)
             try:
                 cus = self.state.claim_cus(rec)
                 alloc = build_response(rec.obj, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
+                self._isolate(rec, device, cus, alloc)
                 try:
                     pod = await self.client.patch("pods", rec.name, assigned_patch(rec.obj, self.profile,
                                                                                     alloc.annotations),
@@ -220,14 +292,29 @@ class GpuSharePlugin:
                 self.state.inflight.discard(rec.uid)
             self.state.observe(pod)
             self.state.first_container_committed(rec, units, whole)
+            self._record(rec, ids, units, alloc)
             return rec, alloc
         raise AllocateError("unreachable")
+
+    def _isolate(self, rec: PodRec, device: Device, cus, alloc: ContainerAllocation):
+        """Enforced isolation: the pod's config + ledger files, mounted (or named, for host processes)."""
+        if self.isolation is None:
+            return
+        limit = rec.request * UNITS[self.unit]
+        try:
+            mounts, envs = self.isolation.prepare(rec.uid, cus, device.cu_count, limit,
+                                                  host_process=self.mount_mode == "all")
+        except OSError as e:
+            raise AllocateError(f"isolation files for {rec.key}: {e}") from e
+        alloc.mounts.extend(mounts)
+        alloc.envs.update(envs)
+        alloc.iso = rec.uid
 
     async def Allocate(self, request, context):
         resp = api.AllocateResponse()
         try:
             for creq in request.container_requests:
-                rec, alloc = await self.allocate_container(len(creq.devices_ids))
+                rec, alloc = await self.allocate_container(len(creq.devices_ids), list(creq.devices_ids))
                 c = resp.container_responses.add()
                 for k, v in alloc.envs.items():
                     c.envs[k] = v
@@ -236,7 +323,11 @@ class GpuSharePlugin:
                 c.annotations[POD_ANNOTATION] = f"{rec.key}/{rec.uid}"
                 for dspec in alloc.devices:
                     c.devices.add(**dspec)
+                for m in alloc.mounts:
+                    c.mounts.add(**m)
             self.stats["allocate_ok"] += 1
+            if self.reconciler is not None:
+                self.reconciler.kick()
             return resp
         except (AllocateError, ApiError, OSError) as e:
             self.stats["allocate_fail"] += 1
@@ -316,12 +407,19 @@ class GpuSharePlugin:
                              "cu": d.cu_count, "partition": d.partition} for d in self.devices.values()],
                 "informer": {"synced": self.pods.synced.is_set(), "relists": self.pods.relists,
                              "rewatches": self.pods.rewatches, "events": self.pods.events},
-                "stats": dict(self.stats), **self.state.snapshot()}
+                "stats": dict(self.stats), **self.state.snapshot(),
+                "reconcile": dict(self.reconciler.stats) if self.reconciler is not None else None,
+                "isolation": dict(self.isolation.stats) if self.isolation is not None else None}
 
     def metrics_text(self) -> str:
         lines = []
         for k, v in sorted(self.stats.items()):
             lines += [f"# TYPE gpushare_plugin_{k}_total counter", f"gpushare_plugin_{k}_total {v}"]
+        if self.reconciler is not None:
+            for k, v in sorted(self.reconciler.stats.items()):
+                kind = "gauge" if k.endswith("_max") else "counter"
+                name = f"gpushare_plugin_reconcile_{k}" + ("" if kind == "gauge" else "_total")
+                lines += [f"# TYPE {name} {kind}", f"{name} {v}"]
         for k, v in sorted(self.state.stats.items()):
             lines += [f"# TYPE gpushare_plugin_state_{k}_total counter", f"gpushare_plugin_state_{k}_total {v}"]
         lines.append("# TYPE gpushare_plugin_device_healthy gauge")
@@ -416,6 +514,13 @@ class GpuSharePlugin:
             await self.pods.wait_synced(sync_timeout)
         except asyncio.TimeoutError:
             log.warning("pod informer of %s not synced after %.0fs; Allocate will LIST", self.node, sync_timeout)
+        n = self.load_records()
+        if n:
+            log.info("restored %d allocation records from %s", n, self.checkpoint)
+        if self.isolation is not None and self.pods.synced.is_set():
+            self.isolation.gc({r.iso for r in self.state.records.values() if r.iso} | set(self.state.pods))
+        if self.reconciler is not None:
+            self.reconciler.start()
         if not serve:
             return
         await self.serve()
@@ -434,6 +539,8 @@ class GpuSharePlugin:
     async def stop(self):
         self._stopped = True
         self._changed.set()
+        if self.reconciler is not None:
+            await self.reconciler.stop()
         for t in self._tasks:
             t.cancel()
         if self._own_informer:

@@ -13,6 +13,10 @@ by both the gRPC plugin (:mod:`.plugin`) and the kubelet stand-in (:mod:`.agent`
   every re-list, ownership is rebuilt from the ``gpushare.amd.com/cu-mask`` annotation of
   ``ASSIGNED=true``, non-terminated pods, so a restarted plugin never hands out a CU that a
   running pod still holds;
+* **allocation records** — every Allocate is recorded with the device IDs kubelet passed, the pod it was
+  matched to and the GPU / CU partition it handed out.  kubelet's own record of which pod holds those IDs
+  (PodResources API) is compared with it by :mod:`.reconcile`; a record whose *owner* (the pod kubelet gave it
+  to) is not the pod it was matched to is a swap, and the annotations follow the record;
 * **multi-container progress** — kubelet calls Allocate once per container.  The first
   container of a pod commits ``ASSIGNED=true``; the remaining container sizes are kept until
   they are allocated or the pod leaves Pending / goes away.  After a restart the progress of
@@ -26,7 +30,8 @@ import logging
 from dataclasses import dataclass, field
 
 from ..models import pod as podutil
-from ..models.profile import POD_CU_MASK_ANNOTATION, NamingProfile
+from ..models.profile import (POD_CU_MASK_ANNOTATION, POD_HOLD_IDX_ANNOTATION, POD_HOLD_PARTNER_ANNOTATION,
+                              NamingProfile)
 from .allocator import CU_COUNT_ANNOTATION, AllocateError, CUPartitioner
 from .devices import Device
 
@@ -40,6 +45,34 @@ def parse_cu_mask(words: str) -> list[int]:
         v = int(w, 16)
         out.extend(32 * wi + b for b in range(32) if v >> b & 1)
     return out
+
+
+@dataclass
+class AllocRecord:
+    """One Allocate: what the plugin handed out, for whom it built it, and (once kubelet says so) who got it."""
+    aid: str
+    ids: tuple  # kubelet's device IDs, sorted
+    uid: str  # the pod whose annotations describe this allocation (the matched pod, until a move)
+    dev: int
+    units: int
+    cu_mask: str  # the cu-mask annotation value of the partition handed out ("" if none)
+    owner: str = ""  # the pod kubelet gave the IDs to ("" until PodResources has reported them)
+    t: float = 0.0
+    iso: str = ""  # isolation directory key the container's mounts point at
+
+    @property
+    def holder(self) -> str:
+        return self.owner or self.uid
+
+    def to_dict(self) -> dict:
+        return {"aid": self.aid, "ids": list(self.ids), "uid": self.uid, "dev": self.dev, "units": self.units,
+                "cu_mask": self.cu_mask, "owner": self.owner, "t": self.t, "iso": self.iso}
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "AllocRecord":
+        return cls(aid=d["aid"], ids=tuple(d.get("ids") or ()), uid=d.get("uid", ""), dev=int(d.get("dev", -1)),
+                   units=int(d.get("units", 0)), cu_mask=d.get("cu_mask", ""), owner=d.get("owner", ""),
+                   t=float(d.get("t", 0.0)), iso=d.get("iso", ""))
 
 
 @dataclass
@@ -59,6 +92,8 @@ class PodRec:
     complete: bool
     cu_count: int
     cu_mask: str
+    hold_idx: int = -1
+    hold_partner: str = ""
     obj: dict = field(repr=False, default_factory=dict)
 
     @property
@@ -80,8 +115,12 @@ class AllocationState:
         self.partial: dict[str, list[int]] = {}  # uid -> container sizes not yet allocated
         self.local_commits: set[str] = set()  # first container committed by this process
         self.inflight: set[str] = set()  # claimed by an Allocate whose ASSIGNED patch is in flight
+        self.records: dict[str, AllocRecord] = {}  # aid -> record
+        self.by_ids: dict[tuple, str] = {}  # sorted device IDs -> aid
+        self.keys: dict[str, str] = {}  # ns/name -> uid of the live pod
+        self.on_drop: list = []  # callbacks(record) when a record's holder is gone
         self.stats = {"cu_released": 0, "cu_adopted": 0, "cu_conflicts": 0, "partial_released": 0,
-                      "pods_released": 0}
+                      "pods_released": 0, "records_dropped": 0}
 
     # ------------------------------------------------------------ informer feed
     def _rec(self, pod: dict) -> PodRec:
@@ -99,7 +138,9 @@ class AllocationState:
                       request=sum(conts), containers=[c for c in conts if c > 0],
                       assume_time=podutil.assume_time(pod, p), creation=md.get("creationTimestamp", ""),
                       assigned=ann.get(p.annotation_assigned, ""), complete=podutil.is_complete(pod),
-                      cu_count=cu_count, cu_mask=ann.get(POD_CU_MASK_ANNOTATION, ""), obj=pod)
+                      cu_count=cu_count, cu_mask=ann.get(POD_CU_MASK_ANNOTATION, ""),
+                      hold_idx=podutil.hold_idx(pod), hold_partner=ann.get(POD_HOLD_PARTNER_ANNOTATION, ""),
+                      obj=pod)
 
     def observe(self, pod: dict) -> None:
         """An added / updated pod (informer event, LIST item, or our own PATCH response)."""
@@ -113,6 +154,7 @@ class AllocationState:
             self.release(rec.uid)
             return
         self.pods[rec.uid] = rec
+        self.keys[rec.key] = rec.uid
         if rec.assigned != "true":
             return
         # an assigned pod: its CU partition is owned (rebuild after restart / adopt another agent's record)
@@ -162,10 +204,15 @@ class AllocationState:
             self.stats["cu_released"] += n
         if self.partial.pop(uid, None) is not None:
             self.stats["partial_released"] += 1
-        if self.pods.pop(uid, None) is not None:
+        gone = self.pods.pop(uid, None)
+        if gone is not None:
             self.stats["pods_released"] += 1
+            if self.keys.get(gone.key) == uid:
+                del self.keys[gone.key]
         self.local_commits.discard(uid)
         self.inflight.discard(uid)
+        for r in [r for r in self.records.values() if r.holder == uid]:
+            self.drop_record(r)
 
     # ------------------------------------------------------------ Allocate
     def candidates(self) -> list[PodRec]:
@@ -219,6 +266,47 @@ class AllocationState:
         if not left:
             del self.partial[rec.uid]
 
+    # ------------------------------------------------------------ allocation records
+    def record(self, rec: PodRec, ids, units: int, cu_mask: str, aid: str, t: float = 0.0) -> AllocRecord:
+        """An Allocate of ``ids`` was matched to ``rec`` (kubelet re-using the IDs of a finished pod replaces the
+        older record)."""
+        key = tuple(sorted(ids))
+        old = self.by_ids.get(key) if key else None
+        if old is not None and old in self.records:
+            self.drop_record(self.records[old])
+        r = AllocRecord(aid=aid, ids=key, uid=rec.uid, dev=rec.dev, units=units, cu_mask=cu_mask, t=t)
+        self.records[aid] = r
+        if key:
+            self.by_ids[key] = aid
+        return r
+
+    def drop_record(self, r: AllocRecord) -> None:
+        if self.records.pop(r.aid, None) is None:
+            return
+        if r.ids and self.by_ids.get(r.ids) == r.aid:
+            del self.by_ids[r.ids]
+        self.stats["records_dropped"] += 1
+        for cb in self.on_drop:
+            cb(r)
+
+    def record_for_ids(self, ids) -> AllocRecord | None:
+        aid = self.by_ids.get(tuple(sorted(ids)))
+        return self.records.get(aid) if aid else None
+
+    def pod_by_key(self, key: str) -> PodRec | None:
+        uid = self.keys.get(key)
+        return self.pods.get(uid) if uid else None
+
+    def move_records(self, p_uid: str, q_uid: str, r: AllocRecord) -> None:
+        """After the annotations of P and Q were exchanged because P holds ``r`` (built for Q): ``r`` now
+        describes P, and whatever described P describes Q.  The CU partitions follow the same exchange."""
+        for other in self.records.values():
+            if other is not r and other.uid == p_uid:
+                other.uid = q_uid
+        r.uid = p_uid
+        for cp in self.cus.values():
+            cp.swap_owners(p_uid, q_uid)
+
     def snapshot(self) -> dict:
         """What ``/debug/state`` and the tests look at."""
         return {
@@ -229,6 +317,7 @@ class AllocationState:
             "cu_partitions": {str(i): {self.pods[u].key if u in self.pods else u: len(c) for u, c in cp.held().items()}
                               for i, cp in self.cus.items()},
             "cu_free": {str(i): cp.free_count() for i, cp in self.cus.items()},
+            "records": len(self.records),
             "stats": dict(self.stats),
         }
 

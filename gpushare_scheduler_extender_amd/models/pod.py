@@ -86,6 +86,14 @@ def gpu_id_from_annotation(pod: dict, profile: NamingProfile) -> int:
     return -1 if v is None or v < 0 else v
 
 
+def hold_idx(pod: dict) -> int:
+    """``gpushare.amd.com/hold-idx``: the second device a pod is charged on during a reconciliation, else -1."""
+    from .profile import POD_HOLD_IDX_ANNOTATION  # noqa: PLC0415
+
+    v = _atoi(annotations(pod).get(POD_HOLD_IDX_ANNOTATION))
+    return -1 if v is None or v < 0 else v
+
+
 def gpu_mem_from_annotation(pod: dict, profile: NamingProfile) -> int:
     """pkg/utils/pod.go:94-113: parse errors / negatives -> 0."""
     v = _atoi(annotations(pod).get(profile.annotation_pod))

@@ -16,6 +16,12 @@ NODE_DEVICE_INFO_ANNOTATION = "gpushare.amd.com/devices"  # JSON device inventor
 POD_CU_MASK_ANNOTATION = "gpushare.amd.com/cu-mask"  # per-pod CU partition (isolation)
 POD_CU_COUNT_ANNOTATION = "gpushare.amd.com/cu-count"  # the pod asks for a CU partition of this size
 POD_ASSIGN_TIME_ANNOTATION = "gpushare.amd.com/assign-time"
+# reconciliation with kubelet's device assignments (deviceplugin/reconcile.py): while the plugin moves a pod's
+# allocation record to the GPU kubelet really gave it, the pod is charged on its old device too (hold-idx);
+# hold-partner keeps what the partner pod must receive, so a plugin restart can finish the move
+POD_HOLD_IDX_ANNOTATION = "gpushare.amd.com/hold-idx"
+POD_HOLD_PARTNER_ANNOTATION = "gpushare.amd.com/hold-partner"
+POD_RECONCILED_ANNOTATION = "gpushare.amd.com/reconciled"  # count of record moves applied to this pod
 NODE_RUNTIME_ENDPOINTS_ANNOTATION = "gpushare.amd.com/runtime-endpoints"  # JSON {gpu index: runtime shim URL}
 
 

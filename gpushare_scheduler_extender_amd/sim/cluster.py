@@ -143,7 +143,8 @@ NODEAGENT = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-nodeagen
 
 
 def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", workers: int = 32,
-                     native: bool = True, plugin: str = "grpc", cpus: list[int] | None = None) -> ChildProc:
+                     native: bool = True, plugin: str = "grpc", cpus: list[int] | None = None,
+                     extra: list[str] | None = None) -> ChildProc:
     """kubelet + device-plugin Allocate + runtime stand-in for ``node``.
 
     ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent, its own Allocate matching);
@@ -157,8 +158,8 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
         return ChildProc([str(exe), "--node", node, "--apiserver", apiserver, "--profile", profile,
                           "--workers", str(min(workers, 16))], "node-agent", cpus=cpus)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
-                      apiserver, "--profile", profile, "--workers", str(workers), "--plugin", plugin], "node-agent",
-                     cpus=cpus)
+                      apiserver, "--profile", profile, "--workers", str(workers), "--plugin", plugin,
+                      *(extra or [])], "node-agent", cpus=cpus)
 
 
 SCHEDSIM = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-schedsim"

@@ -100,7 +100,7 @@ class Cluster:
 
     def __init__(self, profile: NamingProfile, totals: list[int], gpu: bool | int, cu_count: int = 256,
                  native: bool = True, partition: str = "SPX", xcc_count: int = 8, agent: str | None = None,
-                 pool_gib: int = 0, bind_mode: str = "binding"):
+                 pool_gib: int = 0, bind_mode: str = "binding", agent_args: list[str] | None = None):
         self.profile = profile
         self.totals = totals
         self.children = []
@@ -111,9 +111,8 @@ class Cluster:
         # native: compiled kube-scheduler / node-agent stand-ins; otherwise the asyncio ones
         self.children.append(start_scheduler(self.api.url, self.ext.url, profile=profile.name, native=native))
         self.agent_kind = agent or AGENT["kind"]
-        self.children.append(start_node_agent(self.api.url, NODE, profile=profile.name,
-                                              native=self.agent_kind == "native",
-                                              plugin="inproc" if self.agent_kind == "inproc" else "grpc"))
+        self.agent_args = list(agent_args or [])
+        self.children.append(self._agent())
         self.rt = Runtimes(len(totals), GIB, max(totals), gpu)
         self.cu_count = cu_count
         self.xcc_count = xcc_count
@@ -147,6 +146,41 @@ class Cluster:
                 return
             await asyncio.sleep(0.005)
         raise TimeoutError("node agent never became ready")
+
+    def _agent(self):
+        return start_node_agent(self.api.url, NODE, profile=self.profile.name, native=self.agent_kind == "native",
+                                plugin="inproc" if self.agent_kind == "inproc" else "grpc", extra=self.agent_args)
+
+    def agent_child(self):
+        return next(ch for ch in self.children if ch.name == "node-agent")
+
+    def stop_agent(self):
+        """kubelet (and the plugin beside it) goes down; pods bound meanwhile are admitted as one batch later."""
+        self.agent_child().stop()
+
+    async def start_agent(self):
+        old = self.agent_child()
+        new = self._agent()
+        self.children[self.children.index(old)] = new
+        await self.agent_http.close()
+        self.agent_http = HttpClient(new.url)
+        for _ in range(6000):
+            if (await self.agent_http.request("GET", "/v1/stats")).status == 200:
+                return
+            await asyncio.sleep(0.005)
+        raise TimeoutError("node agent never became ready")
+
+    async def bind(self, pod: dict) -> int:
+        """kube-scheduler's filter + bind for one pod (tests that choose the binding order themselves)."""
+        from ..models import wire
+
+        f = await self.filter(pod)
+        if NODE not in (f.get("NodeNames") or []):
+            return 0
+        md = pod["metadata"]
+        args = wire.ExtenderBindingArgs(md["name"], md.get("namespace", "default"), md["uid"], NODE)
+        r = await self.ext_http.request("POST", "/gpushare-scheduler/bind", args.encode())
+        return r.status
 
     async def inspect(self) -> dict:
         r = await self.ext_http.request("GET", "/gpushare-scheduler/inspect")

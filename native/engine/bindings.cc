@@ -660,6 +660,7 @@ PYBIND11_MODULE(_engine, m) {
       .def_readwrite("assigned", &PodView::assigned)
       .def_readwrite("assume_time", &PodView::assume_time)
       .def_readwrite("cu_mask", &PodView::cu_mask)
+      .def_readwrite("hold_idx", &PodView::hold_idx)
       .def_property_readonly("terminal", &PodView::terminal)
       .def_property_readonly("complete", &PodView::complete)
       .def_property_readonly("assigned_non_terminated", &PodView::assigned_non_terminated)

@@ -153,9 +153,8 @@ void Controller::sync(const std::string& key) {
 void Controller::h_add(const std::string& key) { sync(key); }
 
 void Controller::h_update(const Entry& old, const std::string& key) {
-  (void)old;
-  // controller.go:257-305 enqueue rules (+ "assumed by our bind, now observed"
-  // and "device index rewritten")
+  // controller.go:257-305 enqueue rules (+ "assumed by our bind, now observed",
+  // "device index rewritten" and "reconciliation hold set or cleared")
   const Entry& cur = store_[key];
   int64_t dev = -1;
   int state;
@@ -169,6 +168,8 @@ void Controller::h_update(const Entry& old, const std::string& key) {
   } else if (cur.v.dev_idx >= 0 && (state == 0 || state == 2)) {
     enqueue = true;
   } else if (state == 1 && cur.v.dev_idx != dev) {
+    enqueue = true;
+  } else if (state != 0 && cur.v.hold_idx != old.v.hold_idx) {
     enqueue = true;
   }
   if (enqueue) sync(key);

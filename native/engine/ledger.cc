@@ -18,6 +18,9 @@ void Ledger::account(PodRec& r) {
   d.used += r.mem;
   d.npods += 1;
   if (d.used > d.total) stats_.overcommit_events++;
+  // a pod being moved between devices is charged on both until the move completes: never under-counted
+  r.held_on = (r.hold >= 0 && r.hold != r.dev && r.hold < static_cast<int64_t>(n.devs.size())) ? r.hold : -1;
+  if (r.held_on >= 0) n.devs[static_cast<size_t>(r.held_on)].used += r.mem;
   r.accounted = true;
 }
 
@@ -31,6 +34,8 @@ void Ledger::unaccount(PodRec& r) {
   DevState& d = n.devs[static_cast<size_t>(r.dev)];
   d.used -= r.mem;
   d.npods -= 1;
+  if (r.held_on >= 0 && r.held_on < static_cast<int64_t>(n.devs.size())) n.devs[static_cast<size_t>(r.held_on)].used -= r.mem;
+  r.held_on = -1;
 }
 
 void Ledger::rebuild(NodeState& n) {
@@ -126,6 +131,7 @@ int Ledger::upsert_pod(const PodView& v) {
     if (v.dev_idx >= 0) {
       r.dev = v.dev_idx;
       r.mem = v.annot_mem;
+      r.hold = v.hold_idx;
       r.assumed = false;  // observed with annotations: reservation confirmed
     } else if (!r.assumed) {
       r.dev = -1;
@@ -140,6 +146,7 @@ int Ledger::upsert_pod(const PodView& v) {
   r.name = v.name;
   r.node = v.node;
   r.dev = v.dev_idx;
+  r.hold = v.hold_idx;
   r.mem = v.annot_mem;
   r.request = v.request;
   r.terminal = v.terminal();

@@ -42,6 +42,7 @@ enum class Check : int { Ok = 0, NodeNotFound = 1, NotGPUShare = 2, Insufficient
 struct PodRec {
   std::string uid, ns, name, node;
   int64_t dev = -1;      // device index on node (-1: not placed)
+  int64_t hold = -1;     // second device charged while a reconciliation moves the pod (-1: none)
   int64_t mem = 0;       // accounted memory (annotation POD / assumed request)
   int64_t request = 0;   // container-limit sum (inspect "usedGPU" per pod)
   bool terminal = false; // Succeeded/Failed -> not counted
@@ -52,6 +53,7 @@ struct PodRec {
   double bound_at = 0;   // when the bind's apiserver write succeeded
   double deadline = 0;   // expiry of an assumed+bound reservation
   bool accounted = false;
+  int64_t held_on = -1;  // the hold device actually charged by account() (node may have changed since)
 };
 
 struct DevState {

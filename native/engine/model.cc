@@ -107,6 +107,11 @@ bool parse_pod(const json::Doc& d, uint32_t pod, const Profile& p, PodView* out)
       }
       i = d.find(a, "gpushare.amd.com/cu-mask");
       if (i >= 0) out->cu_mask = str_at(d, i);
+      i = d.find(a, "gpushare.amd.com/hold-idx");
+      if (i >= 0) {
+        std::string s = str_at(d, i);
+        out->hold_idx = parse_atoi(s, &v) && v >= 0 ? v : -1;
+      }
     }
   }
   out->node = str_at(d, d.path(pod, {"spec", "nodeName"}));

@@ -46,6 +46,9 @@ struct PodView {
   int assigned = -1;         // annotation ASSIGNED: -1 absent, 0 false, 1 true
   int64_t assume_time = -1;  // annotation ASSUME_TIME (unix ns)
   std::string cu_mask;       // optional per-pod CU mask annotation (isolation)
+  // gpushare.amd.com/hold-idx: a second device the pod is charged on while the device plugin moves its
+  // allocation record to the GPU kubelet really gave it (deviceplugin/reconcile.py); -1 if absent
+  int64_t hold_idx = -1;
 
   bool terminal() const { return phase == "Succeeded" || phase == "Failed"; }
   // pod.go:28-37 IsCompletePod

@@ -450,3 +450,32 @@ def test_bind_wait_returns_when_its_own_entry_is_left():
         assert done.wait(2.0)
         t.join()
     eng.bind_leave(s4)
+
+
+def test_reconcile_hold_charges_both_devices():
+    """A pod whose allocation record the device plugin is moving (hold-idx) is charged on its new and its old
+    device until the hold is cleared: no device is ever under-counted mid-move (deviceplugin/reconcile.py)."""
+    eng = new_engine()
+    eng.upsert_node("n", 20, 2)
+    a = _annotated("a", "n", 0, 8, uid="ua")
+    b = _annotated("b", "n", 1, 8, uid="ub")
+    _load(eng, a)
+    _load(eng, b)
+    assert eng.node_devices("n") == [(10, 8), (10, 8)]
+    a["metadata"]["annotations"][SHARED_GPU.annotation_idx] = "1"
+    a["metadata"]["annotations"]["gpushare.amd.com/hold-idx"] = "0"
+    _load(eng, a)  # step 1: a moves to GPU 1, still held on GPU 0
+    assert eng.node_devices("n") == [(10, 8), (10, 16)]
+    b["metadata"]["annotations"][SHARED_GPU.annotation_idx] = "0"
+    _load(eng, b)  # step 2: b takes GPU 0 (over-counted while the hold lasts, never under)
+    assert eng.node_devices("n") == [(10, 16), (10, 8)]
+    del a["metadata"]["annotations"]["gpushare.amd.com/hold-idx"]
+    _load(eng, a)  # step 3: hold cleared
+    assert eng.node_devices("n") == [(10, 8), (10, 8)]
+    a["metadata"]["annotations"]["gpushare.amd.com/hold-idx"] = "1"  # a hold on its own device counts once
+    _load(eng, a)
+    assert eng.node_devices("n") == [(10, 8), (10, 8)]
+    a["metadata"]["annotations"]["gpushare.amd.com/hold-idx"] = "0"
+    _load(eng, a)
+    eng.remove_pod("ua")  # removal drops both charges
+    assert eng.node_devices("n") == [(10, 8), (10, 0)]

@@ -1,0 +1,100 @@
+"""Enforced isolation, CPU side: the library against a fake HSA runtime, and the plugin's per-pod files and
+mounts (the GPU behaviour is tests/test_gpu_isolate.py)."""
+import asyncio
+import os
+import subprocess
+from pathlib import Path
+
+from gpushare_scheduler_extender_amd.deviceplugin.allocator import CUPartitioner
+from gpushare_scheduler_extender_amd.deviceplugin.isolation import CONTAINER_DIR, IsolationManager, config_text
+
+ROOT = Path(__file__).resolve().parents[1]
+LIB = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "libgsx_isolate.so"
+
+
+def test_library_against_fake_hsa_runtime(tmp_path):
+    from gpushare_scheduler_extender_amd.utils.build import build_native
+
+    build_native(["isolate"])
+    r = subprocess.run([str(ROOT / "build" / "isolate_test"), str(LIB), str(tmp_path)], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0 and "isolate_test: OK" in r.stdout, r.stderr
+
+
+def test_config_text_words_match_the_cu_mask_annotation():
+    cus = CUPartitioner(256, 8).allocate("u", 64)
+    t = config_text(cus, 256, 64 << 30)
+    words = [int(w, 16) for w in t.split("cu_mask=")[1].split("\n")[0].split(",")]
+    assert len(words) == 8 and sum(bin(w).count("1") for w in words) == 64
+    assert all(bin(w).count("1") == 8 for w in words)  # 8 CUs on each XCD (32-CU block)
+    assert f"hbm_limit_bytes={64 << 30}" in t and f"ledger={CONTAINER_DIR}/hbm.ledger" in t
+
+
+def test_manager_files_mounts_and_release(tmp_path):
+    m = IsolationManager(str(tmp_path / "iso"), library=str(LIB))
+    mounts, envs = m.prepare("uid-1", [0, 1, 2], 256, 8 << 30)
+    paths = {x["container_path"]: x for x in mounts}
+    assert paths["/etc/ld.so.preload"]["read_only"] and paths[f"{CONTAINER_DIR}/isolation.conf"]["read_only"]
+    assert not paths[f"{CONTAINER_DIR}/hbm.ledger"]["read_only"]  # every process of the pod writes its slot
+    assert envs["HSA_TOOLS_LIB"] == f"{CONTAINER_DIR}/libgsx_isolate.so"
+    assert Path(paths["/etc/ld.so.preload"]["host_path"]).read_text().strip() == f"{CONTAINER_DIR}/libgsx_isolate.so"
+    conf = Path(paths[f"{CONTAINER_DIR}/isolation.conf"]["host_path"])
+    assert oct(conf.stat().st_mode & 0o777) == "0o444" and "hbm_limit_bytes=8589934592" in conf.read_text()
+    assert os.path.getsize(paths[f"{CONTAINER_DIR}/libgsx_isolate.so"]["host_path"]) > 0
+    # host processes: no mounts, host paths in env
+    mounts2, envs2 = m.prepare("uid-2", None, 256, 4 << 30, host_process=True)
+    assert mounts2 == [] and Path(envs2["GSX_ISOLATION_CONFIG"]).exists()
+    assert "cu_mask" not in Path(envs2["GSX_ISOLATION_CONFIG"]).read_text()
+    m.release("uid-1")
+    assert not m.pod_dir("uid-1").exists() and m.pod_dir("uid-2").exists()
+    assert m.gc({"uid-3"}) == 1 and not m.pod_dir("uid-2").exists()
+
+
+def test_plugin_allocate_mounts_isolation_and_records(tmp_path):
+    """The gRPC Allocate answers the isolation mounts, and the record of the allocation is checkpointed."""
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import Device
+    from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin, PluginClient
+    from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+    from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+    from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+
+    async def go():
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 16, 1))
+        ann = {SHARED_GPU.annotation_idx: "0", SHARED_GPU.annotation_dev: "16", SHARED_GPU.annotation_pod: "4",
+               SHARED_GPU.annotation_assigned: "false", SHARED_GPU.annotation_assume_time: "1",
+               "gpushare.amd.com/cu-count": "64"}
+        pod = await c.create("pods", make_pod("a", 4, node="n", annotations=ann))
+        iso = IsolationManager(str(tmp_path / "iso"), library=str(LIB))
+        plugin = GpuSharePlugin(KubeClient(api.url), "n", [Device(index=0, total_bytes=16 << 30)], SHARED_GPU,
+                                socket_dir=str(tmp_path / "dp"), isolation=iso)
+        await plugin.start(register=False, publish=False)
+        cl = PluginClient(plugin.socket_path)
+        try:
+            r = (await cl.allocate([[f"gpu0-_-{i}" for i in range(4)]])).container_responses[0]
+            mounts = {m.container_path: m for m in r.mounts}
+            assert set(mounts) == {"/run/gsx/isolation.conf", "/run/gsx/hbm.ledger", "/run/gsx/libgsx_isolate.so",
+                                   "/etc/ld.so.preload"}
+            conf = Path(mounts["/run/gsx/isolation.conf"].host_path).read_text()
+            assert "cu_mask=" in conf and f"hbm_limit_bytes={4 << 30}" in conf
+            assert r.envs["HSA_TOOLS_LIB"] == "/run/gsx/libgsx_isolate.so"
+            assert len(plugin.state.records) == 1
+            import json
+            saved = json.loads(Path(plugin.checkpoint).read_text())["records"]
+            assert saved[0]["uid"] == pod["metadata"]["uid"] and len(saved[0]["ids"]) == 4
+            # the pod goes away: its record and its isolation files go with it
+            await c.delete("pods", "a", "default")
+            for _ in range(100):
+                if not plugin.state.records:
+                    break
+                await asyncio.sleep(0.02)
+            assert not plugin.state.records and not iso.pod_dir(pod["metadata"]["uid"]).exists()
+        finally:
+            await cl.close()
+            await plugin.stop()
+            await plugin.client.close()
+            await c.close()
+            await api.stop()
+    asyncio.run(go())
