@@ -89,6 +89,8 @@ class Controller:
             enqueue = True  # device index rewritten: re-account
         elif state != 0 and podutil.hold_idx(new) != podutil.hold_idx(old):
             enqueue = True  # the device plugin's reconciliation set / cleared a hold (charged on two devices)
+        elif state == 2 and podutil.gpu_id_from_annotation(new, self.profile) < 0 and podutil.node_name(new):
+            enqueue = True  # our reservation, bound without its annotations: the ledger queues a repair
         if enqueue:
             if raw is not None:
                 self._raw[key] = raw

@@ -253,6 +253,8 @@ class GpuSharePlugin:
                 await self.refresh()
                 refreshed = True
                 rec, whole = self.state.match(units)
+            if rec is None and self.state.unannotated(units):
+                rec, whole = await self._wait_for_annotations(units)
             if rec is None:
                 raise AllocateError(f"no pending pod on {self.node} requests {units} {self.profile.resource} "
                                     f"with {self.profile.annotation_assigned}=false")
@@ -295,6 +297,20 @@ class GpuSharePlugin:
             self._record(rec, ids, units, alloc)
             return rec, alloc
         raise AllocateError("unreachable")
+
+    async def _wait_for_annotations(self, units: int, timeout: float = 10.0):
+        """A pod of this size is bound to the node but carries no allocation record yet: the extender is writing
+        it back (an apiserver that dropped the Binding's annotations).  Failing now would fail the pod."""
+        self.stats["annotation_waits"] = self.stats.get("annotation_waits", 0) + 1
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            await asyncio.sleep(0.02)
+            rec, whole = self.state.match(units)
+            if rec is not None:
+                return rec, whole
+            if not self.state.unannotated(units):
+                break
+        return self.state.match(units)
 
     def _isolate(self, rec: PodRec, device: Device, cus, alloc: ContainerAllocation):
         """Enforced isolation: the pod's config + ledger files, mounted (or named, for host processes)."""

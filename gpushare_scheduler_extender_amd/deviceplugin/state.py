@@ -238,6 +238,11 @@ class AllocationState:
                 return r, False
         return None, False
 
+    def unannotated(self, units: int) -> bool:
+        """A pending pod of this size bound to the node without any allocation annotation (``*_IDX``)."""
+        return any(r.pending and r.dev < 0 and r.assigned != "true" and r.request == units
+                   and r.uid not in self.inflight for r in self.pods.values())
+
     def preferred_device(self, units: int) -> int:
         rec, _ = self.match(units)
         return rec.dev if rec is not None else -1

@@ -89,6 +89,8 @@ class ExtenderServer:
         self.pprof = pprof
         self.app = self._make_app()
         self._gc_task: asyncio.Task | None = None
+        self._repair_task: asyncio.Task | None = None
+        self.annotation_repairs = 0
         self._bg: set[asyncio.Task] = set()
         self.native_server = False
         self.elector = None
@@ -114,6 +116,8 @@ class ExtenderServer:
     async def start(self):
         await self.controller.start()
         self._gc_task = asyncio.get_running_loop().create_task(self._gc_loop())
+        self._repair_task = asyncio.get_running_loop().create_task(self._repair_loop())
+        self.metrics.bind_mode.set(1 if self.bind_mode == "update" else 0)
         if self.elector is not None:
             await self.elector.start()  # informers + ledger are warm before we can win
 
@@ -122,6 +126,8 @@ class ExtenderServer:
             await self.elector.stop()
         if self._gc_task:
             self._gc_task.cancel()
+        if self._repair_task:
+            self._repair_task.cancel()
         await self.controller.stop()
 
     async def _gc_loop(self):
@@ -134,6 +140,43 @@ class ExtenderServer:
                 log.warning("expired %d bind reservations a fresh LIST did not confirm", n)
             if relist:
                 log.info("bind reservations overdue: forcing a pod re-list to confirm them")
+
+    async def _repair_loop(self):
+        """Self-check of the ``binding`` bind mode.  It relies on kube-apiserver copying the Binding's
+        ``metadata.annotations`` onto the pod; an apiserver or admission webhook that drops them leaves the pod
+        bound without ``*_IDX`` -- the device plugin then has no candidate and every Allocate fails.  The ledger
+        flags such pods (bound by us, observed on the node, annotations missing); here the annotations are
+        written back with the reference's pod update (``pkg/cache/nodeinfo.go:150-189``), later binds switch to
+        ``update`` mode (annotate, then bind), and a metric and a Warning event record it."""
+        while True:
+            await asyncio.sleep(0.05)
+            for a in self.engine.drain_annotation_repairs():
+                ann = podutil.bind_annotations(self.profile, a["dev"], a["dev_total"], a["mem"], now_ns=a["assume_ns"])
+                pod = {"kind": "Pod", "metadata": {"name": a["name"], "namespace": a["namespace"], "uid": a["uid"]}}
+                if self.bind_mode != "update":
+                    self.bind_mode = "update"
+                    self.engine.set_update_mode(True)
+                    self.metrics.bind_mode.set(1)
+                    log.warning("the apiserver dropped the annotations of a Binding (pod %s/%s): binds now write "
+                                "the annotations first (bind mode 'update')", a["namespace"], a["name"])
+                    self._event(pod, "BindingAnnotationsDropped",
+                                "the apiserver did not keep the Binding's annotations; switched to annotate-then-bind")
+                for attempt in range(20):
+                    try:
+                        await self.client.patch("pods", a["name"], {"metadata": {"annotations": ann}}, a["namespace"])
+                        self.annotation_repairs += 1
+                        self.metrics.annotation_repairs.labels("ok").inc()
+                        break
+                    except ApiError as e:
+                        if e.not_found:
+                            self.metrics.annotation_repairs.labels("gone").inc()
+                            break
+                        await asyncio.sleep(min(0.5, 0.01 * 2 ** attempt))
+                    except OSError:
+                        await asyncio.sleep(min(0.5, 0.01 * 2 ** attempt))
+                else:
+                    self.metrics.annotation_repairs.labels("failed").inc()
+                    log.error("could not write the allocation annotations back onto %s/%s", a["namespace"], a["name"])
 
     # ------------------------------------------------------------ verbs
     def filter(self, body: bytes) -> bytes:

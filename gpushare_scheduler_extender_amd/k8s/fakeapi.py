@@ -199,13 +199,14 @@ class Faults:
         self.expire_watches = 0  # the next N watch requests get 410 Gone (history compacted)
         self.hold_watches = False  # new watch requests wait until this is cleared
         self.fail_lists = False  # LIST requests answer 503 (an apiserver that cannot serve reads)
+        self.drop_binding_annotations = False  # Binding.metadata.annotations are not copied onto the pod
         self.slow_bindings: dict[str, float] = {}  # pod name -> ms a binding of it takes
         self.seed = 0
         self.rng = random.Random(0)
 
     def update(self, d: dict):
         for k in ("conflict_rate", "error_rate", "latency_ms", "drop_watch_after", "expire_watches", "hold_watches",
-                  "fail_lists"):
+                  "fail_lists", "drop_binding_annotations"):
             if k in d:
                 setattr(self, k, type(getattr(self, k))(d[k]))
         if "slow_bindings" in d:
@@ -218,7 +219,7 @@ class Faults:
         return {"conflict_rate": self.conflict_rate, "error_rate": self.error_rate,
                 "latency_ms": self.latency_ms, "drop_watch_after": self.drop_watch_after,
                 "expire_watches": self.expire_watches, "hold_watches": self.hold_watches,
-                "fail_lists": self.fail_lists}
+                "fail_lists": self.fail_lists, "drop_binding_annotations": self.drop_binding_annotations}
 
 
 class FakeApiServer:
@@ -378,7 +379,7 @@ class FakeApiServer:
         new["spec"] = dict(cur.get("spec") or {})
         new["spec"]["nodeName"] = target
         new["metadata"] = dict(cur["metadata"])
-        ann = bmd.get("annotations") or {}
+        ann = {} if self.faults.drop_binding_annotations else (bmd.get("annotations") or {})
         if ann:
             new["metadata"]["annotations"] = {**(cur["metadata"].get("annotations") or {}), **ann}
         st = new["status"] = dict(cur.get("status") or {})

@@ -7,7 +7,7 @@ binpack utilisation) that are computed at scrape time from the native ledger.
 """
 from __future__ import annotations
 
-from prometheus_client import CollectorRegistry, Counter, Histogram, generate_latest
+from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
 from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, HistogramMetricFamily
 
 LAT_BUCKETS = (0.0001, 0.00025, 0.0005, 0.001, 0.0025, 0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1.0, 2.5, 5.0)
@@ -83,6 +83,11 @@ class Metrics:
         self.bind_results = Counter(f"{prefix}_bind_results", "bind outcomes", ["result"], registry=self.registry)
         self.allocate_results = Counter(f"{prefix}_allocate_results", "device-plugin Allocate outcomes",
                                         ["result"], registry=self.registry)
+        self.annotation_repairs = Counter(f"{prefix}_bind_annotation_repairs",
+                                          "pods bound without the annotations their Binding carried, written back",
+                                          ["result"], registry=self.registry)
+        self.bind_mode = Gauge(f"{prefix}_bind_mode_update", "1: binds annotate then bind (reference's two calls)",
+                               registry=self.registry)
         if engine is not None:
             self.registry.register(_LedgerCollector(engine))
 

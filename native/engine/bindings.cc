@@ -299,6 +299,7 @@ class Engine {
     d["bind_fail"] = s.bind_fail;
     d["expired"] = s.expired;
     d["expiry_deferred"] = s.expiry_deferred;
+    d["annotations_missing"] = s.annotations_missing;
     d["overcommit_events"] = s.overcommit_events;
     d["pod_upserts"] = s.pod_upserts;
     d["pod_removes"] = s.pod_removes;
@@ -326,6 +327,7 @@ class Engine {
     if (cfg.api.server.empty()) cfg.native_bind = false;
     srv_.reset(new NativeServer(&l_, cfg));
     srv_->set_binds_enabled(binds_enabled_);
+    if (update_mode_) srv_->set_update_mode(true);
     std::string err;
     int p = srv_->start(&err);
     if (p < 0) {
@@ -467,6 +469,33 @@ class Engine {
     if (srv_) srv_->set_binds_enabled(on);
   }
 
+  py::list drain_annotation_repairs() {
+    std::vector<AnnotationRepair> rs;
+    {
+      std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
+      rs = l_.drain_repairs();
+    }
+    py::list out;
+    for (auto& a : rs) {
+      py::dict d;
+      d["uid"] = a.uid;
+      d["namespace"] = a.ns;
+      d["name"] = a.name;
+      d["node"] = a.node;
+      d["dev"] = a.dev;
+      d["dev_total"] = a.dev_total;
+      d["mem"] = a.mem;
+      d["assume_ns"] = a.assume_ns;
+      out.append(d);
+    }
+    return out;
+  }
+
+  void set_update_mode(bool on) {
+    update_mode_ = on;
+    if (srv_) srv_->set_update_mode(on);
+  }
+
   py::list drain_bind_failures() {
     py::list out;
     if (!srv_) return out;
@@ -501,6 +530,7 @@ class Engine {
 
  private:
   Ledger l_;
+  bool update_mode_ = false;
   std::unique_ptr<NativeServer> srv_;  // declared after l_: destroyed (stopped) first
   std::unique_ptr<Controller> ctl_;
   bool binds_enabled_ = true;
@@ -715,6 +745,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("ledger_mutex", &Engine::ledger_mutex)
       .def("drain_bind_failures", &Engine::drain_bind_failures)
       .def("set_binds_enabled", &Engine::set_binds_enabled)
+      .def("set_update_mode", &Engine::set_update_mode)
+      .def("drain_annotation_repairs", &Engine::drain_annotation_repairs)
       .def("pending_count", &Engine::pending_count);
 
   py::class_<PyPodTracker>(m, "PodTracker")

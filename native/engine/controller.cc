@@ -171,6 +171,8 @@ void Controller::h_update(const Entry& old, const std::string& key) {
     enqueue = true;
   } else if (state != 0 && cur.v.hold_idx != old.v.hold_idx) {
     enqueue = true;
+  } else if (state == 2 && cur.v.dev_idx < 0 && !cur.v.node.empty()) {
+    enqueue = true;  // our reservation, bound, but without its annotations: the ledger queues a repair
   }
   if (enqueue) sync(key);
 }

@@ -133,8 +133,14 @@ int Ledger::upsert_pod(const PodView& v) {
       r.mem = v.annot_mem;
       r.hold = v.hold_idx;
       r.assumed = false;  // observed with annotations: reservation confirmed
+      r.unannotated = false;
     } else if (!r.assumed) {
       r.dev = -1;
+    } else if (r.dev >= 0) {
+      // our reservation, bound to its node, but the allocation annotations the Binding carried are missing:
+      // the apiserver did not copy them (the reservation stays; the server writes them back)
+      r.unannotated = true;
+      queue_repair(r);
     }
     account(r);
     return r.dev >= 0 ? 1 : 0;
@@ -261,6 +267,8 @@ int64_t Ledger::assume_ordered(const std::string& uid, const std::string& ns, co
   std::lock_guard<std::mutex> o(order_mu_);
   last_assume_ns_ = std::max(now, last_assume_ns_ + 1);  // strictly increasing in assume order
   *assume_ns = last_assume_ns_;
+  auto pit = pods_.find(uid);
+  if (pit != pods_.end()) pit->second.assume_ns = last_assume_ns_;
   *seq = ++order_seq_;
   inflight_.push_back(InflightBind{node, req, dev, *seq, cu_count});
   return dev;
@@ -343,6 +351,32 @@ void Ledger::finish_bind(const std::string& uid, bool ok, double ttl_s) {
   it->second.bound = true;
   it->second.bound_at = now_s();
   it->second.deadline = it->second.bound_at + ttl_s;
+  if (it->second.unannotated) queue_repair(it->second);  // the watch event raced the binding's response
+}
+
+void Ledger::queue_repair(PodRec& r) {
+  if (!r.bound || r.repair_queued || r.dev < 0) return;
+  r.repair_queued = true;
+  stats_.annotations_missing++;
+  AnnotationRepair a;
+  a.uid = r.uid;
+  a.ns = r.ns;
+  a.name = r.name;
+  a.node = r.node;
+  a.dev = r.dev;
+  a.mem = r.mem;
+  a.assume_ns = r.assume_ns;
+  auto nit = nodes_.find(r.node);
+  if (nit != nodes_.end() && r.dev < static_cast<int64_t>(nit->second.devs.size())) {
+    a.dev_total = nit->second.devs[static_cast<size_t>(r.dev)].total;
+  }
+  repairs_.push_back(std::move(a));
+}
+
+std::vector<AnnotationRepair> Ledger::drain_repairs() {
+  std::vector<AnnotationRepair> out;
+  out.swap(repairs_);
+  return out;
 }
 
 int Ledger::gc(double confirmed_list_start, bool* need_relist) {
@@ -352,7 +386,9 @@ int Ledger::gc(double confirmed_list_start, bool* need_relist) {
   for (auto it = pods_.begin(); it != pods_.end();) {
     const PodRec& r = it->second;
     bool expire = false;
-    if (r.assumed && r.bound && r.deadline < now) {
+    if (r.assumed && r.bound && r.unannotated) {
+      // seen bound on its node (only the annotations are missing): never expired, the repair confirms it
+    } else if (r.assumed && r.bound && r.deadline < now) {
       // overdue: only a LIST begun after the binding was written can prove the binding absent
       if (confirmed_list_start > r.bound_at) {
         expire = true;

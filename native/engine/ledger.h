@@ -54,6 +54,16 @@ struct PodRec {
   double deadline = 0;   // expiry of an assumed+bound reservation
   bool accounted = false;
   int64_t held_on = -1;  // the hold device actually charged by account() (node may have changed since)
+  int64_t assume_ns = 0;      // ASSUME_TIME written by our bind
+  bool unannotated = false;   // observed bound to its node WITHOUT the allocation annotations we sent
+  bool repair_queued = false;
+};
+
+// A pod this extender bound whose allocation annotations the apiserver did not keep (an apiserver or
+// admission webhook that drops Binding.metadata.annotations): what to write back onto it.
+struct AnnotationRepair {
+  std::string uid, ns, name, node;
+  int64_t dev = -1, dev_total = -1, mem = 0, assume_ns = 0;
 };
 
 struct DevState {
@@ -78,6 +88,7 @@ struct Stats {
   uint64_t assume_ok = 0, assume_fail = 0, bind_ok = 0, bind_fail = 0;
   uint64_t expired = 0, overcommit_events = 0, pod_upserts = 0, pod_removes = 0;
   uint64_t expiry_deferred = 0;  // GC passes that kept an overdue reservation until a LIST could confirm it
+  uint64_t annotations_missing = 0;  // binds observed bound without the annotations they carried
 };
 
 class Ledger {
@@ -101,6 +112,8 @@ class Ledger {
   // yet confirmed by the informer).  The controller uses it to decide whether
   // an update event must be synced (pkg/gpushare/controller.go:257-305).
   int pod_state(const std::string& uid, int64_t* dev) const;
+  // Binds observed without their annotations since the last call (see AnnotationRepair)
+  std::vector<AnnotationRepair> drain_repairs();
 
   // ---- scheduling verbs ----
   Check check(const std::string& node, int64_t req) const;  // nodeinfo.go:113-137
@@ -180,6 +193,8 @@ class Ledger {
   Profile profile_;
   std::map<std::string, NodeState> nodes_;  // ordered: deterministic inspect
   std::unordered_map<std::string, PodRec> pods_;
+  std::vector<AnnotationRepair> repairs_;
+  void queue_repair(PodRec& r);
   Stats stats_;
   mutable introspect::ProfiledMutex mu_;  // every caller locks it; contention is exported to /debug/pprof/mutex
   std::unordered_map<std::string, PendingPod> pending_;

@@ -117,7 +117,9 @@ struct NativeServer::Loop {
   std::deque<std::tuple<uint64_t, std::string, bool>> done;
 };
 
-NativeServer::NativeServer(Ledger* ledger, ServerConfig cfg) : l_(ledger), cfg_(std::move(cfg)) {}
+NativeServer::NativeServer(Ledger* ledger, ServerConfig cfg) : l_(ledger), cfg_(std::move(cfg)) {
+  update_mode_.store(cfg_.update_mode);
+}
 
 NativeServer::~NativeServer() { stop(); }
 
@@ -628,7 +630,8 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
     record_failure(BindFailure{ns, name, uid, node, m});
     return bind_error_response(m);
   };
-  if (cfg_.update_mode) {
+  const bool update_mode = update_mode_.load();
+  if (update_mode) {
     // the reference's first call: write the annotations, guarded by the resourceVersion the scheduler saw;
     // on the optimistic-lock conflict retry once on the latest version (nodeinfo.go:150-168).  Not ordered:
     // a pod without spec.nodeName is no device-plugin candidate yet
@@ -661,7 +664,7 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
   json::append_quoted(&b, ns);
   b.append(",\"uid\":");
   json::append_quoted(&b, uid);
-  if (!cfg_.update_mode) b.append(",\"annotations\":{").append(ann).push_back('}');
+  if (!update_mode) b.append(",\"annotations\":{").append(ann).push_back('}');
   b.append("},\"target\":{\"apiVersion\":\"v1\",\"kind\":\"Node\",\"name\":");
   json::append_quoted(&b, node);
   b.append("}}");

@@ -90,6 +90,9 @@ class NativeServer {
   std::vector<BindFailure> drain_failures();
   // HA standby: a replica that does not hold the leader Lease refuses binds.
   void set_binds_enabled(bool on) { binds_enabled_.store(on); }
+  // switch to the reference's annotate-then-bind calls at run time (the apiserver dropped Binding annotations)
+  void set_update_mode(bool on) { update_mode_.store(on); }
+  bool update_mode() const { return update_mode_.load(); }
   bool binds_enabled() const { return binds_enabled_.load(); }
 
  private:
@@ -125,6 +128,7 @@ class NativeServer {
   int port_ = -1;
   std::atomic<bool> stop_{false};
   std::atomic<bool> binds_enabled_{true};
+  std::atomic<bool> update_mode_{false};
   std::vector<std::unique_ptr<Loop>> loops_;
   std::vector<std::thread> loop_threads_;
   std::vector<std::thread> pool_threads_;

@@ -354,13 +354,15 @@ struct Faults {
   double conflict_rate = 0, error_rate = 0, latency_ms = 0;
   int64_t drop_watch_after = 0, expire_watches = 0;
   bool hold_watches = false;
+  // an apiserver (or admission webhook) that does not copy Binding.metadata.annotations onto the pod
+  bool drop_binding_annotations = false;
   std::string json() const {
-    char b[320];
+    char b[384];
     std::snprintf(b, sizeof(b),
                   "{\"conflict_rate\":%g,\"error_rate\":%g,\"latency_ms\":%g,\"drop_watch_after\":%lld,"
-                  "\"expire_watches\":%lld,\"hold_watches\":%s}",
+                  "\"expire_watches\":%lld,\"hold_watches\":%s,\"drop_binding_annotations\":%s}",
                   conflict_rate, error_rate, latency_ms, (long long)drop_watch_after, (long long)expire_watches,
-                  hold_watches ? "true" : "false");
+                  hold_watches ? "true" : "false", drop_binding_annotations ? "true" : "false");
     return b;
   }
 };
@@ -1133,6 +1135,7 @@ class Server {
     jd::Value nv = cur->v;
     nv.member("spec").set("nodeName", jd::Value::string(target));
     const jd::Value* ann = bmd ? bmd->get("annotations") : nullptr;
+    if (faults_.drop_binding_annotations) ann = nullptr;
     if (ann && ann->is_obj() && !ann->o.empty()) {
       jd::Value& a = nv.member("metadata").member("annotations");
       for (const auto& m : ann->o) a.set(m.first, m.second);
@@ -1284,6 +1287,8 @@ class Server {
         inum("expire_watches", &faults_.expire_watches);
         const jd::Value* h = b.get("hold_watches");
         if (h && h->k == jd::Value::Bool) faults_.hold_watches = h->b;
+        const jd::Value* dba = b.get("drop_binding_annotations");
+        if (dba && dba->k == jd::Value::Bool) faults_.drop_binding_annotations = dba->b;
         const jd::Value* seed = b.get("seed");
         if (seed && seed->k == jd::Value::Num) rng().seed(static_cast<uint64_t>(std::atoll(seed->s.c_str())));
         const jd::Value* drop = b.get("drop_watches_now");

@@ -57,6 +57,8 @@ def test_bench_single_process_fake_devices():
     ref = {r["bind_mode"]: r for r in d["reference_client"]}
     assert 2.0 <= ref["update"]["pods_per_s"] <= 3.0
     assert ref["binding"]["pods_per_s"] > ref["update"]["pods_per_s"]
+    assert d["vs_baseline_same_condition"] == round(ref["binding"]["pods_per_s"] / 2.5, 2)
+    assert "bind_order_waits" in rows[("binding", 0)]
 
 
 @pytest.mark.slow
@@ -78,10 +80,9 @@ def test_bench_two_ranks_gloo(agent, extra):
 
 @pytest.mark.slow
 def test_bench_eight_ranks_gloo():
-    """The N=8 launch the driver uses on an 8 x MI355X node, rehearsed with 8 gloo ranks on fake devices."""
-    port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "8", "--steps", "2",
+    """The N=8 run of an 8 x MI355X node, rehearsed with 8 gloo ranks on fake devices -- started as
+    ``python bench.py --gpus 8`` with no launcher: bench.py starts torch.distributed.run as a child itself."""
+    cmd = [sys.executable, "bench.py", "--gpus", "8", "--steps", "2",
            "--warmup", "1", "--devices", "fake", "--agent", "node", "--sweep", "0"]
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])

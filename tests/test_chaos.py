@@ -219,3 +219,44 @@ def test_reservation_gc_never_frees_a_device_behind_a_stalled_watch(native_contr
             await c.close()
             await api.stop()
     asyncio.run(go())
+
+
+@pytest.mark.parametrize("impl", ["native", "python"])
+def test_binding_annotations_dropped_by_apiserver_self_heals(impl):
+    """``binding`` mode trusts kube-apiserver to copy Binding.metadata.annotations onto the pod.
+    An apiserver that drops them leaves pods bound without ``*_IDX``; the extender must notice, write the
+    annotations back (the reference's update call), switch to annotate-then-bind, and nothing may fail."""
+    async def go():
+        cl = Cluster(ALIYUN, [96] * 4, gpu=False, native=impl == "native", agent="plugin")
+        try:
+            await cl.start()
+            api = HttpClient(cl.api.url)
+            await api.request("POST", "/fake/faults", json.dumps({"drop_binding_annotations": True}).encode())
+            names = [f"d{i}" for i in range(10)]
+            sizes = [48, 24, 24, 48, 32, 16, 64, 8, 24, 40]
+            for n, g in zip(names, sizes):
+                await cl.create(n, g)
+            pods = await cl.wait(names, timeout=60)
+            used = [0] * 4
+            for p in pods.values():
+                ann = p["metadata"]["annotations"]
+                assert ALIYUN.annotation_idx in ann and ann[ALIYUN.annotation_assigned] == "true", ann
+                used[cl.device_of(p)] += int(ann[ALIYUN.annotation_pod])
+            assert all(u <= 96 for u in used), used
+            insp = await cl.inspect()
+            assert [d["usedGPU"] for d in insp["nodes"][0]["devs"]] == used
+            st = await cl.agent_stats()
+            assert st["allocate_errors"] == 0 and st["failed"] == 0, st
+            ext = HttpClient(cl.ext.url)
+            metrics = (await ext.request("GET", "/metrics")).body.decode()
+            await ext.close()
+            assert "gpushare_bind_mode_update 1.0" in metrics
+            assert 'gpushare_bind_annotation_repairs_total{result="ok"}' in metrics
+            # after the switch, binds write the annotations first: new pods arrive annotated without repair
+            await cl.create("late", 8)
+            late = (await cl.wait(["late"]))["late"]
+            assert ALIYUN.annotation_idx in late["metadata"]["annotations"]
+            await api.close()
+        finally:
+            await cl.close()
+    asyncio.run(go())
