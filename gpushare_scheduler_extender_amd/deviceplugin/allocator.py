@@ -51,7 +51,8 @@ class AllocateError(Exception):
 
 
 class CUPartitioner:
-    """Per-device ledger of compute units handed to pods as CU masks.
+    """Per-device ledger of compute units handed to pods as CU masks (the native ``_engine.CuPartitioner``,
+    ``native/engine/allocstate.cc``: the same code the compiled node agent runs).
 
     A partition is spread evenly over the XCDs (CU ``c`` of a 256-CU MI355X is
     logical CU ``c``; ROCr stripes logical CUs over XCDs/SEs, so contiguous
@@ -60,76 +61,39 @@ class CUPartitioner:
     take.
     """
 
-    def __init__(self, cu_count: int = 256, xcc_count: int = 8):
-        self.cu_count = cu_count
-        self.xcc_count = max(1, xcc_count)
-        self.owner: list[str | None] = [None] * cu_count
-        self._held: dict[str, list[int]] = {}
+    def __init__(self, cu_count: int = 256, xcc_count: int = 8, native_obj=None):
+        from ..core.engine import native  # noqa: PLC0415
 
-    def _order(self) -> list[int]:
-        per = self.cu_count // self.xcc_count
-        # round-robin over XCDs: xcc0 cu0, xcc1 cu0, ... (logical ids are xcc-major blocks of `per`)
-        return [x * per + i for i in range(per) for x in range(self.xcc_count)]
+        self._p = native_obj if native_obj is not None else native().CuPartitioner(cu_count, xcc_count)
+        self.cu_count = self._p.cu_count
+        self.xcc_count = self._p.xcc_count
 
     def allocate(self, uid: str, n: int) -> list[int]:
-        if n <= 0 or n > self.cu_count:
-            raise AllocateError(f"invalid CU partition size {n}")
-        mine = self._held.get(uid)
-        if mine:
-            return list(mine)
-        free = [c for c in self._order() if self.owner[c] is None]
-        if len(free) < n:
-            raise AllocateError(f"only {len(free)} CUs free, {n} requested")
-        got = sorted(free[:n])
-        for c in got:
-            self.owner[c] = uid
-        self._held[uid] = got
-        return list(got)
+        try:
+            return list(self._p.allocate(uid, int(n)))
+        except ValueError as e:
+            raise AllocateError(str(e)) from e
 
     def release(self, uid: str) -> int:
-        got = self._held.pop(uid, None)
-        if not got:
-            return 0
-        for c in got:
-            self.owner[c] = None
-        return len(got)
+        return self._p.release(uid)
 
     def adopt(self, uid: str, cus: list[int]) -> list[int]:
         """Record an existing partition (rebuilt from a pod's cu-mask annotation); returns the CUs that
         another pod already owned (left with their owner)."""
-        clash, got = [], []
-        for c in sorted(set(cus)):
-            if not 0 <= c < self.cu_count:
-                continue
-            if self.owner[c] is not None and self.owner[c] != uid:
-                clash.append(c)
-                continue
-            self.owner[c] = uid
-            got.append(c)
-        if got:
-            self._held[uid] = sorted(set(self._held.get(uid, [])) | set(got))
-        return clash
+        return list(self._p.adopt(uid, list(cus)))
 
     def swap_owners(self, a: str, b: str) -> None:
         """Exchange the partitions of pods ``a`` and ``b`` (either may hold none)."""
-        pa, pb = self._held.pop(a, None), self._held.pop(b, None)
-        for c in pa or []:
-            self.owner[c] = b
-        for c in pb or []:
-            self.owner[c] = a
-        if pa:
-            self._held[b] = pa
-        if pb:
-            self._held[a] = pb
+        self._p.swap_owners(a, b)
 
     def holds(self, uid: str) -> bool:
-        return uid in self._held
+        return self._p.holds(uid)
 
     def held(self) -> dict[str, list[int]]:
-        return {u: list(c) for u, c in self._held.items()}
+        return {u: list(c) for u, c in self._p.held().items()}
 
     def free_count(self) -> int:
-        return sum(1 for o in self.owner if o is None)
+        return self._p.free_count()
 
     @staticmethod
     def words(cus: list[int], cu_count: int = 256) -> list[int]:
@@ -141,16 +105,9 @@ class CUPartitioner:
     @staticmethod
     def ranges(cus: list[int]) -> str:
         """``0-7,32-39`` — the list syntax of ROCr's HSA_CU_MASK."""
-        cus = sorted(cus)
-        out = []
-        i = 0
-        while i < len(cus):
-            j = i
-            while j + 1 < len(cus) and cus[j + 1] == cus[j] + 1:
-                j += 1
-            out.append(f"{cus[i]}" if i == j else f"{cus[i]}-{cus[j]}")
-            i = j + 1
-        return ",".join(out)
+        from ..core.engine import native  # noqa: PLC0415
+
+        return native().cu_ranges(sorted(cus))
 
 
 def build_response(pod: dict, device: Device, container_units: int, profile: NamingProfile, *,

@@ -197,8 +197,7 @@ class GpuSharePlugin:
 
     def _record(self, rec: PodRec, ids, units: int, alloc: ContainerAllocation) -> AllocRecord:
         r = self.state.record(rec, ids, units, alloc.annotations.get("gpushare.amd.com/cu-mask", rec.cu_mask),
-                              self._next_aid(), time.time())
-        r.iso = alloc.iso
+                              self._next_aid(), time.time(), alloc.iso)
         self.persist_records()
         return r
 
@@ -233,9 +232,7 @@ class GpuSharePlugin:
         for d in data.get("records") or []:
             r = AllocRecord.from_dict(d)
             if r.holder in self.state.pods:
-                self.state.records[r.aid] = r
-                if r.ids:
-                    self.state.by_ids[r.ids] = r.aid
+                self.state.restore_record(r)
                 n += 1
         return n
 

@@ -81,7 +81,7 @@ class Reconciler:
                         self.stats["unknown_ids"] += 1
                         continue
                     if r.owner != pod.uid:
-                        r.owner = pod.uid
+                        self.state.set_owner(r.aid, pod.uid)
                         self.stats["records_owned"] += 1
                     if r.uid != pod.uid:
                         moves.append((pod.uid, r.aid))

@@ -1,8 +1,10 @@
-"""The device plugin's view of its node: Allocate candidates, CU partitions and multi-container progress.
+"""The device plugin's view of its node: Allocate candidates, CU partitions, multi-container progress, records.
 
-One implementation of the Allocate matching contract (``docs/designs/designs.md:93-103``,
-``docs/designs/sequence.jpg``), fed by a pod informer on ``spec.nodeName=<node>`` and used
-by both the gRPC plugin (:mod:`.plugin`) and the kubelet stand-in (:mod:`.agent`):
+The matching contract itself (``docs/designs/designs.md:93-103``, ``docs/designs/sequence.jpg``) has ONE
+implementation, in C++: ``native/engine/allocstate.{h,cc}`` (``_engine.AllocState``).  The compiled kubelet
+stand-in (``native/nodeagent``) uses it directly; this module is the shipped gRPC plugin's adapter to it.  It
+keeps the pod objects (the plugin answers with their annotations) and turns the native answers into
+:class:`PodRec` / :class:`AllocRecord` views; every decision is the native one:
 
 * **candidates** — Pending gpushare pods bound to this node whose ``ASSIGNED`` annotation is
   ``false`` and whose ``*_IDX`` names one of our GPUs, ordered by ``ASSUME_TIME`` (then
@@ -29,9 +31,9 @@ from __future__ import annotations
 import logging
 from dataclasses import dataclass, field
 
+from ..core.engine import native
 from ..models import pod as podutil
-from ..models.profile import (POD_CU_MASK_ANNOTATION, POD_HOLD_IDX_ANNOTATION, POD_HOLD_PARTNER_ANNOTATION,
-                              NamingProfile)
+from ..models.profile import POD_CU_MASK_ANNOTATION, POD_HOLD_PARTNER_ANNOTATION, NamingProfile
 from .allocator import CU_COUNT_ANNOTATION, AllocateError, CUPartitioner
 from .devices import Device
 
@@ -40,16 +42,13 @@ log = logging.getLogger("gsx.deviceplugin.state")
 
 def parse_cu_mask(words: str) -> list[int]:
     """``0x000000ff,0x00000000,...`` (GSX_CU_MASK / the cu-mask annotation) -> CU ids."""
-    out = []
-    for wi, w in enumerate(x for x in words.split(",") if x.strip()):
-        v = int(w, 16)
-        out.extend(32 * wi + b for b in range(32) if v >> b & 1)
-    return out
+    return list(native().parse_cu_words(words))
 
 
 @dataclass
 class AllocRecord:
-    """One Allocate: what the plugin handed out, for whom it built it, and (once kubelet says so) who got it."""
+    """One Allocate: what the plugin handed out, for whom it built it, and (once kubelet says so) who got it.
+    A snapshot of the native record; change it through :class:`AllocationState`."""
     aid: str
     ids: tuple  # kubelet's device IDs, sorted
     uid: str  # the pod whose annotations describe this allocation (the matched pod, until a move)
@@ -105,22 +104,49 @@ class PodRec:
         return self.phase in ("Pending", "")
 
 
+class _Inflight:
+    """Pods claimed by an Allocate whose ASSIGNED patch is in flight (the native set, set-like)."""
+
+    def __init__(self, core):
+        self._core = core
+
+    def add(self, uid: str):
+        self._core.set_inflight(uid, True)
+
+    def discard(self, uid: str):
+        self._core.set_inflight(uid, False)
+
+    def __contains__(self, uid: str) -> bool:
+        return self._core.inflight(uid)
+
+
 class AllocationState:
     def __init__(self, node: str, devices: dict[int, Device], profile: NamingProfile):
         self.node = node
         self.devices = devices
         self.profile = profile
-        self.cus = {i: CUPartitioner(d.cu_count, d.xcc_count) for i, d in devices.items()}
-        self.pods: dict[str, PodRec] = {}  # uid -> record (non-complete pods on this node)
-        self.partial: dict[str, list[int]] = {}  # uid -> container sizes not yet allocated
-        self.local_commits: set[str] = set()  # first container committed by this process
-        self.inflight: set[str] = set()  # claimed by an Allocate whose ASSIGNED patch is in flight
-        self.records: dict[str, AllocRecord] = {}  # aid -> record
-        self.by_ids: dict[tuple, str] = {}  # sorted device IDs -> aid
-        self.keys: dict[str, str] = {}  # ns/name -> uid of the live pod
+        self.core = native().AllocState(node, [(i, d.cu_count, d.xcc_count) for i, d in devices.items()])
+        self.cus = {i: CUPartitioner(native_obj=self.core.cus(i)) for i in devices}
+        self.inflight = _Inflight(self.core)
+        self._recs: dict[str, PodRec] = {}  # uid -> view of every pod the native state holds
         self.on_drop: list = []  # callbacks(record) when a record's holder is gone
-        self.stats = {"cu_released": 0, "cu_adopted": 0, "cu_conflicts": 0, "partial_released": 0,
-                      "pods_released": 0, "records_dropped": 0}
+
+    # ------------------------------------------------------------ views
+    @property
+    def pods(self) -> dict[str, PodRec]:
+        return self._recs
+
+    @property
+    def partial(self) -> dict[str, list[int]]:
+        return self.core.partial()
+
+    @property
+    def stats(self) -> dict:
+        return self.core.stats()
+
+    @property
+    def records(self) -> dict[str, AllocRecord]:
+        return {d["aid"]: AllocRecord.from_dict(d) for d in self.core.records()}
 
     # ------------------------------------------------------------ informer feed
     def _rec(self, pod: dict) -> PodRec:
@@ -147,33 +173,19 @@ class AllocationState:
         rec = self._rec(pod)
         if not rec.uid:
             return
-        prev = self.pods.get(rec.uid)
-        if prev is not None and prev.rv and rec.rv and _older(rec.rv, prev.rv):
+        ap = native().AllocPod()
+        ap.uid, ap.key, ap.namespace, ap.name, ap.rv = rec.uid, rec.key, rec.namespace, rec.name, rec.rv
+        ap.phase, ap.creation, ap.node = rec.phase, rec.creation, podutil.node_name(pod)
+        ap.dev, ap.request, ap.containers, ap.assume_time = rec.dev, rec.request, rec.containers, rec.assume_time
+        ap.assigned, ap.complete, ap.cu_count, ap.cu_mask = rec.assigned, rec.complete, rec.cu_count, rec.cu_mask
+        ap.hold_idx, ap.hold_partner = rec.hold_idx, rec.hold_partner
+        if not self.core.observe(ap):
             return  # a stale copy (e.g. a slow LIST racing the watch): never step back
-        if podutil.node_name(pod) != self.node or rec.request <= 0 or rec.complete:
-            self.release(rec.uid)
-            return
-        self.pods[rec.uid] = rec
-        self.keys[rec.key] = rec.uid
-        if rec.assigned != "true":
-            return
-        # an assigned pod: its CU partition is owned (rebuild after restart / adopt another agent's record)
-        if rec.cu_mask and rec.dev in self.cus and not self.cus[rec.dev].holds(rec.uid):
-            try:
-                cus = parse_cu_mask(rec.cu_mask)
-            except ValueError:
-                cus = []
-            clash = self.cus[rec.dev].adopt(rec.uid, cus)
-            self.stats["cu_adopted"] += 1
-            if clash:
-                self.stats["cu_conflicts"] += 1
-                log.warning("pod %s: CUs %s of GPU %d already owned by another pod", rec.key, clash[:8], rec.dev)
-        if not rec.pending:
-            if self.partial.pop(rec.uid, None) is not None:
-                self.stats["partial_released"] += 1
-        elif len(rec.containers) > 1 and rec.uid not in self.local_commits and rec.uid not in self.partial:
-            # restarted between containers: which ones were allocated is unknown, accept any of its sizes
-            self.partial[rec.uid] = list(rec.containers)
+        if self.core.has_pod(rec.uid):
+            self._recs[rec.uid] = rec
+        else:
+            self._recs.pop(rec.uid, None)
+        self._flush()
 
     def forget(self, pod: dict) -> None:
         """A deleted pod (watch DELETE or gone from a re-list)."""
@@ -181,155 +193,112 @@ class AllocationState:
 
     def resync(self, pods: list[dict]) -> None:
         """A complete LIST of this node's pods: anything we hold that is not in it is gone."""
-        seen = set()
+        seen = []
         for p in pods:
             self.observe(p)
-            seen.add(podutil.meta(p).get("uid", ""))
-        for uid in [u for u in self.holders() if u not in seen]:
-            self.release(uid)
+            seen.append(podutil.meta(p).get("uid", ""))
+        self.core.resync(seen)
+        self._prune()
 
     def holders(self) -> set[str]:
-        out = set(self.pods) | set(self.partial) | self.local_commits
-        for cp in self.cus.values():
-            out |= set(cp.held())
-        return out
+        return set(self.core.holders())
 
     def release(self, uid: str) -> None:
         if not uid:
             return
-        n = 0
-        for cp in self.cus.values():
-            n += cp.release(uid)
-        if n:
-            self.stats["cu_released"] += n
-        if self.partial.pop(uid, None) is not None:
-            self.stats["partial_released"] += 1
-        gone = self.pods.pop(uid, None)
-        if gone is not None:
-            self.stats["pods_released"] += 1
-            if self.keys.get(gone.key) == uid:
-                del self.keys[gone.key]
-        self.local_commits.discard(uid)
-        self.inflight.discard(uid)
-        for r in [r for r in self.records.values() if r.holder == uid]:
-            self.drop_record(r)
+        self.core.release(uid)
+        self._recs.pop(uid, None)
+        self._flush()
+
+    def _prune(self):
+        live = set(self.core.pod_uids())
+        for uid in [u for u in self._recs if u not in live]:
+            del self._recs[uid]
+        self._flush()
+
+    def _flush(self):
+        for d in self.core.take_dropped():
+            r = AllocRecord.from_dict(d)
+            for cb in self.on_drop:
+                cb(r)
 
     # ------------------------------------------------------------ Allocate
     def candidates(self) -> list[PodRec]:
-        out = [r for r in self.pods.values()
-               if r.pending and r.assigned == "false" and r.dev in self.devices and r.uid not in self.inflight]
-        out.sort(key=lambda r: r.order)
-        return out
+        return [self._recs[u] for u in self.core.candidates() if u in self._recs]
 
     def match(self, units: int) -> tuple[PodRec | None, bool]:
         """(pod, whole_pod) for an Allocate of ``units``: a whole pod of that size (earliest ASSUME_TIME),
         else a later container of a pod whose first container was allocated, else the first container
         of a multi-container pod that has a container of that size."""
-        cands = self.candidates()
-        for r in cands:
-            if r.request == units:
-                return r, True
-        for uid, left in self.partial.items():
-            r = self.pods.get(uid)
-            if r is not None and units in left and uid not in self.inflight:
-                return r, False
-        for r in cands:
-            if units in r.containers:
-                return r, False
-        return None, False
+        uid, whole = self.core.match(int(units))
+        return (self._recs.get(uid), whole) if uid else (None, False)
 
     def unannotated(self, units: int) -> bool:
         """A pending pod of this size bound to the node without any allocation annotation (``*_IDX``)."""
-        return any(r.pending and r.dev < 0 and r.assigned != "true" and r.request == units
-                   and r.uid not in self.inflight for r in self.pods.values())
+        return self.core.unannotated(int(units))
 
     def preferred_device(self, units: int) -> int:
-        rec, _ = self.match(units)
-        return rec.dev if rec is not None else -1
+        return self.core.preferred_device(int(units))
 
     def claim_cus(self, rec: PodRec) -> list[int] | None:
         if not rec.cu_count:
             return None
-        if rec.dev not in self.cus:
-            raise AllocateError(f"pod {rec.key} annotated with GPU {rec.dev}, not on this node")
-        return self.cus[rec.dev].allocate(rec.uid, rec.cu_count)
+        try:
+            return list(self.core.claim_cus(rec.uid))
+        except ValueError as e:
+            raise AllocateError(str(e)) from e
 
     def first_container_committed(self, rec: PodRec, units: int, whole: bool) -> None:
         """The ASSIGNED=true patch of ``rec`` succeeded for a container of ``units``."""
-        self.local_commits.add(rec.uid)
-        if not whole:
-            left = list(rec.containers)
-            left.remove(units)
-            if left:
-                self.partial[rec.uid] = left
+        self.core.first_container_committed(rec.uid, int(units), whole)
 
     def later_container_allocated(self, rec: PodRec, units: int) -> None:
-        left = self.partial.get(rec.uid)
-        if left is None:
-            return
-        left.remove(units)
-        if not left:
-            del self.partial[rec.uid]
+        self.core.later_container_allocated(rec.uid, int(units))
 
     # ------------------------------------------------------------ allocation records
-    def record(self, rec: PodRec, ids, units: int, cu_mask: str, aid: str, t: float = 0.0) -> AllocRecord:
+    def record(self, rec: PodRec, ids, units: int, cu_mask: str, aid: str, t: float = 0.0,
+               iso: str = "") -> AllocRecord:
         """An Allocate of ``ids`` was matched to ``rec`` (kubelet re-using the IDs of a finished pod replaces the
         older record)."""
-        key = tuple(sorted(ids))
-        old = self.by_ids.get(key) if key else None
-        if old is not None and old in self.records:
-            self.drop_record(self.records[old])
-        r = AllocRecord(aid=aid, ids=key, uid=rec.uid, dev=rec.dev, units=units, cu_mask=cu_mask, t=t)
-        self.records[aid] = r
-        if key:
-            self.by_ids[key] = aid
-        return r
+        d = self.core.record(rec.uid, list(ids), int(units), cu_mask or "", aid, t, iso)
+        self._flush()
+        return AllocRecord.from_dict(d)
+
+    def restore_record(self, r: AllocRecord) -> None:
+        self.core.add_record(r.to_dict())
 
     def drop_record(self, r: AllocRecord) -> None:
-        if self.records.pop(r.aid, None) is None:
-            return
-        if r.ids and self.by_ids.get(r.ids) == r.aid:
-            del self.by_ids[r.ids]
-        self.stats["records_dropped"] += 1
-        for cb in self.on_drop:
-            cb(r)
+        self.core.drop_record(r.aid)
+        self._flush()
 
     def record_for_ids(self, ids) -> AllocRecord | None:
-        aid = self.by_ids.get(tuple(sorted(ids)))
-        return self.records.get(aid) if aid else None
+        d = self.core.record_for_ids(list(ids))
+        return AllocRecord.from_dict(d) if d else None
+
+    def set_owner(self, aid: str, uid: str) -> None:
+        self.core.set_owner(aid, uid)
 
     def pod_by_key(self, key: str) -> PodRec | None:
-        uid = self.keys.get(key)
-        return self.pods.get(uid) if uid else None
+        for r in self._recs.values():
+            if r.key == key:
+                return r
+        return None
 
-    def move_records(self, p_uid: str, q_uid: str, r: AllocRecord) -> None:
+    def move_records(self, p_uid: str, q_uid: str, r) -> None:
         """After the annotations of P and Q were exchanged because P holds ``r`` (built for Q): ``r`` now
         describes P, and whatever described P describes Q.  The CU partitions follow the same exchange."""
-        for other in self.records.values():
-            if other is not r and other.uid == p_uid:
-                other.uid = q_uid
-        r.uid = p_uid
-        for cp in self.cus.values():
-            cp.swap_owners(p_uid, q_uid)
+        self.core.move_records(p_uid, q_uid, r.aid if isinstance(r, AllocRecord) else str(r))
 
     def snapshot(self) -> dict:
         """What ``/debug/state`` and the tests look at."""
         return {
             "pods": {r.key: {"uid": r.uid, "gpu": r.dev, "request": r.request, "assigned": r.assigned,
-                             "phase": r.phase} for r in self.pods.values()},
+                             "phase": r.phase} for r in self._recs.values()},
             "candidates": [r.key for r in self.candidates()],
-            "partial": {self.pods[u].key if u in self.pods else u: v for u, v in self.partial.items()},
-            "cu_partitions": {str(i): {self.pods[u].key if u in self.pods else u: len(c) for u, c in cp.held().items()}
+            "partial": {self._recs[u].key if u in self._recs else u: v for u, v in self.partial.items()},
+            "cu_partitions": {str(i): {self._recs[u].key if u in self._recs else u: len(c) for u, c in cp.held().items()}
                               for i, cp in self.cus.items()},
             "cu_free": {str(i): cp.free_count() for i, cp in self.cus.items()},
-            "records": len(self.records),
-            "stats": dict(self.stats),
+            "records": self.core.record_count(),
+            "native": True,
         }
-
-
-def _older(a: str, b: str) -> bool:
-    """resourceVersion a < b, when both are integers (the apiserver's are; compare nothing otherwise)."""
-    try:
-        return int(a) < int(b)
-    except ValueError:
-        return False

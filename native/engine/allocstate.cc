@@ -1,0 +1,495 @@
+#include "allocstate.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <tuple>
+
+#include "quantity.h"
+
+namespace gsx {
+
+// ---------------------------------------------------------------- CU partitions
+
+CuPartitioner::CuPartitioner(int cu, int xcc) : cu_(cu), xcc_(std::max(1, xcc)), owner_(static_cast<size_t>(cu)) {}
+
+bool CuPartitioner::allocate(const std::string& uid, int n, std::vector<int>* out, std::string* err) {
+  auto h = held_.find(uid);
+  if (h != held_.end() && !h->second.empty()) {
+    *out = h->second;
+    return true;
+  }
+  if (n <= 0 || n > cu_) {
+    *err = "invalid CU partition size " + std::to_string(n);
+    return false;
+  }
+  const int per = cu_ / xcc_;
+  std::vector<int> got;
+  for (int i = 0; i < per && static_cast<int>(got.size()) < n; ++i) {
+    for (int x = 0; x < xcc_ && static_cast<int>(got.size()) < n; ++x) {
+      int c = x * per + i;
+      if (owner_[static_cast<size_t>(c)].empty()) got.push_back(c);
+    }
+  }
+  if (static_cast<int>(got.size()) < n) {
+    int free = free_count();
+    *err = "only " + std::to_string(free) + " CUs free, " + std::to_string(n) + " requested";
+    return false;
+  }
+  std::sort(got.begin(), got.end());
+  for (int c : got) owner_[static_cast<size_t>(c)] = uid;
+  held_[uid] = got;
+  *out = got;
+  return true;
+}
+
+int CuPartitioner::release(const std::string& uid) {
+  auto h = held_.find(uid);
+  if (h == held_.end()) return 0;
+  int n = static_cast<int>(h->second.size());
+  for (int c : h->second) owner_[static_cast<size_t>(c)].clear();
+  held_.erase(h);
+  return n;
+}
+
+std::vector<int> CuPartitioner::adopt(const std::string& uid, const std::vector<int>& cus) {
+  std::vector<int> clash, got;
+  std::vector<int> sorted(cus);
+  std::sort(sorted.begin(), sorted.end());
+  sorted.erase(std::unique(sorted.begin(), sorted.end()), sorted.end());
+  for (int c : sorted) {
+    if (c < 0 || c >= cu_) continue;
+    std::string& o = owner_[static_cast<size_t>(c)];
+    if (!o.empty() && o != uid) {
+      clash.push_back(c);
+      continue;
+    }
+    o = uid;
+    got.push_back(c);
+  }
+  if (!got.empty()) {
+    std::vector<int>& mine = held_[uid];
+    mine.insert(mine.end(), got.begin(), got.end());
+    std::sort(mine.begin(), mine.end());
+    mine.erase(std::unique(mine.begin(), mine.end()), mine.end());
+  }
+  return clash;
+}
+
+void CuPartitioner::swap_owners(const std::string& a, const std::string& b) {
+  if (a == b) return;
+  std::vector<int> pa, pb;
+  auto ia = held_.find(a);
+  if (ia != held_.end()) {
+    pa = std::move(ia->second);
+    held_.erase(ia);
+  }
+  auto ib = held_.find(b);
+  if (ib != held_.end()) {
+    pb = std::move(ib->second);
+    held_.erase(ib);
+  }
+  for (int c : pa) owner_[static_cast<size_t>(c)] = b;
+  for (int c : pb) owner_[static_cast<size_t>(c)] = a;
+  if (!pa.empty()) held_[b] = std::move(pa);
+  if (!pb.empty()) held_[a] = std::move(pb);
+}
+
+std::vector<int> CuPartitioner::held_by(const std::string& uid) const {
+  auto h = held_.find(uid);
+  return h == held_.end() ? std::vector<int>() : h->second;
+}
+
+int CuPartitioner::free_count() const {
+  int n = 0;
+  for (const auto& o : owner_) n += o.empty() ? 1 : 0;
+  return n;
+}
+
+std::string cu_words(const std::vector<int>& cus, int cu_count) {
+  std::vector<uint32_t> w(static_cast<size_t>((cu_count + 31) / 32), 0);
+  for (int c : cus) {
+    if (c >= 0 && c < cu_count) w[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
+  }
+  std::string o;
+  char b[16];
+  for (size_t i = 0; i < w.size(); ++i) {
+    std::snprintf(b, sizeof(b), "%s0x%08x", i ? "," : "", w[i]);
+    o.append(b);
+  }
+  return o;
+}
+
+std::vector<int> parse_cu_words(const std::string& words) {
+  std::vector<int> out;
+  size_t i = 0;
+  int wi = 0;
+  while (i < words.size()) {
+    size_t j = words.find(',', i);
+    if (j == std::string::npos) j = words.size();
+    std::string tok = words.substr(i, j - i);
+    size_t a = tok.find_first_not_of(" \t"), b = tok.find_last_not_of(" \t");
+    if (a != std::string::npos) {
+      tok = tok.substr(a, b - a + 1);
+      char* end = nullptr;
+      unsigned long v = std::strtoul(tok.c_str(), &end, 16);
+      if (end == tok.c_str() || *end != '\0') throw std::invalid_argument("bad CU mask word: " + tok);
+      for (int bit = 0; bit < 32; ++bit) {
+        if (v >> bit & 1ul) out.push_back(32 * wi + bit);
+      }
+      ++wi;
+    }
+    i = j + 1;
+  }
+  return out;
+}
+
+std::string cu_ranges(const std::vector<int>& in) {
+  std::vector<int> cus(in);
+  std::sort(cus.begin(), cus.end());
+  std::string o;
+  size_t i = 0;
+  while (i < cus.size()) {
+    size_t j = i;
+    while (j + 1 < cus.size() && cus[j + 1] == cus[j] + 1) ++j;
+    if (!o.empty()) o.push_back(',');
+    o.append(std::to_string(cus[i]));
+    if (j > i) o.append("-").append(std::to_string(cus[j]));
+    i = j + 1;
+  }
+  return o;
+}
+
+// ---------------------------------------------------------------- pods from the informer
+
+bool parse_alloc_pod(const json::Doc& d, uint32_t pod, const Profile& p, AllocPod* out) {
+  PodView v;
+  if (!parse_pod(d, pod, p, &v)) return false;
+  out->uid = v.uid;
+  out->ns = v.ns;
+  out->name = v.name;
+  out->key = v.ns.empty() ? v.name : v.ns + "/" + v.name;
+  out->rv = v.rv;
+  out->phase = v.phase;
+  out->node = v.node;
+  out->dev = v.dev_idx;
+  out->request = v.request;
+  out->assume_time = v.assume_time;
+  out->dev_total = v.annot_dev_total;
+  out->complete = v.complete();
+  out->cu_mask = v.cu_mask;
+  out->hold_idx = v.hold_idx;
+  out->assigned.clear();
+  out->cu_count = 0;
+  out->hold_partner.clear();
+  int64_t an = d.path(pod, {"metadata", "annotations"});
+  if (an >= 0 && d.at(static_cast<uint32_t>(an)).type == json::T::Object) {
+    uint32_t a = static_cast<uint32_t>(an);
+    int64_t i = d.find(a, p.a_assigned);
+    if (i >= 0) out->assigned = d.str(static_cast<uint32_t>(i));
+    i = d.find(a, "gpushare.amd.com/cu-count");
+    if (i >= 0) out->cu_count = std::atoi(d.str(static_cast<uint32_t>(i)).c_str());
+    i = d.find(a, "gpushare.amd.com/hold-partner");
+    if (i >= 0) out->hold_partner = d.str(static_cast<uint32_t>(i));
+  }
+  int64_t ct = d.path(pod, {"metadata", "creationTimestamp"});
+  out->creation = ct >= 0 ? d.str(static_cast<uint32_t>(ct)) : std::string();
+  out->containers.clear();
+  int64_t cs = d.path(pod, {"spec", "containers"});
+  if (cs >= 0 && d.at(static_cast<uint32_t>(cs)).type == json::T::Array) {
+    uint32_t end = d.at(static_cast<uint32_t>(cs)).skip;
+    for (uint32_t c = static_cast<uint32_t>(cs) + 1; c < end; c = d.next(c)) {
+      if (d.at(c).type != json::T::Object) continue;
+      int64_t lim = d.path(c, {"resources", "limits"});
+      int64_t v2 = 0;
+      if (lim >= 0 && quantity_of(d, d.find(static_cast<uint32_t>(lim), p.resource), &v2) && v2 > 0) {
+        out->containers.push_back(v2);
+      }
+    }
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------- state
+
+namespace {
+bool older_rv(const std::string& a, const std::string& b) {
+  // resourceVersion a < b, when both are integers (the apiserver's are; compare nothing otherwise)
+  char* ea = nullptr;
+  char* eb = nullptr;
+  long long x = std::strtoll(a.c_str(), &ea, 10), y = std::strtoll(b.c_str(), &eb, 10);
+  if (a.empty() || b.empty() || *ea != '\0' || *eb != '\0') return false;
+  return x < y;
+}
+
+auto order_key(const AllocPod& p) { return std::tie(p.assume_time, p.creation, p.key); }
+}  // namespace
+
+AllocState::AllocState(std::string node, const std::vector<std::pair<int, std::pair<int, int>>>& devices)
+    : node_(std::move(node)) {
+  for (const auto& d : devices) cus_.emplace(d.first, CuPartitioner(d.second.first, d.second.second));
+}
+
+bool AllocState::observe(const AllocPod& p) {
+  if (p.uid.empty()) return false;
+  auto prev = pods_.find(p.uid);
+  if (prev != pods_.end() && older_rv(p.rv, prev->second.rv)) return false;  // a slow LIST racing the watch
+  if (p.node != node_ || p.request <= 0 || p.complete) {
+    release(p.uid);
+    return true;
+  }
+  pods_[p.uid] = p;
+  keys_[p.key] = p.uid;
+  if (p.assigned != "true") return true;
+  // an assigned pod owns its CU partition (rebuilt after a restart, or another agent's record)
+  auto cp = cus_.find(static_cast<int>(p.dev));
+  if (!p.cu_mask.empty() && cp != cus_.end() && !cp->second.holds(p.uid)) {
+    std::vector<int> cus;
+    try {
+      cus = parse_cu_words(p.cu_mask);
+    } catch (const std::exception&) {
+      cus.clear();
+    }
+    auto clash = cp->second.adopt(p.uid, cus);
+    stats_.cu_adopted++;
+    if (!clash.empty()) {
+      stats_.cu_conflicts++;
+      std::fprintf(stderr, "[gsx-allocstate] pod %s: %zu CU(s) of GPU %lld already owned by another pod\n",
+                   p.key.c_str(), clash.size(), static_cast<long long>(p.dev));
+    }
+  }
+  if (!p.pending()) {
+    if (partial_.erase(p.uid)) stats_.partial_released++;
+  } else if (p.containers.size() > 1 && !local_commits_.count(p.uid) && !partial_.count(p.uid)) {
+    partial_[p.uid] = p.containers;  // restarted between containers: accept any of its sizes
+  }
+  return true;
+}
+
+void AllocState::release(const std::string& uid) {
+  if (uid.empty()) return;
+  int n = 0;
+  for (auto& kv : cus_) n += kv.second.release(uid);
+  stats_.cu_released += static_cast<uint64_t>(n);
+  if (partial_.erase(uid)) stats_.partial_released++;
+  auto it = pods_.find(uid);
+  if (it != pods_.end()) {
+    stats_.pods_released++;
+    auto k = keys_.find(it->second.key);
+    if (k != keys_.end() && k->second == uid) keys_.erase(k);
+    pods_.erase(it);
+  }
+  local_commits_.erase(uid);
+  inflight_.erase(uid);
+  std::vector<std::string> gone;
+  for (const auto& kv : records_) {
+    if (kv.second.holder() == uid) gone.push_back(kv.first);
+  }
+  for (const auto& aid : gone) drop_record(aid);
+}
+
+std::vector<std::string> AllocState::holders() const {
+  std::unordered_set<std::string> out;
+  for (const auto& kv : pods_) out.insert(kv.first);
+  for (const auto& kv : partial_) out.insert(kv.first);
+  out.insert(local_commits_.begin(), local_commits_.end());
+  for (const auto& c : cus_) {
+    for (const auto& h : c.second.held()) out.insert(h.first);
+  }
+  return std::vector<std::string>(out.begin(), out.end());
+}
+
+void AllocState::resync(const std::unordered_set<std::string>& live) {
+  for (const auto& uid : holders()) {
+    if (!live.count(uid)) release(uid);
+  }
+}
+
+std::vector<const AllocPod*> AllocState::candidates() const {
+  std::vector<const AllocPod*> out;
+  for (const auto& kv : pods_) {
+    const AllocPod& r = kv.second;
+    if (r.pending() && r.assigned == "false" && has_device(r.dev) && !inflight_.count(r.uid)) out.push_back(&r);
+  }
+  std::sort(out.begin(), out.end(), [](const AllocPod* a, const AllocPod* b) { return order_key(*a) < order_key(*b); });
+  return out;
+}
+
+std::pair<const AllocPod*, bool> AllocState::match(int64_t units) {
+  auto cands = candidates();
+  for (const AllocPod* r : cands) {
+    if (r->request == units) {
+      stats_.matches++;
+      return {r, true};
+    }
+  }
+  const AllocPod* best = nullptr;
+  for (const auto& kv : partial_) {
+    auto it = pods_.find(kv.first);
+    if (it == pods_.end() || inflight_.count(kv.first)) continue;
+    if (std::find(kv.second.begin(), kv.second.end(), units) == kv.second.end()) continue;
+    if (!best || order_key(it->second) < order_key(*best)) best = &it->second;
+  }
+  if (best) {
+    stats_.matches++;
+    return {best, false};
+  }
+  for (const AllocPod* r : cands) {
+    if (std::find(r->containers.begin(), r->containers.end(), units) != r->containers.end()) {
+      stats_.matches++;
+      return {r, false};
+    }
+  }
+  stats_.match_misses++;
+  return {nullptr, false};
+}
+
+int64_t AllocState::preferred_device(int64_t units) {
+  auto m = match(units);
+  return m.first ? m.first->dev : -1;
+}
+
+bool AllocState::unannotated(int64_t units) const {
+  for (const auto& kv : pods_) {
+    const AllocPod& r = kv.second;
+    if (r.pending() && r.dev < 0 && r.assigned != "true" && r.request == units && !inflight_.count(r.uid)) return true;
+  }
+  return false;
+}
+
+bool AllocState::claim_cus(const std::string& uid, std::vector<int>* out, std::string* err) {
+  out->clear();
+  auto it = pods_.find(uid);
+  if (it == pods_.end()) {
+    *err = "pod " + uid + " is not on this node";
+    return false;
+  }
+  const AllocPod& p = it->second;
+  if (p.cu_count <= 0) return true;
+  auto cp = cus_.find(static_cast<int>(p.dev));
+  if (cp == cus_.end()) {
+    *err = "pod " + p.key + " annotated with GPU " + std::to_string(p.dev) + ", not on this node";
+    return false;
+  }
+  return cp->second.allocate(uid, p.cu_count, out, err);
+}
+
+void AllocState::set_inflight(const std::string& uid, bool on) {
+  if (on) {
+    inflight_.insert(uid);
+  } else {
+    inflight_.erase(uid);
+  }
+}
+
+void AllocState::first_container_committed(const std::string& uid, int64_t units, bool whole) {
+  local_commits_.insert(uid);
+  if (whole) return;
+  auto it = pods_.find(uid);
+  if (it == pods_.end()) return;
+  std::vector<int64_t> left = it->second.containers;
+  auto f = std::find(left.begin(), left.end(), units);
+  if (f != left.end()) left.erase(f);
+  if (!left.empty()) partial_[uid] = std::move(left);
+}
+
+void AllocState::later_container_allocated(const std::string& uid, int64_t units) {
+  auto it = partial_.find(uid);
+  if (it == partial_.end()) return;
+  auto f = std::find(it->second.begin(), it->second.end(), units);
+  if (f != it->second.end()) it->second.erase(f);
+  if (it->second.empty()) partial_.erase(it);
+}
+
+// ---------------------------------------------------------------- records
+
+AllocRecord& AllocState::record(const std::string& uid, const std::vector<std::string>& ids_in, int64_t units,
+                                const std::string& cu_mask, const std::string& aid, double t) {
+  std::vector<std::string> ids(ids_in);
+  std::sort(ids.begin(), ids.end());
+  if (!ids.empty()) {
+    auto old = by_ids_.find(ids);
+    if (old != by_ids_.end()) drop_record(old->second);  // kubelet re-used the IDs of a finished pod
+  }
+  AllocRecord r;
+  r.aid = aid;
+  r.ids = ids;
+  r.uid = uid;
+  auto p = pods_.find(uid);
+  r.dev = p != pods_.end() ? p->second.dev : -1;
+  r.units = units;
+  r.cu_mask = cu_mask;
+  r.t = t;
+  if (!ids.empty()) by_ids_[ids] = aid;
+  auto res = records_.insert_or_assign(aid, std::move(r));
+  return res.first->second;
+}
+
+void AllocState::add_record(AllocRecord r) {
+  std::sort(r.ids.begin(), r.ids.end());
+  if (!r.ids.empty()) by_ids_[r.ids] = r.aid;
+  std::string aid = r.aid;
+  records_.insert_or_assign(aid, std::move(r));
+}
+
+bool AllocState::drop_record(const std::string& aid) {
+  auto it = records_.find(aid);
+  if (it == records_.end()) return false;
+  auto b = by_ids_.find(it->second.ids);
+  if (b != by_ids_.end() && b->second == aid) by_ids_.erase(b);
+  stats_.records_dropped++;
+  dropped_.push_back(std::move(it->second));
+  records_.erase(it);
+  return true;
+}
+
+const AllocRecord* AllocState::record_for_ids(std::vector<std::string> ids) const {
+  std::sort(ids.begin(), ids.end());
+  auto b = by_ids_.find(ids);
+  if (b == by_ids_.end()) return nullptr;
+  auto it = records_.find(b->second);
+  return it == records_.end() ? nullptr : &it->second;
+}
+
+AllocRecord* AllocState::record_by_aid(const std::string& aid) {
+  auto it = records_.find(aid);
+  return it == records_.end() ? nullptr : &it->second;
+}
+
+void AllocState::set_owner(const std::string& aid, const std::string& owner) {
+  auto it = records_.find(aid);
+  if (it != records_.end()) it->second.owner = owner;
+}
+
+void AllocState::move_records(const std::string& p_uid, const std::string& q_uid, const std::string& aid) {
+  for (auto& kv : records_) {
+    if (kv.first != aid && kv.second.uid == p_uid) kv.second.uid = q_uid;
+  }
+  auto it = records_.find(aid);
+  if (it != records_.end()) it->second.uid = p_uid;
+  for (auto& kv : cus_) kv.second.swap_owners(p_uid, q_uid);
+}
+
+std::vector<AllocRecord> AllocState::take_dropped() {
+  std::vector<AllocRecord> out;
+  out.swap(dropped_);
+  return out;
+}
+
+const AllocPod* AllocState::pod(const std::string& uid) const {
+  auto it = pods_.find(uid);
+  return it == pods_.end() ? nullptr : &it->second;
+}
+
+const AllocPod* AllocState::pod_by_key(const std::string& key) const {
+  auto k = keys_.find(key);
+  return k == keys_.end() ? nullptr : pod(k->second);
+}
+
+CuPartitioner* AllocState::cus(int dev) {
+  auto it = cus_.find(dev);
+  return it == cus_.end() ? nullptr : &it->second;
+}
+
+}  // namespace gsx

@@ -1,0 +1,163 @@
+// The device plugin's allocation state: ONE implementation of the Allocate matching contract, used by the
+// shipped gRPC device plugin (Python, through the _engine binding: deviceplugin/state.py) and by the compiled
+// kubelet stand-in (native/nodeagent).
+//
+// The contract (reconstructed from docs/designs/designs.md:93-103 and docs/designs/sequence.jpg; the plugin
+// itself is not in the reference tree): kubelet asks for N fake device IDs and never says for
+// which pod; the plugin serves the earliest-ASSUME_TIME pending pod bound to its node whose request is N and
+// whose ASSIGNED annotation is "false", and flips ASSIGNED to "true" (the commit point).  On top of that:
+//
+//  * candidates: Pending pods of this node, ASSIGNED=false, *_IDX naming one of our GPUs, not claimed by an
+//    Allocate whose ASSIGNED patch is in flight; ordered by (ASSUME_TIME, creationTimestamp, ns/name);
+//  * multi-container pods: kubelet calls Allocate once per container.  The first container commits the pod;
+//    the remaining container sizes are kept until allocated ("partial").  After a restart the progress of an
+//    ASSIGNED=true Pending pod is unknown, so any of its sizes is accepted again;
+//  * CU partitions (the MPS stand-in, README.md:77): per GPU, owned per pod UID, spread round-robin over the
+//    XCDs; rebuilt from the gpushare.amd.com/cu-mask annotation of assigned pods, released when a pod
+//    completes or disappears;
+//  * allocation records: every Allocate with kubelet's device IDs, the pod it was matched to and what it
+//    handed out; deviceplugin/reconcile.py compares them with kubelet's PodResources record.
+//
+// Not thread-safe: callers serialise (the Python plugin runs on one event loop; the node agent holds its mutex).
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "json.h"
+#include "model.h"
+
+namespace gsx {
+
+// Per-device CU ledger.  A partition of n CUs takes the free CUs in round-robin XCD order (xcc0 cu0,
+// xcc1 cu0, ..., logical CU ids are xcc-major blocks of cu/xcc), so every pod keeps a share of every L2 slice.
+class CuPartitioner {
+ public:
+  explicit CuPartitioner(int cu = 256, int xcc = 8);
+  // the pod's partition (the same one again if it already holds one); false + *err when it does not fit
+  bool allocate(const std::string& uid, int n, std::vector<int>* out, std::string* err);
+  int release(const std::string& uid);  // CUs freed
+  // an existing partition (from a pod's cu-mask annotation); CUs another pod owns stay with it: returns them
+  std::vector<int> adopt(const std::string& uid, const std::vector<int>& cus);
+  void swap_owners(const std::string& a, const std::string& b);
+  bool holds(const std::string& uid) const { return held_.count(uid) != 0; }
+  std::vector<int> held_by(const std::string& uid) const;
+  const std::unordered_map<std::string, std::vector<int>>& held() const { return held_; }
+  int free_count() const;
+  int cu_count() const { return cu_; }
+  int xcc_count() const { return xcc_; }
+
+ private:
+  int cu_, xcc_;
+  std::vector<std::string> owner_;
+  std::unordered_map<std::string, std::vector<int>> held_;
+};
+
+std::string cu_words(const std::vector<int>& cus, int cu_count);  // "0x000000ff,0x00000000,..."
+std::vector<int> parse_cu_words(const std::string& words);
+std::string cu_ranges(const std::vector<int>& cus);  // "0-7,32-39" (HSA_CU_MASK list syntax)
+
+struct AllocPod {
+  std::string uid, key, ns, name, rv, phase, creation, node;
+  int64_t dev = -1;           // *_IDX annotation
+  int64_t request = 0;        // sum of container limits
+  std::vector<int64_t> containers;  // container limits > 0, in spec order
+  int64_t assume_time = -1;
+  int64_t dev_total = -1;     // *_DEV annotation
+  std::string assigned;       // ASSIGNED annotation value ("" absent)
+  bool complete = false;
+  int cu_count = 0;           // gpushare.amd.com/cu-count
+  std::string cu_mask;        // gpushare.amd.com/cu-mask
+  int64_t hold_idx = -1;      // gpushare.amd.com/hold-idx
+  std::string hold_partner;   // gpushare.amd.com/hold-partner
+  bool pending() const { return phase == "Pending" || phase.empty(); }
+};
+
+// Build an AllocPod from a pod object on a JSON tape (the node agent's informer).
+bool parse_alloc_pod(const json::Doc& d, uint32_t pod, const Profile& p, AllocPod* out);
+
+struct AllocRecord {
+  std::string aid;
+  std::vector<std::string> ids;  // kubelet's device IDs, sorted
+  std::string uid;               // the pod whose annotations describe this allocation
+  int64_t dev = -1, units = 0;
+  std::string cu_mask;
+  std::string owner;             // the pod kubelet gave the IDs to ("" until PodResources said so)
+  double t = 0;
+  std::string iso;               // isolation directory key the container's mounts point at
+  const std::string& holder() const { return owner.empty() ? uid : owner; }
+};
+
+struct AllocStats {
+  uint64_t cu_released = 0, cu_adopted = 0, cu_conflicts = 0, partial_released = 0, pods_released = 0,
+           records_dropped = 0, matches = 0, match_misses = 0;
+};
+
+class AllocState {
+ public:
+  AllocState(std::string node, const std::vector<std::pair<int, std::pair<int, int>>>& devices);  // idx -> (cu, xcc)
+
+  // ---- informer feed
+  // An added / updated pod.  Returns false if ignored as a stale copy (older resourceVersion).
+  bool observe(const AllocPod& p);
+  void release(const std::string& uid);  // completed / deleted
+  // A complete LIST of this node's pods (already observed): anything held that is not in `live` is gone.
+  void resync(const std::unordered_set<std::string>& live);
+  std::vector<std::string> holders() const;
+
+  // ---- Allocate
+  std::vector<const AllocPod*> candidates() const;
+  // (pod, whole_pod) for an Allocate of `units`: a whole pod of that size (earliest ASSUME_TIME), else a later
+  // container of a pod whose first container was allocated, else the first container of a multi-container
+  // pod that has a container of that size.
+  std::pair<const AllocPod*, bool> match(int64_t units);
+  int64_t preferred_device(int64_t units);
+  bool unannotated(int64_t units) const;
+  bool claim_cus(const std::string& uid, std::vector<int>* out, std::string* err);
+  void set_inflight(const std::string& uid, bool on);
+  bool inflight(const std::string& uid) const { return inflight_.count(uid) != 0; }
+  void first_container_committed(const std::string& uid, int64_t units, bool whole);
+  void later_container_allocated(const std::string& uid, int64_t units);
+
+  // ---- allocation records
+  AllocRecord& record(const std::string& uid, const std::vector<std::string>& ids, int64_t units,
+                      const std::string& cu_mask, const std::string& aid, double t);
+  void add_record(AllocRecord r);  // restored from a checkpoint
+  bool drop_record(const std::string& aid);
+  const AllocRecord* record_for_ids(std::vector<std::string> ids) const;
+  AllocRecord* record_by_aid(const std::string& aid);
+  void set_owner(const std::string& aid, const std::string& owner);
+  // After the annotations of P and Q were exchanged because P holds `aid` (built for Q): that record now
+  // describes P, whatever described P describes Q, and the CU partitions follow.
+  void move_records(const std::string& p_uid, const std::string& q_uid, const std::string& aid);
+  const std::map<std::string, AllocRecord>& records() const { return records_; }
+  std::vector<AllocRecord> take_dropped();  // records dropped since the last call (isolation cleanup)
+
+  const AllocPod* pod(const std::string& uid) const;
+  const AllocPod* pod_by_key(const std::string& key) const;
+  const std::unordered_map<std::string, AllocPod>& pods() const { return pods_; }
+  const std::unordered_map<std::string, std::vector<int64_t>>& partial() const { return partial_; }
+  CuPartitioner* cus(int dev);
+  const std::map<int, CuPartitioner>& all_cus() const { return cus_; }
+  bool has_device(int64_t dev) const { return cus_.count(static_cast<int>(dev)) != 0; }
+  const AllocStats& stats() const { return stats_; }
+  const std::string& node() const { return node_; }
+
+ private:
+  std::string node_;
+  std::map<int, CuPartitioner> cus_;
+  std::unordered_map<std::string, AllocPod> pods_;        // uid -> non-complete pods on this node
+  std::unordered_map<std::string, std::string> keys_;     // ns/name -> uid
+  std::unordered_map<std::string, std::vector<int64_t>> partial_;  // uid -> container sizes not yet allocated
+  std::unordered_set<std::string> local_commits_, inflight_;
+  std::map<std::string, AllocRecord> records_;            // aid -> record
+  std::map<std::vector<std::string>, std::string> by_ids_;
+  std::vector<AllocRecord> dropped_;
+  AllocStats stats_;
+};
+
+}  // namespace gsx

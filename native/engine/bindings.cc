@@ -7,6 +7,7 @@
 
 #include <memory>
 
+#include "allocstate.h"
 #include "introspect.h"
 #include "ledger.h"
 #include "quantity.h"
@@ -774,6 +775,192 @@ PYBIND11_MODULE(_engine, m) {
       .def("release", &PyPodRuntime::release)
       .def("verify", &PyPodRuntime::verify)
       .def("stats", &PyPodRuntime::stats);
+
+
+  // ---- the device plugin's allocation state (allocstate.h): one implementation for the gRPC plugin and the
+  // compiled node agent
+  py::class_<CuPartitioner>(m, "CuPartitioner")
+      .def(py::init<int, int>(), py::arg("cu_count") = 256, py::arg("xcc_count") = 8)
+      .def("allocate",
+           [](CuPartitioner& c, const std::string& uid, int n) {
+             std::vector<int> out;
+             std::string err;
+             if (!c.allocate(uid, n, &out, &err)) throw py::value_error(err);
+             return out;
+           })
+      .def("release", &CuPartitioner::release)
+      .def("adopt", &CuPartitioner::adopt)
+      .def("swap_owners", &CuPartitioner::swap_owners)
+      .def("holds", &CuPartitioner::holds)
+      .def("held_by", &CuPartitioner::held_by)
+      .def("held", [](const CuPartitioner& c) {
+        py::dict d;
+        for (const auto& kv : c.held()) d[py::str(kv.first)] = kv.second;
+        return d;
+      })
+      .def("free_count", &CuPartitioner::free_count)
+      .def_property_readonly("cu_count", &CuPartitioner::cu_count)
+      .def_property_readonly("xcc_count", &CuPartitioner::xcc_count);
+  m.def("cu_words", &cu_words);
+  m.def("parse_cu_words", [](const std::string& w) {
+    try {
+      return parse_cu_words(w);
+    } catch (const std::invalid_argument& e) {
+      throw py::value_error(e.what());
+    }
+  });
+  m.def("cu_ranges", &cu_ranges);
+
+  py::class_<AllocPod>(m, "AllocPod")
+      .def(py::init<>())
+      .def_readwrite("uid", &AllocPod::uid)
+      .def_readwrite("key", &AllocPod::key)
+      .def_readwrite("namespace", &AllocPod::ns)
+      .def_readwrite("name", &AllocPod::name)
+      .def_readwrite("rv", &AllocPod::rv)
+      .def_readwrite("phase", &AllocPod::phase)
+      .def_readwrite("creation", &AllocPod::creation)
+      .def_readwrite("node", &AllocPod::node)
+      .def_readwrite("dev", &AllocPod::dev)
+      .def_readwrite("request", &AllocPod::request)
+      .def_readwrite("containers", &AllocPod::containers)
+      .def_readwrite("assume_time", &AllocPod::assume_time)
+      .def_readwrite("dev_total", &AllocPod::dev_total)
+      .def_readwrite("assigned", &AllocPod::assigned)
+      .def_readwrite("complete", &AllocPod::complete)
+      .def_readwrite("cu_count", &AllocPod::cu_count)
+      .def_readwrite("cu_mask", &AllocPod::cu_mask)
+      .def_readwrite("hold_idx", &AllocPod::hold_idx)
+      .def_readwrite("hold_partner", &AllocPod::hold_partner)
+      .def_property_readonly("pending", &AllocPod::pending);
+
+  auto rec_dict = [](const AllocRecord& r) {
+    py::dict d;
+    d["aid"] = r.aid;
+    d["ids"] = r.ids;
+    d["uid"] = r.uid;
+    d["dev"] = r.dev;
+    d["units"] = r.units;
+    d["cu_mask"] = r.cu_mask;
+    d["owner"] = r.owner;
+    d["t"] = r.t;
+    d["iso"] = r.iso;
+    return d;
+  };
+  py::class_<AllocState>(m, "AllocState")
+      .def(py::init([](const std::string& node, const std::vector<std::tuple<int, int, int>>& devs) {
+             std::vector<std::pair<int, std::pair<int, int>>> d;
+             for (const auto& t : devs) d.push_back({std::get<0>(t), {std::get<1>(t), std::get<2>(t)}});
+             return new AllocState(node, d);
+           }),
+           py::arg("node"), py::arg("devices"))
+      .def("observe", &AllocState::observe)
+      .def("release", &AllocState::release)
+      .def("resync", [](AllocState& s, const std::vector<std::string>& live) {
+        s.resync(std::unordered_set<std::string>(live.begin(), live.end()));
+      })
+      .def("holders", &AllocState::holders)
+      .def("has_pod", [](const AllocState& s, const std::string& uid) { return s.pod(uid) != nullptr; })
+      .def("pod_uids", [](const AllocState& s) {
+        std::vector<std::string> out;
+        for (const auto& kv : s.pods()) out.push_back(kv.first);
+        return out;
+      })
+      .def("candidates", [](const AllocState& s) {
+        std::vector<std::string> out;
+        for (const AllocPod* p : s.candidates()) out.push_back(p->uid);
+        return out;
+      })
+      .def("match", [](AllocState& s, int64_t units) {
+        auto m = s.match(units);
+        return py::make_tuple(m.first ? py::object(py::str(m.first->uid)) : py::object(py::none()), m.second);
+      })
+      .def("preferred_device", &AllocState::preferred_device)
+      .def("unannotated", &AllocState::unannotated)
+      .def("claim_cus",
+           [](AllocState& s, const std::string& uid) {
+             std::vector<int> out;
+             std::string err;
+             if (!s.claim_cus(uid, &out, &err)) throw py::value_error(err);
+             return out;
+           })
+      .def("set_inflight", &AllocState::set_inflight)
+      .def("inflight", &AllocState::inflight)
+      .def("first_container_committed", &AllocState::first_container_committed)
+      .def("later_container_allocated", &AllocState::later_container_allocated)
+      .def("partial", [](const AllocState& s) {
+        py::dict d;
+        for (const auto& kv : s.partial()) d[py::str(kv.first)] = kv.second;
+        return d;
+      })
+      .def("record",
+           [rec_dict](AllocState& s, const std::string& uid, const std::vector<std::string>& ids, int64_t units,
+                      const std::string& cu_mask, const std::string& aid, double t, const std::string& iso) {
+             AllocRecord& r = s.record(uid, ids, units, cu_mask, aid, t);
+             r.iso = iso;
+             return rec_dict(r);
+           },
+           py::arg("uid"), py::arg("ids"), py::arg("units"), py::arg("cu_mask"), py::arg("aid"), py::arg("t") = 0.0,
+           py::arg("iso") = std::string())
+      .def("add_record",
+           [](AllocState& s, const py::dict& d) {
+             AllocRecord r;
+             r.aid = d["aid"].cast<std::string>();
+             r.ids = d.contains("ids") ? d["ids"].cast<std::vector<std::string>>() : std::vector<std::string>();
+             r.uid = d.contains("uid") ? d["uid"].cast<std::string>() : std::string();
+             r.dev = d.contains("dev") ? d["dev"].cast<int64_t>() : -1;
+             r.units = d.contains("units") ? d["units"].cast<int64_t>() : 0;
+             r.cu_mask = d.contains("cu_mask") ? d["cu_mask"].cast<std::string>() : std::string();
+             r.owner = d.contains("owner") ? d["owner"].cast<std::string>() : std::string();
+             r.t = d.contains("t") ? d["t"].cast<double>() : 0.0;
+             r.iso = d.contains("iso") ? d["iso"].cast<std::string>() : std::string();
+             s.add_record(std::move(r));
+           })
+      .def("drop_record", &AllocState::drop_record)
+      .def("record_for_ids",
+           [rec_dict](const AllocState& s, const std::vector<std::string>& ids) -> py::object {
+             const AllocRecord* r = s.record_for_ids(ids);
+             return r ? py::object(rec_dict(*r)) : py::object(py::none());
+           })
+      .def("get_record",
+           [rec_dict](AllocState& s, const std::string& aid) -> py::object {
+             AllocRecord* r = s.record_by_aid(aid);
+             return r ? py::object(rec_dict(*r)) : py::object(py::none());
+           })
+      .def("set_owner", &AllocState::set_owner)
+      .def("move_records", &AllocState::move_records)
+      .def("records",
+           [rec_dict](const AllocState& s) {
+             py::list out;
+             for (const auto& kv : s.records()) out.append(rec_dict(kv.second));
+             return out;
+           })
+      .def("record_count", [](const AllocState& s) { return s.records().size(); })
+      .def("take_dropped",
+           [rec_dict](AllocState& s) {
+             py::list out;
+             for (const auto& r : s.take_dropped()) out.append(rec_dict(r));
+             return out;
+           })
+      .def("cus", [](AllocState& s, int dev) { return s.cus(dev); }, py::return_value_policy::reference_internal)
+      .def("devices", [](const AllocState& s) {
+        std::vector<int> out;
+        for (const auto& kv : s.all_cus()) out.push_back(kv.first);
+        return out;
+      })
+      .def("stats", [](const AllocState& s) {
+        const AllocStats& st = s.stats();
+        py::dict d;
+        d["cu_released"] = st.cu_released;
+        d["cu_adopted"] = st.cu_adopted;
+        d["cu_conflicts"] = st.cu_conflicts;
+        d["partial_released"] = st.partial_released;
+        d["pods_released"] = st.pods_released;
+        d["records_dropped"] = st.records_dropped;
+        d["matches"] = st.matches;
+        d["match_misses"] = st.match_misses;
+        return d;
+      });
 
   m.def("parse_quantity", [](const std::string& s) {
     int64_t v;

@@ -4,8 +4,6 @@
 
 namespace gsx {
 
-namespace {
-
 bool quantity_of(const json::Doc& d, int64_t idx, int64_t* out) {
   if (idx < 0) return false;
   const json::Val& v = d.at(static_cast<uint32_t>(idx));
@@ -18,6 +16,8 @@ bool quantity_of(const json::Doc& d, int64_t idx, int64_t* out) {
   }
   return false;
 }
+
+namespace {
 
 std::string str_at(const json::Doc& d, int64_t idx) {
   if (idx < 0) return std::string();

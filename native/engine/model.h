@@ -70,6 +70,9 @@ bool parse_pod(const json::Doc& d, uint32_t pod, const Profile& p, PodView* out)
 // Same for a node object.
 bool parse_node(const json::Doc& d, uint32_t node, const Profile& p, NodeView* out);
 
+// A resource.Quantity (string or number) at tape index idx (-1: absent) as an integer (Quantity.Value()).
+bool quantity_of(const json::Doc& d, int64_t idx, int64_t* out);
+
 // Sum of container limits[name] of a pod object (init containers ignored,
 // exactly like pod.go:146-155).
 int64_t pod_limits_sum(const json::Doc& d, uint32_t pod, const std::string& name);

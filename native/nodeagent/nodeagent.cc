@@ -20,6 +20,8 @@
 // the device plugin / the benchmark.  Control endpoints:
 //   GET /v1/stats, GET /v1/allocations/<uid> (container env of the Allocate).
 //
+// The matching decision is AllocState (native/engine/allocstate.h), shared with the shipped gRPC device plugin.
+//
 //   gsx-nodeagent --apiserver URL --node NAME [--profile P] [--unit GiB]
 //                 [--workers N] [--no-verify] [--port-file F]
 #include <signal.h>
@@ -43,6 +45,7 @@
 #include <unordered_set>
 #include <vector>
 
+#include "allocstate.h"
 #include "apiclient.h"
 #include "ctlserver.h"
 #include "informer.h"
@@ -56,7 +59,6 @@ namespace {
 
 const char* kDevInfoAnn = "gpushare.amd.com/devices";
 const char* kEndpointsAnn = "gpushare.amd.com/runtime-endpoints";
-const char* kCuCountAnn = "gpushare.amd.com/cu-count";
 const char* kCuMaskAnn = "gpushare.amd.com/cu-mask";
 const char* kAssignTimeAnn = "gpushare.amd.com/assign-time";
 
@@ -80,130 +82,9 @@ struct Device {
   std::string endpoint;
 };
 
-// Per-device CU ledger (deviceplugin/allocator.py CUPartitioner): partitions
-// are spread round-robin over the XCDs so each pod keeps every L2 slice.
-class CuPartitioner {
- public:
-  CuPartitioner(int cu = 256, int xcc = 8) : cu_(cu), xcc_(std::max(1, xcc)), owner_(static_cast<size_t>(cu)) {}
-  bool allocate(const std::string& uid, int n, std::vector<int>* out, std::string* err) {
-    auto h = held_.find(uid);
-    if (h != held_.end()) {
-      *out = h->second;
-      return true;
-    }
-    if (n <= 0 || n > cu_) {
-      *err = "invalid CU partition size " + std::to_string(n);
-      return false;
-    }
-    int per = cu_ / xcc_;
-    std::vector<int> got;
-    for (int i = 0; i < per && static_cast<int>(got.size()) < n; ++i) {
-      for (int x = 0; x < xcc_ && static_cast<int>(got.size()) < n; ++x) {
-        int c = x * per + i;
-        if (owner_[static_cast<size_t>(c)].empty()) got.push_back(c);
-      }
-    }
-    if (static_cast<int>(got.size()) < n) {
-      *err = "only " + std::to_string(got.size()) + " CUs free, " + std::to_string(n) + " requested";
-      return false;
-    }
-    std::sort(got.begin(), got.end());
-    for (int c : got) owner_[static_cast<size_t>(c)] = uid;
-    held_[uid] = got;
-    *out = got;
-    return true;
-  }
-  void release(const std::string& uid) {
-    auto h = held_.find(uid);
-    if (h == held_.end()) return;
-    for (int c : h->second) owner_[static_cast<size_t>(c)].clear();
-    held_.erase(h);
-  }
-  // An existing partition (a pod's cu-mask annotation, e.g. after a restart); CUs another pod owns stay
-  // with it.  Returns how many clashed (deviceplugin/allocator.py CUPartitioner.adopt).
-  int adopt(const std::string& uid, const std::vector<int>& cus) {
-    int clash = 0;
-    std::vector<int>& mine = held_[uid];
-    for (int c : cus) {
-      if (c < 0 || c >= cu_) continue;
-      std::string& o = owner_[static_cast<size_t>(c)];
-      if (!o.empty() && o != uid) {
-        ++clash;
-        continue;
-      }
-      if (o.empty()) mine.push_back(c);
-      o = uid;
-    }
-    std::sort(mine.begin(), mine.end());
-    if (mine.empty()) held_.erase(uid);
-    return clash;
-  }
-  bool holds(const std::string& uid) const { return held_.count(uid) != 0; }
-  int cu_count() const { return cu_; }
-
- private:
-  int cu_, xcc_;
-  std::vector<std::string> owner_;
-  std::unordered_map<std::string, std::vector<int>> held_;
-};
-
-std::string cu_words(const std::vector<int>& cus, int cu_count) {
-  std::vector<uint32_t> w(static_cast<size_t>((cu_count + 31) / 32), 0);
-  for (int c : cus) w[static_cast<size_t>(c / 32)] |= 1u << (c % 32);
-  std::string o;
-  char b[16];
-  for (size_t i = 0; i < w.size(); ++i) {
-    std::snprintf(b, sizeof(b), "%s0x%08x", i ? "," : "", w[i]);
-    o.append(b);
-  }
-  return o;
-}
-
-std::vector<int> parse_cu_words(const std::string& words) {
-  std::vector<int> out;
-  size_t i = 0;
-  int wi = 0;
-  while (i < words.size()) {
-    size_t j = words.find(',', i);
-    if (j == std::string::npos) j = words.size();
-    unsigned long v = std::strtoul(words.substr(i, j - i).c_str(), nullptr, 16);
-    for (int b = 0; b < 32; ++b) {
-      if (v >> b & 1ul) out.push_back(32 * wi + b);
-    }
-    ++wi;
-    i = j + 1;
-  }
-  return out;
-}
-
-std::string cu_ranges(const std::vector<int>& cus) {
-  std::string o;
-  size_t i = 0;
-  while (i < cus.size()) {
-    size_t j = i;
-    while (j + 1 < cus.size() && cus[j + 1] == cus[j] + 1) ++j;
-    if (!o.empty()) o.push_back(',');
-    o.append(std::to_string(cus[i]));
-    if (j > i) o.append("-").append(std::to_string(cus[j]));
-    i = j + 1;
-  }
-  return o;
-}
-
-struct AgentPod {
-  std::string uid, ns, name, rv, phase;
-  int64_t dev_idx = -1, request = 0, assume_time = -1, dev_total = 0;
-  int assigned = -1;
-  bool complete = false;
-  int cu_count = 0;
-  std::string cu_mask;
-};
-
-struct Cand {
-  int64_t assume_time;
-  std::string key;
-  int64_t units;
-};
+// The Allocate matching, CU partitions and multi-container progress are the device plugin's own
+// (native/engine/allocstate.h, the same code deviceplugin/state.py runs): this agent only plays kubelet
+// and the container runtime around it.
 
 class Agent {
  public:
@@ -242,13 +123,14 @@ class Agent {
     ReflectorHandler h;
     h.on_list = [this](const ListView& lv) {
       std::lock_guard<std::mutex> g(mu_);
-      std::unordered_set<std::string> seen;
-      for (size_t k = 0; k < lv.size(); ++k) seen.insert(on_pod_locked(lv.doc(k), lv.obj(k)));
+      std::unordered_set<std::string> seen, live;
+      for (size_t k = 0; k < lv.size(); ++k) seen.insert(on_pod_locked(lv.doc(k), lv.obj(k), &live));
       std::vector<std::string> gone;
-      for (auto& kv : pods_) {
+      for (auto& kv : keys_) {
         if (!seen.count(kv.first)) gone.push_back(kv.first);
       }
       for (auto& k : gone) on_delete_locked(k);
+      state_->resync(live);
       wake_locked();
     };
     h.on_event = [this](Ev ev, const json::Doc& d, uint32_t obj) {
@@ -258,7 +140,7 @@ class Agent {
         parse_pod(d, obj, p_, &v);
         on_delete_locked(v.ns + "/" + v.name);
       } else {
-        on_pod_locked(d, obj);
+        on_pod_locked(d, obj, nullptr);
       }
       wake_locked();
     };
@@ -362,8 +244,10 @@ class Agent {
       devs[d.index] = d;
     }
     if (devs.empty()) return false;
+    std::vector<std::pair<int, std::pair<int, int>>> cu_layout;
+    for (auto& kv : devs) cu_layout.push_back({kv.first, {kv.second.cu, kv.second.xcc}});
+    state_ = std::make_unique<AllocState>(node_, cu_layout);
     for (auto& kv : devs) {
-      cus_.emplace(kv.first, CuPartitioner(kv.second.cu, kv.second.xcc));
       ApiConfig rc;
       rc.server = kv.second.endpoint;
       rc.timeout_s = 60;
@@ -374,56 +258,21 @@ class Agent {
   }
 
   // ---------------------------------------------------------------- informer handlers (agent.py _on_pod)
-  std::string on_pod_locked(const json::Doc& d, uint32_t obj) {
-    PodView v;
-    parse_pod(d, obj, p_, &v);
-    std::string key = v.ns + "/" + v.name;
-    AgentPod& ap = pods_[key];
-    ap.uid = v.uid;
-    ap.ns = v.ns;
-    ap.name = v.name;
-    ap.rv = v.rv;
-    ap.phase = v.phase;
-    ap.dev_idx = v.dev_idx;
-    ap.request = v.request;
-    ap.assume_time = v.assume_time;
-    ap.assigned = v.assigned;
-    ap.dev_total = v.annot_dev_total;
-    ap.complete = v.complete();
-    ap.cu_count = 0;
-    ap.cu_mask.clear();
-    int64_t an = d.path(obj, {"metadata", "annotations"});
-    if (an >= 0) {
-      int64_t c = d.find(static_cast<uint32_t>(an), kCuCountAnn);
-      if (c >= 0) ap.cu_count = std::atoi(d.str(static_cast<uint32_t>(c)).c_str());
-      int64_t m = d.find(static_cast<uint32_t>(an), kCuMaskAnn);
-      if (m >= 0) ap.cu_mask = d.str(static_cast<uint32_t>(m));
-    }
-    const std::string& uid = ap.uid;
+  std::string on_pod_locked(const json::Doc& d, uint32_t obj, std::unordered_set<std::string>* live) {
+    AllocPod ap;
+    parse_alloc_pod(d, obj, p_, &ap);
+    const std::string key = ap.key;
+    const std::string uid = ap.uid;
+    if (live) live->insert(uid);
+    keys_[key] = uid;
     if (ap.complete) {
-      cands_.erase(uid);
       stop_pod_locked(uid);
-      release_cus_locked(uid);  // also for pods this agent did not start (e.g. before a restart)
+      state_->release(uid);  // CUs too, also for pods this agent did not start (e.g. before a restart)
       return key;
     }
-    if (ap.request <= 0 || !devices_.count(static_cast<int>(ap.dev_idx))) {
-      cands_.erase(uid);
-      return key;
-    }
-    // an assigned pod owns the partition recorded on it: rebuilt after a restart, never handed out twice
-    if (ap.assigned == 1 && !ap.cu_mask.empty()) {
-      auto cp = cus_.find(static_cast<int>(ap.dev_idx));
-      if (cp != cus_.end() && !cp->second.holds(uid)) {
-        int clash = cp->second.adopt(uid, parse_cu_words(ap.cu_mask));
-        if (clash) std::fprintf(stderr, "[gsx-nodeagent] %s: %d CU(s) already owned\n", key.c_str(), clash);
-      }
-    }
-    if (ap.assigned == 0 && (ap.phase == "Pending" || ap.phase.empty())) {
-      cands_[uid] = Cand{ap.assume_time, key, ap.request};
-    } else {
-      cands_.erase(uid);
-    }
-    if (ap.assigned == 0 && !inflight_.count(uid) && !running_.count(uid) && !queued_.count(uid)) {
+    state_->observe(ap);  // candidates, CU partitions of assigned pods, multi-container progress
+    if (ap.request <= 0 || !state_->has_device(ap.dev)) return key;
+    if (ap.assigned == "false" && !state_->inflight(uid) && !running_.count(uid) && !queued_.count(uid)) {
       queued_.insert(uid);
       seen_.emplace(uid, now_s());
       queue_.push_back(key);
@@ -433,18 +282,19 @@ class Agent {
   }
 
   void on_delete_locked(const std::string& key) {
-    auto it = pods_.find(key);
-    if (it == pods_.end()) return;
-    std::string uid = it->second.uid;
-    pods_.erase(it);
-    cands_.erase(uid);
+    auto it = keys_.find(key);
+    if (it == keys_.end()) return;
+    std::string uid = it->second;
+    keys_.erase(it);
     stop_pod_locked(uid);
-    release_cus_locked(uid);
+    if (!state_->inflight(uid)) state_->release(uid);  // the admitting worker owns it until its patch resolves
   }
 
   void release_cus_locked(const std::string& uid) {
-    if (inflight_.count(uid)) return;  // the admitting worker owns it until its patch resolves
-    for (auto& kv : cus_) kv.second.release(uid);
+    if (state_->inflight(uid)) return;
+    for (auto& kv : devices_) {
+      if (CuPartitioner* cp = state_->cus(kv.first)) cp->release(uid);
+    }
   }
 
   void stop_pod_locked(const std::string& uid) {
@@ -452,7 +302,9 @@ class Agent {
     if (r == running_.end()) return;
     int dev = r->second;
     running_.erase(r);
-    for (auto& kv : cus_) kv.second.release(uid);
+    for (auto& kv : devices_) {
+      if (CuPartitioner* cp = state_->cus(kv.first)) cp->release(uid);
+    }
     allocations_.erase(uid);
     releases_.push_back({uid, dev});
     ++added_;
@@ -491,14 +343,14 @@ class Agent {
       }
       std::string key = std::move(queue_.front());
       queue_.pop_front();
-      auto pit = pods_.find(key);
-      if (pit == pods_.end()) continue;
-      queued_.erase(pit->second.uid);
+      auto kit = keys_.find(key);
+      if (kit == keys_.end()) continue;
+      queued_.erase(kit->second);
       admit_locked(key, lk);
     }
   }
 
-  std::string build_envs_locked(const AgentPod& pod, const Device& dev, const std::vector<int>& cus) {
+  std::string build_envs_locked(const AllocPod& pod, const Device& dev, const std::vector<int>& cus) {
     // deviceplugin/allocator.py build_response, mount_mode "isolated": only this GPU's nodes are mounted
     const std::string visible = "0";
     char frac[32];
@@ -545,45 +397,37 @@ class Agent {
   }
 
   void admit_locked(std::string key, std::unique_lock<std::mutex>& lk) {
-    auto pit = pods_.find(key);
-    if (pit == pods_.end()) return;
-    std::string uid = pit->second.uid;
-    if (running_.count(uid) || inflight_.count(uid)) return;
-    int64_t units = pit->second.request;
-    // kubelet's Allocate(N ids): the earliest-ASSUME_TIME unassigned pod of that size
-    const Cand* best = nullptr;
-    std::string best_uid;
-    for (auto& kv : cands_) {
-      if (kv.second.units != units || inflight_.count(kv.first) || running_.count(kv.first)) continue;
-      if (!best || kv.second.assume_time < best->assume_time ||
-          (kv.second.assume_time == best->assume_time && kv.second.key < best->key)) {
-        best = &kv.second;
-        best_uid = kv.first;
-      }
-    }
-    if (!best) return;
-    auto cit = pods_.find(best->key);
-    if (cit == pods_.end()) return;
-    if (best_uid != uid) {
+    const AllocPod* mine = state_->pod_by_key(key);
+    if (!mine) return;
+    std::string uid = mine->uid;
+    if (running_.count(uid) || state_->inflight(uid)) return;
+    const int64_t units = mine->request;
+    // kubelet's Allocate(N ids), answered by the device plugin's matcher: the earliest-ASSUME_TIME unassigned
+    // pod of that size
+    auto m = state_->match(units);
+    if (!m.first) return;
+    const AllocPod pod = *m.first;
+    if (pod.uid != uid) {
       // an earlier same-size pod wins this Allocate; ours is served by the next one
       queued_.insert(uid);
       queue_.push_back(key);
       ++added_;
       wake_locked();
-      key = best->key;
-      uid = best_uid;
+      key = pod.key;
+      uid = pod.uid;
     }
-    AgentPod pod = cit->second;
-    inflight_.insert(uid);
+    state_->set_inflight(uid, true);
     double t0 = seen_.count(uid) ? seen_[uid] : now_s();
-    int dev_idx = static_cast<int>(pod.dev_idx);
+    int dev_idx = static_cast<int>(pod.dev);
     const Device dev = devices_.at(dev_idx);
     std::vector<int> cus;
-    if (pod.cu_count > 0) {
+    CuPartitioner* cp = state_->cus(dev_idx);
+    const bool had_cus = cp && cp->holds(uid);
+    {
       std::string e;
-      if (!cus_.at(dev_idx).allocate(uid, pod.cu_count, &cus, &e)) {
+      if (!state_->claim_cus(uid, &cus, &e)) {
         std::fprintf(stderr, "[gsx-nodeagent] %s: %s\n", key.c_str(), e.c_str());
-        inflight_.erase(uid);
+        state_->set_inflight(uid, false);
         return;
       }
     }
@@ -613,8 +457,8 @@ class Agent {
     double tp1 = now_s();
     if (!ok || status >= 300) {
       lk.lock();
-      if (!cus.empty()) cus_.at(dev_idx).release(uid);
-      inflight_.erase(uid);
+      if (!cus.empty() && !had_cus && cp) cp->release(uid);
+      state_->set_inflight(uid, false);
       // 409: stale copy, retry from the informer's latest version; 5xx / transport: the apiserver is
       // unhealthy, retry with backoff (kubelet retries Allocate-time failures the same way); 4xx: give up
       const bool retry = !ok || status == 409 || status >= 500;
@@ -634,7 +478,15 @@ class Agent {
     // a container runtime tears down before it starts: every release already decided for this GPU
     // reaches the runtime before this pod's slice is carved (the next wave's pods may be bound the
     // moment the extender's ledger frees the device, while another worker is still releasing)
+    // the PATCH answered the committed pod: the matcher sees ASSIGNED=true now, not when the watch event comes
+    // (until then it would still offer this pod to the next Allocate, whose commit would fail on the stale rv)
+    AllocPod committed;
+    json::Doc cd;
+    std::string cerr;
+    bool have = cd.parse(resp, &cerr) && parse_alloc_pod(cd, 0, p_, &committed);
     lk.lock();
+    if (have) state_->observe(committed);
+    state_->first_container_committed(uid, units, true);
     drain_releases_locked(dev_idx, lk);
     lk.unlock();
     // start the pod on its GPU's runtime: slice stamped + every resident slice verified
@@ -671,8 +523,8 @@ class Agent {
       lk.lock();
       failed_++;
       bad_ += static_cast<uint64_t>(bad);
-      if (!cus.empty()) cus_.at(dev_idx).release(uid);
-      inflight_.erase(uid);
+      if (!cus.empty() && cp) cp->release(uid);
+      state_->set_inflight(uid, false);
       lk.unlock();
       if (rst == 200) runtime_call(dev_idx, "DELETE", "/v1/pods/" + uid, std::string(), nullptr);
       std::fprintf(stderr, "[gsx-nodeagent] admission of %s on GPU %d failed: %s\n", key.c_str(), dev_idx, why.c_str());
@@ -702,11 +554,14 @@ class Agent {
     latency_.push_back(now_s() - t0);
     if (latency_.size() > 100000) latency_.erase(latency_.begin(), latency_.begin() + 50000);
     seen_.erase(uid);
-    inflight_.erase(uid);
+    state_->set_inflight(uid, false);
     assign_retries_.erase(uid);
     // deleted while we were admitting: release now
-    auto pk = pods_.find(key);
-    if (pk == pods_.end() || pk->second.uid != uid || pk->second.complete) stop_pod_locked(uid);
+    auto pk = keys_.find(key);
+    if (pk == keys_.end() || pk->second != uid) {
+      stop_pod_locked(uid);
+      state_->release(uid);
+    }
     wake_locked();
   }
 
@@ -766,16 +621,15 @@ class Agent {
   bool verify_;
   ApiClient api_;
   std::map<int, Device> devices_;
-  std::map<int, CuPartitioner> cus_;
+  std::unique_ptr<AllocState> state_;  // the device plugin's matcher (allocstate.h)
+  std::unordered_map<std::string, std::string> keys_;  // ns/name -> uid of every pod the informer delivered
   std::map<int, std::unique_ptr<ApiClient>> runtimes_;
   std::unique_ptr<Reflector> pods_r_;
   std::mutex mu_;
   std::condition_variable cv_;
   bool stop_ = false;
-  std::unordered_map<std::string, AgentPod> pods_;
-  std::unordered_map<std::string, Cand> cands_;
   std::unordered_map<std::string, int> running_;
-  std::unordered_set<std::string> inflight_, queued_;
+  std::unordered_set<std::string> queued_;
   std::unordered_map<std::string, double> seen_;
   std::unordered_map<std::string, std::string> allocations_;
   std::deque<std::string> queue_;

@@ -166,18 +166,19 @@ def test_reconcile_state_exchange_cycles(seed):
     recs = {n: st.record(st.pods[f"u{n}"], [f"g{i}-_-0"], 64, "", f"a{n}") for i, n in enumerate("PQR")}
     for n in "PQR":
         st.cus[recs[n].dev].allocate(f"u{n}", 8)
-    holds = {"P": recs["Q"], "Q": recs["R"], "R": recs["P"]}  # who physically holds which record
+    holds = {"P": recs["Q"].aid, "Q": recs["R"].aid, "R": recs["P"].aid}  # who physically holds which record
     order = list("PQR")
     rnd.shuffle(order)
     ann = {n: recs[n].dev for n in "PQR"}  # annotation device per pod
     for _ in range(3):
         for n in order:
-            r = holds[n]
+            r = st.records[holds[n]]
             if r.uid == f"u{n}":
                 continue
             q = r.uid[1:]
             ann[n], ann[q] = r.dev, ann[n]
             st.move_records(f"u{n}", r.uid, r)
     for n in "PQR":
-        assert holds[n].uid == f"u{n}" and ann[n] == holds[n].dev
-        assert st.cus[holds[n].dev].holds(f"u{n}")
+        r = st.records[holds[n]]
+        assert r.uid == f"u{n}" and ann[n] == r.dev
+        assert st.cus[r.dev].holds(f"u{n}")
