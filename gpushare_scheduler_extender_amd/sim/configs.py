@@ -44,13 +44,13 @@ from ..k8s.client import KubeClient
 from ..k8s.fasthttp import Client as HttpClient
 from ..k8s.objects import make_node, make_pod
 from ..models.profile import (ALIYUN, NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION,
-                              POD_CU_MASK_ANNOTATION, SHARED_GPU, NamingProfile)
+                              POD_CU_MASK_ANNOTATION, POD_HOLD_IDX_ANNOTATION, SHARED_GPU, NamingProfile)
 from .cluster import start_apiserver, start_extender, start_node_agent, start_scheduler
 
 GIB = 1 << 30
 NODE = "mi355x-node-0"
 CU_COUNT_ANNOTATION = "gpushare.amd.com/cu-count"
-AGENT = {"kind": "plugin"}  # --agent: plugin | inproc | native
+AGENT = {"kind": "plugin", "args": [], "api_latency_ms": 0.0}  # --agent, --faithful, --api-latency-ms
 
 
 class Runtimes:
@@ -111,7 +111,8 @@ class Cluster:
         # native: compiled kube-scheduler / node-agent stand-ins; otherwise the asyncio ones
         self.children.append(start_scheduler(self.api.url, self.ext.url, profile=profile.name, native=native))
         self.agent_kind = agent or AGENT["kind"]
-        self.agent_args = list(agent_args or [])
+        self.agent_args = list(agent_args if agent_args is not None else AGENT["args"])
+        self.api_latency_ms = AGENT["api_latency_ms"]
         self.children.append(self._agent())
         self.rt = Runtimes(len(totals), GIB, max(totals), gpu)
         self.cu_count = cu_count
@@ -132,6 +133,10 @@ class Cluster:
                          labels={"gpushare": "true"})
         await self.c.create("nodes", node)
         self.ext_http = HttpClient(self.ext.url)
+        if self.api_latency_ms:
+            api = HttpClient(self.api.url)
+            await api.request("POST", "/fake/faults", json.dumps({"latency_ms": self.api_latency_ms}).encode())
+            await api.close()
         self.agent_http = HttpClient(next(ch.url for ch in self.children if ch.name == "node-agent"))
         for _ in range(2000):  # the extender has seen the node
             if (await self.inspect()).get("nodes"):
@@ -238,6 +243,27 @@ class Cluster:
     def device_of(self, pod: dict) -> int:
         return int(pod["metadata"]["annotations"][self.profile.annotation_idx])
 
+    async def physical_drift(self, names: list[str], timeout: float = 10.0) -> tuple[int, dict]:
+        """Pods whose container runs on another GPU than their ``*_IDX`` annotation says (the env kubelet gave
+        the container, from the kubelet stand-in), after waiting up to ``timeout`` for reconciliation."""
+        deadline = time.monotonic() + timeout
+        while True:
+            pods = {p["metadata"]["name"]: p for p in (await self.c.list("pods", "default"))["items"]}
+            drift = {}
+            for n in names:
+                p = pods.get(n)
+                if p is None or p.get("status", {}).get("phase") != "Running":
+                    continue
+                if POD_HOLD_IDX_ANNOTATION in (p["metadata"].get("annotations") or {}):
+                    drift[n] = "reconciliation in progress"
+                    continue
+                env = (await self.allocation(p["metadata"]["uid"])).get("envs", {})
+                if env and int(env.get(self.profile.annotation_idx, -1)) != self.device_of(p):
+                    drift[n] = (self.device_of(p), int(env[self.profile.annotation_idx]))  # (annotated, physical)
+            if not drift or time.monotonic() > deadline:
+                return len(drift), drift
+            await asyncio.sleep(0.05)
+
     async def close(self):
         await self.c.close()
         await self.ext_http.close()
@@ -309,6 +335,10 @@ async def config3(gpu: bool) -> dict:
         await asyncio.gather(*(cl.create(f"p64-{i}", 64) for i in range(32)))
         pods = await cl.wait([f"p64-{i}" for i in range(32)])
         dt = time.perf_counter() - t0
+        # physical placement (the env each container got) == the annotation the extender accounts (a faithful
+        # kubelet may start a container with another pod's Allocate; reconciliation must then fix the record)
+        drift, drifted = await cl.physical_drift(list(pods))
+        pods = {p["metadata"]["name"]: p for p in (await cl.c.list("pods", "default"))["items"] if p["metadata"]["name"] in pods}
         per_dev = [0] * 8
         for p in pods.values():
             per_dev[cl.device_of(p)] += 64
@@ -320,12 +350,15 @@ async def config3(gpu: bool) -> dict:
         # allocation (the extender keeps their binds in ASSUME_TIME order; the plugin matches on ASSUME_TIME)
         ast = await cl.agent_stats()
         mismatch = ast.get("mismatch", 0)
-        ok = per_dev == [256] * 8 and used == 256 * 8 and bad == 0 and mismatch == 0
+        faithful = "--faithful" in cl.agent_args
+        ok = per_dev == [256] * 8 and used == 256 * 8 and bad == 0 and drift == 0 and (faithful or mismatch == 0)
         if real:  # 32 x 64 GiB co-resident in 8 real HBM arenas, 4 slices each
             ok = ok and resident == [4] * 8
         return {"ok": ok, "per_device_gib": per_dev, "device_gib": per, "util_pct": round(100 * used / (8 * per), 2),
                 "real_gpus": real, "resident_slices": resident, "bad_stamps": bad, "seconds": round(dt, 4),
-                "allocate_mismatch": mismatch, "allocate_swapped_equivalent": ast.get("swapped_equivalent", 0)}
+                "allocate_mismatch": mismatch, "allocate_swapped_equivalent": ast.get("swapped_equivalent", 0),
+                "physical_drift": drift, "drifted": drifted, "faithful_kubelet": faithful,
+                "api_latency_ms": cl.api_latency_ms, "reconcile": ast.get("reconcile")}
     finally:
         await cl.close()
 
@@ -465,9 +498,15 @@ def main(argv=None) -> int:
     ap.add_argument("--agent", default="plugin", choices=["plugin", "inproc", "native"],
                     help="kubelet + device plugin: the shipped gRPC plugin driven over its socket (default), "
                          "the same in-process, or the compiled gsx-nodeagent")
+    ap.add_argument("--faithful", action="store_true",
+                    help="the kubelet stand-in behaves like kubelet (no re-routing, sorted batches, PodResources); "
+                         "the plugin reconciles against it")
+    ap.add_argument("--api-latency-ms", type=float, default=0.0, help="fake apiserver latency per request")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args(argv)
     AGENT["kind"] = a.agent
+    AGENT["args"] = ["--faithful"] if a.faithful else []
+    AGENT["api_latency_ms"] = a.api_latency_ms
     which = [int(x) for x in a.only.split(",") if x] or sorted(CONFIGS)
     report = {}
     for k in which:

@@ -32,14 +32,20 @@ async def _retry(fn, *a, tries=50, **kw):
                                                        (23, "native", "native", "binding"),
                                                        (7, "python", "plugin", "binding"),
                                                        (11, "native", "native", "binding"),
-                                                       (13, "native", "plugin", "update")])
+                                                       (13, "native", "plugin", "update"),
+                                                       (7, "native", "faithful", "binding"),
+                                                       (29, "native", "faithful", "update")])
 def test_chaos_whole_stack_converges_without_overcommit(seed, impl, agent, bind_mode):
     """``impl``: compiled or asyncio scheduler stand-in; ``agent``: kubelet + the shipped gRPC device plugin
-    (the product path) or the compiled node agent; ``bind_mode``: one annotated Binding, or the reference's
-    annotation write + Binding (two calls, the first guarded by resourceVersion)."""
+    (the product path), the same behind a *faithful* kubelet (no re-routing, creationTimestamp-sorted batches,
+    PodResources reconciliation), or the compiled node agent; ``bind_mode``: one annotated Binding, or the
+    reference's annotation write + Binding (two calls, the first guarded by resourceVersion)."""
+    faithful = agent == "faithful"
+
     async def go():
         rnd = random.Random(seed)
-        cl = Cluster(ALIYUN, [96] * 4, gpu=False, native=impl == "native", agent=agent, bind_mode=bind_mode)
+        cl = Cluster(ALIYUN, [96] * 4, gpu=False, native=impl == "native", agent="plugin" if faithful else agent,
+                     bind_mode=bind_mode, agent_args=["--faithful"] if faithful else [])
         try:
             await cl.start()
             api = HttpClient(cl.api.url)
@@ -83,6 +89,9 @@ def test_chaos_whole_stack_converges_without_overcommit(seed, impl, agent, bind_
                 assert time.monotonic() < deadline, {"used": used, "ledger": ledger, "pending": pending,
                                                      "running": len(running), "bound": len(bound)}
                 await asyncio.sleep(0.05)
+            # every running container is on the GPU its annotation names (physical == *_IDX), holds cleared
+            drift, drifted = await cl.physical_drift(sorted(live), timeout=15)
+            assert drift == 0, drifted
             st = json.loads((await api.request("GET", "/fake/stats")).body)
             assert st["counts"].get("injected_conflict", 0) > 0 and st["counts"].get("injected_error", 0) > 0
             await api.close()
