@@ -82,12 +82,9 @@ class GpuSharePlugin:
         self.mount_mode = mount_mode
         self.health_backend = health_backend
         self.health_interval = health_interval
-        self.units = {d.index: d.units(unit, reserve_bytes) for d in devices}
-        self.ids = {d.index: fake_ids(d, self.units[d.index]) for d in devices}
-        self.id_owner = {i: d for d, ids in self.ids.items() for i in ids}
-        self.state = AllocationState(node, self.devices, profile)
+        self.reserve_bytes = reserve_bytes
         self.isolation = isolation
-        self.state.on_drop.append(self._record_dropped)
+        self._set_devices(devices)
         self.checkpoint = checkpoint if checkpoint is not None else os.path.join(socket_dir, "gsx-allocations.json")
         self._aid = 0
         self.reconciler = None
@@ -110,6 +107,40 @@ class GpuSharePlugin:
         self.stats = {"allocate_ok": 0, "allocate_fail": 0, "allocate_retries": 0, "preferred": 0,
                       "registrations": 0, "refreshes": 0}
         self._debug = None
+
+    def _set_devices(self, devices: list[Device]):
+        """(Re)build everything derived from the device layout: fake IDs per GPU and the allocation state."""
+        self.devices = {d.index: d for d in devices}
+        self.units = {d.index: d.units(self.unit, self.reserve_bytes) for d in devices}
+        self.ids = {d.index: fake_ids(d, self.units[d.index]) for d in devices}
+        self.id_owner = {i: d for d, ids in self.ids.items() for i in ids}
+        self.state = AllocationState(self.node, self.devices, self.profile)
+        self.state.on_drop.append(self._record_dropped)
+        self.health_info: dict[int, dict] = {}
+
+    async def reload_devices(self, devices: list[Device] | None = None):
+        """The node's GPUs were re-partitioned at run time (amd-smi set --compute-partition / --memory-partition):
+        a new set of logical devices, so new fake IDs (ListAndWatch), new per-device totals (node annotation)
+        and an allocation state rebuilt from the pods on the node."""
+        if devices is None:
+            from ..ops import mxdev  # noqa: PLC0415
+
+            from .devices import apply_memory_pools  # noqa: PLC0415
+
+            raw = await asyncio.get_running_loop().run_in_executor(None, mxdev.enumerate_devices, self.health_backend)
+            devices = apply_memory_pools([Device(**d) for d in raw])
+        old = sorted((d.index, d.partition, d.memory_partition) for d in self.devices.values())
+        self._set_devices(devices)
+        self.state.resync(self.pods.list())
+        self.stats["layout_changes"] = self.stats.get("layout_changes", 0) + 1
+        log.warning("device layout changed: %s -> %s", old,
+                    sorted((d.index, d.partition, d.memory_partition) for d in devices))
+        self._version += 1
+        self._changed.set()
+        try:
+            await self.publish_node()
+        except ApiError as e:
+            log.warning("re-publishing node info failed: %s", e)
 
     # ------------------------------------------------------------ paths
     @property
@@ -417,7 +448,8 @@ class GpuSharePlugin:
     def debug_state(self) -> dict:
         return {"node": self.node, "resource": self.profile.resource, "unit": self.unit,
                 "devices": [{"index": d.index, "bdf": d.bdf, "healthy": d.healthy, "units": self.units[d.index],
-                             "cu": d.cu_count, "partition": d.partition} for d in self.devices.values()],
+                             "cu": d.cu_count, "partition": d.partition, "memory_partition": d.memory_partition,
+                             "health": self.health_info.get(d.index)} for d in self.devices.values()],
                 "informer": {"synced": self.pods.synced.is_set(), "relists": self.pods.relists,
                              "rewatches": self.pods.rewatches, "events": self.pods.events},
                 "stats": dict(self.stats), **self.state.snapshot(),
@@ -437,6 +469,14 @@ class GpuSharePlugin:
             lines += [f"# TYPE gpushare_plugin_state_{k}_total counter", f"gpushare_plugin_state_{k}_total {v}"]
         lines.append("# TYPE gpushare_plugin_device_healthy gauge")
         lines += [f'gpushare_plugin_device_healthy{{device="{d.index}"}} {int(d.healthy)}' for d in self.devices.values()]
+        for name, key in (("thermal_throttle", "thermal_throttle"), ("power_throttle", "power_throttle"),
+                          ("xgmi_error", "xgmi_error"), ("ras_uncorrectable", None)):
+            lines.append(f"# TYPE gpushare_plugin_device_{name} gauge")
+            for i, h in sorted(self.health_info.items()):
+                v = (h.get("ecc_uncorrectable", 0) + h.get("ras_umc_uncorrectable", 0) + h.get("ras_gfx_uncorrectable", 0)
+                     + h.get("ras_sdma_uncorrectable", 0) + h.get("ras_xgmi_uncorrectable", 0)) if key is None \
+                    else int(h.get(key, 0))
+                lines.append(f'gpushare_plugin_device_{name}{{device="{i}"}} {v}')
         lines.append("# TYPE gpushare_plugin_cu_free gauge")
         lines += [f'gpushare_plugin_cu_free{{device="{i}"}} {cp.free_count()}' for i, cp in self.state.cus.items()]
         lines.append("# TYPE gpushare_plugin_allocate_candidates gauge")
@@ -488,16 +528,34 @@ class GpuSharePlugin:
             await asyncio.sleep(1.0)
 
     async def _health_loop(self):
+        """Poll amdsmi health: uncorrectable ECC / RAS (HBM, GFX, SDMA, xGMI) or an xGMI link error makes a GPU's
+        IDs Unhealthy in ListAndWatch; thermal / power throttling is exported as a metric; a compute or memory
+        partition change re-shapes the advertised devices (:meth:`reload_devices`)."""
         from ..ops import mxdev  # noqa: PLC0415
 
+        loop = asyncio.get_running_loop()
         while True:
+            changed = False
             for idx in list(self.devices):
+                d = self.devices.get(idx)
                 try:
-                    h = await asyncio.get_running_loop().run_in_executor(None, mxdev.health, idx,
-                                                                         self.health_backend)
-                    self.set_health(idx, bool(h["healthy"]), f"(ecc uncorrectable={h['ecc_uncorrectable']})")
+                    h = await loop.run_in_executor(None, mxdev.health, idx, self.health_backend)
                 except Exception as e:  # noqa: BLE001
                     log.debug("health of GPU %d: %r", idx, e)
+                    continue
+                if d is None or self.devices.get(idx) is not d:
+                    break  # re-shaped meanwhile
+                self.health_info[idx] = h
+                if h.get("partition") and (h["partition"] != d.partition or
+                                           (h.get("memory_partition") or "") != (d.memory_partition or "")):
+                    changed = True
+                    break
+                self.set_health(idx, bool(h["healthy"]), f"({h.get('reason') or 'ok'})")
+            if changed:
+                try:
+                    await self.reload_devices()
+                except Exception as e:  # noqa: BLE001
+                    log.error("re-enumerating devices after a partition change failed: %r", e)
             await asyncio.sleep(self.health_interval)
 
     async def _event_loop(self):
@@ -516,7 +574,11 @@ class GpuSharePlugin:
                 if ev["name"] in ("GPU_PRE_RESET", "VMFAULT"):
                     self.set_health(ev["index"], False, f"({ev['name']}: {ev['message']})")
                 elif ev["name"] == "GPU_POST_RESET":
-                    self.set_health(ev["index"], True, "(post reset)")
+                    h = self.health_info.get(ev["index"]) or {}
+                    if h.get("healthy", True):  # a reset does not clear uncorrectable-error counters
+                        self.set_health(ev["index"], True, "(post reset)")
+                elif ev["name"] == "THERMAL_THROTTLE":
+                    self.health_info.setdefault(ev["index"], {})["thermal_throttle"] = True
 
     async def start(self, register: bool = True, publish: bool = True, serve: bool = True,
                     sync_timeout: float = 30.0):

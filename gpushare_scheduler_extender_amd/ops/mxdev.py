@@ -36,4 +36,11 @@ def enumerate_devices(backend: str = "amdsmi") -> list[dict]:
 
 
 def health(index: int, backend: str = "amdsmi") -> dict:
+    """ECC / RAS (HBM, GFX, SDMA, xGMI) counters, xGMI link status, thermal / power throttle, partition modes."""
     return session(backend).health(index)
+
+
+def inject(index: int, what: str, backend: str) -> None:
+    """Fake backend only: ``ecc_uncorrectable=1``, ``xgmi_error=1``, ``thermal_throttle=1``, ``partition=CPX``,
+    ``memory_partition=NPS2``, ``event=GPU_PRE_RESET`` ..."""
+    session(backend).inject(index, what)

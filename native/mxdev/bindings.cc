@@ -68,9 +68,25 @@ class Session {
     if (!ok) throw std::runtime_error(err);
     py::dict d;
     d["healthy"] = r.healthy;
+    d["reason"] = r.reason;
     d["ecc_uncorrectable"] = r.ecc_uncorrectable;
     d["ecc_correctable"] = r.ecc_correctable;
+    d["ras_umc_uncorrectable"] = r.ras_umc_uncorrectable;
+    d["ras_gfx_uncorrectable"] = r.ras_gfx_uncorrectable;
+    d["ras_sdma_uncorrectable"] = r.ras_sdma_uncorrectable;
+    d["ras_xgmi_uncorrectable"] = r.ras_xgmi_uncorrectable;
+    d["ras_xgmi_correctable"] = r.ras_xgmi_correctable;
+    d["xgmi_error"] = r.xgmi_error;
+    d["thermal_throttle"] = r.thermal_throttle;
+    d["power_throttle"] = r.power_throttle;
+    d["partition"] = r.partition;
+    d["memory_partition"] = r.memory_partition;
     return d;
+  }
+  void inject(int index, const std::string& what) {
+    std::string err;
+    std::lock_guard<std::mutex> g(mu_);
+    if (!b_->inject(index, what, &err)) throw std::runtime_error(err);
   }
   void watch_events() {
     std::string err;
@@ -110,7 +126,8 @@ PYBIND11_MODULE(_mxdev, m) {
       .def("devices", &Session::devices)
       .def("health", &Session::health)
       .def("watch_events", &Session::watch_events)
-      .def("poll_events", &Session::poll_events, py::arg("timeout_ms") = 1000);
+      .def("poll_events", &Session::poll_events, py::arg("timeout_ms") = 1000)
+      .def("inject", &Session::inject, py::arg("index"), py::arg("what"));
   m.def("fake_spec_ok", [](const std::string& s) {
     std::vector<mxdev::DeviceRec> v;
     std::string err;

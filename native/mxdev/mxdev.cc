@@ -7,6 +7,9 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <regex>
 
 #include <amd_smi/amdsmi.h>
@@ -34,6 +37,9 @@ struct Api {
   decltype(&amdsmi_get_gpu_compute_partition) cpart = nullptr;
   decltype(&amdsmi_get_gpu_memory_partition) mpart = nullptr;
   decltype(&amdsmi_get_gpu_total_ecc_count) ecc = nullptr;
+  decltype(&amdsmi_get_gpu_ecc_count) ecc_block = nullptr;
+  decltype(&amdsmi_gpu_xgmi_error_status) xgmi_status = nullptr;
+  decltype(&amdsmi_get_violation_status) violation = nullptr;
   decltype(&amdsmi_topo_get_link_type) link_type = nullptr;
   decltype(&amdsmi_topo_get_numa_node_number) numa = nullptr;
   decltype(&amdsmi_init_gpu_event_notification) evt_init = nullptr;
@@ -73,6 +79,9 @@ struct Api {
            sym(&cpart, "amdsmi_get_gpu_compute_partition", false, err) &&
            sym(&mpart, "amdsmi_get_gpu_memory_partition", false, err) &&
            sym(&ecc, "amdsmi_get_gpu_total_ecc_count", false, err) &&
+           sym(&ecc_block, "amdsmi_get_gpu_ecc_count", false, err) &&
+           sym(&xgmi_status, "amdsmi_gpu_xgmi_error_status", false, err) &&
+           sym(&violation, "amdsmi_get_violation_status", false, err) &&
            sym(&link_type, "amdsmi_topo_get_link_type", false, err) &&
            sym(&numa, "amdsmi_topo_get_numa_node_number", false, err) &&
            sym(&evt_init, "amdsmi_init_gpu_event_notification", false, err) &&
@@ -254,17 +263,53 @@ class AmdSmi : public Backend {
   }
 
   bool health_of(amdsmi_processor_handle p, DeviceRec* r, std::string* err) {
-    if (!api_.ecc) return true;
-    amdsmi_error_count_t ec;
-    std::memset(&ec, 0, sizeof(ec));
-    amdsmi_status_t st = api_.ecc(p, &ec);
-    if (st != AMDSMI_STATUS_SUCCESS) {
-      // ECC unsupported (e.g. inside some VMs) is not unhealthy
-      return true;
+    // every counter is optional: unsupported (e.g. inside some VMs) is not unhealthy
+    if (api_.ecc) {
+      amdsmi_error_count_t ec;
+      std::memset(&ec, 0, sizeof(ec));
+      if (api_.ecc(p, &ec) == AMDSMI_STATUS_SUCCESS) {
+        r->ecc_uncorrectable = ec.uncorrectable_count;
+        r->ecc_correctable = ec.correctable_count;
+      }
     }
-    r->ecc_uncorrectable = ec.uncorrectable_count;
-    r->ecc_correctable = ec.correctable_count;
-    r->healthy = ec.uncorrectable_count == 0;
+    if (api_.ecc_block) {
+      auto block = [&](amdsmi_gpu_block_t b, uint64_t* unc, uint64_t* cor) {
+        amdsmi_error_count_t ec;
+        std::memset(&ec, 0, sizeof(ec));
+        if (api_.ecc_block(p, b, &ec) == AMDSMI_STATUS_SUCCESS) {
+          *unc = ec.uncorrectable_count;
+          if (cor) *cor = ec.correctable_count;
+        }
+      };
+      block(AMDSMI_GPU_BLOCK_UMC, &r->ras_umc_uncorrectable, nullptr);
+      block(AMDSMI_GPU_BLOCK_GFX, &r->ras_gfx_uncorrectable, nullptr);
+      block(AMDSMI_GPU_BLOCK_SDMA, &r->ras_sdma_uncorrectable, nullptr);
+      block(AMDSMI_GPU_BLOCK_XGMI_WAFL, &r->ras_xgmi_uncorrectable, &r->ras_xgmi_correctable);
+    }
+    if (api_.xgmi_status) {
+      amdsmi_xgmi_status_t xs = AMDSMI_XGMI_STATUS_NO_ERRORS;
+      if (api_.xgmi_status(p, &xs) == AMDSMI_STATUS_SUCCESS) r->xgmi_error = static_cast<int>(xs);
+    }
+    if (api_.violation) {
+      amdsmi_violation_status_t v;
+      std::memset(&v, 0, sizeof(v));
+      if (api_.violation(p, &v) == AMDSMI_STATUS_SUCCESS) {
+        auto on = [](uint8_t x) { return x == 1; };  // 0xFF = unsupported
+        r->thermal_throttle = on(v.active_prochot_thrm) || on(v.active_socket_thrm) || on(v.active_hbm_thrm) ||
+                              on(v.active_vr_thrm);
+        r->power_throttle = on(v.active_ppt_pwr);
+      }
+    }
+    // the partition modes are re-read every poll: a runtime change re-shapes the node's devices
+    if (api_.cpart) {
+      char buf[64] = {0};
+      if (api_.cpart(p, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS && buf[0]) r->partition = buf;
+    }
+    if (api_.mpart) {
+      char buf[64] = {0};
+      if (api_.mpart(p, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) r->memory_partition = buf;
+    }
+    classify(r);
     return true;
   }
 
@@ -337,16 +382,19 @@ class AmdSmi : public Backend {
 
 class Fake : public Backend {
  public:
-  explicit Fake(std::vector<DeviceRec> d) : devs_(std::move(d)) {}
+  Fake(std::vector<DeviceRec> d, std::string spec) : devs_(std::move(d)), spec_(std::move(spec)) {}
   std::string name() const override { return "fake"; }
   bool enumerate(std::vector<DeviceRec>* out, std::string*) override {
+    std::lock_guard<std::mutex> g(mu_);
     *out = devs_;
     return true;
   }
   bool health(int index, DeviceRec* rec, std::string* err) override {
+    std::lock_guard<std::mutex> g(mu_);
     for (auto& d : devs_) {
       if (d.index == index) {
         *rec = d;
+        classify(rec);
         return true;
       }
     }
@@ -354,13 +402,82 @@ class Fake : public Backend {
     return false;
   }
   bool watch_events(std::string*) override { return true; }
-  std::vector<Event> poll_events(int) override { return {}; }
+  std::vector<Event> poll_events(int timeout_ms) override {
+    std::unique_lock<std::mutex> g(mu_);
+    if (events_.empty()) cv_.wait_for(g, std::chrono::milliseconds(timeout_ms));
+    std::vector<Event> out;
+    out.swap(events_);
+    return out;
+  }
+  bool inject(int index, const std::string& what, std::string* err) override {
+    size_t eq = what.find('=');
+    if (eq == std::string::npos) {
+      *err = "inject wants key=value";
+      return false;
+    }
+    std::string k = what.substr(0, eq), v = what.substr(eq + 1);
+    std::lock_guard<std::mutex> g(mu_);
+    if (k == "partition" || k == "memory_partition") {
+      // the whole node re-partitions (amd-smi set on every GPU): the logical devices are generated again
+      std::string mode = k == "partition" ? v : devs_.empty() ? "SPX" : devs_[0].partition;
+      std::string nps = k == "memory_partition" ? v : devs_.empty() ? "NPS1" : devs_[0].memory_partition;
+      size_t c1 = spec_.find(':');
+      std::string base = c1 == std::string::npos ? spec_ : spec_.substr(0, c1);
+      std::string spec = base + ":" + mode + (nps.empty() || nps == "NPS1" ? "" : ":" + nps);
+      std::vector<DeviceRec> d;
+      if (!fake_spec(spec, &d, err)) return false;
+      devs_ = std::move(d);
+      spec_ = spec;
+      return true;
+    }
+    for (auto& d : devs_) {
+      if (d.index != index) continue;
+      uint64_t n = std::strtoull(v.c_str(), nullptr, 10);
+      if (k == "ecc_uncorrectable") d.ecc_uncorrectable = n;
+      else if (k == "ecc_correctable") d.ecc_correctable = n;
+      else if (k == "ras_umc_uncorrectable") d.ras_umc_uncorrectable = n;
+      else if (k == "ras_gfx_uncorrectable") d.ras_gfx_uncorrectable = n;
+      else if (k == "ras_xgmi_uncorrectable") d.ras_xgmi_uncorrectable = n;
+      else if (k == "xgmi_error") d.xgmi_error = static_cast<int>(n);
+      else if (k == "thermal_throttle") d.thermal_throttle = n != 0;
+      else if (k == "power_throttle") d.power_throttle = n != 0;
+      else if (k == "event") {
+        int t = v == "GPU_PRE_RESET" ? AMDSMI_EVT_NOTIF_GPU_PRE_RESET : v == "GPU_POST_RESET" ? AMDSMI_EVT_NOTIF_GPU_POST_RESET
+                : v == "VMFAULT" ? AMDSMI_EVT_NOTIF_VMFAULT : AMDSMI_EVT_NOTIF_THERMAL_THROTTLE;
+        events_.push_back(Event{index, t, event_name(t), "injected"});
+        cv_.notify_all();
+      } else {
+        *err = "unknown fault " + k;
+        return false;
+      }
+      return true;
+    }
+    *err = "no device with index " + std::to_string(index);
+    return false;
+  }
 
  private:
+  std::mutex mu_;
+  std::condition_variable cv_;
   std::vector<DeviceRec> devs_;
+  std::string spec_;
+  std::vector<Event> events_;
 };
 
 }  // namespace
+
+void classify(DeviceRec* r) {
+  std::string why;
+  auto add = [&](const std::string& s) { why += (why.empty() ? "" : ", ") + s; };
+  if (r->ecc_uncorrectable) add("ecc uncorrectable=" + std::to_string(r->ecc_uncorrectable));
+  if (r->ras_umc_uncorrectable) add("HBM (UMC) uncorrectable=" + std::to_string(r->ras_umc_uncorrectable));
+  if (r->ras_gfx_uncorrectable) add("GFX uncorrectable=" + std::to_string(r->ras_gfx_uncorrectable));
+  if (r->ras_sdma_uncorrectable) add("SDMA uncorrectable=" + std::to_string(r->ras_sdma_uncorrectable));
+  if (r->ras_xgmi_uncorrectable) add("xGMI uncorrectable=" + std::to_string(r->ras_xgmi_uncorrectable));
+  if (r->xgmi_error) add(r->xgmi_error == 2 ? "xGMI multiple errors" : "xGMI error");
+  r->healthy = why.empty();
+  r->reason = why;
+}
 
 int partitions_for_mode(const std::string& mode) {
   if (mode == "CPX") return 8;
@@ -435,7 +552,7 @@ Backend* make_backend(const std::string& kind, std::string* err) {
   if (kind.rfind("fake:", 0) == 0) {
     std::vector<DeviceRec> d;
     if (!fake_spec(kind.substr(5), &d, err)) return nullptr;
-    return new Fake(std::move(d));
+    return new Fake(std::move(d), kind.substr(5));
   }
   if (kind == "amdsmi" || kind == "auto") {
     auto* b = new AmdSmi();

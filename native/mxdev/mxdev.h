@@ -39,6 +39,13 @@ struct DeviceRec {
   bool healthy = true;
   uint64_t ecc_uncorrectable = 0;
   uint64_t ecc_correctable = 0;
+  // RAS: uncorrectable errors of the blocks a pod's work depends on (HBM/UMC, GFX, SDMA, xGMI WAFL)
+  uint64_t ras_umc_uncorrectable = 0, ras_gfx_uncorrectable = 0, ras_sdma_uncorrectable = 0;
+  uint64_t ras_xgmi_uncorrectable = 0, ras_xgmi_correctable = 0;
+  int xgmi_error = 0;            // amdsmi_xgmi_status_t: 0 none, 1 error, 2 multiple errors
+  bool thermal_throttle = false; // prochot / socket / HBM / VR thermal violation active
+  bool power_throttle = false;   // package power tracking violation active
+  std::string reason;            // why unhealthy ("" when healthy)
   int numa_node = -1;
   std::vector<std::string> link_types;  // per peer index: XGMI / PCIE / SELF / UNKNOWN
 };
@@ -61,7 +68,17 @@ class Backend {
   virtual bool watch_events(std::string* err) = 0;
   // wait up to timeout_ms for events
   virtual std::vector<Event> poll_events(int timeout_ms) = 0;
+  // fake backend only: inject a fault / change ("ecc_uncorrectable=3", "xgmi_error=1", "thermal_throttle=1",
+  // "partition=CPX", "memory_partition=NPS2", "event=GPU_PRE_RESET"); false + *err elsewhere
+  virtual bool inject(int index, const std::string& what, std::string* err) {
+    *err = "fault injection is only supported by the fake backend";
+    return false;
+  }
 };
+
+// healthy = no uncorrectable ECC / RAS error in HBM, GFX, SDMA or xGMI, and no xGMI link error; a thermal or
+// power throttle is reported but does not make a device unhealthy (it slows pods, it does not corrupt them)
+void classify(DeviceRec* r);
 
 // "amdsmi", "fake:<spec>", or "auto" (amdsmi, error if unavailable).
 Backend* make_backend(const std::string& kind, std::string* err);
