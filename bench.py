@@ -254,20 +254,24 @@ def latency_sweep(a, children, api_url, api_batch, runner: WaveRunner, inspect_u
     driver's headline.  Returns (sweep rows, reference_client rows)."""
     from gpushare_scheduler_extender_amd.sim.cluster import start_extender
 
-    def restart_extender(mode: str, qps: float = 0.0, burst: int = 1000):
+    def restart_extender(mode: str, qps: float = 0.0, burst: int = 1000, order: str | None = None):
         restart_child(children, "extender", lambda old: start_extender(
-            api_url, profile=a.profile, bind_mode=mode, port=old.port, cpus=old.cpus, kube_qps=qps, kube_burst=burst))
+            api_url, profile=a.profile, bind_mode=mode, port=old.port, cpus=old.cpus, kube_qps=qps, kube_burst=burst,
+            bind_order=order or a.bind_order))
         # serving and synced: the node is in its ledger
         wait_until(lambda: bool(inspect_used().get("nodes")), 60, "restarted extender never saw the node")
 
-    rows, mode = [], a.bind_mode
-    for m in ("binding", "update"):
-        if m != mode:
-            restart_extender(m)
-            mode = m
-        for ms in SWEEP_LATENCIES_MS:
-            set_latency(api_batch, ms)
-            rows.append({"bind_mode": m, "api_latency_ms": ms, **runner.measure(1, a.sweep_steps)})
+    rows, cur = [], (a.bind_mode, a.bind_order)
+    orders = [o for o in a.sweep_orders.split(",") if o]
+    for order in orders:
+        for m in ("binding", "update"):
+            if (m, order) != cur:
+                restart_extender(m, order=order)
+                cur = (m, order)
+            for ms in SWEEP_LATENCIES_MS:
+                set_latency(api_batch, ms)
+                rows.append({"bind_mode": m, "bind_order": order, "api_latency_ms": ms,
+                             **runner.measure(1, a.sweep_steps)})
     set_latency(api_batch, 0)
     # the reference's client: client-go defaults QPS 5 / burst 10 (cmd/main.go:76-82 never overrides them).
     # The warm-up waves drain the burst, so the timed waves see the sustained rate.
@@ -288,13 +292,15 @@ def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
     from gpushare_scheduler_extender_amd.sim.cluster import start_node_agent
 
     na = restart_child(children, "node-agent", lambda old: start_node_agent(
-        api_url, NODE, profile=a.profile, native=False, plugin="grpc", cpus=old.cpus))
+        api_url, NODE, profile=a.profile, native=False, plugin="grpc", cpus=old.cpus,
+        extra=["--faithful"] if a.kubelet == "faithful" else []))
     client = E.BatchClient({"server": na.url})
     wait_until(lambda: client.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 120, "plugin agent never ready")
     row = runner.measure(2, a.sweep_steps)
     st, body = client.run([("GET", "/v1/stats", b"")], 1)[0]
     stats = json.loads(body) if st == 200 else {}
-    return {**row, "admit_p50_ms": stats.get("admit_p50_ms"), "allocate_calls": stats.get("allocate_calls"),
+    return {**row, "admit_p50_ms": stats.get("admit_p50_ms"), "breakdown_ms": stats.get("breakdown_ms"),
+            "plugin_breakdown_ms": stats.get("plugin_breakdown_ms"), "allocate_calls": stats.get("allocate_calls"),
             "allocate_errors": stats.get("allocate_errors"), "mismatch": stats.get("mismatch"),
             "swapped_equivalent": stats.get("swapped_equivalent"),
             "plugin_stats": stats.get("plugin_stats")}
@@ -342,6 +348,13 @@ def parse():
                          "L3 domain (5 cores); 0: two physical cores")
     ap.add_argument("--api-latency-ms", type=float, default=0.0,
                     help="fake kube-apiserver answers every non-watch request after this delay (timed region)")
+    ap.add_argument("--bind-order", default="strict", choices=["strict", "relaxed"],
+                    help="extender --bind-order: strict ASSUME_TIME order of equal-size cross-GPU binds (default) or "
+                         "relaxed (all concurrent; swaps repaired by the plugin's PodResources reconciliation)")
+    ap.add_argument("--sweep-orders", default="strict", help="bind orders the latency sweep covers (comma list)")
+    ap.add_argument("--kubelet", default="standin", choices=["standin", "faithful"],
+                    help="with --node-agent plugin: the kubelet stand-in re-routes a mismatched Allocate (standin) or "
+                         "behaves like kubelet and lets the plugin reconcile (faithful)")
     ap.add_argument("--sweep", type=int, default=1, help="1: run the latency sweep after the timed region")
     ap.add_argument("--sweep-steps", type=int, default=8)
     ap.add_argument("--inproc", action="store_true",
@@ -448,7 +461,8 @@ def main():
 
         api = start_apiserver(native=a.apiserver == "native", cpus=cpu_plan.get("apiserver"))
         children.append(api)
-        ext = start_extender(api.url, profile=a.profile, bind_mode=a.bind_mode, cpus=cpu_plan.get("extender"))
+        ext = start_extender(api.url, profile=a.profile, bind_mode=a.bind_mode, cpus=cpu_plan.get("extender"),
+                             bind_order=a.bind_order)
         children.append(ext)
         # kube-scheduler stand-in: its own process, like the real one (serial scheduling cycle)
         children.append(start_scheduler(api.url, ext.url, profile=a.profile, native=a.scheduler == "native",
@@ -458,7 +472,8 @@ def main():
             children.append(start_node_agent(api.url, NODE, profile=a.profile, native=a.node_agent == "native",
                                              plugin="inproc" if a.node_agent == "inproc" else "grpc",
                                              workers=min(16, max(8, 2 * a.pods_per_gpu * world)),
-                                             cpus=cpu_plan.get("node-agent")))
+                                             cpus=cpu_plan.get("node-agent"),
+                                             extra=["--faithful"] if a.kubelet == "faithful" else []))
         api_url, ext_url = api.url, ext.url
 
     import torch
@@ -848,7 +863,7 @@ def main():
                                 f"({profile.resource}), binpack", "global_batch": n_pods, "seq_len": 0,
                        "parallelism": f"{world} GPU(s) advertised on 1 node; 1 rank (HBM runtime) per GPU; "
                                       f"agent={a.agent}",
-                       "bind_mode": a.bind_mode, "device_backend": backend},
+                       "bind_mode": a.bind_mode, "bind_order": a.bind_order, "device_backend": backend},
             "p50_bind_latency_ms": round(1e3 * pct(lat, 50), 3),
             "p99_bind_latency_ms": round(1e3 * pct(lat, 99), 3),
             "p50_bind_rtt_ms": round(1e3 * pct(rtt, 50), 3),

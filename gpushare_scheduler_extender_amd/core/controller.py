@@ -53,6 +53,7 @@ class Controller:
         self._raw: dict[str, bytes] = {}  # key -> raw JSON of the latest event (native parse fast path)
         self._tasks: list[asyncio.Task] = []
         self.synced_pods = 0
+        self._confirmed_list_start = 0.0  # the last LIST start whose keys the workers have all applied
         self.overcommitted: list = []
         self.sync_errors = 0
         self.pods.add_handler(Handler(self._on_pod_add, self._on_pod_update, self._on_pod_delete,
@@ -185,8 +186,15 @@ class Controller:
         return self.pods.get_by(name, ns)
 
     def gc_reservations(self) -> tuple[int, bool]:
-        """Ledger GC gated on the pod informer's last LIST (see Ledger::gc); forces a re-list when needed."""
-        n, need = self.engine.gc(self.pods.last_list_start)
+        """Ledger GC gated on the pod informer's last LIST (see Ledger::gc); forces a re-list when needed.
+
+        A LIST only proves a binding absent once the ledger has applied it: its handlers merely queue keys, the
+        workers upsert later.  So the LIST start that confirms counts only when the work queue has
+        drained (no key queued, in process or waiting for a rate-limited retry) since that LIST."""
+        start = self.pods.last_list_start
+        if self.queue.idle():
+            self._confirmed_list_start = start
+        n, need = self.engine.gc(self._confirmed_list_start)
         if need:
             self.pods.request_relist()
         return n, need

@@ -91,6 +91,10 @@ class NodeAgent:
         self.stats = {"allocate_calls": 0, "allocate_errors": 0, "mismatch": 0, "swapped_equivalent": 0,
                       "gone_during_allocate": 0,
                       "allocate_ms_max": 0.0}
+        # kubelet-side time per admission step (seconds, summed): the pod's wait for admission, the two gRPC
+        # calls as kubelet sees them, the wait for a pod worker, the runtime start, the Running status patch
+        self.timing = {"n": 0, "admit_queue": 0.0, "grpc_preferred": 0.0, "grpc_allocate": 0.0, "start_queue": 0.0,
+                       "runtime": 0.0, "status_patch": 0.0}
         self._bg: set[asyncio.Task] = set()
         self._releasing: set[asyncio.Task] = set()
         self.admit_q: asyncio.Queue = asyncio.Queue()
@@ -107,6 +111,7 @@ class NodeAgent:
         self.batch_window = batch_window
         self._held_starts: list | None = None
         self._last_of_batch = False
+        self._enqueued: dict[str, float] = {}
         # kubelet's device-ID accounting (gRPC mode): all plugin IDs, and the ones each pod holds
         self.all_ids: list[str] = []
         self.used_ids: dict[str, list[str]] = {}
@@ -174,9 +179,13 @@ class NodeAgent:
         free = sorted(set(self.all_ids) - {i for ids in self.used_ids.values() for i in ids})
         if len(free) < units:
             raise AllocateError(f"kubelet: {units} {self.profile.resource} requested, {len(free)} IDs free")
+        t0 = time.perf_counter()
         pref = await self.pclient.preferred(free, units)
         ids = list(pref.container_responses[0].deviceIDs)
+        t1 = time.perf_counter()
         r = (await self.pclient.allocate([ids])).container_responses[0]
+        self.timing["grpc_preferred"] += t1 - t0
+        self.timing["grpc_allocate"] += time.perf_counter() - t1
         who = r.annotations.get(POD_ANNOTATION, "")
         envs = dict(r.envs)
         cus = None
@@ -258,6 +267,7 @@ class NodeAgent:
                     self._flush_starts()
 
     async def _admit(self, key: str, pod: dict, uid: str):
+        self.timing["admit_queue"] += time.perf_counter() - self.seen.get(uid, time.perf_counter())
         conts = [podutil.container_limit(c, self.profile.resource) for c in (pod.get("spec") or {}).get("containers") or []]
         allocs: list[_Alloc] = []
         try:
@@ -315,6 +325,7 @@ class NodeAgent:
             self.used_ids[got.uid] = [i for a in allocs for i in a.ids]
             self.id_keys[got.uid] = got.key or key
         self.allocations[got.uid] = got.envs
+        self._enqueued[got.uid] = time.perf_counter()
         if self._held_starts is not None:
             self._held_starts.append((got.uid, key, allocs))
         else:
@@ -347,10 +358,13 @@ class NodeAgent:
             return  # deleted while waiting to start
         pod = self.pods.get(key)
         t0 = self.seen.pop(uid, time.perf_counter())
+        ts = time.perf_counter()
+        self.timing["start_queue"] += ts - self._enqueued.pop(uid, ts)
         dev = allocs[0].dev
         units = sum(int(a.envs.get(self.profile.env_container, "0") or 0) for a in allocs)
         try:
             bad = await self._admit_runtime(uid, dev, units * self.unit_bytes, allocs[0].cus)
+            self.timing["runtime"] += time.perf_counter() - ts
             if bad:
                 self.bad_stamps += bad
                 raise AdmissionError(f"{bad} bad HBM stamps after admitting {key}")
@@ -369,8 +383,11 @@ class NodeAgent:
             return
         self.running[uid] = key
         self.admitted += 1
+        tp = time.perf_counter()
         if self.report_status and pod is not None:
             await self._patch_status(pod, {"phase": "Running"})
+        self.timing["status_patch"] += time.perf_counter() - tp
+        self.timing["n"] += 1
         self.latency.append(time.perf_counter() - t0)
 
     async def _patch_status(self, pod: dict, status: dict):
@@ -462,8 +479,24 @@ async def serve_stats(box: dict, host: str = "127.0.0.1", port: int = 0):
                 "running": len(agent.running), "admit_p50_ms": round(1e3 * lat[len(lat) // 2], 3) if lat else 0.0,
                 "admit_max_ms": round(1e3 * lat[-1], 3) if lat else 0.0, **agent.stats, "native": False,
                 "plugin": "grpc" if agent.pclient is not None else "inproc"}
+        n = max(1, agent.timing["n"])
+        body["breakdown_ms"] = {k: round(1e3 * v / n, 4) for k, v in agent.timing.items() if k != "n"}
         if agent.plugin is not None:
             body["plugin_stats"] = dict(agent.plugin.stats)
+            pt = getattr(agent.plugin, "timing", None)
+            if pt:
+                na, npf = max(1, pt["n"]), max(1, pt["preferred_n"])
+                body["plugin_breakdown_ms"] = {
+                    "preferred_handler": round(1e3 * pt["preferred"] / npf, 4),
+                    "allocate_handler": round(1e3 * pt["handler"] / na, 4),
+                    "match": round(1e3 * pt["match"] / na, 4), "assign_patch": round(1e3 * pt["assign_patch"] / na, 4),
+                    "isolate": round(1e3 * pt["isolate"] / na, 4)}
+                bd = body["breakdown_ms"]
+                # gRPC + serialisation as kubelet pays it = client-side call time minus the handler's own time
+                body["plugin_breakdown_ms"]["grpc_overhead_preferred"] = round(
+                    bd["grpc_preferred"] - body["plugin_breakdown_ms"]["preferred_handler"], 4)
+                body["plugin_breakdown_ms"]["grpc_overhead_allocate"] = round(
+                    bd["grpc_allocate"] - body["plugin_breakdown_ms"]["allocate_handler"], 4)
             rc = getattr(agent.plugin, "reconciler", None)
             if rc is not None:
                 body["reconcile"] = dict(rc.stats)

@@ -86,6 +86,13 @@ class GpuSharePlugin:
         self.isolation = isolation
         self._set_devices(devices)
         self.checkpoint = checkpoint if checkpoint is not None else os.path.join(socket_dir, "gsx-allocations.json")
+        self.checkpoint_interval = 0.2
+        self._dirty = False
+        self._persist_task: asyncio.Task | None = None
+        # where an Allocate's time goes (plugin side, seconds summed over calls): matching, the ASSIGNED patch
+        # (apiserver round trip), isolation files, the whole handler
+        self.timing = {"n": 0, "match": 0.0, "assign_patch": 0.0, "isolate": 0.0, "handler": 0.0,
+                       "preferred_n": 0, "preferred": 0.0}
         self._aid = 0
         self.reconciler = None
         if podresources_socket:
@@ -199,6 +206,7 @@ class GpuSharePlugin:
         self.stats["refreshes"] += 1
 
     async def GetPreferredAllocation(self, request, context):
+        t0 = time.perf_counter()
         resp = api.PreferredAllocationResponse()
         for creq in request.container_requests:
             size = creq.allocation_size
@@ -219,6 +227,8 @@ class GpuSharePlugin:
                 chosen.append(i)
             resp.container_responses.add(deviceIDs=chosen[:size])
             self.stats["preferred"] += 1
+        self.timing["preferred_n"] += 1
+        self.timing["preferred"] += time.perf_counter() - t0
         return resp
 
     # ------------------------------------------------------------ allocation records
@@ -237,9 +247,26 @@ class GpuSharePlugin:
             self.isolation.release(r.iso)
 
     def persist_records(self):
-        """Checkpoint of the Allocate records (a restarted plugin still knows what each set of IDs was)."""
-        if not self.checkpoint:
+        """Checkpoint of the Allocate records (a restarted plugin still knows what each set of IDs was): written
+        by a background task at most every ``checkpoint_interval`` seconds, not on the Allocate path (a JSON dump
+        + rename per Allocate cost ~1 ms of the plugin's ~2.8 ms admission on MI355X, profiles/r03_gpu)."""
+        self._dirty = True
+        if self._persist_task is None or self._persist_task.done():
+            try:
+                loop = asyncio.get_running_loop()
+            except RuntimeError:
+                self._write_checkpoint()
+                return
+            self._persist_task = loop.create_task(self._persist_later())
+
+    async def _persist_later(self):
+        await asyncio.sleep(self.checkpoint_interval)
+        self._write_checkpoint()
+
+    def _write_checkpoint(self):
+        if not self.checkpoint or not self._dirty:
             return
+        self._dirty = False
         import json  # noqa: PLC0415
 
         tmp = self.checkpoint + ".tmp"
@@ -276,7 +303,9 @@ class GpuSharePlugin:
         kubelet reject the pod (UnexpectedAdmissionError) over a transient apiserver hiccup."""
         refreshed = False
         for attempt in range(ALLOCATE_ATTEMPTS):
+            tm = time.perf_counter()
             rec, whole = self.state.match(units)
+            self.timing["match"] += time.perf_counter() - tm
             if rec is None and not refreshed:
                 await self.refresh()
                 refreshed = True
@@ -302,7 +331,10 @@ class GpuSharePlugin:
             try:
                 cus = self.state.claim_cus(rec)
                 alloc = build_response(rec.obj, device, units, self.profile, mount_mode=self.mount_mode, cus=cus)
+                ti = time.perf_counter()
                 self._isolate(rec, device, cus, alloc)
+                tp = time.perf_counter()
+                self.timing["isolate"] += tp - ti
                 try:
                     pod = await self.client.patch("pods", rec.name, assigned_patch(rec.obj, self.profile,
                                                                                     alloc.annotations),
@@ -320,6 +352,7 @@ class GpuSharePlugin:
                     continue
             finally:
                 self.state.inflight.discard(rec.uid)
+            self.timing["assign_patch"] += time.perf_counter() - tp
             self.state.observe(pod)
             self.state.first_container_committed(rec, units, whole)
             self._record(rec, ids, units, alloc)
@@ -356,6 +389,7 @@ class GpuSharePlugin:
 
     async def Allocate(self, request, context):
         resp = api.AllocateResponse()
+        t0 = time.perf_counter()
         try:
             for creq in request.container_requests:
                 rec, alloc = await self.allocate_container(len(creq.devices_ids), list(creq.devices_ids))
@@ -372,6 +406,8 @@ class GpuSharePlugin:
             self.stats["allocate_ok"] += 1
             if self.reconciler is not None:
                 self.reconciler.kick()
+            self.timing["n"] += 1
+            self.timing["handler"] += time.perf_counter() - t0
             return resp
         except (AllocateError, ApiError, OSError) as e:
             self.stats["allocate_fail"] += 1
@@ -614,6 +650,9 @@ class GpuSharePlugin:
     async def stop(self):
         self._stopped = True
         self._changed.set()
+        if self._persist_task is not None:
+            self._persist_task.cancel()
+        self._write_checkpoint()
         if self.reconciler is not None:
             await self.reconciler.stop()
         for t in self._tasks:

@@ -43,6 +43,10 @@ def parse_args(argv=None):
                     help="also write per-level rotating log files here (the reference used /var/log/device-plugin)")
     ap.add_argument("--profile", default=env.get("GSX_PROFILE", "shared-gpu"))
     ap.add_argument("--bind-mode", default=env.get("GSX_BIND_MODE", "binding"), choices=["binding", "update"])
+    ap.add_argument("--bind-order", default=env.get("GSX_BIND_ORDER", "strict"), choices=["strict", "relaxed"],
+                    help="strict: equal-size binds of one node for different GPUs land in ASSUME_TIME order (default); "
+                         "relaxed: all binds concurrent, swaps repaired by the device plugin's PodResources "
+                         "reconciliation")
     ap.add_argument("--kube-qps", type=float, default=float(env.get("GSX_KUBE_QPS", "0")))
     ap.add_argument("--kube-burst", type=int, default=int(env.get("GSX_KUBE_BURST", "1000")))
     ap.add_argument("--resync", type=float, default=float(env.get("GSX_RESYNC", "30")))
@@ -76,7 +80,7 @@ def main(argv=None) -> int:
                              reservation_ttl=a.reservation_ttl, resync_period=a.resync,
                              leader_elect=bool(a.leader_elect), lease_name=a.lease_name,
                              lease_namespace=a.lease_namespace, native_controller=bool(a.native_controller),
-                             pprof=bool(a.pprof))
+                             pprof=bool(a.pprof), bind_order=a.bind_order)
         runner = await ExtenderRunner(srv, a.host, a.port, native=bool(a.native_http), http_threads=a.http_threads,
                                       pool_threads=a.bind_threads).start()
         if a.port_file:

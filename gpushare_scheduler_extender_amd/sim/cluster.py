@@ -132,9 +132,10 @@ def start_apiserver(native: bool = True, history: int = 200000, threads: int | N
 
 def start_extender(apiserver: str, profile: str = "shared-gpu", bind_mode: str = "binding", threadness: int = 1,
                    log_level: str = "warning", port: int = 0, cpus: list[int] | None = None,
-                   kube_qps: float = 0.0, kube_burst: int = 1000) -> ChildProc:
+                   kube_qps: float = 0.0, kube_burst: int = 1000, bind_order: str = "strict") -> ChildProc:
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.extender", "--host", "127.0.0.1", "--port", str(port),
                       "--apiserver", apiserver, "--profile", profile, "--bind-mode", bind_mode,
+                      "--bind-order", bind_order,
                       "--threadness", str(threadness), "--log-level", log_level, "--kube-qps", str(kube_qps),
                       "--kube-burst", str(kube_burst)], "extender", cpus=cpus)
 

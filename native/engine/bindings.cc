@@ -492,6 +492,9 @@ class Engine {
     return out;
   }
 
+  void set_relaxed_order(bool on) { l_.set_relaxed_order(on); }
+  bool relaxed_order() const { return l_.relaxed_order(); }
+
   void set_update_mode(bool on) {
     update_mode_ = on;
     if (srv_) srv_->set_update_mode(on);
@@ -747,6 +750,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("drain_bind_failures", &Engine::drain_bind_failures)
       .def("set_binds_enabled", &Engine::set_binds_enabled)
       .def("set_update_mode", &Engine::set_update_mode)
+      .def("set_relaxed_order", &Engine::set_relaxed_order)
+      .def_property_readonly("relaxed_order", &Engine::relaxed_order)
       .def("drain_annotation_repairs", &Engine::drain_annotation_repairs)
       .def("pending_count", &Engine::pending_count);
 

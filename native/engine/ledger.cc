@@ -275,6 +275,7 @@ int64_t Ledger::assume_ordered(const std::string& uid, const std::string& ns, co
 }
 
 bool Ledger::blocked_locked(const InflightBind& me) const {
+  if (relaxed_order_.load(std::memory_order_relaxed)) return false;
   for (const auto& f : inflight_) {
     if (f.seq < me.seq && f.node == me.node && f.size == me.size && (f.dev != me.dev || f.cu_count != me.cu_count)) {
       return true;

@@ -114,6 +114,11 @@ class Ledger {
   int pod_state(const std::string& uid, int64_t* dev) const;
   // Binds observed without their annotations since the last call (see AnnotationRepair)
   std::vector<AnnotationRepair> drain_repairs();
+  // "relaxed": no bind waits for another (see bind ordering below).  Safe only where the device plugin
+  // reconciles its Allocates with kubelet's PodResources record (deviceplugin/reconcile.py), which rewrites
+  // the annotations of pods kubelet started with each other's allocation.
+  void set_relaxed_order(bool on) { relaxed_order_.store(on); }
+  bool relaxed_order() const { return relaxed_order_.load(); }
 
   // ---- scheduling verbs ----
   Check check(const std::string& node, int64_t req) const;  // nodeinfo.go:113-137
@@ -209,6 +214,7 @@ class Ledger {
   };
   bool blocked_locked(const InflightBind& me) const;
   std::mutex order_mu_;
+  std::atomic<bool> relaxed_order_{false};
   std::list<InflightBind> inflight_;
   uint64_t order_seq_ = 0;
   int64_t last_assume_ns_ = 0;

@@ -191,11 +191,26 @@ void PodRuntime::admit_group_locked(const std::vector<Pending*>& group) {
     return;
   }
   bad_ += bad;
+  // An admission that asked for verification answers for every resident slice (the group's total).  One that
+  // did not is charged only with its own slice (another pod's corrupted slice must not fail it): on
+  // the rare bad group its extents are verified once more on their own.
+  auto own_bad = [&](Pending* p) -> int64_t {
+    if (p->verify || bad == 0) return static_cast<int64_t>(bad);
+    std::vector<GsxSlice> mine;
+    auto it = slices_.find(p->uid);
+    if (it == slices_.end()) return 0;
+    for (auto& e : it->second.ext) mine.push_back(GsxSlice{cfg_.arena_addr + e.first, e.second, it->second.tag});
+    uint64_t b = 0;
+    if (!mine.empty() && admit_n_(cfg_.stream, mine.data(), static_cast<int>(mine.size()), 0, 1, cfg_.stride, &b) != 0) {
+      return static_cast<int64_t>(bad);  // cannot tell: keep the conservative answer
+    }
+    return static_cast<int64_t>(b);
+  };
   for (Pending* p : fresh) {
     admitted_++;
-    p->result = static_cast<int64_t>(bad);  // a bad stamp fails every admission of its group
+    p->result = own_bad(p);
   }
-  for (Pending* p : again) p->result = static_cast<int64_t>(bad);  // its slice was re-verified in the launch
+  for (Pending* p : again) p->result = own_bad(p);  // its slice was re-verified in the launch
 }
 
 int64_t PodRuntime::admit(const std::string& uid, uint64_t bytes, bool verify, std::string* err) {

@@ -393,7 +393,9 @@ int gsx_hbm_admit_n(void* stream, const gsx_slice* slices, int n, int n_stamp, i
   // (every pair: two new extents that overlap each other must be caught by the verify launch as well)
   // opt-in (GSX_ADMIT_ONE_LAUNCH=1): it cuts GPU time per admission (6.5 vs 10.2 us) but not the wall-clock of an
   // admission, and its kernel-time tail is longer; interleaved A/Bs of the driver's bench showed no gain
-  // (profiles/r02_fused_admit/), so two launches stay the default
+  // (profiles/r02_fused_admit/), so two launches stay the default.  Its contract is weaker: the fresh stamps are
+  // written, not read back (the rows of one launch are unordered), so a bad count covers the resident slices only,
+  // where the default path also verifies every new extent it just stamped
   static const bool one_launch = [] {
     const char* e = std::getenv("GSX_ADMIT_ONE_LAUNCH");
     return e && e[0] == '1';
