@@ -326,8 +326,6 @@ def parse():
                     help="write every timed pod's scheduler timeline (CLOCK_MONOTONIC, like the wave's t0) here")
     ap.add_argument("--agent", default="node", choices=["node", "rank"],
                     help="node: one node-agent process (the node's device plugin) driving a runtime shim per GPU rank (default); rank: one agent per GPU rank")
-    ap.add_argument("--scheduler", default="native", choices=["native", "python"],
-                    help="kube-scheduler stand-in: compiled gsx-schedsim (default) or the asyncio simulator")
     ap.add_argument("--apiserver", default="native", choices=["native", "python"],
                     help="fake kube-apiserver: gsx-fakeapi (default) or the asyncio one")
     ap.add_argument("--node-agent", default="native", choices=["native", "plugin", "inproc"],
@@ -357,8 +355,6 @@ def parse():
                          "behaves like kubelet and lets the plugin reconcile (faithful)")
     ap.add_argument("--sweep", type=int, default=1, help="1: run the latency sweep after the timed region")
     ap.add_argument("--sweep-steps", type=int, default=8)
-    ap.add_argument("--inproc", action="store_true",
-                    help="run apiserver + extender in this process (no child processes; used under rocprofv3)")
     return ap.parse_args()
 
 
@@ -394,8 +390,6 @@ def main():
     # torchrun stops the other ranks with SIGTERM when one fails: exit through atexit so child servers stop too
     signal.signal(signal.SIGTERM, lambda *_: sys.exit(143))
     a = parse()
-    if a.inproc:
-        a.agent = "rank"  # no child processes at all: the agents run in-process too
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         # `python bench.py --gpus N` without a launcher: start torchrun as a CHILD process (this process has not
         # touched the GPU, and is never replaced by exec) and exit with its code
@@ -444,18 +438,7 @@ def main():
     children = []
     api_url = ext_url = ""
     lt = LoopThread()
-    inproc = []
-    if rank == 0 and a.inproc:
-        from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
-        from gpushare_scheduler_extender_amd.k8s.client import KubeClient as _KC
-        from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
-        from gpushare_scheduler_extender_amd.models.profile import get_profile as _gp
-
-        api_r = lt.run(FakeApiServerRunner().start())
-        ext_r = lt.run(ExtenderRunner(ExtenderServer(_KC(api_r.url), _gp(a.profile), bind_mode=a.bind_mode)).start())
-        inproc = [ext_r, api_r]
-        api_url, ext_url = api_r.url, ext_r.url
-    elif rank == 0:
+    if rank == 0:
         from gpushare_scheduler_extender_amd.sim.cluster import (start_apiserver, start_extender, start_node_agent,
                                                                  start_scheduler)
 
@@ -465,7 +448,7 @@ def main():
                              bind_order=a.bind_order)
         children.append(ext)
         # kube-scheduler stand-in: its own process, like the real one (serial scheduling cycle)
-        children.append(start_scheduler(api.url, ext.url, profile=a.profile, native=a.scheduler == "native",
+        children.append(start_scheduler(api.url, ext.url, profile=a.profile, native=True,
                                         cpus=cpu_plan.get("scheduler")))
         if a.agent == "node":
             # the node's device plugin / kubelet stand-in: one process for all GPUs of the node, like a DaemonSet
@@ -485,7 +468,6 @@ def main():
     from gpushare_scheduler_extender_amd.k8s.client import KubeClient
     from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
     from gpushare_scheduler_extender_amd.models.profile import get_profile
-    from gpushare_scheduler_extender_amd.sim.scheduler import SchedulerSim
 
     # ranks do no CPU tensor work: one intra-op thread each, so 8 ranks never burst past a container's CPU quota
     torch.set_num_threads(1)
@@ -578,18 +560,14 @@ def main():
                           mount_mode="isolated")
         lt.run(agent.start())
 
-    sim = client = tracker = sched_http = None
+    client = tracker = sched_http = None
     if rank == 0:
         from gpushare_scheduler_extender_amd.core.engine import native as _native_engine
         from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as _HttpClient
 
         E = _native_engine()
         client = KubeClient(api_url)
-        if a.inproc:
-            sim = SchedulerSim(KubeClient(api_url), ext_url, profile, max_inflight_binds=256)
-            lt.run(sim.start())
-        else:
-            sched_http = _HttpClient(next(c.url for c in children if c.name == "scheduler"))
+        sched_http = _HttpClient(next(c.url for c in children if c.name == "scheduler"))
         # the wave driver (load generator) is native: a reflector over the wave's pods that answers
         # "all bound / Running / gone?" and a keep-alive batch client for the creates (native/engine/tracker.cc)
         tracker = E.PodTracker({"server": api_url}, "default", "gsx-wave")
@@ -607,7 +585,7 @@ def main():
         pod_tmpl = json.dumps(pod_tmpl, separators=(",", ":"))
     from gpushare_scheduler_extender_amd.utils.gctune import tune
 
-    if rank == 0 and a.api_latency_ms and not a.inproc:
+    if rank == 0 and a.api_latency_ms:
         set_latency(api_batch, a.api_latency_ms)
     tune()
     if use_gpu and a.gpu_warm_ms > 0:
@@ -684,10 +662,6 @@ def main():
                 "t_bound": t_bound - t0, "t_run": t_run - t0, "t_total": t_end - t0, "t0": t0}
 
     async def fetch_timings(keys):
-        if sim is not None:
-            tm = [vars(sim.stats.timings[k]) for k in keys]
-            sim.forget(keys)
-            return tm
         # the scheduler process's per-pod timings (its own clock; only differences are used)
         body = json.dumps(keys).encode()
         got = json.loads((await sched_http.request("POST", "/v1/timings", body)).body)
@@ -804,13 +778,13 @@ def main():
             n = d[h + "_n"]
             extender_stats[h + "_mean_ms"] = round(1e3 * d[h + "_s"] / n, 4) if n else None
     apiserver_stats = None
-    if rank == 0 and not a.inproc:
+    if rank == 0:
         st, body = api_batch.run([("GET", "/fake/stats", b"")], 1)[0]
         apiserver_stats = json.loads(body) if st == 200 else {"error": st}
         apiserver_stats.pop("counts", None)
 
     sweep = ref_client = plugin_row = None
-    if rank == 0 and a.sweep and not a.inproc:
+    if rank == 0 and a.sweep:
         runner = WaveRunner(wave, fetch_timings, lt, n_pods, a.warmup + a.steps, extender_counters)
         try:
             sweep, ref_client = latency_sweep(a, children, api_url, api_batch, runner, inspect_used)
@@ -924,15 +898,10 @@ def main():
         else:
             lt.run(shim.stop(), 30)
         if rank == 0:
-            if sim is not None:
-                lt.run(sim.stop(), 30)
-                lt.run(sim.client.close(), 30)
             tracker.stop()
             if sched_http is not None:
                 lt.run(sched_http.close(), 30)
             lt.run(client.close(), 30)
-            for r in inproc:
-                lt.run(r.stop(), 30)
     finally:
         runtime.close()
         lt.stop()

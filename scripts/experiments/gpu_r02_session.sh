@@ -23,6 +23,6 @@ for i in 1 2 3; do
 import json; d=json.load(open('$OUT/bench$i.json'))
 print($i, d['value'], d['wave_pods_per_s'], d['p50_bind_latency_ms'], d['p99_bind_latency_ms'])"
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --steps 20 --warmup 5 --inproc --sweep 0 > $OUT/prof.log 2>&1; rc=$?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --steps 20 --warmup 5 --sweep 0 > $OUT/prof.log 2>&1; rc=$?
 echo "rocprof rc=$rc"; tail -2 $OUT/prof.log
 exit 0

@@ -20,7 +20,7 @@ timeout -k 10 300 python bench.py --json-out "$out/bench_n1.json" > "$out/bench_
 echo "bench N=1 rc=$rc"; tail -1 "$out/bench_n1.log"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o bench -- python3 bench.py --steps 20 --warmup 5 \
-  --inproc > "$out/prof.log" 2>&1; rc=$?
+  > "$out/prof.log" 2>&1; rc=$?
 echo "rocprof rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 db=$(find "$out/prof" -name '*.db' | head -n 1)

@@ -15,5 +15,5 @@ import json; d=json.load(open('$OUT/b_${s}_$i.json')); na=d['node_agent']
 print('$s', $i, d['value'], d['wave_pods_per_s']['p50'], d['wave_ms_p50'], na.get('mean_ms') or na.get('max_ms'))"
   done
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --steps 20 --warmup 5 --inproc --sweep 0 --stamp-stride 2097152 > $OUT/prof.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --steps 20 --warmup 5 --sweep 0 --stamp-stride 2097152 > $OUT/prof.log 2>&1 || exit $?
 echo rocprof ok

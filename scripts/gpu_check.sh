@@ -16,7 +16,7 @@ timeout -k 10 600 python bench.py --steps 20 --warmup 3 --json-out gpurun_out/be
 echo "bench rc=$rc"; tail -3 gpurun_out/bench1.log
 ok $rc || exit $rc
 if [ "${GSX_PROFILE_RUN:-1}" = "1" ]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench -- python3 bench.py --steps 10 --warmup 2 --inproc > gpurun_out/prof.log 2>&1; rc=$?
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench -- python3 bench.py --steps 10 --warmup 2 > gpurun_out/prof.log 2>&1; rc=$?
   echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
 fi
 exit 0

@@ -18,7 +18,7 @@ for i in 1 2 3; do
 import json; d=json.load(open('$OUT/bench$i.json'))
 print('bench', $i, d['value'], d['wave_pods_per_s']['p50'], d['p50_bind_latency_ms'], d['p99_bind_latency_ms'], d['timed_region_ms']['max_over_ranks'])"
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --steps 20 --warmup 5 --inproc --sweep 0 > $OUT/prof.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --steps 20 --warmup 5 --sweep 0 > $OUT/prof.log 2>&1 || exit $?
 echo "rocprof ok"
 for n in 2 4 8; do
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
