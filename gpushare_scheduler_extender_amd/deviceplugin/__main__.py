@@ -37,6 +37,14 @@ def main(argv=None) -> int:
     ap.add_argument("--debug-port", type=int, default=int(env.get("GSX_DEBUG_PORT", "0")),
                     help="serve /healthz, /metrics and /debug/state on this port (0: off)")
     ap.add_argument("--debug-host", default=env.get("GSX_DEBUG_HOST", "127.0.0.1"))
+    ap.add_argument("--isolation", default=env.get("GSX_ISOLATION", "enforce"), choices=["enforce", "advisory"],
+                    help="enforce: Allocate mounts the pod's CU partition / HBM share config and libgsx_isolate.so "
+                         "(via /etc/ld.so.preload); advisory: env hints only (HSA_CU_MASK, GSX_GPU_MEM_FRACTION)")
+    ap.add_argument("--isolation-dir", default=env.get("GSX_ISOLATION_DIR", "/var/lib/gsx/isolation"))
+    ap.add_argument("--podresources-socket", default=env.get("GSX_PODRESOURCES_SOCKET",
+                                                              "/var/lib/kubelet/pod-resources/kubelet.sock"),
+                    help="kubelet's PodResources API; '' disables the reconciliation of Allocates")
+    ap.add_argument("--reconcile-interval", type=float, default=float(env.get("GSX_RECONCILE_INTERVAL", "2")))
     ap.add_argument("--log-level", default=env.get("LOG_LEVEL", "info"))
     ap.add_argument("--log-dir", default=env.get("GSX_LOG_DIR", ""))
     a = ap.parse_args(argv)
@@ -49,9 +57,14 @@ def main(argv=None) -> int:
         logging.getLogger("gsx.main").info("%d GPU(s) via %s: %s", len(devs), backend,
                                            ", ".join(f"{d.index}:{d.bdf}:{d.total_bytes >> 30}GiB" for d in devs))
         client = KubeClient(KubeConfig.auto(a.kubeconfig, a.apiserver))
+        from .isolation import IsolationManager  # noqa: PLC0415
+
+        iso = IsolationManager(a.isolation_dir) if a.isolation == "enforce" else None
         plugin = GpuSharePlugin(client, a.node, devs, get_profile(a.profile), unit=a.unit, socket_dir=a.socket_dir,
                                 mount_mode=a.mount_mode, health_backend="amdsmi" if backend == "amdsmi" else None,
-                                health_interval=a.health_interval, reserve_bytes=int(a.reserve_gib * (1 << 30)))
+                                health_interval=a.health_interval, reserve_bytes=int(a.reserve_gib * (1 << 30)),
+                                podresources_socket=a.podresources_socket or None,
+                                reconcile_interval=a.reconcile_interval, isolation=iso)
         await plugin.start()
         if a.debug_port:
             port = await plugin.serve_debug(a.debug_host, a.debug_port)
