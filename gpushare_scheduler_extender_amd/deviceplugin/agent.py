@@ -552,6 +552,9 @@ def main(argv=None) -> int:
     ap.add_argument("--batch-window", type=float, default=-1.0,
                     help="seconds kubelet collects pods into one admission batch (default 0.02 with --faithful)")
     ap.add_argument("--no-reconcile", action="store_true", help="the plugin does not reconcile with PodResources")
+    ap.add_argument("--isolation-dir", default="",
+                    help="enforced isolation: the plugin writes each pod's config + HBM ledger here (and answers the "
+                         "container mounts); '' = advisory env only")
     ap.add_argument("--port-file", default="")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.WARNING)
@@ -572,10 +575,15 @@ def main(argv=None) -> int:
         prsock = os.path.join(sock_dir, "pod-resources", "kubelet.sock") if a.faithful else None
         window = a.batch_window if a.batch_window >= 0 else (0.02 if a.faithful else 0.0)
         if a.plugin == "grpc":
+            iso = None
+            if a.isolation_dir:
+                from .isolation import IsolationManager  # noqa: PLC0415
+
+                iso = IsolationManager(a.isolation_dir)
             plugin = GpuSharePlugin(KubeClient(KubeConfig.auto(a.kubeconfig, a.apiserver)), a.node, devs, profile,
                                     unit=a.unit, socket_dir=sock_dir,
                                     podresources_socket=None if a.no_reconcile else prsock,
-                                    reconcile_interval=0.5)
+                                    reconcile_interval=0.5, isolation=iso)
             await plugin.start(register=False, publish=False)
             agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
                               workers=a.workers, plugin_socket=plugin.socket_path, faithful=a.faithful,

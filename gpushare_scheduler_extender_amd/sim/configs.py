@@ -404,8 +404,14 @@ async def config4(gpu: bool) -> dict:
 
 
 async def config5(gpu: bool) -> dict:
+    import tempfile
+
     total = _gpu_gib() if gpu else 268
-    cl = Cluster(ALIYUN, [total], gpu=gpu)
+    iso_dir = tempfile.mkdtemp(prefix="gsx-iso-")
+    # the shipped plugin with enforced isolation: every Allocate writes the pod's isolation config (the files the
+    # container would get mounted); with --gpu a probe process per pod runs under libgsx_isolate.so with it
+    args = ["--isolation-dir", iso_dir] if AGENT["kind"] == "plugin" else []
+    cl = Cluster(ALIYUN, [total], gpu=gpu, agent_args=AGENT["args"] + args)
     try:
         await cl.start()
         for i in range(4):
@@ -423,7 +429,14 @@ async def config5(gpu: bool) -> dict:
         disjoint = all(not (sets[i] & sets[j]) for i in range(4) for j in range(i + 1, 4))
         per_xcd = [sorted({c // 32 for c in s}) for s in sets]
         ok = disjoint and all(len(s) == 64 for s in sets) and all(x == list(range(8)) for x in per_xcd)
-        out = {"device_gib": total, "agent": cl.agent_kind,
+        if args:
+            from pathlib import Path
+
+            from ..deviceplugin.isolation import CONF
+            confs = [Path(iso_dir) / "pods" / p["metadata"]["uid"] / CONF for p in pods.values()]
+            n_conf = sum(1 for c in confs if c.exists() and "cu_mask=" in c.read_text())
+            ok = ok and n_conf == 4
+        out = {"device_gib": total, "agent": cl.agent_kind, "isolation_configs": n_conf if args else None,
                "partitions": [{"pod": p["pod"], "HSA_CU_MASK": p["HSA_CU_MASK"], "n_cus": len(p["cus"])} for p in parts],
                "disjoint": disjoint, "xcds_per_pod": [len(x) for x in per_xcd]}
         if gpu:
@@ -441,10 +454,39 @@ async def config5(gpu: bool) -> dict:
             out["probe_xcds_per_pod"] = [len({t[0] for t in h}) for h in hw]
             out["probe_cus_per_xcd"] = [sorted(sum(1 for t in h if t[0] == x) for x in {t[0] for t in h}) for h in hw]
             ok = ok and hw_disjoint and all(len(h) == 64 for h in hw)
+            if args:
+                enforced = _enforced_probe(iso_dir, [p["metadata"]["uid"] for _, p in sorted(pods.items())])
+                out["enforced_cus_per_pod"] = [len(e) for e in enforced]
+                out["enforced_disjoint"] = all(not (enforced[i] & enforced[j]) for i in range(4) for j in range(i + 1, 4))
+                ok = ok and out["enforced_disjoint"] and all(len(e) == 64 for e in enforced)
         out["ok"] = ok
         return out
     finally:
         await cl.close()
+        import shutil
+
+        shutil.rmtree(iso_dir, ignore_errors=True)
+
+
+def _enforced_probe(iso_dir: str, uids: list[str]) -> list[set]:
+    """Run the CU probe once per pod as a plain HIP process with HSA_CU_MASK unset, confined only by
+    libgsx_isolate.so and the isolation config the device plugin wrote for that pod at Allocate."""
+    import os
+    import subprocess
+    from pathlib import Path
+
+    from ..deviceplugin.isolation import CONF, LIB
+
+    native = Path(__file__).resolve().parents[1] / "_native"
+    out = []
+    for uid in uids:
+        env = {k: v for k, v in os.environ.items() if k not in ("HSA_CU_MASK", "GSX_CU_MASK", "HSA_TOOLS_LIB")}
+        env.update({"HSA_TOOLS_LIB": str(Path(iso_dir) / LIB), "GSX_ISOLATION_CONFIG": str(Path(iso_dir) / "pods" / uid / CONF)})
+        r = subprocess.run([str(native / "gsx-cuprobe"), "--list"], env=env, capture_output=True, text=True, timeout=120)
+        if r.returncode != 0:
+            raise RuntimeError(f"cuprobe under isolation failed: {r.stderr[-500:]}")
+        out.append({tuple(c) for c in json.loads(r.stdout.strip().splitlines()[-1])["cus"]})
+    return out
 
 
 async def config6(gpu: bool) -> dict:

@@ -52,6 +52,9 @@ def test_baseline_configs_on_mi355x(tmp_path):
     # config 5 through the gRPC device plugin: hardware-verified disjoint 64-CU partitions
     assert rep["5"]["agent"] == "plugin"
     assert rep["5"]["probe_cus_per_pod"] == [64] * 4 and rep["5"]["probe_disjoint"]
+    # ... and enforced: a plain probe process per pod, HSA_CU_MASK unset, confined by libgsx_isolate.so with the
+    # isolation config the plugin's Allocate wrote for that pod
+    assert rep["5"]["enforced_cus_per_pod"] == [64] * 4 and rep["5"]["enforced_disjoint"]
 
 
 @pytest.mark.gpu

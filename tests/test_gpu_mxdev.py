@@ -78,8 +78,16 @@ def test_amdsmi_health_counters_readable():
     for d in s.devices():
         h = s.health(d["index"])
         print(d["index"], h)
-        assert h["healthy"] is True
+        assert h["healthy"] is True and h["reason"] == ""
         assert h["ecc_uncorrectable"] >= 0 and h["ecc_correctable"] >= 0
+        # RAS per block (HBM / GFX / SDMA / xGMI), the xGMI link status, throttle state and the partition modes
+        # the plugin polls (a partition change re-shapes the advertised devices)
+        for k in ("ras_umc_uncorrectable", "ras_gfx_uncorrectable", "ras_sdma_uncorrectable",
+                  "ras_xgmi_uncorrectable", "ras_xgmi_correctable"):
+            assert h[k] >= 0, (k, h)
+        assert h["xgmi_error"] == 0, h
+        assert isinstance(h["thermal_throttle"], bool) and isinstance(h["power_throttle"], bool)
+        assert h["partition"] == d["partition"] and h["memory_partition"] == d["memory_partition"], (h, d)
 
 
 def test_device_plugin_advertises_real_inventory():
