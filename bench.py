@@ -44,6 +44,7 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import gc
 import json
 import os
 import statistics
@@ -326,8 +327,6 @@ def parse():
                     help="write every timed pod's scheduler timeline (CLOCK_MONOTONIC, like the wave's t0) here")
     ap.add_argument("--agent", default="node", choices=["node", "rank"],
                     help="node: one node-agent process (the node's device plugin) driving a runtime shim per GPU rank (default); rank: one agent per GPU rank")
-    ap.add_argument("--apiserver", default="native", choices=["native", "python"],
-                    help="fake kube-apiserver: gsx-fakeapi (default) or the asyncio one")
     ap.add_argument("--node-agent", default="native", choices=["native", "plugin", "inproc"],
                     help="kubelet + device plugin: gsx-nodeagent (default), or the kubelet stand-in driving the "
                          "shipped gRPC device plugin over its unix socket (plugin) / in-process (inproc)")
@@ -442,13 +441,13 @@ def main():
         from gpushare_scheduler_extender_amd.sim.cluster import (start_apiserver, start_extender, start_node_agent,
                                                                  start_scheduler)
 
-        api = start_apiserver(native=a.apiserver == "native", cpus=cpu_plan.get("apiserver"))
+        api = start_apiserver(cpus=cpu_plan.get("apiserver"))
         children.append(api)
         ext = start_extender(api.url, profile=a.profile, bind_mode=a.bind_mode, cpus=cpu_plan.get("extender"),
                              bind_order=a.bind_order)
         children.append(ext)
         # kube-scheduler stand-in: its own process, like the real one (serial scheduling cycle)
-        children.append(start_scheduler(api.url, ext.url, profile=a.profile, native=True,
+        children.append(start_scheduler(api.url, ext.url, profile=a.profile,
                                         cpus=cpu_plan.get("scheduler")))
         if a.agent == "node":
             # the node's device plugin / kubelet stand-in: one process for all GPUs of the node, like a DaemonSet
@@ -712,6 +711,10 @@ def main():
             cpu0 = _cpu_times(children)
             rss0 = _rss_mib(children)
             cg0 = _cgroup_cpu()
+            # the wave driver's objects are long-lived: a cyclic-GC pass inside a 0.3 ms wave is pure noise
+            gc.collect()
+            gc.freeze()
+            gc.disable()
             bracket()
             if world > 1:
                 # rank 0 leaves the barrier up to ~1.5 ms after the others (its one core also runs the wave
@@ -737,6 +740,7 @@ def main():
     t_waves_end = time.perf_counter()
     bracket()
     elapsed = time.perf_counter() - t_start
+    gc.enable()
     own_elapsed = elapsed
     cpu1 = _cpu_times(children)
     rss1 = _rss_mib(children)

@@ -37,6 +37,9 @@ def main(argv=None) -> int:
     ap.add_argument("--debug-port", type=int, default=int(env.get("GSX_DEBUG_PORT", "0")),
                     help="serve /healthz, /metrics and /debug/state on this port (0: off)")
     ap.add_argument("--debug-host", default=env.get("GSX_DEBUG_HOST", "127.0.0.1"))
+    ap.add_argument("--debug-port-file", default="", help="write the debug port here once it listens (port 0)")
+    ap.add_argument("--no-publish", action="store_true",
+                    help="do not publish the node's capacity / device inventory (a harness already did)")
     ap.add_argument("--isolation", default=env.get("GSX_ISOLATION", "enforce"), choices=["enforce", "advisory"],
                     help="enforce: Allocate mounts the pod's CU partition / HBM share config and libgsx_isolate.so "
                          "(via /etc/ld.so.preload); advisory: env hints only (HSA_CU_MASK, GSX_GPU_MEM_FRACTION)")
@@ -65,9 +68,13 @@ def main(argv=None) -> int:
                                 health_interval=a.health_interval, reserve_bytes=int(a.reserve_gib * (1 << 30)),
                                 podresources_socket=a.podresources_socket or None,
                                 reconcile_interval=a.reconcile_interval, isolation=iso)
-        await plugin.start()
-        if a.debug_port:
+        await plugin.start(publish=not a.no_publish)
+        if a.debug_port or a.debug_port_file:
             port = await plugin.serve_debug(a.debug_host, a.debug_port)
+            if a.debug_port_file:
+                with open(a.debug_port_file + ".tmp", "w") as f:
+                    f.write(str(port))
+                os.replace(a.debug_port_file + ".tmp", a.debug_port_file)
             logging.getLogger("gsx.main").info("debug endpoints on %s:%d", a.debug_host, port)
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()

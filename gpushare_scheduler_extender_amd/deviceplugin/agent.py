@@ -116,6 +116,7 @@ class NodeAgent:
         self.all_ids: list[str] = []
         self.used_ids: dict[str, list[str]] = {}
         self.id_keys: dict[str, str] = {}  # uid -> ns/name of the pod holding used_ids[uid]
+        self.plugin_stats_url: str | None = None  # the plugin's /debug/state when it runs as its own process
         self.prserver = None
         if podresources_socket:
             from .podresources import PodResourcesServer  # noqa: PLC0415
@@ -434,6 +435,52 @@ class NodeAgent:
         await self.pods.stop()
 
 
+async def _spawn_plugin(a, sock_dir: str, devs: list[Device], prsock: str | None, box: dict):
+    """Start the shipped device plugin as its own process, the way the DaemonSet runs it, and wait for it to
+    register with kubelet (this stand-in's Registration service).  Returns (child, endpoint socket, stats URL)."""
+    import dataclasses  # noqa: PLC0415
+    import json  # noqa: PLC0415
+    import os  # noqa: PLC0415
+    import sys  # noqa: PLC0415
+
+    from .plugin import FakeKubelet  # noqa: PLC0415
+
+    kubelet = FakeKubelet(sock_dir)
+    await kubelet.start()
+    box["kubelet"] = kubelet
+    spec = os.path.join(sock_dir, "devices.json")  # the node's inventory, as the plugin's (fake) backend sees it
+    with open(spec, "w") as f:
+        json.dump([dataclasses.asdict(d) for d in devs], f)
+    port_file = os.path.join(sock_dir, "plugin-debug.port")
+    cmd = [sys.executable, "-m", "gpushare_scheduler_extender_amd.deviceplugin", "--node", a.node,
+           "--profile", a.profile, "--unit", a.unit, "--backend", "fake", "--socket-dir", sock_dir, "--no-publish",
+           "--podresources-socket", "" if (a.no_reconcile or not prsock) else prsock, "--reconcile-interval", "0.5",
+           "--isolation", "enforce" if a.isolation_dir else "advisory", "--debug-port", "0",
+           "--debug-port-file", port_file, "--log-level", "warning"]
+    if a.isolation_dir:
+        cmd += ["--isolation-dir", a.isolation_dir]
+    if a.apiserver:
+        cmd += ["--apiserver", a.apiserver]
+    if a.kubeconfig:
+        cmd += ["--kubeconfig", a.kubeconfig]
+    env = dict(os.environ, GSX_FAKE_DEVICES=spec)
+    child = await asyncio.create_subprocess_exec(*cmd, env=env)
+    box["plugin_child"] = child
+    try:
+        await asyncio.wait_for(kubelet.registered.wait(), 120)
+    except asyncio.TimeoutError:
+        raise RuntimeError("the device plugin never registered with kubelet") from None
+    reg = kubelet.registrations[-1]
+    deadline = time.monotonic() + 30
+    while not os.path.exists(port_file):
+        if time.monotonic() > deadline:
+            raise RuntimeError("the device plugin published no debug port")
+        await asyncio.sleep(0.02)
+    with open(port_file) as f:
+        url = f"http://127.0.0.1:{int(f.read().strip())}"
+    return child, os.path.join(sock_dir, reg.endpoint), url
+
+
 async def node_devices_and_endpoints(client: KubeClient, node: str, timeout: float = 60.0):
     """Wait for the node's device inventory + runtime endpoints annotations; return (devices, endpoints)."""
     import json  # noqa: PLC0415
@@ -478,12 +525,29 @@ async def serve_stats(box: dict, host: str = "127.0.0.1", port: int = 0):
         body = {"admitted": agent.admitted, "failed": agent.failed, "bad_stamps": agent.bad_stamps,
                 "running": len(agent.running), "admit_p50_ms": round(1e3 * lat[len(lat) // 2], 3) if lat else 0.0,
                 "admit_max_ms": round(1e3 * lat[-1], 3) if lat else 0.0, **agent.stats, "native": False,
-                "plugin": "grpc" if agent.pclient is not None else "inproc"}
+                "plugin": ("process" if getattr(agent, "plugin_stats_url", None) else "grpc")
+                if agent.pclient is not None else "inproc"}
         n = max(1, agent.timing["n"])
         body["breakdown_ms"] = {k: round(1e3 * v / n, 4) for k, v in agent.timing.items() if k != "n"}
+        pstats = pt = prec = None
         if agent.plugin is not None:
-            body["plugin_stats"] = dict(agent.plugin.stats)
-            pt = getattr(agent.plugin, "timing", None)
+            pstats, pt = dict(agent.plugin.stats), getattr(agent.plugin, "timing", None)
+            rc = getattr(agent.plugin, "reconciler", None)
+            prec = dict(rc.stats) if rc is not None else None
+        elif getattr(agent, "plugin_stats_url", None):  # the plugin's own process: its /debug/state
+            try:
+                from ..k8s.fasthttp import Client as HttpClient  # noqa: PLC0415
+
+                hc = HttpClient(agent.plugin_stats_url)
+                try:
+                    st = json.loads((await hc.request("GET", "/debug/state")).body)
+                finally:
+                    await hc.close()
+                pstats, pt, prec = st.get("stats"), st.get("timing"), st.get("reconcile")
+            except (OSError, ValueError) as e:
+                body["plugin_error"] = repr(e)
+        if pstats is not None:
+            body["plugin_stats"] = pstats
             if pt:
                 na, npf = max(1, pt["n"]), max(1, pt["preferred_n"])
                 body["plugin_breakdown_ms"] = {
@@ -497,9 +561,8 @@ async def serve_stats(box: dict, host: str = "127.0.0.1", port: int = 0):
                     bd["grpc_preferred"] - body["plugin_breakdown_ms"]["preferred_handler"], 4)
                 body["plugin_breakdown_ms"]["grpc_overhead_allocate"] = round(
                     bd["grpc_allocate"] - body["plugin_breakdown_ms"]["allocate_handler"], 4)
-            rc = getattr(agent.plugin, "reconciler", None)
-            if rc is not None:
-                body["reconcile"] = dict(rc.stats)
+            if prec is not None:
+                body["reconcile"] = prec
         body["faithful"] = agent.faithful
         return web.Response(text=json.dumps(body), content_type="application/json")
 
@@ -525,6 +588,9 @@ def main(argv=None) -> int:
 
     ``--plugin grpc`` (default): the shipped :class:`GpuSharePlugin` is served on a unix socket in this process
     (devices from the node's inventory annotation) and driven over gRPC like kubelet drives it;
+    ``--plugin process``: the plugin runs as deployed -- its own process (``python -m
+    gpushare_scheduler_extender_amd.deviceplugin``) that registers with this stand-in's Registration service on
+    ``<socket-dir>/kubelet.sock`` and is then called on the endpoint it registered;
     ``--plugin inproc``: the same plugin called directly.
     """
     import argparse  # noqa: PLC0415
@@ -543,7 +609,9 @@ def main(argv=None) -> int:
     ap.add_argument("--profile", default="shared-gpu")
     ap.add_argument("--unit", default="GiB")
     ap.add_argument("--workers", type=int, default=32)
-    ap.add_argument("--plugin", default="grpc", choices=["grpc", "inproc"])
+    ap.add_argument("--plugin", default="grpc", choices=["grpc", "process", "inproc"],
+                    help="grpc: the plugin served from this process; process: the shipped plugin as its own process "
+                         "(python -m ...deviceplugin), found through kubelet's Registration service; inproc: called")
     ap.add_argument("--socket-dir", default="")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--faithful", action="store_true",
@@ -588,6 +656,12 @@ def main(argv=None) -> int:
             agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
                               workers=a.workers, plugin_socket=plugin.socket_path, faithful=a.faithful,
                               batch_window=window, podresources_socket=prsock)
+        elif a.plugin == "process":
+            child, endpoint, stats_url = await _spawn_plugin(a, sock_dir, devs, prsock, box)
+            agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
+                              workers=a.workers, plugin_socket=endpoint, faithful=a.faithful,
+                              batch_window=window, podresources_socket=prsock)
+            agent.plugin_stats_url = stats_url
         else:
             agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
                               workers=a.workers)
@@ -604,6 +678,13 @@ def main(argv=None) -> int:
             loop.add_signal_handler(s, stop.set)
         await stop.wait()
         await agent.stop()
+        if box.get("plugin_child") is not None:
+            box["plugin_child"].terminate()
+            try:
+                await asyncio.wait_for(box["plugin_child"].wait(), 10)
+            except asyncio.TimeoutError:
+                box["plugin_child"].kill()
+            await box["kubelet"].stop()
         if plugin is not None:
             await plugin.stop()
             await plugin.client.close()

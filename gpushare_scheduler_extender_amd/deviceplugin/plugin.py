@@ -63,6 +63,7 @@ def fake_ids(dev: Device, units: int) -> list[str]:
 
 
 ALLOCATE_ATTEMPTS = 8  # per container request: transient apiserver failures retried with capped backoff
+GUARD_WAIT_S = 5.0  # how long an Allocate waits for a physically full GPU to drain a stopping container
 POD_ANNOTATION = "gpushare.amd.com/pod"  # container annotation: the pod this Allocate was matched to
 
 class GpuSharePlugin:
@@ -312,9 +313,22 @@ class GpuSharePlugin:
                 rec, whole = self.state.match(units)
             if rec is None and self.state.unannotated(units):
                 rec, whole = await self._wait_for_annotations(units)
+            if rec is None and self.reconciler is not None and self.reconciler.pr.available():
+                # kubelet may have started another pod's container with this pod's allocation (a swap the
+                # reconciliation has not repaired yet): repair now, the exchange makes this pod a candidate again
+                self.stats["reconcile_on_miss"] = self.stats.get("reconcile_on_miss", 0) + 1
+                for k in range(8):
+                    await self._reconcile_now(urgent=True)
+                    rec, whole = self.state.match(units)
+                    if rec is not None:
+                        break
+                    await asyncio.sleep(0.02 * (k + 1))
             if rec is None:
+                same = [f"{p.key}:{p.phase}:{p.assigned}:gpu{p.dev}" for p in self.state.pods.values()
+                        if p.request == units]
                 raise AllocateError(f"no pending pod on {self.node} requests {units} {self.profile.resource} "
-                                    f"with {self.profile.annotation_assigned}=false")
+                                    f"with {self.profile.annotation_assigned}=false (pods of that size: "
+                                    f"{', '.join(same[:8]) or 'none'})")
             device = self.devices.get(rec.dev)
             if device is None:
                 raise AllocateError(f"pod {rec.key} annotated with GPU {rec.dev}, not on this node")
@@ -327,6 +341,11 @@ class GpuSharePlugin:
                 self.state.later_container_allocated(rec, units)
                 self._record(rec, ids, units, alloc)
                 return rec, alloc
+            if self.reconciler is not None:
+                rec = await self._physical_guard(rec, units)
+                device = self.devices[rec.dev]
+                cp = self.state.cus.get(rec.dev)
+                had_cus = cp is not None and cp.holds(rec.uid)
             self.state.inflight.add(rec.uid)
             try:
                 cus = self.state.claim_cus(rec)
@@ -358,6 +377,87 @@ class GpuSharePlugin:
             self._record(rec, ids, units, alloc)
             return rec, alloc
         raise AllocateError("unreachable")
+
+    async def _reconcile_now(self, urgent: bool = False):
+        try:
+            await self.reconciler.run_once(urgent)
+        except Exception as e:  # noqa: BLE001 - an apiserver error: the caller retries
+            log.debug("reconcile pass: %r", e)
+
+    def _physical_used(self, dev: int) -> int:
+        """Units kubelet has handed out on ``dev`` (the Allocate records of live pods: what really runs there)."""
+        return sum(r.units for r in self.state.records.values() if r.dev == dev)
+
+    def _annotated_used(self, dev: int, skip: str = "") -> int:
+        """Units the pod annotations put on ``dev`` (what the extender's ledger accounts)."""
+        return sum(p.request for p in self.state.pods.values() if p.dev == dev and p.uid != skip and not p.complete)
+
+    async def _physical_guard(self, rec: PodRec, units: int) -> PodRec:
+        """Never start a container on a GPU that is physically full.  The extender placed ``rec`` by the
+        annotations; after a swap kubelet has not told us about yet, a deletion can free the GPU the annotation
+        names while the container that really ran there lives on.  Repair the records first; if the GPU is still
+        full, move ``rec`` (not yet started) to a GPU of this node with room by both counts, hold-protected like a
+        reconciliation exchange; with no such GPU, fail the Allocate rather than over-commit."""
+        cap = self.units.get(rec.dev, 0)
+        if self._physical_used(rec.dev) + units <= cap:
+            return rec
+        self.stats["physical_guard"] = self.stats.get("physical_guard", 0) + 1
+        # a deleted pod's container may still be stopping (its record goes once kubelet stops listing its IDs):
+        # give it GUARD_WAIT_S before moving the pod or failing the Allocate
+        deadline = time.monotonic() + GUARD_WAIT_S
+        delay = 0.02
+        while True:
+            await self._reconcile_now(urgent=True)
+            rec = self.state.pods.get(rec.uid, rec)
+            if self._physical_used(rec.dev) + units <= self.units.get(rec.dev, 0):
+                return rec
+            if time.monotonic() >= deadline:
+                break
+            await asyncio.sleep(delay)
+            delay = min(0.2, delay * 2)
+        if rec.uid in self.reconciler.busy():
+            raise AllocateError(f"GPU {rec.dev} of {self.node} is physically full and {rec.key} is in an unfinished "
+                                f"reconciliation exchange")
+        best = self.room_for(rec, units)
+        if best < 0:
+            keys = {p.uid: p.key for p in self.state.pods.values()}
+            held = [f"{keys.get(r.holder, r.holder)}:{r.units}" for r in self.state.records.values() if r.dev == rec.dev]
+            raise AllocateError(f"GPU {rec.dev} of {self.node} is physically full ({self._physical_used(rec.dev)} of "
+                                f"{self.units.get(rec.dev)} {self.unit} handed out: {', '.join(held)}) and no other "
+                                f"GPU has room for {rec.key}")
+        log.warning("moving %s from GPU %d (physically full) to GPU %d before it starts", rec.key, rec.dev, best)
+        try:
+            return await self.move_unstarted(rec, best)
+        except ApiError as e:
+            raise AllocateError(f"moving {rec.key} off a physically full GPU failed: {e}") from e
+
+    def room_for(self, rec: PodRec, units: int, exclude: int = -1) -> int:
+        """Best-fit healthy GPU other than ``rec``'s (and ``exclude``) with room for ``rec`` by both counts: the
+        annotations (the extender's ledger) and the Allocate records (what really runs).  -1 if none."""
+        best, best_free = -1, None
+        for d, cap_d in self.units.items():
+            if d in (rec.dev, exclude) or not self.devices[d].healthy:
+                continue
+            free_ann = cap_d - self._annotated_used(d, skip=rec.uid)
+            if free_ann >= rec.request and cap_d - self._physical_used(d) >= units and (best < 0 or free_ann < best_free):
+                best, best_free = d, free_ann
+        return best
+
+    async def move_unstarted(self, rec: PodRec, dev: int) -> PodRec:
+        """Re-place a bound pod none of whose containers started onto GPU ``dev`` of this node: ``*_IDX`` = dev
+        with ``hold-idx`` = the old GPU (the ledger charges both), then the hold is cleared.  Raises ApiError."""
+        from ..models.profile import POD_HOLD_IDX_ANNOTATION  # noqa: PLC0415
+
+        body = {"metadata": {"resourceVersion": rec.rv, "annotations": {
+            self.profile.annotation_idx: str(dev), POD_HOLD_IDX_ANNOTATION: str(rec.dev)}}}
+        pod = await self.client.patch("pods", rec.name, body, rec.namespace)
+        self.state.observe(pod)
+        rec = self.state.pods.get(rec.uid, rec)
+        pod = await self.client.patch("pods", rec.name, {"metadata": {"resourceVersion": rec.rv, "annotations": {
+            POD_HOLD_IDX_ANNOTATION: None}}}, rec.namespace)
+        self.state.observe(pod)
+        self.stats["moved_before_start"] = self.stats.get("moved_before_start", 0) + 1
+        return self.state.pods.get(rec.uid, rec)
 
     async def _wait_for_annotations(self, units: int, timeout: float = 10.0):
         """A pod of this size is bound to the node but carries no allocation record yet: the extender is writing
@@ -488,7 +588,7 @@ class GpuSharePlugin:
                              "health": self.health_info.get(d.index)} for d in self.devices.values()],
                 "informer": {"synced": self.pods.synced.is_set(), "relists": self.pods.relists,
                              "rewatches": self.pods.rewatches, "events": self.pods.events},
-                "stats": dict(self.stats), **self.state.snapshot(),
+                "stats": dict(self.stats), "timing": dict(self.timing), **self.state.snapshot(),
                 "reconcile": dict(self.reconciler.stats) if self.reconciler is not None else None,
                 "isolation": dict(self.isolation.stats) if self.isolation is not None else None}
 

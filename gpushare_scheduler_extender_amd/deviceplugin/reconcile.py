@@ -22,6 +22,14 @@ device is ever under-counted by the extender in between:
 Every PATCH carries the pod's resourceVersion; a conflict ends the pass and the next one re-plans from fresh
 state.  A plugin restarted between steps finds the hold on P and finishes steps 2-3 from ``hold-partner``.
 Cycles (P holds Q's, Q holds R's, R holds P's) resolve as a chain of such exchanges.
+
+Two repairs keep the records honest when a pod goes away before a pass has seen its container:
+
+* a record whose IDs kubelet no longer reports (``stale_after`` past its Allocate) is dropped -- its container
+  is gone, so its GPU share is physically free, whichever pod the record's chain of exchanges names now;
+* a pod marked ``ASSIGNED=true`` that no record describes and no container of which kubelet reports
+  (``stale_after`` in that state) got that mark through an exchange with an allocation nobody holds any more:
+  it is reset to ``ASSIGNED=false`` so the next Allocate of its size can serve it.
 """
 from __future__ import annotations
 
@@ -44,13 +52,18 @@ def fields(p: PodRec) -> dict:
 
 
 class Reconciler:
-    def __init__(self, plugin, client: PodResourcesClient, interval: float = 2.0, after_allocate: float = 0.02):
+    def __init__(self, plugin, client: PodResourcesClient, interval: float = 2.0, after_allocate: float = 0.02,
+                 stale_after: float = 0.5):
         self.plugin = plugin
         self.pr = client
         self.interval = interval
         self.after_allocate = after_allocate
+        self.stale_after = stale_after
         self.stats = {"passes": 0, "swaps": 0, "records_owned": 0, "unknown_ids": 0, "unreconcilable": 0,
-                      "holds_finished": 0, "conflicts": 0, "errors": 0, "list_ms_max": 0.0}
+                      "holds_finished": 0, "conflicts": 0, "errors": 0, "list_ms_max": 0.0, "records_stale": 0,
+                      "assigned_reset": 0, "deferred": 0,
+                      "made_room": 0, "stand_in_partners": 0}
+        self._orphan_since: dict[str, float] = {}
         self._kick = asyncio.Event()
         self._task: asyncio.Task | None = None
         self._lock = asyncio.Lock()
@@ -64,13 +77,17 @@ class Reconciler:
         self._kick.set()
 
     # ------------------------------------------------------------ one pass
-    async def run_once(self) -> dict:
+    async def run_once(self, urgent: bool = False) -> dict:
+        """``urgent``: an Allocate found no candidate -- reset orphaned ``ASSIGNED`` marks without waiting."""
         async with self._lock:
             self.stats["passes"] += 1
             t0 = time.perf_counter()
             truth = await self.pr.device_ids(self.plugin.profile.resource)
+            self.state.core.set_owners_reported(True)  # from now on kubelet's report decides who holds a record
             self.stats["list_ms_max"] = max(self.stats["list_ms_max"], 1e3 * (time.perf_counter() - t0))
             moves: list[tuple[str, str]] = []  # (P uid, record aid)
+            seen = {tuple(ids) for per_container in truth.values() for ids in per_container}
+            self._drop_stale(seen, 0.1 if urgent else self.stale_after)
             for (ns, name), per_container in truth.items():
                 pod = self.state.pod_by_key(f"{ns}/{name}")
                 if pod is None:
@@ -86,17 +103,52 @@ class Reconciler:
                     if r.uid != pod.uid:
                         moves.append((pod.uid, r.aid))
             done = 0
+            started = {f"{ns}/{name}" for ns, name in truth}
+            await self._finish_holds()
             for p_uid, aid in moves:
                 r = self.state.records.get(aid)
                 p = self.state.pods.get(p_uid)
                 if r is None or p is None or r.uid == p_uid:
                     continue  # resolved by an earlier exchange of this pass
-                if await self._exchange(p, r):
+                if {p_uid, r.uid} & self.busy():
+                    self.stats["deferred"] += 1
+                    continue  # an interrupted exchange involves one of them: finish it first (next pass)
+                if await self._exchange(p, r, started):
                     done += 1
             await self._finish_holds()
+            await self._reset_orphans(started, 0.0 if urgent else self.stale_after)
             if done:
                 self.plugin.persist_records()
             return {"moves": done, "pods": len(truth)}
+
+    def _drop_stale(self, seen: set, grace: float) -> None:
+        now = time.time()
+        stale = [r for r in self.state.records.values() if tuple(sorted(r.ids)) not in seen and now - r.t > grace]
+        for r in stale:
+            log.info("allocation %s (GPU %d) is held by no container kubelet reports: dropped", r.aid, r.dev)
+            self.state.drop_record(r)
+            self.stats["records_stale"] += 1
+        if stale:
+            self.plugin.persist_records()
+
+    async def _reset_orphans(self, started: set, grace: float) -> None:
+        described = {r.uid for r in self.state.records.values()} | {r.holder for r in self.state.records.values()}
+        busy = self.busy()
+        now = time.monotonic()
+        orphans = set()
+        for p in list(self.state.pods.values()):
+            if (p.assigned != "true" or p.complete or p.key in started or p.uid in described
+                    or p.uid in self.state.inflight or p.uid in busy):
+                continue
+            orphans.add(p.uid)
+            since = self._orphan_since.setdefault(p.uid, now)
+            if now - since < grace:
+                continue
+            log.warning("pod %s is ASSIGNED but holds no allocation: making it an Allocate candidate again", p.key)
+            if await self._patch(p, {self.plugin.profile.annotation_assigned: "false"}):
+                self.stats["assigned_reset"] += 1
+                orphans.discard(p.uid)
+        self._orphan_since = {u: t for u, t in self._orphan_since.items() if u in orphans}
 
     async def _patch(self, p: PodRec, ann: dict) -> bool:
         body = {"metadata": {"resourceVersion": p.rv, "annotations": ann}}
@@ -115,7 +167,7 @@ class Reconciler:
         return {prof.annotation_idx: str(f["idx"]), prof.annotation_assigned: f["assigned"] or "false",
                 POD_CU_MASK_ANNOTATION: f["cu_mask"] or None}
 
-    async def _exchange(self, p: PodRec, r: AllocRecord) -> bool:
+    async def _exchange(self, p: PodRec, r: AllocRecord, started: set) -> bool:
         q = self.state.pods.get(r.uid)
         if q is None:
             # the pod the record was built for is gone: P simply takes the record's fields
@@ -127,7 +179,24 @@ class Reconciler:
                 log.warning("pod %s holds the allocation of %s, of another size (%d vs %d); not reconciled",
                             p.key, q.key, p.request, q.request)
                 return False
+        if q is None:
+            # its deletion freed r.dev in the extender's ledger although P's container runs there.  An unstarted
+            # pod of P's size the extender has since placed on r.dev is the natural partner: exchanging with it
+            # keeps the annotations' per-GPU sums exactly as they are (it starts on P's old GPU instead)
+            q = self._stand_in_partner(r.dev, p, started)
+            if q is None:
+                await self._make_room(r.dev, p, started)
+            else:
+                self.stats["stand_in_partners"] += 1
         p_old = fields(p)
+        # Q takes P's old allocation fields; it is ASSIGNED only if an Allocate was served for them, i.e. a record
+        # describes P now (it will describe Q after the exchange) -- in a chain (P holds Q's, Q holds R's, ...)
+        # P's own allocation may have gone to nobody, and then Q must stay an Allocate candidate
+        # (Q itself may already run a container -- with yet another pod's allocation -- and then stays ASSIGNED)
+        recs = self.state.records.values()
+        served = q is not None and (q.key in started or any(o.owner == q.uid for o in recs))
+        q_new = dict(p_old, assigned="true" if served or any(o.uid == p.uid and o.aid != r.aid for o in recs)
+                     else "false")
         new_p = {"idx": r.dev, "assigned": "true", "cu_mask": r.cu_mask}
         ann = self._ann(new_p)
         n = int((p.obj.get("metadata", {}).get("annotations") or {}).get(POD_RECONCILED_ANNOTATION, "0") or 0)
@@ -135,25 +204,81 @@ class Reconciler:
         holding = q is not None and p_old["idx"] >= 0 and p_old["idx"] != r.dev
         if holding:
             ann[POD_HOLD_IDX_ANNOTATION] = str(p_old["idx"])
-            ann[POD_HOLD_PARTNER_ANNOTATION] = json.dumps({"uid": q.uid, "key": q.key, **p_old}, separators=(",", ":"))
+            ann[POD_HOLD_PARTNER_ANNOTATION] = json.dumps({"uid": q.uid, "key": q.key, **q_new}, separators=(",", ":"))
         log.warning("kubelet gave pod %s the allocation built for %s (GPU %d): exchanging their records",
                     p.key, q.key if q else r.uid, r.dev)
         if not await self._patch(p, ann):  # step 1
             return False
-        self.state.move_records(p.uid, r.uid, r)
+        self.state.move_records(p.uid, q.uid if q is not None else r.uid, r)
         self.stats["swaps"] += 1
         if q is not None:
-            if await self._patch(self.state.pods.get(q.uid, q), self._ann(p_old)):  # step 2
+            if await self._patch(self.state.pods.get(q.uid, q), self._ann(q_new)):  # step 2
                 if holding:
                     await self._clear_hold(self.state.pods.get(p.uid, p))  # step 3
             # on a conflict the hold stays; _finish_holds completes the move on a later pass
         return True
+
+    def _stand_in_partner(self, dev: int, p: PodRec, started: set) -> PodRec | None:
+        recs = self.state.records.values()
+        taken = {r.holder for r in recs} | {r.uid for r in recs} | self.busy()
+        cands = [q for q in self.state.pods.values()
+                 if q.dev == dev and q.request == p.request and q.uid != p.uid and not q.complete
+                 and q.key not in started and q.uid not in taken and q.uid not in self.state.inflight]
+        return min(cands, key=lambda q: q.order) if cands else None
+
+    async def _make_room(self, dev: int, p: PodRec, started: set) -> None:
+        """P is about to be annotated with GPU ``dev`` alone (the pod the allocation was built for is gone -- and
+        its deletion freed ``dev`` in the extender's ledger although P's container runs there).  Pods the extender
+        has since placed on ``dev`` and that have not started are moved to GPUs with room first, so the
+        annotations never promise ``dev`` beyond its capacity."""
+        plugin = self.plugin
+        need = plugin._annotated_used(dev, skip=p.uid) + p.request - plugin.units.get(dev, 0)
+        if need <= 0:
+            return
+        owned = {r.holder for r in self.state.records.values()} | {r.uid for r in self.state.records.values()}
+        busy = self.busy()
+        movable = sorted((q for q in self.state.pods.values()
+                          if q.dev == dev and q.uid != p.uid and not q.complete and q.key not in started
+                          and q.uid not in owned and q.uid not in busy and q.uid not in self.state.inflight),
+                         key=lambda q: -q.request)
+        for q in movable:
+            if need <= 0:
+                break
+            to = plugin.room_for(q, q.request)
+            if to < 0:
+                continue
+            log.warning("GPU %d is needed back for %s: moving %s (not started) to GPU %d", dev, p.key, q.key, to)
+            try:
+                await plugin.move_unstarted(q, to)
+            except ApiError:
+                self.stats["conflicts"] += 1
+                continue
+            need -= q.request
+            self.stats["made_room"] += 1
+        if need > 0:
+            log.warning("GPU %d stays over-committed by %d after the deletion of the pod %s's allocation was built "
+                        "for; its unstarted pods move when they are admitted", dev, need, p.key)
 
     async def _clear_hold(self, p: PodRec) -> bool:
         ok = await self._patch(p, {POD_HOLD_IDX_ANNOTATION: None, POD_HOLD_PARTNER_ANNOTATION: None})
         if ok:
             self.stats["holds_finished"] += 1
         return ok
+
+    def busy(self) -> set:
+        """Pods an unfinished exchange involves: P (carrying the hold) and the partner Q named in it.  Neither
+        takes part in another exchange (or a physical-guard move) until the hold is cleared, so the partner's
+        fields are still what the hold's payload compares them with."""
+        out = set()
+        for p in self.state.pods.values():
+            if p.hold_idx >= 0 or p.hold_partner:
+                out.add(p.uid)
+                try:
+                    out.add(json.loads(p.hold_partner).get("uid", "") if p.hold_partner else "")
+                except ValueError:
+                    pass
+        out.discard("")
+        return out
 
     async def _finish_holds(self):
         """Complete moves interrupted after step 1 (a conflict, or a plugin restart in between)."""
@@ -178,6 +303,7 @@ class Reconciler:
                 pass
             self._kick.clear()
             if not self.pr.available():
+                self.state.core.set_owners_reported(False)  # nobody will report owners: drop records by pod
                 continue
             try:
                 await self.run_once()

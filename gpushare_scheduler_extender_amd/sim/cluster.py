@@ -112,22 +112,20 @@ def tool_path(name: str) -> Path:
 FAKEAPI = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-fakeapi"
 
 
-def start_apiserver(native: bool = True, history: int = 200000, threads: int | None = None,
-                    cpus: list[int] | None = None) -> ChildProc:
-    """Fake kube-apiserver: the compiled ``gsx-fakeapi`` (native/fakeapi) or ``python -m ...k8s.fakeapi``.
+def start_apiserver(history: int = 200000, threads: int | None = None, cpus: list[int] | None = None) -> ChildProc:
+    """Fake kube-apiserver: the compiled ``gsx-fakeapi`` (native/fakeapi).  (``tests/fixtures/fakeapi.py`` is its
+    in-process test-only twin.)
 
     ``threads``: event loops of the native server (default ``GSX_FAKEAPI_THREADS`` or 1).
     ``GSX_FAKEAPI_WATCH_FLUSH``: ``iteration`` (default) or ``request`` -- when watch events are pushed.
     """
-    if native:
-        exe = tool_path("gsx-fakeapi")
-        if not exe.exists():
-            raise FileNotFoundError(f"{exe} missing; run `python native/build.py fakeapi`")
-        threads = threads or int(os.environ.get("GSX_FAKEAPI_THREADS", "1"))
-        flush = os.environ.get("GSX_FAKEAPI_WATCH_FLUSH", "iteration")
-        return ChildProc([str(exe), "--port", "0", "--history", str(history), "--threads", str(threads),
-                          "--watch-flush", flush], "apiserver", cpus=cpus)
-    return ChildProc(["-m", "gpushare_scheduler_extender_amd.k8s.fakeapi", "--port", "0"], "apiserver", cpus=cpus)
+    exe = tool_path("gsx-fakeapi")
+    if not exe.exists():
+        raise FileNotFoundError(f"{exe} missing; run `python native/build.py fakeapi`")
+    threads = threads or int(os.environ.get("GSX_FAKEAPI_THREADS", "1"))
+    flush = os.environ.get("GSX_FAKEAPI_WATCH_FLUSH", "iteration")
+    return ChildProc([str(exe), "--port", "0", "--history", str(history), "--threads", str(threads),
+                      "--watch-flush", flush], "apiserver", cpus=cpus)
 
 
 def start_extender(apiserver: str, profile: str = "shared-gpu", bind_mode: str = "binding", threadness: int = 1,
@@ -167,19 +165,13 @@ SCHEDSIM = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-schedsim"
 
 
 def start_scheduler(apiserver: str, extender: str, profile: str = "shared-gpu", max_inflight_binds: int = 256,
-                    native: bool = True, cpus: list[int] | None = None, nodes_to_score: str = "") -> ChildProc:
-    """kube-scheduler stand-in with a timings endpoint.
-
-    ``native=True``: the compiled ``gsx-schedsim`` (native/schedsim, built by
-    ``native/build.py``); otherwise ``python -m gpushare_scheduler_extender_amd.sim``.
-    Both serve the same ``/v1/timings``, ``/v1/forget`` and ``/v1/stats``.
-    """
-    if native:
-        exe = tool_path("gsx-schedsim")
-        if not exe.exists():
-            raise FileNotFoundError(f"{exe} missing; run `python native/build.py schedsim`")
-        extra = ["--nodes-to-score", nodes_to_score] if nodes_to_score else []
-        return ChildProc([str(exe), "--apiserver", apiserver, "--extender", extender, "--profile", profile,
-                          "--bind-threads", str(min(16, max_inflight_binds)), *extra], "scheduler", cpus=cpus)
-    return ChildProc(["-m", "gpushare_scheduler_extender_amd.sim", "--apiserver", apiserver, "--extender", extender,
-                      "--profile", profile, "--max-inflight-binds", str(max_inflight_binds)], "scheduler", cpus=cpus)
+                    cpus: list[int] | None = None, nodes_to_score: str = "") -> ChildProc:
+    """kube-scheduler stand-in: the compiled ``gsx-schedsim`` (native/schedsim, built by ``native/build.py``) with a
+    timings endpoint (``/v1/timings``, ``/v1/forget``, ``/v1/stats``).  (``tests/fixtures/schedsim.py`` is its
+    in-process test-only twin.)"""
+    exe = tool_path("gsx-schedsim")
+    if not exe.exists():
+        raise FileNotFoundError(f"{exe} missing; run `python native/build.py schedsim`")
+    extra = ["--nodes-to-score", nodes_to_score] if nodes_to_score else []
+    return ChildProc([str(exe), "--apiserver", apiserver, "--extender", extender, "--profile", profile,
+                      "--bind-threads", str(min(16, max_inflight_binds)), *extra], "scheduler", cpus=cpus)

@@ -99,7 +99,7 @@ class Cluster:
     """apiserver + extender + scheduler + node agent (child processes) and one node with ``len(totals)`` devices."""
 
     def __init__(self, profile: NamingProfile, totals: list[int], gpu: bool | int, cu_count: int = 256,
-                 native: bool = True, partition: str = "SPX", xcc_count: int = 8, agent: str | None = None,
+                 partition: str = "SPX", xcc_count: int = 8, agent: str | None = None,
                  pool_gib: int = 0, bind_mode: str = "binding", agent_args: list[str] | None = None):
         self.profile = profile
         self.totals = totals
@@ -108,8 +108,8 @@ class Cluster:
         self.children.append(self.api)
         self.ext = start_extender(self.api.url, profile=profile.name, bind_mode=bind_mode)
         self.children.append(self.ext)
-        # native: compiled kube-scheduler / node-agent stand-ins; otherwise the asyncio ones
-        self.children.append(start_scheduler(self.api.url, self.ext.url, profile=profile.name, native=native))
+        # the compiled kube-scheduler stand-in, its own process like the real one
+        self.children.append(start_scheduler(self.api.url, self.ext.url, profile=profile.name))
         self.agent_kind = agent or AGENT["kind"]
         self.agent_args = list(agent_args if agent_args is not None else AGENT["args"])
         self.api_latency_ms = AGENT["api_latency_ms"]

@@ -119,7 +119,7 @@ def build_nodeagent(force: bool = False, verbose: bool = False) -> Path:
 
 
 def build_fakeapi(force: bool = False, verbose: bool = False) -> Path:
-    """``gsx-fakeapi``: the compiled fake kube-apiserver (same REST subset as k8s/fakeapi.py)."""
+    """``gsx-fakeapi``: the compiled fake kube-apiserver (its asyncio twin is the test fixture tests/fixtures/fakeapi.py)."""
     return _build_native_tool("gsx-fakeapi", "fakeapi", force, verbose)
 
 

@@ -284,7 +284,8 @@ void AllocState::release(const std::string& uid) {
   inflight_.erase(uid);
   std::vector<std::string> gone;
   for (const auto& kv : records_) {
-    if (kv.second.holder() == uid) gone.push_back(kv.first);
+    const AllocRecord& r = kv.second;
+    if (r.owner == uid || (r.owner.empty() && r.uid == uid && !owners_reported_)) gone.push_back(kv.first);
   }
   for (const auto& aid : gone) drop_record(aid);
 }

@@ -131,6 +131,11 @@ class AllocState {
   const AllocRecord* record_for_ids(std::vector<std::string> ids) const;
   AllocRecord* record_by_aid(const std::string& aid);
   void set_owner(const std::string& aid, const std::string& owner);
+  // With kubelet's PodResources reconciled (`on`), a record whose holder kubelet has not reported yet is not
+  // dropped with the pod it was built for: after a swap another pod's container may be running with it.  The
+  // reconciler drops it once kubelet no longer lists its IDs.
+  void set_owners_reported(bool on) { owners_reported_ = on; }
+  bool owners_reported() const { return owners_reported_; }
   // After the annotations of P and Q were exchanged because P holds `aid` (built for Q): that record now
   // describes P, whatever described P describes Q, and the CU partitions follow.
   void move_records(const std::string& p_uid, const std::string& q_uid, const std::string& aid);
@@ -157,6 +162,7 @@ class AllocState {
   std::map<std::string, AllocRecord> records_;            // aid -> record
   std::map<std::vector<std::string>, std::string> by_ids_;
   std::vector<AllocRecord> dropped_;
+  bool owners_reported_ = false;
   AllocStats stats_;
 };
 

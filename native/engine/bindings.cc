@@ -890,6 +890,8 @@ PYBIND11_MODULE(_engine, m) {
              return out;
            })
       .def("set_inflight", &AllocState::set_inflight)
+      .def("set_owners_reported", &AllocState::set_owners_reported)
+      .def("owners_reported", &AllocState::owners_reported)
       .def("inflight", &AllocState::inflight)
       .def("first_container_committed", &AllocState::first_container_committed)
       .def("later_container_allocated", &AllocState::later_container_allocated)

@@ -1,7 +1,9 @@
-"""In-process fake kube-apiserver (pods, nodes, bindings, events) over real HTTP.
+"""Test fixture: in-process fake kube-apiserver (pods, nodes, bindings, events) over real HTTP.
 
-The reference was only ever validated by hand on a live cluster;
-this stands in for that cluster in tests and in ``bench.py``.  It speaks the
+Not shipped: the stack, ``sim/`` and ``bench.py`` run the compiled ``gsx-fakeapi`` (``native/fakeapi``), which
+speaks the same REST subset.  This asyncio twin stays for tests that reach into the object store directly
+(``FakeApiServer``) or run the apiserver in the test's own event loop.  The reference was only ever validated
+by hand on a live cluster.  It speaks the
 subset of the core/v1 REST API the scheduler extender, the controller, the
 device plugin and the CLI use, with the semantics they rely on:
 
@@ -23,7 +25,7 @@ device plugin and the CLI use, with the semantics they rely on:
 * fault injection: conflict / error rates, latency and watch drops
   (``POST /fake/faults``), which the reference never had.
 
-Run standalone with ``python -m gpushare_scheduler_extender_amd.k8s.fakeapi``.
+Run standalone with ``python -m tests.fixtures.fakeapi`` (or use ``gsx-fakeapi``).
 """
 from __future__ import annotations
 
@@ -37,7 +39,7 @@ import time
 import uuid
 from datetime import datetime, timezone
 
-from .fasthttp import HTTPError, Request, Response, Server, Stream
+from gpushare_scheduler_extender_amd.k8s.fasthttp import HTTPError, Request, Response, Server, Stream
 
 log = logging.getLogger("gsx.fakeapi")
 

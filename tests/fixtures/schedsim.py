@@ -1,4 +1,8 @@
-"""kube-scheduler simulator speaking the extender protocol.
+"""Test fixture: in-process kube-scheduler simulator speaking the extender protocol.
+
+Not shipped: ``sim/`` and ``bench.py`` run the compiled ``gsx-schedsim`` (``native/schedsim``), which replays the
+same cycle with C++ reflectors and bind threads; this asyncio twin stays for tests that drive scheduling from
+their own event loop.
 
 There is no kube-scheduler, kind or kubectl in this environment (SURVEY.md
 §4), so this replays what kube-scheduler does for a pod that requests a
@@ -26,12 +30,12 @@ import logging
 import time
 from dataclasses import dataclass, field
 
-from ..k8s.client import KubeClient
-from ..k8s.fasthttp import Client
-from ..k8s.informer import Handler, Informer, obj_key
-from ..models import pod as podutil
-from ..models import wire
-from ..models.profile import NamingProfile
+from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+from gpushare_scheduler_extender_amd.k8s.fasthttp import Client
+from gpushare_scheduler_extender_amd.k8s.informer import Handler, Informer, obj_key
+from gpushare_scheduler_extender_amd.models import pod as podutil
+from gpushare_scheduler_extender_amd.models import wire
+from gpushare_scheduler_extender_amd.models.profile import NamingProfile
 
 log = logging.getLogger("gsx.sim")
 

@@ -8,7 +8,7 @@ import json
 from gpushare_scheduler_extender_amd.deviceplugin.devices import Device, apply_memory_pools
 from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin, PluginClient
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient
-from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+from tests.fixtures.fakeapi import FakeApiServerRunner
 from gpushare_scheduler_extender_amd.k8s.objects import make_node
 from gpushare_scheduler_extender_amd.models.profile import NODE_DEVICE_MEMORY_ANNOTATION, SHARED_GPU
 from gpushare_scheduler_extender_amd.ops import mxdev

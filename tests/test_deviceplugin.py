@@ -13,7 +13,7 @@ from gpushare_scheduler_extender_amd.deviceplugin.plugin import FakeKubelet, Gpu
 from gpushare_scheduler_extender_amd.deviceplugin.runtime import AdmissionError, LedgerRuntime
 from gpushare_scheduler_extender_amd.deviceplugin.state import AllocationState
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient
-from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+from tests.fixtures.fakeapi import FakeApiServerRunner
 from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
 from gpushare_scheduler_extender_amd.models.profile import ALIYUN, SHARED_GPU
 
@@ -490,8 +490,8 @@ def test_process_runtime_starts_container_with_allocate_env():
     from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
     from gpushare_scheduler_extender_amd.deviceplugin.runtime import ProcessRuntime
     from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
-    from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
-    from gpushare_scheduler_extender_amd.sim.scheduler import SchedulerSim
+    from tests.fixtures.fakeapi import FakeApiServerRunner
+    from tests.fixtures.schedsim import SchedulerSim
 
     code = "import json,os;print(json.dumps({k:v for k,v in os.environ.items() if k.startswith(('SHARED_','HIP_','ROCR_'))}))"
 

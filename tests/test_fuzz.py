@@ -71,7 +71,7 @@ def test_native_front_end_survives_generated_requests():
     answers a filter request on a fresh connection."""
     from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
     from gpushare_scheduler_extender_amd.k8s.client import KubeClient
-    from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+    from tests.fixtures.fakeapi import FakeApiServerRunner
 
     methods = st.sampled_from([b"GET", b"POST", b"PUT", b"DELETE", b"BREW", b""])
     paths = st.sampled_from([b"/gpushare-scheduler/filter", b"/gpushare-scheduler/bind", b"/version",

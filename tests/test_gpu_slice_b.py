@@ -24,11 +24,11 @@ from gpushare_scheduler_extender_amd.deviceplugin.devices import discover
 from gpushare_scheduler_extender_amd.deviceplugin.runtime import ProcessRuntime
 from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient
-from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+from tests.fixtures.fakeapi import FakeApiServerRunner
 from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
 from gpushare_scheduler_extender_amd.models import pod as podutil
 from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
-from gpushare_scheduler_extender_amd.sim.scheduler import SchedulerSim
+from tests.fixtures.schedsim import SchedulerSim
 
 pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]

@@ -55,7 +55,7 @@ def test_plugin_allocate_mounts_isolation_and_records(tmp_path):
     from gpushare_scheduler_extender_amd.deviceplugin.devices import Device
     from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin, PluginClient
     from gpushare_scheduler_extender_amd.k8s.client import KubeClient
-    from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+    from tests.fixtures.fakeapi import FakeApiServerRunner
     from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
     from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
 
@@ -82,6 +82,10 @@ def test_plugin_allocate_mounts_isolation_and_records(tmp_path):
             assert r.envs["HSA_TOOLS_LIB"] == "/run/gsx/libgsx_isolate.so"
             assert len(plugin.state.records) == 1
             import json
+            for _ in range(100):  # the checkpoint write is debounced (one write per burst of Allocates)
+                if Path(plugin.checkpoint).exists():
+                    break
+                await asyncio.sleep(0.02)
             saved = json.loads(Path(plugin.checkpoint).read_text())["records"]
             assert saved[0]["uid"] == pod["metadata"]["uid"] and len(saved[0]["ids"]) == 4
             # the pod goes away: its record and its isolation files go with it

@@ -10,7 +10,7 @@ import pytest
 import yaml
 
 from gpushare_scheduler_extender_amd.k8s.client import ApiError, KubeClient, KubeConfig, RateLimiter
-from gpushare_scheduler_extender_amd.k8s.fakeapi import CONFLICT_MSG, FakeApiServer, FakeApiServerRunner, merge_patch
+from tests.fixtures.fakeapi import CONFLICT_MSG, FakeApiServer, FakeApiServerRunner, merge_patch
 from gpushare_scheduler_extender_amd.k8s.fasthttp import Client, Response, Server
 from gpushare_scheduler_extender_amd.k8s.informer import Handler, Informer
 from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
@@ -28,7 +28,7 @@ class _NativeApi:
     def __init__(self, history, threads=1):
         from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver
 
-        self.proc = start_apiserver(native=True, history=history, threads=threads)
+        self.proc = start_apiserver(history=history, threads=threads)
         self.url = self.proc.url
 
     async def stop(self):
@@ -445,7 +445,7 @@ def test_paginated_list_limit_continue(impl):
             runner = await FakeApiServerRunner().start()
             url, child = runner.url, None
         else:
-            child = start_apiserver(native=True)
+            child = start_apiserver()
             url, runner = child.url, None
         c = KubeClient(url)
         try:

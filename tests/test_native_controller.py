@@ -11,7 +11,7 @@ import asyncio
 from gpushare_scheduler_extender_amd.core.controller import NativeController
 from gpushare_scheduler_extender_amd.core.engine import new_engine
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient
-from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServer, FakeApiServerRunner
+from tests.fixtures.fakeapi import FakeApiServer, FakeApiServerRunner
 from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
 from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
 

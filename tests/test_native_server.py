@@ -8,7 +8,7 @@ import pytest
 
 from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient
-from gpushare_scheduler_extender_amd.k8s.fakeapi import FakeApiServerRunner
+from tests.fixtures.fakeapi import FakeApiServerRunner
 from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
 from gpushare_scheduler_extender_amd.models import wire
 

@@ -42,8 +42,8 @@ async def _wait(pred, timeout=30.0, what=""):
         await asyncio.sleep(0.05)
 
 
-async def _swap_scenario(reconcile: bool):
-    args = ["--faithful"] + ([] if reconcile else ["--no-reconcile"])
+async def _swap_scenario(reconcile: bool, plugin: str = "grpc"):
+    args = ["--faithful", "--plugin", plugin] + ([] if reconcile else ["--no-reconcile"])
     cl = Cluster(ALIYUN, [96] * 4, gpu=False, agent="plugin", agent_args=args)
     try:
         await cl.start()
@@ -105,8 +105,11 @@ async def _swap_scenario(reconcile: bool):
         await cl.close()
 
 
-def test_kubelet_batch_swap_is_reconciled_and_deletes_free_the_right_gpu():
-    phases, per_gpu, phys, live = asyncio.run(_swap_scenario(reconcile=True))
+@pytest.mark.parametrize("plugin", ["grpc", "process"])
+def test_kubelet_batch_swap_is_reconciled_and_deletes_free_the_right_gpu(plugin):
+    """``process``: the plugin runs as deployed (``python -m ...deviceplugin``, registered with the stand-in's
+    Registration service), so the reconciliation works across the process boundary kubelet really has."""
+    phases, per_gpu, phys, live = asyncio.run(_swap_scenario(reconcile=True, plugin=plugin))
     assert phases == {"c0": "Running", "c1": "Running"}, phases
     assert all(u <= 96 for u in per_gpu), per_gpu  # never two 64 GiB containers on one 96 GiB GPU
     assert sorted(phys.values()) == [0, 1, 2, 3]
@@ -182,3 +185,31 @@ def test_reconcile_state_exchange_cycles(seed):
         r = st.records[holds[n]]
         assert r.uid == f"u{n}" and ann[n] == r.dev
         assert st.cus[r.dev].holds(f"u{n}")
+
+
+def test_unowned_record_outlives_the_pod_it_was_built_for_while_kubelet_reports_owners():
+    """A record built for Q may be running in P's container (a swap no pass has seen yet).  Once PodResources is
+    reconciled, deleting Q must not drop it -- only kubelet no longer listing its IDs does."""
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import Device
+    from gpushare_scheduler_extender_amd.deviceplugin.state import AllocationState
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+
+    def make():
+        st = AllocationState("n", {0: Device(index=0, total_bytes=96 << 30)}, SHARED_GPU)
+        q = make_pod("q", 32, node="n", uid="uQ", annotations={SHARED_GPU.annotation_idx: "0",
+                                                                SHARED_GPU.annotation_assigned: "false"})
+        q["metadata"]["resourceVersion"] = "1"
+        st.observe(q)
+        st.record(st.pods["uQ"], ["g0-_-0"], 32, "", "aQ")
+        return st
+
+    st = make()  # no PodResources: the pod's records go with it
+    st.release("uQ")
+    assert "aQ" not in st.records
+    st = make()
+    st.core.set_owners_reported(True)
+    st.release("uQ")
+    assert "aQ" in st.records  # kept until kubelet's report decides
+    st.set_owner("aQ", "uP")
+    st.release("uP")  # its owner's deletion does drop it
+    assert "aQ" not in st.records

@@ -42,7 +42,7 @@ def test_controller_stack_under_sanitizer(target):
     from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver
 
     build_native([target, "fakeapi"])
-    api = start_apiserver(native=True)
+    api = start_apiserver()
     try:
         r = subprocess.run([str(REPO / "build" / f"controller_test_{target}"), "--apiserver", api.url,
                             "--seconds", "3"], capture_output=True, text=True, timeout=240, env=ENV)
@@ -62,7 +62,7 @@ def test_standins_under_tsan(tmp_path):
                         "--only", "2,3,5"], capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider",
-                        "tests/test_chaos.py::test_chaos_whole_stack_converges_without_overcommit[23-native-native-binding]"],
+                        "tests/test_chaos.py::test_chaos_whole_stack_converges_without_overcommit[23-native-binding]"],
                        capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout[-3000:]
     reports = sorted(glob.glob(str(logs) + "*"))
