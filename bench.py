@@ -289,11 +289,13 @@ def latency_sweep(a, children, api_url, api_batch, runner: WaveRunner, inspect_u
 def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
     """The same waves with kubelet + device plugin = the shipped gRPC GpuSharePlugin, driven over its unix socket
     by the kubelet stand-in (serial admission, GetPreferredAllocation + Allocate per pod) instead of the
-    compiled node agent.  The plugin's own pod informer and allocation state decide every Allocate."""
+    compiled node agent.  The plugin's own pod informer and allocation state decide every Allocate.  With
+    ``--plugin-proc process`` (default) the plugin is its own process (``python -m ...deviceplugin``) that
+    registers with the stand-in's Registration service, as under a real kubelet."""
     from gpushare_scheduler_extender_amd.sim.cluster import start_node_agent
 
     na = restart_child(children, "node-agent", lambda old: start_node_agent(
-        api_url, NODE, profile=a.profile, native=False, plugin="grpc", cpus=old.cpus,
+        api_url, NODE, profile=a.profile, native=False, plugin=a.plugin_proc, cpus=old.cpus,
         extra=["--faithful"] if a.kubelet == "faithful" else []))
     client = E.BatchClient({"server": na.url})
     wait_until(lambda: client.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 120, "plugin agent never ready")
@@ -304,7 +306,7 @@ def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
             "plugin_breakdown_ms": stats.get("plugin_breakdown_ms"), "allocate_calls": stats.get("allocate_calls"),
             "allocate_errors": stats.get("allocate_errors"), "mismatch": stats.get("mismatch"),
             "swapped_equivalent": stats.get("swapped_equivalent"),
-            "plugin_stats": stats.get("plugin_stats")}
+            "plugin_stats": stats.get("plugin_stats"), "plugin": stats.get("plugin")}
 
 
 def parse():
@@ -352,6 +354,9 @@ def parse():
     ap.add_argument("--kubelet", default="standin", choices=["standin", "faithful"],
                     help="with --node-agent plugin: the kubelet stand-in re-routes a mismatched Allocate (standin) or "
                          "behaves like kubelet and lets the plugin reconcile (faithful)")
+    ap.add_argument("--plugin-proc", default="process", choices=["process", "grpc"],
+                    help="device-plugin path row: the plugin as its own process registered with the kubelet "
+                         "stand-in, as the DaemonSet runs it (process), or served from the stand-in's process (grpc)")
     ap.add_argument("--sweep", type=int, default=1, help="1: run the latency sweep after the timed region")
     ap.add_argument("--sweep-steps", type=int, default=8)
     return ap.parse_args()
