@@ -123,3 +123,43 @@ def test_pytorch_sees_and_respects_the_share(iso):
     out = _run([sys.executable, "-c", code], _env(env), timeout=300)
     assert out["total"] == share and out["props"] == share, out
     assert out["oom"] is True and out["sum"] == 1024
+
+
+@pytest.mark.parametrize("api", ["async", "finegrained", "pitch", "vmem"])
+def test_hbm_share_covers_every_device_allocation_api(iso, api):
+    """Stream-ordered pools, fine-grained device memory, pitched allocations and the virtual-memory API
+    (hipMemCreate: PyTorch's expandable segments) all take HBM, so all count against the pod's share."""
+    probe = NATIVE / "gsx-memprobe"
+    _, env = iso.prepare(f"api-{api}", None, 256, 8 * GIB, host_process=True)
+    out = _run([probe, "--api", api, "--alloc", f"{6 * GIB},{6 * GIB}"], _env(env))
+    assert [a["ok"] for a in out["allocs"]] == [True, False], out
+    ctl = _run([probe, "--api", api, "--alloc", f"{6 * GIB},{6 * GIB}"], _env({}))  # unconfined: both fit
+    assert [a["ok"] for a in ctl["allocs"]] == [True, True], ctl
+
+
+def test_host_memory_is_not_the_share(iso):
+    """Pinned host memory (hipHostMalloc) lives in system RAM: it must not count against the HBM share."""
+    probe = NATIVE / "gsx-memprobe"
+    _, env = iso.prepare("api-host", None, 256, 4 * GIB, host_process=True)
+    out = _run([probe, "--api", "host", "--alloc", f"{3 * GIB},{3 * GIB}"], _env(env))
+    assert [a["ok"] for a in out["allocs"]] == [True, True], out
+
+
+def test_pytorch_expandable_segments_respect_the_share(iso):
+    """PYTORCH_HIP_ALLOC_CONF=expandable_segments:True maps growing segments through the virtual-memory API."""
+    share = 16 * GIB
+    _, env = iso.prepare("torch-exp", None, 256, share, host_process=True)
+    env = dict(env, PYTORCH_HIP_ALLOC_CONF="expandable_segments:True", PYTORCH_CUDA_ALLOC_CONF="expandable_segments:True")
+    code = (
+        "import json,torch\n"
+        "xs=[]\n"
+        "oom=False\n"
+        "try:\n"
+        "    for _ in range(24):\n"
+        "        xs.append(torch.empty(1<<30,dtype=torch.uint8,device='cuda'))\n"
+        "except torch.OutOfMemoryError:\n"
+        "    oom=True\n"
+        "print(json.dumps({'gib':len(xs),'oom':oom,'reserved':torch.cuda.memory_reserved()}))\n")
+    out = _run([sys.executable, "-c", code], _env(env), timeout=300)
+    assert out["oom"] is True and out["gib"] <= 16, out
+    assert out["reserved"] <= share, out
