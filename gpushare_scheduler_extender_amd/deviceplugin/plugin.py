@@ -324,8 +324,15 @@ class GpuSharePlugin:
                         break
                     await asyncio.sleep(0.02 * (k + 1))
             if rec is None:
-                same = [f"{p.key}:{p.phase}:{p.assigned}:gpu{p.dev}" for p in self.state.pods.values()
-                        if p.request == units]
+                keys = {p.uid: p.key for p in self.state.pods.values()}
+                recs = self.state.records.values()
+                busy = self.reconciler.busy() if self.reconciler is not None else set()
+
+                def why(p):  # the records naming this pod, and who really holds them
+                    held = [f"{keys.get(r.holder, r.holder[:8])}@gpu{r.dev}" for r in recs if r.uid == p.uid]
+                    return f"{p.key}:{p.phase}:{p.assigned}:gpu{p.dev}" + (f"[{','.join(held)}]" if held else "") + (
+                        "*" if p.uid in busy else "")
+                same = [why(p) for p in self.state.pods.values() if p.request == units]
                 raise AllocateError(f"no pending pod on {self.node} requests {units} {self.profile.resource} "
                                     f"with {self.profile.annotation_assigned}=false (pods of that size: "
                                     f"{', '.join(same[:8]) or 'none'})")

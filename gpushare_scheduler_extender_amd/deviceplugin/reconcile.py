@@ -51,6 +51,11 @@ def fields(p: PodRec) -> dict:
     return {"idx": p.dev, "assigned": p.assigned, "cu_mask": p.cu_mask}
 
 
+def _drifted(p: PodRec, r: AllocRecord) -> bool:
+    """P's annotation names another GPU (or CU partition) than the allocation its container holds."""
+    return p.dev != r.dev or (p.cu_mask or "") != (r.cu_mask or "")
+
+
 class Reconciler:
     def __init__(self, plugin, client: PodResourcesClient, interval: float = 2.0, after_allocate: float = 0.02,
                  stale_after: float = 0.5):
@@ -62,7 +67,8 @@ class Reconciler:
         self.stats = {"passes": 0, "swaps": 0, "records_owned": 0, "unknown_ids": 0, "unreconcilable": 0,
                       "holds_finished": 0, "conflicts": 0, "errors": 0, "list_ms_max": 0.0, "records_stale": 0,
                       "assigned_reset": 0, "deferred": 0,
-                      "made_room": 0, "stand_in_partners": 0}
+                      "made_room": 0, "stand_in_partners": 0,
+                      "drift_repaired": 0}
         self._orphan_since: dict[str, float] = {}
         self._kick = asyncio.Event()
         self._task: asyncio.Task | None = None
@@ -86,6 +92,7 @@ class Reconciler:
             self.state.core.set_owners_reported(True)  # from now on kubelet's report decides who holds a record
             self.stats["list_ms_max"] = max(self.stats["list_ms_max"], 1e3 * (time.perf_counter() - t0))
             moves: list[tuple[str, str]] = []  # (P uid, record aid)
+            drifts: list[tuple[str, str]] = []  # P holds its own record, but its annotation names another GPU
             seen = {tuple(ids) for per_container in truth.values() for ids in per_container}
             self._drop_stale(seen, 0.1 if urgent else self.stale_after)
             for (ns, name), per_container in truth.items():
@@ -102,6 +109,8 @@ class Reconciler:
                         self.stats["records_owned"] += 1
                     if r.uid != pod.uid:
                         moves.append((pod.uid, r.aid))
+                    elif _drifted(pod, r):
+                        drifts.append((pod.uid, r.aid))
             done = 0
             started = {f"{ns}/{name}" for ns, name in truth}
             await self._finish_holds()
@@ -114,6 +123,19 @@ class Reconciler:
                     self.stats["deferred"] += 1
                     continue  # an interrupted exchange involves one of them: finish it first (next pass)
                 if await self._exchange(p, r, started):
+                    done += 1
+            for p_uid, aid in drifts:
+                r = self.state.records.get(aid)
+                p = self.state.pods.get(p_uid)
+                if r is None or p is None or r.uid != p_uid or not _drifted(p, r) or {p_uid} & self.busy():
+                    continue
+                q = self._drift_partner(p, r, started)
+                log.warning("pod %s is annotated with GPU %d but its container runs on GPU %d: re-annotating%s",
+                            p.key, p.dev, r.dev, f" (exchanging with {q.key})" if q else "")
+                if q is None:
+                    await self._make_room(r.dev, p, started)
+                if await self._exchange(p, r, started, partner=q, move=False):
+                    self.stats["drift_repaired"] += 1
                     done += 1
             await self._finish_holds()
             await self._reset_orphans(started, 0.0 if urgent else self.stale_after)
@@ -167,19 +189,21 @@ class Reconciler:
         return {prof.annotation_idx: str(f["idx"]), prof.annotation_assigned: f["assigned"] or "false",
                 POD_CU_MASK_ANNOTATION: f["cu_mask"] or None}
 
-    async def _exchange(self, p: PodRec, r: AllocRecord, started: set) -> bool:
-        q = self.state.pods.get(r.uid)
-        if q is None:
-            # the pod the record was built for is gone: P simply takes the record's fields
-            q_fields = None
+    async def _exchange(self, p: PodRec, r: AllocRecord, started: set, partner: PodRec | None = None,
+                        move: bool = True) -> bool:
+        """P takes ``r``'s fields, its partner Q (the pod ``r`` was built for, or ``partner``) P's old ones.
+        ``move=False``: the records and CU partitions already describe who runs what; only the annotations
+        are wrong (a drift repair)."""
+        if partner is not None or not move:
+            q = partner
         else:
-            q_fields = fields(q)
-            if q.request != p.request:
+            q = self.state.pods.get(r.uid)
+            if q is not None and q.request != p.request:
                 self.stats["unreconcilable"] += 1
                 log.warning("pod %s holds the allocation of %s, of another size (%d vs %d); not reconciled",
                             p.key, q.key, p.request, q.request)
                 return False
-        if q is None:
+        if q is None and move:
             # its deletion freed r.dev in the extender's ledger although P's container runs there.  An unstarted
             # pod of P's size the extender has since placed on r.dev is the natural partner: exchanging with it
             # keeps the annotations' per-GPU sums exactly as they are (it starts on P's old GPU instead)
@@ -209,14 +233,37 @@ class Reconciler:
                     p.key, q.key if q else r.uid, r.dev)
         if not await self._patch(p, ann):  # step 1
             return False
-        self.state.move_records(p.uid, q.uid if q is not None else r.uid, r)
-        self.stats["swaps"] += 1
+        if move:
+            self.state.move_records(p.uid, q.uid if q is not None else r.uid, r)
+            self.stats["swaps"] += 1
         if q is not None:
             if await self._patch(self.state.pods.get(q.uid, q), self._ann(q_new)):  # step 2
                 if holding:
                     await self._clear_hold(self.state.pods.get(p.uid, p))  # step 3
             # on a conflict the hold stays; _finish_holds completes the move on a later pass
         return True
+
+    def _drift_partner(self, p: PodRec, r: AllocRecord, started: set) -> PodRec | None:
+        """A pod of P's size annotated with what P's container really has, whose own annotation is not what its
+        container has either (or which has not started): exchanging the two annotations fixes both."""
+        recs = list(self.state.records.values())
+        own = {}
+        for o in recs:
+            if o.uid == o.holder:
+                own.setdefault(o.uid, o)
+        cands = []
+        for q in self.state.pods.values():
+            if q.uid == p.uid or q.request != p.request or q.complete or (q.dev, q.cu_mask or "") != (r.dev, r.cu_mask or ""):
+                continue
+            if q.uid in self.busy() or q.uid in self.state.inflight:
+                continue
+            o = own.get(q.uid)
+            if o is not None and not _drifted(q, o):
+                continue  # Q's annotation is its own container's truth
+            if o is None and q.key in started:
+                continue
+            cands.append(q)
+        return min(cands, key=lambda q: q.order) if cands else None
 
     def _stand_in_partner(self, dev: int, p: PodRec, started: set) -> PodRec | None:
         recs = self.state.records.values()

@@ -184,8 +184,14 @@ def build_isolate(force: bool = False, verbose: bool = False) -> list[Path]:
     deps = [src / "gsx_isolate.cc"]
     if force or _newer(lib, deps):
         OUT.mkdir(parents=True, exist_ok=True)
-        _run(["g++", *CXXFLAGS, *HSA_FLAGS, "-shared", str(src / "gsx_isolate.cc"), "-o", str(lib), "-ldl",
-              "-lpthread"], verbose)
+        # loaded into arbitrary container userlands: libc only (no C++ runtime: compiled without exceptions /
+        # RTTI / thread-safe statics and linked by the C driver)
+        obj = ROOT / "build" / "gsx_isolate.o"
+        obj.parent.mkdir(parents=True, exist_ok=True)
+        _run(["g++", *CXXFLAGS, *HSA_FLAGS, "-fno-exceptions", "-fno-rtti", "-fno-threadsafe-statics", "-c",
+              str(src / "gsx_isolate.cc"), "-o", str(obj)], verbose)
+        _run(["gcc", "-shared", str(obj), "-o", str(lib), "-static-libgcc", "-Wl,--exclude-libs,ALL",
+              "-Wl,-z,defs", "-lpthread"], verbose)
     test = ROOT / "build" / "isolate_test"
     if force or _newer(test, [src / "isolate_test.cc"]):
         test.parent.mkdir(parents=True, exist_ok=True)

@@ -26,39 +26,37 @@
 //     ledger=/run/gsx/hbm.ledger
 // Loaded through /etc/ld.so.preload (mounted by the plugin), the constructor below adds the library to
 // HSA_TOOLS_LIB before the program's first HIP call, so unsetting environment variables does not escape it.
-// Not covered: statically linked programs, and processes that drive /dev/kfd ioctls directly.
-#include <dlfcn.h>
+// Not covered: statically linked programs, and processes that drive /dev/kfd ioctls directly.  It confines
+// programs, not adversaries (like MPS): a process can rewrite its own pod's ledger file.
+//
+// Portability: the library is loaded into whatever userland the container image has, and a preload that fails to
+// load is skipped by ld.so with only a warning.  So it needs nothing but libc: no C++ runtime (plain data, pthread
+// mutexes, its own hash table; built with -fno-exceptions -fno-rtti and linked without libstdc++) and no glibc
+// symbol newer than 2.14 (stat/fstat@2.33 and dladdr@2.34 are avoided).  tests/test_isolation.py checks both.
+#include <errno.h>
 #include <execinfo.h>
 #include <fcntl.h>
-#include <signal.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_api_trace.h>
 #include <hsa/hsa_ext_amd.h>
 #include <pthread.h>
+#include <signal.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 #include <sys/mman.h>
-#include <sys/stat.h>
 #include <unistd.h>
-
-#include <atomic>
-#include <cerrno>
-#include <cstddef>
-#include <cstdint>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <mutex>
-#include <new>
-#include <string>
-#include <unordered_map>
-#include <vector>
 
 #define GSX_EXPORT extern "C" __attribute__((visibility("default")))
 
 namespace {
 
-constexpr const char* kFixedConfig = "/run/gsx/isolation.conf";
+const char kFixedConfig[] = "/run/gsx/isolation.conf";
 constexpr uint64_t kMagic = 0x31304d4248585347ull;  // "GSXHBM01"
 constexpr int kSlots = 256;
+constexpr int kMaxMaskWords = 64;  // 2048 CUs
 
 struct LedgerFile {
   uint64_t magic;
@@ -66,24 +64,25 @@ struct LedgerFile {
   uint64_t bytes[kSlots];        // slot i = device bytes held by the process that holds the lock on byte 64+i
 };
 
+// Plain data only: no constructors or destructors run for process state (HIP's own static destructors, which
+// run after ours, still free device memory through the hooks at exit), and no C++ runtime library is needed.
 struct Config {
-  std::vector<uint32_t> cu_mask;  // empty: no CU partition
-  uint64_t hbm_limit = 0;         // 0: no cap
-  std::string ledger;             // empty: per-process account
-  std::string source;
-  bool verbose = false;
+  uint32_t cu_mask[kMaxMaskWords];
+  int cu_words;                   // 0: no CU partition
+  uint64_t hbm_limit;             // 0: no cap
+  char ledger[1024];              // "": per-process account
+  char source[1024];
+  bool verbose;
 };
 
-// Process state is never destroyed: HIP's own static destructors (which run after ours, the library having
-// been loaded after libamdhip64) still free device memory through the hooks at exit.
-Config& g_cfg = *new Config;
-std::mutex& g_mu = *new std::mutex;  // the process-local half of the ledger lock (OFD locks do not exclude threads)
-std::unordered_map<uintptr_t, uint64_t>& g_allocs = *new std::unordered_map<uintptr_t, uint64_t>;  // ptr -> bytes
+Config g_cfg;
+pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;  // process-local half of the ledger lock (OFD locks do not
+                                                    // exclude threads of one process)
 uint64_t g_local_used = 0;        // this process's device bytes (the ledger slot mirrors it)
 int g_fd = -1;
 LedgerFile* g_map = nullptr;
 int g_slot = -1;
-std::atomic<uint64_t> g_stats_queues{0}, g_stats_masked{0}, g_stats_denied{0}, g_stats_reduced{0};
+uint64_t g_stats_queues = 0, g_stats_masked = 0, g_stats_denied = 0, g_stats_reduced = 0;  // __atomic ops
 
 // the runtime's own entry points, saved by OnLoad
 decltype(hsa_queue_create)* real_queue_create = nullptr;
@@ -96,114 +95,186 @@ decltype(hsa_amd_memory_pool_free)* real_pool_free = nullptr;
 decltype(hsa_amd_vmem_handle_create)* real_vmem_create = nullptr;
 decltype(hsa_amd_vmem_handle_release)* real_vmem_release = nullptr;
 
-#define GSX_LOG(...)                                                        \
-  do {                                                                      \
-    if (g_cfg.verbose) {                                                    \
-      std::fprintf(stderr, "gsx-isolate[%d]: ", static_cast<int>(getpid())); \
-      std::fprintf(stderr, __VA_ARGS__);                                    \
-      std::fputc('\n', stderr);                                             \
-    }                                                                       \
+#define GSX_LOG(...)                                                   \
+  do {                                                                 \
+    if (g_cfg.verbose) {                                               \
+      fprintf(stderr, "gsx-isolate[%d]: ", static_cast<int>(getpid())); \
+      fprintf(stderr, __VA_ARGS__);                                    \
+      fputc('\n', stderr);                                             \
+    }                                                                  \
   } while (0)
 
-std::string trim(const std::string& s) {
-  size_t a = s.find_first_not_of(" \t\r\n"), b = s.find_last_not_of(" \t\r\n");
-  return a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
+void bump(uint64_t* c) { __atomic_fetch_add(c, 1, __ATOMIC_RELAXED); }
+
+struct Lock {  // scoped pthread mutex
+  pthread_mutex_t* m;
+  explicit Lock(pthread_mutex_t* mu) : m(mu) { pthread_mutex_lock(m); }
+  ~Lock() { pthread_mutex_unlock(m); }
+};
+
+// ------------------------------------------------------------------ live allocations (ptr / handle -> bytes)
+// open addressing, linear probing; key 0 = empty, 1 = tombstone (pointers and tagged handles are neither)
+struct Entry {
+  uintptr_t key;
+  uint64_t bytes;
+};
+Entry* g_tab = nullptr;
+size_t g_cap = 0, g_fill = 0;  // g_fill: live entries + tombstones
+
+size_t hash_key(uintptr_t k) {
+  uint64_t x = k;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  return static_cast<size_t>(x);
+}
+
+void tab_insert_raw(Entry* tab, size_t cap, uintptr_t k, uint64_t v) {
+  for (size_t i = hash_key(k) & (cap - 1);; i = (i + 1) & (cap - 1)) {
+    if (tab[i].key == 0) {
+      tab[i].key = k;
+      tab[i].bytes = v;
+      return;
+    }
+  }
+}
+
+bool tab_put(uintptr_t k, uint64_t v) {  // g_mu held
+  if ((g_fill + 1) * 4 >= g_cap * 3) {
+    size_t live = 0;
+    for (size_t i = 0; i < g_cap; ++i) live += g_tab[i].key > 1;
+    size_t cap = 1024;
+    while ((live + 1) * 2 >= cap) cap *= 2;
+    Entry* t = static_cast<Entry*>(calloc(cap, sizeof(Entry)));
+    if (!t) return false;
+    for (size_t i = 0; i < g_cap; ++i) {
+      if (g_tab[i].key > 1) tab_insert_raw(t, cap, g_tab[i].key, g_tab[i].bytes);
+    }
+    free(g_tab);
+    g_tab = t;
+    g_cap = cap;
+    g_fill = live;
+  }
+  tab_insert_raw(g_tab, g_cap, k, v);
+  g_fill++;
+  return true;
+}
+
+bool tab_take(uintptr_t k, uint64_t* v) {  // g_mu held
+  if (g_cap == 0) return false;
+  for (size_t i = hash_key(k) & (g_cap - 1);; i = (i + 1) & (g_cap - 1)) {
+    if (g_tab[i].key == 0) return false;
+    if (g_tab[i].key == k) {
+      *v = g_tab[i].bytes;
+      g_tab[i].key = 1;
+      return true;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ configuration
+char* trim(char* s) {
+  while (*s == ' ' || *s == '\t') ++s;
+  char* e = s + strlen(s);
+  while (e > s && (e[-1] == ' ' || e[-1] == '\t' || e[-1] == '\r' || e[-1] == '\n')) *--e = 0;
+  return s;
 }
 
 bool parse_config(const char* path, Config* out) {
-  FILE* f = std::fopen(path, "r");
+  FILE* f = fopen(path, "r");
   if (!f) return false;
   char line[4096];
-  while (std::fgets(line, sizeof line, f)) {
-    std::string l = trim(line);
-    if (l.empty() || l[0] == '#') continue;
-    size_t eq = l.find('=');
-    if (eq == std::string::npos) continue;
-    std::string k = trim(l.substr(0, eq)), v = trim(l.substr(eq + 1));
-    if (k == "cu_mask") {
-      size_t i = 0;
-      while (i < v.size()) {
-        size_t j = v.find(',', i);
-        if (j == std::string::npos) j = v.size();
-        std::string w = trim(v.substr(i, j - i));
-        if (!w.empty()) out->cu_mask.push_back(static_cast<uint32_t>(std::strtoul(w.c_str(), nullptr, 16)));
-        i = j + 1;
+  while (fgets(line, sizeof line, f)) {
+    char* l = trim(line);
+    if (!*l || *l == '#') continue;
+    char* eq = strchr(l, '=');
+    if (!eq) continue;
+    *eq = 0;
+    char* k = trim(l);
+    char* v = trim(eq + 1);
+    if (!strcmp(k, "cu_mask")) {
+      out->cu_words = 0;
+      for (char* p = v; *p && out->cu_words < kMaxMaskWords;) {
+        char* end = nullptr;
+        unsigned long w = strtoul(p, &end, 16);
+        if (end == p) break;
+        out->cu_mask[out->cu_words++] = static_cast<uint32_t>(w);
+        p = end;
+        while (*p == ',' || *p == ' ') ++p;
       }
-    } else if (k == "hbm_limit_bytes") {
-      out->hbm_limit = std::strtoull(v.c_str(), nullptr, 10);
-    } else if (k == "ledger") {
-      out->ledger = v;
-    } else if (k == "verbose") {
-      out->verbose = v == "1" || v == "true";
+    } else if (!strcmp(k, "hbm_limit_bytes")) {
+      out->hbm_limit = strtoull(v, nullptr, 10);
+    } else if (!strcmp(k, "ledger")) {
+      snprintf(out->ledger, sizeof out->ledger, "%s", v);
+    } else if (!strcmp(k, "verbose")) {
+      out->verbose = !strcmp(v, "1") || !strcmp(v, "true");
     }
   }
-  std::fclose(f);
+  fclose(f);
   bool any = false;
-  for (uint32_t w : out->cu_mask) any = any || w != 0;
-  if (!any) out->cu_mask.clear();  // an all-zero mask would stop every queue: treat it as "no partition"
-  out->source = path;
+  for (int i = 0; i < out->cu_words; ++i) any = any || out->cu_mask[i] != 0;
+  if (!any) out->cu_words = 0;  // an all-zero mask would stop every queue: treat it as "no partition"
+  snprintf(out->source, sizeof out->source, "%s", path);
   return true;
 }
 
 const char* config_path() {
-  struct stat st;
-  if (::stat(kFixedConfig, &st) == 0) return kFixedConfig;
-  const char* e = std::getenv("GSX_ISOLATION_CONFIG");
+  if (access(kFixedConfig, F_OK) == 0) return kFixedConfig;
+  const char* e = getenv("GSX_ISOLATION_CONFIG");
   return e && *e ? e : nullptr;
 }
 
 // ------------------------------------------------------------------ shared per-pod HBM ledger
 int ofd_lock(int fd, short type, off_t off, bool wait) {
   struct flock fl;
-  std::memset(&fl, 0, sizeof fl);
+  memset(&fl, 0, sizeof fl);
   fl.l_type = type;
   fl.l_whence = SEEK_SET;
   fl.l_start = off;
   fl.l_len = 1;
   int r;
   do {
-    r = ::fcntl(fd, wait ? F_OFD_SETLKW : F_OFD_SETLK, &fl);
+    r = fcntl(fd, wait ? F_OFD_SETLKW : F_OFD_SETLK, &fl);
   } while (r != 0 && errno == EINTR);
   return r;
 }
 
 bool slot_alive(int fd, int i) {
   struct flock fl;
-  std::memset(&fl, 0, sizeof fl);
+  memset(&fl, 0, sizeof fl);
   fl.l_type = F_WRLCK;
   fl.l_whence = SEEK_SET;
   fl.l_start = static_cast<off_t>(offsetof(LedgerFile, bytes) + i);
   fl.l_len = 1;
-  if (::fcntl(fd, F_OFD_GETLK, &fl) != 0) return false;
+  if (fcntl(fd, F_OFD_GETLK, &fl) != 0) return false;
   return fl.l_type != F_UNLCK;  // another open file description holds the slot: its process is alive
 }
 
 // open + map the ledger and claim a free slot (caller holds g_mu); false: fall back to a per-process account
 bool ledger_open() {
   if (g_map) return true;
-  if (g_cfg.ledger.empty()) return false;
-  int fd = ::open(g_cfg.ledger.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  if (!g_cfg.ledger[0]) return false;
+  int fd = open(g_cfg.ledger, O_RDWR | O_CREAT | O_CLOEXEC, 0666);
   if (fd < 0) return false;
   if (ofd_lock(fd, F_WRLCK, 0, true) != 0) {
-    ::close(fd);
+    close(fd);
     return false;
   }
-  struct stat st;
-  if (::fstat(fd, &st) != 0 || (st.st_size < static_cast<off_t>(sizeof(LedgerFile)) &&
-                                ::ftruncate(fd, sizeof(LedgerFile)) != 0)) {
+  off_t size = lseek(fd, 0, SEEK_END);
+  if (size < 0 || (size < static_cast<off_t>(sizeof(LedgerFile)) && ftruncate(fd, sizeof(LedgerFile)) != 0)) {
     ofd_lock(fd, F_UNLCK, 0, false);
-    ::close(fd);
+    close(fd);
     return false;
   }
-  void* p = ::mmap(nullptr, sizeof(LedgerFile), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  void* p = mmap(nullptr, sizeof(LedgerFile), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   if (p == MAP_FAILED) {
     ofd_lock(fd, F_UNLCK, 0, false);
-    ::close(fd);
+    close(fd);
     return false;
   }
   auto* m = static_cast<LedgerFile*>(p);
   if (m->magic != kMagic) {
-    std::memset(m, 0, sizeof(LedgerFile));
+    memset(m, 0, sizeof(LedgerFile));
     m->magic = kMagic;
   }
   int slot = -1;
@@ -213,8 +284,8 @@ bool ledger_open() {
   }
   if (slot < 0) {
     ofd_lock(fd, F_UNLCK, 0, false);
-    ::munmap(p, sizeof(LedgerFile));
-    ::close(fd);
+    munmap(p, sizeof(LedgerFile));
+    close(fd);
     return false;
   }
   m->bytes[slot] = g_local_used;  // a dead owner's count is dropped with its slot
@@ -222,7 +293,7 @@ bool ledger_open() {
   g_fd = fd;
   g_map = m;
   g_slot = slot;
-  GSX_LOG("ledger %s slot %d", g_cfg.ledger.c_str(), slot);
+  GSX_LOG("ledger %s slot %d", g_cfg.ledger, slot);
   return true;
 }
 
@@ -247,26 +318,40 @@ struct LedgerGuard {
   }
 };
 
+void publish_locked() {
+  if (g_map) g_map->bytes[g_slot] = g_local_used;
+}
+
 void after_fork_child() {
-  // the child shares the parent's open file description (and so its slot lock): give it its own slot
-  if (g_map) ::munmap(g_map, sizeof(LedgerFile));
-  if (g_fd >= 0) ::close(g_fd);
+  // the child shares the parent's open file description (and so its slot lock): give it its own slot; the
+  // parent's device allocations are not the child's
+  if (g_map) munmap(g_map, sizeof(LedgerFile));
+  if (g_fd >= 0) close(g_fd);
   g_map = nullptr;
   g_fd = -1;
   g_slot = -1;
-  g_allocs.clear();
+  if (g_tab) memset(g_tab, 0, g_cap * sizeof(Entry));
+  g_fill = 0;
   g_local_used = 0;
-  new (&g_mu) std::mutex();
+  pthread_mutex_t fresh = PTHREAD_MUTEX_INITIALIZER;
+  g_mu = fresh;
 }
 
 // ------------------------------------------------------------------ pool / agent classification
+struct PoolKind {
+  uint64_t handle;
+  bool gpu;
+};
+PoolKind g_pools[256];
+int g_npools = 0;
+pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
+
 bool is_gpu_pool(hsa_amd_memory_pool_t pool) {
-  static std::mutex& mu = *new std::mutex;
-  static std::unordered_map<uint64_t, bool>& cache = *new std::unordered_map<uint64_t, bool>;
   {
-    std::lock_guard<std::mutex> l(mu);
-    auto it = cache.find(pool.handle);
-    if (it != cache.end()) return it->second;
+    Lock l(&g_pool_mu);
+    for (int i = 0; i < g_npools; ++i) {
+      if (g_pools[i].handle == pool.handle) return g_pools[i].gpu;
+    }
   }
   hsa_amd_segment_t seg = HSA_AMD_SEGMENT_GLOBAL;
   hsa_amd_memory_pool_location_t loc = HSA_AMD_MEMORY_POOL_LOCATION_CPU;
@@ -274,8 +359,8 @@ bool is_gpu_pool(hsa_amd_memory_pool_t pool) {
              seg == HSA_AMD_SEGMENT_GLOBAL &&
              real_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_LOCATION, &loc) == HSA_STATUS_SUCCESS &&
              loc == HSA_AMD_MEMORY_POOL_LOCATION_GPU;
-  std::lock_guard<std::mutex> l(mu);
-  cache[pool.handle] = gpu;
+  Lock l(&g_pool_mu);
+  if (g_npools < static_cast<int>(sizeof g_pools / sizeof g_pools[0])) g_pools[g_npools++] = PoolKind{pool.handle, gpu};
   return gpu;
 }
 
@@ -286,9 +371,11 @@ bool is_gpu_agent(hsa_agent_t agent) {
 
 // ------------------------------------------------------------------ CU partition hooks
 void apply_mask(hsa_queue_t* q) {
-  if (g_cfg.cu_mask.empty() || q == nullptr) return;
-  hsa_status_t s = real_cu_set_mask(q, static_cast<uint32_t>(32 * g_cfg.cu_mask.size()), g_cfg.cu_mask.data());
-  if (s == HSA_STATUS_SUCCESS || static_cast<int>(s) == static_cast<int>(HSA_STATUS_CU_MASK_REDUCED)) g_stats_masked++;
+  if (g_cfg.cu_words == 0 || q == nullptr) return;
+  hsa_status_t s = real_cu_set_mask(q, static_cast<uint32_t>(32 * g_cfg.cu_words), g_cfg.cu_mask);
+  if (s == HSA_STATUS_SUCCESS || static_cast<int>(s) == static_cast<int>(HSA_STATUS_CU_MASK_REDUCED)) {
+    bump(&g_stats_masked);
+  }
 }
 
 hsa_status_t hook_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type32_t type,
@@ -296,7 +383,7 @@ hsa_status_t hook_queue_create(hsa_agent_t agent, uint32_t size, hsa_queue_type3
                                uint32_t group, hsa_queue_t** queue) {
   hsa_status_t s = real_queue_create(agent, size, type, cb, data, priv, group, queue);
   if (s == HSA_STATUS_SUCCESS && queue) {
-    g_stats_queues++;
+    bump(&g_stats_queues);
     apply_mask(*queue);
   }
   return s;
@@ -307,69 +394,84 @@ hsa_status_t hook_intercept_create(hsa_agent_t agent, uint32_t size, hsa_queue_t
                                    uint32_t group, hsa_queue_t** queue) {
   hsa_status_t s = real_intercept_create(agent, size, type, cb, data, priv, group, queue);
   if (s == HSA_STATUS_SUCCESS && queue) {
-    g_stats_queues++;
+    bump(&g_stats_queues);
     apply_mask(*queue);
   }
   return s;
 }
 
 hsa_status_t hook_cu_set_mask(const hsa_queue_t* q, uint32_t nbits, const uint32_t* mask) {
-  if (g_cfg.cu_mask.empty()) return real_cu_set_mask(q, nbits, mask);
+  if (g_cfg.cu_words == 0) return real_cu_set_mask(q, nbits, mask);
   // the queue may narrow its partition, never leave it: AND with the pod's mask ("0 bits" = all CUs = the pod's)
-  std::vector<uint32_t> m(g_cfg.cu_mask);
+  uint32_t m[kMaxMaskWords];
+  const int n = g_cfg.cu_words;
+  memcpy(m, g_cfg.cu_mask, sizeof(uint32_t) * static_cast<size_t>(n));
   bool reduced = false;
   if (nbits != 0 && mask != nullptr) {
     size_t words = (nbits + 31) / 32;
     bool any = false;
-    for (size_t i = 0; i < m.size(); ++i) {
-      uint32_t w = i < words ? mask[i] : 0u;
-      if (i + 1 == words && nbits % 32) w &= (1u << (nbits % 32)) - 1u;
+    for (int i = 0; i < n; ++i) {
+      uint32_t w = static_cast<size_t>(i) < words ? mask[i] : 0u;
+      if (static_cast<size_t>(i) + 1 == words && nbits % 32) w &= (1u << (nbits % 32)) - 1u;
       reduced = reduced || (w & ~m[i]) != 0;
       m[i] &= w;
       any = any || m[i] != 0;
     }
-    if (!any) m = g_cfg.cu_mask;  // nothing of the request lies in the partition: keep the partition
+    if (!any) memcpy(m, g_cfg.cu_mask, sizeof(uint32_t) * static_cast<size_t>(n));  // nothing of it lies inside
   }
-  hsa_status_t s = real_cu_set_mask(q, static_cast<uint32_t>(32 * m.size()), m.data());
-  g_stats_masked++;
-  if (reduced) g_stats_reduced++;
+  hsa_status_t s = real_cu_set_mask(q, static_cast<uint32_t>(32 * n), m);
+  bump(&g_stats_masked);
+  if (reduced) bump(&g_stats_reduced);
   // a request that reached outside the partition is honoured only inside it, silently (as under MPS): HIP
   // treats any status but SUCCESS from this call as a failed stream creation
   return static_cast<int>(s) == static_cast<int>(HSA_STATUS_CU_MASK_REDUCED) ? HSA_STATUS_SUCCESS : s;
 }
 
 // ------------------------------------------------------------------ HBM share hooks
-hsa_status_t hook_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr) {
-  if (g_cfg.hbm_limit == 0 || !is_gpu_pool(pool)) return real_pool_allocate(pool, size, flags, ptr);
-  std::lock_guard<std::mutex> l(g_mu);
+constexpr uintptr_t kHandleTag = uintptr_t{1} << 63;  // vmem handles and pointers share the table
+
+// charge `size` bytes to the pod if they fit (g_mu held): false = over the share
+bool charge_locked(uint64_t size) {
   ledger_open();
   LedgerGuard lg;
   uint64_t used = pod_used_locked();
   if (used + size > g_cfg.hbm_limit) {
-    g_stats_denied++;
-    GSX_LOG("denied %zu bytes (pod holds %llu of %llu)", size, static_cast<unsigned long long>(used),
-            static_cast<unsigned long long>(g_cfg.hbm_limit));
-    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
+    bump(&g_stats_denied);
+    GSX_LOG("denied %llu bytes (pod holds %llu of %llu)", static_cast<unsigned long long>(size),
+            static_cast<unsigned long long>(used), static_cast<unsigned long long>(g_cfg.hbm_limit));
+    return false;
   }
+  return true;
+}
+
+void record_locked(uintptr_t key, uint64_t size) {
+  LedgerGuard lg;
+  if (!tab_put(key, size)) return;  // out of host memory for the table: the bytes go unaccounted
+  g_local_used += size;
+  publish_locked();
+}
+
+void forget_locked(uintptr_t key) {
+  uint64_t bytes = 0;
+  if (!tab_take(key, &bytes)) return;
+  LedgerGuard lg;
+  g_local_used -= bytes;
+  publish_locked();
+}
+
+hsa_status_t hook_pool_allocate(hsa_amd_memory_pool_t pool, size_t size, uint32_t flags, void** ptr) {
+  if (g_cfg.hbm_limit == 0 || !is_gpu_pool(pool)) return real_pool_allocate(pool, size, flags, ptr);
+  Lock l(&g_mu);
+  if (!charge_locked(size)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   hsa_status_t s = real_pool_allocate(pool, size, flags, ptr);
-  if (s == HSA_STATUS_SUCCESS && ptr && *ptr) {
-    g_allocs[reinterpret_cast<uintptr_t>(*ptr)] = size;
-    g_local_used += size;
-    if (g_map) g_map->bytes[g_slot] = g_local_used;
-  }
+  if (s == HSA_STATUS_SUCCESS && ptr && *ptr) record_locked(reinterpret_cast<uintptr_t>(*ptr), size);
   return s;
 }
 
 hsa_status_t hook_pool_free(void* ptr) {
   if (g_cfg.hbm_limit != 0 && ptr) {
-    std::lock_guard<std::mutex> l(g_mu);
-    auto it = g_allocs.find(reinterpret_cast<uintptr_t>(ptr));
-    if (it != g_allocs.end()) {
-      LedgerGuard lg;
-      g_local_used -= it->second;
-      if (g_map) g_map->bytes[g_slot] = g_local_used;
-      g_allocs.erase(it);
-    }
+    Lock l(&g_mu);
+    forget_locked(reinterpret_cast<uintptr_t>(ptr));
   }
   return real_pool_free(ptr);
 }
@@ -377,33 +479,18 @@ hsa_status_t hook_pool_free(void* ptr) {
 hsa_status_t hook_vmem_create(hsa_amd_memory_pool_t pool, size_t size, hsa_amd_memory_type_t type, uint64_t flags,
                               hsa_amd_vmem_alloc_handle_t* handle) {
   if (g_cfg.hbm_limit == 0 || !is_gpu_pool(pool)) return real_vmem_create(pool, size, type, flags, handle);
-  std::lock_guard<std::mutex> l(g_mu);
-  ledger_open();
-  LedgerGuard lg;
-  if (pod_used_locked() + size > g_cfg.hbm_limit) {
-    g_stats_denied++;
-    return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
-  }
+  Lock l(&g_mu);
+  if (!charge_locked(size)) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   hsa_status_t s = real_vmem_create(pool, size, type, flags, handle);
-  if (s == HSA_STATUS_SUCCESS && handle) {
-    g_allocs[static_cast<uintptr_t>(handle->handle) | (uintptr_t{1} << 63)] = size;
-    g_local_used += size;
-    if (g_map) g_map->bytes[g_slot] = g_local_used;
-  }
+  if (s == HSA_STATUS_SUCCESS && handle) record_locked(static_cast<uintptr_t>(handle->handle) | kHandleTag, size);
   return s;
 }
 
 hsa_status_t hook_vmem_release(hsa_amd_vmem_alloc_handle_t handle) {
   hsa_status_t s = real_vmem_release(handle);
   if (g_cfg.hbm_limit != 0 && s == HSA_STATUS_SUCCESS) {
-    std::lock_guard<std::mutex> l(g_mu);
-    auto it = g_allocs.find(static_cast<uintptr_t>(handle.handle) | (uintptr_t{1} << 63));
-    if (it != g_allocs.end()) {
-      LedgerGuard lg;
-      g_local_used -= it->second;
-      if (g_map) g_map->bytes[g_slot] = g_local_used;
-      g_allocs.erase(it);
-    }
+    Lock l(&g_mu);
+    forget_locked(static_cast<uintptr_t>(handle.handle) | kHandleTag);
   }
   return s;
 }
@@ -425,7 +512,7 @@ hsa_status_t hook_agent_get_info(hsa_agent_t agent, hsa_agent_info_t attr, void*
   if (static_cast<int>(attr) == static_cast<int>(HSA_AMD_AGENT_INFO_MEMORY_AVAIL) && is_gpu_agent(agent)) {
     uint64_t used;
     {
-      std::lock_guard<std::mutex> l(g_mu);
+      Lock l(&g_mu);
       ledger_open();
       LedgerGuard lg;
       used = pod_used_locked();
@@ -450,17 +537,30 @@ void crash_report(int sig) {
   void* frames[64];
   int n = backtrace(frames, 64);
   char msg[64];
-  int m = std::snprintf(msg, sizeof msg, "gsx-isolate[%d]: signal %d\n", static_cast<int>(getpid()), sig);
-  if (m > 0) (void)!::write(2, msg, static_cast<size_t>(m));
+  int m = snprintf(msg, sizeof msg, "gsx-isolate[%d]: signal %d\n", static_cast<int>(getpid()), sig);
+  if (m > 0) (void)!write(2, msg, static_cast<size_t>(m));
   backtrace_symbols_fd(frames, n, 2);
-  ::signal(sig, SIG_DFL);
-  ::raise(sig);
+  signal(sig, SIG_DFL);
+  raise(sig);
 }
 
-std::string self_path() {
-  Dl_info info;
-  if (dladdr(reinterpret_cast<void*>(&self_path), &info) && info.dli_fname) return info.dli_fname;
-  return "";
+// the mapped file that contains this function (/proc/self/maps: no dladdr, whose symbol version would tie the
+// library to the build host's glibc); "" if not found
+void self_path(char* out, size_t cap) {
+  out[0] = 0;
+  uintptr_t me = reinterpret_cast<uintptr_t>(&self_path);
+  FILE* f = fopen("/proc/self/maps", "r");
+  if (!f) return;
+  char line[4096];
+  while (fgets(line, sizeof line, f)) {
+    unsigned long lo = 0, hi = 0;
+    if (sscanf(line, "%lx-%lx", &lo, &hi) != 2 || me < lo || me >= hi) continue;
+    const char* path = strchr(line, '/');
+    if (path) snprintf(out, cap, "%s", path);
+    break;
+  }
+  fclose(f);
+  trim(out);
 }
 
 }  // namespace
@@ -468,10 +568,11 @@ std::string self_path() {
 // ------------------------------------------------------------------ HSA tools-library entry points
 GSX_EXPORT bool OnLoad(HsaApiTable* table, uint64_t runtime_version, uint64_t failed_tool_count,
                        const char* const* failed_tool_names) {
-  if (std::getenv("GSX_ISOLATION_VERBOSE")) {
+  (void)failed_tool_names;
+  if (getenv("GSX_ISOLATION_VERBOSE")) {
     g_cfg.verbose = true;
-    ::signal(SIGSEGV, crash_report);
-    ::signal(SIGBUS, crash_report);
+    signal(SIGSEGV, crash_report);
+    signal(SIGBUS, crash_report);
     GSX_LOG("OnLoad(runtime %llu, failed tools %llu): core table %u bytes, amd_ext %u bytes (ours %zu / %zu)",
             static_cast<unsigned long long>(runtime_version), static_cast<unsigned long long>(failed_tool_count),
             table && table->core_ ? table->core_->version.minor_id : 0u,
@@ -480,17 +581,17 @@ GSX_EXPORT bool OnLoad(HsaApiTable* table, uint64_t runtime_version, uint64_t fa
   }
   const char* path = config_path();
   if (!path || !parse_config(path, &g_cfg)) {
-    if (path) std::fprintf(stderr, "gsx-isolate: cannot read %s; not isolating\n", path);
+    if (path) fprintf(stderr, "gsx-isolate: cannot read %s; not isolating\n", path);
     return true;  // nothing to enforce: stay loaded and inert
   }
-  if (std::getenv("GSX_ISOLATION_VERBOSE")) g_cfg.verbose = true;
+  if (getenv("GSX_ISOLATION_VERBOSE")) g_cfg.verbose = true;
   if (table == nullptr || table->core_ == nullptr || table->amd_ext_ == nullptr) return false;
   CoreApiTable* core = table->core_;
   AmdExtTable* amd = table->amd_ext_;
   if (!has_field(core, &CoreApiTable::hsa_queue_create_fn) || !has_field(core, &CoreApiTable::hsa_agent_get_info_fn) ||
       !has_field(amd, &AmdExtTable::hsa_amd_queue_cu_set_mask_fn) ||
       !has_field(amd, &AmdExtTable::hsa_amd_memory_pool_free_fn)) {
-    std::fprintf(stderr, "gsx-isolate: HSA API table too old; refusing to run unconfined\n");
+    fprintf(stderr, "gsx-isolate: HSA API table too old; refusing to run unconfined\n");
     return false;
   }
   real_queue_create = core->hsa_queue_create_fn;
@@ -517,9 +618,8 @@ GSX_EXPORT bool OnLoad(HsaApiTable* table, uint64_t runtime_version, uint64_t fa
   }
   pthread_atfork(nullptr, nullptr, after_fork_child);
   int cus = 0;
-  for (uint32_t w : g_cfg.cu_mask) cus += __builtin_popcount(w);
-  GSX_LOG("%s: %d CUs, hbm_limit %llu bytes", g_cfg.source.c_str(), cus,
-          static_cast<unsigned long long>(g_cfg.hbm_limit));
+  for (int i = 0; i < g_cfg.cu_words; ++i) cus += __builtin_popcount(g_cfg.cu_mask[i]);
+  GSX_LOG("%s: %d CUs, hbm_limit %llu bytes", g_cfg.source, cus, static_cast<unsigned long long>(g_cfg.hbm_limit));
   return true;
 }
 
@@ -528,22 +628,30 @@ GSX_EXPORT void OnUnload() {}
 // counters for tests and for the workload's self-report: queues created, mask applications, allocations
 // denied, this process's device bytes, mask requests narrowed to the partition
 GSX_EXPORT void gsx_isolate_stats(uint64_t out[5]) {
-  out[0] = g_stats_queues.load();
-  out[1] = g_stats_masked.load();
-  out[2] = g_stats_denied.load();
-  out[4] = g_stats_reduced.load();
-  std::lock_guard<std::mutex> l(g_mu);
+  out[0] = __atomic_load_n(&g_stats_queues, __ATOMIC_RELAXED);
+  out[1] = __atomic_load_n(&g_stats_masked, __ATOMIC_RELAXED);
+  out[2] = __atomic_load_n(&g_stats_denied, __ATOMIC_RELAXED);
+  out[4] = __atomic_load_n(&g_stats_reduced, __ATOMIC_RELAXED);
+  Lock l(&g_mu);
   out[3] = g_local_used;
 }
 
 // loaded by /etc/ld.so.preload or LD_PRELOAD: make sure ROCr loads us as a tools library (before any hsa_init)
 __attribute__((constructor)) static void gsx_isolate_preload() {
   if (!config_path()) return;
-  std::string me = self_path();
-  if (me.empty()) return;
-  const char* cur = std::getenv("HSA_TOOLS_LIB");
-  std::string v = cur ? cur : "";
-  if (v.find(me) != std::string::npos) return;
-  v = v.empty() ? me : me + " " + v;
-  ::setenv("HSA_TOOLS_LIB", v.c_str(), 1);
+  char me[4096];
+  self_path(me, sizeof me);
+  if (!me[0]) return;
+  const char* cur = getenv("HSA_TOOLS_LIB");
+  if (cur && strstr(cur, me)) return;
+  size_t n = strlen(me) + (cur ? strlen(cur) + 1 : 0) + 1;
+  char* v = static_cast<char*>(malloc(n));
+  if (!v) return;
+  if (cur && *cur) {
+    snprintf(v, n, "%s %s", me, cur);
+  } else {
+    snprintf(v, n, "%s", me);
+  }
+  setenv("HSA_TOOLS_LIB", v, 1);
+  free(v);
 }

@@ -102,3 +102,23 @@ def test_plugin_allocate_mounts_isolation_and_records(tmp_path):
             await c.close()
             await api.stop()
     asyncio.run(go())
+
+
+def test_library_loads_into_any_container_userland():
+    """ld.so skips a preload that fails to load with only a warning, and the container image's userland is not
+    ours: the library may need nothing but libc, and no glibc symbol version newer than 2.17 (CentOS 7 /
+    Ubuntu 18.04 era); no libstdc++ (whose GLIBCXX versions would tie it to this build host's GCC)."""
+    import re
+    import shutil
+    import subprocess
+
+    objdump = shutil.which("objdump") or "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    p = subprocess.run([objdump, "-p", str(LIB)], capture_output=True, text=True, check=True).stdout
+    needed = set(re.findall(r"NEEDED\s+(\S+)", p))
+    assert needed <= {"libc.so.6", "ld-linux-x86-64.so.2"}, needed
+    t = subprocess.run([objdump, "-T", str(LIB)], capture_output=True, text=True, check=True).stdout
+    assert "GLIBCXX" not in t and "CXXABI" not in t
+    versions = {tuple(int(x) for x in v.split(".")) for v in re.findall(r"GLIBC_(\d+\.\d+(?:\.\d+)?)", t)}
+    assert versions and max(versions) <= (2, 17), sorted(versions)
+    exported = {ln.split()[-1] for ln in t.splitlines() if " g " in ln and ".text" in ln}
+    assert exported == {"OnLoad", "OnUnload", "gsx_isolate_stats"}, exported

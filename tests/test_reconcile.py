@@ -213,3 +213,31 @@ def test_unowned_record_outlives_the_pod_it_was_built_for_while_kubelet_reports_
     st.set_owner("aQ", "uP")
     st.release("uP")  # its owner's deletion does drop it
     assert "aQ" not in st.records
+
+
+def test_annotations_edited_behind_the_plugins_back_are_repaired():
+    """Any cause (an operator's edit, a half-applied exchange from an older plugin): a pod whose annotation names
+    another GPU than its container's allocation is re-annotated from kubelet's record, by exchanging with the
+    pod that carries its real GPU."""
+    async def go():
+        cl = Cluster(ALIYUN, [96] * 4, gpu=False, agent="plugin", agent_args=["--faithful"])
+        try:
+            await cl.start()
+            for n in ("a", "b"):
+                await cl.create(n, 64)
+            pods = await cl.wait(["a", "b"])
+            phys = await _physical(cl, pods)
+            assert phys["a"] != phys["b"]
+            for n, other in (("a", "b"), ("b", "a")):  # swap the two pods' *_IDX behind everyone's back
+                await cl.c.patch("pods", n, {"metadata": {"annotations": {
+                    ALIYUN.annotation_idx: str(phys[other])}}}, "default")
+            drift, drifted = await cl.physical_drift(["a", "b"], timeout=15)
+            assert drift == 0, drifted
+            st = await cl.agent_stats()
+            assert st["reconcile"]["drift_repaired"] >= 1, st["reconcile"]
+            insp = await cl.inspect()
+            used = [d["usedGPU"] for d in insp["nodes"][0]["devs"]]
+            assert sorted(used) == [0, 0, 64, 64] and used[phys["a"]] == 64 and used[phys["b"]] == 64
+        finally:
+            await cl.close()
+    asyncio.run(go())
