@@ -287,7 +287,9 @@ class NodeAgent:
                                                "message": f"Allocate failed: {e}"})
             return
         got = allocs[0]
-        if not self._alive(got.uid, got.key or key):
+        if self.faithful and got.uid != uid and self._alive(uid, key):
+            pass  # kubelet starts the pod it admitted with whatever it got, whether or not its builder still exists
+        elif not self._alive(got.uid, got.key or key):
             # the pod went away (deleted / completed) while its Allocate was in flight: kubelet's pod worker
             # drops it; its device IDs and runtime slice are never taken (the plugin's informer frees its CUs)
             self.stats["gone_during_allocate"] += 1

@@ -350,6 +350,9 @@ class GpuSharePlugin:
                 return rec, alloc
             if self.reconciler is not None:
                 rec = await self._physical_guard(rec, units)
+                if rec is None:  # the repair it ran made the pod no candidate (it was served meanwhile): re-match
+                    refreshed = True
+                    continue
                 device = self.devices[rec.dev]
                 cp = self.state.cus.get(rec.dev)
                 had_cus = cp is not None and cp.holds(rec.uid)
@@ -399,7 +402,7 @@ class GpuSharePlugin:
         """Units the pod annotations put on ``dev`` (what the extender's ledger accounts)."""
         return sum(p.request for p in self.state.pods.values() if p.dev == dev and p.uid != skip and not p.complete)
 
-    async def _physical_guard(self, rec: PodRec, units: int) -> PodRec:
+    async def _physical_guard(self, rec: PodRec, units: int) -> PodRec | None:
         """Never start a container on a GPU that is physically full.  The extender placed ``rec`` by the
         annotations; after a swap kubelet has not told us about yet, a deletion can free the GPU the annotation
         names while the container that really ran there lives on.  Repair the records first; if the GPU is still
@@ -415,7 +418,9 @@ class GpuSharePlugin:
         delay = 0.02
         while True:
             await self._reconcile_now(urgent=True)
-            rec = self.state.pods.get(rec.uid, rec)
+            rec = self.state.pods.get(rec.uid)
+            if rec is None or rec.assigned != "false" or not rec.pending or rec.uid in self.state.inflight:
+                return None
             if self._physical_used(rec.dev) + units <= self.units.get(rec.dev, 0):
                 return rec
             if time.monotonic() >= deadline:

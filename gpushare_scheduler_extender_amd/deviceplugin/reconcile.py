@@ -47,6 +47,9 @@ from .state import AllocRecord, PodRec
 log = logging.getLogger("gsx.deviceplugin.reconcile")
 
 
+GONE = "~"  # owner prefix of an allocation held by a pod that is no longer on this node (ns/name follows)
+
+
 def fields(p: PodRec) -> dict:
     return {"idx": p.dev, "assigned": p.assigned, "cu_mask": p.cu_mask}
 
@@ -98,6 +101,12 @@ class Reconciler:
             for (ns, name), per_container in truth.items():
                 pod = self.state.pod_by_key(f"{ns}/{name}")
                 if pod is None:
+                    # a pod this plugin no longer knows (deleted; its container still stopping): its allocations
+                    # are physically held, but by no live pod -- they describe nobody who could be served them
+                    for ids in per_container:
+                        r = self.state.record_for_ids(ids)
+                        if r is not None and r.owner != GONE + f"{ns}/{name}":
+                            self.state.set_owner(r.aid, GONE + f"{ns}/{name}")
                     continue
                 for ids in per_container:
                     r = self.state.record_for_ids(ids)
@@ -154,7 +163,8 @@ class Reconciler:
             self.plugin.persist_records()
 
     async def _reset_orphans(self, started: set, grace: float) -> None:
-        described = {r.uid for r in self.state.records.values()} | {r.holder for r in self.state.records.values()}
+        live = [r for r in self.state.records.values() if not r.owner.startswith(GONE)]
+        described = {r.uid for r in live} | {r.holder for r in live}
         busy = self.busy()
         now = time.monotonic()
         orphans = set()
