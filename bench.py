@@ -32,7 +32,8 @@ Stability: every control-plane process is pinned to its own physical core, the i
 After the timed region rank 0 runs, as extra keys outside ``value``:
 ``device_plugin_path``: the same waves with kubelet + device plugin played by the shipped gRPC
 ``GpuSharePlugin`` over its unix socket (the kubelet stand-in in deviceplugin/agent.py) instead of the
-compiled node agent; and ``latency_sweep`` (extra keys, not part of
+compiled node agent; ``device_plugin_path_native_kubelet``: the compiled kubelet stand-in calling the shipped
+plugin process over gRPC; and ``latency_sweep`` (extra keys, not part of
 ``value``): the same waves with the fake kube-apiserver answering every
 non-watch request after 0 / 1 / 2 / 5 ms, for ``--bind-mode binding`` (one
 ``pods/binding`` POST per pod) and ``update`` (the reference's PUT + POST), and
@@ -309,6 +310,27 @@ def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
             "plugin_stats": stats.get("plugin_stats"), "plugin": stats.get("plugin")}
 
 
+def plugin_path_native_kubelet(a, children, api_url, runner: WaveRunner, E) -> dict:
+    """The same waves with the compiled kubelet stand-in (gsx-nodeagent --plugin-spawn) calling the shipped plugin
+    process over the device-plugin gRPC API: GetPreferredAllocation + Allocate per pod, serially as kubelet
+    admits, answered by the plugin's native endpoint (native/engine/h2.cc + dpcore.cc) on its own informer and
+    allocation state.  Every Allocate decision and ASSIGNED patch is the product's."""
+    from gpushare_scheduler_extender_amd.sim.cluster import start_node_agent
+
+    na = restart_child(children, "node-agent", lambda old: start_node_agent(
+        api_url, NODE, profile=a.profile, native=True, plugin="spawn", cpus=old.cpus))
+    client = E.BatchClient({"server": na.url})
+    wait_until(lambda: client.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 120, "plugin agent never ready")
+    row = runner.measure(2, a.sweep_steps)
+    st, body = client.run([("GET", "/v1/stats", b"")], 1)[0]
+    stats = json.loads(body) if st == 200 else {}
+    return {**row, "admit_p50_ms": stats.get("admit_p50_ms"), "failed": stats.get("failed"),
+            "kubelet_mean_ms": {"queue": (stats.get("mean_ms") or {}).get("queue"),
+                                "preferred_plus_allocate_grpc": (stats.get("mean_ms") or {}).get("assign_patch"),
+                                "runtime": (stats.get("mean_ms") or {}).get("runtime"),
+                                "running_patch": (stats.get("mean_ms") or {}).get("running_patch")}}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -329,9 +351,10 @@ def parse():
                     help="write every timed pod's scheduler timeline (CLOCK_MONOTONIC, like the wave's t0) here")
     ap.add_argument("--agent", default="node", choices=["node", "rank"],
                     help="node: one node-agent process (the node's device plugin) driving a runtime shim per GPU rank (default); rank: one agent per GPU rank")
-    ap.add_argument("--node-agent", default="native", choices=["native", "plugin", "inproc"],
-                    help="kubelet + device plugin: gsx-nodeagent (default), or the kubelet stand-in driving the "
-                         "shipped gRPC device plugin over its unix socket (plugin) / in-process (inproc)")
+    ap.add_argument("--node-agent", default="native", choices=["native", "native-plugin", "plugin", "inproc"],
+                    help="kubelet + device plugin: gsx-nodeagent with the plugin's matcher in-process (native), "
+                         "gsx-nodeagent calling the shipped plugin process over gRPC (native-plugin), or the Python "
+                         "kubelet stand-in driving the shipped plugin over its socket (plugin) / in-process (inproc)")
     ap.add_argument("--pin", default="auto", choices=["auto", "spread", "static", "compact", "none"],
                     help="CPU placement of the control-plane processes (auto = spread: the idlest physical cores, "
                          "sampled at start; static: topology order without the load sample)")
@@ -456,8 +479,10 @@ def main():
                                         cpus=cpu_plan.get("scheduler")))
         if a.agent == "node":
             # the node's device plugin / kubelet stand-in: one process for all GPUs of the node, like a DaemonSet
-            children.append(start_node_agent(api.url, NODE, profile=a.profile, native=a.node_agent == "native",
-                                             plugin="inproc" if a.node_agent == "inproc" else "grpc",
+            children.append(start_node_agent(api.url, NODE, profile=a.profile,
+                                             native=a.node_agent in ("native", "native-plugin"),
+                                             plugin={"inproc": "inproc", "native-plugin": "spawn"}.get(a.node_agent,
+                                                                                                        "grpc"),
                                              workers=min(16, max(8, 2 * a.pods_per_gpu * world)),
                                              cpus=cpu_plan.get("node-agent"),
                                              extra=["--faithful"] if a.kubelet == "faithful" else []))
@@ -792,7 +817,7 @@ def main():
         apiserver_stats = json.loads(body) if st == 200 else {"error": st}
         apiserver_stats.pop("counts", None)
 
-    sweep = ref_client = plugin_row = None
+    sweep = ref_client = plugin_row = plugin_row_native = None
     if rank == 0 and a.sweep:
         runner = WaveRunner(wave, fetch_timings, lt, n_pods, a.warmup + a.steps, extender_counters)
         try:
@@ -804,6 +829,10 @@ def main():
                 plugin_row = plugin_path(a, children, api_url, runner, E)
             except Exception as e:  # noqa: BLE001
                 plugin_row = {"error": f"{type(e).__name__}: {e}"}
+            try:
+                plugin_row_native = plugin_path_native_kubelet(a, children, api_url, runner, E)
+            except Exception as e:  # noqa: BLE001
+                plugin_row_native = {"error": f"{type(e).__name__}: {e}"}
     if world > 1:
         dist.barrier(group=ctl)  # every rank's runtime endpoint stays up until rank 0's sweep is done
 
@@ -862,6 +891,9 @@ def main():
                             for k, t in (("bound", "t_bound"), ("running", "t_run"), ("total", "t_total"))},
             "wave_ms_max": {k: round(1e3 * max(s[t] for s in step_stats), 3)
                             for k, t in (("bound", "t_bound"), ("running", "t_run"), ("total", "t_total"))},
+            # every timed wave: [bound, running, total] ms (where a slow wave lost its time)
+            "wave_ms_each": [[round(1e3 * s["t_bound"], 3), round(1e3 * s["t_run"], 3), round(1e3 * s["t_total"], 3)]
+                             for s in step_stats] if len(step_stats) <= 400 else None,
             # per-wave throughput distribution: p50 and IQR next to `value` (one number from ~20 short waves is
             # sensitive to single slow waves)
             "wave_pods_per_s": wave_dist([n_pods / s["t_total"] for s in step_stats]),
@@ -876,6 +908,7 @@ def main():
             "reference_client": ref_client,
             # the shipped gRPC device plugin on the kubelet path (untimed by the headline, same waves)
             "device_plugin_path": plugin_row,
+            "device_plugin_path_native_kubelet": plugin_row_native,
             "bind_retries": sum(sum(s["attempts"]) - len(s["attempts"]) for s in step_stats),
             "agents": agent_stats,
             "node_agent": node_agent_stats,

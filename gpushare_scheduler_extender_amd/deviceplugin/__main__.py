@@ -38,6 +38,8 @@ def main(argv=None) -> int:
                     help="serve /healthz, /metrics and /debug/state on this port (0: off)")
     ap.add_argument("--debug-host", default=env.get("GSX_DEBUG_HOST", "127.0.0.1"))
     ap.add_argument("--debug-port-file", default="", help="write the debug port here once it listens (port 0)")
+    ap.add_argument("--no-register", action="store_true",
+                    help="do not register with kubelet (a stand-in that connects to the endpoint directly)")
     ap.add_argument("--no-publish", action="store_true",
                     help="do not publish the node's capacity / device inventory (a harness already did)")
     ap.add_argument("--isolation", default=env.get("GSX_ISOLATION", "enforce"), choices=["enforce", "advisory"],
@@ -68,7 +70,7 @@ def main(argv=None) -> int:
                                 health_interval=a.health_interval, reserve_bytes=int(a.reserve_gib * (1 << 30)),
                                 podresources_socket=a.podresources_socket or None,
                                 reconcile_interval=a.reconcile_interval, isolation=iso)
-        await plugin.start(publish=not a.no_publish)
+        await plugin.start(publish=not a.no_publish, register=not a.no_register)
         if a.debug_port or a.debug_port_file:
             port = await plugin.serve_debug(a.debug_host, a.debug_port)
             if a.debug_port_file:
@@ -81,6 +83,10 @@ def main(argv=None) -> int:
         for s in (signal.SIGINT, signal.SIGTERM):
             loop.add_signal_handler(s, stop.set)
         await stop.wait()
+        n = max(1, plugin.timing["n"])
+        logging.getLogger("gsx.main").warning(
+            "stopping: %s; grpc %s; per Allocate ms: %s", plugin.stats, plugin.debug_state().get("grpc"),
+            {k: round(1e3 * v / n, 4) for k, v in plugin.timing.items() if isinstance(v, float)})
         await plugin.stop()
         await client.close()
 

@@ -29,9 +29,9 @@ from __future__ import annotations
 import time
 from dataclasses import dataclass, field
 
+from ..core.engine import native as _native
 from ..models import pod as podutil
-from ..models.profile import (POD_ASSIGN_TIME_ANNOTATION, POD_CU_COUNT_ANNOTATION, POD_CU_MASK_ANNOTATION,
-                              NamingProfile)
+from ..models.profile import POD_ASSIGN_TIME_ANNOTATION, POD_CU_COUNT_ANNOTATION, NamingProfile
 from .devices import Device
 
 CU_COUNT_ANNOTATION = POD_CU_COUNT_ANNOTATION  # pod asks for a CU partition of this size
@@ -112,33 +112,23 @@ class CUPartitioner:
 
 def build_response(pod: dict, device: Device, container_units: int, profile: NamingProfile, *,
                    mount_mode: str = "isolated", cus: list[int] | None = None) -> ContainerAllocation:
-    """Env + device nodes for one container of ``pod`` on ``device``."""
-    idx = device.index
-    dev_total = int(podutil.annotations(pod).get(profile.annotation_dev, "0") or 0)
-    pod_mem = podutil.gpu_mem_request(pod, profile)
-    visible = "0" if mount_mode == "isolated" else str(idx)
-    frac = (container_units / dev_total) if dev_total else 0.0
-    if device.share_bytes and device.total_bytes > device.share_bytes:
-        # a partition that shares its HBM pool sees the whole pool as device memory: scale to the pool
-        frac *= device.share_bytes / device.total_bytes
-    envs = {
-        "HIP_VISIBLE_DEVICES": visible,
-        "ROCR_VISIBLE_DEVICES": visible,
-        profile.annotation_idx: str(idx),
-        profile.annotation_dev: str(dev_total),
-        profile.annotation_pod: str(pod_mem),
-        profile.env_container: str(container_units),
-        "GSX_GPU_MEM_FRACTION": f"{frac:.6f}",
-        "GSX_GPU_BDF": device.bdf,
-    }
-    ann = {}
-    if cus:
-        envs["GSX_CU_MASK"] = ",".join(f"0x{w:08x}" for w in CUPartitioner.words(cus, device.cu_count))
-        envs["HSA_CU_MASK"] = f"{visible}:{CUPartitioner.ranges(cus)}"
-        ann[POD_CU_MASK_ANNOTATION] = envs["GSX_CU_MASK"]
-    nodes = device.device_nodes() if mount_mode == "isolated" else []
-    devs = [{"container_path": p, "host_path": p, "permissions": "rw"} for p in nodes]
-    return ContainerAllocation(envs=envs, devices=devs, annotations=ann)
+    """Env + device nodes for one container of ``pod`` on ``device``: the reference's env contract
+    (``*_IDX``, ``*_DEV``, ``*_POD``, the container's share), ``HIP/ROCR_VISIBLE_DEVICES``, the memory fraction
+    (scaled to the HBM pool of a partition that shares one), the CU partition (``GSX_CU_MASK`` bitmap words,
+    ``HSA_CU_MASK`` ranges, the ``cu-mask`` pod annotation) and, in ``isolated`` mount mode, the GPU's device
+    nodes.  One implementation: ``native/engine/dpcore.cc`` build_response, which the native Allocate path uses."""
+    E = _native()
+    ap = E.AllocPod()
+    try:
+        ap.dev_total = int(podutil.annotations(pod).get(profile.annotation_dev, "0") or 0)
+    except ValueError:
+        ap.dev_total = 0
+    ap.request = podutil.gpu_mem_request(pod, profile)
+    dev = {"index": device.index, "bdf": device.bdf, "cu_count": device.cu_count, "total_bytes": device.total_bytes,
+           "share_bytes": device.share_bytes, "nodes": device.device_nodes()}
+    r = E.build_response(ap, dev, int(container_units), list(cus or []), mount_mode,
+                         {**profile.engine_dict(), "env_container": profile.env_container})
+    return ContainerAllocation(envs=dict(r["envs"]), devices=list(r["devices"]), annotations=dict(r["annotations"]))
 
 
 def assigned_patch(pod: dict, profile: NamingProfile, extra: dict | None = None) -> dict:

@@ -31,7 +31,7 @@ import os
 import shutil
 from pathlib import Path
 
-from .allocator import CUPartitioner
+from ..core.engine import native
 
 log = logging.getLogger("gsx.deviceplugin.isolation")
 
@@ -48,13 +48,9 @@ def shipped_library() -> Path:
 
 
 def config_text(cus: list[int] | None, cu_count: int, limit_bytes: int) -> str:
-    lines = ["# written by the gpushare device plugin; read by libgsx_isolate.so"]
-    if cus:
-        lines.append("cu_mask=" + ",".join(f"0x{w:08x}" for w in CUPartitioner.words(cus, cu_count)))
-    if limit_bytes > 0:
-        lines.append(f"hbm_limit_bytes={int(limit_bytes)}")
-    lines.append(f"ledger={CONTAINER_DIR}/{LEDGER}")
-    return "\n".join(lines) + "\n"
+    """The library's config file (one implementation: ``native/engine/dpcore.cc``, shared with the native
+    Allocate path)."""
+    return native().isolation_config_text(list(cus or []), cu_count, int(limit_bytes))
 
 
 class IsolationManager:
@@ -67,7 +63,7 @@ class IsolationManager:
         self.stats = {"prepared": 0, "released": 0}
         self._installed = False
 
-    def _install(self):
+    def install(self):
         """The library and the preload list, once per host directory (kubelet's runtime mounts them from here)."""
         if self._installed:
             return
@@ -89,30 +85,19 @@ class IsolationManager:
                 host_process: bool = False) -> tuple[list[dict], dict[str, str]]:
         """Write the pod's files (idempotent: every container of a pod shares them) and return
         (Allocate ``mounts``, Allocate ``envs``)."""
-        self._install()
-        d = self.pod_dir(uid)
-        d.mkdir(parents=True, exist_ok=True)
-        conf = config_text(cus, cu_count, limit_bytes)
-        if host_process:  # no mount namespace: the ledger is named by its host path
-            conf = conf.replace(f"ledger={CONTAINER_DIR}/{LEDGER}", f"ledger={d / LEDGER}")
-        _write_atomic(d / CONF, conf, 0o444)
-        ledger = d / LEDGER
-        if not ledger.exists():
-            fd = os.open(ledger, os.O_CREAT | os.O_RDWR, 0o666)
-            os.close(fd)
-            os.chmod(ledger, 0o666)  # the container's user is not ours
+        self.install()
+        try:  # one implementation (native/engine/dpcore.cc isolation_prepare), shared with the native Allocate path
+            mounts, envs = native().isolation_prepare(str(self.host_dir), uid, list(cus or []), cu_count,
+                                                      int(limit_bytes), host_process)
+        except RuntimeError as e:
+            raise OSError(str(e)) from e
+        self.note_prepared(uid)
+        return list(mounts), dict(envs)
+
+    def note_prepared(self, uid: str) -> None:
         if uid not in self.prepared:
             self.prepared.add(uid)
             self.stats["prepared"] += 1
-        if host_process:
-            return [], {"HSA_TOOLS_LIB": str(self.host_dir / LIB), "GSX_ISOLATION_CONFIG": str(d / CONF)}
-        mounts = [
-            {"container_path": f"{CONTAINER_DIR}/{CONF}", "host_path": str(d / CONF), "read_only": True},
-            {"container_path": f"{CONTAINER_DIR}/{LEDGER}", "host_path": str(ledger), "read_only": False},
-            {"container_path": f"{CONTAINER_DIR}/{LIB}", "host_path": str(self.host_dir / LIB), "read_only": True},
-            {"container_path": "/etc/ld.so.preload", "host_path": str(self.host_dir / PRELOAD), "read_only": True},
-        ]
-        return mounts, {"HSA_TOOLS_LIB": f"{CONTAINER_DIR}/{LIB}"}
 
     def release(self, uid: str) -> None:
         if not uid:

@@ -63,8 +63,34 @@ def fake_ids(dev: Device, units: int) -> list[str]:
 
 
 ALLOCATE_ATTEMPTS = 8  # per container request: transient apiserver failures retried with capped backoff
+INFORMER_WAIT_S = 0.02  # how long an Allocate waits for the pod event before LISTing
 GUARD_WAIT_S = 5.0  # how long an Allocate waits for a physically full GPU to drain a stopping container
 POD_ANNOTATION = "gpushare.amd.com/pod"  # container annotation: the pod this Allocate was matched to
+
+
+class _Aborted(Exception):
+    def __init__(self, code: int, details: str):
+        super().__init__(details)
+        self.code, self.details = code, details
+
+
+class _NativeContext:
+    """The slice of grpc.aio.ServicerContext the handlers use, for calls the native endpoint hands over."""
+
+    async def abort(self, code, details=""):
+        raise _Aborted(code.value[0] if isinstance(code, grpc.StatusCode) else int(code), details)
+
+
+def native_grpc_available() -> tuple[bool, str]:
+    """The native endpoint needs the engine module and the system's libnghttp2."""
+    if os.environ.get("GSX_PLUGIN_GRPC", "native") == "grpcio":
+        return False, "GSX_PLUGIN_GRPC=grpcio"
+    try:
+        from ..core.engine import native  # noqa: PLC0415
+
+        return tuple(native().h2_available())
+    except (ImportError, AttributeError) as e:
+        return False, repr(e)
 
 class GpuSharePlugin:
     def __init__(self, client: KubeClient, node: str, devices: list[Device], profile: NamingProfile, *,
@@ -103,18 +129,43 @@ class GpuSharePlugin:
         # a kubelet stand-in in the same process may share its pod informer (one watch per node)
         self._own_informer = informer is None
         self.pods = informer or Informer(client, "pods", field_selector=f"spec.nodeName={node}")
-        self.pods.add_handler(Handler(lambda o, raw: self.state.observe(o),
-                                      lambda old, new, raw: self.state.observe(new),
+        self._observed = asyncio.Event()  # set by every pod event: an Allocate waiting for its pod to arrive
+        self.pods.add_handler(Handler(lambda o, raw: self._observe(o),
+                                      lambda old, new, raw: self._observe(new),
                                       lambda o, raw: self.state.forget(o)))
         self._changed = asyncio.Event()
         self._version = 0
         self._stopped = False
         self._server: grpc.aio.Server | None = None
+        self._native = None  # _engine.DpServer: the gRPC endpoint in native code (default)
+        self.grpc_impl = ""
+        self._slow: set[asyncio.Task] = set()
         self._tasks: list[asyncio.Task] = []
         self.allocations = 0
         self.stats = {"allocate_ok": 0, "allocate_fail": 0, "allocate_retries": 0, "preferred": 0,
                       "registrations": 0, "refreshes": 0}
         self._debug = None
+
+    def _observe(self, pod: dict):
+        self.state.observe(pod)
+        self._observed.set()
+
+    async def _await_informer(self, found, timeout: float = INFORMER_WAIT_S):
+        """kubelet can call before this plugin's watch has delivered the pod it is admitting (they are separate
+        processes with separate watches).  Waiting a few ms for the event is far cheaper than a full LIST."""
+        deadline = time.monotonic() + timeout
+        while True:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                return found()
+            self._observed.clear()
+            try:
+                await asyncio.wait_for(self._observed.wait(), left)
+            except asyncio.TimeoutError:
+                return found()
+            got = found()
+            if got:
+                return got
 
     def _set_devices(self, devices: list[Device]):
         """(Re)build everything derived from the device layout: fake IDs per GPU and the allocation state."""
@@ -125,6 +176,10 @@ class GpuSharePlugin:
         self.state = AllocationState(self.node, self.devices, self.profile)
         self.state.on_drop.append(self._record_dropped)
         self.health_info: dict[int, dict] = {}
+        native = getattr(self, "_native", None)
+        if native is not None:
+            native.set_state(self.state.core)
+            self._sync_native()
 
     async def reload_devices(self, devices: list[Device] | None = None):
         """The node's GPUs were re-partitioned at run time (amd-smi set --compute-partition / --memory-partition):
@@ -143,8 +198,7 @@ class GpuSharePlugin:
         self.stats["layout_changes"] = self.stats.get("layout_changes", 0) + 1
         log.warning("device layout changed: %s -> %s", old,
                     sorted((d.index, d.partition, d.memory_partition) for d in devices))
-        self._version += 1
-        self._changed.set()
+        self._devices_changed()
         try:
             await self.publish_node()
         except ApiError as e:
@@ -179,8 +233,92 @@ class GpuSharePlugin:
             return
         d.healthy = healthy
         log.warning("GPU %d (%s) is now %s %s", index, d.bdf, "Healthy" if healthy else "Unhealthy", why)
+        self._devices_changed()
+
+    def _devices_changed(self):
+        """ListAndWatch streams (grpcio and native) send the new device list."""
         self._version += 1
         self._changed.set()
+        self._sync_native()
+
+    # ------------------------------------------------------------ native gRPC endpoint
+    def _native_config(self) -> dict:
+        from ..core.controller import api_dict  # noqa: PLC0415
+
+        return {"node": self.node, "profile": {**self.profile.engine_dict(), "env_container": self.profile.env_container},
+                "mount_mode": self.mount_mode, "unit_bytes": UNITS[self.unit],
+                "iso_dir": str(self.isolation.host_dir) if self.isolation is not None else None,
+                "guard": self.reconciler is not None, "api": api_dict(self.client.config),
+                "fast": os.environ.get("GSX_PLUGIN_FAST", "1") == "1"}
+
+    def native_device(self, d: Device) -> dict:
+        return {"index": d.index, "bdf": d.bdf, "cu_count": d.cu_count, "total_bytes": d.total_bytes,
+                "share_bytes": d.share_bytes, "units": self.units.get(d.index, 0), "nodes": d.device_nodes(),
+                "healthy": d.healthy}
+
+    def _sync_native(self):
+        if self._native is None:
+            return
+        self._native.set_devices([self.native_device(d) for d in self.devices.values()], self.id_owner)
+        self._native.set_device_list(api.ListAndWatchResponse(devices=self.device_list()).SerializeToString())
+
+    def _native_poll(self):
+        srv = self._native
+        if srv is None:
+            return
+        pending, events = srv.poll()
+        for ev in events:
+            self._fast_allocated(ev)
+        if pending:
+            loop = asyncio.get_running_loop()
+            for cid, method, payload in pending:
+                t = loop.create_task(self._native_slow(srv, cid, method, payload))
+                self._slow.add(t)
+                t.add_done_callback(self._slow.discard)
+
+    def _fast_allocated(self, ev: dict):
+        """A native fast-path Allocate: what the Python handler would have done after it."""
+        import json  # noqa: PLC0415
+
+        if ev["pod_json"]:
+            self.state.observe(json.loads(ev["pod_json"]))  # the committed pod, before its watch event arrives
+        if ev["iso"] and self.isolation is not None:
+            self.isolation.note_prepared(ev["iso"])
+        self.stats["allocate_ok"] += 1
+        self.stats["allocate_native"] = self.stats.get("allocate_native", 0) + 1
+        t = self.timing
+        t["n"] += 1
+        t["handler"] += ev["t_handler"]
+        t["match"] += ev["t_match"]
+        t["assign_patch"] += ev["t_patch"]
+        t["isolate"] += ev["t_isolate"]
+        self.persist_records()
+        if self.reconciler is not None:
+            self.reconciler.kick()
+
+    async def _native_slow(self, srv, cid: int, method: str, payload: bytes):
+        """A call the native fast path left to Python: the same handler grpcio would run."""
+        try:
+            if method == "Allocate":
+                resp = await self.Allocate(api.AllocateRequest.FromString(payload), _NativeContext())
+            else:
+                resp = await self.GetPreferredAllocation(api.PreferredAllocationRequest.FromString(payload),
+                                                         _NativeContext())
+            srv.respond(cid, 0, resp.SerializeToString())
+        except _Aborted as e:
+            srv.respond(cid, e.code, e.details.encode())
+        except Exception as e:  # noqa: BLE001 - kubelet gets an error, the plugin lives on
+            log.exception("native %s slow path", method)
+            srv.respond(cid, grpc.StatusCode.INTERNAL.value[0], repr(e).encode())
+
+    def _close_native(self):
+        if self._native is not None:
+            try:
+                asyncio.get_running_loop().remove_reader(self._native.fd())
+            except RuntimeError:
+                pass
+            self._native.close()
+            self._native = None
 
     # ------------------------------------------------------------ gRPC handlers
     async def GetDevicePluginOptions(self, request, context):
@@ -212,6 +350,8 @@ class GpuSharePlugin:
         for creq in request.container_requests:
             size = creq.allocation_size
             want_dev = self.state.preferred_device(size)
+            if want_dev < 0 and await self._await_informer(lambda: self.state.preferred_device(size) >= 0):
+                want_dev = self.state.preferred_device(size)
             if want_dev < 0:
                 try:
                     await self.refresh()
@@ -307,6 +447,9 @@ class GpuSharePlugin:
             tm = time.perf_counter()
             rec, whole = self.state.match(units)
             self.timing["match"] += time.perf_counter() - tm
+            if rec is None and not refreshed:
+                m = await self._await_informer(lambda: self.state.match(units)[0] is not None)
+                rec, whole = self.state.match(units) if m else (None, False)
             if rec is None and not refreshed:
                 await self.refresh()
                 refreshed = True
@@ -547,11 +690,28 @@ class GpuSharePlugin:
         if self._server is not None:  # re-serving after a kubelet restart: retire the old server first
             await self._server.stop(0)
             self._server = None
+        self._close_native()
         os.makedirs(self.socket_dir, exist_ok=True)
         try:
             os.unlink(self.socket_path)
         except FileNotFoundError:
             pass
+        ok, why = native_grpc_available()
+        if ok:
+            from ..core.engine import native  # noqa: PLC0415
+
+            if self.isolation is not None:
+                self.isolation.install()  # the fast path writes per-pod files next to the installed library
+            cfg = self._native_config()
+            self._native = native().DpServer(self.socket_path, self.state.core, cfg)
+            if os.environ.get("GSX_PLUGIN_FEED", "1") == "1":
+                self._native.start_feed(cfg["api"])  # this node's pods into the state from a native reflector
+            self._sync_native()
+            asyncio.get_running_loop().add_reader(self._native.fd(), self._native_poll)
+            self.grpc_impl = "native"
+            return
+        log.info("device-plugin endpoint on grpcio (%s)", why)
+        self.grpc_impl = "grpcio"
         self._server = grpc.aio.server()
         self._server.add_generic_rpc_handlers((self._handlers(),))
         self._server.add_insecure_port(f"unix://{self.socket_path}")
@@ -602,6 +762,7 @@ class GpuSharePlugin:
                              "rewatches": self.pods.rewatches, "events": self.pods.events},
                 "stats": dict(self.stats), "timing": dict(self.timing), **self.state.snapshot(),
                 "reconcile": dict(self.reconciler.stats) if self.reconciler is not None else None,
+                "grpc": {"impl": self.grpc_impl, **(self._native.stats() if self._native is not None else {})},
                 "isolation": dict(self.isolation.stats) if self.isolation is not None else None}
 
     def metrics_text(self) -> str:
@@ -776,6 +937,9 @@ class GpuSharePlugin:
             self._debug = None
         if self._server is not None:
             await self._server.stop(0.5)
+        self._close_native()
+        for t in list(self._slow):
+            t.cancel()
         try:
             os.unlink(self.socket_path)
         except FileNotFoundError:

@@ -179,6 +179,10 @@ class AllocationState:
         ap.dev, ap.request, ap.containers, ap.assume_time = rec.dev, rec.request, rec.containers, rec.assume_time
         ap.assigned, ap.complete, ap.cu_count, ap.cu_mask = rec.assigned, rec.complete, rec.cu_count, rec.cu_mask
         ap.hold_idx, ap.hold_partner = rec.hold_idx, rec.hold_partner
+        try:
+            ap.dev_total = int(podutil.annotations(pod).get(self.profile.annotation_dev, "-1") or -1)
+        except ValueError:
+            ap.dev_total = -1
         if not self.core.observe(ap):
             return  # a stale copy (e.g. a slow LIST racing the watch): never step back
         if self.core.has_pod(rec.uid):

@@ -146,7 +146,8 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
                      extra: list[str] | None = None) -> ChildProc:
     """kubelet + device-plugin Allocate + runtime stand-in for ``node``.
 
-    ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent, its own Allocate matching);
+    ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent, the plugin's native matcher in-process, or
+    with ``plugin="spawn"`` the shipped plugin as its child process, called over the device-plugin gRPC API);
     otherwise ``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``: a kubelet stand-in driving
     the shipped device plugin, over its unix socket (``plugin="grpc"``) or in-process (``"inproc"``).
     """
@@ -154,8 +155,9 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
         exe = tool_path("gsx-nodeagent")
         if not exe.exists():
             raise FileNotFoundError(f"{exe} missing; run `python native/build.py nodeagent`")
+        spawn = ["--plugin-spawn", sys.executable] if plugin == "spawn" else []
         return ChildProc([str(exe), "--node", node, "--apiserver", apiserver, "--profile", profile,
-                          "--workers", str(min(workers, 16))], "node-agent", cpus=cpus)
+                          "--workers", str(min(workers, 16)), *spawn], "node-agent", cpus=cpus)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
                       apiserver, "--profile", profile, "--workers", str(workers), "--plugin", plugin,
                       *(extra or [])], "node-agent", cpus=cpus)

@@ -5,9 +5,20 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <sys/eventfd.h>
+#include <sys/timerfd.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <condition_variable>
+#include <deque>
 #include <memory>
+#include <mutex>
+#include <thread>
 
 #include "allocstate.h"
+#include "dpcore.h"
+#include "h2.h"
 #include "introspect.h"
 #include "ledger.h"
 #include "quantity.h"
@@ -34,6 +45,7 @@ Profile profile_from(const py::dict& d) {
   get("annotation_assigned", &p.a_assigned);
   get("annotation_assume_time", &p.a_assume);
   get("annotation_node_devices", &p.a_node_devs);
+  get("env_container", &p.env_container);
   return p;
 }
 
@@ -656,6 +668,431 @@ class PyPodRuntime {
 
 }  // namespace
 
+// ---------------------------------------------------------------- device plugin: native gRPC server
+py::dict container_response_dict(const dp::ContainerResponse& r) {
+  py::dict d;
+  d["envs"] = r.envs;
+  d["annotations"] = r.annotations;
+  py::list mounts, devices;
+  for (const auto& m : r.mounts) {
+    py::dict e;
+    e["container_path"] = m.container_path;
+    e["host_path"] = m.host_path;
+    e["read_only"] = m.read_only;
+    mounts.append(e);
+  }
+  for (const auto& x : r.devices) {
+    py::dict e;
+    e["container_path"] = x.container_path;
+    e["host_path"] = x.host_path;
+    e["permissions"] = x.permissions;
+    devices.append(e);
+  }
+  d["mounts"] = mounts;
+  d["devices"] = devices;
+  return d;
+}
+
+DpDevice dp_device_from(const py::dict& d) {
+  DpDevice x;
+  x.index = d["index"].cast<int>();
+  if (d.contains("bdf")) x.bdf = d["bdf"].cast<std::string>();
+  if (d.contains("cu_count")) x.cu_count = d["cu_count"].cast<int>();
+  if (d.contains("total_bytes")) x.total_bytes = d["total_bytes"].cast<int64_t>();
+  if (d.contains("share_bytes")) x.share_bytes = d["share_bytes"].cast<int64_t>();
+  if (d.contains("units")) x.units = d["units"].cast<int64_t>();
+  if (d.contains("nodes")) x.nodes = d["nodes"].cast<std::vector<std::string>>();
+  if (d.contains("healthy")) x.healthy = d["healthy"].cast<bool>();
+  return x;
+}
+
+// The plugin's gRPC endpoint in native code, driven by the plugin's asyncio loop (add_reader(fd, poll)).
+// GetDevicePluginOptions / ListAndWatch / PreStartContainer are answered here; GetPreferredAllocation and
+// Allocate take DpCore's fast path and otherwise come back from poll() as pending calls for the Python handlers,
+// answered with respond().
+class PyDpServer {
+ public:
+  static constexpr const char* kSvc = "/v1beta1.DevicePlugin/";
+  PyDpServer(const std::string& socket, AllocState& state, const py::dict& cfg) {
+    DpConfig c;
+    c.node = cfg["node"].cast<std::string>();
+    c.profile = profile_from(cfg["profile"].cast<py::dict>());
+    if (cfg.contains("mount_mode")) c.mount_mode = cfg["mount_mode"].cast<std::string>();
+    if (cfg.contains("unit_bytes")) c.unit_bytes = cfg["unit_bytes"].cast<int64_t>();
+    if (cfg.contains("iso_dir") && !cfg["iso_dir"].is_none()) c.iso_dir = cfg["iso_dir"].cast<std::string>();
+    if (cfg.contains("guard")) c.guard = cfg["guard"].cast<bool>();
+    if (cfg.contains("api") && !cfg["api"].is_none()) c.api = api_from(cfg["api"].cast<py::dict>());
+    if (cfg.contains("fast")) fast_ = cfg["fast"].cast<bool>();
+    node_ = c.node;
+    profile_ = c.profile;
+    state_ = &state;
+    core_ = std::make_unique<DpCore>(std::move(c), &state);
+    srv_ = std::make_unique<h2::Server>(socket, [this](h2::Server& s, const h2::Call& call) { on_call(s, call); });
+    if (!srv_->ok()) throw std::runtime_error(srv_->init_error());
+    efd_ = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    srv_->watch_fd(efd_);
+    tfd_ = ::timerfd_create(CLOCK_MONOTONIC, TFD_NONBLOCK | TFD_CLOEXEC);
+    srv_->watch_fd(tfd_);
+    worker_ = std::thread([this] { work(); });
+  }
+  ~PyDpServer() {
+    if (feed_r_) feed_r_->stop();
+    stop_worker();
+    if (efd_ >= 0) ::close(efd_);
+    if (tfd_ >= 0) ::close(tfd_);
+  }
+
+  // This node's pods straight into the allocation state from a native reflector (the plugin's Python informer,
+  // slower to decode a burst of events, keeps its own views): an Allocate that kubelet sends right after the
+  // binding finds its pod without waiting for Python.  Events are applied on the owner's thread, in poll().
+  void start_feed(const py::dict& api) {
+    if (feed_r_) return;
+    ReflectorConfig rc;
+    rc.path = "/api/v1/pods";
+    rc.field_selector = "spec.nodeName=" + node_;
+    ReflectorHandler h;
+    h.on_list = [this](const ListView& lv) {
+      Feed f;
+      f.resync = true;
+      for (size_t k = 0; k < lv.size(); ++k) {
+        AllocPod ap;
+        if (parse_alloc_pod(lv.doc(k), lv.obj(k), profile_, &ap)) f.pods.push_back(std::move(ap));
+      }
+      push_feed(std::move(f));
+    };
+    h.on_event = [this](Ev ev, const json::Doc& d, uint32_t obj) {
+      Feed f;
+      AllocPod ap;
+      if (!parse_alloc_pod(d, obj, profile_, &ap)) return;
+      f.deleted = ev == Ev::Deleted;
+      f.pods.push_back(std::move(ap));
+      push_feed(std::move(f));
+    };
+    feed_r_ = std::make_unique<Reflector>(api_from(api), rc, h);
+    feed_r_->start();
+  }
+
+  int fd() const { return srv_ ? srv_->fd() : -1; }
+
+  py::tuple poll() {
+    drain_feed();
+    if (srv_) srv_->poll();
+    drain_feed();
+    retry_waiting(false);
+    finish_patches();
+    retry_waiting(true);
+    py::list pending, events;
+    for (auto& p : pending_) pending.append(py::make_tuple(std::get<0>(p), std::get<1>(p), py::bytes(std::get<2>(p))));
+    pending_.clear();
+    for (auto& e : events_) {
+      py::dict d;
+      d["uid"] = e.uid;
+      d["key"] = e.key;
+      d["aid"] = e.aid;
+      d["iso"] = e.iso;
+      d["committed"] = e.committed;
+      d["pod_json"] = py::bytes(e.pod_json);
+      d["t_handler"] = e.t_handler;
+      d["t_match"] = e.t_match;
+      d["t_patch"] = e.t_patch;
+      d["t_isolate"] = e.t_isolate;
+      events.append(d);
+    }
+    events_.clear();
+    return py::make_tuple(pending, events);
+  }
+
+  bool respond(uint64_t call, int status, const py::bytes& payload) {
+    return srv_ && srv_->respond(call, status, std::string(view_of(payload)));
+  }
+
+  void set_devices(const py::list& devs, const std::map<std::string, int>& id_owner) {
+    std::vector<DpDevice> v;
+    for (const auto& d : devs) v.push_back(dp_device_from(d.cast<py::dict>()));
+    core_->set_devices(std::move(v), id_owner);
+  }
+
+  // the encoded ListAndWatchResponse; every open ListAndWatch stream gets it
+  void set_device_list(const py::bytes& msg) {
+    device_list_ = std::string(view_of(msg));
+    have_list_ = true;
+    if (!srv_) return;
+    for (uint64_t id : srv_->open_streams(std::string(kSvc) + "ListAndWatch")) srv_->stream_send(id, device_list_);
+  }
+
+  void set_fast(bool on) { fast_ = on; }
+  void set_state(AllocState& state) {
+    core_->set_state(&state);
+    state_ = &state;
+  }
+
+  py::dict stats() const {
+    py::dict d;
+    const auto& s = core_->stats();
+    d["fast_allocate"] = s.fast_allocate;
+    d["fast_preferred"] = s.fast_preferred;
+    d["slow_allocate"] = s.slow_allocate;
+    d["slow_preferred"] = s.slow_preferred;
+    d["patch_failures"] = s.patch_failures;
+    d["calls"] = srv_ ? srv_->calls() : 0;
+    d["connections"] = srv_ ? srv_->connections() : 0;
+    d["fast"] = fast_;
+    d["last_slow_reason"] = last_why_;
+    d["waited"] = waited_;
+    d["feed_events"] = feed_events_;
+    d["feed"] = static_cast<bool>(feed_r_);
+    return d;
+  }
+
+  void close() {
+    if (feed_r_) feed_r_->stop();
+    stop_worker();
+    finish_patches();
+    if (srv_) {
+      for (uint64_t id : srv_->open_streams(std::string(kSvc) + "ListAndWatch")) srv_->stream_end(id, 0, "");
+      srv_->poll();
+    }
+    srv_.reset();
+  }
+
+ private:
+  void on_call(h2::Server& s, const h2::Call& call) {
+    const std::string svc = kSvc;
+    if (call.path.compare(0, svc.size(), svc) != 0) {
+      s.respond(call.id, 12, "unknown service " + call.path);
+      return;
+    }
+    std::string m = call.path.substr(svc.size());
+    std::string resp, why;
+    if (m == "GetDevicePluginOptions") {
+      s.respond(call.id, 0, dp::encode_options(false, true));
+    } else if (m == "PreStartContainer") {
+      s.respond(call.id, 0, std::string());
+    } else if (m == "ListAndWatch") {
+      if (have_list_) s.stream_send(call.id, device_list_);
+    } else if (m == "GetPreferredAllocation" && fast_ && core_->preferred(call.message, &resp, &why)) {
+      s.respond(call.id, 0, resp);
+    } else if (m == "GetPreferredAllocation" && fast_ && feed_r_ && why == kNoPodYet) {
+      wait_for_pod(call.id, m, call.message);
+    } else if (m == "Allocate" && fast_) {
+      DpEvent ev;
+      std::unique_ptr<DpPending> pend;
+      DpStep step = core_->allocate(call.message, &resp, &ev, &pend, &why);
+      if (step == DpStep::Answered) {
+        s.respond(call.id, 0, resp);
+        events_.push_back(std::move(ev));
+      } else if (step == DpStep::Pending) {
+        pend->call = call.id;
+        pend->request = call.message;
+        std::lock_guard<std::mutex> l(wmu_);
+        todo_.push_back(std::move(pend));
+        wcv_.notify_one();
+      } else if (feed_r_ && why == kNoCandidate) {
+        wait_for_pod(call.id, m, call.message);
+      } else {
+        last_why_ = why;
+        pending_.emplace_back(call.id, m, call.message);
+      }
+    } else if (m == "GetPreferredAllocation" || m == "Allocate") {
+      if (!why.empty()) last_why_ = why;
+      pending_.emplace_back(call.id, m, call.message);
+    } else {
+      s.respond(call.id, 12, "unknown method " + m);
+    }
+  }
+
+  static constexpr const char* kNoCandidate = "no candidate";
+  static constexpr const char* kNoPodYet = "no pending pod of that size known yet";
+  static constexpr double kWaitS = 0.02;  // how long a call waits for its pod's event before Python takes it
+
+  struct Feed {
+    bool resync = false, deleted = false;
+    std::vector<AllocPod> pods;
+  };
+  struct Waiting {
+    uint64_t call;
+    std::string method, message;
+    double deadline;
+  };
+
+  static double mono() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+  }
+
+  void push_feed(Feed f) {
+    {
+      std::lock_guard<std::mutex> l(fmu_);
+      feed_.push_back(std::move(f));
+    }
+    uint64_t one = 1;
+    (void)!::write(efd_, &one, sizeof one);
+  }
+
+  void drain_feed() {
+    std::vector<Feed> fs;
+    {
+      std::lock_guard<std::mutex> l(fmu_);
+      fs.swap(feed_);
+    }
+    for (auto& f : fs) {
+      feed_events_ += f.pods.size();
+      if (f.resync) {
+        std::unordered_set<std::string> live;
+        for (const auto& ap : f.pods) {
+          live.insert(ap.uid);
+          state_->observe(ap);
+        }
+        state_->resync(live);
+      } else if (f.deleted) {
+        for (const auto& ap : f.pods) state_->release(ap.uid);
+      } else {
+        for (const auto& ap : f.pods) state_->observe(ap);
+      }
+    }
+  }
+
+  void arm_timer() {
+    if (waiting_.empty()) return;
+    double first = waiting_.front().deadline;
+    for (const auto& w : waiting_) first = std::min(first, w.deadline);
+    double dt = std::max(0.0005, first - mono());
+    itimerspec its{};
+    its.it_value.tv_sec = static_cast<time_t>(dt);
+    its.it_value.tv_nsec = static_cast<long>((dt - static_cast<double>(its.it_value.tv_sec)) * 1e9);
+    ::timerfd_settime(tfd_, 0, &its, nullptr);
+  }
+
+  void wait_for_pod(uint64_t call, const std::string& method, const std::string& message) {
+    waiting_.push_back({call, method, message, mono() + kWaitS});
+    waited_++;
+    arm_timer();
+  }
+
+  // calls that found no pod yet: again through the fast path; past their deadline, to Python
+  void retry_waiting(bool expire) {
+    uint64_t n;
+    if (tfd_ >= 0) (void)!::read(tfd_, &n, sizeof n);
+    if (waiting_.empty() || !srv_) return;
+    std::vector<Waiting> still;
+    const double now = mono();
+    for (auto& w : waiting_) {
+      std::string resp, why;
+      if (w.method == "GetPreferredAllocation") {
+        if (core_->preferred(w.message, &resp, &why)) {
+          srv_->respond(w.call, 0, resp);
+          continue;
+        }
+      } else {
+        DpEvent ev;
+        std::unique_ptr<DpPending> pend;
+        DpStep step = core_->allocate(w.message, &resp, &ev, &pend, &why);
+        if (step == DpStep::Answered) {
+          srv_->respond(w.call, 0, resp);
+          events_.push_back(std::move(ev));
+          continue;
+        }
+        if (step == DpStep::Pending) {
+          pend->call = w.call;
+          pend->request = w.message;
+          std::lock_guard<std::mutex> l(wmu_);
+          todo_.push_back(std::move(pend));
+          wcv_.notify_one();
+          continue;
+        }
+        if (why != kNoCandidate) {
+          last_why_ = why;
+          pending_.emplace_back(w.call, w.method, w.message);
+          continue;
+        }
+      }
+      if (expire && now >= w.deadline) {
+        last_why_ = why;
+        pending_.emplace_back(w.call, w.method, w.message);
+      } else {
+        still.push_back(std::move(w));
+      }
+    }
+    waiting_.swap(still);
+    arm_timer();
+  }
+
+  // the ASSIGNED patches run here, never on the owner's event loop
+  void work() {
+    for (;;) {
+      std::unique_ptr<DpPending> p;
+      {
+        std::unique_lock<std::mutex> l(wmu_);
+        wcv_.wait(l, [&] { return stopping_ || !todo_.empty(); });
+        if (todo_.empty()) return;
+        p = std::move(todo_.front());
+        todo_.pop_front();
+      }
+      core_->run_patch(*p);
+      {
+        std::lock_guard<std::mutex> l(wmu_);
+        done_.push_back(std::move(p));
+      }
+      uint64_t one = 1;
+      (void)!::write(efd_, &one, sizeof one);
+    }
+  }
+
+  void stop_worker() {
+    if (!worker_.joinable()) return;
+    {
+      std::lock_guard<std::mutex> l(wmu_);
+      stopping_ = true;
+    }
+    wcv_.notify_all();
+    worker_.join();
+  }
+
+  void finish_patches() {
+    uint64_t n;
+    if (efd_ >= 0) (void)!::read(efd_, &n, sizeof n);
+    std::deque<std::unique_ptr<DpPending>> done;
+    {
+      std::lock_guard<std::mutex> l(wmu_);
+      done.swap(done_);
+    }
+    for (auto& p : done) {
+      std::string resp, why;
+      DpEvent ev;
+      if (core_->finish(*p, &resp, &ev, &why)) {
+        if (srv_) srv_->respond(p->call, 0, resp);
+        events_.push_back(std::move(ev));
+      } else {
+        last_why_ = why;
+        pending_.emplace_back(p->call, std::string("Allocate"), p->request);
+      }
+    }
+  }
+
+  std::string node_;
+  Profile profile_;
+  AllocState* state_ = nullptr;
+  std::unique_ptr<Reflector> feed_r_;
+  std::mutex fmu_;
+  std::vector<Feed> feed_;
+  std::vector<Waiting> waiting_;
+  uint64_t waited_ = 0, feed_events_ = 0;
+  int tfd_ = -1;
+  std::thread worker_;
+  std::mutex wmu_;
+  std::condition_variable wcv_;
+  std::deque<std::unique_ptr<DpPending>> todo_, done_;
+  bool stopping_ = false;
+  int efd_ = -1;
+  std::unique_ptr<DpCore> core_;
+  std::unique_ptr<h2::Server> srv_;
+  std::vector<std::tuple<uint64_t, std::string, std::string>> pending_;
+  std::vector<DpEvent> events_;
+  std::string device_list_, last_why_;
+  bool have_list_ = false, fast_ = true;
+};
+
 PYBIND11_MODULE(_engine, m) {
   m.def(
       "native_symbol", [](uint64_t pc) { return introspect::symbol_at(static_cast<uintptr_t>(pc)); },
@@ -984,5 +1421,73 @@ PYBIND11_MODULE(_engine, m) {
     std::string err;
     bool ok = d.parse(view_of(b), &err);
     return py::make_tuple(ok, err, static_cast<int64_t>(d.size()));
+  });
+
+  // ---- device plugin: native gRPC endpoint + the response / isolation code the Python plugin shares
+  m.def("h2_available", []() {
+    std::string err;
+    bool ok = h2::available(&err);
+    return py::make_tuple(ok, err);
+  });
+  m.def("build_response",
+        [](const AllocPod& pod, const py::dict& dev, int64_t units, const std::vector<int>& cus,
+           const std::string& mount_mode, const py::dict& profile) {
+          return container_response_dict(
+              build_response(pod, dp_device_from(dev), units, cus, mount_mode, profile_from(profile)));
+        });
+  m.def("isolation_config_text", &isolation_config_text);
+  m.def("isolation_prepare", [](const std::string& host_dir, const std::string& uid, const std::vector<int>& cus,
+                                int cu_count, int64_t limit, bool host_process) {
+    std::vector<dp::MountMsg> mounts;
+    std::map<std::string, std::string> envs;
+    std::string err;
+    if (!isolation_prepare(host_dir, uid, cus, cu_count, limit, host_process, &mounts, &envs, &err))
+      throw std::runtime_error(err);
+    py::list ml;
+    for (const auto& x : mounts) {
+      py::dict e;
+      e["container_path"] = x.container_path;
+      e["host_path"] = x.host_path;
+      e["read_only"] = x.read_only;
+      ml.append(e);
+    }
+    return py::make_tuple(ml, envs);
+  });
+  py::class_<PyDpServer>(m, "DpServer")
+      .def(py::init<const std::string&, AllocState&, const py::dict&>(), py::keep_alive<1, 3>())
+      .def("fd", &PyDpServer::fd)
+      .def("poll", &PyDpServer::poll)
+      .def("respond", &PyDpServer::respond)
+      .def("set_devices", &PyDpServer::set_devices)
+      .def("set_device_list", &PyDpServer::set_device_list)
+      .def("set_fast", &PyDpServer::set_fast)
+      .def("set_state", &PyDpServer::set_state, py::keep_alive<1, 2>())
+      .def("start_feed", &PyDpServer::start_feed)
+      .def("stats", &PyDpServer::stats)
+      .def("close", &PyDpServer::close);
+  py::class_<h2::Client>(m, "H2Client")
+      .def(py::init<const std::string&>())
+      .def("call", [](h2::Client& c, const std::string& path, const py::bytes& req, double timeout) {
+        std::string resp, err;
+        int status = 0;
+        bool ok;
+        std::string r(view_of(req));
+        {
+          py::gil_scoped_release nogil;
+          ok = c.call(path, r, &resp, &status, &err, timeout);
+        }
+        return py::make_tuple(ok ? 0 : status, py::bytes(ok ? resp : err));
+      }, py::arg("path"), py::arg("req"), py::arg("timeout") = 10.0);
+  // test client (the compiled kubelet stand-in uses h2::Client directly)
+  m.def("h2_call", [](const std::string& sock, const std::string& path, const py::bytes& req, double timeout) {
+    h2::Client c(sock);
+    std::string resp, err;
+    int status = 0;
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = c.call(path, std::string(view_of(req)), &resp, &status, &err, timeout);
+    }
+    return py::make_tuple(ok ? 0 : status, py::bytes(ok ? resp : err));
   });
 }

@@ -1,0 +1,374 @@
+#include "dpcore.h"
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <set>
+
+#include "json.h"
+
+namespace gsx {
+namespace {
+
+const char kCuMaskAnn[] = "gpushare.amd.com/cu-mask";
+const char kAssignTimeAnn[] = "gpushare.amd.com/assign-time";
+const char kPodAnn[] = "gpushare.amd.com/pod";  // container annotation: which pod the allocation was built for
+const char kContainerDir[] = "/run/gsx";
+
+double mono_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+double wall_s() {
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+int64_t wall_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+
+bool mkdirs(const std::string& path) {
+  std::string cur;
+  size_t i = 0;
+  while (i <= path.size()) {
+    size_t j = path.find('/', i);
+    if (j == std::string::npos) j = path.size();
+    cur = path.substr(0, j);
+    if (!cur.empty() && ::mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return false;
+    i = j + 1;
+  }
+  return true;
+}
+
+bool write_atomic(const std::string& path, const std::string& text, mode_t mode, std::string* err) {
+  std::string tmp = path + ".tmp";
+  ::chmod(tmp.c_str(), 0644);  // a previous attempt's read-only leftover
+  int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) {
+    *err = "open " + tmp + ": " + std::strerror(errno);
+    return false;
+  }
+  size_t off = 0;
+  while (off < text.size()) {
+    ssize_t n = ::write(fd, text.data() + off, text.size() - off);
+    if (n < 0 && errno == EINTR) continue;
+    if (n <= 0) {
+      *err = "write " + tmp + ": " + std::strerror(errno);
+      ::close(fd);
+      return false;
+    }
+    off += static_cast<size_t>(n);
+  }
+  ::close(fd);
+  if (::chmod(tmp.c_str(), mode) != 0 || ::rename(tmp.c_str(), path.c_str()) != 0) {
+    *err = "install " + path + ": " + std::strerror(errno);
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+dp::ContainerResponse build_response(const AllocPod& pod, const DpDevice& d, int64_t container_units,
+                                     const std::vector<int>& cus, const std::string& mount_mode, const Profile& p) {
+  // deviceplugin/allocator.py documents the contract; both call this
+  dp::ContainerResponse r;
+  const int64_t dev_total = pod.dev_total > 0 ? pod.dev_total : 0;
+  const bool isolated = mount_mode == "isolated";
+  const std::string visible = isolated ? "0" : std::to_string(d.index);
+  double frac = dev_total ? static_cast<double>(container_units) / static_cast<double>(dev_total) : 0.0;
+  if (d.share_bytes && d.total_bytes > d.share_bytes) {
+    // a partition that shares its HBM pool sees the whole pool as device memory: scale to the pool
+    frac *= static_cast<double>(d.share_bytes) / static_cast<double>(d.total_bytes);
+  }
+  char fbuf[32];
+  std::snprintf(fbuf, sizeof fbuf, "%.6f", frac);
+  r.envs["HIP_VISIBLE_DEVICES"] = visible;
+  r.envs["ROCR_VISIBLE_DEVICES"] = visible;
+  r.envs[p.a_idx] = std::to_string(d.index);
+  r.envs[p.a_dev] = std::to_string(dev_total);
+  r.envs[p.a_pod] = std::to_string(pod.request);
+  r.envs[p.env_container] = std::to_string(container_units);
+  r.envs["GSX_GPU_MEM_FRACTION"] = fbuf;
+  r.envs["GSX_GPU_BDF"] = d.bdf;
+  if (!cus.empty()) {
+    std::string words = cu_words(cus, d.cu_count);
+    r.envs["GSX_CU_MASK"] = words;
+    r.envs["HSA_CU_MASK"] = visible + ":" + cu_ranges(cus);
+    r.annotations[kCuMaskAnn] = words;
+  }
+  if (isolated) {
+    for (const auto& n : d.nodes) r.devices.push_back(dp::DeviceSpecMsg{n, n, "rw"});
+  }
+  return r;
+}
+
+std::string isolation_config_text(const std::vector<int>& cus, int cu_count, int64_t limit_bytes) {
+  std::string t = "# written by the gpushare device plugin; read by libgsx_isolate.so\n";
+  if (!cus.empty()) t += "cu_mask=" + cu_words(cus, cu_count) + "\n";
+  if (limit_bytes > 0) t += "hbm_limit_bytes=" + std::to_string(limit_bytes) + "\n";
+  t += std::string("ledger=") + kContainerDir + "/hbm.ledger\n";
+  return t;
+}
+
+bool isolation_prepare(const std::string& host_dir, const std::string& uid, const std::vector<int>& cus, int cu_count,
+                       int64_t limit_bytes, bool host_process, std::vector<dp::MountMsg>* mounts,
+                       std::map<std::string, std::string>* envs, std::string* err) {
+  if (uid.empty() || uid.find('/') != std::string::npos || uid == "." || uid == "..") {
+    *err = "bad pod uid for the isolation directory";
+    return false;
+  }
+  const std::string d = host_dir + "/pods/" + uid;
+  if (!mkdirs(d)) {
+    *err = "mkdir " + d + ": " + std::strerror(errno);
+    return false;
+  }
+  std::string conf = isolation_config_text(cus, cu_count, limit_bytes);
+  const std::string ledger = d + "/hbm.ledger";
+  if (host_process) {  // no mount namespace: the ledger is named by its host path
+    std::string from = std::string("ledger=") + kContainerDir + "/hbm.ledger";
+    size_t at = conf.find(from);
+    if (at != std::string::npos) conf.replace(at, from.size(), "ledger=" + ledger);
+  }
+  if (!write_atomic(d + "/isolation.conf", conf, 0444, err)) return false;
+  if (::access(ledger.c_str(), F_OK) != 0) {
+    int fd = ::open(ledger.c_str(), O_CREAT | O_RDWR | O_CLOEXEC, 0666);
+    if (fd < 0) {
+      *err = "create " + ledger + ": " + std::strerror(errno);
+      return false;
+    }
+    ::close(fd);
+    ::chmod(ledger.c_str(), 0666);  // the container's user is not ours
+  }
+  if (host_process) {
+    (*envs)["HSA_TOOLS_LIB"] = host_dir + "/libgsx_isolate.so";
+    (*envs)["GSX_ISOLATION_CONFIG"] = d + "/isolation.conf";
+    return true;
+  }
+  const std::string c = kContainerDir;
+  mounts->push_back(dp::MountMsg{c + "/isolation.conf", d + "/isolation.conf", true});
+  mounts->push_back(dp::MountMsg{c + "/hbm.ledger", ledger, false});
+  mounts->push_back(dp::MountMsg{c + "/libgsx_isolate.so", host_dir + "/libgsx_isolate.so", true});
+  mounts->push_back(dp::MountMsg{"/etc/ld.so.preload", host_dir + "/ld.so.preload", true});
+  (*envs)["HSA_TOOLS_LIB"] = c + "/libgsx_isolate.so";
+  return true;
+}
+
+DpCore::DpCore(DpConfig cfg, AllocState* state) : cfg_(std::move(cfg)), state_(state) {
+  if (!cfg_.api.server.empty()) api_ = std::make_unique<ApiClient>(cfg_.api);
+}
+
+void DpCore::set_devices(std::vector<DpDevice> devs, std::map<std::string, int> id_owner) {
+  devs_.clear();
+  for (auto& d : devs) devs_[d.index] = std::move(d);
+  id_owner_ = std::move(id_owner);
+}
+
+int64_t DpCore::physical_used(int dev) const {
+  int64_t n = 0;
+  for (const auto& kv : state_->records()) {
+    if (kv.second.dev == dev) n += kv.second.units;
+  }
+  return n;
+}
+
+bool DpCore::preferred(const std::string& req, std::string* resp, std::string* why) {
+  std::vector<dp::PreferredRequest> reqs;
+  if (!dp::decode_preferred_request(req, &reqs)) {
+    *why = "malformed request";
+    return false;
+  }
+  std::vector<std::vector<std::string>> out;
+  for (const auto& r : reqs) {
+    int64_t want = state_->preferred_device(r.size);
+    if (want < 0) {
+      stats_.slow_preferred++;
+      *why = "no pending pod of that size known yet";
+      return false;
+    }
+    std::vector<std::string> chosen(r.must_include);
+    std::set<std::string> taken(chosen.begin(), chosen.end());
+    std::vector<std::string> pref, rest;
+    for (const auto& id : r.available) {
+      if (taken.count(id)) continue;
+      auto o = id_owner_.find(id);
+      (o != id_owner_.end() && o->second == want ? pref : rest).push_back(id);
+    }
+    for (auto* v : {&pref, &rest}) {
+      for (const auto& id : *v) {
+        if (static_cast<int32_t>(chosen.size()) >= r.size) break;
+        chosen.push_back(id);
+      }
+    }
+    if (static_cast<int32_t>(chosen.size()) > r.size) chosen.resize(static_cast<size_t>(r.size));
+    out.push_back(std::move(chosen));
+  }
+  *resp = dp::encode_preferred_response(out);
+  stats_.fast_preferred++;
+  return true;
+}
+
+DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, std::unique_ptr<DpPending>* pend,
+                        std::string* why) {
+  const double t0 = mono_s();
+  std::vector<std::vector<std::string>> ids_per;
+  if (!dp::decode_allocate_request(req, &ids_per) || ids_per.size() != 1 || ids_per[0].empty()) {
+    stats_.slow_allocate++;
+    *why = "not a single-container request";
+    return DpStep::Slow;
+  }
+  const std::vector<std::string>& ids = ids_per[0];
+  const int64_t units = static_cast<int64_t>(ids.size());
+  auto m = state_->match(units);
+  const double tm = mono_s();
+  if (!m.first) {
+    stats_.slow_allocate++;
+    *why = "no candidate";
+    return DpStep::Slow;
+  }
+  const AllocPod pod = *m.first;  // a copy: observe() later replaces the state's
+  auto dit = devs_.find(static_cast<int>(pod.dev));
+  if (dit == devs_.end() || pod.hold_idx >= 0 || !pod.hold_partner.empty()) {
+    stats_.slow_allocate++;
+    *why = dit == devs_.end() ? "GPU not on this node" : "pod in a reconciliation exchange";
+    return DpStep::Slow;
+  }
+  const DpDevice& dev = dit->second;
+  const bool later = pod.assigned == "true";
+  if (!later && cfg_.guard && physical_used(dev.index) + units > dev.units) {
+    stats_.slow_allocate++;
+    *why = "GPU physically full by the records";
+    return DpStep::Slow;
+  }
+  if (!later && !api_) {
+    stats_.slow_allocate++;
+    *why = "no apiserver client";
+    return DpStep::Slow;
+  }
+  CuPartitioner* cp = state_->cus(dev.index);
+  const bool had_cus = cp && cp->holds(pod.uid);
+  if (!later) state_->set_inflight(pod.uid, true);
+  std::vector<int> cus;
+  std::string err;
+  auto undo = [&] {
+    if (!later) {
+      if (cp && !had_cus) cp->release(pod.uid);
+      state_->set_inflight(pod.uid, false);
+    }
+  };
+  if (!state_->claim_cus(pod.uid, &cus, &err)) {
+    undo();
+    stats_.slow_allocate++;
+    *why = "CU partition: " + err;
+    return DpStep::Slow;
+  }
+  auto p = std::make_unique<DpPending>();
+  p->pod = pod;
+  p->whole = m.second;
+  p->had_cus = had_cus;
+  p->units = units;
+  p->ids = ids;
+  p->cr = build_response(pod, dev, units, cus, cfg_.mount_mode, cfg_.profile);
+  p->t0 = t0;
+  p->tm = tm;
+  p->ti0 = mono_s();
+  if (!cfg_.iso_dir.empty()) {
+    if (!isolation_prepare(cfg_.iso_dir, pod.uid, cus, dev.cu_count, pod.request * cfg_.unit_bytes,
+                           cfg_.mount_mode == "all", &p->cr.mounts, &p->cr.envs, &err)) {
+      undo();
+      stats_.slow_allocate++;
+      *why = "isolation files: " + err;
+      return DpStep::Slow;
+    }
+    p->iso = pod.uid;
+  }
+  p->ti1 = p->tp0 = p->tp1 = mono_s();
+  p->cr.annotations[kPodAnn] = pod.key + "/" + pod.uid;
+  if (later) {
+    state_->later_container_allocated(pod.uid, units);
+    p->ok = true;
+    finish(*p, resp, ev, why);
+    return DpStep::Answered;
+  }
+  std::string patch = "{\"metadata\":{\"resourceVersion\":";
+  json::append_quoted(&patch, pod.rv);
+  patch.append(",\"annotations\":{");
+  json::append_quoted(&patch, cfg_.profile.a_assigned);
+  patch.append(":\"true\",");
+  json::append_quoted(&patch, kAssignTimeAnn);
+  patch.append(":\"").append(std::to_string(wall_ns())).append("\"");
+  auto cm = p->cr.annotations.find(kCuMaskAnn);
+  if (cm != p->cr.annotations.end()) {
+    patch.push_back(',');
+    json::append_quoted(&patch, kCuMaskAnn);
+    patch.push_back(':');
+    json::append_quoted(&patch, cm->second);
+  }
+  patch.append("}}}");
+  p->body = std::move(patch);
+  p->path = "/api/v1/namespaces/" + pod.ns + "/pods/" + pod.name;
+  *pend = std::move(p);
+  return DpStep::Pending;
+}
+
+void DpCore::run_patch(DpPending& p) {
+  p.tp0 = mono_s();
+  p.ok = api_->request("PATCH", p.path, p.body, "application/merge-patch+json", &p.status, &p.resp, &p.err);
+  p.tp1 = mono_s();
+}
+
+bool DpCore::finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* why) {
+  const bool later = p.path.empty();
+  if (!later) {
+    json::Doc d;
+    AllocPod committed;
+    std::string perr;
+    bool good = p.ok && p.status < 300 && d.parse(p.resp, &perr) && parse_alloc_pod(d, 0, cfg_.profile, &committed);
+    if (!good) {
+      CuPartitioner* cp = state_->cus(static_cast<int>(p.pod.dev));
+      if (cp && !p.had_cus) cp->release(p.pod.uid);
+      state_->set_inflight(p.pod.uid, false);
+      stats_.patch_failures++;
+      stats_.slow_allocate++;
+      *why = p.ok ? "ASSIGNED patch answered " + std::to_string(p.status) : "ASSIGNED patch: " + p.err;
+      return false;
+    }
+    state_->observe(committed);
+    state_->set_inflight(p.pod.uid, false);
+    state_->first_container_committed(p.pod.uid, p.units, p.whole);
+    ev->pod_json = std::move(p.resp);
+    ev->committed = true;
+  }
+  char aid[64];
+  std::snprintf(aid, sizeof aid, "%llx-%x-n%llu", static_cast<unsigned long long>(wall_ns() / 1000000),
+                static_cast<unsigned>(::getpid()), static_cast<unsigned long long>(++aid_));
+  auto cm = p.cr.annotations.find(kCuMaskAnn);
+  AllocRecord& rec = state_->record(p.pod.uid, p.ids, p.units,
+                                    cm != p.cr.annotations.end() ? cm->second : p.pod.cu_mask, aid, wall_s());
+  rec.iso = p.iso;
+  *resp = dp::encode_allocate_response({p.cr});
+  stats_.fast_allocate++;
+  ev->uid = p.pod.uid;
+  ev->key = p.pod.key;
+  ev->aid = aid;
+  ev->iso = p.iso;
+  const double t1 = mono_s();
+  ev->t_handler = t1 - p.t0;
+  ev->t_match = p.tm - p.t0;
+  ev->t_isolate = p.ti1 - p.ti0;
+  ev->t_patch = p.tp1 - p.tp0;
+  return true;
+}
+
+}  // namespace gsx

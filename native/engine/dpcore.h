@@ -1,0 +1,116 @@
+// The device plugin's Allocate path in native code, on the one matcher (allocstate.h) — used by the shipped
+// plugin's native gRPC server (bindings: _engine.DpServer) for the common case, with the Python plugin
+// (deviceplugin/plugin.py allocate_container) answering everything else, and by the Python code itself for the
+// pieces that must have one implementation: the container response (build_response, the reference's env
+// contract plus /dev nodes and the CU partition) and the enforced-isolation files (isolation_prepare).
+//
+// Fast path of one Allocate (one container request, as kubelet sends them): match the earliest-ASSUME_TIME
+// pending pod of that size; a later container of a committed pod is answered from the pod's state; a first
+// container commits ASSIGNED=true with a resourceVersion-guarded PATCH.  Anything unusual -- no candidate, an
+// unknown or physically full GPU (by the Allocate records), a pod in a reconciliation exchange, a failed PATCH --
+// returns false and the Python slow path (refresh, wait for annotations, reconcile, guard, retries) decides.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "allocstate.h"
+#include "apiclient.h"
+#include "dpproto.h"
+#include "model.h"
+
+namespace gsx {
+
+struct DpDevice {
+  int index = 0;
+  std::string bdf;
+  int cu_count = 256;
+  int64_t total_bytes = 0, share_bytes = 0;
+  int64_t units = 0;                // capacity in the advertised unit
+  std::vector<std::string> nodes;   // /dev/kfd, /dev/dri/renderD*, ... (mount mode "isolated")
+  bool healthy = true;
+};
+
+struct DpConfig {
+  std::string node;
+  Profile profile;
+  std::string mount_mode = "isolated";
+  int64_t unit_bytes = int64_t{1} << 30;
+  std::string iso_dir;  // enforced isolation host directory ("" = advisory)
+  bool guard = false;   // reconciliation on: refuse a first container on a GPU its records say is full
+  ApiConfig api;
+};
+
+// ---- the single implementations the Python plugin calls too
+dp::ContainerResponse build_response(const AllocPod& pod, const DpDevice& d, int64_t container_units,
+                                     const std::vector<int>& cus, const std::string& mount_mode, const Profile& p);
+std::string isolation_config_text(const std::vector<int>& cus, int cu_count, int64_t limit_bytes);
+// Writes <host_dir>/pods/<uid>/{isolation.conf,hbm.ledger}; fills the Allocate mounts / envs.
+bool isolation_prepare(const std::string& host_dir, const std::string& uid, const std::vector<int>& cus, int cu_count,
+                       int64_t limit_bytes, bool host_process, std::vector<dp::MountMsg>* mounts,
+                       std::map<std::string, std::string>* envs, std::string* err);
+
+struct DpEvent {  // what the Python side learns after a fast-path Allocate
+  std::string uid, key, aid, iso, pod_json;
+  bool committed = false;  // a first container (ASSIGNED patch) rather than a later one
+  double t_handler = 0, t_match = 0, t_patch = 0, t_isolate = 0;
+};
+
+// A first container waiting for its ASSIGNED patch.  The PATCH runs off the owner's thread (the plugin's event
+// loop must never block on the apiserver -- in tests the apiserver is served by that very loop); begin / finish
+// and every AllocState access stay on the owner's thread.
+struct DpPending {
+  uint64_t call = 0;
+  std::string request;  // the Allocate request, for the slow path if the PATCH fails
+  AllocPod pod;
+  bool whole = false, had_cus = false;
+  int64_t units = 0;
+  std::vector<std::string> ids;
+  dp::ContainerResponse cr;
+  std::string iso, path, body;
+  double t0 = 0, tm = 0, ti0 = 0, ti1 = 0, tp0 = 0, tp1 = 0;
+  // filled by the worker
+  bool ok = false;
+  int status = 0;
+  std::string resp, err;
+};
+
+enum class DpStep { Answered, Pending, Slow };
+
+class DpCore {
+ public:
+  DpCore(DpConfig cfg, AllocState* state);
+  void set_devices(std::vector<DpDevice> devs, std::map<std::string, int> id_owner);
+  void set_state(AllocState* state) { state_ = state; }  // the device layout changed: a rebuilt state
+  const std::map<int, DpDevice>& devices() const { return devs_; }
+
+  // true: answered (*resp = the response message); false: the slow path answers (*why says why)
+  bool preferred(const std::string& req, std::string* resp, std::string* why);
+  // Answered: *resp / *ev set.  Pending: *pend holds the PATCH to run (then finish()).  Slow: Python answers.
+  DpStep allocate(const std::string& req, std::string* resp, DpEvent* ev, std::unique_ptr<DpPending>* pend,
+                  std::string* why);
+  // after the PATCH: true = answered (*resp / *ev); false = undone, the slow path answers
+  bool finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* why);
+  // the worker's half: the blocking apiserver call
+  void run_patch(DpPending& p);
+
+  struct Stats {
+    uint64_t fast_allocate = 0, fast_preferred = 0, slow_allocate = 0, slow_preferred = 0, patch_failures = 0;
+  };
+  const Stats& stats() const { return stats_; }
+  int64_t physical_used(int dev) const;
+
+ private:
+  DpConfig cfg_;
+  AllocState* state_;
+  std::unique_ptr<ApiClient> api_;
+  std::map<int, DpDevice> devs_;
+  std::map<std::string, int> id_owner_;
+  uint64_t aid_ = 0;
+  Stats stats_;
+};
+
+}  // namespace gsx

@@ -1,0 +1,275 @@
+#include "dpproto.h"
+
+namespace gsx::dp {
+namespace {
+
+// ------------------------------------------------------------------ writer
+void varint(std::string* o, uint64_t v) {
+  while (v >= 0x80) {
+    o->push_back(static_cast<char>((v & 0x7f) | 0x80));
+    v >>= 7;
+  }
+  o->push_back(static_cast<char>(v));
+}
+void tag(std::string* o, int field, int wire) { varint(o, (static_cast<uint64_t>(field) << 3) | wire); }
+void bytes(std::string* o, int field, const std::string& s) {
+  tag(o, field, 2);
+  varint(o, s.size());
+  o->append(s);
+}
+void str_if(std::string* o, int field, const std::string& s) {
+  if (!s.empty()) bytes(o, field, s);
+}
+void boolean(std::string* o, int field, bool b) {
+  if (!b) return;
+  tag(o, field, 0);
+  varint(o, 1);
+}
+void int_field(std::string* o, int field, int64_t v) {
+  if (v == 0) return;
+  tag(o, field, 0);
+  varint(o, static_cast<uint64_t>(v));
+}
+std::string map_entry(const std::string& k, const std::string& v) {
+  std::string e;
+  str_if(&e, 1, k);
+  str_if(&e, 2, v);
+  return e;
+}
+
+// ------------------------------------------------------------------ reader
+struct Reader {
+  const uint8_t* p;
+  const uint8_t* end;
+  explicit Reader(const std::string& s)
+      : p(reinterpret_cast<const uint8_t*>(s.data())), end(reinterpret_cast<const uint8_t*>(s.data()) + s.size()) {}
+  bool done() const { return p >= end; }
+  bool varint(uint64_t* v) {
+    *v = 0;
+    for (int shift = 0; shift < 64 && p < end; shift += 7) {
+      uint8_t b = *p++;
+      *v |= static_cast<uint64_t>(b & 0x7f) << shift;
+      if (!(b & 0x80)) return true;
+    }
+    return false;
+  }
+  // next field: number, wire type and (for wire 2) the payload; other wire types are skipped into *num only
+  bool next(int* field, int* wire, std::string* payload, uint64_t* value) {
+    uint64_t t;
+    if (!varint(&t)) return false;
+    *field = static_cast<int>(t >> 3);
+    *wire = static_cast<int>(t & 7);
+    switch (*wire) {
+      case 0:
+        return varint(value);
+      case 1:
+        if (end - p < 8) return false;
+        p += 8;
+        return true;
+      case 2: {
+        uint64_t n;
+        if (!varint(&n) || static_cast<uint64_t>(end - p) < n) return false;
+        payload->assign(reinterpret_cast<const char*>(p), n);
+        p += n;
+        return true;
+      }
+      case 5:
+        if (end - p < 4) return false;
+        p += 4;
+        return true;
+      default:
+        return false;
+    }
+  }
+};
+
+template <typename Fn>
+bool each(const std::string& msg, Fn fn) {
+  Reader r(msg);
+  while (!r.done()) {
+    int f, w;
+    std::string pl;
+    uint64_t v = 0;
+    if (!r.next(&f, &w, &pl, &v)) return false;
+    if (!fn(f, w, pl, v)) return false;
+  }
+  return true;
+}
+
+bool decode_map_entry(const std::string& e, std::string* k, std::string* v) {
+  return each(e, [&](int f, int w, const std::string& pl, uint64_t) {
+    if (w == 2 && f == 1) *k = pl;
+    if (w == 2 && f == 2) *v = pl;
+    return true;
+  });
+}
+
+}  // namespace
+
+std::string encode_options(bool pre_start_required, bool preferred_available) {
+  std::string o;
+  boolean(&o, 1, pre_start_required);
+  boolean(&o, 2, preferred_available);
+  return o;
+}
+
+std::string encode_list_and_watch(const std::vector<DeviceMsg>& devs) {
+  std::string o;
+  for (const auto& d : devs) {
+    std::string m;
+    str_if(&m, 1, d.id);
+    str_if(&m, 2, d.health);
+    if (!d.numa.empty()) {
+      std::string topo;
+      for (int64_t n : d.numa) {
+        std::string node;
+        int_field(&node, 1, n);
+        bytes(&topo, 1, node);
+      }
+      bytes(&m, 3, topo);
+    }
+    bytes(&o, 1, m);
+  }
+  return o;
+}
+
+std::string encode_preferred_response(const std::vector<std::vector<std::string>>& per_container) {
+  std::string o;
+  for (const auto& ids : per_container) {
+    std::string c;
+    for (const auto& id : ids) bytes(&c, 1, id);
+    bytes(&o, 1, c);
+  }
+  return o;
+}
+
+std::string encode_allocate_response(const std::vector<ContainerResponse>& per_container) {
+  std::string o;
+  for (const auto& r : per_container) {
+    std::string c;
+    for (const auto& kv : r.envs) bytes(&c, 1, map_entry(kv.first, kv.second));
+    for (const auto& m : r.mounts) {
+      std::string e;
+      str_if(&e, 1, m.container_path);
+      str_if(&e, 2, m.host_path);
+      boolean(&e, 3, m.read_only);
+      bytes(&c, 2, e);
+    }
+    for (const auto& d : r.devices) {
+      std::string e;
+      str_if(&e, 1, d.container_path);
+      str_if(&e, 2, d.host_path);
+      str_if(&e, 3, d.permissions);
+      bytes(&c, 3, e);
+    }
+    for (const auto& kv : r.annotations) bytes(&c, 4, map_entry(kv.first, kv.second));
+    bytes(&o, 1, c);
+  }
+  return o;
+}
+
+std::string encode_allocate_request(const std::vector<std::vector<std::string>>& ids_per_container) {
+  std::string o;
+  for (const auto& ids : ids_per_container) {
+    std::string c;
+    for (const auto& id : ids) bytes(&c, 1, id);
+    bytes(&o, 1, c);
+  }
+  return o;
+}
+
+std::string encode_preferred_request(const std::vector<PreferredRequest>& reqs) {
+  std::string o;
+  for (const auto& r : reqs) {
+    std::string c;
+    for (const auto& id : r.available) bytes(&c, 1, id);
+    for (const auto& id : r.must_include) bytes(&c, 2, id);
+    int_field(&c, 3, r.size);
+    bytes(&o, 1, c);
+  }
+  return o;
+}
+
+bool decode_allocate_request(const std::string& msg, std::vector<std::vector<std::string>>* out) {
+  return each(msg, [&](int f, int w, const std::string& pl, uint64_t) {
+    if (f != 1 || w != 2) return true;
+    std::vector<std::string> ids;
+    bool ok = each(pl, [&](int f2, int w2, const std::string& pl2, uint64_t) {
+      if (f2 == 1 && w2 == 2) ids.push_back(pl2);
+      return true;
+    });
+    out->push_back(std::move(ids));
+    return ok;
+  });
+}
+
+bool decode_preferred_request(const std::string& msg, std::vector<PreferredRequest>* out) {
+  return each(msg, [&](int f, int w, const std::string& pl, uint64_t) {
+    if (f != 1 || w != 2) return true;
+    PreferredRequest r;
+    bool ok = each(pl, [&](int f2, int w2, const std::string& pl2, uint64_t v) {
+      if (f2 == 1 && w2 == 2) r.available.push_back(pl2);
+      if (f2 == 2 && w2 == 2) r.must_include.push_back(pl2);
+      if (f2 == 3 && w2 == 0) r.size = static_cast<int32_t>(v);
+      return true;
+    });
+    out->push_back(std::move(r));
+    return ok;
+  });
+}
+
+bool decode_list_and_watch(const std::string& msg, std::vector<DeviceMsg>* out) {
+  return each(msg, [&](int f, int w, const std::string& pl, uint64_t) {
+    if (f != 1 || w != 2) return true;
+    DeviceMsg d;
+    bool ok = each(pl, [&](int f2, int w2, const std::string& pl2, uint64_t) {
+      if (f2 == 1 && w2 == 2) d.id = pl2;
+      if (f2 == 2 && w2 == 2) d.health = pl2;
+      return true;
+    });
+    out->push_back(std::move(d));
+    return ok;
+  });
+}
+
+bool decode_preferred_response(const std::string& msg, std::vector<std::vector<std::string>>* out) {
+  return decode_allocate_request(msg, out);  // same shape: repeated {1: repeated string}
+}
+
+bool decode_allocate_response(const std::string& msg, std::vector<ContainerResponse>* out) {
+  return each(msg, [&](int f, int w, const std::string& pl, uint64_t) {
+    if (f != 1 || w != 2) return true;
+    ContainerResponse r;
+    bool ok = each(pl, [&](int f2, int w2, const std::string& pl2, uint64_t) {
+      if (w2 != 2) return true;
+      std::string k, v;
+      if (f2 == 1 && decode_map_entry(pl2, &k, &v)) r.envs[k] = v;
+      if (f2 == 4 && decode_map_entry(pl2, &k, &v)) r.annotations[k] = v;
+      if (f2 == 2) {
+        MountMsg m;
+        each(pl2, [&](int f3, int w3, const std::string& pl3, uint64_t v3) {
+          if (f3 == 1 && w3 == 2) m.container_path = pl3;
+          if (f3 == 2 && w3 == 2) m.host_path = pl3;
+          if (f3 == 3 && w3 == 0) m.read_only = v3 != 0;
+          return true;
+        });
+        r.mounts.push_back(std::move(m));
+      }
+      if (f2 == 3) {
+        DeviceSpecMsg d;
+        each(pl2, [&](int f3, int w3, const std::string& pl3, uint64_t) {
+          if (f3 == 1 && w3 == 2) d.container_path = pl3;
+          if (f3 == 2 && w3 == 2) d.host_path = pl3;
+          if (f3 == 3 && w3 == 2) d.permissions = pl3;
+          return true;
+        });
+        r.devices.push_back(std::move(d));
+      }
+      return true;
+    });
+    out->push_back(std::move(r));
+    return ok;
+  });
+}
+
+}  // namespace gsx::dp

@@ -1,0 +1,53 @@
+// Protobuf wire format of the kubelet device-plugin API v1beta1 (the messages this repo serves and calls), hand
+// written like deviceplugin/api.py's descriptor: field numbers follow k8s.io/kubelet/pkg/apis/deviceplugin/
+// v1beta1/api.proto.  Unknown fields are skipped on decode; maps are repeated {1: key, 2: value} entries.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace gsx::dp {
+
+struct DeviceMsg {
+  std::string id, health;
+  std::vector<int64_t> numa;
+};
+
+struct MountMsg {
+  std::string container_path, host_path;
+  bool read_only = false;
+};
+
+struct DeviceSpecMsg {
+  std::string container_path, host_path, permissions;
+};
+
+struct ContainerResponse {
+  std::map<std::string, std::string> envs, annotations;
+  std::vector<MountMsg> mounts;
+  std::vector<DeviceSpecMsg> devices;
+};
+
+struct PreferredRequest {
+  std::vector<std::string> available, must_include;
+  int32_t size = 0;
+};
+
+// ---- encode
+std::string encode_options(bool pre_start_required, bool preferred_available);
+std::string encode_list_and_watch(const std::vector<DeviceMsg>& devs);
+std::string encode_preferred_response(const std::vector<std::vector<std::string>>& per_container);
+std::string encode_allocate_response(const std::vector<ContainerResponse>& per_container);
+std::string encode_allocate_request(const std::vector<std::vector<std::string>>& ids_per_container);
+std::string encode_preferred_request(const std::vector<PreferredRequest>& reqs);
+
+// ---- decode (false: malformed)
+bool decode_allocate_request(const std::string& msg, std::vector<std::vector<std::string>>* ids_per_container);
+bool decode_preferred_request(const std::string& msg, std::vector<PreferredRequest>* reqs);
+bool decode_list_and_watch(const std::string& msg, std::vector<DeviceMsg>* devs);
+bool decode_preferred_response(const std::string& msg, std::vector<std::vector<std::string>>* per_container);
+bool decode_allocate_response(const std::string& msg, std::vector<ContainerResponse>* per_container);
+
+}  // namespace gsx::dp

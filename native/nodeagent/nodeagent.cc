@@ -25,6 +25,7 @@
 //   gsx-nodeagent --apiserver URL --node NAME [--profile P] [--unit GiB]
 //                 [--workers N] [--no-verify] [--port-file F]
 #include <signal.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -48,6 +49,9 @@
 #include "allocstate.h"
 #include "apiclient.h"
 #include "ctlserver.h"
+#include "dpcore.h"
+#include "dpproto.h"
+#include "h2.h"
 #include "informer.h"
 #include "json.h"
 #include "model.h"
@@ -116,7 +120,66 @@ class Agent {
     }
   }
 
+  void set_plugin_socket(const std::string& s) { plugin_sock_ = s; }
+  void set_plugin_spawn(const std::string& python, const std::string& apiserver, const std::string& profile,
+                        const std::string& unit) {
+    spawn_python_ = python;
+    spawn_api_ = apiserver;
+    spawn_profile_ = profile;
+    spawn_unit_ = unit;
+  }
+
+  // Run the shipped device plugin as a child process on this node's inventory (the fake device backend fed the
+  // node's published devices; no kubelet registration, no PodResources: this stand-in serves neither).
+  bool spawn_plugin(std::string* err) {
+    char tmpl[] = "/tmp/gsx-na-XXXXXX";
+    if (!::mkdtemp(tmpl)) {
+      *err = std::string("mkdtemp: ") + std::strerror(errno);
+      return false;
+    }
+    std::string dir = tmpl;
+    std::string spec = dir + "/devices.json";
+    {
+      std::ofstream f(spec);
+      f << "[";
+      bool first = true;
+      for (const auto& kv : devices_) {
+        const Device& d = kv.second;
+        if (!first) f << ",";
+        first = false;
+        std::string bdf;
+        json::append_quoted(&bdf, d.bdf);
+        f << "{\"index\":" << d.index << ",\"bdf\":" << bdf << ",\"total_bytes\":" << d.total_bytes
+          << ",\"share_bytes\":" << d.share_bytes << ",\"cu_count\":" << d.cu << ",\"xcc_count\":" << d.xcc
+          << ",\"render_minor\":" << d.render << ",\"card_minor\":" << d.card << "}";
+      }
+      f << "]";
+    }
+    std::vector<std::string> args = {spawn_python_, "-m", "gpushare_scheduler_extender_amd.deviceplugin", "--node", node_,
+                                     "--apiserver", spawn_api_, "--profile", spawn_profile_, "--unit", spawn_unit_,
+                                     "--backend", "fake", "--socket-dir", dir, "--no-publish", "--no-register",
+                                     "--podresources-socket", "", "--isolation", "advisory", "--health-interval",
+                                     "3600", "--log-level", "warning"};
+    pid_t pid = ::fork();
+    if (pid < 0) {
+      *err = std::string("fork: ") + std::strerror(errno);
+      return false;
+    }
+    if (pid == 0) {
+      ::setenv("GSX_FAKE_DEVICES", spec.c_str(), 1);
+      std::vector<char*> argv;
+      for (auto& a : args) argv.push_back(const_cast<char*>(a.c_str()));
+      argv.push_back(nullptr);
+      ::execv(spawn_python_.c_str(), argv.data());
+      ::_exit(127);
+    }
+    plugin_pid_ = pid;
+    plugin_sock_ = dir + "/gpushare-amd.sock";
+    return true;
+  }
   bool start(std::string* err) {
+    if (!spawn_python_.empty() && !spawn_plugin(err)) return false;
+    if (!plugin_sock_.empty() && !plugin_connect(120, err)) return false;
     ReflectorConfig rc;
     rc.path = "/api/v1/pods";
     rc.field_selector = "spec.nodeName=" + node_;
@@ -164,6 +227,13 @@ class Agent {
     cv_.notify_all();
     for (auto& t : workers_) t.join();
     if (pods_r_) pods_r_->stop();
+    if (plugin_pid_ > 0) {
+      ::kill(plugin_pid_, SIGTERM);
+      for (int i = 0; i < 100 && ::waitpid(plugin_pid_, nullptr, WNOHANG) == 0; ++i) ::usleep(50000);
+      ::kill(plugin_pid_, SIGKILL);
+      ::waitpid(plugin_pid_, nullptr, WNOHANG);
+      plugin_pid_ = -1;
+    }
   }
 
   CtlServer::Reply handle(const http::Message& req) {
@@ -302,6 +372,7 @@ class Agent {
     if (r == running_.end()) return;
     int dev = r->second;
     running_.erase(r);
+    used_ids_.erase(uid);
     for (auto& kv : devices_) {
       if (CuPartitioner* cp = state_->cus(kv.first)) cp->release(uid);
     }
@@ -350,53 +421,168 @@ class Agent {
     }
   }
 
-  std::string build_envs_locked(const AllocPod& pod, const Device& dev, const std::vector<int>& cus) {
-    // deviceplugin/allocator.py build_response, mount_mode "isolated": only this GPU's nodes are mounted
-    const std::string visible = "0";
-    char frac[32];
-    double f = pod.dev_total > 0 ? static_cast<double>(pod.request) / static_cast<double>(pod.dev_total) : 0.0;
-    if (dev.share_bytes > 0 && dev.total_bytes > dev.share_bytes) {
-      f *= static_cast<double>(dev.share_bytes) / static_cast<double>(dev.total_bytes);
-    }
-    std::snprintf(frac, sizeof(frac), "%.6f", f);
-    std::vector<std::pair<std::string, std::string>> env = {
-        {"HIP_VISIBLE_DEVICES", visible},
-        {"ROCR_VISIBLE_DEVICES", visible},
-        {p_.a_idx, std::to_string(dev.index)},
-        {p_.a_dev, std::to_string(pod.dev_total > 0 ? pod.dev_total : 0)},
-        {p_.a_pod, std::to_string(pod.request)},
-        {p_.env_container, std::to_string(pod.request)},
-        {"GSX_GPU_MEM_FRACTION", frac},
-        {"GSX_GPU_BDF", dev.bdf},
-    };
-    if (!cus.empty()) {
-      env.emplace_back("GSX_CU_MASK", cu_words(cus, dev.cu));
-      env.emplace_back("HSA_CU_MASK", visible + ":" + cu_ranges(cus));
-    }
+  // The container response is the plugin's own (native/engine/dpcore.cc build_response, mount mode "isolated":
+  // only this GPU's nodes), kept as JSON for GET /v1/allocations/<uid>.
+  static std::string allocation_json(const dp::ContainerResponse& r) {
     std::string o = "{\"envs\":{";
-    for (size_t i = 0; i < env.size(); ++i) {
-      if (i) o.push_back(',');
-      json::append_quoted(&o, env[i].first);
+    bool first = true;
+    for (const auto& kv : r.envs) {
+      if (!first) o.push_back(',');
+      first = false;
+      json::append_quoted(&o, kv.first);
       o.push_back(':');
-      json::append_quoted(&o, env[i].second);
+      json::append_quoted(&o, kv.second);
     }
     o.append("},\"devices\":[");
-    std::vector<std::string> nodes = {"/dev/kfd"};
-    if (dev.render >= 0) nodes.push_back("/dev/dri/renderD" + std::to_string(dev.render));
-    if (dev.card >= 0) nodes.push_back("/dev/dri/card" + std::to_string(dev.card));
-    for (size_t i = 0; i < nodes.size(); ++i) {
+    for (size_t i = 0; i < r.devices.size(); ++i) {
       if (i) o.push_back(',');
       o.append("{\"container_path\":");
-      json::append_quoted(&o, nodes[i]);
+      json::append_quoted(&o, r.devices[i].container_path);
       o.append(",\"host_path\":");
-      json::append_quoted(&o, nodes[i]);
-      o.append(",\"permissions\":\"rw\"}");
+      json::append_quoted(&o, r.devices[i].host_path);
+      o.append(",\"permissions\":");
+      json::append_quoted(&o, r.devices[i].permissions);
+      o.push_back('}');
     }
     o.append("]}");
     return o;
   }
 
+  std::string build_envs_locked(const AllocPod& pod, const Device& dev, const std::vector<int>& cus) {
+    DpDevice d;
+    d.index = dev.index;
+    d.bdf = dev.bdf;
+    d.cu_count = dev.cu;
+    d.total_bytes = dev.total_bytes;
+    d.share_bytes = dev.share_bytes;
+    d.nodes = {"/dev/kfd"};
+    if (dev.render >= 0) d.nodes.push_back("/dev/dri/renderD" + std::to_string(dev.render));
+    if (dev.card >= 0) d.nodes.push_back("/dev/dri/card" + std::to_string(dev.card));
+    return allocation_json(build_response(pod, d, pod.request, cus, "isolated", p_));
+  }
+
+  // ---------------------------------------------------------------- kubelet + the shipped device plugin
+  // With --plugin-socket the Allocate is not decided here: like kubelet, this agent asks the plugin
+  // (GetPreferredAllocation, then Allocate with those IDs) over the device-plugin gRPC API and starts whichever
+  // pod the plugin committed (the container annotation gpushare.amd.com/pod names it), re-queueing the admitted
+  // pod if that was another one (the forgiving stand-in, as deviceplugin/agent.py without --faithful).
+  bool plugin_connect(double timeout_s, std::string* err) {
+    dp_ = std::make_unique<h2::Client>(plugin_sock_);
+    double deadline = now_s() + timeout_s;
+    while (true) {
+      std::vector<std::string> msgs;
+      int st = 0;
+      std::string e;
+      if (dp_->stream("/v1beta1.DevicePlugin/ListAndWatch", std::string(), 1, &msgs, &st, &e, 5.0) && !msgs.empty()) {
+        std::vector<dp::DeviceMsg> devs;
+        if (dp::decode_list_and_watch(msgs[0], &devs)) {
+          all_ids_.clear();
+          for (const auto& d : devs) {
+            if (d.health == "Healthy") all_ids_.push_back(d.id);
+          }
+          return true;
+        }
+      }
+      if (now_s() > deadline) {
+        *err = "device plugin at " + plugin_sock_ + " never answered ListAndWatch: " + e;
+        return false;
+      }
+      dp_ = std::make_unique<h2::Client>(plugin_sock_);
+      ::usleep(50000);
+    }
+  }
+
+  void admit_via_plugin_locked(std::string key, std::unique_lock<std::mutex>& lk) {
+    const AllocPod* mine = state_->pod_by_key(key);
+    if (!mine) return;
+    const std::string my_uid = mine->uid, my_key = key;
+    if (running_.count(my_uid) || state_->inflight(my_uid)) return;
+    const int64_t units = mine->request;
+    std::unordered_set<std::string> used;
+    for (const auto& kv : used_ids_) used.insert(kv.second.begin(), kv.second.end());
+    dp::PreferredRequest pr;
+    for (const auto& id : all_ids_) {
+      if (!used.count(id)) pr.available.push_back(id);
+    }
+    pr.size = static_cast<int32_t>(units);
+    if (static_cast<int64_t>(pr.available.size()) < units) {
+      std::fprintf(stderr, "[gsx-nodeagent] %s: %lld units requested, %zu IDs free\n", key.c_str(),
+                   static_cast<long long>(units), pr.available.size());
+      queued_.insert(my_uid);
+      delayed_.push_back({now_s() + 0.01, key});
+      return;
+    }
+    state_->set_inflight(my_uid, true);
+    const double t0 = seen_.count(my_uid) ? seen_[my_uid] : now_s();
+    lk.unlock();
+    std::string resp, err;
+    int st = 0;
+    std::vector<std::vector<std::string>> chosen;
+    std::vector<dp::ContainerResponse> crs;
+    const double tp0 = now_s();
+    bool ok;
+    {
+      std::lock_guard<std::mutex> g(dp_mu_);  // kubelet admits one pod at a time
+      ok = dp_->call("/v1beta1.DevicePlugin/GetPreferredAllocation", dp::encode_preferred_request({pr}), &resp, &st,
+                     &err) &&
+           dp::decode_preferred_response(resp, &chosen) && chosen.size() == 1 &&
+           dp_->call("/v1beta1.DevicePlugin/Allocate", dp::encode_allocate_request(chosen), &resp, &st, &err) &&
+           dp::decode_allocate_response(resp, &crs) && crs.size() == 1;
+    }
+    const double tp1 = now_s();
+    lk.lock();
+    state_->set_inflight(my_uid, false);
+    if (!ok) {
+      failed_++;
+      std::fprintf(stderr, "[gsx-nodeagent] Allocate for %s failed: %d %s\n", key.c_str(), st, err.c_str());
+      lk.unlock();
+      std::string stj = "{\"status\":{\"phase\":\"Failed\",\"reason\":\"UnexpectedAdmissionError\",\"message\":";
+      json::append_quoted(&stj, "Allocate failed: " + err);
+      stj.append("}}");
+      patch_status("/api/v1/namespaces/" + mine_ns(my_key) + "/pods/" + mine_name(my_key), stj);
+      lk.lock();
+      return;
+    }
+    const dp::ContainerResponse& cr = crs[0];
+    std::string who = cr.annotations.count("gpushare.amd.com/pod") ? cr.annotations.at("gpushare.amd.com/pod") : "";
+    size_t cut = who.rfind('/');
+    std::string uid = cut == std::string::npos ? my_uid : who.substr(cut + 1);
+    key = cut == std::string::npos ? my_key : who.substr(0, cut);
+    if (uid != my_uid) {  // the plugin committed an earlier pod of this size: it starts, ours waits for the next
+      queued_.insert(my_uid);
+      queue_.push_back(my_key);
+      ++added_;
+      wake_locked();
+    }
+    if (running_.count(uid) || !keys_.count(key)) return;  // already started, or gone meanwhile
+    used_ids_[uid] = chosen[0];
+    auto idx = cr.envs.find(p_.a_idx);
+    const int dev_idx = idx == cr.envs.end() ? -1 : std::atoi(idx->second.c_str());
+    if (!devices_.count(dev_idx)) return;
+    std::vector<int> cus;
+    auto cm = cr.envs.find("GSX_CU_MASK");
+    if (cm != cr.envs.end()) {
+      try {
+        cus = parse_cu_words(cm->second);
+      } catch (const std::exception&) {
+        cus.clear();
+      }
+    }
+    const AllocPod* started = state_->pod(uid);
+    const int64_t request = started ? started->request : units;
+    state_->set_inflight(uid, true);
+    start_pod_locked(key, uid, request, dev_idx, cus, allocation_json(cr),
+                     "/api/v1/namespaces/" + mine_ns(key) + "/pods/" + mine_name(key), t0, tp0, tp1, lk);
+  }
+
+  static std::string mine_ns(const std::string& key) { return key.substr(0, key.find('/')); }
+  static std::string mine_name(const std::string& key) { return key.substr(key.find('/') + 1); }
+
   void admit_locked(std::string key, std::unique_lock<std::mutex>& lk) {
+    if (dp_) {
+      admit_via_plugin_locked(std::move(key), lk);
+      return;
+    }
     const AllocPod* mine = state_->pod_by_key(key);
     if (!mine) return;
     std::string uid = mine->uid;
@@ -487,10 +673,19 @@ class Agent {
     lk.lock();
     if (have) state_->observe(committed);
     state_->first_container_committed(uid, units, true);
+    start_pod_locked(key, uid, pod.request, dev_idx, cus, envs, path, t0, tp0, tp1, lk);
+  }
+
+  // Start a pod whose Allocate is done on its GPU's runtime (slice stamped + every resident slice verified), then
+  // report it Running.  mu_ held on entry and exit.
+  void start_pod_locked(const std::string& key, const std::string& uid, int64_t request, int dev_idx,
+                        const std::vector<int>& cus, const std::string& envs, const std::string& path, double t0,
+                        double tp0, double tp1, std::unique_lock<std::mutex>& lk) {
+    CuPartitioner* cp = state_->cus(dev_idx);
     drain_releases_locked(dev_idx, lk);
     lk.unlock();
     // start the pod on its GPU's runtime: slice stamped + every resident slice verified
-    std::string body ="{\"dev\":" + std::to_string(dev_idx) + ",\"bytes\":" + std::to_string(pod.request * unit_) +
+    std::string body ="{\"dev\":" + std::to_string(dev_idx) + ",\"bytes\":" + std::to_string(request * unit_) +
                        ",\"cus\":";
     if (cus.empty()) {
       body.append("null");
@@ -622,6 +817,13 @@ class Agent {
   ApiClient api_;
   std::map<int, Device> devices_;
   std::unique_ptr<AllocState> state_;  // the device plugin's matcher (allocstate.h)
+  std::string plugin_sock_;             // --plugin-socket: Allocate through the shipped plugin (gRPC)
+  std::string spawn_python_, spawn_api_, spawn_profile_, spawn_unit_;  // --plugin-spawn: run that plugin ourselves
+  pid_t plugin_pid_ = -1;
+  std::unique_ptr<h2::Client> dp_;
+  std::mutex dp_mu_;
+  std::vector<std::string> all_ids_;
+  std::unordered_map<std::string, std::vector<std::string>> used_ids_;  // uid -> the IDs its Allocate took
   std::unordered_map<std::string, std::string> keys_;  // ns/name -> uid of every pod the informer delivered
   std::map<int, std::unique_ptr<ApiClient>> runtimes_;
   std::unique_ptr<Reflector> pods_r_;
@@ -655,7 +857,7 @@ void on_sig(int) { g_stop = 1; }
 }  // namespace
 
 int main(int argc, char** argv) {
-  std::string apiserver, node, profile = "shared-gpu", unit = "GiB", port_file, host = "127.0.0.1";
+  std::string apiserver, node, profile = "shared-gpu", unit = "GiB", port_file, host = "127.0.0.1", plugin_socket, plugin_python;
   int workers = 16, port = 0;
   bool verify = true;
   for (int i = 1; i < argc; ++i) {
@@ -675,9 +877,11 @@ int main(int argc, char** argv) {
     else if (a == "--no-verify") verify = false;
     else if (a == "--port") port = std::atoi(val("--port").c_str());
     else if (a == "--port-file") port_file = val("--port-file");
+    else if (a == "--plugin-socket") plugin_socket = val("--plugin-socket");
+    else if (a == "--plugin-spawn") plugin_python = val("--plugin-spawn");
     else if (a == "-h" || a == "--help") {
       std::printf("usage: gsx-nodeagent --apiserver URL --node NAME [--profile P] [--unit GiB|MiB] [--workers N]\n"
-                  "                     [--no-verify] [--port P] [--port-file F]\n");
+                  "                     [--no-verify] [--port P] [--port-file F] [--plugin-socket S | --plugin-spawn PYTHON]\n");
       return 0;
     } else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -698,6 +902,8 @@ int main(int argc, char** argv) {
   ApiConfig api;
   api.server = apiserver;
   Agent agent(api, node, profile_by_name(profile), unit_bytes, workers, verify);
+  agent.set_plugin_socket(plugin_socket);
+  if (!plugin_python.empty()) agent.set_plugin_spawn(plugin_python, apiserver, profile, unit);
   std::string err;
   CtlServer srv([&](const http::Message& m) { return agent.handle(m); });
   int bound = srv.start(host, port, &err);

@@ -336,7 +336,7 @@ def test_plugin_reregisters_after_kubelet_restart():
         kubelet2 = None
         try:
             await asyncio.wait_for(kubelet.registered.wait(), 5)
-            first_server = plugin._server
+            first_server = plugin._native or plugin._server
             await kubelet.stop()
             kubelet2 = FakeKubelet(d)
             await kubelet2.start()  # new socket inode: the plugin's watcher notices within ~1 s
@@ -346,7 +346,7 @@ def test_plugin_reregisters_after_kubelet_restart():
                     break
                 await asyncio.sleep(0.01)
             assert plugin.stats["registrations"] == 2
-            assert plugin._server is not first_server
+            assert (plugin._native or plugin._server) is not first_server
             pc = PluginClient(plugin.socket_path)
             opts = await pc.options()
             assert opts.get_preferred_allocation_available
@@ -390,7 +390,9 @@ def test_plugin_allocate_retries_conflicts_and_apiserver_errors():
             for i in range(4):
                 p = await client.get("pods", f"p{i}", "default")
                 assert p["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
-            assert plugin.stats["allocate_retries"] > 0 and plugin.stats["allocate_fail"] == 0
+            # retried: by the Python handler, or a native fast-path patch that failed and was handed to it
+            native_failures = plugin.debug_state()["grpc"].get("patch_failures", 0)
+            assert plugin.stats["allocate_retries"] + native_failures > 0 and plugin.stats["allocate_fail"] == 0
             await pc.close()
         finally:
             await plugin.stop()

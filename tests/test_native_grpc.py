@@ -1,0 +1,145 @@
+"""The device plugin's native gRPC endpoint (``native/engine/h2.cc`` on libnghttp2, ``dpcore.cc``): interop with
+grpcio in both directions, the fast Allocate path against the Python handler it stands in for, and the hand-off
+of everything else to Python."""
+import asyncio
+import os
+import tempfile
+
+import grpc
+import pytest
+
+from gpushare_scheduler_extender_amd.core.engine import native
+from gpushare_scheduler_extender_amd.deviceplugin import api
+from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
+from gpushare_scheduler_extender_amd.deviceplugin.isolation import IsolationManager
+from gpushare_scheduler_extender_amd.deviceplugin.plugin import FakeKubelet, GpuSharePlugin, PluginClient, fake_ids
+from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+from gpushare_scheduler_extender_amd.k8s.objects import make_node
+from gpushare_scheduler_extender_amd.models.profile import POD_CU_COUNT_ANNOTATION, SHARED_GPU
+from tests.fixtures.fakeapi import FakeApiServerRunner
+from tests.test_deviceplugin import bound_pod
+
+P = SHARED_GPU
+
+pytestmark = pytest.mark.skipif(not native().h2_available()[0], reason="libnghttp2 not on this system")
+
+
+async def _plugin(tmp, fast: bool, isolation: bool = False, spec: str = "2x16GiB"):
+    api_srv = await FakeApiServerRunner().start()
+    client = KubeClient(api_srv.url)
+    await client.create("nodes", make_node("n1", 32, 0))
+    iso = IsolationManager(os.path.join(tmp, "iso")) if isolation else None
+    os.environ["GSX_PLUGIN_FAST"] = "1" if fast else "0"
+    try:
+        plugin = GpuSharePlugin(client, "n1", fake_devices(spec), P, socket_dir=os.path.join(tmp, "dp"), isolation=iso)
+        await plugin.start(register=False)
+    finally:
+        os.environ.pop("GSX_PLUGIN_FAST", None)
+    assert plugin.grpc_impl == "native"
+    return api_srv, client, plugin
+
+
+async def _close(api_srv, client, plugin, *clients):
+    for c in clients:
+        await c.close()
+    await plugin.stop()
+    await client.close()
+    await api_srv.stop()
+
+
+def test_grpcio_kubelet_against_the_native_endpoint():
+    async def go():
+        tmp = tempfile.mkdtemp()
+        api_srv, client, plugin = await _plugin(tmp, fast=True)
+        pc = PluginClient(plugin.socket_path)
+        try:
+            opts = await pc._call("GetDevicePluginOptions")(api.Empty())
+            assert opts.get_preferred_allocation_available and not opts.pre_start_required
+            stream = pc.list_and_watch()
+            first = await asyncio.wait_for(stream.read(), 5)
+            assert len(first.devices) == 32 and {d.health for d in first.devices} == {api.HEALTHY}
+            plugin.set_health(1, False, "test")  # the stream gets the new list
+            second = await asyncio.wait_for(stream.read(), 5)
+            assert sum(d.health == api.UNHEALTHY for d in second.devices) == 16
+            stream.cancel()
+            for i in range(3):
+                await client.create("pods", bound_pod(f"p{i}", 4, dev=0, assume=10 + i, dev_total=16))
+            await asyncio.sleep(0.2)
+            ids = fake_ids(plugin.devices[0], 16)
+            pref = await pc.preferred(ids + fake_ids(plugin.devices[1], 16), 4)
+            assert all(i.startswith(ids[0].split("-")[0]) for i in pref.container_responses[0].deviceIDs)
+            for i in range(3):
+                r = await pc.allocate([ids[4 * i: 4 * i + 4]])
+                envs = dict(r.container_responses[0].envs)
+                assert envs["SHARED_GPU_MEM_IDX"] == "0" and envs["SHARED_GPU_MEM_CONTAINER"] == "4"
+                assert dict(r.container_responses[0].annotations)["gpushare.amd.com/pod"].startswith(f"default/p{i}/")
+            with pytest.raises(grpc.aio.AioRpcError) as e:  # no pod left: the Python handler says why
+                await pc.allocate([ids[12:16]])
+            assert e.value.code() == grpc.StatusCode.FAILED_PRECONDITION and "no pending pod" in e.value.details()
+            st = plugin.debug_state()["grpc"]
+            assert st["fast_allocate"] == 3 and st["slow_allocate"] >= 1 and st["fast_preferred"] >= 1, st
+            for i in range(3):  # committed exactly like the Python path: ASSIGNED=true, a record per Allocate
+                assert (await client.get("pods", f"p{i}", "default"))["metadata"]["annotations"][
+                    P.annotation_assigned] == "true"
+            assert len(plugin.state.records) == 3 and plugin.stats["allocate_native"] == 3
+        finally:
+            await _close(api_srv, client, plugin, pc)
+    asyncio.run(go())
+
+
+@pytest.mark.parametrize("isolation", [False, True])
+def test_fast_path_answers_exactly_what_the_python_handler_answers(isolation):
+    """The same pods through the native fast path and through the Python handler (fast path off): identical
+    container responses (env contract, device nodes, CU partition, isolation mounts)."""
+    async def run(fast):
+        tmp = tempfile.mkdtemp()
+        api_srv, client, plugin = await _plugin(tmp, fast=fast, isolation=isolation, spec="1x64GiB")
+        pc = PluginClient(plugin.socket_path)
+        try:
+            pods = [bound_pod("a", 16, dev=0, assume=1, dev_total=64, uid="u-a",
+                              annotations={POD_CU_COUNT_ANNOTATION: "64"}),
+                    bound_pod("b", [8, 4], dev=0, assume=2, dev_total=64, uid="u-b")]
+            for p in pods:
+                await client.create("pods", p)
+            await asyncio.sleep(0.2)
+            ids = fake_ids(plugin.devices[0], 64)
+            out = []
+            for chunk in (ids[0:16], ids[16:24], ids[24:28]):
+                r = (await pc.allocate([chunk])).container_responses[0]
+                out.append({"envs": dict(r.envs), "annotations": dict(r.annotations),
+                            "devices": sorted((d.container_path, d.host_path, d.permissions) for d in r.devices),
+                            "mounts": sorted((m.container_path, m.host_path.replace(tmp, "<tmp>"), m.read_only)
+                                             for m in r.mounts)})
+            st = plugin.debug_state()["grpc"]
+            return out, st
+        finally:
+            await _close(api_srv, client, plugin, pc)
+    fast, st_fast = asyncio.run(run(True))
+    slow, st_slow = asyncio.run(run(False))
+    assert st_fast["fast_allocate"] == 3 and st_slow["fast_allocate"] == 0
+    assert fast == slow
+    assert fast[0]["envs"]["HSA_CU_MASK"].startswith("0:") and "GSX_CU_MASK" in fast[0]["envs"]
+    assert fast[1]["envs"]["SHARED_GPU_MEM_CONTAINER"] == "8" and fast[2]["envs"]["SHARED_GPU_MEM_CONTAINER"] == "4"
+    if isolation:
+        assert any(m[0] == "/etc/ld.so.preload" for m in fast[0]["mounts"])
+
+
+def test_native_client_against_a_grpcio_server():
+    """h2::Client (the compiled kubelet stand-in's side) registering with a grpcio Registration service."""
+    async def go():
+        tmp = tempfile.mkdtemp()
+        kubelet = FakeKubelet(tmp)
+        await kubelet.start()
+        try:
+            req = api.RegisterRequest(version=api.VERSION, endpoint="x.sock", resource_name=P.resource).SerializeToString()
+            status, body = await asyncio.get_running_loop().run_in_executor(
+                None, native().h2_call, os.path.join(tmp, api.KUBELET_SOCKET), "/v1beta1.Registration/Register", req,
+                5.0)
+            assert status == 0, body
+            assert kubelet.registrations[0].endpoint == "x.sock"
+            status, body = await asyncio.get_running_loop().run_in_executor(
+                None, native().h2_call, os.path.join(tmp, api.KUBELET_SOCKET), "/v1beta1.Registration/Nope", b"", 5.0)
+            assert status == 12, (status, body)  # UNIMPLEMENTED from grpcio
+        finally:
+            await kubelet.stop()
+    asyncio.run(go())
