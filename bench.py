@@ -370,10 +370,12 @@ def parse():
                          "L3 domain (5 cores); 0: two physical cores")
     ap.add_argument("--api-latency-ms", type=float, default=0.0,
                     help="fake kube-apiserver answers every non-watch request after this delay (timed region)")
-    ap.add_argument("--bind-order", default="strict", choices=["strict", "relaxed"],
-                    help="extender --bind-order: strict ASSUME_TIME order of equal-size cross-GPU binds (default) or "
-                         "relaxed (all concurrent; swaps repaired by the plugin's PodResources reconciliation)")
-    ap.add_argument("--sweep-orders", default="strict", help="bind orders the latency sweep covers (comma list)")
+    ap.add_argument("--bind-order", default="auto", choices=["auto", "strict", "relaxed"],
+                    help="extender --bind-order: auto (default; no order on this node, whose plugin matches in landing "
+                         "order), strict ASSUME_TIME order of equal-size cross-GPU binds (the reference plugin's "
+                         "contract) or relaxed (all concurrent; swaps repaired by the plugin's PodResources "
+                         "reconciliation)")
+    ap.add_argument("--sweep-orders", default="auto", help="bind orders the latency sweep covers (comma list)")
     ap.add_argument("--kubelet", default="standin", choices=["standin", "faithful"],
                     help="with --node-agent plugin: the kubelet stand-in re-routes a mismatched Allocate (standin) or "
                          "behaves like kubelet and lets the plugin reconcile (faithful)")
@@ -558,7 +560,8 @@ def main():
         shim_url = lt.run(shim.start("127.0.0.1", 0))
     all_devs = gather((dev.to_dict(), shim_url))
     from gpushare_scheduler_extender_amd.deviceplugin.devices import Device
-    from gpushare_scheduler_extender_amd.models.profile import (NODE_DEVICE_INFO_ANNOTATION,
+    from gpushare_scheduler_extender_amd.models.profile import (NODE_ALLOCATE_ORDER_ANNOTATION,
+                                                                NODE_DEVICE_INFO_ANNOTATION,
                                                                 NODE_RUNTIME_ENDPOINTS_ANNOTATION)
 
     agent_client = KubeClient(api_url)

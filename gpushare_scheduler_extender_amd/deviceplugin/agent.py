@@ -22,10 +22,15 @@ container env -> the pod runs on the chosen GPU.
   and the admitted pod waits for the next Allocate.  ``stats["swapped_equivalent"]`` counts swaps between
   pods with the same allocation (same GPU and partition request, which the extender binds unordered);
   ``stats["mismatch"]`` counts the others, where a real kubelet would have started a container on another
-  pod's GPU (the ASSUME_TIME ordering of binds exists to keep this at 0).
+  pod's GPU (the plugin's landing-order matching, or the extender's ASSUME_TIME ordering of binds for an
+  ASSUME_TIME-matching plugin, keeps this at 0).
 * ``faithful=True`` plays kubelet as it is, not as the protocol would like it: the container of the pod
-  being admitted starts with whatever allocation the plugin returned (no re-routing), pods met together are
-  admitted as one batch sorted by creationTimestamp (kubelet's ``HandlePodAdditions``), and kubelet's record
+  being admitted starts with whatever allocation the plugin returned (no re-routing), pods are admitted one
+  at a time in watch order (kubelet's apiserver config source pushes every watch event and its pod config
+  merges it into an ADD of just the new pod, so ``HandlePodAdditions`` sees one pod per batch in steady state),
+  or, with ``batch_window`` > 0, the pods met within the window as one batch sorted by creationTimestamp (what
+  kubelet does with the pods of its initial LIST after a restart: the case reconciliation exists for), and
+  kubelet's record
   of device IDs per container is served on the PodResources API (:mod:`.podresources`), which the plugin
   reconciles against (:mod:`.reconcile`).  ``/v1/allocations/<uid>`` is then the container's real env.
 * A pod that completes or is deleted is stopped and its slice released; the
@@ -620,7 +625,9 @@ def main(argv=None) -> int:
                     help="kubelet as it is: no re-routing of a mismatched Allocate, creationTimestamp-sorted batches, "
                          "PodResources API served for the plugin's reconciliation")
     ap.add_argument("--batch-window", type=float, default=-1.0,
-                    help="seconds kubelet collects pods into one admission batch (default 0.02 with --faithful)")
+                    help="seconds kubelet collects pods into one creationTimestamp-sorted admission batch (default 0: "
+                         "one pod per watch event, kubelet's steady state; > 0 models the multi-pod batch of "
+                         "kubelet's initial LIST after a restart)")
     ap.add_argument("--no-reconcile", action="store_true", help="the plugin does not reconcile with PodResources")
     ap.add_argument("--isolation-dir", default="",
                     help="enforced isolation: the plugin writes each pod's config + HBM ledger here (and answers the "
@@ -643,7 +650,7 @@ def main(argv=None) -> int:
         plugin = None
         sock_dir = a.socket_dir or tempfile.mkdtemp(prefix="gsx-dp-")
         prsock = os.path.join(sock_dir, "pod-resources", "kubelet.sock") if a.faithful else None
-        window = a.batch_window if a.batch_window >= 0 else (0.02 if a.faithful else 0.0)
+        window = max(0.0, a.batch_window)
         if a.plugin == "grpc":
             iso = None
             if a.isolation_dir:

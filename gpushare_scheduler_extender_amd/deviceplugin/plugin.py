@@ -43,7 +43,8 @@ import grpc
 
 from ..k8s.client import ApiError, KubeClient
 from ..models import pod as podutil
-from ..models.profile import NODE_DEVICE_INFO_ANNOTATION, NODE_DEVICE_MEMORY_ANNOTATION, NamingProfile
+from ..models.profile import (NODE_ALLOCATE_ORDER_ANNOTATION, NODE_DEVICE_INFO_ANNOTATION, NODE_DEVICE_MEMORY_ANNOTATION,
+                              NamingProfile)
 from . import api
 from ..k8s.informer import Handler, Informer
 from .allocator import AllocateError, ContainerAllocation, assigned_patch, build_response
@@ -730,7 +731,8 @@ class GpuSharePlugin:
         log.info("registered %s with kubelet at %s", self.profile.resource, self.kubelet_socket)
 
     async def publish_node(self):
-        """gpu-count capacity + per-device totals / inventory annotations (what kubelet does not publish)."""
+        """gpu-count capacity + per-device totals / inventory annotations (what kubelet does not publish), and
+        the Allocate order this plugin matches in (landing order: the extender may bind concurrently)."""
         import json  # noqa: PLC0415
 
         totals = [self.units[i] for i in sorted(self.units)]
@@ -740,7 +742,8 @@ class GpuSharePlugin:
                for d in sorted(self.devices.values(), key=lambda d: d.index)]
         await self.client.patch("nodes", self.node, {"metadata": {"annotations": {
             NODE_DEVICE_MEMORY_ANNOTATION: ",".join(str(t) for t in totals),
-            NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv, separators=(",", ":"))}}})
+            NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv, separators=(",", ":")),
+            NODE_ALLOCATE_ORDER_ANNOTATION: "landing"}}})
         await self.client.patch("nodes", self.node, {"status": {"capacity": {
             self.profile.count: str(len(self.devices))}}}, sub="status")
 

@@ -43,8 +43,10 @@ def parse_args(argv=None):
                     help="also write per-level rotating log files here (the reference used /var/log/device-plugin)")
     ap.add_argument("--profile", default=env.get("GSX_PROFILE", "shared-gpu"))
     ap.add_argument("--bind-mode", default=env.get("GSX_BIND_MODE", "binding"), choices=["binding", "update"])
-    ap.add_argument("--bind-order", default=env.get("GSX_BIND_ORDER", "strict"), choices=["strict", "relaxed"],
-                    help="strict: equal-size binds of one node for different GPUs land in ASSUME_TIME order (default); "
+    ap.add_argument("--bind-order", default=env.get("GSX_BIND_ORDER", "auto"), choices=["auto", "strict", "relaxed"],
+                    help="auto (default): equal-size binds of one node for different GPUs land in ASSUME_TIME order, "
+                         "except on nodes whose device plugin advertises landing-order matching "
+                         "(gpushare.amd.com/allocate-order=landing); strict: ASSUME_TIME order on every node; "
                          "relaxed: all binds concurrent, swaps repaired by the device plugin's PodResources "
                          "reconciliation")
     ap.add_argument("--kube-qps", type=float, default=float(env.get("GSX_KUBE_QPS", "0")))

@@ -72,19 +72,21 @@ class ExtenderServer:
                  emit_events: bool = True, leader_elect: bool = False, lease_name: str = "gpushare-schd-extender",
                  lease_namespace: str = "kube-system", lease_duration: float = 15.0, renew_deadline: float = 10.0,
                  retry_period: float = 2.0, native_controller: bool = True, pprof: bool = True,
-                 bind_order: str = "strict"):
+                 bind_order: str = "auto"):
         if bind_mode not in ("binding", "update"):
             raise ValueError("bind_mode must be 'binding' or 'update'")
         self.client = client
         self.profile = profile
         self.engine = new_engine(profile)
-        if bind_order not in ("strict", "relaxed"):
-            raise ValueError("bind_order must be 'strict' or 'relaxed'")
+        if bind_order not in ("auto", "strict", "relaxed"):
+            raise ValueError("bind_order must be 'auto', 'strict' or 'relaxed'")
         # strict: equal-size binds of one node for different GPUs reach the apiserver in ASSUME_TIME order (the
-        # reference's node lock, pkg/cache/nodeinfo.go:141-189); relaxed: every bind is concurrent and the device
-        # plugin's reconciliation with kubelet (deviceplugin/reconcile.py) repairs the swaps that can follow
+        # reference's node lock, pkg/cache/nodeinfo.go:141-189); auto: the same, except on nodes whose device
+        # plugin matches Allocates in landing order (gpushare.amd.com/allocate-order=landing, native/engine/
+        # allocstate.h), where binds need no order; relaxed: every bind is concurrent and the device plugin's
+        # reconciliation with kubelet (deviceplugin/reconcile.py) repairs the swaps that can follow
         self.bind_order = bind_order
-        self.engine.set_relaxed_order(bind_order == "relaxed")
+        self.engine.set_bind_order(bind_order)
         self.metrics = Metrics(self.engine)
         if native_controller:
             self.controller = NativeController(client, self.engine, profile, resync_period=resync_period)

@@ -13,6 +13,9 @@ from dataclasses import asdict, dataclass, replace
 # Annotations that are ours (not in the reference) and profile-independent.
 NODE_DEVICE_MEMORY_ANNOTATION = "gpushare.amd.com/device-memory"  # "268,268,..." per-device totals
 NODE_DEVICE_INFO_ANNOTATION = "gpushare.amd.com/devices"  # JSON device inventory from the plugin
+# "landing": the node's device plugin matches an Allocate to the earliest pod *landed* on the node (kubelet's
+# admission order, native/engine/allocstate.h); the extender then needs no ASSUME_TIME order of binds there
+NODE_ALLOCATE_ORDER_ANNOTATION = "gpushare.amd.com/allocate-order"
 POD_CU_MASK_ANNOTATION = "gpushare.amd.com/cu-mask"  # per-pod CU partition (isolation)
 POD_CU_COUNT_ANNOTATION = "gpushare.amd.com/cu-count"  # the pod asks for a CU partition of this size
 POD_ASSIGN_TIME_ANNOTATION = "gpushare.amd.com/assign-time"

@@ -130,7 +130,7 @@ def start_apiserver(history: int = 200000, threads: int | None = None, cpus: lis
 
 def start_extender(apiserver: str, profile: str = "shared-gpu", bind_mode: str = "binding", threadness: int = 1,
                    log_level: str = "warning", port: int = 0, cpus: list[int] | None = None,
-                   kube_qps: float = 0.0, kube_burst: int = 1000, bind_order: str = "strict") -> ChildProc:
+                   kube_qps: float = 0.0, kube_burst: int = 1000, bind_order: str = "auto") -> ChildProc:
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.extender", "--host", "127.0.0.1", "--port", str(port),
                       "--apiserver", apiserver, "--profile", profile, "--bind-mode", bind_mode,
                       "--bind-order", bind_order,

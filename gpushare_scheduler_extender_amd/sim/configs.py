@@ -43,7 +43,7 @@ import time
 from ..k8s.client import KubeClient
 from ..k8s.fasthttp import Client as HttpClient
 from ..k8s.objects import make_node, make_pod
-from ..models.profile import (ALIYUN, NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION,
+from ..models.profile import (ALIYUN, NODE_ALLOCATE_ORDER_ANNOTATION, NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION,
                               POD_CU_MASK_ANNOTATION, POD_HOLD_IDX_ANNOTATION, SHARED_GPU, NamingProfile)
 from .cluster import start_apiserver, start_extender, start_node_agent, start_scheduler
 
@@ -128,6 +128,8 @@ class Cluster:
                for i, t in enumerate(self.totals)]
         node = make_node(NODE, sum(self.totals), len(self.totals), profile=self.profile, device_totals=self.totals,
                          annotations={NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv),
+                                      # what the device plugin publishes: its matcher is landing-ordered
+                                      NODE_ALLOCATE_ORDER_ANNOTATION: "landing",
                                       NODE_RUNTIME_ENDPOINTS_ANNOTATION: json.dumps(
                                           {str(i): u for i, u in enumerate(self.rt.urls)})},
                          labels={"gpushare": "true"})
@@ -347,7 +349,8 @@ async def config3(gpu: bool) -> dict:
         bad = cl.rt.verify() if real else 0
         resident = [st.get("resident") for st in cl.rt.stats()]
         # 32 equal-size pods for 8 GPUs of one node: kubelet's Allocate must never be matched to a pod with another
-        # allocation (the extender keeps their binds in ASSUME_TIME order; the plugin matches on ASSUME_TIME)
+        # allocation (the plugin matches in landing order, the order kubelet admits in; the extender binds them
+        # concurrently because the node advertises it)
         ast = await cl.agent_stats()
         mismatch = ast.get("mismatch", 0)
         faithful = "--faithful" in cl.agent_args

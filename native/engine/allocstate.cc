@@ -1,6 +1,7 @@
 #include "allocstate.h"
 
 #include <algorithm>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
@@ -223,7 +224,13 @@ bool older_rv(const std::string& a, const std::string& b) {
   return x < y;
 }
 
-auto order_key(const AllocPod& p) { return std::tie(p.assume_time, p.creation, p.key); }
+auto order_key(const AllocPod& p) { return std::tie(p.landed, p.assume_time, p.creation, p.key); }
+
+int64_t rv_int(const std::string& rv) {
+  char* e = nullptr;
+  long long x = std::strtoll(rv.c_str(), &e, 10);
+  return rv.empty() || *e != '\0' ? -1 : static_cast<int64_t>(x);
+}
 }  // namespace
 
 AllocState::AllocState(std::string node, const std::vector<std::pair<int, std::pair<int, int>>>& devices)
@@ -239,7 +246,13 @@ bool AllocState::observe(const AllocPod& p) {
     release(p.uid);
     return true;
   }
-  pods_[p.uid] = p;
+  // the landing key survives every later copy of the pod (annotation patches, status, our own PATCH response)
+  const int64_t landed = prev != pods_.end() && prev->second.landed != INT64_MAX ? prev->second.landed : -1;
+  AllocPod& cur = pods_[p.uid];
+  cur = p;
+  // no integer resourceVersion (never from an apiserver, whose are etcd revisions): landing unknown, the
+  // order falls back to ASSUME_TIME
+  cur.landed = landed >= 0 ? landed : (rv_int(p.rv) >= 0 ? rv_int(p.rv) : INT64_MAX);
   keys_[p.key] = p.uid;
   if (p.assigned != "true") return true;
   // an assigned pod owns its CU partition (rebuilt after a restart, or another agent's record)

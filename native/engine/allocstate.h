@@ -8,7 +8,17 @@
 // whose ASSIGNED annotation is "false", and flips ASSIGNED to "true" (the commit point).  On top of that:
 //
 //  * candidates: Pending pods of this node, ASSIGNED=false, *_IDX naming one of our GPUs, not claimed by an
-//    Allocate whose ASSIGNED patch is in flight; ordered by (ASSUME_TIME, creationTimestamp, ns/name);
+//    Allocate whose ASSIGNED patch is in flight; ordered by (landing, ASSUME_TIME, creationTimestamp, ns/name).
+//    `landing` is the resourceVersion at which the pod was first seen bound to this node: kubelet admits
+//    the pods of its node one at a time in the order its watch delivers them (one admission batch per watch
+//    event: the apiserver config source pushes every event, kubelet's pod config merges it into an ADD of
+//    the pods it had not seen), and that order is resourceVersion order for every watcher.  So the earliest
+//    landed candidate is the pod kubelet is admitting, whatever order the extender's binds reached the
+//    apiserver in; with binds landing in ASSUME_TIME order (the reference's only guarantee) the two keys
+//    agree.  The plugin advertises this on its node (gpushare.amd.com/allocate-order=landing) and the
+//    extender then binds equal-size pods for different GPUs concurrently (ledger.h, bind ordering).  Only a
+//    multi-pod admission batch (kubelet's initial LIST after a restart, sorted by creationTimestamp) can
+//    still disagree; deviceplugin/reconcile.py repairs those from kubelet's PodResources record;
 //  * multi-container pods: kubelet calls Allocate once per container.  The first container commits the pod;
 //    the remaining container sizes are kept until allocated ("partial").  After a restart the progress of an
 //    ASSIGNED=true Pending pod is unknown, so any of its sizes is accepted again;
@@ -67,6 +77,7 @@ struct AllocPod {
   int64_t request = 0;        // sum of container limits
   std::vector<int64_t> containers;  // container limits > 0, in spec order
   int64_t assume_time = -1;
+  int64_t landed = -1;        // set by AllocState::observe: resourceVersion first seen bound to the node
   int64_t dev_total = -1;     // *_DEV annotation
   std::string assigned;       // ASSIGNED annotation value ("" absent)
   bool complete = false;

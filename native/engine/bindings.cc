@@ -504,8 +504,18 @@ class Engine {
     return out;
   }
 
-  void set_relaxed_order(bool on) { l_.set_relaxed_order(on); }
-  bool relaxed_order() const { return l_.relaxed_order(); }
+  void set_bind_order(const std::string& m) {
+    if (m == "auto") {
+      l_.set_order_mode(Ledger::kOrderAuto);
+    } else if (m == "strict") {
+      l_.set_order_mode(Ledger::kOrderStrict);
+    } else if (m == "relaxed") {
+      l_.set_order_mode(Ledger::kOrderRelaxed);
+    } else {
+      throw py::value_error("bind order must be auto, strict or relaxed");
+    }
+  }
+  std::string bind_order() const { return Ledger::order_mode_name(l_.order_mode()); }
 
   void set_update_mode(bool on) {
     update_mode_ = on;
@@ -1187,8 +1197,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("drain_bind_failures", &Engine::drain_bind_failures)
       .def("set_binds_enabled", &Engine::set_binds_enabled)
       .def("set_update_mode", &Engine::set_update_mode)
-      .def("set_relaxed_order", &Engine::set_relaxed_order)
-      .def_property_readonly("relaxed_order", &Engine::relaxed_order)
+      .def("set_bind_order", &Engine::set_bind_order)
+      .def_property_readonly("bind_order", &Engine::bind_order)
       .def("drain_annotation_repairs", &Engine::drain_annotation_repairs)
       .def("pending_count", &Engine::pending_count);
 

@@ -64,6 +64,7 @@ bool Ledger::upsert_node(const NodeView& nv) {
     n.total = nv.total;
     n.count = nv.count;
     n.dev_totals_override = nv.dev_totals;
+    n.landing_order = nv.landing_order;
     // adopt pods that arrived before their node
     for (auto& kv : pods_) {
       if (kv.second.node == nv.name) n.pods.insert(kv.first);
@@ -74,6 +75,7 @@ bool Ledger::upsert_node(const NodeView& nv) {
   }
   NodeState& n = it->second;
   n.address = nv.address;
+  n.landing_order = nv.landing_order;
   if (n.total == nv.total && n.count == nv.count && n.dev_totals_override == nv.dev_totals) return false;
   n.total = nv.total;
   n.count = nv.count;
@@ -270,12 +272,25 @@ int64_t Ledger::assume_ordered(const std::string& uid, const std::string& ns, co
   auto pit = pods_.find(uid);
   if (pit != pods_.end()) pit->second.assume_ns = last_assume_ns_;
   *seq = ++order_seq_;
-  inflight_.push_back(InflightBind{node, req, dev, *seq, cu_count});
+  inflight_.push_back(InflightBind{node, req, dev, *seq, cu_count, node_ordered_locked(node)});
   return dev;
 }
 
+bool Ledger::node_ordered_locked(const std::string& node) const {
+  switch (order_mode()) {
+    case kOrderStrict:
+      return true;
+    case kOrderRelaxed:
+      return false;
+    default: {
+      auto it = nodes_.find(node);
+      return it == nodes_.end() || !it->second.landing_order;
+    }
+  }
+}
+
 bool Ledger::blocked_locked(const InflightBind& me) const {
-  if (relaxed_order_.load(std::memory_order_relaxed)) return false;
+  if (!me.ordered) return false;
   for (const auto& f : inflight_) {
     if (f.seq < me.seq && f.node == me.node && f.size == me.size && (f.dev != me.dev || f.cu_count != me.cu_count)) {
       return true;

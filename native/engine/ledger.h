@@ -80,6 +80,7 @@ struct NodeState {
   std::vector<int64_t> dev_totals_override;
   std::vector<DevState> devs;
   std::unordered_set<std::string> pods;  // uids whose rec.node == name
+  bool landing_order = false;            // NodeView::landing_order
   bool gpushare() const { return total > 0 && count > 0; }
 };
 
@@ -114,11 +115,20 @@ class Ledger {
   int pod_state(const std::string& uid, int64_t* dev) const;
   // Binds observed without their annotations since the last call (see AnnotationRepair)
   std::vector<AnnotationRepair> drain_repairs();
-  // "relaxed": no bind waits for another (see bind ordering below).  Safe only where the device plugin
-  // reconciles its Allocates with kubelet's PodResources record (deviceplugin/reconcile.py), which rewrites
-  // the annotations of pods kubelet started with each other's allocation.
-  void set_relaxed_order(bool on) { relaxed_order_.store(on); }
-  bool relaxed_order() const { return relaxed_order_.load(); }
+  // Bind order (see bind ordering below):
+  //   kOrderAuto (default): ASSUME_TIME order on nodes whose device plugin matches by ASSUME_TIME (the
+  //     reference's contract), none on nodes that advertise landing-order matching (allocstate.h);
+  //   kOrderStrict: ASSUME_TIME order everywhere;
+  //   kOrderRelaxed: no bind waits for another anywhere.  Safe only where the device plugin reconciles its
+  //     Allocates with kubelet's PodResources record (deviceplugin/reconcile.py).
+  enum OrderMode : int { kOrderAuto = 0, kOrderStrict = 1, kOrderRelaxed = 2 };
+  void set_order_mode(OrderMode m) { order_mode_.store(m); }
+  OrderMode order_mode() const { return static_cast<OrderMode>(order_mode_.load()); }
+  static const char* order_mode_name(OrderMode m) {
+    return m == kOrderStrict ? "strict" : m == kOrderRelaxed ? "relaxed" : "auto";
+  }
+  // true: binds to this node wait for earlier equal-size binds headed for another GPU
+  bool node_ordered_locked(const std::string& node) const;
 
   // ---- scheduling verbs ----
   Check check(const std::string& node, int64_t req) const;  // nodeinfo.go:113-137
@@ -210,11 +220,12 @@ class Ledger {
     int64_t size, dev;
     uint64_t seq;
     std::string cu_count;
+    bool ordered = true;                        // node_ordered_locked() when the bind was assumed
     std::condition_variable* waiter = nullptr;  // set while its bind sits in bind_wait()
   };
   bool blocked_locked(const InflightBind& me) const;
   std::mutex order_mu_;
-  std::atomic<bool> relaxed_order_{false};
+  std::atomic<int> order_mode_{kOrderAuto};
   std::list<InflightBind> inflight_;
   uint64_t order_seq_ = 0;
   int64_t last_assume_ns_ = 0;

@@ -63,7 +63,12 @@ struct NodeView {
   int64_t count = 0;  // capacity[count] (node.go:24-30)
   std::vector<int64_t> dev_totals;  // optional per-device totals annotation
   std::string address;              // first InternalIP (kubectl-inspect output)
+  // the node's device plugin matches Allocates in landing order (annotation gpushare.amd.com/allocate-order
+  // = "landing", published by deviceplugin/plugin.py): binds need no ASSUME_TIME order there (ledger.h)
+  bool landing_order = false;
 };
+
+inline constexpr const char* kAllocateOrderAnnotation = "gpushare.amd.com/allocate-order";
 
 // Extract a PodView from the pod object at tape index `pod`.
 bool parse_pod(const json::Doc& d, uint32_t pod, const Profile& p, PodView* out);

@@ -35,11 +35,11 @@ fi
 if [ "$STAGE" = all ] || [ "$STAGE" = scale ]; then
   for n in 2 4 8; do
     timeout -k 10 600 python bench.py --gpus $n --steps 20 --warmup 5 --devices fake --sweep 1 --sweep-steps 4 \
-      --json-out $OUT/fake_n$n.json > $OUT/fake_n$n.log 2>&1 || exit $?
+      --sweep-orders ${SWEEP_ORDERS:-auto} --json-out $OUT/fake_n$n.json > $OUT/fake_n$n.log 2>&1 || exit $?
     python -c "
 import json; d=json.load(open('$OUT/fake_n$n.json'))
 print('fake n$n', d['value'], d['wave_pods_per_s']['p50'], d['timed_region_ms']['max_over_ranks'])
 for r in d['latency_sweep'] or []:
-    print('   ', r.get('bind_mode'), r.get('api_latency_ms'), r.get('pods_per_s'), r.get('bind_order_waits'), r.get('bind_order_wait_ms_per_wave'))"
+    print('   ', r.get('bind_mode'), r.get('bind_order'), r.get('api_latency_ms'), r.get('pods_per_s'), r.get('bind_order_waits'), r.get('bind_order_wait_ms_per_wave'))"
   done
 fi

@@ -57,15 +57,16 @@ def _committed_use(cl, bound: dict) -> tuple[list[int], int]:
                                                   (29, "faithful", "update")])
 def test_chaos_whole_stack_converges_without_overcommit(seed, agent, bind_mode):
     """``agent``: kubelet + the shipped gRPC device plugin
-    (the product path), the same behind a *faithful* kubelet (no re-routing, creationTimestamp-sorted batches,
-    PodResources reconciliation), or the compiled node agent; ``bind_mode``: one annotated Binding, or the
+    (the product path), the same behind a *faithful* kubelet (no re-routing, PodResources reconciliation; here
+    with 20 ms creationTimestamp-sorted admission batches, kubelet's restart case, so swaps do happen), or the
+    compiled node agent; ``bind_mode``: one annotated Binding, or the
     reference's annotation write + Binding (two calls, the first guarded by resourceVersion)."""
     faithful = agent == "faithful"
 
     async def go():
         rnd = random.Random(seed)
         cl = Cluster(ALIYUN, [96] * 4, gpu=False, agent="plugin" if faithful else agent,
-                     bind_mode=bind_mode, agent_args=["--faithful"] if faithful else [])
+                     bind_mode=bind_mode, agent_args=["--faithful", "--batch-window", "0.02"] if faithful else [])
         try:
             await cl.start()
             api = HttpClient(cl.api.url)

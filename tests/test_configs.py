@@ -32,14 +32,17 @@ def test_configs_agree_across_agents(agent, tmp_path):
 
 @pytest.mark.parametrize("latency_ms", [0, 5])
 def test_config3_through_a_faithful_kubelet(latency_ms, tmp_path):
-    """32 x 64 GiB on 8 devices with kubelet as it is (no re-routing, creationTimestamp-sorted
-    batches, PodResources reconciliation) at 0 and 5 ms apiserver latency: binpack 4 per device and every
-    container runs on the GPU its annotation names."""
+    """32 x 64 GiB on 8 devices with kubelet as it is (no re-routing, one admission per watch event,
+    PodResources reconciliation) at 0 and 5 ms apiserver latency: binpack 4 per device and every container runs on
+    the GPU its annotation names.  The node advertises landing-order matching, so the extender binds the 32 pods
+    concurrently, in no particular order, and still no Allocate is matched to another pod than the one kubelet
+    admits: nothing is left for reconciliation to repair."""
     out = tmp_path / "r.json"
     rc = configs.main(["--only", "3", "--faithful", "--api-latency-ms", str(latency_ms), "--json-out", str(out)])
     rep = json.loads(out.read_text())["3"]
     assert rc == 0, rep
     assert rep["faithful_kubelet"] and rep["per_device_gib"] == [256] * 8 and rep["physical_drift"] == 0
+    assert rep["allocate_mismatch"] == 0 and rep["reconcile"]["swaps"] == 0, rep
 
 
 @pytest.mark.gpu

@@ -48,6 +48,30 @@ def test_candidate_order_and_pick_by_size():
     assert st.match(8)[0].name == "late"
 
 
+def test_candidates_follow_landing_order_not_assume_time():
+    """kubelet admits a node's pods one at a time in the order its watch delivers them (resourceVersion order), so
+    the plugin serves the earliest *landed* candidate: the resourceVersion at which it was first seen bound here,
+    kept across later copies of the pod (annotation patches); ASSUME_TIME only breaks ties."""
+    st = _state()
+
+    def at(pod, rv):
+        pod["metadata"]["resourceVersion"] = str(rv)
+        return pod
+
+    late = at(bound_pod("late", 8, assume=30, uid="u-late"), 5)   # assumed last, landed first
+    early = at(bound_pod("early", 8, assume=10, uid="u-early"), 9)
+    st.observe(late)
+    st.observe(early)
+    assert [r.name for r in st.candidates()] == ["late", "early"]
+    # a later copy of "late" (e.g. an annotation written back after the binding) keeps its landing
+    st.observe(at(bound_pod("late", 8, assume=30, uid="u-late", annotations={"x": "y"}), 12))
+    assert st.match(8)[0].name == "late"
+    # a pod first seen unbound and then bound lands when it is bound
+    st.observe(at(bound_pod("mid", 8, assume=1, uid="u-mid", node=""), 3))
+    st.observe(at(bound_pod("mid", 8, assume=1, uid="u-mid"), 14))
+    assert [r.name for r in st.candidates()] == ["late", "early", "mid"]
+
+
 def test_state_releases_cus_and_partial_on_completion_and_delete():
     st = _state("1x64GiB")
     a = bound_pod("a", 16, annotations={CU_COUNT_ANNOTATION: "64"})
@@ -285,7 +309,8 @@ def test_plugin_register_listandwatch_allocate():
             stream = pc.list_and_watch()
             first = await stream.read()
             assert len(first.devices) == 32 and all(x.health == "Healthy" for x in first.devices)
-            # two bound pods of 8 on GPU1; the earlier ASSUME_TIME wins the first Allocate
+            # two bound pods of 8 on GPU1: "b" lands first (its ASSUME_TIME is the later one).  kubelet admits pods
+            # in the order they land, so the first Allocate is b's (landing order, native/engine/allocstate.h)
             await client.create("pods", bound_pod("b", 8, dev=1, assume=20, dev_total=16))
             await client.create("pods", bound_pod("a", 8, dev=1, assume=10, dev_total=16))
             ids = fake_ids(devs[0], 16) + fake_ids(devs[1], 16)
@@ -297,11 +322,13 @@ def test_plugin_register_listandwatch_allocate():
             assert [x.host_path for x in r.container_responses[0].devices][0] == "/dev/kfd"
             a = await client.get("pods", "a", "default")
             b = await client.get("pods", "b", "default")
-            assert a["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
-            assert b["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "false"
-            await pc.allocate([ids[:8]])
-            b = await client.get("pods", "b", "default")
             assert b["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
+            assert a["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "false"
+            await pc.allocate([ids[:8]])
+            a = await client.get("pods", "a", "default")
+            assert a["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
+            node = await client.get("nodes", "n1")
+            assert node["metadata"]["annotations"]["gpushare.amd.com/allocate-order"] == "landing"
             # nothing left to match
             with pytest.raises(Exception) as ei:
                 await pc.allocate([ids[:8]])

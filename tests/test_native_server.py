@@ -456,3 +456,53 @@ def test_bind_order_spans_native_and_python_paths():
         finally:
             await _teardown(api, c, ext)
     asyncio.run(go())
+
+
+@pytest.mark.parametrize("order,landing,want", [("auto", True, ["b", "a"]), ("auto", False, ["a", "b"]),
+                                                ("strict", True, ["a", "b"]), ("relaxed", False, ["b", "a"])])
+def test_bind_order_follows_the_nodes_allocate_order(order, landing, want):
+    """``--bind-order auto`` (default): equal-size binds for different GPUs of a node wait for each other (ASSUME_TIME
+    order, for a plugin that matches by ASSUME_TIME) unless the node's device plugin advertises landing-order
+    matching (``gpushare.amd.com/allocate-order=landing``, native/engine/allocstate.h): then b, bound while a's
+    binding is slow, lands first.  ``strict`` orders every node, ``relaxed`` none."""
+    async def go():
+        import aiohttp
+
+        from gpushare_scheduler_extender_amd.models.profile import NODE_ALLOCATE_ORDER_ANNOTATION
+
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        node = make_node("n", 2 * 16, 2)
+        if landing:
+            node["metadata"].setdefault("annotations", {})[NODE_ALLOCATE_ORDER_ANNOTATION] = "landing"
+        await c.create("nodes", node)
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), bind_order=order), native=True,
+                                   http_threads=2).start()
+        try:
+            pa = await c.create("pods", make_pod("a", 10))
+            pb = await c.create("pods", make_pod("b", 10))
+            for _ in range(300):
+                if ext.server.engine.has_node("n") and ext.server.controller.get_pod("b", "default"):
+                    break
+                await asyncio.sleep(0.01)
+            async with aiohttp.ClientSession() as s:
+                for p in (pa, pb):
+                    async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(p, ["n"])) as r:
+                        assert json.loads(await r.read())["NodeNames"] == ["n"]
+
+                async def bind(p):
+                    async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
+                            p["metadata"]["name"], "default", p["metadata"]["uid"], "n").encode()) as r:
+                        assert r.status == 200, await r.read()
+
+                api.server.faults.slow_bindings = {"a": 300.0}
+                ta = asyncio.create_task(bind(pa))
+                await asyncio.sleep(0.05)
+                await asyncio.gather(ta, bind(pb))
+            assert api.server.binding_log == want
+            got = {n: (await c.get("pods", n, "default"))["metadata"]["annotations"] for n in ("a", "b")}
+            assert [got[n]["SHARED_GPU_MEM_IDX"] for n in ("a", "b")] == ["0", "1"]
+            assert ext.server.engine.bind_order == order
+        finally:
+            await _teardown(api, c, ext)
+    asyncio.run(go())

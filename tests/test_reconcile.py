@@ -43,7 +43,8 @@ async def _wait(pred, timeout=30.0, what=""):
 
 
 async def _swap_scenario(reconcile: bool, plugin: str = "grpc"):
-    args = ["--faithful", "--plugin", plugin] + ([] if reconcile else ["--no-reconcile"])
+    # kubelet restarting meets the pods of its initial LIST as one creationTimestamp-sorted batch
+    args = ["--faithful", "--batch-window", "0.02", "--plugin", plugin] + ([] if reconcile else ["--no-reconcile"])
     cl = Cluster(ALIYUN, [96] * 4, gpu=False, agent="plugin", agent_args=args)
     try:
         await cl.start()
