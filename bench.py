@@ -576,6 +576,8 @@ def main():
                for d in devs_]
         node = make_node(NODE, sum(totals), len(totals), profile=profile, device_totals=totals,
                          annotations={NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv),
+                                      # as the device plugin publishes it: its matcher is landing-ordered
+                                      NODE_ALLOCATE_ORDER_ANNOTATION: "landing",
                                       NODE_RUNTIME_ENDPOINTS_ANNOTATION: json.dumps(
                                           {str(d.index): u for d, (_, u) in zip(devs_, all_devs)})})
         node["metadata"].setdefault("labels", {})["gpushare"] = "true"

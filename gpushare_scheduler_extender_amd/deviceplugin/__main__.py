@@ -87,9 +87,23 @@ def main(argv=None) -> int:
         logging.getLogger("gsx.main").warning(
             "stopping: %s; grpc %s; per Allocate ms: %s", plugin.stats, plugin.debug_state().get("grpc"),
             {k: round(1e3 * v / n, 4) for k, v in plugin.timing.items() if isinstance(v, float)})
+        if os.environ.get("GSX_PLUGIN_CPROFILE_DIR"):
+            import json  # noqa: PLC0415
+
+            with open(os.path.join(os.environ["GSX_PLUGIN_CPROFILE_DIR"], f"plugin-{os.getpid()}.json"), "w") as f:
+                json.dump({"stats": plugin.stats, "debug": plugin.debug_state(), "timing": plugin.timing}, f,
+                          default=str)
         await plugin.stop()
         await client.close()
 
+    prof_dir = os.environ.get("GSX_PLUGIN_CPROFILE_DIR")  # diagnosis: where the plugin process spends its time
+    if prof_dir:
+        import cProfile  # noqa: PLC0415
+
+        prof = cProfile.Profile()
+        prof.runcall(asyncio.run, run())
+        prof.dump_stats(os.path.join(prof_dir, f"plugin-{os.getpid()}.prof"))
+        return 0
     asyncio.run(run())
     return 0
 

@@ -37,6 +37,7 @@ from __future__ import annotations
 import asyncio
 import logging
 import os
+import sys
 import time
 
 import grpc
@@ -139,6 +140,7 @@ class GpuSharePlugin:
         self._stopped = False
         self._server: grpc.aio.Server | None = None
         self._native = None  # _engine.DpServer: the gRPC endpoint in native code (default)
+        self._native_fd = -1  # what the loop watches for it (the serving thread's eventfd, or its epoll fd)
         self.grpc_impl = ""
         self._slow: set[asyncio.Task] = set()
         self._tasks: list[asyncio.Task] = []
@@ -315,7 +317,7 @@ class GpuSharePlugin:
     def _close_native(self):
         if self._native is not None:
             try:
-                asyncio.get_running_loop().remove_reader(self._native.fd())
+                asyncio.get_running_loop().remove_reader(self._native_fd)
             except RuntimeError:
                 pass
             self._native.close()
@@ -708,7 +710,14 @@ class GpuSharePlugin:
             if os.environ.get("GSX_PLUGIN_FEED", "1") == "1":
                 self._native.start_feed(cfg["api"])  # this node's pods into the state from a native reflector
             self._sync_native()
-            asyncio.get_running_loop().add_reader(self._native.fd(), self._native_poll)
+            if os.environ.get("GSX_PLUGIN_SERVE_THREAD", "1") == "1":
+                # the endpoint is served from a native thread (the GIL guards the shared state); a short switch
+                # interval bounds how long it waits for the GIL while this loop runs Python
+                self._native_fd = self._native.start_serving()
+                sys.setswitchinterval(min(sys.getswitchinterval(), 0.0005))
+            else:
+                self._native_fd = self._native.fd()
+            asyncio.get_running_loop().add_reader(self._native_fd, self._native_poll)
             self.grpc_impl = "native"
             return
         log.info("device-plugin endpoint on grpcio (%s)", why)

@@ -5,6 +5,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <poll.h>
+#include <pthread.h>
 #include <sys/eventfd.h>
 #include <sys/timerfd.h>
 #include <time.h>
@@ -746,10 +748,25 @@ class PyDpServer {
     worker_ = std::thread([this] { work(); });
   }
   ~PyDpServer() {
+    stop_serving();
     if (feed_r_) feed_r_->stop();
     stop_worker();
     if (efd_ >= 0) ::close(efd_);
     if (tfd_ >= 0) ::close(tfd_);
+    if (pyfd_ >= 0) ::close(pyfd_);
+  }
+
+  // Serve from a native thread instead of the owner's event loop: accept, read, the fast paths, the pod feed
+  // and the patch completions run as soon as their fd is ready, however busy the Python loop is (its own pod
+  // informer decodes every event of the node).  The GIL is the state mutex: every Python call into the
+  // AllocState holds it, and the thread holds it for each pass (microseconds of C++).  Returns an eventfd that
+  // turns readable when calls for the Python slow path or fast-path events wait for poll().
+  int start_serving() {
+    if (serving_.joinable()) return pyfd_;
+    pyfd_ = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    stop_serving_ = false;
+    serving_ = std::thread([this] { serve(); });
+    return pyfd_;
   }
 
   // This node's pods straight into the allocation state from a native reflector (the plugin's Python informer,
@@ -785,12 +802,12 @@ class PyDpServer {
   int fd() const { return srv_ ? srv_->fd() : -1; }
 
   py::tuple poll() {
-    drain_feed();
-    if (srv_) srv_->poll();
-    drain_feed();
-    retry_waiting(false);
-    finish_patches();
-    retry_waiting(true);
+    if (serving_.joinable()) {
+      uint64_t n;
+      (void)!::read(pyfd_, &n, sizeof n);  // the serving thread did the pass; collect what it left for Python
+    } else {
+      one_pass();
+    }
     py::list pending, events;
     for (auto& p : pending_) pending.append(py::make_tuple(std::get<0>(p), std::get<1>(p), py::bytes(std::get<2>(p))));
     pending_.clear();
@@ -810,6 +827,16 @@ class PyDpServer {
     }
     events_.clear();
     return py::make_tuple(pending, events);
+  }
+
+  void one_pass() {
+    drain_feed();
+    if (srv_) srv_->poll();
+    drain_feed();
+    retry_waiting(false);
+    finish_patches();
+    retry_waiting(true);
+    passes_++;
   }
 
   bool respond(uint64_t call, int status, const py::bytes& payload) {
@@ -851,10 +878,13 @@ class PyDpServer {
     d["waited"] = waited_;
     d["feed_events"] = feed_events_;
     d["feed"] = static_cast<bool>(feed_r_);
+    d["serving_thread"] = serving_.joinable();
+    d["passes"] = passes_;
     return d;
   }
 
   void close() {
+    stop_serving();
     if (feed_r_) feed_r_->stop();
     stop_worker();
     finish_patches();
@@ -909,6 +939,32 @@ class PyDpServer {
     } else {
       s.respond(call.id, 12, "unknown method " + m);
     }
+  }
+
+  void serve() {
+    pthread_setname_np(pthread_self(), "gsx-dp-serve");
+    const int ep = srv_ ? srv_->fd() : -1;
+    for (;;) {
+      pollfd pf{ep, POLLIN, 0};
+      ::poll(&pf, 1, 100);  // GIL released: the Python loop runs meanwhile
+      py::gil_scoped_acquire gil;
+      if (stop_serving_ || !srv_) return;
+      one_pass();
+      if (!pending_.empty() || !events_.empty()) {
+        uint64_t one = 1;
+        (void)!::write(pyfd_, &one, sizeof one);
+      }
+    }
+  }
+
+  // GIL held by the caller (close / the destructor): released while the thread finishes its pass
+  void stop_serving() {
+    if (!serving_.joinable()) return;
+    stop_serving_ = true;
+    uint64_t one = 1;
+    (void)!::write(efd_, &one, sizeof one);
+    py::gil_scoped_release nogil;
+    serving_.join();
   }
 
   static constexpr const char* kNoCandidate = "no candidate";
@@ -1101,6 +1157,11 @@ class PyDpServer {
   std::vector<DpEvent> events_;
   std::string device_list_, last_why_;
   bool have_list_ = false, fast_ = true;
+  // start_serving(): the pass runs on this thread, the GIL as the state mutex
+  std::thread serving_;
+  bool stop_serving_ = false;  // GIL held
+  int pyfd_ = -1;              // readable: pending_ / events_ waiting for poll()
+  uint64_t passes_ = 0;
 };
 
 PYBIND11_MODULE(_engine, m) {
@@ -1467,6 +1528,7 @@ PYBIND11_MODULE(_engine, m) {
       .def(py::init<const std::string&, AllocState&, const py::dict&>(), py::keep_alive<1, 3>())
       .def("fd", &PyDpServer::fd)
       .def("poll", &PyDpServer::poll)
+      .def("start_serving", &PyDpServer::start_serving)
       .def("respond", &PyDpServer::respond)
       .def("set_devices", &PyDpServer::set_devices)
       .def("set_device_list", &PyDpServer::set_device_list)
