@@ -445,7 +445,7 @@ def main():
     # single CPU the endpoint thread waited behind gloo's threads for up to 9 ms (N=4/8 rehearsal, 2 CPUs fix it)
     widths.update({f"rank{r}": 2 for r in range(1, world)})
     if a.pin_widths:
-        widths = json.loads(a.pin_widths)
+        widths.update(json.loads(a.pin_widths))
     mode = a.pin if a.pin != "auto" else "spread"
     if world > 1 and mode != "none":
         # one plan for the whole job (the ranks' load samples would differ): keyed by the torchrun agent

@@ -112,20 +112,25 @@ def tool_path(name: str) -> Path:
 FAKEAPI = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-fakeapi"
 
 
-def start_apiserver(history: int = 200000, threads: int | None = None, cpus: list[int] | None = None) -> ChildProc:
+def start_apiserver(history: int = 200000, threads: int | None = None, cpus: list[int] | None = None,
+                    watch_loop: bool | None = None) -> ChildProc:
     """Fake kube-apiserver: the compiled ``gsx-fakeapi`` (native/fakeapi).  (``tests/fixtures/fakeapi.py`` is its
     in-process test-only twin.)
 
     ``threads``: event loops of the native server (default ``GSX_FAKEAPI_THREADS`` or 1).
     ``GSX_FAKEAPI_WATCH_FLUSH``: ``iteration`` (default) or ``request`` -- when watch events are pushed.
+    ``GSX_FAKEAPI_WATCH_LOOP=1``: with 2+ threads, loop 0 serves only the watch streams (``--watch-loop``).
     """
     exe = tool_path("gsx-fakeapi")
     if not exe.exists():
         raise FileNotFoundError(f"{exe} missing; run `python native/build.py fakeapi`")
     threads = threads or int(os.environ.get("GSX_FAKEAPI_THREADS", "1"))
     flush = os.environ.get("GSX_FAKEAPI_WATCH_FLUSH", "iteration")
+    if watch_loop is None:
+        watch_loop = os.environ.get("GSX_FAKEAPI_WATCH_LOOP", "0") == "1"
+    extra = ["--watch-loop"] if watch_loop else []
     return ChildProc([str(exe), "--port", "0", "--history", str(history), "--threads", str(threads),
-                      "--watch-flush", flush], "apiserver", cpus=cpus)
+                      "--watch-flush", flush, *extra], "apiserver", cpus=cpus)
 
 
 def start_extender(apiserver: str, profile: str = "shared-gpu", bind_mode: str = "binding", threadness: int = 1,

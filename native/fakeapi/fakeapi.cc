@@ -27,6 +27,11 @@
 // revision order and sent by the loop that owns the watch connection (woken
 // through its eventfd), one chunk per watcher per loop iteration.
 //
+// --watch-loop (with --threads N >= 2): loop 0 serves only watch streams and has no listener; loops 1..N-1
+// accept and serve requests.  A request that becomes a watch is handed over with its connection, so a write
+// emits its events to watcher buffers (state mutex) and at most one eventfd wakes the watch loop per batch;
+// the request loops never send watch chunks and never wake each other.
+//
 // Default 1 loop.  Measured on the MI355X box (bench.py, fake devices, N=8:
 // 32 pods per wave, ~5 writes per pod): 4 loops were slower (10.7k vs 13.6k
 // pods/s) -- each write is still serialised under the mutex, its hold time
@@ -36,7 +41,7 @@
 // chain of dependent writes.  GET /fake/stats reports lock wait / hold times.
 //
 //   gsx-fakeapi [--host 127.0.0.1] [--port 0] [--port-file F] [--history N] [--threads N]
-//               [--watch-flush request|iteration]
+//               [--watch-flush request|iteration] [--watch-loop]
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -301,6 +306,7 @@ struct Conn {
   std::string rbuf, wbuf;
   bool want_close = false;
   bool busy = false;                // a delayed response is pending
+  bool handoff = false;             // became a watch owned by the watch loop: moves there after this request
   std::shared_ptr<Watcher> watch;   // streaming
   bool epollout = false;
 };
@@ -318,6 +324,7 @@ struct Watcher {
   std::atomic<bool> closed{false};  // written under the state mutex, read anywhere
   bool dirty = false;          // queued on owner->dirty
   bool end_requested = false;  // another loop asked the owner to end it
+  bool adopted = true;         // its connection is in owner->conns (false while handed over to the watch loop)
 };
 
 struct Delayed {
@@ -341,6 +348,7 @@ struct Loop {
   std::vector<Delayed> delayed;
   std::vector<Held> held;
   std::vector<std::shared_ptr<Watcher>> dirty;
+  std::vector<std::unique_ptr<Conn>> inbox;  // watch connections handed over by request loops (state mutex)
   bool signaled = false;
   std::atomic<bool> has_dirty{false};  // `dirty` is non-empty (checked before taking the mutex)
   // owner-written, read by /fake/stats
@@ -418,8 +426,9 @@ class StateLock {
 
 class Server {
  public:
-  Server(size_t history, int threads, bool flush_per_request)
-      : history_max_(history), nloops_(std::max(1, std::min(64, threads))), flush_per_request_(flush_per_request) {
+  Server(size_t history, int threads, bool flush_per_request, bool watch_loop)
+      : history_max_(history), nloops_(std::max(1, std::min(64, threads))), flush_per_request_(flush_per_request),
+        watch_loop_(watch_loop && nloops_ >= 2) {
     for (const char* k : {"pods", "nodes", "events", "leases"}) store_[k];
   }
 
@@ -428,6 +437,16 @@ class Server {
     for (int i = 0; i < nloops_; ++i) {
       auto L = std::make_unique<Loop>();
       L->idx = i;
+      if (watch_loop_ && i == 0) {  // the watch loop: no listener, only its eventfd and adopted connections
+        L->ep = epoll_create1(EPOLL_CLOEXEC);
+        L->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+        epoll_event ev;
+        ev.events = EPOLLIN;
+        ev.data.u64 = kWakeId;
+        epoll_ctl(L->ep, EPOLL_CTL_ADD, L->efd, &ev);
+        loops_.push_back(std::move(L));
+        continue;
+      }
       L->lfd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
       int one = 1;
       setsockopt(L->lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
@@ -476,6 +495,7 @@ class Server {
       int timeout = next_timeout_ms(L);
       int n = epoll_wait(L->ep, evs.data(), static_cast<int>(evs.size()), timeout);
       double t_iter = now_s();
+      if (watch_loop_ && L->idx == 0) adopt_watches(L);
       for (int i = 0; i < n; ++i) {
         uint64_t id = evs[i].data.u64;
         if (id == kListenId) {
@@ -634,8 +654,54 @@ class Server {
     }
     if (reply) {
       respond(L, c, rep, req.keep_alive);
+    } else if (c->handoff) {
+      hand_over(L, c);
     } else if (!c->wbuf.empty() || c->want_close) {
       flush_conn(L, c);
+    }
+  }
+
+  // A request loop's connection that became a watch: off this loop's epoll, into the watch loop's inbox.
+  void hand_over(Loop* L, Conn* c) {
+    c->handoff = false;
+    epoll_ctl(L->ep, EPOLL_CTL_DEL, c->fd, nullptr);
+    auto it = L->conns.find(c->id);
+    std::unique_ptr<Conn> up = std::move(it->second);
+    L->conns.erase(it);
+    Loop* W = loops_[0].get();
+    StateLock g(smu_, lstats_);
+    W->inbox.push_back(std::move(up));
+    W->signaled = true;
+    wake(W);
+  }
+
+  // The watch loop: take over the handed-over connections, then send what their watchers hold.
+  void adopt_watches(Loop* L) {
+    std::vector<std::unique_ptr<Conn>> in;
+    {
+      StateLock g(smu_, lstats_);
+      if (L->inbox.empty()) return;
+      in.swap(L->inbox);
+      for (auto& c : in) {
+        c->watch->adopted = true;
+        if (c->watch->closed) continue;
+        L->mine.push_back(c->watch);
+        mark_dirty_locked(c->watch);  // no-op if an event already queued it here (flushed once adopted)
+      }
+    }
+    for (auto& c : in) {
+      Conn* raw = c.get();
+      if (raw->watch->closed) {
+        ::close(raw->fd);
+        continue;
+      }
+      epoll_event ev;
+      ev.events = EPOLLIN | EPOLLRDHUP;
+      ev.data.u64 = raw->id;
+      epoll_ctl(L->ep, EPOLL_CTL_ADD, raw->fd, &ev);
+      raw->epollout = false;
+      L->conns[raw->id] = std::move(c);
+      flush_conn(L, raw);  // the response head (and anything the request loop had queued)
     }
   }
 
@@ -850,7 +916,7 @@ class Server {
       if (L->dirty.empty()) return false;
       for (auto& w : L->dirty) {
         w->dirty = false;
-        if (w->closed) continue;
+        if (w->closed || !w->adopted) continue;  // not adopted yet: adopt_watches re-queues it
         Out o{w, std::move(w->pending), w->end_requested};
         w->pending.clear();
         // one chunk per loop iteration; count events for drop_watch_after
@@ -976,8 +1042,14 @@ class Server {
     }
     c->wbuf.append(head);
     c->watch = w;
-    L->mine.push_back(w);
     watchers_.push_back(w);
+    if (watch_loop_ && L->idx != 0) {
+      w->owner = loops_[0].get();
+      w->adopted = false;
+      c->handoff = true;  // handle() moves the connection after this request
+      return false;
+    }
+    L->mine.push_back(w);
     if (!w->pending.empty()) mark_dirty_locked(w);
     return false;
   }
@@ -1487,6 +1559,7 @@ class Server {
   std::vector<std::unique_ptr<Loop>> loops_;
   LockStats lstats_;
   const bool flush_per_request_;  // --watch-flush request
+  const bool watch_loop_;         // --watch-loop: loop 0 owns every watch stream
   std::atomic<int> ngraces_{0};  // graces_.size(), readable without the mutex
   std::mutex smu_;  // the state below: store, revision, history, watchers, faults, counters, graces
   std::atomic<uint64_t> next_id_{0};
@@ -1509,7 +1582,7 @@ int main(int argc, char** argv) {
   int port = 0;
   size_t history = 200000;
   int threads = 1;
-  bool flush_per_request = false;
+  bool flush_per_request = false, watch_loop = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&]() -> std::string {
@@ -1524,6 +1597,7 @@ int main(int argc, char** argv) {
     else if (a == "--port-file") port_file = val();
     else if (a == "--history") history = static_cast<size_t>(std::max(1, std::atoi(val().c_str())));
     else if (a == "--threads") threads = std::atoi(val().c_str());
+    else if (a == "--watch-loop") watch_loop = true;
     else if (a == "--watch-flush") {
       std::string m = val();
       if (m != "request" && m != "iteration") {
@@ -1533,7 +1607,7 @@ int main(int argc, char** argv) {
       flush_per_request = m == "request";
     } else if (a == "-h" || a == "--help") {
       std::printf("usage: gsx-fakeapi [--host H] [--port P] [--port-file F] [--history N] [--threads N]\n"
-                  "                   [--watch-flush request|iteration]\n");
+                  "                   [--watch-flush request|iteration] [--watch-loop]\n");
       return 0;
     } else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -1546,7 +1620,7 @@ int main(int argc, char** argv) {
   sa.sa_handler = on_sig;
   sigaction(SIGTERM, &sa, nullptr);
   sigaction(SIGINT, &sa, nullptr);
-  Server srv(history, threads, flush_per_request);
+  Server srv(history, threads, flush_per_request, watch_loop);
   std::string err;
   int bound = srv.listen_on(host, port, &err);
   if (bound < 0) {

@@ -126,7 +126,9 @@ __global__ __launch_bounds__(256) void stamp_slices_kernel(SliceTable t, uint64_
 // One launch per admission: grid.y rows [0, n_stamp) stamp the new extents, the other rows verify the resident
 // ones.  Only used when the host has checked that no two extents of the table overlap, so the two kinds of block
 // touch disjoint memory and need no ordering between them; with an overlap the two-launch path runs instead, and the
-// verify launch counts the overwritten stamps.
+// verify launch counts the overwritten stamps.  The stamp rows do not read back what they wrote (the two-launch
+// path verifies fresh stamps in its second launch): in this mode a fresh slice is first verified by the next
+// admission on the device, so the two modes' bad counts differ by the current admission's own new stamps.
 __global__ __launch_bounds__(256) void admit_slices_kernel(SliceTable t, int n_stamp, uint64_t stride,
                                                            unsigned long long* bad) {
   const gsx_slice sl = t.s[blockIdx.y];

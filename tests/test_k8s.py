@@ -25,10 +25,10 @@ def run(coro):
 class _NativeApi:
     """gsx-fakeapi (native/fakeapi) as a child process, with the runner interface the tests use."""
 
-    def __init__(self, history, threads=1):
+    def __init__(self, history, threads=1, watch_loop=False):
         from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver
 
-        self.proc = start_apiserver(history=history, threads=threads)
+        self.proc = start_apiserver(history=history, threads=threads, watch_loop=watch_loop)
         self.url = self.proc.url
 
     async def stop(self):
@@ -38,14 +38,15 @@ class _NativeApi:
 async def _api(history=200000, impl="python"):
     """The asyncio fake apiserver in-process, or the compiled one (same REST semantics)."""
     if impl.startswith("native"):
-        r = _NativeApi(history, threads=4 if impl == "native-mt" else 1)
+        r = _NativeApi(history, threads={"native-mt": 4, "native-wl": 3}.get(impl, 1), watch_loop=impl == "native-wl")
     else:
         r = await FakeApiServerRunner(FakeApiServer(history=history)).start()
     return r, KubeClient(r.url)
 
 
-# native-mt: the compiled server with 4 event loops sharing the store (watch events cross loops)
-IMPLS = pytest.mark.parametrize("impl", ["python", "native", "native-mt"])
+# native-mt: the compiled server with 4 event loops sharing the store (watch events cross loops); native-wl: one
+# loop owning every watch stream (handed over by the request loops that received them) + 2 request loops
+IMPLS = pytest.mark.parametrize("impl", ["python", "native", "native-mt", "native-wl"])
 
 
 # ---------------------------------------------------------------- fake apiserver semantics
@@ -155,7 +156,7 @@ def test_watch_from_compacted_version_is_410(impl):
     run(go())
 
 
-@pytest.mark.parametrize("impl", ["native", "native-mt"])
+@pytest.mark.parametrize("impl", ["native", "native-mt", "native-wl"])
 def test_concurrent_writers_watch_in_revision_order(impl):
     """Many connections writing at once: every watcher sees every event exactly once, in resourceVersion order."""
     async def go():
