@@ -37,7 +37,6 @@ from __future__ import annotations
 import asyncio
 import logging
 import os
-import sys
 import time
 
 import grpc
@@ -711,10 +710,9 @@ class GpuSharePlugin:
                 self._native.start_feed(cfg["api"])  # this node's pods into the state from a native reflector
             self._sync_native()
             if os.environ.get("GSX_PLUGIN_SERVE_THREAD", "1") == "1":
-                # the endpoint is served from a native thread (the GIL guards the shared state); a short switch
-                # interval bounds how long it waits for the GIL while this loop runs Python
+                # the endpoint is served from a native thread that never needs the GIL (a native lock guards the
+                # allocation state shared with this loop), so a busy Python loop does not delay a fast Allocate
                 self._native_fd = self._native.start_serving()
-                sys.setswitchinterval(min(sys.getswitchinterval(), 0.0005))
             else:
                 self._native_fd = self._native.fd()
             asyncio.get_running_loop().add_reader(self._native_fd, self._native_poll)

@@ -718,6 +718,21 @@ DpDevice dp_device_from(const py::dict& d) {
   return x;
 }
 
+// The device plugin's allocation state is shared by the plugin's Python code (state.py, through the AllocState /
+// CuPartitioner bindings) and the native endpoint's serving thread.  One process-wide lock guards it: every binding
+// of those classes takes it (py::call_guard), and so does the serving thread for each pass.  The serving thread
+// never takes the GIL, so a Python caller holding the GIL while it waits for this lock cannot deadlock with it.
+std::recursive_mutex& alloc_mu() {
+  static std::recursive_mutex m;
+  return m;
+}
+struct AllocLock {
+  AllocLock() { alloc_mu().lock(); }
+  ~AllocLock() { alloc_mu().unlock(); }
+  AllocLock(const AllocLock&) = delete;
+  AllocLock& operator=(const AllocLock&) = delete;
+};
+
 // The plugin's gRPC endpoint in native code, driven by the plugin's asyncio loop (add_reader(fd, poll)).
 // GetDevicePluginOptions / ListAndWatch / PreStartContainer are answered here; GetPreferredAllocation and
 // Allocate take DpCore's fast path and otherwise come back from poll() as pending calls for the Python handlers,
@@ -758,8 +773,8 @@ class PyDpServer {
 
   // Serve from a native thread instead of the owner's event loop: accept, read, the fast paths, the pod feed
   // and the patch completions run as soon as their fd is ready, however busy the Python loop is (its own pod
-  // informer decodes every event of the node).  The GIL is the state mutex: every Python call into the
-  // AllocState holds it, and the thread holds it for each pass (microseconds of C++).  Returns an eventfd that
+  // informer decodes every event of the node).  The state lock (alloc_mu) guards the shared state: every Python
+  // call into it takes the lock, and so does the thread for each pass (microseconds of C++).  Returns an eventfd that
   // turns readable when calls for the Python slow path or fast-path events wait for poll().
   int start_serving() {
     if (serving_.joinable()) return pyfd_;
@@ -887,6 +902,7 @@ class PyDpServer {
     stop_serving();
     if (feed_r_) feed_r_->stop();
     stop_worker();
+    AllocLock lock;
     finish_patches();
     if (srv_) {
       for (uint64_t id : srv_->open_streams(std::string(kSvc) + "ListAndWatch")) srv_->stream_end(id, 0, "");
@@ -946,8 +962,8 @@ class PyDpServer {
     const int ep = srv_ ? srv_->fd() : -1;
     for (;;) {
       pollfd pf{ep, POLLIN, 0};
-      ::poll(&pf, 1, 100);  // GIL released: the Python loop runs meanwhile
-      py::gil_scoped_acquire gil;
+      ::poll(&pf, 1, 100);
+      AllocLock lock;  // the state lock, not the GIL: a busy Python loop does not delay the pass
       if (stop_serving_ || !srv_) return;
       one_pass();
       if (!pending_.empty() || !events_.empty()) {
@@ -957,10 +973,13 @@ class PyDpServer {
     }
   }
 
-  // GIL held by the caller (close / the destructor): released while the thread finishes its pass
+  // Not under the state lock (the thread needs it to finish its pass); the GIL is released while joining.
   void stop_serving() {
     if (!serving_.joinable()) return;
-    stop_serving_ = true;
+    {
+      AllocLock lock;
+      stop_serving_ = true;
+    }
     uint64_t one = 1;
     (void)!::write(efd_, &one, sizeof one);
     py::gil_scoped_release nogil;
@@ -1294,35 +1313,34 @@ PYBIND11_MODULE(_engine, m) {
   // compiled node agent
   py::class_<CuPartitioner>(m, "CuPartitioner")
       .def(py::init<int, int>(), py::arg("cu_count") = 256, py::arg("xcc_count") = 8)
-      .def("allocate",
-           [](CuPartitioner& c, const std::string& uid, int n) {
+      .def("allocate", [](CuPartitioner& c, const std::string& uid, int n) {
              std::vector<int> out;
              std::string err;
              if (!c.allocate(uid, n, &out, &err)) throw py::value_error(err);
              return out;
-           })
-      .def("release", &CuPartitioner::release)
-      .def("adopt", &CuPartitioner::adopt)
-      .def("swap_owners", &CuPartitioner::swap_owners)
-      .def("holds", &CuPartitioner::holds)
-      .def("held_by", &CuPartitioner::held_by)
+           }, py::call_guard<AllocLock>())
+      .def("release", &CuPartitioner::release, py::call_guard<AllocLock>())
+      .def("adopt", &CuPartitioner::adopt, py::call_guard<AllocLock>())
+      .def("swap_owners", &CuPartitioner::swap_owners, py::call_guard<AllocLock>())
+      .def("holds", &CuPartitioner::holds, py::call_guard<AllocLock>())
+      .def("held_by", &CuPartitioner::held_by, py::call_guard<AllocLock>())
       .def("held", [](const CuPartitioner& c) {
         py::dict d;
         for (const auto& kv : c.held()) d[py::str(kv.first)] = kv.second;
         return d;
-      })
-      .def("free_count", &CuPartitioner::free_count)
+      }, py::call_guard<AllocLock>())
+      .def("free_count", &CuPartitioner::free_count, py::call_guard<AllocLock>())
       .def_property_readonly("cu_count", &CuPartitioner::cu_count)
       .def_property_readonly("xcc_count", &CuPartitioner::xcc_count);
-  m.def("cu_words", &cu_words);
+  m.def("cu_words", &cu_words, py::call_guard<AllocLock>());
   m.def("parse_cu_words", [](const std::string& w) {
     try {
       return parse_cu_words(w);
     } catch (const std::invalid_argument& e) {
       throw py::value_error(e.what());
     }
-  });
-  m.def("cu_ranges", &cu_ranges);
+  }, py::call_guard<AllocLock>());
+  m.def("cu_ranges", &cu_ranges, py::call_guard<AllocLock>());
 
   py::class_<AllocPod>(m, "AllocPod")
       .def(py::init<>())
@@ -1367,58 +1385,55 @@ PYBIND11_MODULE(_engine, m) {
              return new AllocState(node, d);
            }),
            py::arg("node"), py::arg("devices"))
-      .def("observe", &AllocState::observe)
-      .def("release", &AllocState::release)
+      .def("observe", &AllocState::observe, py::call_guard<AllocLock>())
+      .def("release", &AllocState::release, py::call_guard<AllocLock>())
       .def("resync", [](AllocState& s, const std::vector<std::string>& live) {
         s.resync(std::unordered_set<std::string>(live.begin(), live.end()));
-      })
-      .def("holders", &AllocState::holders)
-      .def("has_pod", [](const AllocState& s, const std::string& uid) { return s.pod(uid) != nullptr; })
+      }, py::call_guard<AllocLock>())
+      .def("holders", &AllocState::holders, py::call_guard<AllocLock>())
+      .def("has_pod", [](const AllocState& s, const std::string& uid) { return s.pod(uid) != nullptr; }, py::call_guard<AllocLock>())
       .def("pod_uids", [](const AllocState& s) {
         std::vector<std::string> out;
         for (const auto& kv : s.pods()) out.push_back(kv.first);
         return out;
-      })
+      }, py::call_guard<AllocLock>())
       .def("candidates", [](const AllocState& s) {
         std::vector<std::string> out;
         for (const AllocPod* p : s.candidates()) out.push_back(p->uid);
         return out;
-      })
+      }, py::call_guard<AllocLock>())
       .def("match", [](AllocState& s, int64_t units) {
         auto m = s.match(units);
         return py::make_tuple(m.first ? py::object(py::str(m.first->uid)) : py::object(py::none()), m.second);
-      })
-      .def("preferred_device", &AllocState::preferred_device)
-      .def("unannotated", &AllocState::unannotated)
-      .def("claim_cus",
-           [](AllocState& s, const std::string& uid) {
+      }, py::call_guard<AllocLock>())
+      .def("preferred_device", &AllocState::preferred_device, py::call_guard<AllocLock>())
+      .def("unannotated", &AllocState::unannotated, py::call_guard<AllocLock>())
+      .def("claim_cus", [](AllocState& s, const std::string& uid) {
              std::vector<int> out;
              std::string err;
              if (!s.claim_cus(uid, &out, &err)) throw py::value_error(err);
              return out;
-           })
-      .def("set_inflight", &AllocState::set_inflight)
-      .def("set_owners_reported", &AllocState::set_owners_reported)
-      .def("owners_reported", &AllocState::owners_reported)
-      .def("inflight", &AllocState::inflight)
-      .def("first_container_committed", &AllocState::first_container_committed)
-      .def("later_container_allocated", &AllocState::later_container_allocated)
+           }, py::call_guard<AllocLock>())
+      .def("set_inflight", &AllocState::set_inflight, py::call_guard<AllocLock>())
+      .def("set_owners_reported", &AllocState::set_owners_reported, py::call_guard<AllocLock>())
+      .def("owners_reported", &AllocState::owners_reported, py::call_guard<AllocLock>())
+      .def("inflight", &AllocState::inflight, py::call_guard<AllocLock>())
+      .def("first_container_committed", &AllocState::first_container_committed, py::call_guard<AllocLock>())
+      .def("later_container_allocated", &AllocState::later_container_allocated, py::call_guard<AllocLock>())
       .def("partial", [](const AllocState& s) {
         py::dict d;
         for (const auto& kv : s.partial()) d[py::str(kv.first)] = kv.second;
         return d;
-      })
-      .def("record",
-           [rec_dict](AllocState& s, const std::string& uid, const std::vector<std::string>& ids, int64_t units,
+      }, py::call_guard<AllocLock>())
+      .def("record", [rec_dict](AllocState& s, const std::string& uid, const std::vector<std::string>& ids, int64_t units,
                       const std::string& cu_mask, const std::string& aid, double t, const std::string& iso) {
              AllocRecord& r = s.record(uid, ids, units, cu_mask, aid, t);
              r.iso = iso;
              return rec_dict(r);
            },
            py::arg("uid"), py::arg("ids"), py::arg("units"), py::arg("cu_mask"), py::arg("aid"), py::arg("t") = 0.0,
-           py::arg("iso") = std::string())
-      .def("add_record",
-           [](AllocState& s, const py::dict& d) {
+           py::arg("iso") = std::string(), py::call_guard<AllocLock>())
+      .def("add_record", [](AllocState& s, const py::dict& d) {
              AllocRecord r;
              r.aid = d["aid"].cast<std::string>();
              r.ids = d.contains("ids") ? d["ids"].cast<std::vector<std::string>>() : std::vector<std::string>();
@@ -1430,39 +1445,35 @@ PYBIND11_MODULE(_engine, m) {
              r.t = d.contains("t") ? d["t"].cast<double>() : 0.0;
              r.iso = d.contains("iso") ? d["iso"].cast<std::string>() : std::string();
              s.add_record(std::move(r));
-           })
-      .def("drop_record", &AllocState::drop_record)
-      .def("record_for_ids",
-           [rec_dict](const AllocState& s, const std::vector<std::string>& ids) -> py::object {
+           }, py::call_guard<AllocLock>())
+      .def("drop_record", &AllocState::drop_record, py::call_guard<AllocLock>())
+      .def("record_for_ids", [rec_dict](const AllocState& s, const std::vector<std::string>& ids) -> py::object {
              const AllocRecord* r = s.record_for_ids(ids);
              return r ? py::object(rec_dict(*r)) : py::object(py::none());
-           })
-      .def("get_record",
-           [rec_dict](AllocState& s, const std::string& aid) -> py::object {
+           }, py::call_guard<AllocLock>())
+      .def("get_record", [rec_dict](AllocState& s, const std::string& aid) -> py::object {
              AllocRecord* r = s.record_by_aid(aid);
              return r ? py::object(rec_dict(*r)) : py::object(py::none());
-           })
-      .def("set_owner", &AllocState::set_owner)
-      .def("move_records", &AllocState::move_records)
-      .def("records",
-           [rec_dict](const AllocState& s) {
+           }, py::call_guard<AllocLock>())
+      .def("set_owner", &AllocState::set_owner, py::call_guard<AllocLock>())
+      .def("move_records", &AllocState::move_records, py::call_guard<AllocLock>())
+      .def("records", [rec_dict](const AllocState& s) {
              py::list out;
              for (const auto& kv : s.records()) out.append(rec_dict(kv.second));
              return out;
-           })
-      .def("record_count", [](const AllocState& s) { return s.records().size(); })
-      .def("take_dropped",
-           [rec_dict](AllocState& s) {
+           }, py::call_guard<AllocLock>())
+      .def("record_count", [](const AllocState& s) { return s.records().size(); }, py::call_guard<AllocLock>())
+      .def("take_dropped", [rec_dict](AllocState& s) {
              py::list out;
              for (const auto& r : s.take_dropped()) out.append(rec_dict(r));
              return out;
-           })
-      .def("cus", [](AllocState& s, int dev) { return s.cus(dev); }, py::return_value_policy::reference_internal)
+           }, py::call_guard<AllocLock>())
+      .def("cus", [](AllocState& s, int dev) { return s.cus(dev); }, py::return_value_policy::reference_internal, py::call_guard<AllocLock>())
       .def("devices", [](const AllocState& s) {
         std::vector<int> out;
         for (const auto& kv : s.all_cus()) out.push_back(kv.first);
         return out;
-      })
+      }, py::call_guard<AllocLock>())
       .def("stats", [](const AllocState& s) {
         const AllocStats& st = s.stats();
         py::dict d;
@@ -1475,7 +1486,7 @@ PYBIND11_MODULE(_engine, m) {
         d["matches"] = st.matches;
         d["match_misses"] = st.match_misses;
         return d;
-      });
+      }, py::call_guard<AllocLock>());
 
   m.def("parse_quantity", [](const std::string& s) {
     int64_t v;
@@ -1527,15 +1538,15 @@ PYBIND11_MODULE(_engine, m) {
   py::class_<PyDpServer>(m, "DpServer")
       .def(py::init<const std::string&, AllocState&, const py::dict&>(), py::keep_alive<1, 3>())
       .def("fd", &PyDpServer::fd)
-      .def("poll", &PyDpServer::poll)
+      .def("poll", &PyDpServer::poll, py::call_guard<AllocLock>())
       .def("start_serving", &PyDpServer::start_serving)
-      .def("respond", &PyDpServer::respond)
-      .def("set_devices", &PyDpServer::set_devices)
-      .def("set_device_list", &PyDpServer::set_device_list)
-      .def("set_fast", &PyDpServer::set_fast)
-      .def("set_state", &PyDpServer::set_state, py::keep_alive<1, 2>())
+      .def("respond", &PyDpServer::respond, py::call_guard<AllocLock>())
+      .def("set_devices", &PyDpServer::set_devices, py::call_guard<AllocLock>())
+      .def("set_device_list", &PyDpServer::set_device_list, py::call_guard<AllocLock>())
+      .def("set_fast", &PyDpServer::set_fast, py::call_guard<AllocLock>())
+      .def("set_state", &PyDpServer::set_state, py::keep_alive<1, 2>(), py::call_guard<AllocLock>())
       .def("start_feed", &PyDpServer::start_feed)
-      .def("stats", &PyDpServer::stats)
+      .def("stats", &PyDpServer::stats, py::call_guard<AllocLock>())
       .def("close", &PyDpServer::close);
   py::class_<h2::Client>(m, "H2Client")
       .def(py::init<const std::string&>())
