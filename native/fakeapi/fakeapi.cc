@@ -30,7 +30,8 @@
 // --watch-loop (with --threads N >= 2): loop 0 serves only watch streams and has no listener; loops 1..N-1
 // accept and serve requests.  A request that becomes a watch is handed over with its connection, so a write
 // emits its events to watcher buffers (state mutex) and at most one eventfd wakes the watch loop per batch;
-// the request loops never send watch chunks and never wake each other.
+// the request loops never send watch chunks and never wake each other.  At N = 8 on the MI355X box it does not
+// move the wave either (per-wave p50 17.3-18.8k pods/s in every layout, profiles/r03e/watchloop_ab.md).
 //
 // Default 1 loop.  Measured on the MI355X box (bench.py, fake devices, N=8:
 // 32 pods per wave, ~5 writes per pod): 4 loops were slower (10.7k vs 13.6k
