@@ -297,10 +297,10 @@ def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
 
     na = restart_child(children, "node-agent", lambda old: start_node_agent(
         api_url, NODE, profile=a.profile, native=False, plugin=a.plugin_proc, cpus=old.cpus,
-        extra=["--faithful"] if a.kubelet == "faithful" else []))
+        extra=["--faithful"] if a.kubelet == "faithful" else [], plugin_cpus=a.plugin_cpus))
     client = E.BatchClient({"server": na.url})
     wait_until(lambda: client.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 120, "plugin agent never ready")
-    row = runner.measure(2, a.sweep_steps)
+    row = runner.measure(3, max(a.sweep_steps, 40))  # ~2 ms waves: 40 of them cost little and steady the row
     st, body = client.run([("GET", "/v1/stats", b"")], 1)[0]
     stats = json.loads(body) if st == 200 else {}
     return {**row, "admit_p50_ms": stats.get("admit_p50_ms"), "breakdown_ms": stats.get("breakdown_ms"),
@@ -318,17 +318,19 @@ def plugin_path_native_kubelet(a, children, api_url, runner: WaveRunner, E) -> d
     from gpushare_scheduler_extender_amd.sim.cluster import start_node_agent
 
     na = restart_child(children, "node-agent", lambda old: start_node_agent(
-        api_url, NODE, profile=a.profile, native=True, plugin="spawn", cpus=old.cpus))
+        api_url, NODE, profile=a.profile, native=True, plugin="spawn", cpus=old.cpus, plugin_cpus=a.plugin_cpus))
     client = E.BatchClient({"server": na.url})
     wait_until(lambda: client.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 120, "plugin agent never ready")
-    row = runner.measure(2, a.sweep_steps)
+    row = runner.measure(3, max(a.sweep_steps, 40))  # ~2 ms waves: 40 of them cost little and steady the row
     st, body = client.run([("GET", "/v1/stats", b"")], 1)[0]
     stats = json.loads(body) if st == 200 else {}
     return {**row, "admit_p50_ms": stats.get("admit_p50_ms"), "failed": stats.get("failed"),
             "kubelet_mean_ms": {"queue": (stats.get("mean_ms") or {}).get("queue"),
                                 "preferred_plus_allocate_grpc": (stats.get("mean_ms") or {}).get("assign_patch"),
                                 "runtime": (stats.get("mean_ms") or {}).get("runtime"),
-                                "running_patch": (stats.get("mean_ms") or {}).get("running_patch")}}
+                                "running_patch": (stats.get("mean_ms") or {}).get("running_patch")},
+            # kubelet's serial admission per pod: waiting for the slot, then the two calls as the client sees them
+            "plugin_calls_mean_ms": stats.get("plugin_calls_mean_ms")}
 
 
 def parse():
@@ -432,11 +434,12 @@ def main():
     # ---- CPU placement (the same plan on every rank: each takes its own slot)
     from gpushare_scheduler_extender_amd.utils.cpuset import forget_shared_plan, pin_self, plan, shared_plan
 
-    names = ["rank0", "apiserver", "extender", "scheduler", "node-agent"] + [f"rank{r}" for r in range(1, world)]
+    # "plugin": the shipped device-plugin process when an agent starts one (its own CPUs, as a DaemonSet pod)
+    names = ["rank0", "apiserver", "extender", "scheduler", "node-agent", "plugin"] + [f"rank{r}" for r in range(1, world)]
     # CPUs per process: the extender (2 loops + bind pool + reflectors), schedsim (cycle + bind threads) and the
     # node agent (reflector + workers) get two; rank 0 stays on one core (a second one let its driver, tracker
     # and runtime threads migrate: 7.5-9.4k vs 10.1k pods/s, interleaved A/B in profiles/r02_bench_stability.md)
-    widths = {"extender": 2, "scheduler": 2, "node-agent": 2}
+    widths = {"extender": 2, "scheduler": 2, "node-agent": 2, "plugin": 2}
     if a.runtime_cpu == "split":
         # rank 0 = the wave driver + GPU 0's runtime endpoint (the CRI-runtime role): one core, the driver on
         # one SMT thread and the endpoint's threads on the other, instead of both time-sharing one thread
@@ -444,6 +447,11 @@ def main():
     # ranks > 0 idle in a gloo barrier during the timed waves while their runtime endpoint admits pods: on a
     # single CPU the endpoint thread waited behind gloo's threads for up to 9 ms (N=4/8 rehearsal, 2 CPUs fix it)
     widths.update({f"rank{r}": 2 for r in range(1, world)})
+    if world > 1:
+        # with N GPUs rank 0's wave driver creates and tracks N x 4 pods per wave: on one CPU the creates trickled
+        # out (scheduler saw the 32nd pod of an N = 8 wave 0.96 ms in, 0.53 ms with a second CPU; per-wave p50
+        # 13.0k -> 19.2k pods/s at N = 8, 10.6k -> 15.7k at N = 4; N = 1 unchanged, profiles/r03_ab/)
+        widths["rank0"] = 2
     if a.pin_widths:
         widths.update(json.loads(a.pin_widths))
     mode = a.pin if a.pin != "auto" else "spread"
@@ -458,6 +466,7 @@ def main():
     else:
         cpu_plan = plan(names, widths, mode, smt=bool(a.pin_smt), local=5)
     mine_cpus = cpu_plan.get(f"rank{rank}")
+    a.plugin_cpus = cpu_plan.get("plugin")
     runtime_cpus = None
     if rank == 0 and a.runtime_cpu == "split" and mine_cpus and len(mine_cpus) >= 2:
         mine_cpus, runtime_cpus = mine_cpus[:1], mine_cpus[1:]
@@ -487,7 +496,8 @@ def main():
                                                                                                         "grpc"),
                                              workers=min(16, max(8, 2 * a.pods_per_gpu * world)),
                                              cpus=cpu_plan.get("node-agent"),
-                                             extra=["--faithful"] if a.kubelet == "faithful" else []))
+                                             extra=["--faithful"] if a.kubelet == "faithful" else [],
+                                             plugin_cpus=a.plugin_cpus))
         api_url, ext_url = api.url, ext.url
 
     import torch

@@ -20,7 +20,19 @@ from .devices import discover
 from .plugin import GpuSharePlugin
 
 
+def _pin_from_env() -> None:
+    """``GSX_PLUGIN_CPUS=a,b``: run on these CPUs (the benchmark gives the plugin process its own, as a DaemonSet pod
+    has, instead of the CPUs of the kubelet stand-in that started it)."""
+    cpus = os.environ.get("GSX_PLUGIN_CPUS", "")
+    if cpus:
+        try:
+            os.sched_setaffinity(0, {int(c) for c in cpus.split(",") if c.strip()})
+        except (OSError, ValueError):
+            pass
+
+
 def main(argv=None) -> int:
+    _pin_from_env()
     env = os.environ
     ap = argparse.ArgumentParser(prog="gpushare-device-plugin-amd")
     ap.add_argument("--node", default=env.get("NODE_NAME", ""))

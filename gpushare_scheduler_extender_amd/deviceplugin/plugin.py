@@ -271,6 +271,7 @@ class GpuSharePlugin:
         pending, events = srv.poll()
         for ev in events:
             self._fast_allocated(ev)
+        self.state.flush_dropped()  # records the native pod feed dropped with their pods: isolation cleanup
         if pending:
             loop = asyncio.get_running_loop()
             for cid, method, payload in pending:

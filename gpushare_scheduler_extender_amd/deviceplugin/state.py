@@ -220,6 +220,10 @@ class AllocationState:
             del self._recs[uid]
         self._flush()
 
+    def flush_dropped(self) -> None:
+        """Run the drop callbacks for records the native side dropped on its own (the plugin's pod feed)."""
+        self._flush()
+
     def _flush(self):
         for d in self.core.take_dropped():
             r = AllocRecord.from_dict(d)

@@ -148,24 +148,27 @@ NODEAGENT = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-nodeagen
 
 def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", workers: int = 32,
                      native: bool = True, plugin: str = "grpc", cpus: list[int] | None = None,
-                     extra: list[str] | None = None) -> ChildProc:
+                     extra: list[str] | None = None, plugin_cpus: list[int] | None = None) -> ChildProc:
     """kubelet + device-plugin Allocate + runtime stand-in for ``node``.
 
     ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent, the plugin's native matcher in-process, or
     with ``plugin="spawn"`` the shipped plugin as its child process, called over the device-plugin gRPC API);
     otherwise ``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``: a kubelet stand-in driving
     the shipped device plugin, over its unix socket (``plugin="grpc"``) or in-process (``"inproc"``).
+    ``plugin_cpus``: CPUs of the plugin process the agent starts (as a DaemonSet pod has its own, instead of
+    sharing the kubelet stand-in's), through ``GSX_PLUGIN_CPUS``.
     """
+    env = {"GSX_PLUGIN_CPUS": ",".join(map(str, plugin_cpus))} if plugin_cpus else None
     if native:
         exe = tool_path("gsx-nodeagent")
         if not exe.exists():
             raise FileNotFoundError(f"{exe} missing; run `python native/build.py nodeagent`")
         spawn = ["--plugin-spawn", sys.executable] if plugin == "spawn" else []
         return ChildProc([str(exe), "--node", node, "--apiserver", apiserver, "--profile", profile,
-                          "--workers", str(min(workers, 16)), *spawn], "node-agent", cpus=cpus)
+                          "--workers", str(min(workers, 16)), *spawn], "node-agent", cpus=cpus, env=env)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
                       apiserver, "--profile", profile, "--workers", str(workers), "--plugin", plugin,
-                      *(extra or [])], "node-agent", cpus=cpus)
+                      *(extra or [])], "node-agent", cpus=cpus, env=env)
 
 
 SCHEDSIM = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-schedsim"

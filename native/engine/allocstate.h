@@ -152,6 +152,7 @@ class AllocState {
   void move_records(const std::string& p_uid, const std::string& q_uid, const std::string& aid);
   const std::map<std::string, AllocRecord>& records() const { return records_; }
   std::vector<AllocRecord> take_dropped();  // records dropped since the last call (isolation cleanup)
+  bool dropped_pending() const { return !dropped_.empty(); }
 
   const AllocPod* pod(const std::string& uid) const;
   const AllocPod* pod_by_key(const std::string& key) const;

@@ -966,7 +966,8 @@ class PyDpServer {
       AllocLock lock;  // the state lock, not the GIL: a busy Python loop does not delay the pass
       if (stop_serving_ || !srv_) return;
       one_pass();
-      if (!pending_.empty() || !events_.empty()) {
+      // also when the feed released a pod whose records went: Python cleans up their isolation files
+      if (!pending_.empty() || !events_.empty() || (state_ && state_->dropped_pending())) {
         uint64_t one = 1;
         (void)!::write(pyfd_, &one, sizeof one);
       }

@@ -358,6 +358,9 @@ struct Loop {
 };
 
 thread_local Loop* tl_loop = nullptr;
+// --watch-loop: a request loop wakes the watch loop once, at the end of its iteration, for all the events its
+// requests of that iteration produced (as the single loop sends them in one chunk per watcher per iteration)
+thread_local Loop* tl_deferred_wake = nullptr;
 
 struct Faults {
   double conflict_rate = 0, error_rate = 0, latency_ms = 0;
@@ -520,6 +523,10 @@ class Server {
         if (L->conns.count(id) && (evs[i].events & EPOLLOUT)) flush_conn(L, c);
       }
       run_timers(L);
+      if (tl_deferred_wake != nullptr) {
+        wake(tl_deferred_wake);
+        tl_deferred_wake = nullptr;
+      }
       double t_flush = now_s();
       if (flush_watchers(L)) {
         L->flushes.fetch_add(1, std::memory_order_relaxed);
@@ -891,7 +898,11 @@ class Server {
     L->has_dirty.store(true);
     if (L != tl_loop && !L->signaled) {
       L->signaled = true;
-      wake(L);
+      if (watch_loop_ && tl_loop != nullptr && tl_loop->idx != 0) {
+        tl_deferred_wake = L;
+      } else {
+        wake(L);
+      }
     }
   }
 

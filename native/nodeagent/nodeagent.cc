@@ -250,18 +250,22 @@ class Agent {
       std::sort(lat.begin(), lat.end());
       double p50 = lat.empty() ? 0 : lat[lat.size() / 2];
       const double n = admitted_ ? static_cast<double>(admitted_) : 1.0;
-      char b[768];
+      char b[1024];
       std::snprintf(b, sizeof(b),
                     "{\"admitted\":%llu,\"failed\":%llu,\"bad_stamps\":%llu,\"conflicts\":%llu,\"running\":%zu,"
                     "\"admit_p50_ms\":%.3f,\"admit_max_ms\":%.3f,\"max_ms\":{\"queue\":%.3f,\"assign_patch\":%.3f,"
                     "\"runtime\":%.3f,\"running_patch\":%.3f},\"mean_ms\":{\"queue\":%.4f,\"assign_patch\":%.4f,"
                     "\"runtime\":%.4f,\"running_patch\":%.4f},\"status_retries\":%llu,\"api_connects\":%llu,"
+                    "\"plugin_calls_mean_ms\":{\"n\":%llu,\"slot_wait\":%.4f,\"get_preferred\":%.4f,\"allocate\":%.4f},"
                     "\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
                     (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
                     max_queue_ * 1e3, max_patch_ * 1e3, max_runtime_ * 1e3, max_status_ * 1e3, sum_queue_ / n * 1e3,
                     sum_patch_ / n * 1e3, sum_runtime_ / n * 1e3, sum_status_ / n * 1e3,
-                    (unsigned long long)status_retries_.load(), (unsigned long long)api_.reconnects());
+                    (unsigned long long)status_retries_.load(), (unsigned long long)api_.reconnects(),
+                    (unsigned long long)dp_calls_, sum_dp_slot_ / std::max<double>(1.0, dp_calls_) * 1e3,
+                    sum_dp_pref_ / std::max<double>(1.0, dp_calls_) * 1e3,
+                    sum_dp_alloc_ / std::max<double>(1.0, dp_calls_) * 1e3);
       rep.body = b;
       return rep;
     }
@@ -412,6 +416,15 @@ class Agent {
         cv_.wait_for(lk, std::chrono::duration<double>(wait));
         continue;
       }
+      std::unique_lock<std::mutex> slot;
+      if (dp_) {
+        // kubelet admits one pod at a time, in the order it met them: take the admission slot first, then the
+        // queue's front (a worker that popped first but reached the slot later would reorder the Allocates)
+        lk.unlock();
+        slot = std::unique_lock<std::mutex>(dp_mu_);
+        lk.lock();
+        if (queue_.empty() || stop_) continue;
+      }
       std::string key = std::move(queue_.front());
       queue_.pop_front();
       auto kit = keys_.find(key);
@@ -521,16 +534,23 @@ class Agent {
     std::vector<dp::ContainerResponse> crs;
     const double tp0 = now_s();
     bool ok;
+    double ts = 0, tpref = 0;
     {
-      std::lock_guard<std::mutex> g(dp_mu_);  // kubelet admits one pod at a time
+      // the worker holds the admission slot (dp_mu_) from the queue pop on: kubelet admits one pod at a time
+      ts = now_s();
       ok = dp_->call("/v1beta1.DevicePlugin/GetPreferredAllocation", dp::encode_preferred_request({pr}), &resp, &st,
                      &err) &&
-           dp::decode_preferred_response(resp, &chosen) && chosen.size() == 1 &&
-           dp_->call("/v1beta1.DevicePlugin/Allocate", dp::encode_allocate_request(chosen), &resp, &st, &err) &&
+           dp::decode_preferred_response(resp, &chosen) && chosen.size() == 1;
+      tpref = now_s();
+      ok = ok && dp_->call("/v1beta1.DevicePlugin/Allocate", dp::encode_allocate_request(chosen), &resp, &st, &err) &&
            dp::decode_allocate_response(resp, &crs) && crs.size() == 1;
     }
     const double tp1 = now_s();
     lk.lock();
+    dp_calls_++;
+    sum_dp_slot_ += ts - tp0;  // waiting for the admission slot (another pod's calls)
+    sum_dp_pref_ += tpref - ts;
+    sum_dp_alloc_ += tp1 - tpref;
     state_->set_inflight(my_uid, false);
     if (!ok) {
       failed_++;
@@ -848,6 +868,8 @@ class Agent {
   // worst case per admission step (seconds): queue wait, ASSIGNED patch, runtime admit, Running patch
   double max_queue_ = 0, max_patch_ = 0, max_runtime_ = 0, max_status_ = 0;
   double sum_queue_ = 0, sum_patch_ = 0, sum_runtime_ = 0, sum_status_ = 0;  // over admitted_ pods
+  uint64_t dp_calls_ = 0;  // GetPreferredAllocation + Allocate pairs to the plugin (--plugin-socket / --plugin-spawn)
+  double sum_dp_slot_ = 0, sum_dp_pref_ = 0, sum_dp_alloc_ = 0;
   std::vector<std::thread> workers_;
 };
 

@@ -91,7 +91,7 @@ def test_plugin_allocate_mounts_isolation_and_records(tmp_path):
             # the pod goes away: its record and its isolation files go with it
             await c.delete("pods", "a", "default")
             for _ in range(100):
-                if not plugin.state.records:
+                if not plugin.state.records and not iso.pod_dir(pod["metadata"]["uid"]).exists():
                     break
                 await asyncio.sleep(0.02)
             assert not plugin.state.records and not iso.pod_dir(pod["metadata"]["uid"]).exists()
