@@ -1540,13 +1540,13 @@ PYBIND11_MODULE(_engine, m) {
       .def(py::init<const std::string&, AllocState&, const py::dict&>(), py::keep_alive<1, 3>())
       .def("fd", &PyDpServer::fd)
       .def("poll", &PyDpServer::poll, py::call_guard<AllocLock>())
-      .def("start_serving", &PyDpServer::start_serving)
+      .def("start_serving", &PyDpServer::start_serving, py::call_guard<AllocLock>())
       .def("respond", &PyDpServer::respond, py::call_guard<AllocLock>())
       .def("set_devices", &PyDpServer::set_devices, py::call_guard<AllocLock>())
       .def("set_device_list", &PyDpServer::set_device_list, py::call_guard<AllocLock>())
       .def("set_fast", &PyDpServer::set_fast, py::call_guard<AllocLock>())
       .def("set_state", &PyDpServer::set_state, py::keep_alive<1, 2>(), py::call_guard<AllocLock>())
-      .def("start_feed", &PyDpServer::start_feed)
+      .def("start_feed", &PyDpServer::start_feed, py::call_guard<AllocLock>())
       .def("stats", &PyDpServer::stats, py::call_guard<AllocLock>())
       .def("close", &PyDpServer::close);
   py::class_<h2::Client>(m, "H2Client")
