@@ -845,6 +845,9 @@ class PyDpServer {
   }
 
   void one_pass() {
+    // clear the wake-up first, then drain: a feed event or patch completion after this read signals again
+    uint64_t n;
+    if (efd_ >= 0) (void)!::read(efd_, &n, sizeof n);
     drain_feed();
     if (srv_) srv_->poll();
     drain_feed();
@@ -942,7 +945,7 @@ class PyDpServer {
         pend->request = call.message;
         std::lock_guard<std::mutex> l(wmu_);
         todo_.push_back(std::move(pend));
-        wcv_.notify_one();
+        if (!serving_.joinable()) wcv_.notify_one();  // the serving thread runs its patches itself
       } else if (feed_r_ && why == kNoCandidate) {
         wait_for_pod(call.id, m, call.message);
       } else {
@@ -963,9 +966,29 @@ class PyDpServer {
     for (;;) {
       pollfd pf{ep, POLLIN, 0};
       ::poll(&pf, 1, 100);
-      AllocLock lock;  // the state lock, not the GIL: a busy Python loop does not delay the pass
+      std::unique_lock<std::recursive_mutex> lock(alloc_mu());  // the state lock, not the GIL
       if (stop_serving_ || !srv_) return;
       one_pass();
+      // the ASSIGNED patches of this pass's Allocates, here rather than on the worker (two thread hops fewer on
+      // kubelet's serial admission); the state lock is released around each apiserver call
+      for (;;) {
+        std::unique_ptr<DpPending> p;
+        {
+          std::lock_guard<std::mutex> l(wmu_);
+          if (todo_.empty()) break;
+          p = std::move(todo_.front());
+          todo_.pop_front();
+        }
+        lock.unlock();
+        core_->run_patch(*p);
+        lock.lock();
+        {
+          std::lock_guard<std::mutex> l(wmu_);
+          done_.push_back(std::move(p));
+        }
+        finish_patches();
+        if (stop_serving_ || !srv_) return;
+      }
       // also when the feed released a pod whose records went: Python cleans up their isolation files
       if (!pending_.empty() || !events_.empty() || (state_ && state_->dropped_pending())) {
         uint64_t one = 1;
@@ -1084,7 +1107,7 @@ class PyDpServer {
           pend->request = w.message;
           std::lock_guard<std::mutex> l(wmu_);
           todo_.push_back(std::move(pend));
-          wcv_.notify_one();
+          if (!serving_.joinable()) wcv_.notify_one();
           continue;
         }
         if (why != kNoCandidate) {
@@ -1136,8 +1159,6 @@ class PyDpServer {
   }
 
   void finish_patches() {
-    uint64_t n;
-    if (efd_ >= 0) (void)!::read(efd_, &n, sizeof n);
     std::deque<std::unique_ptr<DpPending>> done;
     {
       std::lock_guard<std::mutex> l(wmu_);
