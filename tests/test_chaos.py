@@ -54,19 +54,23 @@ def _committed_use(cl, bound: dict) -> tuple[list[int], int]:
                                                   (11, "native", "binding"),
                                                   (13, "plugin", "update"),
                                                   (7, "faithful", "binding"),
-                                                  (29, "faithful", "update")])
+                                                  (29, "faithful", "update"),
+                                                  (13, "faithful-event", "binding"),
+                                                  (31, "faithful-event", "update")])
 def test_chaos_whole_stack_converges_without_overcommit(seed, agent, bind_mode):
     """``agent``: kubelet + the shipped gRPC device plugin
     (the product path), the same behind a *faithful* kubelet (no re-routing, PodResources reconciliation; here
     with 20 ms creationTimestamp-sorted admission batches, kubelet's restart case, so swaps do happen), or the
-    compiled node agent; ``bind_mode``: one annotated Binding, or the
+    compiled node agent; ``faithful-event``: the faithful kubelet admitting one pod per watch event (its steady
+    state) with every bind concurrent (landing-order node); ``bind_mode``: one annotated Binding, or the
     reference's annotation write + Binding (two calls, the first guarded by resourceVersion)."""
-    faithful = agent == "faithful"
+    faithful = agent.startswith("faithful")
+    kubelet_args = ["--faithful"] + (["--batch-window", "0.02"] if agent == "faithful" else [])
 
     async def go():
         rnd = random.Random(seed)
         cl = Cluster(ALIYUN, [96] * 4, gpu=False, agent="plugin" if faithful else agent,
-                     bind_mode=bind_mode, agent_args=["--faithful", "--batch-window", "0.02"] if faithful else [])
+                     bind_mode=bind_mode, agent_args=kubelet_args if faithful else [])
         try:
             await cl.start()
             api = HttpClient(cl.api.url)
