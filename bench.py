@@ -378,6 +378,10 @@ def parse():
                          "contract) or relaxed (all concurrent; swaps repaired by the plugin's PodResources "
                          "reconciliation)")
     ap.add_argument("--sweep-orders", default="auto", help="bind orders the latency sweep covers (comma list)")
+    ap.add_argument("--admission", default="parallel", choices=["parallel", "serial"],
+                    help="compiled node agent with its in-process matcher: admit (Allocate + ASSIGNED commit) on all "
+                         "workers at once (parallel), or one pod at a time in arrival order as kubelet does (serial); "
+                         "containers start in parallel either way")
     ap.add_argument("--kubelet", default="standin", choices=["standin", "faithful"],
                     help="with --node-agent plugin: the kubelet stand-in re-routes a mismatched Allocate (standin) or "
                          "behaves like kubelet and lets the plugin reconcile (faithful)")
@@ -497,7 +501,7 @@ def main():
                                              workers=min(16, max(8, 2 * a.pods_per_gpu * world)),
                                              cpus=cpu_plan.get("node-agent"),
                                              extra=["--faithful"] if a.kubelet == "faithful" else [],
-                                             plugin_cpus=a.plugin_cpus))
+                                             plugin_cpus=a.plugin_cpus, serial_admission=a.admission == "serial"))
         api_url, ext_url = api.url, ext.url
 
     import torch
@@ -890,7 +894,8 @@ def main():
                                 f"({profile.resource}), binpack", "global_batch": n_pods, "seq_len": 0,
                        "parallelism": f"{world} GPU(s) advertised on 1 node; 1 rank (HBM runtime) per GPU; "
                                       f"agent={a.agent}",
-                       "bind_mode": a.bind_mode, "bind_order": a.bind_order, "device_backend": backend},
+                       "bind_mode": a.bind_mode, "bind_order": a.bind_order, "admission": a.admission,
+                       "node_agent": a.node_agent, "device_backend": backend},
             "p50_bind_latency_ms": round(1e3 * pct(lat, 50), 3),
             "p99_bind_latency_ms": round(1e3 * pct(lat, 99), 3),
             "p50_bind_rtt_ms": round(1e3 * pct(rtt, 50), 3),

@@ -148,13 +148,16 @@ NODEAGENT = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-nodeagen
 
 def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", workers: int = 32,
                      native: bool = True, plugin: str = "grpc", cpus: list[int] | None = None,
-                     extra: list[str] | None = None, plugin_cpus: list[int] | None = None) -> ChildProc:
+                     extra: list[str] | None = None, plugin_cpus: list[int] | None = None,
+                     serial_admission: bool = False) -> ChildProc:
     """kubelet + device-plugin Allocate + runtime stand-in for ``node``.
 
     ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent, the plugin's native matcher in-process, or
     with ``plugin="spawn"`` the shipped plugin as its child process, called over the device-plugin gRPC API);
     otherwise ``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``: a kubelet stand-in driving
     the shipped device plugin, over its unix socket (``plugin="grpc"``) or in-process (``"inproc"``).
+    ``serial_admission``: the compiled agent admits one pod at a time with its in-process matcher too, as kubelet
+    does (with ``plugin="spawn"`` it always does).
     ``plugin_cpus``: CPUs of the plugin process the agent starts (as a DaemonSet pod has its own, instead of
     sharing the kubelet stand-in's), through ``GSX_PLUGIN_CPUS``.
     """
@@ -164,6 +167,8 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
         if not exe.exists():
             raise FileNotFoundError(f"{exe} missing; run `python native/build.py nodeagent`")
         spawn = ["--plugin-spawn", sys.executable] if plugin == "spawn" else []
+        if serial_admission:
+            spawn.append("--serial-admission")
         return ChildProc([str(exe), "--node", node, "--apiserver", apiserver, "--profile", profile,
                           "--workers", str(min(workers, 16)), *spawn], "node-agent", cpus=cpus, env=env)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",

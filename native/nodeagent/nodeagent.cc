@@ -23,7 +23,13 @@
 // The matching decision is AllocState (native/engine/allocstate.h), shared with the shipped gRPC device plugin.
 //
 //   gsx-nodeagent --apiserver URL --node NAME [--profile P] [--unit GiB]
-//                 [--workers N] [--no-verify] [--port-file F]
+//                 [--workers N] [--no-verify] [--serial-admission] [--port-file F]
+//
+// Admission: with the shipped plugin (--plugin-socket / --plugin-spawn), or with --serial-admission for the
+// in-process matcher, pods are admitted one at a time in the order the informer met them, as kubelet does (the
+// Allocate, and the plugin's ASSIGNED commit inside it, are serial); starting the container (runtime + Running
+// patch) runs on the workers in parallel, as kubelet's pod workers do.  Without it the in-process matcher admits
+// on all workers at once.
 #include <signal.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -417,7 +423,7 @@ class Agent {
         continue;
       }
       std::unique_lock<std::mutex> slot;
-      if (dp_) {
+      if (dp_ || serial_admission_) {
         // kubelet admits one pod at a time, in the order it met them: take the admission slot first, then the
         // queue's front (a worker that popped first but reached the slot later would reorder the Allocates)
         lk.unlock();
@@ -430,7 +436,7 @@ class Agent {
       auto kit = keys_.find(key);
       if (kit == keys_.end()) continue;
       queued_.erase(kit->second);
-      admit_locked(key, lk);
+      admit_locked(key, lk, &slot);
     }
   }
 
@@ -505,7 +511,9 @@ class Agent {
     }
   }
 
-  void admit_via_plugin_locked(std::string key, std::unique_lock<std::mutex>& lk) {
+  // `slot`: the admission slot (held when admissions are serial); given up once the Allocate is answered, as
+  // kubelet's pod workers start containers after admission, in parallel
+  void admit_via_plugin_locked(std::string key, std::unique_lock<std::mutex>& lk, std::unique_lock<std::mutex>* slot) {
     const AllocPod* mine = state_->pod_by_key(key);
     if (!mine) return;
     const std::string my_uid = mine->uid, my_key = key;
@@ -546,6 +554,7 @@ class Agent {
            dp::decode_allocate_response(resp, &crs) && crs.size() == 1;
     }
     const double tp1 = now_s();
+    if (slot && slot->owns_lock()) slot->unlock();
     lk.lock();
     dp_calls_++;
     sum_dp_slot_ += ts - tp0;  // waiting for the admission slot (another pod's calls)
@@ -598,9 +607,9 @@ class Agent {
   static std::string mine_ns(const std::string& key) { return key.substr(0, key.find('/')); }
   static std::string mine_name(const std::string& key) { return key.substr(key.find('/') + 1); }
 
-  void admit_locked(std::string key, std::unique_lock<std::mutex>& lk) {
+  void admit_locked(std::string key, std::unique_lock<std::mutex>& lk, std::unique_lock<std::mutex>* slot) {
     if (dp_) {
-      admit_via_plugin_locked(std::move(key), lk);
+      admit_via_plugin_locked(std::move(key), lk, slot);
       return;
     }
     const AllocPod* mine = state_->pod_by_key(key);
@@ -661,6 +670,7 @@ class Agent {
     double tp0 = now_s();
     bool ok = api_.request("PATCH", path, patch, "application/merge-patch+json", &status, &resp, &err);
     double tp1 = now_s();
+    if (slot && slot->owns_lock()) slot->unlock();  // the Allocate (its commit) is done: the next admission may go
     if (!ok || status >= 300) {
       lk.lock();
       if (!cus.empty() && !had_cus && cp) cp->release(uid);
@@ -834,6 +844,12 @@ class Agent {
   int64_t unit_;
   int nworkers_;
   bool verify_;
+ public:
+  // kubelet admits a node's pods one at a time (Allocate included): with this set the in-process matcher does too
+  void set_serial_admission(bool on) { serial_admission_ = on; }
+
+ private:
+  bool serial_admission_ = false;
   ApiClient api_;
   std::map<int, Device> devices_;
   std::unique_ptr<AllocState> state_;  // the device plugin's matcher (allocstate.h)
@@ -881,7 +897,7 @@ void on_sig(int) { g_stop = 1; }
 int main(int argc, char** argv) {
   std::string apiserver, node, profile = "shared-gpu", unit = "GiB", port_file, host = "127.0.0.1", plugin_socket, plugin_python;
   int workers = 16, port = 0;
-  bool verify = true;
+  bool verify = true, serial = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&](const char* name) -> std::string {
@@ -897,13 +913,15 @@ int main(int argc, char** argv) {
     else if (a == "--unit") unit = val("--unit");
     else if (a == "--workers") workers = std::max(1, std::min(128, std::atoi(val("--workers").c_str())));
     else if (a == "--no-verify") verify = false;
+    else if (a == "--serial-admission") serial = true;
     else if (a == "--port") port = std::atoi(val("--port").c_str());
     else if (a == "--port-file") port_file = val("--port-file");
     else if (a == "--plugin-socket") plugin_socket = val("--plugin-socket");
     else if (a == "--plugin-spawn") plugin_python = val("--plugin-spawn");
     else if (a == "-h" || a == "--help") {
       std::printf("usage: gsx-nodeagent --apiserver URL --node NAME [--profile P] [--unit GiB|MiB] [--workers N]\n"
-                  "                     [--no-verify] [--port P] [--port-file F] [--plugin-socket S | --plugin-spawn PYTHON]\n");
+                  "                     [--no-verify] [--serial-admission] [--port P] [--port-file F]\n"
+                  "                     [--plugin-socket S | --plugin-spawn PYTHON]\n");
       return 0;
     } else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -925,6 +943,7 @@ int main(int argc, char** argv) {
   api.server = apiserver;
   Agent agent(api, node, profile_by_name(profile), unit_bytes, workers, verify);
   agent.set_plugin_socket(plugin_socket);
+  agent.set_serial_admission(serial);
   if (!plugin_python.empty()) agent.set_plugin_spawn(plugin_python, apiserver, profile, unit);
   std::string err;
   CtlServer srv([&](const http::Message& m) { return agent.handle(m); });
