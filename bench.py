@@ -378,10 +378,12 @@ def parse():
                          "contract) or relaxed (all concurrent; swaps repaired by the plugin's PodResources "
                          "reconciliation)")
     ap.add_argument("--sweep-orders", default="auto", help="bind orders the latency sweep covers (comma list)")
-    ap.add_argument("--admission", default="parallel", choices=["parallel", "serial"],
-                    help="compiled node agent with its in-process matcher: admit (Allocate + ASSIGNED commit) on all "
-                         "workers at once (parallel), or one pod at a time in arrival order as kubelet does (serial); "
-                         "containers start in parallel either way")
+    # serial by default: kubelet admits a node's pods one at a time.  Measured on MI355X boxes: N = 1 unchanged
+    # (wave p50 10.2-11.1k vs 10.1-11.6k parallel), N = 8 -10 % (16.9-17.6k vs 18.7-19.8k), profiles/r03_admission/
+    ap.add_argument("--admission", default="serial", choices=["parallel", "serial"],
+                    help="compiled node agent with its in-process matcher: admit (Allocate + ASSIGNED commit) one pod "
+                         "at a time in arrival order as kubelet does (serial, default), or on all workers at once "
+                         "(parallel); containers start in parallel either way")
     ap.add_argument("--kubelet", default="standin", choices=["standin", "faithful"],
                     help="with --node-agent plugin: the kubelet stand-in re-routes a mismatched Allocate (standin) or "
                          "behaves like kubelet and lets the plugin reconcile (faithful)")
