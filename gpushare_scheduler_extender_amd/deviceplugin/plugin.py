@@ -140,6 +140,7 @@ class GpuSharePlugin:
         self._server: grpc.aio.Server | None = None
         self._native = None  # _engine.DpServer: the gRPC endpoint in native code (default)
         self._native_fd = -1  # what the loop watches for it (the serving thread's eventfd, or its epoll fd)
+        self._feed = False  # the native endpoint's pod feed runs (the Python informer then mirrors only)
         self.grpc_impl = ""
         self._slow: set[asyncio.Task] = set()
         self._tasks: list[asyncio.Task] = []
@@ -149,7 +150,10 @@ class GpuSharePlugin:
         self._debug = None
 
     def _observe(self, pod: dict):
-        self.state.observe(pod)
+        # with the native pod feed on, the native state has this event from its own watch: the Python informer
+        # only keeps the Python views (the per-event native update from here cost the plugin's loop most of its
+        # time at a few thousand pods/s)
+        self.state.observe(pod, mirror_only=self._feed)
         self._observed.set()
 
     async def _await_informer(self, found, timeout: float = INFORMER_WAIT_S):
@@ -322,6 +326,7 @@ class GpuSharePlugin:
                 pass
             self._native.close()
             self._native = None
+        self._feed = False
 
     # ------------------------------------------------------------ gRPC handlers
     async def GetDevicePluginOptions(self, request, context):
@@ -709,6 +714,7 @@ class GpuSharePlugin:
             self._native = native().DpServer(self.socket_path, self.state.core, cfg)
             if os.environ.get("GSX_PLUGIN_FEED", "1") == "1":
                 self._native.start_feed(cfg["api"])  # this node's pods into the state from a native reflector
+                self._feed = True
             self._sync_native()
             if os.environ.get("GSX_PLUGIN_SERVE_THREAD", "1") == "1":
                 # the endpoint is served from a native thread that never needs the GIL (a native lock guards the

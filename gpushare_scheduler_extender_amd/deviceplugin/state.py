@@ -104,6 +104,11 @@ class PodRec:
         return self.phase in ("Pending", "")
 
 
+def _older_rv(a: str, b: str) -> bool:
+    """resourceVersion a < b when both are integers (the native state's rule)."""
+    return a.isdigit() and b.isdigit() and int(a) < int(b)
+
+
 class _Inflight:
     """Pods claimed by an Allocate whose ASSIGNED patch is in flight (the native set, set-like)."""
 
@@ -168,10 +173,23 @@ class AllocationState:
                       hold_idx=podutil.hold_idx(pod), hold_partner=ann.get(POD_HOLD_PARTNER_ANNOTATION, ""),
                       obj=pod)
 
-    def observe(self, pod: dict) -> None:
-        """An added / updated pod (informer event, LIST item, or our own PATCH response)."""
+    def observe(self, pod: dict, mirror_only: bool = False) -> None:
+        """An added / updated pod (informer event, LIST item, or our own PATCH response).
+
+        ``mirror_only``: the native state already receives this event from its own pod feed (the plugin's native
+        endpoint watches the node's pods itself): only the Python view is updated, with the native state's rule for
+        which pods it holds, and the native state is left to the feed."""
         rec = self._rec(pod)
         if not rec.uid:
+            return
+        if mirror_only:
+            old = self._recs.get(rec.uid)
+            if old is not None and _older_rv(rec.rv, old.rv):
+                return  # a slow copy: never step back
+            if podutil.node_name(pod) == self.node and rec.request > 0 and not rec.complete:
+                self._recs[rec.uid] = rec
+            else:
+                self._recs.pop(rec.uid, None)
             return
         ap = native().AllocPod()
         ap.uid, ap.key, ap.namespace, ap.name, ap.rv = rec.uid, rec.key, rec.namespace, rec.name, rec.rv
