@@ -99,10 +99,11 @@ def main(argv=None) -> int:
         logging.getLogger("gsx.main").warning(
             "stopping: %s; grpc %s; per Allocate ms: %s", plugin.stats, plugin.debug_state().get("grpc"),
             {k: round(1e3 * v / n, 4) for k, v in plugin.timing.items() if isinstance(v, float)})
-        if os.environ.get("GSX_PLUGIN_CPROFILE_DIR"):
+        stats_dir = os.environ.get("GSX_PLUGIN_STATS_DIR") or os.environ.get("GSX_PLUGIN_CPROFILE_DIR")
+        if stats_dir:  # diagnosis: the plugin's counters and timings at exit
             import json  # noqa: PLC0415
 
-            with open(os.path.join(os.environ["GSX_PLUGIN_CPROFILE_DIR"], f"plugin-{os.getpid()}.json"), "w") as f:
+            with open(os.path.join(stats_dir, f"plugin-{os.getpid()}.json"), "w") as f:
                 json.dump({"stats": plugin.stats, "debug": plugin.debug_state(), "timing": plugin.timing}, f,
                           default=str)
         await plugin.stop()
