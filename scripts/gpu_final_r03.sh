@@ -28,7 +28,7 @@ timeout -k 10 900 python -u bench.py --gpus 1 --steps 25000 --warmup 5 --sweep 0
 python -c "
 import json; d=json.load(open('$OUT/soak.json'))
 print('soak', d['steps'], d['value'], d['wave_pods_per_s'], d['rss_mib'], {k: d['node_agent'].get(k) for k in ('admitted','failed','bad_stamps')})"
-timeout -k 10 900 python -u bench.py --gpus 1 --steps 5000 --warmup 10 --sweep 0 --node-agent native-plugin \
+GSX_PLUGIN_STATS_DIR=$PWD/$OUT timeout -k 10 900 python -u bench.py --gpus 1 --steps 5000 --warmup 10 --sweep 0 --node-agent native-plugin \
   --json-out $OUT/soak_plugin.json > $OUT/soak_plugin.log 2>&1 || exit $?
 python -c "
 import json; d=json.load(open('$OUT/soak_plugin.json'))
