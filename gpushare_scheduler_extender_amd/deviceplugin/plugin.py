@@ -255,7 +255,9 @@ class GpuSharePlugin:
                 "mount_mode": self.mount_mode, "unit_bytes": UNITS[self.unit],
                 "iso_dir": str(self.isolation.host_dir) if self.isolation is not None else None,
                 "guard": self.reconciler is not None, "api": api_dict(self.client.config),
-                "fast": os.environ.get("GSX_PLUGIN_FAST", "1") == "1"}
+                "fast": os.environ.get("GSX_PLUGIN_FAST", "1") == "1",
+                # the serving thread polls this long after a pass before it sleeps (kubelet's calls come in bursts)
+                "spin_us": float(os.environ.get("GSX_PLUGIN_SPIN_US", "200"))}
 
     def native_device(self, d: Device) -> dict:
         return {"index": d.index, "bdf": d.bdf, "cu_count": d.cu_count, "total_bytes": d.total_bytes,

@@ -327,7 +327,7 @@ class Engine {
 
   // ---- native HTTP front end (server.h) ----
   int serve(const std::string& host, int port, int threads, int pool_threads, int fallback_port, bool native_bind,
-            double ttl, const py::dict& api, bool update_mode) {
+            double ttl, const py::dict& api, bool update_mode, double spin_us) {
     if (srv_) throw std::runtime_error("native server already running");
     ServerConfig cfg;
     cfg.host = host;
@@ -338,6 +338,7 @@ class Engine {
     cfg.native_bind = native_bind;
     cfg.update_mode = update_mode;
     cfg.reservation_ttl = ttl;
+    cfg.spin_us = spin_us;
     cfg.api = api_from(api);
     if (cfg.api.server.empty()) cfg.native_bind = false;
     srv_.reset(new NativeServer(&l_, cfg));
@@ -750,6 +751,7 @@ class PyDpServer {
     if (cfg.contains("guard")) c.guard = cfg["guard"].cast<bool>();
     if (cfg.contains("api") && !cfg["api"].is_none()) c.api = api_from(cfg["api"].cast<py::dict>());
     if (cfg.contains("fast")) fast_ = cfg["fast"].cast<bool>();
+    if (cfg.contains("spin_us")) spin_us_ = cfg["spin_us"].cast<double>();
     node_ = c.node;
     profile_ = c.profile;
     state_ = &state;
@@ -963,9 +965,20 @@ class PyDpServer {
   void serve() {
     pthread_setname_np(pthread_self(), "gsx-dp-serve");
     const int ep = srv_ ? srv_->fd() : -1;
+    // kubelet's calls come in bursts (GetPreferredAllocation, then Allocate, then the next pod's): after a pass
+    // the thread polls without sleeping for spin_us_ before it blocks, so the next call of the burst does not pay
+    // a sleep / wake-up of this thread (and of its idle core) on kubelet's serial admission path
+    double spin_until = 0;
     for (;;) {
       pollfd pf{ep, POLLIN, 0};
-      ::poll(&pf, 1, 100);
+      if (mono() < spin_until) {
+        if (::poll(&pf, 1, 0) == 0) {
+          if (stop_serving_) return;  // read without the lock: only a faster exit; checked again below
+          continue;
+        }
+      } else {
+        ::poll(&pf, 1, 100);
+      }
       std::unique_lock<std::recursive_mutex> lock(alloc_mu());  // the state lock, not the GIL
       if (stop_serving_ || !srv_) return;
       one_pass();
@@ -989,6 +1002,7 @@ class PyDpServer {
         finish_patches();
         if (stop_serving_ || !srv_) return;
       }
+      spin_until = spin_us_ > 0 ? mono() + spin_us_ * 1e-6 : 0;
       // also when the feed released a pod whose records went: Python cleans up their isolation files
       if (!pending_.empty() || !events_.empty() || (state_ && state_->dropped_pending())) {
         uint64_t one = 1;
@@ -1200,8 +1214,9 @@ class PyDpServer {
   bool have_list_ = false, fast_ = true;
   // start_serving(): the pass runs on this thread, the GIL as the state mutex
   std::thread serving_;
-  bool stop_serving_ = false;  // GIL held
+  std::atomic<bool> stop_serving_{false};  // written under the state lock
   int pyfd_ = -1;              // readable: pending_ / events_ waiting for poll()
+  double spin_us_ = 200;       // poll without sleeping this long after a pass (cfg "spin_us"; 0: always block)
   uint64_t passes_ = 0;
 };
 
@@ -1285,7 +1300,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("parse_pod", &Engine::parse_pod)
       .def("serve", &Engine::serve, py::arg("host"), py::arg("port"), py::arg("threads") = 2,
            py::arg("pool_threads") = 16, py::arg("fallback_port") = 0, py::arg("native_bind") = true,
-           py::arg("ttl") = 60.0, py::arg("api") = py::dict(), py::arg("update_mode") = false)
+           py::arg("ttl") = 60.0, py::arg("api") = py::dict(), py::arg("update_mode") = false,
+           py::arg("spin_us") = 0.0)
       .def("stop_server", &Engine::stop_server)
       .def("start_controller", &Engine::start_controller, py::arg("api"), py::arg("resync") = 30.0,
            py::arg("sync_timeout") = 60.0, py::arg("watch_timeout") = 300)
