@@ -41,7 +41,6 @@ annotations, same best-fit device, same error strings):
 from __future__ import annotations
 
 import asyncio
-import os
 import json
 import logging
 import time
@@ -429,8 +428,7 @@ class ExtenderRunner:
             native_bind = self.server.client.limiter.qps <= 0
             self.port = self.server.engine.serve(self.host, self.port, self.http_threads, self.pool_threads,
                                                  self.internal_port, native_bind, self.server.reservation_ttl, api,
-                                                 update_mode=self.server.bind_mode == "update",
-                                                 spin_us=float(os.environ.get("GSX_SPIN_US", "0") or 0))
+                                                 update_mode=self.server.bind_mode == "update")
             self.server.native_server = True
             self._drain = asyncio.get_running_loop().create_task(self._drain_failures())
         else:

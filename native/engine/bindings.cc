@@ -327,7 +327,7 @@ class Engine {
 
   // ---- native HTTP front end (server.h) ----
   int serve(const std::string& host, int port, int threads, int pool_threads, int fallback_port, bool native_bind,
-            double ttl, const py::dict& api, bool update_mode, double spin_us) {
+            double ttl, const py::dict& api, bool update_mode) {
     if (srv_) throw std::runtime_error("native server already running");
     ServerConfig cfg;
     cfg.host = host;
@@ -338,7 +338,6 @@ class Engine {
     cfg.native_bind = native_bind;
     cfg.update_mode = update_mode;
     cfg.reservation_ttl = ttl;
-    cfg.spin_us = spin_us;
     cfg.api = api_from(api);
     if (cfg.api.server.empty()) cfg.native_bind = false;
     srv_.reset(new NativeServer(&l_, cfg));
@@ -1300,8 +1299,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("parse_pod", &Engine::parse_pod)
       .def("serve", &Engine::serve, py::arg("host"), py::arg("port"), py::arg("threads") = 2,
            py::arg("pool_threads") = 16, py::arg("fallback_port") = 0, py::arg("native_bind") = true,
-           py::arg("ttl") = 60.0, py::arg("api") = py::dict(), py::arg("update_mode") = false,
-           py::arg("spin_us") = 0.0)
+           py::arg("ttl") = 60.0, py::arg("api") = py::dict(), py::arg("update_mode") = false)
       .def("stop_server", &Engine::stop_server)
       .def("start_controller", &Engine::start_controller, py::arg("api"), py::arg("resync") = 30.0,
            py::arg("sync_timeout") = 60.0, py::arg("watch_timeout") = 300)

@@ -243,11 +243,8 @@ void NativeServer::record_failure(BindFailure f) {
 
 void NativeServer::run_loop(Loop* lp) {
   epoll_event evs[128];
-  double spin_until = 0;
   while (!stop_.load()) {
-    const bool spinning = cfg_.spin_us > 0 && mono() < spin_until;
-    int n = epoll_wait(lp->ep, evs, 128, spinning ? 0 : 500);
-    if (n > 0 && cfg_.spin_us > 0) spin_until = mono() + cfg_.spin_us * 1e-6;
+    int n = epoll_wait(lp->ep, evs, 128, 500);
     for (int i = 0; i < n; ++i) {
       uint64_t id = evs[i].data.u64;
       if (id == kListenId) {

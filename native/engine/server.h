@@ -54,9 +54,6 @@ struct ServerConfig {
   double reservation_ttl = 60.0;
   ApiConfig api;
   size_t max_body = 64u << 20;
-  // after serving events an epoll loop polls without sleeping this long before it blocks again (kube-scheduler's
-  // filter and bind calls come in bursts; 0: always block)
-  double spin_us = 0;
 };
 
 struct BindFailure {
