@@ -155,8 +155,10 @@ class Cluster:
         raise TimeoutError("node agent never became ready")
 
     def _agent(self):
-        return start_node_agent(self.api.url, NODE, profile=self.profile.name, native=self.agent_kind == "native",
-                                plugin="inproc" if self.agent_kind == "inproc" else "grpc", extra=self.agent_args)
+        kind = self.agent_kind
+        plugin = {"inproc": "inproc", "native-plugin": "spawn"}.get(kind, "grpc")
+        return start_node_agent(self.api.url, NODE, profile=self.profile.name, native=kind.startswith("native"),
+                                plugin=plugin, extra=self.agent_args, serial_admission=kind == "native-serial")
 
     def agent_child(self):
         return next(ch for ch in self.children if ch.name == "node-agent")
@@ -540,9 +542,11 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpu", action="store_true", help="real MI355X sizes, HBM arena and CU probe (needs a GPU)")
     ap.add_argument("--only", default="", help="comma-separated config numbers")
-    ap.add_argument("--agent", default="plugin", choices=["plugin", "inproc", "native"],
+    ap.add_argument("--agent", default="plugin", choices=["plugin", "inproc", "native", "native-serial", "native-plugin"],
                     help="kubelet + device plugin: the shipped gRPC plugin driven over its socket (default), "
-                         "the same in-process, or the compiled gsx-nodeagent")
+                         "the same in-process, the compiled gsx-nodeagent (its in-process matcher admitting on all "
+                         "workers, or serially as kubelet: native-serial), or gsx-nodeagent calling the shipped "
+                         "plugin process over gRPC (native-plugin)")
     ap.add_argument("--faithful", action="store_true",
                     help="the kubelet stand-in behaves like kubelet (no re-routing, sorted batches, PodResources); "
                          "the plugin reconciles against it")

@@ -52,6 +52,7 @@ def _committed_use(cl, bound: dict) -> tuple[list[int], int]:
                                                   (11, "plugin", "binding"),
                                                   (23, "native", "binding"),
                                                   (11, "native", "binding"),
+                                                  (17, "native-plugin", "binding"),
                                                   (13, "plugin", "update"),
                                                   (7, "faithful", "binding"),
                                                   (29, "faithful", "update"),

@@ -15,7 +15,7 @@ def test_baseline_config_cpu(k, tmp_path):
     assert configs.main(["--only", str(k), "--json-out", str(tmp_path / "r.json")]) == 0
 
 
-@pytest.mark.parametrize("agent", ["inproc", "native"])
+@pytest.mark.parametrize("agent", ["inproc", "native", "native-serial", "native-plugin"])
 def test_configs_agree_across_agents(agent, tmp_path):
     """Same placements and partitions whichever agent plays kubelet + plugin (one Allocate contract)."""
     outs = {}
