@@ -56,6 +56,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# the load generator's pod creates in flight at once (keep-alive connections of its batch client)
+CREATE_CONCURRENCY = int(os.environ.get("GSX_CREATE_CONCURRENCY", "16"))
 BASELINE_BINDS_PER_S = 2.5  # derived reference ceiling (client-go QPS 5 / 2 calls per bind)
 NODE = "mi355x-node-0"
 
@@ -675,7 +677,7 @@ def main():
     def wave(step: int):
         names, keys, reqs = wave_requests(step)
         t0 = time.perf_counter()
-        res = api_batch.run(reqs, min(16, n_pods))
+        res = api_batch.run(reqs, min(CREATE_CONCURRENCY, n_pods))
         bad = [(st, b[:200]) for st, b in res if st != 201]
         if bad:
             raise RuntimeError(f"pod create failed: {bad[:3]}")
