@@ -809,6 +809,18 @@ class GpuSharePlugin:
         lines += [f'gpushare_plugin_cu_free{{device="{i}"}} {cp.free_count()}' for i, cp in self.state.cus.items()]
         lines.append("# TYPE gpushare_plugin_allocate_candidates gauge")
         lines.append(f"gpushare_plugin_allocate_candidates {len(self.state.candidates())}")
+        if self._native is not None:
+            # the native gRPC endpoint: calls answered on its fast path vs handed to the Python handlers
+            ns = self._native.stats()
+            for k in ("fast_allocate", "fast_preferred", "slow_allocate", "slow_preferred", "patch_failures", "waited",
+                      "feed_events", "calls"):
+                lines += [f"# TYPE gpushare_plugin_native_{k}_total counter", f"gpushare_plugin_native_{k}_total {ns.get(k, 0)}"]
+        n = self.timing.get("n", 0)
+        if n:
+            # mean time per Allocate inside the plugin: handler total, match, ASSIGNED patch (seconds)
+            for k in ("handler", "match", "assign_patch"):
+                lines += [f"# TYPE gpushare_plugin_allocate_{k}_seconds gauge",
+                          f"gpushare_plugin_allocate_{k}_seconds {self.timing.get(k, 0.0) / n:.9f}"]
         return "\n".join(lines) + "\n"
 
     async def serve_debug(self, host: str, port: int) -> int:

@@ -82,6 +82,11 @@ def test_grpcio_kubelet_against_the_native_endpoint():
                 assert (await client.get("pods", f"p{i}", "default"))["metadata"]["annotations"][
                     P.annotation_assigned] == "true"
             assert len(plugin.state.records) == 3 and plugin.stats["allocate_native"] == 3
+            # the endpoint's own counters and the plugin's per-Allocate times on /metrics
+            m = plugin.metrics_text()
+            assert "gpushare_plugin_native_fast_allocate_total 3" in m, m
+            assert "gpushare_plugin_native_slow_allocate_total" in m and "gpushare_plugin_allocate_handler_seconds" in m
+            assert st["serving_thread"], st  # served from the native thread, not the event loop
         finally:
             await _close(api_srv, client, plugin, pc)
     asyncio.run(go())
