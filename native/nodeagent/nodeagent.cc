@@ -126,6 +126,9 @@ class Agent {
     }
   }
 
+  // kubelet admits a node's pods one at a time (Allocate included): with this set the in-process matcher does too
+  void set_serial_admission(bool on) { serial_admission_ = on; }
+
   void set_plugin_socket(const std::string& s) { plugin_sock_ = s; }
   void set_plugin_spawn(const std::string& python, const std::string& apiserver, const std::string& profile,
                         const std::string& unit) {
@@ -844,12 +847,7 @@ class Agent {
   int64_t unit_;
   int nworkers_;
   bool verify_;
- public:
-  // kubelet admits a node's pods one at a time (Allocate included): with this set the in-process matcher does too
-  void set_serial_admission(bool on) { serial_admission_ = on; }
-
- private:
-  bool serial_admission_ = false;
+  bool serial_admission_ = false;  // set_serial_admission
   ApiClient api_;
   std::map<int, Device> devices_;
   std::unique_ptr<AllocState> state_;  // the device plugin's matcher (allocstate.h)
