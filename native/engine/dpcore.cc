@@ -172,7 +172,9 @@ DpCore::DpCore(DpConfig cfg, AllocState* state) : cfg_(std::move(cfg)), state_(s
 void DpCore::set_devices(std::vector<DpDevice> devs, std::map<std::string, int> id_owner) {
   devs_.clear();
   for (auto& d : devs) devs_[d.index] = std::move(d);
-  id_owner_ = std::move(id_owner);
+  id_owner_ = std::unordered_map<std::string, int>(id_owner.begin(), id_owner.end());
+  id_owner_view_.clear();
+  for (const auto& kv : id_owner_) id_owner_view_.emplace(std::string_view(kv.first), kv.second);
 }
 
 int64_t DpCore::physical_used(int dev) const {
@@ -184,8 +186,8 @@ int64_t DpCore::physical_used(int dev) const {
 }
 
 bool DpCore::preferred(const std::string& req, std::string* resp, std::string* why) {
-  std::vector<dp::PreferredRequest> reqs;
-  if (!dp::decode_preferred_request(req, &reqs)) {
+  std::vector<dp::PreferredRequestView> reqs;  // views into `req`: no string per ID
+  if (!dp::decode_preferred_request(std::string_view(req), &reqs)) {
     *why = "malformed request";
     return false;
   }
@@ -197,18 +199,18 @@ bool DpCore::preferred(const std::string& req, std::string* resp, std::string* w
       *why = "no pending pod of that size known yet";
       return false;
     }
-    std::vector<std::string> chosen(r.must_include);
-    std::set<std::string> taken(chosen.begin(), chosen.end());
-    std::vector<std::string> pref, rest;
-    for (const auto& id : r.available) {
-      if (taken.count(id)) continue;
-      auto o = id_owner_.find(id);
-      (o != id_owner_.end() && o->second == want ? pref : rest).push_back(id);
-    }
-    for (auto* v : {&pref, &rest}) {
-      for (const auto& id : *v) {
+    // kubelet sends every free ID of the node (hundreds): pick the first `size` of them, the pod's GPU's first,
+    // copying only what is chosen
+    std::vector<std::string> chosen;
+    for (auto id : r.must_include) chosen.emplace_back(id);
+    std::set<std::string_view> taken(r.must_include.begin(), r.must_include.end());
+    for (int pass = 0; pass < 2 && static_cast<int32_t>(chosen.size()) < r.size; ++pass) {
+      for (auto id : r.available) {
         if (static_cast<int32_t>(chosen.size()) >= r.size) break;
-        chosen.push_back(id);
+        auto o = id_owner_view_.find(id);
+        const bool on_gpu = o != id_owner_view_.end() && o->second == want;
+        if (on_gpu != (pass == 0) || (!taken.empty() && taken.count(id))) continue;
+        chosen.emplace_back(id);
       }
     }
     if (static_cast<int32_t>(chosen.size()) > r.size) chosen.resize(static_cast<size_t>(r.size));

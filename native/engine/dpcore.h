@@ -13,8 +13,10 @@
 
 #include <cstdint>
 #include <map>
+#include <unordered_map>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "allocstate.h"
@@ -108,7 +110,8 @@ class DpCore {
   AllocState* state_;
   std::unique_ptr<ApiClient> api_;
   std::map<int, DpDevice> devs_;
-  std::map<std::string, int> id_owner_;
+  std::unordered_map<std::string, int> id_owner_;
+  std::unordered_map<std::string_view, int> id_owner_view_;  // keys view id_owner_'s strings
   uint64_t aid_ = 0;
   Stats stats_;
 };

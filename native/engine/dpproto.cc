@@ -1,5 +1,7 @@
 #include "dpproto.h"
 
+#include <string_view>
+
 namespace gsx::dp {
 namespace {
 
@@ -41,7 +43,7 @@ std::string map_entry(const std::string& k, const std::string& v) {
 struct Reader {
   const uint8_t* p;
   const uint8_t* end;
-  explicit Reader(const std::string& s)
+  explicit Reader(std::string_view s)
       : p(reinterpret_cast<const uint8_t*>(s.data())), end(reinterpret_cast<const uint8_t*>(s.data()) + s.size()) {}
   bool done() const { return p >= end; }
   bool varint(uint64_t* v) {
@@ -54,7 +56,7 @@ struct Reader {
     return false;
   }
   // next field: number, wire type and (for wire 2) the payload; other wire types are skipped into *num only
-  bool next(int* field, int* wire, std::string* payload, uint64_t* value) {
+  bool next(int* field, int* wire, std::string_view* payload, uint64_t* value) {
     uint64_t t;
     if (!varint(&t)) return false;
     *field = static_cast<int>(t >> 3);
@@ -69,7 +71,7 @@ struct Reader {
       case 2: {
         uint64_t n;
         if (!varint(&n) || static_cast<uint64_t>(end - p) < n) return false;
-        payload->assign(reinterpret_cast<const char*>(p), n);
+        *payload = std::string_view(reinterpret_cast<const char*>(p), n);  // a view into the message: no copy
         p += n;
         return true;
       }
@@ -84,11 +86,11 @@ struct Reader {
 };
 
 template <typename Fn>
-bool each(const std::string& msg, Fn fn) {
+bool each(std::string_view msg, Fn fn) {
   Reader r(msg);
   while (!r.done()) {
     int f, w;
-    std::string pl;
+    std::string_view pl;
     uint64_t v = 0;
     if (!r.next(&f, &w, &pl, &v)) return false;
     if (!fn(f, w, pl, v)) return false;
@@ -96,8 +98,8 @@ bool each(const std::string& msg, Fn fn) {
   return true;
 }
 
-bool decode_map_entry(const std::string& e, std::string* k, std::string* v) {
-  return each(e, [&](int f, int w, const std::string& pl, uint64_t) {
+bool decode_map_entry(std::string_view e, std::string* k, std::string* v) {
+  return each(e, [&](int f, int w, std::string_view pl, uint64_t) {
     if (w == 2 && f == 1) *k = pl;
     if (w == 2 && f == 2) *v = pl;
     return true;
@@ -191,11 +193,11 @@ std::string encode_preferred_request(const std::vector<PreferredRequest>& reqs) 
 }
 
 bool decode_allocate_request(const std::string& msg, std::vector<std::vector<std::string>>* out) {
-  return each(msg, [&](int f, int w, const std::string& pl, uint64_t) {
+  return each(msg, [&](int f, int w, std::string_view pl, uint64_t) {
     if (f != 1 || w != 2) return true;
     std::vector<std::string> ids;
-    bool ok = each(pl, [&](int f2, int w2, const std::string& pl2, uint64_t) {
-      if (f2 == 1 && w2 == 2) ids.push_back(pl2);
+    bool ok = each(pl, [&](int f2, int w2, std::string_view pl2, uint64_t) {
+      if (f2 == 1 && w2 == 2) ids.emplace_back(pl2);
       return true;
     });
     out->push_back(std::move(ids));
@@ -203,11 +205,11 @@ bool decode_allocate_request(const std::string& msg, std::vector<std::vector<std
   });
 }
 
-bool decode_preferred_request(const std::string& msg, std::vector<PreferredRequest>* out) {
-  return each(msg, [&](int f, int w, const std::string& pl, uint64_t) {
+bool decode_preferred_request(std::string_view msg, std::vector<PreferredRequestView>* out) {
+  return each(msg, [&](int f, int w, std::string_view pl, uint64_t) {
     if (f != 1 || w != 2) return true;
-    PreferredRequest r;
-    bool ok = each(pl, [&](int f2, int w2, const std::string& pl2, uint64_t v) {
+    PreferredRequestView r;
+    bool ok = each(pl, [&](int f2, int w2, std::string_view pl2, uint64_t v) {
       if (f2 == 1 && w2 == 2) r.available.push_back(pl2);
       if (f2 == 2 && w2 == 2) r.must_include.push_back(pl2);
       if (f2 == 3 && w2 == 0) r.size = static_cast<int32_t>(v);
@@ -219,10 +221,10 @@ bool decode_preferred_request(const std::string& msg, std::vector<PreferredReque
 }
 
 bool decode_list_and_watch(const std::string& msg, std::vector<DeviceMsg>* out) {
-  return each(msg, [&](int f, int w, const std::string& pl, uint64_t) {
+  return each(msg, [&](int f, int w, std::string_view pl, uint64_t) {
     if (f != 1 || w != 2) return true;
     DeviceMsg d;
-    bool ok = each(pl, [&](int f2, int w2, const std::string& pl2, uint64_t) {
+    bool ok = each(pl, [&](int f2, int w2, std::string_view pl2, uint64_t) {
       if (f2 == 1 && w2 == 2) d.id = pl2;
       if (f2 == 2 && w2 == 2) d.health = pl2;
       return true;
@@ -237,17 +239,17 @@ bool decode_preferred_response(const std::string& msg, std::vector<std::vector<s
 }
 
 bool decode_allocate_response(const std::string& msg, std::vector<ContainerResponse>* out) {
-  return each(msg, [&](int f, int w, const std::string& pl, uint64_t) {
+  return each(msg, [&](int f, int w, std::string_view pl, uint64_t) {
     if (f != 1 || w != 2) return true;
     ContainerResponse r;
-    bool ok = each(pl, [&](int f2, int w2, const std::string& pl2, uint64_t) {
+    bool ok = each(pl, [&](int f2, int w2, std::string_view pl2, uint64_t) {
       if (w2 != 2) return true;
       std::string k, v;
       if (f2 == 1 && decode_map_entry(pl2, &k, &v)) r.envs[k] = v;
       if (f2 == 4 && decode_map_entry(pl2, &k, &v)) r.annotations[k] = v;
       if (f2 == 2) {
         MountMsg m;
-        each(pl2, [&](int f3, int w3, const std::string& pl3, uint64_t v3) {
+        each(pl2, [&](int f3, int w3, std::string_view pl3, uint64_t v3) {
           if (f3 == 1 && w3 == 2) m.container_path = pl3;
           if (f3 == 2 && w3 == 2) m.host_path = pl3;
           if (f3 == 3 && w3 == 0) m.read_only = v3 != 0;
@@ -257,7 +259,7 @@ bool decode_allocate_response(const std::string& msg, std::vector<ContainerRespo
       }
       if (f2 == 3) {
         DeviceSpecMsg d;
-        each(pl2, [&](int f3, int w3, const std::string& pl3, uint64_t) {
+        each(pl2, [&](int f3, int w3, std::string_view pl3, uint64_t) {
           if (f3 == 1 && w3 == 2) d.container_path = pl3;
           if (f3 == 2 && w3 == 2) d.host_path = pl3;
           if (f3 == 3 && w3 == 2) d.permissions = pl3;

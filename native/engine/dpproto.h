@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <map>
 #include <string>
+#include <string_view>
 #include <vector>
 
 namespace gsx::dp {
@@ -34,6 +35,11 @@ struct PreferredRequest {
   std::vector<std::string> available, must_include;
   int32_t size = 0;
 };
+// The same, as views into the request message (kubelet sends every free ID of the node: hundreds of strings)
+struct PreferredRequestView {
+  std::vector<std::string_view> available, must_include;
+  int32_t size = 0;
+};
 
 // ---- encode
 std::string encode_options(bool pre_start_required, bool preferred_available);
@@ -45,7 +51,7 @@ std::string encode_preferred_request(const std::vector<PreferredRequest>& reqs);
 
 // ---- decode (false: malformed)
 bool decode_allocate_request(const std::string& msg, std::vector<std::vector<std::string>>* ids_per_container);
-bool decode_preferred_request(const std::string& msg, std::vector<PreferredRequest>* reqs);
+bool decode_preferred_request(std::string_view msg, std::vector<PreferredRequestView>* reqs);  // views into msg
 bool decode_list_and_watch(const std::string& msg, std::vector<DeviceMsg>* devs);
 bool decode_preferred_response(const std::string& msg, std::vector<std::vector<std::string>>* per_container);
 bool decode_allocate_response(const std::string& msg, std::vector<ContainerResponse>* per_container);
