@@ -385,7 +385,11 @@ class Agent {
     if (r == running_.end()) return;
     int dev = r->second;
     running_.erase(r);
-    used_ids_.erase(uid);
+    auto ui = used_ids_.find(uid);
+    if (ui != used_ids_.end()) {
+      for (const auto& id : ui->second) used_all_.erase(id);
+      used_ids_.erase(ui);
+    }
     for (auto& kv : devices_) {
       if (CuPartitioner* cp = state_->cus(kv.first)) cp->release(uid);
     }
@@ -522,11 +526,10 @@ class Agent {
     const std::string my_uid = mine->uid, my_key = key;
     if (running_.count(my_uid) || state_->inflight(my_uid)) return;
     const int64_t units = mine->request;
-    std::unordered_set<std::string> used;
-    for (const auto& kv : used_ids_) used.insert(kv.second.begin(), kv.second.end());
-    dp::PreferredRequest pr;
+    dp::PreferredRequest pr;  // kubelet's free IDs: every healthy ID no running container holds
+    pr.available.reserve(all_ids_.size());
     for (const auto& id : all_ids_) {
-      if (!used.count(id)) pr.available.push_back(id);
+      if (!used_all_.count(id)) pr.available.push_back(id);
     }
     pr.size = static_cast<int32_t>(units);
     if (static_cast<int64_t>(pr.available.size()) < units) {
@@ -588,6 +591,7 @@ class Agent {
     }
     if (running_.count(uid) || !keys_.count(key)) return;  // already started, or gone meanwhile
     used_ids_[uid] = chosen[0];
+    used_all_.insert(chosen[0].begin(), chosen[0].end());
     auto idx = cr.envs.find(p_.a_idx);
     const int dev_idx = idx == cr.envs.end() ? -1 : std::atoi(idx->second.c_str());
     if (!devices_.count(dev_idx)) return;
@@ -858,6 +862,7 @@ class Agent {
   std::mutex dp_mu_;
   std::vector<std::string> all_ids_;
   std::unordered_map<std::string, std::vector<std::string>> used_ids_;  // uid -> the IDs its Allocate took
+  std::unordered_set<std::string> used_all_;                             // the union of used_ids_, kept with it
   std::unordered_map<std::string, std::string> keys_;  // ns/name -> uid of every pod the informer delivered
   std::map<int, std::unique_ptr<ApiClient>> runtimes_;
   std::unique_ptr<Reflector> pods_r_;
