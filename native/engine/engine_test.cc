@@ -19,6 +19,7 @@
 #include <memory>
 #include <vector>
 
+#include "allocstate.h"
 #include "http.h"
 #include "json.h"
 #include "ledger.h"
@@ -394,10 +395,66 @@ static void test_server_stress() {
   api.join();
 }
 
+// Landing-order Allocate matching (allocstate.h) and the per-node bind order it lets the ledger drop (ledger.h).
+static void test_landing_order() {
+  AllocState st("n", {{0, {256, 8}}, {1, {256, 8}}});
+  auto pod = [](const char* uid, const char* rv, int64_t dev, int64_t assume) {
+    AllocPod p;
+    p.uid = uid;
+    p.key = std::string("default/") + uid;
+    p.ns = "default";
+    p.name = uid;
+    p.rv = rv;
+    p.phase = "Pending";
+    p.node = "n";
+    p.dev = dev;
+    p.request = 8;
+    p.containers = {8};
+    p.assume_time = assume;
+    p.assigned = "false";
+    return p;
+  };
+  CHECK(st.observe(pod("late", "5", 0, 30)));    // assumed last, landed first
+  CHECK(st.observe(pod("early", "9", 1, 10)));
+  auto c = st.candidates();
+  CHECK(c.size() == 2 && c[0]->uid == "late" && c[1]->uid == "early");
+  CHECK(st.observe(pod("late", "12", 0, 30)));   // a later copy keeps its landing
+  CHECK(st.match(8).first && st.match(8).first->uid == "late");
+  CHECK(!st.observe(pod("early", "3", 1, 10)));  // an older copy is ignored
+  AllocPod norv = pod("norv", "", 0, 1);         // no integer resourceVersion: ASSUME_TIME decides, after both
+  CHECK(st.observe(norv));
+  c = st.candidates();
+  CHECK(c.size() == 3 && c[2]->uid == "norv");
+
+  for (int mode = 0; mode < 3; ++mode) {  // auto / strict / relaxed on a landing-order node and a plain one
+    for (int landing = 0; landing < 2; ++landing) {
+      Ledger l{Profile()};
+      l.set_order_mode(static_cast<Ledger::OrderMode>(mode));
+      NodeView nv;
+      nv.name = "n";
+      nv.total = 2 * 16;
+      nv.count = 2;
+      nv.landing_order = landing == 1;
+      l.upsert_node(nv);
+      int64_t total = 0, ns = 0;
+      uint64_t sa = 0, sb = 0;
+      CHECK(l.assume_ordered("ua", "default", "a", "n", 10, &total, &sa, &ns) == 0);
+      CHECK(l.assume_ordered("ub", "default", "b", "n", 10, &total, &sb, &ns) == 1);
+      const bool want_blocked = mode == Ledger::kOrderStrict || (mode == Ledger::kOrderAuto && !landing);
+      CHECK(l.bind_blocked(sb) == want_blocked);
+      CHECK(!l.bind_blocked(sa));
+      l.bind_leave(sa);
+      CHECK(!l.bind_blocked(sb));
+      l.bind_leave(sb);
+    }
+  }
+}
+
 int main() {
   test_json();
   test_quantity();
   test_ledger();
+  test_landing_order();
   test_http();
   test_request_parser();
   test_server_stress();
