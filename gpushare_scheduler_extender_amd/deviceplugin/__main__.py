@@ -104,7 +104,10 @@ def main(argv=None) -> int:
             import json  # noqa: PLC0415
 
             with open(os.path.join(stats_dir, f"plugin-{os.getpid()}.json"), "w") as f:
-                json.dump({"stats": plugin.stats, "debug": plugin.debug_state(), "timing": plugin.timing}, f,
+                import resource  # noqa: PLC0415
+
+                json.dump({"stats": plugin.stats, "debug": plugin.debug_state(), "timing": plugin.timing,
+                           "max_rss_mib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024, 1)}, f,
                           default=str)
         await plugin.stop()
         await client.close()
