@@ -44,7 +44,7 @@ import grpc
 from ..k8s.client import ApiError, KubeClient
 from ..models import pod as podutil
 from ..models.profile import (NODE_ALLOCATE_ORDER_ANNOTATION, NODE_DEVICE_INFO_ANNOTATION, NODE_DEVICE_MEMORY_ANNOTATION,
-                              NamingProfile)
+                              POD_CU_MASK_ANNOTATION, NamingProfile)
 from . import api
 from ..k8s.informer import Handler, Informer
 from .allocator import AllocateError, ContainerAllocation, assigned_patch, build_response
@@ -114,6 +114,9 @@ class GpuSharePlugin:
         self.isolation = isolation
         self._set_devices(devices)
         self.checkpoint = checkpoint if checkpoint is not None else os.path.join(socket_dir, "gsx-allocations.json")
+        self.journal_path = (self.checkpoint or os.path.join(socket_dir, "gsx-allocations.json")) + ".journal"
+        # opt-in: needs the journal next to the checkpoint (the record must be durable before kubelet's answer)
+        self.early_answer = bool(self.checkpoint) and os.environ.get("GSX_PLUGIN_EARLY_ANSWER", "0") == "1"
         self.checkpoint_interval = 0.2
         self._dirty = False
         self._persist_task: asyncio.Task | None = None
@@ -257,7 +260,10 @@ class GpuSharePlugin:
                 "guard": self.reconciler is not None, "api": api_dict(self.client.config),
                 "fast": os.environ.get("GSX_PLUGIN_FAST", "1") == "1",
                 # the serving thread polls this long after a pass before it sleeps (kubelet's calls come in bursts)
-                "spin_us": float(os.environ.get("GSX_PLUGIN_SPIN_US", "200"))}
+                "spin_us": float(os.environ.get("GSX_PLUGIN_SPIN_US", "200")),
+                # early answer (opt-in): answer a first container's Allocate once its record is journaled, commit
+                # ASSIGNED=true behind it (kubelet's serial admission no longer waits an apiserver round trip)
+                "early_answer": self.early_answer, "journal": self.journal_path}
 
     def native_device(self, d: Device) -> dict:
         return {"index": d.index, "bdf": d.bdf, "cu_count": d.cu_count, "total_bytes": d.total_bytes,
@@ -289,6 +295,10 @@ class GpuSharePlugin:
         """A native fast-path Allocate: what the Python handler would have done after it."""
         import json  # noqa: PLC0415
 
+        if ev.get("patch_only"):  # early answer: the commit of an Allocate answered before has landed
+            if ev["pod_json"]:
+                self.state.observe(json.loads(ev["pod_json"]))
+            return
         if ev["pod_json"]:
             self.state.observe(json.loads(ev["pod_json"]))  # the committed pod, before its watch event arrives
         if ev["iso"] and self.isolation is not None:
@@ -421,28 +431,74 @@ class GpuSharePlugin:
         import json  # noqa: PLC0415
 
         tmp = self.checkpoint + ".tmp"
+        if self.early_answer and self._native is not None:
+            # the records and the journal's truncation in one step: every journaled Allocate is in this snapshot
+            records = self._native.journal_checkpoint()
+        else:
+            records = [r.to_dict() for r in self.state.records.values()]
         try:
             with open(tmp, "w") as f:
-                json.dump({"node": self.node, "records": [r.to_dict() for r in self.state.records.values()]}, f)
+                json.dump({"node": self.node, "records": records}, f)
             os.replace(tmp, self.checkpoint)
         except OSError as e:
             log.warning("checkpoint %s: %s", self.checkpoint, e)
 
     def load_records(self) -> int:
-        """Records of pods that are still on this node (after the informer's first sync)."""
+        """Records of pods that are still on this node (after the informer's first sync): the checkpoint, then the
+        early-answer journal of Allocates made after it."""
         import json  # noqa: PLC0415
 
+        recs: list[tuple[dict, bool]] = []
         try:
             with open(self.checkpoint) as f:
-                data = json.load(f)
+                recs += [(d, False) for d in json.load(f).get("records") or []]
         except (OSError, ValueError):
-            return 0
-        n = 0
-        for d in data.get("records") or []:
+            pass
+        try:
+            with open(self.journal_path) as f:
+                for line in f:
+                    try:
+                        recs.append((json.loads(line), True))
+                    except ValueError:
+                        pass  # a torn last line
+        except OSError:
+            pass
+        n, seen = 0, set()
+        self._journaled = []
+        for d, journaled in recs:
             r = AllocRecord.from_dict(d)
-            if r.holder in self.state.pods:
-                self.state.restore_record(r)
-                n += 1
+            if r.aid in seen or r.holder not in self.state.pods:
+                continue
+            seen.add(r.aid)
+            self.state.restore_record(r)
+            if journaled or self.early_answer:  # early answer: a checkpointed record may precede its commit too
+                self._journaled.append(r)
+            n += 1
+        return n
+
+    async def commit_unlanded(self) -> int:
+        """Early answer: an Allocate was answered before its ASSIGNED patch landed, and the plugin went away in between.
+        The pod holds a journaled record but still reads ASSIGNED=false.  Claim it and land the commit before any
+        Allocate is served, so it is never matched again; if the patch fails the claim stays."""
+        n = 0
+        for r in getattr(self, "_journaled", []):
+            p = self.state.pods.get(r.uid)
+            if p is None or p.assigned == "true" or not p.pending:
+                continue
+            self.state.inflight.add(p.uid)
+            ann = {self.profile.annotation_assigned: "true"}
+            if r.cu_mask:
+                ann[POD_CU_MASK_ANNOTATION] = r.cu_mask
+            try:
+                pod = await self.client.patch("pods", p.name, {"metadata": {"annotations": ann}}, p.namespace)
+            except (ApiError, OSError) as e:
+                log.warning("committing the answered Allocate of %s: %s (the pod stays claimed)", p.key, e)
+                continue
+            self.state.inflight.discard(p.uid)
+            self.state.observe(pod)
+            n += 1
+        self._journaled = []
+        self.stats["commits_after_restart"] = self.stats.get("commits_after_restart", 0) + n
         return n
 
     async def allocate_container(self, units: int, ids=()) -> tuple[PodRec, ContainerAllocation]:
@@ -932,6 +988,8 @@ class GpuSharePlugin:
         n = self.load_records()
         if n:
             log.info("restored %d allocation records from %s", n, self.checkpoint)
+        if await self.commit_unlanded():
+            log.warning("landed the ASSIGNED commits of Allocates answered before a restart")
         if self.isolation is not None and self.pods.synced.is_set():
             self.isolation.gc({r.iso for r in self.state.records.values() if r.iso} | set(self.state.pods))
         if self.reconciler is not None:

@@ -749,6 +749,8 @@ class PyDpServer {
     if (cfg.contains("iso_dir") && !cfg["iso_dir"].is_none()) c.iso_dir = cfg["iso_dir"].cast<std::string>();
     if (cfg.contains("guard")) c.guard = cfg["guard"].cast<bool>();
     if (cfg.contains("api") && !cfg["api"].is_none()) c.api = api_from(cfg["api"].cast<py::dict>());
+    if (cfg.contains("early_answer")) c.early_answer = cfg["early_answer"].cast<bool>();
+    if (cfg.contains("journal") && !cfg["journal"].is_none()) c.journal = cfg["journal"].cast<std::string>();
     if (cfg.contains("fast")) fast_ = cfg["fast"].cast<bool>();
     if (cfg.contains("spin_us")) spin_us_ = cfg["spin_us"].cast<double>();
     node_ = c.node;
@@ -834,6 +836,7 @@ class PyDpServer {
       d["aid"] = e.aid;
       d["iso"] = e.iso;
       d["committed"] = e.committed;
+      d["patch_only"] = e.patch_only;
       d["pod_json"] = py::bytes(e.pod_json);
       d["t_handler"] = e.t_handler;
       d["t_match"] = e.t_match;
@@ -856,6 +859,30 @@ class PyDpServer {
     finish_patches();
     retry_waiting(true);
     passes_++;
+  }
+
+  // Early answer: the records to checkpoint, and the journal emptied in the same step (under the state lock, so
+  // no Allocate falls between the two).
+  py::list journal_checkpoint() {
+    py::list out;
+    if (state_) {
+      for (const auto& kv : state_->records()) {
+        const AllocRecord& r = kv.second;
+        py::dict d;
+        d["aid"] = r.aid;
+        d["ids"] = r.ids;
+        d["uid"] = r.uid;
+        d["dev"] = r.dev;
+        d["units"] = r.units;
+        d["cu_mask"] = r.cu_mask;
+        d["owner"] = r.owner;
+        d["t"] = r.t;
+        d["iso"] = r.iso;
+        out.append(d);
+      }
+    }
+    core_->journal_reset();
+    return out;
   }
 
   bool respond(uint64_t call, int status, const py::bytes& payload) {
@@ -938,9 +965,10 @@ class PyDpServer {
       DpEvent ev;
       std::unique_ptr<DpPending> pend;
       DpStep step = core_->allocate(call.message, &resp, &ev, &pend, &why);
-      if (step == DpStep::Answered) {
+      if (step == DpStep::Answered || step == DpStep::AnsweredPending) {
         s.respond(call.id, 0, resp);
         events_.push_back(std::move(ev));
+        if (step == DpStep::AnsweredPending) queue_patch(std::move(pend), call.id, call.message);
       } else if (step == DpStep::Pending) {
         pend->call = call.id;
         pend->request = call.message;
@@ -1110,9 +1138,10 @@ class PyDpServer {
         DpEvent ev;
         std::unique_ptr<DpPending> pend;
         DpStep step = core_->allocate(w.message, &resp, &ev, &pend, &why);
-        if (step == DpStep::Answered) {
+        if (step == DpStep::Answered || step == DpStep::AnsweredPending) {
           srv_->respond(w.call, 0, resp);
           events_.push_back(std::move(ev));
+          if (step == DpStep::AnsweredPending) queue_patch(std::move(pend), w.call, w.message);
           continue;
         }
         if (step == DpStep::Pending) {
@@ -1146,10 +1175,13 @@ class PyDpServer {
       std::unique_ptr<DpPending> p;
       {
         std::unique_lock<std::mutex> l(wmu_);
-        wcv_.wait(l, [&] { return stopping_ || !todo_.empty(); });
-        if (todo_.empty()) return;
-        p = std::move(todo_.front());
-        todo_.pop_front();
+        wcv_.wait(l, [&] { return stopping_ || !todo_.empty() || !todo_bg_.empty(); });
+        // stopping: early-answered commits still queued are left to the journal (a restarted plugin lands them)
+        if (stopping_ && todo_.empty()) return;
+        std::deque<std::unique_ptr<DpPending>>& q = !todo_bg_.empty() && !stopping_ ? todo_bg_ : todo_;
+        if (q.empty()) continue;
+        p = std::move(q.front());
+        q.pop_front();
       }
       core_->run_patch(*p);
       {
@@ -1171,6 +1203,21 @@ class PyDpServer {
     worker_.join();
   }
 
+  void queue_patch(std::unique_ptr<DpPending> pend, uint64_t call, const std::string& message) {
+    if (call) {
+      pend->call = call;
+      pend->request = message;
+    }
+    std::lock_guard<std::mutex> l(wmu_);
+    if (pend->answered) {
+      todo_bg_.push_back(std::move(pend));
+      wcv_.notify_one();
+      return;
+    }
+    todo_.push_back(std::move(pend));
+    if (!serving_.joinable()) wcv_.notify_one();  // the serving thread runs its patches itself
+  }
+
   void finish_patches() {
     std::deque<std::unique_ptr<DpPending>> done;
     {
@@ -1180,6 +1227,15 @@ class PyDpServer {
     for (auto& p : done) {
       std::string resp, why;
       DpEvent ev;
+      if (p->answered) {  // early answer: kubelet has its response; only the commit's outcome remains
+        core_->finish(*p, &resp, &ev, &why);
+        if (p->retry) {
+          queue_patch(std::move(p), 0, std::string());
+        } else if (ev.patch_only) {
+          events_.push_back(std::move(ev));
+        }
+        continue;
+      }
       if (core_->finish(*p, &resp, &ev, &why)) {
         if (srv_) srv_->respond(p->call, 0, resp);
         events_.push_back(std::move(ev));
@@ -1203,6 +1259,8 @@ class PyDpServer {
   std::mutex wmu_;
   std::condition_variable wcv_;
   std::deque<std::unique_ptr<DpPending>> todo_, done_;
+  // early-answered commits: always on the worker, so a slow apiserver never holds up the serving thread
+  std::deque<std::unique_ptr<DpPending>> todo_bg_;
   bool stopping_ = false;
   int efd_ = -1;
   std::unique_ptr<DpCore> core_;
@@ -1576,6 +1634,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("fd", &PyDpServer::fd)
       .def("poll", &PyDpServer::poll, py::call_guard<AllocLock>())
       .def("start_serving", &PyDpServer::start_serving, py::call_guard<AllocLock>())
+      .def("journal_checkpoint", &PyDpServer::journal_checkpoint, py::call_guard<AllocLock>())
       .def("respond", &PyDpServer::respond, py::call_guard<AllocLock>())
       .def("set_devices", &PyDpServer::set_devices, py::call_guard<AllocLock>())
       .def("set_device_list", &PyDpServer::set_device_list, py::call_guard<AllocLock>())

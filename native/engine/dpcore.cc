@@ -167,6 +167,47 @@ bool isolation_prepare(const std::string& host_dir, const std::string& uid, cons
 
 DpCore::DpCore(DpConfig cfg, AllocState* state) : cfg_(std::move(cfg)), state_(state) {
   if (!cfg_.api.server.empty()) api_ = std::make_unique<ApiClient>(cfg_.api);
+  if (cfg_.early_answer && !cfg_.journal.empty()) {
+    jfd_ = ::open(cfg_.journal.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+    if (jfd_ < 0) {
+      std::fprintf(stderr, "[gsx-dpcore] journal %s: %s; answering after the ASSIGNED patch instead\n",
+                   cfg_.journal.c_str(), std::strerror(errno));
+      cfg_.early_answer = false;  // no durable record before the answer: keep the synchronous commit
+    }
+  }
+}
+
+DpCore::~DpCore() {
+  if (jfd_ >= 0) ::close(jfd_);
+}
+
+void DpCore::journal_append(const AllocRecord& r) {
+  if (jfd_ < 0) return;
+  // one line per Allocate, the record's fields as the plugin's checkpoint has them (AllocRecord.to_dict)
+  std::string line = "{\"aid\":";
+  json::append_quoted(&line, r.aid);
+  line.append(",\"uid\":");
+  json::append_quoted(&line, r.uid);
+  line.append(",\"ids\":[");
+  for (size_t i = 0; i < r.ids.size(); ++i) {
+    if (i) line.push_back(',');
+    json::append_quoted(&line, r.ids[i]);
+  }
+  line.append("],\"dev\":").append(std::to_string(r.dev)).append(",\"units\":").append(std::to_string(r.units));
+  line.append(",\"cu_mask\":");
+  json::append_quoted(&line, r.cu_mask);
+  line.append(",\"owner\":\"\",\"t\":").append(std::to_string(r.t)).append(",\"iso\":");
+  json::append_quoted(&line, r.iso);
+  line.append("}\n");
+  // O_APPEND: one write per line, so a crash leaves whole lines (the page cache outlives this process)
+  ssize_t n = ::write(jfd_, line.data(), line.size());
+  (void)n;
+}
+
+void DpCore::journal_reset() {
+  if (jfd_ >= 0 && ::ftruncate(jfd_, 0) != 0) {
+    std::fprintf(stderr, "[gsx-dpcore] truncating the journal: %s\n", std::strerror(errno));
+  }
 }
 
 void DpCore::set_devices(std::vector<DpDevice> devs, std::map<std::string, int> id_owner) {
@@ -320,6 +361,25 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   patch.append("}}}");
   p->body = std::move(patch);
   p->path = "/api/v1/namespaces/" + pod.ns + "/pods/" + pod.name;
+  if (cfg_.early_answer) {
+    // the same patch without the resourceVersion precondition, for a retry after a 409: kubelet already has this
+    // allocation, so the commit must land on whatever version the pod has now
+    const std::string pre = "\"resourceVersion\":";
+    std::string any = p->body;
+    size_t at = any.find(pre);
+    if (at != std::string::npos) {
+      size_t end = any.find(',', at);
+      if (end != std::string::npos) any.erase(at, end - at + 1);
+    }
+    p->body_any = std::move(any);
+    p->answered = true;
+    p->ok = true;
+    state_->first_container_committed(pod.uid, units, p->whole);  // claimed (in flight) until the patch lands
+    record_and_answer(*p, resp, ev);
+    ev->committed = true;
+    *pend = std::move(p);
+    return DpStep::AnsweredPending;
+  }
   *pend = std::move(p);
   return DpStep::Pending;
 }
@@ -332,6 +392,36 @@ void DpCore::run_patch(DpPending& p) {
 
 bool DpCore::finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* why) {
   const bool later = p.path.empty();
+  if (p.answered) {
+    p.retry = false;
+    json::Doc d;
+    AllocPod committed;
+    std::string perr;
+    if (p.ok && p.status < 300 && d.parse(p.resp, &perr) && parse_alloc_pod(d, 0, cfg_.profile, &committed)) {
+      state_->observe(committed);
+      state_->set_inflight(p.pod.uid, false);
+      ev->uid = p.pod.uid;
+      ev->key = p.pod.key;
+      ev->patch_only = true;
+      ev->pod_json = std::move(p.resp);
+      return true;
+    }
+    if (p.ok && p.status == 404) {  // the pod went away: nothing to commit (the pod feed releases it)
+      state_->set_inflight(p.pod.uid, false);
+      return true;
+    }
+    stats_.patch_failures++;
+    if (++p.attempts < 8) {
+      if (p.ok && p.status == 409) p.body = p.body_any;
+      p.retry = true;
+      return true;
+    }
+    // it never landed: the pod stays claimed by its record; the reconciliation pass reports it
+    *why = p.ok ? "ASSIGNED patch answered " + std::to_string(p.status) : "ASSIGNED patch: " + p.err;
+    std::fprintf(stderr, "[gsx-dpcore] %s: %s after %d attempts (the Allocate was answered)\n", p.pod.key.c_str(),
+                 why->c_str(), p.attempts);
+    return true;
+  }
   if (!later) {
     json::Doc d;
     AllocPod committed;
@@ -352,6 +442,11 @@ bool DpCore::finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* w
     ev->pod_json = std::move(p.resp);
     ev->committed = true;
   }
+  record_and_answer(p, resp, ev);
+  return true;
+}
+
+void DpCore::record_and_answer(DpPending& p, std::string* resp, DpEvent* ev) {
   char aid[64];
   std::snprintf(aid, sizeof aid, "%llx-%x-n%llu", static_cast<unsigned long long>(wall_ns() / 1000000),
                 static_cast<unsigned>(::getpid()), static_cast<unsigned long long>(++aid_));
@@ -359,6 +454,7 @@ bool DpCore::finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* w
   AllocRecord& rec = state_->record(p.pod.uid, p.ids, p.units,
                                     cm != p.cr.annotations.end() ? cm->second : p.pod.cu_mask, aid, wall_s());
   rec.iso = p.iso;
+  if (p.answered) journal_append(rec);  // durable before kubelet has the answer
   *resp = dp::encode_allocate_response({p.cr});
   stats_.fast_allocate++;
   ev->uid = p.pod.uid;
@@ -370,7 +466,6 @@ bool DpCore::finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* w
   ev->t_match = p.tm - p.t0;
   ev->t_isolate = p.ti1 - p.ti0;
   ev->t_patch = p.tp1 - p.tp0;
-  return true;
 }
 
 }  // namespace gsx

@@ -44,6 +44,11 @@ struct DpConfig {
   std::string iso_dir;  // enforced isolation host directory ("" = advisory)
   bool guard = false;   // reconciliation on: refuse a first container on a GPU its records say is full
   ApiConfig api;
+  // early answer: a first container's Allocate is answered once its record is in `journal` (appended, one JSON
+  // line per Allocate), and the ASSIGNED patch follows; the pod stays claimed (in flight) until the patch lands.
+  // kubelet admits a node's pods one at a time, so the apiserver round trip leaves its admission path.
+  bool early_answer = false;
+  std::string journal;
 };
 
 // ---- the single implementations the Python plugin calls too
@@ -58,6 +63,7 @@ bool isolation_prepare(const std::string& host_dir, const std::string& uid, cons
 struct DpEvent {  // what the Python side learns after a fast-path Allocate
   std::string uid, key, aid, iso, pod_json;
   bool committed = false;  // a first container (ASSIGNED patch) rather than a later one
+  bool patch_only = false;  // early answer: the ASSIGNED patch of an Allocate answered before landed (pod_json)
   double t_handler = 0, t_match = 0, t_patch = 0, t_isolate = 0;
 };
 
@@ -74,27 +80,37 @@ struct DpPending {
   dp::ContainerResponse cr;
   std::string iso, path, body;
   double t0 = 0, tm = 0, ti0 = 0, ti1 = 0, tp0 = 0, tp1 = 0;
+  bool answered = false;  // early answer: kubelet has its response; only the patch remains
+  bool retry = false;     // finish() asks for the patch to be run again
+  int attempts = 0;
+  std::string body_any;   // the patch without its resourceVersion precondition (early-answer retries)
   // filled by the worker
   bool ok = false;
   int status = 0;
   std::string resp, err;
 };
 
-enum class DpStep { Answered, Pending, Slow };
+enum class DpStep { Answered, AnsweredPending, Pending, Slow };
 
 class DpCore {
  public:
   DpCore(DpConfig cfg, AllocState* state);
+  ~DpCore();
+  DpCore(const DpCore&) = delete;
+  DpCore& operator=(const DpCore&) = delete;
   void set_devices(std::vector<DpDevice> devs, std::map<std::string, int> id_owner);
   void set_state(AllocState* state) { state_ = state; }  // the device layout changed: a rebuilt state
   const std::map<int, DpDevice>& devices() const { return devs_; }
 
   // true: answered (*resp = the response message); false: the slow path answers (*why says why)
   bool preferred(const std::string& req, std::string* resp, std::string* why);
-  // Answered: *resp / *ev set.  Pending: *pend holds the PATCH to run (then finish()).  Slow: Python answers.
+  // Answered: *resp / *ev set.  Pending: *pend holds the PATCH to run (then finish()).  AnsweredPending (early
+  // answer): *resp / *ev set and *pend holds the PATCH still to run.  Slow: Python answers.
   DpStep allocate(const std::string& req, std::string* resp, DpEvent* ev, std::unique_ptr<DpPending>* pend,
                   std::string* why);
-  // after the PATCH: true = answered (*resp / *ev); false = undone, the slow path answers
+  // after the PATCH: true = answered (*resp / *ev); false = undone, the slow path answers.  For an early-answered
+  // Allocate nothing is answered: *ev->patch_only carries the committed pod, or p.retry asks for another run
+  // (409: without the precondition; transport / 5xx: up to 8 times); 404: the pod is gone.
   bool finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* why);
   // the worker's half: the blocking apiserver call
   void run_patch(DpPending& p);
@@ -103,6 +119,8 @@ class DpCore {
     uint64_t fast_allocate = 0, fast_preferred = 0, slow_allocate = 0, slow_preferred = 0, patch_failures = 0;
   };
   const Stats& stats() const { return stats_; }
+  // early answer: empty the journal (the records it holds are in the caller's checkpoint now)
+  void journal_reset();
   int64_t physical_used(int dev) const;
 
  private:
@@ -113,7 +131,10 @@ class DpCore {
   std::unordered_map<std::string, int> id_owner_;
   std::unordered_map<std::string_view, int> id_owner_view_;  // keys view id_owner_'s strings
   uint64_t aid_ = 0;
+  int jfd_ = -1;  // the early-answer journal
   Stats stats_;
+  void record_and_answer(DpPending& p, std::string* resp, DpEvent* ev);
+  void journal_append(const AllocRecord& r);
 };
 
 }  // namespace gsx

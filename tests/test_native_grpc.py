@@ -2,6 +2,7 @@
 grpcio in both directions, the fast Allocate path against the Python handler it stands in for, and the hand-off
 of everything else to Python."""
 import asyncio
+import json
 import os
 import tempfile
 
@@ -147,4 +148,83 @@ def test_native_client_against_a_grpcio_server():
             assert status == 12, (status, body)  # UNIMPLEMENTED from grpcio
         finally:
             await kubelet.stop()
+    asyncio.run(go())
+
+
+def test_early_answer_claims_the_pod_until_its_commit_lands():
+    """Opt-in early answer (GSX_PLUGIN_EARLY_ANSWER=1): an Allocate is answered once its record is journaled and
+    the ASSIGNED patch follows.  With a slow apiserver the answer comes first, the pod stays claimed (a second
+    Allocate of that size gets the other pod), both commits land, and the checkpoint takes over the journal."""
+    async def go():
+        tmp = tempfile.mkdtemp()
+        os.environ["GSX_PLUGIN_EARLY_ANSWER"] = "1"
+        try:
+            api_srv, client, plugin = await _plugin(tmp, fast=True)
+        finally:
+            os.environ.pop("GSX_PLUGIN_EARLY_ANSWER", None)
+        pc = PluginClient(plugin.socket_path)
+        try:
+            assert plugin.early_answer
+            await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
+            await client.create("pods", bound_pod("b", 4, dev=1, assume=2, dev_total=16))
+            await asyncio.sleep(0.3)
+            api_srv.server.faults.latency_ms = 400.0  # every apiserver call now takes 0.4 s
+            ids = fake_ids(plugin.devices[0], 16) + fake_ids(plugin.devices[1], 16)
+            t0 = asyncio.get_running_loop().time()
+            got = []
+            for chunk in (ids[0:4], ids[16:20]):
+                r = (await pc.allocate([chunk])).container_responses[0]
+                got.append(dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1])
+            assert asyncio.get_running_loop().time() - t0 < 0.35, "answers waited for the apiserver"
+            assert got == ["a", "b"], got  # a stayed claimed while its commit was in flight
+            with open(plugin.journal_path) as f:
+                assert len(f.read().splitlines()) == 2
+            api_srv.server.faults.latency_ms = 0.0
+            for _ in range(200):  # both commits land
+                anns = [(await client.get("pods", n, "default"))["metadata"]["annotations"] for n in ("a", "b")]
+                if all(a[P.annotation_assigned] == "true" for a in anns):
+                    break
+                await asyncio.sleep(0.02)
+            assert all(a[P.annotation_assigned] == "true" for a in anns), anns
+            for _ in range(100):  # the debounced checkpoint took the records and emptied the journal
+                if os.path.exists(plugin.checkpoint) and os.path.getsize(plugin.journal_path) == 0:
+                    break
+                await asyncio.sleep(0.02)
+            assert os.path.getsize(plugin.journal_path) == 0
+            with open(plugin.checkpoint) as f:
+                assert len(json.load(f)["records"]) == 2
+        finally:
+            await _close(api_srv, client, plugin, pc)
+    asyncio.run(go())
+
+
+def test_early_answer_commit_lands_after_a_restart():
+    """The plugin went away between an early answer and its commit: the journal still holds the record, the pod
+    still reads ASSIGNED=false.  A restarted plugin lands the commit before it serves, and never offers the pod
+    to another Allocate."""
+    async def go():
+        tmp = tempfile.mkdtemp()
+        os.environ["GSX_PLUGIN_EARLY_ANSWER"] = "1"
+        try:
+            api_srv, client, plugin = await _plugin(tmp, fast=True)
+            a = await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
+            await client.create("pods", bound_pod("b", 4, dev=0, assume=2, dev_total=16))
+            await plugin.stop()
+            ids = fake_ids(plugin.devices[0], 16)
+            with open(plugin.journal_path, "w") as f:  # the answered Allocate of "a", its commit never sent
+                f.write(json.dumps({"aid": "x-1", "uid": a["metadata"]["uid"], "ids": sorted(ids[0:4]), "dev": 0,
+                                    "units": 4, "cu_mask": "", "owner": "", "t": 0.0, "iso": ""}) + "\n")
+            again = GpuSharePlugin(client, "n1", fake_devices("2x16GiB"), P, socket_dir=os.path.join(tmp, "dp"))
+            await again.start(register=False)
+        finally:
+            os.environ.pop("GSX_PLUGIN_EARLY_ANSWER", None)
+        pc = PluginClient(again.socket_path)
+        try:
+            assert again.stats.get("commits_after_restart") == 1
+            assert (await client.get("pods", "a", "default"))["metadata"]["annotations"][P.annotation_assigned] == "true"
+            r = (await pc.allocate([ids[4:8]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "b"
+            assert any(rec.uid == a["metadata"]["uid"] for rec in again.state.records.values())
+        finally:
+            await _close(api_srv, client, again, pc)
     asyncio.run(go())
