@@ -115,8 +115,9 @@ class GpuSharePlugin:
         self._set_devices(devices)
         self.checkpoint = checkpoint if checkpoint is not None else os.path.join(socket_dir, "gsx-allocations.json")
         self.journal_path = (self.checkpoint or os.path.join(socket_dir, "gsx-allocations.json")) + ".journal"
-        # opt-in: needs the journal next to the checkpoint (the record must be durable before kubelet's answer)
-        self.early_answer = bool(self.checkpoint) and os.environ.get("GSX_PLUGIN_EARLY_ANSWER", "0") == "1"
+        # early answer (default; GSX_PLUGIN_EARLY_ANSWER=0 turns it off): needs the journal next to the checkpoint
+        # (the record must be durable before kubelet has the answer)
+        self.early_answer = bool(self.checkpoint) and os.environ.get("GSX_PLUGIN_EARLY_ANSWER", "1") == "1"
         self.checkpoint_interval = 0.2
         self._dirty = False
         self._persist_task: asyncio.Task | None = None
@@ -425,15 +426,22 @@ class GpuSharePlugin:
         self._write_checkpoint()
 
     def _write_checkpoint(self):
+        """The records snapshot, then the journal generations it covers go.  With the native endpoint journaling
+        (early answer) the snapshot and the journal's rotation to ``<journal>.old`` are one step under the state
+        lock; ``.old`` is deleted only once the checkpoint is in place, so a failed write or a crash in between
+        loses no journaled record (the next start reads checkpoint, ``.old`` and journal)."""
         if not self.checkpoint or not self._dirty:
             return
         self._dirty = False
         import json  # noqa: PLC0415
 
         tmp = self.checkpoint + ".tmp"
-        if self.early_answer and self._native is not None:
-            # the records and the journal's truncation in one step: every journaled Allocate is in this snapshot
-            records = self._native.journal_checkpoint()
+        journaling = self._native is not None and self._native.stats().get("journaling", False)
+        rotated = False
+        if journaling:
+            records, rotated, err = self._native.journal_checkpoint()
+            if not rotated:
+                log.warning("rotating the Allocate journal %s: %s (it keeps every line)", self.journal_path, err)
         else:
             records = [r.to_dict() for r in self.state.records.values()]
         try:
@@ -441,65 +449,120 @@ class GpuSharePlugin:
                 json.dump({"node": self.node, "records": records}, f)
             os.replace(tmp, self.checkpoint)
         except OSError as e:
+            self._dirty = True  # the next pass tries again; the journal generations stay
             log.warning("checkpoint %s: %s", self.checkpoint, e)
+            return
+        # the checkpoint holds every record the journal generations held
+        old = [self.journal_path + ".old"] if (rotated or not journaling) else []
+        if not journaling:
+            old.append(self.journal_path)  # nobody appends to it: lines from an earlier run, now checkpointed
+        for path in old:
+            try:
+                os.unlink(path)
+            except FileNotFoundError:
+                pass
+            except OSError as e:
+                log.warning("removing %s: %s", path, e)
 
     def load_records(self) -> int:
         """Records of pods that are still on this node (after the informer's first sync): the checkpoint, then the
         early-answer journal of Allocates made after it."""
         import json  # noqa: PLC0415
 
-        recs: list[tuple[dict, bool]] = []
+        recs: list[dict] = []
         try:
             with open(self.checkpoint) as f:
-                recs += [(d, False) for d in json.load(f).get("records") or []]
+                recs += list(json.load(f).get("records") or [])
         except (OSError, ValueError):
             pass
-        try:
-            with open(self.journal_path) as f:
-                for line in f:
-                    try:
-                        recs.append((json.loads(line), True))
-                    except ValueError:
-                        pass  # a torn last line
-        except OSError:
-            pass
+        journal_lines = 0
+        # .old: a generation a checkpoint was about to cover when the plugin went away (plugin._write_checkpoint)
+        for path in (self.journal_path + ".old", self.journal_path):
+            try:
+                with open(path) as f:
+                    for line in f:
+                        try:
+                            recs.append(json.loads(line))
+                            journal_lines += 1
+                        except ValueError:
+                            pass  # a torn last line
+            except OSError:
+                pass
         n, seen = 0, set()
         self._journaled = []
-        for d, journaled in recs:
+        for d in recs:
             r = AllocRecord.from_dict(d)
             if r.aid in seen or r.holder not in self.state.pods:
                 continue
             seen.add(r.aid)
             self.state.restore_record(r)
-            if journaled or self.early_answer:  # early answer: a checkpointed record may precede its commit too
-                self._journaled.append(r)
+            # whatever the early-answer setting was or is: a record is written once kubelet has (or is about to
+            # have) the answer, so a pod it names that still reads ASSIGNED!=true has a commit that never landed
+            self._journaled.append(r)
             n += 1
+        if journal_lines:
+            self.persist_records()  # the first checkpoint supersedes the journal lines read here
         return n
 
     async def commit_unlanded(self) -> int:
         """Early answer: an Allocate was answered before its ASSIGNED patch landed, and the plugin went away in between.
         The pod holds a journaled record but still reads ASSIGNED=false.  Claim it and land the commit before any
         Allocate is served, so it is never matched again; if the patch fails the claim stays."""
-        n = 0
+        n, late = 0, []
         for r in getattr(self, "_journaled", []):
             p = self.state.pods.get(r.uid)
             if p is None or p.assigned == "true" or not p.pending:
                 continue
             self.state.inflight.add(p.uid)
-            ann = {self.profile.annotation_assigned: "true"}
-            if r.cu_mask:
-                ann[POD_CU_MASK_ANNOTATION] = r.cu_mask
-            try:
-                pod = await self.client.patch("pods", p.name, {"metadata": {"annotations": ann}}, p.namespace)
-            except (ApiError, OSError) as e:
-                log.warning("committing the answered Allocate of %s: %s (the pod stays claimed)", p.key, e)
-                continue
-            self.state.inflight.discard(p.uid)
-            self.state.observe(pod)
-            n += 1
+            if await self._land_commit(p, r):
+                n += 1
+            else:
+                late.append((p, r))
         self._journaled = []
+        if late:  # the pods stay claimed; their commits are retried with backoff while the pods exist
+            t = asyncio.get_running_loop().create_task(self._land_late(late))
+            self._tasks.append(t)
         self.stats["commits_after_restart"] = self.stats.get("commits_after_restart", 0) + n
         return n
+
+    async def _land_commit(self, p: PodRec, r: AllocRecord) -> bool:
+        """One attempt at an answered Allocate's ASSIGNED commit, guarded by the pod's UID (never lands on a pod
+        re-created under the name).  True when there is nothing left to do (landed, or the pod went away)."""
+        ann = {self.profile.annotation_assigned: "true"}
+        if r.cu_mask:
+            ann[POD_CU_MASK_ANNOTATION] = r.cu_mask
+        try:
+            pod = await self.client.patch("pods", p.name, {"metadata": {"uid": p.uid, "annotations": ann}},
+                                          p.namespace)
+        except ApiError as e:
+            if e.status == 404 or (e.status == 409 and "UID in precondition" in str(e)):
+                self.state.inflight.discard(p.uid)
+                return True
+            log.warning("committing the answered Allocate of %s: %s (the pod stays claimed; retrying)", p.key, e)
+            return False
+        except OSError as e:
+            log.warning("committing the answered Allocate of %s: %s (the pod stays claimed; retrying)", p.key, e)
+            return False
+        self.state.inflight.discard(p.uid)
+        self.state.observe(pod)
+        return True
+
+    async def _land_late(self, todo: list):
+        delay = 0.01
+        while todo and not self._stopped:
+            await asyncio.sleep(delay)
+            delay = min(2.0, delay * 2)
+            still = []
+            for p, r in todo:
+                cur = self.state.pods.get(p.uid)
+                if cur is None:
+                    self.state.inflight.discard(p.uid)
+                    continue
+                if await self._land_commit(cur, r):
+                    self.stats["commits_after_restart"] = self.stats.get("commits_after_restart", 0) + 1
+                else:
+                    still.append((cur, r))
+            todo = still
 
     async def allocate_container(self, units: int, ids=()) -> tuple[PodRec, ContainerAllocation]:
         """Match one container request of ``units`` to its pod and build its allocation.

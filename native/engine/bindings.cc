@@ -783,6 +783,10 @@ class PyDpServer {
     if (serving_.joinable()) return pyfd_;
     pyfd_ = ::eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     stop_serving_ = false;
+    {
+      std::lock_guard<std::mutex> l(wmu_);
+      serving_on_ = true;  // from now on the serving thread runs the synchronous patches (todo_) itself
+    }
     serving_ = std::thread([this] { serve(); });
     return pyfd_;
   }
@@ -861,9 +865,10 @@ class PyDpServer {
     passes_++;
   }
 
-  // Early answer: the records to checkpoint, and the journal emptied in the same step (under the state lock, so
-  // no Allocate falls between the two).
-  py::list journal_checkpoint() {
+  // Early answer: the records to checkpoint, and the journal rotated to <journal>.old in the same step (under the
+  // state lock, so no Allocate falls between the two).  The caller writes the checkpoint and deletes .old only once
+  // it is in place: a failed or interrupted checkpoint loses no journaled record.  Returns (records, rotated, err).
+  py::tuple journal_checkpoint() {
     py::list out;
     if (state_) {
       for (const auto& kv : state_->records()) {
@@ -881,8 +886,9 @@ class PyDpServer {
         out.append(d);
       }
     }
-    core_->journal_reset();
-    return out;
+    std::string err;
+    const bool rotated = core_->journal_rotate(&err);
+    return py::make_tuple(out, rotated, err);
   }
 
   bool respond(uint64_t call, int status, const py::bytes& payload) {
@@ -909,7 +915,12 @@ class PyDpServer {
     state_ = &state;
   }
 
-  py::dict stats() const {
+  size_t bg_backlog() {
+    std::lock_guard<std::mutex> l(wmu_);
+    return todo_bg_.size();
+  }
+
+  py::dict stats() {
     py::dict d;
     const auto& s = core_->stats();
     d["fast_allocate"] = s.fast_allocate;
@@ -925,6 +936,8 @@ class PyDpServer {
     d["feed_events"] = feed_events_;
     d["feed"] = static_cast<bool>(feed_r_);
     d["serving_thread"] = serving_.joinable();
+    d["journaling"] = core_->journaling();
+    d["early_answer_backlog"] = static_cast<uint64_t>(bg_backlog());
     d["passes"] = passes_;
     return d;
   }
@@ -1049,6 +1062,11 @@ class PyDpServer {
     (void)!::write(efd_, &one, sizeof one);
     py::gil_scoped_release nogil;
     serving_.join();
+    {
+      std::lock_guard<std::mutex> l(wmu_);
+      serving_on_ = false;  // synchronous patches left in todo_ go to the worker again
+    }
+    wcv_.notify_all();
   }
 
   static constexpr const char* kNoCandidate = "no candidate";
@@ -1170,18 +1188,37 @@ class PyDpServer {
   }
 
   // the ASSIGNED patches run here, never on the owner's event loop
+  // Takes the synchronous patches (todo_) only while no serving thread runs them itself, and the early-answered
+  // commits (todo_bg_) once their backoff (not_before) has passed.
   void work() {
     for (;;) {
       std::unique_ptr<DpPending> p;
       {
         std::unique_lock<std::mutex> l(wmu_);
-        wcv_.wait(l, [&] { return stopping_ || !todo_.empty() || !todo_bg_.empty(); });
-        // stopping: early-answered commits still queued are left to the journal (a restarted plugin lands them)
-        if (stopping_ && todo_.empty()) return;
-        std::deque<std::unique_ptr<DpPending>>& q = !todo_bg_.empty() && !stopping_ ? todo_bg_ : todo_;
-        if (q.empty()) continue;
-        p = std::move(q.front());
-        q.pop_front();
+        for (;;) {
+          if ((!serving_on_ || stopping_) && !todo_.empty()) {
+            p = std::move(todo_.front());
+            todo_.pop_front();
+            break;
+          }
+          // stopping: early-answered commits still queued are left to the journal (a restarted plugin lands them)
+          if (stopping_) return;
+          if (todo_bg_.empty()) {
+            wcv_.wait(l);
+            continue;
+          }
+          const double now = mono();
+          auto it = std::find_if(todo_bg_.begin(), todo_bg_.end(),
+                                 [now](const std::unique_ptr<DpPending>& q) { return q->not_before <= now; });
+          if (it != todo_bg_.end()) {
+            p = std::move(*it);
+            todo_bg_.erase(it);
+            break;
+          }
+          double first = todo_bg_.front()->not_before;
+          for (const auto& q : todo_bg_) first = std::min(first, q->not_before);
+          wcv_.wait_for(l, std::chrono::duration<double>(first - now));
+        }
       }
       core_->run_patch(*p);
       {
@@ -1262,6 +1299,7 @@ class PyDpServer {
   // early-answered commits: always on the worker, so a slow apiserver never holds up the serving thread
   std::deque<std::unique_ptr<DpPending>> todo_bg_;
   bool stopping_ = false;
+  bool serving_on_ = false;  // (wmu_) a serving thread runs todo_ itself
   int efd_ = -1;
   std::unique_ptr<DpCore> core_;
   std::unique_ptr<h2::Server> srv_;

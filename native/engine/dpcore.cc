@@ -204,10 +204,47 @@ void DpCore::journal_append(const AllocRecord& r) {
   (void)n;
 }
 
-void DpCore::journal_reset() {
-  if (jfd_ >= 0 && ::ftruncate(jfd_, 0) != 0) {
-    std::fprintf(stderr, "[gsx-dpcore] truncating the journal: %s\n", std::strerror(errno));
+bool DpCore::journal_rotate(std::string* err) {
+  if (jfd_ < 0) return true;
+  const std::string& path = cfg_.journal;
+  const std::string old = path + ".old";
+  if (::access(old.c_str(), F_OK) != 0) {
+    // the common case: the journal becomes .old, a fresh journal takes the next Allocates
+    if (::rename(path.c_str(), old.c_str()) != 0) {
+      *err = "rename " + path + ": " + std::strerror(errno);
+      return false;
+    }
+    int nfd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+    if (nfd < 0) {
+      *err = "open " + path + ": " + std::strerror(errno);
+      (void)::rename(old.c_str(), path.c_str());  // keep appending where we were
+      return false;
+    }
+    ::close(jfd_);
+    jfd_ = nfd;
+    return true;
   }
+  // a previous checkpoint did not land: .old still holds records it was to cover; append this generation to it
+  int in = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  int out = ::open(old.c_str(), O_WRONLY | O_APPEND | O_CLOEXEC);
+  bool ok = in >= 0 && out >= 0;
+  char buf[65536];
+  while (ok) {
+    ssize_t n = ::read(in, buf, sizeof buf);
+    if (n < 0 && errno == EINTR) continue;
+    if (n <= 0) {
+      ok = n == 0;
+      break;
+    }
+    ok = ::write(out, buf, static_cast<size_t>(n)) == n;
+  }
+  if (in >= 0) ::close(in);
+  if (out >= 0) ::close(out);
+  if (!ok || ::ftruncate(jfd_, 0) != 0) {
+    *err = "appending " + path + " to " + old + ": " + std::strerror(errno);
+    return false;
+  }
+  return true;
 }
 
 void DpCore::set_devices(std::vector<DpDevice> devs, std::map<std::string, int> id_owner) {
@@ -344,8 +381,12 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
     finish(*p, resp, ev, why);
     return DpStep::Answered;
   }
-  std::string patch = "{\"metadata\":{\"resourceVersion\":";
-  json::append_quoted(&patch, pod.rv);
+  // The precondition: synchronous answer -- the resourceVersion the match was made on (the commit IS the claim:
+  // a stale view loses with 409 and the slow path re-decides).  Early answer -- the pod's UID: kubelet already
+  // has this allocation, so the commit must land on whatever version the pod has by then (kubelet's status
+  // updates move it), but never on a pod re-created under the same name.
+  std::string patch = cfg_.early_answer ? "{\"metadata\":{\"uid\":" : "{\"metadata\":{\"resourceVersion\":";
+  json::append_quoted(&patch, cfg_.early_answer ? pod.uid : pod.rv);
   patch.append(",\"annotations\":{");
   json::append_quoted(&patch, cfg_.profile.a_assigned);
   patch.append(":\"true\",");
@@ -362,16 +403,6 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   p->body = std::move(patch);
   p->path = "/api/v1/namespaces/" + pod.ns + "/pods/" + pod.name;
   if (cfg_.early_answer) {
-    // the same patch without the resourceVersion precondition, for a retry after a 409: kubelet already has this
-    // allocation, so the commit must land on whatever version the pod has now
-    const std::string pre = "\"resourceVersion\":";
-    std::string any = p->body;
-    size_t at = any.find(pre);
-    if (at != std::string::npos) {
-      size_t end = any.find(',', at);
-      if (end != std::string::npos) any.erase(at, end - at + 1);
-    }
-    p->body_any = std::move(any);
     p->answered = true;
     p->ok = true;
     state_->first_container_committed(pod.uid, units, p->whole);  // claimed (in flight) until the patch lands
@@ -406,20 +437,24 @@ bool DpCore::finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* w
       ev->pod_json = std::move(p.resp);
       return true;
     }
-    if (p.ok && p.status == 404) {  // the pod went away: nothing to commit (the pod feed releases it)
+    const bool recreated = p.ok && p.status == 409 && p.resp.find("UID in precondition") != std::string::npos;
+    if ((p.ok && p.status == 404) || recreated || !state_->pod(p.pod.uid)) {
+      // the pod went away (deleted, or re-created under its name): nothing to commit; the pod feed releases it
       state_->set_inflight(p.pod.uid, false);
       return true;
     }
+    // transport error, 5xx, an injected or transient 409: the commit is retried with capped exponential backoff
+    // for as long as the pod exists -- kubelet has its answer, so giving up would leave the pod ASSIGNED=false
+    // (claimed here, but a match candidate for a restarted plugin) with its container running
     stats_.patch_failures++;
-    if (++p.attempts < 8) {
-      if (p.ok && p.status == 409) p.body = p.body_any;
-      p.retry = true;
-      return true;
+    p.attempts++;
+    p.retry = true;
+    p.not_before = mono_s() + std::min(1.0, 0.002 * static_cast<double>(1 << std::min(p.attempts, 10)));
+    if (p.attempts == 1 || p.attempts % 32 == 0) {
+      *why = p.ok ? "ASSIGNED patch answered " + std::to_string(p.status) : "ASSIGNED patch: " + p.err;
+      std::fprintf(stderr, "[gsx-dpcore] %s: %s (attempt %d; the Allocate was answered, retrying)\n",
+                   p.pod.key.c_str(), why->c_str(), p.attempts);
     }
-    // it never landed: the pod stays claimed by its record; the reconciliation pass reports it
-    *why = p.ok ? "ASSIGNED patch answered " + std::to_string(p.status) : "ASSIGNED patch: " + p.err;
-    std::fprintf(stderr, "[gsx-dpcore] %s: %s after %d attempts (the Allocate was answered)\n", p.pod.key.c_str(),
-                 why->c_str(), p.attempts);
     return true;
   }
   if (!later) {

@@ -83,7 +83,7 @@ struct DpPending {
   bool answered = false;  // early answer: kubelet has its response; only the patch remains
   bool retry = false;     // finish() asks for the patch to be run again
   int attempts = 0;
-  std::string body_any;   // the patch without its resourceVersion precondition (early-answer retries)
+  double not_before = 0;  // early-answer retry: not before this CLOCK_MONOTONIC time (backoff)
   // filled by the worker
   bool ok = false;
   int status = 0;
@@ -109,8 +109,9 @@ class DpCore {
   DpStep allocate(const std::string& req, std::string* resp, DpEvent* ev, std::unique_ptr<DpPending>* pend,
                   std::string* why);
   // after the PATCH: true = answered (*resp / *ev); false = undone, the slow path answers.  For an early-answered
-  // Allocate nothing is answered: *ev->patch_only carries the committed pod, or p.retry asks for another run
-  // (409: without the precondition; transport / 5xx: up to 8 times); 404: the pod is gone.
+  // Allocate nothing is answered: *ev->patch_only carries the committed pod, or p.retry asks for another run at
+  // p.not_before (transport / 5xx / transient 409: capped exponential backoff, for as long as the pod exists);
+  // 404, a UID-precondition 409 (re-created) or a pod the state no longer has: nothing left to commit.
   bool finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* why);
   // the worker's half: the blocking apiserver call
   void run_patch(DpPending& p);
@@ -119,8 +120,12 @@ class DpCore {
     uint64_t fast_allocate = 0, fast_preferred = 0, slow_allocate = 0, slow_preferred = 0, patch_failures = 0;
   };
   const Stats& stats() const { return stats_; }
-  // early answer: empty the journal (the records it holds are in the caller's checkpoint now)
-  void journal_reset();
+  // early answer: the journal's lines move to <journal>.old (appended if a previous checkpoint left one) and the
+  // journal starts empty; the caller deletes .old once the checkpoint holding those records is in place.  Called
+  // under the state lock, so no Allocate falls between the records snapshot and the rotation.
+  bool journal_rotate(std::string* err);
+  bool journaling() const { return jfd_ >= 0; }
+  const std::string& journal_path() const { return cfg_.journal; }
   int64_t physical_used(int dev) const;
 
  private:

@@ -1173,6 +1173,13 @@ class Server {
     const jd::Value* pmd = patch.get("metadata");
     std::string want = pmd ? pmd->str_or("resourceVersion") : std::string();
     if (!want.empty() && want != cmd.str_or("resourceVersion")) throw conflict(kind, name);
+    // kube-apiserver's registry store refuses an update whose object UID differs from the stored one: a merge
+    // patch naming metadata.uid is a UID precondition
+    std::string want_uid = pmd ? pmd->str_or("uid") : std::string();
+    if (!want_uid.empty() && want_uid != cmd.str_or("uid")) {
+      throw HttpError{409, status_body(409, "Conflict", "Precondition failed: UID in precondition: " + want_uid +
+                                                            ", UID in object meta: " + cmd.str_or("uid"))};
+    }
     if (kind == "pods" && injected_conflict()) throw conflict(kind, name);
     if (sub == "status") {
       jd::Value p = jd::Value::object();

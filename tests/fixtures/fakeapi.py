@@ -335,6 +335,12 @@ class FakeApiServer:
         want_rv = ((patch or {}).get("metadata") or {}).get("resourceVersion")
         if want_rv and want_rv != cur["metadata"]["resourceVersion"]:
             raise self._conflict(kind, name)
+        want_uid = ((patch or {}).get("metadata") or {}).get("uid")
+        if want_uid and want_uid != cur["metadata"].get("uid"):
+            # kube-apiserver's registry store: a UID in the new object that differs from the stored one
+            raise HTTPError(409, status_body(
+                409, "Conflict", f'Precondition failed: UID in precondition: {want_uid}, '
+                                 f'UID in object meta: {cur["metadata"].get("uid")}'))
         if kind == "pods" and self.faults.conflict_rate and self.faults.rng.random() < self.faults.conflict_rate:
             self.counts["injected_conflict"] += 1
             raise self._conflict(kind, name)

@@ -28,6 +28,19 @@ def bound_pod(name, mem, node="n1", dev=0, assume=1, assigned="false", dev_total
     return make_pod(name, mem, node=node, annotations=ann, **kw)
 
 
+async def assigned_value(client, name, want="true", ns="default", timeout=3.0):
+    """The pod's ASSIGNED annotation once it reads ``want`` (or the last value after ``timeout``): with early answer
+    (the default) an Allocate's commit lands just after kubelet has the answer."""
+    import time as _time
+
+    deadline = _time.monotonic() + timeout
+    while True:
+        v = (await client.get("pods", name, ns))["metadata"]["annotations"].get(P.annotation_assigned)
+        if v == want or _time.monotonic() > deadline:
+            return v
+        await asyncio.sleep(0.01)
+
+
 # ---------------------------------------------------------------- allocator (pure)
 
 def _state(spec="2x16GiB"):
@@ -320,13 +333,11 @@ def test_plugin_register_listandwatch_allocate():
             env = dict(r.container_responses[0].envs)
             assert env["SHARED_GPU_MEM_IDX"] == "1" and env["SHARED_GPU_MEM_CONTAINER"] == "8"
             assert [x.host_path for x in r.container_responses[0].devices][0] == "/dev/kfd"
+            assert await assigned_value(client, "b") == "true"
             a = await client.get("pods", "a", "default")
-            b = await client.get("pods", "b", "default")
-            assert b["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
             assert a["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "false"
             await pc.allocate([ids[:8]])
-            a = await client.get("pods", "a", "default")
-            assert a["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
+            assert await assigned_value(client, "a") == "true"
             node = await client.get("nodes", "n1")
             assert node["metadata"]["annotations"]["gpushare.amd.com/allocate-order"] == "landing"
             # nothing left to match
@@ -414,8 +425,12 @@ def test_plugin_allocate_retries_conflicts_and_apiserver_errors():
                 r = await pc.allocate([ids[4 * i: 4 * i + 4]])
                 assert dict(r.container_responses[0].envs)["SHARED_GPU_MEM_IDX"] == "0"
             api_srv.server.faults.update({"conflict_rate": 0, "error_rate": 0})
-            for i in range(4):
-                p = await client.get("pods", f"p{i}", "default")
+            for i in range(4):  # early answer (default): a commit that hit a fault lands on its backoff retry
+                for _ in range(200):
+                    p = await client.get("pods", f"p{i}", "default")
+                    if p["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true":
+                        break
+                    await asyncio.sleep(0.01)
                 assert p["metadata"]["annotations"]["SHARED_GPU_MEM_ASSIGNED"] == "true"
             # retried: by the Python handler, or a native fast-path patch that failed and was handed to it
             native_failures = plugin.debug_state()["grpc"].get("patch_failures", 0)

@@ -228,3 +228,117 @@ def test_early_answer_commit_lands_after_a_restart():
         finally:
             await _close(api_srv, client, again, pc)
     asyncio.run(go())
+
+
+def test_early_answer_is_the_default_and_commits_with_a_uid_precondition():
+    """Early answer is on by default; its commit is guarded by the pod's UID, not the resourceVersion the match was
+    made on, so kubelet's status updates landing first do not make it conflict."""
+    async def go():
+        tmp = tempfile.mkdtemp()
+        api_srv, client, plugin = await _plugin(tmp, fast=True)
+        pc = PluginClient(plugin.socket_path)
+        try:
+            assert plugin.early_answer and plugin.debug_state()["grpc"]["journaling"]
+            await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
+            await asyncio.sleep(0.2)
+            api_srv.server.faults.latency_ms = 200.0
+            ids = fake_ids(plugin.devices[0], 16)
+            r = (await pc.allocate([ids[0:4]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "a"
+            # kubelet's status update lands before the commit: it moves the resourceVersion
+            api_srv.server.faults.latency_ms = 0.0
+            await client.patch("pods", "a", {"status": {"phase": "Running"}}, "default", sub="status")
+            for _ in range(100):
+                a = await client.get("pods", "a", "default")
+                if a["metadata"]["annotations"][P.annotation_assigned] == "true":
+                    break
+                await asyncio.sleep(0.02)
+            assert a["metadata"]["annotations"][P.annotation_assigned] == "true"
+            assert plugin.debug_state()["grpc"]["patch_failures"] == 0  # no 409 from the moved resourceVersion
+        finally:
+            await _close(api_srv, client, plugin, pc)
+    asyncio.run(go())
+
+
+def test_early_answer_commit_retries_with_backoff_until_the_apiserver_recovers():
+    """an answered Allocate's commit that hits 5xx is retried with capped backoff for as long as the pod
+    exists (not 8 times in a few ms): an apiserver outage of a second still ends with ASSIGNED=true."""
+    async def go():
+        tmp = tempfile.mkdtemp()
+        api_srv, client, plugin = await _plugin(tmp, fast=True)
+        pc = PluginClient(plugin.socket_path)
+        try:
+            await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
+            await asyncio.sleep(0.2)
+            api_srv.server.faults.error_rate = 1.0  # every mutating pod call answers 500
+            ids = fake_ids(plugin.devices[0], 16)
+            await pc.allocate([ids[0:4]])
+            await asyncio.sleep(1.0)
+            st = plugin.debug_state()["grpc"]
+            assert st["patch_failures"] >= 8 and st["early_answer_backlog"] == 1, st
+            assert (await client.get("pods", "a", "default"))["metadata"]["annotations"][P.annotation_assigned] == "false"
+            assert plugin.state.match(4) == (None, False)  # still claimed: never offered to another Allocate
+            api_srv.server.faults.error_rate = 0.0
+            for _ in range(200):
+                a = await client.get("pods", "a", "default")
+                if a["metadata"]["annotations"][P.annotation_assigned] == "true":
+                    break
+                await asyncio.sleep(0.02)
+            assert a["metadata"]["annotations"][P.annotation_assigned] == "true"
+            assert plugin.debug_state()["grpc"]["early_answer_backlog"] == 0
+        finally:
+            api_srv.server.faults.error_rate = 0.0
+            await _close(api_srv, client, plugin, pc)
+    asyncio.run(go())
+
+
+def test_early_answer_checkpoint_failure_keeps_the_journal_generation():
+    """the journal is rotated (not truncated) with the records snapshot; a checkpoint that fails to land
+    leaves the rotated generation in place, and a restarted plugin still finds the record."""
+    async def go():
+        tmp = tempfile.mkdtemp()
+        api_srv, client, plugin = await _plugin(tmp, fast=True)
+        pc = PluginClient(plugin.socket_path)
+        try:
+            a = await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
+            await client.create("pods", bound_pod("b", 4, dev=0, assume=2, dev_total=16))
+            await asyncio.sleep(0.2)
+            os.makedirs(plugin.checkpoint + ".tmp")  # the checkpoint write fails (a directory where its file goes)
+            api_srv.server.faults.error_rate = 1.0  # and the commit never lands before the plugin goes away
+            ids = fake_ids(plugin.devices[0], 16)
+            await pc.allocate([ids[0:4]])
+            for _ in range(100):  # the debounced checkpoint ran and failed
+                if os.path.exists(plugin.journal_path + ".old"):
+                    break
+                await asyncio.sleep(0.02)
+            with open(plugin.journal_path + ".old") as f:
+                assert a["metadata"]["uid"] in f.read()
+            assert not os.path.exists(plugin.checkpoint)
+            await pc.close()
+            pc = None
+            await plugin.stop()
+            os.rmdir(plugin.checkpoint + ".tmp")
+            api_srv.server.faults.error_rate = 0.0
+            os.environ["GSX_PLUGIN_EARLY_ANSWER"] = "0"  # restarted with the knob off: still lands the commit
+            try:
+                again = GpuSharePlugin(client, "n1", fake_devices("2x16GiB"), P, socket_dir=os.path.join(tmp, "dp"))
+                await again.start(register=False)
+            finally:
+                os.environ.pop("GSX_PLUGIN_EARLY_ANSWER", None)
+            plugin = again
+            assert again.stats.get("commits_after_restart") == 1
+            assert (await client.get("pods", "a", "default"))["metadata"]["annotations"][P.annotation_assigned] == "true"
+            pc = PluginClient(again.socket_path)
+            r = (await pc.allocate([ids[4:8]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "b"
+            for _ in range(100):  # the first checkpoint supersedes both journal generations
+                if os.path.exists(again.checkpoint) and not os.path.exists(again.journal_path + ".old"):
+                    break
+                await asyncio.sleep(0.02)
+            with open(again.checkpoint) as f:
+                assert len(json.load(f)["records"]) == 2
+            assert not os.path.exists(again.journal_path + ".old")
+        finally:
+            api_srv.server.faults.error_rate = 0.0
+            await _close(api_srv, client, plugin, *([pc] if pc else []))
+    asyncio.run(go())
