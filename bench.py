@@ -632,6 +632,11 @@ def main():
             if st == 200 and json.loads(body).get("nodes"):
                 break
             time.sleep(0.005)
+        if a.agent == "node":
+            # kubelet (the node agent) watches the node's pods before the first wave is bound, as on a live node:
+            # pods it first met in one LIST would be admitted as one batch in name order, not as they landed
+            na_batch = E.BatchClient({"server": next(c.url for c in children if c.name == "node-agent")})
+            wait_until(lambda: na_batch.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 300, "node agent never ready")
         pod_tmpl = make_pod("__NAME__", a.pod_gib, profile=profile, labels={"gsx-wave": "__STEP__"})
         del pod_tmpl["metadata"]["uid"]  # the apiserver assigns one per pod
         pod_tmpl = json.dumps(pod_tmpl, separators=(",", ":"))

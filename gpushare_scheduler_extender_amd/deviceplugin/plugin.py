@@ -399,8 +399,9 @@ class GpuSharePlugin:
         return f"{time.time_ns() // 1_000_000:x}-{os.getpid():x}-{self._aid}"
 
     def _record(self, rec: PodRec, ids, units: int, alloc: ContainerAllocation) -> AllocRecord:
+        on_gpu = bool(ids) and all(self.id_owner.get(i) == rec.dev for i in ids)
         r = self.state.record(rec, ids, units, alloc.annotations.get("gpushare.amd.com/cu-mask", rec.cu_mask),
-                              self._next_aid(), time.time(), alloc.iso)
+                              self._next_aid(), time.time(), alloc.iso, on_gpu=on_gpu)
         self.persist_records()
         return r
 
@@ -621,7 +622,7 @@ class GpuSharePlugin:
                 self._record(rec, ids, units, alloc)
                 return rec, alloc
             if self.reconciler is not None:
-                rec = await self._physical_guard(rec, units)
+                rec = await self._physical_guard(rec, units, ids)
                 if rec is None:  # the repair it ran made the pod no candidate (it was served meanwhile): re-match
                     refreshed = True
                     continue
@@ -668,20 +669,27 @@ class GpuSharePlugin:
 
     def _physical_used(self, dev: int) -> int:
         """Units kubelet has handed out on ``dev`` (the Allocate records of live pods: what really runs there)."""
-        return sum(r.units for r in self.state.records.values() if r.dev == dev)
+        return self.state.core.physical_used(dev)
 
     def _annotated_used(self, dev: int, skip: str = "") -> int:
         """Units the pod annotations put on ``dev`` (what the extender's ledger accounts)."""
         return sum(p.request for p in self.state.pods.values() if p.dev == dev and p.uid != skip and not p.complete)
 
-    async def _physical_guard(self, rec: PodRec, units: int) -> PodRec | None:
+    def _kubelet_bounds(self, dev: int, ids) -> bool:
+        """kubelet's own per-ID accounting bounds GPU ``dev``: this Allocate's IDs all lie on it and so do those of
+        every recorded allocation (GetPreferredAllocation steered them), so kubelet cannot have handed out more of
+        ``dev`` than it has, whatever records of containers it has since freed still say (native twin:
+        dpcore.cc allocate)."""
+        return bool(ids) and all(self.id_owner.get(i) == dev for i in ids) and self.state.core.off_gpu_records() == 0
+
+    async def _physical_guard(self, rec: PodRec, units: int, ids=()) -> PodRec | None:
         """Never start a container on a GPU that is physically full.  The extender placed ``rec`` by the
         annotations; after a swap kubelet has not told us about yet, a deletion can free the GPU the annotation
         names while the container that really ran there lives on.  Repair the records first; if the GPU is still
         full, move ``rec`` (not yet started) to a GPU of this node with room by both counts, hold-protected like a
         reconciliation exchange; with no such GPU, fail the Allocate rather than over-commit."""
         cap = self.units.get(rec.dev, 0)
-        if self._physical_used(rec.dev) + units <= cap:
+        if self._physical_used(rec.dev) + units <= cap or self._kubelet_bounds(rec.dev, ids):
             return rec
         self.stats["physical_guard"] = self.stats.get("physical_guard", 0) + 1
         # a deleted pod's container may still be stopping (its record goes once kubelet stops listing its IDs):

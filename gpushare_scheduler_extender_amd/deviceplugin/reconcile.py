@@ -61,12 +61,15 @@ def _drifted(p: PodRec, r: AllocRecord) -> bool:
 
 class Reconciler:
     def __init__(self, plugin, client: PodResourcesClient, interval: float = 2.0, after_allocate: float = 0.02,
-                 stale_after: float = 0.5):
+                 stale_after: float = 0.5, gone_after: float = 0.02):
         self.plugin = plugin
         self.pr = client
         self.interval = interval
         self.after_allocate = after_allocate
         self.stale_after = stale_after
+        # a record kubelet does not list whose pods (built for, and held by) are both gone: kubelet records an
+        # Allocate's IDs within the admission call that made it, so past a moment nobody can hold them any more
+        self.gone_after = gone_after
         self.stats = {"passes": 0, "swaps": 0, "records_owned": 0, "unknown_ids": 0, "unreconcilable": 0,
                       "holds_finished": 0, "conflicts": 0, "errors": 0, "list_ms_max": 0.0, "records_stale": 0,
                       "assigned_reset": 0, "deferred": 0,
@@ -91,13 +94,18 @@ class Reconciler:
         async with self._lock:
             self.stats["passes"] += 1
             t0 = time.perf_counter()
+            # kubelet's answer describes the Allocates made before it was asked: the native endpoint keeps serving
+            # (and recording) while it is awaited, and kubelet re-uses the IDs of finished pods -- a record made
+            # after this point must not be judged by this answer (it would pin a re-used ID set on a pod of
+            # an earlier wave, or look unheld)
+            t_list = time.time()
             truth = await self.pr.device_ids(self.plugin.profile.resource)
             self.state.core.set_owners_reported(True)  # from now on kubelet's report decides who holds a record
             self.stats["list_ms_max"] = max(self.stats["list_ms_max"], 1e3 * (time.perf_counter() - t0))
             moves: list[tuple[str, str]] = []  # (P uid, record aid)
             drifts: list[tuple[str, str]] = []  # P holds its own record, but its annotation names another GPU
             seen = {tuple(ids) for per_container in truth.values() for ids in per_container}
-            self._drop_stale(seen, 0.1 if urgent else self.stale_after)
+            self._drop_stale(seen, 0.1 if urgent else self.stale_after, self.gone_after, t_list)
             for (ns, name), per_container in truth.items():
                 pod = self.state.pod_by_key(f"{ns}/{name}")
                 if pod is None:
@@ -105,11 +113,13 @@ class Reconciler:
                     # are physically held, but by no live pod -- they describe nobody who could be served them
                     for ids in per_container:
                         r = self.state.record_for_ids(ids)
-                        if r is not None and r.owner != GONE + f"{ns}/{name}":
+                        if r is not None and r.t <= t_list and r.owner != GONE + f"{ns}/{name}":
                             self.state.set_owner(r.aid, GONE + f"{ns}/{name}")
                     continue
                 for ids in per_container:
                     r = self.state.record_for_ids(ids)
+                    if r is not None and r.t > t_list:
+                        continue  # made after kubelet answered: the IDs were re-used since
                     if r is None:
                         self.stats["unknown_ids"] += 1
                         continue
@@ -152,9 +162,20 @@ class Reconciler:
                 self.plugin.persist_records()
             return {"moves": done, "pods": len(truth)}
 
-    def _drop_stale(self, seen: set, grace: float) -> None:
-        now = time.time()
-        stale = [r for r in self.state.records.values() if tuple(sorted(r.ids)) not in seen and now - r.t > grace]
+    def _drop_stale(self, seen: set, grace: float, gone_grace: float | None = None, asked: float | None = None) -> None:
+        """``asked``: when kubelet's answer (``seen``) was requested; a record is judged by it only if it was made
+        that long before."""
+        now = time.time() if asked is None else asked
+        pods = self.state.pods
+        gone_grace = grace if gone_grace is None else min(grace, gone_grace)
+
+        def stale(r) -> bool:
+            if tuple(sorted(r.ids)) in seen:
+                return False
+            gone = r.uid not in pods and (r.owner in ("", r.uid) or r.owner.startswith(GONE) or r.owner not in pods)
+            return now - r.t > (gone_grace if gone else grace)
+
+        stale = [r for r in self.state.records.values() if stale(r)]
         for r in stale:
             log.info("allocation %s (GPU %d) is held by no container kubelet reports: dropped", r.aid, r.dev)
             self.state.drop_record(r)

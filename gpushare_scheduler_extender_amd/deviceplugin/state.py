@@ -58,6 +58,7 @@ class AllocRecord:
     owner: str = ""  # the pod kubelet gave the IDs to ("" until PodResources has reported them)
     t: float = 0.0
     iso: str = ""  # isolation directory key the container's mounts point at
+    on_gpu: bool = False  # every ID lies on ``dev``: kubelet's per-ID accounting bounds that GPU (allocstate.h)
 
     @property
     def holder(self) -> str:
@@ -65,13 +66,13 @@ class AllocRecord:
 
     def to_dict(self) -> dict:
         return {"aid": self.aid, "ids": list(self.ids), "uid": self.uid, "dev": self.dev, "units": self.units,
-                "cu_mask": self.cu_mask, "owner": self.owner, "t": self.t, "iso": self.iso}
+                "cu_mask": self.cu_mask, "owner": self.owner, "t": self.t, "iso": self.iso, "on_gpu": self.on_gpu}
 
     @classmethod
     def from_dict(cls, d: dict) -> "AllocRecord":
         return cls(aid=d["aid"], ids=tuple(d.get("ids") or ()), uid=d.get("uid", ""), dev=int(d.get("dev", -1)),
                    units=int(d.get("units", 0)), cu_mask=d.get("cu_mask", ""), owner=d.get("owner", ""),
-                   t=float(d.get("t", 0.0)), iso=d.get("iso", ""))
+                   t=float(d.get("t", 0.0)), iso=d.get("iso", ""), on_gpu=bool(d.get("on_gpu", False)))
 
 
 @dataclass
@@ -283,10 +284,13 @@ class AllocationState:
 
     # ------------------------------------------------------------ allocation records
     def record(self, rec: PodRec, ids, units: int, cu_mask: str, aid: str, t: float = 0.0,
-               iso: str = "") -> AllocRecord:
+               iso: str = "", on_gpu: bool = False) -> AllocRecord:
         """An Allocate of ``ids`` was matched to ``rec`` (kubelet re-using the IDs of a finished pod replaces the
-        older record)."""
+        older record).  ``on_gpu``: every ID lies on the pod's GPU."""
         d = self.core.record(rec.uid, list(ids), int(units), cu_mask or "", aid, t, iso)
+        if on_gpu:
+            self.core.mark_on_gpu(aid, True)
+            d["on_gpu"] = True
         self._flush()
         return AllocRecord.from_dict(d)
 

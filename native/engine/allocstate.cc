@@ -436,6 +436,9 @@ AllocRecord& AllocState::record(const std::string& uid, const std::vector<std::s
   r.cu_mask = cu_mask;
   r.t = t;
   if (!ids.empty()) by_ids_[ids] = aid;
+  auto prev = records_.find(aid);
+  if (prev != records_.end()) count_record(prev->second, -1);
+  count_record(r, +1);
   auto res = records_.insert_or_assign(aid, std::move(r));
   return res.first->second;
 }
@@ -444,12 +447,38 @@ void AllocState::add_record(AllocRecord r) {
   std::sort(r.ids.begin(), r.ids.end());
   if (!r.ids.empty()) by_ids_[r.ids] = r.aid;
   std::string aid = r.aid;
+  auto prev = records_.find(aid);
+  if (prev != records_.end()) count_record(prev->second, -1);
+  count_record(r, +1);
   records_.insert_or_assign(aid, std::move(r));
+}
+
+void AllocState::count_record(const AllocRecord& r, int sign) {
+  if (r.dev >= 0) {
+    int64_t& u = phys_[r.dev];
+    u += sign * r.units;
+    if (u == 0) phys_.erase(r.dev);
+  }
+  if (!r.on_gpu) off_gpu_ = sign > 0 ? off_gpu_ + 1 : off_gpu_ - 1;
+}
+
+int64_t AllocState::physical_used(int64_t dev) const {
+  auto it = phys_.find(dev);
+  return it == phys_.end() ? 0 : it->second;
+}
+
+void AllocState::mark_on_gpu(const std::string& aid, bool on) {
+  auto it = records_.find(aid);
+  if (it == records_.end() || it->second.on_gpu == on) return;
+  count_record(it->second, -1);
+  it->second.on_gpu = on;
+  count_record(it->second, +1);
 }
 
 bool AllocState::drop_record(const std::string& aid) {
   auto it = records_.find(aid);
   if (it == records_.end()) return false;
+  count_record(it->second, -1);
   auto b = by_ids_.find(it->second.ids);
   if (b != by_ids_.end() && b->second == aid) by_ids_.erase(b);
   stats_.records_dropped++;

@@ -100,6 +100,9 @@ struct AllocRecord {
   std::string owner;             // the pod kubelet gave the IDs to ("" until PodResources said so)
   double t = 0;
   std::string iso;               // isolation directory key the container's mounts point at
+  // every ID lies on `dev` (by the plugin's fake-ID layout): kubelet's own per-ID accounting then bounds what
+  // physically runs on that GPU (false: unknown or mixed -- only the records can tell)
+  bool on_gpu = false;
   const std::string& holder() const { return owner.empty() ? uid : owner; }
 };
 
@@ -151,6 +154,10 @@ class AllocState {
   // describes P, whatever described P describes Q, and the CU partitions follow.
   void move_records(const std::string& p_uid, const std::string& q_uid, const std::string& aid);
   const std::map<std::string, AllocRecord>& records() const { return records_; }
+  // Units the records put on `dev` (what kubelet has handed out there, whoever holds it): kept incrementally
+  int64_t physical_used(int64_t dev) const;
+  void mark_on_gpu(const std::string& aid, bool on);
+  size_t off_gpu_records() const { return off_gpu_; }
   std::vector<AllocRecord> take_dropped();  // records dropped since the last call (isolation cleanup)
   bool dropped_pending() const { return !dropped_.empty(); }
 
@@ -174,6 +181,9 @@ class AllocState {
   std::map<std::string, AllocRecord> records_;            // aid -> record
   std::map<std::vector<std::string>, std::string> by_ids_;
   std::vector<AllocRecord> dropped_;
+  std::unordered_map<int64_t, int64_t> phys_;  // dev -> sum of record units (records_ kept in step)
+  size_t off_gpu_ = 0;                          // records with on_gpu == false
+  void count_record(const AllocRecord& r, int sign);
   bool owners_reported_ = false;
   AllocStats stats_;
 };

@@ -883,6 +883,7 @@ class PyDpServer {
         d["owner"] = r.owner;
         d["t"] = r.t;
         d["iso"] = r.iso;
+        d["on_gpu"] = r.on_gpu;
         out.append(d);
       }
     }
@@ -1508,6 +1509,7 @@ PYBIND11_MODULE(_engine, m) {
     d["owner"] = r.owner;
     d["t"] = r.t;
     d["iso"] = r.iso;
+    d["on_gpu"] = r.on_gpu;
     return d;
   };
   py::class_<AllocState>(m, "AllocState")
@@ -1576,9 +1578,13 @@ PYBIND11_MODULE(_engine, m) {
              r.owner = d.contains("owner") ? d["owner"].cast<std::string>() : std::string();
              r.t = d.contains("t") ? d["t"].cast<double>() : 0.0;
              r.iso = d.contains("iso") ? d["iso"].cast<std::string>() : std::string();
+             r.on_gpu = d.contains("on_gpu") && d["on_gpu"].cast<bool>();
              s.add_record(std::move(r));
            }, py::call_guard<AllocLock>())
       .def("drop_record", &AllocState::drop_record, py::call_guard<AllocLock>())
+      .def("mark_on_gpu", &AllocState::mark_on_gpu, py::call_guard<AllocLock>())
+      .def("physical_used", &AllocState::physical_used, py::call_guard<AllocLock>())
+      .def("off_gpu_records", &AllocState::off_gpu_records, py::call_guard<AllocLock>())
       .def("record_for_ids", [rec_dict](const AllocState& s, const std::vector<std::string>& ids) -> py::object {
              const AllocRecord* r = s.record_for_ids(ids);
              return r ? py::object(rec_dict(*r)) : py::object(py::none());

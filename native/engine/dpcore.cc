@@ -7,6 +7,7 @@
 
 #include <cerrno>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <set>
 
@@ -198,7 +199,7 @@ void DpCore::journal_append(const AllocRecord& r) {
   json::append_quoted(&line, r.cu_mask);
   line.append(",\"owner\":\"\",\"t\":").append(std::to_string(r.t)).append(",\"iso\":");
   json::append_quoted(&line, r.iso);
-  line.append("}\n");
+  line.append(",\"on_gpu\":").append(r.on_gpu ? "true" : "false").append("}\n");
   // O_APPEND: one write per line, so a crash leaves whole lines (the page cache outlives this process)
   ssize_t n = ::write(jfd_, line.data(), line.size());
   (void)n;
@@ -255,12 +256,14 @@ void DpCore::set_devices(std::vector<DpDevice> devs, std::map<std::string, int> 
   for (const auto& kv : id_owner_) id_owner_view_.emplace(std::string_view(kv.first), kv.second);
 }
 
-int64_t DpCore::physical_used(int dev) const {
-  int64_t n = 0;
-  for (const auto& kv : state_->records()) {
-    if (kv.second.dev == dev) n += kv.second.units;
+int64_t DpCore::physical_used(int dev) const { return state_->physical_used(dev); }
+
+bool DpCore::ids_on(const std::vector<std::string>& ids, int dev) const {
+  for (const auto& id : ids) {
+    auto o = id_owner_.find(id);
+    if (o == id_owner_.end() || o->second != dev) return false;
   }
-  return n;
+  return !ids.empty();
 }
 
 bool DpCore::preferred(const std::string& req, std::string* resp, std::string* why) {
@@ -326,10 +329,18 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   }
   const DpDevice& dev = dit->second;
   const bool later = pod.assigned == "true";
+  // kubelet hands out each fake ID once and GetPreferredAllocation steers a pod's IDs onto its GPU: when this
+  // Allocate's IDs all lie on the pod's GPU and so do those of every recorded allocation, kubelet's own per-ID
+  // accounting bounds what runs on that GPU (it holds exactly `units` IDs of it), whatever the records of pods
+  // it has since freed still say.  Otherwise the records decide (the Python guard repairs and waits).
+  const bool on_gpu = ids_on(ids, dev.index);
   if (!later && cfg_.guard && physical_used(dev.index) + units > dev.units) {
-    stats_.slow_allocate++;
-    *why = "GPU physically full by the records";
-    return DpStep::Slow;
+    if (!on_gpu || state_->off_gpu_records() != 0) {
+      stats_.slow_allocate++;
+      *why = "GPU physically full by the records";
+      return DpStep::Slow;
+    }
+    stats_.guard_by_ids++;
   }
   if (!later && !api_) {
     stats_.slow_allocate++;
@@ -359,6 +370,7 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   p->had_cus = had_cus;
   p->units = units;
   p->ids = ids;
+  p->on_gpu = on_gpu;
   p->cr = build_response(pod, dev, units, cus, cfg_.mount_mode, cfg_.profile);
   p->t0 = t0;
   p->tm = tm;
@@ -489,7 +501,8 @@ void DpCore::record_and_answer(DpPending& p, std::string* resp, DpEvent* ev) {
   AllocRecord& rec = state_->record(p.pod.uid, p.ids, p.units,
                                     cm != p.cr.annotations.end() ? cm->second : p.pod.cu_mask, aid, wall_s());
   rec.iso = p.iso;
-  if (p.answered) journal_append(rec);  // durable before kubelet has the answer
+  if (p.on_gpu) state_->mark_on_gpu(aid, true);
+  if (p.answered) journal_append(*state_->record_by_aid(aid));  // durable before kubelet has the answer
   *resp = dp::encode_allocate_response({p.cr});
   stats_.fast_allocate++;
   ev->uid = p.pod.uid;

@@ -77,6 +77,7 @@ struct DpPending {
   bool whole = false, had_cus = false;
   int64_t units = 0;
   std::vector<std::string> ids;
+  bool on_gpu = false;  // every ID lies on the pod's GPU
   dp::ContainerResponse cr;
   std::string iso, path, body;
   double t0 = 0, tm = 0, ti0 = 0, ti1 = 0, tp0 = 0, tp1 = 0;
@@ -118,6 +119,7 @@ class DpCore {
 
   struct Stats {
     uint64_t fast_allocate = 0, fast_preferred = 0, slow_allocate = 0, slow_preferred = 0, patch_failures = 0;
+    uint64_t guard_by_ids = 0;  // the records said full, kubelet's IDs said there is room
   };
   const Stats& stats() const { return stats_; }
   // early answer: the journal's lines move to <journal>.old (appended if a previous checkpoint left one) and the
@@ -127,6 +129,7 @@ class DpCore {
   bool journaling() const { return jfd_ >= 0; }
   const std::string& journal_path() const { return cfg_.journal; }
   int64_t physical_used(int dev) const;
+  bool ids_on(const std::vector<std::string>& ids, int dev) const;
 
  private:
   DpConfig cfg_;

@@ -1,5 +1,7 @@
 #include "dpproto.h"
 
+#include <algorithm>
+
 #include <string_view>
 
 namespace gsx::dp {
@@ -271,6 +273,79 @@ bool decode_allocate_response(const std::string& msg, std::vector<ContainerRespo
     });
     out->push_back(std::move(r));
     return ok;
+  });
+}
+
+std::string encode_pod_resources_list(const std::vector<PodDevicesMsg>& entries) {
+  // PodResources{1 name, 2 namespace, 3 repeated ContainerResources{1 name, 2 repeated ContainerDevices{
+  // 1 resource_name, 2 repeated device_ids}}}; ListPodResourcesResponse{1 repeated PodResources}
+  std::vector<std::pair<std::pair<std::string, std::string>, std::string>> pods;  // (ns, name) -> containers
+  for (const auto& e : entries) {
+    std::string dev;
+    str_if(&dev, 1, e.resource);
+    for (const auto& id : e.ids) bytes(&dev, 2, id);
+    std::string c;
+    str_if(&c, 1, e.container);
+    bytes(&c, 2, dev);
+    auto it = std::find_if(pods.begin(), pods.end(), [&](const auto& p) {
+      return p.first.first == e.ns && p.first.second == e.name;
+    });
+    if (it == pods.end()) {
+      pods.push_back({{e.ns, e.name}, std::string()});
+      it = pods.end() - 1;
+    }
+    bytes(&it->second, 3, c);
+  }
+  std::string out;
+  for (const auto& p : pods) {
+    std::string pr;
+    str_if(&pr, 1, p.first.second);
+    str_if(&pr, 2, p.first.first);
+    pr += p.second;
+    bytes(&out, 1, pr);
+  }
+  return out;
+}
+
+bool decode_pod_resources_list(const std::string& msg, std::vector<PodDevicesMsg>* entries) {
+  return each(msg, [&](int f, int w, std::string_view pr, uint64_t) {
+    if (f != 1 || w != 2) return true;
+    std::string ns, name;
+    std::vector<std::string_view> containers;
+    bool ok = each(pr, [&](int f2, int w2, std::string_view pl, uint64_t) {
+      if (w2 != 2) return true;
+      if (f2 == 1) name = pl;
+      if (f2 == 2) ns = pl;
+      if (f2 == 3) containers.push_back(pl);
+      return true;
+    });
+    if (!ok) return false;
+    for (auto c : containers) {
+      std::string cname;
+      std::vector<std::string_view> devs;
+      if (!each(c, [&](int f3, int w3, std::string_view pl, uint64_t) {
+            if (w3 == 2 && f3 == 1) cname = pl;
+            if (w3 == 2 && f3 == 2) devs.push_back(pl);
+            return true;
+          })) {
+        return false;
+      }
+      for (auto d : devs) {
+        PodDevicesMsg m;
+        m.ns = ns;
+        m.name = name;
+        m.container = cname;
+        if (!each(d, [&](int f4, int w4, std::string_view pl, uint64_t) {
+              if (w4 == 2 && f4 == 1) m.resource = pl;
+              if (w4 == 2 && f4 == 2) m.ids.emplace_back(pl);
+              return true;
+            })) {
+          return false;
+        }
+        entries->push_back(std::move(m));
+      }
+    }
+    return true;
   });
 }
 

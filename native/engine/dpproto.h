@@ -41,7 +41,17 @@ struct PreferredRequestView {
   int32_t size = 0;
 };
 
+// kubelet PodResources API v1 (k8s.io/kubelet/pkg/apis/podresources/v1/api.proto, deviceplugin/podresources.py):
+// the devices of one container of one pod
+struct PodDevicesMsg {
+  std::string ns, name, container, resource;
+  std::vector<std::string> ids;
+};
+
 // ---- encode
+// ListPodResourcesResponse: one PodResources per (ns, name) in first-seen order, one ContainerResources per entry
+std::string encode_pod_resources_list(const std::vector<PodDevicesMsg>& entries);
+bool decode_pod_resources_list(const std::string& msg, std::vector<PodDevicesMsg>* entries);
 std::string encode_options(bool pre_start_required, bool preferred_available);
 std::string encode_list_and_watch(const std::vector<DeviceMsg>& devs);
 std::string encode_preferred_response(const std::vector<std::vector<std::string>>& per_container);

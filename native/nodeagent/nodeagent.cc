@@ -30,6 +30,7 @@
 // Allocate, and the plugin's ASSIGNED commit inside it, are serial); starting the container (runtime + Running
 // patch) runs on the workers in parallel, as kubelet's pod workers do.  Without it the in-process matcher admits
 // on all workers at once.
+#include <poll.h>
 #include <signal.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -164,10 +165,14 @@ class Agent {
       }
       f << "]";
     }
+    // kubelet's PodResources API, served by this agent (pr_serve): the plugin reconciles its Allocate records
+    // against it, as under a real kubelet
+    pr_sock_ = dir + "/pod-resources.sock";
+    if (!pr_start(err)) return false;
     std::vector<std::string> args = {spawn_python_, "-m", "gpushare_scheduler_extender_amd.deviceplugin", "--node", node_,
                                      "--apiserver", spawn_api_, "--profile", spawn_profile_, "--unit", spawn_unit_,
                                      "--backend", "fake", "--socket-dir", dir, "--no-publish", "--no-register",
-                                     "--podresources-socket", "", "--isolation", "advisory", "--health-interval",
+                                     "--podresources-socket", pr_sock_, "--isolation", "advisory", "--health-interval",
                                      "3600", "--log-level", "warning"};
     pid_t pid = ::fork();
     if (pid < 0) {
@@ -236,6 +241,7 @@ class Agent {
     cv_.notify_all();
     for (auto& t : workers_) t.join();
     if (pods_r_) pods_r_->stop();
+    pr_stop();
     if (plugin_pid_ > 0) {
       ::kill(plugin_pid_, SIGTERM);
       for (int i = 0; i < 100 && ::waitpid(plugin_pid_, nullptr, WNOHANG) == 0; ++i) ::usleep(50000);
@@ -266,7 +272,7 @@ class Agent {
                     "\"runtime\":%.3f,\"running_patch\":%.3f},\"mean_ms\":{\"queue\":%.4f,\"assign_patch\":%.4f,"
                     "\"runtime\":%.4f,\"running_patch\":%.4f},\"status_retries\":%llu,\"api_connects\":%llu,"
                     "\"plugin_calls_mean_ms\":{\"n\":%llu,\"slot_wait\":%.4f,\"get_preferred\":%.4f,\"allocate\":%.4f},"
-                    "\"native\":true}",
+                    "\"mismatch\":%llu,\"podresources_calls\":%llu,\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
                     (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
                     max_queue_ * 1e3, max_patch_ * 1e3, max_runtime_ * 1e3, max_status_ * 1e3, sum_queue_ / n * 1e3,
@@ -274,7 +280,8 @@ class Agent {
                     (unsigned long long)status_retries_.load(), (unsigned long long)api_.reconnects(),
                     (unsigned long long)dp_calls_, sum_dp_slot_ / std::max<double>(1.0, dp_calls_) * 1e3,
                     sum_dp_pref_ / std::max<double>(1.0, dp_calls_) * 1e3,
-                    sum_dp_alloc_ / std::max<double>(1.0, dp_calls_) * 1e3);
+                    sum_dp_alloc_ / std::max<double>(1.0, dp_calls_) * 1e3, (unsigned long long)mismatch_,
+                    (unsigned long long)pr_calls_.load());
       rep.body = b;
       return rep;
     }
@@ -385,11 +392,7 @@ class Agent {
     if (r == running_.end()) return;
     int dev = r->second;
     running_.erase(r);
-    auto ui = used_ids_.find(uid);
-    if (ui != used_ids_.end()) {
-      for (const auto& id : ui->second) used_all_.erase(id);
-      used_ids_.erase(ui);
-    }
+    forget_ids_locked(uid);
     for (auto& kv : devices_) {
       if (CuPartitioner* cp = state_->cus(kv.first)) cp->release(uid);
     }
@@ -488,10 +491,10 @@ class Agent {
   }
 
   // ---------------------------------------------------------------- kubelet + the shipped device plugin
-  // With --plugin-socket the Allocate is not decided here: like kubelet, this agent asks the plugin
-  // (GetPreferredAllocation, then Allocate with those IDs) over the device-plugin gRPC API and starts whichever
-  // pod the plugin committed (the container annotation gpushare.amd.com/pod names it), re-queueing the admitted
-  // pod if that was another one (the forgiving stand-in, as deviceplugin/agent.py without --faithful).
+  // With --plugin-socket / --plugin-spawn the Allocate is not decided here: like kubelet, this agent asks the
+  // plugin (GetPreferredAllocation, then Allocate with those IDs) over the device-plugin gRPC API and starts the
+  // pod it admitted with whatever came back (never re-routed: a swap is the plugin's to repair, from this agent's
+  // PodResources record), as kubelet does.
   bool plugin_connect(double timeout_s, std::string* err) {
     dp_ = std::make_unique<h2::Client>(plugin_sock_);
     double deadline = now_s() + timeout_s;
@@ -560,7 +563,11 @@ class Agent {
            dp::decode_allocate_response(resp, &crs) && crs.size() == 1;
     }
     const double tp1 = now_s();
-    if (slot && slot->owns_lock()) slot->unlock();
+    // the admission slot is given up only once the IDs are recorded as used (below): kubelet's device manager
+    // records an allocation before its next admission, which must never be offered the same IDs
+    auto release_slot = [slot] {
+      if (slot && slot->owns_lock()) slot->unlock();
+    };
     lk.lock();
     dp_calls_++;
     sum_dp_slot_ += ts - tp0;  // waiting for the admission slot (another pod's calls)
@@ -569,6 +576,7 @@ class Agent {
     state_->set_inflight(my_uid, false);
     if (!ok) {
       failed_++;
+      release_slot();
       std::fprintf(stderr, "[gsx-nodeagent] Allocate for %s failed: %d %s\n", key.c_str(), st, err.c_str());
       lk.unlock();
       std::string stj = "{\"status\":{\"phase\":\"Failed\",\"reason\":\"UnexpectedAdmissionError\",\"message\":";
@@ -579,22 +587,31 @@ class Agent {
       return;
     }
     const dp::ContainerResponse& cr = crs[0];
+    // kubelet never re-routes an allocation: the container of the pod it admitted starts with whatever the plugin
+    // answered.  An answer built for another pod (the plugin names it in the gpushare.amd.com/pod container
+    // annotation) is a swap the plugin repairs from this agent's PodResources record, as under a real kubelet
     std::string who = cr.annotations.count("gpushare.amd.com/pod") ? cr.annotations.at("gpushare.amd.com/pod") : "";
     size_t cut = who.rfind('/');
-    std::string uid = cut == std::string::npos ? my_uid : who.substr(cut + 1);
-    key = cut == std::string::npos ? my_key : who.substr(0, cut);
-    if (uid != my_uid) {  // the plugin committed an earlier pod of this size: it starts, ours waits for the next
-      queued_.insert(my_uid);
-      queue_.push_back(my_key);
-      ++added_;
-      wake_locked();
+    if (cut != std::string::npos && who.substr(cut + 1) != my_uid) {
+      mismatch_++;
+      std::fprintf(stderr, "[gsx-nodeagent] %s admitted with the allocation built for %s\n", my_key.c_str(),
+                   who.c_str());
     }
-    if (running_.count(uid) || !keys_.count(key)) return;  // already started, or gone meanwhile
-    used_ids_[uid] = chosen[0];
+    auto kit = keys_.find(my_key);
+    if (running_.count(my_uid) || kit == keys_.end() || kit->second != my_uid) {  // gone meanwhile
+      release_slot();
+      return;
+    }
+    used_ids_[my_uid] = chosen[0];
+    uid_key_[my_uid] = my_key;
     used_all_.insert(chosen[0].begin(), chosen[0].end());
+    release_slot();
     auto idx = cr.envs.find(p_.a_idx);
     const int dev_idx = idx == cr.envs.end() ? -1 : std::atoi(idx->second.c_str());
-    if (!devices_.count(dev_idx)) return;
+    if (!devices_.count(dev_idx)) {
+      forget_ids_locked(my_uid);
+      return;
+    }
     std::vector<int> cus;
     auto cm = cr.envs.find("GSX_CU_MASK");
     if (cm != cr.envs.end()) {
@@ -604,11 +621,82 @@ class Agent {
         cus.clear();
       }
     }
-    const AllocPod* started = state_->pod(uid);
-    const int64_t request = started ? started->request : units;
-    state_->set_inflight(uid, true);
-    start_pod_locked(key, uid, request, dev_idx, cus, allocation_json(cr),
-                     "/api/v1/namespaces/" + mine_ns(key) + "/pods/" + mine_name(key), t0, tp0, tp1, lk);
+    // the container's share is what the plugin's env says it got (SHARED_GPU_MEM_CONTAINER)
+    auto ce = cr.envs.find(p_.env_container);
+    const int64_t request = ce == cr.envs.end() ? units : std::max<int64_t>(1, std::atoll(ce->second.c_str()));
+    state_->set_inflight(my_uid, true);
+    start_pod_locked(my_key, my_uid, request, dev_idx, cus, allocation_json(cr),
+                     "/api/v1/namespaces/" + mine_ns(my_key) + "/pods/" + mine_name(my_key), t0, tp0, tp1, lk);
+  }
+
+  void forget_ids_locked(const std::string& uid) {
+    auto ui = used_ids_.find(uid);
+    if (ui != used_ids_.end()) {
+      for (const auto& id : ui->second) used_all_.erase(id);
+      used_ids_.erase(ui);
+    }
+    uid_key_.erase(uid);
+  }
+
+  // ---------------------------------------------------------------- kubelet's PodResources API (v1 List / Get)
+  // What kubelet's device manager recorded: the device IDs each admitted container holds, until the pod goes.
+  bool pr_start(std::string* err) {
+    pr_srv_ = std::make_unique<h2::Server>(pr_sock_, [this](h2::Server& s, const h2::Call& c) { pr_call(s, c); });
+    if (!pr_srv_->ok()) {
+      *err = "PodResources endpoint: " + pr_srv_->init_error();
+      return false;
+    }
+    pr_thread_ = std::thread([this] {
+      const int ep = pr_srv_->fd();
+      while (!pr_stop_.load()) {
+        pollfd pf{ep, POLLIN, 0};
+        ::poll(&pf, 1, 100);
+        pr_srv_->poll();
+      }
+    });
+    return true;
+  }
+
+  void pr_stop() {
+    if (!pr_thread_.joinable()) return;
+    pr_stop_.store(true);
+    pr_thread_.join();
+    pr_srv_.reset();
+  }
+
+  void pr_call(h2::Server& s, const h2::Call& call) {
+    pr_calls_.fetch_add(1);
+    const std::string svc = "/v1.PodResourcesLister/";
+    if (call.path.compare(0, svc.size(), svc) != 0) {
+      s.respond(call.id, 12, "unknown service " + call.path);
+      return;
+    }
+    const std::string m = call.path.substr(svc.size());
+    if (m == "GetAllocatableResources") {
+      s.respond(call.id, 0, std::string());
+      return;
+    }
+    if (m != "List") {
+      s.respond(call.id, 12, "unknown method " + m);
+      return;
+    }
+    std::vector<dp::PodDevicesMsg> out;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      out.reserve(used_ids_.size());
+      for (const auto& kv : used_ids_) {
+        auto k = uid_key_.find(kv.first);
+        if (k == uid_key_.end()) continue;
+        dp::PodDevicesMsg e;
+        e.ns = mine_ns(k->second);
+        e.name = mine_name(k->second);
+        e.container = "main";
+        e.resource = p_.resource;
+        e.ids = kv.second;
+        out.push_back(std::move(e));
+      }
+    }
+    s.respond(call.id, 0, dp::encode_pod_resources_list(out));
   }
 
   static std::string mine_ns(const std::string& key) { return key.substr(0, key.find('/')); }
@@ -757,6 +845,7 @@ class Agent {
       bad_ += static_cast<uint64_t>(bad);
       if (!cus.empty() && cp) cp->release(uid);
       state_->set_inflight(uid, false);
+      forget_ids_locked(uid);
       lk.unlock();
       if (rst == 200) runtime_call(dev_idx, "DELETE", "/v1/pods/" + uid, std::string(), nullptr);
       std::fprintf(stderr, "[gsx-nodeagent] admission of %s on GPU %d failed: %s\n", key.c_str(), dev_idx, why.c_str());
@@ -863,6 +952,13 @@ class Agent {
   std::vector<std::string> all_ids_;
   std::unordered_map<std::string, std::vector<std::string>> used_ids_;  // uid -> the IDs its Allocate took
   std::unordered_set<std::string> used_all_;                             // the union of used_ids_, kept with it
+  std::unordered_map<std::string, std::string> uid_key_;                 // uid -> ns/name of every used_ids_ pod
+  std::string pr_sock_;                    // kubelet's PodResources API socket (with --plugin-spawn)
+  std::unique_ptr<h2::Server> pr_srv_;
+  std::thread pr_thread_;
+  std::atomic<bool> pr_stop_{false};
+  std::atomic<uint64_t> pr_calls_{0};
+  uint64_t mismatch_ = 0;  // admissions answered with an allocation built for another pod (swaps)
   std::unordered_map<std::string, std::string> keys_;  // ns/name -> uid of every pod the informer delivered
   std::map<int, std::unique_ptr<ApiClient>> runtimes_;
   std::unique_ptr<Reflector> pods_r_;
