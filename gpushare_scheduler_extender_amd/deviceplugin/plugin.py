@@ -854,7 +854,9 @@ class GpuSharePlugin:
             asyncio.get_running_loop().add_reader(self._native_fd, self._native_poll)
             self.grpc_impl = "native"
             return
-        log.info("device-plugin endpoint on grpcio (%s)", why)
+        # loud: the native endpoint is the product path (kubelet's serial admission pays every call's overhead)
+        log.warning("device-plugin endpoint on grpc.aio, not the native endpoint (%s): Allocate admissions are "
+                    "about 2x slower; install libnghttp2 (libnghttp2-14) to restore it", why)
         self.grpc_impl = "grpcio"
         self._server = grpc.aio.server()
         self._server.add_generic_rpc_handlers((self._handlers(),))
@@ -922,6 +924,9 @@ class GpuSharePlugin:
                 lines += [f"# TYPE {name} {kind}", f"{name} {v}"]
         for k, v in sorted(self.state.stats.items()):
             lines += [f"# TYPE gpushare_plugin_state_{k}_total counter", f"gpushare_plugin_state_{k}_total {v}"]
+        # 1: kubelet's calls are served by the native endpoint (h2.cc on libnghttp2); 0: the grpc.aio fallback
+        lines += ["# TYPE gpushare_plugin_native_endpoint gauge",
+                  f"gpushare_plugin_native_endpoint {int(self.grpc_impl == 'native')}"]
         lines.append("# TYPE gpushare_plugin_device_healthy gauge")
         lines += [f'gpushare_plugin_device_healthy{{device="{d.index}"}} {int(d.healthy)}' for d in self.devices.values()]
         for name, key in (("thermal_throttle", "thermal_throttle"), ("power_throttle", "power_throttle"),

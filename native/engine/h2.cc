@@ -108,8 +108,10 @@ bool sym(void* h, const char* name, F* out) {
 }
 
 void load() {
-  void* h = dlopen("libnghttp2.so.14", RTLD_NOW | RTLD_LOCAL);
-  if (!h) h = dlopen("libnghttp2.so", RTLD_NOW | RTLD_LOCAL);
+  // GSX_NGHTTP2_LIB: the library to load instead (an image with another soname, or a test hiding it)
+  const char* want = std::getenv("GSX_NGHTTP2_LIB");
+  void* h = dlopen(want && *want ? want : "libnghttp2.so.14", RTLD_NOW | RTLD_LOCAL);
+  if (!h && !(want && *want)) h = dlopen("libnghttp2.so", RTLD_NOW | RTLD_LOCAL);
   if (!h) {
     g_load_err = std::string("dlopen libnghttp2: ") + dlerror();
     return;

@@ -342,3 +342,49 @@ def test_early_answer_checkpoint_failure_keeps_the_journal_generation():
             api_srv.server.faults.error_rate = 0.0
             await _close(api_srv, client, plugin, *([pc] if pc else []))
     asyncio.run(go())
+
+
+def test_missing_libnghttp2_falls_back_loudly():
+    """without libnghttp2 the plugin serves kubelet from grpc.aio; it must say so -- a WARNING at
+    startup and gpushare_plugin_native_endpoint 0 on /metrics (1 with the library)."""
+    import subprocess
+    import sys
+
+    script = r'''
+import asyncio, logging, os, sys, tempfile
+sys.path.insert(0, os.getcwd())
+from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
+from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin
+from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+from gpushare_scheduler_extender_amd.k8s.objects import make_node
+from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+from tests.fixtures.fakeapi import FakeApiServerRunner
+logging.basicConfig(level=logging.WARNING, stream=sys.stdout, format="%(levelname)s %(message)s")
+async def go():
+    tmp = tempfile.mkdtemp()
+    api = await FakeApiServerRunner().start()
+    c = KubeClient(api.url)
+    await c.create("nodes", make_node("n1", 16, 0))
+    p = GpuSharePlugin(c, "n1", fake_devices("1x16GiB"), SHARED_GPU, socket_dir=os.path.join(tmp, "dp"))
+    await p.start(register=False)
+    print("IMPL", p.grpc_impl)
+    print([l for l in p.metrics_text().splitlines() if l.startswith("gpushare_plugin_native_endpoint ")][0])
+    await p.stop(); await c.close(); await api.stop()
+asyncio.run(go())
+'''
+    import pathlib
+
+    root = str(pathlib.Path(__file__).resolve().parents[1])
+    out = {}
+    for hide in (True, False):
+        env = dict(os.environ)
+        env.pop("GSX_PLUGIN_GRPC", None)
+        if hide:
+            env["GSX_NGHTTP2_LIB"] = "/nonexistent/libnghttp2.so.14"
+        r = subprocess.run([sys.executable, "-c", script], env=env, cwd=root, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[hide] = r.stdout
+    assert "IMPL grpcio" in out[True] and "gpushare_plugin_native_endpoint 0" in out[True], out[True]
+    assert "WARNING device-plugin endpoint on grpc.aio" in out[True] and "libnghttp2" in out[True], out[True]
+    assert "IMPL native" in out[False] and "gpushare_plugin_native_endpoint 1" in out[False], out[False]
