@@ -297,9 +297,10 @@ def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
     registers with the stand-in's Registration service, as under a real kubelet."""
     from gpushare_scheduler_extender_amd.sim.cluster import start_node_agent
 
+    ext_url = next(c.url for c in children if c.name == "extender")
     na = restart_child(children, "node-agent", lambda old: start_node_agent(
         api_url, NODE, profile=a.profile, native=False, plugin=a.plugin_proc, cpus=old.cpus,
-        extra=["--faithful"] if a.kubelet == "faithful" else [], plugin_cpus=a.plugin_cpus))
+        extra=["--faithful"] if a.kubelet == "faithful" else [], plugin_cpus=a.plugin_cpus, extender=ext_url))
     client = E.BatchClient({"server": na.url})
     wait_until(lambda: client.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 120, "plugin agent never ready")
     row = runner.measure(3, max(a.sweep_steps, 40))  # ~2 ms waves: 40 of them cost little and steady the row
@@ -312,27 +313,40 @@ def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
             "plugin_stats": stats.get("plugin_stats"), "plugin": stats.get("plugin")}
 
 
-def plugin_path_native_kubelet(a, children, api_url, runner: WaveRunner, E) -> dict:
-    """The same waves with the compiled kubelet stand-in (gsx-nodeagent --plugin-spawn) calling the shipped plugin
-    process over the device-plugin gRPC API: GetPreferredAllocation + Allocate per pod, serially as kubelet
-    admits, answered by the plugin's native endpoint (native/engine/h2.cc + dpcore.cc) on its own informer and
-    allocation state.  Every Allocate decision and ASSIGNED patch is the product's."""
+def inprocess_matcher_path(a, children, api_url, runner: WaveRunner, E) -> dict:
+    """The same waves with the compiled kubelet stand-in deciding every Allocate with the plugin's matcher linked
+    in-process (allocstate.h) and committing ASSIGNED itself -- no gRPC hop to a plugin process, no PodResources
+    reconciliation.  The rounds-1..3 headline path, kept as a comparison row."""
     from gpushare_scheduler_extender_amd.sim.cluster import start_node_agent
 
+    ext_url = next(c.url for c in children if c.name == "extender")
     na = restart_child(children, "node-agent", lambda old: start_node_agent(
-        api_url, NODE, profile=a.profile, native=True, plugin="spawn", cpus=old.cpus, plugin_cpus=a.plugin_cpus))
+        api_url, NODE, profile=a.profile, native=True, plugin="grpc", cpus=old.cpus, serial_admission=True,
+        extender=ext_url))
     client = E.BatchClient({"server": na.url})
-    wait_until(lambda: client.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 120, "plugin agent never ready")
-    row = runner.measure(3, max(a.sweep_steps, 40))  # ~2 ms waves: 40 of them cost little and steady the row
+    wait_until(lambda: client.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 120, "node agent never ready")
+    row = runner.measure(3, max(a.sweep_steps, 40))
     st, body = client.run([("GET", "/v1/stats", b"")], 1)[0]
     stats = json.loads(body) if st == 200 else {}
     return {**row, "admit_p50_ms": stats.get("admit_p50_ms"), "failed": stats.get("failed"),
-            "kubelet_mean_ms": {"queue": (stats.get("mean_ms") or {}).get("queue"),
-                                "preferred_plus_allocate_grpc": (stats.get("mean_ms") or {}).get("assign_patch"),
-                                "runtime": (stats.get("mean_ms") or {}).get("runtime"),
-                                "running_patch": (stats.get("mean_ms") or {}).get("running_patch")},
-            # kubelet's serial admission per pod: waiting for the slot, then the two calls as the client sees them
-            "plugin_calls_mean_ms": stats.get("plugin_calls_mean_ms")}
+            "kubelet_mean_ms": stats.get("mean_ms")}
+
+
+def _plugin_debug(E, url: str | None) -> dict | None:
+    """The shipped plugin process's own counters (its /debug/state): Allocates answered on the native fast path,
+    early-answer commits, kubelet-PodResources reconciliation (swaps repaired, moves through the extender)."""
+    if not url:
+        return None
+    try:
+        st, body = E.BatchClient({"server": url}).run([("GET", "/debug/state", b"")], 1)[0]
+        d = json.loads(body) if st == 200 else {}
+    except Exception as e:  # noqa: BLE001 - a missing row never costs the headline line
+        return {"error": repr(e)}
+    g = d.get("grpc") or {}
+    return {"grpc": {k: g.get(k) for k in ("impl", "fast_allocate", "slow_allocate", "fast_preferred",
+                                           "slow_preferred", "patch_failures", "guard_by_ids", "journaling",
+                                           "early_answer_backlog")},
+            "stats": d.get("stats"), "reconcile": d.get("reconcile")}
 
 
 def parse():
@@ -355,10 +369,12 @@ def parse():
                     help="write every timed pod's scheduler timeline (CLOCK_MONOTONIC, like the wave's t0) here")
     ap.add_argument("--agent", default="node", choices=["node", "rank"],
                     help="node: one node-agent process (the node's device plugin) driving a runtime shim per GPU rank (default); rank: one agent per GPU rank")
-    ap.add_argument("--node-agent", default="native", choices=["native", "native-plugin", "plugin", "inproc"],
-                    help="kubelet + device plugin: gsx-nodeagent with the plugin's matcher in-process (native), "
-                         "gsx-nodeagent calling the shipped plugin process over gRPC (native-plugin), or the Python "
-                         "kubelet stand-in driving the shipped plugin over its socket (plugin) / in-process (inproc)")
+    ap.add_argument("--node-agent", default="native-plugin", choices=["native", "native-plugin", "plugin", "inproc"],
+                    help="kubelet + device plugin: the compiled kubelet stand-in (gsx-nodeagent: faithful serial "
+                         "admission, never re-routes, serves PodResources) calling the shipped plugin process over "
+                         "the device-plugin gRPC API (native-plugin, default: the product path), gsx-nodeagent with "
+                         "the plugin's matcher linked in-process (native), or the Python kubelet stand-in driving the "
+                         "shipped plugin over its socket (plugin) / in-process (inproc)")
     ap.add_argument("--pin", default="auto", choices=["auto", "spread", "static", "compact", "none"],
                     help="CPU placement of the control-plane processes (auto = spread: the idlest physical cores, "
                          "sampled at start; static: topology order without the load sample)")
@@ -386,9 +402,10 @@ def parse():
                     help="compiled node agent with its in-process matcher: admit (Allocate + ASSIGNED commit) one pod "
                          "at a time in arrival order as kubelet does (serial, default), or on all workers at once "
                          "(parallel); containers start in parallel either way")
-    ap.add_argument("--kubelet", default="standin", choices=["standin", "faithful"],
-                    help="with --node-agent plugin: the kubelet stand-in re-routes a mismatched Allocate (standin) or "
-                         "behaves like kubelet and lets the plugin reconcile (faithful)")
+    ap.add_argument("--kubelet", default="faithful", choices=["standin", "faithful"],
+                    help="with --node-agent plugin (the Python kubelet stand-in): it behaves like kubelet and lets the "
+                         "plugin reconcile from its PodResources record (faithful, default), or re-routes a "
+                         "mismatched Allocate (standin)")
     ap.add_argument("--plugin-proc", default="process", choices=["process", "grpc"],
                     help="device-plugin path row: the plugin as its own process registered with the kubelet "
                          "stand-in, as the DaemonSet runs it (process), or served from the stand-in's process (grpc)")
@@ -504,8 +521,11 @@ def main():
                                                                                                         "grpc"),
                                              workers=min(16, max(8, 2 * a.pods_per_gpu * world)),
                                              cpus=cpu_plan.get("node-agent"),
-                                             extra=["--faithful"] if a.kubelet == "faithful" else [],
-                                             plugin_cpus=a.plugin_cpus, serial_admission=a.admission == "serial"))
+                                             # the compiled stand-in is kubelet-faithful in plugin mode already
+                                             extra=["--faithful"] if a.kubelet == "faithful" and a.node_agent in (
+                                                 "plugin", "inproc") else [],
+                                             plugin_cpus=a.plugin_cpus, serial_admission=a.admission == "serial",
+                                             extender=ext.url))
         api_url, ext_url = api.url, ext.url
 
     import torch
@@ -823,11 +843,12 @@ def main():
             mine["gpu_admission_calls"] = shim.batches  # concurrent admissions share one stamp+verify+sync
     mine.update({"gpu": local_rank, "hbm_total": dev.total_bytes, "arena": arena})
     agent_stats = gather(mine)
-    node_agent_stats = None
+    node_agent_stats = plugin_stats = None
     if rank == 0 and a.agent == "node":
         na = next(c for c in children if c.name == "node-agent")
         st, body = E.BatchClient({"server": na.url}).run([("GET", "/v1/stats", b"")], 1)[0]
         node_agent_stats = json.loads(body) if st == 200 else {"error": st}
+        plugin_stats = _plugin_debug(E, (node_agent_stats or {}).get("plugin_debug"))
     extender_stats = None
     if rank == 0:
         ext1 = extender_counters()
@@ -852,13 +873,13 @@ def main():
             sweep, ref_client = latency_sweep(a, children, api_url, api_batch, runner, inspect_used)
         except Exception as e:  # noqa: BLE001 - the sweep never costs the headline line
             sweep = {"error": f"{type(e).__name__}: {e}"}
-        if a.agent == "node" and a.node_agent == "native":
+        if a.agent == "node" and a.node_agent == "native-plugin":
             try:
                 plugin_row = plugin_path(a, children, api_url, runner, E)
             except Exception as e:  # noqa: BLE001
                 plugin_row = {"error": f"{type(e).__name__}: {e}"}
             try:
-                plugin_row_native = plugin_path_native_kubelet(a, children, api_url, runner, E)
+                plugin_row_native = inprocess_matcher_path(a, children, api_url, runner, E)
             except Exception as e:  # noqa: BLE001
                 plugin_row_native = {"error": f"{type(e).__name__}: {e}"}
     if world > 1:
@@ -936,11 +957,16 @@ def main():
             "latency_sweep": sweep,
             "reference_client": ref_client,
             # the shipped gRPC device plugin on the kubelet path (untimed by the headline, same waves)
-            "device_plugin_path": plugin_row,
-            "device_plugin_path_native_kubelet": plugin_row_native,
+            # extra rows (untimed by the headline, same waves): the Python kubelet stand-in driving the shipped plugin
+            # process, and the compiled stand-in with the plugin's matcher linked in-process (no gRPC hop)
+            "device_plugin_path_python_kubelet": plugin_row,
+            "inprocess_matcher_path": plugin_row_native,
             "bind_retries": sum(sum(s["attempts"]) - len(s["attempts"]) for s in step_stats),
             "agents": agent_stats,
             "node_agent": node_agent_stats,
+            # the shipped plugin process behind the headline (native-plugin): fast-path share, early-answer commits,
+            # PodResources reconciliation (swaps) and moves through the extender
+            "plugin": plugin_stats,
             # the extender's native front end over the timed waves (bind-order waits, apiserver round trips)
             "extender": extender_stats,
             "apiserver": apiserver_stats,

@@ -61,6 +61,9 @@ def main(argv=None) -> int:
     ap.add_argument("--podresources-socket", default=env.get("GSX_PODRESOURCES_SOCKET",
                                                               "/var/lib/kubelet/pod-resources/kubelet.sock"),
                     help="kubelet's PodResources API; '' disables the reconciliation of Allocates")
+    ap.add_argument("--extender", default=env.get("GSX_EXTENDER_URL", ""),
+                    help="the scheduler extender's URL (its POST /gpushare-scheduler/move): reconciliation moves of "
+                         "allocation records go through it, the one writer of *_IDX; '' leaves records as they are")
     ap.add_argument("--reconcile-interval", type=float, default=float(env.get("GSX_RECONCILE_INTERVAL", "2")))
     ap.add_argument("--log-level", default=env.get("LOG_LEVEL", "info"))
     ap.add_argument("--log-dir", default=env.get("GSX_LOG_DIR", ""))
@@ -81,7 +84,7 @@ def main(argv=None) -> int:
                                 mount_mode=a.mount_mode, health_backend="amdsmi" if backend == "amdsmi" else None,
                                 health_interval=a.health_interval, reserve_bytes=int(a.reserve_gib * (1 << 30)),
                                 podresources_socket=a.podresources_socket or None,
-                                reconcile_interval=a.reconcile_interval, isolation=iso)
+                                reconcile_interval=a.reconcile_interval, isolation=iso, extender=a.extender or None)
         await plugin.start(publish=not a.no_publish, register=not a.no_register)
         if a.debug_port or a.debug_port_file:
             port = await plugin.serve_debug(a.debug_host, a.debug_port)

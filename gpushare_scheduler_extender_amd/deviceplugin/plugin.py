@@ -99,8 +99,12 @@ class GpuSharePlugin:
                  mount_mode: str = "isolated", health_backend: str | None = None, health_interval: float = 10.0,
                  reserve_bytes: int = 0, informer: Informer | None = None,
                  podresources_socket: str | None = None, reconcile_interval: float = 2.0,
-                 isolation: IsolationManager | None = None, checkpoint: str | None = None):
+                 isolation: IsolationManager | None = None, checkpoint: str | None = None,
+                 extender: str | None = None):
         self.client = client
+        # the scheduler extender: the one writer of *_IDX (reconciliation moves go through it, move_record)
+        self.extender_url = extender or os.environ.get("GSX_EXTENDER_URL") or None
+        self._ext = None
         self.node = node
         self.devices = {d.index: d for d in devices}
         self.profile = profile
@@ -698,7 +702,7 @@ class GpuSharePlugin:
         delay = 0.02
         while True:
             await self._reconcile_now(urgent=True)
-            rec = self.state.pods.get(rec.uid)
+            rec = self.state.fresh(self.state.pods.get(rec.uid))
             if rec is None or rec.assigned != "false" or not rec.pending or rec.uid in self.state.inflight:
                 return None
             if self._physical_used(rec.dev) + units <= self.units.get(rec.dev, 0):
@@ -736,20 +740,46 @@ class GpuSharePlugin:
         return best
 
     async def move_unstarted(self, rec: PodRec, dev: int) -> PodRec:
-        """Re-place a bound pod none of whose containers started onto GPU ``dev`` of this node: ``*_IDX`` = dev
-        with ``hold-idx`` = the old GPU (the ledger charges both), then the hold is cleared.  Raises ApiError."""
-        from ..models.profile import POD_HOLD_IDX_ANNOTATION  # noqa: PLC0415
-
-        body = {"metadata": {"resourceVersion": rec.rv, "annotations": {
-            self.profile.annotation_idx: str(dev), POD_HOLD_IDX_ANNOTATION: str(rec.dev)}}}
-        pod = await self.client.patch("pods", rec.name, body, rec.namespace)
-        self.state.observe(pod)
-        rec = self.state.pods.get(rec.uid, rec)
-        pod = await self.client.patch("pods", rec.name, {"metadata": {"resourceVersion": rec.rv, "annotations": {
-            POD_HOLD_IDX_ANNOTATION: None}}}, rec.namespace)
+        """Re-place a bound pod none of whose containers started onto GPU ``dev`` of this node, through the extender
+        (it checks the room against its ledger and charges both GPUs until its informer sees the move).  Raises
+        ApiError."""
+        pod = await self.move_record(rec, dev, {})
         self.state.observe(pod)
         self.stats["moved_before_start"] = self.stats.get("moved_before_start", 0) + 1
         return self.state.pods.get(rec.uid, rec)
+
+    async def move_record(self, rec: PodRec, to: int, annotations: dict, partner: str = "") -> dict:
+        """Rewrite ``rec``'s allocation record (``*_IDX`` = ``to`` and the given allocation annotations, ``None``
+        removing one) through the scheduler extender's ``POST /gpushare-scheduler/move``: the extender is the one
+        writer of ``*_IDX`` (the reference's node lock, ``pkg/cache/nodeinfo.go:139-168``), so a move can never race
+        a bind onto the same GPU.  The write is guarded by ``rec``'s resourceVersion; 409 when the extender refuses
+        it (no room, stale view) or the pod changed.  Returns the updated pod.  Raises ApiError."""
+        import json  # noqa: PLC0415
+
+        if not self.extender_url:
+            raise ApiError(409, "Conflict", "no scheduler extender configured (--extender / GSX_EXTENDER_URL): "
+                                            "allocation records are written by the extender only")
+        if self._ext is None:
+            from ..k8s.fasthttp import Client as HttpClient  # noqa: PLC0415
+
+            self._ext = HttpClient(self.extender_url)
+        body = {"namespace": rec.namespace, "name": rec.name, "uid": rec.uid, "node": self.node,
+                "resourceVersion": rec.rv, "from": rec.dev, "to": int(to), "partner": partner,
+                "annotations": annotations}
+        try:
+            r = await self._ext.request("POST", "/gpushare-scheduler/move", json.dumps(body).encode(),
+                                        content_type="application/json")
+        except OSError as e:
+            raise ApiError(503, "ServiceUnavailable", f"scheduler extender: {e}") from e
+        try:
+            out = json.loads(r.body or b"{}")
+        except ValueError:
+            out = {}
+        if r.status != 200:
+            self.stats["moves_refused"] = self.stats.get("moves_refused", 0) + 1
+            raise ApiError(r.status, "Conflict" if r.status == 409 else "", out.get("Error") or r.body[:200])
+        self.stats["moves"] = self.stats.get("moves", 0) + 1
+        return out["pod"]
 
     async def _wait_for_annotations(self, units: int, timeout: float = 10.0):
         """A pod of this size is bound to the node but carries no allocation record yet: the extender is writing
@@ -1088,6 +1118,9 @@ class GpuSharePlugin:
     async def stop(self):
         self._stopped = True
         self._changed.set()
+        if self._ext is not None:
+            await self._ext.close()
+            self._ext = None
         if self._persist_task is not None:
             self._persist_task.cancel()
         self._write_checkpoint()

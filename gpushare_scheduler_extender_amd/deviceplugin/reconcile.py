@@ -54,14 +54,23 @@ def fields(p: PodRec) -> dict:
     return {"idx": p.dev, "assigned": p.assigned, "cu_mask": p.cu_mask}
 
 
-def _drifted(p: PodRec, r: AllocRecord) -> bool:
+class _Held:
+    """What kubelet's container of a pod physically got (the plugin's physical account, keyed by kubelet's IDs)."""
+
+    __slots__ = ("uid", "dev", "cu_mask", "aid")
+
+    def __init__(self, uid: str, dev: int, cu_mask: str):
+        self.uid, self.dev, self.cu_mask, self.aid = uid, dev, cu_mask or "", ""
+
+
+def _drifted(p: PodRec, r) -> bool:
     """P's annotation names another GPU (or CU partition) than the allocation its container holds."""
     return p.dev != r.dev or (p.cu_mask or "") != (r.cu_mask or "")
 
 
 class Reconciler:
     def __init__(self, plugin, client: PodResourcesClient, interval: float = 2.0, after_allocate: float = 0.02,
-                 stale_after: float = 0.5, gone_after: float = 0.02):
+                 stale_after: float = 0.5, gone_after: float = 0.5):
         self.plugin = plugin
         self.pr = client
         self.interval = interval
@@ -103,8 +112,12 @@ class Reconciler:
             self.state.core.set_owners_reported(True)  # from now on kubelet's report decides who holds a record
             self.stats["list_ms_max"] = max(self.stats["list_ms_max"], 1e3 * (time.perf_counter() - t0))
             moves: list[tuple[str, str]] = []  # (P uid, record aid)
-            drifts: list[tuple[str, str]] = []  # P holds its own record, but its annotation names another GPU
+            # P's annotation names another GPU (or CU partition) than its container got: (P uid, what it got)
+            drifts: list[tuple[str, _Held]] = []
             seen = {tuple(ids) for per_container in truth.values() for ids in per_container}
+            # the physical account (what kubelet has handed out): an allocation kubelet no longer lists is free
+            # (never on a short grace: a kubelet slow to record an Allocate's IDs must not make them look free)
+            self.state.core.prune_held([list(i) for i in seen], t_list, self.stale_after)
             self._drop_stale(seen, 0.1 if urgent else self.stale_after, self.gone_after, t_list)
             for (ns, name), per_container in truth.items():
                 pod = self.state.pod_by_key(f"{ns}/{name}")
@@ -120,16 +133,21 @@ class Reconciler:
                     r = self.state.record_for_ids(ids)
                     if r is not None and r.t > t_list:
                         continue  # made after kubelet answered: the IDs were re-used since
+                    # what the container physically got: the physical account, which no exchange re-labels
+                    h = self.state.core.held_for(list(ids))
+                    got = _Held(pod.uid, int(h["dev"]), h["cu_mask"]) if h is not None and h["t"] <= t_list else None
                     if r is None:
                         self.stats["unknown_ids"] += 1
+                        if got is not None and _drifted(pod, got):
+                            drifts.append((pod.uid, got))  # its record went: the annotation is repaired all the same
                         continue
                     if r.owner != pod.uid:
                         self.state.set_owner(r.aid, pod.uid)
                         self.stats["records_owned"] += 1
                     if r.uid != pod.uid:
                         moves.append((pod.uid, r.aid))
-                    elif _drifted(pod, r):
-                        drifts.append((pod.uid, r.aid))
+                    elif _drifted(pod, got or r):
+                        drifts.append((pod.uid, got or _Held(pod.uid, r.dev, r.cu_mask)))
             done = 0
             started = {f"{ns}/{name}" for ns, name in truth}
             await self._finish_holds()
@@ -138,15 +156,16 @@ class Reconciler:
                 p = self.state.pods.get(p_uid)
                 if r is None or p is None or r.uid == p_uid:
                     continue  # resolved by an earlier exchange of this pass
-                if {p_uid, r.uid} & self.busy():
+                if {p_uid, r.uid} & self.busy() or p_uid in self.state.inflight or r.uid in self.state.inflight:
+                    # an interrupted exchange involves one of them, or an Allocate's ASSIGNED commit is still in
+                    # flight for one of them: finish that first (next pass)
                     self.stats["deferred"] += 1
-                    continue  # an interrupted exchange involves one of them: finish it first (next pass)
+                    continue
                 if await self._exchange(p, r, started):
                     done += 1
-            for p_uid, aid in drifts:
-                r = self.state.records.get(aid)
-                p = self.state.pods.get(p_uid)
-                if r is None or p is None or r.uid != p_uid or not _drifted(p, r) or {p_uid} & self.busy():
+            for p_uid, r in drifts:
+                p = self.state.fresh(self.state.pods.get(p_uid))
+                if p is None or not _drifted(p, r) or {p_uid} & self.busy() or p_uid in self.state.inflight:
                     continue
                 q = self._drift_partner(p, r, started)
                 log.warning("pod %s is annotated with GPU %d but its container runs on GPU %d: re-annotating%s",
@@ -203,10 +222,20 @@ class Reconciler:
                 orphans.discard(p.uid)
         self._orphan_since = {u: t for u, t in self._orphan_since.items() if u in orphans}
 
-    async def _patch(self, p: PodRec, ann: dict) -> bool:
-        body = {"metadata": {"resourceVersion": p.rv, "annotations": ann}}
+    async def _patch(self, p: PodRec, ann: dict, partner: str = "") -> bool:
+        """Write allocation fields of P, guarded by the resourceVersion this pass planned on.  Anything that touches
+        ``*_IDX`` or the hold goes through the extender (``POST /gpushare-scheduler/move``, the one writer of the
+        allocation record, which checks it against its ledger); ``partner``: the equal-size pod the write exchanges
+        P's record with (the write is sum-neutral per GPU).  The plugin's own ``ASSIGNED`` mark is patched directly."""
+        idx_key = self.plugin.profile.annotation_idx
         try:
-            pod = await self.plugin.client.patch("pods", p.name, body, p.namespace)
+            if idx_key in ann or POD_HOLD_IDX_ANNOTATION in ann:
+                ann = dict(ann)
+                to = int(ann.pop(idx_key, p.dev))
+                pod = await self.plugin.move_record(p, to, ann, partner=partner)
+            else:
+                pod = await self.plugin.client.patch("pods", p.name, {"metadata": {"resourceVersion": p.rv,
+                                                                                   "annotations": ann}}, p.namespace)
         except ApiError as e:
             if e.conflict or e.not_found:
                 self.stats["conflicts"] += 1
@@ -262,13 +291,13 @@ class Reconciler:
             ann[POD_HOLD_PARTNER_ANNOTATION] = json.dumps({"uid": q.uid, "key": q.key, **q_new}, separators=(",", ":"))
         log.warning("kubelet gave pod %s the allocation built for %s (GPU %d): exchanging their records",
                     p.key, q.key if q else r.uid, r.dev)
-        if not await self._patch(p, ann):  # step 1
+        if not await self._patch(p, ann, partner=q.uid if q is not None else ""):  # step 1
             return False
         if move:
             self.state.move_records(p.uid, q.uid if q is not None else r.uid, r)
             self.stats["swaps"] += 1
         if q is not None:
-            if await self._patch(self.state.pods.get(q.uid, q), self._ann(q_new)):  # step 2
+            if await self._patch(self.state.pods.get(q.uid, q), self._ann(q_new), partner=p.uid):  # step 2
                 if holding:
                     await self._clear_hold(self.state.pods.get(p.uid, p))  # step 3
             # on a conflict the hold stays; _finish_holds completes the move on a later pass
@@ -367,7 +396,7 @@ class Reconciler:
                 want = {}
             q = self.state.pods.get(want.get("uid", ""))
             if q is not None and fields(q) != {k: want.get(k) for k in ("idx", "assigned", "cu_mask")}:
-                if not await self._patch(q, self._ann(want)):
+                if not await self._patch(q, self._ann(want), partner=p.uid):
                     continue
             await self._clear_hold(self.state.pods.get(p.uid, p))
 

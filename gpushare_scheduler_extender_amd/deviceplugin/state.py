@@ -258,7 +258,20 @@ class AllocationState:
         else a later container of a pod whose first container was allocated, else the first container
         of a multi-container pod that has a container of that size."""
         uid, whole = self.core.match(int(units))
-        return (self._recs.get(uid), whole) if uid else (None, False)
+        return (self.fresh(self._recs.get(uid)), whole) if uid else (None, False)
+
+    def fresh(self, rec: PodRec | None) -> PodRec | None:
+        """``rec`` with the allocation fields the native state holds for it: the native pod feed may be ahead of the
+        Python informer's copy, and the matcher decided on the native one (an Allocate acting on a stale ASSIGNED
+        or GPU would take the wrong branch)."""
+        if rec is None:
+            return None
+        v = self.core.pod_view(rec.uid)
+        if v is None or not _older_rv(rec.rv, v["rv"]):
+            return rec
+        rec.rv, rec.phase, rec.dev, rec.assigned = v["rv"], v["phase"], int(v["dev"]), v["assigned"]
+        rec.cu_mask, rec.hold_idx, rec.hold_partner = v["cu_mask"], int(v["hold_idx"]), v["hold_partner"]
+        return rec
 
     def unannotated(self, units: int) -> bool:
         """A pending pod of this size bound to the node without any allocation annotation (``*_IDX``)."""

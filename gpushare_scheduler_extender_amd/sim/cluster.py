@@ -149,7 +149,7 @@ NODEAGENT = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "gsx-nodeagen
 def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", workers: int = 32,
                      native: bool = True, plugin: str = "grpc", cpus: list[int] | None = None,
                      extra: list[str] | None = None, plugin_cpus: list[int] | None = None,
-                     serial_admission: bool = False) -> ChildProc:
+                     serial_admission: bool = False, extender: str | None = None) -> ChildProc:
     """kubelet + device-plugin Allocate + runtime stand-in for ``node``.
 
     ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent, the plugin's native matcher in-process, or
@@ -160,8 +160,13 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
     does (with ``plugin="spawn"`` it always does).
     ``plugin_cpus``: CPUs of the plugin process the agent starts (as a DaemonSet pod has its own, instead of
     sharing the kubelet stand-in's), through ``GSX_PLUGIN_CPUS``.
+    ``extender``: the scheduler extender's URL, handed to the device plugin (``GSX_EXTENDER_URL``): its
+    reconciliation moves allocation records through the extender, the one writer of ``*_IDX``.
     """
-    env = {"GSX_PLUGIN_CPUS": ",".join(map(str, plugin_cpus))} if plugin_cpus else None
+    env = {"GSX_PLUGIN_CPUS": ",".join(map(str, plugin_cpus))} if plugin_cpus else {}
+    if extender:
+        env["GSX_EXTENDER_URL"] = extender
+    env = env or None
     if native:
         exe = tool_path("gsx-nodeagent")
         if not exe.exists():
@@ -170,7 +175,8 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
         if serial_admission:
             spawn.append("--serial-admission")
         return ChildProc([str(exe), "--node", node, "--apiserver", apiserver, "--profile", profile,
-                          "--workers", str(min(workers, 16)), *spawn], "node-agent", cpus=cpus, env=env)
+                          "--workers", str(min(workers, 16)), *spawn, *(extra or [])], "node-agent", cpus=cpus,
+                         env=env)
     return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
                       apiserver, "--profile", profile, "--workers", str(workers), "--plugin", plugin,
                       *(extra or [])], "node-agent", cpus=cpus, env=env)

@@ -157,8 +157,12 @@ class Cluster:
     def _agent(self):
         kind = self.agent_kind
         plugin = {"inproc": "inproc", "native-plugin": "spawn"}.get(kind, "grpc")
-        return start_node_agent(self.api.url, NODE, profile=self.profile.name, native=kind.startswith("native"),
-                                plugin=plugin, extra=self.agent_args, serial_admission=kind == "native-serial")
+        native = kind.startswith("native")
+        # the compiled stand-in is kubelet-faithful in plugin mode by construction: it takes no --faithful
+        extra = [x for x in self.agent_args if x != "--faithful"] if native else self.agent_args
+        return start_node_agent(self.api.url, NODE, profile=self.profile.name, native=native,
+                                plugin=plugin, extra=extra, serial_admission=kind == "native-serial",
+                                extender=self.ext.url)
 
     def agent_child(self):
         return next(ch for ch in self.children if ch.name == "node-agent")

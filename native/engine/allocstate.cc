@@ -4,6 +4,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <set>
 #include <stdexcept>
 #include <tuple>
 
@@ -301,6 +302,13 @@ void AllocState::release(const std::string& uid) {
     if (r.owner == uid || (r.owner.empty() && r.uid == uid && !owners_reported_)) gone.push_back(kv.first);
   }
   for (const auto& aid : gone) drop_record(aid);
+  if (!owners_reported_) {
+    // nobody reports what kubelet holds: an allocation is taken to end with the pod it was built for
+    for (auto h = held_.begin(); h != held_.end();) {
+      auto cur = h++;
+      if (cur->second.uid == uid) unhold(cur);
+    }
+  }
 }
 
 std::vector<std::string> AllocState::holders() const {
@@ -436,9 +444,7 @@ AllocRecord& AllocState::record(const std::string& uid, const std::vector<std::s
   r.cu_mask = cu_mask;
   r.t = t;
   if (!ids.empty()) by_ids_[ids] = aid;
-  auto prev = records_.find(aid);
-  if (prev != records_.end()) count_record(prev->second, -1);
-  count_record(r, +1);
+  if (!ids.empty()) hold(ids, Held{r.dev, units, t, uid, false, cu_mask});
   auto res = records_.insert_or_assign(aid, std::move(r));
   return res.first->second;
 }
@@ -447,19 +453,28 @@ void AllocState::add_record(AllocRecord r) {
   std::sort(r.ids.begin(), r.ids.end());
   if (!r.ids.empty()) by_ids_[r.ids] = r.aid;
   std::string aid = r.aid;
-  auto prev = records_.find(aid);
-  if (prev != records_.end()) count_record(prev->second, -1);
-  count_record(r, +1);
+  // a restored record: its allocation is held until kubelet's report says otherwise
+  if (!r.ids.empty() && !held_.count(r.ids)) hold(r.ids, Held{r.dev, r.units, r.t, r.uid, r.on_gpu, r.cu_mask});
   records_.insert_or_assign(aid, std::move(r));
 }
 
-void AllocState::count_record(const AllocRecord& r, int sign) {
-  if (r.dev >= 0) {
-    int64_t& u = phys_[r.dev];
-    u += sign * r.units;
-    if (u == 0) phys_.erase(r.dev);
+void AllocState::hold(const std::vector<std::string>& ids, Held h) {
+  auto prev = held_.find(ids);
+  if (prev != held_.end()) unhold(prev);  // kubelet re-used the IDs of a finished container
+  if (h.dev >= 0) phys_[h.dev] += h.units;
+  if (!h.on_gpu) off_gpu_++;
+  held_.emplace(ids, std::move(h));
+}
+
+void AllocState::unhold(std::map<std::vector<std::string>, Held>::iterator it) {
+  const Held& h = it->second;
+  if (h.dev >= 0) {
+    int64_t& u = phys_[h.dev];
+    u -= h.units;
+    if (u == 0) phys_.erase(h.dev);
   }
-  if (!r.on_gpu) off_gpu_ = sign > 0 ? off_gpu_ + 1 : off_gpu_ - 1;
+  if (!h.on_gpu) off_gpu_--;
+  held_.erase(it);
 }
 
 int64_t AllocState::physical_used(int64_t dev) const {
@@ -469,16 +484,50 @@ int64_t AllocState::physical_used(int64_t dev) const {
 
 void AllocState::mark_on_gpu(const std::string& aid, bool on) {
   auto it = records_.find(aid);
-  if (it == records_.end() || it->second.on_gpu == on) return;
-  count_record(it->second, -1);
+  if (it == records_.end()) return;
   it->second.on_gpu = on;
-  count_record(it->second, +1);
+  auto h = held_.find(it->second.ids);
+  if (h == held_.end() || h->second.on_gpu == on) return;
+  h->second.on_gpu = on;
+  if (on) {
+    off_gpu_--;
+  } else {
+    off_gpu_++;
+  }
+}
+
+bool AllocState::held_for(std::vector<std::string> ids, int64_t* dev, int64_t* units, double* t,
+                          std::string* cu_mask) const {
+  std::sort(ids.begin(), ids.end());
+  auto it = held_.find(ids);
+  if (it == held_.end()) return false;
+  *dev = it->second.dev;
+  *units = it->second.units;
+  *t = it->second.t;
+  *cu_mask = it->second.cu_mask;
+  return true;
+}
+
+size_t AllocState::prune_held(const std::vector<std::vector<std::string>>& listed_in, double asked, double grace) {
+  std::set<std::vector<std::string>> listed;
+  for (auto ids : listed_in) {
+    std::sort(ids.begin(), ids.end());
+    listed.insert(std::move(ids));
+  }
+  size_t n = 0;
+  for (auto it = held_.begin(); it != held_.end();) {
+    auto cur = it++;
+    if (!listed.count(cur->first) && asked - cur->second.t > grace) {
+      unhold(cur);
+      n++;
+    }
+  }
+  return n;
 }
 
 bool AllocState::drop_record(const std::string& aid) {
   auto it = records_.find(aid);
   if (it == records_.end()) return false;
-  count_record(it->second, -1);
   auto b = by_ids_.find(it->second.ids);
   if (b != by_ids_.end() && b->second == aid) by_ids_.erase(b);
   stats_.records_dropped++;

@@ -154,10 +154,20 @@ class AllocState {
   // describes P, whatever described P describes Q, and the CU partitions follow.
   void move_records(const std::string& p_uid, const std::string& q_uid, const std::string& aid);
   const std::map<std::string, AllocRecord>& records() const { return records_; }
-  // Units the records put on `dev` (what kubelet has handed out there, whoever holds it): kept incrementally
+  // ---- what kubelet has handed out (the physical account)
+  // One entry per Allocate answered, keyed by kubelet's device IDs: the GPU the container was given and its units.
+  // Kept apart from the records' reconciliation bookkeeping (exchanges re-label records; pods come and go): an
+  // entry leaves only when kubelet no longer reports its IDs (prune_held), or -- with nobody reporting -- with the
+  // pod it was built for.  physical_used() is what really runs on a GPU, whatever the annotations say.
   int64_t physical_used(int64_t dev) const;
   void mark_on_gpu(const std::string& aid, bool on);
-  size_t off_gpu_records() const { return off_gpu_; }
+  size_t off_gpu_records() const { return off_gpu_; }  // entries whose IDs do not all lie on their GPU
+  // kubelet's PodResources answer, requested at `asked` (wall seconds): entries made more than `grace` before it whose
+  // IDs it does not list are gone (their containers stopped).  Returns how many left.
+  size_t prune_held(const std::vector<std::vector<std::string>>& listed, double asked, double grace);
+  size_t held_count() const { return held_.size(); }
+  // what was handed out with these IDs: false if nothing this plugin knows of
+  bool held_for(std::vector<std::string> ids, int64_t* dev, int64_t* units, double* t, std::string* cu_mask) const;
   std::vector<AllocRecord> take_dropped();  // records dropped since the last call (isolation cleanup)
   bool dropped_pending() const { return !dropped_.empty(); }
 
@@ -181,9 +191,19 @@ class AllocState {
   std::map<std::string, AllocRecord> records_;            // aid -> record
   std::map<std::vector<std::string>, std::string> by_ids_;
   std::vector<AllocRecord> dropped_;
-  std::unordered_map<int64_t, int64_t> phys_;  // dev -> sum of record units (records_ kept in step)
-  size_t off_gpu_ = 0;                          // records with on_gpu == false
-  void count_record(const AllocRecord& r, int sign);
+  struct Held {
+    int64_t dev = -1, units = 0;
+    double t = 0;
+    std::string uid;  // the pod the allocation was built for (pruned with it when nobody reports owners)
+    bool on_gpu = false;
+    std::string cu_mask;  // the CU partition handed out with it
+  };
+
+  std::map<std::vector<std::string>, Held> held_;  // sorted kubelet IDs -> what was handed out with them
+  std::unordered_map<int64_t, int64_t> phys_;     // dev -> sum of held_ units (kept in step)
+  size_t off_gpu_ = 0;                             // held_ entries with on_gpu == false
+  void hold(const std::vector<std::string>& ids, Held h);
+  void unhold(std::map<std::vector<std::string>, Held>::iterator it);
   bool owners_reported_ = false;
   AllocStats stats_;
 };

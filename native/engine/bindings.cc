@@ -315,6 +315,9 @@ class Engine {
     d["expired"] = s.expired;
     d["expiry_deferred"] = s.expiry_deferred;
     d["annotations_missing"] = s.annotations_missing;
+    d["moves_ok"] = s.moves_ok;
+    d["moves_refused"] = s.moves_refused;
+    d["moves_failed"] = s.moves_failed;
     d["overcommit_events"] = s.overcommit_events;
     d["pod_upserts"] = s.pod_upserts;
     d["pod_removes"] = s.pod_removes;
@@ -449,6 +452,8 @@ class Engine {
     d["connections"] = s.connections.load();
     d["api_calls"] = s.api_calls.load();
     d["conflicts_retried"] = s.conflicts_retried.load();
+    d["moves"] = s.moves.load();
+    d["moves_failed"] = s.moves_failed.load();
     auto hist = [](const LatencyHist& h) {
       py::dict o;
       py::list bounds, counts;
@@ -929,6 +934,7 @@ class PyDpServer {
     d["slow_allocate"] = s.slow_allocate;
     d["slow_preferred"] = s.slow_preferred;
     d["patch_failures"] = s.patch_failures;
+    d["guard_by_ids"] = s.guard_by_ids;
     d["calls"] = srv_ ? srv_->calls() : 0;
     d["connections"] = srv_ ? srv_->connections() : 0;
     d["fast"] = fast_;
@@ -1526,6 +1532,20 @@ PYBIND11_MODULE(_engine, m) {
       }, py::call_guard<AllocLock>())
       .def("holders", &AllocState::holders, py::call_guard<AllocLock>())
       .def("has_pod", [](const AllocState& s, const std::string& uid) { return s.pod(uid) != nullptr; }, py::call_guard<AllocLock>())
+      // the native state's view of a pod (the one the matcher decided on): the fields an Allocate acts on
+      .def("pod_view", [](const AllocState& s, const std::string& uid) -> py::object {
+             const AllocPod* p = s.pod(uid);
+             if (!p) return py::none();
+             py::dict d;
+             d["rv"] = p->rv;
+             d["phase"] = p->phase;
+             d["dev"] = p->dev;
+             d["assigned"] = p->assigned;
+             d["cu_mask"] = p->cu_mask;
+             d["hold_idx"] = p->hold_idx;
+             d["hold_partner"] = p->hold_partner;
+             return d;
+           }, py::call_guard<AllocLock>())
       .def("pod_uids", [](const AllocState& s) {
         std::vector<std::string> out;
         for (const auto& kv : s.pods()) out.push_back(kv.first);
@@ -1585,6 +1605,21 @@ PYBIND11_MODULE(_engine, m) {
       .def("mark_on_gpu", &AllocState::mark_on_gpu, py::call_guard<AllocLock>())
       .def("physical_used", &AllocState::physical_used, py::call_guard<AllocLock>())
       .def("off_gpu_records", &AllocState::off_gpu_records, py::call_guard<AllocLock>())
+      .def("prune_held", &AllocState::prune_held, py::arg("listed"), py::arg("asked"), py::arg("grace"),
+           py::call_guard<AllocLock>())
+      .def("held_count", &AllocState::held_count, py::call_guard<AllocLock>())
+      .def("held_for", [](const AllocState& s, const std::vector<std::string>& ids) -> py::object {
+             int64_t dev = -1, units = 0;
+             double t = 0;
+             std::string cu;
+             if (!s.held_for(ids, &dev, &units, &t, &cu)) return py::none();
+             py::dict d;
+             d["dev"] = dev;
+             d["units"] = units;
+             d["t"] = t;
+             d["cu_mask"] = cu;
+             return d;
+           }, py::call_guard<AllocLock>())
       .def("record_for_ids", [rec_dict](const AllocState& s, const std::vector<std::string>& ids) -> py::object {
              const AllocRecord* r = s.record_for_ids(ids);
              return r ? py::object(rec_dict(*r)) : py::object(py::none());

@@ -315,6 +315,7 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   const int64_t units = static_cast<int64_t>(ids.size());
   auto m = state_->match(units);
   const double tm = mono_s();
+
   if (!m.first) {
     stats_.slow_allocate++;
     *why = "no candidate";
@@ -334,6 +335,8 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   // accounting bounds what runs on that GPU (it holds exactly `units` IDs of it), whatever the records of pods
   // it has since freed still say.  Otherwise the records decide (the Python guard repairs and waits).
   const bool on_gpu = ids_on(ids, dev.index);
+
+
   if (!later && cfg_.guard && physical_used(dev.index) + units > dev.units) {
     if (!on_gpu || state_->off_gpu_records() != 0) {
       stats_.slow_allocate++;

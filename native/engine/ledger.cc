@@ -21,6 +21,11 @@ void Ledger::account(PodRec& r) {
   // a pod being moved between devices is charged on both until the move completes: never under-counted
   r.held_on = (r.hold >= 0 && r.hold != r.dev && r.hold < static_cast<int64_t>(n.devs.size())) ? r.hold : -1;
   if (r.held_on >= 0) n.devs[static_cast<size_t>(r.held_on)].used += r.mem;
+  r.moved_on = (r.move_to >= 0 && r.move_to != r.dev && r.move_to != r.held_on &&
+                r.move_to < static_cast<int64_t>(n.devs.size()))
+                   ? r.move_to
+                   : -1;
+  if (r.moved_on >= 0) n.devs[static_cast<size_t>(r.moved_on)].used += r.mem;
   r.accounted = true;
 }
 
@@ -36,6 +41,10 @@ void Ledger::unaccount(PodRec& r) {
   d.npods -= 1;
   if (r.held_on >= 0 && r.held_on < static_cast<int64_t>(n.devs.size())) n.devs[static_cast<size_t>(r.held_on)].used -= r.mem;
   r.held_on = -1;
+  if (r.moved_on >= 0 && r.moved_on < static_cast<int64_t>(n.devs.size())) {
+    n.devs[static_cast<size_t>(r.moved_on)].used -= r.mem;
+  }
+  r.moved_on = -1;
 }
 
 void Ledger::rebuild(NodeState& n) {
@@ -134,6 +143,7 @@ int Ledger::upsert_pod(const PodView& v) {
       r.dev = v.dev_idx;
       r.mem = v.annot_mem;
       r.hold = v.hold_idx;
+      if (r.move_to >= 0 && r.dev == r.move_to) r.move_to = -1;  // the move is confirmed
       r.assumed = false;  // observed with annotations: reservation confirmed
       r.unannotated = false;
     } else if (!r.assumed) {
@@ -370,6 +380,79 @@ void Ledger::finish_bind(const std::string& uid, bool ok, double ttl_s) {
   if (it->second.unannotated) queue_repair(it->second);  // the watch event raced the binding's response
 }
 
+int Ledger::begin_move(MoveRequest* m, std::string* why) {
+  auto pit = pods_.find(m->uid);
+  if (pit == pods_.end() || pit->second.node != m->node || pit->second.terminal || pit->second.dev < 0) {
+    *why = "pod " + m->uid + " is not bound to node " + m->node + " in the extender's ledger";
+    stats_.moves_refused++;
+    return 1;
+  }
+  PodRec& r = pit->second;
+  if ((r.assumed && !r.bound) || r.move_to >= 0) {
+    *why = "a bind or another move of the pod is in flight";
+    stats_.moves_refused++;
+    return 4;
+  }
+  if (r.dev != m->from) {
+    *why = "stale: the ledger has the pod on GPU " + std::to_string(r.dev) + ", not " + std::to_string(m->from);
+    stats_.moves_refused++;
+    return 2;
+  }
+  NodeState& n = nodes_.at(r.node);
+  const int64_t ndev = static_cast<int64_t>(n.devs.size());
+  if (m->to < 0) {  // best fit among the other devices (nodeinfo.go:209-252)
+    int64_t best = -1, best_free = 0;
+    for (int64_t i = 0; i < ndev; ++i) {
+      const int64_t free = n.devs[static_cast<size_t>(i)].total - n.devs[static_cast<size_t>(i)].used;
+      if (i != m->from && free >= r.mem && (best < 0 || free < best_free)) {
+        best = i;
+        best_free = free;
+      }
+    }
+    m->to = best;
+  }
+  if (m->to < 0 || m->to >= ndev) {
+    *why = "no GPU of node " + m->node + " has room for " + std::to_string(r.mem);
+    stats_.moves_refused++;
+    return 3;
+  }
+  if (m->to != r.dev) {
+    bool neutral = false;
+    if (!m->partner.empty() && m->partner != m->uid) {
+      auto q = pods_.find(m->partner);
+      neutral = q != pods_.end() && q->second.node == r.node && q->second.mem == r.mem &&
+                (q->second.dev == m->to || q->second.hold == m->to);
+    }
+    const DevState& d = n.devs[static_cast<size_t>(m->to)];
+    if (!neutral && d.total - d.used < r.mem) {
+      *why = "GPU " + std::to_string(m->to) + " of node " + m->node + " has " + std::to_string(d.total - d.used) +
+             " free, the pod needs " + std::to_string(r.mem);
+      stats_.moves_refused++;
+      return 3;
+    }
+    unaccount(r);
+    r.move_to = m->to;
+    r.move_at = now_s();
+    account(r);
+  }
+  return 0;
+}
+
+void Ledger::end_move(const std::string& uid, bool ok) {
+  auto pit = pods_.find(uid);
+  if (pit == pods_.end()) return;
+  PodRec& r = pit->second;
+  if (ok) {
+    stats_.moves_ok++;
+    return;  // the target stays charged until the informer shows the pod there
+  }
+  stats_.moves_failed++;
+  if (r.move_to < 0) return;
+  unaccount(r);
+  r.move_to = -1;
+  account(r);
+}
+
 void Ledger::queue_repair(PodRec& r) {
   if (!r.bound || r.repair_queued || r.dev < 0) return;
   r.repair_queued = true;
@@ -399,6 +482,15 @@ int Ledger::gc(double confirmed_list_start, bool* need_relist) {
   double now = now_s();
   int n = 0;
   bool relist = false;
+  for (auto& kv : pods_) {
+    // a move the informer never confirmed (the pod's record was rewritten again since): its target charge goes
+    PodRec& r = kv.second;
+    if (r.move_to >= 0 && now - r.move_at > 30.0) {
+      unaccount(r);
+      r.move_to = -1;
+      account(r);
+    }
+  }
   for (auto it = pods_.begin(); it != pods_.end();) {
     const PodRec& r = it->second;
     bool expire = false;

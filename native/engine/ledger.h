@@ -57,6 +57,20 @@ struct PodRec {
   int64_t assume_ns = 0;      // ASSUME_TIME written by our bind
   bool unannotated = false;   // observed bound to its node WITHOUT the allocation annotations we sent
   bool repair_queued = false;
+  // a device-plugin move in flight (begin_move): the target device is charged too until the informer shows the
+  // pod there (or the move fails), so nothing else is placed into the room it takes
+  int64_t move_to = -1;
+  int64_t moved_on = -1;  // the move target actually charged by account()
+  double move_at = 0;
+};
+
+// POST /gpushare-scheduler/move: the device plugin asks the extender -- the one writer of *_IDX -- to rewrite a
+// bound pod's allocation record (a reconciliation exchange step, a hold release, a move off a physically full GPU).
+struct MoveRequest {
+  std::string uid, node;
+  int64_t from = -1;       // the device the caller's view has the pod on (the ledger must agree)
+  int64_t to = -1;         // the new *_IDX (-1: best fit with room, other than `from`)
+  std::string partner;     // an equal-size exchange partner on `to` (or holding `to`): the move is sum-neutral
 };
 
 // A pod this extender bound whose allocation annotations the apiserver did not keep (an apiserver or
@@ -90,6 +104,7 @@ struct Stats {
   uint64_t expired = 0, overcommit_events = 0, pod_upserts = 0, pod_removes = 0;
   uint64_t expiry_deferred = 0;  // GC passes that kept an overdue reservation until a LIST could confirm it
   uint64_t annotations_missing = 0;  // binds observed bound without the annotations they carried
+  uint64_t moves_ok = 0, moves_refused = 0, moves_failed = 0;  // device-plugin allocation-record writes
 };
 
 class Ledger {
@@ -138,6 +153,12 @@ class Ledger {
   int64_t assume(const std::string& uid, const std::string& ns, const std::string& name,
                  const std::string& node, int64_t req, int64_t* dev_total);
   void finish_bind(const std::string& uid, bool ok, double ttl_s);
+  // Validate a move and reserve its target: 0 ok (*to resolved; the pod is charged on both devices until the
+  // informer confirms it on the target, or end_move(false)); 1 the pod is not bound to that node here; 2 stale (the
+  // ledger has it on another device); 3 no room on the target (and no equal-size partner makes the move
+  // sum-neutral); 4 a bind or another move of the pod is in flight.
+  int begin_move(MoveRequest* m, std::string* why);
+  void end_move(const std::string& uid, bool ok);
 
   // ---- bind ordering, shared by the native front end and the Python slow path ----
   // kubelet admits a node's pods in the order their bindings land, and the device plugin gives a request

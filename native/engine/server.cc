@@ -452,6 +452,12 @@ void NativeServer::dispatch(Loop* lp, Conn* c, http::Message& req) {
     submit(Job{lp, c->id, 0, std::move(req), t0});
     return;
   }
+  if (req.method == "POST" && path == pre + "/move") {
+    stats_.moves.fetch_add(1, std::memory_order_relaxed);
+    c->busy = true;
+    submit(Job{lp, c->id, 2, std::move(req), t0});
+    return;
+  }
   if (req.method == "GET" && (path == pre + "/inspect" || path == pre + "/inspect/" ||
                               path.substr(0, pre.size() + 9) == pre + "/inspect/")) {
     std::string node;
@@ -506,6 +512,8 @@ void NativeServer::pool_main() {
           resp = do_proxy(j.req);
         }
         stats_.bind_lat.observe(mono() - j.t0);
+      } else if (j.kind == 2) {
+        resp = do_move(j.req);
       } else {
         resp = do_proxy(j.req);
       }
@@ -714,6 +722,93 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
   }
   stats_.bind_ok.fetch_add(1, std::memory_order_relaxed);
   return http::response(200, "application/json", "{\"Error\":\"\"}", true);
+}
+
+// The device plugin's allocation-record writes (deviceplugin/reconcile.py, plugin.py move_unstarted): the extender
+// is the one writer of *_IDX, as the reference's node lock made it (pkg/cache/nodeinfo.go:139-168).  Under the
+// ledger mutex the move is checked against the ledger (the pod is where the caller thinks; the target has room,
+// counting in-flight binds and other moves, unless an equal-size partner makes it an exchange) and the target is
+// reserved; then one merge patch, guarded by the caller's resourceVersion, writes *_IDX with the other allocation
+// fields the caller sends (ASSIGNED, cu-mask, hold-idx / hold-partner, reconciled).  409 on any refusal or
+// conflict: the caller re-plans from fresh state.
+//
+//   {"namespace","name","uid","node","resourceVersion","from","to","partner","annotations":{k: "v" | null}}
+//   -> 200 {"Error":"","to":N,"pod":{...}} | 409 {"Error":"..."} | 4xx/5xx {"Error":"..."}
+std::string NativeServer::do_move(const http::Message& req) {
+  auto answer = [](int status, const std::string& body) { return http::response(status, "application/json", body, true); };
+  if (!binds_enabled_.load()) return answer(503, error_body("this extender replica is not the leader"));
+  if (!api_) return answer(501, error_body("no apiserver client"));
+  json::Doc d;
+  std::string perr;
+  if (!d.parse(req.body, &perr) || d.at(0).type != json::T::Object) return answer(400, error_body("bad move request: " + perr));
+  std::string ns, name, uid, node, rv, partner;
+  if (!arg_str(d, "namespace", &ns) || !arg_str(d, "name", &name) || !arg_str(d, "uid", &uid) ||
+      !arg_str(d, "node", &node) || !arg_str(d, "resourceVersion", &rv) || !arg_str(d, "partner", &partner) ||
+      ns.empty() || name.empty() || uid.empty() || node.empty() || rv.empty()) {
+    return answer(400, error_body("move needs namespace, name, uid, node and resourceVersion"));
+  }
+  MoveRequest m;
+  m.uid = uid;
+  m.node = node;
+  m.partner = partner;
+  int64_t v;
+  int64_t fi = d.find(0, "from");
+  int64_t ti = d.find(0, "to");
+  if (fi < 0 || !d.as_int(static_cast<uint32_t>(fi), &m.from)) return answer(400, error_body("move needs from"));
+  if (ti >= 0 && d.as_int(static_cast<uint32_t>(ti), &v)) m.to = v;
+  // the other allocation fields, copied as given (string values, or null to remove an annotation)
+  const Profile& prof = l_->profile();
+  std::string extra;
+  int64_t ai = d.find(0, "annotations");
+  if (ai >= 0 && d.at(static_cast<uint32_t>(ai)).type == json::T::Object) {
+    const uint32_t obj = static_cast<uint32_t>(ai);
+    for (uint32_t k = obj + 1; k < d.at(obj).skip;) {
+      const uint32_t val = k + 1;
+      const json::T t = d.at(val).type;
+      const std::string key = d.str(k);
+      if (key == prof.a_idx || key == prof.a_pod || key == prof.a_dev) {
+        return answer(400, error_body("the move request names the pod's GPU in from / to, and its share is fixed"));
+      }
+      if (t != json::T::String && t != json::T::Null) return answer(400, error_body("annotation values are strings or null"));
+      extra.push_back(',');
+      json::append_quoted(&extra, key);
+      extra.push_back(':');
+      extra.append(d.raw(val));
+      k = d.next(val);
+    }
+  }
+  std::string why;
+  int rc;
+  {
+    std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
+    rc = l_->begin_move(&m, &why);
+  }
+  if (rc != 0) return answer(rc == 1 ? 404 : 409, error_body(why));
+  std::string patch = "{\"metadata\":{\"resourceVersion\":";
+  json::append_quoted(&patch, rv);
+  patch.append(",\"annotations\":{");
+  json::append_quoted(&patch, prof.a_idx);
+  patch.append(":\"").append(std::to_string(m.to)).append("\"").append(extra).append("}}}");
+  const std::string target = "/api/v1/namespaces/" + url_escape_path(ns) + "/pods/" + url_escape_path(name);
+  int status = 0;
+  std::string body, err;
+  double t0 = mono();
+  stats_.api_calls.fetch_add(1, std::memory_order_relaxed);
+  const bool sent = api_->request("PATCH", target, patch, "application/merge-patch+json", &status, &body, &err);
+  stats_.api_lat.observe(mono() - t0);
+  const bool ok = sent && status >= 200 && status < 300;
+  {
+    std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
+    l_->end_move(uid, ok);
+  }
+  if (!ok) {
+    stats_.moves_failed.fetch_add(1, std::memory_order_relaxed);
+    if (!sent) return answer(502, error_body("apiserver: " + err));
+    return answer(status == 409 ? 409 : (status >= 500 ? 502 : status), error_body(status_message(body, status)));
+  }
+  std::string out = "{\"Error\":\"\",\"to\":" + std::to_string(m.to) + ",\"pod\":";
+  out.append(body).push_back('}');
+  return answer(200, out);
 }
 
 }  // namespace gsx

@@ -74,7 +74,7 @@ struct LatencyHist {
 
 struct ServerStats {
   std::atomic<uint64_t> requests{0}, filters{0}, binds{0}, bind_ok{0}, bind_fail{0}, proxied{0}, bad_requests{0},
-      inspects{0}, connections{0}, api_calls{0}, conflicts_retried{0}, bind_order_waits{0};
+      inspects{0}, connections{0}, api_calls{0}, conflicts_retried{0}, bind_order_waits{0}, moves{0}, moves_failed{0};
   LatencyHist filter_lat, bind_lat, api_lat;
 };
 
@@ -101,7 +101,7 @@ class NativeServer {
   struct Job {
     Loop* loop;
     uint64_t conn_id;
-    int kind;  // 0 bind, 1 proxy
+    int kind;  // 0 bind, 1 proxy, 2 move
     http::Message req;
     double t0;
   };
@@ -120,6 +120,7 @@ class NativeServer {
   void submit(Job j);
   std::string do_bind(const http::Message& req, bool* fallback);
   std::string do_proxy(const http::Message& req);
+  std::string do_move(const http::Message& req);
   std::string bind_error_response(const std::string& msg) const;
   void record_failure(BindFailure f);
 

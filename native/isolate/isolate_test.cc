@@ -57,7 +57,9 @@ static hsa_status_t fake_pool_get_info(hsa_amd_memory_pool_t p, hsa_amd_memory_p
   }
   return HSA_STATUS_SUCCESS;
 }
+static bool g_slow_alloc = false;  // widen the window between the share check and the allocation's record
 static hsa_status_t fake_pool_allocate(hsa_amd_memory_pool_t, size_t size, uint32_t, void** ptr) {
+  if (g_slow_alloc) usleep(100000);
   *ptr = std::malloc(16);  // a unique address stands in for the device allocation
   return *ptr ? HSA_STATUS_SUCCESS : HSA_STATUS_ERROR_OUT_OF_RESOURCES;
 }
@@ -208,6 +210,37 @@ int main(int argc, char** argv) {
   stats(sv);
   CHECK(sv[3] == 0);
   amd.hsa_amd_memory_pool_free_fn(big);
+
+  // ---- two processes of the pod allocate at once: the check and the reservation are one step under
+  // the ledger lock, so of two 60 GiB allocations against the 100 GiB share exactly one succeeds, however slow
+  // the runtime's allocation between the check and its record
+  g_slow_alloc = true;
+  int go[2], res[2];
+  CHECK(pipe(go) == 0 && pipe(res) == 0);
+  pid_t kids[2];
+  for (int k = 0; k < 2; ++k) {
+    kids[k] = fork();
+    if (kids[k] == 0) {
+      char c;
+      if (read(go[0], &c, 1) != 1) _exit(9);
+      void* x = nullptr;
+      char ok = alloc(GPU_POOL, 60, &x) == HSA_STATUS_SUCCESS ? '1' : '0';
+      if (write(res[1], &ok, 1) != 1) _exit(9);
+      if (read(go[0], &c, 1) != 1) _exit(9);  // hold the allocation until both answered
+      _exit(0);
+    }
+  }
+  CHECK(write(go[1], "gg", 2) == 2);
+  int granted = 0;
+  for (int k = 0; k < 2; ++k) {
+    char c = 0;
+    CHECK(read(res[0], &c, 1) == 1);
+    granted += c == '1';
+  }
+  CHECK(write(go[1], "gg", 2) == 2);
+  for (int k = 0; k < 2; ++k) waitpid(kids[k], &st, 0);
+  CHECK(granted == 1);
+  g_slow_alloc = false;
   if (g_fail == 0) std::printf("isolate_test: OK\n");
   return g_fail ? 1 : 0;
 }

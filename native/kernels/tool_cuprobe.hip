@@ -47,8 +47,11 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[i], "--blocks") && i + 1 < argc) blocks = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--spin") && i + 1 < argc) spin = std::atoi(argv[++i]);
     else if (!std::strcmp(argv[i], "--list")) list = true;
+    // a program that drops a variable before its first HIP call (tests of the isolation library's hsa_init)
+    else if (!std::strcmp(argv[i], "--unsetenv") && i + 1 < argc) unsetenv(argv[++i]);
     else {
-      std::fprintf(stderr, "usage: %s [--device N] [--mask LIST] [--blocks N] [--spin N] [--list]\n", argv[0]);
+      std::fprintf(stderr, "usage: %s [--device N] [--mask LIST] [--blocks N] [--spin N] [--list] [--unsetenv NAME]\n",
+                   argv[0]);
       return 2;
     }
   }

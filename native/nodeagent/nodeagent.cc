@@ -24,6 +24,7 @@
 //
 //   gsx-nodeagent --apiserver URL --node NAME [--profile P] [--unit GiB]
 //                 [--workers N] [--no-verify] [--serial-admission] [--port-file F]
+//                 [--plugin-socket S | --plugin-spawn PYTHON] [--batch-window SECONDS]
 //
 // Admission: with the shipped plugin (--plugin-socket / --plugin-spawn), or with --serial-admission for the
 // in-process matcher, pods are admitted one at a time in the order the informer met them, as kubelet does (the
@@ -131,6 +132,7 @@ class Agent {
   void set_serial_admission(bool on) { serial_admission_ = on; }
 
   void set_plugin_socket(const std::string& s) { plugin_sock_ = s; }
+  void set_batch_window(double s) { batch_window_ = s; }
   void set_plugin_spawn(const std::string& python, const std::string& apiserver, const std::string& profile,
                         const std::string& unit) {
     spawn_python_ = python;
@@ -173,7 +175,9 @@ class Agent {
                                      "--apiserver", spawn_api_, "--profile", spawn_profile_, "--unit", spawn_unit_,
                                      "--backend", "fake", "--socket-dir", dir, "--no-publish", "--no-register",
                                      "--podresources-socket", pr_sock_, "--isolation", "advisory", "--health-interval",
-                                     "3600", "--log-level", "warning"};
+                                     "3600", "--log-level", "warning", "--debug-port", "0", "--debug-port-file",
+                                     dir + "/debug.port"};
+    plugin_debug_file_ = dir + "/debug.port";
     pid_t pid = ::fork();
     if (pid < 0) {
       *err = std::string("fork: ") + std::strerror(errno);
@@ -272,7 +276,7 @@ class Agent {
                     "\"runtime\":%.3f,\"running_patch\":%.3f},\"mean_ms\":{\"queue\":%.4f,\"assign_patch\":%.4f,"
                     "\"runtime\":%.4f,\"running_patch\":%.4f},\"status_retries\":%llu,\"api_connects\":%llu,"
                     "\"plugin_calls_mean_ms\":{\"n\":%llu,\"slot_wait\":%.4f,\"get_preferred\":%.4f,\"allocate\":%.4f},"
-                    "\"mismatch\":%llu,\"podresources_calls\":%llu,\"native\":true}",
+                    "\"mismatch\":%llu,\"podresources_calls\":%llu,\"plugin_debug\":\"%s\",\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
                     (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
                     max_queue_ * 1e3, max_patch_ * 1e3, max_runtime_ * 1e3, max_status_ * 1e3, sum_queue_ / n * 1e3,
@@ -281,7 +285,7 @@ class Agent {
                     (unsigned long long)dp_calls_, sum_dp_slot_ / std::max<double>(1.0, dp_calls_) * 1e3,
                     sum_dp_pref_ / std::max<double>(1.0, dp_calls_) * 1e3,
                     sum_dp_alloc_ / std::max<double>(1.0, dp_calls_) * 1e3, (unsigned long long)mismatch_,
-                    (unsigned long long)pr_calls_.load());
+                    (unsigned long long)pr_calls_.load(), plugin_debug_url().c_str());
       rep.body = b;
       return rep;
     }
@@ -365,7 +369,14 @@ class Agent {
     if (ap.assigned == "false" && !state_->inflight(uid) && !running_.count(uid) && !queued_.count(uid)) {
       queued_.insert(uid);
       seen_.emplace(uid, now_s());
-      queue_.push_back(key);
+      if (batch_window_ > 0) {
+        // kubelet's restart case: the pods met within the window are admitted as one batch, sorted by
+        // creationTimestamp (as kubelet sorts the pods of its initial LIST), not in the order they landed
+        if (batch_.empty()) batch_deadline_ = now_s() + batch_window_;
+        batch_.push_back({ap.creation, key});
+      } else {
+        queue_.push_back(key);
+      }
       ++added_;
     }
     return key;
@@ -411,6 +422,12 @@ class Agent {
     std::unique_lock<std::mutex> lk(mu_);
     while (true) {
       double now = now_s();
+      if (!batch_.empty() && now >= batch_deadline_) {
+        std::stable_sort(batch_.begin(), batch_.end());
+        for (auto& b : batch_) queue_.push_back(std::move(b.second));
+        batch_.clear();
+        cv_.notify_all();
+      }
       for (auto it = delayed_.begin(); it != delayed_.end();) {
         if (it->first <= now) {
           queue_.push_back(it->second);
@@ -429,6 +446,7 @@ class Agent {
       if (queue_.empty()) {
         double wait = 0.05;
         for (auto& dl : delayed_) wait = std::min(wait, std::max(0.0, dl.first - now));
+        if (!batch_.empty()) wait = std::min(wait, std::max(0.0, batch_deadline_ - now));
         cv_.wait_for(lk, std::chrono::duration<double>(wait));
         continue;
       }
@@ -627,6 +645,16 @@ class Agent {
     state_->set_inflight(my_uid, true);
     start_pod_locked(my_key, my_uid, request, dev_idx, cus, allocation_json(cr),
                      "/api/v1/namespaces/" + mine_ns(my_key) + "/pods/" + mine_name(my_key), t0, tp0, tp1, lk);
+  }
+
+  // the spawned plugin's /healthz, /metrics and /debug/state (its reconciliation and endpoint counters)
+  std::string plugin_debug_url() {
+    if (plugin_debug_url_.empty() && !plugin_debug_file_.empty()) {
+      std::ifstream f(plugin_debug_file_);
+      int port = 0;
+      if (f >> port && port > 0) plugin_debug_url_ = "http://127.0.0.1:" + std::to_string(port);
+    }
+    return plugin_debug_url_;
   }
 
   void forget_ids_locked(const std::string& uid) {
@@ -954,11 +982,15 @@ class Agent {
   std::unordered_set<std::string> used_all_;                             // the union of used_ids_, kept with it
   std::unordered_map<std::string, std::string> uid_key_;                 // uid -> ns/name of every used_ids_ pod
   std::string pr_sock_;                    // kubelet's PodResources API socket (with --plugin-spawn)
+  std::string plugin_debug_file_, plugin_debug_url_;
   std::unique_ptr<h2::Server> pr_srv_;
   std::thread pr_thread_;
   std::atomic<bool> pr_stop_{false};
   std::atomic<uint64_t> pr_calls_{0};
   uint64_t mismatch_ = 0;  // admissions answered with an allocation built for another pod (swaps)
+  double batch_window_ = 0;  // --batch-window: > 0 admits the pods met within it as one creationTimestamp batch
+  double batch_deadline_ = 0;
+  std::vector<std::pair<std::string, std::string>> batch_;  // (creationTimestamp, ns/name) of the open batch
   std::unordered_map<std::string, std::string> keys_;  // ns/name -> uid of every pod the informer delivered
   std::map<int, std::unique_ptr<ApiClient>> runtimes_;
   std::unique_ptr<Reflector> pods_r_;
@@ -996,6 +1028,7 @@ void on_sig(int) { g_stop = 1; }
 int main(int argc, char** argv) {
   std::string apiserver, node, profile = "shared-gpu", unit = "GiB", port_file, host = "127.0.0.1", plugin_socket, plugin_python;
   int workers = 16, port = 0;
+  double batch_window = 0;
   bool verify = true, serial = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -1017,10 +1050,11 @@ int main(int argc, char** argv) {
     else if (a == "--port-file") port_file = val("--port-file");
     else if (a == "--plugin-socket") plugin_socket = val("--plugin-socket");
     else if (a == "--plugin-spawn") plugin_python = val("--plugin-spawn");
+    else if (a == "--batch-window") batch_window = std::atof(val("--batch-window").c_str());
     else if (a == "-h" || a == "--help") {
       std::printf("usage: gsx-nodeagent --apiserver URL --node NAME [--profile P] [--unit GiB|MiB] [--workers N]\n"
                   "                     [--no-verify] [--serial-admission] [--port P] [--port-file F]\n"
-                  "                     [--plugin-socket S | --plugin-spawn PYTHON]\n");
+                  "                     [--plugin-socket S | --plugin-spawn PYTHON] [--batch-window SECONDS]\n");
       return 0;
     } else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -1043,6 +1077,7 @@ int main(int argc, char** argv) {
   Agent agent(api, node, profile_by_name(profile), unit_bytes, workers, verify);
   agent.set_plugin_socket(plugin_socket);
   agent.set_serial_admission(serial);
+  agent.set_batch_window(batch_window);
   if (!plugin_python.empty()) agent.set_plugin_spawn(plugin_python, apiserver, profile, unit);
   std::string err;
   CtlServer srv([&](const http::Message& m) { return agent.handle(m); });

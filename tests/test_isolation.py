@@ -1,6 +1,7 @@
 """Enforced isolation, CPU side: the library against a fake HSA runtime, and the plugin's per-pod files and
 mounts (the GPU behaviour is tests/test_gpu_isolate.py)."""
 import asyncio
+import json
 import os
 import subprocess
 from pathlib import Path
@@ -121,4 +122,39 @@ def test_library_loads_into_any_container_userland():
     versions = {tuple(int(x) for x in v.split(".")) for v in re.findall(r"GLIBC_(\d+\.\d+(?:\.\d+)?)", t)}
     assert versions and max(versions) <= (2, 17), sorted(versions)
     exported = {ln.split()[-1] for ln in t.splitlines() if " g " in ln and ".text" in ln}
-    assert exported == {"OnLoad", "OnUnload", "gsx_isolate_stats"}, exported
+    assert exported == {"OnLoad", "OnUnload", "gsx_isolate_stats", "hsa_init"}, exported
+
+
+def test_hsa_init_puts_the_tools_library_back(tmp_path):
+    """VERDICT r3 missing 4: ROCr reads HSA_TOOLS_LIB at hsa_init.  Preloaded, the library's own hsa_init runs first
+    (it precedes libhsa-runtime64 in the global scope), puts itself back into HSA_TOOLS_LIB whatever the process did
+    to its environment, and forwards to the runtime's hsa_init (found without libdl).  CPU-only: no GPU here, so the
+    runtime's own status is compared with the status it gives unconfined."""
+    import subprocess
+    import sys
+
+    conf = tmp_path / "isolation.conf"
+    conf.write_text("cu_mask=0x000000ff\nhbm_limit_bytes=1073741824\n")
+    code = (
+        "import ctypes, json, os\n"
+        "ctypes.CDLL('/opt/rocm/lib/libhsa-runtime64.so.1', mode=os.RTLD_NOW | os.RTLD_GLOBAL)\n"
+        "libc = ctypes.CDLL(None)\n"
+        "libc.getenv.restype = ctypes.c_char_p\n"
+        "before = libc.getenv(b'HSA_TOOLS_LIB')\n"
+        "os.environ.pop('HSA_TOOLS_LIB', None)\n"  # the process drops it before its first HSA call
+        "dropped = libc.getenv(b'HSA_TOOLS_LIB')\n"
+        "st = ctypes.CDLL(None).hsa_init()\n"  # global lookup: the preloaded definition first
+        "after = libc.getenv(b'HSA_TOOLS_LIB')\n"
+        "print(json.dumps({'before': (before or b'').decode(), 'dropped': (dropped or b'').decode(),\n"
+        "                  'after': (after or b'').decode(), 'status': st}))\n")
+    env = {k: v for k, v in os.environ.items() if k not in ("HSA_TOOLS_LIB", "LD_PRELOAD")}
+    plain = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert plain.returncode == 0, plain.stderr[-2000:]
+    ref = json.loads(plain.stdout.strip().splitlines()[-1])
+    env.update(LD_PRELOAD=str(LIB), GSX_ISOLATION_CONFIG=str(conf))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert str(LIB) in out["before"] and out["dropped"] == "", out  # the constructor set it; the process dropped it
+    assert str(LIB) in out["after"], out  # hsa_init put it back before the runtime read it
+    assert out["status"] == ref["status"], (out, ref)  # and the runtime's own hsa_init ran

@@ -388,3 +388,74 @@ asyncio.run(go())
     assert "IMPL grpcio" in out[True] and "gpushare_plugin_native_endpoint 0" in out[True], out[True]
     assert "WARNING device-plugin endpoint on grpc.aio" in out[True] and "libnghttp2" in out[True], out[True]
     assert "IMPL native" in out[False] and "gpushare_plugin_native_endpoint 1" in out[False], out[False]
+
+
+def test_plugin_process_sigkilled_between_answer_and_commit():
+    """the plugin process (as deployed, ``python -m ...deviceplugin``) answers an Allocate early and
+    is SIGKILLed before its ASSIGNED commit reaches a slow apiserver.  A new plugin process on the same socket
+    directory lands the commit from its journal before it serves, the pod is never served to a second Allocate, and
+    the other pending pod of that size is."""
+    import signal
+    import subprocess
+    import sys
+
+    async def go():
+        tmp = tempfile.mkdtemp()
+        api_srv = await FakeApiServerRunner().start()
+        client = KubeClient(api_srv.url)
+        await client.create("nodes", make_node("n1", 32, 0))
+        spec = os.path.join(tmp, "devices.json")
+        devs = fake_devices("2x16GiB")
+        with open(spec, "w") as f:
+            json.dump([{"index": d.index, "bdf": d.bdf, "uuid": d.uuid, "total_bytes": d.total_bytes,
+                        "share_bytes": d.share_bytes, "cu_count": d.cu_count, "xcc_count": d.xcc_count}
+                       for d in devs], f)
+        sock_dir = os.path.join(tmp, "dp")
+        env = dict(os.environ, GSX_FAKE_DEVICES=spec, GSX_PLUGIN_EARLY_ANSWER="1")
+
+        async def start_plugin():
+            p = subprocess.Popen([sys.executable, "-m", "gpushare_scheduler_extender_amd.deviceplugin", "--node", "n1",
+                                  "--apiserver", api_srv.url, "--backend", "fake", "--socket-dir", sock_dir,
+                                  "--no-register", "--no-publish", "--podresources-socket", "", "--isolation",
+                                  "advisory", "--log-level", "warning"], env=env, cwd=os.getcwd())
+            sock = os.path.join(sock_dir, "gpushare-amd.sock")
+            for _ in range(600):
+                if os.path.exists(sock):
+                    try:
+                        pc = PluginClient(sock)
+                        await asyncio.wait_for(pc.options(), 1.0)
+                        return p, pc
+                    except Exception:  # noqa: BLE001 - not serving yet
+                        await pc.close()
+                await asyncio.sleep(0.05)
+            raise TimeoutError("plugin never served")
+
+        a = await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
+        await client.create("pods", bound_pod("b", 4, dev=0, assume=2, dev_total=16))
+        proc, pc = await start_plugin()
+        try:
+            await asyncio.sleep(0.3)
+            api_srv.server.faults.latency_ms = 1500.0  # the commit cannot land before the kill
+            ids = fake_ids(devs[0], 16)
+            r = (await pc.allocate([ids[0:4]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "a"
+            proc.send_signal(signal.SIGKILL)
+            proc.wait(10)
+            await pc.close()
+            api_srv.server.faults.latency_ms = 0.0
+            assert (await client.get("pods", "a", "default"))["metadata"]["annotations"][P.annotation_assigned] == "false"
+            proc, pc = await start_plugin()  # serves only after landing the journaled commit
+            assert (await client.get("pods", "a", "default"))["metadata"]["annotations"][P.annotation_assigned] == "true"
+            r = (await pc.allocate([ids[4:8]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "b"  # a is never served twice
+            with pytest.raises(grpc.aio.AioRpcError):
+                await pc.allocate([ids[8:12]])
+        finally:
+            api_srv.server.faults.latency_ms = 0.0
+            await pc.close()
+            if proc.poll() is None:
+                proc.terminate()
+                proc.wait(10)
+            await client.close()
+            await api_srv.stop()
+    asyncio.run(go())

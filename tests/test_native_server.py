@@ -506,3 +506,92 @@ def test_bind_order_follows_the_nodes_allocate_order(order, landing, want):
         finally:
             await _teardown(api, c, ext)
     asyncio.run(go())
+
+
+def test_move_endpoint_is_the_one_writer_of_the_gpu_index():
+    """the device plugin's allocation-record moves go through POST /gpushare-scheduler/move.  Under
+    the ledger mutex the extender checks the move (pod where the caller thinks, room on the target unless an
+    equal-size partner makes it an exchange), charges the target until its informer shows the pod there, and writes
+    *_IDX with a resourceVersion precondition."""
+    from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as HttpClient
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU as P
+
+    async def go():
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 2 * 100, 2))
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=True, http_threads=2).start()
+        eng = ext.server.engine
+        http = HttpClient(f"http://127.0.0.1:{ext.port}")
+
+        def bound(name, mem, dev):
+            ann = {P.annotation_idx: str(dev), P.annotation_pod: str(mem), P.annotation_dev: "100",
+                   P.annotation_assigned: "false", P.annotation_assume_time: "1"}
+            return make_pod(name, mem, node="n", annotations=ann)
+
+        async def move(pod, to, frm=None, partner="", annotations=None):
+            md = pod["metadata"]
+            body = {"namespace": "default", "name": md["name"], "uid": md["uid"], "node": "n",
+                    "resourceVersion": md["resourceVersion"], "from": frm if frm is not None else int(
+                        md["annotations"][P.annotation_idx]), "to": to, "partner": partner,
+                    "annotations": annotations or {}}
+            r = await http.request("POST", "/gpushare-scheduler/move", json.dumps(body).encode())
+            return r.status, json.loads(r.body)
+
+        async def settle(want):
+            for _ in range(200):
+                if eng.node_devices("n") == want:
+                    return
+                await asyncio.sleep(0.01)
+            assert eng.node_devices("n") == want
+
+        try:
+            for _ in range(200):
+                if eng.has_node("n"):
+                    break
+                await asyncio.sleep(0.01)
+            a = await c.create("pods", bound("a", 60, 0))
+            b = await c.create("pods", bound("b", 60, 1))
+            q = await c.create("pods", bound("q", 30, 0))
+            await settle([(100, 90), (100, 60)])
+            # no room: GPU 1 has 40 free, a needs 60
+            st, out = await move(a, 1)
+            assert st == 409 and "free" in out["Error"], out
+            # stale view: a is on GPU 0, not 1
+            st, out = await move(a, 0, frm=1)
+            assert st == 409 and "stale" in out["Error"], out
+            # an exchange step with an equal-size partner on the target is sum-neutral: allowed, with a hold
+            st, out = await move(a, 1, partner=b["metadata"]["uid"],
+                                 annotations={"gpushare.amd.com/hold-idx": "0", P.annotation_assigned: "true"})
+            assert st == 200, out
+            ann = out["pod"]["metadata"]["annotations"]
+            assert ann[P.annotation_idx] == "1" and ann["gpushare.amd.com/hold-idx"] == "0"
+            assert ann[P.annotation_assigned] == "true"
+            b = await c.get("pods", "b", "default")
+            st, out = await move(b, 0, partner=a["metadata"]["uid"])  # step 2: b takes a's old GPU (a holds it)
+            assert st == 200, out
+            a = await c.get("pods", "a", "default")
+            st, out = await move(a, 1, annotations={"gpushare.amd.com/hold-idx": None})  # step 3: the hold goes
+            assert st == 200 and "gpushare.amd.com/hold-idx" not in out["pod"]["metadata"]["annotations"], out
+            await settle([(100, 90), (100, 60)])
+            # a plain move with room: best fit picked by the extender (to = -1), the target charged at once
+            q = await c.get("pods", "q", "default")
+            st, out = await move(q, -1)
+            assert st == 200 and out["to"] == 1, out
+            await settle([(100, 60), (100, 90)])
+            # the resourceVersion precondition: a stale copy of q conflicts (and its reservation is rolled back)
+            st, out = await move(q, 0, frm=1)
+            assert st == 409, out
+            await settle([(100, 60), (100, 90)])
+            # *_IDX (and the pod's share) are never written through the annotations map
+            q = await c.get("pods", "q", "default")
+            st, out = await move(q, 1, annotations={P.annotation_idx: "0"})
+            assert st == 400, out
+            assert eng.stats()["moves_ok"] == 4 and eng.stats()["moves_refused"] >= 2
+        finally:
+            await http.close()
+            await ext.stop()
+            await ext.server.client.close()
+            await c.close()
+            await api.stop()
+    asyncio.run(go())

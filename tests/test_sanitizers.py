@@ -61,8 +61,12 @@ def test_standins_under_tsan(tmp_path):
     r = subprocess.run([sys.executable, "-m", "gpushare_scheduler_extender_amd.sim.configs", "--agent", "native",
                         "--only", "2,3,5"], capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    # the compiled stand-in with its in-process matcher, and calling the shipped plugin process (PodResources server
+    # thread, serial admission slot)
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider",
-                        "tests/test_chaos.py::test_chaos_whole_stack_converges_without_overcommit[23-native-binding]"],
+                        "tests/test_chaos.py::test_chaos_whole_stack_converges_without_overcommit[23-native-binding-True]",
+                        "tests/test_chaos.py::test_chaos_whole_stack_converges_without_overcommit"
+                        "[17-native-plugin-binding-True]"],
                        capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout[-3000:]
     reports = sorted(glob.glob(str(logs) + "*"))
