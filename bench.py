@@ -31,7 +31,7 @@ Stability: every control-plane process is pinned to its own physical core, the i
 
 After the timed region rank 0 runs, as extra keys outside ``value``:
 ``device_plugin_path``: the same waves with kubelet + device plugin played by the shipped gRPC
-``GpuSharePlugin`` over its unix socket (the kubelet stand-in in deviceplugin/agent.py) instead of the
+``GpuSharePlugin`` over its unix socket (the kubelet stand-in in gsxtools/agent.py) instead of the
 compiled node agent; ``device_plugin_path_native_kubelet``: the compiled kubelet stand-in calling the shipped
 plugin process over gRPC; and ``latency_sweep`` (extra keys, not part of
 ``value``): the same waves with the fake kube-apiserver answering every
@@ -256,7 +256,7 @@ def latency_sweep(a, children, api_url, api_batch, runner: WaveRunner, inspect_u
     """Waves of the headline shape with the apiserver answering after L ms, for both bind modes, and behind
     client-go's default token bucket (QPS 5 / burst 10, the reference's client).  Rank 0 only; untimed by the
     driver's headline.  Returns (sweep rows, reference_client rows)."""
-    from gpushare_scheduler_extender_amd.sim.cluster import start_extender
+    from gsxtools.cluster import start_extender
 
     def restart_extender(mode: str, qps: float = 0.0, burst: int = 1000, order: str | None = None):
         restart_child(children, "extender", lambda old: start_extender(
@@ -295,7 +295,7 @@ def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
     compiled node agent.  The plugin's own pod informer and allocation state decide every Allocate.  With
     ``--plugin-proc process`` (default) the plugin is its own process (``python -m ...deviceplugin``) that
     registers with the stand-in's Registration service, as under a real kubelet."""
-    from gpushare_scheduler_extender_amd.sim.cluster import start_node_agent
+    from gsxtools.cluster import start_node_agent
 
     ext_url = next(c.url for c in children if c.name == "extender")
     na = restart_child(children, "node-agent", lambda old: start_node_agent(
@@ -317,7 +317,7 @@ def inprocess_matcher_path(a, children, api_url, runner: WaveRunner, E) -> dict:
     """The same waves with the compiled kubelet stand-in deciding every Allocate with the plugin's matcher linked
     in-process (allocstate.h) and committing ASSIGNED itself -- no gRPC hop to a plugin process, no PodResources
     reconciliation.  The rounds-1..3 headline path, kept as a comparison row."""
-    from gpushare_scheduler_extender_amd.sim.cluster import start_node_agent
+    from gsxtools.cluster import start_node_agent
 
     ext_url = next(c.url for c in children if c.name == "extender")
     na = restart_child(children, "node-agent", lambda old: start_node_agent(
@@ -345,7 +345,8 @@ def _plugin_debug(E, url: str | None) -> dict | None:
     g = d.get("grpc") or {}
     return {"grpc": {k: g.get(k) for k in ("impl", "fast_allocate", "slow_allocate", "fast_preferred",
                                            "slow_preferred", "patch_failures", "guard_by_ids", "journaling",
-                                           "early_answer_backlog")},
+                                           "early_answer_backlog", "waited", "feed_events", "passes",
+                                           "last_slow_reason")},
             "stats": d.get("stats"), "reconcile": d.get("reconcile")}
 
 
@@ -502,7 +503,7 @@ def main():
     api_url = ext_url = ""
     lt = LoopThread()
     if rank == 0:
-        from gpushare_scheduler_extender_amd.sim.cluster import (start_apiserver, start_extender, start_node_agent,
+        from gsxtools.cluster import (start_apiserver, start_extender, start_node_agent,
                                                                  start_scheduler)
 
         api = start_apiserver(cpus=cpu_plan.get("apiserver"))
@@ -531,7 +532,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from gpushare_scheduler_extender_amd.deviceplugin.agent import NodeAgent
+    from gsxtools.agent import NodeAgent
     from gpushare_scheduler_extender_amd.deviceplugin.devices import UNITS, discover
     from gpushare_scheduler_extender_amd.deviceplugin.runtime import HbmArenaRuntime, LedgerRuntime, RuntimeShim
     from gpushare_scheduler_extender_amd.k8s.client import KubeClient

@@ -1,27 +1,9 @@
-"""Cluster-state sync controller: informers -> work queue -> native ledger.
+"""The extender's cluster-state controller: the C++ pod / node reflectors of ``native/engine/controller.cc``.
 
-Re-design of ``pkg/gpushare/controller.go`` and ``pkg/cache/cache.go:49-127``:
-
-* pod events pass the reference's filter (only pods requesting gpu-mem,
-  ``controller.go:77-100``) and its enqueue rules: add -> enqueue;
-  update -> enqueue iff (known and now complete) or (unknown and annotated
-  with a device index) (``controller.go:257-305``), plus "assumed by our bind
-  and now observed", which confirms a bind reservation; delete -> enqueue and
-  remember the last state for the tombstone path (``controller.go:307-332``);
-* ``sync_pod`` is ``controller.go:174-205``: gone -> remove using the
-  remembered object; complete (deleting / Succeeded / Failed) -> remove;
-  otherwise add-or-update from annotations;
-* ``build_cache`` replays annotated, bound pods at start-up — the crash
-  recovery path of ``cache.go:49-74`` (pod annotations are the durable state);
-* nodes feed the ledger directly from the node informer (the reference built
-  ``NodeInfo`` lazily on first lookup, ``cache.go:130-162``, and missed
-  capacity changes);
-* ``THREADNESS`` workers really run (the reference's ``StringToInt`` always
-  returned 1, ``cmd/main.go:133-137``) and never sleep between items
-  (``controller.go:218-223`` capped sync at one pod per second).
-
-Everything runs on one asyncio loop, so the reference's data races on
-``removePodCache`` and the node map cannot occur.
+Re-design of ``pkg/gpushare/controller.go`` and ``pkg/cache/cache.go:49-127`` (one controller, as the reference
+has): the reference's pod filter and enqueue rules (``controller.go:77-100,257-332``), ``syncPod``
+(``controller.go:174-205``) and ``BuildCache`` crash recovery (``cache.go:49-74``) are applied on the reflector
+threads as events are decoded, and nodes feed the ledger directly.  This module is its Python handle.
 """
 from __future__ import annotations
 
@@ -30,184 +12,9 @@ import json
 import logging
 
 from ..k8s.client import KubeClient
-from ..k8s.informer import Handler, Informer, dumps, obj_key
-from ..models import pod as podutil
 from ..models.profile import NamingProfile
-from ..parallel.workqueue import ShutDown, WorkQueue
 
 log = logging.getLogger("gsx.controller")
-
-
-class Controller:
-    def __init__(self, client: KubeClient, engine, profile: NamingProfile, workers: int = 1,
-                 resync_period: float = 30.0, metrics=None):
-        self.client = client
-        self.engine = engine
-        self.profile = profile
-        self.workers = max(1, int(workers))
-        self.metrics = metrics
-        self.pods = Informer(client, "pods", resync_period=resync_period)
-        self.nodes = Informer(client, "nodes", resync_period=resync_period)
-        self.queue = WorkQueue(name="pods")
-        self.removed: dict[str, dict] = {}  # key -> last state of deleted pods (removePodCache)
-        self._raw: dict[str, bytes] = {}  # key -> raw JSON of the latest event (native parse fast path)
-        self._tasks: list[asyncio.Task] = []
-        self.synced_pods = 0
-        self._confirmed_list_start = 0.0  # the last LIST start whose keys the workers have all applied
-        self.overcommitted: list = []
-        self.sync_errors = 0
-        self.pods.add_handler(Handler(self._on_pod_add, self._on_pod_update, self._on_pod_delete,
-                                      filter_fn=self._is_gpushare_pod))
-        self.nodes.add_handler(Handler(self._on_node, lambda old, new, raw: self._on_node(new, raw),
-                                       self._on_node_delete))
-
-    # ------------------------------------------------------------ filters / handlers
-    def _is_gpushare_pod(self, pod: dict) -> bool:
-        return podutil.is_gpushare_pod(pod, self.profile)
-
-    def _on_node(self, node: dict, raw: bytes | None):
-        self.engine.upsert_node_json(raw if raw is not None else dumps(node))
-
-    def _on_node_delete(self, node: dict, raw):
-        self.engine.remove_node((node.get("metadata") or {}).get("name", ""))
-
-    def _on_pod_add(self, pod: dict, raw):
-        key = obj_key(pod)
-        if raw is not None:
-            self._raw[key] = raw
-        self.queue.add(key)
-
-    def _on_pod_update(self, old: dict, new: dict, raw):
-        key = obj_key(new)
-        uid = (new.get("metadata") or {}).get("uid", "")
-        state, _dev = self.engine.pod_state(uid)
-        enqueue = False
-        if state != 0 and podutil.is_complete(new):
-            enqueue = True
-        elif podutil.gpu_id_from_annotation(new, self.profile) >= 0 and (state == 0 or state == 2):
-            enqueue = True
-        elif state == 1 and podutil.gpu_id_from_annotation(new, self.profile) != _dev:
-            enqueue = True  # device index rewritten: re-account
-        elif state != 0 and podutil.hold_idx(new) != podutil.hold_idx(old):
-            enqueue = True  # the device plugin's reconciliation set / cleared a hold (charged on two devices)
-        elif state == 2 and podutil.gpu_id_from_annotation(new, self.profile) < 0 and podutil.node_name(new):
-            enqueue = True  # our reservation, bound without its annotations: the ledger queues a repair
-        if enqueue:
-            if raw is not None:
-                self._raw[key] = raw
-            else:
-                self._raw.pop(key, None)
-            self.queue.add(key)
-
-    def _on_pod_delete(self, pod: dict, raw):
-        key = obj_key(pod)
-        self.removed[key] = pod
-        self._raw.pop(key, None)
-        self.queue.add(key)
-
-    # ------------------------------------------------------------ sync
-    def sync_pod(self, key: str):
-        pod = self.pods.get(key)
-        if pod is None or not self._is_gpushare_pod(pod):
-            gone = self.removed.pop(key, None)
-            if gone is not None:
-                self.engine.remove_pod((gone.get("metadata") or {}).get("uid", ""))
-            self._raw.pop(key, None)
-            return
-        self.removed.pop(key, None)
-        if podutil.is_complete(pod):
-            self.engine.remove_pod((pod.get("metadata") or {}).get("uid", ""))
-            self._raw.pop(key, None)
-            return
-        raw = self._raw.pop(key, None)
-        if raw is not None:
-            self.engine.upsert_pod_json(raw)
-        else:
-            self.engine.upsert_pod_json(dumps(pod))
-
-    def build_cache(self):
-        """cache.go:49-74: replay every annotated, scheduled pod into the ledger."""
-        n = 0
-        for pod in self.pods.list():
-            if podutil.gpu_mem_from_annotation(pod, self.profile) > 0 and podutil.node_name(pod):
-                if podutil.is_complete(pod):
-                    continue
-                self.engine.upsert_pod_json(dumps(pod))
-                n += 1
-        log.info("build_cache: recovered %d pods from annotations", n)
-        # consistency check (SURVEY.md §5): the reference's uint arithmetic would have wrapped here
-        self.overcommitted = []
-        for node in self.engine.node_names():
-            for i, (total, used) in enumerate(self.engine.node_devices(node)):
-                if used > total:
-                    self.overcommitted.append((node, i, used, total))
-                    log.warning("node %s GPU %d is over-committed after recovery: %d > %d (annotations disagree "
-                                "with capacity); it accepts no new pods until it drains", node, i, used, total)
-        return n
-
-    async def _worker(self):
-        while True:
-            try:
-                key = await self.queue.get()
-            except ShutDown:
-                return
-            try:
-                self.sync_pod(key)
-                self.queue.forget(key)
-                self.synced_pods += 1
-            except Exception as e:  # noqa: BLE001 - controller.go:228: retry with backoff
-                self.sync_errors += 1
-                log.warning("sync %s failed: %r; requeue", key, e)
-                self.queue.add_rate_limited(key)
-            finally:
-                self.queue.done(key)
-
-    async def start(self, sync_timeout: float | None = 60.0):
-        """NewController + BuildCache + Run (controller.go:62-161, cmd/main.go:104-113)."""
-        await self.nodes.start()
-        await self.nodes.wait_synced(sync_timeout)
-        await self.pods.start()
-        await self.pods.wait_synced(sync_timeout)
-        self.build_cache()
-        loop = asyncio.get_running_loop()
-        for i in range(self.workers):
-            self._tasks.append(loop.create_task(self._worker(), name=f"controller-worker-{i}"))
-
-    async def stop(self):
-        await self.queue.shutdown()
-        await self.pods.stop()
-        await self.nodes.stop()
-        for t in self._tasks:
-            t.cancel()
-        self._tasks.clear()
-
-    # lister / status API shared with NativeController
-    def get_pod(self, name: str, ns: str | None = None) -> dict | None:
-        return self.pods.get_by(name, ns)
-
-    def gc_reservations(self) -> tuple[int, bool]:
-        """Ledger GC gated on the pod informer's last LIST (see Ledger::gc); forces a re-list when needed.
-
-        A LIST only proves a binding absent once the ledger has applied it: its handlers merely queue keys, the
-        workers upsert later.  So the LIST start that confirms counts only when the work queue has
-        drained (no key queued, in process or waiting for a rate-limited retry) since that LIST."""
-        start = self.pods.last_list_start
-        if self.queue.idle():
-            self._confirmed_list_start = start
-        n, need = self.engine.gc(self._confirmed_list_start)
-        if need:
-            self.pods.request_relist()
-        return n, need
-
-    def is_synced(self) -> bool:
-        return self.pods.synced.is_set() and self.nodes.synced.is_set()
-
-    async def wait_idle(self, timeout: float = 10.0):
-        deadline = asyncio.get_running_loop().time() + timeout
-        while not self.queue.idle():
-            if asyncio.get_running_loop().time() > deadline:
-                raise TimeoutError("controller queue not idle")
-            await asyncio.sleep(0.001)
 
 
 def api_dict(cfg) -> dict:
@@ -220,11 +27,9 @@ def api_dict(cfg) -> dict:
 class NativeController:
     """The controller in C++ (``native/engine/controller.cc``): pod and node reflectors feed the ledger directly.
 
-    Same rules as :class:`Controller` (filter transitions, enqueue rules,
-    syncPod, BuildCache + over-commit check), applied on the reflector threads
-    as events are decoded, so no pod or node event is ever turned into a
-    Python object on the extender's hot path.  The lister keeps the raw JSON
-    of gpu-share pods for the Python slow-path bind.
+    Filter transitions, enqueue rules, syncPod, BuildCache + over-commit check, applied on the reflector threads
+    as events are decoded, so no pod or node event is ever turned into a Python object.  The lister keeps the
+    raw JSON of gpu-share pods for binds the filter did not see (``server.cc: lookup_pod``).
     """
 
     def __init__(self, client: KubeClient, engine, profile: NamingProfile, resync_period: float = 30.0,

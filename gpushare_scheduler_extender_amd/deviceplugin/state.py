@@ -211,8 +211,14 @@ class AllocationState:
         self._flush()
 
     def forget(self, pod: dict) -> None:
-        """A deleted pod (watch DELETE or gone from a re-list)."""
-        self.release(podutil.meta(pod).get("uid", ""))
+        """A deleted pod (watch DELETE or gone from a re-list): released and remembered (AllocState::deleted), so a
+        copy of it another feed still delivers cannot bring it back."""
+        uid = podutil.meta(pod).get("uid", "")
+        if not uid:
+            return
+        self.core.deleted(uid)
+        self._recs.pop(uid, None)
+        self._flush()
 
     def resync(self, pods: list[dict]) -> None:
         """A complete LIST of this node's pods: anything we hold that is not in it is gone."""

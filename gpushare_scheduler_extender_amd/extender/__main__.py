@@ -5,7 +5,7 @@ Environment (same names as the reference, ``cmd/main.go:23,92-98`` and
 
 * ``PORT``        listen port (default 39999)
 * ``KUBECONFIG``  kubeconfig path; in-cluster service account otherwise
-* ``THREADNESS``  controller workers (honoured; the reference ignored it)
+* ``THREADNESS``  bind threads (a floor under ``--bind-threads``; the reference ignored it)
 * ``LOG_LEVEL``   debug|info|warning|error (set by the reference's yaml, never read)
 
 Ours: ``GSX_PROFILE`` (shared-gpu|aliyun), ``GSX_BIND_MODE`` (binding|update),
@@ -53,10 +53,6 @@ def parse_args(argv=None):
     ap.add_argument("--kube-burst", type=int, default=int(env.get("GSX_KUBE_BURST", "1000")))
     ap.add_argument("--resync", type=float, default=float(env.get("GSX_RESYNC", "30")))
     ap.add_argument("--reservation-ttl", type=float, default=float(env.get("GSX_RESERVATION_TTL", "60")))
-    ap.add_argument("--native-http", type=int, default=int(env.get("GSX_NATIVE_HTTP", "1")),
-                    help="1: C++ front end serves filter/bind/inspect (default); 0: aiohttp only")
-    ap.add_argument("--native-controller", type=int, default=int(env.get("GSX_NATIVE_CONTROLLER", "1")),
-                    help="1: pod/node informers + controller in C++ (default); 0: asyncio controller")
     ap.add_argument("--http-threads", type=int, default=int(env.get("GSX_HTTP_THREADS", "2")))
     ap.add_argument("--bind-threads", type=int, default=int(env.get("GSX_BIND_THREADS", "16")))
     ap.add_argument("--leader-elect", type=int, default=int(env.get("GSX_LEADER_ELECT", "0")),
@@ -78,13 +74,12 @@ def main(argv=None) -> int:
     async def run():
         cfg = KubeConfig.auto(a.kubeconfig, a.apiserver)
         client = KubeClient(cfg, qps=a.kube_qps, burst=a.kube_burst)
-        srv = ExtenderServer(client, get_profile(a.profile), workers=a.threadness, bind_mode=a.bind_mode,
+        srv = ExtenderServer(client, get_profile(a.profile), bind_mode=a.bind_mode,
                              reservation_ttl=a.reservation_ttl, resync_period=a.resync,
                              leader_elect=bool(a.leader_elect), lease_name=a.lease_name,
-                             lease_namespace=a.lease_namespace, native_controller=bool(a.native_controller),
-                             pprof=bool(a.pprof), bind_order=a.bind_order)
-        runner = await ExtenderRunner(srv, a.host, a.port, native=bool(a.native_http), http_threads=a.http_threads,
-                                      pool_threads=a.bind_threads).start()
+                             lease_namespace=a.lease_namespace, pprof=bool(a.pprof), bind_order=a.bind_order)
+        runner = await ExtenderRunner(srv, a.host, a.port, http_threads=a.http_threads,
+                                      pool_threads=max(a.bind_threads, a.threadness)).start()
         if a.port_file:
             with open(a.port_file + ".tmp", "w") as f:
                 f.write(str(runner.port))

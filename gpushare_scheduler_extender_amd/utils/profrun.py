@@ -2,7 +2,7 @@
 
     python -m gpushare_scheduler_extender_amd.utils.profrun OUT.prof some.module [args...]
 
-The process harness (``sim/cluster.py``) wraps its children with this when
+The process harness (``gsxtools/cluster.py``) wraps its children with this when
 ``GSX_CPROFILE_DIR`` is set, to see where the control plane spends its CPU.
 """
 import cProfile

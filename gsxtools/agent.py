@@ -46,14 +46,14 @@ import asyncio
 import logging
 import time
 
-from ..k8s.client import ApiError, KubeClient
-from ..k8s.informer import Handler, Informer, obj_key
-from ..models import pod as podutil
-from ..models.profile import NamingProfile
-from .allocator import CU_COUNT_ANNOTATION, AllocateError
-from .devices import UNITS, Device
-from .plugin import POD_ANNOTATION, GpuSharePlugin, PluginClient
-from .runtime import AdmissionError, admit_local
+from gpushare_scheduler_extender_amd.k8s.client import ApiError, KubeClient
+from gpushare_scheduler_extender_amd.k8s.informer import Handler, Informer, obj_key
+from gpushare_scheduler_extender_amd.models import pod as podutil
+from gpushare_scheduler_extender_amd.models.profile import NamingProfile
+from gpushare_scheduler_extender_amd.deviceplugin.allocator import CU_COUNT_ANNOTATION, AllocateError
+from gpushare_scheduler_extender_amd.deviceplugin.devices import UNITS, Device
+from gpushare_scheduler_extender_amd.deviceplugin.plugin import POD_ANNOTATION, GpuSharePlugin, PluginClient
+from gpushare_scheduler_extender_amd.deviceplugin.runtime import AdmissionError, admit_local
 
 log = logging.getLogger("gsx.agent")
 
@@ -124,7 +124,7 @@ class NodeAgent:
         self.plugin_stats_url: str | None = None  # the plugin's /debug/state when it runs as its own process
         self.prserver = None
         if podresources_socket:
-            from .podresources import PodResourcesServer  # noqa: PLC0415
+            from gpushare_scheduler_extender_amd.deviceplugin.podresources import PodResourcesServer  # noqa: PLC0415
 
             self.prserver = PodResourcesServer(podresources_socket, self._pod_resources)
         self.pods.add_handler(Handler(self._on_pod, lambda o, n, r: self._on_pod(n, r), self._on_delete))
@@ -196,7 +196,7 @@ class NodeAgent:
         envs = dict(r.envs)
         cus = None
         if envs.get("GSX_CU_MASK"):
-            from .state import parse_cu_mask  # noqa: PLC0415
+            from gpushare_scheduler_extender_amd.deviceplugin.state import parse_cu_mask  # noqa: PLC0415
 
             cus = parse_cu_mask(envs["GSX_CU_MASK"])
         key, _, cuid = who.rpartition("/")
@@ -206,7 +206,7 @@ class NodeAgent:
         rec, alloc = await self.plugin.allocate_container(units)
         cus = None
         if alloc.envs.get("GSX_CU_MASK"):
-            from .state import parse_cu_mask  # noqa: PLC0415
+            from gpushare_scheduler_extender_amd.deviceplugin.state import parse_cu_mask  # noqa: PLC0415
 
             cus = parse_cu_mask(alloc.envs["GSX_CU_MASK"])
         return _Alloc(rec.uid, rec.key, rec.dev, alloc.envs, cus, [])
@@ -450,7 +450,7 @@ async def _spawn_plugin(a, sock_dir: str, devs: list[Device], prsock: str | None
     import os  # noqa: PLC0415
     import sys  # noqa: PLC0415
 
-    from .plugin import FakeKubelet  # noqa: PLC0415
+    from gpushare_scheduler_extender_amd.deviceplugin.plugin import FakeKubelet  # noqa: PLC0415
 
     kubelet = FakeKubelet(sock_dir)
     await kubelet.start()
@@ -492,7 +492,7 @@ async def node_devices_and_endpoints(client: KubeClient, node: str, timeout: flo
     """Wait for the node's device inventory + runtime endpoints annotations; return (devices, endpoints)."""
     import json  # noqa: PLC0415
 
-    from ..models.profile import NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION  # noqa: PLC0415
+    from gpushare_scheduler_extender_amd.models.profile import NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION  # noqa: PLC0415
 
     deadline = time.monotonic() + timeout
     while True:
@@ -543,7 +543,7 @@ async def serve_stats(box: dict, host: str = "127.0.0.1", port: int = 0):
             prec = dict(rc.stats) if rc is not None else None
         elif getattr(agent, "plugin_stats_url", None):  # the plugin's own process: its /debug/state
             try:
-                from ..k8s.fasthttp import Client as HttpClient  # noqa: PLC0415
+                from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as HttpClient  # noqa: PLC0415
 
                 hc = HttpClient(agent.plugin_stats_url)
                 try:
@@ -591,7 +591,7 @@ async def serve_stats(box: dict, host: str = "127.0.0.1", port: int = 0):
 
 
 def main(argv=None) -> int:
-    """``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``: kubelet stand-in for one node.
+    """``python -m gsxtools.agent``: kubelet stand-in for one node.
 
     ``--plugin grpc`` (default): the shipped :class:`GpuSharePlugin` is served on a unix socket in this process
     (devices from the node's inventory annotation) and driven over gRPC like kubelet drives it;
@@ -605,9 +605,9 @@ def main(argv=None) -> int:
     import signal  # noqa: PLC0415
     import tempfile  # noqa: PLC0415
 
-    from ..k8s.client import KubeConfig  # noqa: PLC0415
-    from ..models.profile import get_profile  # noqa: PLC0415
-    from .runtime import RemoteRuntime  # noqa: PLC0415
+    from gpushare_scheduler_extender_amd.k8s.client import KubeConfig  # noqa: PLC0415
+    from gpushare_scheduler_extender_amd.models.profile import get_profile  # noqa: PLC0415
+    from gpushare_scheduler_extender_amd.deviceplugin.runtime import RemoteRuntime  # noqa: PLC0415
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--node", required=True)
@@ -654,7 +654,7 @@ def main(argv=None) -> int:
         if a.plugin == "grpc":
             iso = None
             if a.isolation_dir:
-                from .isolation import IsolationManager  # noqa: PLC0415
+                from gpushare_scheduler_extender_amd.deviceplugin.isolation import IsolationManager  # noqa: PLC0415
 
                 iso = IsolationManager(a.isolation_dir)
             plugin = GpuSharePlugin(KubeClient(KubeConfig.auto(a.kubeconfig, a.apiserver)), a.node, devs, profile,
@@ -678,7 +678,7 @@ def main(argv=None) -> int:
         if plugin is not None:
             agent.plugin = plugin  # for /v1/stats
         box["agent"] = agent
-        from ..utils.gctune import tune  # noqa: PLC0415
+        from gpushare_scheduler_extender_amd.utils.gctune import tune  # noqa: PLC0415
 
         tune()
         stop = asyncio.Event()

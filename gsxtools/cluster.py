@@ -16,7 +16,7 @@ import tempfile
 import time
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parents[2]
+ROOT = Path(__file__).resolve().parents[1]
 
 
 def _wait_port(path: str, proc: subprocess.Popen, timeout: float = 60.0) -> int:
@@ -154,7 +154,7 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
 
     ``native=True``: the compiled ``gsx-nodeagent`` (native/nodeagent, the plugin's native matcher in-process, or
     with ``plugin="spawn"`` the shipped plugin as its child process, called over the device-plugin gRPC API);
-    otherwise ``python -m gpushare_scheduler_extender_amd.deviceplugin.agent``: a kubelet stand-in driving
+    otherwise ``python -m gsxtools.agent``: a kubelet stand-in driving
     the shipped device plugin, over its unix socket (``plugin="grpc"``) or in-process (``"inproc"``).
     ``serial_admission``: the compiled agent admits one pod at a time with its in-process matcher too, as kubelet
     does (with ``plugin="spawn"`` it always does).
@@ -177,7 +177,7 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
         return ChildProc([str(exe), "--node", node, "--apiserver", apiserver, "--profile", profile,
                           "--workers", str(min(workers, 16)), *spawn, *(extra or [])], "node-agent", cpus=cpus,
                          env=env)
-    return ChildProc(["-m", "gpushare_scheduler_extender_amd.deviceplugin.agent", "--node", node, "--apiserver",
+    return ChildProc(["-m", "gsxtools.agent", "--node", node, "--apiserver",
                       apiserver, "--profile", profile, "--workers", str(workers), "--plugin", plugin,
                       *(extra or [])], "node-agent", cpus=cpus, env=env)
 

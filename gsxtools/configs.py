@@ -1,6 +1,6 @@
 """The five BASELINE.json configurations (plus hardware partitions), end to end through the whole stack.
 
-    python -m gpushare_scheduler_extender_amd.sim.configs [--gpu] [--json-out F] [--only 1,4]
+    python -m gsxtools.configs [--gpu] [--json-out F] [--only 1,4]
 
 Every configuration starts the same processes as ``bench.py`` (fake kube-apiserver, the extender, the
 kube-scheduler stand-in and the node agent as child processes; a pod runtime endpoint per GPU in this
@@ -29,7 +29,7 @@ process), registers one node, creates pods and checks where they land:
 devices beyond the box's GPUs are fakes of the same size.  Without ``--gpu`` everything is CPU-only.
 
 ``--agent``: who plays kubelet + device plugin.  ``plugin`` (default): the kubelet stand-in
-(``deviceplugin/agent.py``) drives the shipped gRPC :class:`GpuSharePlugin` over its unix socket;
+(``gsxtools/agent.py``) drives the shipped gRPC :class:`GpuSharePlugin` over its unix socket;
 ``inproc``: the same plugin called in-process; ``native``: the compiled ``gsx-nodeagent``.
 """
 from __future__ import annotations
@@ -40,12 +40,12 @@ import json
 import sys
 import time
 
-from ..k8s.client import KubeClient
-from ..k8s.fasthttp import Client as HttpClient
-from ..k8s.objects import make_node, make_pod
-from ..models.profile import (ALIYUN, NODE_ALLOCATE_ORDER_ANNOTATION, NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION,
+from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as HttpClient
+from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
+from gpushare_scheduler_extender_amd.models.profile import (ALIYUN, NODE_ALLOCATE_ORDER_ANNOTATION, NODE_DEVICE_INFO_ANNOTATION, NODE_RUNTIME_ENDPOINTS_ANNOTATION,
                               POD_CU_MASK_ANNOTATION, POD_HOLD_IDX_ANNOTATION, SHARED_GPU, NamingProfile)
-from .cluster import start_apiserver, start_extender, start_node_agent, start_scheduler
+from gsxtools.cluster import start_apiserver, start_extender, start_node_agent, start_scheduler
 
 GIB = 1 << 30
 NODE = "mi355x-node-0"
@@ -58,7 +58,7 @@ class Runtimes:
 
     def __init__(self, n: int, unit_bytes: int, gib_per_dev: int, gpu: bool | int):
         """``gpu``: False, True (GPU 0 backs device 0) or the number of leading devices backed by real GPUs."""
-        from ..core.engine import native
+        from gpushare_scheduler_extender_amd.core.engine import native
 
         E = native()
         n_real = int(gpu)
@@ -67,7 +67,7 @@ class Runtimes:
         for i in range(n):
             arena = gib_per_dev * unit_bytes
             if i < n_real:
-                from ..ops import hip
+                from gpushare_scheduler_extender_amd.ops import hip
 
                 buf = hip.DeviceBuffer(i, arena)
                 st = hip.Stream(i)
@@ -185,7 +185,7 @@ class Cluster:
 
     async def bind(self, pod: dict) -> int:
         """kube-scheduler's filter + bind for one pod (tests that choose the binding order themselves)."""
-        from ..models import wire
+        from gpushare_scheduler_extender_amd.models import wire
 
         f = await self.filter(pod)
         if NODE not in (f.get("NodeNames") or []):
@@ -282,7 +282,7 @@ class Cluster:
 
 
 def _gpu_gib() -> int:
-    from ..ops import hip
+    from gpushare_scheduler_extender_amd.ops import hip
 
     return hip.mem_info(0)[1] // GIB
 
@@ -426,8 +426,8 @@ async def config5(gpu: bool) -> dict:
         for i in range(4):
             await cl.create(f"cu-{i}", 64, annotations={CU_COUNT_ANNOTATION: "64"})
         pods = await cl.wait([f"cu-{i}" for i in range(4)])
-        from ..deviceplugin.allocator import CUPartitioner
-        from ..deviceplugin.state import parse_cu_mask
+        from gpushare_scheduler_extender_amd.deviceplugin.allocator import CUPartitioner
+        from gpushare_scheduler_extender_amd.deviceplugin.state import parse_cu_mask
 
         parts = []
         for name in sorted(pods):
@@ -441,7 +441,7 @@ async def config5(gpu: bool) -> dict:
         if args:
             from pathlib import Path
 
-            from ..deviceplugin.isolation import CONF
+            from gpushare_scheduler_extender_amd.deviceplugin.isolation import CONF
             confs = [Path(iso_dir) / "pods" / p["metadata"]["uid"] / CONF for p in pods.values()]
             n_conf = sum(1 for c in confs if c.exists() and "cu_mask=" in c.read_text())
             ok = ok and n_conf == 4
@@ -449,7 +449,7 @@ async def config5(gpu: bool) -> dict:
                "partitions": [{"pod": p["pod"], "HSA_CU_MASK": p["HSA_CU_MASK"], "n_cus": len(p["cus"])} for p in parts],
                "disjoint": disjoint, "xcds_per_pod": [len(x) for x in per_xcd]}
         if gpu:
-            from ..ops import hip
+            from gpushare_scheduler_extender_amd.ops import hip
 
             hw = []
             for p in parts:
@@ -484,9 +484,9 @@ def _enforced_probe(iso_dir: str, uids: list[str]) -> list[set]:
     import subprocess
     from pathlib import Path
 
-    from ..deviceplugin.isolation import CONF, LIB
+    from gpushare_scheduler_extender_amd.deviceplugin.isolation import CONF, LIB
 
-    native = Path(__file__).resolve().parents[1] / "_native"
+    native = Path(__file__).resolve().parents[1] / "gpushare_scheduler_extender_amd" / "_native"
     out = []
     for uid in uids:
         env = {k: v for k, v in os.environ.items() if k not in ("HSA_CU_MASK", "GSX_CU_MASK", "HSA_TOOLS_LIB")}
@@ -499,7 +499,7 @@ def _enforced_probe(iso_dir: str, uids: list[str]) -> list[set]:
 
 
 async def config6(gpu: bool) -> dict:
-    from ..deviceplugin.devices import apply_memory_pools, fake_devices
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import apply_memory_pools, fake_devices
 
     total = _gpu_gib() if gpu else 268
     devs = apply_memory_pools(fake_devices(f"1x{total}GiB:CPX:NPS1"), "auto")

@@ -19,7 +19,7 @@ exact environment the device plugin's Allocate produces, in four scenarios:
                     is the interference the partition removes.
 
 Reported per scenario: per-pod TFLOP/s, aggregate, and fairness (min/max).
-Run: ``python -m gpushare_scheduler_extender_amd.sim.isolation --seconds 8``.
+Run: ``python -m gsxtools.isolation --seconds 8``.
 """
 from __future__ import annotations
 
@@ -31,12 +31,12 @@ import sys
 import time
 from pathlib import Path
 
-from ..deviceplugin.allocator import CUPartitioner, build_response
-from ..deviceplugin.devices import Device
-from ..k8s.objects import make_pod
-from ..models.profile import SHARED_GPU
+from gpushare_scheduler_extender_amd.deviceplugin.allocator import CUPartitioner, build_response
+from gpushare_scheduler_extender_amd.deviceplugin.devices import Device
+from gpushare_scheduler_extender_amd.k8s.objects import make_pod
+from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
 
-ROOT = Path(__file__).resolve().parents[2]
+ROOT = Path(__file__).resolve().parents[1]
 
 
 def pod_envs(n_pods: int, cus_each: int, gpu_total_gib: int, pod_gib: int, with_mask: bool) -> list[dict]:
@@ -66,7 +66,7 @@ def run_pods(envs: list[dict], seconds: float, kernel: str, size, mask_mode: str
         env["ROCR_VISIBLE_DEVICES"] = "0"
         env["GSX_START_AT"] = str(start_at)
         env["PYTHONPATH"] = str(ROOT) + os.pathsep + env.get("PYTHONPATH", "")
-        cmd = [sys.executable, "-m", "gpushare_scheduler_extender_amd.sim.workload", "--total",
+        cmd = [sys.executable, "-m", "gsxtools.workload", "--total",
                e["SHARED_GPU_MEM_DEV"], "--allocated", e["SHARED_GPU_MEM_CONTAINER"], "--kernel", kernel,
                "--size", str(sz), "--seconds", str(seconds), "--json"]
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,

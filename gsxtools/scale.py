@@ -1,6 +1,6 @@
 """Cluster scale: the extender against 100 / 1,000 / 5,000 GPU nodes (8 x MI355X each) with pod churn.
 
-    python -m gpushare_scheduler_extender_amd.sim.scale [--nodes 100,1000,5000] [--pods-per-node 2]
+    python -m gsxtools.scale [--nodes 100,1000,5000] [--pods-per-node 2]
                                                        [--churn-batches 8] [--batch 250] [--json-out F]
 
 The reference's filter walks every NodeName under a global write lock and re-sums every pod annotation
@@ -28,10 +28,10 @@ import json
 import sys
 import time
 
-from ..k8s.objects import make_node, make_pod
-from ..models.profile import ALIYUN
-from ..utils.cpuset import plan
-from .cluster import start_apiserver, start_extender, start_scheduler
+from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
+from gpushare_scheduler_extender_amd.models.profile import ALIYUN
+from gpushare_scheduler_extender_amd.utils.cpuset import plan
+from gsxtools.cluster import start_apiserver, start_extender, start_scheduler
 
 GIB_PER_DEV = 268  # a 288 GB MI355X in GiB units
 DEVS = 8
@@ -168,7 +168,7 @@ def churn(E, api_url: str, sched_url: str, batches: int, batch: int) -> dict:
 
 
 def run_one(n_nodes: int, pods_per_node: int, churn_batches: int, batch: int, filter_reps: int) -> dict:
-    from ..core.engine import native
+    from gpushare_scheduler_extender_amd.core.engine import native
 
     E = native()
     cpus = plan(["apiserver", "extender", "scheduler"], {"extender": 2}, "spread")
@@ -209,7 +209,7 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     out = {}
     # process start-up alone (empty cluster): what extender_ready_s includes besides LIST + BuildCache
-    from ..core.engine import native
+    from gpushare_scheduler_extender_amd.core.engine import native
 
     E = native()
     api = start_apiserver()

@@ -168,7 +168,7 @@ def build_tools(force: bool = False, verbose: bool = False) -> list[Path]:
             OUT.mkdir(parents=True, exist_ok=True)
             others = [str(x) for x in sorted(src.glob("*.hip")) if not x.stem.startswith("tool_")]
             _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-I" + str(src), str(s), *others,
-                  "-o", str(out)], verbose)
+                  "-L" + str(ROCM / "lib"), "-lhsa-runtime64", "-o", str(out)], verbose)
         outs.append(out)
     return outs
 
@@ -236,7 +236,7 @@ def build_tsan(force: bool = False, verbose: bool = False) -> list[Path]:
 
 def build_tools_tsan(force: bool = False, verbose: bool = False) -> list[Path]:
     """ThreadSanitizer builds of the compiled stand-ins (``build/gsx-{fakeapi,schedsim,nodeagent}_tsan``);
-    ``GSX_NATIVE_TOOLS_SUFFIX=_tsan`` makes sim/cluster.py start these instead of the optimised ones."""
+    ``GSX_NATIVE_TOOLS_SUFFIX=_tsan`` makes gsxtools/cluster.py start these instead of the optimised ones."""
     src = NATIVE / "engine"
     lib = [s for s in sorted(src.glob("*.cc")) if s.name != "bindings.cc" and s.name not in TEST_MAINS]
     outs = []

@@ -1,5 +1,7 @@
 #include "allocstate.h"
 
+#include <chrono>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
@@ -241,9 +243,15 @@ AllocState::AllocState(std::string node, const std::vector<std::pair<int, std::p
 
 bool AllocState::observe(const AllocPod& p) {
   if (p.uid.empty()) return false;
+  if (gone_.count(p.uid)) return false;  // deleted or complete: a late copy never brings it back
   auto prev = pods_.find(p.uid);
   if (prev != pods_.end() && older_rv(p.rv, prev->second.rv)) return false;  // a slow LIST racing the watch
-  if (p.node != node_ || p.request <= 0 || p.complete) {
+  if (p.complete) {
+    tombstone(p.uid);
+    release(p.uid);
+    return true;
+  }
+  if (p.node != node_ || p.request <= 0) {
     release(p.uid);
     return true;
   }
@@ -309,6 +317,23 @@ void AllocState::release(const std::string& uid) {
       if (cur->second.uid == uid) unhold(cur);
     }
   }
+}
+
+void AllocState::tombstone(const std::string& uid) {
+  if (uid.empty()) return;
+  const double now = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  while (!gone_order_.empty() && (gone_order_.front().first < now - kTombstoneS || gone_order_.size() > 200000)) {
+    auto it = gone_.find(gone_order_.front().second);
+    if (it != gone_.end() && it->second == gone_order_.front().first) gone_.erase(it);
+    gone_order_.pop_front();
+  }
+  gone_[uid] = now;
+  gone_order_.emplace_back(now, uid);
+}
+
+void AllocState::deleted(const std::string& uid) {
+  tombstone(uid);
+  release(uid);
 }
 
 std::vector<std::string> AllocState::holders() const {

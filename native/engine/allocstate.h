@@ -32,6 +32,7 @@
 #pragma once
 
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <string>
 #include <unordered_map>
@@ -119,6 +120,14 @@ class AllocState {
   // An added / updated pod.  Returns false if ignored as a stale copy (older resourceVersion).
   bool observe(const AllocPod& p);
   void release(const std::string& uid);  // completed / deleted
+  // A pod the apiserver deleted (a watch DELETE): released, and its UID remembered, so that a copy of it still in
+  // flight (a second feed that lags, a PATCH response read after the delete) cannot bring it back with its CU
+  // partition.  UIDs are never reused; a complete pod is remembered the same way (terminal phases and deletion
+  // timestamps are never undone).  Kept for kTombstoneS seconds.
+  void deleted(const std::string& uid);
+  void tombstone(const std::string& uid);
+  bool is_tombstoned(const std::string& uid) const { return gone_.count(uid) != 0; }
+  static constexpr double kTombstoneS = 600.0;
   // A complete LIST of this node's pods (already observed): anything held that is not in `live` is gone.
   void resync(const std::unordered_set<std::string>& live);
   std::vector<std::string> holders() const;
@@ -185,6 +194,8 @@ class AllocState {
   std::string node_;
   std::map<int, CuPartitioner> cus_;
   std::unordered_map<std::string, AllocPod> pods_;        // uid -> non-complete pods on this node
+  std::unordered_map<std::string, double> gone_;          // deleted / complete UIDs -> when (see deleted())
+  std::deque<std::pair<double, std::string>> gone_order_;
   std::unordered_map<std::string, std::string> keys_;     // ns/name -> uid
   std::unordered_map<std::string, std::vector<int64_t>> partial_;  // uid -> container sizes not yet allocated
   std::unordered_set<std::string> local_commits_, inflight_;

@@ -15,6 +15,7 @@
 #include <condition_variable>
 #include <deque>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <thread>
 
@@ -329,8 +330,8 @@ class Engine {
   }
 
   // ---- native HTTP front end (server.h) ----
-  int serve(const std::string& host, int port, int threads, int pool_threads, int fallback_port, bool native_bind,
-            double ttl, const py::dict& api, bool update_mode) {
+  int serve(const std::string& host, int port, int threads, int pool_threads, int fallback_port, double ttl,
+            const py::dict& api, bool update_mode, double qps, int burst) {
     if (srv_) throw std::runtime_error("native server already running");
     ServerConfig cfg;
     cfg.host = host;
@@ -338,12 +339,14 @@ class Engine {
     cfg.threads = threads;
     cfg.pool_threads = pool_threads;
     cfg.fallback_port = fallback_port;
-    cfg.native_bind = native_bind;
     cfg.update_mode = update_mode;
     cfg.reservation_ttl = ttl;
+    cfg.qps = qps;
+    cfg.burst = burst;
     cfg.api = api_from(api);
-    if (cfg.api.server.empty()) cfg.native_bind = false;
     srv_.reset(new NativeServer(&l_, cfg));
+    // the controller outlives the server (stop_server runs before stop_controller)
+    srv_->set_lister([this](const std::string& key, std::string* raw) { return ctl_ && ctl_->get_pod(key, raw); });
     srv_->set_binds_enabled(binds_enabled_);
     if (update_mode_) srv_->set_update_mode(true);
     std::string err;
@@ -453,6 +456,9 @@ class Engine {
     d["api_calls"] = s.api_calls.load();
     d["conflicts_retried"] = s.conflicts_retried.load();
     d["moves"] = s.moves.load();
+    d["unfiltered_binds"] = s.unfiltered_binds.load();
+    d["live_gets"] = s.live_gets.load();
+    d["qps_waits"] = s.qps_waits.load();
     d["moves_failed"] = s.moves_failed.load();
     auto hist = [](const LatencyHist& h) {
       py::dict o;
@@ -599,6 +605,87 @@ class PyPodTracker {
 
  private:
   PodTracker t_;
+};
+
+// The reflector the extender's controller and the plugin's pod feed run, with a plain key -> resourceVersion
+// view: tests/test_k8s.py holds it against the Python informer the device plugin still runs (the one Python
+// twin left, fenced by that cross-check).
+class PyReflectorProbe {
+ public:
+  PyReflectorProbe(const py::dict& api, const std::string& path, const std::string& field_selector, int page) {
+    ReflectorConfig rc;
+    rc.path = path;
+    rc.field_selector = field_selector;
+    rc.list_page_size = page;
+    ReflectorHandler h;
+    h.on_list = [this](const ListView& lv) {
+      std::map<std::string, std::string> fresh;
+      for (size_t k = 0; k < lv.size(); ++k) {
+        std::string key, rv;
+        if (key_rv(lv.doc(k), lv.obj(k), &key, &rv)) fresh[key] = rv;
+      }
+      std::lock_guard<std::mutex> g(mu_);
+      view_.swap(fresh);
+      lists_++;
+    };
+    h.on_event = [this](Ev ev, const json::Doc& d, uint32_t obj) {
+      std::string key, rv;
+      if (!key_rv(d, obj, &key, &rv)) return;
+      std::lock_guard<std::mutex> g(mu_);
+      if (ev == Ev::Deleted) {
+        view_.erase(key);
+      } else {
+        view_[key] = rv;
+      }
+      events_++;
+    };
+    r_ = std::make_unique<Reflector>(api_from(api), rc, h);
+  }
+  ~PyReflectorProbe() { stop(); }
+  void start() { r_->start(); }
+  void stop() {
+    if (r_) {
+      py::gil_scoped_release rel;
+      r_->stop();
+    }
+  }
+  bool wait_synced(double t) {
+    py::gil_scoped_release rel;
+    return r_->wait_synced(t);
+  }
+  void request_relist() { r_->request_relist(); }
+  py::dict view() {
+    py::dict d;
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : view_) d[py::str(kv.first)] = kv.second;
+    return d;
+  }
+  py::dict stats() {
+    py::dict d;
+    d["relists"] = r_->relists();
+    d["rewatches"] = r_->rewatches();
+    d["errors"] = r_->errors();
+    d["resource_version"] = r_->resource_version();
+    std::lock_guard<std::mutex> g(mu_);
+    d["lists"] = lists_;
+    d["events"] = events_;
+    return d;
+  }
+
+ private:
+  static bool key_rv(const json::Doc& d, uint32_t obj, std::string* key, std::string* rv) {
+    int64_t n = d.path(obj, {"metadata", "name"});
+    if (n < 0) return false;
+    int64_t ns = d.path(obj, {"metadata", "namespace"});
+    int64_t r = d.path(obj, {"metadata", "resourceVersion"});
+    *key = (ns >= 0 ? d.str(static_cast<uint32_t>(ns)) + "/" : std::string()) + d.str(static_cast<uint32_t>(n));
+    *rv = r >= 0 ? d.str(static_cast<uint32_t>(r)) : std::string();
+    return true;
+  }
+  std::unique_ptr<Reflector> r_;
+  std::mutex mu_;
+  std::map<std::string, std::string> view_;
+  uint64_t lists_ = 0, events_ = 0;
 };
 
 class PyBatchClient {
@@ -1121,7 +1208,7 @@ class PyDpServer {
         }
         state_->resync(live);
       } else if (f.deleted) {
-        for (const auto& ap : f.pods) state_->release(ap.uid);
+        for (const auto& ap : f.pods) state_->deleted(ap.uid);
       } else {
         for (const auto& ap : f.pods) state_->observe(ap);
       }
@@ -1401,8 +1488,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("stats", &Engine::stats)
       .def("parse_pod", &Engine::parse_pod)
       .def("serve", &Engine::serve, py::arg("host"), py::arg("port"), py::arg("threads") = 2,
-           py::arg("pool_threads") = 16, py::arg("fallback_port") = 0, py::arg("native_bind") = true,
-           py::arg("ttl") = 60.0, py::arg("api") = py::dict(), py::arg("update_mode") = false)
+           py::arg("pool_threads") = 16, py::arg("fallback_port") = 0, py::arg("ttl") = 60.0,
+           py::arg("api") = py::dict(), py::arg("update_mode") = false, py::arg("qps") = 0.0, py::arg("burst") = 10)
       .def("stop_server", &Engine::stop_server)
       .def("start_controller", &Engine::start_controller, py::arg("api"), py::arg("resync") = 30.0,
            py::arg("sync_timeout") = 60.0, py::arg("watch_timeout") = 300)
@@ -1431,6 +1518,16 @@ PYBIND11_MODULE(_engine, m) {
   m.attr("TRACK_BOUND") = static_cast<int>(PodTracker::Bound);
   m.attr("TRACK_RUNNING") = static_cast<int>(PodTracker::Running);
   m.attr("TRACK_GONE") = static_cast<int>(PodTracker::Gone);
+  py::class_<PyReflectorProbe>(m, "ReflectorProbe")
+      .def(py::init<const py::dict&, const std::string&, const std::string&, int>(), py::arg("api"),
+           py::arg("path") = "/api/v1/pods", py::arg("field_selector") = "", py::arg("page") = 500)
+      .def("start", &PyReflectorProbe::start)
+      .def("stop", &PyReflectorProbe::stop)
+      .def("wait_synced", &PyReflectorProbe::wait_synced, py::arg("timeout") = 10.0)
+      .def("request_relist", &PyReflectorProbe::request_relist)
+      .def("view", &PyReflectorProbe::view)
+      .def("stats", &PyReflectorProbe::stats);
+
   py::class_<PyBatchClient>(m, "BatchClient")
       .def(py::init<const py::dict&>())
       .def("run", &PyBatchClient::run, py::arg("requests"), py::arg("concurrency") = 8);
@@ -1527,6 +1624,8 @@ PYBIND11_MODULE(_engine, m) {
            py::arg("node"), py::arg("devices"))
       .def("observe", &AllocState::observe, py::call_guard<AllocLock>())
       .def("release", &AllocState::release, py::call_guard<AllocLock>())
+      .def("deleted", &AllocState::deleted, py::call_guard<AllocLock>())
+      .def("is_tombstoned", &AllocState::is_tombstoned, py::call_guard<AllocLock>())
       .def("resync", [](AllocState& s, const std::vector<std::string>& live) {
         s.resync(std::unordered_set<std::string>(live.begin(), live.end()));
       }, py::call_guard<AllocLock>())

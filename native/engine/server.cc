@@ -68,6 +68,33 @@ bool arg_str(const json::Doc& d, const char* key, std::string* out) {
   return true;
 }
 
+// encoding/json's name for a JSON value that cannot fill a Go string field
+const char* go_json_type(json::T t) {
+  switch (t) {
+    case json::T::Object: return "object";
+    case json::T::Array: return "array";
+    case json::T::True:
+    case json::T::False: return "bool";
+    default: return "number";
+  }
+}
+
+// ExtenderBindingArgs (types.go:287-296) as encoding/json decodes it: keys match case-insensitively, null leaves
+// a field empty, any other non-string is the decoder's type error
+bool binding_args(const json::Doc& d, std::string* name, std::string* ns, std::string* uid, std::string* node,
+                  std::string* err) {
+  const char* keys[4] = {"PodName", "PodNamespace", "PodUID", "Node"};
+  std::string* outs[4] = {name, ns, uid, node};
+  for (int k = 0; k < 4; ++k) {
+    if (arg_str(d, keys[k], outs[k])) continue;
+    int64_t i = d.find(0, keys[k], true);
+    *err = std::string("json: cannot unmarshal ") + go_json_type(d.at(static_cast<uint32_t>(i)).type) +
+           " into Go struct field ExtenderBindingArgs." + keys[k] + " of type string";
+    return false;
+  }
+  return true;
+}
+
 std::string status_message(const std::string& body, int status) {
   json::Doc d;
   std::string e;
@@ -126,7 +153,7 @@ NativeServer::~NativeServer() { stop(); }
 int NativeServer::start(std::string* err) {
   if (cfg_.threads < 1) cfg_.threads = 1;
   if (cfg_.pool_threads < 1) cfg_.pool_threads = 1;
-  if (cfg_.native_bind) {
+  if (!cfg_.api.server.empty()) {
     api_.reset(new ApiClient(cfg_.api));
     if (!api_->ok()) {
       *err = "apiserver client: " + api_->init_error();
@@ -506,11 +533,7 @@ void NativeServer::pool_main() {
     const bool ka = j.req.keep_alive;
     try {
       if (j.kind == 0) {
-        bool fallback = false;
-        resp = do_bind(j.req, &fallback);
-        if (fallback) {
-          resp = do_proxy(j.req);
-        }
+        resp = do_bind(j.req);
         stats_.bind_lat.observe(mono() - j.t0);
       } else if (j.kind == 2) {
         resp = do_move(j.req);
@@ -547,15 +570,11 @@ std::string NativeServer::do_proxy(const http::Message& req) {
 
 // Native bind: reserve on the ledger, then one POST pods/{name}/binding whose
 // metadata.annotations carry the allocation record (pkg/utils/pod.go:192-206).
-std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
-  *fallback = false;
+std::string NativeServer::do_bind(const http::Message& req) {
   if (!binds_enabled_.load()) {
     return bind_error_response("this extender replica is not the leader");
   }
-  if (!cfg_.native_bind || !api_) {
-    *fallback = true;
-    return {};
-  }
+  if (!api_) return bind_error_response("the extender has no apiserver client");
   json::Doc d;
   std::string perr;
   if (!d.parse(req.body, &perr)) return bind_error_response(perr);
@@ -563,22 +582,29 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
     return bind_error_response("json: cannot unmarshal value into Go value of type api.ExtenderBindingArgs");
   }
   std::string name, ns, uid, node;
-  if (!arg_str(d, "PodName", &name) || !arg_str(d, "PodNamespace", &ns) || !arg_str(d, "PodUID", &uid) ||
-      !arg_str(d, "Node", &node)) {
-    *fallback = true;  // let the Python decoder produce Go's exact type error
-    return {};
-  }
+  if (!binding_args(d, &name, &ns, &uid, &node, &perr)) return bind_error_response(perr);
   Ledger::PendingPod pp;
-  int64_t dev, dev_total = -1, assume_ns = 0;
+  int64_t dev = -1, dev_total = -1, assume_ns = 0;
   uint64_t seq = 0;
   const Profile& prof = l_->profile();
+  bool filtered;
   {
     std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
-    if (!l_->pending(uid, &pp) || pp.name != name || pp.ns != ns) {
-      *fallback = true;  // never filtered here (e.g. restart between filter and bind): slow path
-      return {};
+    filtered = l_->pending(uid, &pp) && pp.name == name && pp.ns == ns;
+    // reservation, ASSUME_TIME and the ordering sequence in one step
+    if (filtered) dev = l_->assume_ordered(uid, ns, name, node, pp.req, &dev_total, &seq, &assume_ns, pp.cu_count);
+  }
+  if (!filtered) {
+    // never filtered here (a restart between filter and bind, another replica's filter): the pod's request
+    // comes from the lister or the apiserver
+    stats_.unfiltered_binds.fetch_add(1, std::memory_order_relaxed);
+    std::string err;
+    if (!lookup_pod(ns, name, uid, false, &pp, &err)) {
+      stats_.bind_fail.fetch_add(1, std::memory_order_relaxed);
+      record_failure(BindFailure{ns, name, uid, node, err});
+      return bind_error_response(err);
     }
-    // reservation, ASSUME_TIME and the ordering sequence in one step, shared with the Python slow path
+    std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
     dev = l_->assume_ordered(uid, ns, name, node, pp.req, &dev_total, &seq, &assume_ns, pp.cu_count);
   }
   if (dev < 0) {
@@ -622,10 +648,7 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
   auto call = [&](const char* method, const std::string& target, const std::string& body, const char* ct,
                   int* status, std::string* resp) {
     std::string err;
-    double t0 = mono();
-    stats_.api_calls.fetch_add(1, std::memory_order_relaxed);
-    bool sent = api_->request(method, target, body, ct, status, resp, &err);
-    stats_.api_lat.observe(mono() - t0);
+    bool sent = api_call(method, target, body, ct, status, resp, &err);
     if (!sent) msg = err;
     return sent;
   };
@@ -696,12 +719,12 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
     }
     msg = status_message(body, status);
     if (status == 409 && msg.find("Precondition failed") != std::string::npos) {
-      // UID mismatch: release and let the slow path produce the reference's
-      // exact error (gpushare-bind.go:44-65 does a live GET).
-      std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
-      l_->finish_bind(uid, false, 0.0);
-      *fallback = true;
-      return {};
+      // UID mismatch (the pod was re-created under its name): the reference's exact error comes from a live
+      // GET (gpushare-bind.go:44-65)
+      Ledger::PendingPod live;
+      std::string err;
+      if (!lookup_pod(ns, name, uid, true, &live, &err)) msg = err;
+      break;
     }
     if (status == 409 && msg.find("already assigned") == std::string::npos && attempt < 2) {
       stats_.conflicts_retried.fetch_add(1, std::memory_order_relaxed);
@@ -722,6 +745,81 @@ std::string NativeServer::do_bind(const http::Message& req, bool* fallback) {
   }
   stats_.bind_ok.fetch_add(1, std::memory_order_relaxed);
   return http::response(200, "application/json", "{\"Error\":\"\"}", true);
+}
+
+void NativeServer::throttle() {
+  if (cfg_.qps <= 0) return;
+  double wait;
+  {
+    std::lock_guard<std::mutex> g(qmu_);
+    const double now = mono();
+    const double burst = std::max(1, cfg_.burst);
+    if (q_last_ == 0.0) q_tokens_ = burst;
+    q_tokens_ = std::min(burst, q_tokens_ + (now - q_last_) * cfg_.qps);
+    q_last_ = now;
+    q_tokens_ -= 1.0;  // reserved now, so waiters queue in arrival order
+    wait = q_tokens_ < 0 ? -q_tokens_ / cfg_.qps : 0.0;
+  }
+  if (wait > 0) {
+    stats_.qps_waits.fetch_add(1, std::memory_order_relaxed);
+    std::this_thread::sleep_for(std::chrono::duration<double>(wait));
+  }
+}
+
+bool NativeServer::api_call(const char* method, const std::string& target, const std::string& body, const char* ct,
+                            int* status, std::string* resp, std::string* err) {
+  throttle();
+  double t0 = mono();
+  stats_.api_calls.fetch_add(1, std::memory_order_relaxed);
+  bool sent = api_->request(method, target, body, ct, status, resp, err);
+  stats_.api_lat.observe(mono() - t0);
+  return sent;
+}
+
+bool NativeServer::lookup_pod(const std::string& ns, const std::string& name, const std::string& uid, bool live,
+                              Ledger::PendingPod* out, std::string* err) {
+  std::string raw;
+  json::Doc d;
+  std::string perr;
+  auto uid_of = [&d]() {
+    int64_t u = d.path(0, {"metadata", "uid"});
+    return u >= 0 && d.at(static_cast<uint32_t>(u)).type == json::T::String ? d.str(static_cast<uint32_t>(u))
+                                                                             : std::string();
+  };
+  bool have = !live && lister_ && lister_(ns + "/" + name, &raw) && d.parse(raw, &perr) &&
+              d.at(0).type == json::T::Object && uid_of() == uid;
+  if (!have) {
+    stats_.live_gets.fetch_add(1, std::memory_order_relaxed);
+    int status = 0;
+    raw.clear();
+    if (!api_call("GET", "/api/v1/namespaces/" + url_escape_path(ns) + "/pods/" + url_escape_path(name), "",
+                  "application/json", &status, &raw, err)) {
+      return false;
+    }
+    if (status != 200) {
+      *err = status_message(raw, status);
+      return false;
+    }
+    if (!d.parse(raw, &perr) || d.at(0).type != json::T::Object) {
+      *err = "apiserver returned an unreadable pod: " + perr;
+      return false;
+    }
+    const std::string puid = uid_of();
+    if (puid != uid) {
+      *err = "The pod " + name + " in ns " + ns + "'s uid is " + puid + ", and it's not equal with expected " + uid;
+      return false;
+    }
+  }
+  out->ns = ns;
+  out->name = name;
+  out->req = pod_limits_sum(d, 0, l_->profile().resource);
+  out->cu_count.clear();
+  out->rv.clear();
+  int64_t cu = d.path(0, {"metadata", "annotations", kCuCountAnnotation});
+  if (cu >= 0 && d.at(static_cast<uint32_t>(cu)).type == json::T::String) out->cu_count = d.str(static_cast<uint32_t>(cu));
+  int64_t rv = d.path(0, {"metadata", "resourceVersion"});
+  if (rv >= 0 && d.at(static_cast<uint32_t>(rv)).type == json::T::String) out->rv = d.str(static_cast<uint32_t>(rv));
+  return true;
 }
 
 // The device plugin's allocation-record writes (deviceplugin/reconcile.py, plugin.py move_unstarted): the extender
@@ -792,10 +890,7 @@ std::string NativeServer::do_move(const http::Message& req) {
   const std::string target = "/api/v1/namespaces/" + url_escape_path(ns) + "/pods/" + url_escape_path(name);
   int status = 0;
   std::string body, err;
-  double t0 = mono();
-  stats_.api_calls.fetch_add(1, std::memory_order_relaxed);
-  const bool sent = api_->request("PATCH", target, patch, "application/merge-patch+json", &status, &body, &err);
-  stats_.api_lat.observe(mono() - t0);
+  const bool sent = api_call("PATCH", target, patch, "application/merge-patch+json", &status, &body, &err);
   const bool ok = sent && status >= 200 && status < 300;
   {
     std::lock_guard<introspect::ProfiledMutex> g(l_->mu());

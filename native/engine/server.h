@@ -10,10 +10,12 @@
 //   GET  /gpushare-scheduler/inspect  native
 //   GET  /version                     native
 //
-// Anything else (/metrics, /debug/pprof/*, /healthz, and binds the native
-// path cannot decide: pod never filtered here, "update" bind mode, UID
-// precondition failures) is proxied to the Python aiohttp app on a loopback
-// port, so the observable API is one server.
+// Every bind is decided here, including the ones the filter never saw (the pod
+// then comes from the controller's lister or one live GET, gpushare-bind.go:
+// 44-65) and both bind modes; a client-side QPS limit (--kube-qps) is a token
+// bucket in front of every apiserver call this server makes.  Anything else
+// (/metrics, /debug/pprof/*, /healthz) is proxied to the Python aiohttp app on
+// a loopback port, so the observable API is one server.
 //
 // Design: N event-loop threads, each with its own SO_REUSEPORT listening
 // socket and epoll set (the kernel spreads connections); blocking work (the
@@ -47,11 +49,13 @@ struct ServerConfig {
   int threads = 2;
   int pool_threads = 16;
   int fallback_port = 0;      // Python app on 127.0.0.1 (0: none)
-  bool native_bind = true;
   // bind_mode "update": the reference's two calls, annotate the pod (merge patch, resourceVersion precondition,
   // one retry on the optimistic-lock conflict) then POST a plain Binding (pkg/cache/nodeinfo.go:145-189)
   bool update_mode = false;
   double reservation_ttl = 60.0;
+  // client-side apiserver rate limit of the bind / move calls (client-go's QPS / Burst); qps <= 0: unlimited
+  double qps = 0.0;
+  int burst = 10;
   ApiConfig api;
   size_t max_body = 64u << 20;
 };
@@ -74,7 +78,8 @@ struct LatencyHist {
 
 struct ServerStats {
   std::atomic<uint64_t> requests{0}, filters{0}, binds{0}, bind_ok{0}, bind_fail{0}, proxied{0}, bad_requests{0},
-      inspects{0}, connections{0}, api_calls{0}, conflicts_retried{0}, bind_order_waits{0}, moves{0}, moves_failed{0};
+      inspects{0}, connections{0}, api_calls{0}, conflicts_retried{0}, bind_order_waits{0}, moves{0}, moves_failed{0},
+      unfiltered_binds{0}, live_gets{0}, qps_waits{0};
   LatencyHist filter_lat, bind_lat, api_lat;
 };
 
@@ -94,6 +99,9 @@ class NativeServer {
   void set_update_mode(bool on) { update_mode_.store(on); }
   bool update_mode() const { return update_mode_.load(); }
   bool binds_enabled() const { return binds_enabled_.load(); }
+  // the controller's lister: raw JSON of the pod "ns/name" (false: not held).  Set before start().
+  using Lister = std::function<bool(const std::string& key, std::string* raw)>;
+  void set_lister(Lister f) { lister_ = std::move(f); }
 
  private:
   struct Loop;
@@ -118,7 +126,15 @@ class NativeServer {
   void drain_completions(Loop* lp);
   void pool_main();
   void submit(Job j);
-  std::string do_bind(const http::Message& req, bool* fallback);
+  std::string do_bind(const http::Message& req);
+  // the pod of a bind the filter did not see here: lister first, one live GET when the lister does not hold
+  // it under that UID; false with the reference's error string (gpushare-bind.go:44-65)
+  bool lookup_pod(const std::string& ns, const std::string& name, const std::string& uid, bool live,
+                  Ledger::PendingPod* out, std::string* err);
+  // one apiserver call behind the QPS limit
+  bool api_call(const char* method, const std::string& target, const std::string& body, const char* ct, int* status,
+                std::string* resp, std::string* err);
+  void throttle();
   std::string do_proxy(const http::Message& req);
   std::string do_move(const http::Message& req);
   std::string bind_error_response(const std::string& msg) const;
@@ -138,6 +154,9 @@ class NativeServer {
   std::deque<Job> jobs_;
   std::unique_ptr<ApiClient> api_;
   std::unique_ptr<ApiClient> fallback_;
+  Lister lister_;
+  std::mutex qmu_;  // token bucket
+  double q_tokens_ = 0.0, q_last_ = 0.0;
   std::mutex fmu_;
   std::vector<BindFailure> failures_;
   ServerStats stats_;

@@ -1,17 +1,25 @@
 // gsx-memprobe: how much device memory does this process (pod) get?
 //
 //   gsx-memprobe [--device N] [--alloc BYTES[,BYTES...]] [--hold-ms MS] [--touch]
-//                [--api malloc|async|finegrained|pitch|vmem|host]
+//                [--api malloc|async|finegrained|pitch|vmem|host] [--scratch KIB --blocks N]
 //
 // --api picks the allocation entry point (the isolation library must cap every one that takes HBM):
 // hipMalloc, hipMallocAsync (stream-ordered pool), hipExtMallocWithFlags(fine-grained), hipMallocPitch,
 // hipMemCreate (the virtual-memory API PyTorch's expandable segments use), or hipHostMalloc (host memory,
 // which is not the device's and must not count).
 //
+// --scratch launches, after the allocations, a kernel whose every lane keeps a KIB-KiB private array (1, 4, 16
+// or 64) in scratch, over N 256-lane workgroups: the runtime sizes the queue's scratch for it behind any
+// allocation API.  The JSON then carries the launch status and this process's VRAM as the kernel driver counts
+// it (/sys/class/kfd/kfd/proc/<pid>/vram_*) before and after.
+//
 // Prints hipMemGetInfo before and after, then tries each allocation in turn (kept until exit) and prints one
 // JSON line.  Operators run it inside a pod to see the HBM share the device plugin's isolation library enforces
 // (native/isolate/gsx_isolate.cc); tests/test_gpu_isolate.py drives it against the share and past it.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <dirent.h>
 #include <unistd.h>
 
 #include <cstdio>
@@ -76,10 +84,86 @@ void free_one(const Held& h) {
   }
 }
 
+template <int N>
+__global__ void __launch_bounds__(256) scratch_kernel(int* out, int seed) {
+  volatile int a[N];  // volatile + a data-dependent index: the array cannot live in registers
+  const int t = static_cast<int>(threadIdx.x);
+  for (int i = t % 64; i < N; i += 64) a[i] = seed + i + t;
+  int s = 0;
+  for (int i = 0; i < N; i += 64) s += a[(i + seed * t) & (N - 1)];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+// this process's VRAM as amdkfd accounts it (every GPU it has opened); -1 if the file is not there
+long long kfd_vram() {
+  char dir[128];
+  std::snprintf(dir, sizeof dir, "/sys/class/kfd/kfd/proc/%d", static_cast<int>(getpid()));
+  DIR* d = opendir(dir);
+  if (!d) return -1;
+  long long sum = -1;
+  while (dirent* e = readdir(d)) {
+    if (std::strncmp(e->d_name, "vram_", 5) != 0) continue;
+    char path[512];
+    std::snprintf(path, sizeof path, "%s/%s", dir, e->d_name);
+    FILE* f = std::fopen(path, "r");
+    if (!f) continue;
+    long long v = 0;
+    if (std::fscanf(f, "%lld", &v) == 1) sum = (sum < 0 ? 0 : sum) + v;
+    std::fclose(f);
+  }
+  closedir(d);
+  return sum;
+}
+
+// the HSA runtime's scratch thresholds for the first GPU agent (HIP has initialised the runtime already)
+struct ScratchLimits {
+  uint64_t max = 0, current = 0;
+  hsa_agent_t agent{};
+  bool found = false;
+};
+
+hsa_status_t find_gpu(hsa_agent_t a, void* data) {
+  auto* sl = static_cast<ScratchLimits*>(data);
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU) {
+    return HSA_STATUS_SUCCESS;
+  }
+  sl->agent = a;
+  sl->found = true;
+  (void)hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX), &sl->max);
+  (void)hsa_agent_get_info(a, static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_CURRENT), &sl->current);
+  return HSA_STATUS_INFO_BREAK;
+}
+
+ScratchLimits scratch_limits() {
+  ScratchLimits sl;
+  (void)hsa_iterate_agents(find_gpu, &sl);
+  return sl;
+}
+
+hipError_t run_scratch(int kib, int blocks) {
+  int* out = nullptr;
+  hipError_t r = hipMalloc(&out, static_cast<size_t>(blocks) * 256 * sizeof(int));
+  if (r != hipSuccess) return r;
+  switch (kib) {
+    case 1: scratch_kernel<256><<<blocks, 256>>>(out, 3); break;
+    case 4: scratch_kernel<1024><<<blocks, 256>>>(out, 3); break;
+    case 16: scratch_kernel<4096><<<blocks, 256>>>(out, 3); break;
+    case 64: scratch_kernel<16384><<<blocks, 256>>>(out, 3); break;
+    default: (void)hipFree(out); return hipErrorInvalidValue;
+  }
+  r = hipGetLastError();
+  hipError_t s = hipDeviceSynchronize();
+  if (r == hipSuccess) r = s;
+  (void)hipFree(out);
+  return r;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
-  int dev = 0, hold_ms = 0;
+  int dev = 0, hold_ms = 0, scratch_kib = 0, blocks = 8192;
+  long long set_limit = -1;
   bool touch = false;
   std::string api = "malloc";
   std::vector<size_t> sizes;
@@ -99,10 +183,16 @@ int main(int argc, char** argv) {
       hold_ms = std::atoi(argv[++i]);
     } else if (!std::strcmp(argv[i], "--touch")) {
       touch = true;
+    } else if (!std::strcmp(argv[i], "--scratch") && i + 1 < argc) {
+      scratch_kib = std::atoi(argv[++i]);
+    } else if (!std::strcmp(argv[i], "--scratch-limit") && i + 1 < argc) {
+      set_limit = std::atoll(argv[++i]);
+    } else if (!std::strcmp(argv[i], "--blocks") && i + 1 < argc) {
+      blocks = std::atoi(argv[++i]);
     } else if (!std::strcmp(argv[i], "--api") && i + 1 < argc) {
       api = argv[++i];
     } else {
-      std::fprintf(stderr, "usage: %s [--device N] [--alloc B,...] [--hold-ms MS] [--touch] [--api A]\n", argv[0]);
+      std::fprintf(stderr, "usage: %s [--device N] [--alloc B,...] [--hold-ms MS] [--touch] [--api A] [--scratch KIB --blocks N --scratch-limit B]\n", argv[0]);
       return 2;
     }
   }
@@ -129,10 +219,34 @@ int main(int argc, char** argv) {
                   ok ? "true" : "false", ok ? "" : hipGetErrorName(r));
     rows += buf;
   }
+  std::string scratch = "null";
+  if (scratch_kib > 0) {
+    if (set_limit >= 0) {
+      ScratchLimits sl = scratch_limits();
+      if (sl.found) (void)hsa_amd_agent_set_async_scratch_limit(sl.agent, static_cast<size_t>(set_limit));
+    }
+    long long v0 = kfd_vram();
+    hipError_t r = run_scratch(scratch_kib, blocks);
+    (void)hipGetLastError();
+    long long v1 = kfd_vram();
+    size_t f = 0, t = 0;
+    (void)hipMemGetInfo(&f, &t);
+    char buf[512];
+    std::snprintf(buf, sizeof buf,
+                  "{\"kib_per_lane\":%d,\"blocks\":%d,\"ok\":%s,\"err\":\"%s\",\"kfd_vram_before\":%lld,"
+                  "\"kfd_vram_after\":%lld,\"free_after\":%zu}",
+                  scratch_kib, blocks, r == hipSuccess ? "true" : "false", r == hipSuccess ? "" : hipGetErrorName(r), v0,
+                  v1, f);
+    scratch = buf;
+  }
   size_t free1 = 0, total1 = 0;
   (void)hipMemGetInfo(&free1, &total1);
+  ScratchLimits sl = scratch_limits();
   std::printf("{\"device\":%d,\"api\":\"%s\",\"total\":%zu,\"free\":%zu,\"allocs\":[%s],\"free_after\":%zu,"
-              "\"total_after\":%zu}\n", dev, api.c_str(), total0, free0, rows.c_str(), free1, total1);
+              "\"total_after\":%zu,\"scratch\":%s,\"kfd_vram\":%lld,\"scratch_limit_max\":%llu,"
+              "\"scratch_limit_current\":%llu}\n", dev, api.c_str(), total0, free0, rows.c_str(), free1, total1,
+              scratch.c_str(), kfd_vram(), static_cast<unsigned long long>(sl.max),
+              static_cast<unsigned long long>(sl.current));
   std::fflush(stdout);
   if (hold_ms > 0) usleep(static_cast<useconds_t>(hold_ms) * 1000u);
   for (const Held& h : held) free_one(h);

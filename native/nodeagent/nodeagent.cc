@@ -388,6 +388,7 @@ class Agent {
     std::string uid = it->second;
     keys_.erase(it);
     stop_pod_locked(uid);
+    state_->tombstone(uid);  // a late copy of it (a PATCH response) never re-queues it
     if (!state_->inflight(uid)) state_->release(uid);  // the admitting worker owns it until its patch resolves
   }
 

@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -m gpushare_scheduler_extender_amd.sim.isolation --seconds 6 \
+timeout -k 10 900 python -m gsxtools.isolation --seconds 6 \
   --json-out gpurun_out/isolation.json > gpurun_out/isolation.log 2>&1; rc=$?
 cat gpurun_out/isolation.log | tail -12
 exit $rc

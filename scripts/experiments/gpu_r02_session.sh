@@ -13,7 +13,7 @@ ok $rc || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1; rc=$?
 echo "smoke rc=$rc"; tail -1 $OUT/smoke.log
 ok $rc || exit $rc
-timeout -k 10 600 python -m gpushare_scheduler_extender_amd.sim.scale --json-out $OUT/scale.json > $OUT/scale.log 2>&1; rc=$?
+timeout -k 10 600 python -m gsxtools.scale --json-out $OUT/scale.json > $OUT/scale.log 2>&1; rc=$?
 echo "scale rc=$rc"; cut -c1-300 $OUT/scale.log
 for i in 1 2 3; do
   timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --json-out $OUT/bench$i.json > $OUT/bench$i.log 2>&1; rc=$?

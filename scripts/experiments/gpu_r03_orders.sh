@@ -22,6 +22,6 @@ for k in standin faithful; do
 import json; d=json.load(open('$OUT/plugin_$k.json')); na=d['node_agent']
 print('plugin', '$k', d['value'], na.get('admit_p50_ms'), na.get('breakdown_ms'), na.get('plugin_breakdown_ms'), na.get('reconcile'))"
 done
-timeout -k 10 300 python -m gpushare_scheduler_extender_amd.sim.configs --only 3 --faithful --api-latency-ms 5 \
+timeout -k 10 300 python -m gsxtools.configs --only 3 --faithful --api-latency-ms 5 \
   --json-out $OUT/config3_faithful_5ms.json > $OUT/config3_faithful.log 2>&1 || exit $?
 tail -2 $OUT/config3_faithful.log

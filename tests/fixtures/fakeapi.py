@@ -1,6 +1,6 @@
 """Test fixture: in-process fake kube-apiserver (pods, nodes, bindings, events) over real HTTP.
 
-Not shipped: the stack, ``sim/`` and ``bench.py`` run the compiled ``gsx-fakeapi`` (``native/fakeapi``), which
+Not shipped: the stack, ``gsxtools/`` and ``bench.py`` run the compiled ``gsx-fakeapi`` (``native/fakeapi``), which
 speaks the same REST subset.  This asyncio twin stays for tests that reach into the object store directly
 (``FakeApiServer``) or run the apiserver in the test's own event loop.  The reference was only ever validated
 by hand on a live cluster.  It speaks the

@@ -1,6 +1,6 @@
 """Test fixture: in-process kube-scheduler simulator speaking the extender protocol.
 
-Not shipped: ``sim/`` and ``bench.py`` run the compiled ``gsx-schedsim`` (``native/schedsim``), which replays the
+Not shipped: ``gsxtools/`` and ``bench.py`` run the compiled ``gsx-schedsim`` (``native/schedsim``), which replays the
 same cycle with C++ reflectors and bind threads; this asyncio twin stays for tests that drive scheduling from
 their own event loop.
 

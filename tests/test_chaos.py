@@ -14,7 +14,7 @@ from gpushare_scheduler_extender_amd.k8s.client import ApiError
 from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as HttpClient
 from gpushare_scheduler_extender_amd.models.profile import (ALIYUN, POD_HOLD_IDX_ANNOTATION,
                                                             POD_HOLD_PARTNER_ANNOTATION)
-from gpushare_scheduler_extender_amd.sim.configs import NODE, Cluster
+from gsxtools.configs import NODE, Cluster
 
 
 # kubelet's restart case through the compiled stand-in (--batch-window: pods met within 20 ms admitted as one
@@ -219,8 +219,7 @@ def test_extender_crash_restart_rebuilds_ledger_from_annotations():
     asyncio.run(go())
 
 
-@pytest.mark.parametrize("native_controller", [True, False])
-def test_reservation_gc_never_frees_a_device_behind_a_stalled_watch(native_controller):
+def test_reservation_gc_never_frees_a_device_behind_a_stalled_watch():
     """a bound reservation the informer has not confirmed within its TTL must not be dropped
     while the pod watch is stalled and LISTs fail (the device would look free while the pod holds it); once
     a LIST begun after the binding succeeds it decides: confirmed -> kept, absent -> expired."""
@@ -235,8 +234,8 @@ def test_reservation_gc_never_frees_a_device_behind_a_stalled_watch(native_contr
         api = await FakeApiServerRunner().start()
         c = KubeClient(api.url)
         await c.create("nodes", make_node("n", 100, 1))
-        srv = ExtenderServer(KubeClient(api.url), SHARED_GPU, reservation_ttl=0.2, native_controller=native_controller)
-        ext = await ExtenderRunner(srv, native=True).start()
+        srv = ExtenderServer(KubeClient(api.url), SHARED_GPU, reservation_ttl=0.2)
+        ext = await ExtenderRunner(srv).start()
         http = HttpClient(ext.url)
         eng = srv.engine
         try:

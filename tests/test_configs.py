@@ -1,4 +1,4 @@
-"""BASELINE.json configurations 1-5 and the hardware-partition scenario (6) through the whole stack (sim/configs.py):
+"""BASELINE.json configurations 1-5 and the hardware-partition scenario (6) through the whole stack (gsxtools/configs.py):
 CPU plumbing and, on MI355X, real device sizes, the HBM arena and hardware-verified CU partitions.
 
 The default kubelet + device-plugin path is the shipped gRPC plugin driven over its unix socket
@@ -7,7 +7,7 @@ import json
 
 import pytest
 
-from gpushare_scheduler_extender_amd.sim import configs
+from gsxtools import configs
 
 
 @pytest.mark.parametrize("k", sorted(configs.CONFIGS))
@@ -83,7 +83,7 @@ def test_node_agent_restart_keeps_cu_partitions_disjoint(agent):
 
     from gpushare_scheduler_extender_amd.deviceplugin.state import parse_cu_mask
     from gpushare_scheduler_extender_amd.models.profile import ALIYUN, POD_CU_MASK_ANNOTATION
-    from gpushare_scheduler_extender_amd.sim.cluster import start_node_agent
+    from gsxtools.cluster import start_node_agent
 
     async def go():
         cl = configs.Cluster(ALIYUN, [268], gpu=False, agent=agent)

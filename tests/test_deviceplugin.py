@@ -7,7 +7,7 @@ import pytest
 
 from gpushare_scheduler_extender_amd.deviceplugin import api
 from gpushare_scheduler_extender_amd.deviceplugin.allocator import CU_COUNT_ANNOTATION, CUPartitioner, build_response
-from gpushare_scheduler_extender_amd.deviceplugin.agent import NodeAgent
+from gsxtools.agent import NodeAgent
 from gpushare_scheduler_extender_amd.deviceplugin.devices import Device, discover, fake_devices
 from gpushare_scheduler_extender_amd.deviceplugin.plugin import FakeKubelet, GpuSharePlugin, PluginClient, fake_ids
 from gpushare_scheduler_extender_amd.deviceplugin.runtime import AdmissionError, LedgerRuntime
@@ -542,7 +542,7 @@ def test_process_runtime_starts_container_with_allocate_env():
     async def go():
         api = await FakeApiServerRunner().start()
         client = KubeClient(api.url)
-        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), P), native=True).start()
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), P)).start()
         devs = fake_devices("2x288GB")
         rt = ProcessRuntime([_sys.executable, "-c", code])
         agent = NodeAgent(KubeClient(api.url), "n1", devs, P, rt, unit="GiB")
@@ -626,7 +626,10 @@ class _PluginStack:
             if pred():
                 return
             await asyncio.sleep(0.01)
-        raise TimeoutError("condition not reached")
+        st = self.plugin.state
+        raise TimeoutError(f"condition not reached: cu holders {[sorted(c.held()) for c in st.cus.values()]}, "
+                           f"pods {sorted(st.pods)}, records {[(r.uid, r.dev) for r in st.records.values()] if not callable(st.records) else [(r.uid, r.dev) for r in st.records().values()]}, "
+                           f"stats {self.plugin.stats}")
 
     async def phase(self, name):
         return (await self.client.get("pods", name, "default"))["status"].get("phase")
@@ -637,6 +640,17 @@ class _PluginStack:
                 return await self.client.get("pods", name, "default")
             await asyncio.sleep(0.01)
         raise TimeoutError(f"{name} not {phase}: {await self.phase(name)}")
+
+    async def wait_committed(self, name, timeout=10.0):
+        """Running, and the plugin's commit (ASSIGNED=true with the CU mask) landed: with early answer (the
+        default) kubelet starts the container before the commit is written."""
+        await self.wait_phase(name, timeout=timeout)
+        for _ in range(int(timeout / 0.01)):
+            pod = await self.client.get("pods", name, "default")
+            if pod["metadata"].get("annotations", {}).get("SHARED_GPU_MEM_ASSIGNED") == "true":
+                return pod
+            await asyncio.sleep(0.01)
+        raise TimeoutError(f"{name}: the ASSIGNED commit never landed")
 
     async def __aexit__(self, *exc):
         await self.agent.stop()
@@ -661,7 +675,7 @@ def test_cu_partitions_are_released_when_pods_go_away():
             cu = {CU_COUNT_ANNOTATION: "64"}
             for i in range(4):
                 await s.client.create("pods", bound_pod(f"p{i}", 16, assume=i, annotations=cu))
-            pods = [await s.wait_phase(f"p{i}") for i in range(4)]
+            pods = [await s.wait_committed(f"p{i}") for i in range(4)]
             sets = [_cus_of(p) for p in pods]
             assert all(len(x) == 64 for x in sets) and len(set().union(*sets)) == 256
             assert s.plugin.state.cus[0].free_count() == 0
@@ -669,7 +683,7 @@ def test_cu_partitions_are_released_when_pods_go_away():
             await s.client.delete("pods", "p1", "default")
             await s.wait(lambda: s.plugin.state.cus[0].free_count() == 64)
             await s.client.create("pods", bound_pod("p4", 16, assume=4, annotations=cu))
-            p4 = await s.wait_phase("p4")
+            p4 = await s.wait_committed("p4")
             assert _cus_of(p4) == sets[1]
             # five sequential pods, each deleted before the next: all allocate
             for i in (0, 2, 3, 4):
@@ -677,7 +691,7 @@ def test_cu_partitions_are_released_when_pods_go_away():
             await s.wait(lambda: s.plugin.state.cus[0].free_count() == 256)
             for i in range(5):
                 await s.client.create("pods", bound_pod(f"s{i}", 16, assume=10 + i, annotations=cu))
-                assert len(_cus_of(await s.wait_phase(f"s{i}"))) == 64
+                assert len(_cus_of(await s.wait_committed(f"s{i}"))) == 64
                 await s.client.delete("pods", f"s{i}", "default")
             await s.wait(lambda: s.plugin.state.cus[0].free_count() == 256 and not s.plugin.state.pods)
             assert s.plugin.stats["allocate_fail"] == 0 and s.agent.failed == 0
@@ -696,12 +710,12 @@ def test_plugin_restart_rebuilds_partitions_from_annotations():
             cu = {CU_COUNT_ANNOTATION: "64"}
             for i in range(3):
                 await s.client.create("pods", bound_pod(f"r{i}", 16, assume=i, annotations=cu))
-            running = [_cus_of(await s.wait_phase(f"r{i}")) for i in range(3)]
+            running = [_cus_of(await s.wait_committed(f"r{i}")) for i in range(3)]
             await s.restart_plugin()
             assert s.plugin.state.cus[0].free_count() == 64  # rebuilt before serving
             assert s.plugin.state.stats["cu_adopted"] == 3
             await s.client.create("pods", bound_pod("new", 16, assume=9, annotations=cu))
-            new = _cus_of(await s.wait_phase("new"))
+            new = _cus_of(await s.wait_committed("new"))
             assert len(new) == 64 and all(not new & r for r in running)
             # and a fifth partition does not exist until one goes away
             await s.client.create("pods", bound_pod("extra", 16, assume=10, annotations=cu))

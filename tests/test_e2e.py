@@ -18,17 +18,6 @@ from gpushare_scheduler_extender_amd.models.profile import ALIYUN, SHARED_GPU
 from tests.fixtures.schedsim import SchedulerSim
 
 
-NATIVE = {"on": True}
-
-
-@pytest.fixture(autouse=True, params=["native-http", "aiohttp"])
-def _frontend(request):
-    """Every end-to-end test runs twice: C++ front end + C++ controller, and aiohttp + asyncio controller."""
-    NATIVE["on"] = request.param == "native-http"
-    yield
-    NATIVE["on"] = True
-
-
 class Cluster:
     def __init__(self, profile=SHARED_GPU, bind_mode="binding", **ext_kw):
         self.profile = profile
@@ -38,10 +27,8 @@ class Cluster:
     async def __aenter__(self):
         self.api = await FakeApiServerRunner().start()
         self.client = KubeClient(self.api.url)
-        kw = {"native_controller": NATIVE["on"], **self.ext_kw}
         self.ext = await ExtenderRunner(ExtenderServer(KubeClient(self.api.url), self.profile,
-                                                       bind_mode=self.bind_mode, **kw),
-                                        native=NATIVE["on"]).start()
+                                                       bind_mode=self.bind_mode, **self.ext_kw)).start()
         self.sim = None
         self.http = aiohttp.ClientSession()
         return self
@@ -209,7 +196,7 @@ def test_pod_lifecycle_frees_memory_and_restart_recovery():
             eng = c.ext.server.engine
             await c.settle(lambda: eng.node_devices("n") == [(10, 6)])
             # a second extender started now rebuilds the ledger from annotations (cache.go:49-74)
-            srv2 = ExtenderServer(KubeClient(c.api.url), SHARED_GPU, native_controller=NATIVE["on"])
+            srv2 = ExtenderServer(KubeClient(c.api.url), SHARED_GPU)
             await srv2.start()
             assert srv2.engine.node_devices("n") == [(10, 6)]
             await srv2.stop()
@@ -269,7 +256,7 @@ def test_recovery_consistency_check_flags_overcommit():
             for nm in ("a", "b"):
                 await c.client.create("pods", make_pod(nm, 8, node="n", phase="Running", annotations={
                     "SHARED_GPU_MEM_IDX": "0", "SHARED_GPU_MEM_POD": "8"}))
-            srv2 = ExtenderServer(KubeClient(c.api.url), SHARED_GPU, native_controller=NATIVE["on"])
+            srv2 = ExtenderServer(KubeClient(c.api.url), SHARED_GPU)
             await srv2.start()
             try:
                 assert srv2.controller.overcommitted == [("n", 0, 16, 10)]
@@ -308,11 +295,9 @@ def test_leader_election_failover():
             await c.client.create("nodes", make_node("n", 100, 1))
             kw = dict(leader_elect=True, lease_namespace="default", lease_duration=2.0, renew_deadline=1.2,
                       retry_period=0.05)
-            a = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, native_controller=NATIVE["on"], **kw),
-                                     native=NATIVE["on"]).start()
+            a = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, **kw)).start()
             await asyncio.sleep(0.2)
-            b = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, native_controller=NATIVE["on"], **kw),
-                                     native=NATIVE["on"]).start()
+            b = await ExtenderRunner(ExtenderServer(KubeClient(c.api.url), SHARED_GPU, **kw)).start()
             try:
                 await c.settle(lambda: a.server.is_leader, 3)
                 await asyncio.sleep(0.3)

@@ -89,7 +89,7 @@ def test_native_front_end_survives_generated_requests():
         api = await FakeApiServerRunner().start()
         c = KubeClient(api.url)
         await c.create("nodes", make_node("n", 8 * 100, 8))
-        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=True, http_threads=2).start()
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), http_threads=2).start()
         try:
             def send(payload: bytes):
                 s = socket.create_connection(("127.0.0.1", ext.port), timeout=2)

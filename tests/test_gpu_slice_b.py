@@ -19,7 +19,7 @@ from pathlib import Path
 
 import pytest
 
-from gpushare_scheduler_extender_amd.deviceplugin.agent import NodeAgent
+from gsxtools.agent import NodeAgent
 from gpushare_scheduler_extender_amd.deviceplugin.devices import discover
 from gpushare_scheduler_extender_amd.deviceplugin.runtime import ProcessRuntime
 from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
@@ -44,8 +44,8 @@ def test_slice_b_pod_runs_inside_its_share_on_mi355x():
     async def go():
         api = await FakeApiServerRunner().start()
         client = KubeClient(api.url)
-        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), SHARED_GPU), native=True).start()
-        cmd = [sys.executable, "-m", "gpushare_scheduler_extender_amd.sim.workload", "--iters", "40", "--size", "4096",
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), SHARED_GPU)).start()
+        cmd = [sys.executable, "-m", "gsxtools.workload", "--iters", "40", "--size", "4096",
                "--touch", "--probe-limit", "--json"]
         rt = ProcessRuntime(cmd, extra_env={"PYTHONPATH": str(ROOT)}, cwd=str(ROOT))
         agent = NodeAgent(KubeClient(api.url), "mi355x-0", [dev], SHARED_GPU, rt, unit="GiB")

@@ -14,8 +14,6 @@ from tests.fixtures.fakeapi import CONFLICT_MSG, FakeApiServer, FakeApiServerRun
 from gpushare_scheduler_extender_amd.k8s.fasthttp import Client, Response, Server
 from gpushare_scheduler_extender_amd.k8s.informer import Handler, Informer
 from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod
-from gpushare_scheduler_extender_amd.parallel.workqueue import (BucketLimiter, ItemExponentialBackoff, ShutDown,
-                                                                WorkQueue)
 
 
 def run(coro):
@@ -26,7 +24,7 @@ class _NativeApi:
     """gsx-fakeapi (native/fakeapi) as a child process, with the runner interface the tests use."""
 
     def __init__(self, history, threads=1, watch_loop=False):
-        from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver
+        from gsxtools.cluster import start_apiserver
 
         self.proc = start_apiserver(history=history, threads=threads, watch_loop=watch_loop)
         self.url = self.proc.url
@@ -309,54 +307,7 @@ def test_rate_limiter_token_bucket():
     run(go())
 
 
-# ---------------------------------------------------------------- work queue
-
-def test_workqueue_dedup_and_processing_semantics():
-    async def go():
-        q = WorkQueue()
-        q.add("a")
-        q.add("a")
-        q.add("b")
-        assert len(q) == 2
-        a = await q.get()
-        q.add("a")  # re-added while processing: not handed out twice
-        b = await q.get()
-        assert (a, b) == ("a", "b") and len(q) == 0
-        q.done("a")
-        assert len(q) == 1  # replayed on done
-        assert await q.get() == "a"
-        q.done("a")
-        q.done("b")
-        assert q.idle()
-        await q.shutdown()
-        with pytest.raises(ShutDown):
-            await q.get()
-    run(go())
-
-
-def test_rate_limiters():
-    ex = ItemExponentialBackoff(0.005, 1.0)
-    assert [ex.when("x") for _ in range(4)] == [0.005, 0.01, 0.02, 0.04]
-    assert ex.num_requeues("x") == 4
-    ex.forget("x")
-    assert ex.when("x") == 0.005
-    for _ in range(20):
-        ex.when("y")
-    assert ex.when("y") == 1.0
-    b = BucketLimiter(qps=10, burst=2)
-    assert b.when("a") == 0 and b.when("a") == 0 and b.when("a") > 0
-
-
-def test_rate_limited_requeue_delivers_later():
-    async def go():
-        q = WorkQueue()
-        q.add_rate_limited("x")
-        assert len(q) == 0
-        item = await asyncio.wait_for(q.get(), 1)
-        assert item == "x"
-        await q.shutdown()
-    run(go())
-
+# ---------------------------------------------------------------- leader election
 
 class _StallingClient:
     """A KubeClient stand-in whose Lease calls fail fast once, then hang, once ``stall`` is set."""
@@ -439,7 +390,7 @@ def test_leader_steps_down_before_standby_can_acquire():
 def test_paginated_list_limit_continue(impl):
     """kube-apiserver pagination on both fake apiservers: pages of `limit`, `continue` resumes in key order,
     every page carries the first page's resourceVersion; the reflectors assemble complete LISTs from pages."""
-    from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver
+    from gsxtools.cluster import start_apiserver
 
     async def go():
         if impl == "python":
@@ -682,3 +633,59 @@ def test_tls_apiserver_verified_by_ca_and_ip_san(tmp_path):
         assert st != 200 and len(seen) == 2 and b"TLS handshake" in body, (st, body)
     finally:
         srv.shutdown()
+
+
+def test_python_informer_and_native_reflector_agree_under_churn():
+    """The one Python twin left after the prune: the device plugin's pod informer
+    (k8s/informer.py) next to the C++ reflector the extender's controller and the plugin's pod feed run
+    (native/engine/informer.cc).  Same node selector, same apiserver, the same churn with dropped watches, a
+    compacted history (410 -> re-list) and paginated LISTs: both end on the same key -> resourceVersion view."""
+    from gpushare_scheduler_extender_amd.core.controller import api_dict
+    from gpushare_scheduler_extender_amd.core.engine import native
+
+    async def go():
+        r, c = await _api(history=40)
+        client = KubeClient(r.url)
+        inf = Informer(client, "pods", field_selector="spec.nodeName=n1")
+        probe = native().ReflectorProbe(api_dict(client.config), "/api/v1/pods", "spec.nodeName=n1", 7)
+        try:
+            for i in range(12):
+                await c.create("pods", make_pod(f"pre{i}", 1, node="n1" if i % 3 else "n2"))
+            await inf.start()
+            await inf.wait_synced(5)
+            probe.start()
+            loop = asyncio.get_running_loop()
+            assert await loop.run_in_executor(None, probe.wait_synced, 10.0)  # the fake apiserver runs on this loop
+            r.server.faults.update({"drop_watch_after": 5})
+            for i in range(60):
+                name = f"p{i}"
+                await c.create("pods", make_pod(name, 1, node="n1" if i % 4 else "n2"))
+                if i % 5 == 0:
+                    await c.patch("pods", name, {"metadata": {"annotations": {"x": str(i)}}}, "default")
+                if i % 7 == 0:
+                    await c.delete("pods", f"p{i // 2}", "default")
+                if i == 30:
+                    probe.request_relist()
+                    inf.request_relist()
+            r.server.faults.update({"drop_watch_after": 0})
+            want = None
+            for _ in range(500):
+                py_view = {k: (v.get("metadata") or {}).get("resourceVersion") for k, v in inf.store.items()}
+                nat_view = dict(probe.view())
+                want = {k: v["metadata"]["resourceVersion"] for k, v in
+                        ((f"default/{p['metadata']['name']}", p) for p in (await c.list("pods"))["items"]
+                         if (p.get("spec") or {}).get("nodeName") == "n1")}
+                if py_view == want and nat_view == want:
+                    break
+                await asyncio.sleep(0.02)
+            assert py_view == want, "python informer diverged"
+            assert nat_view == want, "native reflector diverged"
+            st = probe.stats()
+            assert st["rewatches"] >= 1 and inf.rewatches >= 1 and st["lists"] >= 2, st
+        finally:
+            await asyncio.get_running_loop().run_in_executor(None, probe.stop)
+            await inf.stop()
+            await client.close()
+            await c.close()
+            await r.stop()
+    run(go())

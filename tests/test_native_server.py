@@ -1,4 +1,4 @@
-"""C++ front end of the extender (native/engine/server.cc): HTTP edge cases, concurrency, fallback routing."""
+"""C++ front end of the extender (native/engine/server.cc): HTTP edge cases, concurrency, unfiltered binds, proxied routes."""
 import asyncio
 import json
 import socket
@@ -17,7 +17,7 @@ async def _stack():
     api = await FakeApiServerRunner().start()
     c = KubeClient(api.url)
     await c.create("nodes", make_node("n", 8 * 100, 8))
-    ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=True, http_threads=2).start()
+    ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), http_threads=2).start()
     for _ in range(200):
         if ext.server.engine.has_node("n"):
             break
@@ -151,7 +151,7 @@ def test_concurrent_filters_from_threads_and_stats():
     asyncio.run(go())
 
 
-def test_native_bind_fast_path_and_python_fallback():
+def test_native_bind_fast_path_and_unfiltered_bind():
     async def go():
         api, c, ext = await _stack()
         try:
@@ -173,11 +173,12 @@ def test_native_bind_fast_path_and_python_fallback():
                         "fast", "default", p1["metadata"]["uid"], "n").encode()) as r:
                     assert r.status == 200 and json.loads(await r.read()) == {"Error": ""}
                 assert eng.server_stats()["proxied"] == before
-                # never filtered here -> the Python slow path binds it (proxied)
+                # never filtered here -> the request comes from the controller's lister, still in C++
                 async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
                         "slow", "default", p2["metadata"]["uid"], "n").encode()) as r:
                     assert r.status == 200, await r.read()
-                assert eng.server_stats()["proxied"] == before + 1
+                st = eng.server_stats()
+                assert st["proxied"] == before and st["unfiltered_binds"] == 1 and st["live_gets"] == 0
                 # non-native routes are served through the proxy
                 async with s.get(ext.url + "/metrics") as r:
                     text = await r.text()
@@ -191,7 +192,7 @@ def test_native_bind_fast_path_and_python_fallback():
             assert fast["metadata"]["annotations"]["SHARED_GPU_MEM_IDX"] == "0"
             assert slow["metadata"]["annotations"]["SHARED_GPU_MEM_IDX"] == "0"
             assert eng.node_devices("n")[0] == (100, 50)
-            assert eng.server_stats()["bind_ok"] == 1
+            assert eng.server_stats()["bind_ok"] == 2
         finally:
             await _teardown(api, c, ext)
     asyncio.run(go())
@@ -222,8 +223,8 @@ def test_native_bind_failure_becomes_event():
     asyncio.run(go())
 
 
-@pytest.mark.parametrize("native", [True, False], ids=["native-bind", "python-bind"])
-def test_equal_size_binds_for_different_gpus_land_in_assume_order(native):
+@pytest.mark.parametrize("filtered", [True, False], ids=["filtered", "unfiltered"])
+def test_equal_size_binds_for_different_gpus_land_in_assume_order(filtered):
     """kubelet admits pods in binding order and the device plugin serves a request of N units with the
     earliest-ASSUME_TIME pod of that size: two equal-size pods bound to different GPUs of one node must
     commit in ASSUME_TIME order even when the first binding is slow; other binds do not wait."""
@@ -233,7 +234,7 @@ def test_equal_size_binds_for_different_gpus_land_in_assume_order(native):
         api = await FakeApiServerRunner().start()
         c = KubeClient(api.url)
         await c.create("nodes", make_node("n", 2 * 16, 2))
-        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=native, http_threads=2).start()
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), http_threads=2).start()
         try:
             pods = {}
             for name, mem in (("a", 10), ("b", 10), ("x", 6), ("y", 5)):
@@ -245,8 +246,9 @@ def test_equal_size_binds_for_different_gpus_land_in_assume_order(native):
             async with aiohttp.ClientSession() as s:
                 async def bind(name):
                     p = pods[name]
-                    async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(p, ["n"])) as r:
-                        assert json.loads(await r.read())["NodeNames"] == ["n"]
+                    if filtered:
+                        async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(p, ["n"])) as r:
+                            assert json.loads(await r.read())["NodeNames"] == ["n"]
                     async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
                             name, "default", p["metadata"]["uid"], "n").encode()) as r:
                         assert r.status == 200, await r.read()
@@ -264,15 +266,14 @@ def test_equal_size_binds_for_different_gpus_land_in_assume_order(native):
             got = {n: (await c.get("pods", n, "default"))["metadata"]["annotations"] for n in pods}
             assert [got[n]["SHARED_GPU_MEM_IDX"] for n in ("a", "b", "x", "y")] == ["0", "1", "0", "1"]
             assert int(got["a"]["SHARED_GPU_MEM_ASSUME_TIME"]) < int(got["b"]["SHARED_GPU_MEM_ASSUME_TIME"])
-            if native:
-                assert ext.server.engine.server_stats()["bind_order_waits"] == 1
+            assert ext.server.engine.server_stats()["bind_order_waits"] == 1
         finally:
             await _teardown(api, c, ext)
     asyncio.run(go())
 
 
-@pytest.mark.parametrize("native", [True, False], ids=["native-bind", "python-bind"])
-def test_same_gpu_binds_with_different_cu_partitions_land_in_assume_order(native):
+@pytest.mark.parametrize("filtered", [True, False], ids=["filtered", "unfiltered"])
+def test_same_gpu_binds_with_different_cu_partitions_land_in_assume_order(filtered):
     """Equal-size pods for the same GPU are interchangeable for the device plugin unless their CU-partition
     requests differ (gpushare.amd.com/cu-count): then a swap would start one pod's container with the other's
     partition size, so they are ordered too. Equal-size, same-class pods still bind concurrently."""
@@ -282,7 +283,7 @@ def test_same_gpu_binds_with_different_cu_partitions_land_in_assume_order(native
         api = await FakeApiServerRunner().start()
         c = KubeClient(api.url)
         await c.create("nodes", make_node("n", 64, 1))
-        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=native, http_threads=2).start()
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), http_threads=2).start()
         try:
             cu = {"gpushare.amd.com/cu-count": "64"}
             pods = {}
@@ -295,8 +296,9 @@ def test_same_gpu_binds_with_different_cu_partitions_land_in_assume_order(native
             async with aiohttp.ClientSession() as s:
                 async def bind(name):
                     p = pods[name]
-                    async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(p, ["n"])) as r:
-                        assert json.loads(await r.read())["NodeNames"] == ["n"]
+                    if filtered:
+                        async with s.post(ext.url + "/gpushare-scheduler/filter", data=wire.filter_args(p, ["n"])) as r:
+                            assert json.loads(await r.read())["NodeNames"] == ["n"]
                     async with s.post(ext.url + "/gpushare-scheduler/bind", data=wire.ExtenderBindingArgs(
                             name, "default", p["metadata"]["uid"], "n").encode()) as r:
                         assert r.status == 200, await r.read()
@@ -309,7 +311,7 @@ def test_same_gpu_binds_with_different_cu_partitions_land_in_assume_order(native
                 await asyncio.sleep(0.05)
                 await asyncio.gather(te, bind("f"))  # f asks for the same partition size: does not wait
             assert api.server.binding_log == ["c", "d", "f", "e"]
-            assert ext.server.engine.stats()["bind_order_waits"] == 1  # d, on either bind path
+            assert ext.server.engine.stats()["bind_order_waits"] == 1  # d
             async with aiohttp.ClientSession() as s:
                 async with s.get(ext.url + "/metrics") as r:
                     assert "gpushare_bind_order_waits_total 1.0" in await r.text()
@@ -328,7 +330,7 @@ def test_native_update_mode_annotates_then_binds_with_one_conflict_retry():
         api = await FakeApiServerRunner().start()
         c = KubeClient(api.url)
         await c.create("nodes", make_node("n", 2 * 16, 2))
-        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), bind_mode="update"), native=True,
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), bind_mode="update"),
                                    http_threads=2).start()
         try:
             pa = await c.create("pods", make_pod("a", 10))
@@ -416,17 +418,17 @@ def test_pprof_sees_native_threads():
     asyncio.run(go())
 
 
-def test_bind_order_spans_native_and_python_paths():
-    """one in-flight set for both bind paths.  a is bound natively (filtered here) with a slow
-    binding; b, equal-size for the other GPU, arrives on the Python slow path (never filtered by this
-    process, e.g. after a restart between filter and bind) and must still commit after a."""
+def test_bind_order_spans_filtered_and_unfiltered_binds():
+    """one in-flight set for every bind.  a is filtered here and has a slow binding; b, equal-size for
+    the other GPU, was never filtered by this process (e.g. a restart between filter and bind) and must still
+    commit after a."""
     async def go():
         import aiohttp
 
         api = await FakeApiServerRunner().start()
         c = KubeClient(api.url)
         await c.create("nodes", make_node("n", 2 * 16, 2))
-        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=True, http_threads=2).start()
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), http_threads=2).start()
         try:
             pa = await c.create("pods", make_pod("a", 10))
             pb = await c.create("pods", make_pod("b", 10))
@@ -444,11 +446,10 @@ def test_bind_order_spans_native_and_python_paths():
                         assert r.status == 200, await r.read()
 
                 api.server.faults.slow_bindings = {"a": 300.0}
-                before = ext.server.engine.server_stats()["proxied"]
                 ta = asyncio.create_task(bind(pa))
                 await asyncio.sleep(0.05)
                 await asyncio.gather(ta, bind(pb))
-                assert ext.server.engine.server_stats()["proxied"] == before + 1  # b took the Python path
+                assert ext.server.engine.server_stats()["unfiltered_binds"] == 1  # b
             assert api.server.binding_log == ["a", "b"]
             got = {n: (await c.get("pods", n, "default"))["metadata"]["annotations"] for n in ("a", "b")}
             assert [got[n]["SHARED_GPU_MEM_IDX"] for n in ("a", "b")] == ["0", "1"]
@@ -476,7 +477,7 @@ def test_bind_order_follows_the_nodes_allocate_order(order, landing, want):
         if landing:
             node["metadata"].setdefault("annotations", {})[NODE_ALLOCATE_ORDER_ANNOTATION] = "landing"
         await c.create("nodes", node)
-        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), bind_order=order), native=True,
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), bind_order=order),
                                    http_threads=2).start()
         try:
             pa = await c.create("pods", make_pod("a", 10))
@@ -520,7 +521,7 @@ def test_move_endpoint_is_the_one_writer_of_the_gpu_index():
         api = await FakeApiServerRunner().start()
         c = KubeClient(api.url)
         await c.create("nodes", make_node("n", 2 * 100, 2))
-        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), native=True, http_threads=2).start()
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), http_threads=2).start()
         eng = ext.server.engine
         http = HttpClient(f"http://127.0.0.1:{ext.port}")
 
@@ -594,4 +595,52 @@ def test_move_endpoint_is_the_one_writer_of_the_gpu_index():
             await ext.server.client.close()
             await c.close()
             await api.stop()
+    asyncio.run(go())
+
+
+def test_unfiltered_bind_errors_match_the_reference_and_qps_limits_native_binds():
+    """Binds the filter never saw are decided in C++ too (the Python bind path is gone): Go's decoder error for
+    a mistyped field, the reference's UID error after one live GET (gpushare-bind.go:44-65), and a client-side
+    QPS limit (--kube-qps) paces the front end's apiserver calls."""
+    async def go():
+        import time
+
+        import aiohttp
+
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 8 * 100, 8))
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url, qps=20, burst=1)), http_threads=2).start()
+        try:
+            pods = [await c.create("pods", make_pod(f"q{i}", 10)) for i in range(6)]
+            for _ in range(300):
+                if ext.server.engine.has_node("n") and ext.server.controller.get_pod("q5", "default"):
+                    break
+                await asyncio.sleep(0.01)
+            url = ext.url + "/gpushare-scheduler/bind"
+            async with aiohttp.ClientSession() as s:
+                async with s.post(url, data=b'{"PodName":"q0","PodNamespace":"default","PodUID":7,"Node":"n"}') as r:
+                    assert r.status == 500
+                    assert json.loads(await r.read())["Error"] == (
+                        "json: cannot unmarshal number into Go struct field ExtenderBindingArgs.PodUID of type string")
+                async with s.post(url, data=wire.ExtenderBindingArgs("q0", "default", "not-its-uid", "n").encode()) as r:
+                    assert r.status == 500
+                    assert json.loads(await r.read())["Error"] == (
+                        f"The pod q0 in ns default's uid is {pods[0]['metadata']['uid']}, and it's not equal with "
+                        "expected not-its-uid")
+                async with s.post(url, data=wire.ExtenderBindingArgs("gone", "default", "u", "n").encode()) as r:
+                    assert r.status == 500 and "not found" in json.loads(await r.read())["Error"]
+
+                async def bind(p):
+                    async with s.post(url, data=wire.ExtenderBindingArgs(
+                            p["metadata"]["name"], "default", p["metadata"]["uid"], "n").encode()) as r:
+                        assert r.status == 200, await r.read()
+                t0 = time.monotonic()
+                await asyncio.gather(*(bind(p) for p in pods))
+                dt = time.monotonic() - t0
+            st = ext.server.engine.server_stats()
+            assert st["unfiltered_binds"] == 8 and st["live_gets"] == 2 and st["bind_ok"] == 6
+            assert st["qps_waits"] >= 5 and dt >= 0.2, (st, dt)  # 6 bindings at 20 qps, burst 1
+        finally:
+            await _teardown(api, c, ext)
     asyncio.run(go())

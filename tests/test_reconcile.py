@@ -15,7 +15,7 @@ import pytest
 from gpushare_scheduler_extender_amd.k8s.client import ApiError
 from gpushare_scheduler_extender_amd.k8s.objects import make_pod
 from gpushare_scheduler_extender_amd.models.profile import ALIYUN, POD_HOLD_IDX_ANNOTATION
-from gpushare_scheduler_extender_amd.sim.configs import Cluster
+from gsxtools.configs import Cluster
 
 
 async def _pods(cl) -> dict:

@@ -39,7 +39,7 @@ def test_engine_under_sanitizer(target):
 @pytest.mark.slow
 @pytest.mark.parametrize("target", ["asan", "tsan"])
 def test_controller_stack_under_sanitizer(target):
-    from gpushare_scheduler_extender_amd.sim.cluster import start_apiserver
+    from gsxtools.cluster import start_apiserver
 
     build_native([target, "fakeapi"])
     api = start_apiserver()
@@ -58,7 +58,7 @@ def test_standins_under_tsan(tmp_path):
     logs = tmp_path / "tsan"
     env = dict(os.environ, GSX_NATIVE_TOOLS_SUFFIX="_tsan", PYTHONPATH=str(REPO),
                TSAN_OPTIONS=f"halt_on_error=0 second_deadlock_stack=1 log_path={logs}")
-    r = subprocess.run([sys.executable, "-m", "gpushare_scheduler_extender_amd.sim.configs", "--agent", "native",
+    r = subprocess.run([sys.executable, "-m", "gsxtools.configs", "--agent", "native",
                         "--only", "2,3,5"], capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     # the compiled stand-in with its in-process matcher, and calling the shipped plugin process (PodResources server

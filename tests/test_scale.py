@@ -1,8 +1,8 @@
 """Cluster scale: 5,000 nodes x 8 devices with 10,000 resident pods sync through paginated
-LISTs and filter at full NodeNames in bounded time; pods keep binding under churn (sim/scale.py)."""
+LISTs and filter at full NodeNames in bounded time; pods keep binding under churn (gsxtools/scale.py)."""
 import json
 
-from gpushare_scheduler_extender_amd.sim import scale
+from gsxtools import scale
 
 
 def test_5000_nodes_sync_filter_and_churn(tmp_path):
