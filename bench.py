@@ -78,19 +78,53 @@ class LoopThread:
         self.t.join(5)
 
 
-def _cpu_times(children) -> dict:
-    """user+sys CPU seconds of this process and the child servers (where the control plane spends time)."""
-    import resource
-
-    ru = resource.getrusage(resource.RUSAGE_SELF)
-    out = {"rank0": ru.ru_utime + ru.ru_stime}
-    for c in children:
+def _task_cpu_s(pid: int) -> float | None:
+    """On-CPU seconds of every thread of `pid` (/proc/<pid>/task/*/schedstat, nanosecond resolution: the
+    timed region is milliseconds, far below the 10 ms ticks of /proc/<pid>/stat)."""
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return None
+    ns = 0
+    for t in tids:
         try:
-            with open(f"/proc/{c.proc.pid}/stat") as f:
-                parts = f.read().rsplit(")", 1)[1].split()
-            out[c.name] = (int(parts[11]) + int(parts[12])) / os.sysconf("SC_CLK_TCK")
-        except (OSError, AttributeError, IndexError):
+            with open(f"/proc/{pid}/task/{t}/schedstat") as f:
+                ns += int(f.read().split()[0])
+        except (OSError, ValueError, IndexError):
             pass
+    return ns / 1e9
+
+
+def _child_pids(pid: int) -> list[int]:
+    out = []
+    try:
+        for t in os.listdir(f"/proc/{pid}/task"):
+            with open(f"/proc/{pid}/task/{t}/children") as f:
+                out += [int(x) for x in f.read().split()]
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def _cpu_times(children) -> dict:
+    """On-CPU seconds of this process (rank 0), the child servers and the device-plugin process the node agent
+    spawned (the shipped plugin, the node's DaemonSet pod)."""
+    out = {}
+    me = _task_cpu_s(os.getpid())
+    if me is not None:
+        out["rank0"] = me
+    for c in children:
+        pid = getattr(getattr(c, "proc", None), "pid", None)
+        if pid is None:
+            continue
+        v = _task_cpu_s(pid)
+        if v is not None:
+            out[c.name] = v
+        if c.name == "node-agent":
+            for k in _child_pids(pid):
+                pv = _task_cpu_s(k)
+                if pv is not None:
+                    out["plugin"] = out.get("plugin", 0.0) + pv
     return out
 
 
@@ -346,7 +380,7 @@ def _plugin_debug(E, url: str | None) -> dict | None:
     return {"grpc": {k: g.get(k) for k in ("impl", "fast_allocate", "slow_allocate", "fast_preferred",
                                            "slow_preferred", "patch_failures", "guard_by_ids", "journaling",
                                            "early_answer_backlog", "waited", "feed_events", "passes",
-                                           "last_slow_reason")},
+                                           "last_slow_reason", "handler_us")},
             "stats": d.get("stats"), "reconcile": d.get("reconcile")}
 
 
@@ -658,6 +692,16 @@ def main():
             # pods it first met in one LIST would be admitted as one batch in name order, not as they landed
             na_batch = E.BatchClient({"server": next(c.url for c in children if c.name == "node-agent")})
             wait_until(lambda: na_batch.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 300, "node agent never ready")
+            if a.node_agent == "native-plugin":
+                # the spawned plugin serves kubelet before its debug endpoint is up: wait for it (bounded), so that
+                # its counters reach the JSON line even on a slow host
+                def _debug_up():
+                    st, body = na_batch.run([("GET", "/v1/stats", b"")], 1)[0]
+                    return st == 200 and bool(json.loads(body).get("plugin_debug"))
+                try:
+                    wait_until(_debug_up, 20, "plugin debug endpoint")
+                except TimeoutError:
+                    pass
         pod_tmpl = make_pod("__NAME__", a.pod_gib, profile=profile, labels={"gsx-wave": "__STEP__"})
         del pod_tmpl["metadata"]["uid"]  # the apiserver assigns one per pod
         pod_tmpl = json.dumps(pod_tmpl, separators=(",", ":"))
@@ -971,7 +1015,10 @@ def main():
             # the extender's native front end over the timed waves (bind-order waits, apiserver round trips)
             "extender": extender_stats,
             "apiserver": apiserver_stats,
-            "cpu_s": {k: round(cpu1[k] - cpu0.get(k, 0.0), 3) for k in cpu1},
+            "cpu_s": {k: round(cpu1[k] - cpu0.get(k, 0.0), 4) for k in cpu1},
+            # on-CPU time of each process over the timed region's wall time (all its threads; 100 = one CPU busy):
+            # which process the wave pipeline waits on
+            "busy_pct": {k: round(100.0 * (cpu1[k] - cpu0.get(k, 0.0)) / max(elapsed, 1e-9), 1) for k in cpu1},
             # resident memory of each process at the start and the end of the timed region
             "rss_mib": {k: [rss0.get(k), rss1[k]] for k in rss1},
             # CPU-quota throttling of the container during the timed region (cgroup v2), if any

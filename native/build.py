@@ -170,6 +170,15 @@ def build_tools(force: bool = False, verbose: bool = False) -> list[Path]:
             _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-I" + str(src), str(s), *others,
                   "-L" + str(ROCM / "lib"), "-lhsa-runtime64", "-o", str(out)], verbose)
         outs.append(out)
+    # the scratch probe's kernels, one code object per private-array size (gsx-memprobe --scratch KIB)
+    probe = src / "probes" / "scratch.hip"
+    for kib, ints in ((1, 256), (4, 1024), (16, 4096), (64, 16384)):
+        out = OUT / f"gsx-scratch-{kib}.hsaco"
+        if force or _newer(out, [probe]):
+            OUT.mkdir(parents=True, exist_ok=True)
+            _run([_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "--genco", f"-DSCRATCH_INTS={ints}",
+                  str(probe), "-o", str(out)], verbose)
+        outs.append(out)
     return outs
 
 

@@ -1033,6 +1033,10 @@ class PyDpServer {
     d["journaling"] = core_->journaling();
     d["early_answer_backlog"] = static_cast<uint64_t>(bg_backlog());
     d["passes"] = passes_;
+    // time inside the handlers (decode, match, respond), per call: what the plugin adds to kubelet's round trip
+    d["handler_us"] = py::dict(py::arg("get_preferred") = h_pref_n_ ? 1e6 * h_pref_s_ / h_pref_n_ : 0.0,
+                               py::arg("allocate") = h_alloc_n_ ? 1e6 * h_alloc_s_ / h_alloc_n_ : 0.0,
+                               py::arg("n_preferred") = h_pref_n_, py::arg("n_allocate") = h_alloc_n_);
     return d;
   }
 
@@ -1051,6 +1055,21 @@ class PyDpServer {
 
  private:
   void on_call(h2::Server& s, const h2::Call& call) {
+    const double t0 = mono();
+    handle_call(s, call);
+    const double dt = mono() - t0;
+    const std::string_view m(call.path);
+    auto ends = [&m](std::string_view suf) { return m.size() >= suf.size() && m.substr(m.size() - suf.size()) == suf; };
+    if (ends("/GetPreferredAllocation")) {
+      h_pref_s_ += dt;
+      h_pref_n_++;
+    } else if (ends("/Allocate")) {
+      h_alloc_s_ += dt;
+      h_alloc_n_++;
+    }
+  }
+
+  void handle_call(h2::Server& s, const h2::Call& call) {
     const std::string svc = kSvc;
     if (call.path.compare(0, svc.size(), svc) != 0) {
       s.respond(call.id, 12, "unknown service " + call.path);
@@ -1405,6 +1424,8 @@ class PyDpServer {
   std::thread serving_;
   std::atomic<bool> stop_serving_{false};  // written under the state lock
   int pyfd_ = -1;              // readable: pending_ / events_ waiting for poll()
+  double h_pref_s_ = 0, h_alloc_s_ = 0;
+  uint64_t h_pref_n_ = 0, h_alloc_n_ = 0;
   double spin_us_ = 200;       // poll without sleeping this long after a pass (cfg "spin_us"; 0: always block)
   uint64_t passes_ = 0;
 };

@@ -76,7 +76,44 @@ static hsa_status_t fake_agent_get_info(hsa_agent_t a, hsa_agent_info_t attr, vo
     *static_cast<uint64_t*>(v) = POOL_SIZE;
     return HSA_STATUS_SUCCESS;
   }
+  switch (static_cast<int>(attr)) {  // an MI355X: 256 CUs x 32 wave slots of 64 lanes, 32 GiB scratch at most
+    case HSA_AMD_AGENT_INFO_COMPUTE_UNIT_COUNT: *static_cast<uint32_t*>(v) = 256; return HSA_STATUS_SUCCESS;
+    case HSA_AMD_AGENT_INFO_MAX_WAVES_PER_CU: *static_cast<uint32_t*>(v) = 32; return HSA_STATUS_SUCCESS;
+    case HSA_AGENT_INFO_WAVEFRONT_SIZE: *static_cast<uint32_t*>(v) = 64; return HSA_STATUS_SUCCESS;
+    case HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX: *static_cast<uint64_t*>(v) = uint64_t{32} << 30; return HSA_STATUS_SUCCESS;
+    default: break;
+  }
   return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+}
+
+// ---- a fake loader: executable handle -> the private bytes per lane of its kernels
+static std::vector<std::vector<uint32_t>> g_exes;
+static uint64_t g_scratch_limit_set = 0;
+static hsa_status_t fake_freeze(hsa_executable_t, const char*) { return HSA_STATUS_SUCCESS; }
+static hsa_status_t fake_iterate_symbols(hsa_executable_t e,
+                                         hsa_status_t (*cb)(hsa_executable_t, hsa_executable_symbol_t, void*),
+                                         void* data) {
+  for (size_t k = 0; k < g_exes[e.handle].size(); ++k) {
+    hsa_status_t s = cb(e, hsa_executable_symbol_t{(e.handle << 16) | k}, data);
+    if (s != HSA_STATUS_SUCCESS) return s;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t fake_symbol_get_info(hsa_executable_symbol_t sym, hsa_executable_symbol_info_t attr, void* v) {
+  switch (attr) {
+    case HSA_EXECUTABLE_SYMBOL_INFO_TYPE: *static_cast<hsa_symbol_kind_t*>(v) = HSA_SYMBOL_KIND_KERNEL; break;
+    case HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE:
+      *static_cast<uint32_t*>(v) = g_exes[sym.handle >> 16][sym.handle & 0xffff];
+      break;
+    case HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_DYNAMIC_CALLSTACK: *static_cast<bool*>(v) = false; break;
+    case HSA_EXECUTABLE_SYMBOL_INFO_AGENT: *static_cast<hsa_agent_t*>(v) = hsa_agent_t{GPU_AGENT}; break;
+    default: return HSA_STATUS_ERROR_INVALID_ARGUMENT;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t fake_set_scratch_limit(hsa_agent_t, size_t threshold) {
+  g_scratch_limit_set = threshold;
+  return HSA_STATUS_SUCCESS;
 }
 
 static CoreApiTable core;
@@ -118,6 +155,10 @@ int main(int argc, char** argv) {
   amd.hsa_amd_memory_pool_get_info_fn = fake_pool_get_info;
   amd.hsa_amd_memory_pool_allocate_fn = fake_pool_allocate;
   amd.hsa_amd_memory_pool_free_fn = fake_pool_free;
+  core.hsa_executable_freeze_fn = fake_freeze;
+  core.hsa_executable_iterate_symbols_fn = fake_iterate_symbols;
+  core.hsa_executable_symbol_get_info_fn = fake_symbol_get_info;
+  amd.hsa_amd_agent_set_async_scratch_limit_fn = fake_set_scratch_limit;
   HsaApiTable table;
   std::memset(&table, 0, sizeof table);
   table.core_ = &core;
@@ -241,6 +282,33 @@ int main(int argc, char** argv) {
   for (int k = 0; k < 2; ++k) waitpid(kids[k], &st, 0);
   CHECK(granted == 1);
   g_slow_alloc = false;
+
+  // ---- scratch: a loaded code object charges its worst kernel (lane bytes in 256-byte granules x 64 lanes x 32
+  // waves x 256 CUs) against the share, sets the agent's async scratch limit to it, and is refused if it cannot fit
+  auto scratch = reinterpret_cast<void (*)(uint64_t*)>(dlsym(h, "gsx_isolate_scratch"));
+  CHECK(scratch != nullptr);
+  g_exes = {{0, 1040, 200}, {4112}, {16400}, {0}};
+  const uint64_t slots = uint64_t{64} * 32 * 256;
+  uint64_t sc[3];
+  CHECK(core.hsa_executable_freeze_fn(hsa_executable_t{0}, nullptr) == HSA_STATUS_SUCCESS);
+  scratch(sc);
+  CHECK(sc[0] == 1280 * slots && sc[1] == 0 && sc[2] == 1280 * slots && g_scratch_limit_set == 1280 * slots);
+  stats(sv);
+  CHECK(sv[3] == 1280 * slots);  // part of this process's share
+  CHECK(core.hsa_executable_freeze_fn(hsa_executable_t{3}, nullptr) == HSA_STATUS_SUCCESS);  // no scratch: no change
+  CHECK(core.hsa_executable_freeze_fn(hsa_executable_t{1}, nullptr) == HSA_STATUS_SUCCESS);  // raised, not added
+  scratch(sc);
+  CHECK(sc[0] == 4352 * slots && g_scratch_limit_set == 4352 * slots);
+  void* e = nullptr;
+  CHECK(alloc(GPU_POOL, 95, &e) == HSA_STATUS_SUCCESS);  // 95 GiB + 2.3 GB of scratch: fits the 100 GiB share
+  // 16400 bytes a lane: 8.7 GB at full occupancy, more than the share has left
+  CHECK(core.hsa_executable_freeze_fn(hsa_executable_t{2}, nullptr) == HSA_STATUS_ERROR_OUT_OF_RESOURCES);
+  scratch(sc);
+  CHECK(sc[0] == 4352 * slots && sc[1] == 1);
+  CHECK(amd.hsa_amd_memory_pool_free_fn(e) == HSA_STATUS_SUCCESS);
+  CHECK(core.hsa_executable_freeze_fn(hsa_executable_t{2}, nullptr) == HSA_STATUS_SUCCESS);  // room again
+  scratch(sc);
+  CHECK(sc[0] == 16640 * slots);
   if (g_fail == 0) std::printf("isolate_test: OK\n");
   return g_fail ? 1 : 0;
 }

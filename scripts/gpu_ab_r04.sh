@@ -13,6 +13,7 @@ for i in 1 2 3; do
       ${EXTRA:-} --json-out $OUT/$na.$i.json > $OUT/$na.$i.log 2>&1 || { echo "bench $na $i failed"; tail -20 $OUT/$na.$i.log; exit 1; }
     python -c "
 import json; d=json.load(open('$OUT/$na.$i.json')); na=d['node_agent']
-print('$na', $i, d['value'], d['wave_pods_per_s']['p50'], d['wave_ms_p50'], na.get('plugin_calls_mean_ms'), na.get('mean_ms'))"
+g=((d.get('plugin') or {}).get('grpc') or {})
+print('$na', $i, d['value'], d['wave_pods_per_s']['p50'], d['wave_ms_p50'], na.get('plugin_calls_mean_ms'), na.get('mean_ms'), g.get('handler_us'), d.get('busy_pct'))"
   done
 done
