@@ -381,7 +381,10 @@ def _plugin_debug(E, url: str | None) -> dict | None:
                                            "slow_preferred", "patch_failures", "guard_by_ids", "journaling",
                                            "early_answer_backlog", "waited", "feed_events", "passes",
                                            "last_slow_reason", "handler_us")},
-            "stats": d.get("stats"), "reconcile": d.get("reconcile")}
+            "stats": d.get("stats"), "reconcile": d.get("reconcile"),
+            # mean seconds per native fast-path Allocate: match, isolation files, record + answer (handler)
+            "timing": {k: (v / max(1, (d.get("timing") or {}).get("n", 0)) if k != "n" else v)
+                       for k, v in (d.get("timing") or {}).items() if not k.startswith("preferred")}}
 
 
 def parse():

@@ -93,6 +93,44 @@ def native_grpc_available() -> tuple[bool, str]:
     except (ImportError, AttributeError) as e:
         return False, repr(e)
 
+class _FeedInformer:
+    """Stands in for the Python pod informer when the native endpoint's pod feed is the node's only watch: the
+    Python side reads pods from the native state (:class:`.state._NativePods`) and decodes no pod event."""
+
+    def __init__(self, plugin):
+        self._plugin = plugin
+        self.synced = asyncio.Event()
+        self.synced.set()
+
+    def _stat(self, k: str) -> int:
+        n = self._plugin._native
+        return int(n.stats().get(k, 0)) if n is not None else 0
+
+    @property
+    def relists(self) -> int:
+        return self._stat("feed_relists")
+
+    @property
+    def rewatches(self) -> int:
+        return self._stat("feed_rewatches")
+
+    @property
+    def events(self) -> int:
+        return self._stat("feed_events")
+
+    async def start(self):
+        return None
+
+    async def stop(self):
+        return None
+
+    async def wait_synced(self, timeout=None):
+        return None
+
+    def list(self) -> list[dict]:
+        return [r.obj for r in self._plugin.state.pods.values()]
+
+
 class GpuSharePlugin:
     def __init__(self, client: KubeClient, node: str, devices: list[Device], profile: NamingProfile, *,
                  unit: str = "GiB", socket_dir: str = api.DEVICE_PLUGIN_PATH, endpoint: str = "gpushare-amd.sock",
@@ -148,6 +186,7 @@ class GpuSharePlugin:
         self._server: grpc.aio.Server | None = None
         self._native = None  # _engine.DpServer: the gRPC endpoint in native code (default)
         self._native_fd = -1  # what the loop watches for it (the serving thread's eventfd, or its epoll fd)
+        self._native_serving = False
         self._feed = False  # the native endpoint's pod feed runs (the Python informer then mirrors only)
         self.grpc_impl = ""
         self._slow: set[asyncio.Task] = set()
@@ -168,6 +207,12 @@ class GpuSharePlugin:
         """kubelet can call before this plugin's watch has delivered the pod it is admitting (they are separate
         processes with separate watches).  Waiting a few ms for the event is far cheaper than a full LIST."""
         deadline = time.monotonic() + timeout
+        if self.state.native_views:  # the native feed applies events on its own thread: look again shortly
+            while True:
+                got = found()
+                if got or time.monotonic() >= deadline:
+                    return got
+                await asyncio.sleep(0.001)
         while True:
             left = deadline - time.monotonic()
             if left <= 0:
@@ -207,8 +252,12 @@ class GpuSharePlugin:
             raw = await asyncio.get_running_loop().run_in_executor(None, mxdev.enumerate_devices, self.health_backend)
             devices = apply_memory_pools([Device(**d) for d in raw])
         old = sorted((d.index, d.partition, d.memory_partition) for d in self.devices.values())
+        pods = self.pods.list()  # before the state is rebuilt (with the native feed, the pods live in it)
+        native_views = self.state.native_views
         self._set_devices(devices)
-        self.state.resync(self.pods.list())
+        if native_views:
+            self.state.use_native_views()
+        self.state.resync(pods)
         self.stats["layout_changes"] = self.stats.get("layout_changes", 0) + 1
         log.warning("device layout changed: %s -> %s", old,
                     sorted((d.index, d.partition, d.memory_partition) for d in devices))
@@ -300,11 +349,12 @@ class GpuSharePlugin:
         """A native fast-path Allocate: what the Python handler would have done after it."""
         import json  # noqa: PLC0415
 
+        native_views = self.state.native_views  # the native state observed the committed pod itself
         if ev.get("patch_only"):  # early answer: the commit of an Allocate answered before has landed
-            if ev["pod_json"]:
+            if ev["pod_json"] and not native_views:
                 self.state.observe(json.loads(ev["pod_json"]))
             return
-        if ev["pod_json"]:
+        if ev["pod_json"] and not native_views:
             self.state.observe(json.loads(ev["pod_json"]))  # the committed pod, before its watch event arrives
         if ev["iso"] and self.isolation is not None:
             self.isolation.note_prepared(ev["iso"])
@@ -343,6 +393,7 @@ class GpuSharePlugin:
                 pass
             self._native.close()
             self._native = None
+        self._native_serving = False
         self._feed = False
 
     # ------------------------------------------------------------ gRPC handlers
@@ -853,27 +904,44 @@ class GpuSharePlugin:
                                                                     response_serializer=oc.SerializeToString)
         return grpc.method_handlers_generic_handler(f"{api.PKG}.DevicePlugin", methods)
 
-    async def serve(self):
-        if self._server is not None:  # re-serving after a kubelet restart: retire the old server first
-            await self._server.stop(0)
-            self._server = None
-        self._close_native()
+    def _open_native(self) -> bool:
+        """The native endpoint and (GSX_PLUGIN_FEED, default on) its pod feed, not serving yet: kubelet learns the
+        socket only from the registration that follows start-up.  Switches the state to native views when the feed
+        runs.  False if the native endpoint is unavailable."""
+        ok, _why = native_grpc_available()
+        if not ok:
+            return False
+        from ..core.engine import native  # noqa: PLC0415
+
         os.makedirs(self.socket_dir, exist_ok=True)
         try:
             os.unlink(self.socket_path)
         except FileNotFoundError:
             pass
+        if self.isolation is not None:
+            self.isolation.install()  # the fast path writes per-pod files next to the installed library
+        cfg = self._native_config()
+        self._native = native().DpServer(self.socket_path, self.state.core, cfg)
+        self._native_serving = False
+        if os.environ.get("GSX_PLUGIN_FEED", "1") == "1":
+            self._native.start_feed(cfg["api"])  # this node's pods into the state from a native reflector
+            self._feed = True
+            if self._own_informer:
+                self.state.use_native_views()
+        return True
+
+    async def serve(self):
+        if self._server is not None:  # re-serving after a kubelet restart: retire the old server first
+            await self._server.stop(0)
+            self._server = None
+        reuse = self._native is not None and not self._native_serving
+        if not reuse:
+            self._close_native()
         ok, why = native_grpc_available()
         if ok:
-            from ..core.engine import native  # noqa: PLC0415
-
-            if self.isolation is not None:
-                self.isolation.install()  # the fast path writes per-pod files next to the installed library
-            cfg = self._native_config()
-            self._native = native().DpServer(self.socket_path, self.state.core, cfg)
-            if os.environ.get("GSX_PLUGIN_FEED", "1") == "1":
-                self._native.start_feed(cfg["api"])  # this node's pods into the state from a native reflector
-                self._feed = True
+            if not reuse:
+                self._open_native()
+            self._native_serving = True
             self._sync_native()
             if os.environ.get("GSX_PLUGIN_SERVE_THREAD", "1") == "1":
                 # the endpoint is served from a native thread that never needs the GIL (a native lock guards the
@@ -888,6 +956,11 @@ class GpuSharePlugin:
         log.warning("device-plugin endpoint on grpc.aio, not the native endpoint (%s): Allocate admissions are "
                     "about 2x slower; install libnghttp2 (libnghttp2-14) to restore it", why)
         self.grpc_impl = "grpcio"
+        os.makedirs(self.socket_dir, exist_ok=True)
+        try:
+            os.unlink(self.socket_path)
+        except FileNotFoundError:
+            pass
         self._server = grpc.aio.server()
         self._server.add_generic_rpc_handlers((self._handlers(),))
         self._server.add_insecure_port(f"unix://{self.socket_path}")
@@ -1085,12 +1158,21 @@ class GpuSharePlugin:
     async def start(self, register: bool = True, publish: bool = True, serve: bool = True,
                     sync_timeout: float = 30.0):
         # state first: CU partitions of running pods are rebuilt before the first Allocate can be served
-        if self._own_informer:
-            await self.pods.start()
-        try:
-            await self.pods.wait_synced(sync_timeout)
-        except asyncio.TimeoutError:
-            log.warning("pod informer of %s not synced after %.0fs; Allocate will LIST", self.node, sync_timeout)
+        if self._own_informer and serve and self._open_native():
+            # the native endpoint's pod feed is the node's one watch (no Python informer decodes pod events)
+            loop = asyncio.get_running_loop()
+            if not await loop.run_in_executor(None, self._native.feed_synced, sync_timeout):
+                log.warning("pod feed of %s not synced after %.0fs; Allocate will LIST", self.node, sync_timeout)
+            self._native.poll()  # apply the first LIST (the serving thread does this from now on)
+            self.state.flush_dropped()
+            self.pods = _FeedInformer(self)
+        else:
+            if self._own_informer:
+                await self.pods.start()
+            try:
+                await self.pods.wait_synced(sync_timeout)
+            except asyncio.TimeoutError:
+                log.warning("pod informer of %s not synced after %.0fs; Allocate will LIST", self.node, sync_timeout)
         n = self.load_records()
         if n:
             log.info("restored %d allocation records from %s", n, self.checkpoint)

@@ -28,7 +28,9 @@ Everything here is synchronous and I/O free; the callers own the apiserver calls
 """
 from __future__ import annotations
 
+import json
 import logging
+from collections.abc import Mapping
 from dataclasses import dataclass, field
 
 from ..core.engine import native
@@ -94,7 +96,15 @@ class PodRec:
     cu_mask: str
     hold_idx: int = -1
     hold_partner: str = ""
-    obj: dict = field(repr=False, default_factory=dict)
+    pod: dict | None = field(repr=False, default=None, compare=False)
+    loader: object = field(repr=False, default=None, compare=False)  # () -> pod dict, read on first use
+
+    @property
+    def obj(self) -> dict:
+        """The pod object (from the Python informer, or the raw JSON the native pod feed kept)."""
+        if self.pod is None:
+            self.pod = (self.loader() if self.loader is not None else None) or {}
+        return self.pod
 
     @property
     def order(self) -> tuple:
@@ -126,6 +136,63 @@ class _Inflight:
         return self._core.inflight(uid)
 
 
+class _NativePods(Mapping):
+    """uid -> :class:`PodRec` read from the native state (the shipped plugin's pod feed keeps it current): no
+    Python watch decodes the node's pod events.  Views are rebuilt only for pods whose resourceVersion changed."""
+
+    def __init__(self, core):
+        self._core = core
+        self._cache: dict[str, PodRec] = {}
+
+    def _make(self, t) -> PodRec:
+        uid = t[0]
+        old = self._cache.get(uid)
+        if old is not None and old.rv == t[4] and old.phase == t[5] and old.assigned == t[11]:
+            return old
+        core = self._core
+
+        def load(uid=uid):
+            raw = core.pod_json(uid)
+            return json.loads(raw) if raw else None
+        rec = PodRec(uid=uid, key=t[1], namespace=t[2], name=t[3], rv=t[4], phase=t[5], dev=int(t[6]),
+                     request=int(t[7]), containers=list(t[8]), assume_time=int(t[9]), creation=t[10], assigned=t[11],
+                     complete=bool(t[12]), cu_count=int(t[13]), cu_mask=t[14], hold_idx=int(t[15]),
+                     hold_partner=t[16], loader=load)
+        self._cache[uid] = rec
+        return rec
+
+    def _all(self) -> dict[str, PodRec]:
+        out = {t[0]: self._make(t) for t in self._core.pod_views()}
+        for uid in [u for u in self._cache if u not in out]:
+            del self._cache[uid]
+        return out
+
+    def __getitem__(self, uid: str) -> PodRec:
+        t = self._core.pod_full(uid)
+        if t is None:
+            self._cache.pop(uid, None)
+            raise KeyError(uid)
+        return self._make(t)
+
+    def __contains__(self, uid) -> bool:
+        return self._core.has_pod(uid)
+
+    def __iter__(self):
+        return iter(self._all())
+
+    def __len__(self) -> int:
+        return len(self._core.pod_uids())
+
+    def values(self):
+        return self._all().values()
+
+    def items(self):
+        return self._all().items()
+
+    def keys(self):
+        return self._all().keys()
+
+
 class AllocationState:
     def __init__(self, node: str, devices: dict[int, Device], profile: NamingProfile):
         self.node = node
@@ -134,13 +201,23 @@ class AllocationState:
         self.core = native().AllocState(node, [(i, d.cu_count, d.xcc_count) for i, d in devices.items()])
         self.cus = {i: CUPartitioner(native_obj=self.core.cus(i)) for i in devices}
         self.inflight = _Inflight(self.core)
-        self._recs: dict[str, PodRec] = {}  # uid -> view of every pod the native state holds
+        self._recs: dict[str, PodRec] = {}  # uid -> view of every pod the native state holds (Python-fed mode)
+        self._native_pods: _NativePods | None = None
         self.on_drop: list = []  # callbacks(record) when a record's holder is gone
+
+    def use_native_views(self) -> None:
+        """The native pod feed is the only feed: :attr:`pods` reads the native state (no Python mirror)."""
+        self._native_pods = _NativePods(self.core)
+        self._recs = {}
+
+    @property
+    def native_views(self) -> bool:
+        return self._native_pods is not None
 
     # ------------------------------------------------------------ views
     @property
-    def pods(self) -> dict[str, PodRec]:
-        return self._recs
+    def pods(self):
+        return self._native_pods if self._native_pods is not None else self._recs
 
     @property
     def partial(self) -> dict[str, list[int]]:
@@ -172,7 +249,7 @@ class AllocationState:
                       assigned=ann.get(p.annotation_assigned, ""), complete=podutil.is_complete(pod),
                       cu_count=cu_count, cu_mask=ann.get(POD_CU_MASK_ANNOTATION, ""),
                       hold_idx=podutil.hold_idx(pod), hold_partner=ann.get(POD_HOLD_PARTNER_ANNOTATION, ""),
-                      obj=pod)
+                      pod=pod)
 
     def observe(self, pod: dict, mirror_only: bool = False) -> None:
         """An added / updated pod (informer event, LIST item, or our own PATCH response).
@@ -183,7 +260,10 @@ class AllocationState:
         rec = self._rec(pod)
         if not rec.uid:
             return
-        if mirror_only:
+        if self._native_pods is not None:
+            if mirror_only:
+                return  # the feed has it
+        elif mirror_only:
             old = self._recs.get(rec.uid)
             if old is not None and _older_rv(rec.rv, old.rv):
                 return  # a slow copy: never step back
@@ -202,8 +282,13 @@ class AllocationState:
             ap.dev_total = int(podutil.annotations(pod).get(self.profile.annotation_dev, "-1") or -1)
         except ValueError:
             ap.dev_total = -1
+        if self._native_pods is not None:
+            ap.raw = json.dumps(pod, separators=(",", ":"))
         if not self.core.observe(ap):
             return  # a stale copy (e.g. a slow LIST racing the watch): never step back
+        if self._native_pods is not None:
+            self._flush()
+            return
         if self.core.has_pod(rec.uid):
             self._recs[rec.uid] = rec
         else:
@@ -257,14 +342,15 @@ class AllocationState:
 
     # ------------------------------------------------------------ Allocate
     def candidates(self) -> list[PodRec]:
-        return [self._recs[u] for u in self.core.candidates() if u in self._recs]
+        pods = self.pods
+        return [pods[u] for u in self.core.candidates() if u in pods]
 
     def match(self, units: int) -> tuple[PodRec | None, bool]:
         """(pod, whole_pod) for an Allocate of ``units``: a whole pod of that size (earliest ASSUME_TIME),
         else a later container of a pod whose first container was allocated, else the first container
         of a multi-container pod that has a container of that size."""
         uid, whole = self.core.match(int(units))
-        return (self.fresh(self._recs.get(uid)), whole) if uid else (None, False)
+        return (self.fresh(self.pods.get(uid)), whole) if uid else (None, False)
 
     def fresh(self, rec: PodRec | None) -> PodRec | None:
         """``rec`` with the allocation fields the native state holds for it: the native pod feed may be ahead of the
@@ -272,6 +358,8 @@ class AllocationState:
         or GPU would take the wrong branch)."""
         if rec is None:
             return None
+        if self._native_pods is not None:
+            return self._native_pods.get(rec.uid, rec)  # the native state is the one view
         v = self.core.pod_view(rec.uid)
         if v is None or not _older_rv(rec.rv, v["rv"]):
             return rec
@@ -328,7 +416,7 @@ class AllocationState:
         self.core.set_owner(aid, uid)
 
     def pod_by_key(self, key: str) -> PodRec | None:
-        for r in self._recs.values():
+        for r in self.pods.values():
             if r.key == key:
                 return r
         return None
@@ -340,12 +428,13 @@ class AllocationState:
 
     def snapshot(self) -> dict:
         """What ``/debug/state`` and the tests look at."""
+        pods = dict(self.pods.items())
         return {
             "pods": {r.key: {"uid": r.uid, "gpu": r.dev, "request": r.request, "assigned": r.assigned,
-                             "phase": r.phase} for r in self._recs.values()},
+                             "phase": r.phase} for r in pods.values()},
             "candidates": [r.key for r in self.candidates()],
-            "partial": {self._recs[u].key if u in self._recs else u: v for u, v in self.partial.items()},
-            "cu_partitions": {str(i): {self._recs[u].key if u in self._recs else u: len(c) for u, c in cp.held().items()}
+            "partial": {pods[u].key if u in pods else u: v for u, v in self.partial.items()},
+            "cu_partitions": {str(i): {pods[u].key if u in pods else u: len(c) for u, c in cp.held().items()}
                               for i, cp in self.cus.items()},
             "cu_free": {str(i): cp.free_count() for i, cp in self.cus.items()},
             "records": self.core.record_count(),

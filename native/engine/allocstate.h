@@ -86,6 +86,9 @@ struct AllocPod {
   std::string cu_mask;        // gpushare.amd.com/cu-mask
   int64_t hold_idx = -1;      // gpushare.amd.com/hold-idx
   std::string hold_partner;   // gpushare.amd.com/hold-partner
+  // the pod object as the apiserver sent it, when a feed kept it (the shipped plugin's pod feed and its own PATCH
+  // responses: the Python side reads pod objects from here instead of running a second watch); "" otherwise
+  std::string raw;
   bool pending() const { return phase == "Pending" || phase.empty(); }
 };
 

@@ -897,7 +897,10 @@ class PyDpServer {
       f.resync = true;
       for (size_t k = 0; k < lv.size(); ++k) {
         AllocPod ap;
-        if (parse_alloc_pod(lv.doc(k), lv.obj(k), profile_, &ap)) f.pods.push_back(std::move(ap));
+        if (parse_alloc_pod(lv.doc(k), lv.obj(k), profile_, &ap)) {
+          ap.raw = std::string(lv.doc(k).raw(lv.obj(k)));
+          f.pods.push_back(std::move(ap));
+        }
       }
       push_feed(std::move(f));
     };
@@ -905,12 +908,20 @@ class PyDpServer {
       Feed f;
       AllocPod ap;
       if (!parse_alloc_pod(d, obj, profile_, &ap)) return;
+      if (ev != Ev::Deleted) ap.raw = std::string(d.raw(obj));
       f.deleted = ev == Ev::Deleted;
       f.pods.push_back(std::move(ap));
       push_feed(std::move(f));
     };
     feed_r_ = std::make_unique<Reflector>(api_from(api), rc, h);
     feed_r_->start();
+  }
+
+  // the feed's first LIST has arrived (false: timeout or no feed); poll() then applies it
+  bool feed_synced(double timeout_s) {
+    if (!feed_r_) return false;
+    py::gil_scoped_release nogil;
+    return feed_r_->wait_synced(timeout_s);
   }
 
   int fd() const { return srv_ ? srv_->fd() : -1; }
@@ -1028,6 +1039,11 @@ class PyDpServer {
     d["last_slow_reason"] = last_why_;
     d["waited"] = waited_;
     d["feed_events"] = feed_events_;
+    if (feed_r_) {
+      d["feed_relists"] = feed_r_->relists();
+      d["feed_rewatches"] = feed_r_->rewatches();
+      d["feed_errors"] = feed_r_->errors();
+    }
     d["feed"] = static_cast<bool>(feed_r_);
     d["serving_thread"] = serving_.joinable();
     d["journaling"] = core_->journaling();
@@ -1620,6 +1636,7 @@ PYBIND11_MODULE(_engine, m) {
       .def_readwrite("cu_mask", &AllocPod::cu_mask)
       .def_readwrite("hold_idx", &AllocPod::hold_idx)
       .def_readwrite("hold_partner", &AllocPod::hold_partner)
+      .def_readwrite("raw", &AllocPod::raw)
       .def_property_readonly("pending", &AllocPod::pending);
 
   auto rec_dict = [](const AllocRecord& r) {
@@ -1666,6 +1683,31 @@ PYBIND11_MODULE(_engine, m) {
              d["hold_partner"] = p->hold_partner;
              return d;
            }, py::call_guard<AllocLock>())
+      // every pod the state holds, for the Python views: (uid, key, ns, name, rv, phase, dev, request, containers,
+      // assume_time, creation, assigned, complete, cu_count, cu_mask, hold_idx, hold_partner)
+      .def("pod_views", [](const AllocState& s) {
+        py::list out;
+        for (const auto& kv : s.pods()) {
+          const AllocPod& p = kv.second;
+          out.append(py::make_tuple(p.uid, p.key, p.ns, p.name, p.rv, p.phase, p.dev, p.request, p.containers,
+                                    p.assume_time, p.creation, p.assigned, p.complete, p.cu_count, p.cu_mask,
+                                    p.hold_idx, p.hold_partner));
+        }
+        return out;
+      }, py::call_guard<AllocLock>())
+      .def("pod_full", [](const AllocState& s, const std::string& uid) -> py::object {
+        const AllocPod* pp = s.pod(uid);
+        if (!pp) return py::none();
+        const AllocPod& p = *pp;
+        return py::make_tuple(p.uid, p.key, p.ns, p.name, p.rv, p.phase, p.dev, p.request, p.containers,
+                              p.assume_time, p.creation, p.assigned, p.complete, p.cu_count, p.cu_mask, p.hold_idx,
+                              p.hold_partner);
+      }, py::call_guard<AllocLock>())
+      .def("pod_json", [](const AllocState& s, const std::string& uid) -> py::object {
+        const AllocPod* p = s.pod(uid);
+        if (!p || p->raw.empty()) return py::none();
+        return py::bytes(p->raw);
+      }, py::call_guard<AllocLock>())
       .def("pod_uids", [](const AllocState& s) {
         std::vector<std::string> out;
         for (const auto& kv : s.pods()) out.push_back(kv.first);
@@ -1840,6 +1882,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("set_fast", &PyDpServer::set_fast, py::call_guard<AllocLock>())
       .def("set_state", &PyDpServer::set_state, py::keep_alive<1, 2>(), py::call_guard<AllocLock>())
       .def("start_feed", &PyDpServer::start_feed, py::call_guard<AllocLock>())
+      .def("feed_synced", &PyDpServer::feed_synced, py::arg("timeout") = 30.0)
       .def("stats", &PyDpServer::stats, py::call_guard<AllocLock>())
       .def("close", &PyDpServer::close);
   py::class_<h2::Client>(m, "H2Client")

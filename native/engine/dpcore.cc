@@ -444,6 +444,7 @@ bool DpCore::finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* w
     AllocPod committed;
     std::string perr;
     if (p.ok && p.status < 300 && d.parse(p.resp, &perr) && parse_alloc_pod(d, 0, cfg_.profile, &committed)) {
+      committed.raw = p.resp;
       state_->observe(committed);
       state_->set_inflight(p.pod.uid, false);
       ev->uid = p.pod.uid;
@@ -477,6 +478,7 @@ bool DpCore::finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* w
     AllocPod committed;
     std::string perr;
     bool good = p.ok && p.status < 300 && d.parse(p.resp, &perr) && parse_alloc_pod(d, 0, cfg_.profile, &committed);
+    if (good) committed.raw = p.resp;
     if (!good) {
       CuPartitioner* cp = state_->cus(static_cast<int>(p.pod.dev));
       if (cp && !p.had_cus) cp->release(p.pod.uid);

@@ -419,7 +419,8 @@ def test_plugin_allocate_retries_conflicts_and_apiserver_errors():
             pc = PluginClient(plugin.socket_path)
             for i in range(4):
                 await client.create("pods", bound_pod(f"p{i}", 4, dev=0, assume=10 + i, dev_total=16))
-            api_srv.server.faults.update({"conflict_rate": 0.25, "error_rate": 0.25, "seed": 5})
+            # every commit meets a 500 or a 409 while the faults are on (early answer: the Allocate is answered first)
+            api_srv.server.faults.update({"conflict_rate": 0.5, "error_rate": 1.0, "seed": 5})
             ids = fake_ids(devs[0], 16)
             for i in range(4):
                 r = await pc.allocate([ids[4 * i: 4 * i + 4]])
