@@ -225,6 +225,7 @@ def set_latency(api_batch, ms: float):
 
 
 SWEEP_LATENCIES_MS = (0, 1, 2, 5)
+APISERVER_THREADS_MULTI = 1
 
 
 class WaveRunner:
@@ -380,7 +381,7 @@ def _plugin_debug(E, url: str | None) -> dict | None:
     return {"grpc": {k: g.get(k) for k in ("impl", "fast_allocate", "slow_allocate", "fast_preferred",
                                            "slow_preferred", "patch_failures", "guard_by_ids", "journaling",
                                            "early_answer_backlog", "waited", "feed_events", "passes",
-                                           "last_slow_reason", "handler_us")},
+                                           "last_slow_reason", "handler_us", "allocate_phases_us", "lock_wait")},
             "stats": d.get("stats"), "reconcile": d.get("reconcile"),
             # mean seconds per native fast-path Allocate: match, isolation files, record + answer (handler)
             "timing": {k: (v / max(1, (d.get("timing") or {}).get("n", 0)) if k != "n" else v)
@@ -449,6 +450,8 @@ def parse():
                          "stand-in, as the DaemonSet runs it (process), or served from the stand-in's process (grpc)")
     ap.add_argument("--sweep", type=int, default=1, help="1: run the latency sweep after the timed region")
     ap.add_argument("--sweep-steps", type=int, default=8)
+    ap.add_argument("--apiserver-threads", type=int, default=0,
+                    help="event loops of the fake apiserver (0: auto; GSX_FAKEAPI_THREADS overrides)")
     return ap.parse_args()
 
 
@@ -515,6 +518,11 @@ def main():
         # out (scheduler saw the 32nd pod of an N = 8 wave 0.96 ms in, 0.53 ms with a second CPU; per-wave p50
         # 13.0k -> 19.2k pods/s at N = 8, 10.6k -> 15.7k at N = 4; N = 1 unchanged, profiles/r03_ab/)
         widths["rank0"] = 2
+    # the fake apiserver's event loops (a shared store): GSX_FAKEAPI_THREADS, else --apiserver-threads, else one loop
+    # at N = 1 and APISERVER_THREADS_MULTI at N > 1, each on its own CPU
+    api_threads = int(os.environ.get("GSX_FAKEAPI_THREADS", "0")) or a.apiserver_threads or (
+        1 if world == 1 else APISERVER_THREADS_MULTI)
+    widths["apiserver"] = api_threads
     if a.pin_widths:
         widths.update(json.loads(a.pin_widths))
     mode = a.pin if a.pin != "auto" else "spread"
@@ -543,7 +551,7 @@ def main():
         from gsxtools.cluster import (start_apiserver, start_extender, start_node_agent,
                                                                  start_scheduler)
 
-        api = start_apiserver(cpus=cpu_plan.get("apiserver"))
+        api = start_apiserver(cpus=cpu_plan.get("apiserver"), threads=api_threads)
         children.append(api)
         ext = start_extender(api.url, profile=a.profile, bind_mode=a.bind_mode, cpus=cpu_plan.get("extender"),
                              bind_order=a.bind_order)
@@ -1003,6 +1011,10 @@ def main():
             "cpu_pinning": {k: v for k, v in cpu_plan.items()} or "none",
             "api_latency_ms": a.api_latency_ms,
             "latency_sweep": sweep,
+            # the headline path (node agent + plugin as above, bind mode binding, default bind order) per apiserver
+            # latency: kubelet admits serially, so each ms of apiserver latency the Allocate waits costs throughput
+            "latency_sweep_pods_per_s": {str(r["api_latency_ms"]): r["pods_per_s"] for r in (sweep or [])
+                                         if r.get("bind_mode") == "binding" and r.get("bind_order") == a.bind_order},
             "reference_client": ref_client,
             # the shipped gRPC device plugin on the kubelet path (untimed by the headline, same waves)
             # extra rows (untimed by the headline, same waves): the Python kubelet stand-in driving the shipped plugin

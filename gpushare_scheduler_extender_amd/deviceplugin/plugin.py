@@ -257,6 +257,8 @@ class GpuSharePlugin:
         self._set_devices(devices)
         if native_views:
             self.state.use_native_views()
+        if self.reconciler is not None:
+            self.state.core.expect_owner_reports(True)
         self.state.resync(pods)
         self.stats["layout_changes"] = self.stats.get("layout_changes", 0) + 1
         log.warning("device layout changed: %s -> %s", old,
@@ -315,6 +317,8 @@ class GpuSharePlugin:
                 "fast": os.environ.get("GSX_PLUGIN_FAST", "1") == "1",
                 # the serving thread polls this long after a pass before it sleeps (kubelet's calls come in bursts)
                 "spin_us": float(os.environ.get("GSX_PLUGIN_SPIN_US", "200")),
+                # answered Allocates reach this loop's bookkeeping at most this often (a pass takes the state lock)
+                "py_event_ms": float(os.environ.get("GSX_PLUGIN_PY_EVENT_MS", "2")),
                 # early answer (opt-in): answer a first container's Allocate once its record is journaled, commit
                 # ASSIGNED=true behind it (kubelet's serial admission no longer waits an apiserver round trip)
                 "early_answer": self.early_answer, "journal": self.journal_path}

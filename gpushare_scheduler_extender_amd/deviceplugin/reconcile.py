@@ -421,6 +421,9 @@ class Reconciler:
                 log.warning("reconcile pass failed: %r", e)
 
     def start(self):
+        # until the first report, a pod's going does not end the allocations built for it (a swapped container may
+        # hold one): kubelet's report decides (AllocState::expect_owner_reports)
+        self.state.core.expect_owner_reports(True)
         if self._task is None:
             self._task = asyncio.get_running_loop().create_task(self.run(), name="gsx-reconcile")
 

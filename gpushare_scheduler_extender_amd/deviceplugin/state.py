@@ -438,5 +438,8 @@ class AllocationState:
                               for i, cp in self.cus.items()},
             "cu_free": {str(i): cp.free_count() for i, cp in self.cus.items()},
             "records": self.core.record_count(),
+            # the physical account (units kubelet has handed out per GPU, by Allocate IDs) the Allocate guard reads
+            "physical": {str(i): self.core.physical_used(i) for i in self.cus},
+            "held": self.core.held_count(),
             "native": True,
         }

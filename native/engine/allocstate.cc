@@ -307,10 +307,10 @@ void AllocState::release(const std::string& uid) {
   std::vector<std::string> gone;
   for (const auto& kv : records_) {
     const AllocRecord& r = kv.second;
-    if (r.owner == uid || (r.owner.empty() && r.uid == uid && !owners_reported_)) gone.push_back(kv.first);
+    if (r.owner == uid || (r.owner.empty() && r.uid == uid && !owners_known())) gone.push_back(kv.first);
   }
   for (const auto& aid : gone) drop_record(aid);
-  if (!owners_reported_) {
+  if (!owners_known()) {
     // nobody reports what kubelet holds: an allocation is taken to end with the pod it was built for
     for (auto h = held_.begin(); h != held_.end();) {
       auto cur = h++;

@@ -160,8 +160,15 @@ class AllocState {
   // With kubelet's PodResources reconciled (`on`), a record whose holder kubelet has not reported yet is not
   // dropped with the pod it was built for: after a swap another pod's container may be running with it.  The
   // reconciler drops it once kubelet no longer lists its IDs.
-  void set_owners_reported(bool on) { owners_reported_ = on; }
+  void set_owners_reported(bool on) {
+    owners_reported_ = on;
+    if (!on) owners_expected_ = false;  // nobody will report: records and holds end with their pods again
+  }
   bool owners_reported() const { return owners_reported_; }
+  // A PodResources reconciler runs but has not reported yet: a pod's going does not end the allocations built
+  // for it (another container may hold one: a swap), until kubelet's first report says who holds what.
+  void expect_owner_reports(bool on) { owners_expected_ = on; }
+  bool owners_known() const { return owners_reported_ || owners_expected_; }
   // After the annotations of P and Q were exchanged because P holds `aid` (built for Q): that record now
   // describes P, whatever described P describes Q, and the CU partitions follow.
   void move_records(const std::string& p_uid, const std::string& q_uid, const std::string& aid);
@@ -219,6 +226,7 @@ class AllocState {
   void hold(const std::vector<std::string>& ids, Held h);
   void unhold(std::map<std::vector<std::string>, Held>::iterator it);
   bool owners_reported_ = false;
+  bool owners_expected_ = false;
   AllocStats stats_;
 };
 

@@ -845,6 +845,7 @@ class PyDpServer {
     if (cfg.contains("journal") && !cfg["journal"].is_none()) c.journal = cfg["journal"].cast<std::string>();
     if (cfg.contains("fast")) fast_ = cfg["fast"].cast<bool>();
     if (cfg.contains("spin_us")) spin_us_ = cfg["spin_us"].cast<double>();
+    if (cfg.contains("py_event_ms")) py_event_s_ = cfg["py_event_ms"].cast<double>() * 1e-3;
     node_ = c.node;
     profile_ = c.profile;
     state_ = &state;
@@ -1033,6 +1034,13 @@ class PyDpServer {
     d["slow_preferred"] = s.slow_preferred;
     d["patch_failures"] = s.patch_failures;
     d["guard_by_ids"] = s.guard_by_ids;
+    if (s.phased) {
+      const double k = 1e6 / static_cast<double>(s.phased);
+      d["allocate_phases_us"] = py::dict(py::arg("decode") = s.ph_decode * k, py::arg("match") = s.ph_match * k,
+                                         py::arg("claim") = s.ph_claim * k, py::arg("build") = s.ph_build * k,
+                                         py::arg("body") = s.ph_body * k, py::arg("record") = s.ph_record * k,
+                                         py::arg("journal") = s.ph_journal * k, py::arg("encode") = s.ph_encode * k);
+    }
     d["calls"] = srv_ ? srv_->calls() : 0;
     d["connections"] = srv_ ? srv_->connections() : 0;
     d["fast"] = fast_;
@@ -1050,6 +1058,8 @@ class PyDpServer {
     d["early_answer_backlog"] = static_cast<uint64_t>(bg_backlog());
     d["passes"] = passes_;
     // time inside the handlers (decode, match, respond), per call: what the plugin adds to kubelet's round trip
+    d["lock_wait"] = py::dict(py::arg("total_ms") = 1e3 * lock_wait_s_, py::arg("max_us") = 1e6 * lock_wait_max_s_,
+                              py::arg("over_5us") = lock_waits_);
     d["handler_us"] = py::dict(py::arg("get_preferred") = h_pref_n_ ? 1e6 * h_pref_s_ / h_pref_n_ : 0.0,
                                py::arg("allocate") = h_alloc_n_ ? 1e6 * h_alloc_s_ / h_alloc_n_ : 0.0,
                                py::arg("n_preferred") = h_pref_n_, py::arg("n_allocate") = h_alloc_n_);
@@ -1141,14 +1151,21 @@ class PyDpServer {
     for (;;) {
       pollfd pf{ep, POLLIN, 0};
       if (mono() < spin_until) {
-        if (::poll(&pf, 1, 0) == 0) {
+        if (::poll(&pf, 1, 0) == 0 && !(py_deferred_ && mono() >= py_due_)) {
           if (stop_serving_) return;  // read without the lock: only a faster exit; checked again below
           continue;
         }
       } else {
-        ::poll(&pf, 1, 100);
+        int ms = 100;
+        if (py_deferred_) ms = std::max(0, std::min(ms, static_cast<int>((py_due_ - mono()) * 1e3) + 1));
+        ::poll(&pf, 1, ms);
       }
+      const double tl0 = mono();
       std::unique_lock<std::recursive_mutex> lock(alloc_mu());  // the state lock, not the GIL
+      const double tl = mono() - tl0;
+      lock_wait_s_ += tl;
+      lock_wait_max_s_ = std::max(lock_wait_max_s_, tl);
+      lock_waits_ += tl > 5e-6;
       if (stop_serving_ || !srv_) return;
       one_pass();
       // the ASSIGNED patches of this pass's Allocates, here rather than on the worker (two thread hops fewer on
@@ -1172,10 +1189,21 @@ class PyDpServer {
         if (stop_serving_ || !srv_) return;
       }
       spin_until = spin_us_ > 0 ? mono() + spin_us_ * 1e-6 : 0;
-      // also when the feed released a pod whose records went: Python cleans up their isolation files
-      if (!pending_.empty() || !events_.empty() || (state_ && state_->dropped_pending())) {
-        uint64_t one = 1;
-        (void)!::write(pyfd_, &one, sizeof one);
+      // also when the feed released a pod whose records went: Python cleans up their isolation files.  Calls for
+      // the Python slow path wake it at once; bookkeeping events (answered Allocates, landed commits) at most every
+      // py_event_s_: a Python pass takes the state lock, and one per Allocate would sit in the next admission's way
+      const bool urgent = !pending_.empty();
+      if (urgent || !events_.empty() || (state_ && state_->dropped_pending())) {
+        const double now = mono();
+        if (urgent || now - py_signal_at_ >= py_event_s_) {
+          uint64_t one = 1;
+          (void)!::write(pyfd_, &one, sizeof one);
+          py_signal_at_ = now;
+          py_deferred_ = false;
+        } else if (!py_deferred_) {
+          py_deferred_ = true;
+          py_due_ = py_signal_at_ + py_event_s_;
+        }
       }
     }
   }
@@ -1441,6 +1469,11 @@ class PyDpServer {
   std::atomic<bool> stop_serving_{false};  // written under the state lock
   int pyfd_ = -1;              // readable: pending_ / events_ waiting for poll()
   double h_pref_s_ = 0, h_alloc_s_ = 0;
+  double py_event_s_ = 0.002;  // cfg "py_event_ms": how often answered Allocates are handed to Python at most
+  double py_signal_at_ = 0, py_due_ = 0;
+  bool py_deferred_ = false;
+  double lock_wait_s_ = 0, lock_wait_max_s_ = 0;  // the serving thread waiting for the state lock (Python holds it)
+  uint64_t lock_waits_ = 0;                        // waits over 5 us
   uint64_t h_pref_n_ = 0, h_alloc_n_ = 0;
   double spin_us_ = 200;       // poll without sleeping this long after a pass (cfg "spin_us"; 0: always block)
   uint64_t passes_ = 0;
@@ -1686,15 +1719,28 @@ PYBIND11_MODULE(_engine, m) {
       // every pod the state holds, for the Python views: (uid, key, ns, name, rv, phase, dev, request, containers,
       // assume_time, creation, assigned, complete, cu_count, cu_mask, hold_idx, hold_partner)
       .def("pod_views", [](const AllocState& s) {
+        std::vector<AllocPod> copy;
+        {
+          AllocLock lock;
+          copy.resize(s.pods().size());
+          size_t i = 0;
+          for (const auto& kv : s.pods()) {  // every field but the raw JSON
+            const AllocPod& p = kv.second;
+            AllocPod& c = copy[i++];
+            c.uid = p.uid, c.key = p.key, c.ns = p.ns, c.name = p.name, c.rv = p.rv, c.phase = p.phase;
+            c.creation = p.creation, c.dev = p.dev, c.request = p.request, c.containers = p.containers;
+            c.assume_time = p.assume_time, c.assigned = p.assigned, c.complete = p.complete;
+            c.cu_count = p.cu_count, c.cu_mask = p.cu_mask, c.hold_idx = p.hold_idx, c.hold_partner = p.hold_partner;
+          }
+        }
         py::list out;
-        for (const auto& kv : s.pods()) {
-          const AllocPod& p = kv.second;
+        for (const AllocPod& p : copy) {
           out.append(py::make_tuple(p.uid, p.key, p.ns, p.name, p.rv, p.phase, p.dev, p.request, p.containers,
                                     p.assume_time, p.creation, p.assigned, p.complete, p.cu_count, p.cu_mask,
                                     p.hold_idx, p.hold_partner));
         }
         return out;
-      }, py::call_guard<AllocLock>())
+      })
       .def("pod_full", [](const AllocState& s, const std::string& uid) -> py::object {
         const AllocPod* pp = s.pod(uid);
         if (!pp) return py::none();
@@ -1733,6 +1779,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("set_inflight", &AllocState::set_inflight, py::call_guard<AllocLock>())
       .def("set_owners_reported", &AllocState::set_owners_reported, py::call_guard<AllocLock>())
       .def("owners_reported", &AllocState::owners_reported, py::call_guard<AllocLock>())
+      .def("expect_owner_reports", &AllocState::expect_owner_reports, py::call_guard<AllocLock>())
       .def("inflight", &AllocState::inflight, py::call_guard<AllocLock>())
       .def("first_container_committed", &AllocState::first_container_committed, py::call_guard<AllocLock>())
       .def("later_container_allocated", &AllocState::later_container_allocated, py::call_guard<AllocLock>())
@@ -1792,11 +1839,18 @@ PYBIND11_MODULE(_engine, m) {
            }, py::call_guard<AllocLock>())
       .def("set_owner", &AllocState::set_owner, py::call_guard<AllocLock>())
       .def("move_records", &AllocState::move_records, py::call_guard<AllocLock>())
+      // copied under the state lock, converted to Python objects after it (the serving thread may be waiting)
       .def("records", [rec_dict](const AllocState& s) {
+             std::vector<AllocRecord> copy;
+             {
+               AllocLock lock;
+               copy.reserve(s.records().size());
+               for (const auto& kv : s.records()) copy.push_back(kv.second);
+             }
              py::list out;
-             for (const auto& kv : s.records()) out.append(rec_dict(kv.second));
+             for (const auto& r : copy) out.append(rec_dict(r));
              return out;
-           }, py::call_guard<AllocLock>())
+           })
       .def("record_count", [](const AllocState& s) { return s.records().size(); }, py::call_guard<AllocLock>())
       .def("take_dropped", [rec_dict](AllocState& s) {
              py::list out;

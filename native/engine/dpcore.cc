@@ -313,6 +313,7 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   }
   const std::vector<std::string>& ids = ids_per[0];
   const int64_t units = static_cast<int64_t>(ids.size());
+  const double td = mono_s();
   auto m = state_->match(units);
   const double tm = mono_s();
 
@@ -367,6 +368,7 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
     *why = "CU partition: " + err;
     return DpStep::Slow;
   }
+  const double tc = mono_s();
   auto p = std::make_unique<DpPending>();
   p->pod = pod;
   p->whole = m.second;
@@ -375,6 +377,7 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   p->ids = ids;
   p->on_gpu = on_gpu;
   p->cr = build_response(pod, dev, units, cus, cfg_.mount_mode, cfg_.profile);
+  const double tb = mono_s();
   p->t0 = t0;
   p->tm = tm;
   p->ti0 = mono_s();
@@ -421,7 +424,14 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
     p->answered = true;
     p->ok = true;
     state_->first_container_committed(pod.uid, units, p->whole);  // claimed (in flight) until the patch lands
+    const double tbody = mono_s();
     record_and_answer(*p, resp, ev);
+    stats_.ph_decode += td - t0;
+    stats_.ph_match += tm - td;
+    stats_.ph_claim += tc - tm;
+    stats_.ph_build += tb - tc;
+    stats_.ph_body += tbody - tb;
+    stats_.phased++;
     ev->committed = true;
     *pend = std::move(p);
     return DpStep::AnsweredPending;
@@ -503,12 +513,18 @@ void DpCore::record_and_answer(DpPending& p, std::string* resp, DpEvent* ev) {
   std::snprintf(aid, sizeof aid, "%llx-%x-n%llu", static_cast<unsigned long long>(wall_ns() / 1000000),
                 static_cast<unsigned>(::getpid()), static_cast<unsigned long long>(++aid_));
   auto cm = p.cr.annotations.find(kCuMaskAnn);
+  const double tr0 = mono_s();
   AllocRecord& rec = state_->record(p.pod.uid, p.ids, p.units,
                                     cm != p.cr.annotations.end() ? cm->second : p.pod.cu_mask, aid, wall_s());
   rec.iso = p.iso;
   if (p.on_gpu) state_->mark_on_gpu(aid, true);
+  const double tr1 = mono_s();
   if (p.answered) journal_append(*state_->record_by_aid(aid));  // durable before kubelet has the answer
+  const double tj = mono_s();
   *resp = dp::encode_allocate_response({p.cr});
+  stats_.ph_record += tr1 - tr0;
+  stats_.ph_journal += tj - tr1;
+  stats_.ph_encode += mono_s() - tj;
   stats_.fast_allocate++;
   ev->uid = p.pod.uid;
   ev->key = p.pod.key;

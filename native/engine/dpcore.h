@@ -120,6 +120,11 @@ class DpCore {
   struct Stats {
     uint64_t fast_allocate = 0, fast_preferred = 0, slow_allocate = 0, slow_preferred = 0, patch_failures = 0;
     uint64_t guard_by_ids = 0;  // the records said full, kubelet's IDs said there is room
+    // fast-path Allocate phases, summed seconds over `phased` answers: decode, match, guard + CU claim, response
+    // build, commit body, record (incl. the physical account), journal line, response encode
+    double ph_decode = 0, ph_match = 0, ph_claim = 0, ph_build = 0, ph_body = 0, ph_record = 0, ph_journal = 0,
+           ph_encode = 0;
+    uint64_t phased = 0;
   };
   const Stats& stats() const { return stats_; }
   // early answer: the journal's lines move to <journal>.old (appended if a previous checkpoint left one) and the

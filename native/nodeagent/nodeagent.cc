@@ -404,6 +404,7 @@ class Agent {
     if (r == running_.end()) return;
     int dev = r->second;
     running_.erase(r);
+    running_bytes_.erase(uid);
     forget_ids_locked(uid);
     for (auto& kv : devices_) {
       if (CuPartitioner* cp = state_->cus(kv.first)) cp->release(uid);
@@ -870,6 +871,21 @@ class Agent {
     }
     if (!why.empty()) {
       lk.lock();
+      if (rst == 409) {  // what this agent believes the GPU holds, next to the runtime's refusal
+        int64_t sum = 0;
+        std::string who;
+        for (const auto& kv : running_) {
+          if (kv.second != dev_idx) continue;
+          auto b = running_bytes_.find(kv.first);
+          const int64_t n = b == running_bytes_.end() ? -1 : b->second / unit_;
+          sum += n;
+          who += " " + kv.first.substr(0, 8) + ":" + std::to_string(n);
+        }
+        size_t rel = 0;
+        for (const auto& r : releases_) rel += r.second == dev_idx;
+        why += " (agent: " + std::to_string(sum) + " units running on GPU " + std::to_string(dev_idx) + ":" + who +
+               "; " + std::to_string(rel) + " releases queued, " + std::to_string(releasing_[dev_idx]) + " in flight)";
+      }
       failed_++;
       bad_ += static_cast<uint64_t>(bad);
       if (!cus.empty() && cp) cp->release(uid);
@@ -887,6 +903,7 @@ class Agent {
     }
     lk.lock();
     running_[uid] = dev_idx;
+    running_bytes_[uid] = request * unit_;
     allocations_[uid] = envs;
     admitted_++;
     lk.unlock();
@@ -984,6 +1001,7 @@ class Agent {
   std::unordered_map<std::string, std::string> uid_key_;                 // uid -> ns/name of every used_ids_ pod
   std::string pr_sock_;                    // kubelet's PodResources API socket (with --plugin-spawn)
   std::string plugin_debug_file_, plugin_debug_url_;
+  std::unordered_map<std::string, int64_t> running_bytes_;  // uid -> bytes its slice was carved with
   std::unique_ptr<h2::Server> pr_srv_;
   std::thread pr_thread_;
   std::atomic<bool> pr_stop_{false};
