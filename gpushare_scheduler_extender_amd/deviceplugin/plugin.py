@@ -160,6 +160,11 @@ class GpuSharePlugin:
         # early answer (default; GSX_PLUGIN_EARLY_ANSWER=0 turns it off): needs the journal next to the checkpoint
         # (the record must be durable before kubelet has the answer)
         self.early_answer = bool(self.checkpoint) and os.environ.get("GSX_PLUGIN_EARLY_ANSWER", "1") == "1"
+        # GetPreferredAllocation (GSX_PLUGIN_PREFERRED=1): kubelet then asks before every Allocate, and the answer
+        # steers the pod's unit IDs onto its GPU (kubelet's per-ID accounting then also bounds that GPU).  Off by
+        # default, as the reference's plugin: the IDs are interchangeable units, the Allocate is matched by size, and
+        # kubelet's serial admission pays one gRPC round trip per pod less
+        self.preferred = os.environ.get("GSX_PLUGIN_PREFERRED", "0") == "1"
         self.checkpoint_interval = 0.2
         self._dirty = False
         self._persist_task: asyncio.Task | None = None
@@ -317,6 +322,7 @@ class GpuSharePlugin:
                 "fast": os.environ.get("GSX_PLUGIN_FAST", "1") == "1",
                 # the serving thread polls this long after a pass before it sleeps (kubelet's calls come in bursts)
                 "spin_us": float(os.environ.get("GSX_PLUGIN_SPIN_US", "200")),
+                "preferred": self.preferred,
                 # answered Allocates reach this loop's bookkeeping at most this often (a pass takes the state lock)
                 "py_event_ms": float(os.environ.get("GSX_PLUGIN_PY_EVENT_MS", "2")),
                 # early answer (opt-in): answer a first container's Allocate once its record is journaled, commit
@@ -402,7 +408,7 @@ class GpuSharePlugin:
 
     # ------------------------------------------------------------ gRPC handlers
     async def GetDevicePluginOptions(self, request, context):
-        return api.DevicePluginOptions(pre_start_required=False, get_preferred_allocation_available=True)
+        return api.DevicePluginOptions(pre_start_required=False, get_preferred_allocation_available=self.preferred)
 
     async def ListAndWatch(self, request, context):
         seen = -1
@@ -926,6 +932,7 @@ class GpuSharePlugin:
             self.isolation.install()  # the fast path writes per-pod files next to the installed library
         cfg = self._native_config()
         self._native = native().DpServer(self.socket_path, self.state.core, cfg)
+        self._native.set_ready(False)  # every call UNAVAILABLE until serve(): records and unlanded commits first
         self._native_serving = False
         if os.environ.get("GSX_PLUGIN_FEED", "1") == "1":
             self._native.start_feed(cfg["api"])  # this node's pods into the state from a native reflector
@@ -947,6 +954,7 @@ class GpuSharePlugin:
                 self._open_native()
             self._native_serving = True
             self._sync_native()
+            self._native.set_ready(True)
             if os.environ.get("GSX_PLUGIN_SERVE_THREAD", "1") == "1":
                 # the endpoint is served from a native thread that never needs the GIL (a native lock guards the
                 # allocation state shared with this loop), so a busy Python loop does not delay a fast Allocate
@@ -977,7 +985,8 @@ class GpuSharePlugin:
                                   response_deserializer=oc.FromString)
             await call(api.RegisterRequest(version=api.VERSION, endpoint=self.endpoint,
                                            resource_name=self.profile.resource,
-                                           options=api.DevicePluginOptions(get_preferred_allocation_available=True)),
+                                           options=api.DevicePluginOptions(
+                                               get_preferred_allocation_available=self.preferred)),
                        timeout=timeout)
         self.stats["registrations"] += 1
         log.info("registered %s with kubelet at %s", self.profile.resource, self.kubelet_socket)

@@ -82,6 +82,7 @@ class NodeAgent:
         self.report_status = report_status
         self.pods = Informer(client, "pods", field_selector=f"spec.nodeName={node}")
         self.pclient = PluginClient(plugin_socket) if plugin_socket else None
+        self._preferred: bool | None = None  # the plugin's GetPreferredAllocation option, read on first use
         self._own_plugin = plugin is None and plugin_socket is None
         if self._own_plugin:
             plugin = GpuSharePlugin(client, node, devices, profile, unit=unit, mount_mode=self.mount_mode,
@@ -186,8 +187,13 @@ class NodeAgent:
         if len(free) < units:
             raise AllocateError(f"kubelet: {units} {self.profile.resource} requested, {len(free)} IDs free")
         t0 = time.perf_counter()
-        pref = await self.pclient.preferred(free, units)
-        ids = list(pref.container_responses[0].deviceIDs)
+        if self._preferred is None:  # as kubelet: ask GetPreferredAllocation only if the plugin advertises it
+            self._preferred = bool((await self.pclient.options()).get_preferred_allocation_available)
+        if self._preferred:
+            pref = await self.pclient.preferred(free, units)
+            ids = list(pref.container_responses[0].deviceIDs)
+        else:
+            ids = free[:units]  # kubelet's own pick without a preference
         t1 = time.perf_counter()
         r = (await self.pclient.allocate([ids])).container_responses[0]
         self.timing["grpc_preferred"] += t1 - t0

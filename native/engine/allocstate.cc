@@ -1,6 +1,7 @@
 #include "allocstate.h"
 
 #include <chrono>
+#include <unordered_set>
 
 #include <algorithm>
 #include <cstdint>
@@ -455,35 +456,49 @@ AllocRecord& AllocState::record(const std::string& uid, const std::vector<std::s
                                 const std::string& cu_mask, const std::string& aid, double t) {
   std::vector<std::string> ids(ids_in);
   std::sort(ids.begin(), ids.end());
+  const std::string key = ids.empty() ? std::string() : id_key(ids);
   if (!ids.empty()) {
-    auto old = by_ids_.find(ids);
+    auto old = by_ids_.find(key);
     if (old != by_ids_.end()) drop_record(old->second);  // kubelet re-used the IDs of a finished pod
   }
   AllocRecord r;
   r.aid = aid;
-  r.ids = ids;
   r.uid = uid;
   auto p = pods_.find(uid);
   r.dev = p != pods_.end() ? p->second.dev : -1;
   r.units = units;
   r.cu_mask = cu_mask;
   r.t = t;
-  if (!ids.empty()) by_ids_[ids] = aid;
-  if (!ids.empty()) hold(ids, Held{r.dev, units, t, uid, false, cu_mask});
+  if (!ids.empty()) by_ids_[key] = aid;
+  if (!ids.empty()) hold(key, Held{r.dev, units, t, uid, false, cu_mask});
+  r.ids = std::move(ids);
   auto res = records_.insert_or_assign(aid, std::move(r));
   return res.first->second;
 }
 
 void AllocState::add_record(AllocRecord r) {
   std::sort(r.ids.begin(), r.ids.end());
-  if (!r.ids.empty()) by_ids_[r.ids] = r.aid;
+  const std::string key = r.ids.empty() ? std::string() : id_key(r.ids);
+  if (!r.ids.empty()) by_ids_[key] = r.aid;
   std::string aid = r.aid;
   // a restored record: its allocation is held until kubelet's report says otherwise
-  if (!r.ids.empty() && !held_.count(r.ids)) hold(r.ids, Held{r.dev, r.units, r.t, r.uid, r.on_gpu, r.cu_mask});
+  if (!r.ids.empty() && !held_.count(key)) hold(key, Held{r.dev, r.units, r.t, r.uid, r.on_gpu, r.cu_mask});
   records_.insert_or_assign(aid, std::move(r));
 }
 
-void AllocState::hold(const std::vector<std::string>& ids, Held h) {
+std::string AllocState::id_key(const std::vector<std::string>& sorted_ids) {
+  size_t n = 0;
+  for (const auto& id : sorted_ids) n += id.size() + 1;
+  std::string k;
+  k.reserve(n);
+  for (const auto& id : sorted_ids) {
+    k.append(id);
+    k.push_back('\n');
+  }
+  return k;
+}
+
+void AllocState::hold(const std::string& ids, Held h) {
   auto prev = held_.find(ids);
   if (prev != held_.end()) unhold(prev);  // kubelet re-used the IDs of a finished container
   if (h.dev >= 0) phys_[h.dev] += h.units;
@@ -491,7 +506,7 @@ void AllocState::hold(const std::vector<std::string>& ids, Held h) {
   held_.emplace(ids, std::move(h));
 }
 
-void AllocState::unhold(std::map<std::vector<std::string>, Held>::iterator it) {
+void AllocState::unhold(std::unordered_map<std::string, Held>::iterator it) {
   const Held& h = it->second;
   if (h.dev >= 0) {
     int64_t& u = phys_[h.dev];
@@ -511,7 +526,7 @@ void AllocState::mark_on_gpu(const std::string& aid, bool on) {
   auto it = records_.find(aid);
   if (it == records_.end()) return;
   it->second.on_gpu = on;
-  auto h = held_.find(it->second.ids);
+  auto h = held_.find(id_key(it->second.ids));
   if (h == held_.end() || h->second.on_gpu == on) return;
   h->second.on_gpu = on;
   if (on) {
@@ -524,7 +539,7 @@ void AllocState::mark_on_gpu(const std::string& aid, bool on) {
 bool AllocState::held_for(std::vector<std::string> ids, int64_t* dev, int64_t* units, double* t,
                           std::string* cu_mask) const {
   std::sort(ids.begin(), ids.end());
-  auto it = held_.find(ids);
+  auto it = held_.find(id_key(ids));
   if (it == held_.end()) return false;
   *dev = it->second.dev;
   *units = it->second.units;
@@ -534,10 +549,10 @@ bool AllocState::held_for(std::vector<std::string> ids, int64_t* dev, int64_t* u
 }
 
 size_t AllocState::prune_held(const std::vector<std::vector<std::string>>& listed_in, double asked, double grace) {
-  std::set<std::vector<std::string>> listed;
+  std::unordered_set<std::string> listed;
   for (auto ids : listed_in) {
     std::sort(ids.begin(), ids.end());
-    listed.insert(std::move(ids));
+    listed.insert(id_key(ids));
   }
   size_t n = 0;
   for (auto it = held_.begin(); it != held_.end();) {
@@ -553,7 +568,7 @@ size_t AllocState::prune_held(const std::vector<std::vector<std::string>>& liste
 bool AllocState::drop_record(const std::string& aid) {
   auto it = records_.find(aid);
   if (it == records_.end()) return false;
-  auto b = by_ids_.find(it->second.ids);
+  auto b = by_ids_.find(id_key(it->second.ids));
   if (b != by_ids_.end() && b->second == aid) by_ids_.erase(b);
   stats_.records_dropped++;
   dropped_.push_back(std::move(it->second));
@@ -563,7 +578,7 @@ bool AllocState::drop_record(const std::string& aid) {
 
 const AllocRecord* AllocState::record_for_ids(std::vector<std::string> ids) const {
   std::sort(ids.begin(), ids.end());
-  auto b = by_ids_.find(ids);
+  auto b = by_ids_.find(id_key(ids));
   if (b == by_ids_.end()) return nullptr;
   auto it = records_.find(b->second);
   return it == records_.end() ? nullptr : &it->second;

@@ -846,6 +846,7 @@ class PyDpServer {
     if (cfg.contains("fast")) fast_ = cfg["fast"].cast<bool>();
     if (cfg.contains("spin_us")) spin_us_ = cfg["spin_us"].cast<double>();
     if (cfg.contains("py_event_ms")) py_event_s_ = cfg["py_event_ms"].cast<double>() * 1e-3;
+    if (cfg.contains("preferred")) preferred_ = cfg["preferred"].cast<bool>();
     node_ = c.node;
     profile_ = c.profile;
     state_ = &state;
@@ -1015,6 +1016,7 @@ class PyDpServer {
   }
 
   void set_fast(bool on) { fast_ = on; }
+  void set_ready(bool on) { ready_ = on; }
   void set_state(AllocState& state) {
     core_->set_state(&state);
     state_ = &state;
@@ -1096,6 +1098,10 @@ class PyDpServer {
   }
 
   void handle_call(h2::Server& s, const h2::Call& call) {
+    if (!ready_) {  // opened early for its pod feed, not serving yet (records and unlanded commits come first)
+      s.respond(call.id, 14, "device plugin starting");
+      return;
+    }
     const std::string svc = kSvc;
     if (call.path.compare(0, svc.size(), svc) != 0) {
       s.respond(call.id, 12, "unknown service " + call.path);
@@ -1104,7 +1110,7 @@ class PyDpServer {
     std::string m = call.path.substr(svc.size());
     std::string resp, why;
     if (m == "GetDevicePluginOptions") {
-      s.respond(call.id, 0, dp::encode_options(false, true));
+      s.respond(call.id, 0, dp::encode_options(false, preferred_));
     } else if (m == "PreStartContainer") {
       s.respond(call.id, 0, std::string());
     } else if (m == "ListAndWatch") {
@@ -1469,6 +1475,8 @@ class PyDpServer {
   std::atomic<bool> stop_serving_{false};  // written under the state lock
   int pyfd_ = -1;              // readable: pending_ / events_ waiting for poll()
   double h_pref_s_ = 0, h_alloc_s_ = 0;
+  bool ready_ = true;       // false: every call is answered UNAVAILABLE (set_ready)
+  bool preferred_ = false;  // cfg "preferred": advertise GetPreferredAllocation (kubelet then calls it per admission)
   double py_event_s_ = 0.002;  // cfg "py_event_ms": how often answered Allocates are handed to Python at most
   double py_signal_at_ = 0, py_due_ = 0;
   bool py_deferred_ = false;
@@ -1934,6 +1942,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("set_devices", &PyDpServer::set_devices, py::call_guard<AllocLock>())
       .def("set_device_list", &PyDpServer::set_device_list, py::call_guard<AllocLock>())
       .def("set_fast", &PyDpServer::set_fast, py::call_guard<AllocLock>())
+      .def("set_ready", &PyDpServer::set_ready, py::call_guard<AllocLock>())
       .def("set_state", &PyDpServer::set_state, py::keep_alive<1, 2>(), py::call_guard<AllocLock>())
       .def("start_feed", &PyDpServer::start_feed, py::call_guard<AllocLock>())
       .def("feed_synced", &PyDpServer::feed_synced, py::arg("timeout") = 30.0)

@@ -374,7 +374,7 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   p->whole = m.second;
   p->had_cus = had_cus;
   p->units = units;
-  p->ids = ids;
+  p->ids = std::move(ids_per[0]);  // `ids` is not read after this point
   p->on_gpu = on_gpu;
   p->cr = build_response(pod, dev, units, cus, cfg_.mount_mode, cfg_.profile);
   const double tb = mono_s();

@@ -236,6 +236,15 @@ bool decode_list_and_watch(const std::string& msg, std::vector<DeviceMsg>* out) 
   });
 }
 
+bool decode_options(const std::string& msg, bool* pre_start_required, bool* preferred_available) {
+  *pre_start_required = *preferred_available = false;
+  return each(msg, [&](int f, int w, std::string_view, uint64_t v) {
+    if (w == 0 && f == 1) *pre_start_required = v != 0;
+    if (w == 0 && f == 2) *preferred_available = v != 0;
+    return true;
+  });
+}
+
 bool decode_preferred_response(const std::string& msg, std::vector<std::vector<std::string>>* out) {
   return decode_allocate_request(msg, out);  // same shape: repeated {1: repeated string}
 }

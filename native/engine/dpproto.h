@@ -53,6 +53,8 @@ struct PodDevicesMsg {
 std::string encode_pod_resources_list(const std::vector<PodDevicesMsg>& entries);
 bool decode_pod_resources_list(const std::string& msg, std::vector<PodDevicesMsg>* entries);
 std::string encode_options(bool pre_start_required, bool preferred_available);
+// DevicePluginOptions -> (pre_start_required, get_preferred_allocation_available)
+bool decode_options(const std::string& msg, bool* pre_start_required, bool* preferred_available);
 std::string encode_list_and_watch(const std::vector<DeviceMsg>& devs);
 std::string encode_preferred_response(const std::vector<std::vector<std::string>>& per_container);
 std::string encode_allocate_response(const std::vector<ContainerResponse>& per_container);

@@ -529,7 +529,13 @@ class Agent {
           for (const auto& d : devs) {
             if (d.health == "Healthy") all_ids_.push_back(d.id);
           }
-          return true;
+          // as kubelet: GetPreferredAllocation only if the plugin's options advertise it
+          std::string opts;
+          bool pre = false;
+          if (dp_->call("/v1beta1.DevicePlugin/GetDevicePluginOptions", std::string(), &opts, &st, &e) &&
+              dp::decode_options(opts, &pre, &preferred_)) {
+            return true;
+          }
         }
       }
       if (now_s() > deadline) {
@@ -575,9 +581,15 @@ class Agent {
     {
       // the worker holds the admission slot (dp_mu_) from the queue pop on: kubelet admits one pod at a time
       ts = now_s();
-      ok = dp_->call("/v1beta1.DevicePlugin/GetPreferredAllocation", dp::encode_preferred_request({pr}), &resp, &st,
-                     &err) &&
-           dp::decode_preferred_response(resp, &chosen) && chosen.size() == 1;
+      if (preferred_) {
+        ok = dp_->call("/v1beta1.DevicePlugin/GetPreferredAllocation", dp::encode_preferred_request({pr}), &resp,
+                       &st, &err) &&
+             dp::decode_preferred_response(resp, &chosen) && chosen.size() == 1;
+      } else {
+        // kubelet's own pick (devicesToAllocate without a preference): the first free IDs
+        chosen.assign(1, std::vector<std::string>(pr.available.begin(), pr.available.begin() + units));
+        ok = true;
+      }
       tpref = now_s();
       ok = ok && dp_->call("/v1beta1.DevicePlugin/Allocate", dp::encode_allocate_request(chosen), &resp, &st, &err) &&
            dp::decode_allocate_response(resp, &crs) && crs.size() == 1;
@@ -1002,6 +1014,7 @@ class Agent {
   std::string pr_sock_;                    // kubelet's PodResources API socket (with --plugin-spawn)
   std::string plugin_debug_file_, plugin_debug_url_;
   std::unordered_map<std::string, int64_t> running_bytes_;  // uid -> bytes its slice was carved with
+  bool preferred_ = false;  // the plugin advertises GetPreferredAllocation
   std::unique_ptr<h2::Server> pr_srv_;
   std::thread pr_thread_;
   std::atomic<bool> pr_stop_{false};

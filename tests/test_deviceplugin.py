@@ -299,7 +299,9 @@ def run(coro):
     return asyncio.run(coro)
 
 
-def test_plugin_register_listandwatch_allocate():
+def test_plugin_register_listandwatch_allocate(monkeypatch):
+    monkeypatch.setenv("GSX_PLUGIN_PREFERRED", "1")  # GetPreferredAllocation advertised (off by default)
+
     async def go():
         api_srv = await FakeApiServerRunner().start()
         client = KubeClient(api_srv.url)
@@ -387,7 +389,9 @@ def test_plugin_reregisters_after_kubelet_restart():
             assert (plugin._native or plugin._server) is not first_server
             pc = PluginClient(plugin.socket_path)
             opts = await pc.options()
-            assert opts.get_preferred_allocation_available
+            # off by default (GSX_PLUGIN_PREFERRED=1 turns it on): kubelet picks the unit IDs itself, as with the
+            # reference's plugin, and skips one gRPC round trip per admission
+            assert not opts.get_preferred_allocation_available and not opts.pre_start_required
             first = await pc.list_and_watch().read()
             assert len(first.devices) == 32
             await pc.close()

@@ -48,7 +48,9 @@ async def _close(api_srv, client, plugin, *clients):
     await api_srv.stop()
 
 
-def test_grpcio_kubelet_against_the_native_endpoint():
+def test_grpcio_kubelet_against_the_native_endpoint(monkeypatch):
+    monkeypatch.setenv("GSX_PLUGIN_PREFERRED", "1")  # GetPreferredAllocation advertised (off by default)
+
     async def go():
         tmp = tempfile.mkdtemp()
         api_srv, client, plugin = await _plugin(tmp, fast=True)
