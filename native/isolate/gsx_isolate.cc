@@ -36,6 +36,9 @@
 // HSA_TOOLS_LIB before the program's first HIP call, and the library's own hsa_init (which precedes the runtime's
 // in the global symbol scope) puts it back right before the runtime reads it: a process that unsets or rewrites
 // HSA_TOOLS_LIB itself before its first HIP call is still confined.
+// Copies: device->device copies are HIP's blit kernels on the stream's (masked) queue, host<->device copies run on
+// the SDMA engines (profiles/r04_blit/); a process asking for HSA_ENABLE_SDMA=0 (ROCr's own blit queues, unhooked)
+// gets it turned back on when the library is preloaded.
 // Not covered: statically linked programs, and processes that drive /dev/kfd ioctls directly.  It confines
 // programs, not adversaries (like MPS): a process can rewrite its own pod's ledger file.
 //
@@ -785,6 +788,10 @@ namespace {
 // make sure ROCr loads this library as a tools library: HSA_TOOLS_LIB names it (prepended to whatever else)
 void ensure_tools_lib() {
   if (!config_path()) return;
+  // with SDMA off ROCr copies host<->device with blit kernels on queues of its own, which no hook sees (so they
+  // would run on every CU): keep the copy engines on (only when the runtime has not read its flags yet)
+  const char* sdma = getenv("HSA_ENABLE_SDMA");
+  if (sdma && !strcmp(sdma, "0")) setenv("HSA_ENABLE_SDMA", "1", 1);
   char me[4096];
   self_path(me, sizeof me);
   if (!me[0]) return;

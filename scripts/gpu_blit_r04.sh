@@ -31,7 +31,7 @@ st = (ctypes.c_uint64 * 5)()
 lib.gsx_isolate_stats(st)
 print(json.dumps({"queues": st[0], "masked": st[1], "ok": bool(torch.equal(x, y))}))
 PY
-GSX_LIB=$LIB timeout -k 10 120 python $OUT/copies.py > $OUT/copies.json 2> $OUT/copies.err && cat $OUT/copies.json && \
-GSX_LIB=$LIB timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $OUT/prof -o run -- python3 $OUT/copies.py > $OUT/prof.log 2>&1
+GSX_LIB=$HSA_TOOLS_LIB timeout -k 10 120 python $OUT/copies.py > $OUT/copies.json 2> $OUT/copies.err && cat $OUT/copies.json && \
+GSX_LIB=$HSA_TOOLS_LIB timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $OUT/copies.py > $OUT/prof.log 2>&1
 echo "rocprof rc=$?"
 find $OUT/prof -name "*.csv" | head -20

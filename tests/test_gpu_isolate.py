@@ -236,3 +236,18 @@ def test_scratch_fits_in_the_share_or_the_kernel_is_refused(iso):
         holder.kill()
         holder.wait(30)
     assert before - during <= share + 512 * (1 << 20), (before, during)
+
+
+def test_copies_of_a_confined_process_run_on_its_masked_queues(iso):
+    """VERDICT r3 item 4 ("blit queues"): a confined PyTorch process's host<->device and device->device copies
+    complete, and every queue the runtime created for it got the pod's CU mask (device->device copies are HIP blit
+    kernels on those queues; host<->device copies use the SDMA engines: profiles/r04_blit/)."""
+    _, env = iso.prepare("copies", CUPartitioner(256, 8).allocate("copies", 64), 256, 16 * GIB, host_process=True)
+    code = (
+        "import ctypes,json,os,torch\n"
+        "x=torch.randn(16<<20).pin_memory(); a=x.to('cuda',non_blocking=True); b=a.clone(); c=torch.empty_like(a)\n"
+        "c.copy_(b); y=c.to('cpu'); torch.cuda.synchronize()\n"
+        "st=(ctypes.c_uint64*5)(); ctypes.CDLL(os.environ['HSA_TOOLS_LIB']).gsx_isolate_stats(st)\n"
+        "print(json.dumps({'queues':st[0],'masked':st[1],'ok':bool(torch.equal(x,y))}))\n")
+    out = _run([sys.executable, "-c", code], _env(env), timeout=300)
+    assert out["ok"] and out["queues"] >= 1 and out["masked"] >= out["queues"], out
