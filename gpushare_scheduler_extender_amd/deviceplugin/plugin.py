@@ -160,11 +160,13 @@ class GpuSharePlugin:
         # early answer (default; GSX_PLUGIN_EARLY_ANSWER=0 turns it off): needs the journal next to the checkpoint
         # (the record must be durable before kubelet has the answer)
         self.early_answer = bool(self.checkpoint) and os.environ.get("GSX_PLUGIN_EARLY_ANSWER", "1") == "1"
-        # GetPreferredAllocation (GSX_PLUGIN_PREFERRED=1): kubelet then asks before every Allocate, and the answer
-        # steers the pod's unit IDs onto its GPU (kubelet's per-ID accounting then also bounds that GPU).  Off by
-        # default, as the reference's plugin: the IDs are interchangeable units, the Allocate is matched by size, and
-        # kubelet's serial admission pays one gRPC round trip per pod less
-        self.preferred = os.environ.get("GSX_PLUGIN_PREFERRED", "0") == "1"
+        # GetPreferredAllocation: kubelet then asks before every Allocate, and the answer steers the pod's unit IDs
+        # onto its GPU, so kubelet's per-ID accounting also bounds that GPU -- what lets an Allocate pass the
+        # physical guard while the records still count containers kubelet has freed (DpCore: guard_by_ids).  With
+        # one GPU every ID is on it anyway: "auto" (default) advertises it only on multi-GPU nodes, and a one-GPU
+        # node's admissions skip that round trip (the reference's plugin never offered it); "1" / "0" force it
+        pref = os.environ.get("GSX_PLUGIN_PREFERRED", "auto")
+        self.preferred = len(self.devices) > 1 if pref == "auto" else pref == "1"
         self.checkpoint_interval = 0.2
         self._dirty = False
         self._persist_task: asyncio.Task | None = None

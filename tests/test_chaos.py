@@ -331,6 +331,12 @@ def test_binding_annotations_dropped_by_apiserver_self_heals(agent):
             for n, g in zip(names, sizes):
                 await cl.create(n, g)
             pods = await cl.wait(names, timeout=60)
+            for _ in range(500):  # early answer (default): Running can come before the ASSIGNED commit lands
+                if all(p["metadata"]["annotations"].get(ALIYUN.annotation_assigned) == "true" for p in pods.values()):
+                    break
+                await asyncio.sleep(0.02)
+                pods = {p["metadata"]["name"]: p for p in (await cl.c.list("pods", "default"))["items"]
+                        if p["metadata"]["name"] in names}
             used = [0] * 4
             for p in pods.values():
                 ann = p["metadata"]["annotations"]

@@ -389,9 +389,10 @@ def test_plugin_reregisters_after_kubelet_restart():
             assert (plugin._native or plugin._server) is not first_server
             pc = PluginClient(plugin.socket_path)
             opts = await pc.options()
-            # off by default (GSX_PLUGIN_PREFERRED=1 turns it on): kubelet picks the unit IDs itself, as with the
-            # reference's plugin, and skips one gRPC round trip per admission
-            assert not opts.get_preferred_allocation_available and not opts.pre_start_required
+            # "auto" (default): advertised on multi-GPU nodes, where steering the unit IDs onto the pod's GPU lets
+            # kubelet's per-ID accounting bound each GPU; a one-GPU node skips the round trip
+            assert opts.get_preferred_allocation_available == (len(plugin.devices) > 1)
+            assert not opts.pre_start_required
             first = await pc.list_and_watch().read()
             assert len(first.devices) == 32
             await pc.close()

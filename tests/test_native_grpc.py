@@ -437,15 +437,18 @@ def test_plugin_process_sigkilled_between_answer_and_commit():
         proc, pc = await start_plugin()
         try:
             await asyncio.sleep(0.3)
-            api_srv.server.faults.latency_ms = 1500.0  # the commit cannot land before the kill
+            # the commit cannot land before the kill: every pod write fails (a commit the dead plugin had already
+            # sent may be read by the apiserver after the kill, so the writes keep failing until after the check)
+            api_srv.server.faults.update({"error_rate": 1.0})
             ids = fake_ids(devs[0], 16)
             r = (await pc.allocate([ids[0:4]])).container_responses[0]
             assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "a"
             proc.send_signal(signal.SIGKILL)
             proc.wait(10)
             await pc.close()
-            api_srv.server.faults.latency_ms = 0.0
+            await asyncio.sleep(0.05)  # whatever the dead plugin had sent is read (and refused) now
             assert (await client.get("pods", "a", "default"))["metadata"]["annotations"][P.annotation_assigned] == "false"
+            api_srv.server.faults.update({"error_rate": 0.0})
             proc, pc = await start_plugin()  # serves only after landing the journaled commit
             assert (await client.get("pods", "a", "default"))["metadata"]["annotations"][P.annotation_assigned] == "true"
             r = (await pc.allocate([ids[4:8]])).container_responses[0]
@@ -453,7 +456,7 @@ def test_plugin_process_sigkilled_between_answer_and_commit():
             with pytest.raises(grpc.aio.AioRpcError):
                 await pc.allocate([ids[8:12]])
         finally:
-            api_srv.server.faults.latency_ms = 0.0
+            api_srv.server.faults.update({"error_rate": 0.0})
             await pc.close()
             if proc.poll() is None:
                 proc.terminate()
