@@ -323,7 +323,7 @@ class GpuSharePlugin:
                 "guard": self.reconciler is not None, "api": api_dict(self.client.config),
                 "fast": os.environ.get("GSX_PLUGIN_FAST", "1") == "1",
                 # the serving thread polls this long after a pass before it sleeps (kubelet's calls come in bursts)
-                "spin_us": float(os.environ.get("GSX_PLUGIN_SPIN_US", "200")),
+                "spin_us": float(os.environ.get("GSX_PLUGIN_SPIN_US", "1000")),
                 "preferred": self.preferred,
                 # answered Allocates reach this loop's bookkeeping at most this often (a pass takes the state lock)
                 "py_event_ms": float(os.environ.get("GSX_PLUGIN_PY_EVENT_MS", "2")),

@@ -1483,7 +1483,7 @@ class PyDpServer {
   double lock_wait_s_ = 0, lock_wait_max_s_ = 0;  // the serving thread waiting for the state lock (Python holds it)
   uint64_t lock_waits_ = 0;                        // waits over 5 us
   uint64_t h_pref_n_ = 0, h_alloc_n_ = 0;
-  double spin_us_ = 200;       // poll without sleeping this long after a pass (cfg "spin_us"; 0: always block)
+  double spin_us_ = 1000;      // poll without sleeping this long after a pass (cfg "spin_us"; 0: always block)
   uint64_t passes_ = 0;
 };
 
