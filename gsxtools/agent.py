@@ -52,7 +52,8 @@ from gpushare_scheduler_extender_amd.models import pod as podutil
 from gpushare_scheduler_extender_amd.models.profile import NamingProfile
 from gpushare_scheduler_extender_amd.deviceplugin.allocator import CU_COUNT_ANNOTATION, AllocateError
 from gpushare_scheduler_extender_amd.deviceplugin.devices import UNITS, Device
-from gpushare_scheduler_extender_amd.deviceplugin.plugin import POD_ANNOTATION, GpuSharePlugin, PluginClient
+from gpushare_scheduler_extender_amd.deviceplugin.plugin import POD_ANNOTATION, GpuSharePlugin
+from gsxtools.kubeletapi import PluginClient
 from gpushare_scheduler_extender_amd.deviceplugin.runtime import AdmissionError, admit_local
 
 log = logging.getLogger("gsx.agent")
@@ -456,7 +457,7 @@ async def _spawn_plugin(a, sock_dir: str, devs: list[Device], prsock: str | None
     import os  # noqa: PLC0415
     import sys  # noqa: PLC0415
 
-    from gpushare_scheduler_extender_amd.deviceplugin.plugin import FakeKubelet  # noqa: PLC0415
+    from gsxtools.kubeletapi import FakeKubelet  # noqa: PLC0415
 
     kubelet = FakeKubelet(sock_dir)
     await kubelet.start()

@@ -6,7 +6,8 @@ import asyncio
 import json
 
 from gpushare_scheduler_extender_amd.deviceplugin.devices import Device, apply_memory_pools
-from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin, PluginClient
+from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin
+from gsxtools.kubeletapi import PluginClient
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient
 from tests.fixtures.fakeapi import FakeApiServerRunner
 from gpushare_scheduler_extender_amd.k8s.objects import make_node

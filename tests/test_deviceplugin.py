@@ -9,7 +9,8 @@ from gpushare_scheduler_extender_amd.deviceplugin import api
 from gpushare_scheduler_extender_amd.deviceplugin.allocator import CU_COUNT_ANNOTATION, CUPartitioner, build_response
 from gsxtools.agent import NodeAgent
 from gpushare_scheduler_extender_amd.deviceplugin.devices import Device, discover, fake_devices
-from gpushare_scheduler_extender_amd.deviceplugin.plugin import FakeKubelet, GpuSharePlugin, PluginClient, fake_ids
+from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin, fake_ids
+from gsxtools.kubeletapi import FakeKubelet, PluginClient
 from gpushare_scheduler_extender_amd.deviceplugin.runtime import AdmissionError, LedgerRuntime
 from gpushare_scheduler_extender_amd.deviceplugin.state import AllocationState
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient

@@ -54,7 +54,8 @@ def test_manager_files_mounts_and_release(tmp_path):
 def test_plugin_allocate_mounts_isolation_and_records(tmp_path):
     """The gRPC Allocate answers the isolation mounts, and the record of the allocation is checkpointed."""
     from gpushare_scheduler_extender_amd.deviceplugin.devices import Device
-    from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin, PluginClient
+    from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin
+    from gsxtools.kubeletapi import PluginClient
     from gpushare_scheduler_extender_amd.k8s.client import KubeClient
     from tests.fixtures.fakeapi import FakeApiServerRunner
     from gpushare_scheduler_extender_amd.k8s.objects import make_node, make_pod

@@ -13,7 +13,8 @@ from gpushare_scheduler_extender_amd.core.engine import native
 from gpushare_scheduler_extender_amd.deviceplugin import api
 from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
 from gpushare_scheduler_extender_amd.deviceplugin.isolation import IsolationManager
-from gpushare_scheduler_extender_amd.deviceplugin.plugin import FakeKubelet, GpuSharePlugin, PluginClient, fake_ids
+from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin, fake_ids
+from gsxtools.kubeletapi import FakeKubelet, PluginClient
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient
 from gpushare_scheduler_extender_amd.k8s.objects import make_node
 from gpushare_scheduler_extender_amd.models.profile import POD_CU_COUNT_ANNOTATION, SHARED_GPU
