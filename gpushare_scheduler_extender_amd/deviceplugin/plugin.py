@@ -1173,7 +1173,7 @@ class GpuSharePlugin:
     async def start(self, register: bool = True, publish: bool = True, serve: bool = True,
                     sync_timeout: float = 30.0):
         # state first: CU partitions of running pods are rebuilt before the first Allocate can be served
-        if self._own_informer and serve and self._open_native():
+        if self._own_informer and serve and self._open_native() and self._feed:
             # the native endpoint's pod feed is the node's one watch (no Python informer decodes pod events)
             loop = asyncio.get_running_loop()
             if not await loop.run_in_executor(None, self._native.feed_synced, sync_timeout):

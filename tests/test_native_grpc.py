@@ -465,3 +465,37 @@ def test_plugin_process_sigkilled_between_answer_and_commit():
             await client.close()
             await api_srv.stop()
     asyncio.run(go())
+
+
+@pytest.mark.parametrize("feed", ["1", "0"])
+def test_native_endpoint_with_and_without_its_pod_feed(feed, monkeypatch):
+    """GSX_PLUGIN_FEED=1 (default): the native reflector is the node's only pod watch and the Python views read the
+    native state; 0: the Python informer feeds the state.  Either way an Allocate is answered on the fast path for
+    the earliest pod of its size, and the views see the committed pod."""
+    monkeypatch.setenv("GSX_PLUGIN_FEED", feed)
+
+    async def go():
+        tmp = tempfile.mkdtemp()
+        api_srv, client, plugin = await _plugin(tmp, fast=True, spec="1x16GiB")
+        pc = PluginClient(plugin.socket_path)
+        try:
+            assert plugin.state.native_views == (feed == "1")
+            for i in range(3):
+                await client.create("pods", bound_pod(f"f{i}", 4, dev=0, assume=i + 1, dev_total=16))
+            ids = fake_ids(plugin.devices[0], 16)
+            for _ in range(300):
+                if len(plugin.state.candidates()) == 3:
+                    break
+                await asyncio.sleep(0.01)
+            r = (await pc.allocate([ids[0:4]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "f0"
+            for _ in range(300):
+                rec = plugin.state.pods.get(next(u for u, p in plugin.state.pods.items() if p.name == "f0"))
+                if rec is not None and rec.assigned == "true":
+                    break
+                await asyncio.sleep(0.01)
+            assert rec.assigned == "true" and rec.obj["metadata"]["name"] == "f0"
+            assert plugin.debug_state()["grpc"]["fast_allocate"] == 1
+        finally:
+            await _close(api_srv, client, plugin, pc)
+    asyncio.run(go())
