@@ -254,14 +254,49 @@ void DpCore::set_devices(std::vector<DpDevice> devs, std::map<std::string, int> 
   id_owner_ = std::unordered_map<std::string, int>(id_owner.begin(), id_owner.end());
   id_owner_view_.clear();
   for (const auto& kv : id_owner_) id_owner_view_.emplace(std::string_view(kv.first), kv.second);
+  // the plugin's IDs are "<device base><sep><k>" (deviceplugin/plugin.py: fake_ids): when every ID of a device
+  // shares one prefix that no other device's IDs start with, "is this ID on GPU g" is a prefix compare instead of a
+  // hash lookup per ID (kubelet lists every free ID of the node: ~2,300 on an 8-GPU node)
+  id_prefix_.clear();
+  std::map<int, std::string> pre;
+  bool ok = true;
+  for (const auto& kv : id_owner_) {
+    size_t cut = kv.first.rfind(kIdSep);
+    if (cut == std::string::npos) {
+      ok = false;
+      break;
+    }
+    std::string p = kv.first.substr(0, cut + kIdSep.size());
+    auto it = pre.find(kv.second);
+    if (it == pre.end()) {
+      pre.emplace(kv.second, std::move(p));
+    } else if (it->second != p) {
+      ok = false;
+      break;
+    }
+  }
+  for (const auto& a : pre) {
+    for (const auto& b : pre) {
+      if (a.first != b.first && b.second.compare(0, a.second.size(), a.second) == 0) ok = false;
+    }
+  }
+  if (ok) id_prefix_ = std::unordered_map<int, std::string>(pre.begin(), pre.end());
+}
+
+bool DpCore::id_on(std::string_view id, int dev) const {
+  if (!id_prefix_.empty()) {
+    auto p = id_prefix_.find(dev);
+    return p != id_prefix_.end() && id.size() > p->second.size() && id.compare(0, p->second.size(), p->second) == 0;
+  }
+  auto o = id_owner_view_.find(id);
+  return o != id_owner_view_.end() && o->second == dev;
 }
 
 int64_t DpCore::physical_used(int dev) const { return state_->physical_used(dev); }
 
 bool DpCore::ids_on(const std::vector<std::string>& ids, int dev) const {
   for (const auto& id : ids) {
-    auto o = id_owner_.find(id);
-    if (o == id_owner_.end() || o->second != dev) return false;
+    if (!id_on(id, dev)) return false;
   }
   return !ids.empty();
 }
@@ -288,8 +323,7 @@ bool DpCore::preferred(const std::string& req, std::string* resp, std::string* w
     for (int pass = 0; pass < 2 && static_cast<int32_t>(chosen.size()) < r.size; ++pass) {
       for (auto id : r.available) {
         if (static_cast<int32_t>(chosen.size()) >= r.size) break;
-        auto o = id_owner_view_.find(id);
-        const bool on_gpu = o != id_owner_view_.end() && o->second == want;
+        const bool on_gpu = id_on(id, static_cast<int>(want));
         if (on_gpu != (pass == 0) || (!taken.empty() && taken.count(id))) continue;
         chosen.emplace_back(id);
       }

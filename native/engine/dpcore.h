@@ -143,6 +143,9 @@ class DpCore {
   std::map<int, DpDevice> devs_;
   std::unordered_map<std::string, int> id_owner_;
   std::unordered_map<std::string_view, int> id_owner_view_;  // keys view id_owner_'s strings
+  std::unordered_map<int, std::string> id_prefix_;  // dev -> its IDs' common prefix (empty map: use the lookups)
+  static constexpr std::string_view kIdSep = "-_-";  // deviceplugin/plugin.py: ID_SEP
+  bool id_on(std::string_view id, int dev) const;
   uint64_t aid_ = 0;
   int jfd_ = -1;  // the early-answer journal
   Stats stats_;

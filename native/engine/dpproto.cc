@@ -16,7 +16,7 @@ void varint(std::string* o, uint64_t v) {
   o->push_back(static_cast<char>(v));
 }
 void tag(std::string* o, int field, int wire) { varint(o, (static_cast<uint64_t>(field) << 3) | wire); }
-void bytes(std::string* o, int field, const std::string& s) {
+void bytes(std::string* o, int field, std::string_view s) {
   tag(o, field, 2);
   varint(o, s.size());
   o->append(s);
@@ -179,6 +179,19 @@ std::string encode_allocate_request(const std::vector<std::vector<std::string>>&
     for (const auto& id : ids) bytes(&c, 1, id);
     bytes(&o, 1, c);
   }
+  return o;
+}
+
+std::string encode_preferred_request_views(const std::vector<std::string_view>& available, int32_t size) {
+  size_t n = 16;
+  for (auto id : available) n += id.size() + 3;
+  std::string c;
+  c.reserve(n);
+  for (auto id : available) bytes(&c, 1, id);
+  int_field(&c, 3, size);
+  std::string o;
+  o.reserve(c.size() + 8);
+  bytes(&o, 1, c);
   return o;
 }
 

@@ -68,6 +68,13 @@ constexpr uint8_t kFlagEndStream = 0x01;
 constexpr uint32_t kDataEof = 0x01, kDataNoEndStream = 0x02;
 constexpr int kErrDeferred = -508;
 constexpr int32_t kMaxConcurrentStreams = 0x3;
+constexpr int32_t kInitialWindowSize = 0x4;
+constexpr int32_t kMaxFrameSize = 0x5;
+// Flow-control windows and frame size both ends announce: a GetPreferredAllocation of an 8-GPU node lists every
+// free unit ID (~2,300 IDs, ~70 KB), past HTTP/2's default 64 KiB window -- the sender would stall for a
+// WINDOW_UPDATE round trip on kubelet's serial admission path, and send five 16 KiB DATA frames
+constexpr int32_t kWindow = 16 << 20;
+constexpr int32_t kFrame = 1 << 20;
 constexpr uint32_t kCancel = 0x8;
 
 struct Lib {
@@ -82,6 +89,7 @@ struct Lib {
   int (*client_new)(nghttp2_session**, const nghttp2_session_callbacks*, void*);
   void (*session_del)(nghttp2_session*);
   int (*submit_settings)(nghttp2_session*, uint8_t, const nghttp2_settings_entry*, size_t);
+  int (*set_local_window_size)(nghttp2_session*, uint8_t, int32_t, int32_t) = nullptr;
   int (*submit_response)(nghttp2_session*, int32_t, const nghttp2_nv*, size_t, const nghttp2_data_provider*);
   int (*submit_trailer)(nghttp2_session*, int32_t, const nghttp2_nv*, size_t);
   int32_t (*submit_request)(nghttp2_session*, const void*, const nghttp2_nv*, size_t, const nghttp2_data_provider*,
@@ -132,6 +140,14 @@ void load() {
              sym(h, "nghttp2_session_resume_data", &l.resume_data) && sym(h, "nghttp2_session_mem_recv", &l.mem_recv) &&
              sym(h, "nghttp2_session_mem_send", &l.mem_send) && sym(h, "nghttp2_session_want_read", &l.want_read) &&
              sym(h, "nghttp2_session_want_write", &l.want_write) && sym(h, "nghttp2_strerror", &l.strerror);
+  if (g_loaded) sym(h, "nghttp2_session_set_local_window_size", &l.set_local_window_size);  // optional (1.7+)
+}
+
+// the settings above, on a new session (either end)
+void big_windows(nghttp2_session* s, bool server) {
+  nghttp2_settings_entry iv[3] = {{kInitialWindowSize, kWindow}, {kMaxFrameSize, kFrame}, {kMaxConcurrentStreams, 256}};
+  g_lib.submit_settings(s, 0, iv, server ? 3 : 2);
+  if (g_lib.set_local_window_size) g_lib.set_local_window_size(s, 0, 0, kWindow);  // the connection's window
 }
 
 nghttp2_nv nv(const std::string& n, const std::string& v) {
@@ -356,8 +372,7 @@ void Server::accept_all() {
       ::close(fd);
       continue;
     }
-    nghttp2_settings_entry iv[1] = {{kMaxConcurrentStreams, 256}};
-    g_lib.submit_settings(c->s, 0, iv, 1);
+    big_windows(c->s, true);
     epoll_event ev{};
     ev.events = EPOLLIN;
     ev.data.fd = fd;
@@ -664,7 +679,7 @@ struct Client::Impl {
       drop();
       return false;
     }
-    g_lib.submit_settings(s, 0, nullptr, 0);
+    big_windows(s, false);
     return true;
   }
 

@@ -49,6 +49,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <unordered_set>
@@ -529,6 +530,9 @@ class Agent {
           for (const auto& d : devs) {
             if (d.health == "Healthy") all_ids_.push_back(d.id);
           }
+          id_index_.clear();
+          for (size_t i = 0; i < all_ids_.size(); ++i) id_index_.emplace(all_ids_[i], i);
+          id_used_.assign(all_ids_.size(), 0);
           // as kubelet: GetPreferredAllocation only if the plugin's options advertise it
           std::string opts;
           bool pre = false;
@@ -555,15 +559,20 @@ class Agent {
     const std::string my_uid = mine->uid, my_key = key;
     if (running_.count(my_uid) || state_->inflight(my_uid)) return;
     const int64_t units = mine->request;
-    dp::PreferredRequest pr;  // kubelet's free IDs: every healthy ID no running container holds
-    pr.available.reserve(all_ids_.size());
-    for (const auto& id : all_ids_) {
-      if (!used_all_.count(id)) pr.available.push_back(id);
+    // kubelet's free IDs: every healthy ID no running container holds.  Views into all_ids_ (fixed once the plugin
+    // is connected); without GetPreferredAllocation only the first `units` are needed, kubelet's own pick
+    std::vector<std::string_view> available;
+    available.reserve(preferred_ ? all_ids_.size() : static_cast<size_t>(std::max<int64_t>(units, 0)));
+    size_t n_free = 0;
+    for (size_t i = 0; i < all_ids_.size(); ++i) {
+      if (id_used_[i]) continue;
+      ++n_free;
+      if (preferred_ || static_cast<int64_t>(available.size()) < units) available.push_back(all_ids_[i]);
+      else if (n_free >= static_cast<size_t>(units)) break;
     }
-    pr.size = static_cast<int32_t>(units);
-    if (static_cast<int64_t>(pr.available.size()) < units) {
+    if (static_cast<int64_t>(n_free) < units) {
       std::fprintf(stderr, "[gsx-nodeagent] %s: %lld units requested, %zu IDs free\n", key.c_str(),
-                   static_cast<long long>(units), pr.available.size());
+                   static_cast<long long>(units), n_free);
       queued_.insert(my_uid);
       delayed_.push_back({now_s() + 0.01, key});
       return;
@@ -582,12 +591,12 @@ class Agent {
       // the worker holds the admission slot (dp_mu_) from the queue pop on: kubelet admits one pod at a time
       ts = now_s();
       if (preferred_) {
-        ok = dp_->call("/v1beta1.DevicePlugin/GetPreferredAllocation", dp::encode_preferred_request({pr}), &resp,
-                       &st, &err) &&
+        ok = dp_->call("/v1beta1.DevicePlugin/GetPreferredAllocation",
+                       dp::encode_preferred_request_views(available, static_cast<int32_t>(units)), &resp, &st, &err) &&
              dp::decode_preferred_response(resp, &chosen) && chosen.size() == 1;
       } else {
         // kubelet's own pick (devicesToAllocate without a preference): the first free IDs
-        chosen.assign(1, std::vector<std::string>(pr.available.begin(), pr.available.begin() + units));
+        chosen.assign(1, std::vector<std::string>(available.begin(), available.begin() + units));
         ok = true;
       }
       tpref = now_s();
@@ -636,7 +645,7 @@ class Agent {
     }
     used_ids_[my_uid] = chosen[0];
     uid_key_[my_uid] = my_key;
-    used_all_.insert(chosen[0].begin(), chosen[0].end());
+    mark_used_locked(chosen[0], 1);
     release_slot();
     auto idx = cr.envs.find(p_.a_idx);
     const int dev_idx = idx == cr.envs.end() ? -1 : std::atoi(idx->second.c_str());
@@ -671,10 +680,17 @@ class Agent {
     return plugin_debug_url_;
   }
 
+  void mark_used_locked(const std::vector<std::string>& ids, char used) {
+    for (const auto& id : ids) {
+      auto it = id_index_.find(id);
+      if (it != id_index_.end()) id_used_[it->second] = used;
+    }
+  }
+
   void forget_ids_locked(const std::string& uid) {
     auto ui = used_ids_.find(uid);
     if (ui != used_ids_.end()) {
-      for (const auto& id : ui->second) used_all_.erase(id);
+      mark_used_locked(ui->second, 0);
       used_ids_.erase(ui);
     }
     uid_key_.erase(uid);
@@ -1009,7 +1025,8 @@ class Agent {
   std::mutex dp_mu_;
   std::vector<std::string> all_ids_;
   std::unordered_map<std::string, std::vector<std::string>> used_ids_;  // uid -> the IDs its Allocate took
-  std::unordered_set<std::string> used_all_;                             // the union of used_ids_, kept with it
+  std::unordered_map<std::string, size_t> id_index_;                     // ID -> its place in all_ids_
+  std::vector<char> id_used_;  // per all_ids_ entry: held by a running container (the union of used_ids_)
   std::unordered_map<std::string, std::string> uid_key_;                 // uid -> ns/name of every used_ids_ pod
   std::string pr_sock_;                    // kubelet's PodResources API socket (with --plugin-spawn)
   std::string plugin_debug_file_, plugin_debug_url_;
