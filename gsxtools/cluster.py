@@ -96,6 +96,10 @@ class ChildProc:
                 self.proc.kill()
                 self.proc.wait(5)
         self.log.close()
+        keep = os.environ.get("GSX_LOG_DIR")  # a copy of the child's log (stdout + stderr) survives the run
+        if keep:
+            os.makedirs(keep, exist_ok=True)
+            shutil.copyfile(self.log_path, os.path.join(keep, f"{self.name}.{self.proc.pid}.log"))
         if os.environ.get("GSX_KEEP_LOGS") != "1":
             shutil.rmtree(self.tmp, ignore_errors=True)
 
