@@ -744,10 +744,11 @@ class GpuSharePlugin:
 
     def _kubelet_bounds(self, dev: int, ids) -> bool:
         """kubelet's own per-ID accounting bounds GPU ``dev``: this Allocate's IDs all lie on it and so do those of
-        every recorded allocation (GetPreferredAllocation steered them), so kubelet cannot have handed out more of
-        ``dev`` than it has, whatever records of containers it has since freed still say (native twin:
-        dpcore.cc allocate)."""
-        return bool(ids) and all(self.id_owner.get(i) == dev for i in ids) and self.state.core.off_gpu_records() == 0
+        every recorded allocation whose container runs on ``dev`` (GetPreferredAllocation steered them), so every
+        unit there holds one of ``dev``'s IDs and kubelet cannot have handed out more than it has, whatever records
+        of containers it has since freed still say (native twin: dpcore.cc allocate)."""
+        return (bool(ids) and all(self.id_owner.get(i) == dev for i in ids)
+                and self.state.core.off_gpu_records_on(dev) == 0)
 
     async def _physical_guard(self, rec: PodRec, units: int, ids=()) -> PodRec | None:
         """Never start a container on a GPU that is physically full.  The extender placed ``rec`` by the
@@ -1062,8 +1063,8 @@ class GpuSharePlugin:
         if self._native is not None:
             # the native gRPC endpoint: calls answered on its fast path vs handed to the Python handlers
             ns = self._native.stats()
-            for k in ("fast_allocate", "fast_preferred", "slow_allocate", "slow_preferred", "patch_failures", "waited",
-                      "feed_events", "calls"):
+            for k in ("fast_allocate", "fast_preferred", "slow_allocate", "slow_preferred", "patch_failures",
+                      "commits_gone", "waited", "feed_events", "calls"):
                 lines += [f"# TYPE gpushare_plugin_native_{k}_total counter", f"gpushare_plugin_native_{k}_total {ns.get(k, 0)}"]
         n = self.timing.get("n", 0)
         if n:

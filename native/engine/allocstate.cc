@@ -502,7 +502,7 @@ void AllocState::hold(const std::string& ids, Held h) {
   auto prev = held_.find(ids);
   if (prev != held_.end()) unhold(prev);  // kubelet re-used the IDs of a finished container
   if (h.dev >= 0) phys_[h.dev] += h.units;
-  if (!h.on_gpu) off_gpu_++;
+  if (!h.on_gpu) off_gpu_count(h.dev, +1);
   held_.emplace(ids, std::move(h));
 }
 
@@ -513,7 +513,7 @@ void AllocState::unhold(std::unordered_map<std::string, Held>::iterator it) {
     u -= h.units;
     if (u == 0) phys_.erase(h.dev);
   }
-  if (!h.on_gpu) off_gpu_--;
+  if (!h.on_gpu) off_gpu_count(h.dev, -1);
   held_.erase(it);
 }
 
@@ -529,11 +529,19 @@ void AllocState::mark_on_gpu(const std::string& aid, bool on) {
   auto h = held_.find(id_key(it->second.ids));
   if (h == held_.end() || h->second.on_gpu == on) return;
   h->second.on_gpu = on;
-  if (on) {
-    off_gpu_--;
-  } else {
-    off_gpu_++;
-  }
+  off_gpu_count(h->second.dev, on ? -1 : +1);
+}
+
+void AllocState::off_gpu_count(int64_t dev, int d) {
+  off_gpu_ = static_cast<size_t>(static_cast<int64_t>(off_gpu_) + d);
+  size_t& n = off_gpu_dev_[dev];
+  n = static_cast<size_t>(static_cast<int64_t>(n) + d);
+  if (n == 0) off_gpu_dev_.erase(dev);
+}
+
+size_t AllocState::off_gpu_records_on(int64_t dev) const {
+  auto it = off_gpu_dev_.find(dev);
+  return it == off_gpu_dev_.end() ? 0 : it->second;
 }
 
 bool AllocState::held_for(std::vector<std::string> ids, int64_t* dev, int64_t* units, double* t,

@@ -181,6 +181,9 @@ class AllocState {
   int64_t physical_used(int64_t dev) const;
   void mark_on_gpu(const std::string& aid, bool on);
   size_t off_gpu_records() const { return off_gpu_; }  // entries whose IDs do not all lie on their GPU
+  // those of them whose container runs on GPU `dev`: while there are none, kubelet's per-ID accounting bounds what
+  // runs on `dev` (every unit there holds one of its IDs)
+  size_t off_gpu_records_on(int64_t dev) const;
   // kubelet's PodResources answer, requested at `asked` (wall seconds): entries made more than `grace` before it whose
   // IDs it does not list are gone (their containers stopped).  Returns how many left.
   size_t prune_held(const std::vector<std::vector<std::string>>& listed, double asked, double grace);
@@ -226,6 +229,8 @@ class AllocState {
   std::unordered_map<std::string, Held> held_;  // id_key(sorted kubelet IDs) -> what was handed out with them
   std::unordered_map<int64_t, int64_t> phys_;     // dev -> sum of held_ units (kept in step)
   size_t off_gpu_ = 0;                             // held_ entries with on_gpu == false
+  std::unordered_map<int64_t, size_t> off_gpu_dev_;  // ... per GPU their container runs on
+  void off_gpu_count(int64_t dev, int d);
   void hold(const std::string& ids_key, Held h);
   void unhold(std::unordered_map<std::string, Held>::iterator it);
   bool owners_reported_ = false;

@@ -1035,6 +1035,7 @@ class PyDpServer {
     d["slow_allocate"] = s.slow_allocate;
     d["slow_preferred"] = s.slow_preferred;
     d["patch_failures"] = s.patch_failures;
+    d["commits_gone"] = s.commits_gone;
     d["guard_by_ids"] = s.guard_by_ids;
     if (s.phased) {
       const double k = 1e6 / static_cast<double>(s.phased);
@@ -1822,6 +1823,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("mark_on_gpu", &AllocState::mark_on_gpu, py::call_guard<AllocLock>())
       .def("physical_used", &AllocState::physical_used, py::call_guard<AllocLock>())
       .def("off_gpu_records", &AllocState::off_gpu_records, py::call_guard<AllocLock>())
+      .def("off_gpu_records_on", &AllocState::off_gpu_records_on, py::call_guard<AllocLock>())
       .def("prune_held", &AllocState::prune_held, py::arg("listed"), py::arg("asked"), py::arg("grace"),
            py::call_guard<AllocLock>())
       .def("held_count", &AllocState::held_count, py::call_guard<AllocLock>())

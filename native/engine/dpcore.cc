@@ -366,14 +366,14 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   const DpDevice& dev = dit->second;
   const bool later = pod.assigned == "true";
   // kubelet hands out each fake ID once and GetPreferredAllocation steers a pod's IDs onto its GPU: when this
-  // Allocate's IDs all lie on the pod's GPU and so do those of every recorded allocation, kubelet's own per-ID
-  // accounting bounds what runs on that GPU (it holds exactly `units` IDs of it), whatever the records of pods
-  // it has since freed still say.  Otherwise the records decide (the Python guard repairs and waits).
+  // Allocate's IDs all lie on the pod's GPU and so do those of every recorded allocation whose container runs
+  // there, kubelet's own per-ID accounting bounds what runs on that GPU (each unit there holds one of its IDs),
+  // whatever the records of pods it has since freed still say.  Otherwise the records decide (the Python guard
+  // repairs and waits).  A record off its GPU elsewhere on the node does not matter to this GPU.
   const bool on_gpu = ids_on(ids, dev.index);
 
-
   if (!later && cfg_.guard && physical_used(dev.index) + units > dev.units) {
-    if (!on_gpu || state_->off_gpu_records() != 0) {
+    if (!on_gpu || state_->off_gpu_records_on(dev.index) != 0) {
       stats_.slow_allocate++;
       *why = "GPU physically full by the records";
       return DpStep::Slow;
@@ -499,8 +499,12 @@ bool DpCore::finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* w
     }
     const bool recreated = p.ok && p.status == 409 && p.resp.find("UID in precondition") != std::string::npos;
     if ((p.ok && p.status == 404) || recreated || !state_->pod(p.pod.uid)) {
-      // the pod went away (deleted, or re-created under its name): nothing to commit; the pod feed releases it
+      // the pod went away (deleted, or re-created under its name): nothing to commit.  It is released now, not when
+      // the pod feed delivers the deletion: unclaimed but still pending ASSIGNED=false in the state, it would be the
+      // next Allocate's match (kubelet has already started its container and is admitting the next pod)
       state_->set_inflight(p.pod.uid, false);
+      state_->deleted(p.pod.uid);
+      stats_.commits_gone++;
       return true;
     }
     // transport error, 5xx, an injected or transient 409: the commit is retried with capped exponential backoff

@@ -119,6 +119,7 @@ class DpCore {
 
   struct Stats {
     uint64_t fast_allocate = 0, fast_preferred = 0, slow_allocate = 0, slow_preferred = 0, patch_failures = 0;
+    uint64_t commits_gone = 0;  // early-answer commits whose pod was gone (404 / re-created): released at once
     uint64_t guard_by_ids = 0;  // the records said full, kubelet's IDs said there is room
     // fast-path Allocate phases, summed seconds over `phased` answers: decode, match, guard + CU claim, response
     // build, commit body, record (incl. the physical account), journal line, response encode

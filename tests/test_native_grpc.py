@@ -295,6 +295,38 @@ def test_early_answer_commit_retries_with_backoff_until_the_apiserver_recovers()
     asyncio.run(go())
 
 
+def test_early_answer_commit_of_a_deleted_pod_releases_it_before_the_feed_does():
+    """The pod was deleted while its early-answered commit was in flight, and the plugin's watch has not delivered
+    the deletion yet: the commit's 404 releases the pod at once.  Unclaimed but still pending ASSIGNED=false in the
+    state it would be the next Allocate's match -- kubelet has started its container and is admitting the next
+    pod, which would get an allocation built for a deleted pod (seen on an 8-GPU rehearsal, profiles/r04_scale)."""
+    async def go():
+        tmp = tempfile.mkdtemp()
+        api_srv, client, plugin = await _plugin(tmp, fast=True)
+        pc = PluginClient(plugin.socket_path)
+        try:
+            await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
+            await client.create("pods", bound_pod("b", 4, dev=0, assume=2, dev_total=16))
+            await asyncio.sleep(0.3)
+            api_srv.server.faults.latency_ms = 300.0  # the commit of "a" is in flight for 0.3 s
+            ids = fake_ids(plugin.devices[0], 16)
+            r = (await pc.allocate([ids[0:4]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "a"
+            del api_srv.server.store["pods"][("default", "a")]  # gone, and no watch event says so
+            for _ in range(100):
+                if plugin.debug_state()["grpc"].get("commits_gone") == 1:
+                    break
+                await asyncio.sleep(0.02)
+            assert plugin.debug_state()["grpc"]["commits_gone"] == 1
+            api_srv.server.faults.latency_ms = 0.0
+            r = (await pc.allocate([ids[4:8]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "b"
+        finally:
+            api_srv.server.faults.latency_ms = 0.0
+            await _close(api_srv, client, plugin, pc)
+    asyncio.run(go())
+
+
 def test_early_answer_checkpoint_failure_keeps_the_journal_generation():
     """the journal is rotated (not truncated) with the records snapshot; a checkpoint that fails to land
     leaves the rotated generation in place, and a restarted plugin still finds the record."""

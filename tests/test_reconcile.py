@@ -216,6 +216,31 @@ def test_unowned_record_outlives_the_pod_it_was_built_for_while_kubelet_reports_
     assert "aQ" not in st.records
 
 
+def test_off_gpu_records_are_counted_per_gpu_their_container_runs_on():
+    """The guard's ID bound (dpcore.cc allocate, plugin.py _kubelet_bounds) holds for a GPU while every allocation
+    whose container runs there has its IDs there: a record off its GPU elsewhere on the node does not lift it."""
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import Device
+    from gpushare_scheduler_extender_amd.deviceplugin.state import AllocationState
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+
+    st = AllocationState("n", {i: Device(index=i, total_bytes=96 << 30) for i in range(2)}, SHARED_GPU)
+    for n, dev in (("P", 0), ("Q", 1)):
+        p = make_pod(n, 32, node="n", uid=f"u{n}", annotations={SHARED_GPU.annotation_idx: str(dev),
+                                                                 SHARED_GPU.annotation_assigned: "false"})
+        p["metadata"]["resourceVersion"] = "1"
+        st.observe(p)
+    st.record(st.pods["uP"], ["g0-_-0"], 32, "", "aP", on_gpu=True)
+    st.record(st.pods["uQ"], ["g0-_-1"], 32, "", "aQ", on_gpu=False)  # Q runs on GPU 1 with an ID of GPU 0
+    core = st.core
+    assert core.off_gpu_records() == 1
+    assert core.off_gpu_records_on(0) == 0 and core.off_gpu_records_on(1) == 1
+    core.mark_on_gpu("aQ", True)
+    assert core.off_gpu_records() == 0 and core.off_gpu_records_on(1) == 0
+    core.mark_on_gpu("aQ", False)
+    st.release("uQ")  # no PodResources: the record goes with its pod
+    assert core.off_gpu_records() == 0 and core.off_gpu_records_on(1) == 0
+
+
 def test_annotations_edited_behind_the_plugins_back_are_repaired():
     """Any cause (an operator's edit, a half-applied exchange from an older plugin): a pod whose annotation names
     another GPU than its container's allocation is re-annotated from kubelet's record, by exchanging with the
