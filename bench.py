@@ -95,6 +95,38 @@ def _task_cpu_s(pid: int) -> float | None:
     return ns / 1e9
 
 
+def _thread_cpu_s(pid: int) -> dict:
+    """On-CPU seconds of `pid`'s threads summed per thread name (/proc/<pid>/task/*/comm + schedstat)."""
+    out: dict = {}
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return out
+    for t in tids:
+        try:
+            with open(f"/proc/{pid}/task/{t}/comm") as f:
+                name = f.read().strip()
+            with open(f"/proc/{pid}/task/{t}/schedstat") as f:
+                out[name] = out.get(name, 0.0) + int(f.read().split()[0]) / 1e9
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
+
+
+def _threads_of_node(children) -> dict:
+    """Per-thread-name on-CPU seconds of the node agent (kubelet stand-in) and the plugin process it spawned: which
+    thread of the node's serial admission path is busy."""
+    out = {}
+    for c in children:
+        pid = getattr(getattr(c, "proc", None), "pid", None)
+        if pid is None or c.name != "node-agent":
+            continue
+        out["node-agent"] = _thread_cpu_s(pid)
+        for k in _child_pids(pid):
+            out["plugin"] = _thread_cpu_s(k)
+    return out
+
+
 def _child_pids(pid: int) -> list[int]:
     out = []
     try:
@@ -851,6 +883,7 @@ def main():
             # the CPU-time counters are read before the bracket: reading /proc for every child took ~0.5 ms, which
             # sat inside the timed region (rank 0's span exceeded the sum of its waves by that much)
             cpu0 = _cpu_times(children)
+            thr0 = _threads_of_node(children)
             rss0 = _rss_mib(children)
             cg0 = _cgroup_cpu()
             bracket()
@@ -881,6 +914,7 @@ def main():
     gc.enable()
     own_elapsed = elapsed
     cpu1 = _cpu_times(children)
+    thr1 = _threads_of_node(children)
     rss1 = _rss_mib(children)
     cg1 = _cgroup_cpu()
     if prof is not None:
@@ -1038,6 +1072,10 @@ def main():
             # on-CPU time of each process over the timed region's wall time (all its threads; 100 = one CPU busy):
             # which process the wave pipeline waits on
             "busy_pct": {k: round(100.0 * (cpu1[k] - cpu0.get(k, 0.0)) / max(elapsed, 1e-9), 1) for k in cpu1},
+            # the same per thread name inside the node agent and the plugin (threads under 1 % left out)
+            "busy_threads_pct": {p: {t: v for t, v in ((t, round(100.0 * (s1 - thr0.get(p, {}).get(t, 0.0))
+                                                                  / max(elapsed, 1e-9), 1)) for t, s1 in th.items())
+                                     if v >= 1.0} for p, th in thr1.items()},
             # resident memory of each process at the start and the end of the timed region
             "rss_mib": {k: [rss0.get(k), rss1[k]] for k in rss1},
             # CPU-quota throttling of the container during the timed region (cgroup v2), if any

@@ -857,7 +857,10 @@ class PyDpServer {
     srv_->watch_fd(efd_);
     tfd_ = ::timerfd_create(CLOCK_MONOTONIC, TFD_NONBLOCK | TFD_CLOEXEC);
     srv_->watch_fd(tfd_);
-    worker_ = std::thread([this] { work(); });
+    worker_ = std::thread([this] {
+      introspect::name_thread("dp-worker");
+      work();
+    });
   }
   ~PyDpServer() {
     stop_serving();

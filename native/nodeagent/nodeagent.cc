@@ -62,6 +62,7 @@
 #include "dpproto.h"
 #include "h2.h"
 #include "informer.h"
+#include "introspect.h"
 #include "json.h"
 #include "model.h"
 #include "quantity.h"
@@ -232,7 +233,12 @@ class Agent {
       *err = "pod informer did not sync: " + pods_r_->last_error();
       return false;
     }
-    for (int i = 0; i < nworkers_; ++i) workers_.emplace_back([this] { worker(); });
+    for (int i = 0; i < nworkers_; ++i) {
+      workers_.emplace_back([this] {
+        introspect::name_thread("na-worker");
+        worker();
+      });
+    }
     ready_.store(true);
     return true;
   }
@@ -705,6 +711,7 @@ class Agent {
       return false;
     }
     pr_thread_ = std::thread([this] {
+      introspect::name_thread("na-podres");
       const int ep = pr_srv_->fd();
       while (!pr_stop_.load()) {
         pollfd pf{ep, POLLIN, 0};
