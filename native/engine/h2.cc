@@ -254,7 +254,15 @@ struct Callbacks {
   static int data(nghttp2_session*, uint8_t, int32_t id, const uint8_t* d, size_t n, void* ud) {
     auto* c = static_cast<Server::Conn*>(ud);
     Server::Stream* s = stream(c, id);
-    if (s) s->in.append(reinterpret_cast<const char*>(d), n);
+    if (!s) return 0;
+    if (s->in.empty() && n >= 5) {
+      // the gRPC length prefix sizes the message: one allocation, not a doubling per chunk (kubelet's
+      // GetPreferredAllocation lists every free ID of the node, ~60 KB on 8 GPUs)
+      const uint32_t len = (static_cast<uint32_t>(d[1]) << 24) | (static_cast<uint32_t>(d[2]) << 16) |
+                           (static_cast<uint32_t>(d[3]) << 8) | static_cast<uint32_t>(d[4]);
+      if (len > n - 5 && len <= (64u << 20)) s->in.reserve(5 + static_cast<size_t>(len));
+    }
+    s->in.append(reinterpret_cast<const char*>(d), n);
     return 0;
   }
   static int frame(nghttp2_session*, const nghttp2_frame* f, void* ud) {
