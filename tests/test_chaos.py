@@ -23,7 +23,8 @@ from gsxtools.configs import NODE, Cluster
 # held until kubelet's first PodResources report, AllocState::expect_owner_reports), but its exchange-based repair of
 # the annotations does not always converge before the extender binds onto a GPU the annotations show free and the
 # containers fill: the plugin then refuses that Allocate (the pod fails admission, as under a real kubelet) -- in
-# about one run in five (docs/ROUND4.md).  Opt in with GSX_STRESS=1.
+# about one run in five before an early-answered commit that finds its pod gone released the pod at once, one in 26
+# since (docs/ROUND4.md).  Opt in with GSX_STRESS=1.
 STRESS = pytest.mark.skipif(os.environ.get("GSX_STRESS") != "1", reason="swap-storm stress row: GSX_STRESS=1")
 
 
