@@ -413,7 +413,8 @@ def _plugin_debug(E, url: str | None) -> dict | None:
     return {"grpc": {k: g.get(k) for k in ("impl", "fast_allocate", "slow_allocate", "fast_preferred",
                                            "slow_preferred", "patch_failures", "guard_by_ids", "journaling",
                                            "early_answer_backlog", "waited", "feed_events", "passes",
-                                           "last_slow_reason", "handler_us", "allocate_phases_us", "lock_wait")},
+                                           "last_slow_reason", "handler_us", "allocate_phases_us", "lock_wait",
+                                           "wait_ms", "commits_gone")},
             "stats": d.get("stats"), "reconcile": d.get("reconcile"),
             # mean seconds per native fast-path Allocate: match, isolation files, record + answer (handler)
             "timing": {k: (v / max(1, (d.get("timing") or {}).get("n", 0)) if k != "n" else v)

@@ -1052,6 +1052,7 @@ class PyDpServer {
     d["fast"] = fast_;
     d["last_slow_reason"] = last_why_;
     d["waited"] = waited_;
+    d["wait_ms"] = py::dict(py::arg("total") = wait_s_ * 1e3, py::arg("max") = wait_max_s_ * 1e3);
     d["feed_events"] = feed_events_;
     if (feed_r_) {
       d["feed_relists"] = feed_r_->relists();
@@ -1068,7 +1069,8 @@ class PyDpServer {
                               py::arg("over_5us") = lock_waits_);
     d["handler_us"] = py::dict(py::arg("get_preferred") = h_pref_n_ ? 1e6 * h_pref_s_ / h_pref_n_ : 0.0,
                                py::arg("allocate") = h_alloc_n_ ? 1e6 * h_alloc_s_ / h_alloc_n_ : 0.0,
-                               py::arg("n_preferred") = h_pref_n_, py::arg("n_allocate") = h_alloc_n_);
+                               py::arg("n_preferred") = h_pref_n_, py::arg("n_allocate") = h_alloc_n_,
+                               py::arg("max_preferred") = 1e6 * h_pref_max_, py::arg("max_allocate") = 1e6 * h_alloc_max_);
     return d;
   }
 
@@ -1095,9 +1097,11 @@ class PyDpServer {
     if (ends("/GetPreferredAllocation")) {
       h_pref_s_ += dt;
       h_pref_n_++;
+      h_pref_max_ = std::max(h_pref_max_, dt);
     } else if (ends("/Allocate")) {
       h_alloc_s_ += dt;
       h_alloc_n_++;
+      h_alloc_max_ = std::max(h_alloc_max_, dt);
     }
   }
 
@@ -1248,6 +1252,7 @@ class PyDpServer {
     uint64_t call;
     std::string method, message;
     double deadline;
+    double t0 = 0;  // when it started waiting
   };
 
   static double mono() {
@@ -1300,7 +1305,8 @@ class PyDpServer {
   }
 
   void wait_for_pod(uint64_t call, const std::string& method, const std::string& message) {
-    waiting_.push_back({call, method, message, mono() + kWaitS});
+    const double now = mono();
+    waiting_.push_back({call, method, message, now + kWaitS, now});
     waited_++;
     arm_timer();
   }
@@ -1312,11 +1318,17 @@ class PyDpServer {
     if (waiting_.empty() || !srv_) return;
     std::vector<Waiting> still;
     const double now = mono();
+    auto waited = [&](const Waiting& w) {  // how long a call waited for its pod's event (the feed's lag)
+      const double dt = now - w.t0;
+      wait_s_ += dt;
+      wait_max_s_ = std::max(wait_max_s_, dt);
+    };
     for (auto& w : waiting_) {
       std::string resp, why;
       if (w.method == "GetPreferredAllocation") {
         if (core_->preferred(w.message, &resp, &why)) {
           srv_->respond(w.call, 0, resp);
+          waited(w);
           continue;
         }
       } else {
@@ -1325,11 +1337,13 @@ class PyDpServer {
         DpStep step = core_->allocate(w.message, &resp, &ev, &pend, &why);
         if (step == DpStep::Answered || step == DpStep::AnsweredPending) {
           srv_->respond(w.call, 0, resp);
+          waited(w);
           events_.push_back(std::move(ev));
           if (step == DpStep::AnsweredPending) queue_patch(std::move(pend), w.call, w.message);
           continue;
         }
         if (step == DpStep::Pending) {
+          waited(w);
           pend->call = w.call;
           pend->request = w.message;
           std::lock_guard<std::mutex> l(wmu_);
@@ -1344,6 +1358,7 @@ class PyDpServer {
         }
       }
       if (expire && now >= w.deadline) {
+        waited(w);
         last_why_ = why;
         pending_.emplace_back(w.call, w.method, w.message);
       } else {
@@ -1458,6 +1473,7 @@ class PyDpServer {
   std::vector<Feed> feed_;
   std::vector<Waiting> waiting_;
   uint64_t waited_ = 0, feed_events_ = 0;
+  double wait_s_ = 0, wait_max_s_ = 0;  // calls that waited for their pod's event: total / longest wait
   int tfd_ = -1;
   std::thread worker_;
   std::mutex wmu_;
@@ -1478,7 +1494,7 @@ class PyDpServer {
   std::thread serving_;
   std::atomic<bool> stop_serving_{false};  // written under the state lock
   int pyfd_ = -1;              // readable: pending_ / events_ waiting for poll()
-  double h_pref_s_ = 0, h_alloc_s_ = 0;
+  double h_pref_s_ = 0, h_alloc_s_ = 0, h_pref_max_ = 0, h_alloc_max_ = 0;
   bool ready_ = true;       // false: every call is answered UNAVAILABLE (set_ready)
   bool preferred_ = false;  // cfg "preferred": advertise GetPreferredAllocation (kubelet then calls it per admission)
   double py_event_s_ = 0.002;  // cfg "py_event_ms": how often answered Allocates are handed to Python at most
