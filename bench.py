@@ -538,7 +538,11 @@ def main():
     # CPUs per process: the extender (2 loops + bind pool + reflectors), schedsim (cycle + bind threads) and the
     # node agent (reflector + workers) get two; rank 0 stays on one core (a second one let its driver, tracker
     # and runtime threads migrate: 7.5-9.4k vs 10.1k pods/s, interleaved A/B in profiles/r02_bench_stability.md)
-    widths = {"extender": 2, "scheduler": 2, "node-agent": 2, "plugin": 2}
+    # The plugin gets two cores: its serving thread spins after each pass (one SMT thread), and on one core its pod
+    # feed, Python thread and commit worker shared the other -- a pod's event then reached the plugin up to 1.6 ms
+    # after kubelet asked for it (profiles/r04_pinw/: 2 CPUs 9.5 / 7.9 / 7.7k pods/s with 1.5-2 ms waves, 4 CPUs
+    # 9.7 / 9.3 / 10.0k with none, interleaved)
+    widths = {"extender": 2, "scheduler": 2, "node-agent": 2, "plugin": 4}
     if a.runtime_cpu == "split":
         # rank 0 = the wave driver + GPU 0's runtime endpoint (the CRI-runtime role): one core, the driver on
         # one SMT thread and the endpoint's threads on the other, instead of both time-sharing one thread
