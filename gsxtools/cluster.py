@@ -172,7 +172,7 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
         env["GSX_EXTENDER_URL"] = extender
     env = env or None
     if native:
-        exe = tool_path("gsx-nodeagent")
+        exe = Path(os.environ.get("GSX_NODEAGENT_BIN") or tool_path("gsx-nodeagent"))  # an A/B build of the stand-in
         if not exe.exists():
             raise FileNotFoundError(f"{exe} missing; run `python native/build.py nodeagent`")
         spawn = ["--plugin-spawn", sys.executable] if plugin == "spawn" else []

@@ -45,6 +45,7 @@
 #include <cstring>
 #include <deque>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -429,6 +430,7 @@ class Agent {
   // ---------------------------------------------------------------- admission (agent.py _admit)
   void worker() {
     std::unique_lock<std::mutex> lk(mu_);
+    std::unique_lock<std::mutex> slot(dp_mu_, std::defer_lock);  // the admission slot, when this worker holds it
     while (true) {
       double now = now_s();
       if (!batch_.empty() && now >= batch_deadline_) {
@@ -446,34 +448,41 @@ class Agent {
         }
       }
       if (stop_) return;
+      const bool serial = dp_ || serial_admission_;
+      // kubelet admits one pod at a time, in the order it met them (its sync loop), and its pod workers start the
+      // admitted containers in parallel.  The worker holding the admission slot pops the queue's front only while
+      // it holds the slot (taken under mu_, never waited for: a worker that popped first but reached the slot later
+      // would reorder the Allocates), and with the plugin it keeps the slot for the next pod, leaving the start of
+      // the one it admitted to another worker (starts_): admissions follow each other with no thread hand-off
+      if (!queue_.empty() && (!serial || slot.owns_lock() || slot.try_lock())) {
+        std::string key = std::move(queue_.front());
+        queue_.pop_front();
+        auto kit = keys_.find(key);
+        if (kit == keys_.end()) continue;
+        queued_.erase(kit->second);
+        admit_locked(key, lk, serial ? &slot : nullptr);
+        continue;
+      }
+      if (slot.owns_lock()) {  // nothing left to admit: another worker may take the slot
+        slot.unlock();
+        cv_.notify_all();
+      }
       if (!releases_.empty()) {
         auto rel = releases_.front();
         releases_.pop_front();
         release_one(rel, lk);
         continue;
       }
-      if (queue_.empty()) {
-        double wait = 0.05;
-        for (auto& dl : delayed_) wait = std::min(wait, std::max(0.0, dl.first - now));
-        if (!batch_.empty()) wait = std::min(wait, std::max(0.0, batch_deadline_ - now));
-        cv_.wait_for(lk, std::chrono::duration<double>(wait));
+      if (!starts_.empty()) {
+        auto start = std::move(starts_.front());
+        starts_.pop_front();
+        start(lk);
         continue;
       }
-      std::unique_lock<std::mutex> slot;
-      if (dp_ || serial_admission_) {
-        // kubelet admits one pod at a time, in the order it met them: take the admission slot first, then the
-        // queue's front (a worker that popped first but reached the slot later would reorder the Allocates)
-        lk.unlock();
-        slot = std::unique_lock<std::mutex>(dp_mu_);
-        lk.lock();
-        if (queue_.empty() || stop_) continue;
-      }
-      std::string key = std::move(queue_.front());
-      queue_.pop_front();
-      auto kit = keys_.find(key);
-      if (kit == keys_.end()) continue;
-      queued_.erase(kit->second);
-      admit_locked(key, lk, &slot);
+      double wait = 0.05;
+      for (auto& dl : delayed_) wait = std::min(wait, std::max(0.0, dl.first - now));
+      if (!batch_.empty()) wait = std::min(wait, std::max(0.0, batch_deadline_ - now));
+      cv_.wait_for(lk, std::chrono::duration<double>(wait));
     }
   }
 
@@ -651,8 +660,7 @@ class Agent {
     }
     used_ids_[my_uid] = chosen[0];
     uid_key_[my_uid] = my_key;
-    mark_used_locked(chosen[0], 1);
-    release_slot();
+    mark_used_locked(chosen[0], 1);  // recorded before the next admission: it is never offered these IDs
     auto idx = cr.envs.find(p_.a_idx);
     const int dev_idx = idx == cr.envs.end() ? -1 : std::atoi(idx->second.c_str());
     if (!devices_.count(dev_idx)) {
@@ -672,8 +680,13 @@ class Agent {
     auto ce = cr.envs.find(p_.env_container);
     const int64_t request = ce == cr.envs.end() ? units : std::max<int64_t>(1, std::atoll(ce->second.c_str()));
     state_->set_inflight(my_uid, true);
-    start_pod_locked(my_key, my_uid, request, dev_idx, cus, allocation_json(cr),
-                     "/api/v1/namespaces/" + mine_ns(my_key) + "/pods/" + mine_name(my_key), t0, tp0, tp1, lk);
+    // a pod worker starts the container; this worker goes on with the next admission (it keeps the slot)
+    starts_.push_back([this, my_key, my_uid, request, dev_idx, cus, alloc = allocation_json(cr),
+                       path = "/api/v1/namespaces/" + mine_ns(my_key) + "/pods/" + mine_name(my_key), t0, tp0,
+                       tp1](std::unique_lock<std::mutex>& l) {
+      start_pod_locked(my_key, my_uid, request, dev_idx, cus, alloc, path, t0, tp0, tp1, l);
+    });
+    cv_.notify_one();
   }
 
   // the spawned plugin's /healthz, /metrics and /debug/state (its reconciliation and endpoint counters)
@@ -830,7 +843,10 @@ class Agent {
     double tp0 = now_s();
     bool ok = api_.request("PATCH", path, patch, "application/merge-patch+json", &status, &resp, &err);
     double tp1 = now_s();
-    if (slot && slot->owns_lock()) slot->unlock();  // the Allocate (its commit) is done: the next admission may go
+    if (slot && slot->owns_lock()) {  // the Allocate (its commit) is done: the next admission may go
+      slot->unlock();
+      cv_.notify_one();
+    }
     if (!ok || status >= 300) {
       lk.lock();
       if (!cus.empty() && !had_cus && cp) cp->release(uid);
@@ -1058,6 +1074,7 @@ class Agent {
   std::unordered_map<std::string, double> seen_;
   std::unordered_map<std::string, std::string> allocations_;
   std::deque<std::string> queue_;
+  std::deque<std::function<void(std::unique_lock<std::mutex>&)>> starts_;  // admitted pods to start (pod workers)
   std::vector<std::pair<double, std::string>> delayed_;
   std::deque<std::pair<std::string, int>> releases_;
   std::map<int, int> releasing_;  // per GPU: DELETEs in flight on some worker
