@@ -218,15 +218,21 @@ class Agent {
       wake_locked();
     };
     h.on_event = [this](Ev ev, const json::Doc& d, uint32_t obj) {
-      std::lock_guard<std::mutex> g(mu_);
+      // the event is read before the agent's lock is taken: the admitting worker needs that lock between its
+      // two calls to the plugin, and a wave of N x 4 pods brings ~5 events per pod
       if (ev == Ev::Deleted) {
         PodView v;
         parse_pod(d, obj, p_, &v);
+        std::lock_guard<std::mutex> g(mu_);
         on_delete_locked(v.ns + "/" + v.name);
+        wake_locked();
       } else {
-        on_pod_locked(d, obj, nullptr);
+        AllocPod ap;
+        parse_alloc_pod(d, obj, p_, &ap);
+        std::lock_guard<std::mutex> g(mu_);
+        on_pod_parsed_locked(ap, nullptr);
+        wake_locked();
       }
-      wake_locked();
     };
     pods_r_ = std::make_unique<Reflector>(api_cfg_, rc, h);
     pods_r_->start();
@@ -363,6 +369,10 @@ class Agent {
   std::string on_pod_locked(const json::Doc& d, uint32_t obj, std::unordered_set<std::string>* live) {
     AllocPod ap;
     parse_alloc_pod(d, obj, p_, &ap);
+    return on_pod_parsed_locked(ap, live);
+  }
+
+  std::string on_pod_parsed_locked(const AllocPod& ap, std::unordered_set<std::string>* live) {
     const std::string key = ap.key;
     const std::string uid = ap.uid;
     if (live) live->insert(uid);

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r04_admitloop
+OUT=gpurun_out/${TAG:-r04_admitloop}
 mkdir -p $OUT
 run() {  # name bin n extra...
   local name=$1 bin=$2 n=$3; shift 3
@@ -16,7 +16,7 @@ import json; d=json.load(open('$OUT/$name.json')); w=[x[2] for x in d['wave_ms_e
 print('$name', d['value'], d['wave_pods_per_s']['p50'], 'max wave', max(w), d['node_agent'].get('mismatch'), d['node_agent'].get('plugin_calls_mean_ms'), d.get('busy_threads_pct',{}).get('node-agent'))"
 }
 NEW=gpushare_scheduler_extender_amd/_native/gsx-nodeagent
-OLD=abtools/gsx-nodeagent_slot_handoff
+OLD=${OLD:-abtools/gsx-nodeagent_slot_handoff}
 for i in 1 2 3; do
   run n1.old.$i $OLD 1 || exit 1
   run n1.new.$i $NEW 1 || exit 1
