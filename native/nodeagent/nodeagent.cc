@@ -283,13 +283,14 @@ class Agent {
       std::sort(lat.begin(), lat.end());
       double p50 = lat.empty() ? 0 : lat[lat.size() / 2];
       const double n = admitted_ ? static_cast<double>(admitted_) : 1.0;
-      char b[1024];
+      char b[2048];
       std::snprintf(b, sizeof(b),
                     "{\"admitted\":%llu,\"failed\":%llu,\"bad_stamps\":%llu,\"conflicts\":%llu,\"running\":%zu,"
                     "\"admit_p50_ms\":%.3f,\"admit_max_ms\":%.3f,\"max_ms\":{\"queue\":%.3f,\"assign_patch\":%.3f,"
                     "\"runtime\":%.3f,\"running_patch\":%.3f},\"mean_ms\":{\"queue\":%.4f,\"assign_patch\":%.4f,"
                     "\"runtime\":%.4f,\"running_patch\":%.4f},\"status_retries\":%llu,\"api_connects\":%llu,"
-                    "\"plugin_calls_mean_ms\":{\"n\":%llu,\"slot_wait\":%.4f,\"get_preferred\":%.4f,\"allocate\":%.4f},"
+                    "\"plugin_calls_mean_ms\":{\"n\":%llu,\"slot_wait\":%.4f,\"get_preferred\":%.4f,\"allocate\":%.4f,"
+                    "\"encode_preferred\":%.4f,\"gap\":%.4f,\"n_gap\":%llu},"
                     "\"mismatch\":%llu,\"podresources_calls\":%llu,\"plugin_debug\":\"%s\",\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
                     (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
@@ -298,7 +299,10 @@ class Agent {
                     (unsigned long long)status_retries_.load(), (unsigned long long)api_.reconnects(),
                     (unsigned long long)dp_calls_, sum_dp_slot_ / std::max<double>(1.0, dp_calls_) * 1e3,
                     sum_dp_pref_ / std::max<double>(1.0, dp_calls_) * 1e3,
-                    sum_dp_alloc_ / std::max<double>(1.0, dp_calls_) * 1e3, (unsigned long long)mismatch_,
+                    sum_dp_alloc_ / std::max<double>(1.0, dp_calls_) * 1e3,
+                    sum_dp_enc_ / std::max<double>(1.0, dp_calls_) * 1e3,
+                    sum_dp_gap_ / std::max<double>(1.0, n_dp_gap_) * 1e3, (unsigned long long)n_dp_gap_,
+                    (unsigned long long)mismatch_,
                     (unsigned long long)pr_calls_.load(), plugin_debug_url().c_str());
       rep.body = b;
       return rep;
@@ -604,6 +608,7 @@ class Agent {
     }
     state_->set_inflight(my_uid, true);
     const double t0 = seen_.count(my_uid) ? seen_[my_uid] : now_s();
+    const double prev_done = last_admitted_;
     lk.unlock();
     std::string resp, err;
     int st = 0;
@@ -611,13 +616,14 @@ class Agent {
     std::vector<dp::ContainerResponse> crs;
     const double tp0 = now_s();
     bool ok;
-    double ts = 0, tpref = 0;
+    double ts = 0, tpref = 0, tenc = 0;
     {
       // the worker holds the admission slot (dp_mu_) from the queue pop on: kubelet admits one pod at a time
       ts = now_s();
       if (preferred_) {
-        ok = dp_->call("/v1beta1.DevicePlugin/GetPreferredAllocation",
-                       dp::encode_preferred_request_views(available, static_cast<int32_t>(units)), &resp, &st, &err) &&
+        const std::string req = dp::encode_preferred_request_views(available, static_cast<int32_t>(units));
+        tenc = now_s() - ts;
+        ok = dp_->call("/v1beta1.DevicePlugin/GetPreferredAllocation", req, &resp, &st, &err) &&
              dp::decode_preferred_response(resp, &chosen) && chosen.size() == 1;
       } else {
         // kubelet's own pick (devicesToAllocate without a preference): the first free IDs
@@ -639,6 +645,11 @@ class Agent {
     sum_dp_slot_ += ts - tp0;  // waiting for the admission slot (another pod's calls)
     sum_dp_pref_ += tpref - ts;
     sum_dp_alloc_ += tp1 - tpref;
+    sum_dp_enc_ += tenc;
+    if (prev_done > 0 && ts - prev_done < 0.002) {  // back to back: from the last admission's end to this one's calls
+      sum_dp_gap_ += ts - prev_done;
+      n_dp_gap_++;
+    }
     state_->set_inflight(my_uid, false);
     if (!ok) {
       failed_++;
@@ -671,6 +682,7 @@ class Agent {
     used_ids_[my_uid] = chosen[0];
     uid_key_[my_uid] = my_key;
     mark_used_locked(chosen[0], 1);  // recorded before the next admission: it is never offered these IDs
+    last_admitted_ = now_s();
     auto idx = cr.envs.find(p_.a_idx);
     const int dev_idx = idx == cr.envs.end() ? -1 : std::atoi(idx->second.c_str());
     if (!devices_.count(dev_idx)) {
@@ -1099,7 +1111,9 @@ class Agent {
   double max_queue_ = 0, max_patch_ = 0, max_runtime_ = 0, max_status_ = 0;
   double sum_queue_ = 0, sum_patch_ = 0, sum_runtime_ = 0, sum_status_ = 0;  // over admitted_ pods
   uint64_t dp_calls_ = 0;  // GetPreferredAllocation + Allocate pairs to the plugin (--plugin-socket / --plugin-spawn)
-  double sum_dp_slot_ = 0, sum_dp_pref_ = 0, sum_dp_alloc_ = 0;
+  double sum_dp_slot_ = 0, sum_dp_pref_ = 0, sum_dp_alloc_ = 0, sum_dp_enc_ = 0, sum_dp_gap_ = 0;
+  uint64_t n_dp_gap_ = 0;
+  double last_admitted_ = 0;  // when the last admission's IDs were recorded
   std::vector<std::thread> workers_;
 };
 
