@@ -182,19 +182,6 @@ std::string encode_allocate_request(const std::vector<std::vector<std::string>>&
   return o;
 }
 
-std::string encode_preferred_request_views(const std::vector<std::string_view>& available, int32_t size) {
-  size_t n = 16;
-  for (auto id : available) n += id.size() + 3;
-  std::string c;
-  c.reserve(n);
-  for (auto id : available) bytes(&c, 1, id);
-  int_field(&c, 3, size);
-  std::string o;
-  o.reserve(c.size() + 8);
-  bytes(&o, 1, c);
-  return o;
-}
-
 std::string encode_preferred_request(const std::vector<PreferredRequest>& reqs) {
   std::string o;
   for (const auto& r : reqs) {

@@ -35,8 +35,6 @@ struct PreferredRequest {
   std::vector<std::string> available, must_include;
   int32_t size = 0;
 };
-// kubelet's side for one container, the IDs as views (no string per ID: an 8-GPU node lists ~2,300 free IDs)
-std::string encode_preferred_request_views(const std::vector<std::string_view>& available, int32_t size);
 // The same, as views into the request message (kubelet sends every free ID of the node: hundreds of strings)
 struct PreferredRequestView {
   std::vector<std::string_view> available, must_include;

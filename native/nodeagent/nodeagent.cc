@@ -72,6 +72,14 @@ using namespace gsx;
 
 namespace {
 
+void put_varint(std::string* o, uint64_t v) {  // protobuf base-128 varint
+  while (v >= 0x80) {
+    o->push_back(static_cast<char>((v & 0x7f) | 0x80));
+    v >>= 7;
+  }
+  o->push_back(static_cast<char>(v));
+}
+
 const char* kDevInfoAnn = "gpushare.amd.com/devices";
 const char* kEndpointsAnn = "gpushare.amd.com/runtime-endpoints";
 const char* kCuMaskAnn = "gpushare.amd.com/cu-mask";
@@ -560,7 +568,15 @@ class Agent {
             if (d.health == "Healthy") all_ids_.push_back(d.id);
           }
           id_index_.clear();
-          for (size_t i = 0; i < all_ids_.size(); ++i) id_index_.emplace(all_ids_[i], i);
+          id_field_.clear();
+          for (size_t i = 0; i < all_ids_.size(); ++i) {
+            id_index_.emplace(all_ids_[i], i);
+            // the ID as GetPreferredAllocation's field 1 (available_deviceIDs), encoded once
+            std::string f(1, '\x0a');
+            put_varint(&f, all_ids_[i].size());
+            f.append(all_ids_[i]);
+            id_field_.push_back(std::move(f));
+          }
           id_used_.assign(all_ids_.size(), 0);
           // as kubelet: GetPreferredAllocation only if the plugin's options advertise it
           std::string opts;
@@ -588,16 +604,22 @@ class Agent {
     const std::string my_uid = mine->uid, my_key = key;
     if (running_.count(my_uid) || state_->inflight(my_uid)) return;
     const int64_t units = mine->request;
-    // kubelet's free IDs: every healthy ID no running container holds.  Views into all_ids_ (fixed once the plugin
-    // is connected); without GetPreferredAllocation only the first `units` are needed, kubelet's own pick
-    std::vector<std::string_view> available;
-    available.reserve(preferred_ ? all_ids_.size() : static_cast<size_t>(std::max<int64_t>(units, 0)));
-    size_t n_free = 0;
+    // kubelet's free IDs: every healthy ID no running container holds, as indices into all_ids_ (fixed once the
+    // plugin is connected); without GetPreferredAllocation only the first `units` are needed, kubelet's own pick
+    std::vector<uint32_t> free_idx;
+    free_idx.reserve(preferred_ ? all_ids_.size() : static_cast<size_t>(std::max<int64_t>(units, 0)));
+    size_t n_free = 0, field_bytes = 0;
     for (size_t i = 0; i < all_ids_.size(); ++i) {
       if (id_used_[i]) continue;
       ++n_free;
-      if (preferred_ || static_cast<int64_t>(available.size()) < units) available.push_back(all_ids_[i]);
-      else if (n_free >= static_cast<size_t>(units)) break;
+      if (preferred_) {
+        free_idx.push_back(static_cast<uint32_t>(i));
+        field_bytes += id_field_[i].size();
+      } else if (static_cast<int64_t>(free_idx.size()) < units) {
+        free_idx.push_back(static_cast<uint32_t>(i));
+      } else {
+        break;
+      }
     }
     if (static_cast<int64_t>(n_free) < units) {
       std::fprintf(stderr, "[gsx-nodeagent] %s: %lld units requested, %zu IDs free\n", key.c_str(),
@@ -609,7 +631,10 @@ class Agent {
     state_->set_inflight(my_uid, true);
     const double t0 = seen_.count(my_uid) ? seen_[my_uid] : now_s();
     const double prev_done = last_admitted_;
+    const bool wake_starter = start_queued_;  // the previous admission's start, signalled outside the lock
+    start_queued_ = false;
     lk.unlock();
+    if (wake_starter) cv_.notify_one();
     std::string resp, err;
     int st = 0;
     std::vector<std::vector<std::string>> chosen;
@@ -621,13 +646,21 @@ class Agent {
       // the worker holds the admission slot (dp_mu_) from the queue pop on: kubelet admits one pod at a time
       ts = now_s();
       if (preferred_) {
-        const std::string req = dp::encode_preferred_request_views(available, static_cast<int32_t>(units));
+        // kubelet's request: one container, every free ID (the fields encoded at connect), then the size
+        std::string size_field(1, '\x18');
+        put_varint(&size_field, static_cast<uint64_t>(units));
+        std::string req(1, '\x0a');
+        put_varint(&req, field_bytes + size_field.size());
+        req.reserve(req.size() + field_bytes + size_field.size());
+        for (uint32_t i : free_idx) req.append(id_field_[i]);
+        req.append(size_field);
         tenc = now_s() - ts;
         ok = dp_->call("/v1beta1.DevicePlugin/GetPreferredAllocation", req, &resp, &st, &err) &&
              dp::decode_preferred_response(resp, &chosen) && chosen.size() == 1;
       } else {
         // kubelet's own pick (devicesToAllocate without a preference): the first free IDs
-        chosen.assign(1, std::vector<std::string>(available.begin(), available.begin() + units));
+        chosen.assign(1, {});
+        for (uint32_t i : free_idx) chosen[0].push_back(all_ids_[i]);
         ok = true;
       }
       tpref = now_s();
@@ -689,26 +722,27 @@ class Agent {
       forget_ids_locked(my_uid);
       return;
     }
-    std::vector<int> cus;
-    auto cm = cr.envs.find("GSX_CU_MASK");
-    if (cm != cr.envs.end()) {
-      try {
-        cus = parse_cu_words(cm->second);
-      } catch (const std::exception&) {
-        cus.clear();
-      }
-    }
-    // the container's share is what the plugin's env says it got (SHARED_GPU_MEM_CONTAINER)
-    auto ce = cr.envs.find(p_.env_container);
-    const int64_t request = ce == cr.envs.end() ? units : std::max<int64_t>(1, std::atoll(ce->second.c_str()));
     state_->set_inflight(my_uid, true);
-    // a pod worker starts the container; this worker goes on with the next admission (it keeps the slot)
-    starts_.push_back([this, my_key, my_uid, request, dev_idx, cus, alloc = allocation_json(cr),
-                       path = "/api/v1/namespaces/" + mine_ns(my_key) + "/pods/" + mine_name(my_key), t0, tp0,
+    // a pod worker starts the container (reading the plugin's answer there, off the admission path); this worker
+    // goes on with the next admission (it keeps the slot) and wakes a pod worker once it has let go of the lock
+    starts_.push_back([this, my_key, my_uid, units, dev_idx, cr = std::move(crs[0]), t0, tp0,
                        tp1](std::unique_lock<std::mutex>& l) {
-      start_pod_locked(my_key, my_uid, request, dev_idx, cus, alloc, path, t0, tp0, tp1, l);
+      std::vector<int> cus;
+      auto cm = cr.envs.find("GSX_CU_MASK");
+      if (cm != cr.envs.end()) {
+        try {
+          cus = parse_cu_words(cm->second);
+        } catch (const std::exception&) {
+          cus.clear();
+        }
+      }
+      // the container's share is what the plugin's env says it got (SHARED_GPU_MEM_CONTAINER)
+      auto ce = cr.envs.find(p_.env_container);
+      const int64_t request = ce == cr.envs.end() ? units : std::max<int64_t>(1, std::atoll(ce->second.c_str()));
+      start_pod_locked(my_key, my_uid, request, dev_idx, cus, allocation_json(cr),
+                       "/api/v1/namespaces/" + mine_ns(my_key) + "/pods/" + mine_name(my_key), t0, tp0, tp1, l);
     });
-    cv_.notify_one();
+    start_queued_ = true;
   }
 
   // the spawned plugin's /healthz, /metrics and /debug/state (its reconciliation and endpoint counters)
@@ -1071,6 +1105,8 @@ class Agent {
   std::vector<std::string> all_ids_;
   std::unordered_map<std::string, std::vector<std::string>> used_ids_;  // uid -> the IDs its Allocate took
   std::unordered_map<std::string, size_t> id_index_;                     // ID -> its place in all_ids_
+  std::vector<std::string> id_field_;  // per all_ids_ entry: the ID encoded as GetPreferredAllocation's field 1
+  bool start_queued_ = false;          // starts_ got a pod no pod worker was woken for yet
   std::vector<char> id_used_;  // per all_ids_ entry: held by a running container (the union of used_ids_)
   std::unordered_map<std::string, std::string> uid_key_;                 // uid -> ns/name of every used_ids_ pod
   std::string pr_sock_;                    // kubelet's PodResources API socket (with --plugin-spawn)
