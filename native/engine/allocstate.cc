@@ -453,7 +453,7 @@ void AllocState::later_container_allocated(const std::string& uid, int64_t units
 // ---------------------------------------------------------------- records
 
 AllocRecord& AllocState::record(const std::string& uid, const std::vector<std::string>& ids_in, int64_t units,
-                                const std::string& cu_mask, const std::string& aid, double t) {
+                                const std::string& cu_mask, const std::string& aid, double t, bool on_gpu) {
   std::vector<std::string> ids(ids_in);
   std::sort(ids.begin(), ids.end());
   const std::string key = ids.empty() ? std::string() : id_key(ids);
@@ -469,8 +469,9 @@ AllocRecord& AllocState::record(const std::string& uid, const std::vector<std::s
   r.units = units;
   r.cu_mask = cu_mask;
   r.t = t;
+  r.on_gpu = on_gpu;
   if (!ids.empty()) by_ids_[key] = aid;
-  if (!ids.empty()) hold(key, Held{r.dev, units, t, uid, false, cu_mask});
+  if (!ids.empty()) hold(key, Held{r.dev, units, t, uid, on_gpu, cu_mask});
   r.ids = std::move(ids);
   auto res = records_.insert_or_assign(aid, std::move(r));
   return res.first->second;

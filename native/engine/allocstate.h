@@ -150,8 +150,9 @@ class AllocState {
   void later_container_allocated(const std::string& uid, int64_t units);
 
   // ---- allocation records
+  // `on_gpu`: every ID lies on the pod's GPU (set here, not by a later mark_on_gpu: one key and hash fewer)
   AllocRecord& record(const std::string& uid, const std::vector<std::string>& ids, int64_t units,
-                      const std::string& cu_mask, const std::string& aid, double t);
+                      const std::string& cu_mask, const std::string& aid, double t, bool on_gpu = false);
   void add_record(AllocRecord r);  // restored from a checkpoint
   bool drop_record(const std::string& aid);
   const AllocRecord* record_for_ids(std::vector<std::string> ids) const;

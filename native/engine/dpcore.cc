@@ -553,11 +553,10 @@ void DpCore::record_and_answer(DpPending& p, std::string* resp, DpEvent* ev) {
   auto cm = p.cr.annotations.find(kCuMaskAnn);
   const double tr0 = mono_s();
   AllocRecord& rec = state_->record(p.pod.uid, p.ids, p.units,
-                                    cm != p.cr.annotations.end() ? cm->second : p.pod.cu_mask, aid, wall_s());
+                                    cm != p.cr.annotations.end() ? cm->second : p.pod.cu_mask, aid, wall_s(), p.on_gpu);
   rec.iso = p.iso;
-  if (p.on_gpu) state_->mark_on_gpu(aid, true);
   const double tr1 = mono_s();
-  if (p.answered) journal_append(*state_->record_by_aid(aid));  // durable before kubelet has the answer
+  if (p.answered) journal_append(rec);  // durable before kubelet has the answer
   const double tj = mono_s();
   *resp = dp::encode_allocate_response({p.cr});
   stats_.ph_record += tr1 - tr0;
