@@ -163,8 +163,12 @@ def _cpu_times(children) -> dict:
 def _rss_mib(children) -> dict:
     """Resident set of this process and the child servers (a long run shows whether any of them grows)."""
     out = {}
-    for name, pid in [("rank0", os.getpid())] + [(c.name, getattr(getattr(c, "proc", None), "pid", None))
-                                                 for c in children]:
+    procs = [("rank0", os.getpid())] + [(c.name, getattr(getattr(c, "proc", None), "pid", None)) for c in children]
+    for c in children:  # the device-plugin process the node agent spawned (the product's node-side process)
+        pid = getattr(getattr(c, "proc", None), "pid", None)
+        if c.name == "node-agent" and pid is not None:
+            procs += [("plugin", k) for k in _child_pids(pid)]
+    for name, pid in procs:
         try:
             with open(f"/proc/{pid}/status") as f:
                 for ln in f:
