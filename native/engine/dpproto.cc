@@ -223,6 +223,38 @@ bool decode_preferred_request(std::string_view msg, std::vector<PreferredRequest
   });
 }
 
+bool preferred_single(std::string_view msg, int32_t* size, std::string_view* container) {
+  int n = 0;
+  bool ok = each(msg, [&](int f, int w, std::string_view pl, uint64_t) {
+    if (f == 1 && w == 2) {
+      ++n;
+      *container = pl;
+    }
+    return true;
+  });
+  if (!ok || n != 1) return false;
+  bool must = false;
+  *size = 0;
+  ok = each(*container, [&](int f, int w, std::string_view, uint64_t v) {
+    if (f == 2 && w == 2) must = true;
+    if (f == 3 && w == 0) *size = static_cast<int32_t>(v);
+    return true;
+  });
+  return ok && !must;
+}
+
+bool for_each_available(std::string_view container, const std::function<bool(std::string_view)>& fn) {
+  bool stopped = false;
+  const bool ok = each(container, [&](int f, int w, std::string_view pl, uint64_t) {
+    if (f == 1 && w == 2 && !fn(pl)) {
+      stopped = true;
+      return false;  // the rest of the list is not read
+    }
+    return true;
+  });
+  return ok || stopped;
+}
+
 bool decode_list_and_watch(const std::string& msg, std::vector<DeviceMsg>* out) {
   return each(msg, [&](int f, int w, std::string_view pl, uint64_t) {
     if (f != 1 || w != 2) return true;

@@ -4,6 +4,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <string>
 #include <string_view>
@@ -64,6 +65,10 @@ std::string encode_preferred_request(const std::vector<PreferredRequest>& reqs);
 // ---- decode (false: malformed)
 bool decode_allocate_request(const std::string& msg, std::vector<std::vector<std::string>>* ids_per_container);
 bool decode_preferred_request(std::string_view msg, std::vector<PreferredRequestView>* reqs);  // views into msg
+// kubelet's usual GetPreferredAllocation: one container, no must_include.  Its size and the container message (whose
+// available IDs for_each_available walks in order, stopping when `fn` returns false); false for any other shape.
+bool preferred_single(std::string_view msg, int32_t* size, std::string_view* container);
+bool for_each_available(std::string_view container, const std::function<bool(std::string_view)>& fn);
 bool decode_list_and_watch(const std::string& msg, std::vector<DeviceMsg>* devs);
 bool decode_preferred_response(const std::string& msg, std::vector<std::vector<std::string>>* per_container);
 bool decode_allocate_response(const std::string& msg, std::vector<ContainerResponse>* per_container);

@@ -96,6 +96,33 @@ def test_grpcio_kubelet_against_the_native_endpoint(monkeypatch):
     asyncio.run(go())
 
 
+def test_preferred_allocation_steers_ids_onto_the_pods_gpu(monkeypatch):
+    """GetPreferredAllocation on the native endpoint: kubelet's usual request (one container, every free ID, in any
+    order) gets the pod's GPU's IDs first and others only when that GPU has too few; a request with must_include
+    IDs (the general path) keeps them."""
+    monkeypatch.setenv("GSX_PLUGIN_PREFERRED", "1")
+
+    async def go():
+        tmp = tempfile.mkdtemp()
+        api_srv, client, plugin = await _plugin(tmp, fast=True)
+        pc = PluginClient(plugin.socket_path)
+        try:
+            await client.create("pods", bound_pod("a", 4, dev=1, assume=1, dev_total=16))
+            await asyncio.sleep(0.2)
+            ids0, ids1 = fake_ids(plugin.devices[0], 16), fake_ids(plugin.devices[1], 16)
+            on1 = set(ids1)
+            got = list((await pc.preferred(ids0 + ids1[::-1], 4)).container_responses[0].deviceIDs)
+            assert len(got) == 4 and set(got) <= on1 and got == ids1[::-1][:4], got
+            got = list((await pc.preferred(ids0[:8] + ids1[:2] + ids0[8:], 4)).container_responses[0].deviceIDs)
+            assert got[:2] == ids1[:2] and got[2:] == ids0[:2], got  # GPU 1 has two free: the rest in list order
+            got = list((await pc.preferred(ids0 + ids1, 4, must=[ids0[5]])).container_responses[0].deviceIDs)
+            assert got[0] == ids0[5] and set(got[1:]) <= on1 and len(got) == 4, got
+            assert plugin.debug_state()["grpc"]["fast_preferred"] >= 3
+        finally:
+            await _close(api_srv, client, plugin, pc)
+    asyncio.run(go())
+
+
 @pytest.mark.parametrize("isolation", [False, True])
 def test_fast_path_answers_exactly_what_the_python_handler_answers(isolation):
     """The same pods through the native fast path and through the Python handler (fast path off): identical
