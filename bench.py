@@ -19,7 +19,10 @@ every step is one *wave* of ``pods_per_gpu x N`` pods of ``pod_gib`` GiB
   wave is deleted and the step ends when the extender's ledger is empty.
 
 Timed region: exactly K steps bracketed by barrier + torch.cuda.synchronize()
-on both sides; the max over ranks is reported.  ``value`` = pods bound per
+on both sides; the max over ranks is reported.  Every collective is gloo (control traffic only: barriers, small
+objects, one float MAX on a CPU tensor); the scheduling data path has none, so RCCL is never initialised.
+``--share-gpu`` runs N ranks on physical GPU 0 (one logical device per rank), the one-box rehearsal of the
+N-GPU launch.  ``value`` = pods bound per
 second over the whole job (all GPUs).  Synthetic pods; no cluster, no real
 kubelet (there is none in this environment) — see SURVEY.md §4.  ``dtype`` is
 "n/a": the timed region does no floating-point work (the GPU work is the HIP
@@ -487,6 +490,10 @@ def parse():
                          "stand-in, as the DaemonSet runs it (process), or served from the stand-in's process (grpc)")
     ap.add_argument("--sweep", type=int, default=1, help="1: run the latency sweep after the timed region")
     ap.add_argument("--sweep-steps", type=int, default=8)
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="every rank uses physical GPU 0 (a one-box rehearsal of the N-GPU launch): each rank advertises "
+                         "a logical device sized for its wave (pods-per-gpu x pod-gib plus half a pod) and carves its "
+                         "own HBM arena out of GPU 0, so N processes run their stamp / verify kernels on one card")
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="event loops of the fake apiserver (0: auto; GSX_FAKEAPI_THREADS overrides)")
     return ap.parse_args()
@@ -629,13 +636,15 @@ def main():
     torch.set_num_threads(1)
     profile = get_profile(a.profile)
     use_gpu = a.devices != "fake" and torch.cuda.is_available()
+    # the physical GPU this rank's HBM arena and kernels live on (all ranks on GPU 0 with --share-gpu)
+    phys = 0 if a.share_gpu else local_rank
     if use_gpu:
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(phys)
     if world > 1:
-        dist.init_process_group("nccl" if use_gpu else "gloo")
-        ctl = dist.new_group(backend="gloo")
-    else:
-        ctl = None
+        # every collective of the bench is control traffic (barriers, a few small objects, one float MAX): gloo over
+        # loopback TCP.  The scheduling data path has no collectives, so RCCL is never initialised here.
+        dist.init_process_group("gloo")
+    ctl = None  # the default (gloo) group
 
     def barrier():
         if world > 1:
@@ -662,23 +671,31 @@ def main():
     # ---- this rank's GPU
     backend, devs = discover("fake" if not use_gpu else a.devices)
     if use_gpu:
-        mine = [d for d in devs if d.index == local_rank]
+        mine = [d for d in devs if d.index == phys]
         if not mine:
-            raise SystemExit(f"rank {rank}: GPU {local_rank} not found ({backend})")
+            raise SystemExit(f"rank {rank}: GPU {phys} not found ({backend})")
         dev = mine[0]
     else:
         dev = devs[local_rank % len(devs)]
-        dev.index = local_rank
     dev.index = local_rank
     unit = "GiB"
     pod_bytes = a.pod_gib * UNITS[unit]
     arena = a.pods_per_gpu * pod_bytes
+    if a.share_gpu:
+        # one logical device per rank, carved out of GPU 0: room for the wave's pods plus half a pod, so best fit
+        # puts exactly pods_per_gpu pods on each (as 4 x 64 GiB fill one 287 GiB MI355X)
+        if world * arena > 0.85 * dev.total_bytes:
+            raise SystemExit(f"--share-gpu: {world} arenas of {arena >> 30} GiB do not fit GPU 0 "
+                             f"({dev.total_bytes >> 30} GiB); lower --pod-gib")
+        dev.share_bytes = arena + (pod_bytes // 2 // UNITS[unit]) * UNITS[unit]
     # this GPU's runtime endpoint (CRI-runtime role): the node agent starts pods on it over HTTP
     if a.agent == "node":
         # native (native/engine/podruntime.cc): request threads carve the slice and run the HIP admission
-        runtime = shim = NativeRuntime(local_rank, arena, use_gpu, a.stamp_stride, runtime_cpus)
+        runtime = shim = NativeRuntime(phys, arena, use_gpu, a.stamp_stride, runtime_cpus)
         shim_url = shim.url
     else:
+        if a.share_gpu:
+            raise SystemExit("--share-gpu needs --agent node (the per-rank agent keys its arena by the logical index)")
         runtime = (HbmArenaRuntime({local_rank: arena}, stamp_stride=a.stamp_stride) if use_gpu
                    else LedgerRuntime({local_rank: arena}))
         shim = RuntimeShim(runtime)
@@ -932,7 +949,7 @@ def main():
         lt.run(asyncio.sleep(0))
         prof.dump_stats(os.path.join(os.environ["GSX_CPROFILE_DIR"], "rank0-loop.prof"))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if use_gpu else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64)  # gloo: a CPU tensor
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -944,7 +961,8 @@ def main():
         mine = {"admitted": shim.admitted, "failed": shim.failed, "bad_stamps": shim.bad + bad}
         if isinstance(shim, NativeRuntime):
             mine["gpu_admission_calls"] = shim.batches  # concurrent admissions share one stamp+verify+sync
-    mine.update({"gpu": local_rank, "hbm_total": dev.total_bytes, "arena": arena})
+    mine.update({"gpu": local_rank, "physical_gpu": phys if use_gpu else None, "hbm_total": dev.usable_bytes,
+                 "arena": arena})
     agent_stats = gather(mine)
     node_agent_stats = plugin_stats = None
     if rank == 0 and a.agent == "node":
@@ -1026,7 +1044,8 @@ def main():
             "config": {"model": f"gpushare extender+device plugin: {a.pods_per_gpu} pods/GPU x {a.pod_gib} GiB "
                                 f"({profile.resource}), binpack", "global_batch": n_pods, "seq_len": 0,
                        "parallelism": f"{world} GPU(s) advertised on 1 node; 1 rank (HBM runtime) per GPU; "
-                                      f"agent={a.agent}",
+                                      f"agent={a.agent}" + ("; all ranks share physical GPU 0" if a.share_gpu else ""),
+                       "collectives": "gloo (control only)" if world > 1 else "none",
                        "bind_mode": a.bind_mode, "bind_order": a.bind_order, "admission": a.admission,
                        "node_agent": a.node_agent, "device_backend": backend},
             "p50_bind_latency_ms": round(1e3 * pct(lat, 50), 3),

@@ -56,8 +56,9 @@ AGENT = {"kind": "plugin", "args": [], "api_latency_ms": 0.0}  # --agent, --fait
 class Runtimes:
     """One pod runtime endpoint per device (native ``_engine.PodRuntime``): accounting only, or GPU 0's HBM arena."""
 
-    def __init__(self, n: int, unit_bytes: int, gib_per_dev: int, gpu: bool | int):
-        """``gpu``: False, True (GPU 0 backs device 0) or the number of leading devices backed by real GPUs."""
+    def __init__(self, n: int, unit_bytes: int, gib_per_dev: int, gpu: bool | int, share_gpu: bool = False):
+        """``gpu``: False, True (GPU 0 backs device 0) or the number of leading devices backed by real GPUs.
+        ``share_gpu``: every real-backed device is an arena on physical GPU 0 (one-GPU rehearsal of an N-GPU node)."""
         from gpushare_scheduler_extender_amd.core.engine import native
 
         E = native()
@@ -69,9 +70,10 @@ class Runtimes:
             if i < n_real:
                 from gpushare_scheduler_extender_amd.ops import hip
 
-                buf = hip.DeviceBuffer(i, arena)
-                st = hip.Stream(i)
-                rt = E.PodRuntime(i, arena, buf.addr(0), st.ptr, 1 << 20, hip.lib()._name)
+                phys = 0 if share_gpu else i
+                buf = hip.DeviceBuffer(phys, arena)
+                st = hip.Stream(phys)
+                rt = E.PodRuntime(phys, arena, buf.addr(0), st.ptr, 1 << 20, hip.lib()._name)
                 self.bufs.append(buf)
                 self.streams.append(st)
             else:
@@ -100,7 +102,8 @@ class Cluster:
 
     def __init__(self, profile: NamingProfile, totals: list[int], gpu: bool | int, cu_count: int = 256,
                  partition: str = "SPX", xcc_count: int = 8, agent: str | None = None,
-                 pool_gib: int = 0, bind_mode: str = "binding", agent_args: list[str] | None = None):
+                 pool_gib: int = 0, bind_mode: str = "binding", agent_args: list[str] | None = None,
+                 share_gpu: bool = False):
         self.profile = profile
         self.totals = totals
         self.children = []
@@ -114,7 +117,7 @@ class Cluster:
         self.agent_args = list(agent_args if agent_args is not None else AGENT["args"])
         self.api_latency_ms = AGENT["api_latency_ms"]
         self.children.append(self._agent())
-        self.rt = Runtimes(len(totals), GIB, max(totals), gpu)
+        self.rt = Runtimes(len(totals), GIB, max(totals), gpu, share_gpu=share_gpu)
         self.cu_count = cu_count
         self.xcc_count = xcc_count
         self.partition = partition
@@ -287,10 +290,16 @@ def _gpu_gib() -> int:
     return hip.mem_info(0)[1] // GIB
 
 
+SHARE = {"on": False}  # --share-gpu: the 8-device configs carve their devices out of GPU 0
+
+
 def _real_gpus(gpu: bool, want: int) -> int:
-    """How many of ``want`` devices real GPUs back: all of them on a node with that many, else none."""
+    """How many of ``want`` devices real GPUs back: all of them on a node with that many (or, with --share-gpu, all
+    of them as arenas on GPU 0), else none."""
     if not gpu:
         return 0
+    if SHARE["on"]:
+        return want
     import torch
 
     return want if torch.cuda.device_count() >= want else 0
@@ -336,11 +345,17 @@ async def config2(gpu: bool) -> dict:
 async def config3(gpu: bool) -> dict:
     per = _gpu_gib() if gpu else 268
     real = _real_gpus(gpu, 8)
-    cl = Cluster(ALIYUN, [per] * 8, gpu=real)
+    share = bool(gpu and SHARE["on"])
+    # with --share-gpu the eight devices are arenas on GPU 0: scaled down 16x (18 GiB devices, 4 GiB pods), the
+    # same 4-per-device fill as 64 GiB pods on a 287 GiB MI355X
+    pod = 4 if share else 64
+    if share:
+        per = 18
+    cl = Cluster(ALIYUN, [per] * 8, gpu=real, share_gpu=share)
     try:
         await cl.start()
         t0 = time.perf_counter()
-        await asyncio.gather(*(cl.create(f"p64-{i}", 64) for i in range(32)))
+        await asyncio.gather(*(cl.create(f"p64-{i}", pod) for i in range(32)))
         pods = await cl.wait([f"p64-{i}" for i in range(32)])
         dt = time.perf_counter() - t0
         # physical placement (the env each container got) == the annotation the extender accounts (a faithful
@@ -349,7 +364,7 @@ async def config3(gpu: bool) -> dict:
         pods = {p["metadata"]["name"]: p for p in (await cl.c.list("pods", "default"))["items"] if p["metadata"]["name"] in pods}
         per_dev = [0] * 8
         for p in pods.values():
-            per_dev[cl.device_of(p)] += 64
+            per_dev[cl.device_of(p)] += pod
         insp = await cl.inspect()
         used = insp["nodes"][0]["usedGPU"]
         bad = cl.rt.verify() if real else 0
@@ -360,12 +375,12 @@ async def config3(gpu: bool) -> dict:
         ast = await cl.agent_stats()
         mismatch = ast.get("mismatch", 0)
         faithful = "--faithful" in cl.agent_args
-        ok = per_dev == [256] * 8 and used == 256 * 8 and bad == 0 and drift == 0 and (faithful or mismatch == 0)
+        ok = per_dev == [4 * pod] * 8 and used == 4 * pod * 8 and bad == 0 and drift == 0 and (faithful or mismatch == 0)
         if real:  # 32 x 64 GiB co-resident in 8 real HBM arenas, 4 slices each
             ok = ok and resident == [4] * 8
         return {"ok": ok, "per_device_gib": per_dev, "device_gib": per, "util_pct": round(100 * used / (8 * per), 2),
-                "real_gpus": real, "resident_slices": resident, "bad_stamps": bad, "seconds": round(dt, 4),
-                "allocate_mismatch": mismatch, "allocate_swapped_equivalent": ast.get("swapped_equivalent", 0),
+                "real_gpus": real, "shared_gpu": share, "pod_gib": pod, "resident_slices": resident, "bad_stamps": bad,
+                "seconds": round(dt, 4), "allocate_mismatch": mismatch, "allocate_swapped_equivalent": ast.get("swapped_equivalent", 0),
                 "physical_drift": drift, "drifted": drifted, "faithful_kubelet": faithful,
                 "api_latency_ms": cl.api_latency_ms, "reconcile": ast.get("reconcile")}
     finally:
@@ -374,7 +389,7 @@ async def config3(gpu: bool) -> dict:
 
 async def config4(gpu: bool) -> dict:
     per = _gpu_gib() if gpu else 268
-    real = _real_gpus(gpu, 8)
+    real = 0 if SHARE["on"] else _real_gpus(gpu, 8)  # 8 x 287 GiB arenas never fit one GPU: accounting only
     cl = Cluster(ALIYUN, [per] * 8, gpu=real)
     try:
         await cl.start()
@@ -555,8 +570,11 @@ def main(argv=None) -> int:
                     help="the kubelet stand-in behaves like kubelet (no re-routing, sorted batches, PodResources); "
                          "the plugin reconciles against it")
     ap.add_argument("--api-latency-ms", type=float, default=0.0, help="fake apiserver latency per request")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="with --gpu: config 3's eight devices are HBM arenas on GPU 0 (one-GPU rehearsal)")
     ap.add_argument("--json-out", default="")
     a = ap.parse_args(argv)
+    SHARE["on"] = a.share_gpu
     AGENT["kind"] = a.agent
     AGENT["args"] = ["--faithful"] if a.faithful else []
     AGENT["api_latency_ms"] = a.api_latency_ms

@@ -91,3 +91,23 @@ def test_bench_eight_ranks_gloo():
     assert d["per_device_used_gib"] == [256] * 8  # 32 x 64 GiB: 4 per device, binpack-first
     assert sum(a["admitted"] for a in d["agents"]) == 3 * 32 or d["node_agent"]["admitted"] == 3 * 32
     assert all(a["bad_stamps"] == 0 for a in d["agents"])
+
+
+@pytest.mark.gpu
+def test_bench_four_ranks_share_one_gpu():
+    """The driver's N-GPU launch on a one-GPU box: 4 ranks (torch.distributed.run, gloo only) each carve an HBM
+    arena out of GPU 0 and run their own pod runtime endpoint with the stamp / verify kernels."""
+    cmd = [sys.executable, "bench.py", "--gpus", "4", "--share-gpu", "--pod-gib", "8", "--steps", "5", "--warmup", "2",
+           "--sweep", "0", "--gpu-warm-ms", "50"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 4 and d["config"]["global_batch"] == 16 and d["value"] > 0
+    assert d["config"]["collectives"] == "gloo (control only)"
+    assert d["per_device_used_gib"] == [32] * 4  # 4 x 8 GiB per logical device, binpack-first
+    agents = d["agents"]
+    assert len(agents) == 4 and all(a["physical_gpu"] == 0 and a["hbm_total"] > 0 for a in agents)
+    assert all(a["bad_stamps"] == 0 and a["failed"] == 0 for a in agents)
+    assert sum(a["admitted"] for a in agents) == 7 * 16
+    # no rank brought up RCCL: the bench's collectives are gloo
+    assert "NCCL INFO" not in r.stderr and "RCCL" not in r.stderr

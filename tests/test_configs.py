@@ -75,6 +75,19 @@ def test_config3_32_pods_in_8_real_hbm_arenas(tmp_path):
     assert rep["4"]["real_gpus"] == 8
 
 
+@pytest.mark.gpu
+def test_config3_32_pods_in_8_hbm_arenas_on_one_gpu(tmp_path):
+    """The 8-device config on a one-GPU box: eight HBM arenas carved out of GPU 0 (4 GiB pods on 18 GiB devices,
+    the same 4-per-device fill), every slice stamped and verified by the HIP kernels."""
+    out = tmp_path / "r.json"
+    rc = configs.main(["--gpu", "--share-gpu", "--only", "3", "--json-out", str(out)])
+    rep = json.loads(out.read_text())
+    assert rc == 0, rep
+    r3 = rep["3"]
+    assert r3["shared_gpu"] and r3["real_gpus"] == 8 and r3["per_device_gib"] == [16] * 8
+    assert r3["resident_slices"] == [4] * 8 and r3["bad_stamps"] == 0 and r3["physical_drift"] == 0
+
+
 @pytest.mark.parametrize("agent", ["plugin", "native"])
 def test_node_agent_restart_keeps_cu_partitions_disjoint(agent):
     """Kill the device plugin / node agent while 3 CU-partitioned pods run; the restarted one rebuilds ownership
