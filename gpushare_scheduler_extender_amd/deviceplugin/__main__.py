@@ -64,6 +64,9 @@ def main(argv=None) -> int:
     ap.add_argument("--extender", default=env.get("GSX_EXTENDER_URL", ""),
                     help="the scheduler extender's URL (its POST /gpushare-scheduler/move): reconciliation moves of "
                          "allocation records go through it, the one writer of *_IDX; '' leaves records as they are")
+    ap.add_argument("--no-extender", action="store_true", default=env.get("GSX_NO_EXTENDER") == "1",
+                    help="run the PodResources reconciliation without a scheduler extender: swaps are detected and "
+                         "the physical guard holds, but no allocation record can be repaired (tests / diagnosis)")
     ap.add_argument("--reconcile-interval", type=float, default=float(env.get("GSX_RECONCILE_INTERVAL", "2")))
     ap.add_argument("--log-level", default=env.get("LOG_LEVEL", "info"))
     ap.add_argument("--log-dir", default=env.get("GSX_LOG_DIR", ""))
@@ -71,6 +74,12 @@ def main(argv=None) -> int:
     setup_logging(a.log_level, a.log_dir or None, "gpushare-device-plugin")
     if not a.node:
         ap.error("--node / NODE_NAME is required")
+    if a.podresources_socket and not a.extender and not a.no_extender:
+        # every repair of an allocation record goes through the extender (the one writer of *_IDX): without it the
+        # reconciliation could only watch swaps it cannot fix, and the physical guard would fail the pods they hit
+        ap.error("the PodResources reconciliation (--podresources-socket) needs the scheduler extender's URL "
+                 "(--extender / GSX_EXTENDER_URL, e.g. http://gpushare-schd-extender.kube-system.svc:12345); "
+                 "pass --podresources-socket '' to run without reconciliation, or --no-extender to run it unrepaired")
 
     async def run():
         backend, devs = discover(a.backend)
@@ -85,7 +94,8 @@ def main(argv=None) -> int:
                                 health_interval=a.health_interval, reserve_bytes=int(a.reserve_gib * (1 << 30)),
                                 podresources_socket=a.podresources_socket or None,
                                 reconcile_interval=a.reconcile_interval, isolation=iso, extender=a.extender or None)
-        await plugin.start(publish=not a.no_publish, register=not a.no_register)
+        # the debug endpoint first: its setup (importing aiohttp) blocks the loop for a few hundred ms, and once the
+        # plugin serves, kubelet's Allocates must find the reconciliation (this loop) running
         if a.debug_port or a.debug_port_file:
             port = await plugin.serve_debug(a.debug_host, a.debug_port)
             if a.debug_port_file:
@@ -93,6 +103,7 @@ def main(argv=None) -> int:
                     f.write(str(port))
                 os.replace(a.debug_port_file + ".tmp", a.debug_port_file)
             logging.getLogger("gsx.main").info("debug endpoints on %s:%d", a.debug_host, port)
+        await plugin.start(publish=not a.no_publish, register=not a.no_register)
         stop = asyncio.Event()
         loop = asyncio.get_running_loop()
         for s in (signal.SIGINT, signal.SIGTERM):

@@ -65,6 +65,9 @@ def fake_ids(dev: Device, units: int) -> list[str]:
 
 ALLOCATE_ATTEMPTS = 8  # per container request: transient apiserver failures retried with capped backoff
 INFORMER_WAIT_S = 0.02  # how long an Allocate waits for the pod event before LISTing
+PHYSICAL_TTL_S = 60.0  # the extender drops a physical-use publication this plugin stopped refreshing
+PHYSICAL_REFRESH_S = 15.0
+SA_TOKEN_FILE = "/var/run/secrets/kubernetes.io/serviceaccount/token"
 GUARD_WAIT_S = 5.0  # how long an Allocate waits for a physically full GPU to drain a stopping container
 POD_ANNOTATION = "gpushare.amd.com/pod"  # container annotation: the pod this Allocate was matched to
 
@@ -175,6 +178,9 @@ class GpuSharePlugin:
         self.timing = {"n": 0, "match": 0.0, "assign_patch": 0.0, "isolate": 0.0, "handler": 0.0,
                        "preferred_n": 0, "preferred": 0.0}
         self._aid = 0
+        self._tok = None  # (file stamp, service-account token) for the extender's endpoints
+        self._phys_published: list | None = None  # the unaccounted use last published to the extender (None: none)
+        self._phys_at = 0.0
         self.reconciler = None
         if podresources_socket:
             from .reconcile import Reconciler  # noqa: PLC0415
@@ -347,8 +353,9 @@ class GpuSharePlugin:
         if srv is None:
             return
         pending, events = srv.poll()
-        for ev in events:
-            self._fast_allocated(ev)
+        served = [ev["uid"] for ev in events if self._fast_allocated(ev)]
+        if served and self.reconciler is not None:
+            self.reconciler.kick(fast=self._ambiguous(served))
         self.state.flush_dropped()  # records the native pod feed dropped with their pods: isolation cleanup
         if pending:
             loop = asyncio.get_running_loop()
@@ -365,7 +372,7 @@ class GpuSharePlugin:
         if ev.get("patch_only"):  # early answer: the commit of an Allocate answered before has landed
             if ev["pod_json"] and not native_views:
                 self.state.observe(json.loads(ev["pod_json"]))
-            return
+            return False
         if ev["pod_json"] and not native_views:
             self.state.observe(json.loads(ev["pod_json"]))  # the committed pod, before its watch event arrives
         if ev["iso"] and self.isolation is not None:
@@ -379,8 +386,25 @@ class GpuSharePlugin:
         t["assign_patch"] += ev["t_patch"]
         t["isolate"] += ev["t_isolate"]
         self.persist_records()
-        if self.reconciler is not None:
-            self.reconciler.kick()
+        return True
+
+    def _ambiguous(self, uids) -> bool:
+        """kubelet may have admitted another pod than the one these Allocates were matched to: a pending pod of the
+        same size waits for another GPU (a kubelet admission batch can serve the two each other's allocations).
+        Then the reconciliation looks at once, so a swap is known -- and the extender told what the containers
+        hold -- before either pod can be deleted.  One GPU: never (every allocation of a size is the same)."""
+        if len(self.units) < 2:
+            return False
+        spread: dict[int, set] = {}
+        for p in self.state.candidates():
+            spread.setdefault(p.request, set()).add(p.dev)
+        pods = self.state.pods
+        for u in uids:
+            p = pods.get(u)
+            if p is not None and spread.get(p.request, set()) - {p.dev}:
+                self.stats["ambiguous_allocates"] = self.stats.get("ambiguous_allocates", 0) + 1
+                return True
+        return False
 
     async def _native_slow(self, srv, cid: int, method: str, payload: bytes):
         """A call the native fast path left to Python: the same handler grpcio would run."""
@@ -823,18 +847,13 @@ class GpuSharePlugin:
         if not self.extender_url:
             raise ApiError(409, "Conflict", "no scheduler extender configured (--extender / GSX_EXTENDER_URL): "
                                             "allocation records are written by the extender only")
-        if self._ext is None:
-            from ..k8s.fasthttp import Client as HttpClient  # noqa: PLC0415
-
-            self._ext = HttpClient(self.extender_url)
+        # the pod's container already runs on `to` (it holds an allocation there): the extender's physical account
+        # (the use this plugin publishes) has it, only the annotations grow
+        physical_on_to = any(r.owner == rec.uid and r.dev == int(to) for r in self.state.records.values())
         body = {"namespace": rec.namespace, "name": rec.name, "uid": rec.uid, "node": self.node,
                 "resourceVersion": rec.rv, "from": rec.dev, "to": int(to), "partner": partner,
-                "annotations": annotations}
-        try:
-            r = await self._ext.request("POST", "/gpushare-scheduler/move", json.dumps(body).encode(),
-                                        content_type="application/json")
-        except OSError as e:
-            raise ApiError(503, "ServiceUnavailable", f"scheduler extender: {e}") from e
+                "physical_on_to": physical_on_to, "annotations": annotations}
+        r = await self._extender_post("/gpushare-scheduler/move", body)
         try:
             out = json.loads(r.body or b"{}")
         except ValueError:
@@ -844,6 +863,87 @@ class GpuSharePlugin:
             raise ApiError(r.status, "Conflict" if r.status == 409 else "", out.get("Error") or r.body[:200])
         self.stats["moves"] = self.stats.get("moves", 0) + 1
         return out["pod"]
+
+    async def _extender_post(self, path: str, body: dict):
+        """POST to the scheduler extender's device-plugin endpoints, with this plugin's service-account token when
+        it has one (the extender reviews it: ``--plugin-auth tokenreview``).  Raises ApiError(503) on transport."""
+        import json  # noqa: PLC0415
+
+        if self._ext is None:
+            from ..k8s.fasthttp import Client as HttpClient  # noqa: PLC0415
+
+            self._ext = HttpClient(self.extender_url)
+        headers = None
+        tok = self._extender_token()
+        if tok:
+            headers = {"Authorization": f"Bearer {tok}"}
+        try:
+            return await self._ext.request("POST", path, json.dumps(body).encode(), content_type="application/json",
+                                           headers=headers)
+        except OSError as e:
+            raise ApiError(503, "ServiceUnavailable", f"scheduler extender: {e}") from e
+
+    def _extender_token(self) -> str:
+        """The plugin's service-account token (re-read when the kubelet rotates the projected file)."""
+        path = os.environ.get("GSX_PLUGIN_TOKEN_FILE", SA_TOKEN_FILE)
+        try:
+            st = os.stat(path)
+        except OSError:
+            return ""
+        if self._tok is None or self._tok[0] != (st.st_mtime_ns, st.st_size):
+            try:
+                with open(path) as f:
+                    self._tok = ((st.st_mtime_ns, st.st_size), f.read().strip())
+            except OSError:
+                return ""
+        return self._tok[1]
+
+    # ------------------------------------------------------------ physical use -> the extender
+    def unaccounted(self) -> list[int] | None:
+        """Per GPU, the units kubelet's containers hold there that the annotations do not charge there: a record
+        whose holder (kubelet's report, else the pod it was built for) is annotated with another GPU, or is gone.
+        None when every container is charged where it runs (the extender then uses the annotations alone)."""
+        if not self.units:
+            return None
+        pods = self.state.pods
+        out = [0] * (max(self.units) + 1)
+        found = False
+        for r in self.state.records.values():
+            if not 0 <= r.dev < len(out):
+                continue
+            h = r.owner or r.uid
+            p = pods.get(h) if h and not h.startswith("~") else None
+            if p is None or p.complete or p.dev != r.dev:
+                out[r.dev] += r.units
+                found = True
+        return out if found else None
+
+    async def publish_physical(self, force: bool = False) -> bool:
+        """Tell the extender what kubelet's containers hold where the annotations do not charge it
+        (``unaccounted``), and withdraw it once they do: the extender charges it on top of the annotations, so a
+        deleted pod whose allocation another pod's container holds (a kubelet batch swap not yet repaired) never
+        frees that GPU for the next bind.  Refreshed while it lasts (the extender expires an unrefreshed
+        publication).  False if the extender could not be told."""
+        if not self.extender_url or not self.units:
+            return True
+        extra = self.unaccounted()
+        now = time.monotonic()
+        due = extra is not None and now - self._phys_at > PHYSICAL_REFRESH_S
+        if not force and not due and extra == self._phys_published:
+            return True
+        try:
+            r = await self._extender_post("/gpushare-scheduler/physical",
+                                          {"node": self.node, "unaccounted": extra, "ttl": int(PHYSICAL_TTL_S)})
+        except ApiError as e:
+            log.warning("publishing the unaccounted GPU use to the extender failed: %s", e)
+            return False
+        if r.status != 200:
+            log.warning("the extender refused the unaccounted GPU use: %s %s", r.status, r.body[:200])
+            return False
+        self._phys_published, self._phys_at = extra, now
+        self.stats["physical_published"] = self.stats.get("physical_published", 0) + 1
+        log.debug("published unaccounted GPU use %s", extra)
+        return True
 
     async def _wait_for_annotations(self, units: int, timeout: float = 10.0):
         """A pod of this size is bound to the node but carries no allocation record yet: the extender is writing
@@ -891,7 +991,7 @@ class GpuSharePlugin:
                     c.mounts.add(**m)
             self.stats["allocate_ok"] += 1
             if self.reconciler is not None:
-                self.reconciler.kick()
+                self.reconciler.kick(fast=self._ambiguous([rec.uid]))
             self.timing["n"] += 1
             self.timing["handler"] += time.perf_counter() - t0
             return resp

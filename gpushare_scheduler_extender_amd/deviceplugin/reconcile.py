@@ -85,6 +85,10 @@ class Reconciler:
                       "made_room": 0, "stand_in_partners": 0,
                       "drift_repaired": 0}
         self._orphan_since: dict[str, float] = {}
+        # after an ambiguous Allocate (kubelet records an Allocate's IDs before it returns to its admission loop;
+        # a pass skips records made after it asked, so a short delay only saves passes)
+        self.after_ambiguous = 0.002
+        self._fast = False
         self._kick = asyncio.Event()
         self._task: asyncio.Task | None = None
         self._lock = asyncio.Lock()
@@ -93,8 +97,11 @@ class Reconciler:
     def state(self):
         return self.plugin.state
 
-    def kick(self):
-        """An Allocate returned: kubelet records its IDs right after; look soon."""
+    def kick(self, fast: bool = False):
+        """An Allocate returned: kubelet records its IDs right after; look soon.  ``fast``: the Allocate may have been
+        served to another pod than the one it was matched to (``GpuSharePlugin._ambiguous``): look at once."""
+        if fast:
+            self._fast = True
         self._kick.set()
 
     # ------------------------------------------------------------ one pass
@@ -150,6 +157,10 @@ class Reconciler:
                         drifts.append((pod.uid, got or _Held(pod.uid, r.dev, r.cu_mask)))
             done = 0
             started = {f"{ns}/{name}" for ns, name in truth}
+            # before any repair: the extender learns what the containers physically hold (a swap just found, a
+            # pod deleted before its record's holder was known), so no bind lands on a GPU the annotations
+            # under-count while the exchanges below are in flight
+            await self.plugin.publish_physical()
             await self._finish_holds()
             for p_uid, aid in moves:
                 r = self.state.records.get(aid)
@@ -177,6 +188,7 @@ class Reconciler:
                     done += 1
             await self._finish_holds()
             await self._reset_orphans(started, 0.0 if urgent else self.stale_after)
+            await self.plugin.publish_physical()  # withdrawn once the records and the annotations agree
             if done:
                 self.plugin.persist_records()
             return {"moves": done, "pods": len(truth)}
@@ -239,6 +251,7 @@ class Reconciler:
         except ApiError as e:
             if e.conflict or e.not_found:
                 self.stats["conflicts"] += 1
+                log.info("write of %s refused: %s", p.key, e)
                 return False
             raise
         self.state.observe(pod)
@@ -326,12 +339,30 @@ class Reconciler:
         return min(cands, key=lambda q: q.order) if cands else None
 
     def _stand_in_partner(self, dev: int, p: PodRec, started: set) -> PodRec | None:
+        """An unstarted pod Q the extender has placed on ``dev`` (where P's container runs) to exchange GPUs with P:
+        Q takes P's annotated GPU, which P's container never used.  Equal-size first (the exchange keeps every
+        GPU's sum); else the largest Q with which both GPUs fit after the exchange -- P's phantom share on its
+        annotated GPU is exactly the room Q needs there, and the extender checks the same final state."""
         recs = self.state.records.values()
         taken = {r.holder for r in recs} | {r.uid for r in recs} | self.busy()
         cands = [q for q in self.state.pods.values()
-                 if q.dev == dev and q.request == p.request and q.uid != p.uid and not q.complete
+                 if q.dev == dev and q.uid != p.uid and not q.complete and q.request > 0
                  and q.key not in started and q.uid not in taken and q.uid not in self.state.inflight]
-        return min(cands, key=lambda q: q.order) if cands else None
+        same = [q for q in cands if q.request == p.request]
+        if same:
+            return min(same, key=lambda q: q.order)
+        if p.dev < 0 or p.dev == dev:
+            return None
+        plugin = self.plugin
+        cap_to, cap_from = plugin.units.get(dev, 0), plugin.units.get(p.dev, 0)
+        used_to, used_from = plugin._annotated_used(dev), plugin._annotated_used(p.dev)
+        fits = [q for q in cands
+                if used_to - q.request + p.request <= cap_to and used_from - p.request + q.request <= cap_from
+                and plugin._physical_used(p.dev) + q.request <= cap_from]
+        if not fits:
+            return None
+        self.stats["unequal_partners"] = self.stats.get("unequal_partners", 0) + 1
+        return min(fits, key=lambda q: (-q.request, q.order))
 
     async def _make_room(self, dev: int, p: PodRec, started: set) -> None:
         """P is about to be annotated with GPU ``dev`` alone (the pod the allocation was built for is gone -- and
@@ -405,10 +436,12 @@ class Reconciler:
         while True:
             try:
                 await asyncio.wait_for(self._kick.wait(), self.interval)
-                await asyncio.sleep(self.after_allocate)  # let kubelet record the allocation first
+                # let kubelet record the allocation first
+                await asyncio.sleep(self.after_ambiguous if self._fast else self.after_allocate)
             except asyncio.TimeoutError:
                 pass
             self._kick.clear()
+            self._fast = False
             if not self.pr.available():
                 self.state.core.set_owners_reported(False)  # nobody will report owners: drop records by pod
                 continue

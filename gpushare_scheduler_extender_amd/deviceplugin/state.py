@@ -416,7 +416,12 @@ class AllocationState:
         self.core.set_owner(aid, uid)
 
     def pod_by_key(self, key: str) -> PodRec | None:
-        for r in self.pods.values():
+        """ns/name -> pod: one lookup in the native key index (the reconciliation asks for every pod kubelet
+        reports; walking every pod's view per question made a pass O(P^2) copies under the state lock)."""
+        if self._native_pods is not None:
+            uid = self.core.uid_for_key(key)
+            return self._native_pods.get(uid) if uid else None
+        for r in self._recs.values():
             if r.key == key:
                 return r
         return None

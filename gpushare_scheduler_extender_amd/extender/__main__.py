@@ -63,6 +63,13 @@ def parse_args(argv=None):
                     help="1: serve /debug/pprof/* on the API port, as the reference (default); 0: off (the port is "
                          "hostNetwork / NodePort, and profiles cost CPU)")
     ap.add_argument("--port-file", default="", help="write the bound port to this file once serving")
+    ap.add_argument("--plugin-auth", default=env.get("GSX_PLUGIN_AUTH", "none"), choices=["none", "tokenreview"],
+                    help="who may call the device plugin's endpoints (POST /gpushare-scheduler/move, /physical): "
+                         "anyone who reaches the port (none), or a bearer token the apiserver's TokenReview "
+                         "authenticates as one of --plugin-users (tokenreview; the shipped manifests)")
+    ap.add_argument("--plugin-users", default=env.get(
+        "GSX_PLUGIN_USERS", "system:serviceaccount:kube-system:gpushare-device-plugin"),
+                    help="comma-separated usernames allowed with --plugin-auth tokenreview")
     return ap.parse_args(argv)
 
 
@@ -79,7 +86,8 @@ def main(argv=None) -> int:
                              leader_elect=bool(a.leader_elect), lease_name=a.lease_name,
                              lease_namespace=a.lease_namespace, pprof=bool(a.pprof), bind_order=a.bind_order)
         runner = await ExtenderRunner(srv, a.host, a.port, http_threads=a.http_threads,
-                                      pool_threads=max(a.bind_threads, a.threadness)).start()
+                                      pool_threads=max(a.bind_threads, a.threadness), plugin_auth=a.plugin_auth,
+                                      plugin_users=[u for u in a.plugin_users.split(",") if u]).start()
         if a.port_file:
             with open(a.port_file + ".tmp", "w") as f:
                 f.write(str(runner.port))

@@ -222,8 +222,12 @@ class ExtenderRunner:
     """
 
     def __init__(self, server: ExtenderServer, host: str = "127.0.0.1", port: int = 0, *, http_threads: int = 2,
-                 pool_threads: int = 16):
+                 pool_threads: int = 16, plugin_auth: str = "none", plugin_users: list[str] | None = None):
         self.server = server
+        # the device plugin's endpoints (/move, /physical): "tokenreview" = only a bearer token the apiserver
+        # authenticates as one of plugin_users (the plugin's service account)
+        self.plugin_auth = plugin_auth
+        self.plugin_users = list(plugin_users or [])
         self.host = host
         self.port = port
         self.http_threads = http_threads
@@ -247,7 +251,8 @@ class ExtenderRunner:
         self.port = self.server.engine.serve(self.host, self.port, self.http_threads, self.pool_threads,
                                              self.internal_port, self.server.reservation_ttl, api_dict(client.config),
                                              update_mode=self.server.bind_mode == "update",
-                                             qps=float(client.limiter.qps), burst=int(client.limiter.burst))
+                                             qps=float(client.limiter.qps), burst=int(client.limiter.burst),
+                                             plugin_auth=self.plugin_auth, plugin_users=self.plugin_users)
         self.server.native_server = True
         self._drain = asyncio.get_running_loop().create_task(self._drain_failures())
         return self

@@ -473,6 +473,8 @@ async def _spawn_plugin(a, sock_dir: str, devs: list[Device], prsock: str | None
            "--debug-port-file", port_file, "--log-level", "warning"]
     if a.isolation_dir:
         cmd += ["--isolation-dir", a.isolation_dir]
+    if not os.environ.get("GSX_EXTENDER_URL"):
+        cmd.append("--no-extender")  # a harness run without an extender: reconciliation detects, cannot repair
     if a.apiserver:
         cmd += ["--apiserver", a.apiserver]
     if a.kubeconfig:

@@ -292,6 +292,11 @@ class Engine {
     return l_.node_devices(node);
   }
 
+  std::vector<int64_t> node_unaccounted(const std::string& node) {
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
+    return l_.node_unaccounted(node);
+  }
+
   std::vector<std::string> node_names() {
     std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.node_names();
@@ -318,6 +323,9 @@ class Engine {
     d["annotations_missing"] = s.annotations_missing;
     d["moves_ok"] = s.moves_ok;
     d["moves_refused"] = s.moves_refused;
+    d["partner_claims_refused"] = s.partner_claims_refused;
+    d["unaccounted_updates"] = s.unaccounted_updates;
+    d["unaccounted_expired"] = s.unaccounted_expired;
     d["moves_failed"] = s.moves_failed;
     d["overcommit_events"] = s.overcommit_events;
     d["pod_upserts"] = s.pod_upserts;
@@ -331,7 +339,8 @@ class Engine {
 
   // ---- native HTTP front end (server.h) ----
   int serve(const std::string& host, int port, int threads, int pool_threads, int fallback_port, double ttl,
-            const py::dict& api, bool update_mode, double qps, int burst) {
+            const py::dict& api, bool update_mode, double qps, int burst, const std::string& plugin_auth,
+            const std::vector<std::string>& plugin_users) {
     if (srv_) throw std::runtime_error("native server already running");
     ServerConfig cfg;
     cfg.host = host;
@@ -344,6 +353,9 @@ class Engine {
     cfg.qps = qps;
     cfg.burst = burst;
     cfg.api = api_from(api);
+    if (plugin_auth != "none" && plugin_auth != "tokenreview") throw std::invalid_argument("plugin_auth: none|tokenreview");
+    cfg.plugin_auth = plugin_auth;
+    cfg.plugin_users = plugin_users;
     srv_.reset(new NativeServer(&l_, cfg));
     // the controller outlives the server (stop_server runs before stop_controller)
     srv_->set_lister([this](const std::string& key, std::string* raw) { return ctl_ && ctl_->get_pod(key, raw); });
@@ -460,6 +472,9 @@ class Engine {
     d["live_gets"] = s.live_gets.load();
     d["qps_waits"] = s.qps_waits.load();
     d["moves_failed"] = s.moves_failed.load();
+    d["physical_posts"] = s.physical_posts.load();
+    d["plugin_auth_denied"] = s.plugin_auth_denied.load();
+    d["token_reviews"] = s.token_reviews.load();
     auto hist = [](const LatencyHist& h) {
       py::dict o;
       py::list bounds, counts;
@@ -1587,7 +1602,9 @@ PYBIND11_MODULE(_engine, m) {
       .def("parse_pod", &Engine::parse_pod)
       .def("serve", &Engine::serve, py::arg("host"), py::arg("port"), py::arg("threads") = 2,
            py::arg("pool_threads") = 16, py::arg("fallback_port") = 0, py::arg("ttl") = 60.0,
-           py::arg("api") = py::dict(), py::arg("update_mode") = false, py::arg("qps") = 0.0, py::arg("burst") = 10)
+           py::arg("api") = py::dict(), py::arg("update_mode") = false, py::arg("qps") = 0.0, py::arg("burst") = 10,
+           py::arg("plugin_auth") = "none", py::arg("plugin_users") = std::vector<std::string>())
+      .def("node_unaccounted", [](Engine& e, const std::string& node) { return e.node_unaccounted(node); })
       .def("stop_server", &Engine::stop_server)
       .def("start_controller", &Engine::start_controller, py::arg("api"), py::arg("resync") = 30.0,
            py::arg("sync_timeout") = 60.0, py::arg("watch_timeout") = 300)
@@ -1730,6 +1747,11 @@ PYBIND11_MODULE(_engine, m) {
       }, py::call_guard<AllocLock>())
       .def("holders", &AllocState::holders, py::call_guard<AllocLock>())
       .def("has_pod", [](const AllocState& s, const std::string& uid) { return s.pod(uid) != nullptr; }, py::call_guard<AllocLock>())
+      // ns/name -> uid through the state's key index (the reconciliation looks up every pod kubelet reports)
+      .def("uid_for_key", [](const AllocState& s, const std::string& key) -> std::string {
+        const AllocPod* p = s.pod_by_key(key);
+        return p ? p->uid : std::string();
+      }, py::call_guard<AllocLock>())
       // the native state's view of a pod (the one the matcher decided on): the fields an Allocate acts on
       .def("pod_view", [](const AllocState& s, const std::string& uid) -> py::object {
              const AllocPod* p = s.pod(uid);

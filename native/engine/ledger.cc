@@ -20,7 +20,10 @@ void Ledger::account(PodRec& r) {
   if (d.used > d.total) stats_.overcommit_events++;
   // a pod being moved between devices is charged on both until the move completes: never under-counted
   r.held_on = (r.hold >= 0 && r.hold != r.dev && r.hold < static_cast<int64_t>(n.devs.size())) ? r.hold : -1;
-  if (r.held_on >= 0) n.devs[static_cast<size_t>(r.held_on)].used += r.mem;
+  if (r.held_on >= 0) {
+    n.devs[static_cast<size_t>(r.held_on)].used += r.mem;
+    n.devs[static_cast<size_t>(r.held_on)].held += r.mem;
+  }
   r.moved_on = (r.move_to >= 0 && r.move_to != r.dev && r.move_to != r.held_on &&
                 r.move_to < static_cast<int64_t>(n.devs.size()))
                    ? r.move_to
@@ -39,7 +42,10 @@ void Ledger::unaccount(PodRec& r) {
   DevState& d = n.devs[static_cast<size_t>(r.dev)];
   d.used -= r.mem;
   d.npods -= 1;
-  if (r.held_on >= 0 && r.held_on < static_cast<int64_t>(n.devs.size())) n.devs[static_cast<size_t>(r.held_on)].used -= r.mem;
+  if (r.held_on >= 0 && r.held_on < static_cast<int64_t>(n.devs.size())) {
+    n.devs[static_cast<size_t>(r.held_on)].used -= r.mem;
+    n.devs[static_cast<size_t>(r.held_on)].held -= r.mem;
+  }
   r.held_on = -1;
   if (r.moved_on >= 0 && r.moved_on < static_cast<int64_t>(n.devs.size())) {
     n.devs[static_cast<size_t>(r.moved_on)].used -= r.mem;
@@ -203,8 +209,8 @@ Check Ledger::check(const std::string& node, int64_t req) const {
   if (it == nodes_.end()) return Check::NodeNotFound;
   const NodeState& n = it->second;
   if (!n.gpushare()) return Check::NotGPUShare;
-  for (const DevState& d : n.devs) {
-    if (d.total - d.used >= req) return Check::Ok;
+  for (size_t i = 0; i < n.devs.size(); ++i) {
+    if (n.free_of(i) >= req) return Check::Ok;
   }
   return Check::Insufficient;
 }
@@ -240,7 +246,7 @@ int64_t Ledger::assume(const std::string& uid, const std::string& ns, const std:
   int64_t cand = -1;
   int64_t cand_free = 0;
   for (size_t i = 0; i < n.devs.size(); ++i) {
-    int64_t free = n.devs[i].total - n.devs[i].used;
+    int64_t free = n.free_of(i);
     if (free >= req && (cand < 0 || free < cand_free)) {
       cand = static_cast<int64_t>(i);
       cand_free = free;
@@ -403,7 +409,7 @@ int Ledger::begin_move(MoveRequest* m, std::string* why) {
   if (m->to < 0) {  // best fit among the other devices (nodeinfo.go:209-252)
     int64_t best = -1, best_free = 0;
     for (int64_t i = 0; i < ndev; ++i) {
-      const int64_t free = n.devs[static_cast<size_t>(i)].total - n.devs[static_cast<size_t>(i)].used;
+      const int64_t free = n.free_of(static_cast<size_t>(i));
       if (i != m->from && free >= r.mem && (best < 0 || free < best_free)) {
         best = i;
         best_free = free;
@@ -417,16 +423,44 @@ int Ledger::begin_move(MoveRequest* m, std::string* why) {
     return 3;
   }
   if (m->to != r.dev) {
-    bool neutral = false;
+    // An exchange with a partner the ledger can verify:
+    //  step 1 -- Q is on `to`, and this write charges the pod on `from` too (hold-idx = from) and names Q as
+    //            the hold's partner: Q will take `from` in step 2;
+    //  step 2 -- Q (the partner named here) already took this pod's GPU and holds `to` until this lands (or, before
+    //            the informer has seen step 1 land, Q is still on `to` with its move to this pod's GPU charged).
+    // An exchange only relabels who runs where, so it is checked on `to`'s final annotation sum (the holds on
+    // `to` go, a partner still on `to` leaves) and never refused when it adds no load there (the reference's
+    // equal-size exchange).  Any other move also counts the device plugin's unaccounted use.
+    const DevState& d = n.devs[static_cast<size_t>(m->to)];
+    const size_t ti = static_cast<size_t>(m->to);
+    bool exchange = false;
+    int64_t partner_mem = 0, leaving = 0;
     if (!m->partner.empty() && m->partner != m->uid) {
       auto q = pods_.find(m->partner);
-      neutral = q != pods_.end() && q->second.node == r.node && q->second.mem == r.mem &&
-                (q->second.dev == m->to || q->second.hold == m->to);
+      if (q != pods_.end() && q->second.node == r.node && !q->second.terminal) {
+        const PodRec& Q = q->second;
+        const bool step1 = Q.dev == m->to && m->req_hold == r.dev && m->req_hold_partner == m->partner;
+        const bool step2_seen = Q.hold == m->to && Q.dev == r.dev;
+        const bool step2_early = Q.dev == m->to && Q.move_to == r.dev;
+        exchange = step1 || step2_seen || step2_early;
+        partner_mem = Q.mem;
+        leaving = (step1 || step2_early) ? Q.mem : 0;  // step 2 seen: Q's charge on `to` is its hold (in `held`)
+      }
+      if (!exchange) stats_.partner_claims_refused++;
     }
-    const DevState& d = n.devs[static_cast<size_t>(m->to)];
-    if (!neutral && d.total - d.used < r.mem) {
-      *why = "GPU " + std::to_string(m->to) + " of node " + m->node + " has " + std::to_string(d.total - d.used) +
-             " free, the pod needs " + std::to_string(r.mem);
+    bool fits;
+    if (exchange) {
+      fits = r.mem <= partner_mem || d.used - d.held - leaving + r.mem <= d.total;
+    } else {
+      // after the move: the annotations gain the pod; if its container already runs there, its share leaves the
+      // unaccounted use it was part of
+      const int64_t ex = ti < n.extra.size() ? n.extra[ti] : 0;
+      fits = d.used + r.mem + (m->physical_on_to ? std::max<int64_t>(0, ex - r.mem) : ex) <= d.total;
+    }
+    if (!fits) {
+      *why = "GPU " + std::to_string(m->to) + " of node " + m->node + " has " + std::to_string(n.free_of(ti)) +
+             " free" + (exchange ? " (" + std::to_string(leaving) + " leaving)" : std::string()) +
+             ", the pod needs " + std::to_string(r.mem);
       stats_.moves_refused++;
       return 3;
     }
@@ -482,6 +516,13 @@ int Ledger::gc(double confirmed_list_start, bool* need_relist) {
   double now = now_s();
   int n = 0;
   bool relist = false;
+  for (auto& kv : nodes_) {
+    // an unaccounted-use publication its device plugin stopped refreshing (the plugin is gone): annotations only
+    if (!kv.second.extra.empty() && kv.second.extra_until < now) {
+      kv.second.extra.clear();
+      stats_.unaccounted_expired++;
+    }
+  }
   for (auto& kv : pods_) {
     // a move the informer never confirmed (the pod's record was rewritten again since): its target charge goes
     PodRec& r = kv.second;
@@ -521,6 +562,20 @@ int Ledger::gc(double confirmed_list_start, bool* need_relist) {
 }
 
 // ---------------------------------------------------------------- inspect
+
+bool Ledger::set_unaccounted(const std::string& node, const std::vector<int64_t>& extra, double ttl_s) {
+  auto it = nodes_.find(node);
+  if (it == nodes_.end()) return false;
+  it->second.extra = extra;
+  it->second.extra_until = extra.empty() ? 0 : now_s() + ttl_s;
+  stats_.unaccounted_updates++;
+  return true;
+}
+
+std::vector<int64_t> Ledger::node_unaccounted(const std::string& node) const {
+  auto it = nodes_.find(node);
+  return it == nodes_.end() ? std::vector<int64_t>() : it->second.extra;
+}
 
 std::vector<std::pair<int64_t, int64_t>> Ledger::node_devices(const std::string& node) const {
   std::vector<std::pair<int64_t, int64_t>> out;
@@ -834,8 +889,9 @@ std::string prioritize_body(Ledger& l, std::string_view body) {
     const NodeState* n = l.node(names[k]);
     if (n && n->gpushare() && req > 0) {
       int64_t best = -1, best_total = 1;
-      for (const DevState& dv : n->devs) {
-        int64_t left = dv.total - dv.used - req;
+      for (size_t di = 0; di < n->devs.size(); ++di) {
+        const DevState& dv = n->devs[di];
+        int64_t left = n->free_of(di) - req;
         if (left >= 0 && (best < 0 || left < best)) {
           best = left;
           best_total = dv.total > 0 ? dv.total : 1;

@@ -70,7 +70,16 @@ struct MoveRequest {
   std::string uid, node;
   int64_t from = -1;       // the device the caller's view has the pod on (the ledger must agree)
   int64_t to = -1;         // the new *_IDX (-1: best fit with room, other than `from`)
-  std::string partner;     // an equal-size exchange partner on `to` (or holding `to`): the move is sum-neutral
+  // the exchange partner: the pod on `to` that this move's hold swaps with (step 1: the request carries
+  // hold-idx = `from` and a hold-partner naming it), or the pod holding `to` that took this pod's GPU (step 2).  A
+  // verified partner's share is credited on `to` (it leaves `to`), so an exchange of two sizes is checked on the
+  // final state of both GPUs, not refused for the room the partner still occupies
+  std::string partner;
+  // the pod's container already runs on `to` (a drift repair, or taking over the allocation it holds there): the
+  // device plugin's published unaccounted use on `to` includes it, and moves into the annotations
+  bool physical_on_to = false;
+  int64_t req_hold = -1;        // hold-idx the move request writes (-1: none)
+  std::string req_hold_partner; // uid named by the hold-partner the move request writes
 };
 
 // A pod this extender bound whose allocation annotations the apiserver did not keep (an apiserver or
@@ -84,6 +93,7 @@ struct DevState {
   int64_t total = 0;
   int64_t used = 0;
   int64_t npods = 0;
+  int64_t held = 0;  // the part of `used` charged by exchange holds (pods leaving this device once the hold clears)
 };
 
 struct NodeState {
@@ -95,7 +105,16 @@ struct NodeState {
   std::vector<DevState> devs;
   std::unordered_set<std::string> pods;  // uids whose rec.node == name
   bool landing_order = false;            // NodeView::landing_order
+  // the device plugin's unaccounted use (POST /gpushare-scheduler/physical): units kubelet's containers hold on a
+  // device whose pods the annotations put elsewhere, or that are gone -- a kubelet admission batch served two pods
+  // each other's allocations and the exchange of their records has not landed, or the pod an allocation was built
+  // for was deleted while another pod's container holds it.  Charged on top of the annotations, so such a device
+  // takes no bind into room its containers already fill.  Empty: none published (or expired, extra_until)
+  std::vector<int64_t> extra;
+  double extra_until = 0;
   bool gpushare() const { return total > 0 && count > 0; }
+  int64_t used_eff(size_t i) const { return devs[i].used + (i < extra.size() ? extra[i] : 0); }
+  int64_t free_of(size_t i) const { return devs[i].total - used_eff(i); }
 };
 
 struct Stats {
@@ -105,6 +124,8 @@ struct Stats {
   uint64_t expiry_deferred = 0;  // GC passes that kept an overdue reservation until a LIST could confirm it
   uint64_t annotations_missing = 0;  // binds observed bound without the annotations they carried
   uint64_t moves_ok = 0, moves_refused = 0, moves_failed = 0;  // device-plugin allocation-record writes
+  uint64_t partner_claims_refused = 0;
+  uint64_t unaccounted_updates = 0, unaccounted_expired = 0;  // the device plugin's unaccounted-use publications  // a move naming a partner the ledger does not show in an exchange with it
 };
 
 class Ledger {
@@ -189,6 +210,9 @@ class Ledger {
   // ---- observation ----
   std::string inspect_json(const std::string& node, bool* found) const;
   std::vector<std::pair<int64_t, int64_t>> node_devices(const std::string& node) const;
+  // the device plugin's unaccounted use per device of `node` (empty: withdraw), valid for ttl_s; false: unknown node
+  bool set_unaccounted(const std::string& node, const std::vector<int64_t>& extra, double ttl_s);
+  std::vector<int64_t> node_unaccounted(const std::string& node) const;
   std::vector<std::string> node_names() const;
   Stats stats() const { return stats_; }
   Stats& mutable_stats() { return stats_; }

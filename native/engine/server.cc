@@ -1,4 +1,5 @@
 #include "server.h"
+#include "quantity.h"
 #include "introspect.h"
 
 #include <arpa/inet.h>
@@ -37,6 +38,11 @@ constexpr uint64_t kListenId = 1;
 constexpr uint64_t kEventId = 2;
 constexpr const char* kPrefix = "/gpushare-scheduler";
 constexpr const char* kVersion = "0.1.0";
+// the device plugin's allocation annotations a move may write besides *_IDX and ASSIGNED (models/profile.py)
+constexpr std::string_view kAnnCuMask = "gpushare.amd.com/cu-mask";
+constexpr std::string_view kAnnHoldIdx = "gpushare.amd.com/hold-idx";
+constexpr std::string_view kAnnHoldPartner = "gpushare.amd.com/hold-partner";
+constexpr std::string_view kAnnReconciled = "gpushare.amd.com/reconciled";
 
 double mono() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -479,6 +485,12 @@ void NativeServer::dispatch(Loop* lp, Conn* c, http::Message& req) {
     submit(Job{lp, c->id, 0, std::move(req), t0});
     return;
   }
+  if (req.method == "POST" && path == pre + "/physical") {
+    stats_.physical_posts.fetch_add(1, std::memory_order_relaxed);
+    c->busy = true;
+    submit(Job{lp, c->id, 3, std::move(req), t0});
+    return;
+  }
   if (req.method == "POST" && path == pre + "/move") {
     stats_.moves.fetch_add(1, std::memory_order_relaxed);
     c->busy = true;
@@ -535,8 +547,8 @@ void NativeServer::pool_main() {
       if (j.kind == 0) {
         resp = do_bind(j.req);
         stats_.bind_lat.observe(mono() - j.t0);
-      } else if (j.kind == 2) {
-        resp = do_move(j.req);
+      } else if (j.kind == 2 || j.kind == 3) {
+        if (plugin_authorized(j.req, &resp)) resp = j.kind == 2 ? do_move(j.req) : do_physical(j.req);
       } else {
         resp = do_proxy(j.req);
       }
@@ -849,12 +861,16 @@ std::string NativeServer::do_move(const http::Message& req) {
   m.uid = uid;
   m.node = node;
   m.partner = partner;
+  int64_t pi = d.find(0, "physical_on_to");
+  m.physical_on_to = pi >= 0 && d.at(static_cast<uint32_t>(pi)).type == json::T::True;
   int64_t v;
   int64_t fi = d.find(0, "from");
   int64_t ti = d.find(0, "to");
   if (fi < 0 || !d.as_int(static_cast<uint32_t>(fi), &m.from)) return answer(400, error_body("move needs from"));
   if (ti >= 0 && d.as_int(static_cast<uint32_t>(ti), &v)) m.to = v;
-  // the other allocation fields, copied as given (string values, or null to remove an annotation)
+  // the other allocation fields (string values, or null to remove an annotation): only the ones a move rewrites --
+  // ASSIGNED, the CU partition, the exchange hold and its partner, the reconciliation count.  The pod's share
+  // (POD / DEV) is fixed and its GPU is `to`; nothing else of the pod is the device plugin's to write.
   const Profile& prof = l_->profile();
   std::string extra;
   int64_t ai = d.find(0, "annotations");
@@ -867,7 +883,28 @@ std::string NativeServer::do_move(const http::Message& req) {
       if (key == prof.a_idx || key == prof.a_pod || key == prof.a_dev) {
         return answer(400, error_body("the move request names the pod's GPU in from / to, and its share is fixed"));
       }
+      if (key != prof.a_assigned && key != kAnnCuMask && key != kAnnHoldIdx && key != kAnnHoldPartner &&
+          key != kAnnReconciled) {
+        return answer(400, error_body("a move writes only " + prof.a_assigned + ", " + std::string(kAnnCuMask) + ", " +
+                                      std::string(kAnnHoldIdx) + ", " + std::string(kAnnHoldPartner) + " and " +
+                                      std::string(kAnnReconciled) + "; not " + key));
+      }
       if (t != json::T::String && t != json::T::Null) return answer(400, error_body("annotation values are strings or null"));
+      if (t == json::T::String && key == kAnnHoldIdx) {
+        int64_t hv;
+        if (parse_atoi(d.str(val), &hv) && hv >= 0) m.req_hold = hv;
+      }
+      if (t == json::T::String && key == kAnnHoldPartner) {
+        json::Doc hp;
+        std::string herr;
+        const std::string hsrc = d.str(val);  // the tape points into its source: keep it alive
+        if (hp.parse(hsrc, &herr) && hp.at(0).type == json::T::Object) {
+          int64_t ui = hp.find(0, "uid");
+          if (ui >= 0 && hp.at(static_cast<uint32_t>(ui)).type == json::T::String) {
+            m.req_hold_partner = hp.str(static_cast<uint32_t>(ui));
+          }
+        }
+      }
       extra.push_back(',');
       json::append_quoted(&extra, key);
       extra.push_back(':');
@@ -904,6 +941,95 @@ std::string NativeServer::do_move(const http::Message& req) {
   std::string out = "{\"Error\":\"\",\"to\":" + std::to_string(m.to) + ",\"pod\":";
   out.append(body).push_back('}');
   return answer(200, out);
+}
+
+bool NativeServer::plugin_authorized(const http::Message& req, std::string* resp) {
+  if (cfg_.plugin_auth != "tokenreview") return true;
+  auto deny = [&](int status, const std::string& msg) {
+    stats_.plugin_auth_denied.fetch_add(1, std::memory_order_relaxed);
+    *resp = http::response(status, "application/json", error_body(msg), true);
+    return false;
+  };
+  const std::string* h = req.header("authorization");
+  if (!h || h->size() <= 7 || h->compare(0, 7, "Bearer ") != 0) {
+    return deny(401, "the device plugin's endpoints need its service-account token (Authorization: Bearer)");
+  }
+  const std::string token = h->substr(7);
+  const double now = mono();
+  {
+    std::lock_guard<std::mutex> g(amu_);
+    auto it = authz_cache_.find(token);
+    if (it != authz_cache_.end() && it->second > now) return true;
+  }
+  if (!api_) return deny(503, "no apiserver client to review the token");
+  // TokenReview (authentication.k8s.io/v1): the apiserver says whose token it is
+  std::string body = "{\"apiVersion\":\"authentication.k8s.io/v1\",\"kind\":\"TokenReview\",\"spec\":{\"token\":";
+  json::append_quoted(&body, token);
+  body.append("}}");
+  stats_.token_reviews.fetch_add(1, std::memory_order_relaxed);
+  int status = 0;
+  std::string out, err;
+  if (!api_call("POST", "/apis/authentication.k8s.io/v1/tokenreviews", body, "application/json", &status, &out, &err) ||
+      status < 200 || status >= 300) {
+    return deny(503, "token review failed: " + (err.empty() ? std::to_string(status) : err));
+  }
+  json::Doc d;
+  std::string perr;
+  if (!d.parse(out, &perr) || d.at(0).type != json::T::Object) return deny(503, "token review: bad answer");
+  const int64_t au = d.path(0, {"status", "authenticated"});
+  const int64_t un = d.path(0, {"status", "user", "username"});
+  if (au < 0 || d.at(static_cast<uint32_t>(au)).type != json::T::True || un < 0) {
+    return deny(401, "the token is not authenticated");
+  }
+  const std::string user = d.str(static_cast<uint32_t>(un));
+  bool allowed = false;
+  for (const auto& u : cfg_.plugin_users) allowed = allowed || u == user;
+  if (!allowed) return deny(403, "user " + user + " may not write allocation records");
+  std::lock_guard<std::mutex> g(amu_);
+  if (authz_cache_.size() > 1024) authz_cache_.clear();
+  authz_cache_[token] = now + cfg_.plugin_auth_ttl;
+  return true;
+}
+
+// The device plugin's unaccounted use (deviceplugin/plugin.py publish_physical): units kubelet's containers hold on
+// each device of its node whose pods the annotations put on another device, or that are gone (a kubelet admission
+// batch served two equal-size pods each other's allocations and the exchange of their records has not landed, or
+// the pod an allocation was built for was deleted while another pod's container holds it).  The ledger charges it
+// on top of the annotations, so the deletion of a pod whose allocation another pod's container holds never frees
+// that device for the next bind.  Withdrawn (unaccounted: null) once the records agree; it expires on its own after
+// `ttl` seconds unless refreshed (a plugin that died).
+//
+//   {"node": "n", "unaccounted": [u0, u1, ...] | null, "ttl": s}  ->  200 {"Error":""} | 400 | 404
+std::string NativeServer::do_physical(const http::Message& req) {
+  auto answer = [](int status, const std::string& body) { return http::response(status, "application/json", body, true); };
+  json::Doc d;
+  std::string perr;
+  if (!d.parse(req.body, &perr) || d.at(0).type != json::T::Object) return answer(400, error_body("bad request: " + perr));
+  std::string node;
+  if (!arg_str(d, "node", &node) || node.empty()) return answer(400, error_body("physical needs node"));
+  std::vector<int64_t> used;
+  int64_t ui = d.find(0, "unaccounted");
+  if (ui >= 0 && d.at(static_cast<uint32_t>(ui)).type == json::T::Array) {
+    const uint32_t arr = static_cast<uint32_t>(ui);
+    for (uint32_t k = arr + 1; k < d.at(arr).skip; k = d.next(k)) {
+      int64_t v;
+      if (!d.as_int(k, &v) || v < 0) return answer(400, error_body("unaccounted: non-negative integers"));
+      used.push_back(v);
+    }
+  } else if (ui >= 0 && d.at(static_cast<uint32_t>(ui)).type != json::T::Null) {
+    return answer(400, error_body("unaccounted: an array or null"));
+  }
+  double ttl = 60.0;
+  int64_t ti = d.find(0, "ttl");
+  int64_t tv;
+  if (ti >= 0 && d.as_int(static_cast<uint32_t>(ti), &tv) && tv > 0) ttl = static_cast<double>(std::min<int64_t>(tv, 600));
+  bool ok;
+  {
+    std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
+    ok = l_->set_unaccounted(node, used, ttl);
+  }
+  if (!ok) return answer(404, error_body("node " + node + " is not in the extender's ledger"));
+  return answer(200, "{\"Error\":\"\"}");
 }
 
 }  // namespace gsx

@@ -58,6 +58,12 @@ struct ServerConfig {
   int burst = 10;
   ApiConfig api;
   size_t max_body = 64u << 20;
+  // who may call the device plugin's endpoints (/move, /physical): "none" (anyone who reaches the port: tests, a
+  // loopback-only deployment) or "tokenreview" (a bearer token the apiserver's TokenReview authenticates as one of
+  // plugin_users, e.g. system:serviceaccount:kube-system:gpushare-device-plugin; cached plugin_auth_ttl seconds)
+  std::string plugin_auth = "none";
+  std::vector<std::string> plugin_users;
+  double plugin_auth_ttl = 60.0;
 };
 
 struct BindFailure {
@@ -79,7 +85,8 @@ struct LatencyHist {
 struct ServerStats {
   std::atomic<uint64_t> requests{0}, filters{0}, binds{0}, bind_ok{0}, bind_fail{0}, proxied{0}, bad_requests{0},
       inspects{0}, connections{0}, api_calls{0}, conflicts_retried{0}, bind_order_waits{0}, moves{0}, moves_failed{0},
-      unfiltered_binds{0}, live_gets{0}, qps_waits{0};
+      unfiltered_binds{0}, live_gets{0}, qps_waits{0}, physical_posts{0}, plugin_auth_denied{0},
+      token_reviews{0};
   LatencyHist filter_lat, bind_lat, api_lat;
 };
 
@@ -109,7 +116,7 @@ class NativeServer {
   struct Job {
     Loop* loop;
     uint64_t conn_id;
-    int kind;  // 0 bind, 1 proxy, 2 move
+    int kind;  // 0 bind, 1 proxy, 2 move, 3 physical
     http::Message req;
     double t0;
   };
@@ -137,6 +144,9 @@ class NativeServer {
   void throttle();
   std::string do_proxy(const http::Message& req);
   std::string do_move(const http::Message& req);
+  std::string do_physical(const http::Message& req);
+  // the caller of a device-plugin endpoint is the plugin (ServerConfig::plugin_auth); false with the 401/403 answer
+  bool plugin_authorized(const http::Message& req, std::string* resp);
   std::string bind_error_response(const std::string& msg) const;
   void record_failure(BindFailure f);
 
@@ -159,6 +169,8 @@ class NativeServer {
   double q_tokens_ = 0.0, q_last_ = 0.0;
   std::mutex fmu_;
   std::vector<BindFailure> failures_;
+  std::mutex amu_;  // token -> authenticated until (TokenReview cache)
+  std::unordered_map<std::string, double> authz_cache_;
   ServerStats stats_;
   // bind ordering lives in the ledger (Ledger::assume_ordered / bind_wait / bind_leave): one in-flight
   // set for the native binds and the Python slow path alike

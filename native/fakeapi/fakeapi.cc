@@ -1394,6 +1394,32 @@ class Server {
       rep->body = faults_.json();
       return true;
     }
+    if (path == "/fake/tokens" && m == "POST") {  // {"token": "...", "user": "..."}: what a TokenReview answers
+      jd::Value b = take_body(body);
+      const jd::Value* t = b.get("token");
+      const jd::Value* u = b.get("user");
+      if (t && t->k == jd::Value::Str && u && u->k == jd::Value::Str) tokens_[t->s] = u->s;
+      rep->body = "{}";
+      return true;
+    }
+    if (path == "/apis/authentication.k8s.io/v1/tokenreviews" && m == "POST") {
+      jd::Value b = take_body(body);
+      const jd::Value* spec = b.get("spec");
+      const jd::Value* t = spec ? spec->get("token") : nullptr;
+      auto it = (t && t->k == jd::Value::Str) ? tokens_.find(t->s) : tokens_.end();
+      counts_["tokenreviews"]++;
+      std::string o = "{\"kind\":\"TokenReview\",\"apiVersion\":\"authentication.k8s.io/v1\",\"status\":{";
+      if (it != tokens_.end()) {
+        o.append("\"authenticated\":true,\"user\":{\"username\":");
+        json::append_quoted(&o, it->second);
+        o.append("}}}");
+      } else {
+        o.append("\"authenticated\":false}}");
+      }
+      rep->status = 201;
+      rep->body = o;
+      return true;
+    }
     if (path == "/fake/stats") {
       std::string o = "{\"rv\":" + std::to_string(rv_) + ",\"native\":true,\"counts\":{";
       bool first = true;
@@ -1587,6 +1613,7 @@ class Server {
   std::deque<Event> history_;
   int64_t rv_ = 0, oldest_rv_ = 0;
   Faults faults_;
+  std::map<std::string, std::string> tokens_;  // TokenReview: bearer token -> username (/fake/tokens)
   std::map<std::string, uint64_t> counts_;
   std::vector<Grace> graces_;
 };

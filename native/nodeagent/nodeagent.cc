@@ -188,6 +188,8 @@ class Agent {
                                      "--podresources-socket", pr_sock_, "--isolation", "advisory", "--health-interval",
                                      "3600", "--log-level", "warning", "--debug-port", "0", "--debug-port-file",
                                      dir + "/debug.port"};
+    const char* ext_url = std::getenv("GSX_EXTENDER_URL");
+    if (!ext_url || !*ext_url) args.push_back("--no-extender");  // a harness run without an extender
     plugin_debug_file_ = dir + "/debug.port";
     pid_t pid = ::fork();
     if (pid < 0) {

@@ -17,15 +17,14 @@ from gpushare_scheduler_extender_amd.models.profile import (ALIYUN, POD_HOLD_IDX
 from gsxtools.configs import NODE, Cluster
 
 
-# kubelet's restart case through the compiled stand-in (--batch-window: pods met within 20 ms admitted as one
-# creationTimestamp-sorted batch) swaps equal-size pods nearly every batch, while pods are deleted mid-admission.
-# The plugin's physical account keeps it from over-committing a GPU (since round 4 it keeps a swapped allocation
-# held until kubelet's first PodResources report, AllocState::expect_owner_reports), but its exchange-based repair of
-# the annotations does not always converge before the extender binds onto a GPU the annotations show free and the
-# containers fill: the plugin then refuses that Allocate (the pod fails admission, as under a real kubelet) -- in
-# about one run in five before an early-answered commit that finds its pod gone released the pod at once, one in 26
-# since (docs/ROUND4.md).  Opt in with GSX_STRESS=1.
-STRESS = pytest.mark.skipif(os.environ.get("GSX_STRESS") != "1", reason="swap-storm stress row: GSX_STRESS=1")
+# kubelet's restart case (--batch-window: pods met within 20 ms admitted as one creationTimestamp-sorted batch) swaps
+# equal-size pods nearly every batch while pods are deleted mid-admission.  The rows below run it through the compiled
+# stand-in (native-plugin-batch) and the Python faithful kubelet over several seeds each: every surviving pod must end
+# Running with physical == *_IDX.  What makes that hold: the plugin publishes to the extender the GPU use its
+# containers hold where the annotations do not charge it (a deleted pod's allocation held by a swapped container),
+# the extender charges it on top of the annotations, and an exchange of two unequal pods is checked on its final state
+# (docs/ROUND5.md).
+BATCH_SEEDS = (43, 47, 53, 59, 61)
 
 
 async def _retry(fn, *a, tries=50, **kw):
@@ -67,8 +66,9 @@ def _committed_use(cl, bound: dict) -> tuple[list[int], int]:
                                                         (17, "native-plugin", "binding", True),
                                                         (19, "native-plugin", "update", True),
                                                         (41, "native-plugin", "binding", False),
-                                                        pytest.param(43, "native-plugin-batch", "binding", True,
-                                                                     marks=STRESS),
+                                                        *[(sd, "native-plugin-batch", "binding", True)
+                                                          for sd in BATCH_SEEDS],
+                                                        *[(sd, "faithful", "binding", True) for sd in BATCH_SEEDS[1:]],
                                                         (13, "plugin", "update", True),
                                                         (7, "faithful", "binding", True),
                                                         (29, "faithful", "update", False),

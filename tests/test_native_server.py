@@ -561,9 +561,17 @@ def test_move_endpoint_is_the_one_writer_of_the_gpu_index():
             # stale view: a is on GPU 0, not 1
             st, out = await move(a, 0, frm=1)
             assert st == 409 and "stale" in out["Error"], out
-            # an exchange step with an equal-size partner on the target is sum-neutral: allowed, with a hold
+            # a partner claim the ledger cannot verify (no hold on a's old GPU naming b) earns no credit
+            st, out = await move(a, 1, partner=b["metadata"]["uid"], annotations={P.annotation_assigned: "true"})
+            assert st == 409 and "free" in out["Error"], out
+            assert eng.stats()["partner_claims_refused"] >= 1
+            # an exchange step with a partner on the target: a holds its old GPU and names b as the hold's partner,
+            # so b's share is credited on GPU 1 (b leaves it in step 2): allowed
+            hp = json.dumps({"uid": b["metadata"]["uid"], "key": "default/b", "idx": 0, "assigned": "false",
+                             "cu_mask": None})
             st, out = await move(a, 1, partner=b["metadata"]["uid"],
-                                 annotations={"gpushare.amd.com/hold-idx": "0", P.annotation_assigned: "true"})
+                                 annotations={"gpushare.amd.com/hold-idx": "0", "gpushare.amd.com/hold-partner": hp,
+                                              P.annotation_assigned: "true"})
             assert st == 200, out
             ann = out["pod"]["metadata"]["annotations"]
             assert ann[P.annotation_idx] == "1" and ann["gpushare.amd.com/hold-idx"] == "0"
@@ -572,7 +580,8 @@ def test_move_endpoint_is_the_one_writer_of_the_gpu_index():
             st, out = await move(b, 0, partner=a["metadata"]["uid"])  # step 2: b takes a's old GPU (a holds it)
             assert st == 200, out
             a = await c.get("pods", "a", "default")
-            st, out = await move(a, 1, annotations={"gpushare.amd.com/hold-idx": None})  # step 3: the hold goes
+            st, out = await move(a, 1, annotations={"gpushare.amd.com/hold-idx": None,
+                                                    "gpushare.amd.com/hold-partner": None})  # step 3: the hold goes
             assert st == 200 and "gpushare.amd.com/hold-idx" not in out["pod"]["metadata"]["annotations"], out
             await settle([(100, 90), (100, 60)])
             # a plain move with room: best fit picked by the extender (to = -1), the target charged at once
@@ -588,7 +597,31 @@ def test_move_endpoint_is_the_one_writer_of_the_gpu_index():
             q = await c.get("pods", "q", "default")
             st, out = await move(q, 1, annotations={P.annotation_idx: "0"})
             assert st == 400, out
+            # ... and nothing outside the allocation fields a move rewrites (no arbitrary annotation writes)
+            st, out = await move(q, 1, annotations={"example.com/owner": "x"})
+            assert st == 400 and "writes only" in out["Error"], out
             assert eng.stats()["moves_ok"] == 4 and eng.stats()["moves_refused"] >= 2
+            # an exchange of two sizes is checked on the final state: c (20, GPU 0) and q (30, GPU 1);
+            # GPU 0 holds a 60 + c 20 = 80, GPU 1 holds b 60 + q 30 = 90.  q -> GPU 0 alone needs 30 (20 free) ...
+            cpod = await c.create("pods", bound("c", 20, 0))
+            await settle([(100, 80), (100, 90)])
+            q = await c.get("pods", "q", "default")
+            st, out = await move(q, 0)
+            assert st == 409, out
+            # ... as an exchange with c (c leaves GPU 0 for GPU 1): GPU 0 ends at 90, GPU 1 at 80 -- allowed
+            hp = json.dumps({"uid": cpod["metadata"]["uid"], "key": "default/c", "idx": 1, "assigned": "false",
+                             "cu_mask": None})
+            st, out = await move(q, 0, partner=cpod["metadata"]["uid"],
+                                 annotations={"gpushare.amd.com/hold-idx": "1", "gpushare.amd.com/hold-partner": hp})
+            assert st == 200, out
+            cpod = await c.get("pods", "c", "default")
+            st, out = await move(cpod, 1, partner=q["metadata"]["uid"])  # step 2, verified by q's hold
+            assert st == 200, out
+            q = await c.get("pods", "q", "default")
+            st, out = await move(q, 0, annotations={"gpushare.amd.com/hold-idx": None,
+                                                    "gpushare.amd.com/hold-partner": None})
+            assert st == 200, out
+            await settle([(100, 90), (100, 80)])
         finally:
             await http.close()
             await ext.stop()
@@ -643,4 +676,67 @@ def test_unfiltered_bind_errors_match_the_reference_and_qps_limits_native_binds(
             assert st["qps_waits"] >= 5 and dt >= 0.2, (st, dt)  # 6 bindings at 20 qps, burst 1
         finally:
             await _teardown(api, c, ext)
+    asyncio.run(go())
+
+
+def test_plugin_endpoints_take_only_the_plugin_token_and_the_physical_floor_steers_binds():
+    """the device plugin's endpoints (/move, /physical) write allocation records with the extender's
+    rights, so with ``plugin_auth="tokenreview"`` only a bearer token the apiserver's TokenReview authenticates as
+    the plugin's service account gets in (401 without one, 403 for another user; a reviewed token is cached).  The
+    unaccounted use the plugin publishes (containers on a device whose pods the annotations put elsewhere) is
+    charged on top of the annotations: a device those containers fill takes no bind while the annotations still
+    show room."""
+    from gsxtools.cluster import start_apiserver
+    from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as HttpClient
+
+    plugin_user = "system:serviceaccount:kube-system:gpushare-device-plugin"
+
+    async def go():
+        api = start_apiserver()
+        c = KubeClient(api.url)
+        fa = HttpClient(api.url)
+        for tok, user in (("tok-plugin", plugin_user), ("tok-other", "system:serviceaccount:default:app")):
+            await fa.request("POST", "/fake/tokens", json.dumps({"token": tok, "user": user}).encode())
+        await c.create("nodes", make_node("n", 2 * 100, 2))
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), plugin_auth="tokenreview",
+                                   plugin_users=[plugin_user]).start()
+        eng = ext.server.engine
+        http = HttpClient(f"http://127.0.0.1:{ext.port}")
+
+        async def physical(used, tok=None):
+            h = {"Authorization": f"Bearer {tok}"} if tok else None
+            r = await http.request("POST", "/gpushare-scheduler/physical",
+                                   json.dumps({"node": "n", "unaccounted": used, "ttl": 30}).encode(), headers=h)
+            return r.status
+
+        try:
+            for _ in range(200):
+                if eng.has_node("n"):
+                    break
+                await asyncio.sleep(0.01)
+            assert await physical([100, 0]) == 401
+            assert await physical([100, 0], "tok-other") == 403
+            assert await physical([100, 0], "nobody") == 401
+            r = await http.request("POST", "/gpushare-scheduler/move", b"{}", headers={"Authorization": "Bearer x"})
+            assert r.status == 401
+            assert await physical([100, 0], "tok-plugin") == 200
+            assert await physical([100, 0], "tok-plugin") == 200
+            srv = json.loads((await http.request("GET", "/debug/engine")).body)["server"]
+            assert srv["plugin_auth_denied"] == 4 and srv["token_reviews"] == 4  # the plugin's token reviewed once
+            assert eng.node_unaccounted("n") == [100, 0]
+            # GPU 0's containers fill it (the annotations say empty): the bind goes to GPU 1, and after it a
+            # 95-unit pod fits nowhere
+            assert eng.assume("u1", "default", "p1", "n", 10)[0] == 1
+            assert eng.assume("u2", "default", "p2", "n", 95)[0] < 0
+            # withdrawn: the annotations alone again -- GPU 0 takes it
+            assert await physical(None, "tok-plugin") == 200
+            assert eng.node_unaccounted("n") == []
+            assert eng.assume("u3", "default", "p3", "n", 95)[0] == 0
+        finally:
+            await http.close()
+            await fa.close()
+            await ext.stop()
+            await ext.server.client.close()
+            await c.close()
+            api.stop()
     asyncio.run(go())
