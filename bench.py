@@ -494,6 +494,10 @@ def parse():
                     help="every rank uses physical GPU 0 (a one-box rehearsal of the N-GPU launch): each rank advertises "
                          "a logical device sized for its wave (pods-per-gpu x pod-gib plus half a pod) and carves its "
                          "own HBM arena out of GPU 0, so N processes run their stamp / verify kernels on one card")
+    ap.add_argument("--wave-sampler", type=int, default=1,
+                    help="1: a sampler process on a spare CPU records every pipeline process's scheduler run-delay and "
+                         "the host's pressure counters, so each timed wave (and any slow one) is attributed "
+                         "(gsxtools/wavesampler.py; the JSON line's wave_attribution)")
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="event loops of the fake apiserver (0: auto; GSX_FAKEAPI_THREADS overrides)")
     return ap.parse_args()
@@ -889,6 +893,27 @@ def main():
         if use_gpu:
             torch.cuda.synchronize()
 
+    rank_pids = gather(os.getpid())
+    sampler = None
+    if rank == 0 and a.wave_sampler:
+        # per-wave attribution (run-delay of every pipeline process, host pressure) from a process of its own, on a
+        # CPU outside the plan when there is one
+        from gsxtools.wavesampler import Sampler
+
+        pids = {"rank0": os.getpid(), **{f"rank{r}": p for r, p in enumerate(rank_pids) if r > 0}}
+        for c in children:
+            pid = getattr(getattr(c, "proc", None), "pid", None)
+            if pid:
+                pids[c.name] = pid
+                if c.name == "node-agent":
+                    for k in _child_pids(pid):
+                        pids["plugin"] = k
+        planned = {x for v in cpu_plan.values() for x in (v or [])}
+        spare = sorted(set(os.sched_getaffinity(0)) - planned) if planned else []
+        import tempfile
+
+        sampler = Sampler(pids, os.path.join(tempfile.gettempdir(), f"gsx-waves-{os.getpid()}.json"),
+                          cpu=spare[-1] if spare else None)
     if rank == 0:
         for step in range(a.warmup + a.steps):
             wave_requests(step)
@@ -943,6 +968,19 @@ def main():
     thr1 = _threads_of_node(children)
     rss1 = _rss_mib(children)
     cg1 = _cgroup_cpu()
+    wave_attr = None
+    if sampler is not None:
+        from gsxtools.wavesampler import attribute
+
+        data = sampler.stop()
+        try:
+            wave_attr = attribute(data, [(s["t0"], s["t_total"]) for s in step_stats]) if data else None
+        except Exception as e:  # noqa: BLE001 - diagnosis never costs the headline line
+            wave_attr = {"error": repr(e)}
+        try:
+            os.unlink(sampler.out)
+        except OSError:
+            pass
     if prof is not None:
         lt.run(asyncio.sleep(0))
         lt.loop.call_soon_threadsafe(prof.disable)
@@ -1069,6 +1107,9 @@ def main():
             # per-wave throughput distribution: p50 and IQR next to `value` (one number from ~20 short waves is
             # sensitive to single slow waves)
             "wave_pods_per_s": wave_dist([n_pods / s["t_total"] for s in step_stats]),
+            # why a wave was slow: per-wave scheduler run-delay of every pipeline process and the host's pressure
+            # counters, and for each wave over 5 x the p50 the process (or the host) that waited longest for a CPU
+            "wave_attribution": wave_attr,
             # rank 0's view of the timed region: the waves back to back, then the closing barriers
             "timed_region_ms": {"waves": round(1e3 * sum(s["t_total"] for s in step_stats), 3),
                                 "rank0_waves_span": round(1e3 * (t_waves_end - t_start), 3),

@@ -353,9 +353,12 @@ class GpuSharePlugin:
         if srv is None:
             return
         pending, events = srv.poll()
-        served = [ev["uid"] for ev in events if self._fast_allocated(ev)]
+        served = [ev for ev in events if self._fast_allocated(ev)]
         if served and self.reconciler is not None:
-            self.reconciler.kick(fast=self._ambiguous(served))
+            amb = sum(1 for ev in served if ev.get("ambiguous"))
+            if amb:
+                self.stats["ambiguous_allocates"] = self.stats.get("ambiguous_allocates", 0) + amb
+            self.reconciler.kick(fast=amb > 0)
         self.state.flush_dropped()  # records the native pod feed dropped with their pods: isolation cleanup
         if pending:
             loop = asyncio.get_running_loop()
@@ -404,7 +407,7 @@ class GpuSharePlugin:
             if p is not None and spread.get(p.request, set()) - {p.dev}:
                 self.stats["ambiguous_allocates"] = self.stats.get("ambiguous_allocates", 0) + 1
                 return True
-        return False
+        return False  # (the native fast path decides this at match time: DpEvent::ambiguous)
 
     async def _native_slow(self, srv, cid: int, method: str, payload: bytes):
         """A call the native fast path left to Python: the same handler grpcio would run."""
@@ -901,19 +904,24 @@ class GpuSharePlugin:
     # ------------------------------------------------------------ physical use -> the extender
     def unaccounted(self) -> list[int] | None:
         """Per GPU, the units kubelet's containers hold there that the annotations do not charge there: a record
-        whose holder (kubelet's report, else the pod it was built for) is annotated with another GPU, or is gone.
-        None when every container is charged where it runs (the extender then uses the annotations alone)."""
-        if not self.units:
+        kubelet reports held by another, live pod than the one it was built for, and that pod is annotated with
+        another GPU (a swap the exchange has not repaired).
+        None when every container is charged where it runs (the extender then uses the annotations alone), and
+        always on a one-GPU node: whoever holds an allocation there is annotated with that GPU too."""
+        if len(self.units) < 2:
             return None
         pods = self.state.pods
         out = [0] * (max(self.units) + 1)
         found = False
         for r in self.state.records.values():
-            if not 0 <= r.dev < len(out):
+            if not 0 <= r.dev < len(out) or not r.owner or r.owner == r.uid:
+                # not reported by kubelet yet, or held by the pod it was built for: the annotations charge it (a
+                # pod deleted before the first report: its container is stopping, as the extender assumes)
                 continue
-            h = r.owner or r.uid
-            p = pods.get(h) if h and not h.startswith("~") else None
-            if p is None or p.complete or p.dev != r.dev:
+            p = None if r.owner.startswith("~") else pods.get(r.owner)
+            # a holder that is gone: its container is stopping, as for any deleted pod (the extender frees on
+            # deletion, as the reference does)
+            if p is not None and not p.complete and p.dev != r.dev:
                 out[r.dev] += r.units
                 found = True
         return out if found else None

@@ -88,6 +88,7 @@ class Reconciler:
         # after an ambiguous Allocate (kubelet records an Allocate's IDs before it returns to its admission loop;
         # a pass skips records made after it asked, so a short delay only saves passes)
         self.after_ambiguous = 0.002
+        self.unaccounted_poll = 0.01
         self._fast = False
         self._kick = asyncio.Event()
         self._task: asyncio.Task | None = None
@@ -434,8 +435,11 @@ class Reconciler:
     # ------------------------------------------------------------ loop
     async def run(self):
         while True:
+            # while the extender charges unaccounted use, look again soon: it is withdrawn as soon as kubelet's report
+            # lets the records go (a stale publication would keep the GPU from the next pods)
+            wait = self.interval if self.plugin._phys_published is None else min(self.interval, self.unaccounted_poll)
             try:
-                await asyncio.wait_for(self._kick.wait(), self.interval)
+                await asyncio.wait_for(self._kick.wait(), wait)
                 # let kubelet record the allocation first
                 await asyncio.sleep(self.after_ambiguous if self._fast else self.after_allocate)
             except asyncio.TimeoutError:

@@ -963,6 +963,7 @@ class PyDpServer {
       d["aid"] = e.aid;
       d["iso"] = e.iso;
       d["committed"] = e.committed;
+      d["ambiguous"] = e.ambiguous;
       d["patch_only"] = e.patch_only;
       d["pod_json"] = py::bytes(e.pod_json);
       d["t_handler"] = e.t_handler;

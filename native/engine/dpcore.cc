@@ -380,6 +380,15 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
     return DpStep::Slow;
   }
   const AllocPod pod = *m.first;  // a copy: observe() later replaces the state's
+  bool ambiguous = false;
+  if (devs_.size() > 1) {
+    for (const AllocPod* c : state_->candidates()) {
+      if (c->uid != pod.uid && c->request == pod.request && c->dev != pod.dev) {
+        ambiguous = true;
+        break;
+      }
+    }
+  }
   auto dit = devs_.find(static_cast<int>(pod.dev));
   if (dit == devs_.end() || pod.hold_idx >= 0 || !pod.hold_partner.empty()) {
     stats_.slow_allocate++;
@@ -433,6 +442,7 @@ DpStep DpCore::allocate(const std::string& req, std::string* resp, DpEvent* ev, 
   p->units = units;
   p->ids = std::move(ids_per[0]);  // `ids` is not read after this point
   p->on_gpu = on_gpu;
+  p->ambiguous = ambiguous;
   p->cr = build_response(pod, dev, units, cus, cfg_.mount_mode, cfg_.profile);
   const double tb = mono_s();
   p->t0 = t0;
@@ -590,6 +600,7 @@ void DpCore::record_and_answer(DpPending& p, std::string* resp, DpEvent* ev) {
   ev->key = p.pod.key;
   ev->aid = aid;
   ev->iso = p.iso;
+  ev->ambiguous = p.ambiguous;
   const double t1 = mono_s();
   ev->t_handler = t1 - p.t0;
   ev->t_match = p.tm - p.t0;

@@ -63,6 +63,9 @@ bool isolation_prepare(const std::string& host_dir, const std::string& uid, cons
 struct DpEvent {  // what the Python side learns after a fast-path Allocate
   std::string uid, key, aid, iso, pod_json;
   bool committed = false;  // a first container (ASSIGNED patch) rather than a later one
+  // another pending pod of the same size waits for another GPU: a kubelet admission batch may have served this
+  // allocation to that pod (the reconciliation looks at once)
+  bool ambiguous = false;
   bool patch_only = false;  // early answer: the ASSIGNED patch of an Allocate answered before landed (pod_json)
   double t_handler = 0, t_match = 0, t_patch = 0, t_isolate = 0;
 };
@@ -78,6 +81,7 @@ struct DpPending {
   int64_t units = 0;
   std::vector<std::string> ids;
   bool on_gpu = false;  // every ID lies on the pod's GPU
+  bool ambiguous = false;  // DpEvent::ambiguous
   dp::ContainerResponse cr;
   std::string iso, path, body;
   double t0 = 0, tm = 0, ti0 = 0, ti1 = 0, tp0 = 0, tp1 = 0;
