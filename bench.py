@@ -553,11 +553,12 @@ def main():
     # CPUs per process: the extender (2 loops + bind pool + reflectors), schedsim (cycle + bind threads) and the
     # node agent (reflector + workers) get two; rank 0 stays on one core (a second one let its driver, tracker
     # and runtime threads migrate: 7.5-9.4k vs 10.1k pods/s, interleaved A/B in profiles/r02_bench_stability.md)
-    # The plugin gets two cores: its serving thread spins after each pass (one SMT thread), and on one core its pod
-    # feed, Python thread and commit worker shared the other -- a pod's event then reached the plugin up to 1.6 ms
-    # after kubelet asked for it (profiles/r04_pinw/: 2 CPUs 9.5 / 7.9 / 7.7k pods/s with 1.5-2 ms waves, 4 CPUs
-    # 9.7 / 9.3 / 10.0k with none, interleaved)
-    widths = {"extender": 2, "scheduler": 2, "node-agent": 2, "plugin": 4}
+    # The plugin gets one core (2 CPUs) on a one-GPU node, what its DaemonSet requests.  Round 4 gave it two: its
+    # serving thread then busy-looped on a stuck deferred wake-up between bursts (fixed in round 5, bindings.cc
+    # DpServer::serve), and on one core its pod feed queued behind it (profiles/r04_pinw/).  An 8-GPU node admits 8x
+    # the pods through it: two cores there (run-delay of its threads 214 ms per 170 ms region on one core,
+    # profiles/r05_session4/)
+    widths = {"extender": 2, "scheduler": 2, "node-agent": 2, "plugin": 2 if world == 1 else 4}
     if a.runtime_cpu == "split":
         # rank 0 = the wave driver + GPU 0's runtime endpoint (the CRI-runtime role): one core, the driver on
         # one SMT thread and the endpoint's threads on the other, instead of both time-sharing one thread
@@ -780,6 +781,29 @@ def main():
         pod_tmpl = json.dumps(pod_tmpl, separators=(",", ":"))
     from gpushare_scheduler_extender_amd.utils.gctune import tune
 
+    rank_pids = gather(os.getpid())
+    sampler = None
+    if rank == 0 and a.wave_sampler:
+        # per-wave attribution (run-delay of every pipeline process, host pressure) from a process of its own, on a
+        # CPU outside the plan when there is one
+        from gsxtools.wavesampler import Sampler
+
+        pids = {"rank0": os.getpid(), **{f"rank{r}": p for r, p in enumerate(rank_pids) if r > 0}}
+        for c in children:
+            pid = getattr(getattr(c, "proc", None), "pid", None)
+            if pid:
+                pids[c.name] = pid
+                if c.name == "node-agent":
+                    for k in _child_pids(pid):
+                        pids["plugin"] = k
+        planned = {x for v in cpu_plan.values() for x in (v or [])}
+        spare = sorted(set(os.sched_getaffinity(0)) - planned) if planned else []
+        import tempfile
+
+        sampler = Sampler(pids, os.path.join(tempfile.gettempdir(), f"gsx-waves-{os.getpid()}.json"),
+                          cpu=spare[-1] if spare else None)
+        if not sampler.wait_ready():
+            sampler = None  # diagnosis only: the headline runs without it
     if rank == 0 and a.api_latency_ms:
         set_latency(api_batch, a.api_latency_ms)
     tune()
@@ -893,27 +917,6 @@ def main():
         if use_gpu:
             torch.cuda.synchronize()
 
-    rank_pids = gather(os.getpid())
-    sampler = None
-    if rank == 0 and a.wave_sampler:
-        # per-wave attribution (run-delay of every pipeline process, host pressure) from a process of its own, on a
-        # CPU outside the plan when there is one
-        from gsxtools.wavesampler import Sampler
-
-        pids = {"rank0": os.getpid(), **{f"rank{r}": p for r, p in enumerate(rank_pids) if r > 0}}
-        for c in children:
-            pid = getattr(getattr(c, "proc", None), "pid", None)
-            if pid:
-                pids[c.name] = pid
-                if c.name == "node-agent":
-                    for k in _child_pids(pid):
-                        pids["plugin"] = k
-        planned = {x for v in cpu_plan.values() for x in (v or [])}
-        spare = sorted(set(os.sched_getaffinity(0)) - planned) if planned else []
-        import tempfile
-
-        sampler = Sampler(pids, os.path.join(tempfile.gettempdir(), f"gsx-waves-{os.getpid()}.json"),
-                          cpu=spare[-1] if spare else None)
     if rank == 0:
         for step in range(a.warmup + a.steps):
             wave_requests(step)
@@ -977,10 +980,6 @@ def main():
             wave_attr = attribute(data, [(s["t0"], s["t_total"]) for s in step_stats]) if data else None
         except Exception as e:  # noqa: BLE001 - diagnosis never costs the headline line
             wave_attr = {"error": repr(e)}
-        try:
-            os.unlink(sampler.out)
-        except OSError:
-            pass
     if prof is not None:
         lt.run(asyncio.sleep(0))
         lt.loop.call_soon_threadsafe(prof.disable)

@@ -36,6 +36,7 @@ from __future__ import annotations
 import asyncio
 import json
 import logging
+import os
 import time
 
 from ..k8s.client import ApiError
@@ -89,6 +90,9 @@ class Reconciler:
         # a pass skips records made after it asked, so a short delay only saves passes)
         self.after_ambiguous = 0.002
         self.unaccounted_poll = 0.01
+        # kubelet rate-limits its PodResources API (100 calls/s, burst 10, since k8s 1.27): passes stay >= 10 ms apart
+        self.min_spacing = float(os.environ.get("GSX_RECONCILE_MIN_SPACING", "0.01"))
+        self._last_pass = 0.0
         self._fast = False
         self._kick = asyncio.Event()
         self._task: asyncio.Task | None = None
@@ -446,6 +450,10 @@ class Reconciler:
                 pass
             self._kick.clear()
             self._fast = False
+            gap = self._last_pass + self.min_spacing - time.monotonic()
+            if gap > 0:
+                await asyncio.sleep(gap)
+            self._last_pass = time.monotonic()
             if not self.pr.available():
                 self.state.core.set_owners_reported(False)  # nobody will report owners: drop records by pod
                 continue

@@ -55,6 +55,8 @@ def sample_loop(pids: dict[str, int], interval: float, out: str) -> None:
     samples: list[list] = []
     stop = {"now": False}
     signal.signal(signal.SIGTERM, lambda *_: stop.__setitem__("now", True))
+    with open(out + ".ready", "w"):  # the bench waits for this before its warmup waves
+        pass
     tids: dict[str, list[str]] = {}
     t_tids = 0.0
     while not stop["now"]:
@@ -141,10 +143,15 @@ def attribute(data: dict, waves: list[tuple[float, float]], slow_factor: float =
 class Sampler:
     """The sampler as a child process of the bench (started before the timed region, stopped after it)."""
 
-    def __init__(self, pids: dict[str, int], out: str, interval: float = 0.0005, cpu: int | None = None):
+    def __init__(self, pids: dict[str, int], out: str, interval: float = 0.002, cpu: int | None = None):
         import subprocess  # noqa: PLC0415
 
         self.out = out
+        for f in (out, out + ".ready"):
+            try:
+                os.unlink(f)
+            except OSError:
+                pass
         spec = ",".join(f"{n}={p}" for n, p in pids.items() if p)
         pre = None
         if cpu is not None:
@@ -152,6 +159,17 @@ class Sampler:
                 os.sched_setaffinity(0, {cpu})
         self.proc = subprocess.Popen([sys.executable, "-m", "gsxtools.wavesampler", "--pids", spec, "--interval",
                                       str(interval), "--out", out], preexec_fn=pre)
+
+    def wait_ready(self, timeout: float = 30.0) -> bool:
+        """The sampler runs (its SIGTERM handler is in place): it must not start up inside a timed region."""
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            if os.path.exists(self.out + ".ready"):
+                return True
+            if self.proc.poll() is not None:
+                return False
+            time.sleep(0.005)
+        return False
 
     def stop(self) -> dict | None:
         self.proc.terminate()
@@ -165,12 +183,18 @@ class Sampler:
                 return json.load(f)
         except (OSError, ValueError):
             return None
+        finally:
+            for f in (self.out, self.out + ".ready"):
+                try:
+                    os.unlink(f)
+                except OSError:
+                    pass
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="per-wave run-delay / pressure sampler (bench.py)")
     ap.add_argument("--pids", required=True, help="name=pid,name=pid,...")
-    ap.add_argument("--interval", type=float, default=0.0005)
+    ap.add_argument("--interval", type=float, default=0.002)
     ap.add_argument("--out", required=True)
     a = ap.parse_args(argv)
     pids = {}

@@ -1064,6 +1064,9 @@ class PyDpServer {
                                          py::arg("journal") = s.ph_journal * k, py::arg("encode") = s.ph_encode * k);
     }
     d["calls"] = srv_ ? srv_->calls() : 0;
+    d["spins"] = spins_;
+    d["loop_iters"] = loop_iters_;
+    d["spin_iters"] = spin_iters_;
     d["connections"] = srv_ ? srv_->connections() : 0;
     d["fast"] = fast_;
     d["last_slow_reason"] = last_why_;
@@ -1180,8 +1183,10 @@ class PyDpServer {
     double spin_until = 0;
     for (;;) {
       pollfd pf{ep, POLLIN, 0};
+      loop_iters_++;
       if (mono() < spin_until) {
         if (::poll(&pf, 1, 0) == 0 && !(py_deferred_ && mono() >= py_due_)) {
+          spin_iters_++;
           if (stop_serving_) return;  // read without the lock: only a faster exit; checked again below
           continue;
         }
@@ -1218,7 +1223,13 @@ class PyDpServer {
         finish_patches();
         if (stop_serving_ || !srv_) return;
       }
-      spin_until = spin_us_ > 0 ? mono() + spin_us_ * 1e-6 : 0;
+      // spin only after a pass that served kubelet (its calls come in bursts: GetPreferredAllocation, Allocate, the
+      // next pod's); a pass woken by the pod feed, a patch completion or the idle timeout blocks again at once, so an
+      // idle or trickling node costs no polling core
+      const uint64_t calls = srv_ ? srv_->calls() : 0;
+      spin_until = (spin_us_ > 0 && calls != calls_seen_) ? mono() + spin_us_ * 1e-6 : 0;
+      if (spin_until > 0) spins_++;
+      calls_seen_ = calls;
       // also when the feed released a pod whose records went: Python cleans up their isolation files.  Calls for
       // the Python slow path wake it at once; bookkeeping events (answered Allocates, landed commits) at most every
       // py_event_s_: a Python pass takes the state lock, and one per Allocate would sit in the next admission's way
@@ -1234,6 +1245,11 @@ class PyDpServer {
           py_deferred_ = true;
           py_due_ = py_signal_at_ + py_event_s_;
         }
+      } else {
+        // nothing left for Python (it drained the events on a wake-up of its own): no deferred signal is due.  A
+        // deferral left standing made every later poll time out at once -- the thread took the state lock for an
+        // empty pass hundreds of thousands of times a second until the next event (round 4's busy plugin core)
+        py_deferred_ = false;
       }
     }
   }
@@ -1520,6 +1536,9 @@ class PyDpServer {
   uint64_t lock_waits_ = 0;                        // waits over 5 us
   uint64_t h_pref_n_ = 0, h_alloc_n_ = 0;
   double spin_us_ = 1000;      // poll without sleeping this long after a pass (cfg "spin_us"; 0: always block)
+  uint64_t calls_seen_ = 0;    // kubelet calls served as of the last pass (a pass that served none does not spin)
+  uint64_t spins_ = 0;
+  uint64_t loop_iters_ = 0, spin_iters_ = 0;
   uint64_t passes_ = 0;
 };
 

@@ -13,10 +13,13 @@ if [ "${TESTS:-1}" = 1 ]; then
   tail -2 $OUT/gputests.log
 fi
 for i in $(seq 1 ${HEADLINE:-2}); do
-  timeout -k 10 240 python bench.py --gpus 1 --steps 20 --warmup 5 --json-out $OUT/bench_$i.json \
-    > $OUT/bench_$i.log 2>&1 || { tail -30 $OUT/bench_$i.log; exit 1; }
-  python -c "
-import json; d=json.load(open('$OUT/bench_$i.json')); print('headline', d['value'], d['wave_pods_per_s'], d['busy_pct'])"
+  for ws in ${SAMPLER:-1}; do
+    timeout -k 10 240 python bench.py --gpus 1 --steps 20 --warmup 5 --wave-sampler $ws --json-out $OUT/bench_${i}_ws$ws.json \
+      > $OUT/bench_${i}_ws$ws.log 2>&1 || { tail -30 $OUT/bench_${i}_ws$ws.log; exit 1; }
+    python -c "
+import json; d=json.load(open('$OUT/bench_${i}_ws$ws.json')); w=d.get('wave_attribution') or {}
+print('headline ws=$ws', d['value'], d['wave_pods_per_s'], d['busy_pct'], 'slow', w.get('slow_waves'))"
+  done
 done
 if [ "${SHARE:-1}" = 1 ]; then
   timeout -k 10 300 python bench.py --gpus 4 --share-gpu --pod-gib 8 --steps 20 --warmup 5 --sweep 0 \
