@@ -81,9 +81,10 @@ class LoopThread:
         self.t.join(5)
 
 
-def _task_cpu_s(pid: int) -> float | None:
+def _task_cpu_s(pid: int, field: int = 0) -> float | None:
     """On-CPU seconds of every thread of `pid` (/proc/<pid>/task/*/schedstat, nanosecond resolution: the
-    timed region is milliseconds, far below the 10 ms ticks of /proc/<pid>/stat)."""
+    timed region is milliseconds, far below the 10 ms ticks of /proc/<pid>/stat).  ``field=1``: the seconds its
+    threads waited runnable for a CPU (scheduler run-delay) instead."""
     try:
         tids = os.listdir(f"/proc/{pid}/task")
     except OSError:
@@ -92,10 +93,24 @@ def _task_cpu_s(pid: int) -> float | None:
     for t in tids:
         try:
             with open(f"/proc/{pid}/task/{t}/schedstat") as f:
-                ns += int(f.read().split()[0])
+                ns += int(f.read().split()[field])
         except (OSError, ValueError, IndexError):
             pass
     return ns / 1e9
+
+
+def _psi_us() -> dict:
+    """The host's pressure stall totals (/proc/pressure/{cpu,io,memory} "some total=", microseconds), {} without PSI."""
+    out = {}
+    for k in ("cpu", "io", "memory"):
+        try:
+            with open(f"/proc/pressure/{k}") as f:
+                for ln in f:
+                    if ln.startswith("some"):
+                        out[k] = int(ln.rsplit("total=", 1)[1])
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
 
 
 def _thread_cpu_s(pid: int) -> dict:
@@ -141,23 +156,23 @@ def _child_pids(pid: int) -> list[int]:
     return out
 
 
-def _cpu_times(children) -> dict:
-    """On-CPU seconds of this process (rank 0), the child servers and the device-plugin process the node agent
-    spawned (the shipped plugin, the node's DaemonSet pod)."""
+def _cpu_times(children, field: int = 0) -> dict:
+    """On-CPU seconds (``field=1``: run-delay seconds) of this process (rank 0), the child servers and the
+    device-plugin process the node agent spawned (the shipped plugin, the node's DaemonSet pod)."""
     out = {}
-    me = _task_cpu_s(os.getpid())
+    me = _task_cpu_s(os.getpid(), field)
     if me is not None:
         out["rank0"] = me
     for c in children:
         pid = getattr(getattr(c, "proc", None), "pid", None)
         if pid is None:
             continue
-        v = _task_cpu_s(pid)
+        v = _task_cpu_s(pid, field)
         if v is not None:
             out[c.name] = v
         if c.name == "node-agent":
             for k in _child_pids(pid):
-                pv = _task_cpu_s(k)
+                pv = _task_cpu_s(k, field)
                 if pv is not None:
                     out["plugin"] = out.get("plugin", 0.0) + pv
     return out
@@ -494,10 +509,12 @@ def parse():
                     help="every rank uses physical GPU 0 (a one-box rehearsal of the N-GPU launch): each rank advertises "
                          "a logical device sized for its wave (pods-per-gpu x pod-gib plus half a pod) and carves its "
                          "own HBM arena out of GPU 0, so N processes run their stamp / verify kernels on one card")
-    ap.add_argument("--wave-sampler", type=int, default=1,
+    ap.add_argument("--wave-sampler", type=int, default=0,
                     help="1: a sampler process on a spare CPU records every pipeline process's scheduler run-delay and "
                          "the host's pressure counters, so each timed wave (and any slow one) is attributed "
-                         "(gsxtools/wavesampler.py; the JSON line's wave_attribution)")
+                         "(gsxtools/wavesampler.py; the JSON line's wave_attribution).  Off by default: reading the "
+                         "threads' /proc stats every 2 ms slows the pipeline (N = 8: 11.0-11.2k -> 6.0-8.3k pods/s, "
+                         "profiles/r05_session5/).  The region-level run_delay_pct and psi_timed_ms are always there")
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="event loops of the fake apiserver (0: auto; GSX_FAKEAPI_THREADS overrides)")
     return ap.parse_args()
@@ -937,6 +954,8 @@ def main():
             # the CPU-time counters are read before the bracket: reading /proc for every child took ~0.5 ms, which
             # sat inside the timed region (rank 0's span exceeded the sum of its waves by that much)
             cpu0 = _cpu_times(children)
+            rd0 = _cpu_times(children, 1)
+            psi0 = _psi_us()
             thr0 = _threads_of_node(children)
             rss0 = _rss_mib(children)
             cg0 = _cgroup_cpu()
@@ -968,6 +987,8 @@ def main():
     gc.enable()
     own_elapsed = elapsed
     cpu1 = _cpu_times(children)
+    rd1 = _cpu_times(children, 1)
+    psi1 = _psi_us()
     thr1 = _threads_of_node(children)
     rss1 = _rss_mib(children)
     cg1 = _cgroup_cpu()
@@ -1106,7 +1127,13 @@ def main():
             # per-wave throughput distribution: p50 and IQR next to `value` (one number from ~20 short waves is
             # sensitive to single slow waves)
             "wave_pods_per_s": wave_dist([n_pods / s["t_total"] for s in step_stats]),
-            # why a wave was slow: per-wave scheduler run-delay of every pipeline process and the host's pressure
+            # where the timed region lost time to the host: each process's threads' scheduler run-delay (waiting
+            # runnable for a CPU) over the region, in % of its wall time, and the host's pressure-stall deltas (ms).
+            # Read at the bracket, outside the waves.  Per wave (--wave-sampler 1): wave_attribution
+            "run_delay_pct": {k: round(100.0 * (rd1[k] - rd0.get(k, 0.0)) / max(elapsed, 1e-9), 1) for k in rd1},
+            "psi_timed_ms": {k: round((psi1[k] - psi0.get(k, 0)) / 1e3, 3) for k in psi1},
+            # why a wave was slow (opt-in, --wave-sampler 1: the sampler's /proc reads slow the pipeline down, up to
+            # 45 % at N = 8, profiles/r05_session5/): per-wave run-delay of every process and the host's pressure
             # counters, and for each wave over 5 x the p50 the process (or the host) that waited longest for a CPU
             "wave_attribution": wave_attr,
             # rank 0's view of the timed region: the waves back to back, then the closing barriers
