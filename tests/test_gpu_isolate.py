@@ -238,6 +238,45 @@ def test_scratch_fits_in_the_share_or_the_kernel_is_refused(iso):
     assert before - during <= share + 512 * (1 << 20), (before, during)
 
 
+def test_concurrent_scratch_is_charged_per_queue_or_refused(iso):
+    """ROCr gives each hardware queue its own scratch, so four streams running the 1 KiB-a-lane
+    kernel at the same instant hold four times one dispatch's.  The isolation library charges the worst kernel's
+    scratch on every queue: under a share sized for one charge the work is refused cleanly (a queue or the code
+    object, an error code, no fault) or runs fully charged; under a share with room for four it runs, and an
+    unconfined observer sees the pod hold no more than the share (+ the runtime's own small allocations)."""
+    probe = NATIVE / "gsx-memprobe"
+    one = _run([probe, "--scratch", "1", "--blocks", "16384"],
+               _env(iso.prepare("scr-one", None, 256, 8 * GIB, host_process=True)[1]))["scratch"]
+    assert one["ok"] and one["iso"] and one["iso_worst"] > 0, one
+    worst = one["iso_worst"]  # one queue's worst-case scratch for this kernel (~0.67 GB on MI355X)
+    # a share for one charge, not four
+    share = worst + 256 * (1 << 20)
+    _, env = iso.prepare("scr-q1", None, 256, share, host_process=True)
+    out = _run([probe, "--scratch", "1", "--blocks", "16384", "--streams", "4"], _env(env))["scratch"]
+    assert out["iso"], out
+    if out["ok"]:
+        assert out["iso_worst"] * max(1, out["iso_queues"]) <= share, out  # every queue charged, inside the share
+    else:
+        assert out["stage"] in ("stream", "load", "launch"), out
+        assert out["iso_queues_refused"] >= 1 or out["stage"] == "load", out
+    # room for four: runs, every queue charged, and the device holds what the share allows
+    share4 = 4 * worst + 512 * (1 << 20)
+    _, env4 = iso.prepare("scr-q4", None, 256, share4, host_process=True)
+    before = _run([probe], _env({}))["free"]
+    holder = subprocess.Popen([str(probe), "--scratch", "1", "--blocks", "16384", "--streams", "4", "--hold-ms", "20000"],
+                              env=_env(env4), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        first = json.loads(holder.stdout.readline())
+        sc = first["scratch"]
+        assert sc["ok"] is True and sc["iso_queues"] >= 1 and sc["iso_queues_refused"] == 0, first
+        assert sc["iso_worst"] * max(1, sc["iso_queues"]) <= share4, first
+        during = _run([probe], _env({}))["free"]
+    finally:
+        holder.kill()
+        holder.wait(30)
+    assert before - during <= share4 + 512 * (1 << 20), (before, during, share4)
+
+
 def test_copies_of_a_confined_process_run_on_its_masked_queues(iso):
     """VERDICT r3 item 4 ("blit queues"): a confined PyTorch process's host<->device and device->device copies
     complete, and every queue the runtime created for it got the pod's CU mask (device->device copies are HIP blit
