@@ -333,8 +333,9 @@ class GpuSharePlugin:
                 "preferred": self.preferred,
                 # answered Allocates reach this loop's bookkeeping at most this often (a pass takes the state lock)
                 "py_event_ms": float(os.environ.get("GSX_PLUGIN_PY_EVENT_MS", "2")),
-                # early answer (opt-in): answer a first container's Allocate once its record is journaled, commit
-                # ASSIGNED=true behind it (kubelet's serial admission no longer waits an apiserver round trip)
+                # early answer (default; GSX_PLUGIN_EARLY_ANSWER=0 turns it off): answer a first container's Allocate
+                # once its record is journaled, commit ASSIGNED=true behind it (kubelet's serial admission no longer
+                # waits an apiserver round trip)
                 "early_answer": self.early_answer, "journal": self.journal_path}
 
     def native_device(self, d: Device) -> dict:
