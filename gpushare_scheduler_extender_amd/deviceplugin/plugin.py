@@ -631,7 +631,9 @@ class GpuSharePlugin:
             pod = await self.client.patch("pods", p.name, {"metadata": {"uid": p.uid, "annotations": ann}},
                                           p.namespace)
         except ApiError as e:
-            if e.status == 404 or (e.status == 409 and "UID in precondition" in str(e)):
+            # gone, or re-created under its name (kube-apiserver refuses the patch's changed metadata.uid: 422)
+            if e.status == 404 or (e.status == 422 and "metadata.uid" in str(e)) or (
+                    e.status == 409 and "UID in precondition" in str(e)):
                 self.state.inflight.discard(p.uid)
                 return True
             log.warning("committing the answered Allocate of %s: %s (the pod stays claimed; retrying)", p.key, e)

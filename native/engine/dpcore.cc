@@ -530,7 +530,10 @@ bool DpCore::finish(DpPending& p, std::string* resp, DpEvent* ev, std::string* w
       ev->pod_json = std::move(p.resp);
       return true;
     }
-    const bool recreated = p.ok && p.status == 409 && p.resp.find("UID in precondition") != std::string::npos;
+    // re-created under its name: kube-apiserver refuses the changed metadata.uid of the patched object (422 Invalid);
+    // a UID-precondition 409 is what a PUT or Binding would get, accepted too
+    const bool recreated = p.ok && ((p.status == 422 && p.resp.find("metadata.uid") != std::string::npos) ||
+                                    (p.status == 409 && p.resp.find("UID in precondition") != std::string::npos));
     if ((p.ok && p.status == 404) || recreated || !state_->pod(p.pod.uid)) {
       // the pod went away (deleted, or re-created under its name): nothing to commit.  It is released now, not when
       // the pod feed delivers the deletion: unclaimed but still pending ASSIGNED=false in the state, it would be the

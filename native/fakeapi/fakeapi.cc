@@ -1173,12 +1173,16 @@ class Server {
     const jd::Value* pmd = patch.get("metadata");
     std::string want = pmd ? pmd->str_or("resourceVersion") : std::string();
     if (!want.empty() && want != cmd.str_or("resourceVersion")) throw conflict(kind, name);
-    // kube-apiserver's registry store refuses an update whose object UID differs from the stored one: a merge
-    // patch naming metadata.uid is a UID precondition
+    // a merge patch that names another metadata.uid than the stored object's: kube-apiserver applies the patch and
+    // its update validation refuses the changed immutable field (422 Invalid) -- a PATCH carries no UID
+    // precondition (only a PUT's object or a Binding does: 409 below)
     std::string want_uid = pmd ? pmd->str_or("uid") : std::string();
     if (!want_uid.empty() && want_uid != cmd.str_or("uid")) {
-      throw HttpError{409, status_body(409, "Conflict", "Precondition failed: UID in precondition: " + want_uid +
-                                                            ", UID in object meta: " + cmd.str_or("uid"))};
+      throw HttpError{422, status_body(422, "Invalid", kind == "pods" ? "Pod \"" + name + "\" is invalid: metadata.uid: "
+                                                                          "Invalid value: \"" + want_uid +
+                                                                          "\": field is immutable"
+                                                                    : "metadata.uid: Invalid value: \"" + want_uid +
+                                                                          "\": field is immutable")};
     }
     if (kind == "pods" && injected_conflict()) throw conflict(kind, name);
     if (sub == "status") {

@@ -337,10 +337,11 @@ class FakeApiServer:
             raise self._conflict(kind, name)
         want_uid = ((patch or {}).get("metadata") or {}).get("uid")
         if want_uid and want_uid != cur["metadata"].get("uid"):
-            # kube-apiserver's registry store: a UID in the new object that differs from the stored one
-            raise HTTPError(409, status_body(
-                409, "Conflict", f'Precondition failed: UID in precondition: {want_uid}, '
-                                 f'UID in object meta: {cur["metadata"].get("uid")}'))
+            # kube-apiserver: the patched object's metadata.uid changed, which update validation refuses (422); a
+            # PATCH carries no UID precondition (a PUT's object or a Binding does: 409)
+            raise HTTPError(422, status_body(
+                422, "Invalid", f'Pod "{name}" is invalid: metadata.uid: Invalid value: "{want_uid}": '
+                                f'field is immutable'))
         if kind == "pods" and self.faults.conflict_rate and self.faults.rng.random() < self.faults.conflict_rate:
             self.counts["injected_conflict"] += 1
             raise self._conflict(kind, name)

@@ -79,6 +79,27 @@ def test_optimistic_concurrency_exact_message_and_patch(impl):
 
 
 @IMPLS
+def test_patch_naming_another_uid_is_invalid_not_a_precondition(impl):
+    """a merge patch carrying metadata.uid has no UID precondition in kube-apiserver; the patched object's
+    changed uid fails update validation (422 Invalid, "field is immutable").  The device plugin's UID-guarded
+    ASSIGNED commit reads that as "re-created under its name" (dpcore.cc finish, plugin.py _land_commit)."""
+    async def go():
+        r, c = await _api(impl=impl)
+        try:
+            p = await c.create("pods", make_pod("a", 2))
+            ok = await c.patch("pods", "a", {"metadata": {"uid": p["metadata"]["uid"], "annotations": {"x": "1"}}},
+                               "default")
+            assert ok["metadata"]["annotations"]["x"] == "1"
+            with pytest.raises(ApiError) as ei:
+                await c.patch("pods", "a", {"metadata": {"uid": "not-the-uid", "annotations": {"x": "2"}}}, "default")
+            assert ei.value.status == 422 and "metadata.uid" in ei.value.message and "immutable" in ei.value.message
+        finally:
+            await c.close()
+            await r.stop()
+    run(go())
+
+
+@IMPLS
 def test_binding_copies_annotations_once(impl):
     async def go():
         r, c = await _api(impl=impl)
