@@ -58,9 +58,32 @@ log = logging.getLogger("gsx.deviceplugin")
 ID_SEP = "-_-"
 
 
-def fake_ids(dev: Device, units: int) -> list[str]:
-    base = dev.uuid or dev.bdf or f"gpu{dev.index}"
+def device_tag(dev: Device, width: int = 5) -> str:
+    """A short, stable name for a device in its fake IDs: base32 of a hash of its UUID (else BDF, else index).
+
+    kubelet sends every free ID of the node in each GetPreferredAllocation (8 x 287 on an MI355X node), so the ID
+    length is paid per admission: ``<uuid>-_-<k>`` made that ~100 KB a pod on real GPUs, ``<tag>-_-<k>`` ~25 KB.
+    Stable across restarts and re-enumeration (kubelet checkpoints the IDs its pods hold)."""
+    import base64
+    import hashlib
+
+    key = (dev.uuid or dev.bdf or f"gpu{dev.index}").encode()
+    return base64.b32encode(hashlib.blake2b(key, digest_size=8).digest()).decode().lower()[:width]
+
+
+def fake_ids(dev: Device, units: int, tag: str | None = None) -> list[str]:
+    base = tag or device_tag(dev)
     return [f"{base}{ID_SEP}{k}" for k in range(units)]
+
+
+def device_tags(devices) -> dict[int, str]:
+    """index -> tag for a node's devices, widened until no two collide."""
+    devices = list(devices)
+    for width in range(5, 14):
+        tags = {d.index: device_tag(d, width) for d in devices}
+        if len(set(tags.values())) == len(tags):
+            return tags
+    return {d.index: f"{device_tag(d, 13)}{d.index}" for d in devices}
 
 
 ALLOCATE_ATTEMPTS = 8  # per container request: transient apiserver failures retried with capped backoff
@@ -243,7 +266,8 @@ class GpuSharePlugin:
         """(Re)build everything derived from the device layout: fake IDs per GPU and the allocation state."""
         self.devices = {d.index: d for d in devices}
         self.units = {d.index: d.units(self.unit, self.reserve_bytes) for d in devices}
-        self.ids = {d.index: fake_ids(d, self.units[d.index]) for d in devices}
+        tags = device_tags(devices)
+        self.ids = {d.index: fake_ids(d, self.units[d.index], tags[d.index]) for d in devices}
         self.id_owner = {i: d for d, ids in self.ids.items() for i in ids}
         self.state = AllocationState(self.node, self.devices, self.profile)
         self.state.on_drop.append(self._record_dropped)

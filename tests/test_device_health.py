@@ -6,7 +6,7 @@ import asyncio
 import json
 
 from gpushare_scheduler_extender_amd.deviceplugin.devices import Device, apply_memory_pools
-from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin
+from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin, device_tags
 from gsxtools.kubeletapi import PluginClient
 from gpushare_scheduler_extender_amd.k8s.client import KubeClient
 from tests.fixtures.fakeapi import FakeApiServerRunner
@@ -61,7 +61,7 @@ def test_plugin_health_and_partition_change(tmp_path):
             mxdev.inject(1, "ras_umc_uncorrectable=1", backend)  # an HBM uncorrectable error on GPU 1
             upd = await next_list()
             bad = {d.ID.split("-_-")[0] for d in upd.devices if d.health == "Unhealthy"}
-            assert bad == {devs[1].uuid}, bad
+            assert bad == {device_tags(devs)[1]}, bad
             mxdev.inject(0, "thermal_throttle=1", backend)
             await asyncio.sleep(0.3)
             metrics = plugin.metrics_text()

@@ -123,7 +123,8 @@ def test_library_loads_into_any_container_userland():
     versions = {tuple(int(x) for x in v.split(".")) for v in re.findall(r"GLIBC_(\d+\.\d+(?:\.\d+)?)", t)}
     assert versions and max(versions) <= (2, 17), sorted(versions)
     exported = {ln.split()[-1] for ln in t.splitlines() if " g " in ln and ".text" in ln}
-    assert exported == {"OnLoad", "OnUnload", "gsx_isolate_stats", "gsx_isolate_scratch", "hsa_init"}, exported
+    assert exported == {"OnLoad", "OnUnload", "gsx_isolate_stats", "gsx_isolate_scratch", "gsx_isolate_scratch_queues",
+                        "hsa_init"}, exported
 
 
 def test_hsa_init_puts_the_tools_library_back(tmp_path):
