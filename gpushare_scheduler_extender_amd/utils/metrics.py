@@ -24,6 +24,10 @@ class _LedgerCollector:
                                   labels=["node", "device"])
         util = GaugeMetricFamily("gpushare_binpack_utilization", "sum(used)/sum(total) over gpushare nodes")
         pods = GaugeMetricFamily("gpushare_ledger_pods", "pods tracked by the ledger")
+        unacc = GaugeMetricFamily("gpushare_device_unaccounted_gpu_mem",
+                                  "gpu-mem the node's device plugin reports held by containers the annotations put "
+                                  "elsewhere (a kubelet swap not yet repaired); charged on top of the annotations",
+                                  labels=["node", "device"])
         su = st = 0
         for n in self.engine.node_names():
             for i, (t, u) in enumerate(self.engine.node_devices(n)):
@@ -31,6 +35,9 @@ class _LedgerCollector:
                 total.add_metric([n, str(i)], t)
                 su += u
                 st += t
+            if hasattr(self.engine, "node_unaccounted"):
+                for i, x in enumerate(self.engine.node_unaccounted(n)):
+                    unacc.add_metric([n, str(i)], x)
         util.add_metric([], (su / st) if st else 0.0)
         s = self.engine.stats()
         pods.add_metric([], s["pods"])
@@ -38,8 +45,12 @@ class _LedgerCollector:
         yield total
         yield util
         yield pods
+        yield unacc
         for k in ("filter_calls", "assume_ok", "assume_fail", "bind_ok", "bind_fail", "expired", "expiry_deferred",
-                  "overcommit_events", "pod_upserts", "pod_removes"):
+                  "overcommit_events", "pod_upserts", "pod_removes", "moves_ok", "moves_refused",
+                  "partner_claims_refused", "unaccounted_updates", "unaccounted_expired"):
+            if k not in s:
+                continue
             g = GaugeMetricFamily(f"gpushare_engine_{k}", f"native engine counter {k}")
             g.add_metric([], s[k])
             yield g

@@ -724,6 +724,8 @@ def test_plugin_endpoints_take_only_the_plugin_token_and_the_physical_floor_stee
             srv = json.loads((await http.request("GET", "/debug/engine")).body)["server"]
             assert srv["plugin_auth_denied"] == 4 and srv["token_reviews"] == 4  # the plugin's token reviewed once
             assert eng.node_unaccounted("n") == [100, 0]
+            metrics = (await http.request("GET", "/metrics")).body.decode()
+            assert 'gpushare_device_unaccounted_gpu_mem{device="0",node="n"} 100.0' in metrics, metrics[-2000:]
             # GPU 0's containers fill it (the annotations say empty): the bind goes to GPU 1, and after it a
             # 95-unit pod fits nowhere
             assert eng.assume("u1", "default", "p1", "n", 10)[0] == 1
