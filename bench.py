@@ -875,6 +875,7 @@ def main():
             raise RuntimeError(f"pod admission failed: {err}")
         t_run = time.perf_counter()
         insp = inspect_used()
+        t_insp = time.perf_counter()
         used = sum(n["usedGPU"] for n in insp["nodes"])
         total = sum(n["totalGPU"] for n in insp["nodes"])
         per_dev = [d["usedGPU"] for n in insp["nodes"] for d in n["devs"]]
@@ -885,9 +886,11 @@ def main():
                               1)[0]
         if st != 200:
             raise RuntimeError(f"delete collection failed: {st} {b[:200]!r}")
+        t_del = time.perf_counter()
         err = tracker.wait(keys, E.TRACK_GONE, 120)
         if err:
             raise RuntimeError(err)
+        t_gone = time.perf_counter()
         while sum(n["usedGPU"] for n in inspect_used()["nodes"]) != 0:
             if time.perf_counter() - t0 > 120:
                 raise TimeoutError("ledger did not drain")
@@ -895,7 +898,8 @@ def main():
         t_end = time.perf_counter()
         # per-pod scheduler timings are collected after the timed region (fetch_timings)
         return {"keys": keys, "used": used, "total": total, "per_dev": per_dev,
-                "t_bound": t_bound - t0, "t_run": t_run - t0, "t_total": t_end - t0, "t0": t0}
+                "t_bound": t_bound - t0, "t_run": t_run - t0, "t_total": t_end - t0, "t0": t0,
+                "teardown": (t_insp - t_run, t_del - t_insp, t_gone - t_del, t_end - t_gone)}
 
     async def fetch_timings(keys):
         # the scheduler process's per-pod timings (its own clock; only differences are used)
@@ -1119,6 +1123,10 @@ def main():
                         "total": round(1e3 * statistics.mean(s["t_total"] for s in step_stats), 3)},
             "wave_ms_p50": {k: round(1e3 * pct([s[t] for s in step_stats], 50), 3)
                             for k, t in (("bound", "t_bound"), ("running", "t_run"), ("total", "t_total"))},
+            # after Running: the /inspect read (binpack check), the DeleteCollection call, the wave driver's informer
+            # seeing every pod gone, the extender's ledger reading empty
+            "teardown_ms_mean": {k: round(1e3 * statistics.mean(s["teardown"][i] for s in step_stats), 3)
+                                 for i, k in enumerate(("inspect", "delete_call", "gone_seen", "ledger_empty"))},
             "wave_ms_max": {k: round(1e3 * max(s[t] for s in step_stats), 3)
                             for k, t in (("bound", "t_bound"), ("running", "t_run"), ("total", "t_total"))},
             # every timed wave: [bound, running, total] ms (where a slow wave lost its time)

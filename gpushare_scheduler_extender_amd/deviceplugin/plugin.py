@@ -73,7 +73,10 @@ def device_tag(dev: Device, width: int = 5) -> str:
 
 def fake_ids(dev: Device, units: int, tag: str | None = None) -> list[str]:
     base = tag or device_tag(dev)
-    return [f"{base}{ID_SEP}{k}" for k in range(units)]
+    # unit numbers zero-padded to one width, so a GPU's IDs sort as they are numbered (an Allocate's IDs arrive
+    # in that order and are recorded without a sort)
+    w = len(str(max(units - 1, 0)))
+    return [f"{base}{ID_SEP}{k:0{w}d}" for k in range(units)]
 
 
 def device_tags(devices) -> dict[int, str]:

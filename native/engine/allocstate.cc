@@ -455,7 +455,8 @@ void AllocState::later_container_allocated(const std::string& uid, int64_t units
 AllocRecord& AllocState::record(const std::string& uid, const std::vector<std::string>& ids_in, int64_t units,
                                 const std::string& cu_mask, const std::string& aid, double t, bool on_gpu) {
   std::vector<std::string> ids(ids_in);
-  std::sort(ids.begin(), ids.end());
+  // kubelet passes GetPreferredAllocation's pick back in the plugin's own (sorted) order: usually nothing to sort
+  if (!std::is_sorted(ids.begin(), ids.end())) std::sort(ids.begin(), ids.end());
   const std::string key = ids.empty() ? std::string() : id_key(ids);
   if (!ids.empty()) {
     auto old = by_ids_.find(key);

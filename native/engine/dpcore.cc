@@ -1,10 +1,12 @@
 #include "dpcore.h"
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -169,17 +171,58 @@ bool isolation_prepare(const std::string& host_dir, const std::string& uid, cons
 DpCore::DpCore(DpConfig cfg, AllocState* state) : cfg_(std::move(cfg)), state_(state) {
   if (!cfg_.api.server.empty()) api_ = std::make_unique<ApiClient>(cfg_.api);
   if (cfg_.early_answer && !cfg_.journal.empty()) {
-    jfd_ = ::open(cfg_.journal.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
-    if (jfd_ < 0) {
+    std::string err;
+    int fd = ::open(cfg_.journal.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+    if (fd < 0 || !journal_map(fd, &err)) {
+      if (fd < 0) err = std::strerror(errno);
       std::fprintf(stderr, "[gsx-dpcore] journal %s: %s; answering after the ASSIGNED patch instead\n",
-                   cfg_.journal.c_str(), std::strerror(errno));
+                   cfg_.journal.c_str(), err.c_str());
+      if (fd >= 0) ::close(fd);
       cfg_.early_answer = false;  // no durable record before the answer: keep the synchronous commit
     }
   }
 }
 
-DpCore::~DpCore() {
-  if (jfd_ >= 0) ::close(jfd_);
+DpCore::~DpCore() { journal_unmap(true); }
+
+bool DpCore::journal_map(int fd, std::string* err) {
+  struct stat st {};
+  if (::fstat(fd, &st) != 0) {
+    *err = std::string("fstat: ") + std::strerror(errno);
+    return false;
+  }
+  size_t used = static_cast<size_t>(st.st_size);
+  size_t cap = std::max(kJournalChunk, (used / kJournalChunk + 1) * kJournalChunk);
+  if (::ftruncate(fd, static_cast<off_t>(cap)) != 0) {
+    *err = std::string("ftruncate: ") + std::strerror(errno);
+    return false;
+  }
+  void* m = ::mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, 0);
+  if (m == MAP_FAILED) {
+    *err = std::string("mmap: ") + std::strerror(errno);
+    (void)!::ftruncate(fd, static_cast<off_t>(used));
+    return false;
+  }
+  // what an earlier process left: its whole lines (zeros past them, or a line torn by a crash mid-copy -- its
+  // Allocate was never answered -- are written over)
+  const char* b = static_cast<const char*>(m);
+  while (used > 0 && b[used - 1] != '\n') --used;
+  jfd_ = fd;
+  jmap_ = static_cast<char*>(m);
+  jcap_ = cap;
+  jlen_ = used;
+  return true;
+}
+
+void DpCore::journal_unmap(bool trim) {
+  if (jmap_) ::munmap(jmap_, jcap_);
+  if (jfd_ >= 0) {
+    if (trim) (void)!::ftruncate(jfd_, static_cast<off_t>(jlen_));
+    ::close(jfd_);
+  }
+  jmap_ = nullptr;
+  jfd_ = -1;
+  jcap_ = jlen_ = 0;
 }
 
 void DpCore::journal_append(const AllocRecord& r) {
@@ -200,9 +243,25 @@ void DpCore::journal_append(const AllocRecord& r) {
   line.append(",\"owner\":\"\",\"t\":").append(std::to_string(r.t)).append(",\"iso\":");
   json::append_quoted(&line, r.iso);
   line.append(",\"on_gpu\":").append(r.on_gpu ? "true" : "false").append("}\n");
-  // O_APPEND: one write per line, so a crash leaves whole lines (the page cache outlives this process)
-  ssize_t n = ::write(jfd_, line.data(), line.size());
-  (void)n;
+  if (jlen_ + line.size() > jcap_) {
+    // grow by whole chunks (a syscall pair per ~1,000 Allocates): the mapping is re-made over the longer file
+    const size_t cap = ((jlen_ + line.size()) / kJournalChunk + 1) * kJournalChunk;
+    void* m = ::ftruncate(jfd_, static_cast<off_t>(cap)) == 0
+                  ? ::mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, jfd_, 0)
+                  : MAP_FAILED;
+    if (m == MAP_FAILED) {
+      // the line still goes to the file (past the mapped bytes); the next append retries the growth
+      ssize_t n = ::pwrite(jfd_, line.data(), line.size(), static_cast<off_t>(jlen_));
+      if (n == static_cast<ssize_t>(line.size())) jlen_ += line.size();
+      return;
+    }
+    ::munmap(jmap_, jcap_);
+    jmap_ = static_cast<char*>(m);
+    jcap_ = cap;
+  }
+  // the page cache outlives this process: once copied, the line survives a crash of the plugin like a write(2)
+  std::memcpy(jmap_ + jlen_, line.data(), line.size());
+  jlen_ += line.size();
 }
 
 bool DpCore::journal_rotate(std::string* err) {
@@ -210,41 +269,56 @@ bool DpCore::journal_rotate(std::string* err) {
   const std::string& path = cfg_.journal;
   const std::string old = path + ".old";
   if (::access(old.c_str(), F_OK) != 0) {
-    // the common case: the journal becomes .old, a fresh journal takes the next Allocates
+    // the common case: the journal (trimmed to its lines) becomes .old, a fresh journal takes the next Allocates
+    int nfd = -1;
+    std::string e2;
     if (::rename(path.c_str(), old.c_str()) != 0) {
       *err = "rename " + path + ": " + std::strerror(errno);
       return false;
     }
-    int nfd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_APPEND | O_CLOEXEC, 0644);
+    nfd = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
     if (nfd < 0) {
       *err = "open " + path + ": " + std::strerror(errno);
       (void)::rename(old.c_str(), path.c_str());  // keep appending where we were
       return false;
     }
-    ::close(jfd_);
-    jfd_ = nfd;
+    const int ofd = jfd_;
+    char* omap = jmap_;
+    const size_t ocap = jcap_, olen = jlen_;
+    jfd_ = -1;
+    jmap_ = nullptr;
+    if (!journal_map(nfd, &e2)) {
+      ::close(nfd);
+      (void)::rename(old.c_str(), path.c_str());
+      jfd_ = ofd;
+      jmap_ = omap;
+      jcap_ = ocap;
+      jlen_ = olen;
+      *err = "map " + path + ": " + e2;
+      return false;
+    }
+    ::munmap(omap, ocap);
+    (void)!::ftruncate(ofd, static_cast<off_t>(olen));
+    ::close(ofd);
     return true;
   }
   // a previous checkpoint did not land: .old still holds records it was to cover; append this generation to it
-  int in = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
   int out = ::open(old.c_str(), O_WRONLY | O_APPEND | O_CLOEXEC);
-  bool ok = in >= 0 && out >= 0;
-  char buf[65536];
-  while (ok) {
-    ssize_t n = ::read(in, buf, sizeof buf);
+  size_t off = 0;
+  bool ok = out >= 0;
+  while (ok && off < jlen_) {
+    ssize_t n = ::write(out, jmap_ + off, jlen_ - off);
     if (n < 0 && errno == EINTR) continue;
-    if (n <= 0) {
-      ok = n == 0;
-      break;
-    }
-    ok = ::write(out, buf, static_cast<size_t>(n)) == n;
+    ok = n > 0;
+    if (ok) off += static_cast<size_t>(n);
   }
-  if (in >= 0) ::close(in);
   if (out >= 0) ::close(out);
-  if (!ok || ::ftruncate(jfd_, 0) != 0) {
+  if (!ok) {
     *err = "appending " + path + " to " + old + ": " + std::strerror(errno);
     return false;
   }
+  std::memset(jmap_, 0, jlen_);  // the generation lives in .old now
+  jlen_ = 0;
   return true;
 }
 
@@ -315,9 +389,17 @@ bool DpCore::preferred(const std::string& req, std::string* resp, std::string* w
     }
     std::vector<std::vector<std::string>> out(1);
     std::vector<std::string>& chosen = out[0];
+    chosen.reserve(static_cast<size_t>(std::max<int32_t>(size, 0)));
+    // the GPU's ID prefix looked up once, not per listed ID (the walk passes ~2,000 IDs of other GPUs)
+    auto pre = id_prefix_.find(static_cast<int>(want));
+    const std::string_view prefix = pre != id_prefix_.end() ? std::string_view(pre->second) : std::string_view();
+    auto on = [&](std::string_view id) {
+      if (id_prefix_.empty()) return id_on(id, static_cast<int>(want));
+      return !prefix.empty() && id.size() > prefix.size() && id.compare(0, prefix.size(), prefix) == 0;
+    };
     for (int pass = 0; pass < 2 && static_cast<int32_t>(chosen.size()) < size; ++pass) {
       dp::for_each_available(container, [&](std::string_view id) {
-        if (id_on(id, static_cast<int>(want)) == (pass == 0)) chosen.emplace_back(id);
+        if (on(id) == (pass == 0)) chosen.emplace_back(id);
         return static_cast<int32_t>(chosen.size()) < size;
       });
     }

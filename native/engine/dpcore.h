@@ -152,7 +152,15 @@ class DpCore {
   static constexpr std::string_view kIdSep = "-_-";  // deviceplugin/plugin.py: ID_SEP
   bool id_on(std::string_view id, int dev) const;
   uint64_t aid_ = 0;
-  int jfd_ = -1;  // the early-answer journal
+  // The early-answer journal: a MAP_SHARED mapping of the file (a line is durable against a crash of this process
+  // once copied in, as a write(2) to the page cache is, without a syscall per Allocate).  The file is sized ahead in
+  // kJournalChunk steps; bytes past jlen_ are zeros until it is trimmed (close, rotation).
+  int jfd_ = -1;
+  char* jmap_ = nullptr;
+  size_t jcap_ = 0, jlen_ = 0;
+  static constexpr size_t kJournalChunk = size_t(1) << 20;
+  bool journal_map(int fd, std::string* err);  // maps fd, jlen_ = its whole lines
+  void journal_unmap(bool trim);
   Stats stats_;
   void record_and_answer(DpPending& p, std::string* resp, DpEvent* ev);
   void journal_append(const AllocRecord& r);

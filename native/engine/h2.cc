@@ -399,6 +399,11 @@ bool Server::read_conn(Conn* c) {
     if (n > 0) {
       ssize_t r = g_lib.mem_recv(c->s, reinterpret_cast<const uint8_t*>(buf), static_cast<size_t>(n));
       if (r < 0) return false;
+      // a short read that completed a request drained the socket: no second recv just to meet EAGAIN (a syscall
+      // per kubelet call; the epoll registration is level-triggered, so bytes that land meanwhile wake the owner
+      // again).  A short read inside a request (a 25 KB GetPreferredAllocation arrives in several pieces while
+      // the sender still copies it in) reads on.
+      if (static_cast<size_t>(n) < sizeof buf && !ready_.empty()) return true;
       continue;
     }
     if (n == 0) return false;

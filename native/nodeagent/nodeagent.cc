@@ -300,7 +300,8 @@ class Agent {
                     "\"runtime\":%.3f,\"running_patch\":%.3f},\"mean_ms\":{\"queue\":%.4f,\"assign_patch\":%.4f,"
                     "\"runtime\":%.4f,\"running_patch\":%.4f},\"status_retries\":%llu,\"api_connects\":%llu,"
                     "\"plugin_calls_mean_ms\":{\"n\":%llu,\"slot_wait\":%.4f,\"get_preferred\":%.4f,\"allocate\":%.4f,"
-                    "\"encode_preferred\":%.4f,\"gap\":%.4f,\"n_gap\":%llu},"
+                    "\"encode_preferred\":%.4f,\"gap\":%.4f,\"n_gap\":%llu,\"gap_loop\":%.4f,\"gap_list\":%.4f,"
+                    "\"gap_handoff\":%.4f,\"relock\":%.4f,\"gap_kept\":%.4f,\"n_gap_kept\":%llu},"
                     "\"mismatch\":%llu,\"podresources_calls\":%llu,\"plugin_debug\":\"%s\",\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
                     (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
@@ -312,6 +313,11 @@ class Agent {
                     sum_dp_alloc_ / std::max<double>(1.0, dp_calls_) * 1e3,
                     sum_dp_enc_ / std::max<double>(1.0, dp_calls_) * 1e3,
                     sum_dp_gap_ / std::max<double>(1.0, n_dp_gap_) * 1e3, (unsigned long long)n_dp_gap_,
+                    sum_gap_loop_ / std::max<double>(1.0, n_dp_gap_) * 1e3,
+                    sum_gap_list_ / std::max<double>(1.0, n_dp_gap_) * 1e3,
+                    sum_gap_handoff_ / std::max<double>(1.0, n_dp_gap_) * 1e3,
+                    sum_dp_relock_ / std::max<double>(1.0, dp_calls_) * 1e3,
+                    sum_gap_kept_ / std::max<double>(1.0, n_gap_kept_) * 1e3, (unsigned long long)n_gap_kept_,
                     (unsigned long long)mismatch_,
                     (unsigned long long)pr_calls_.load(), plugin_debug_url().c_str());
       rep.body = b;
@@ -478,7 +484,9 @@ class Agent {
       // it holds the slot (taken under mu_, never waited for: a worker that popped first but reached the slot later
       // would reorder the Allocates), and with the plugin it keeps the slot for the next pod, leaving the start of
       // the one it admitted to another worker (starts_): admissions follow each other with no thread hand-off
+      const bool kept = slot.owns_lock();  // still holding the slot from this worker's previous admission
       if (!queue_.empty() && (!serial || slot.owns_lock() || slot.try_lock())) {
+        admit_kept_ = kept;
         std::string key = std::move(queue_.front());
         queue_.pop_front();
         auto kit = keys_.find(key);
@@ -601,6 +609,7 @@ class Agent {
   // `slot`: the admission slot (held when admissions are serial); given up once the Allocate is answered, as
   // kubelet's pod workers start containers after admission, in parallel
   void admit_via_plugin_locked(std::string key, std::unique_lock<std::mutex>& lk, std::unique_lock<std::mutex>* slot) {
+    const double te = now_s();  // gap split: loop + pop before this, the free-ID list after it
     const AllocPod* mine = state_->pod_by_key(key);
     if (!mine) return;
     const std::string my_uid = mine->uid, my_key = key;
@@ -630,6 +639,7 @@ class Agent {
       delayed_.push_back({now_s() + 0.01, key});
       return;
     }
+    const double tl = now_s();
     state_->set_inflight(my_uid, true);
     const double t0 = seen_.count(my_uid) ? seen_[my_uid] : now_s();
     const double prev_done = last_admitted_;
@@ -676,6 +686,7 @@ class Agent {
       if (slot && slot->owns_lock()) slot->unlock();
     };
     lk.lock();
+    sum_dp_relock_ += now_s() - tp1;  // taking the agent's lock back after the Allocate (pod watch, pod workers)
     dp_calls_++;
     sum_dp_slot_ += ts - tp0;  // waiting for the admission slot (another pod's calls)
     sum_dp_pref_ += tpref - ts;
@@ -683,7 +694,14 @@ class Agent {
     sum_dp_enc_ += tenc;
     if (prev_done > 0 && ts - prev_done < 0.002) {  // back to back: from the last admission's end to this one's calls
       sum_dp_gap_ += ts - prev_done;
+      sum_gap_loop_ += te - prev_done;
+      sum_gap_list_ += tl - te;
+      sum_gap_handoff_ += ts - tl;
       n_dp_gap_++;
+      if (admit_kept_) {
+        sum_gap_kept_ += ts - prev_done;
+        n_gap_kept_++;
+      }
     }
     state_->set_inflight(my_uid, false);
     if (!ok) {
@@ -1150,6 +1168,12 @@ class Agent {
   double sum_queue_ = 0, sum_patch_ = 0, sum_runtime_ = 0, sum_status_ = 0;  // over admitted_ pods
   uint64_t dp_calls_ = 0;  // GetPreferredAllocation + Allocate pairs to the plugin (--plugin-socket / --plugin-spawn)
   double sum_dp_slot_ = 0, sum_dp_pref_ = 0, sum_dp_alloc_ = 0, sum_dp_enc_ = 0, sum_dp_gap_ = 0;
+  // the gap split: record + start queued + worker loop + pop (loop), free-ID list (list), unlock + wake (handoff)
+  double sum_gap_loop_ = 0, sum_gap_list_ = 0, sum_gap_handoff_ = 0, sum_dp_relock_ = 0;
+  // back-to-back admissions by the worker that kept the slot (no queue-empty release in between)
+  double sum_gap_kept_ = 0;
+  uint64_t n_gap_kept_ = 0;
+  bool admit_kept_ = false;
   uint64_t n_dp_gap_ = 0;
   double last_admitted_ = 0;  // when the last admission's IDs were recorded
   std::vector<std::thread> workers_;
