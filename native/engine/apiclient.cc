@@ -81,6 +81,12 @@ ApiClient::~ApiClient() {
   if (ctx_) SSL_CTX_free(ctx_);
 }
 
+void ApiClient::abort() {
+  std::lock_guard<std::mutex> g(mu_);
+  aborted_ = true;
+  for (int fd : busy_) ::shutdown(fd, SHUT_RDWR);
+}
+
 void ApiClient::close_conn(Conn* c) {
   if (c->ssl) {
     SSL_shutdown(c->ssl);
@@ -380,12 +386,32 @@ bool ApiClient::request(const std::string& method, const std::string& path, cons
                                  !body.empty() || method == "POST" || method == "PUT" || method == "PATCH");
   req.append(body);
 
+  // a request in flight is listed (abort() shuts its socket) until its connection is released
+  auto done = [this](Conn* c, bool reuse) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      busy_.erase(std::remove(busy_.begin(), busy_.end(), c->fd), busy_.end());
+      reuse = reuse && !aborted_;
+    }
+    release(c, reuse);
+  };
   for (int attempt = 0; attempt < 2; ++attempt) {
     Conn* c = acquire(err);
     if (!c) return false;
+    bool aborted;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      aborted = aborted_;
+      if (!aborted) busy_.push_back(c->fd);
+    }
+    if (aborted) {
+      release(c, false);
+      *err = "apiserver client closed";
+      return false;
+    }
     bool fresh_fail = false;
     if (!send_all(c, req)) {
-      release(c, false);
+      done(c, false);
       if (attempt == 0) continue;  // stale keep-alive connection: retry once on a new one
       *err = "send to apiserver failed";
       return false;
@@ -399,7 +425,7 @@ bool ApiClient::request(const std::string& method, const std::string& path, cons
       long got = parser.parse(c->rbuf.data(), c->rbuf.size(), &m, &perr);
       if (got > 0) break;
       if (got < 0) {
-        release(c, false);
+        done(c, false);
         *err = "bad response from apiserver: " + perr;
         return false;
       }
@@ -417,7 +443,7 @@ bool ApiClient::request(const std::string& method, const std::string& path, cons
       c->rbuf.append(buf, static_cast<size_t>(r));
     }
     if (m.status == 0) {
-      release(c, false);
+      done(c, false);
       if (fresh_fail && attempt == 0) continue;
       *err = "apiserver closed the connection";
       return false;
@@ -429,7 +455,7 @@ bool ApiClient::request(const std::string& method, const std::string& path, cons
       *resp_content_type = ct ? *ct : std::string();
     }
     *resp = std::move(m.body);
-    release(c, m.keep_alive && !m.body_until_close);
+    done(c, m.keep_alive && !m.body_until_close);
     return true;
   }
   *err = "apiserver request failed";

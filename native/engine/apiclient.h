@@ -61,6 +61,10 @@ class ApiClient {
               const std::function<bool(std::string_view)>& on_data, std::string* err, StreamHandle* h,
               double idle_timeout_s);
 
+  // The owner is closing: the sockets of requests in flight are shut (they fail with a transport error at once
+  // instead of waiting out a slow apiserver) and later requests fail without connecting.
+  void abort();
+
   uint64_t requests() const { return requests_; }
   uint64_t reconnects() const { return reconnects_; }
 
@@ -90,6 +94,8 @@ class ApiClient {
   std::string init_err_;
   std::mutex mu_;
   std::vector<Conn*> idle_;
+  std::vector<int> busy_;  // fds of requests in flight (guarded by mu_), for abort()
+  bool aborted_ = false;   // guarded by mu_
   std::atomic<uint64_t> requests_{0}, reconnects_{0};
 };
 

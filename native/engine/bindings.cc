@@ -1095,6 +1095,7 @@ class PyDpServer {
   }
 
   void close() {
+    if (core_) core_->abort_requests();
     stop_serving();
     if (feed_r_) feed_r_->stop();
     stop_worker();
@@ -1105,6 +1106,7 @@ class PyDpServer {
       srv_->poll();
     }
     srv_.reset();
+    if (core_) core_->journal_close();
   }
 
  private:

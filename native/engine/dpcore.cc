@@ -205,8 +205,10 @@ bool DpCore::journal_map(int fd, std::string* err) {
   }
   // what an earlier process left: its whole lines (zeros past them, or a line torn by a crash mid-copy -- its
   // Allocate was never answered -- are written over)
-  const char* b = static_cast<const char*>(m);
+  char* b = static_cast<char*>(m);
   while (used > 0 && b[used - 1] != '\n') --used;
+  // a torn tail is cleared, so a shorter line written over it leaves no fragment behind
+  std::memset(b + used, 0, static_cast<size_t>(st.st_size) - used);
   jfd_ = fd;
   jmap_ = static_cast<char*>(m);
   jcap_ = cap;

@@ -137,6 +137,13 @@ class DpCore {
   // under the state lock, so no Allocate falls between the records snapshot and the rotation.
   bool journal_rotate(std::string* err);
   bool journaling() const { return jfd_ >= 0; }
+  // the mapping trimmed to its lines and closed (the endpoint is closing: no Allocate is answered after this)
+  void journal_close() { journal_unmap(true); }
+  // closing: an ASSIGNED commit in flight fails at once instead of waiting out the apiserver (an early-answered one
+  // is in the journal, and the restarted plugin lands it)
+  void abort_requests() {
+    if (api_) api_->abort();
+  }
   const std::string& journal_path() const { return cfg_.journal; }
   int64_t physical_used(int dev) const;
   bool ids_on(const std::vector<std::string>& ids, int dev) const;

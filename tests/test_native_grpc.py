@@ -233,6 +233,77 @@ def _journal_lines(path: str) -> list:
         return [ln for ln in f.read().rstrip(b"\0").splitlines() if ln.strip(b"\0")]
 
 
+def test_mapped_journal_survives_a_torn_tail_and_is_trimmed_on_close():
+    """The journal is a shared mapping sized ahead (dpcore.cc journal_map): a crash can leave a line torn mid-copy
+    and zeros after it.  A restarted plugin keeps the whole lines, writes over the torn one, and a closed endpoint
+    leaves the file trimmed to whole JSON lines."""
+    async def go():
+        tmp = tempfile.mkdtemp()
+        os.environ["GSX_PLUGIN_EARLY_ANSWER"] = "1"
+        try:
+            api_srv, client, plugin = await _plugin(tmp, fast=True)
+            a = await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
+            await client.create("pods", bound_pod("b", 4, dev=0, assume=2, dev_total=16))
+            await plugin.stop()
+            ids = fake_ids(plugin.devices[0], 16)
+            whole = json.dumps({"aid": "x-1", "uid": a["metadata"]["uid"], "ids": sorted(ids[0:4]), "dev": 0,
+                                "units": 4, "cu_mask": "", "owner": "", "t": 0.0, "iso": ""}) + "\n"
+            with open(plugin.journal_path, "wb") as f:  # a whole line, a line torn by a crash, the mapping's zeros
+                f.write(whole.encode() + b'{"aid":"x-2","uid":"torn-line-with-no-end' + b"\0" * 4096)
+            again = GpuSharePlugin(client, "n1", fake_devices("2x16GiB"), P, socket_dir=os.path.join(tmp, "dp"))
+            await again.start(register=False)
+        finally:
+            os.environ.pop("GSX_PLUGIN_EARLY_ANSWER", None)
+        pc = PluginClient(again.socket_path)
+        try:
+            assert again.stats.get("commits_after_restart") == 1  # the whole line was read, the torn one skipped
+            r = (await pc.allocate([ids[4:8]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "b"
+            lines = _journal_lines(again.journal_path)
+            assert all(json.loads(ln)["uid"] != "torn-line-with-no-end" for ln in lines)
+        finally:
+            await _close(api_srv, client, again, pc)
+        with open(again.journal_path, "rb") as f:
+            raw = f.read()
+        assert b"\0" not in raw and b"torn-line" not in raw, raw[-200:]
+        assert all(json.loads(ln) for ln in raw.splitlines())
+    asyncio.run(go())
+
+
+def test_closing_the_endpoint_does_not_wait_out_a_commit_in_flight():
+    """An early-answered commit stuck on a slow apiserver: closing the native endpoint shuts its socket
+    (ApiClient::abort) instead of waiting for the request to time out; the record stays in the journal."""
+    async def go():
+        tmp = tempfile.mkdtemp()
+        os.environ["GSX_PLUGIN_EARLY_ANSWER"] = "1"
+        try:
+            api_srv, client, plugin = await _plugin(tmp, fast=True)
+        finally:
+            os.environ.pop("GSX_PLUGIN_EARLY_ANSWER", None)
+        pc = PluginClient(plugin.socket_path)
+        try:
+            await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
+            await asyncio.sleep(0.3)
+            api_srv.server.faults.latency_ms = 30000.0  # the commit's PATCH now waits 30 s for its answer
+            r = (await pc.allocate([fake_ids(plugin.devices[0], 16)[0:4]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "a"
+            await asyncio.sleep(0.2)  # the commit is in flight
+            t0 = asyncio.get_running_loop().time()
+            await pc.close()
+            await plugin.stop()
+            assert asyncio.get_running_loop().time() - t0 < 5.0
+            lines = _journal_lines(plugin.journal_path) + _journal_lines(plugin.journal_path + ".old") \
+                if os.path.exists(plugin.journal_path + ".old") else _journal_lines(plugin.journal_path)
+            with open(plugin.checkpoint) as f:
+                recs = json.load(f)["records"]
+            assert recs or lines  # the answered Allocate is on disk for the next start
+        finally:
+            api_srv.server.faults.latency_ms = 0.0
+            await client.close()
+            await api_srv.stop()
+    asyncio.run(go())
+
+
 def test_early_answer_commit_lands_after_a_restart():
     """The plugin went away between an early answer and its commit: the journal still holds the record, the pod
     still reads ASSIGNED=false.  A restarted plugin lands the commit before it serves, and never offers the pod
