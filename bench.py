@@ -956,6 +956,10 @@ def main():
             gc.collect()
             gc.freeze()
             gc.disable()
+            # dirty page cache left by what ran before (a test session, the build) is written back now, not by the
+            # flusher inside the ~10 ms region: a first bench on a fresh box read 3.8 ms of IO pressure and one
+            # 10 ms wave there (profiles/r05_final/bench.1.json)
+            os.sync()
         if step == a.warmup:
             if rank == 0:
                 ext0 = extender_counters()
