@@ -1087,14 +1087,24 @@ class GpuSharePlugin:
             await self._server.stop(0)
             self._server = None
         reuse = self._native is not None and not self._native_serving
+        reserve = self._native is not None and self._native_serving  # kubelet restarted: a new endpoint
         if not reuse:
             self._close_native()
+        if reserve:
+            # commits of Allocates the closed endpoint answered early but had not landed (queued, or in flight and
+            # cut off by the close) are in the journal; land them as a restarted plugin does
+            self._journaled = list(self.state.records.values())
         ok, why = native_grpc_available()
         if ok:
             if not reuse:
                 self._open_native()
             self._native_serving = True
             self._sync_native()
+            if reserve:
+                # in the background: the pods are still claimed in the state, so serving need not wait for a slow
+                # apiserver (a commit that fails is retried with backoff while its pod exists)
+                t = asyncio.get_running_loop().create_task(self.commit_unlanded())
+                self._tasks.append(t)
             self._native.set_ready(True)
             if os.environ.get("GSX_PLUGIN_SERVE_THREAD", "1") == "1":
                 # the endpoint is served from a native thread that never needs the GIL (a native lock guards the

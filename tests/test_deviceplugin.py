@@ -407,6 +407,57 @@ def test_plugin_reregisters_after_kubelet_restart():
     run(go())
 
 
+def test_kubelet_restart_lands_an_early_answered_commit_the_old_endpoint_dropped(monkeypatch):
+    """An Allocate answered early, its ASSIGNED commit still failing (retried with backoff by the endpoint's worker)
+    when kubelet restarts: the plugin's re-serve closes the old endpoint, whose queued retries go with it, and lands
+    the journaled commit itself."""
+    monkeypatch.setenv("GSX_PLUGIN_EARLY_ANSWER", "1")
+
+    async def go():
+        api_srv = await FakeApiServerRunner().start()
+        client = KubeClient(api_srv.url)
+        d = tempfile.mkdtemp(prefix="gsx-dp-")
+        kubelet = FakeKubelet(d)
+        await kubelet.start()
+        await client.create("nodes", make_node("n1", 32, 0))
+        plugin = GpuSharePlugin(client, "n1", fake_devices("2x16GiB"), P, socket_dir=d)
+        await plugin.start(publish=False)
+        kubelet2 = None
+        try:
+            await asyncio.wait_for(kubelet.registered.wait(), 5)
+            if plugin.grpc_impl != "native":
+                pytest.skip("the early answer is the native endpoint's")
+            await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
+            await asyncio.sleep(0.3)
+            api_srv.server.faults.error_rate = 1.0  # the commit's PATCH fails: the endpoint retries it with backoff
+            pc = PluginClient(plugin.socket_path)
+            r = (await pc.allocate([fake_ids(plugin.devices[0], 16)[0:4]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "a"
+            await pc.close()
+            await asyncio.sleep(0.1)  # the commit is queued for its next attempt
+            await kubelet.stop()
+            kubelet2 = FakeKubelet(d)
+            await kubelet2.start()
+            await asyncio.wait_for(kubelet2.registered.wait(), 10)
+            api_srv.server.faults.error_rate = 0.0
+            ann = {}
+            for _ in range(100):  # within ~5 s (the old endpoint's retries went with it)
+                ann = (await client.get("pods", "a", "default"))["metadata"]["annotations"]
+                if ann.get(P.annotation_assigned) == "true":
+                    break
+                await asyncio.sleep(0.05)
+            assert ann.get(P.annotation_assigned) == "true", ann
+        finally:
+            api_srv.server.faults.error_rate = 0.0
+            await plugin.stop()
+            if kubelet2 is not None:
+                await kubelet2.stop()
+            await client.close()
+            await api_srv.stop()
+
+    run(go())
+
+
 def test_plugin_allocate_retries_conflicts_and_apiserver_errors():
     """kubelet's Allocate must not fail over transient apiserver trouble: 409s and 500s on the ASSIGNED patch
     are retried from a fresh LIST; every pod still ends up ASSIGNED=true exactly once."""
