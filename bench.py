@@ -600,16 +600,21 @@ def main():
     if a.pin_widths:
         widths.update(json.loads(a.pin_widths))
     mode = a.pin if a.pin != "auto" else "spread"
+    # the chain of round trips shares one L3 domain: rank 0, apiserver, extender, scheduler, node agent AND the
+    # plugin (kubelet's two calls per admission).  With the plugin left out (round 5 until session 17) it landed in
+    # another CCD whenever the first one was full: N = 8 read 12.1-13.1k pods/s with node agent and plugin in one
+    # L3 domain, 9.8-11.8k across two (profiles/r05_session18/)
+    local = int(os.environ.get("GSX_PIN_LOCAL", "0")) or names.index("plugin") + 1  # (env: A/B only)
     if world > 1 and mode != "none":
         # one plan for the whole job (the ranks' load samples would differ): keyed by the torchrun agent
         key = f"{os.getppid()}-{os.environ.get('MASTER_PORT', '0')}"
-        cpu_plan = shared_plan(names, widths, mode, key, smt=bool(a.pin_smt), local=5)
+        cpu_plan = shared_plan(names, widths, mode, key, smt=bool(a.pin_smt), local=local)
         if rank == 0:
             import atexit
 
             atexit.register(forget_shared_plan, key)
     else:
-        cpu_plan = plan(names, widths, mode, smt=bool(a.pin_smt), local=5)
+        cpu_plan = plan(names, widths, mode, smt=bool(a.pin_smt), local=local)
     mine_cpus = cpu_plan.get(f"rank{rank}")
     a.plugin_cpus = cpu_plan.get("plugin")
     runtime_cpus = None
@@ -866,6 +871,7 @@ def main():
         names, keys, reqs = wave_requests(step)
         t0 = time.perf_counter()
         res = api_batch.run(reqs, min(CREATE_CONCURRENCY, n_pods))
+        t_created = time.perf_counter()
         bad = [(st, b[:200]) for st, b in res if st != 201]
         if bad:
             raise RuntimeError(f"pod create failed: {bad[:3]}")
@@ -903,7 +909,7 @@ def main():
         # per-pod scheduler timings are collected after the timed region (fetch_timings)
         return {"keys": keys, "used": used, "total": total, "per_dev": per_dev,
                 "t_bound": t_bound - t0, "t_run": t_run - t0, "t_total": t_end - t0, "t0": t0,
-                "teardown": (t_insp - t_run, t_del - t_insp, t_gone - t_del, t_end - t_gone)}
+                "teardown": (t_insp - t_run, t_del - t_insp, t_gone - t_del, t_end - t_gone), "t_created": t_created - t0}
 
     async def fetch_timings(keys):
         # the scheduler process's per-pod timings (its own clock; only differences are used)
@@ -1133,6 +1139,8 @@ def main():
                             for k, t in (("bound", "t_bound"), ("running", "t_run"), ("total", "t_total"))},
             # after Running: the /inspect read (binpack check), the DeleteCollection call, the wave driver's informer
             # seeing every pod gone, the extender's ledger reading empty
+            # the load generator's creates of one wave (every POST answered)
+            "create_ms_mean": round(1e3 * statistics.mean(s["t_created"] for s in step_stats), 3),
             "teardown_ms_mean": {k: round(1e3 * statistics.mean(s["teardown"][i] for s in step_stats), 3)
                                  for i, k in enumerate(("inspect", "delete_call", "gone_seen", "ledger_empty"))},
             "wave_ms_max": {k: round(1e3 * max(s[t] for s in step_stats), 3)

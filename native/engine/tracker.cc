@@ -102,29 +102,72 @@ std::string PodTracker::wait(const std::vector<std::string>& keys, int cond, dou
   }
 }
 
-std::vector<std::pair<int, std::string>> BatchClient::run(
-    const std::vector<std::tuple<std::string, std::string, std::string>>& reqs, int concurrency) {
-  std::vector<std::pair<int, std::string>> out(reqs.size());
-  std::atomic<size_t> next{0};
-  auto work = [&] {
-    while (true) {
-      size_t i = next.fetch_add(1);
-      if (i >= reqs.size()) return;
-      int status = 0;
-      std::string body, err;
-      const auto& r = reqs[i];
-      if (api_.request(std::get<0>(r), std::get<1>(r), std::get<2>(r), "application/json", &status, &body, &err)) {
-        out[i] = {status, std::move(body)};
-      } else {
-        out[i] = {-1, err};
-      }
+BatchClient::~BatchClient() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : helpers_) t.join();
+}
+
+void BatchClient::work_on(const std::vector<Req>& reqs, std::vector<std::pair<int, std::string>>* out) {
+  while (true) {
+    size_t i = next_.fetch_add(1);
+    if (i >= reqs.size()) return;
+    int status = 0;
+    std::string body, err;
+    const auto& r = reqs[i];
+    if (api_.request(std::get<0>(r), std::get<1>(r), std::get<2>(r), "application/json", &status, &body, &err)) {
+      (*out)[i] = {status, std::move(body)};
+    } else {
+      (*out)[i] = {-1, err};
     }
-  };
-  int n = std::max(1, std::min<int>(concurrency, static_cast<int>(reqs.size())));
-  std::vector<std::thread> ts;
-  for (int t = 1; t < n; ++t) ts.emplace_back(work);
-  work();
-  for (auto& t : ts) t.join();
+  }
+}
+
+void BatchClient::helper(int me) {
+  uint64_t seen = 0;
+  std::unique_lock<std::mutex> lk(mu_);
+  while (true) {
+    cv_.wait(lk, [&] { return stop_ || (gen_ != seen && me < want_); });
+    if (stop_) return;
+    seen = gen_;
+    const std::vector<Req>* reqs = reqs_;
+    auto* out = out_;
+    ++busy_;
+    lk.unlock();
+    work_on(*reqs, out);
+    lk.lock();
+    if (--busy_ == 0) done_cv_.notify_all();
+  }
+}
+
+std::vector<std::pair<int, std::string>> BatchClient::run(const std::vector<Req>& reqs, int concurrency) {
+  std::lock_guard<std::mutex> one(run_mu_);  // one batch at a time
+  std::vector<std::pair<int, std::string>> out(reqs.size());
+  const int n = std::max(1, std::min<int>(concurrency, static_cast<int>(reqs.size())));
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    while (static_cast<int>(helpers_.size()) < n - 1) {
+      const int k = static_cast<int>(helpers_.size());
+      helpers_.emplace_back([this, k] { helper(k); });
+    }
+    reqs_ = &reqs;
+    out_ = &out;
+    next_.store(0);
+    want_ = n - 1;
+    ++gen_;
+  }
+  if (n > 1) cv_.notify_all();
+  work_on(reqs, &out);
+  std::unique_lock<std::mutex> lk(mu_);
+  // every helper that joined this batch has finished its request before `out` goes out of scope; one that wakes
+  // late finds the batch taken (next_ past the end) and leaves at once
+  done_cv_.wait(lk, [&] { return busy_ == 0; });
+  want_ = 0;
+  reqs_ = nullptr;
+  out_ = nullptr;
   return out;
 }
 

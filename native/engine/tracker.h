@@ -8,10 +8,12 @@
 //                keep-alive connection pool (the wave's pod creates).
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <unordered_map>
 #include <vector>
@@ -46,13 +48,28 @@ class PodTracker {
 
 class BatchClient {
  public:
+  using Req = std::tuple<std::string, std::string, std::string>;
   explicit BatchClient(const ApiConfig& cfg) : api_(cfg) {}
-  // (method, path, body) -> (status or -1, response body / transport error)
-  std::vector<std::pair<int, std::string>> run(
-      const std::vector<std::tuple<std::string, std::string, std::string>>& reqs, int concurrency);
+  ~BatchClient();
+  // (method, path, body) -> (status or -1, response body / transport error).  The helper threads are kept between
+  // calls (a wave's creates used to start and join up to 15 threads inside the timed wave)
+  std::vector<std::pair<int, std::string>> run(const std::vector<Req>& reqs, int concurrency);
 
  private:
+  void work_on(const std::vector<Req>& reqs, std::vector<std::pair<int, std::string>>* out);
+  void helper(int me);
+
   ApiClient api_;
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> helpers_;
+  // the batch in progress: helpers with index < want_ join it
+  const std::vector<Req>* reqs_ = nullptr;
+  std::vector<std::pair<int, std::string>>* out_ = nullptr;
+  std::atomic<size_t> next_{0};
+  uint64_t gen_ = 0;
+  int want_ = 0, busy_ = 0;
+  bool stop_ = false;
 };
 
 }  // namespace gsx

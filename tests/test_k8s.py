@@ -710,3 +710,60 @@ def test_python_informer_and_native_reflector_agree_under_churn():
             await c.close()
             await r.stop()
     run(go())
+
+
+def test_batch_client_keeps_its_helper_threads_and_answers_in_order():
+    """The wave driver's BatchClient (native/engine/tracker.cc): batches of mixed concurrency answer every request
+    in its slot, and the helper threads are started once, not per batch (the server runs in its own process, so
+    this process's thread count is the client's)."""
+    import subprocess
+    import sys
+    import time
+
+    from gpushare_scheduler_extender_amd.core.controller import api_dict
+    from gpushare_scheduler_extender_amd.core.engine import native
+    from gpushare_scheduler_extender_amd.k8s.client import KubeConfig
+
+    server = r"""
+import http.server, sys
+class H(http.server.BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+    def do_POST(self):
+        n = int(self.headers.get("Content-Length", "0"))
+        body = self.rfile.read(n) + self.path.encode()
+        self.send_response(201)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(body)))
+        self.end_headers()
+        self.wfile.write(body)
+    def log_message(self, *a):
+        pass
+srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+print(srv.server_address[1], flush=True)
+srv.serve_forever()
+"""
+    proc = subprocess.Popen([sys.executable, "-c", server], stdout=subprocess.PIPE, text=True)
+
+    def threads() -> int:
+        return len(os.listdir("/proc/self/task"))
+
+    try:
+        port = int(proc.stdout.readline())
+        bc = native().BatchClient(api_dict(KubeConfig(server=f"http://127.0.0.1:{port}")))
+        before, base = threads(), None
+        for k in range(30):
+            conc = (1, 4, 16)[k % 3]
+            reqs = [("POST", f"/p/{k}/{i}", f"b{i}".encode()) for i in range(5 + k)]
+            out = bc.run(reqs, conc)
+            assert [st for st, _ in out] == [201] * len(reqs)
+            assert [body for _, body in out] == [f"b{i}/p/{k}/{i}".encode() for i in range(5 + k)]
+            if k == 11:
+                base = threads()  # 16 requests at concurrency 16: every helper this client will have exists now
+                assert base - before == 15, (before, base)  # they outlive the batch
+        assert threads() == base, (threads(), base)
+        t0 = time.monotonic()
+        del bc  # the helpers are joined
+        assert time.monotonic() - t0 < 5.0
+    finally:
+        proc.kill()
+        proc.wait()
