@@ -305,13 +305,15 @@ bool DpCore::journal_rotate(std::string* err) {
     return true;
   }
   // a previous checkpoint did not land: .old still holds records it was to cover; append this generation to it
+  // (read back from the file: lines past the mapping, written when growing it failed, are in the file only)
   int out = ::open(old.c_str(), O_WRONLY | O_APPEND | O_CLOEXEC);
   size_t off = 0;
   bool ok = out >= 0;
+  char buf[65536];
   while (ok && off < jlen_) {
-    ssize_t n = ::write(out, jmap_ + off, jlen_ - off);
+    ssize_t n = ::pread(jfd_, buf, std::min(sizeof buf, jlen_ - off), static_cast<off_t>(off));
     if (n < 0 && errno == EINTR) continue;
-    ok = n > 0;
+    ok = n > 0 && ::write(out, buf, static_cast<size_t>(n)) == n;
     if (ok) off += static_cast<size_t>(n);
   }
   if (out >= 0) ::close(out);
@@ -319,7 +321,8 @@ bool DpCore::journal_rotate(std::string* err) {
     *err = "appending " + path + " to " + old + ": " + std::strerror(errno);
     return false;
   }
-  std::memset(jmap_, 0, jlen_);  // the generation lives in .old now
+  std::memset(jmap_, 0, std::min(jlen_, jcap_));  // the generation lives in .old now
+  if (jlen_ > jcap_) (void)!::ftruncate(jfd_, static_cast<off_t>(jcap_));  // the unmapped lines went too
   jlen_ = 0;
   return true;
 }
