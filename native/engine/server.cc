@@ -548,7 +548,10 @@ void NativeServer::pool_main() {
         resp = do_bind(j.req);
         stats_.bind_lat.observe(mono() - j.t0);
       } else if (j.kind == 2 || j.kind == 3) {
-        if (plugin_authorized(j.req, &resp)) resp = j.kind == 2 ? do_move(j.req) : do_physical(j.req);
+        std::string token_node;
+        if (plugin_authorized(j.req, &resp, &token_node)) {
+          resp = j.kind == 2 ? do_move(j.req, token_node) : do_physical(j.req, token_node);
+        }
       } else {
         resp = do_proxy(j.req);
       }
@@ -844,7 +847,7 @@ bool NativeServer::lookup_pod(const std::string& ns, const std::string& name, co
 //
 //   {"namespace","name","uid","node","resourceVersion","from","to","partner","annotations":{k: "v" | null}}
 //   -> 200 {"Error":"","to":N,"pod":{...}} | 409 {"Error":"..."} | 4xx/5xx {"Error":"..."}
-std::string NativeServer::do_move(const http::Message& req) {
+std::string NativeServer::do_move(const http::Message& req, const std::string& token_node) {
   auto answer = [](int status, const std::string& body) { return http::response(status, "application/json", body, true); };
   if (!binds_enabled_.load()) return answer(503, error_body("this extender replica is not the leader"));
   if (!api_) return answer(501, error_body("no apiserver client"));
@@ -856,6 +859,10 @@ std::string NativeServer::do_move(const http::Message& req) {
       !arg_str(d, "node", &node) || !arg_str(d, "resourceVersion", &rv) || !arg_str(d, "partner", &partner) ||
       ns.empty() || name.empty() || uid.empty() || node.empty() || rv.empty()) {
     return answer(400, error_body("move needs namespace, name, uid, node and resourceVersion"));
+  }
+  if (!token_node.empty() && token_node != node) {  // the ledger checks the pod is on `node`
+    stats_.plugin_auth_denied.fetch_add(1, std::memory_order_relaxed);
+    return answer(403, error_body("the caller's token is bound to node " + token_node + ", not " + node));
   }
   MoveRequest m;
   m.uid = uid;
@@ -943,7 +950,7 @@ std::string NativeServer::do_move(const http::Message& req) {
   return answer(200, out);
 }
 
-bool NativeServer::plugin_authorized(const http::Message& req, std::string* resp) {
+bool NativeServer::plugin_authorized(const http::Message& req, std::string* resp, std::string* token_node) {
   if (cfg_.plugin_auth != "tokenreview") return true;
   auto deny = [&](int status, const std::string& msg) {
     stats_.plugin_auth_denied.fetch_add(1, std::memory_order_relaxed);
@@ -959,9 +966,28 @@ bool NativeServer::plugin_authorized(const http::Message& req, std::string* resp
   {
     std::lock_guard<std::mutex> g(amu_);
     auto it = authz_cache_.find(token);
-    if (it != authz_cache_.end() && it->second > now) return true;
+    if (it != authz_cache_.end() && it->second.until > now) {
+      if (!it->second.allowed) return deny(it->second.status, it->second.msg);
+      *token_node = it->second.node;
+      return true;
+    }
+    // reviews the cache cannot answer are rate limited (20 a second, bursts of 40): a stream of made-up tokens
+    // must not turn into a stream of TokenReviews against the apiserver
+    review_tokens_ = std::min(40.0, review_tokens_ + (now - review_last_) * 20.0);
+    review_last_ = now;
+    if (review_tokens_ < 1.0) return deny(429, "too many token reviews; retry shortly");
+    review_tokens_ -= 1.0;
   }
   if (!api_) return deny(503, "no apiserver client to review the token");
+  auto remember = [&](Authz a) {
+    std::lock_guard<std::mutex> g(amu_);
+    if (authz_cache_.size() > 1024) authz_cache_.clear();
+    authz_cache_[token] = std::move(a);
+  };
+  auto refuse = [&](int status, const std::string& msg) {
+    remember(Authz{now + 10.0, false, status, msg, std::string()});
+    return deny(status, msg);
+  };
   // TokenReview (authentication.k8s.io/v1): the apiserver says whose token it is
   std::string body = "{\"apiVersion\":\"authentication.k8s.io/v1\",\"kind\":\"TokenReview\",\"spec\":{\"token\":";
   json::append_quoted(&body, token);
@@ -971,7 +997,7 @@ bool NativeServer::plugin_authorized(const http::Message& req, std::string* resp
   std::string out, err;
   if (!api_call("POST", "/apis/authentication.k8s.io/v1/tokenreviews", body, "application/json", &status, &out, &err) ||
       status < 200 || status >= 300) {
-    return deny(503, "token review failed: " + (err.empty() ? std::to_string(status) : err));
+    return deny(503, "token review failed: " + (err.empty() ? std::to_string(status) : err));  // not cached
   }
   json::Doc d;
   std::string perr;
@@ -979,15 +1005,22 @@ bool NativeServer::plugin_authorized(const http::Message& req, std::string* resp
   const int64_t au = d.path(0, {"status", "authenticated"});
   const int64_t un = d.path(0, {"status", "user", "username"});
   if (au < 0 || d.at(static_cast<uint32_t>(au)).type != json::T::True || un < 0) {
-    return deny(401, "the token is not authenticated");
+    return refuse(401, "the token is not authenticated");
   }
   const std::string user = d.str(static_cast<uint32_t>(un));
   bool allowed = false;
   for (const auto& u : cfg_.plugin_users) allowed = allowed || u == user;
-  if (!allowed) return deny(403, "user " + user + " may not write allocation records");
-  std::lock_guard<std::mutex> g(amu_);
-  if (authz_cache_.size() > 1024) authz_cache_.clear();
-  authz_cache_[token] = now + cfg_.plugin_auth_ttl;
+  if (!allowed) return refuse(403, "user " + user + " may not write allocation records");
+  // a bound service-account token names the node its pod runs on (status.user.extra, Kubernetes >= 1.30): the
+  // plugin of one node may then write only that node's records
+  std::string node;
+  const int64_t ex = d.path(0, {"status", "user", "extra", "authentication.kubernetes.io/node-name"});
+  if (ex >= 0 && d.at(static_cast<uint32_t>(ex)).type == json::T::Array) {
+    const uint32_t arr = static_cast<uint32_t>(ex), first = d.first_child(arr);
+    if (first < d.next(arr) && d.at(first).type == json::T::String) node = d.str(first);
+  }
+  remember(Authz{now + cfg_.plugin_auth_ttl, true, 200, std::string(), node});
+  *token_node = node;
   return true;
 }
 
@@ -1000,13 +1033,17 @@ bool NativeServer::plugin_authorized(const http::Message& req, std::string* resp
 // `ttl` seconds unless refreshed (a plugin that died).
 //
 //   {"node": "n", "unaccounted": [u0, u1, ...] | null, "ttl": s}  ->  200 {"Error":""} | 400 | 404
-std::string NativeServer::do_physical(const http::Message& req) {
+std::string NativeServer::do_physical(const http::Message& req, const std::string& token_node) {
   auto answer = [](int status, const std::string& body) { return http::response(status, "application/json", body, true); };
   json::Doc d;
   std::string perr;
   if (!d.parse(req.body, &perr) || d.at(0).type != json::T::Object) return answer(400, error_body("bad request: " + perr));
   std::string node;
   if (!arg_str(d, "node", &node) || node.empty()) return answer(400, error_body("physical needs node"));
+  if (!token_node.empty() && token_node != node) {
+    stats_.plugin_auth_denied.fetch_add(1, std::memory_order_relaxed);
+    return answer(403, error_body("the caller's token is bound to node " + token_node + ", not " + node));
+  }
   std::vector<int64_t> used;
   int64_t ui = d.find(0, "unaccounted");
   if (ui >= 0 && d.at(static_cast<uint32_t>(ui)).type == json::T::Array) {

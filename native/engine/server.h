@@ -143,10 +143,11 @@ class NativeServer {
                 std::string* resp, std::string* err);
   void throttle();
   std::string do_proxy(const http::Message& req);
-  std::string do_move(const http::Message& req);
-  std::string do_physical(const http::Message& req);
+  // token_node: the node the caller's token is bound to (its TokenReview's node-name claim), "" when it has none
+  std::string do_move(const http::Message& req, const std::string& token_node = std::string());
+  std::string do_physical(const http::Message& req, const std::string& token_node = std::string());
   // the caller of a device-plugin endpoint is the plugin (ServerConfig::plugin_auth); false with the 401/403 answer
-  bool plugin_authorized(const http::Message& req, std::string* resp);
+  bool plugin_authorized(const http::Message& req, std::string* resp, std::string* token_node);
   std::string bind_error_response(const std::string& msg) const;
   void record_failure(BindFailure f);
 
@@ -169,8 +170,17 @@ class NativeServer {
   double q_tokens_ = 0.0, q_last_ = 0.0;
   std::mutex fmu_;
   std::vector<BindFailure> failures_;
-  std::mutex amu_;  // token -> authenticated until (TokenReview cache)
-  std::unordered_map<std::string, double> authz_cache_;
+  // TokenReview cache: token -> verdict until `until` (allowed, or denied: a denial is cached briefly too, so a
+  // caller repeating a bad token does not cost the apiserver a review per request), and the node its pod is on
+  struct Authz {
+    double until = 0;
+    bool allowed = false;
+    int status = 0;
+    std::string msg, node;
+  };
+  std::mutex amu_;
+  std::unordered_map<std::string, Authz> authz_cache_;
+  double review_tokens_ = 0, review_last_ = 0;  // token bucket for reviews not answered from the cache
   ServerStats stats_;
   // bind ordering lives in the ledger (Ledger::assume_ordered / bind_wait / bind_leave): one in-flight
   // set for the native binds and the Python slow path alike

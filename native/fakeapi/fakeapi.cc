@@ -1398,11 +1398,16 @@ class Server {
       rep->body = faults_.json();
       return true;
     }
-    if (path == "/fake/tokens" && m == "POST") {  // {"token": "...", "user": "..."}: what a TokenReview answers
+    // {"token": "...", "user": "...", "node": "..."}: what a TokenReview answers (node: the bound token's
+    // authentication.kubernetes.io/node-name claim, optional)
+    if (path == "/fake/tokens" && m == "POST") {
       jd::Value b = take_body(body);
       const jd::Value* t = b.get("token");
       const jd::Value* u = b.get("user");
-      if (t && t->k == jd::Value::Str && u && u->k == jd::Value::Str) tokens_[t->s] = u->s;
+      const jd::Value* nd = b.get("node");
+      if (t && t->k == jd::Value::Str && u && u->k == jd::Value::Str) {
+        tokens_[t->s] = {u->s, nd && nd->k == jd::Value::Str ? nd->s : std::string()};
+      }
       rep->body = "{}";
       return true;
     }
@@ -1415,7 +1420,12 @@ class Server {
       std::string o = "{\"kind\":\"TokenReview\",\"apiVersion\":\"authentication.k8s.io/v1\",\"status\":{";
       if (it != tokens_.end()) {
         o.append("\"authenticated\":true,\"user\":{\"username\":");
-        json::append_quoted(&o, it->second);
+        json::append_quoted(&o, it->second.first);
+        if (!it->second.second.empty()) {
+          o.append(",\"extra\":{\"authentication.kubernetes.io/node-name\":[");
+          json::append_quoted(&o, it->second.second);
+          o.append("]}");
+        }
         o.append("}}}");
       } else {
         o.append("\"authenticated\":false}}");
@@ -1617,7 +1627,7 @@ class Server {
   std::deque<Event> history_;
   int64_t rv_ = 0, oldest_rv_ = 0;
   Faults faults_;
-  std::map<std::string, std::string> tokens_;  // TokenReview: bearer token -> username (/fake/tokens)
+  std::map<std::string, std::pair<std::string, std::string>> tokens_;  // TokenReview: token -> (user, node)
   std::map<std::string, uint64_t> counts_;
   std::vector<Grace> graces_;
 };

@@ -695,8 +695,9 @@ def test_plugin_endpoints_take_only_the_plugin_token_and_the_physical_floor_stee
         api = start_apiserver()
         c = KubeClient(api.url)
         fa = HttpClient(api.url)
-        for tok, user in (("tok-plugin", plugin_user), ("tok-other", "system:serviceaccount:default:app")):
-            await fa.request("POST", "/fake/tokens", json.dumps({"token": tok, "user": user}).encode())
+        for tok, user, node in (("tok-plugin", plugin_user, None), ("tok-other", "system:serviceaccount:default:app", None),
+                                ("tok-node-m", plugin_user, "m"), ("tok-node-n", plugin_user, "n")):
+            await fa.request("POST", "/fake/tokens", json.dumps({"token": tok, "user": user, "node": node}).encode())
         await c.create("nodes", make_node("n", 2 * 100, 2))
         ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url)), plugin_auth="tokenreview",
                                    plugin_users=[plugin_user]).start()
@@ -723,6 +724,17 @@ def test_plugin_endpoints_take_only_the_plugin_token_and_the_physical_floor_stee
             assert await physical([100, 0], "tok-plugin") == 200
             srv = json.loads((await http.request("GET", "/debug/engine")).body)["server"]
             assert srv["plugin_auth_denied"] == 4 and srv["token_reviews"] == 4  # the plugin's token reviewed once
+            # a denial is cached too: the same bad token again costs the apiserver no review
+            assert await physical([100, 0], "tok-other") == 403
+            # a token bound to a node (its pod's node-name claim) writes that node's records only
+            assert await physical([100, 0], "tok-node-m") == 403
+            assert await physical([100, 0], "tok-node-n") == 200
+            srv = json.loads((await http.request("GET", "/debug/engine")).body)["server"]
+            assert srv["token_reviews"] == 6 and srv["plugin_auth_denied"] == 6, srv
+            # made-up tokens: the reviews the cache cannot answer are rate limited (20 a second, bursts of 40)
+            codes = [await physical([100, 0], f"junk-{i}") for i in range(80)]
+            assert codes.count(401) <= 45 and 429 in codes, codes
+            assert await physical([100, 0], "tok-plugin") == 200  # a cached good token is not limited
             assert eng.node_unaccounted("n") == [100, 0]
             metrics = (await http.request("GET", "/metrics")).body.decode()
             assert 'gpushare_device_unaccounted_gpu_mem{device="0",node="n"} 100.0' in metrics, metrics[-2000:]
