@@ -728,6 +728,7 @@ def test_batch_client_keeps_its_helper_threads_and_answers_in_order():
 import http.server, sys
 class H(http.server.BaseHTTPRequestHandler):
     protocol_version = "HTTP/1.1"
+    disable_nagle_algorithm = True  # headers and body go out in two writes
     def do_POST(self):
         n = int(self.headers.get("Content-Length", "0"))
         body = self.rfile.read(n) + self.path.encode()
