@@ -484,7 +484,7 @@ def parse():
                          "interleaved A/B after 20 s idle: 10.5-11.0k vs 8.9-10.8k pods/s, profiles/r02_pinload)")
     ap.add_argument("--pin-smt", type=int, default=1,
                     help="1: a 2-CPU slot is one physical core with both SMT threads, so the N=1 plan fits one "
-                         "L3 domain (5 cores); 0: two physical cores")
+                         "L3 domain (6 cores with the plugin; 7 at N > 1); 0: two physical cores")
     ap.add_argument("--api-latency-ms", type=float, default=0.0,
                     help="fake kube-apiserver answers every non-watch request after this delay (timed region)")
     ap.add_argument("--bind-order", default="auto", choices=["auto", "strict", "relaxed"],
