@@ -383,6 +383,34 @@ bool DpCore::ids_on(const std::vector<std::string>& ids, int dev) const {
 bool DpCore::preferred(const std::string& req, std::string* resp, std::string* why) {
   int32_t size = 0;
   std::string_view container;
+  if (!id_prefix_.empty() && dp::preferred_single_size(std::string_view(req), &size, &container)) {
+    // one walk over kubelet's free IDs (~2,300 on 8 GPUs): the size is read off the container's tail, so the pod's
+    // GPU is known before the walk, which picks its IDs (then others, in order, if it has too few) and validates
+    // the request as it goes
+    const int64_t want = state_->preferred_device(size);
+    if (want < 0) {
+      stats_.slow_preferred++;
+      *why = "no pending pod of that size known yet";
+      return false;
+    }
+    auto pre = id_prefix_.find(static_cast<int>(want));
+    const std::string_view prefix = pre != id_prefix_.end() ? std::string_view(pre->second) : std::string_view();
+    std::vector<std::string_view> mine, other;
+    mine.reserve(static_cast<size_t>(size));
+    const size_t cap = static_cast<size_t>(size);
+    const bool ok = dp::pick_available(container, size, prefix, &mine, &other);
+    if (ok) {
+      std::vector<std::vector<std::string>> out(1);
+      std::vector<std::string>& chosen = out[0];
+      chosen.reserve(cap);
+      for (auto id : mine) chosen.emplace_back(id);
+      for (size_t k = 0; chosen.size() < cap && k < other.size(); ++k) chosen.emplace_back(other[k]);
+      *resp = dp::encode_preferred_response(out);
+      stats_.fast_preferred++;
+      return true;
+    }
+    // another shape after all (must_include, a size that is not the tail's): the general walks below
+  }
   if (dp::preferred_single(std::string_view(req), &size, &container)) {
     // kubelet's usual request (one container, nothing it must include): the free-ID list (~2,300 on 8 GPUs) is
     // walked in place, without a view per ID, and only until `size` IDs of the pod's GPU are found

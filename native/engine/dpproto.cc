@@ -1,5 +1,7 @@
 #include "dpproto.h"
 
+#include <cstring>
+
 #include <algorithm>
 
 #include <string_view>
@@ -241,6 +243,73 @@ bool preferred_single(std::string_view msg, int32_t* size, std::string_view* con
     return true;
   });
   return ok && !must;
+}
+
+bool preferred_single_size(std::string_view msg, int32_t* size, std::string_view* container) {
+  int n = 0;
+  if (!each(msg, [&](int f, int w, std::string_view pl, uint64_t) {
+        if (f == 1 && w == 2) {
+          ++n;
+          *container = pl;
+        }
+        return true;
+      }) ||
+      n != 1) {
+    return false;
+  }
+  // the tail: tag 0x18 (field 3, varint), then the varint (continuation bytes >= 0x80, the last < 0x80).  An ID
+  // byte is printable ASCII, so the tag byte cannot be part of one; the walk confirms it anyway
+  const auto* b = reinterpret_cast<const uint8_t*>(container->data());
+  size_t e = container->size();
+  if (e < 2 || (b[e - 1] & 0x80)) return false;
+  size_t i = e - 1;
+  while (i > 0 && (b[i - 1] & 0x80) && e - i < 5) --i;
+  if (i == 0 || b[i - 1] != 0x18) return false;
+  uint64_t v = 0;
+  for (size_t k = e; k-- > i;) v = (v << 7) | (b[k] & 0x7f);
+  if (v == 0 || v > (1u << 30)) return false;
+  *size = static_cast<int32_t>(v);
+  return true;
+}
+
+bool pick_available(std::string_view container, int32_t size, std::string_view prefix,
+                    std::vector<std::string_view>* mine, std::vector<std::string_view>* other) {
+  const size_t cap = static_cast<size_t>(size), pn = prefix.size();
+  const char* pre = prefix.data();
+  Reader r(container);
+  bool sized = false;
+  while (!r.done()) {
+    // the common entry, an available ID (tag 0x0a, a one-byte length), without the generic decoder
+    if (*r.p == 0x0a && r.end - r.p >= 2 && r.p[1] < 0x80) {
+      const size_t n = r.p[1];
+      r.p += 2;
+      if (static_cast<size_t>(r.end - r.p) < n) return false;
+      const char* id = reinterpret_cast<const char*>(r.p);
+      r.p += n;
+      if (n > pn && pn && std::memcmp(id, pre, pn) == 0) {
+        if (mine->size() < cap) mine->emplace_back(id, n);
+      } else if (other->size() < cap) {
+        other->emplace_back(id, n);
+      }
+      continue;
+    }
+    int f, w;
+    std::string_view pl;
+    uint64_t v = 0;
+    if (!r.next(&f, &w, &pl, &v)) return false;
+    if (f == 1 && w == 2) {  // a long ID (length >= 128)
+      if (pl.size() > pn && pn && pl.compare(0, pn, prefix) == 0) {
+        if (mine->size() < cap) mine->push_back(pl);
+      } else if (other->size() < cap) {
+        other->push_back(pl);
+      }
+    } else if (f == 2 && w == 2) {
+      return false;  // must_include: the general path
+    } else if (f == 3 && w == 0) {
+      sized = static_cast<int64_t>(v) == size;
+    }
+  }
+  return sized;
 }
 
 bool for_each_available(std::string_view container, const std::function<bool(std::string_view)>& fn) {

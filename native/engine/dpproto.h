@@ -69,6 +69,15 @@ bool decode_preferred_request(std::string_view msg, std::vector<PreferredRequest
 // available IDs for_each_available walks in order, stopping when `fn` returns false); false for any other shape.
 bool preferred_single(std::string_view msg, int32_t* size, std::string_view* container);
 bool for_each_available(std::string_view container, const std::function<bool(std::string_view)>& fn);
+// The same request in one walk: `size` read first from the container's tail (kubelet's Go protobuf writes
+// allocation_size, field 3, last), then every entry is walked once -- `fn` sees each available ID, and the walk
+// checks there is no must_include and that field 3 says `size`.  false (use preferred_single) for any other shape.
+bool preferred_single_size(std::string_view msg, int32_t* size, std::string_view* container);
+// One walk over the container's available IDs: the first `size` that start with `prefix` go to *mine, the first
+// `size` others to *other (both in list order); false if the container has must_include, a field 3 that is not
+// `size`, or is malformed.
+bool pick_available(std::string_view container, int32_t size, std::string_view prefix,
+                    std::vector<std::string_view>* mine, std::vector<std::string_view>* other);
 bool decode_list_and_watch(const std::string& msg, std::vector<DeviceMsg>* devs);
 bool decode_preferred_response(const std::string& msg, std::vector<std::vector<std::string>>* per_container);
 bool decode_allocate_response(const std::string& msg, std::vector<ContainerResponse>* per_container);
