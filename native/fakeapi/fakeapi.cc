@@ -272,9 +272,11 @@ HttpError not_found(const std::string& kind, const std::string& name) {
 // A stored object: immutable once stored (writes replace the pointer), with
 // its serialisation cached for GET / LIST / watch / write responses.
 struct Obj {
-  jd::Value v;
+  std::shared_ptr<const jd::Value> vp;  // shared with the DELETED copy of the object (make_deleted)
+  int64_t rv = 0;                       // metadata.resourceVersion
   std::string json;
   std::string ns, name;
+  const jd::Value& v() const { return *vp; }
 };
 using ObjP = std::shared_ptr<const Obj>;
 
@@ -284,9 +286,34 @@ ObjP make_obj(jd::Value v) {
   if (md) {
     o->ns = md->str_or("namespace");
     o->name = md->str_or("name");
+    o->rv = std::atoll(md->str_or("resourceVersion").c_str());
   }
-  o->v = std::move(v);
-  o->json = jd::dump(o->v);
+  o->vp = std::make_shared<const jd::Value>(std::move(v));
+  o->json = jd::dump(*o->vp);
+  return o;
+}
+
+// The object as its DELETED event carries it: the last stored state under a new resourceVersion.  Its JSON is the
+// stored JSON with that one value replaced, and it shares the stored object's tree (the watchers' selectors read
+// labels and fields, which the deletion does not change): no deep copy and re-serialisation per deleted pod, a
+// DeleteCollection of a wave's pods being a loop of them.  Falls back to a copy when the value is not unique.
+ObjP make_deleted(const ObjP& cur, const std::string& rv) {
+  const jd::Value* md = cur->v().get("metadata");
+  const std::string old = "\"resourceVersion\":\"" + (md ? md->str_or("resourceVersion") : std::string()) + "\"";
+  const size_t at = cur->json.find(old);
+  if (at == std::string::npos || cur->json.find(old, at + 1) != std::string::npos) {
+    jd::Value gone = cur->v();
+    gone.member("metadata").set("resourceVersion", jd::Value::string(rv));
+    return make_obj(std::move(gone));
+  }
+  auto o = std::make_shared<Obj>();
+  o->vp = cur->vp;
+  o->ns = cur->ns;
+  o->name = cur->name;
+  o->rv = std::atoll(rv.c_str());
+  o->json.reserve(cur->json.size() + 8);
+  o->json.append(cur->json, 0, at).append("\"resourceVersion\":\"").append(rv).append("\"");
+  o->json.append(cur->json, at + old.size(), std::string::npos);
   return o;
 }
 
@@ -826,7 +853,7 @@ class Server {
           auto& m = store_[gr.kind];
           auto it = m.find({gr.ns, gr.name});
           if (it != m.end()) {
-            const jd::Value* md = it->second->v.get("metadata");
+            const jd::Value* md = it->second->v().get("metadata");
             if (md && md->str_or("uid") == gr.uid) do_delete(gr.kind, gr.ns, gr.name, -1);
           }
         }
@@ -872,8 +899,7 @@ class Server {
   // watcher on its owner loop (woken unless it is the calling loop, which
   // flushes at the end of its iteration).
   void emit(const std::string& kind, const char* etype, const ObjP& o) {
-    const jd::Value* md = o->v.get("metadata");
-    int64_t rv = md ? std::atoll(md->str_or("resourceVersion").c_str()) : 0;
+    const int64_t rv = o->rv;
     auto line = std::make_shared<std::string>();
     line->reserve(o->json.size() + 32);
     line->append("{\"type\":\"").append(etype).append("\",\"object\":").append(o->json).append("}\n");
@@ -908,7 +934,7 @@ class Server {
 
   bool wants(const Watcher& w, const Obj& o) const {
     if (!w.ns.empty() && o.ns != w.ns) return false;
-    return w.fsel.matches(o.v) && w.lsel.matches(o.v);
+    return w.fsel.matches(o.v()) && w.lsel.matches(o.v());
   }
 
   // Send what this loop's dirty watchers accumulated: buffers are taken under the
@@ -1132,14 +1158,14 @@ class Server {
   ObjP do_replace(const std::string& kind, const std::string& ns, const std::string& name, jd::Value obj,
                   const std::string& sub) {
     ObjP cur = get_obj(kind, ns, name);
-    const jd::Value& cmd = *cur->v.get("metadata");
+    const jd::Value& cmd = *cur->v().get("metadata");
     const jd::Value* omd = obj.get("metadata");
     std::string want = omd ? omd->str_or("resourceVersion") : std::string();
     if (!want.empty() && want != cmd.str_or("resourceVersion")) throw conflict(kind, name);
     if (kind == "pods" && injected_conflict()) throw conflict(kind, name);
     jd::Value nv;
     if (sub == "status") {
-      nv = cur->v;
+      nv = cur->v();
       const jd::Value* st = obj.get("status");
       nv.set("status", st ? *st : jd::Value::object());
     } else {
@@ -1147,7 +1173,7 @@ class Server {
       jd::Value& md = nv.member("metadata");
       keep_server_fields(cmd, &md);
       if (kind == "pods") {
-        const jd::Value* cs = cur->v.get("spec");
+        const jd::Value* cs = cur->v().get("spec");
         const jd::Value* on = cs ? cs->get("nodeName") : nullptr;
         jd::Value& spec = nv.member("spec");
         if (on && on->is_str() && !on->s.empty()) {
@@ -1155,7 +1181,7 @@ class Server {
         } else {
           spec.erase("nodeName");
         }
-        const jd::Value* cst = cur->v.get("status");
+        const jd::Value* cst = cur->v().get("status");
         nv.set("status", cst ? *cst : jd::Value::object());
       }
     }
@@ -1169,7 +1195,7 @@ class Server {
   ObjP do_patch(const std::string& kind, const std::string& ns, const std::string& name, jd::Value patch,
                 const std::string& sub) {
     ObjP cur = get_obj(kind, ns, name);
-    const jd::Value& cmd = *cur->v.get("metadata");
+    const jd::Value& cmd = *cur->v().get("metadata");
     const jd::Value* pmd = patch.get("metadata");
     std::string want = pmd ? pmd->str_or("resourceVersion") : std::string();
     if (!want.empty() && want != cmd.str_or("resourceVersion")) throw conflict(kind, name);
@@ -1195,7 +1221,7 @@ class Server {
       if (spec && spec->is_obj()) spec->erase("nodeName");
       if (sub.empty()) patch.erase("status");
     }
-    jd::Value nv = cur->v;
+    jd::Value nv = cur->v();
     jd::merge_patch(&nv, patch);
     jd::Value& md = nv.member("metadata");
     keep_server_fields(cmd, &md);
@@ -1208,7 +1234,7 @@ class Server {
 
   void do_bind(const std::string& ns, const std::string& name, const jd::Value& binding) {
     ObjP cur = get_obj("pods", ns, name);
-    const jd::Value& cmd = *cur->v.get("metadata");
+    const jd::Value& cmd = *cur->v().get("metadata");
     const jd::Value* bmd = binding.get("metadata");
     std::string buid = bmd ? bmd->str_or("uid") : std::string();
     if (!buid.empty() && buid != cmd.str_or("uid")) {
@@ -1216,7 +1242,7 @@ class Server {
                                                             ", UID in object meta: " + cmd.str_or("uid"))};
     }
     if (injected_conflict()) throw conflict("pods", name);
-    const jd::Value* cs = cur->v.get("spec");
+    const jd::Value* cs = cur->v().get("spec");
     std::string cur_node = cs ? cs->str_or("nodeName") : std::string();
     if (!cur_node.empty()) {
       throw HttpError{409, status_body(409, "Conflict", "pod " + name + " is already assigned to node \"" + cur_node + "\"")};
@@ -1227,7 +1253,7 @@ class Server {
     const jd::Value* tgt = binding.get("target");
     std::string target = tgt ? tgt->str_or("name") : std::string();
     if (target.empty()) throw HttpError{422, status_body(422, "Invalid", "target.name: Required value")};
-    jd::Value nv = cur->v;
+    jd::Value nv = cur->v();
     nv.member("spec").set("nodeName", jd::Value::string(target));
     const jd::Value* ann = bmd ? bmd->get("annotations") : nullptr;
     if (faults_.drop_binding_annotations) ann = nullptr;
@@ -1255,12 +1281,12 @@ class Server {
   ObjP do_delete(const std::string& kind, const std::string& ns, const std::string& name, double grace) {
     ObjP cur = get_obj(kind, ns, name);
     Key key{kind == "nodes" ? std::string() : ns, name};
-    const jd::Value* cs = cur->v.get("spec");
+    const jd::Value* cs = cur->v().get("spec");
     if (kind == "pods" && grace > 0 && cs && !cs->str_or("nodeName").empty()) {
-      const jd::Value& cmd = *cur->v.get("metadata");
+      const jd::Value& cmd = *cur->v().get("metadata");
       const jd::Value* dt = cmd.get("deletionTimestamp");
       if (dt && !dt->is_null()) return cur;
-      jd::Value nv = cur->v;
+      jd::Value nv = cur->v();
       jd::Value& md = nv.member("metadata");
       md.set("deletionTimestamp", jd::Value::string(now_iso()));
       md.set("deletionGracePeriodSeconds", jd::Value::number(static_cast<int64_t>(grace)));
@@ -1274,9 +1300,7 @@ class Server {
       return o;
     }
     store_[kind].erase(key);
-    jd::Value gone = cur->v;
-    gone.member("metadata").set("resourceVersion", jd::Value::string(bump()));
-    ObjP o = make_obj(std::move(gone));
+    ObjP o = make_deleted(cur, bump());
     emit(kind, "DELETED", o);
     return o;
   }
@@ -1322,7 +1346,7 @@ class Server {
     Selector fs = Selector::parse(fsel, true), ls = Selector::parse(lsel, false);
     for (; it != m.end(); ++it) {
       if (!ns.empty() && it->second->ns != ns) continue;
-      if (!fs.matches(it->second->v) || !ls.matches(it->second->v)) continue;
+      if (!fs.matches(it->second->v()) || !ls.matches(it->second->v())) continue;
       if (limit > 0 && n == limit) {  // more matching items remain: continue after the last one sent
         next = list_rv + ":" + last_sent->first + "/" + last_sent->second;
         break;
@@ -1549,7 +1573,7 @@ class Server {
         Selector fs = Selector::parse(fsel, true), ls = Selector::parse(lsel, false);
         for (auto& kv : store_[kind]) {
           if (!ns.empty() && kv.second->ns != ns) continue;
-          if (fs.matches(kv.second->v) && ls.matches(kv.second->v)) names.push_back(kv.second->name);
+          if (fs.matches(kv.second->v()) && ls.matches(kv.second->v())) names.push_back(kv.second->name);
         }
         std::string o = "{\"kind\":\"PodList\",\"apiVersion\":\"v1\",\"metadata\":{},\"items\":[";
         for (size_t i = 0; i < names.size(); ++i) {

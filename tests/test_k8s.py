@@ -155,6 +155,38 @@ def test_selectors_graceful_delete_and_deletecollection(impl):
 
 
 @IMPLS
+def test_deleted_events_carry_the_last_state_at_a_new_version(impl):
+    """A DeleteCollection's items and the DELETED events a watch (field selector on the node) gets: the last stored
+    object under a fresh resourceVersion, one per pod, in version order (gsx-fakeapi builds them without copying the
+    object: make_deleted)."""
+    async def go():
+        r, c = await _api(impl=impl)
+        try:
+            for i in range(4):
+                await c.create("pods", make_pod(f"d{i}", 1, node="n1", labels={"wave": "7"},
+                                                annotations={"k": f'v"{i}\\\\'}))
+            await c.create("pods", make_pod("other", 1, node="n2", labels={"wave": "7"}))
+            rv0 = (await c.list("pods"))["metadata"]["resourceVersion"]
+            out = await c.request("DELETE", "/api/v1/namespaces/default/pods", params={"labelSelector": "wave=7"})
+            items = {p["metadata"]["name"]: p for p in out["items"]}
+            assert sorted(items) == ["d0", "d1", "d2", "d3", "other"]
+            rvs = [int(p["metadata"]["resourceVersion"]) for p in out["items"]]
+            assert len(set(rvs)) == 5 and min(rvs) > int(rv0)
+            assert items["d2"]["metadata"]["annotations"]["k"] == 'v"2\\\\' and items["d2"]["spec"]["nodeName"] == "n1"
+            got = []
+            async for ev in c.watch("pods", resource_version=rv0, field_selector="spec.nodeName=n1", timeout_seconds=1):
+                got.append((ev["type"], ev["object"]["metadata"]["name"], int(ev["object"]["metadata"]["resourceVersion"])))
+            assert [g[:2] for g in got] == [("DELETED", f"d{i}") for i in range(4)]
+            assert [g[2] for g in got] == sorted(g[2] for g in got)
+            assert {g[1]: g[2] for g in got} == {n: int(p["metadata"]["resourceVersion"]) for n, p in items.items()
+                                                 if n != "other"}
+        finally:
+            await c.close()
+            await r.stop()
+    run(go())
+
+
+@IMPLS
 def test_watch_from_compacted_version_is_410(impl):
     async def go():
         r, c = await _api(impl=impl, history=3)
