@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cassert>
 #include <cstdio>
 #include <cstring>
@@ -26,6 +27,7 @@
 #include "model.h"
 #include "quantity.h"
 #include "server.h"
+#include "tracker.h"
 
 using namespace gsx;
 
@@ -450,6 +452,75 @@ static void test_landing_order() {
   }
 }
 
+// The wave driver's BatchClient (persistent helper threads, tracker.cc) over many batches of mixed concurrency, and
+// ApiClient::abort shutting requests in flight against an apiserver that never answers.
+static void silent_apiserver(int lfd, std::atomic<bool>* stop) {
+  std::vector<int> held;
+  while (!stop->load()) {
+    int c = ::accept(lfd, nullptr, nullptr);
+    if (c < 0) break;
+    held.push_back(c);  // read nothing, answer nothing
+  }
+  for (int c : held) ::close(c);
+}
+
+static void test_batch_client_and_abort() {
+  int aport = 0;
+  int alfd = listen_any(&aport);
+  std::atomic<bool> stop{false};
+  std::atomic<int> bindings{0};
+  std::thread api(fake_apiserver, alfd, &stop, &bindings);
+  ApiConfig cfg;
+  cfg.server = "http://127.0.0.1:" + std::to_string(aport);
+  {
+    BatchClient bc(cfg);
+    for (int k = 0; k < 60; ++k) {
+      std::vector<BatchClient::Req> reqs;
+      for (int i = 0; i < 3 + k % 20; ++i) reqs.emplace_back("POST", "/api/v1/namespaces/d/pods/p" + std::to_string(i) + "/binding", "{}");
+      auto out = bc.run(reqs, (k % 3 == 0) ? 1 : (k % 3 == 1 ? 4 : 16));
+      CHECK(out.size() == reqs.size());
+      for (auto& o : out) CHECK(o.first == 201);
+    }
+  }
+  CHECK(bindings.load() > 0);
+  // abort: two requests stuck on an apiserver that never answers fail at once, and later ones fail without waiting
+  int sport = 0;
+  int slfd = listen_any(&sport);
+  std::atomic<bool> sstop{false};
+  std::thread silent(silent_apiserver, slfd, &sstop);
+  ApiConfig scfg;
+  scfg.server = "http://127.0.0.1:" + std::to_string(sport);
+  ApiClient c(scfg);
+  std::atomic<int> failed{0};
+  std::vector<std::thread> ts;
+  for (int i = 0; i < 2; ++i) {
+    ts.emplace_back([&] {
+      int st = 0;
+      std::string resp, err;
+      if (!c.request("PATCH", "/api/v1/namespaces/d/pods/x", "{}", "application/merge-patch+json", &st, &resp, &err)) {
+        failed.fetch_add(1);
+      }
+    });
+  }
+  ::usleep(200000);  // both are waiting for an answer
+  const auto t0 = std::chrono::steady_clock::now();
+  c.abort();
+  for (auto& t : ts) t.join();
+  CHECK(failed.load() == 2);
+  CHECK(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5));
+  int st = 0;
+  std::string resp, err;
+  CHECK(!c.request("GET", "/api/v1/pods", "", "application/json", &st, &resp, &err));
+  stop.store(true);
+  sstop.store(true);
+  ::shutdown(alfd, SHUT_RDWR);
+  ::shutdown(slfd, SHUT_RDWR);
+  ::close(alfd);
+  ::close(slfd);
+  api.join();
+  silent.join();
+}
+
 int main() {
   test_json();
   test_quantity();
@@ -458,6 +529,7 @@ int main() {
   test_http();
   test_request_parser();
   test_server_stress();
+  test_batch_client_and_abort();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;
