@@ -1056,10 +1056,13 @@ std::string NativeServer::do_physical(const http::Message& req, const std::strin
   } else if (ui >= 0 && d.at(static_cast<uint32_t>(ui)).type != json::T::Null) {
     return answer(400, error_body("unaccounted: an array or null"));
   }
-  double ttl = 60.0;
+  double ttl = 60.0;  // seconds, fractions allowed (the plugin sends 60.0), at most 600
   int64_t ti = d.find(0, "ttl");
-  int64_t tv;
-  if (ti >= 0 && d.as_int(static_cast<uint32_t>(ti), &tv) && tv > 0) ttl = static_cast<double>(std::min<int64_t>(tv, 600));
+  if (ti >= 0 && d.at(static_cast<uint32_t>(ti)).type == json::T::Number) {
+    const std::string txt(d.raw(static_cast<uint32_t>(ti)));
+    const double tv = std::strtod(txt.c_str(), nullptr);
+    if (tv > 0) ttl = std::min(tv, 600.0);
+  }
   bool ok;
   {
     std::lock_guard<introspect::ProfiledMutex> g(l_->mu());

@@ -754,3 +754,49 @@ def test_plugin_endpoints_take_only_the_plugin_token_and_the_physical_floor_stee
             await c.close()
             api.stop()
     asyncio.run(go())
+
+
+def test_published_unaccounted_use_expires_unless_refreshed():
+    """A plugin that stops refreshing its publication (it died) cannot pin a device: the charge lapses after its
+    ttl (Ledger::gc), and a refresh before that keeps it."""
+    from gpushare_scheduler_extender_amd.k8s.fasthttp import Client as HttpClient
+
+    async def go():
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 2 * 100, 2))
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url))).start()
+        eng = ext.server.engine
+        http = HttpClient(f"http://127.0.0.1:{ext.port}")
+
+        async def physical(used, ttl):
+            r = await http.request("POST", "/gpushare-scheduler/physical",
+                                   json.dumps({"node": "n", "unaccounted": used, "ttl": ttl}).encode())
+            return r.status
+
+        try:
+            for _ in range(200):
+                if eng.has_node("n"):
+                    break
+                await asyncio.sleep(0.01)
+            assert await physical([100, 0], 0.3) == 200
+            eng.gc()
+            assert eng.node_unaccounted("n") == [100, 0]  # within its ttl
+            assert eng.assume("u1", "default", "p1", "n", 95)[0] == 1
+            await asyncio.sleep(0.2)
+            assert await physical([100, 0], 0.3) == 200  # refreshed: a fresh ttl
+            await asyncio.sleep(0.2)
+            eng.gc()
+            assert eng.node_unaccounted("n") == [100, 0]
+            await asyncio.sleep(0.25)
+            eng.gc()
+            assert eng.node_unaccounted("n") == []  # lapsed
+            assert eng.stats()["unaccounted_expired"] == 1
+            assert eng.assume("u2", "default", "p2", "n", 95)[0] == 0  # GPU 0 takes binds again
+        finally:
+            await http.close()
+            await ext.stop()
+            await ext.server.client.close()
+            await c.close()
+            await api.stop()
+    asyncio.run(go())
