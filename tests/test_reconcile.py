@@ -267,3 +267,66 @@ def test_annotations_edited_behind_the_plugins_back_are_repaired():
         finally:
             await cl.close()
     asyncio.run(go())
+
+
+def test_unaccounted_use_is_a_live_holder_on_another_gpu_and_reaches_the_extender():
+    """plugin.py unaccounted / publish_physical: a record kubelet reports held by another live pod annotated with
+    another GPU is charged where the container runs; nothing while the record is unreported, held by its own pod,
+    or held by a pod that is gone; withdrawn once the annotations agree.  The extender charges what is published."""
+    import asyncio
+    import json as _json
+
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
+    from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin
+    from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
+    from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+    from gpushare_scheduler_extender_amd.k8s.objects import make_node
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+    from tests.fixtures.fakeapi import FakeApiServerRunner
+
+    async def go():
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 32, 2))
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url))).start()
+        plugin = GpuSharePlugin(c, "n", fake_devices("2x16GiB"), SHARED_GPU, socket_dir="/tmp/gsx-unacc-test",
+                                extender=f"http://127.0.0.1:{ext.port}")
+        st = plugin.state
+        try:
+            for _ in range(200):
+                if ext.server.engine.has_node("n"):
+                    break
+                await asyncio.sleep(0.01)
+
+            def pod(name, dev):
+                p = make_pod(name, 4, node="n", uid=f"u{name}", annotations={SHARED_GPU.annotation_idx: str(dev),
+                                                                             SHARED_GPU.annotation_assigned: "true"})
+                p["metadata"]["resourceVersion"] = "1"
+                st.observe(p)
+
+            pod("P", 0)
+            pod("Q", 1)
+            st.core.set_owners_reported(True)
+            st.record(st.pods["uQ"], ["g1-_-0"], 4, "", "aQ")  # built for Q, on GPU 1
+            assert plugin.unaccounted() is None  # kubelet has not reported who holds it
+            st.set_owner("aQ", "uQ")
+            assert plugin.unaccounted() is None  # its own pod: the annotations charge it
+            st.set_owner("aQ", "uP")  # P's container runs with it (a swap), P annotated GPU 0
+            assert plugin.unaccounted() == [0, 4]
+            assert await plugin.publish_physical()
+            assert ext.server.engine.node_unaccounted("n") == [0, 4]
+            pod("P", 1)  # the exchange landed: P is annotated where its container runs
+            assert plugin.unaccounted() is None
+            assert await plugin.publish_physical()
+            assert ext.server.engine.node_unaccounted("n") == []
+            pod("P", 0)
+            st.set_owner("aQ", "~gone")  # held by a pod that is gone: its container is stopping
+            assert plugin.unaccounted() is None
+            one = GpuSharePlugin(c, "n", fake_devices("1x16GiB"), SHARED_GPU, socket_dir="/tmp/gsx-unacc-test1")
+            assert one.unaccounted() is None  # one GPU: whoever holds it is annotated with it
+        finally:
+            await ext.stop()
+            await ext.server.client.close()
+            await c.close()
+            await api.stop()
+    asyncio.run(go())
