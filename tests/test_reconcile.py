@@ -330,3 +330,42 @@ def test_unaccounted_use_is_a_live_holder_on_another_gpu_and_reaches_the_extende
             await c.close()
             await api.stop()
     asyncio.run(go())
+
+
+def test_stand_in_partner_prefers_equal_size_then_the_largest_that_fits():
+    """reconcile.py _stand_in_partner: P's container runs on GPU 1 while P is annotated GPU 0 (the pod its allocation
+    was built for is gone).  An unstarted pod the extender placed on GPU 1 exchanges GPUs with P: one of P's size
+    first (every GPU's sum unchanged), else the largest one with which both GPUs fit after the exchange."""
+    import asyncio
+
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
+    from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin
+    from gpushare_scheduler_extender_amd.deviceplugin.reconcile import Reconciler
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+
+    async def go():
+        plugin = GpuSharePlugin(None, "n", fake_devices("2x16GiB"), SHARED_GPU, socket_dir="/tmp/gsx-standin-test")
+        st = plugin.state
+        rec = Reconciler(plugin, None)
+
+        def pod(name, mem, dev, rv):
+            p = make_pod(name, mem, node="n", uid=f"u{name}", annotations={SHARED_GPU.annotation_idx: str(dev),
+                                                                           SHARED_GPU.annotation_assigned: "false"})
+            p["metadata"]["resourceVersion"] = str(rv)
+            st.observe(p)
+            return st.pods[f"u{name}"]
+
+        p = pod("P", 4, 0, 1)
+        pod("Q8", 8, 1, 2)
+        pod("Q2", 2, 1, 3)
+        got = rec._stand_in_partner(1, p, set())
+        assert got is not None and got.name == "Q8"  # no equal size: the largest that fits both GPUs
+        assert rec.stats.get("unequal_partners") == 1
+        pod("Q4", 4, 1, 4)
+        assert rec._stand_in_partner(1, p, set()).name == "Q4"  # equal size first
+        assert rec._stand_in_partner(1, p, {"default/Q4"}).name == "Q8"  # a started pod never stands in
+        pod("Big", 14, 0, 5)  # GPU 0 now holds P 4 + Big 14 by the annotations: Q8 no longer fits there
+        st.release("uQ4")
+        assert rec._stand_in_partner(1, p, set()).name == "Q2"
+
+    asyncio.run(go())
