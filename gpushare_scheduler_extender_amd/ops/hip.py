@@ -258,7 +258,7 @@ def hbm_admit_n(stream: Stream, slices: list[tuple[int, int, int]], n_stamp: int
 
 GEMM_CFGS = {0: "128x128/4w", 1: "256x128/8w", 2: "128x256/8w", 3: "256x256/8w", 4: "128x128/4w-nogroup",
              5: "256x256/8w-phased-g4", 6: "256x256/8w-phased-g8", 7: "256x256/4w-agpr-g4", 8: "256x256/4w-agpr-g8",
-             9: "256x256/4w-asm-agpr-g4"}
+             9: "256x256/4w-asm-agpr-g4", 10: "256x256/8w-phased-g4-mfma32"}
 
 
 def gemm_bf16_nt_cfg(stream: Stream, a: int, b: int, c: int, m: int, n: int, k: int, cfg: int):

@@ -20,6 +20,7 @@ namespace gsxgemm {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef const void __attribute__((address_space(1)))* gptr_t;
 typedef void __attribute__((address_space(3)))* lptr_t;
 
@@ -186,7 +187,10 @@ __device__ __forceinline__ void ph_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int GROUP_M>
+// M32: the same schedule on v_mfma_f32_32x32x16_bf16 (per quadrant 2 x 1 blocks of 32x32 over 4 k-steps: 8 MFMAs
+// of twice the work instead of 16), for the A/B the MFMA-shape rule asks for (the chip may hold a different clock
+// on the other shape; same LDS bytes, same registers).
+template <int GROUP_M, bool M32 = false>
 __global__ __launch_bounds__(512) void gemm_phased_kernel(const uint16_t* __restrict__ A,
                                                          const uint16_t* __restrict__ B, uint16_t* __restrict__ C,
                                                          int M, int N, int K) {
@@ -235,40 +239,72 @@ __global__ __launch_bounds__(512) void gemm_phased_kernel(const uint16_t* __rest
   };
 
   f32x4 acc[8][4];
+  f32x16 acc32[4][2];  // M32: [32-row block][32-col block] of the wave's 128x64 tile
 #pragma unroll
   for (int m = 0; m < 8; ++m)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  bf16x8 af[4][2], bf[2][2][2];  // A: [m][kk]; B: [nh][n][kk]
-
-  auto read_a = [&](const char* base, int mh) {
-    const char* h = base + mh * PH_HALF;
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        af[m][kk] = *reinterpret_cast<const bf16x8*>(h + swz(wr * 64 + m * 16 + fr, kk * 4 + fq));
-  };
-  auto read_b = [&](const char* base, int nh) {
-    const char* h = base + (2 + nh) * PH_HALF;
+  for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        bf[nh][n][kk] = *reinterpret_cast<const bf16x8*>(h + swz(wc * 32 + n * 16 + fr, kk * 4 + fq));
-  };
-  auto mma = [&](int mh, int nh) {
-    __builtin_amdgcn_s_setprio(1);
+      for (int j = 0; j < 16; ++j) acc32[m][n][j] = 0.f;
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int r32 = lane & 31, h32 = lane >> 5;  // M32 operand maps: row / column lane & 31, k = 8 (lane >> 5) + j
+  bf16x8 af[4][2], bf[2][2][2];  // A: [m][kk]; B: [nh][n][kk]  (M32: A [b][kk], B [nh][kk], k-steps of 16)
+
+  auto read_a = [&](const char* base, int mh) {
+    const char* h = base + mh * PH_HALF;
+    if constexpr (M32) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          af[b * 2 + (kk >> 1)][kk & 1] =
+              *reinterpret_cast<const bf16x8*>(h + swz(wr * 64 + b * 32 + r32, kk * 2 + h32));
+    } else {
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
-          acc[mh * 4 + m][nh * 2 + n] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], bf[nh][n][kk], acc[mh * 4 + m][nh * 2 + n], 0, 0, 0);
+        for (int kk = 0; kk < 2; ++kk)
+          af[m][kk] = *reinterpret_cast<const bf16x8*>(h + swz(wr * 64 + m * 16 + fr, kk * 4 + fq));
+    }
+  };
+  auto read_b = [&](const char* base, int nh) {
+    const char* h = base + (2 + nh) * PH_HALF;
+    if constexpr (M32) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        bf[nh][kk >> 1][kk & 1] = *reinterpret_cast<const bf16x8*>(h + swz(wc * 32 + r32, kk * 2 + h32));
+    } else {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          bf[nh][n][kk] = *reinterpret_cast<const bf16x8*>(h + swz(wc * 32 + n * 16 + fr, kk * 4 + fq));
+    }
+  };
+  auto mma = [&](int mh, int nh) {
+    __builtin_amdgcn_s_setprio(1);
+    if constexpr (M32) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc32[mh * 2 + b][nh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              af[b * 2 + (kk >> 1)][kk & 1], bf[nh][kk >> 1][kk & 1], acc32[mh * 2 + b][nh], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+            acc[mh * 4 + m][nh * 2 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m][kk], bf[nh][n][kk],
+                                                                                 acc[mh * 4 + m][nh * 2 + n], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -318,12 +354,23 @@ __global__ __launch_bounds__(512) void gemm_phased_kernel(const uint16_t* __rest
   ph_barrier();
 
   uint16_t* ct = reinterpret_cast<uint16_t*>(lds + wid * (WTM * WTN * 2));
+  if constexpr (M32) {
+    // 32x32 C map: column lane & 31, row (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5)
 #pragma unroll
-  for (int m = 0; m < 8; ++m)
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+      for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ct[(m * 16 + fq * 4 + j) * WTN + n * 16 + fr] = f2bf(acc[m][n][j]);
+        for (int j = 0; j < 16; ++j)
+          ct[(m * 32 + (j & 3) + 8 * (j >> 2) + 4 * h32) * WTN + n * 32 + r32] = f2bf(acc32[m][n][j]);
+  } else {
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ct[(m * 16 + fq * 4 + j) * WTN + n * 16 + fr] = f2bf(acc[m][n][j]);
+  }
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
   __builtin_amdgcn_wave_barrier();
   constexpr int LPR = WTN / 8, RPI = 64 / LPR;
@@ -336,18 +383,18 @@ __global__ __launch_bounds__(512) void gemm_phased_kernel(const uint16_t* __rest
   }
 }
 
-template <int GM>
+template <int GM, bool M32 = false>
 hipError_t launch_phased(hipStream_t s, const void* A, const void* B, void* C, int M, int N, int K) {
   constexpr int lds = 8 * PH_HALF;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_phased_kernel<GM>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_phased_kernel<GM, M32>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
   if (M % 256 || N % 256 || K % BK) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_phased_kernel<GM>), dim3((M / 256) * (N / 256)), dim3(512), lds, s,
+  hipLaunchKernelGGL((gemm_phased_kernel<GM, M32>), dim3((M / 256) * (N / 256)), dim3(512), lds, s,
                      static_cast<const uint16_t*>(A), static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), M,
                      N, K);
   return hipGetLastError();
@@ -553,8 +600,8 @@ hipError_t launch(hipStream_t s, const void* A, const void* B, void* C, int M, i
 // Tile configurations (index -> BM x BN, waves).  Exposed for benchmarking.
 extern "C" int gsx_gemm_cfg_tile(int cfg, int* bm, int* bn) {
   static const int t[][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}, {128, 128},
-                             {256, 256}, {256, 256}, {256, 256}, {256, 256}, {256, 256}};
-  if (cfg < 0 || cfg > 9) return -1;
+                             {256, 256}, {256, 256}, {256, 256}, {256, 256}, {256, 256}, {256, 256}};
+  if (cfg < 0 || cfg > 10) return -1;
   *bm = t[cfg][0];
   *bn = t[cfg][1];
   return 0;
@@ -574,6 +621,7 @@ extern "C" int gsx_gemm_bf16_nt_launch_cfg(void* stream, const void* A, const vo
     case 7: return static_cast<int>(gsxgemm::launch_w4<4, false>(s, A, B, C, M, N, K));
     case 8: return static_cast<int>(gsxgemm::launch_w4<8, false>(s, A, B, C, M, N, K));
     case 9: return static_cast<int>(gsxgemm::launch_w4<4, true>(s, A, B, C, M, N, K));
+    case 10: return static_cast<int>(gsxgemm::launch_phased<4, true>(s, A, B, C, M, N, K));
     default: return static_cast<int>(hipErrorInvalidValue);
   }
 }

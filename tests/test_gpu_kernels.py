@@ -225,7 +225,7 @@ def test_arena_runtime_admits_four_64gib_pods():
         rt.close()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_gemm_tile_configs_match_fp32_reference(hip, cfg):
     m, n, k = 512, 512, 256
     torch.manual_seed(cfg)
@@ -255,7 +255,7 @@ def test_gemm_phased_edge_shapes(hip, m, n, k):
     b = torch.randn(n, k, device="cuda", dtype=torch.bfloat16)
     ref = a.float() @ b.float().t()
     s = hip.Stream(0)
-    for cfg in (5, 6, 7, 8, 9):
+    for cfg in (5, 6, 7, 8, 9, 10):
         c = torch.full((m, n), float("nan"), device="cuda", dtype=torch.bfloat16)
         torch.cuda.synchronize()
         hip.gemm_bf16_nt_cfg(s, a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, cfg)
@@ -271,7 +271,7 @@ def test_gemm_phased_is_deterministic(hip):
     a = torch.rand(m, k, device="cuda", dtype=torch.bfloat16) * 2 - 1
     b = torch.rand(n, k, device="cuda", dtype=torch.bfloat16) * 2 - 1
     s = hip.Stream(0)
-    for cfg in (5, 6, 7, 8, 9):
+    for cfg in (5, 6, 7, 8, 9, 10):
         c0 = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
         c = torch.empty_like(c0)
         torch.cuda.synchronize()
