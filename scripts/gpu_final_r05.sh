@@ -21,3 +21,6 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps 20 --warmup 5 --sweep 0 > $OUT/prof.log 2>&1
 rc=$?; [ $rc -eq 0 ] || { echo "rocprof rc=$rc"; tail -20 $OUT/prof.log; exit $rc; }
 find $OUT/prof -name "*kernel_stats.csv" | head -3
+timeout -k 10 300 python -m gsxtools.plugincpu --gpus 8 --idle 30 --trickle 30 --json-out $OUT/plugincpu.json > $OUT/plugincpu.log 2>&1
+rc=$?; [ $rc -eq 0 ] || { echo "plugincpu rc=$rc"; tail -20 $OUT/plugincpu.log; exit $rc; }
+cat $OUT/plugincpu.json
