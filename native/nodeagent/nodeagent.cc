@@ -588,6 +588,12 @@ class Agent {
             id_field_.push_back(std::move(f));
           }
           id_used_.assign(all_ids_.size(), 0);
+          id_fields_.clear();
+          id_field_off_.assign(1, 0);
+          for (const auto& f : id_field_) {
+            id_fields_.append(f);
+            id_field_off_.push_back(id_fields_.size());
+          }
           // as kubelet: GetPreferredAllocation only if the plugin's options advertise it
           std::string opts;
           bool pre = false;
@@ -618,18 +624,35 @@ class Agent {
     // kubelet's free IDs: every healthy ID no running container holds, as indices into all_ids_ (fixed once the
     // plugin is connected); without GetPreferredAllocation only the first `units` are needed, kubelet's own pick
     std::vector<uint32_t> free_idx;
-    free_idx.reserve(preferred_ ? all_ids_.size() : static_cast<size_t>(std::max<int64_t>(units, 0)));
+    // with GetPreferredAllocation: the free IDs as runs of all_ids_ (a pod's IDs are consecutive, so a node holds a
+    // few dozen runs), each copied from the pre-encoded field image in one piece
+    std::vector<std::pair<size_t, size_t>> runs;
     size_t n_free = 0, field_bytes = 0;
-    for (size_t i = 0; i < all_ids_.size(); ++i) {
-      if (id_used_[i]) continue;
-      ++n_free;
-      if (preferred_) {
-        free_idx.push_back(static_cast<uint32_t>(i));
-        field_bytes += id_field_[i].size();
-      } else if (static_cast<int64_t>(free_idx.size()) < units) {
-        free_idx.push_back(static_cast<uint32_t>(i));
-      } else {
-        break;
+    if (preferred_) {
+      const size_t n = all_ids_.size();
+      const char* used = id_used_.data();
+      size_t i = 0;
+      while (i < n) {
+        const void* f = std::memchr(used + i, 0, n - i);  // the next free ID
+        if (!f) break;
+        i = static_cast<size_t>(static_cast<const char*>(f) - used);
+        const void* u = std::memchr(used + i, 1, n - i);  // the next used one ends the run
+        const size_t j = u ? static_cast<size_t>(static_cast<const char*>(u) - used) : n;
+        runs.emplace_back(i, j);
+        n_free += j - i;
+        field_bytes += id_field_off_[j] - id_field_off_[i];
+        i = j;
+      }
+    } else {
+      free_idx.reserve(static_cast<size_t>(std::max<int64_t>(units, 0)));
+      for (size_t i = 0; i < all_ids_.size(); ++i) {
+        if (id_used_[i]) continue;
+        ++n_free;
+        if (static_cast<int64_t>(free_idx.size()) < units) {
+          free_idx.push_back(static_cast<uint32_t>(i));
+        } else {
+          break;
+        }
       }
     }
     if (static_cast<int64_t>(n_free) < units) {
@@ -664,7 +687,7 @@ class Agent {
         std::string req(1, '\x0a');
         put_varint(&req, field_bytes + size_field.size());
         req.reserve(req.size() + field_bytes + size_field.size());
-        for (uint32_t i : free_idx) req.append(id_field_[i]);
+        for (const auto& r : runs) req.append(id_fields_, id_field_off_[r.first], id_field_off_[r.second] - id_field_off_[r.first]);
         req.append(size_field);
         tenc = now_s() - ts;
         ok = dp_->call("/v1beta1.DevicePlugin/GetPreferredAllocation", req, &resp, &st, &err) &&
@@ -1126,6 +1149,8 @@ class Agent {
   std::unordered_map<std::string, std::vector<std::string>> used_ids_;  // uid -> the IDs its Allocate took
   std::unordered_map<std::string, size_t> id_index_;                     // ID -> its place in all_ids_
   std::vector<std::string> id_field_;  // per all_ids_ entry: the ID encoded as GetPreferredAllocation's field 1
+  std::string id_fields_;                // the same fields back to back, in all_ids_ order
+  std::vector<size_t> id_field_off_;     // entry i's field starts at id_field_off_[i] (size all_ids_ + 1)
   bool start_queued_ = false;          // starts_ got a pod no pod worker was woken for yet
   std::vector<char> id_used_;  // per all_ids_ entry: held by a running container (the union of used_ids_)
   std::unordered_map<std::string, std::string> uid_key_;                 // uid -> ns/name of every used_ids_ pod
