@@ -230,7 +230,11 @@ void DpCore::journal_unmap(bool trim) {
 void DpCore::journal_append(const AllocRecord& r) {
   if (jfd_ < 0) return;
   // one line per Allocate, the record's fields as the plugin's checkpoint has them (AllocRecord.to_dict)
-  std::string line = "{\"aid\":";
+  size_t est = 256 + r.aid.size() + r.uid.size() + r.cu_mask.size() + r.iso.size();
+  for (const auto& id : r.ids) est += id.size() + 3;
+  std::string line;
+  line.reserve(est);
+  line.append("{\"aid\":");
   json::append_quoted(&line, r.aid);
   line.append(",\"uid\":");
   json::append_quoted(&line, r.uid);

@@ -59,6 +59,7 @@ bool decode_options(const std::string& msg, bool* pre_start_required, bool* pref
 std::string encode_list_and_watch(const std::vector<DeviceMsg>& devs);
 std::string encode_preferred_response(const std::vector<std::vector<std::string>>& per_container);
 std::string encode_allocate_response(const std::vector<ContainerResponse>& per_container);
+bool encode_allocate_response_selfcheck(const std::vector<ContainerResponse>& per_container);  // tests
 std::string encode_allocate_request(const std::vector<std::vector<std::string>>& ids_per_container);
 std::string encode_preferred_request(const std::vector<PreferredRequest>& reqs);
 

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "allocstate.h"
+#include "dpproto.h"
 #include "http.h"
 #include "json.h"
 #include "ledger.h"
@@ -521,6 +522,29 @@ static void test_batch_client_and_abort() {
   silent.join();
 }
 
+// The one-pass Allocate response encoder against the straightforward one: byte-identical output for empty and
+// multi-container responses, empty strings (absent fields), read-only mounts and values over 127 bytes.
+static void test_allocate_response_encoding() {
+  std::vector<dp::ContainerResponse> none;
+  CHECK(dp::encode_allocate_response_selfcheck(none));
+  dp::ContainerResponse a;
+  a.envs["HIP_VISIBLE_DEVICES"] = "0";
+  a.envs["EMPTY"] = "";
+  a.envs[std::string(200, 'k')] = std::string(300, 'v');
+  a.annotations["gpushare.amd.com/pod"] = "default/p/uid";
+  a.mounts.push_back(dp::MountMsg{"/run/gsx/isolation.conf", "/var/lib/gsx/x/isolation.conf", true});
+  a.mounts.push_back(dp::MountMsg{"/c", "", false});
+  a.devices.push_back(dp::DeviceSpecMsg{"/dev/kfd", "/dev/kfd", "rw"});
+  a.devices.push_back(dp::DeviceSpecMsg{"", "", ""});
+  dp::ContainerResponse b;  // an empty container
+  std::vector<dp::ContainerResponse> two{a, b};
+  CHECK(dp::encode_allocate_response_selfcheck({a}));
+  CHECK(dp::encode_allocate_response_selfcheck(two));
+  std::vector<dp::ContainerResponse> back;
+  CHECK(dp::decode_allocate_response(dp::encode_allocate_response(two), &back) && back.size() == 2 &&
+        back[0].envs.size() == 3 && back[0].mounts.size() == 2 && back[0].devices.size() == 2);
+}
+
 int main() {
   test_json();
   test_quantity();
@@ -530,6 +554,7 @@ int main() {
   test_request_parser();
   test_server_stress();
   test_batch_client_and_abort();
+  test_allocate_response_encoding();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;
