@@ -341,12 +341,16 @@ struct Conn {
 
 // A watch stream.  `pending`, `dirty`, `closed` and `end_requested` are guarded
 // by the state mutex; the rest is fixed at creation or owned by `owner`.
+using Lines = std::vector<std::shared_ptr<const std::string>>;
 struct Watcher {
   uint64_t conn_id;
   Loop* owner = nullptr;
   std::string kind, ns;
   Selector fsel, lsel;
-  std::string pending;
+  // the event lines queued for the next chunk: shared with the history and with every other watcher of the event
+  // (a DeleteCollection of a wave's pods fans each line out to every pod watcher; it is copied once, into the
+  // connection's buffer)
+  Lines pending;
   uint64_t sent = 0, drop_after = 0;
   double deadline = 0;  // 0: none
   std::atomic<bool> closed{false};  // written under the state mutex, read anywhere
@@ -910,7 +914,7 @@ class Server {
     history_.push_back(Event{rv, kind, line, o});
     for (auto& w : watchers_) {
       if (!w->closed && w->kind == kind && wants(*w, *o)) {
-        w->pending.append(*line);
+        w->pending.push_back(line);
         mark_dirty_locked(w);
       }
     }
@@ -943,7 +947,7 @@ class Server {
   bool flush_watchers(Loop* L) {
     struct Out {
       std::shared_ptr<Watcher> w;
-      std::string data;
+      Lines data;
       bool end;
     };
     std::vector<Out> outs;
@@ -958,7 +962,7 @@ class Server {
         Out o{w, std::move(w->pending), w->end_requested};
         w->pending.clear();
         // one chunk per loop iteration; count events for drop_watch_after
-        w->sent += static_cast<uint64_t>(std::count(o.data.begin(), o.data.end(), '\n'));
+        w->sent += static_cast<uint64_t>(o.data.size());
         if (w->drop_after && w->sent >= w->drop_after) {
           counts_["watch_dropped"]++;
           o.end = true;
@@ -978,11 +982,7 @@ class Server {
         continue;
       }
       Conn* c = it->second.get();
-      if (!o.data.empty()) {
-        char hdr[32];
-        std::snprintf(hdr, sizeof(hdr), "%zx\r\n", o.data.size());
-        c->wbuf.append(hdr).append(o.data).append("\r\n");
-      }
+      append_chunk(c, o.data);
       if (o.end) {
         end_watch(L, o.w);
         continue;
@@ -992,9 +992,22 @@ class Server {
     return true;
   }
 
+  // One HTTP chunk of event lines onto the connection's buffer.
+  static void append_chunk(Conn* c, const Lines& lines) {
+    size_t n = 0;
+    for (const auto& l : lines) n += l->size();
+    if (!n) return;
+    char hdr[32];
+    std::snprintf(hdr, sizeof(hdr), "%zx\r\n", n);
+    c->wbuf.reserve(c->wbuf.size() + n + 40);
+    c->wbuf.append(hdr);
+    for (const auto& l : lines) c->wbuf.append(*l);
+    c->wbuf.append("\r\n");
+  }
+
   // Owner loop only: send what is pending, the terminating chunk, and close.
   void end_watch(Loop* L, const std::shared_ptr<Watcher>& w) {
-    std::string rest;
+    Lines rest;
     {
       StateLock g(smu_, lstats_);
       if (w->closed) return;
@@ -1006,11 +1019,7 @@ class Server {
     if (it == L->conns.end()) return;
     Conn* c = it->second.get();
     c->watch = nullptr;
-    if (!rest.empty()) {
-      char hdr[32];
-      std::snprintf(hdr, sizeof(hdr), "%zx\r\n", rest.size());
-      c->wbuf.append(hdr).append(rest).append("\r\n");
-    }
+    append_chunk(c, rest);
     c->wbuf.append("0\r\n\r\n");
     c->want_close = true;
     flush_conn(L, c);
@@ -1069,12 +1078,15 @@ class Server {
       auto it = std::upper_bound(history_.begin(), history_.end(), rv,
                                  [](int64_t v, const Event& e) { return v < e.rv; });
       for (; it != history_.end(); ++it) {
-        if (it->kind == kind && wants(*w, *it->obj)) w->pending.append(*it->line);
+        if (it->kind == kind && wants(*w, *it->obj)) w->pending.push_back(it->line);
       }
     } else {
       for (auto& kv : store_[kind]) {
         if (wants(*w, *kv.second)) {
-          w->pending.append("{\"type\":\"ADDED\",\"object\":").append(kv.second->json).append("}\n");
+          auto line = std::make_shared<std::string>();
+          line->reserve(kv.second->json.size() + 32);
+          line->append("{\"type\":\"ADDED\",\"object\":").append(kv.second->json).append("}\n");
+          w->pending.push_back(std::move(line));
         }
       }
     }
