@@ -584,6 +584,11 @@ def main():
         # rank 0 = the wave driver + GPU 0's runtime endpoint (the CRI-runtime role): one core, the driver on
         # one SMT thread and the endpoint's threads on the other, instead of both time-sharing one thread
         widths["rank0"] = 2
+    # the kubelet stand-in on a multi-GPU node admits N x 4 pods a wave with its pod workers starting the previous
+    # ones: two cores there (N = 8: 15.2-15.9k pods/s vs 13.2-14.3k on one core, where its threads waited for a CPU
+    # 150-190 % of the region; profiles/r05_session26/).  A real kubelet has the node's cores.
+    if world > 1:
+        widths["node-agent"] = 4
     # ranks > 0 idle in a gloo barrier during the timed waves while their runtime endpoint admits pods: on a
     # single CPU the endpoint thread waited behind gloo's threads for up to 9 ms (N=4/8 rehearsal, 2 CPUs fix it)
     widths.update({f"rank{r}": 2 for r in range(1, world)})
