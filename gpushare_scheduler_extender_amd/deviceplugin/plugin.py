@@ -196,7 +196,11 @@ class GpuSharePlugin:
         # node's admissions skip that round trip (the reference's plugin never offered it); "1" / "0" force it
         pref = os.environ.get("GSX_PLUGIN_PREFERRED", "auto")
         self.preferred = len(self.devices) > 1 if pref == "auto" else pref == "1"
-        self.checkpoint_interval = 0.2
+        # the records checkpoint: with early answer every Allocate is journaled first, so the checkpoint only bounds
+        # how much journal a restart replays -- once a second (each one rotates the journal under the state lock
+        # and writes a file: at 0.2 s it sat inside most of an 8-GPU node's busy seconds); without the journal the
+        # checkpoint is the only record on disk, so it follows the Allocates closely
+        self.checkpoint_interval = float(os.environ.get("GSX_PLUGIN_CHECKPOINT_S", "1.0" if self.early_answer else "0.2"))
         self._dirty = False
         self._persist_task: asyncio.Task | None = None
         # where an Allocate's time goes (plugin side, seconds summed over calls): matching, the ASSIGNED patch

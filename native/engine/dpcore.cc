@@ -197,7 +197,9 @@ bool DpCore::journal_map(int fd, std::string* err) {
     *err = std::string("ftruncate: ") + std::strerror(errno);
     return false;
   }
-  void* m = ::mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, 0);
+  // not prefaulted: a rotation runs under the state lock, and populating 1 MiB there would hold an Allocate up;
+  // the pages fault in as lines reach them (one 4 KiB page per ~4 Allocates)
+  void* m = ::mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   if (m == MAP_FAILED) {
     *err = std::string("mmap: ") + std::strerror(errno);
     (void)!::ftruncate(fd, static_cast<off_t>(used));
@@ -253,7 +255,7 @@ void DpCore::journal_append(const AllocRecord& r) {
     // grow by whole chunks (a syscall pair per ~1,000 Allocates): the mapping is re-made over the longer file
     const size_t cap = ((jlen_ + line.size()) / kJournalChunk + 1) * kJournalChunk;
     void* m = ::ftruncate(jfd_, static_cast<off_t>(cap)) == 0
-                  ? ::mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, jfd_, 0)
+                  ? ::mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED, jfd_, 0)
                   : MAP_FAILED;
     if (m == MAP_FAILED) {
       // the line still goes to the file (past the mapped bytes); the next append retries the growth
@@ -303,8 +305,10 @@ bool DpCore::journal_rotate(std::string* err) {
       *err = "map " + path + ": " + e2;
       return false;
     }
+    // .old is not trimmed: the checkpoint that covers it deletes it, and its readers skip the zeros (a shrinking
+    // truncate under the state lock could wait for the pages' writeback)
+    (void)olen;
     ::munmap(omap, ocap);
-    (void)!::ftruncate(ofd, static_cast<off_t>(olen));
     ::close(ofd);
     return true;
   }
