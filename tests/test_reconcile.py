@@ -97,6 +97,15 @@ async def _swap_scenario(reconcile: bool, plugin: str = "grpc"):
             await asyncio.sleep(0.05)
         live = {n: cur[n] for n in ("p2", "p3", "c0", "c1")}
         phys = await _physical(cl, live)
+        if reconcile:
+            # the new pods may have been served each other's allocations too: the repair is asynchronous
+            async def settled():
+                now = await _pods(cl)
+                ok = all(int(now[n]["metadata"]["annotations"][ALIYUN.annotation_idx]) == phys[n] for n in live
+                         if now[n]["status"].get("phase") == "Running")
+                return now if ok else None
+            cur = await _wait(settled, 10, "the new pods' annotations never matched their containers' GPUs")
+            live = {n: cur[n] for n in ("p2", "p3", "c0", "c1")}
         per_gpu = [0] * 4
         for n, g in phys.items():
             if live[n]["status"].get("phase") == "Running":
