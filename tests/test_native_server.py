@@ -536,8 +536,15 @@ def test_move_endpoint_is_the_one_writer_of_the_gpu_index():
                     "resourceVersion": md["resourceVersion"], "from": frm if frm is not None else int(
                         md["annotations"][P.annotation_idx]), "to": to, "partner": partner,
                     "annotations": annotations or {}}
-            r = await http.request("POST", "/gpushare-scheduler/move", json.dumps(body).encode())
-            return r.status, json.loads(r.body)
+            # the extender refuses a move while the pod's previous one is in flight (until its watch event lands in
+            # the ledger); the plugin's reconciliation retries on its next pass, this waits for it
+            for _ in range(200):
+                r = await http.request("POST", "/gpushare-scheduler/move", json.dumps(body).encode())
+                out = json.loads(r.body)
+                if r.status != 409 or "in flight" not in out.get("Error", ""):
+                    break
+                await asyncio.sleep(0.01)
+            return r.status, out
 
         async def settle(want):
             for _ in range(200):
