@@ -95,6 +95,10 @@ PHYSICAL_TTL_S = 60.0  # the extender drops a physical-use publication this plug
 PHYSICAL_REFRESH_S = 15.0
 SA_TOKEN_FILE = "/var/run/secrets/kubernetes.io/serviceaccount/token"
 GUARD_WAIT_S = 5.0  # how long an Allocate waits for a physically full GPU to drain a stopping container
+# ... and how long when the room it needs is held by deleted pods' containers kubelet still lists: they are stopping
+# (graceful termination takes up to terminationGracePeriodSeconds, 30 s by default), and a failed Allocate fails the
+# pod for good, so the admission waits for them instead
+GUARD_GONE_WAIT_S = 30.0
 POD_ANNOTATION = "gpushare.amd.com/pod"  # container annotation: the pod this Allocate was matched to
 
 
@@ -799,6 +803,12 @@ class GpuSharePlugin:
         """Units kubelet has handed out on ``dev`` (the Allocate records of live pods: what really runs there)."""
         return self.state.core.physical_used(dev)
 
+    def _gone_used(self, dev: int) -> int:
+        """Units of the Allocate records on ``dev`` held by containers of deleted pods that kubelet still lists."""
+        from .reconcile import GONE  # noqa: PLC0415 - only with a reconciler, as the guard itself
+
+        return sum(r.units for r in self.state.records.values() if r.dev == dev and r.owner.startswith(GONE))
+
     def _annotated_used(self, dev: int, skip: str = "") -> int:
         """Units the pod annotations put on ``dev`` (what the extender's ledger accounts)."""
         return sum(p.request for p in self.state.pods.values() if p.dev == dev and p.uid != skip and not p.complete)
@@ -823,17 +833,26 @@ class GpuSharePlugin:
         self.stats["physical_guard"] = self.stats.get("physical_guard", 0) + 1
         # a deleted pod's container may still be stopping (its record goes once kubelet stops listing its IDs):
         # give it GUARD_WAIT_S before moving the pod or failing the Allocate
-        deadline = time.monotonic() + GUARD_WAIT_S
+        t0 = time.monotonic()
+        deadline, gone_deadline = t0 + GUARD_WAIT_S, t0 + GUARD_GONE_WAIT_S
         delay = 0.02
         while True:
             await self._reconcile_now(urgent=True)
             rec = self.state.fresh(self.state.pods.get(rec.uid))
             if rec is None or rec.assigned != "false" or not rec.pending or rec.uid in self.state.inflight:
                 return None
-            if self._physical_used(rec.dev) + units <= self.units.get(rec.dev, 0):
+            used = self._physical_used(rec.dev)
+            if used + units <= self.units.get(rec.dev, 0):
                 return rec
-            if time.monotonic() >= deadline:
-                break
+            now = time.monotonic()
+            if now >= deadline:
+                # past the short wait, keep waiting only for containers that will stop -- deleted pods' (kubelet's
+                # view of a deletion can lag the plugin's by seconds behind a dropped watch) -- and only while no
+                # other GPU has room to move the pod to
+                if (now >= gone_deadline or used - self._gone_used(rec.dev) + units > self.units.get(rec.dev, 0)
+                        or self.room_for(rec, units) >= 0):
+                    break
+                self.stats["physical_guard_gone_waits"] = self.stats.get("physical_guard_gone_waits", 0) + 1
             await asyncio.sleep(delay)
             delay = min(0.2, delay * 2)
         if rec.uid in self.reconciler.busy():
@@ -950,7 +969,10 @@ class GpuSharePlugin:
         for r in self.state.records.values():
             if not 0 <= r.dev < len(out) or not r.owner or r.owner == r.uid:
                 # not reported by kubelet yet, or held by the pod it was built for: the annotations charge it (a
-                # pod deleted before the first report: its container is stopping, as the extender assumes)
+                # pod deleted before the first report: its container is stopping, as the extender assumes).  (Also
+                # charging a pod's own record while its annotation names another GPU -- records exchanged, the
+                # re-annotation refused -- double-charged both GPUs of every exchange in flight: kubelet-restart
+                # chaos seeds then stalled with binds refused, 4 of 380 failing vs 0-2)
                 continue
             p = None if r.owner.startswith("~") else pods.get(r.owner)
             # a holder that is gone: its container is stopping, as for any deleted pod (the extender frees on

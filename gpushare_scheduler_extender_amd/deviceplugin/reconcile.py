@@ -188,6 +188,14 @@ class Reconciler:
                 if p is None or not _drifted(p, r) or {p_uid} & self.busy() or p_uid in self.state.inflight:
                     continue
                 q = self._drift_partner(p, r, started)
+                if q is None:
+                    # no pod of P's size to trade annotations with: an unstarted pod the extender has placed where
+                    # P's container runs, of any size with which both GPUs fit afterwards (the exchange path's
+                    # stand-in partner).  Without one, a bind that landed there in the swap window -- before the
+                    # pass that found the swap -- leaves P unrepairable and fails that pod's Allocate
+                    q = self._stand_in_partner(r.dev, p, started)
+                    if q is not None:
+                        self.stats["stand_in_partners"] += 1
                 log.warning("pod %s is annotated with GPU %d but its container runs on GPU %d: re-annotating%s",
                             p.key, p.dev, r.dev, f" (exchanging with {q.key})" if q else "")
                 if q is None:
@@ -301,7 +309,8 @@ class Reconciler:
         # (Q itself may already run a container -- with yet another pod's allocation -- and then stays ASSIGNED)
         recs = self.state.records.values()
         served = q is not None and (q.key in started or any(o.owner == q.uid for o in recs))
-        q_new = dict(p_old, assigned="true" if served or any(o.uid == p.uid and o.aid != r.aid for o in recs)
+        # (a drift repair moves no record: P's records all describe P's own container, none will describe Q)
+        q_new = dict(p_old, assigned="true" if served or (move and any(o.uid == p.uid and o.aid != r.aid for o in recs))
                      else "false")
         new_p = {"idx": r.dev, "assigned": "true", "cu_mask": r.cu_mask}
         ann = self._ann(new_p)

@@ -16,6 +16,14 @@ def _build_module():
 
 
 def build_native(targets=None, force: bool = False, verbose: bool = False) -> None:
+    """One build at a time per tree: parallel test workers (pytest -n) each build on start, and one worker's
+    half-written object must not be another's input."""
+    import fcntl  # noqa: PLC0415
+
     mod = _build_module()
-    for t in targets or mod.DEFAULT:
-        mod.TARGETS[t](force=force, verbose=verbose)
+    lock = REPO / "build" / ".native-build.lock"
+    lock.parent.mkdir(parents=True, exist_ok=True)
+    with open(lock, "w") as f:
+        fcntl.flock(f, fcntl.LOCK_EX)
+        for t in targets or mod.DEFAULT:
+            mod.TARGETS[t](force=force, verbose=verbose)

@@ -54,6 +54,12 @@ def _newer(out: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
+def _current(out: Path, srcs: list[Path], headers: list[Path], force: bool) -> bool:
+    """``out`` is newer than every source and header it is built from: nothing to do, whatever ``build/obj`` holds
+    (a tree copied without ``build/`` -- a gpurun snapshot -- must not recompile what it ships built)."""
+    return not force and not _newer(out, [*srcs, *headers])
+
+
 def _run(cmd: list[str], verbose: bool) -> None:
     if verbose:
         print("+", " ".join(cmd), flush=True)
@@ -85,6 +91,8 @@ def build_engine(force: bool = False, verbose: bool = False) -> Path:
     srcs = [s for s in srcs if s.name not in ("engine_test.cc", "controller_test.cc")]
     headers = sorted(src.glob("*.h"))
     out = OUT / f"_engine{EXT}"
+    if _current(out, srcs, headers, force):
+        return out
     flags = [*CXXFLAGS, *_pybind_includes(), "-I" + str(src)]
     objs = _compile_objs(srcs, "g++", flags, "engine", force, verbose, headers)
     if force or _newer(out, objs):
@@ -98,10 +106,12 @@ def _build_native_tool(name: str, srcdir: str, force: bool, verbose: bool) -> Pa
     src = NATIVE / "engine"
     eng = [s for s in sorted(src.glob("*.cc")) if s.name not in ("bindings.cc", "engine_test.cc", "controller_test.cc")]
     headers = sorted(src.glob("*.h"))
+    out = OUT / name
+    if _current(out, [*eng, *sorted((NATIVE / srcdir).glob("*.cc"))], headers, force):
+        return out
     flags = [*CXXFLAGS, "-I" + str(src)]
     objs = _compile_objs(eng, "g++", flags, "tool", force, verbose, headers)
     objs += _compile_objs(sorted((NATIVE / srcdir).glob("*.cc")), "g++", flags, srcdir, force, verbose, headers)
-    out = OUT / name
     if force or _newer(out, objs):
         OUT.mkdir(parents=True, exist_ok=True)
         _run(["g++", "-o", str(out), *map(str, objs), "-lssl", "-lcrypto", "-lpthread", "-ldl"], verbose)
@@ -129,6 +139,8 @@ def build_mxdev(force: bool = False, verbose: bool = False) -> Path:
     srcs = [s for s in srcs if not s.name.endswith("_test.cc")]
     headers = sorted(src.glob("*.h"))
     out = OUT / f"_mxdev{EXT}"
+    if _current(out, srcs, [*headers, *sorted((NATIVE / "engine").glob("*.h"))], force):
+        return out
     flags = [*CXXFLAGS, *_pybind_includes(), "-I" + str(src), "-I" + str(ROCM / "include"),
              "-I" + str(NATIVE / "engine")]
     objs = _compile_objs(srcs, "g++", flags, "mxdev", force, verbose, headers)
@@ -149,6 +161,8 @@ def build_kernels(force: bool = False, verbose: bool = False) -> Path:
     srcs = [s for s in srcs if not s.stem.startswith("tool_")]
     headers = sorted(src.glob("*.h"))
     out = OUT / "libgsx_kernels.so"
+    if _current(out, srcs, headers, force):
+        return out
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I" + str(src),
              "-munsafe-fp-atomics"]
     objs = _compile_objs(srcs, _hipcc(), flags, "kern", force, verbose, headers)

@@ -25,6 +25,9 @@ from gsxtools.configs import NODE, Cluster
 # the extender charges it on top of the annotations, and an exchange of two unequal pods is checked on its final state
 # (docs/ROUND5.md).
 BATCH_SEEDS = (43, 47, 53, 59, 61)
+if os.environ.get("GSX_CHAOS_BATCH_SEEDS"):  # a sweep: "first-last" (inclusive)
+    _lo, _hi = (int(x) for x in os.environ["GSX_CHAOS_BATCH_SEEDS"].split("-"))
+    BATCH_SEEDS = tuple(range(_lo, _hi + 1))
 
 
 async def _retry(fn, *a, tries=50, **kw):

@@ -278,6 +278,38 @@ def test_annotations_edited_behind_the_plugins_back_are_repaired():
     asyncio.run(go())
 
 
+def test_a_bind_into_an_unrepaired_drift_trades_gpus_with_the_drifted_pod():
+    """reconcile.py drift repair: P's container runs on GPU X while P is annotated GPU Y, and before a pass finds it
+    the extender binds a larger pod C into the room P's container fills on X.  P cannot be re-annotated onto X (C's
+    annotation fills it) and C cannot move to Y alone (P's annotation holds it); the repair trades their GPUs (C is
+    the stand-in partner, any size with which both GPUs fit afterwards), so C's Allocate starts it on Y instead of
+    failing at the physical guard."""
+    async def go():
+        cl = Cluster(ALIYUN, [96] * 2, gpu=False, agent="plugin", agent_args=["--faithful"])
+        try:
+            await cl.start()
+            await cl.create("p", 32)
+            pods = await cl.wait(["p"])
+            x = (await _physical(cl, pods))["p"]
+            y = 1 - x
+            await cl.c.patch("pods", "p", {"metadata": {"annotations": {ALIYUN.annotation_idx: str(y)}}}, "default")
+            for _ in range(500):  # the extender's ledger follows the edit: X looks empty
+                used = [d["usedGPU"] for d in (await cl.inspect())["nodes"][0]["devs"]]
+                if used[x] == 0:
+                    break
+                await asyncio.sleep(0.002)
+            await cl.create("c", 80)  # fits only X by the annotations; X physically holds P's 32
+            pods = await cl.wait(["p", "c"], timeout=20)
+            assert all(q["status"].get("phase") == "Running" for q in pods.values())
+            drift, drifted = await cl.physical_drift(["p", "c"], timeout=15)
+            assert drift == 0, drifted
+            phys = await _physical(cl, pods)
+            assert phys == {"p": x, "c": y}, phys
+        finally:
+            await cl.close()
+    asyncio.run(go())
+
+
 def test_unaccounted_use_is_a_live_holder_on_another_gpu_and_reaches_the_extender():
     """plugin.py unaccounted / publish_physical: a record kubelet reports held by another live pod annotated with
     another GPU is charged where the container runs; nothing while the record is unreported, held by its own pod,
