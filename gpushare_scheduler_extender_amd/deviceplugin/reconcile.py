@@ -188,11 +188,14 @@ class Reconciler:
                 if p is None or not _drifted(p, r) or {p_uid} & self.busy() or p_uid in self.state.inflight:
                     continue
                 q = self._drift_partner(p, r, started)
-                if q is None:
-                    # no pod of P's size to trade annotations with: an unstarted pod the extender has placed where
-                    # P's container runs, of any size with which both GPUs fit afterwards (the exchange path's
-                    # stand-in partner).  Without one, a bind that landed there in the swap window -- before the
-                    # pass that found the swap -- leaves P unrepairable and fails that pod's Allocate
+                plugin = self.plugin
+                if (q is None and r.dev != p.dev
+                        and plugin._annotated_used(r.dev, skip=p.uid) + p.request > plugin.units.get(r.dev, 0)):
+                    # no pod of P's size to trade annotations with, and P's own GPU is full by the annotations: an
+                    # unstarted pod the extender has placed there, of any size with which both GPUs fit afterwards
+                    # (the exchange path's stand-in partner).  Without one, a bind that landed there in the swap
+                    # window -- before the pass that found the swap -- leaves P unrepairable and fails that pod's
+                    # Allocate
                     q = self._stand_in_partner(r.dev, p, started)
                     if q is not None:
                         self.stats["stand_in_partners"] += 1
