@@ -826,7 +826,8 @@ class GpuSharePlugin:
         annotations; after a swap kubelet has not told us about yet, a deletion can free the GPU the annotation
         names while the container that really ran there lives on.  Repair the records first; if the GPU is still
         full, move ``rec`` (not yet started) to a GPU of this node with room by both counts, hold-protected like a
-        reconciliation exchange; with no such GPU, fail the Allocate rather than over-commit."""
+        reconciliation exchange; with no such GPU, keep waiting (up to GUARD_GONE_WAIT_S) while containers of deleted
+        pods hold the room, then fail the Allocate rather than over-commit."""
         cap = self.units.get(rec.dev, 0)
         if self._physical_used(rec.dev) + units <= cap or self._kubelet_bounds(rec.dev, ids):
             return rec

@@ -410,3 +410,67 @@ def test_stand_in_partner_prefers_equal_size_then_the_largest_that_fits():
         assert rec._stand_in_partner(1, p, set()).name == "Q2"
 
     asyncio.run(go())
+
+
+def test_physical_guard_waits_for_a_deleted_pods_container_when_no_gpu_has_room(monkeypatch):
+    """plugin.py _physical_guard: the GPU a pending pod is annotated with is physically full by a container of a
+    deleted pod that kubelet still lists (owner ``~ns/name``), and no other GPU has room.  Past the short wait the
+    Allocate keeps waiting for that container (up to GUARD_GONE_WAIT_S) and proceeds once it is gone; a GPU full by
+    live containers fails it after the short wait."""
+    import asyncio
+
+    from gpushare_scheduler_extender_amd.deviceplugin import plugin as plugin_mod
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
+    from gpushare_scheduler_extender_amd.deviceplugin.plugin import AllocateError, GpuSharePlugin
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+
+    monkeypatch.setattr(plugin_mod, "GUARD_WAIT_S", 0.05)
+    monkeypatch.setattr(plugin_mod, "GUARD_GONE_WAIT_S", 5.0)
+
+    async def go():
+        plugin = GpuSharePlugin(None, "n", fake_devices("2x16GiB"), SHARED_GPU, socket_dir="/tmp/gsx-guard-test")
+        st = plugin.state
+
+        class _Rec:  # the guard's reconciler: passes are no-ops here, nothing in an exchange
+            def busy(self):
+                return set()
+
+        async def _no_pass(urgent=False):
+            return None
+
+        plugin.reconciler = _Rec()
+        plugin._reconcile_now = _no_pass
+
+        def pod(name, mem, dev, assigned):
+            p = make_pod(name, mem, node="n", uid=f"u{name}", annotations={SHARED_GPU.annotation_idx: str(dev),
+                                                                           SHARED_GPU.annotation_assigned: assigned})
+            p["metadata"]["resourceVersion"] = "1"
+            st.observe(p)
+            return st.pods[f"u{name}"]
+
+        st.core.set_owners_reported(True)
+        old = pod("old", 12, 0, "true")
+        st.record(old, [f"g0-_-{i}" for i in range(12)], 12, "", "aold")
+        st.set_owner("aold", "uold")
+        full = pod("full", 16, 1, "true")  # GPU 1 full by a live container: no room to move to
+        st.record(full, [f"g1-_-{i}" for i in range(16)], 16, "", "afull")
+        st.set_owner("afull", "ufull")
+        new = pod("new", 8, 0, "false")
+        # a live container fills the room: the guard fails after its short wait
+        t0 = time.monotonic()
+        with pytest.raises(AllocateError, match="physically full"):
+            await plugin._physical_guard(new, 8)
+        assert time.monotonic() - t0 < 2.0
+        # the same container, its pod deleted and kubelet still listing it: the guard waits, then proceeds
+        st.set_owner("aold", "~default/old")
+        task = asyncio.ensure_future(plugin._physical_guard(st.pods["unew"], 8))
+        await asyncio.sleep(0.4)
+        assert not task.done()
+        # kubelet stops listing it: the reconciliation prunes the physical account and drops the record
+        st.core.prune_held([], time.time(), 0.0)
+        st.drop_record(st.records["aold"])
+        got = await asyncio.wait_for(task, 3.0)
+        assert got is not None and got.uid == "unew" and got.dev == 0
+        assert plugin.stats.get("physical_guard_gone_waits", 0) >= 1
+
+    asyncio.run(go())
