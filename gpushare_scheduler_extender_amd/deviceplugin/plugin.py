@@ -95,10 +95,11 @@ PHYSICAL_TTL_S = 60.0  # the extender drops a physical-use publication this plug
 PHYSICAL_REFRESH_S = 15.0
 SA_TOKEN_FILE = "/var/run/secrets/kubernetes.io/serviceaccount/token"
 GUARD_WAIT_S = 5.0  # how long an Allocate waits for a physically full GPU to drain a stopping container
-# ... and how long when the room it needs is held by deleted pods' containers kubelet still lists: they are stopping
-# (graceful termination takes up to terminationGracePeriodSeconds, 30 s by default), and a failed Allocate fails the
-# pod for good, so the admission waits for them instead
-GUARD_GONE_WAIT_S = 30.0
+# ... and how long when the room it needs is held by deleted pods' containers kubelet still lists: they are stopping,
+# and a failed Allocate fails the pod for good, so the admission waits for them instead -- bounded, since kubelet's
+# admission of every other pod of the node waits behind this call (30 s, the default termination grace, let the
+# kubelet-restart chaos rows time out with admissions queued: 1 of 1900 seeds)
+GUARD_GONE_WAIT_S = 10.0
 POD_ANNOTATION = "gpushare.amd.com/pod"  # container annotation: the pod this Allocate was matched to
 
 
