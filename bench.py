@@ -381,6 +381,88 @@ def latency_sweep(a, children, api_url, api_batch, runner: WaveRunner, inspect_u
     return rows, ref
 
 
+OPEN_LOOP_LATENCIES_MS = (1, 2, 5)
+OPEN_LOOP_RATES = (500, 1000, 2000, 4000, 8000, 16000)
+
+
+def open_loop(a, api_url, api_batch, E, profile, inspect_used) -> dict:
+    """Open-loop throughput under apiserver latency: pods arrive at a constant rate with many in
+    flight -- no waves in lock-step -- and each is deleted as soon as it runs, so the node's room turns over.  Per
+    apiserver latency the offered rate steps up until the stack stops keeping up (bound rate < 90 % of offered, or
+    p99 arrival-to-bound over 100 ms): the knee.  Every pod's stages are timed by the native driver
+    (native/engine/tracker.cc OpenLoop): create (the client's POST), bind (created -> bound: scheduler + extender),
+    admit (bound -> Running: kubelet + device plugin + runtime + Running patch), free (DELETE -> gone).  The stage
+    that grew most at the first rate that failed is named as the bound.  Pods of ``--open-loop-gib`` (4 GiB: 71 on
+    one MI355X) so that room is not what binds the rate.  Rank 0 only, untimed by the headline."""
+    from gpushare_scheduler_extender_amd.k8s.objects import make_pod
+
+    rates = OPEN_LOOP_RATES if a.open_loop == "auto" else tuple(int(x) for x in a.open_loop.split(",") if x)
+    out = {"pod_gib": a.open_loop_gib, "duration_s": a.open_loop_s, "warm_s": 0.3, "hold_s": 0.0, "rows": [],
+           "knee_pods_per_s": {}, "max_sustained_pods_per_s": {}, "bound_stage": {}}
+
+    def pctl(xs, q):
+        return round(1e3 * pct(xs, q), 3) if xs else None
+
+    def cleanup(run):
+        api_batch.run([("DELETE", f"/api/v1/namespaces/default/pods?labelSelector=gsx-ol%3D{run}", b"")], 1)
+        deadline = time.perf_counter() + 60
+        while sum(n["usedGPU"] for n in inspect_used()["nodes"]) != 0:
+            if time.perf_counter() > deadline:
+                raise TimeoutError("open loop: ledger did not drain")
+            time.sleep(0.005)
+
+    k = 0
+    for ms in OPEN_LOOP_LATENCIES_MS:
+        set_latency(api_batch, ms)
+        first = None
+        for rate in rates:
+            k += 1
+            run = f"r{k}"
+            tmpl = make_pod("__NAME__", a.open_loop_gib, profile=profile, labels={"gsx-ol": run})
+            del tmpl["metadata"]["uid"]
+            res = E.open_loop_run({"server": api_url}, run, json.dumps(tmpl, separators=(",", ":")), float(rate),
+                                  duration_s=a.open_loop_s, warm_s=0.3, drain_s=10.0)
+            cleanup(run)
+            pods = res["pods"]
+            t0 = min(p[0] for p in pods if p[0] > 0)
+            lo, hi = t0 + 0.3, t0 + a.open_loop_s
+            win = [p for p in pods if lo <= p[0] < hi]
+            bound_in = sum(1 for p in pods if lo <= p[2] < hi and p[2] > 0)
+            run_in = sum(1 for p in pods if lo <= p[3] < hi and p[3] > 0)
+            st = {"create": [p[1] - p[0] for p in win if p[1] > 0],
+                  "bind": [p[2] - p[1] for p in win if p[2] > 0 and p[1] > 0],
+                  "admit": [p[3] - p[2] for p in win if p[3] > 0 and p[2] > 0],
+                  "free": [p[5] - p[4] for p in win if p[5] > 0 and p[4] > 0]}
+            arr_bound = [p[2] - p[0] for p in win if p[2] > 0]
+            row = {"api_latency_ms": ms, "offered_pods_per_s": rate,
+                   "bound_pods_per_s": round(bound_in / (hi - lo), 1),
+                   "running_pods_per_s": round(run_in / (hi - lo), 1),
+                   "p50_bind_latency_ms": pctl(arr_bound, 50), "p99_bind_latency_ms": pctl(arr_bound, 99),
+                   "p50_admit_latency_ms": pctl(st["admit"], 50), "p99_admit_latency_ms": pctl(st["admit"], 99),
+                   "p50_e2e_ms": pctl([p[3] - p[0] for p in win if p[3] > 0], 50),
+                   "stage_p50_ms": {k2: pctl(v, 50) for k2, v in st.items()},
+                   "not_bound": sum(1 for p in pods if p[2] == 0), "failed": sum(1 for p in pods if p[6]),
+                   "create_errors": res["create_errors"], "delete_errors": res["delete_errors"]}
+            ok = (row["bound_pods_per_s"] >= 0.9 * rate and (row["p99_bind_latency_ms"] or 1e9) <= 100.0
+                  and row["not_bound"] == 0 and row["failed"] == 0)
+            row["kept_up"] = ok
+            out["rows"].append(row)
+            key = str(ms)
+            out["max_sustained_pods_per_s"][key] = max(out["max_sustained_pods_per_s"].get(key, 0.0),
+                                                       row["bound_pods_per_s"])
+            if first is None:
+                first = row
+            if ok:
+                out["knee_pods_per_s"][key] = rate
+                continue
+            # the stage whose median grew most against the lowest rate of this latency: the serial stage that binds
+            growth = {s2: (row["stage_p50_ms"][s2] or 0.0) - (first["stage_p50_ms"][s2] or 0.0) for s2 in st}
+            out["bound_stage"][key] = max(growth, key=growth.get)
+            break
+    set_latency(api_batch, 0)
+    return out
+
+
 def plugin_path(a, children, api_url, runner: WaveRunner, E) -> dict:
     """The same waves with kubelet + device plugin = the shipped gRPC GpuSharePlugin, driven over its unix socket
     by the kubelet stand-in (serial admission, GetPreferredAllocation + Allocate per pod) instead of the
@@ -509,6 +591,12 @@ def parse():
     ap.add_argument("--sweep", type=int, default=1, help="1: run the latency sweep after the timed region")
     # 20 waves a latency point (~0.4 s at 5 ms): with 8, single points read 20-45 % below their neighbours
     ap.add_argument("--sweep-steps", type=int, default=20)
+    ap.add_argument("--open-loop", default="auto",
+                    help="open-loop throughput rows after the timed region: 'auto' (the rate ladder "
+                         f"{OPEN_LOOP_RATES} at {OPEN_LOOP_LATENCIES_MS} ms apiserver latency), a comma list of "
+                         "rates, or 0 (off)")
+    ap.add_argument("--open-loop-gib", type=int, default=4, help="pod size of the open-loop rows")
+    ap.add_argument("--open-loop-s", type=float, default=1.5, help="seconds of arrivals per open-loop rate")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank uses physical GPU 0 (a one-box rehearsal of the N-GPU launch): each rank advertises "
                          "a logical device sized for its wave (pods-per-gpu x pod-gib plus half a pod) and carves its "
@@ -522,6 +610,45 @@ def parse():
     ap.add_argument("--apiserver-threads", type=int, default=0,
                     help="event loops of the fake apiserver (0: auto; GSX_FAKEAPI_THREADS overrides)")
     return ap.parse_args()
+
+
+def cpu_slots(world: int, runtime_cpu: str = "shared", apiserver_threads: int = 0) -> tuple[list[str], dict, int]:
+    """The processes of a bench run on ``world`` GPUs and the CPUs each asks for (utils/cpuset.py plans them; with
+    fewer CPUs than asked the plan is empty and nothing is pinned).  Returns (names, widths, apiserver threads)."""
+    # "plugin": the shipped device-plugin process when an agent starts one (its own CPUs, as a DaemonSet pod)
+    names = ["rank0", "apiserver", "extender", "scheduler", "node-agent", "plugin"] + [f"rank{r}" for r in range(1, world)]
+    # CPUs per process: the extender (2 loops + bind pool + reflectors), schedsim (cycle + bind threads) and the
+    # node agent (reflector + workers) get two; rank 0 stays on one core (a second one let its driver, tracker
+    # and runtime threads migrate: 7.5-9.4k vs 10.1k pods/s, interleaved A/B in profiles/r02_bench_stability.md)
+    # The plugin gets one core (2 CPUs) on a one-GPU node, what its DaemonSet requests.  Round 4 gave it two: its
+    # serving thread then busy-looped on a stuck deferred wake-up between bursts (fixed in round 5, bindings.cc
+    # DpServer::serve), and on one core its pod feed queued behind it (profiles/r04_pinw/).  An 8-GPU node admits 8x
+    # the pods through it: two cores there (run-delay of its threads 214 ms per 170 ms region on one core,
+    # profiles/r05_session4/)
+    widths = {"extender": 2, "scheduler": 2, "node-agent": 2, "plugin": 2 if world == 1 else 4}
+    if runtime_cpu == "split":
+        # rank 0 = the wave driver + GPU 0's runtime endpoint (the CRI-runtime role): one core, the driver on
+        # one SMT thread and the endpoint's threads on the other, instead of both time-sharing one thread
+        widths["rank0"] = 2
+    # the kubelet stand-in on a multi-GPU node admits N x 4 pods a wave with its pod workers starting the previous
+    # ones: two cores there (N = 8: 15.2-15.9k pods/s vs 13.2-14.3k on one core, where its threads waited for a CPU
+    # 150-190 % of the region; profiles/r05_session26/).  A real kubelet has the node's cores.
+    if world > 1:
+        widths["node-agent"] = 4
+    # ranks > 0 idle in a gloo barrier during the timed waves while their runtime endpoint admits pods: on a
+    # single CPU the endpoint thread waited behind gloo's threads for up to 9 ms (N=4/8 rehearsal, 2 CPUs fix it)
+    widths.update({f"rank{r}": 2 for r in range(1, world)})
+    if world > 1:
+        # with N GPUs rank 0's wave driver creates and tracks N x 4 pods per wave: on one CPU the creates trickled
+        # out (scheduler saw the 32nd pod of an N = 8 wave 0.96 ms in, 0.53 ms with a second CPU; per-wave p50
+        # 13.0k -> 19.2k pods/s at N = 8, 10.6k -> 15.7k at N = 4; N = 1 unchanged, profiles/r03_ab/)
+        widths["rank0"] = 2
+    # the fake apiserver's event loops (a shared store): GSX_FAKEAPI_THREADS, else --apiserver-threads, else one loop
+    # at N = 1 and APISERVER_THREADS_MULTI at N > 1, each on its own CPU
+    api_threads = int(os.environ.get("GSX_FAKEAPI_THREADS", "0")) or apiserver_threads or (
+        1 if world == 1 else APISERVER_THREADS_MULTI)
+    widths["apiserver"] = api_threads
+    return names, widths, api_threads
 
 
 def _same_condition(ref_client) -> float | None:
@@ -569,39 +696,7 @@ def main():
     # ---- CPU placement (the same plan on every rank: each takes its own slot)
     from gpushare_scheduler_extender_amd.utils.cpuset import forget_shared_plan, pin_self, plan, shared_plan
 
-    # "plugin": the shipped device-plugin process when an agent starts one (its own CPUs, as a DaemonSet pod)
-    names = ["rank0", "apiserver", "extender", "scheduler", "node-agent", "plugin"] + [f"rank{r}" for r in range(1, world)]
-    # CPUs per process: the extender (2 loops + bind pool + reflectors), schedsim (cycle + bind threads) and the
-    # node agent (reflector + workers) get two; rank 0 stays on one core (a second one let its driver, tracker
-    # and runtime threads migrate: 7.5-9.4k vs 10.1k pods/s, interleaved A/B in profiles/r02_bench_stability.md)
-    # The plugin gets one core (2 CPUs) on a one-GPU node, what its DaemonSet requests.  Round 4 gave it two: its
-    # serving thread then busy-looped on a stuck deferred wake-up between bursts (fixed in round 5, bindings.cc
-    # DpServer::serve), and on one core its pod feed queued behind it (profiles/r04_pinw/).  An 8-GPU node admits 8x
-    # the pods through it: two cores there (run-delay of its threads 214 ms per 170 ms region on one core,
-    # profiles/r05_session4/)
-    widths = {"extender": 2, "scheduler": 2, "node-agent": 2, "plugin": 2 if world == 1 else 4}
-    if a.runtime_cpu == "split":
-        # rank 0 = the wave driver + GPU 0's runtime endpoint (the CRI-runtime role): one core, the driver on
-        # one SMT thread and the endpoint's threads on the other, instead of both time-sharing one thread
-        widths["rank0"] = 2
-    # the kubelet stand-in on a multi-GPU node admits N x 4 pods a wave with its pod workers starting the previous
-    # ones: two cores there (N = 8: 15.2-15.9k pods/s vs 13.2-14.3k on one core, where its threads waited for a CPU
-    # 150-190 % of the region; profiles/r05_session26/).  A real kubelet has the node's cores.
-    if world > 1:
-        widths["node-agent"] = 4
-    # ranks > 0 idle in a gloo barrier during the timed waves while their runtime endpoint admits pods: on a
-    # single CPU the endpoint thread waited behind gloo's threads for up to 9 ms (N=4/8 rehearsal, 2 CPUs fix it)
-    widths.update({f"rank{r}": 2 for r in range(1, world)})
-    if world > 1:
-        # with N GPUs rank 0's wave driver creates and tracks N x 4 pods per wave: on one CPU the creates trickled
-        # out (scheduler saw the 32nd pod of an N = 8 wave 0.96 ms in, 0.53 ms with a second CPU; per-wave p50
-        # 13.0k -> 19.2k pods/s at N = 8, 10.6k -> 15.7k at N = 4; N = 1 unchanged, profiles/r03_ab/)
-        widths["rank0"] = 2
-    # the fake apiserver's event loops (a shared store): GSX_FAKEAPI_THREADS, else --apiserver-threads, else one loop
-    # at N = 1 and APISERVER_THREADS_MULTI at N > 1, each on its own CPU
-    api_threads = int(os.environ.get("GSX_FAKEAPI_THREADS", "0")) or a.apiserver_threads or (
-        1 if world == 1 else APISERVER_THREADS_MULTI)
-    widths["apiserver"] = api_threads
+    names, widths, api_threads = cpu_slots(world, a.runtime_cpu, a.apiserver_threads)
     if a.pin_widths:
         widths.update(json.loads(a.pin_widths))
     mode = a.pin if a.pin != "auto" else "spread"
@@ -1084,6 +1179,12 @@ def main():
                 plugin_row_native = inprocess_matcher_path(a, children, api_url, runner, E)
             except Exception as e:  # noqa: BLE001
                 plugin_row_native = {"error": f"{type(e).__name__}: {e}"}
+    ol = None
+    if rank == 0 and a.open_loop not in ("", "0"):
+        try:
+            ol = open_loop(a, api_url, api_batch, E, profile, inspect_used)
+        except Exception as e:  # noqa: BLE001 - never costs the headline line
+            ol = {"error": f"{type(e).__name__}: {e}"}
     if world > 1:
         dist.barrier(group=ctl)  # every rank's runtime endpoint stays up until rank 0's sweep is done
 
@@ -1178,6 +1279,10 @@ def main():
             "latency_sweep_pods_per_s": {str(r["api_latency_ms"]): r["pods_per_s"] for r in (sweep or [])
                                          if r.get("bind_mode") == "binding" and r.get("bind_order") == a.bind_order},
             "reference_client": ref_client,
+            # open-loop arrivals with many pods in flight (untimed by the headline): the knee per apiserver latency,
+            # and the stage that bounds it (open_loop)
+            "open_loop": ol,
+            "open_loop_knee_pods_per_s": (ol or {}).get("knee_pods_per_s"),
             # the shipped gRPC device plugin on the kubelet path (untimed by the headline, same waves)
             # extra rows (untimed by the headline, same waves): the Python kubelet stand-in driving the shipped plugin
             # process, and the compiled stand-in with the plugin's matcher linked in-process (no gRPC hop)

@@ -44,6 +44,7 @@ import grpc
 from ..k8s.client import ApiError, KubeClient
 from ..models import pod as podutil
 from ..models.profile import (NODE_ALLOCATE_ORDER_ANNOTATION, NODE_DEVICE_INFO_ANNOTATION, NODE_DEVICE_MEMORY_ANNOTATION,
+                              NODE_PHYSICAL_PUBLICATION_ANNOTATION,
                               POD_CU_MASK_ANNOTATION, NamingProfile)
 from . import api
 from ..k8s.informer import Handler, Informer
@@ -93,13 +94,17 @@ ALLOCATE_ATTEMPTS = 8  # per container request: transient apiserver failures ret
 INFORMER_WAIT_S = 0.02  # how long an Allocate waits for the pod event before LISTing
 PHYSICAL_TTL_S = 60.0  # the extender drops a physical-use publication this plugin stopped refreshing
 PHYSICAL_REFRESH_S = 15.0
+# how often the plugin reads the extender's epoch (GET .../epoch, a few bytes): a restarted extender or a new leader
+# knows nothing of the unaccounted use the old one was told, and holds binds to this node until it is republished
+EPOCH_POLL_S = float(os.environ.get("GSX_PLUGIN_EPOCH_POLL_S", "1.0"))
 SA_TOKEN_FILE = "/var/run/secrets/kubernetes.io/serviceaccount/token"
-GUARD_WAIT_S = 5.0  # how long an Allocate waits for a physically full GPU to drain a stopping container
+# how long an Allocate waits for a physically full GPU to drain a stopping container (env: tests scale it down)
+GUARD_WAIT_S = float(os.environ.get("GSX_PLUGIN_GUARD_WAIT_S", "5.0"))
 # ... and how long when the room it needs is held by deleted pods' containers kubelet still lists: they are stopping,
 # and a failed Allocate fails the pod for good, so the admission waits for them instead -- bounded, since kubelet's
 # admission of every other pod of the node waits behind this call (30 s, the default termination grace, let the
 # kubelet-restart chaos rows time out with admissions queued: 1 of 1900 seeds)
-GUARD_GONE_WAIT_S = 10.0
+GUARD_GONE_WAIT_S = float(os.environ.get("GSX_PLUGIN_GUARD_GONE_WAIT_S", "10.0"))
 POD_ANNOTATION = "gpushare.amd.com/pod"  # container annotation: the pod this Allocate was matched to
 
 
@@ -216,6 +221,7 @@ class GpuSharePlugin:
         self._tok = None  # (file stamp, service-account token) for the extender's endpoints
         self._phys_published: list | None = None  # the unaccounted use last published to the extender (None: none)
         self._phys_at = 0.0
+        self._ext_epoch: str | None = None  # the extender epoch our last publication reached
         self.reconciler = None
         if podresources_socket:
             from .reconcile import Reconciler  # noqa: PLC0415
@@ -613,6 +619,11 @@ class GpuSharePlugin:
             try:
                 with open(path) as f:
                     for line in f:
+                        # a mapped journal is zero-padded past its lines: a generation appended after padding that
+                        # was never trimmed starts with NULs (native dpcore trims .old first; this reads either)
+                        line = line.strip("\x00")
+                        if not line.strip():
+                            continue
                         try:
                             recs.append(json.loads(line))
                             journal_lines += 1
@@ -777,7 +788,8 @@ class GpuSharePlugin:
                 except (ApiError, OSError) as e:
                     if cus and not had_cus:
                         cp.release(rec.uid)
-                    transient = not isinstance(e, ApiError) or e.conflict or e.status >= 500
+                    # a conflict, a 5xx, or a 429 the client's own Retry-After retries did not get through
+                    transient = not isinstance(e, ApiError) or e.transient
                     if not transient or attempt == ALLOCATE_ATTEMPTS - 1:
                         raise AllocateError(f"marking {rec.key} assigned failed: {e}") from e
                     self.stats["allocate_retries"] += 1
@@ -811,8 +823,10 @@ class GpuSharePlugin:
         return sum(r.units for r in self.state.records.values() if r.dev == dev and r.owner.startswith(GONE))
 
     def _annotated_used(self, dev: int, skip: str = "") -> int:
-        """Units the pod annotations put on ``dev`` (what the extender's ledger accounts)."""
-        return sum(p.request for p in self.state.pods.values() if p.dev == dev and p.uid != skip and not p.complete)
+        """Units the pod annotations put on ``dev`` (what the extender's ledger accounts): the live pods, and the
+        terminating ones -- the extender keeps their share charged until their objects are gone."""
+        return (sum(p.request for p in self.state.pods.values() if p.dev == dev and p.uid != skip and not p.complete)
+                + self.state.core.terminating_used(dev))
 
     def _kubelet_bounds(self, dev: int, ids) -> bool:
         """kubelet's own per-ID accounting bounds GPU ``dev``: this Allocate's IDs all lie on it and so do those of
@@ -858,10 +872,12 @@ class GpuSharePlugin:
             await asyncio.sleep(delay)
             delay = min(0.2, delay * 2)
         if rec.uid in self.reconciler.busy():
+            self.stats["physical_guard_failed"] = self.stats.get("physical_guard_failed", 0) + 1
             raise AllocateError(f"GPU {rec.dev} of {self.node} is physically full and {rec.key} is in an unfinished "
                                 f"reconciliation exchange")
         best = self.room_for(rec, units)
         if best < 0:
+            self.stats["physical_guard_failed"] = self.stats.get("physical_guard_failed", 0) + 1
             keys = {p.uid: p.key for p in self.state.pods.values()}
             held = [f"{keys.get(r.holder, r.holder)}:{r.units}" for r in self.state.records.values() if r.dev == rec.dev]
             raise AllocateError(f"GPU {rec.dev} of {self.node} is physically full ({self._physical_used(rec.dev)} of "
@@ -920,13 +936,60 @@ class GpuSharePlugin:
             self.stats["moves_refused"] = self.stats.get("moves_refused", 0) + 1
             raise ApiError(r.status, "Conflict" if r.status == 409 else "", out.get("Error") or r.body[:200])
         self.stats["moves"] = self.stats.get("moves", 0) + 1
+        if out.get("epoch") and out["epoch"] != self._ext_epoch and self.publishes_physical:
+            self._schedule_republish()
         return out["pod"]
 
-    async def _extender_post(self, path: str, body: dict):
-        """POST to the scheduler extender's device-plugin endpoints, with this plugin's service-account token when
-        it has one (the extender reviews it: ``--plugin-auth tokenreview``).  Raises ApiError(503) on transport."""
+    @property
+    def publishes_physical(self) -> bool:
+        """This plugin tells the extender its unaccounted GPU use (it reconciles with kubelet's PodResources and
+        knows the extender): advertised on the node (NODE_PHYSICAL_PUBLICATION_ANNOTATION)."""
+        return bool(self.extender_url) and self.reconciler is not None
+
+    def _schedule_republish(self):
+        t = asyncio.get_running_loop().create_task(self.publish_physical(force=True))
+        self._slow.add(t)
+        t.add_done_callback(self._slow.discard)
+
+    async def check_epoch(self) -> bool:
+        """Read the extender's epoch; when it is not the one our last publication reached (a restarted extender,
+        a new leader), publish again at once -- that extender holds binds to this node until then.  True when the
+        publication is current."""
         import json  # noqa: PLC0415
 
+        try:
+            r = await self._extender_request("GET", "/gpushare-scheduler/epoch")
+            d = json.loads(r.body or b"{}") if r.status == 200 else {}
+        except (ApiError, ValueError):
+            return False
+        epoch = d.get("epoch")
+        if not epoch or not d.get("leader", True):
+            return False
+        if epoch == self._ext_epoch:
+            return True
+        self.stats["epoch_changes"] = self.stats.get("epoch_changes", 0) + 1
+        log.info("scheduler extender epoch %s -> %s: republishing the unaccounted GPU use", self._ext_epoch, epoch)
+        return await self.publish_physical(force=True)
+
+    async def _epoch_loop(self):
+        while not self._stopped:
+            try:
+                await self.check_epoch()
+            except asyncio.CancelledError:
+                raise
+            except Exception as e:  # noqa: BLE001 - the loop outlives a bad poll
+                log.debug("extender epoch poll: %r", e)
+            await asyncio.sleep(EPOCH_POLL_S)
+
+    async def _extender_post(self, path: str, body: dict):
+        import json  # noqa: PLC0415
+
+        return await self._extender_request("POST", path, json.dumps(body).encode())
+
+    async def _extender_request(self, method: str, path: str, data: bytes | None = None):
+        """A request to the scheduler extender's device-plugin endpoints, with this plugin's service-account token
+        when it has one (the extender reviews it: ``--plugin-auth tokenreview``).  Raises ApiError(503) on
+        transport."""
         if self._ext is None:
             from ..k8s.fasthttp import Client as HttpClient  # noqa: PLC0415
 
@@ -936,7 +999,7 @@ class GpuSharePlugin:
         if tok:
             headers = {"Authorization": f"Bearer {tok}"}
         try:
-            return await self._ext.request("POST", path, json.dumps(body).encode(), content_type="application/json",
+            return await self._ext.request(method, path, data, content_type="application/json" if data else None,
                                            headers=headers)
         except OSError as e:
             raise ApiError(503, "ServiceUnavailable", f"scheduler extender: {e}") from e
@@ -977,8 +1040,8 @@ class GpuSharePlugin:
                 # chaos seeds then stalled with binds refused, 4 of 380 failing vs 0-2)
                 continue
             p = None if r.owner.startswith("~") else pods.get(r.owner)
-            # a holder that is gone: its container is stopping, as for any deleted pod (the extender frees on
-            # deletion, as the reference does)
+            # a holder that is gone: its container has stopped (kubelet removes a gracefully deleted pod's object only
+            # then) or is stopping (a force delete; the physical guard waits for it)
             if p is not None and not p.complete and p.dev != r.dev:
                 out[r.dev] += r.units
                 found = True
@@ -1007,6 +1070,12 @@ class GpuSharePlugin:
             log.warning("the extender refused the unaccounted GPU use: %s %s", r.status, r.body[:200])
             return False
         self._phys_published, self._phys_at = extra, now
+        try:
+            import json  # noqa: PLC0415
+
+            self._ext_epoch = json.loads(r.body or b"{}").get("epoch") or self._ext_epoch
+        except ValueError:
+            pass
         self.stats["physical_published"] = self.stats.get("physical_published", 0) + 1
         log.debug("published unaccounted GPU use %s", extra)
         return True
@@ -1183,7 +1252,8 @@ class GpuSharePlugin:
         await self.client.patch("nodes", self.node, {"metadata": {"annotations": {
             NODE_DEVICE_MEMORY_ANNOTATION: ",".join(str(t) for t in totals),
             NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv, separators=(",", ":")),
-            NODE_ALLOCATE_ORDER_ANNOTATION: "landing"}}})
+            NODE_ALLOCATE_ORDER_ANNOTATION: "landing",
+            NODE_PHYSICAL_PUBLICATION_ANNOTATION: "true" if self.publishes_physical else None}}})
         await self.client.patch("nodes", self.node, {"status": {"capacity": {
             self.profile.count: str(len(self.devices))}}}, sub="status")
 
@@ -1374,6 +1444,8 @@ class GpuSharePlugin:
             self.isolation.gc({r.iso for r in self.state.records.values() if r.iso} | set(self.state.pods))
         if self.reconciler is not None:
             self.reconciler.start()
+        if self.publishes_physical:
+            self._tasks.append(asyncio.get_running_loop().create_task(self._epoch_loop(), name="gsx-epoch"))
         if not serve:
             return
         await self.serve()

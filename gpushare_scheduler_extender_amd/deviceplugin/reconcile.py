@@ -93,7 +93,13 @@ class Reconciler:
         # after an ambiguous Allocate (kubelet records an Allocate's IDs before it returns to its admission loop;
         # a pass skips records made after it asked, so a short delay only saves passes)
         self.after_ambiguous = 0.002
+        # while a publication stands, poll kubelet this often at first, doubling (to unaccounted_poll_max) while the
+        # published vector does not change: a drift with no partner can keep one standing, and kubelet's PodResources
+        # budget (100 calls/s) is the node's, not ours
         self.unaccounted_poll = 0.01
+        self.unaccounted_poll_max = 0.5
+        self._poll = self.unaccounted_poll
+        self._poll_for = None  # the publication _poll was backed off for
         # kubelet rate-limits its PodResources API (100 calls/s, burst 10, since k8s 1.27): passes stay >= 10 ms apart
         self.min_spacing = float(os.environ.get("GSX_RECONCILE_MIN_SPACING", "0.01"))
         self._last_pass = 0.0
@@ -118,6 +124,7 @@ class Reconciler:
         """``urgent``: an Allocate found no candidate -- reset orphaned ``ASSIGNED`` marks without waiting."""
         async with self._lock:
             self.stats["passes"] += 1
+            self._last_pass = time.monotonic()  # urgent passes (the guard's, a miss's) count against min_spacing too
             t0 = time.perf_counter()
             # kubelet's answer describes the Allocates made before it was asked: the native endpoint keeps serving
             # (and recording) while it is awaited, and kubelet re-uses the IDs of finished pods -- a record made
@@ -457,7 +464,15 @@ class Reconciler:
         while True:
             # while the extender charges unaccounted use, look again soon: it is withdrawn as soon as kubelet's report
             # lets the records go (a stale publication would keep the GPU from the next pods)
-            wait = self.interval if self.plugin._phys_published is None else min(self.interval, self.unaccounted_poll)
+            pub = self.plugin._phys_published
+            if pub is None:
+                wait, self._poll, self._poll_for = self.interval, self.unaccounted_poll, None
+            else:
+                if pub == self._poll_for:  # unchanged since the last pass: back off
+                    self._poll = min(self.unaccounted_poll_max, self._poll * 2)
+                else:
+                    self._poll, self._poll_for = self.unaccounted_poll, list(pub)
+                wait = min(self.interval, self._poll)
             try:
                 await asyncio.wait_for(self._kick.wait(), wait)
                 # let kubelet record the allocation first

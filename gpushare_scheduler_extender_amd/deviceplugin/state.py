@@ -278,6 +278,7 @@ class AllocationState:
         ap.dev, ap.request, ap.containers, ap.assume_time = rec.dev, rec.request, rec.containers, rec.assume_time
         ap.assigned, ap.complete, ap.cu_count, ap.cu_mask = rec.assigned, rec.complete, rec.cu_count, rec.cu_mask
         ap.hold_idx, ap.hold_partner = rec.hold_idx, rec.hold_partner
+        ap.terminating = bool(podutil.meta(pod).get("deletionTimestamp")) and not podutil.is_terminal(pod)
         try:
             ap.dev_total = int(podutil.annotations(pod).get(self.profile.annotation_dev, "-1") or -1)
         except ValueError:

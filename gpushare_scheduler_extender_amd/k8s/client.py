@@ -14,6 +14,11 @@ handful of core/v1 verbs, so this is a small hand-written client on
   flags of the extender;
 * typed errors carrying the HTTP status so conflicts are detected by ``409``
   rather than by comparing message strings (``pkg/cache/nodeinfo.go:153``);
+* client-go's retry contract (``vendor/k8s.io/client-go/rest/request.go:658-734,973-995``): a ``429 Too Many
+  Requests`` -- API Priority and Fairness rejected the request before it ran, so every verb is safe to repeat -- or
+  a 5xx carrying ``Retry-After`` is sent again after the server's ``Retry-After``, up to 10 sends; a 429 without
+  it waits a capped exponential backoff with jitter.  A 5xx without ``Retry-After`` goes to the caller (a write
+  may have been applied; the caller knows whether repeating it is safe), as in client-go;
 * streaming watches yielding decoded events, with ``410 Gone`` surfaced as
   :class:`ApiError` so reflectors re-list.
 """
@@ -24,6 +29,7 @@ import base64
 import json
 import logging
 import os
+import random
 import ssl
 import tempfile
 import time
@@ -58,6 +64,36 @@ class ApiError(Exception):
     @property
     def gone(self) -> bool:
         return self.status == 410
+
+    @property
+    def throttled(self) -> bool:
+        return self.status == 429
+
+    @property
+    def transient(self) -> bool:
+        """Worth repeating later: a conflict (re-read and retry), throttling, or a server-side error."""
+        return self.status in (409, 429) or self.status >= 500
+
+
+def retry_wait(status: int, retry_after: str | None, attempt: int, max_attempts: int = 10,
+               backoff_base: float = 0.005, backoff_max: float = 1.0, retry_after_max: float = 30.0,
+               jitter: float | None = None) -> float | None:
+    """Seconds to wait before sending a request again that was answered ``status`` (with header ``retry_after``) on
+    send ``attempt`` (0-based); None: do not retry.  The native twin is ``ApiClient::retry_wait``
+    (``native/engine/apiclient.cc``)."""
+    if attempt + 1 >= max_attempts or (status != 429 and status < 500):
+        return None
+    if retry_after:
+        try:
+            s = float(retry_after)
+        except ValueError:
+            s = -1.0  # an HTTP-date: treated as absent
+        if s >= 0:
+            return min(s, retry_after_max)
+    if status != 429:
+        return None
+    b = min(backoff_max, backoff_base * 2 ** min(attempt, 20))
+    return b * (0.5 + 0.5 * (random.random() if jitter is None else jitter))
 
 
 class RateLimiter:
@@ -218,8 +254,12 @@ def _ns_path(kind: str, ns: str | None, name: str | None = None, sub: str | None
 
 class KubeClient:
     def __init__(self, config: KubeConfig | str, qps: float = 0.0, burst: int = 1000,
-                 user_agent: str = "gpushare-schd-extender-amd/0.1.0", connector_limit: int = 256):
+                 user_agent: str = "gpushare-schd-extender-amd/0.1.0", connector_limit: int = 256,
+                 max_attempts: int = 10):
         self.config = KubeConfig.from_url(config) if isinstance(config, str) else config
+        self.max_attempts = max(1, int(max_attempts))  # sends per request under 429 / Retry-After (1: no retry)
+        self.throttled = 0  # responses sent again after a 429 / Retry-After
+        self.throttle_wait_s = 0.0
         self.limiter = RateLimiter(qps, burst)
         self.user_agent = user_agent
         self._limit = connector_limit
@@ -264,20 +304,30 @@ class KubeClient:
 
     async def request(self, method: str, path: str, *, params: dict | None = None, body=None,
                       content_type: str = "application/json", timeout: float | None = 30.0):
-        if self.limiter.qps > 0:
-            await self.limiter.acquire()
         if params:
             path += "?" + urlencode(params)
         data = None
         if body is not None:
             data = body if isinstance(body, bytes) else (body.encode() if isinstance(body, str) else
                                                           json.dumps(body, separators=(",", ":")).encode())
-        self.calls += 1
-        r = await self._client().request(method, path, data, content_type if data is not None else None,
-                                         timeout=timeout)
-        if r.status >= 400:
-            self._raise(r.status, r.body)
-        return json.loads(r.body) if r.body else None
+        attempt = 0
+        while True:
+            if self.limiter.qps > 0:  # every send, retries too (client-go's tryThrottle)
+                await self.limiter.acquire()
+            self.calls += 1
+            r = await self._client().request(method, path, data, content_type if data is not None else None,
+                                             timeout=timeout)
+            if r.status < 400:
+                return json.loads(r.body) if r.body else None
+            wait = retry_wait(r.status, (r.headers or {}).get("retry-after"), attempt, self.max_attempts)
+            if wait is None:
+                self._raise(r.status, r.body)
+            self.throttled += 1
+            self.throttle_wait_s += wait
+            log.debug("%s %s answered %d: sending it again in %.3f s (attempt %d)", method, path, r.status, wait,
+                      attempt + 1)
+            await asyncio.sleep(wait)
+            attempt += 1
 
     # ------------------------------------------------------------ verbs
     async def get(self, kind: str, name: str, ns: str | None = None) -> dict:
@@ -321,9 +371,17 @@ class KubeClient:
               "strategic": "application/strategic-merge-patch+json"}[patch_type]
         return await self.request("PATCH", _ns_path(kind, ns, name, sub), body=patch, content_type=ct)
 
-    async def delete(self, kind: str, name: str, ns: str | None = None, grace_seconds: float | None = None):
+    async def delete(self, kind: str, name: str, ns: str | None = None, grace_seconds: float | None = None,
+                     uid: str | None = None):
+        """DELETE; ``uid`` adds a ``preconditions.uid`` (409 if the object under that name is another one), as
+        kubelet's final grace-0 delete of a terminated pod does."""
         params = {"gracePeriodSeconds": str(int(grace_seconds))} if grace_seconds is not None else None
-        return await self.request("DELETE", _ns_path(kind, ns, name), params=params)
+        body = None
+        if uid:
+            body = {"kind": "DeleteOptions", "apiVersion": "v1", "preconditions": {"uid": uid}}
+            if grace_seconds is not None:
+                body["gracePeriodSeconds"] = int(grace_seconds)
+        return await self.request("DELETE", _ns_path(kind, ns, name), params=params, body=body)
 
     async def bind_pod(self, ns: str, name: str, node: str, uid: str | None = None,
                        annotations: dict | None = None) -> None:

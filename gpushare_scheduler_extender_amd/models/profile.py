@@ -16,6 +16,9 @@ NODE_DEVICE_INFO_ANNOTATION = "gpushare.amd.com/devices"  # JSON device inventor
 # "landing": the node's device plugin matches an Allocate to the earliest pod *landed* on the node (kubelet's
 # admission order, native/engine/allocstate.h); the extender then needs no ASSUME_TIME order of binds there
 NODE_ALLOCATE_ORDER_ANNOTATION = "gpushare.amd.com/allocate-order"
+# "true": the node's device plugin publishes its unaccounted GPU use to the extender (POST .../physical); after an
+# extender restart or leader change binds to the node wait for its first publication (native/engine/ledger.h)
+NODE_PHYSICAL_PUBLICATION_ANNOTATION = "gpushare.amd.com/physical-publication"
 POD_CU_MASK_ANNOTATION = "gpushare.amd.com/cu-mask"  # per-pod CU partition (isolation)
 POD_CU_COUNT_ANNOTATION = "gpushare.amd.com/cu-count"  # the pod asks for a CU partition of this size
 POD_ASSIGN_TIME_ANNOTATION = "gpushare.amd.com/assign-time"

@@ -22,10 +22,12 @@ from __future__ import annotations
 
 import fcntl
 import json
+import logging
 import os
 import tempfile
 import time
 
+log = logging.getLogger("gsx.cpuset")
 IDLE = 0.05  # a CPU busier than this (other jobs, interrupts) over the sample window is avoided
 
 
@@ -165,6 +167,8 @@ def plan(names: list[str], widths: dict[str, int] | None = None, mode: str = "sp
         need = sum((w + 1) // 2 for w in per.values())
         ordered = _order_cores(cores, load if mode == "spread" else None, sum((per[n] + 1) // 2 for n in near))
         if len(ordered) < need:
+            log.warning("CPU plan: %d physical cores asked for (%d processes), %d allowed: not pinning", need,
+                        len(names), len(ordered))
             return {}
         out, i = {}, 0
         for n in names:
@@ -176,6 +180,8 @@ def plan(names: list[str], widths: dict[str, int] | None = None, mode: str = "sp
     ordered = _order_cores(cores, load if mode == "spread" else None, sum(per[n] for n in near))
     cpus = [core[0] for core in ordered] + [c for core in ordered for c in core[1:]]
     if len(cpus) < need:
+        log.warning("CPU plan: %d CPUs asked for (%d processes), %d allowed: not pinning", need, len(names),
+                    len(cpus))
         return {}
     out, i = {}, 0
     for n in names:

@@ -34,7 +34,11 @@ container env -> the pod runs on the chosen GPU.
   of device IDs per container is served on the PodResources API (:mod:`.podresources`), which the plugin
   reconciles against (:mod:`.reconcile`).  ``/v1/allocations/<uid>`` is then the container's real env.
 * A pod that completes or is deleted is stopped and its slice released; the
-  plugin's own informer releases its CU partition.
+  plugin's own informer releases its CU partition.  A graceful deletion is ended
+  the way kubelet ends it: the pod's containers stop (``stop_delay`` seconds, at
+  most its grace period), its slice is released and kubelet's PodResources record
+  drops it, the terminal phase is reported, and the object is deleted with grace 0
+  under a UID precondition -- the apiserver never removes it on its own.
 
 With ``devices`` set to a subset of the node's GPUs, only pods whose
 ``*_IDX`` annotation names one of them are admitted, so one agent per GPU
@@ -70,7 +74,8 @@ class NodeAgent:
     def __init__(self, client: KubeClient, node: str, devices: list[Device], profile: NamingProfile, runtime, *,
                  unit: str = "GiB", verify_each: bool = True, mount_mode: str = "isolated", report_status: bool = True,
                  workers: int = 8, plugin: GpuSharePlugin | None = None, plugin_socket: str | None = None,
-                 faithful: bool = False, batch_window: float = 0.0, podresources_socket: str | None = None):
+                 faithful: bool = False, batch_window: float = 0.0, podresources_socket: str | None = None,
+                 stop_delay: float = 0.0):
         self.client = client
         self.node = node
         self.devices = {d.index: d for d in devices}
@@ -104,6 +109,9 @@ class NodeAgent:
                        "runtime": 0.0, "status_patch": 0.0}
         self._bg: set[asyncio.Task] = set()
         self._releasing: set[asyncio.Task] = set()
+        self.stop_delay = stop_delay
+        self._terminating: set[str] = set()  # uids whose graceful deletion this kubelet is ending
+        self.finalized = 0
         self.admit_q: asyncio.Queue = asyncio.Queue()
         # a pod whose Allocate went to another pod is admitted next, ahead of later arrivals: it was bound before
         # them, and at the back of the queue it would push every later Allocate one pod off (a cascade a real
@@ -137,6 +145,10 @@ class NodeAgent:
 
     def _on_pod(self, pod: dict, raw):
         uid = podutil.meta(pod).get("uid", "")
+        if podutil.meta(pod).get("deletionTimestamp") and not podutil.is_terminal(pod):
+            if podutil.gpu_id_from_annotation(pod, self.profile) < 0 or self._mine(pod):
+                self._terminate(pod)
+            return
         if podutil.is_complete(pod):
             self._stop(uid)
             return
@@ -170,6 +182,46 @@ class NodeAgent:
         self.id_keys.pop(uid, None)
         if self.running.pop(uid, None) is not None:
             self._release(uid)
+
+    def _terminate(self, pod: dict):
+        uid = podutil.meta(pod).get("uid", "")
+        if not uid or uid in self._terminating:
+            return
+        self._terminating.add(uid)
+        t = asyncio.get_running_loop().create_task(self._finalize(pod))
+        self._bg.add(t)
+        t.add_done_callback(self._bg.discard)
+
+    async def _finalize(self, pod: dict):
+        """kubelet's end of a graceful deletion: SIGTERM the containers and give them ``stop_delay`` (at most the
+        grace period) to exit, release what they held, report the terminal phase, then delete the object with grace
+        0 and a UID precondition."""
+        md = podutil.meta(pod)
+        uid = md["uid"]
+        ran = uid in self.running or uid in self.claimed
+        try:
+            if ran and self.stop_delay > 0:
+                grace = md.get("deletionGracePeriodSeconds")
+                await asyncio.sleep(min(self.stop_delay, float(grace)) if grace is not None else self.stop_delay)
+            self._stop(uid)
+            if self._releasing:
+                await asyncio.gather(*list(self._releasing), return_exceptions=True)
+            if ran and self.report_status:
+                await self._patch_status(pod, {"phase": "Succeeded"})
+            for attempt in range(50):
+                try:
+                    await self.client.delete("pods", md["name"], md["namespace"], grace_seconds=0, uid=uid)
+                    break
+                except ApiError as e:
+                    # 404: gone already; 409: the UID precondition failed (a new pod took the name)
+                    if e.not_found or e.conflict or (400 <= e.status < 500 and e.status != 429):
+                        break
+                except OSError:
+                    pass
+                await asyncio.sleep(min(0.1, 0.0005 * 2 ** min(attempt, 8)))
+            self.finalized += 1
+        finally:
+            self._terminating.discard(uid)
 
     def _release(self, uid: str):
         rel = getattr(self.runtime, "release", None)
@@ -413,7 +465,7 @@ class NodeAgent:
                 await self.client.patch("pods", md["name"], {"status": status}, md["namespace"], sub="status")
                 return
             except ApiError as e:
-                if e.not_found or not (e.conflict or e.status >= 500):
+                if e.not_found or not e.transient:
                     return
             except OSError:
                 pass
@@ -541,6 +593,7 @@ async def serve_stats(box: dict, host: str = "127.0.0.1", port: int = 0):
         body = {"admitted": agent.admitted, "failed": agent.failed, "bad_stamps": agent.bad_stamps,
                 "running": len(agent.running), "admit_p50_ms": round(1e3 * lat[len(lat) // 2], 3) if lat else 0.0,
                 "admit_max_ms": round(1e3 * lat[-1], 3) if lat else 0.0, **agent.stats, "native": False,
+                "finalized": agent.finalized,
                 "plugin": ("process" if getattr(agent, "plugin_stats_url", None) else "grpc")
                 if agent.pclient is not None else "inproc"}
         n = max(1, agent.timing["n"])
@@ -641,6 +694,9 @@ def main(argv=None) -> int:
     ap.add_argument("--isolation-dir", default="",
                     help="enforced isolation: the plugin writes each pod's config + HBM ledger here (and answers the "
                          "container mounts); '' = advisory env only")
+    ap.add_argument("--stop-delay", type=float, default=0.0,
+                    help="seconds a container takes to stop after SIGTERM on a graceful deletion (capped by the pod's "
+                         "grace period); kubelet deletes the object once it has")
     ap.add_argument("--port-file", default="")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.WARNING)
@@ -673,16 +729,16 @@ def main(argv=None) -> int:
             await plugin.start(register=False, publish=False)
             agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
                               workers=a.workers, plugin_socket=plugin.socket_path, faithful=a.faithful,
-                              batch_window=window, podresources_socket=prsock)
+                              batch_window=window, podresources_socket=prsock, stop_delay=a.stop_delay)
         elif a.plugin == "process":
             child, endpoint, stats_url = await _spawn_plugin(a, sock_dir, devs, prsock, box)
             agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
                               workers=a.workers, plugin_socket=endpoint, faithful=a.faithful,
-                              batch_window=window, podresources_socket=prsock)
+                              batch_window=window, podresources_socket=prsock, stop_delay=a.stop_delay)
             agent.plugin_stats_url = stats_url
         else:
             agent = NodeAgent(client, a.node, devs, profile, rt, unit=a.unit, verify_each=not a.no_verify,
-                              workers=a.workers)
+                              workers=a.workers, stop_delay=a.stop_delay)
         await agent.start()
         if plugin is not None:
             agent.plugin = plugin  # for /v1/stats

@@ -61,12 +61,24 @@ def _current(out: Path, srcs: list[Path], headers: list[Path], force: bool) -> b
 
 
 def _run(cmd: list[str], verbose: bool) -> None:
+    # an artifact under _native/ is linked to a temporary name and renamed over the old one: a process that has the
+    # old library mapped (a test run, a plugin) keeps its inode, instead of reading a file rewritten under it
+    final = None
+    if "-o" in cmd:
+        i = cmd.index("-o") + 1
+        if i < len(cmd) and Path(cmd[i]).parent == OUT:
+            final = cmd[i]
+            cmd = [*cmd[:i], f"{final}.tmp{os.getpid()}", *cmd[i + 1:]]
     if verbose:
         print("+", " ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
+        if final:
+            Path(f"{final}.tmp{os.getpid()}").unlink(missing_ok=True)
         raise RuntimeError(f"native build failed: {' '.join(cmd[:3])} ... (exit {r.returncode})")
+    if final:
+        os.replace(f"{final}.tmp{os.getpid()}", final)
 
 
 def _compile_objs(srcs: list[Path], compiler: str, flags: list[str], tag: str, force: bool, verbose: bool,

@@ -183,6 +183,10 @@ bool parse_alloc_pod(const json::Doc& d, uint32_t pod, const Profile& p, AllocPo
   out->assume_time = v.assume_time;
   out->dev_total = v.annot_dev_total;
   out->complete = v.complete();
+  out->terminating = v.deleting && !v.terminal();
+  int64_t gp = d.path(pod, {"metadata", "deletionGracePeriodSeconds"});
+  int64_t gv = -1;
+  out->grace_s = (gp >= 0 && d.as_int(static_cast<uint32_t>(gp), &gv)) ? static_cast<double>(gv) : -1.0;
   out->cu_mask = v.cu_mask;
   out->hold_idx = v.hold_idx;
   out->assigned.clear();
@@ -244,12 +248,21 @@ AllocState::AllocState(std::string node, const std::vector<std::pair<int, std::p
 
 bool AllocState::observe(const AllocPod& p) {
   if (p.uid.empty()) return false;
-  if (gone_.count(p.uid)) return false;  // deleted or complete: a late copy never brings it back
+  if (gone_.count(p.uid)) {  // deleted or complete: a late copy never brings it back
+    auto t = terminating_.find(p.uid);
+    if (t != terminating_.end() && p.complete && !p.terminating) terminating_.erase(t);  // now terminal
+    return false;
+  }
   auto prev = pods_.find(p.uid);
   if (prev != pods_.end() && older_rv(p.rv, prev->second.rv)) return false;  // a slow LIST racing the watch
   if (p.complete) {
     tombstone(p.uid);
     release(p.uid);
+    if (p.terminating && p.node == node_ && p.request > 0 && p.dev >= 0) {
+      terminating_[p.uid] = Terminating{p.dev, p.request, p.hold_idx};
+    } else {
+      terminating_.erase(p.uid);  // terminal now: the extender freed it
+    }
     return true;
   }
   if (p.node != node_ || p.request <= 0) {
@@ -335,6 +348,21 @@ void AllocState::tombstone(const std::string& uid) {
 void AllocState::deleted(const std::string& uid) {
   tombstone(uid);
   release(uid);
+  terminating_.erase(uid);
+}
+
+int64_t AllocState::terminating_used(int64_t dev) const {
+  int64_t n = 0;
+  for (const auto& kv : terminating_) {
+    // a hold charges the hold device too (the extender's ledger.cc account())
+    if (kv.second.dev == dev || (kv.second.hold >= 0 && kv.second.hold == dev)) n += kv.second.request;
+  }
+  return n;
+}
+
+int64_t AllocState::terminating_dev(const std::string& uid) const {
+  auto it = terminating_.find(uid);
+  return it == terminating_.end() ? -1 : it->second.dev;
 }
 
 std::vector<std::string> AllocState::holders() const {
@@ -351,6 +379,13 @@ std::vector<std::string> AllocState::holders() const {
 void AllocState::resync(const std::unordered_set<std::string>& live) {
   for (const auto& uid : holders()) {
     if (!live.count(uid)) release(uid);
+  }
+  for (auto it = terminating_.begin(); it != terminating_.end();) {
+    if (!live.count(it->first)) {
+      it = terminating_.erase(it);
+    } else {
+      ++it;
+    }
   }
 }
 

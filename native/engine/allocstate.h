@@ -82,6 +82,11 @@ struct AllocPod {
   int64_t dev_total = -1;     // *_DEV annotation
   std::string assigned;       // ASSIGNED annotation value ("" absent)
   bool complete = false;
+  // deletionTimestamp set, phase not terminal: kubelet is stopping its containers.  Complete for matching (no
+  // Allocate serves it), but the scheduler extender keeps its share charged until the object is gone
+  // (controller.cc sync), so the annotated account below keeps it too
+  bool terminating = false;
+  double grace_s = -1;        // metadata.deletionGracePeriodSeconds (-1 absent)
   int cu_count = 0;           // gpushare.amd.com/cu-count
   std::string cu_mask;        // gpushare.amd.com/cu-mask
   int64_t hold_idx = -1;      // gpushare.amd.com/hold-idx
@@ -134,6 +139,11 @@ class AllocState {
   // A complete LIST of this node's pods (already observed): anything held that is not in `live` is gone.
   void resync(const std::unordered_set<std::string>& live);
   std::vector<std::string> holders() const;
+  // ---- terminating pods (AllocPod::terminating): what the extender still charges for them, per GPU
+  int64_t terminating_used(int64_t dev) const;
+  // the GPU a terminating pod's annotation names (-1: not terminating here)
+  int64_t terminating_dev(const std::string& uid) const;
+  size_t terminating_count() const { return terminating_.size(); }
 
   // ---- Allocate
   std::vector<const AllocPod*> candidates() const;
@@ -208,6 +218,10 @@ class AllocState {
   std::string node_;
   std::map<int, CuPartitioner> cus_;
   std::unordered_map<std::string, AllocPod> pods_;        // uid -> non-complete pods on this node
+  struct Terminating {
+    int64_t dev = -1, request = 0, hold = -1;
+  };
+  std::unordered_map<std::string, Terminating> terminating_;  // uid -> terminating pods on this node
   std::unordered_map<std::string, double> gone_;          // deleted / complete UIDs -> when (see deleted())
   std::deque<std::pair<double, std::string>> gone_order_;
   std::unordered_map<std::string, std::string> keys_;     // ns/name -> uid

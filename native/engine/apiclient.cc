@@ -82,9 +82,39 @@ ApiClient::~ApiClient() {
 }
 
 void ApiClient::abort() {
-  std::lock_guard<std::mutex> g(mu_);
-  aborted_ = true;
-  for (int fd : busy_) ::shutdown(fd, SHUT_RDWR);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    aborted_ = true;
+    for (int fd : busy_) ::shutdown(fd, SHUT_RDWR);
+  }
+  std::lock_guard<std::mutex> w(wait_mu_);
+  wait_cv_.notify_all();
+}
+
+bool ApiClient::wait_or_abort(double seconds) {
+  std::unique_lock<std::mutex> w(wait_mu_);
+  return !wait_cv_.wait_for(w, std::chrono::duration<double>(seconds), [this] {
+    std::lock_guard<std::mutex> g(mu_);
+    return aborted_;
+  });
+}
+
+double ApiClient::retry_wait(const ApiConfig& cfg, const std::string& method, int status,
+                             const std::string& retry_after, int attempt, double jitter01) {
+  (void)method;  // 429s are rejected before any handler ran: every verb is safe to repeat
+  if (attempt + 1 >= cfg.max_attempts) return -1;
+  const bool throttled = status == 429;
+  if (!throttled && status < 500) return -1;
+  if (!retry_after.empty()) {
+    char* end = nullptr;
+    double s = std::strtod(retry_after.c_str(), &end);
+    // seconds (client-go reads an integer; a fraction is honoured too); an HTTP-date is treated as absent
+    if (end != retry_after.c_str() && *end == '\0' && s >= 0) return std::min(s, cfg.retry_after_max_s);
+  }
+  if (!throttled) return -1;  // 5xx without Retry-After: the caller decides
+  double b = cfg.backoff_base_s * static_cast<double>(1ull << std::min(attempt, 20));
+  b = std::min(b, cfg.backoff_max_s);
+  return b * (0.5 + 0.5 * jitter01);  // jitter: [b/2, b)
 }
 
 void ApiClient::close_conn(Conn* c) {
@@ -382,9 +412,32 @@ bool ApiClient::request(const std::string& method, const std::string& path, cons
     *err = init_err_;
     return false;
   }
-  std::string req = request_head(method, path, body.size(), content_type,
-                                 !body.empty() || method == "POST" || method == "PUT" || method == "PATCH");
-  req.append(body);
+  const bool has_body = !body.empty() || method == "POST" || method == "PUT" || method == "PATCH";
+  thread_local uint64_t rng = 0x9e3779b97f4a7c15ull ^ reinterpret_cast<uintptr_t>(&rng);
+  for (int attempt = 0;; ++attempt) {
+    // the head is rebuilt per send: a rotated service-account token is picked up between attempts
+    std::string req = request_head(method, path, body.size(), content_type, has_body);
+    req.append(body);
+    std::string retry_after;
+    if (!request_once(req, status, resp, err, resp_content_type, &retry_after)) return false;
+    if (*status != 429 && (*status < 500 || retry_after.empty())) return true;
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    const double wait = retry_wait(cfg_, method, *status, retry_after, attempt,
+                                   static_cast<double>(rng >> 11) * (1.0 / 9007199254740992.0));
+    if (wait < 0) return true;  // out of attempts (or not retried): the caller sees the status
+    throttled_.fetch_add(1, std::memory_order_relaxed);
+    throttle_wait_ns_.fetch_add(static_cast<uint64_t>(wait * 1e9), std::memory_order_relaxed);
+    if (!wait_or_abort(wait)) {
+      *err = "apiserver client closed";
+      return false;
+    }
+  }
+}
+
+bool ApiClient::request_once(const std::string& req, int* status, std::string* resp, std::string* err,
+                             std::string* resp_content_type, std::string* retry_after) {
 
   // a request in flight is listed (abort() shuts its socket) until its connection is released
   auto done = [this](Conn* c, bool reuse) {
@@ -453,6 +506,10 @@ bool ApiClient::request(const std::string& method, const std::string& path, cons
     if (resp_content_type) {
       const std::string* ct = m.header("content-type");
       *resp_content_type = ct ? *ct : std::string();
+    }
+    if (m.status == 429 || m.status >= 500) {
+      const std::string* ra = m.header("retry-after");
+      *retry_after = ra ? *ra : std::string();
     }
     *resp = std::move(m.body);
     done(c, m.keep_alive && !m.body_until_close);

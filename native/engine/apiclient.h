@@ -6,6 +6,7 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
 #include <functional>
 #include <string_view>
 #include <memory>
@@ -29,6 +30,15 @@ struct ApiConfig {
   bool insecure = false;
   double timeout_s = 30.0;
   std::string user_agent = "gpushare-schd-extender-amd/0.1.0 (native)";
+  // client-go's contract (vendor/k8s.io/client-go/rest/request.go:658-734,973-995): a 429 Too Many Requests (API
+  // Priority and Fairness rejected the request before it ran, so any method is safe to repeat), or a 5xx that
+  // carries Retry-After, is sent again after the server's Retry-After -- at most max_attempts sends in all.  A 429
+  // without Retry-After waits a capped exponential backoff with jitter instead (backoff_base_s doubling up to
+  // backoff_max_s).  A 5xx without Retry-After is returned to the caller: a write may have been applied, and the
+  // caller knows whether repeating it is safe (the bind path does, with its own backoff).  max_attempts 1: off.
+  int max_attempts = 10;
+  double backoff_base_s = 0.005, backoff_max_s = 1.0;
+  double retry_after_max_s = 30.0;  // a longer Retry-After is clamped (kube-apiserver's APF sends 1-8 s)
 };
 
 // Lets another thread end a running ApiClient::stream() (shuts the socket).
@@ -67,6 +77,13 @@ class ApiClient {
 
   uint64_t requests() const { return requests_; }
   uint64_t reconnects() const { return reconnects_; }
+  // responses answered 429 / 5xx-with-Retry-After that were sent again, and the time spent waiting for that
+  uint64_t throttled() const { return throttled_; }
+  double throttle_wait_s() const { return static_cast<double>(throttle_wait_ns_.load()) * 1e-9; }
+  // the wait before resending a request answered `status` with Retry-After `retry_after` ("" absent) on send
+  // `attempt` (0-based); < 0: not retried (see ApiConfig::max_attempts)
+  static double retry_wait(const ApiConfig& cfg, const std::string& method, int status, const std::string& retry_after,
+                           int attempt, double jitter01);
 
  private:
   struct Conn {
@@ -74,6 +91,12 @@ class ApiClient {
     SSL* ssl = nullptr;
     std::string rbuf;
   };
+  bool request_once(const std::string& req, int* status, std::string* resp, std::string* err,
+                    std::string* resp_content_type, std::string* retry_after);
+  bool wait_or_abort(double seconds);  // false: abort() was called
+  std::mutex wait_mu_;
+  std::condition_variable wait_cv_;
+  std::atomic<uint64_t> throttled_{0}, throttle_wait_ns_{0};
   Conn* acquire(std::string* err);
   Conn* connect_new(std::string* err);
   std::string request_head(const std::string& method, const std::string& path, size_t body_len,

@@ -357,6 +357,7 @@ class Engine {
     if (plugin_auth != "none" && plugin_auth != "tokenreview") throw std::invalid_argument("plugin_auth: none|tokenreview");
     cfg.plugin_auth = plugin_auth;
     cfg.plugin_users = plugin_users;
+    if (const char* h = std::getenv("GSX_PUBLICATION_HOLD_S")) cfg.publication_hold_s = std::atof(h);
     srv_.reset(new NativeServer(&l_, cfg));
     // the controller outlives the server (stop_server runs before stop_controller)
     srv_->set_lister([this](const std::string& key, std::string* raw) { return ctl_ && ctl_->get_pod(key, raw); });
@@ -476,6 +477,12 @@ class Engine {
     d["physical_posts"] = s.physical_posts.load();
     d["plugin_auth_denied"] = s.plugin_auth_denied.load();
     d["token_reviews"] = s.token_reviews.load();
+    d["backoffs"] = s.backoffs.load();
+    d["publication_waits"] = s.publication_waits.load();
+    d["physical_refused"] = s.physical_refused.load();
+    d["epoch"] = srv_->epoch();
+    d["api_throttled"] = srv_->api_throttled();
+    d["api_throttle_wait_s"] = srv_->api_throttle_wait_s();
     auto hist = [](const LatencyHist& h) {
       py::dict o;
       py::list bounds, counts;
@@ -724,6 +731,40 @@ class PyBatchClient {
  private:
   BatchClient c_;
 };
+
+// bench.py --open-loop: constant-rate arrivals, every pod's stage times (tracker.h OpenLoop)
+py::dict open_loop_run(const py::dict& api, const std::string& run, const std::string& pod_tmpl, double rate,
+                       double duration_s, double warm_s, double hold_s, double drain_s, int creators, int deleters,
+                       const std::string& ns) {
+  OpenLoopConfig c;
+  c.run = run;
+  c.pod_tmpl = pod_tmpl;
+  c.rate = rate;
+  c.duration_s = duration_s;
+  c.warm_s = warm_s;
+  c.hold_s = hold_s;
+  c.drain_s = drain_s;
+  c.creators = creators;
+  c.deleters = deleters;
+  c.ns = ns;
+  OpenLoop ol(api_from(api));
+  std::vector<OpenLoopPod> pods;
+  std::string err;
+  int ce = 0, de = 0;
+  bool ok;
+  {
+    py::gil_scoped_release rel;
+    ok = ol.run(c, &pods, &err, &ce, &de);
+  }
+  if (!ok) throw std::runtime_error(err);
+  py::list l;
+  for (const auto& p : pods) l.append(py::make_tuple(p.arrival, p.created, p.bound, p.running, p.deleted, p.gone, p.failed));
+  py::dict d;
+  d["pods"] = l;
+  d["create_errors"] = ce;
+  d["delete_errors"] = de;
+  return d;
+}
 
 class PyPodRuntime {
  public:
@@ -1055,6 +1096,7 @@ class PyDpServer {
     d["slow_allocate"] = s.slow_allocate;
     d["slow_preferred"] = s.slow_preferred;
     d["patch_failures"] = s.patch_failures;
+    d["journal_failures"] = s.journal_failures;
     d["commits_gone"] = s.commits_gone;
     d["guard_by_ids"] = s.guard_by_ids;
     if (s.phased) {
@@ -1670,6 +1712,9 @@ PYBIND11_MODULE(_engine, m) {
       .def("view", &PyReflectorProbe::view)
       .def("stats", &PyReflectorProbe::stats);
 
+  m.def("open_loop_run", &open_loop_run, py::arg("api"), py::arg("run"), py::arg("pod_tmpl"), py::arg("rate"),
+        py::arg("duration_s") = 2.0, py::arg("warm_s") = 0.5, py::arg("hold_s") = 0.0, py::arg("drain_s") = 20.0,
+        py::arg("creators") = 16, py::arg("deleters") = 16, py::arg("ns") = "default");
   py::class_<PyBatchClient>(m, "BatchClient")
       .def(py::init<const py::dict&>())
       .def("run", &PyBatchClient::run, py::arg("requests"), py::arg("concurrency") = 8);
@@ -1737,6 +1782,7 @@ PYBIND11_MODULE(_engine, m) {
       .def_readwrite("dev_total", &AllocPod::dev_total)
       .def_readwrite("assigned", &AllocPod::assigned)
       .def_readwrite("complete", &AllocPod::complete)
+      .def_readwrite("terminating", &AllocPod::terminating)
       .def_readwrite("cu_count", &AllocPod::cu_count)
       .def_readwrite("cu_mask", &AllocPod::cu_mask)
       .def_readwrite("hold_idx", &AllocPod::hold_idx)
@@ -1890,6 +1936,9 @@ PYBIND11_MODULE(_engine, m) {
       .def("drop_record", &AllocState::drop_record, py::call_guard<AllocLock>())
       .def("mark_on_gpu", &AllocState::mark_on_gpu, py::call_guard<AllocLock>())
       .def("physical_used", &AllocState::physical_used, py::call_guard<AllocLock>())
+      .def("terminating_used", &AllocState::terminating_used, py::call_guard<AllocLock>())
+      .def("terminating_dev", &AllocState::terminating_dev, py::call_guard<AllocLock>())
+      .def("terminating_count", &AllocState::terminating_count, py::call_guard<AllocLock>())
       .def("off_gpu_records", &AllocState::off_gpu_records, py::call_guard<AllocLock>())
       .def("off_gpu_records_on", &AllocState::off_gpu_records_on, py::call_guard<AllocLock>())
       .def("prune_held", &AllocState::prune_held, py::arg("listed"), py::arg("asked"), py::arg("grace"),
@@ -1955,6 +2004,10 @@ PYBIND11_MODULE(_engine, m) {
         return d;
       }, py::call_guard<AllocLock>());
 
+  // ApiClient's wait before resending a request answered `status` (Retry-After `retry_after`); < 0: not resent
+  m.def("api_retry_wait", [](int status, const std::string& retry_after, int attempt, double jitter01) {
+    return ApiClient::retry_wait(ApiConfig{}, "GET", status, retry_after, attempt, jitter01);
+  });
   m.def("parse_quantity", [](const std::string& s) {
     int64_t v;
     if (!parse_quantity(s, &v)) throw py::value_error("quantities must match the regular expression");

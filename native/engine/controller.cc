@@ -141,7 +141,11 @@ void Controller::sync(const std::string& key) {
   removed_.erase(key);
   const PodView& v = it->second.v;
   std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
-  if (v.complete()) {
+  // controller.go:193-195 frees a pod at IsCompletePod, i.e. already at its deletionTimestamp.  Here a terminating
+  // pod stays charged until its object is gone (the DELETED event, above) or its phase turns terminal: kubelet
+  // stops its containers during the grace period, and kube-scheduler's own NodeInfo counts it until then too
+  // ("deleting pods still count -- keep (conservative)")
+  if (v.terminal()) {
     l_->remove_pod(v.uid);
     stats_.removes++;
     return;
@@ -163,8 +167,8 @@ void Controller::h_update(const Entry& old, const std::string& key) {
     state = l_->pod_state(cur.v.uid, &dev);
   }
   bool enqueue = false;
-  if (state != 0 && cur.v.complete()) {
-    enqueue = true;
+  if (state != 0 && (cur.v.terminal() || cur.v.deleting != old.v.deleting)) {
+    enqueue = true;  // now terminal (freed), or terminating (still charged; inspect lists it no more)
   } else if (cur.v.dev_idx >= 0 && (state == 0 || state == 2)) {
     enqueue = true;
   } else if (state == 1 && cur.v.dev_idx != dev) {
@@ -269,7 +273,7 @@ void Controller::build_cache() {
     std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
     for (auto& kv : store_) {
       const PodView& v = kv.second.v;
-      if (!kv.second.share || v.complete()) continue;
+      if (!kv.second.share || v.terminal()) continue;  // a terminating pod still holds its share (sync)
       if (v.annot_mem > 0 && !v.node.empty()) {
         if (l_->upsert_pod(v) > 0) ++n;
       }

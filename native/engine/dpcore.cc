@@ -197,6 +197,13 @@ bool DpCore::journal_map(int fd, std::string* err) {
     *err = std::string("ftruncate: ") + std::strerror(errno);
     return false;
   }
+  // blocks reserved up front: a store into a mapped page the filesystem cannot back raises SIGBUS (a full disk would
+  // kill the plugin inside an Allocate); a reservation that fails is an error here, where the caller can fall back
+  if (int fe = ::posix_fallocate(fd, 0, static_cast<off_t>(cap)); fe != 0) {
+    *err = std::string("posix_fallocate: ") + std::strerror(fe);
+    (void)!::ftruncate(fd, static_cast<off_t>(used));
+    return false;
+  }
   // not prefaulted: a rotation runs under the state lock, and populating 1 MiB there would hold an Allocate up;
   // the pages fault in as lines reach them (one 4 KiB page per ~4 Allocates)
   void* m = ::mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
@@ -229,8 +236,8 @@ void DpCore::journal_unmap(bool trim) {
   jcap_ = jlen_ = 0;
 }
 
-void DpCore::journal_append(const AllocRecord& r) {
-  if (jfd_ < 0) return;
+bool DpCore::journal_append(const AllocRecord& r) {
+  if (jfd_ < 0) return true;
   // one line per Allocate, the record's fields as the plugin's checkpoint has them (AllocRecord.to_dict)
   size_t est = 256 + r.aid.size() + r.uid.size() + r.cu_mask.size() + r.iso.size();
   for (const auto& id : r.ids) est += id.size() + 3;
@@ -254,14 +261,21 @@ void DpCore::journal_append(const AllocRecord& r) {
   if (jlen_ + line.size() > jcap_) {
     // grow by whole chunks (a syscall pair per ~1,000 Allocates): the mapping is re-made over the longer file
     const size_t cap = ((jlen_ + line.size()) / kJournalChunk + 1) * kJournalChunk;
-    void* m = ::ftruncate(jfd_, static_cast<off_t>(cap)) == 0
+    // the new chunk's blocks are reserved before it is mapped (see journal_map: no SIGBUS on a full disk)
+    void* m = (::ftruncate(jfd_, static_cast<off_t>(cap)) == 0 &&
+               ::posix_fallocate(jfd_, static_cast<off_t>(jcap_), static_cast<off_t>(cap - jcap_)) == 0)
                   ? ::mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED, jfd_, 0)
                   : MAP_FAILED;
     if (m == MAP_FAILED) {
-      // the line still goes to the file (past the mapped bytes); the next append retries the growth
+      (void)!::ftruncate(jfd_, static_cast<off_t>(std::max(jcap_, jlen_)));  // no unreserved tail left mapped later
+      // the line still goes to the file (past the mapped bytes), where a full disk fails the write, not the process;
+      // the next append retries the growth
       ssize_t n = ::pwrite(jfd_, line.data(), line.size(), static_cast<off_t>(jlen_));
-      if (n == static_cast<ssize_t>(line.size())) jlen_ += line.size();
-      return;
+      if (n == static_cast<ssize_t>(line.size())) {
+        jlen_ += line.size();
+        return true;
+      }
+      return false;
     }
     ::munmap(jmap_, jcap_);
     jmap_ = static_cast<char*>(m);
@@ -270,6 +284,7 @@ void DpCore::journal_append(const AllocRecord& r) {
   // the page cache outlives this process: once copied, the line survives a crash of the plugin like a write(2)
   std::memcpy(jmap_ + jlen_, line.data(), line.size());
   jlen_ += line.size();
+  return true;
 }
 
 bool DpCore::journal_rotate(std::string* err) {
@@ -313,10 +328,35 @@ bool DpCore::journal_rotate(std::string* err) {
     return true;
   }
   // a previous checkpoint did not land: .old still holds records it was to cover; append this generation to it
-  // (read back from the file: lines past the mapping, written when growing it failed, are in the file only)
-  int out = ::open(old.c_str(), O_WRONLY | O_APPEND | O_CLOEXEC);
-  size_t off = 0;
+  // (read back from the file: lines past the mapping, written when growing it failed, are in the file only).  .old is
+  // a renamed journal and keeps its zero padding: trimmed back to its last whole line first, or the appended
+  // generation's first line would follow a run of NULs
+  int out = ::open(old.c_str(), O_RDWR | O_CLOEXEC);
   bool ok = out >= 0;
+  if (ok) {
+    struct stat ost {};
+    ok = ::fstat(out, &ost) == 0;
+    off_t end = ok ? ost.st_size : 0;
+    char tail[4096];
+    while (ok && end > 0) {
+      const off_t from = std::max<off_t>(0, end - static_cast<off_t>(sizeof tail));
+      ssize_t n = ::pread(out, tail, static_cast<size_t>(end - from), from);
+      if (n < 0 && errno == EINTR) continue;
+      if (n <= 0) {
+        ok = false;
+        break;
+      }
+      ssize_t k = n;
+      while (k > 0 && tail[k - 1] != '\n') --k;
+      if (k > 0) {
+        end = from + k;
+        break;
+      }
+      end = from;
+    }
+    ok = ok && ::ftruncate(out, end) == 0 && ::lseek(out, 0, SEEK_END) == end;
+  }
+  size_t off = 0;
   char buf[65536];
   while (ok && off < jlen_) {
     ssize_t n = ::pread(jfd_, buf, std::min(sizeof buf, jlen_ - off), static_cast<off_t>(off));
@@ -715,7 +755,14 @@ void DpCore::record_and_answer(DpPending& p, std::string* resp, DpEvent* ev) {
                                     cm != p.cr.annotations.end() ? cm->second : p.pod.cu_mask, aid, wall_s(), p.on_gpu);
   rec.iso = p.iso;
   const double tr1 = mono_s();
-  if (p.answered) journal_append(rec);  // durable before kubelet has the answer
+  if (p.answered && !journal_append(rec)) {  // durable before kubelet has the answer
+    // the disk is full (or the journal unwritable): later Allocates answer after their commit instead, as when the
+    // journal could not be opened at all
+    stats_.journal_failures++;
+    cfg_.early_answer = false;
+    std::fprintf(stderr, "[gsx-dpcore] journal %s: write failed (%s); answering after the ASSIGNED patch from now on\n",
+                 cfg_.journal.c_str(), std::strerror(errno));
+  }
   const double tj = mono_s();
   *resp = dp::encode_allocate_response({p.cr});
   stats_.ph_record += tr1 - tr0;

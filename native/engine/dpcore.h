@@ -123,6 +123,7 @@ class DpCore {
 
   struct Stats {
     uint64_t fast_allocate = 0, fast_preferred = 0, slow_allocate = 0, slow_preferred = 0, patch_failures = 0;
+    uint64_t journal_failures = 0;  // early-answer journal lines that did not reach the file (then early answer off)
     uint64_t commits_gone = 0;  // early-answer commits whose pod was gone (404 / re-created): released at once
     uint64_t guard_by_ids = 0;  // the records said full, kubelet's IDs said there is room
     // fast-path Allocate phases, summed seconds over `phased` answers: decode, match, guard + CU claim, response
@@ -170,7 +171,7 @@ class DpCore {
   void journal_unmap(bool trim);
   Stats stats_;
   void record_and_answer(DpPending& p, std::string* resp, DpEvent* ev);
-  void journal_append(const AllocRecord& r);
+  bool journal_append(const AllocRecord& r);  // false: the line did not reach the file
 };
 
 }  // namespace gsx

@@ -80,6 +80,8 @@ bool Ledger::upsert_node(const NodeView& nv) {
     n.count = nv.count;
     n.dev_totals_override = nv.dev_totals;
     n.landing_order = nv.landing_order;
+    n.publishes = nv.publishes;
+    arm_publication_wait(n);
     // adopt pods that arrived before their node
     for (auto& kv : pods_) {
       if (kv.second.node == nv.name) n.pods.insert(kv.first);
@@ -91,6 +93,10 @@ bool Ledger::upsert_node(const NodeView& nv) {
   NodeState& n = it->second;
   n.address = nv.address;
   n.landing_order = nv.landing_order;
+  if (nv.publishes != n.publishes) {
+    n.publishes = nv.publishes;
+    arm_publication_wait(n);
+  }
   if (n.total == nv.total && n.count == nv.count && n.dev_totals_override == nv.dev_totals) return false;
   n.total = nv.total;
   n.count = nv.count;
@@ -568,8 +574,29 @@ bool Ledger::set_unaccounted(const std::string& node, const std::vector<int64_t>
   if (it == nodes_.end()) return false;
   it->second.extra = extra;
   it->second.extra_until = extra.empty() ? 0 : now_s() + ttl_s;
+  it->second.published = true;
+  it->second.pub_wait_until = 0;
   stats_.unaccounted_updates++;
   return true;
+}
+
+void Ledger::arm_publication_wait(NodeState& n) {
+  n.pub_wait_until = (n.publishes && !n.published && pub_hold_s_ > 0) ? now_s() + pub_hold_s_ : 0;
+}
+
+void Ledger::begin_epoch(double hold_s) {
+  pub_hold_s_ = hold_s > 0 ? hold_s : 0;
+  for (auto& kv : nodes_) {
+    kv.second.published = false;
+    arm_publication_wait(kv.second);
+  }
+}
+
+double Ledger::publication_wait(const std::string& node) const {
+  auto it = nodes_.find(node);
+  if (it == nodes_.end() || it->second.pub_wait_until <= 0) return 0;
+  const double left = it->second.pub_wait_until - now_s();
+  return left > 0 ? left : 0;
 }
 
 std::vector<int64_t> Ledger::node_unaccounted(const std::string& node) const {

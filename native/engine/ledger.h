@@ -112,6 +112,9 @@ struct NodeState {
   // takes no bind into room its containers already fill.  Empty: none published (or expired, extra_until)
   std::vector<int64_t> extra;
   double extra_until = 0;
+  bool publishes = false;      // NodeView::publishes
+  bool published = false;      // a publication of the node's plugin arrived in this epoch
+  double pub_wait_until = 0;   // binds to the node wait for that publication until then (0: no wait)
   bool gpushare() const { return total > 0 && count > 0; }
   int64_t used_eff(size_t i) const { return devs[i].used + (i < extra.size() ? extra[i] : 0); }
   int64_t free_of(size_t i) const { return devs[i].total - used_eff(i); }
@@ -212,6 +215,12 @@ class Ledger {
   std::vector<std::pair<int64_t, int64_t>> node_devices(const std::string& node) const;
   // the device plugin's unaccounted use per device of `node` (empty: withdraw), valid for ttl_s; false: unknown node
   bool set_unaccounted(const std::string& node, const std::vector<int64_t>& extra, double ttl_s);
+  // A new extender epoch (process start, or this replica became the leader): the unaccounted use its predecessor
+  // was told is unknown here, so binds to every node whose plugin publishes wait (at most hold_s) for that plugin's
+  // first publication of the epoch -- the plugin republishes as soon as it sees the epoch change.  hold_s 0: off.
+  void begin_epoch(double hold_s);
+  // seconds a bind to `node` still waits for its plugin's publication (0: none)
+  double publication_wait(const std::string& node) const;
   std::vector<int64_t> node_unaccounted(const std::string& node) const;
   std::vector<std::string> node_names() const;
   Stats stats() const { return stats_; }
@@ -254,6 +263,8 @@ class Ledger {
   std::map<std::string, NodeState> nodes_;  // ordered: deterministic inspect
   std::unordered_map<std::string, PodRec> pods_;
   std::vector<AnnotationRepair> repairs_;
+  double pub_hold_s_ = 0;  // begin_epoch(): nodes first seen later in the epoch wait that long too
+  void arm_publication_wait(NodeState& n);
   void queue_repair(PodRec& r);
   Stats stats_;
   mutable introspect::ProfiledMutex mu_;  // every caller locks it; contention is exported to /debug/pprof/mutex

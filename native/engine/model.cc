@@ -153,6 +153,7 @@ bool parse_node(const json::Doc& d, uint32_t node, const Profile& p, NodeView* o
       if (ok) out->dev_totals = std::move(vals);
     }
     out->landing_order = str_at(d, d.find(static_cast<uint32_t>(an), kAllocateOrderAnnotation)) == "landing";
+    out->publishes = str_at(d, d.find(static_cast<uint32_t>(an), kPhysicalPublicationAnnotation)) == "true";
   }
   int64_t addrs = d.path(node, {"status", "addresses"});
   if (addrs >= 0 && d.at(static_cast<uint32_t>(addrs)).type == json::T::Array) {

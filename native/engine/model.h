@@ -66,9 +66,14 @@ struct NodeView {
   // the node's device plugin matches Allocates in landing order (annotation gpushare.amd.com/allocate-order
   // = "landing", published by deviceplugin/plugin.py): binds need no ASSUME_TIME order there (ledger.h)
   bool landing_order = false;
+  // the node's device plugin publishes its unaccounted GPU use to the extender (POST .../physical; annotation
+  // gpushare.amd.com/physical-publication = "true", deviceplugin/plugin.py publish_node): after an extender (re)start
+  // or a leader change, binds to the node wait for its first publication (ledger.h publication_wait)
+  bool publishes = false;
 };
 
 inline constexpr const char* kAllocateOrderAnnotation = "gpushare.amd.com/allocate-order";
+inline constexpr const char* kPhysicalPublicationAnnotation = "gpushare.amd.com/physical-publication";
 
 // Extract a PodView from the pod object at tape index `pod`.
 bool parse_pod(const json::Doc& d, uint32_t pod, const Profile& p, PodView* out);

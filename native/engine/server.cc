@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <random>
 
 #include "json.h"
 
@@ -152,6 +153,46 @@ struct NativeServer::Loop {
 
 NativeServer::NativeServer(Ledger* ledger, ServerConfig cfg) : l_(ledger), cfg_(std::move(cfg)) {
   update_mode_.store(cfg_.update_mode);
+  std::random_device rd;
+  char b[24];
+  std::snprintf(b, sizeof(b), "%08x%08x", rd(), rd());
+  boot_id_ = b;
+}
+
+void NativeServer::set_binds_enabled(bool on) {
+  const bool was = binds_enabled_.exchange(on);
+  if (on && !was && port_ > 0) new_epoch();  // became the leader (before start(): start() begins the first epoch)
+}
+
+std::string NativeServer::epoch() const { return boot_id_ + "." + std::to_string(epoch_gen_.load()); }
+
+void NativeServer::new_epoch() {
+  epoch_gen_.fetch_add(1);
+  {
+    std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
+    l_->begin_epoch(cfg_.publication_hold_s);
+  }
+  std::lock_guard<std::mutex> p(pub_mu_);
+  pub_cv_.notify_all();
+}
+
+void NativeServer::wait_publication(const std::string& node) {
+  double t0 = 0;
+  while (!stop_.load()) {
+    double left;
+    {
+      std::lock_guard<introspect::ProfiledMutex> g(l_->mu());
+      left = l_->publication_wait(node);
+    }
+    if (left <= 0) break;
+    if (t0 == 0) {
+      t0 = mono();
+      stats_.publication_waits.fetch_add(1, std::memory_order_relaxed);
+    }
+    std::unique_lock<std::mutex> p(pub_mu_);
+    pub_cv_.wait_for(p, std::chrono::duration<double>(std::min(left, 0.05)));
+  }
+  if (t0 > 0) publication_wait_ns_.fetch_add(static_cast<uint64_t>((mono() - t0) * 1e9), std::memory_order_relaxed);
 }
 
 NativeServer::~NativeServer() { stop(); }
@@ -217,6 +258,7 @@ int NativeServer::start(std::string* err) {
     epoll_ctl(lp->ep, EPOLL_CTL_ADD, lp->efd, &ev);
     loops_.push_back(std::move(lp));
   }
+  if (binds_enabled_.load()) new_epoch();  // the first epoch: what a predecessor was told is unknown here
   port_ = port;
   int li = 0;
   for (auto& lp : loops_) {
@@ -511,6 +553,11 @@ void NativeServer::dispatch(Loop* lp, Conn* c, http::Message& req) {
     respond(lp, c, http::response(200, "application/json", out, ka), ka);
     return;
   }
+  if (req.method == "GET" && path == pre + "/epoch") {
+    std::string out = "{\"epoch\":\"" + epoch() + "\",\"leader\":" + (binds_enabled_.load() ? "true" : "false") + "}";
+    respond(lp, c, http::response(200, "application/json", out, ka), ka);
+    return;
+  }
   if (req.method == "GET" && path == "/version") {
     respond(lp, c, http::response(200, "text/plain; charset=utf-8", kVersion, ka), ka);
     return;
@@ -598,6 +645,9 @@ std::string NativeServer::do_bind(const http::Message& req) {
   }
   std::string name, ns, uid, node;
   if (!binding_args(d, &name, &ns, &uid, &node, &perr)) return bind_error_response(perr);
+  // a new epoch does not know what the node's containers hold beyond the annotations: its plugin republishes
+  // as soon as it sees the epoch change, and the placement below must count that
+  wait_publication(node);
   Ledger::PendingPod pp;
   int64_t dev = -1, dev_total = -1, assume_ns = 0;
   uint64_t seq = 0;
@@ -676,14 +726,28 @@ std::string NativeServer::do_bind(const http::Message& req) {
     record_failure(BindFailure{ns, name, uid, node, m});
     return bind_error_response(m);
   };
+  // a 5xx the apiserver sent without Retry-After (ApiClient already waited out 429s and Retry-After 5xx): sent
+  // again after a capped exponential backoff with jitter, the reservation kept meanwhile
+  auto backoff = [this](int attempt) {
+    thread_local uint64_t r = 0x2545f4914f6cdd1dull ^ reinterpret_cast<uintptr_t>(&r);
+    r ^= r << 13;
+    r ^= r >> 7;
+    r ^= r << 17;
+    const double b = std::min(0.2, 0.005 * static_cast<double>(1 << std::min(attempt, 6)));
+    stats_.backoffs.fetch_add(1, std::memory_order_relaxed);
+    std::this_thread::sleep_for(std::chrono::duration<double>(b * (0.5 + 0.5 * static_cast<double>(r >> 11) *
+                                                                            (1.0 / 9007199254740992.0))));
+  };
+  constexpr int kServerErrorAttempts = 5;
   const bool update_mode = update_mode_.load();
   if (update_mode) {
     // the reference's first call: write the annotations, guarded by the resourceVersion the scheduler saw;
     // on the optimistic-lock conflict retry once on the latest version (nodeinfo.go:150-168).  Not ordered:
     // a pod without spec.nodeName is no device-plugin candidate yet
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    int conflicts = 0;
+    for (int attempt = 0; attempt < kServerErrorAttempts; ++attempt) {
       std::string patch = "{\"metadata\":{";
-      if (attempt == 0 && !pp.rv.empty()) {
+      if (attempt == 0 && conflicts == 0 && !pp.rv.empty()) {
         patch.append("\"resourceVersion\":");
         json::append_quoted(&patch, pp.rv);
         patch.push_back(',');
@@ -694,8 +758,13 @@ std::string NativeServer::do_bind(const http::Message& req) {
       if (!call("PATCH", pod_path, patch, "application/merge-patch+json", &status, &body)) return fail(msg);
       if (status == 200 || status == 201) break;
       msg = status_message(body, status);
-      if (attempt == 0 && status == 409) {  // a conflict is detected by status, not by message
+      if (conflicts == 0 && status == 409) {  // a conflict is detected by status, not by message
+        ++conflicts;
         stats_.conflicts_retried.fetch_add(1, std::memory_order_relaxed);
+        continue;
+      }
+      if (status >= 500 && attempt + 1 < kServerErrorAttempts) {  // the same annotations again: idempotent
+        backoff(attempt);
         continue;
       }
       return fail(msg);
@@ -724,7 +793,7 @@ std::string NativeServer::do_bind(const http::Message& req) {
     stats_.bind_order_waits.fetch_add(1, std::memory_order_relaxed);
     l_->bind_wait(seq, &stop_);
   }
-  for (int attempt = 0; attempt < 3; ++attempt) {
+  for (int attempt = 0, conflicts = 0; attempt < kServerErrorAttempts; ++attempt) {
     int status = 0;
     std::string body;
     if (!call("POST", path, b, "application/json", &status, &body)) break;
@@ -741,11 +810,15 @@ std::string NativeServer::do_bind(const http::Message& req) {
       if (!lookup_pod(ns, name, uid, true, &live, &err)) msg = err;
       break;
     }
-    if (status == 409 && msg.find("already assigned") == std::string::npos && attempt < 2) {
+    if (status == 409 && msg.find("already assigned") == std::string::npos && conflicts < 2) {
+      ++conflicts;
       stats_.conflicts_retried.fetch_add(1, std::memory_order_relaxed);
       continue;
     }
-    if (status >= 500 && attempt < 2) continue;
+    if (status >= 500 && attempt + 1 < kServerErrorAttempts) {
+      backoff(attempt);
+      continue;
+    }
     break;
   }
   {
@@ -945,7 +1018,7 @@ std::string NativeServer::do_move(const http::Message& req, const std::string& t
     if (!sent) return answer(502, error_body("apiserver: " + err));
     return answer(status == 409 ? 409 : (status >= 500 ? 502 : status), error_body(status_message(body, status)));
   }
-  std::string out = "{\"Error\":\"\",\"to\":" + std::to_string(m.to) + ",\"pod\":";
+  std::string out = "{\"Error\":\"\",\"epoch\":\"" + epoch() + "\",\"to\":" + std::to_string(m.to) + ",\"pod\":";
   out.append(body).push_back('}');
   return answer(200, out);
 }
@@ -1035,6 +1108,11 @@ bool NativeServer::plugin_authorized(const http::Message& req, std::string* resp
 //   {"node": "n", "unaccounted": [u0, u1, ...] | null, "ttl": s}  ->  200 {"Error":""} | 400 | 404
 std::string NativeServer::do_physical(const http::Message& req, const std::string& token_node) {
   auto answer = [](int status, const std::string& body) { return http::response(status, "application/json", body, true); };
+  if (!binds_enabled_.load()) {
+    // a standby keeps no publication the leader would need: the plugin must not count this one as delivered
+    stats_.physical_refused.fetch_add(1, std::memory_order_relaxed);
+    return answer(503, error_body("this extender replica is not the leader"));
+  }
   json::Doc d;
   std::string perr;
   if (!d.parse(req.body, &perr) || d.at(0).type != json::T::Object) return answer(400, error_body("bad request: " + perr));
@@ -1069,7 +1147,11 @@ std::string NativeServer::do_physical(const http::Message& req, const std::strin
     ok = l_->set_unaccounted(node, used, ttl);
   }
   if (!ok) return answer(404, error_body("node " + node + " is not in the extender's ledger"));
-  return answer(200, "{\"Error\":\"\"}");
+  {
+    std::lock_guard<std::mutex> p(pub_mu_);
+    pub_cv_.notify_all();  // binds waiting for this node's first publication of the epoch
+  }
+  return answer(200, "{\"Error\":\"\",\"epoch\":\"" + epoch() + "\"}");
 }
 
 }  // namespace gsx

@@ -64,6 +64,9 @@ struct ServerConfig {
   std::string plugin_auth = "none";
   std::vector<std::string> plugin_users;
   double plugin_auth_ttl = 60.0;
+  // after a (re)start or a leader change, binds to a node whose device plugin publishes its unaccounted GPU use wait
+  // at most this long for the plugin's first publication of the new epoch (Ledger::begin_epoch); 0: no wait
+  double publication_hold_s = 5.0;
 };
 
 struct BindFailure {
@@ -86,7 +89,7 @@ struct ServerStats {
   std::atomic<uint64_t> requests{0}, filters{0}, binds{0}, bind_ok{0}, bind_fail{0}, proxied{0}, bad_requests{0},
       inspects{0}, connections{0}, api_calls{0}, conflicts_retried{0}, bind_order_waits{0}, moves{0}, moves_failed{0},
       unfiltered_binds{0}, live_gets{0}, qps_waits{0}, physical_posts{0}, plugin_auth_denied{0},
-      token_reviews{0};
+      token_reviews{0}, backoffs{0}, publication_waits{0}, physical_refused{0};
   LatencyHist filter_lat, bind_lat, api_lat;
 };
 
@@ -99,9 +102,16 @@ class NativeServer {
   void stop();
   int port() const { return port_; }
   const ServerStats& stats() const { return stats_; }
+  // apiserver responses sent again after a 429 / Retry-After (ApiClient), and the seconds waited for them
+  uint64_t api_throttled() const { return api_ ? api_->throttled() : 0; }
+  double api_throttle_wait_s() const { return api_ ? api_->throttle_wait_s() : 0.0; }
   std::vector<BindFailure> drain_failures();
-  // HA standby: a replica that does not hold the leader Lease refuses binds.
-  void set_binds_enabled(bool on) { binds_enabled_.store(on); }
+  // HA standby: a replica that does not hold the leader Lease refuses binds (and the device plugin's /move and
+  // /physical).  Becoming the leader starts a new epoch (new_epoch).
+  void set_binds_enabled(bool on);
+  // this extender's epoch: a boot id and the number of times it became the leader ("<boot>.<n>").  Answered on
+  // GET .../epoch and with every /physical and /move; a device plugin that sees it change republishes at once
+  std::string epoch() const;
   // switch to the reference's annotate-then-bind calls at run time (the apiserver dropped Binding annotations)
   void set_update_mode(bool on) { update_mode_.store(on); }
   bool update_mode() const { return update_mode_.load(); }
@@ -150,6 +160,14 @@ class NativeServer {
   bool plugin_authorized(const http::Message& req, std::string* resp, std::string* token_node);
   std::string bind_error_response(const std::string& msg) const;
   void record_failure(BindFailure f);
+  void new_epoch();
+  // wait (bounded) until `node`'s device plugin has published in this epoch; false: stopping
+  void wait_publication(const std::string& node);
+  std::string boot_id_;
+  std::atomic<uint64_t> epoch_gen_{0};
+  std::mutex pub_mu_;
+  std::condition_variable pub_cv_;
+  std::atomic<uint64_t> publication_wait_ns_{0};
 
   Ledger* l_;
   ServerConfig cfg_;

@@ -5,7 +5,11 @@
 //                that answers "are all these pods bound / Running / gone?"
 //                with a blocking wait woken by watch events;
 //   BatchClient  issues a list of apiserver requests concurrently over a
-//                keep-alive connection pool (the wave's pod creates).
+//                keep-alive connection pool (the wave's pod creates);
+//   OpenLoop     constant-rate pod arrivals with every pod's stages timed
+//                (arrival -> bound -> Running -> deleted -> gone), each pod
+//                deleted once it runs: the sustained throughput of the whole
+//                stack with many pods in flight (bench.py --open-loop).
 #pragma once
 
 #include <atomic>
@@ -44,6 +48,36 @@ class PodTracker {
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::unordered_map<std::string, St> pods_;
+};
+
+struct OpenLoopConfig {
+  std::string ns = "default";
+  std::string label_key = "gsx-ol";  // the run's pods carry label_key=<run> (the watch selects them)
+  std::string run;
+  // the pod object with __NAME__ where its name goes (its labels must include label_key: run)
+  std::string pod_tmpl;
+  double rate = 1000;        // arrivals per second
+  double duration_s = 2.0;   // arrivals for this long
+  double warm_s = 0.5;       // the first warm_s of arrivals are not counted
+  double hold_s = 0.0;       // a pod runs this long before it is deleted
+  double drain_s = 20.0;     // after the last arrival: wait this long for the pods to run and go
+  int creators = 16, deleters = 16;
+};
+
+struct OpenLoopPod {
+  double arrival = 0, created = 0, bound = 0, running = 0, deleted = 0, gone = 0;
+  bool failed = false;
+};
+
+class OpenLoop {
+ public:
+  explicit OpenLoop(const ApiConfig& cfg) : cfg_(cfg) {}
+  // runs to the end (all pods gone, or drain_s passed); false + *err only when the watch never synced
+  bool run(const OpenLoopConfig& c, std::vector<OpenLoopPod>* pods, std::string* err, int* create_errors,
+           int* delete_errors);
+
+ private:
+  ApiConfig cfg_;
 };
 
 class BatchClient {

@@ -12,10 +12,14 @@
 //     Binding's annotations into the pod (kube-apiserver's
 //     setPodHostAndAnnotations), plus a PodScheduled condition;
 //   * JSON merge patch (strategic merge patch treated as merge patch),
-//     graceful pod deletion, DeleteCollection with selectors;
+//     DeleteCollection with selectors, DELETE preconditions.uid;
+//   * graceful pod deletion as kube-apiserver does it: a bound, non-terminal
+//     pod only gets deletionTimestamp; its kubelet removes the object with a
+//     grace-0 delete once the containers stopped (no timer here);
 //   * fault injection (POST /fake/faults): conflict_rate, error_rate,
-//     latency_ms, drop_watch_after, expire_watches, hold_watches,
-//     drop_watches_now; GET /fake/stats.
+//     throttle_rate + retry_after (429 Too Many Requests), latency_ms,
+//     drop_watch_after, expire_watches, hold_watches, drop_watches_now;
+//     GET /fake/stats.
 //
 // Concurrency (a real kube-apiserver serves requests on many cores in front of
 // one etcd revision counter): N epoll loops, each with its own SO_REUSEPORT
@@ -395,17 +399,22 @@ thread_local Loop* tl_deferred_wake = nullptr;
 
 struct Faults {
   double conflict_rate = 0, error_rate = 0, latency_ms = 0;
+  // API Priority and Fairness: this share of non-watch /api/v1 requests answers 429 with Retry-After: retry_after
+  // seconds (fractional in tests; kube-apiserver sends whole seconds)
+  double throttle_rate = 0, retry_after = 1;
   int64_t drop_watch_after = 0, expire_watches = 0;
   bool hold_watches = false;
   // an apiserver (or admission webhook) that does not copy Binding.metadata.annotations onto the pod
   bool drop_binding_annotations = false;
   std::string json() const {
-    char b[384];
+    char b[448];
     std::snprintf(b, sizeof(b),
                   "{\"conflict_rate\":%g,\"error_rate\":%g,\"latency_ms\":%g,\"drop_watch_after\":%lld,"
-                  "\"expire_watches\":%lld,\"hold_watches\":%s,\"drop_binding_annotations\":%s}",
+                  "\"expire_watches\":%lld,\"hold_watches\":%s,\"drop_binding_annotations\":%s,"
+                  "\"throttle_rate\":%g,\"retry_after\":%g}",
                   conflict_rate, error_rate, latency_ms, (long long)drop_watch_after, (long long)expire_watches,
-                  hold_watches ? "true" : "false", drop_binding_annotations ? "true" : "false");
+                  hold_watches ? "true" : "false", drop_binding_annotations ? "true" : "false", throttle_rate,
+                  retry_after);
     return b;
   }
 };
@@ -414,6 +423,7 @@ struct Reply {
   int status = 200;
   std::string body;
   const char* ct = "application/json";
+  std::string headers;  // extra header lines ("Name: value\r\n")
 };
 
 class Server;
@@ -683,11 +693,21 @@ class Server {
       double t0 = now_s();
       RouteTime& rt = route_time_[cls];
       rt.n++;
-      try {
-        reply = route(L, c, req, body, &rep);  // false: became a watch stream (or is held)
-      } catch (const HttpError& e) {
-        rep.status = e.code;
-        rep.body = e.body;
+      if (!is_watch && faults_.throttle_rate > 0 && req.path().substr(0, 8) == "/api/v1/" &&
+          std::uniform_real_distribution<double>(0, 1)(rng()) < faults_.throttle_rate) {
+        counts_["injected_throttle"]++;
+        char ra[64];
+        std::snprintf(ra, sizeof(ra), "Retry-After: %g\r\n", faults_.retry_after);
+        rep.status = 429;
+        rep.headers = ra;
+        rep.body = status_body(429, "TooManyRequests", "Too many requests, please try again later.");
+      } else {
+        try {
+          reply = route(L, c, req, body, &rep);  // false: became a watch stream (or is held)
+        } catch (const HttpError& e) {
+          rep.status = e.code;
+          rep.body = e.body;
+        }
       }
       rt.s += now_s() - t0;
     }
@@ -760,7 +780,7 @@ class Server {
   }
 
   void respond(Loop* L, Conn* c, const Reply& r, bool keep_alive) {
-    c->wbuf.append(http::response(r.status, r.ct, r.body, keep_alive));
+    c->wbuf.append(http::response(r.status, r.ct, r.body, keep_alive, r.headers));
     if (!keep_alive) c->want_close = true;
     flush_conn(L, c);
   }
@@ -811,10 +831,6 @@ class Server {
       if (w->deadline > 0) next = std::min(next, w->deadline);
     }
     if (!L->held.empty()) next = std::min(next, now + 0.005);
-    if (L->idx == 0 && ngraces_.load() > 0) {
-      StateLock g(smu_, lstats_);
-      for (auto& gr : graces_) next = std::min(next, gr.due);
-    }
     double ms = (next - now) * 1000.0;
     return ms <= 0 ? 0 : static_cast<int>(ms) + 1;
   }
@@ -838,29 +854,6 @@ class Server {
         c->busy = false;
         handle(L, c, d.req, false);
         if (L->conns.count(d.conn)) process(L, c);
-      }
-    }
-    if (L->idx == 0 && ngraces_.load() > 0) {
-      StateLock g(smu_, lstats_);
-      if (!graces_.empty()) {
-        std::vector<Grace> due;
-        for (auto it = graces_.begin(); it != graces_.end();) {
-          if (it->due <= now) {
-            due.push_back(*it);
-            it = graces_.erase(it);
-          } else {
-            ++it;
-          }
-        }
-        ngraces_.store(static_cast<int>(graces_.size()));
-        for (auto& gr : due) {
-          auto& m = store_[gr.kind];
-          auto it = m.find({gr.ns, gr.name});
-          if (it != m.end()) {
-            const jd::Value* md = it->second->v().get("metadata");
-            if (md && md->str_or("uid") == gr.uid) do_delete(gr.kind, gr.ns, gr.name, -1);
-          }
-        }
       }
     }
     if (!L->mine.empty()) {
@@ -1290,11 +1283,29 @@ class Server {
     emit("pods", "MODIFIED", o);
   }
 
-  ObjP do_delete(const std::string& kind, const std::string& ns, const std::string& name, double grace) {
+  // DELETE as kube-apiserver answers it.  A bound pod that is not terminal is deleted gracefully: it gets
+  // deletionTimestamp and stays until a delete with grace 0 -- its kubelet's, once the containers stopped (the
+  // kubelet stand-ins, gsxtools/agent.py and native/nodeagent, do that).  grace < 0 (none given) takes the pod's
+  // spec.terminationGracePeriodSeconds, absent: 0 (the pods the harness builds carry none).  `uid`: the
+  // DeleteOptions' preconditions.uid (409 on mismatch).
+  ObjP do_delete(const std::string& kind, const std::string& ns, const std::string& name, double grace,
+                 const std::string& uid = std::string()) {
     ObjP cur = get_obj(kind, ns, name);
     Key key{kind == "nodes" ? std::string() : ns, name};
+    const jd::Value& cmd0 = *cur->v().get("metadata");
+    if (!uid.empty() && uid != cmd0.str_or("uid")) {
+      throw HttpError{409, status_body(409, "Conflict", "Precondition failed: UID in precondition: " + uid +
+                                                            ", UID in object meta: " + cmd0.str_or("uid"))};
+    }
     const jd::Value* cs = cur->v().get("spec");
-    if (kind == "pods" && grace > 0 && cs && !cs->str_or("nodeName").empty()) {
+    if (kind == "pods" && grace < 0 && cs) {
+      const jd::Value* tg = cs->get("terminationGracePeriodSeconds");
+      grace = (tg && tg->k == jd::Value::Num) ? std::atof(tg->s.c_str()) : 0;
+    }
+    const jd::Value* st = cur->v().get("status");
+    std::string phase = st ? st->str_or("phase") : std::string();
+    if (kind == "pods" && grace > 0 && cs && !cs->str_or("nodeName").empty() && phase != "Succeeded" &&
+        phase != "Failed") {
       const jd::Value& cmd = *cur->v().get("metadata");
       const jd::Value* dt = cmd.get("deletionTimestamp");
       if (dt && !dt->is_null()) return cur;
@@ -1306,9 +1317,6 @@ class Server {
       ObjP o = make_obj(std::move(nv));
       store_[kind][key] = o;
       emit(kind, "MODIFIED", o);
-      graces_.push_back(Grace{now_s() + grace, kind, ns, name, cmd.str_or("uid")});
-      ngraces_.store(static_cast<int>(graces_.size()));
-      if (tl_loop != loops_[0].get()) wake(loops_[0].get());  // loop 0 runs the grace timers
       return o;
     }
     store_[kind].erase(key);
@@ -1318,18 +1326,23 @@ class Server {
   }
 
   // ---------------------------------------------------------------- routing
-  static double grace_of(const http::Message& req, const std::map<std::string, std::string>& q) {
-    auto it = q.find("gracePeriodSeconds");
-    if (it != q.end()) return std::atof(it->second.c_str());
+  // DeleteOptions: gracePeriodSeconds (query or body; -1 none given) and preconditions.uid (body)
+  static double grace_of(const http::Message& req, const std::map<std::string, std::string>& q,
+                         std::string* uid = nullptr) {
+    double grace = -1;
     if (!req.body.empty()) {
       jd::Value v;
       std::string err;
       if (jd::parse(req.body, &v, &err)) {
         const jd::Value* g = v.get("gracePeriodSeconds");
-        if (g && g->k == jd::Value::Num) return std::atof(g->s.c_str());
+        if (g && g->k == jd::Value::Num) grace = std::atof(g->s.c_str());
+        const jd::Value* pc = v.get("preconditions");
+        if (uid && pc && pc->is_obj()) *uid = pc->str_or("uid");
       }
     }
-    return -1;
+    auto it = q.find("gracePeriodSeconds");
+    if (it != q.end()) grace = std::atof(it->second.c_str());
+    return grace;
   }
 
   // LIST, optionally paginated like kube-apiserver: `limit` caps the items of one response and
@@ -1414,6 +1427,8 @@ class Server {
         num("conflict_rate", &faults_.conflict_rate);
         num("error_rate", &faults_.error_rate);
         num("latency_ms", &faults_.latency_ms);
+        num("throttle_rate", &faults_.throttle_rate);
+        num("retry_after", &faults_.retry_after);
         inum("drop_watch_after", &faults_.drop_watch_after);
         inum("expire_watches", &faults_.expire_watches);
         const jd::Value* h = b.get("hold_watches");
@@ -1632,16 +1647,13 @@ class Server {
       return true;
     }
     if (m == "DELETE" && sub.empty()) {
-      rep->body = do_delete(kind, ns, name, grace_of(req, q))->json;
+      std::string uid;
+      double grace = grace_of(req, q, &uid);
+      rep->body = do_delete(kind, ns, name, grace, uid)->json;
       return true;
     }
     throw HttpError{405, status_body(405, "MethodNotAllowed", "method not allowed")};
   }
-
-  struct Grace {
-    double due;
-    std::string kind, ns, name, uid;
-  };
 
   struct RouteTime {
     uint64_t n = 0;
@@ -1655,8 +1667,7 @@ class Server {
   LockStats lstats_;
   const bool flush_per_request_;  // --watch-flush request
   const bool watch_loop_;         // --watch-loop: loop 0 owns every watch stream
-  std::atomic<int> ngraces_{0};  // graces_.size(), readable without the mutex
-  std::mutex smu_;  // the state below: store, revision, history, watchers, faults, counters, graces
+  std::mutex smu_;  // the state below: store, revision, history, watchers, faults, counters
   std::atomic<uint64_t> next_id_{0};
   std::vector<std::shared_ptr<Watcher>> watchers_;
   std::map<std::string, std::map<Key, ObjP>> store_;
@@ -1665,7 +1676,6 @@ class Server {
   Faults faults_;
   std::map<std::string, std::pair<std::string, std::string>> tokens_;  // TokenReview: token -> (user, node)
   std::map<std::string, uint64_t> counts_;
-  std::vector<Grace> graces_;
 };
 
 volatile sig_atomic_t g_stop = 0;

@@ -37,8 +37,10 @@ static hsa_queue_t g_queue;
 
 static hsa_queue_t g_more[16];
 static int g_nmore = 0;
+static bool g_fail_create = false;  // the runtime refuses the next queue creations
 static hsa_status_t fake_queue_create(hsa_agent_t, uint32_t, hsa_queue_type32_t, void (*)(hsa_status_t, hsa_queue_t*, void*),
                                       void*, uint32_t, uint32_t, hsa_queue_t** q) {
+  if (g_fail_create) return HSA_STATUS_ERROR_OUT_OF_RESOURCES;
   *q = g_nmore == 0 ? &g_queue : &g_more[g_nmore - 1];
   if (g_nmore < 16) g_nmore++;
   g_last_mask.clear();
@@ -354,6 +356,27 @@ int main(int argc, char** argv) {
   CHECK(core.hsa_executable_freeze_fn(hsa_executable_t{4}, nullptr) == HSA_STATUS_SUCCESS);  // one queue: fits
   scratch(sc);
   CHECK(sc[0] == 20736 * slots);
+  // a queue is counted and its share charged in one step before the runtime creates it; one the runtime
+  // fails gives both back (the count and the charge of a second queue that was never made)
+  g_fail_create = true;
+  hsa_queue_t* nq = nullptr;
+  CHECK(core.hsa_queue_create_fn(hsa_agent_t{GPU_AGENT}, 1024, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0, &nq) ==
+        HSA_STATUS_ERROR_OUT_OF_RESOURCES);
+  g_fail_create = false;
+  squeues(sq);
+  scratch(sc);
+  CHECK(sq[1] == 1 && sc[0] == 20736 * slots);
+  stats(sv);
+  CHECK(sv[3] == 20736 * slots);
+  CHECK(core.hsa_queue_create_fn(hsa_agent_t{GPU_AGENT}, 1024, HSA_QUEUE_TYPE_MULTI, nullptr, nullptr, 0, 0, &nq) ==
+        HSA_STATUS_SUCCESS);
+  squeues(sq);
+  scratch(sc);
+  CHECK(sq[1] == 2 && sc[0] == 2 * 20736 * slots);
+  CHECK(core.hsa_queue_destroy_fn(nq) == HSA_STATUS_SUCCESS);
+  squeues(sq);
+  scratch(sc);
+  CHECK(sq[1] == 1 && sc[0] == 20736 * slots);
   if (g_fail == 0) std::printf("isolate_test: OK\n");
   return g_fail ? 1 : 0;
 }

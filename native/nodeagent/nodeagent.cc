@@ -1,5 +1,5 @@
 // gsx-nodeagent: kubelet + device-plugin + container-runtime stand-in for one
-// node, in C++ (the compiled counterpart of deviceplugin/agent.py).
+// node, in C++ (the compiled counterpart of gsxtools/agent.py).
 //
 // Where there is no kubelet (bench.py on the GPU box, simulators), this drives
 // the device plugin's Allocate logic for every pod bound to the node and
@@ -14,6 +14,9 @@
 //   the GPU's HBM arena is stamped by a HIP kernel and every resident slice is
 //   verified ──► PATCH status Running.
 //   completed / deleted pod ──► DELETE <runtime>/v1/pods/<uid>, CUs released.
+//   terminating pod (deletionTimestamp, graceful delete) ──► its containers stop (--stop-delay seconds, at most
+//   its grace period) ──► DELETE <runtime>/v1/pods/<uid> ──► PATCH status Succeeded ──► DELETE the pod with
+//   gracePeriodSeconds 0 and a UID precondition: kubelet, not the apiserver, ends a graceful deletion.
 //
 // Devices and runtime endpoints come from the node's annotations
 // (gpushare.amd.com/devices, gpushare.amd.com/runtime-endpoints), written by
@@ -143,6 +146,8 @@ class Agent {
   void set_serial_admission(bool on) { serial_admission_ = on; }
 
   void set_plugin_socket(const std::string& s) { plugin_sock_ = s; }
+  // how long a container takes to stop after SIGTERM (graceful deletion), capped by the pod's grace period
+  void set_stop_delay(double s) { stop_delay_ = std::max(0.0, s); }
   void set_batch_window(double s) { batch_window_ = s; }
   void set_plugin_spawn(const std::string& python, const std::string& apiserver, const std::string& profile,
                         const std::string& unit) {
@@ -302,7 +307,8 @@ class Agent {
                     "\"plugin_calls_mean_ms\":{\"n\":%llu,\"slot_wait\":%.4f,\"get_preferred\":%.4f,\"allocate\":%.4f,"
                     "\"encode_preferred\":%.4f,\"gap\":%.4f,\"n_gap\":%llu,\"gap_loop\":%.4f,\"gap_list\":%.4f,"
                     "\"gap_handoff\":%.4f,\"relock\":%.4f,\"gap_kept\":%.4f,\"n_gap_kept\":%llu},"
-                    "\"mismatch\":%llu,\"podresources_calls\":%llu,\"plugin_debug\":\"%s\",\"native\":true}",
+                    "\"mismatch\":%llu,\"podresources_calls\":%llu,\"plugin_debug\":\"%s\",\"finalized\":%llu,"
+                    "\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
                     (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
                     max_queue_ * 1e3, max_patch_ * 1e3, max_runtime_ * 1e3, max_status_ * 1e3, sum_queue_ / n * 1e3,
@@ -319,7 +325,8 @@ class Agent {
                     sum_dp_relock_ / std::max<double>(1.0, dp_calls_) * 1e3,
                     sum_gap_kept_ / std::max<double>(1.0, n_gap_kept_) * 1e3, (unsigned long long)n_gap_kept_,
                     (unsigned long long)mismatch_,
-                    (unsigned long long)pr_calls_.load(), plugin_debug_url().c_str());
+                    (unsigned long long)pr_calls_.load(), plugin_debug_url().c_str(),
+                    (unsigned long long)finals_done_);
       rep.body = b;
       return rep;
     }
@@ -340,6 +347,12 @@ class Agent {
   }
 
  private:
+  struct Final {
+    double due;
+    std::string uid, ns, name;
+    bool ran;  // a container of it was running (or starting) when the deletion was seen
+  };
+
   bool parse_devices(const std::string& inv, const std::string& eps) {
     json::Doc di, de;
     std::string e;
@@ -397,6 +410,17 @@ class Agent {
     const std::string uid = ap.uid;
     if (live) live->insert(uid);
     keys_[key] = uid;
+    if (ap.terminating && (ap.dev < 0 || state_->has_device(ap.dev))) {
+      // graceful deletion: kubelet stops the containers, then removes the object itself (finalize_locked)
+      if (finals_set_.insert(uid).second) {
+        const bool runs = running_.count(uid) != 0 || state_->inflight(uid);
+        double delay = runs ? std::min(stop_delay_, ap.grace_s >= 0 ? ap.grace_s : stop_delay_) : 0.0;
+        finals_.push_back(Final{now_s() + delay, uid, ap.ns, ap.name, runs});
+        ++added_;
+      }
+      state_->release(uid);  // CUs: no new container of it starts
+      return key;
+    }
     if (ap.complete) {
       stop_pod_locked(uid);
       state_->release(uid);  // CUs too, also for pods this agent did not start (e.g. before a restart)
@@ -425,6 +449,7 @@ class Agent {
     if (it == keys_.end()) return;
     std::string uid = it->second;
     keys_.erase(it);
+    finals_set_.erase(uid);
     stop_pod_locked(uid);
     state_->tombstone(uid);  // a late copy of it (a PATCH response) never re-queues it
     if (!state_->inflight(uid)) state_->release(uid);  // the admitting worker owns it until its patch resolves
@@ -511,7 +536,15 @@ class Agent {
         start(lk);
         continue;
       }
+      auto fin = std::find_if(finals_.begin(), finals_.end(), [now](const Final& f) { return f.due <= now; });
+      if (fin != finals_.end()) {
+        Final f = *fin;
+        finals_.erase(fin);
+        finalize_locked(f, lk);
+        continue;
+      }
       double wait = 0.05;
+      for (auto& f : finals_) wait = std::min(wait, std::max(0.0, f.due - now));
       for (auto& dl : delayed_) wait = std::min(wait, std::max(0.0, dl.first - now));
       if (!batch_.empty()) wait = std::min(wait, std::max(0.0, batch_deadline_ - now));
       cv_.wait_for(lk, std::chrono::duration<double>(wait));
@@ -1089,10 +1122,44 @@ class Agent {
       int status = 0;
       std::string resp, err;
       bool ok = api_.request("PATCH", path + "/status", body, "application/merge-patch+json", &status, &resp, &err);
-      if (ok && (status < 300 || status == 404 || (status >= 400 && status < 500 && status != 409))) return;
+      if (ok && (status < 300 || status == 404 || (status >= 400 && status < 500 && status != 409 && status != 429)))
+        return;
       status_retries_.fetch_add(1);
       std::this_thread::sleep_for(std::chrono::microseconds(std::min(100000, 500 << std::min(attempt, 8))));
     }
+  }
+
+  // The end of a graceful deletion, as kubelet does it: the containers have stopped (runtime slice released), the
+  // terminal phase is reported, and the object is deleted with grace 0 under a UID precondition (a pod re-created
+  // under the same name is not touched).  mu_ held on entry and exit, dropped around the API calls.
+  void finalize_locked(const Final& f, std::unique_lock<std::mutex>& lk) {
+    stop_pod_locked(f.uid);
+    for (auto it = releases_.begin(); it != releases_.end(); ++it) {
+      if (it->first != f.uid) continue;
+      auto rel = *it;
+      releases_.erase(it);
+      release_one(rel, lk);
+      break;
+    }
+    finals_done_++;
+    lk.unlock();
+    const std::string path = "/api/v1/namespaces/" + f.ns + "/pods/" + f.name;
+    if (f.ran) patch_status(path, "{\"status\":{\"phase\":\"Succeeded\"}}");
+    std::string body = "{\"kind\":\"DeleteOptions\",\"apiVersion\":\"v1\",\"gracePeriodSeconds\":0,"
+                       "\"preconditions\":{\"uid\":";
+    json::append_quoted(&body, f.uid);
+    body.append("}}");
+    for (int attempt = 0; attempt < 50 && !stop_flag_.load(); ++attempt) {
+      int status = 0;
+      std::string resp, err;
+      bool ok = api_.request("DELETE", path, body, "application/json", &status, &resp, &err);
+      // 409: the UID precondition failed (another pod has the name now); 404: already gone
+      if (ok && (status < 300 || status == 404 || status == 409 || (status >= 400 && status < 500 && status != 429)))
+        break;
+      status_retries_.fetch_add(1);
+      std::this_thread::sleep_for(std::chrono::microseconds(std::min(100000, 500 << std::min(attempt, 8))));
+    }
+    lk.lock();
   }
 
   // DELETE a pod's slice on its runtime; mu_ held on entry and exit, dropped around the call.
@@ -1180,6 +1247,10 @@ class Agent {
   std::deque<std::function<void(std::unique_lock<std::mutex>&)>> starts_;  // admitted pods to start (pod workers)
   std::vector<std::pair<double, std::string>> delayed_;
   std::deque<std::pair<std::string, int>> releases_;
+  std::vector<Final> finals_;                 // graceful deletions to end (finalize_locked)
+  std::unordered_set<std::string> finals_set_;
+  uint64_t finals_done_ = 0;
+  double stop_delay_ = 0;
   std::map<int, int> releasing_;  // per GPU: DELETEs in flight on some worker
   std::unordered_map<std::string, int> assign_retries_;  // per pod: ASSIGNED patch attempts (backoff)
   std::atomic<uint64_t> status_retries_{0};
@@ -1212,7 +1283,7 @@ void on_sig(int) { g_stop = 1; }
 int main(int argc, char** argv) {
   std::string apiserver, node, profile = "shared-gpu", unit = "GiB", port_file, host = "127.0.0.1", plugin_socket, plugin_python;
   int workers = 16, port = 0;
-  double batch_window = 0;
+  double batch_window = 0, stop_delay = 0;
   bool verify = true, serial = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -1235,10 +1306,12 @@ int main(int argc, char** argv) {
     else if (a == "--plugin-socket") plugin_socket = val("--plugin-socket");
     else if (a == "--plugin-spawn") plugin_python = val("--plugin-spawn");
     else if (a == "--batch-window") batch_window = std::atof(val("--batch-window").c_str());
+    else if (a == "--stop-delay") stop_delay = std::atof(val("--stop-delay").c_str());
     else if (a == "-h" || a == "--help") {
       std::printf("usage: gsx-nodeagent --apiserver URL --node NAME [--profile P] [--unit GiB|MiB] [--workers N]\n"
                   "                     [--no-verify] [--serial-admission] [--port P] [--port-file F]\n"
-                  "                     [--plugin-socket S | --plugin-spawn PYTHON] [--batch-window SECONDS]\n");
+                  "                     [--plugin-socket S | --plugin-spawn PYTHON] [--batch-window SECONDS]\n"
+                  "                     [--stop-delay SECONDS]\n");
       return 0;
     } else {
       std::fprintf(stderr, "unknown argument %s\n", a.c_str());
@@ -1262,6 +1335,7 @@ int main(int argc, char** argv) {
   agent.set_plugin_socket(plugin_socket);
   agent.set_serial_admission(serial);
   agent.set_batch_window(batch_window);
+  agent.set_stop_delay(stop_delay);
   if (!plugin_python.empty()) agent.set_plugin_spawn(plugin_python, apiserver, profile, unit);
   std::string err;
   CtlServer srv([&](const http::Message& m) { return agent.handle(m); });

@@ -20,9 +20,12 @@ device plugin and the CLI use, with the semantics they rely on:
   ``pkg/cache/nodeinfo.go:150-189``);
 * JSON merge patch and strategic-merge-patch (treated as merge patch, which is
   exact for the metadata/annotation/status patches used here);
-* graceful pod deletion (``deletionTimestamp`` first, object removed after the
-  grace period) and immediate deletion;
-* fault injection: conflict / error rates, latency and watch drops
+* graceful pod deletion as kube-apiserver does it: a bound, non-terminal pod only gets ``deletionTimestamp`` (the
+  grace from the request, else ``spec.terminationGracePeriodSeconds``); the object stays until the node's kubelet,
+  having stopped the containers, deletes it with grace 0 (the kubelet stand-ins in ``gsxtools/agent.py`` and
+  ``native/nodeagent`` do).  Unbound or terminal pods, and grace 0, are removed at once.  DELETE honours
+  ``preconditions.uid`` (409 on mismatch), as kubelet's final delete relies on;
+* fault injection: conflict / error / throttle (429 + ``Retry-After``) rates, latency and watch drops
   (``POST /fake/faults``), which the reference never had.
 
 Run standalone with ``python -m tests.fixtures.fakeapi`` (or use ``gsx-fakeapi``).
@@ -203,12 +206,16 @@ class Faults:
         self.fail_lists = False  # LIST requests answer 503 (an apiserver that cannot serve reads)
         self.drop_binding_annotations = False  # Binding.metadata.annotations are not copied onto the pod
         self.slow_bindings: dict[str, float] = {}  # pod name -> ms a binding of it takes
+        # API Priority and Fairness: this share of non-watch /api/v1 requests answers 429 Too Many Requests with
+        # Retry-After: retry_after seconds (fractional in tests; kube-apiserver sends whole seconds)
+        self.throttle_rate = 0.0
+        self.retry_after = 1.0
         self.seed = 0
         self.rng = random.Random(0)
 
     def update(self, d: dict):
         for k in ("conflict_rate", "error_rate", "latency_ms", "drop_watch_after", "expire_watches", "hold_watches",
-                  "fail_lists", "drop_binding_annotations"):
+                  "fail_lists", "drop_binding_annotations", "throttle_rate", "retry_after"):
             if k in d:
                 setattr(self, k, type(getattr(self, k))(d[k]))
         if "slow_bindings" in d:
@@ -221,7 +228,8 @@ class Faults:
         return {"conflict_rate": self.conflict_rate, "error_rate": self.error_rate,
                 "latency_ms": self.latency_ms, "drop_watch_after": self.drop_watch_after,
                 "expire_watches": self.expire_watches, "hold_watches": self.hold_watches,
-                "fail_lists": self.fail_lists, "drop_binding_annotations": self.drop_binding_annotations}
+                "fail_lists": self.fail_lists, "drop_binding_annotations": self.drop_binding_annotations,
+                "throttle_rate": self.throttle_rate, "retry_after": self.retry_after}
 
 
 class FakeApiServer:
@@ -238,7 +246,6 @@ class FakeApiServer:
         self.faults = Faults()
         self.binding_log: list[str] = []  # pod names in binding commit order
         self.counts = collections.Counter()
-        self._grace_tasks: set[asyncio.Task] = set()
         self._last: tuple | None = None
         self.app = self._make_app()
 
@@ -398,10 +405,22 @@ class FakeApiServer:
         self.store["pods"][(ns, name)] = new
         self._emit("pods", "MODIFIED", new)
 
-    def delete(self, kind: str, ns: str, name: str, grace: float | None = None) -> dict:
+    def delete(self, kind: str, ns: str, name: str, grace: float | None = None, uid: str = "") -> dict:
+        """DELETE as kube-apiserver answers it.  A bound pod that is not terminal is deleted gracefully: it gets
+        ``deletionTimestamp`` and stays until a delete with grace 0 (its kubelet's, once the containers stopped).
+        ``grace`` None takes the pod's ``spec.terminationGracePeriodSeconds`` (absent: 0 -- the pods the tests build
+        carry none, and a delete without a grace was immediate in every round so far)."""
         cur = self._get(kind, ns, name)
+        if uid and uid != cur["metadata"].get("uid"):
+            raise HTTPError(409, status_body(
+                409, "Conflict", f"Precondition failed: UID in precondition: {uid}, "
+                                 f"UID in object meta: {cur['metadata'].get('uid')}"))
         key = (ns if kind != "nodes" else "", name)
-        if kind == "pods" and grace and grace > 0 and (cur.get("spec") or {}).get("nodeName"):
+        if kind == "pods" and grace is None:
+            grace = float((cur.get("spec") or {}).get("terminationGracePeriodSeconds") or 0)
+        phase = (cur.get("status") or {}).get("phase", "")
+        if (kind == "pods" and grace and grace > 0 and (cur.get("spec") or {}).get("nodeName")
+                and phase not in ("Succeeded", "Failed")):
             if cur["metadata"].get("deletionTimestamp"):
                 return cur
             new = dict(cur)
@@ -411,10 +430,6 @@ class FakeApiServer:
             new["metadata"]["resourceVersion"] = self._bump()
             self.store[kind][key] = new
             self._emit(kind, "MODIFIED", new)
-            loop = asyncio.get_running_loop()
-            t = loop.create_task(self._finalize_later(kind, ns, name, new["metadata"]["uid"], grace))
-            self._grace_tasks.add(t)
-            t.add_done_callback(self._grace_tasks.discard)
             return new
         del self.store[kind][key]
         gone = dict(cur)
@@ -422,12 +437,6 @@ class FakeApiServer:
         gone["metadata"]["resourceVersion"] = self._bump()
         self._emit(kind, "DELETED", gone)
         return gone
-
-    async def _finalize_later(self, kind, ns, name, uid, grace):
-        await asyncio.sleep(grace)
-        cur = self.store[kind].get((ns, name))
-        if cur is not None and cur["metadata"]["uid"] == uid:
-            self.delete(kind, ns, name, None)
 
     def list(self, kind: str, ns: str = "", fsel: str = "", lsel: str = "") -> list[dict]:
         out = []
@@ -486,7 +495,15 @@ class FakeApiServer:
 
         def h(request):
             self.counts[request.method] += 1
-            if self.faults.latency_ms and request.query.get("watch") not in ("1", "true"):
+            watch = request.query.get("watch") in ("1", "true")
+            if (self.faults.throttle_rate and not watch and request.path.startswith("/api/v1/")
+                    and self.faults.rng.random() < self.faults.throttle_rate):
+                self.counts["injected_throttle"] += 1
+                ra = self.faults.retry_after
+                return Response(json.dumps(status_body(429, "TooManyRequests", "Too many requests, please try again "
+                                                       "later.", {"retryAfterSeconds": int(ra)})).encode(), 429,
+                                headers={"Retry-After": f"{ra:g}"})
+            if self.faults.latency_ms and not watch:
                 return slow(request)
             return handler(request)
         return h
@@ -644,21 +661,30 @@ class FakeApiServer:
         return h
 
     @staticmethod
-    def _grace(request):
-        if "gracePeriodSeconds" in request.query:
-            return float(request.query["gracePeriodSeconds"])
+    def _delete_options(request) -> tuple[float | None, str]:
+        """(gracePeriodSeconds, preconditions.uid) from the query or the DeleteOptions body."""
+        grace, uid = None, ""
         if request.body:
             try:
                 b = request.json()
-                if isinstance(b, dict) and b.get("gracePeriodSeconds") is not None:
-                    return float(b["gracePeriodSeconds"])
             except ValueError:
-                pass
-        return None
+                b = None
+            if isinstance(b, dict):
+                if b.get("gracePeriodSeconds") is not None:
+                    grace = float(b["gracePeriodSeconds"])
+                uid = ((b.get("preconditions") or {}).get("uid")) or ""
+        if "gracePeriodSeconds" in request.query:
+            grace = float(request.query["gracePeriodSeconds"])
+        return grace, uid
+
+    @classmethod
+    def _grace(cls, request):
+        return cls._delete_options(request)[0]
 
     def _mk_delete(self, kind):
         def h(request):
-            obj = self.delete(kind, request.match_info.get("ns", ""), request.match_info["name"], self._grace(request))
+            grace, uid = self._delete_options(request)
+            obj = self.delete(kind, request.match_info.get("ns", ""), request.match_info["name"], grace, uid)
             return self._json(obj)
         return h
 

@@ -364,3 +364,199 @@ def test_binding_annotations_dropped_by_apiserver_self_heals(agent):
         finally:
             await cl.close()
     asyncio.run(go())
+
+
+GRACE_SEEDS = (3, 5, 8)
+if os.environ.get("GSX_CHAOS_GRACE_SEEDS"):  # a sweep: "first-last" (inclusive)
+    _lo, _hi = (int(x) for x in os.environ["GSX_CHAOS_GRACE_SEEDS"].split("-"))
+    GRACE_SEEDS = tuple(range(_lo, _hi + 1))
+
+
+@pytest.mark.parametrize("agent", ["native-plugin", "faithful"])
+@pytest.mark.parametrize("seed", GRACE_SEEDS)
+def test_chaos_graceful_deletes_on_a_full_node(seed, agent, monkeypatch):
+    """pods are deleted the way users delete them -- gracefully, ``gracePeriodSeconds`` 2-3 s -- on a
+    node whose GPUs are full, with containers that take that long to stop (``--stop-delay``), while new pods wait
+    for the room.  kube-apiserver only marks such a pod; its kubelet stops the containers, reports the terminal phase
+    and deletes the object with grace 0.  The extender keeps a terminating pod's share charged until then, so no
+    pod is bound into room a stopping container still fills: no pod fails, the plugin's physical guard never takes
+    its fail-closed branch, and neither the annotations nor the containers ever promise a GPU past its capacity."""
+    monkeypatch.setenv("GSX_PLUGIN_GUARD_WAIT_S", "0.5")
+    monkeypatch.setenv("GSX_PLUGIN_GUARD_GONE_WAIT_S", "1.0")
+    faithful = agent == "faithful"
+    cl_agent = "plugin" if faithful else "native-plugin"
+    args = (["--faithful"] if faithful else []) + ["--stop-delay", "2.0"]
+
+    async def go():
+        rnd = random.Random(seed)
+        cl = Cluster(ALIYUN, [96] * 4, gpu=False, agent=cl_agent, agent_args=args)
+        try:
+            await cl.start()
+            live: dict[str, int] = {}
+            for i in range(16):  # full: 4 x 24 GiB per GPU
+                live[f"f{i}"] = 24
+                await cl.create(f"f{i}", 24)
+            await cl.wait(sorted(live), timeout=30)
+            terminating: set[str] = set()
+            for rnd_no in range(3):
+                victims = rnd.sample(sorted(live), 4)
+                for n in victims:
+                    await cl.c.delete("pods", n, "default", grace_seconds=rnd.choice([2, 3]))
+                    live.pop(n)
+                    terminating.add(n)
+                new = [f"r{rnd_no}-{k}" for k in range(4)]
+                for n in new:  # the same room again, in other sizes: they wait for the stopping containers
+                    live[n] = rnd.choice([8, 16, 24])
+                    await cl.create(n, live[n])
+                deadline = time.monotonic() + 30
+                while True:
+                    pods = {p["metadata"]["name"]: p for p in (await cl.c.list("pods", "default"))["items"]}
+                    failed = [n for n, p in pods.items() if p["status"].get("phase") == "Failed"]
+                    assert not failed, (failed, await _plugin_state(cl))
+                    bound = {n: p for n, p in pods.items() if p["spec"].get("nodeName")}
+                    running = [n for n, p in bound.items() if p["status"].get("phase") == "Running"]
+                    used, holds = _committed_use(cl, bound)
+                    assert all(u <= 96 for u in used), ("annotations", used)
+                    phys = await _physical_use(cl, bound, running)
+                    assert all(u <= 96 for u in phys), ("physical", phys)
+                    terminating &= set(pods)
+                    if not terminating and all(n in running for n in live) and not holds:
+                        break
+                    assert time.monotonic() < deadline, {"terminating": sorted(terminating), "used": used,
+                                                         "running": len(running), "live": len(live)}
+                    await asyncio.sleep(0.05)
+            drift, drifted = await cl.physical_drift(sorted(live), timeout=15)
+            assert drift == 0, drifted
+            insp = await cl.inspect()
+            assert [d["usedGPU"] for d in insp["nodes"][0]["devs"]] == _committed_use(cl, {
+                n: p for n, p in pods.items() if n in live})[0]
+            st = await cl.agent_stats()
+            assert st["failed"] == 0 and st.get("finalized", 0) >= 12, st
+            ps = (await _plugin_debug(cl)).get("stats") or {}
+            assert ps.get("physical_guard_failed", 0) == 0 and ps.get("allocate_fail", 0) == 0, ps
+        finally:
+            await cl.close()
+    asyncio.run(go())
+
+
+@pytest.mark.parametrize("agent", ["native-plugin", "plugin"])
+def test_chaos_apiserver_throttling_every_call_retried(agent):
+    """API Priority and Fairness answers 20 % of the stack's apiserver calls 429 with Retry-After
+    (scheduler, extender binds and reflectors, plugin commits, kubelet status).  Every client waits the server's
+    Retry-After and sends again (client-go's contract), so every pod ends bound and Running and no bind fails."""
+    async def go():
+        cl = Cluster(ALIYUN, [96] * 4, gpu=False, agent=agent)
+        try:
+            await cl.start()
+            api = HttpClient(cl.api.url)
+            await api.request("POST", "/fake/faults", json.dumps({"throttle_rate": 0.2, "retry_after": 0.01,
+                                                                  "seed": 9}).encode())
+            names = [f"t{i}" for i in range(24)]
+            rnd = random.Random(9)
+            for n in names:
+                await cl.create(n, rnd.choice([8, 12, 16]))
+            await cl.wait(names, timeout=60)
+            for n in names[:8]:
+                await cl.c.delete("pods", n, "default")
+            more = [f"u{i}" for i in range(8)]
+            for n in more:
+                await cl.create(n, 8)
+            await cl.wait(more, timeout=60)
+            st = json.loads((await api.request("GET", "/fake/stats")).body)
+            await api.request("POST", "/fake/faults", json.dumps({"throttle_rate": 0}).encode())
+            await api.close()
+            assert st["counts"].get("injected_throttle", 0) >= 15, st["counts"]
+            ext = HttpClient(cl.ext.url)
+            srv = json.loads((await ext.request("GET", "/debug/engine")).body)["server"]
+            await ext.close()
+            assert srv["bind_fail"] == 0 and srv["bind_ok"] >= 32, srv
+            ast = await cl.agent_stats()
+            assert ast["failed"] == 0 and ast.get("allocate_errors", 0) == 0, ast
+        finally:
+            await cl.close()
+    asyncio.run(go())
+
+
+async def _plugin_debug(cl) -> dict:
+    try:
+        url = (await cl.agent_stats()).get("plugin_debug")
+        if not url:
+            return {}
+        h = HttpClient(url)
+        try:
+            return json.loads((await h.request("GET", "/debug/state")).body)
+        finally:
+            await h.close()
+    except (OSError, ValueError):
+        return {}
+
+
+def test_extender_restart_holds_binds_until_the_node_republishes_its_physical_use():
+    """VERDICT r5 #3 / ADVICE r5: the device plugin's publication of its unaccounted GPU use (containers holding room
+    the annotations put elsewhere) lives only in the extender's memory.  A SIGKILLed extender comes back in a new
+    epoch; binds to a node whose plugin publishes (node annotation) wait for that plugin's first publication of the
+    epoch, so no bind lands in room a swapped container still fills, and binds resume as soon as it arrives.  A
+    standby answers /physical 503 (the plugin must not count it delivered)."""
+    from gpushare_scheduler_extender_amd.models.profile import NODE_PHYSICAL_PUBLICATION_ANNOTATION
+    from gsxtools.configs import NODE as N
+
+    async def go():
+        cl = Cluster(ALIYUN, [96, 96], gpu=False, agent="inproc")
+        try:
+            await cl.start()
+            await cl.c.patch("nodes", N, {"metadata": {"annotations": {NODE_PHYSICAL_PUBLICATION_ANNOTATION: "true"}}})
+
+            async def ext(method, path, body=None):
+                h = HttpClient(cl.ext.url)
+                try:
+                    r = await h.request(method, path, json.dumps(body).encode() if body is not None else None)
+                    return r.status, json.loads(r.body or b"{}")
+                finally:
+                    await h.close()
+
+            async def publish(extra):
+                return await ext("POST", "/gpushare-scheduler/physical", {"node": N, "unaccounted": extra, "ttl": 60})
+
+            async def node_of(name):
+                return (await cl.c.get("pods", name, "default"))["spec"].get("nodeName")
+
+            st, e1 = await ext("GET", "/gpushare-scheduler/epoch")
+            assert st == 200 and e1["leader"] and e1["epoch"]
+            st, body = await publish(None)  # the plugin's first publication of the epoch: nothing unaccounted
+            assert st == 200 and body["epoch"] == e1["epoch"]
+            await cl.create("a", 60)  # best fit: GPU 0 (36 free after)
+            await cl.wait(["a"])
+            assert cl.device_of(await cl.c.get("pods", "a", "default")) == 0
+            # a swapped container physically fills 90 of GPU 1 that no annotation charges there
+            assert (await publish([0, 90]))[0] == 200
+            cl.kill_extender()
+            cl.restart_extender()  # rebuilt from the annotations: the publication is gone
+            for _ in range(400):
+                st, e2 = await ext("GET", "/gpushare-scheduler/epoch")
+                if st == 200:
+                    break
+                await asyncio.sleep(0.01)
+            assert e2["epoch"] != e1["epoch"]
+            # 48 GiB fits GPU 1 by the annotations only: held while the node has not republished
+            await cl.create("b", 48)
+            await asyncio.sleep(1.0)
+            assert await node_of("b") is None, "bound before the node republished its physical use"
+            t0 = time.monotonic()
+            st, body = await publish([0, 90])  # the plugin saw the epoch change and republishes
+            assert st == 200 and body["epoch"] == e2["epoch"]
+            await asyncio.sleep(1.0)
+            assert await node_of("b") is None  # no room anywhere: never into the unaccounted room
+            t1 = time.monotonic()
+            assert (await publish(None))[0] == 200  # the swapped container stopped: withdrawn
+            for _ in range(200):
+                if await node_of("b"):
+                    break
+                await asyncio.sleep(0.01)
+            assert await node_of("b") == N and time.monotonic() - t1 < 1.0
+            assert cl.device_of(await cl.c.get("pods", "b", "default")) == 1
+            srv = (await ext("GET", "/debug/engine"))[1]["server"]
+            assert srv["publication_waits"] >= 1, srv
+            assert t1 - t0 >= 1.0
+        finally:
+            await cl.close()
+    asyncio.run(go())

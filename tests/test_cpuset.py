@@ -92,3 +92,31 @@ def test_order_cores_least_busy_domain_when_none_is_idle(monkeypatch):
     load[12] = 0.9  # domain B: one core taken by another job
     assert [c[0] for c in cpuset._order_cores(cores, load, need=4)[:4]] == [8, 9, 10, 11]
     assert [c[0] for c in cpuset._order_cores(cores, load, need=3)[:3]] == [13, 14, 15]
+
+
+def test_n8_plan_degrades_to_unpinned_on_a_16_cpu_cgroup(monkeypatch, caplog):
+    """the N = 8 bench asks for more CPUs (29) than a 16-CPU share of an 8-GPU node may give; the plan
+    comes back empty -- nothing pinned -- with a warning, and the run goes on (bench.py pins nothing with {})."""
+    import logging
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    names, widths, _ = bench.cpu_slots(8)
+    asked = sum(widths.get(n, 1) for n in names)
+    assert asked == 29, (asked, widths)
+    allowed = list(range(100, 116))  # a 16-CPU cgroup, SMT pairs (100,101), (102,103), ...
+    monkeypatch.setattr(cpuset.os, "sched_getaffinity", lambda pid: set(allowed))
+    monkeypatch.setattr(cpuset, "_cores", lambda cpus: [(c, c + 1) for c in sorted(cpus) if c % 2 == 0])
+    monkeypatch.setattr(cpuset, "_group_key", lambda cpu: (0,))
+    with caplog.at_level(logging.WARNING, logger="gsx.cpuset"):
+        assert cpuset.plan(names, widths, "spread", load={c: 0.0 for c in allowed}, smt=True) == {}
+        assert cpuset.plan(names, widths, "spread", load={c: 0.0 for c in allowed}, smt=False) == {}
+    assert sum("not pinning" in r.message for r in caplog.records) == 2
+    # the N = 1 plan (10 CPUs) still fits such a share
+    n1, w1, _ = bench.cpu_slots(1)
+    p = cpuset.plan(n1, w1, "spread", load={c: 0.0 for c in allowed}, smt=True)
+    assert p and sum(len(v) for v in p.values()) == sum(w1.get(n, 1) for n in n1)
+    cpuset.pin_self(None)  # an empty slot pins nothing (bench.py with the degraded plan)

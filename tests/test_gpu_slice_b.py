@@ -5,7 +5,7 @@ fake kube-apiserver, the extender (native front end), the kube-scheduler
 simulator's filter and bind, the device plugin's Allocate (``ASSIGNED=true``)
 — and is then started by :class:`ProcessRuntime` with exactly the container
 environment Allocate returned.  The container is the sample workload
-(``samples/workload``, bf16 MFMA GEMM loop) which must run on the assigned
+(``samples/workload``: its ``run.sh`` entry and standalone ``main.py``, bf16 MFMA GEMM loop) which must run on the assigned
 GPU inside its memory share: ``set_per_process_memory_fraction`` =
 share / device total, and a second share-sized allocation is refused.
 
@@ -45,9 +45,14 @@ def test_slice_b_pod_runs_inside_its_share_on_mi355x():
         api = await FakeApiServerRunner().start()
         client = KubeClient(api.url)
         ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url), SHARED_GPU)).start()
-        cmd = [sys.executable, "-m", "gsxtools.workload", "--iters", "40", "--size", "4096",
-               "--touch", "--probe-limit", "--json"]
-        rt = ProcessRuntime(cmd, extra_env={"PYTHONPATH": str(ROOT)}, cwd=str(ROOT))
+        # the sample image's entry (samples/workload/run.sh -> main.py, standalone), with the MFMA kernel library
+        # the image builds -- here the repository's build of it, as if mounted; nothing else of the repo is visible
+        app = ROOT / "samples" / "workload"
+        cmd = ["bash", str(app / "run.sh"), "--iters", "40", "--size", "4096", "--touch", "--probe-limit", "--json",
+               "--kernel", "gsx"]
+        lib = ROOT / "gpushare_scheduler_extender_amd" / "_native" / "libgsx_kernels.so"
+        rt = ProcessRuntime(cmd, extra_env={"GSX_APP_DIR": str(app), "GSX_KERNELS_LIB": str(lib), "PYTHONPATH": ""},
+                            cwd="/tmp")
         agent = NodeAgent(KubeClient(api.url), "mi355x-0", [dev], SHARED_GPU, rt, unit="GiB")
         sim = SchedulerSim(KubeClient(api.url), ext.url, SHARED_GPU)
         try:
@@ -86,5 +91,6 @@ def test_slice_b_pod_runs_inside_its_share_on_mi355x():
     assert res["visible_devices"] == "0"
     assert abs(res["fraction"] - 64 / gib) < 1e-6
     assert res["limit_enforced"] is True
+    assert res["kernel"] == "gsx" and res["kernels_lib"].endswith("_native/libgsx_kernels.so"), res
     assert res["tflops"] > 100, res  # bf16 MFMA GEMM at 4096^3 on MI355X runs at ~1 PFLOP/s
     print("slice B:", json.dumps(res))

@@ -5,6 +5,7 @@ import json
 import os
 import socket
 import tempfile
+import time
 
 import pytest
 import yaml
@@ -139,12 +140,35 @@ def test_selectors_graceful_delete_and_deletecollection(impl):
             lst = await c.list("pods", label_selector="wave!=1")
             assert [p["metadata"]["name"] for p in lst["items"]] == ["c"]
             d = await c.delete("pods", "a", "default", grace_seconds=1)
-            assert d["metadata"]["deletionTimestamp"]
+            assert d["metadata"]["deletionTimestamp"] and d["metadata"]["deletionGracePeriodSeconds"] == 1
             assert (await c.get("pods", "a", "default"))["metadata"]["deletionTimestamp"]
+            # kube-apiserver never ends a graceful deletion on its own: the object stays (Terminating) past the
+            # grace period until the node's kubelet deletes it with grace 0 once its containers stopped
             await asyncio.sleep(1.2)
+            assert (await c.get("pods", "a", "default"))["metadata"]["deletionTimestamp"]
+            # kubelet's final delete carries a UID precondition: another UID is refused (409), the right one goes
+            with pytest.raises(ApiError) as ei:
+                await c.delete("pods", "a", "default", grace_seconds=0, uid="not-the-uid")
+            assert ei.value.conflict and "Precondition failed" in ei.value.message
+            await c.delete("pods", "a", "default", grace_seconds=0, uid=d["metadata"]["uid"])
             with pytest.raises(ApiError) as ei:
                 await c.get("pods", "a", "default")
             assert ei.value.not_found
+            # an unbound pod, or a terminal one, goes at once whatever the grace
+            await c.create("pods", make_pod("u", 1, labels={"wave": "3"}))
+            assert "deletionTimestamp" not in (await c.delete("pods", "u", "default", grace_seconds=30))["metadata"]
+            await c.create("pods", make_pod("t", 1, node="n1", labels={"wave": "3"}))
+            await c.patch("pods", "t", {"status": {"phase": "Succeeded"}}, "default", sub="status")
+            await c.delete("pods", "t", "default", grace_seconds=30)
+            with pytest.raises(ApiError) as ei:
+                await c.get("pods", "t", "default")
+            assert ei.value.not_found
+            # no grace given: the pod's spec.terminationGracePeriodSeconds
+            g = make_pod("g", 1, node="n1", labels={"wave": "3"})
+            g["spec"]["terminationGracePeriodSeconds"] = 30
+            await c.create("pods", g)
+            assert (await c.delete("pods", "g", "default"))["metadata"]["deletionGracePeriodSeconds"] == 30
+            await c.delete("pods", "g", "default", grace_seconds=0)
             out = await c.request("DELETE", "/api/v1/namespaces/default/pods", params={"labelSelector": "wave=1"})
             assert [p["metadata"]["name"] for p in out["items"]] == ["b"]
             assert [p["metadata"]["name"] for p in (await c.list("pods"))["items"]] == ["c"]
@@ -800,3 +824,56 @@ srv.serve_forever()
     finally:
         proc.kill()
         proc.wait()
+
+
+@IMPLS
+def test_throttled_requests_wait_retry_after_and_go_through(impl):
+    """API Priority and Fairness answers 429 + Retry-After.  The fakes inject it (throttle_rate) and
+    the client sends the request again after the server's Retry-After, up to 10 sends (client-go,
+    vendor/k8s.io/client-go/rest/request.go:658-734,973-995): every call lands, and the waits add up to what the
+    server asked for."""
+    async def go():
+        r, c = await _api(impl=impl)
+        try:
+            await c.request("POST", "/fake/faults", body={"throttle_rate": 0.3, "retry_after": 0.01, "seed": 5})
+            t0 = time.monotonic()
+            for i in range(30):
+                await c.create("pods", make_pod(f"p{i}", 1, node="n1"))
+                await c.patch("pods", f"p{i}", {"metadata": {"annotations": {"k": str(i)}}}, "default")
+            assert len((await c.list("pods"))["items"]) == 30
+            st = (await c.request("GET", "/fake/stats"))["counts"]
+            assert st.get("injected_throttle", 0) == c.throttled > 5
+            assert abs(c.throttle_wait_s - 0.01 * c.throttled) < 1e-6  # exactly Retry-After each time
+            assert time.monotonic() - t0 >= c.throttle_wait_s
+            # the server keeps refusing: the 10th send's 429 reaches the caller
+            await c.request("POST", "/fake/faults", body={"throttle_rate": 1.0, "retry_after": 0.001})
+            before = c.throttled
+            with pytest.raises(ApiError) as ei:
+                await c.get("pods", "p0", "default")
+            assert ei.value.throttled and ei.value.transient and c.throttled - before == 9
+            await c.request("POST", "/fake/faults", body={"throttle_rate": 0})
+        finally:
+            await c.close()
+            await r.stop()
+    run(go())
+
+
+def test_retry_wait_contract_python_and_native_agree():
+    """Retry-After honoured (fractions too, clamped at 30 s), 429 without it backs off exponentially with jitter,
+    a 5xx without it is the caller's, nothing after the 10th send; the C++ ApiClient computes the same waits."""
+    from gpushare_scheduler_extender_amd.core.engine import native
+    from gpushare_scheduler_extender_amd.k8s.client import retry_wait
+
+    cases = [(429, "1", 0), (429, "0.25", 3), (503, "2", 0), (500, "", 0), (503, "", 4), (429, "", 0), (429, "", 5),
+             (429, "", 30), (429, "Wed, 21 Oct 2015 07:28:00 GMT", 1), (429, "120", 0), (409, "1", 0), (429, "1", 9),
+             (429, "1", 8), (404, "", 0)]
+    eng = native()
+    for status, ra, attempt in cases:
+        for jit in (0.0, 0.5, 0.999):
+            py = retry_wait(status, ra, attempt, jitter=jit)
+            cc = eng.api_retry_wait(status, ra, attempt, jit)
+            assert (py is None and cc < 0) or (py is not None and abs(py - cc) < 1e-12), (status, ra, attempt, py, cc)
+    assert retry_wait(429, "1", 0) == 1.0 and retry_wait(429, "120", 0) == 30.0
+    assert retry_wait(500, "", 0) is None and retry_wait(429, "1", 9) is None
+    assert 0.0025 <= retry_wait(429, "", 0) < 0.005 and retry_wait(429, "", 8, jitter=0.0) == 0.5
+    assert retry_wait(429, "", 8, max_attempts=100, jitter=0.999) < 1.0 and retry_wait(429, "", 30, max_attempts=100) <= 1.0

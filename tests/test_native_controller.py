@@ -165,3 +165,35 @@ def test_native_controller_rewatch_and_relist_after_410():
             await e.c.create("pods", annotated("late", 2, 1))
             await settle(lambda: e.used() == [2, 5])
     run(go())
+
+
+def test_terminating_pod_stays_charged_until_its_object_goes():
+    """VERDICT r5 #1 / SURVEY §7.5 ("deleting pods still count -- keep (conservative)"): a pod with a
+    deletionTimestamp keeps its share charged -- kubelet is still stopping its containers, and kube-scheduler's own
+    NodeInfo counts it until the object is gone.  Freed when its phase turns terminal (kubelet reports the stopped
+    containers) or when the DELETED event arrives (kubelet's grace-0 delete); BuildCache counts it too."""
+    async def go():
+        async with Env() as e:
+            await e.c.create("nodes", make_node("n", 32, 2, profile=P))
+            await e.c.create("pods", annotated("early", 4, 0))
+            await e.c.delete("pods", "early", "default", grace_seconds=30)  # terminating before the extender starts
+            await e.start()
+            assert e.used() == [4, 0]  # BuildCache: a terminating pod is charged
+            await e.c.create("pods", annotated("a", 8, 1))
+            await settle(lambda: e.used() == [4, 8])
+            await e.c.delete("pods", "a", "default", grace_seconds=30)
+            await asyncio.sleep(0.2)
+            assert e.used() == [4, 8], "a terminating pod's share was freed at its deletionTimestamp"
+            assert e.eng.check("n", 16) == 3  # no device has 16 free while it terminates
+            insp = __import__("json").loads(e.eng.inspect("")[0])
+            dev1 = insp["nodes"][0]["devs"][1]
+            assert dev1["usedGPU"] == 8 and dev1["pods"] == []  # listed no more (AssignedNonTerminatedPod)
+            # kubelet stopped the containers and reports the terminal phase: freed
+            await e.c.patch("pods", "a", {"status": {"phase": "Succeeded"}}, "default", sub="status")
+            await settle(lambda: e.used() == [4, 0])
+            # the other way out: kubelet's grace-0 delete (DELETED event)
+            uid = (await e.c.get("pods", "early", "default"))["metadata"]["uid"]
+            await e.c.delete("pods", "early", "default", grace_seconds=0, uid=uid)
+            await settle(lambda: e.used() == [0, 0])
+            assert e.eng.check("n", 16) == 0
+    run(go())

@@ -432,14 +432,17 @@ def test_early_answer_commit_of_a_deleted_pod_releases_it_before_the_feed_does()
 
 def test_early_answer_checkpoint_failure_keeps_the_journal_generation():
     """the journal is rotated (not truncated) with the records snapshot; a checkpoint that fails to land
-    leaves the rotated generation in place, and a restarted plugin still finds the record."""
+    leaves the rotated generation in place, and a restarted plugin still finds the record.  ADVICE r5: a second
+    failed checkpoint appends the next generation to .old after trimming its zero padding, so both records are
+    recovered (a NUL run before the appended line made the loader skip it as torn)."""
     async def go():
         tmp = tempfile.mkdtemp()
         api_srv, client, plugin = await _plugin(tmp, fast=True)
         pc = PluginClient(plugin.socket_path)
         try:
             a = await client.create("pods", bound_pod("a", 4, dev=0, assume=1, dev_total=16))
-            await client.create("pods", bound_pod("b", 4, dev=0, assume=2, dev_total=16))
+            b = await client.create("pods", bound_pod("b", 4, dev=0, assume=2, dev_total=16))
+            await client.create("pods", bound_pod("c", 4, dev=0, assume=3, dev_total=16))
             await asyncio.sleep(0.2)
             os.makedirs(plugin.checkpoint + ".tmp")  # the checkpoint write fails (a directory where its file goes)
             api_srv.server.faults.error_rate = 1.0  # and the commit never lands before the plugin goes away
@@ -451,6 +454,16 @@ def test_early_answer_checkpoint_failure_keeps_the_journal_generation():
                 await asyncio.sleep(0.02)
             with open(plugin.journal_path + ".old") as f:
                 assert a["metadata"]["uid"] in f.read()
+            assert not os.path.exists(plugin.checkpoint)
+            await pc.allocate([ids[4:8]])  # b: a second generation, and a second checkpoint that fails
+            for _ in range(200):
+                with open(plugin.journal_path + ".old", "rb") as f:
+                    raw = f.read()
+                if b["metadata"]["uid"].encode() in raw:
+                    break
+                await asyncio.sleep(0.02)
+            lines = [ln for ln in raw.rstrip(b"\x00").split(b"\n") if ln]
+            assert len(lines) == 2 and all(ln.startswith(b"{") for ln in lines), raw[:400]
             assert not os.path.exists(plugin.checkpoint)
             await pc.close()
             pc = None
@@ -464,17 +477,18 @@ def test_early_answer_checkpoint_failure_keeps_the_journal_generation():
             finally:
                 os.environ.pop("GSX_PLUGIN_EARLY_ANSWER", None)
             plugin = again
-            assert again.stats.get("commits_after_restart") == 1
-            assert (await client.get("pods", "a", "default"))["metadata"]["annotations"][P.annotation_assigned] == "true"
+            assert again.stats.get("commits_after_restart") == 2
+            for n in ("a", "b"):
+                assert (await client.get("pods", n, "default"))["metadata"]["annotations"][P.annotation_assigned] == "true"
             pc = PluginClient(again.socket_path)
-            r = (await pc.allocate([ids[4:8]])).container_responses[0]
-            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "b"
+            r = (await pc.allocate([ids[8:12]])).container_responses[0]
+            assert dict(r.annotations)["gpushare.amd.com/pod"].split("/")[1] == "c"
             for _ in range(100):  # the first checkpoint supersedes both journal generations
                 if os.path.exists(again.checkpoint) and not os.path.exists(again.journal_path + ".old"):
                     break
                 await asyncio.sleep(0.02)
             with open(again.checkpoint) as f:
-                assert len(json.load(f)["records"]) == 2
+                assert len(json.load(f)["records"]) == 3
             assert not os.path.exists(again.journal_path + ".old")
         finally:
             api_srv.server.faults.error_rate = 0.0

@@ -90,3 +90,78 @@ def test_docs_do_not_describe_removed_code():
     hits = [(f.name, s) for f in files if not f.name.startswith("ROUND") for s in STALE if s in f.read_text()]
     assert not hits, hits
     assert not (ROOT / "gpushare_scheduler_extender_amd" / "parallel").exists()
+
+
+# phrases code comments must not carry any more: a file that moved, figures re-measured since, behaviour changed
+CODE_STALE = ("deviceplugin/agent.py", "idle 0.3 %", "one pod a second 0.7 %", "/opt/gpushare",
+              "the extender frees on deletion", "finalise graceful deletes on their own timer")
+
+
+def test_code_comments_do_not_describe_removed_code():
+    """the doc-drift check covers code comments and manifests too."""
+    exts = {".py", ".cc", ".h", ".hip", ".yaml", ".sh", ".md"}
+    roots = [ROOT / d for d in ("native", "gpushare_scheduler_extender_amd", "gsxtools", "deploy", "samples", "docs")]
+    files = [f for r in roots for f in r.rglob("*") if f.suffix in exts and f.is_file()] + [ROOT / "bench.py"]
+    hits = [(str(f.relative_to(ROOT)), s) for f in files for s in CODE_STALE if s in f.read_text(errors="replace")]
+    assert not hits, hits
+
+
+def _dockerfile_copies(dockerfile: Path) -> tuple[list[tuple[list[str], str]], list[str]]:
+    """(COPY sources -> destination) and RUN commands of a Dockerfile, in order (continuation lines joined)."""
+    lines, cur = [], ""
+    for raw in dockerfile.read_text().splitlines():
+        s = raw.strip()
+        if not s or s.startswith("#"):
+            continue
+        cur = f"{cur} {s[:-1]}" if s.endswith("\\") else f"{cur} {s}"
+        if not s.endswith("\\"):
+            lines.append(cur.strip())
+            cur = ""
+    copies, runs = [], []
+    for ln in lines:
+        op, _, rest = ln.partition(" ")
+        if op == "COPY":
+            *src, dst = rest.split()
+            copies.append((src, dst))
+        elif op == "RUN":
+            runs.append(rest)
+    return copies, runs
+
+
+def test_sample_workload_image_is_self_contained(tmp_path):
+    """the sample image's file set, assembled exactly as its Dockerfile does (its COPY lines, and its
+    hipcc RUN line cross-compiling the MFMA GEMM for gfx950), runs ``main.py --help`` from there with nothing of the
+    repository on the path; ``run.sh`` is the entry and passes its arguments on."""
+    df = ROOT / "samples" / "workload" / "Dockerfile"
+    copies, runs = _dockerfile_copies(df)
+    text = df.read_text()
+    assert "ARG BASE=rocm/pytorch:rocm" in text and ":latest" not in text  # a pinned base
+    assert 'ENTRYPOINT ["/app/run.sh"]' in text
+
+    def here(p: str) -> Path:  # an image path under the temp root
+        return tmp_path / p.lstrip("/")
+    for srcs, dst in copies:
+        for s in srcs:
+            target = here(dst) / Path(s).name if dst.endswith("/") else here(dst)
+            target.parent.mkdir(parents=True, exist_ok=True)
+            target.write_bytes((ROOT / s).read_bytes())
+            target.chmod((ROOT / s).stat().st_mode)
+    (hip,) = [r for r in runs if r.startswith("hipcc")]
+    cmd = hip.split("&&")[0].replace("${GPU_ARCH}", "gfx950").replace("/build", str(here("build"))).replace(
+        "/app", str(here("app")))
+    r = subprocess.run(cmd, shell=True, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert (here("app") / "libgsx_kernels.so").stat().st_size > 0
+    env = {k: v for k, v in os.environ.items() if k not in ("PYTHONPATH", "GSX_KERNELS_LIB")}
+    app = here("app")
+    assert sorted(p.name for p in app.iterdir()) == ["libgsx_kernels.so", "main.py", "run.sh"]
+    out = subprocess.run(["bash", str(app / "run.sh"), "--help"], capture_output=True, text=True, cwd=str(tmp_path),
+                         env={**env, "GSX_APP_DIR": str(app)}, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "GEMM loop inside the pod's GPU share" in out.stdout and "--probe-limit" in out.stdout
+    # the library the image built is the one main.py finds
+    probe = ("import sys; sys.argv = ['x']; import runpy; m = runpy.run_path(sys.argv[0] if False else "
+             f"'{app / 'main.py'}', run_name='probe'); print(m['kernels_lib_path']())")
+    got = subprocess.run([sys.executable, "-c", probe], capture_output=True, text=True, cwd=str(tmp_path), env=env,
+                         timeout=120)
+    assert got.stdout.strip() == str(app / "libgsx_kernels.so"), got.stderr[-1000:]

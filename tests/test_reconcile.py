@@ -62,8 +62,13 @@ async def _swap_scenario(reconcile: bool, plugin: str = "grpc"):
         await cl.start_agent()
         running = await cl.wait(names)
         phys = await _physical(cl, running)
-        # kubelet admitted p0 first and the plugin served it p3's allocation (earliest ASSUME_TIME): a real swap
-        assert phys == {"p0": 0, "p1": 1, "p2": 2, "p3": 3}, phys
+        # kubelet admitted p0 first and the plugin served it p3's allocation (earliest ASSUME_TIME): a real swap.
+        # Without a reconcile pass inside the batch the pattern is {p0: 0, p1: 1, p2: 2, p3: 3}; a pass that lands
+        # between two of its Allocates (the plugin's loop is busy elsewhere for a moment) repairs the first swaps
+        # before the later admissions, which then swap among themselves -- either way containers run on other GPUs
+        # than their pods were bound to, one per GPU
+        assert sorted(phys.values()) == [0, 1, 2, 3], phys
+        assert sum(phys[n] != cl.device_of(bound[n]) for n in names) >= 2, (phys, bound)
         st = await cl.agent_stats()
         assert st["faithful"] and st["mismatch"] >= 2, st
 
@@ -473,4 +478,79 @@ def test_physical_guard_waits_for_a_deleted_pods_container_when_no_gpu_has_room(
         assert got is not None and got.uid == "unew" and got.dev == 0
         assert plugin.stats.get("physical_guard_gone_waits", 0) >= 1
 
+    asyncio.run(go())
+
+
+def test_plugin_republishes_on_a_new_extender_epoch_and_counts_terminating_holders():
+    """a publishing plugin reads the extender's epoch and republishes the moment it changes (a new
+    leader knows nothing of what the old one was told); a standby answers /physical 503, never counted as delivered.
+    VERDICT r5 #1: the plugin's annotated view (where it may move a pod) counts terminating pods as the extender
+    does: charged until their objects are gone."""
+    import asyncio
+
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
+    from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin
+    from gpushare_scheduler_extender_amd.deviceplugin.reconcile import Reconciler
+    from gpushare_scheduler_extender_amd.extender.server import ExtenderRunner, ExtenderServer
+    from gpushare_scheduler_extender_amd.k8s.client import KubeClient
+    from gpushare_scheduler_extender_amd.k8s.objects import make_node
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+    from tests.fixtures.fakeapi import FakeApiServerRunner
+
+    async def go():
+        api = await FakeApiServerRunner().start()
+        c = KubeClient(api.url)
+        await c.create("nodes", make_node("n", 32, 2))
+        ext = await ExtenderRunner(ExtenderServer(KubeClient(api.url))).start()
+        plugin = GpuSharePlugin(c, "n", fake_devices("2x16GiB"), SHARED_GPU, socket_dir="/tmp/gsx-epoch-test",
+                                extender=f"http://127.0.0.1:{ext.port}")
+        plugin.reconciler = Reconciler(plugin, None)  # publishing (PodResources reconciled)
+        st = plugin.state
+        eng = ext.server.engine
+        try:
+            assert plugin.publishes_physical
+            for _ in range(200):
+                if eng.has_node("n"):
+                    break
+                await asyncio.sleep(0.01)
+
+            def pod(name, dev, deleting=False):
+                p = make_pod(name, 4, node="n", uid=f"u{name}", annotations={SHARED_GPU.annotation_idx: str(dev),
+                                                                             SHARED_GPU.annotation_assigned: "true"})
+                p["metadata"]["resourceVersion"] = "2" if deleting else "1"
+                if deleting:
+                    p["metadata"]["deletionTimestamp"] = "2026-01-01T00:00:00Z"
+                    p["status"]["phase"] = "Running"
+                st.observe(p)
+
+            pod("P", 0)
+            pod("Q", 1)
+            st.core.set_owners_reported(True)
+            st.record(st.pods["uQ"], ["g1-_-0"], 4, "", "aQ")
+            st.set_owner("aQ", "uP")  # P's container runs with Q's allocation on GPU 1
+            assert await plugin.check_epoch()  # first sight of the epoch: published
+            assert eng.node_unaccounted("n") == [0, 4]
+            n0 = plugin.stats["physical_published"]
+            assert await plugin.check_epoch() and plugin.stats["physical_published"] == n0  # same epoch: nothing
+            # a standby: /physical is refused and the epoch says "not leader"
+            eng.set_binds_enabled(False)
+            assert not await plugin.publish_physical(force=True)
+            assert not await plugin.check_epoch()
+            eng.set_binds_enabled(True)  # leader again: a new epoch
+            assert await plugin.check_epoch()
+            assert plugin.stats["physical_published"] == n0 + 1 and plugin.stats["epoch_changes"] >= 2
+            assert eng.node_unaccounted("n") == [0, 4]  # republished at once
+            # P is being deleted gracefully while its container stops: the extender charges P's annotated GPU 0
+            # until the object goes, and so does the plugin's annotated view
+            pod("P", 0, deleting=True)
+            assert st.core.terminating_dev("uP") == 0 and st.core.terminating_used(0) == 4
+            assert plugin._annotated_used(0) == 4 and "uP" not in st.pods
+            gone = make_pod("P", 4, node="n", uid="uP")
+            st.forget(gone)  # kubelet's grace-0 delete
+            assert st.core.terminating_used(0) == 0 and plugin._annotated_used(0) == 0
+        finally:
+            await ext.stop()
+            await ext.server.client.close()
+            await c.close()
+            await api.stop()
     asyncio.run(go())
