@@ -385,15 +385,17 @@ OPEN_LOOP_LATENCIES_MS = (1, 2, 5)
 OPEN_LOOP_RATES = (500, 1000, 2000, 4000, 8000, 16000)
 
 
-def open_loop(a, api_url, api_batch, E, profile, inspect_used) -> dict:
+def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats) -> dict:
     """Open-loop throughput under apiserver latency: pods arrive at a constant rate with many in
     flight -- no waves in lock-step -- and each is deleted as soon as it runs, so the node's room turns over.  Per
     apiserver latency the offered rate steps up until the stack stops keeping up (bound rate < 90 % of offered, or
     p99 arrival-to-bound over 100 ms): the knee.  Every pod's stages are timed by the native driver
     (native/engine/tracker.cc OpenLoop): create (the client's POST), bind (created -> bound: scheduler + extender),
-    admit (bound -> Running: kubelet + device plugin + runtime + Running patch), free (DELETE -> gone).  The stage
-    that grew most at the first rate that failed is named as the bound.  Pods of ``--open-loop-gib`` (4 GiB: 71 on
-    one MI355X) so that room is not what binds the rate.  Rank 0 only, untimed by the headline."""
+    admit (bound -> Running: kubelet + device plugin + runtime + Running patch), free (DELETE -> gone).  At the first
+    rate that failed the bound is named: when the scheduler found no room meanwhile (``room_waits``: its filter
+    found the node full and it retried), pods held their room too long -- the one of admit / free that grew most;
+    otherwise the one of create / bind / admit that grew most.  Pods of ``--open-loop-gib`` (1 GiB: 287 on one
+    MI355X), so that room binds only a stack whose pods sit in admission.  Rank 0 only, untimed by the headline."""
     from gpushare_scheduler_extender_amd.k8s.objects import make_pod
 
     rates = OPEN_LOOP_RATES if a.open_loop == "auto" else tuple(int(x) for x in a.open_loop.split(",") if x)
@@ -420,8 +422,10 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used) -> dict:
             run = f"r{k}"
             tmpl = make_pod("__NAME__", a.open_loop_gib, profile=profile, labels={"gsx-ol": run})
             del tmpl["metadata"]["uid"]
+            u0 = sched_stats().get("unschedulable", 0)
             res = E.open_loop_run({"server": api_url}, run, json.dumps(tmpl, separators=(",", ":")), float(rate),
                                   duration_s=a.open_loop_s, warm_s=0.3, drain_s=10.0)
+            room_waits = sched_stats().get("unschedulable", 0) - u0
             cleanup(run)
             pods = res["pods"]
             t0 = min(p[0] for p in pods if p[0] > 0)
@@ -442,6 +446,7 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used) -> dict:
                    "p50_e2e_ms": pctl([p[3] - p[0] for p in win if p[3] > 0], 50),
                    "stage_p50_ms": {k2: pctl(v, 50) for k2, v in st.items()},
                    "not_bound": sum(1 for p in pods if p[2] == 0), "failed": sum(1 for p in pods if p[6]),
+                   "room_waits": room_waits,
                    "create_errors": res["create_errors"], "delete_errors": res["delete_errors"]}
             ok = (row["bound_pods_per_s"] >= 0.9 * rate and (row["p99_bind_latency_ms"] or 1e9) <= 100.0
                   and row["not_bound"] == 0 and row["failed"] == 0)
@@ -457,7 +462,8 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used) -> dict:
                 continue
             # the stage whose median grew most against the lowest rate of this latency: the serial stage that binds
             growth = {s2: (row["stage_p50_ms"][s2] or 0.0) - (first["stage_p50_ms"][s2] or 0.0) for s2 in st}
-            out["bound_stage"][key] = max(growth, key=growth.get)
+            cands = ("admit", "free") if room_waits > 0 else ("create", "bind", "admit")
+            out["bound_stage"][key] = max(cands, key=growth.get) + (" (room held)" if room_waits > 0 else "")
             break
     set_latency(api_batch, 0)
     return out
@@ -595,7 +601,7 @@ def parse():
                     help="open-loop throughput rows after the timed region: 'auto' (the rate ladder "
                          f"{OPEN_LOOP_RATES} at {OPEN_LOOP_LATENCIES_MS} ms apiserver latency), a comma list of "
                          "rates, or 0 (off)")
-    ap.add_argument("--open-loop-gib", type=int, default=4, help="pod size of the open-loop rows")
+    ap.add_argument("--open-loop-gib", type=int, default=1, help="pod size of the open-loop rows")
     ap.add_argument("--open-loop-s", type=float, default=1.5, help="seconds of arrivals per open-loop rate")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank uses physical GPU 0 (a one-box rehearsal of the N-GPU launch): each rank advertises "
@@ -1182,7 +1188,10 @@ def main():
     ol = None
     if rank == 0 and a.open_loop not in ("", "0"):
         try:
-            ol = open_loop(a, api_url, api_batch, E, profile, inspect_used)
+            def sched_stats():
+                return json.loads(lt.run(sched_http.request("GET", "/v1/stats"), 30).body)
+
+            ol = open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats)
         except Exception as e:  # noqa: BLE001 - never costs the headline line
             ol = {"error": f"{type(e).__name__}: {e}"}
     if world > 1:

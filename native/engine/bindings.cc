@@ -914,10 +914,17 @@ class PyDpServer {
     srv_->watch_fd(efd_);
     tfd_ = ::timerfd_create(CLOCK_MONOTONIC, TFD_NONBLOCK | TFD_CLOEXEC);
     srv_->watch_fd(tfd_);
-    worker_ = std::thread([this] {
-      introspect::name_thread("dp-worker");
-      work();
-    });
+    // the ASSIGNED commits of early-answered Allocates are independent (one pod each): several in flight, so the
+    // node's admission rate is not capped at one commit per apiserver round trip (1 ms: 1,000 pods/s; the open-loop
+    // rows of bench.py found that bound).  Worker 0 also runs the synchronous patches, in order
+    int nw = 8;
+    if (const char* e = std::getenv("GSX_PLUGIN_COMMIT_THREADS")) nw = std::max(1, std::min(64, std::atoi(e)));
+    for (int i = 0; i < nw; ++i) {
+      workers_.emplace_back([this, i] {
+        introspect::name_thread("dp-worker");
+        work(i);
+      });
+    }
   }
   ~PyDpServer() {
     stop_serving();
@@ -1204,7 +1211,7 @@ class PyDpServer {
         pend->request = call.message;
         std::lock_guard<std::mutex> l(wmu_);
         todo_.push_back(std::move(pend));
-        if (!serving_.joinable()) wcv_.notify_one();  // the serving thread runs its patches itself
+        if (!serving_.joinable()) wcv_.notify_all();  // the serving thread runs its patches itself
       } else if (feed_r_ && why == kNoCandidate) {
         wait_for_pod(call.id, m, call.message);
       } else {
@@ -1429,7 +1436,7 @@ class PyDpServer {
           pend->request = w.message;
           std::lock_guard<std::mutex> l(wmu_);
           todo_.push_back(std::move(pend));
-          if (!serving_.joinable()) wcv_.notify_one();
+          if (!serving_.joinable()) wcv_.notify_all();
           continue;
         }
         if (why != kNoCandidate) {
@@ -1453,13 +1460,13 @@ class PyDpServer {
   // the ASSIGNED patches run here, never on the owner's event loop
   // Takes the synchronous patches (todo_) only while no serving thread runs them itself, and the early-answered
   // commits (todo_bg_) once their backoff (not_before) has passed.
-  void work() {
+  void work(int me) {
     for (;;) {
       std::unique_ptr<DpPending> p;
       {
         std::unique_lock<std::mutex> l(wmu_);
         for (;;) {
-          if ((!serving_on_ || stopping_) && !todo_.empty()) {
+          if (me == 0 && (!serving_on_ || stopping_) && !todo_.empty()) {
             p = std::move(todo_.front());
             todo_.pop_front();
             break;
@@ -1494,13 +1501,14 @@ class PyDpServer {
   }
 
   void stop_worker() {
-    if (!worker_.joinable()) return;
+    if (workers_.empty()) return;
     {
       std::lock_guard<std::mutex> l(wmu_);
       stopping_ = true;
     }
     wcv_.notify_all();
-    worker_.join();
+    for (auto& w : workers_) w.join();
+    workers_.clear();
   }
 
   void queue_patch(std::unique_ptr<DpPending> pend, uint64_t call, const std::string& message) {
@@ -1511,11 +1519,11 @@ class PyDpServer {
     std::lock_guard<std::mutex> l(wmu_);
     if (pend->answered) {
       todo_bg_.push_back(std::move(pend));
-      wcv_.notify_one();
+      wcv_.notify_all();  // any worker (worker 0 may be the one a synchronous patch needs)
       return;
     }
     todo_.push_back(std::move(pend));
-    if (!serving_.joinable()) wcv_.notify_one();  // the serving thread runs its patches itself
+    if (!serving_.joinable()) wcv_.notify_all();  // worker 0 takes it (the serving thread runs its patches itself)
   }
 
   void finish_patches() {
@@ -1556,7 +1564,7 @@ class PyDpServer {
   uint64_t waited_ = 0, feed_events_ = 0;
   double wait_s_ = 0, wait_max_s_ = 0;  // calls that waited for their pod's event: total / longest wait
   int tfd_ = -1;
-  std::thread worker_;
+  std::vector<std::thread> workers_;
   std::mutex wmu_;
   std::condition_variable wcv_;
   std::deque<std::unique_ptr<DpPending>> todo_, done_;

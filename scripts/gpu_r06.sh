@@ -17,10 +17,10 @@ for i in 1 2 3; do
   tail -1 $OUT/bench.$i.log > $OUT/bench.$i.json
   python -c "
 import json; d=json.load(open('$OUT/bench.$i.json'))
-print('bench', $i, d['value'], d['wave_pods_per_s'], round(max(w[2] for w in d['wave_ms_each']), 2), d.get('latency_sweep_pods_per_s'))"
+print('bench', $i, d['value'], d['wave_pods_per_s'], round(max(w[2] for w in d['wave_ms_each']), 2), d.get('latency_sweep_pods_per_s'), d.get('open_loop_knee_pods_per_s'), (d.get('open_loop') or {}).get('bound_stage'))"
 done
 if [ "${PROFILE:-1}" = "1" ]; then
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps 20 --warmup 5 --sweep 0 > $OUT/prof.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps 20 --warmup 5 --sweep 0 --open-loop 0 > $OUT/prof.log 2>&1
   rc=$?; [ $rc -eq 0 ] || { echo "rocprof rc=$rc"; tail -20 $OUT/prof.log; exit $rc; }
   find $OUT/prof -name "*kernel_stats.csv" | head -3
 fi
