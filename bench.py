@@ -618,6 +618,29 @@ def parse():
     return ap.parse_args()
 
 
+def rank_device(devs, phys: int, local_rank: int, use_gpu: bool, who: str = "rank"):
+    """The device a rank advertises: the one whose HIP ordinal is ``phys`` -- the GPU its HBM arena and kernels live on
+    (``torch.cuda.set_device(phys)``).  Device indices are HIP ordinals (libmxdev orders amdsmi's devices by their
+    hip_id), so this holds on platforms whose amdsmi order is not the HIP order (tests/test_device_topology.py).
+    Without a GPU: the fake inventory's entry.  The advertised index is the rank's (one GPU per rank)."""
+    if use_gpu:
+        mine = [d for d in devs if d.index == phys]
+        if not mine:
+            raise SystemExit(f"{who}: GPU {phys} not found")
+        dev = mine[0]
+    else:
+        dev = devs[local_rank % len(devs)]
+    dev.index = local_rank
+    return dev
+
+
+def node_inventory(devs, unit: str = "GiB") -> list[dict]:
+    """The node's device inventory annotation (what the device plugin publishes, plugin.py publish_node)."""
+    return [{"index": d.index, "bdf": d.bdf, "uuid": d.uuid, "units": d.units(unit), "total_bytes": d.total_bytes,
+             "share_bytes": d.share_bytes, "cu": d.cu_count, "xcc": d.xcc_count, "render": d.render_minor,
+             "card": d.card_minor, "partition": d.partition} for d in devs]
+
+
 def cpu_slots(world: int, runtime_cpu: str = "shared", apiserver_threads: int = 0) -> tuple[list[str], dict, int]:
     """The processes of a bench run on ``world`` GPUs and the CPUs each asks for (utils/cpuset.py plans them; with
     fewer CPUs than asked the plan is empty and nothing is pinned).  Returns (names, widths, apiserver threads)."""
@@ -807,14 +830,7 @@ def main():
 
     # ---- this rank's GPU
     backend, devs = discover("fake" if not use_gpu else a.devices)
-    if use_gpu:
-        mine = [d for d in devs if d.index == phys]
-        if not mine:
-            raise SystemExit(f"rank {rank}: GPU {phys} not found ({backend})")
-        dev = mine[0]
-    else:
-        dev = devs[local_rank % len(devs)]
-    dev.index = local_rank
+    dev = rank_device(devs, phys, local_rank, use_gpu, f"rank {rank} ({backend})")
     unit = "GiB"
     pod_bytes = a.pod_gib * UNITS[unit]
     arena = a.pods_per_gpu * pod_bytes
@@ -849,10 +865,7 @@ def main():
         c = KubeClient(api_url)
         devs_ = [Device(**d) for d, _ in all_devs]
         totals = [d.units(unit) for d in devs_]
-        inv = [{"index": d.index, "bdf": d.bdf, "uuid": d.uuid, "units": d.units(unit), "total_bytes": d.total_bytes,
-                "share_bytes": d.share_bytes, "cu": d.cu_count, "xcc": d.xcc_count, "render": d.render_minor,
-                "card": d.card_minor, "partition": d.partition}
-               for d in devs_]
+        inv = node_inventory(devs_, unit)
         node = make_node(NODE, sum(totals), len(totals), profile=profile, device_totals=totals,
                          annotations={NODE_DEVICE_INFO_ANNOTATION: json.dumps(inv),
                                       # as the device plugin publishes it: its matcher is landing-ordered

@@ -148,9 +148,15 @@ def build_fakeapi(force: bool = False, verbose: bool = False) -> Path:
 def build_mxdev(force: bool = False, verbose: bool = False) -> Path:
     src = NATIVE / "mxdev"
     srcs = sorted(src.glob("*.cc"))
-    srcs = [s for s in srcs if not s.name.endswith("_test.cc")]
+    srcs = [s for s in srcs if not s.name.endswith("_test.cc") and not s.name.startswith("fake_")]
     headers = sorted(src.glob("*.h"))
     out = OUT / f"_mxdev{EXT}"
+    # the test-only stand-in for libamd_smi.so (a shuffled amdsmi/HIP topology, tests/test_device_topology.py)
+    fake = ROOT / "build" / "libfake_amdsmi.so"
+    if force or _newer(fake, [src / "fake_amdsmi.cc"]):
+        fake.parent.mkdir(parents=True, exist_ok=True)
+        _run(["g++", *CXXFLAGS, "-I" + str(ROCM / "include"), "-shared", str(src / "fake_amdsmi.cc"), "-o",
+              str(fake)], verbose)
     if _current(out, srcs, [*headers, *sorted((NATIVE / "engine").glob("*.h"))], force):
         return out
     flags = [*CXXFLAGS, *_pybind_includes(), "-I" + str(src), "-I" + str(ROCM / "include"),

@@ -58,10 +58,13 @@ struct Api {
   }
 
   bool load(std::string* err) {
+    // GSX_AMDSMI_LIB: another amdsmi library first (tests load native/mxdev/fake_amdsmi.cc, a shuffled topology)
+    const char* over = std::getenv("GSX_AMDSMI_LIB");
+    if (over && *over) h = dlopen(over, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
     const char* cands[] = {"/opt/rocm/lib/libamd_smi.so", "libamd_smi.so.26", "libamd_smi.so"};
     for (const char* c : cands) {
-      h = dlopen(c, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
       if (h) break;
+      h = dlopen(c, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
     }
     if (!h) {
       *err = std::string("dlopen libamd_smi failed: ") + dlerror();
