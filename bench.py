@@ -385,7 +385,59 @@ OPEN_LOOP_LATENCIES_MS = (1, 2, 5)
 OPEN_LOOP_RATES = (500, 1000, 2000, 4000, 8000, 16000)
 
 
-def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats) -> dict:
+def _grpc_delta(p0, p1) -> dict | None:
+    g0, g1 = (p0 or {}).get("grpc") or {}, (p1 or {}).get("grpc") or {}
+    if not g1:
+        return None
+    out = {k: g1.get(k, 0) - g0.get(k, 0) for k in ("fast_allocate", "slow_allocate", "waited", "guard_by_ids",
+                                                      "patch_failures")}
+    out["wait_ms_total"] = round((g1.get("wait_ms") or {}).get("total", 0.0) - (g0.get("wait_ms") or {}).get("total", 0.0), 3)
+    out["handler_us_allocate"] = (g1.get("handler_us") or {}).get("allocate")
+    out["early_answer_backlog"] = g1.get("early_answer_backlog")
+    out["allocate_phases_us"] = g1.get("allocate_phases_us")  # cumulative means
+    out["last_slow_reason"] = g1.get("last_slow_reason")
+    return out
+
+
+def _allowed_cpus() -> list[int]:
+    """The CPUs this container may use (its cgroup cpuset), whatever this process is pinned to now."""
+    for path in ("/sys/fs/cgroup/cpuset.cpus.effective", "/sys/fs/cgroup/cpuset/cpuset.effective_cpus"):
+        try:
+            with open(path) as f:
+                txt = f.read().strip()
+        except OSError:
+            continue
+        out = []
+        for part in txt.split(","):
+            if "-" in part:
+                lo, hi = part.split("-")
+                out.extend(range(int(lo), int(hi) + 1))
+            elif part:
+                out.append(int(part))
+        if out:
+            return out
+    return list(range(os.cpu_count() or 1))
+
+
+def _agent_delta(s0, s1) -> dict | None:
+    """Per-admission means (ms) of the node agent's steps between two /v1/stats reads."""
+    if not s0 or not s1 or "mean_ms" not in s1:
+        return None
+    n0, n1 = s0.get("admitted", 0), s1.get("admitted", 0)
+    c0, c1 = (s0.get("plugin_calls_mean_ms") or {}).get("n", 0), (s1.get("plugin_calls_mean_ms") or {}).get("n", 0)
+    out = {}
+    if n1 > n0:
+        for k in ("queue", "runtime", "running_patch"):
+            out[k] = round((s1["mean_ms"][k] * n1 - s0["mean_ms"][k] * n0) / (n1 - n0), 4)
+    if c1 > c0:
+        for k in ("slot_wait", "get_preferred", "allocate"):
+            out["plugin_" + k] = round((s1["plugin_calls_mean_ms"][k] * c1 - s0["plugin_calls_mean_ms"][k] * c0)
+                                       / (c1 - c0), 4)
+    out["admitted"] = n1 - n0
+    return out
+
+
+def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats, agent_stats=None) -> dict:
     """Open-loop throughput under apiserver latency: pods arrive at a constant rate with many in
     flight -- no waves in lock-step -- and each is deleted as soon as it runs, so the node's room turns over.  Per
     apiserver latency the offered rate steps up until the stack stops keeping up (bound rate < 90 % of offered, or
@@ -423,9 +475,13 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats) -> d
             tmpl = make_pod("__NAME__", a.open_loop_gib, profile=profile, labels={"gsx-ol": run})
             del tmpl["metadata"]["uid"]
             u0 = sched_stats().get("unschedulable", 0)
+            na0 = agent_stats() if agent_stats else None
+            pg0 = _plugin_debug(E, (na0 or {}).get("plugin_debug"))
             res = E.open_loop_run({"server": api_url}, run, json.dumps(tmpl, separators=(",", ":")), float(rate),
                                   duration_s=a.open_loop_s, warm_s=0.3, drain_s=10.0)
             room_waits = sched_stats().get("unschedulable", 0) - u0
+            na1 = agent_stats() if agent_stats else None
+            pg1 = _plugin_debug(E, (na1 or {}).get("plugin_debug"))
             cleanup(run)
             pods = res["pods"]
             t0 = min(p[0] for p in pods if p[0] > 0)
@@ -447,6 +503,12 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats) -> d
                    "stage_p50_ms": {k2: pctl(v, 50) for k2, v in st.items()},
                    "not_bound": sum(1 for p in pods if p[2] == 0), "failed": sum(1 for p in pods if p[6]),
                    "room_waits": room_waits,
+                   # kubelet stand-in over the row: mean ms per admission of its serial steps (the queue wait, the
+                   # plugin's Allocate as kubelet sees it) and of the pod workers' (runtime, Running patch)
+                   "kubelet_mean_ms": _agent_delta(na0, na1),
+                   # the plugin's gRPC endpoint over the row: Allocates on its native fast path / handed to Python,
+                   # calls that waited for their pod's event, and how long in all
+                   "plugin_grpc": _grpc_delta(pg0, pg1),
                    "create_errors": res["create_errors"], "delete_errors": res["delete_errors"]}
             ok = (row["bound_pods_per_s"] >= 0.9 * rate and (row["p99_bind_latency_ms"] or 1e9) <= 100.0
                   and row["not_bound"] == 0 and row["failed"] == 0)
@@ -1204,7 +1266,29 @@ def main():
             def sched_stats():
                 return json.loads(lt.run(sched_http.request("GET", "/v1/stats"), 30).body)
 
-            ol = open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats)
+            na_client = None
+            if a.agent == "node":
+                na_client = E.BatchClient({"server": next(c.url for c in children if c.name == "node-agent")})
+
+            def na_stats():
+                st_, body_ = na_client.run([("GET", "/v1/stats", b"")], 1)[0]
+                return json.loads(body_) if st_ == 200 else None
+
+            # the open-loop driver (its creators, deleters and watch are threads of this process) is a load
+            # generator, not the cluster: it gets every allowed CPU no other process of the run is pinned to, not
+            # rank 0's one (on one CPU its 32 threads throttled the arrivals, profiles/r06_first/)
+            own = set(os.sched_getaffinity(0))
+            others = {c for k, v in cpu_plan.items() if k != f"rank{rank}" for c in (v or [])}
+            try:
+                spare = set(_allowed_cpus()) - others
+                if len(spare) > len(own):
+                    os.sched_setaffinity(0, spare)
+                ol = open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats,
+                               na_stats if na_client is not None else None)
+                if isinstance(ol, dict):
+                    ol["driver_cpus"] = len(os.sched_getaffinity(0))
+            finally:
+                os.sched_setaffinity(0, own)
         except Exception as e:  # noqa: BLE001 - never costs the headline line
             ol = {"error": f"{type(e).__name__}: {e}"}
     if world > 1:
