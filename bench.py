@@ -525,7 +525,15 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats, agen
             # the stage whose median grew most against the lowest rate of this latency: the serial stage that binds
             growth = {s2: (row["stage_p50_ms"][s2] or 0.0) - (first["stage_p50_ms"][s2] or 0.0) for s2 in st}
             cands = ("admit", "free") if room_waits > 0 else ("create", "bind", "admit")
-            out["bound_stage"][key] = max(cands, key=growth.get) + (" (room held)" if room_waits > 0 else "")
+            stage = max(cands, key=growth.get)
+            km, k0 = row.get("kubelet_mean_ms") or {}, first.get("kubelet_mean_ms") or {}
+            if stage == "admit" and km:
+                # which step of an admission grew: the serial queue, the plugin's Allocate (kubelet's serial call),
+                # the runtime (the container start, here the HBM stand-in) or the Running status patch
+                sub = {k2: km.get(k2, 0.0) - k0.get(k2, 0.0) for k2 in ("queue", "plugin_allocate", "runtime",
+                                                                       "running_patch")}
+                stage += "/" + max(sub, key=sub.get)
+            out["bound_stage"][key] = stage + (" (room held)" if room_waits > 0 else "")
             break
     set_latency(api_batch, 0)
     return out
@@ -1274,6 +1282,10 @@ def main():
                 st_, body_ = na_client.run([("GET", "/v1/stats", b"")], 1)[0]
                 return json.loads(body_) if st_ == 200 else None
 
+            def na_verify(on: bool):
+                if na_client is not None:
+                    na_client.run([("POST", "/v1/config", json.dumps({"verify": on}).encode())], 1)
+
             # the open-loop driver (its creators, deleters and watch are threads of this process) is a load
             # generator, not the cluster: it gets every allowed CPU no other process of the run is pinned to, not
             # rank 0's one (on one CPU its 32 threads throttled the arrivals, profiles/r06_first/)
@@ -1283,11 +1295,17 @@ def main():
                 spare = set(_allowed_cpus()) - others
                 if len(spare) > len(own):
                     os.sched_setaffinity(0, spare)
+                # each admission stamps and verifies its own HBM slice only: with hundreds of pods resident the
+                # stand-in runtime's check of every resident slice per admission bounded the rows (runtime 60-150 ms
+                # per admission at the knee, profiles/r06_ol/), and it is the harness, not the stack under test
+                na_verify(False)
                 ol = open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats,
                                na_stats if na_client is not None else None)
                 if isinstance(ol, dict):
                     ol["driver_cpus"] = len(os.sched_getaffinity(0))
+                    ol["runtime_verify"] = "own slice"
             finally:
+                na_verify(True)
                 os.sched_setaffinity(0, own)
         except Exception as e:  # noqa: BLE001 - never costs the headline line
             ol = {"error": f"{type(e).__name__}: {e}"}

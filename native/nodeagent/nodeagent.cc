@@ -330,6 +330,18 @@ class Agent {
       rep.body = b;
       return rep;
     }
+    if (req.method == "POST" && path == "/v1/config") {
+      // {"verify": bool}: whether an admission verifies every resident slice of its GPU (default) or only its own
+      // (bench.py's open-loop rows: hundreds of resident pods, the stand-in runtime's check is not the stack under test)
+      json::Doc d;
+      std::string e;
+      if (d.parse(req.body, &e)) {
+        int64_t v = d.find(0, "verify");
+        if (v >= 0) verify_ = d.at(static_cast<uint32_t>(v)).type == json::T::True;
+      }
+      rep.body = std::string("{\"verify\":") + (verify_ ? "true" : "false") + "}";
+      return rep;
+    }
     const std::string_view pre = "/v1/allocations/";
     if (req.method == "GET" && path.substr(0, pre.size()) == pre) {
       auto it = allocations_.find(std::string(path.substr(pre.size())));
@@ -1202,7 +1214,7 @@ class Agent {
   Profile p_;
   int64_t unit_;
   int nworkers_;
-  bool verify_;
+  bool verify_;  // (mu_) POST /v1/config
   bool serial_admission_ = false;  // set_serial_admission
   ApiClient api_;
   std::map<int, Device> devices_;
