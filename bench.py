@@ -1284,7 +1284,10 @@ def main():
 
             def na_verify(on: bool):
                 if na_client is not None:
-                    na_client.run([("POST", "/v1/config", json.dumps({"verify": on}).encode())], 1)
+                    # and 64 pod workers for the open loop: each blocks on the runtime call and the Running patch
+                    # (one apiserver round trip), and kubelet's status manager does not hold a pod worker for it
+                    cfg = {"verify": on, **({} if on else {"workers": 64})}
+                    na_client.run([("POST", "/v1/config", json.dumps(cfg).encode())], 1)
 
             # the open-loop driver (its creators, deleters and watch are threads of this process) is a load
             # generator, not the cluster: it gets every allowed CPU no other process of the run is pinned to, not

@@ -333,13 +333,27 @@ class Agent {
     if (req.method == "POST" && path == "/v1/config") {
       // {"verify": bool}: whether an admission verifies every resident slice of its GPU (default) or only its own
       // (bench.py's open-loop rows: hundreds of resident pods, the stand-in runtime's check is not the stack under test)
+      // {"workers": n}: at least n pod workers (kubelet's pod workers are one goroutine per pod; these block on the
+      // runtime call and the Running patch, so at 5 ms per apiserver call 16 of them start ~3k pods/s at most)
       json::Doc d;
       std::string e;
       if (d.parse(req.body, &e)) {
         int64_t v = d.find(0, "verify");
         if (v >= 0) verify_ = d.at(static_cast<uint32_t>(v)).type == json::T::True;
+        int64_t w = d.find(0, "workers");
+        int64_t nw = 0;
+        if (w >= 0 && d.as_int(static_cast<uint32_t>(w), &nw)) {
+          nw = std::min<int64_t>(nw, 256);
+          while (static_cast<int64_t>(workers_.size()) < nw && !stop_) {
+            workers_.emplace_back([this] {
+              introspect::name_thread("na-worker");
+              worker();
+            });
+          }
+        }
       }
-      rep.body = std::string("{\"verify\":") + (verify_ ? "true" : "false") + "}";
+      rep.body = std::string("{\"verify\":") + (verify_ ? "true" : "false") + ",\"workers\":" +
+                 std::to_string(workers_.size()) + "}";
       return rep;
     }
     const std::string_view pre = "/v1/allocations/";
