@@ -382,7 +382,11 @@ def latency_sweep(a, children, api_url, api_batch, runner: WaveRunner, inspect_u
 
 
 OPEN_LOOP_LATENCIES_MS = (1, 2, 5)
-OPEN_LOOP_RATES = (500, 1000, 2000, 4000, 8000, 16000)
+# the pods' spec.terminationGracePeriodSeconds, as the apiserver's defaulting writes it into every pod: deleting one
+# is a graceful deletion its kubelet (the node agent) ends once the containers stopped.  (Deleted outright, a pod's
+# containers could outlive the object by their grace -- the device plugin keeps such a pod's share counted that long.)
+TERM_GRACE_S = 30
+OPEN_LOOP_RATES = (500, 1000, 2000, 4000, 8000, 16000, 32000)
 
 
 def _grpc_delta(p0, p1) -> dict | None:
@@ -451,7 +455,8 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats, agen
     from gpushare_scheduler_extender_amd.k8s.objects import make_pod
 
     rates = OPEN_LOOP_RATES if a.open_loop == "auto" else tuple(int(x) for x in a.open_loop.split(",") if x)
-    out = {"pod_gib": a.open_loop_gib, "duration_s": a.open_loop_s, "warm_s": 0.3, "hold_s": 0.0, "rows": [],
+    out = {"pod_gib": a.open_loop_gib, "duration_s": a.open_loop_s, "warm_s": 0.3, "hold_s": 0.0,
+           "creators": a.open_loop_creators, "rows": [],
            "knee_pods_per_s": {}, "max_sustained_pods_per_s": {}, "bound_stage": {}}
 
     def pctl(xs, q):
@@ -474,11 +479,13 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats, agen
             run = f"r{k}"
             tmpl = make_pod("__NAME__", a.open_loop_gib, profile=profile, labels={"gsx-ol": run})
             del tmpl["metadata"]["uid"]
+            tmpl["spec"]["terminationGracePeriodSeconds"] = TERM_GRACE_S
             u0 = sched_stats().get("unschedulable", 0)
             na0 = agent_stats() if agent_stats else None
             pg0 = _plugin_debug(E, (na0 or {}).get("plugin_debug"))
             res = E.open_loop_run({"server": api_url}, run, json.dumps(tmpl, separators=(",", ":")), float(rate),
-                                  duration_s=a.open_loop_s, warm_s=0.3, drain_s=10.0)
+                                  duration_s=a.open_loop_s, warm_s=0.3, drain_s=10.0,
+                                  creators=a.open_loop_creators, deleters=a.open_loop_creators)
             room_waits = sched_stats().get("unschedulable", 0) - u0
             na1 = agent_stats() if agent_stats else None
             pg1 = _plugin_debug(E, (na1 or {}).get("plugin_debug"))
@@ -501,6 +508,7 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats, agen
                    "p50_admit_latency_ms": pctl(st["admit"], 50), "p99_admit_latency_ms": pctl(st["admit"], 99),
                    "p50_e2e_ms": pctl([p[3] - p[0] for p in win if p[3] > 0], 50),
                    "stage_p50_ms": {k2: pctl(v, 50) for k2, v in st.items()},
+                   "stage_p99_ms": {k2: pctl(v, 99) for k2, v in st.items()},
                    "not_bound": sum(1 for p in pods if p[2] == 0), "failed": sum(1 for p in pods if p[6]),
                    "room_waits": room_waits,
                    # kubelet stand-in over the row: mean ms per admission of its serial steps (the queue wait, the
@@ -523,7 +531,9 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats, agen
                 out["knee_pods_per_s"][key] = rate
                 continue
             # the stage whose median grew most against the lowest rate of this latency: the serial stage that binds
-            growth = {s2: (row["stage_p50_ms"][s2] or 0.0) - (first["stage_p50_ms"][s2] or 0.0) for s2 in st}
+            # (the bound rate kept up but its p99 did not: the stage whose p99 grew most -- a tail, not a queue)
+            q = "stage_p50_ms" if row["bound_pods_per_s"] < 0.9 * rate else "stage_p99_ms"
+            growth = {s2: (row[q][s2] or 0.0) - (first[q][s2] or 0.0) for s2 in st}
             cands = ("admit", "free") if room_waits > 0 else ("create", "bind", "admit")
             stage = max(cands, key=growth.get)
             km, k0 = row.get("kubelet_mean_ms") or {}, first.get("kubelet_mean_ms") or {}
@@ -533,6 +543,11 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats, agen
                 sub = {k2: km.get(k2, 0.0) - k0.get(k2, 0.0) for k2 in ("queue", "plugin_allocate", "runtime",
                                                                        "running_patch")}
                 stage += "/" + max(sub, key=sub.get)
+            if stage == "create" and rate >= 0.8 * a.open_loop_creators * 1e3 / ms:
+                # the driver's own creators (each a POST at the injected latency): not the product's bound
+                stage += f" (driver: {a.open_loop_creators} creators at {ms} ms)"
+            elif q == "stage_p99_ms":
+                stage += " (p99)"
             out["bound_stage"][key] = stage + (" (room held)" if room_waits > 0 else "")
             break
     set_latency(api_batch, 0)
@@ -673,6 +688,9 @@ def parse():
                          "rates, or 0 (off)")
     ap.add_argument("--open-loop-gib", type=int, default=1, help="pod size of the open-loop rows")
     ap.add_argument("--open-loop-s", type=float, default=1.5, help="seconds of arrivals per open-loop rate")
+    ap.add_argument("--open-loop-creators", type=int, default=64,
+                    help="open-loop driver threads creating (and as many deleting) pods: at apiserver latency L they "
+                         "offer at most creators / L pods/s (16 made the 2 ms row's knee the driver's own)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="every rank uses physical GPU 0 (a one-box rehearsal of the N-GPU launch): each rank advertises "
                          "a logical device sized for its wave (pods-per-gpu x pod-gib plus half a pod) and carves its "
@@ -992,6 +1010,7 @@ def main():
                 except TimeoutError:
                     pass
         pod_tmpl = make_pod("__NAME__", a.pod_gib, profile=profile, labels={"gsx-wave": "__STEP__"})
+        pod_tmpl["spec"]["terminationGracePeriodSeconds"] = TERM_GRACE_S
         del pod_tmpl["metadata"]["uid"]  # the apiserver assigns one per pod
         pod_tmpl = json.dumps(pod_tmpl, separators=(",", ":"))
     from gpushare_scheduler_extender_amd.utils.gctune import tune
@@ -1086,7 +1105,10 @@ def main():
         if st != 200:
             raise RuntimeError(f"delete collection failed: {st} {b[:200]!r}")
         t_del = time.perf_counter()
-        err = tracker.wait(keys, E.TRACK_GONE, 120)
+        # the wave's pods are deleted gracefully (TERM_GRACE_S): the node agent stops each pod's containers, reports
+        # the terminal phase -- which frees its share in the extender -- and then deletes the object.  The next wave
+        # needs the room, not the old objects gone
+        err = tracker.wait(keys, E.TRACK_STOPPED, 120)
         if err:
             raise RuntimeError(err)
         t_gone = time.perf_counter()
@@ -1375,7 +1397,7 @@ def main():
             # the load generator's creates of one wave (every POST answered)
             "create_ms_mean": round(1e3 * statistics.mean(s["t_created"] for s in step_stats), 3),
             "teardown_ms_mean": {k: round(1e3 * statistics.mean(s["teardown"][i] for s in step_stats), 3)
-                                 for i, k in enumerate(("inspect", "delete_call", "gone_seen", "ledger_empty"))},
+                                 for i, k in enumerate(("inspect", "delete_call", "stopped_seen", "ledger_empty"))},
             "wave_ms_max": {k: round(1e3 * max(s[t] for s in step_stats), 3)
                             for k, t in (("bound", "t_bound"), ("running", "t_run"), ("total", "t_total"))},
             # every timed wave: [bound, running, total] ms (where a slow wave lost its time)

@@ -788,8 +788,13 @@ class GpuSharePlugin:
                 except (ApiError, OSError) as e:
                     if cus and not had_cus:
                         cp.release(rec.uid)
-                    # a conflict, a 5xx, or a 429 the client's own Retry-After retries did not get through
-                    transient = not isinstance(e, ApiError) or e.transient
+                    # a conflict, a 5xx, or a 429 the client's own Retry-After retries did not get through; or the
+                    # matched pod is gone (deleted after this view matched it): kubelet's pod is another one, so
+                    # re-match rather than fail it (tests/interleave.py: swap-graceful seed 132)
+                    gone = isinstance(e, ApiError) and e.not_found
+                    if gone:
+                        self.state.forget(rec.obj)
+                    transient = not isinstance(e, ApiError) or e.transient or gone
                     if not transient or attempt == ALLOCATE_ATTEMPTS - 1:
                         raise AllocateError(f"marking {rec.key} assigned failed: {e}") from e
                     self.stats["allocate_retries"] += 1
@@ -817,10 +822,12 @@ class GpuSharePlugin:
         return self.state.core.physical_used(dev)
 
     def _gone_used(self, dev: int) -> int:
-        """Units of the Allocate records on ``dev`` held by containers of deleted pods that kubelet still lists."""
+        """Units on ``dev`` held by containers of deleted pods: records kubelet still lists, and the allocations of
+        force-deleted pods that linger for their termination grace (AllocState::deleted)."""
         from .reconcile import GONE  # noqa: PLC0415 - only with a reconciler, as the guard itself
 
-        return sum(r.units for r in self.state.records.values() if r.dev == dev and r.owner.startswith(GONE))
+        return (sum(r.units for r in self.state.records.values() if r.dev == dev and r.owner.startswith(GONE))
+                + self.state.core.lingering(dev))
 
     def _annotated_used(self, dev: int, skip: str = "") -> int:
         """Units the pod annotations put on ``dev`` (what the extender's ledger accounts): the live pods, and the
@@ -1023,15 +1030,16 @@ class GpuSharePlugin:
     def unaccounted(self) -> list[int] | None:
         """Per GPU, the units kubelet's containers hold there that the annotations do not charge there: a record
         kubelet reports held by another, live pod than the one it was built for, and that pod is annotated with
-        another GPU (a swap the exchange has not repaired).
-        None when every container is charged where it runs (the extender then uses the annotations alone), and
-        always on a one-GPU node: whoever holds an allocation there is annotated with that GPU too."""
-        if len(self.units) < 2:
+        another GPU (a swap the exchange has not repaired); and what the containers of force-deleted pods hold
+        while they linger.  None when every container is charged where it runs (the extender then uses the
+        annotations alone).  On a one-GPU node only lingering counts: whoever holds an allocation there is annotated
+        with that GPU too."""
+        if not self.units:
             return None
         pods = self.state.pods
         out = [0] * (max(self.units) + 1)
         found = False
-        for r in self.state.records.values():
+        for r in (self.state.records.values() if len(self.units) > 1 else ()):
             if not 0 <= r.dev < len(out) or not r.owner or r.owner == r.uid:
                 # not reported by kubelet yet, or held by the pod it was built for: the annotations charge it (a
                 # pod deleted before the first report: its container is stopping, as the extender assumes).  (Also
@@ -1041,9 +1049,16 @@ class GpuSharePlugin:
                 continue
             p = None if r.owner.startswith("~") else pods.get(r.owner)
             # a holder that is gone: its container has stopped (kubelet removes a gracefully deleted pod's object only
-            # then) or is stopping (a force delete; the physical guard waits for it)
+            # then) or is stopping (a force delete: counted below while it lingers)
             if p is not None and not p.complete and p.dev != r.dev:
                 out[r.dev] += r.units
+                found = True
+        # force-deleted pods' containers, given their termination grace: the extender freed their share when the
+        # objects went, kubelet no longer lists them, but they may still hold the GPU (AllocState::deleted)
+        for d in range(len(out)):
+            n = self.state.core.lingering(d)
+            if n:
+                out[d] += n
                 found = True
         return out if found else None
 

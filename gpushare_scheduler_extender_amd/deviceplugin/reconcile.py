@@ -454,6 +454,12 @@ class Reconciler:
             except ValueError:
                 want = {}
             q = self.state.pods.get(want.get("uid", ""))
+            if q is not None and q.assigned == "true" and want.get("assigned") != "true":
+                # Q was served an Allocate since step 1 was planned (its ASSIGNED is that Allocate's commit now):
+                # the payload's "not served" is stale, and re-applying it would make a running pod an Allocate
+                # candidate again (tests/interleave.py found it: swap-graceful seed 25).  Whatever GPU Q's
+                # container got, the next pass compares it with Q's annotation (a drift repair)
+                q = None
             if q is not None and fields(q) != {k: want.get(k) for k in ("idx", "assigned", "cu_mask")}:
                 if not await self._patch(q, self._ann(want), partner=p.uid):
                     continue

@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import json
 import logging
+import time
 from collections.abc import Mapping
 from dataclasses import dataclass, field
 
@@ -279,6 +280,8 @@ class AllocationState:
         ap.assigned, ap.complete, ap.cu_count, ap.cu_mask = rec.assigned, rec.complete, rec.cu_count, rec.cu_mask
         ap.hold_idx, ap.hold_partner = rec.hold_idx, rec.hold_partner
         ap.terminating = bool(podutil.meta(pod).get("deletionTimestamp")) and not podutil.is_terminal(pod)
+        tg = (pod.get("spec") or {}).get("terminationGracePeriodSeconds")
+        ap.term_grace_s = float(tg) if isinstance(tg, (int, float)) and tg >= 0 else 0.0
         try:
             ap.dev_total = int(podutil.annotations(pod).get(self.profile.annotation_dev, "-1") or -1)
         except ValueError:
@@ -298,11 +301,12 @@ class AllocationState:
 
     def forget(self, pod: dict) -> None:
         """A deleted pod (watch DELETE or gone from a re-list): released and remembered (AllocState::deleted), so a
-        copy of it another feed still delivers cannot bring it back."""
+        copy of it another feed still delivers cannot bring it back.  Deleted while live here (a force delete), what
+        its containers hold lingers on their GPUs for their termination grace."""
         uid = podutil.meta(pod).get("uid", "")
         if not uid:
             return
-        self.core.deleted(uid)
+        self.core.deleted(uid, time.time())
         self._recs.pop(uid, None)
         self._flush()
 
@@ -312,7 +316,7 @@ class AllocationState:
         for p in pods:
             self.observe(p)
             seen.append(podutil.meta(p).get("uid", ""))
-        self.core.resync(seen)
+        self.core.resync(seen, time.time())
         self._prune()
 
     def holders(self) -> set[str]:

@@ -187,6 +187,9 @@ bool parse_alloc_pod(const json::Doc& d, uint32_t pod, const Profile& p, AllocPo
   int64_t gp = d.path(pod, {"metadata", "deletionGracePeriodSeconds"});
   int64_t gv = -1;
   out->grace_s = (gp >= 0 && d.as_int(static_cast<uint32_t>(gp), &gv)) ? static_cast<double>(gv) : -1.0;
+  int64_t tg = d.path(pod, {"spec", "terminationGracePeriodSeconds"});
+  int64_t tv = 0;
+  out->term_grace_s = (tg >= 0 && d.as_int(static_cast<uint32_t>(tg), &tv) && tv >= 0) ? static_cast<double>(tv) : 0.0;
   out->cu_mask = v.cu_mask;
   out->hold_idx = v.hold_idx;
   out->assigned.clear();
@@ -345,10 +348,48 @@ void AllocState::tombstone(const std::string& uid) {
   gone_order_.emplace_back(now, uid);
 }
 
-void AllocState::deleted(const std::string& uid) {
+void AllocState::deleted(const std::string& uid, double now) {
+  force_gone(uid, now);
   tombstone(uid);
   release(uid);
   terminating_.erase(uid);
+}
+
+void AllocState::force_gone(const std::string& uid, double now) {
+  auto p = pods_.find(uid);
+  if (p != pods_.end() && owners_known()) {
+    // live until now: a force delete.  Its containers (the entries it holds, or was built for and nobody else was
+    // reported holding) keep their GPU share until kubelet has killed them: their termination grace from now
+    if (now < 0) now = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+    const double until = now + std::min(std::max(p->second.term_grace_s, 0.0), 600.0) + kLingerSlackS;
+    forced_[uid] = until;
+    forced_["~" + p->second.key] = until;  // the reconciler's name for a holder it no longer knows (reconcile.py GONE)
+    std::vector<std::string> keys;
+    for (const auto& kv : records_) {
+      const AllocRecord& r = kv.second;
+      if (!r.ids.empty() && (r.owner == uid || (r.owner.empty() && r.uid == uid))) keys.push_back(id_key(r.ids));
+    }
+    for (auto h = held_.begin(); h != held_.end(); ++h) {
+      if (h->second.owner == uid) keys.push_back(h->first);
+    }
+    for (const auto& k : keys) {
+      auto h = held_.find(k);
+      if (h == held_.end()) continue;
+      linger(h->second, until);
+      unhold(h);
+    }
+  }
+}
+
+double AllocState::ghost_until(const Held& h) const {
+  if (!h.owner.empty()) {
+    auto f = forced_.find(h.owner);
+    return f == forced_.end() ? 0.0 : f->second;
+  }
+  // never reported: kubelet may have given the IDs to any pod force-deleted before its admission
+  double until = 0;
+  for (const auto& kv : forced_) until = std::max(until, kv.second);
+  return until;
 }
 
 int64_t AllocState::terminating_used(int64_t dev) const {
@@ -376,9 +417,11 @@ std::vector<std::string> AllocState::holders() const {
   return std::vector<std::string>(out.begin(), out.end());
 }
 
-void AllocState::resync(const std::unordered_set<std::string>& live) {
+void AllocState::resync(const std::unordered_set<std::string>& live, double now) {
   for (const auto& uid : holders()) {
-    if (!live.count(uid)) release(uid);
+    if (live.count(uid)) continue;
+    force_gone(uid, now);  // gone while live here: deleted outright (not tombstoned: a LIST may lag a watch)
+    release(uid);
   }
   for (auto it = terminating_.begin(); it != terminating_.end();) {
     if (!live.count(it->first)) {
@@ -519,7 +562,7 @@ void AllocState::add_record(AllocRecord r) {
   if (!r.ids.empty()) by_ids_[key] = r.aid;
   std::string aid = r.aid;
   // a restored record: its allocation is held until kubelet's report says otherwise
-  if (!r.ids.empty() && !held_.count(key)) hold(key, Held{r.dev, r.units, r.t, r.uid, r.on_gpu, r.cu_mask});
+  if (!r.ids.empty() && !held_.count(key)) hold(key, Held{r.dev, r.units, r.t, r.uid, r.on_gpu, r.cu_mask, r.owner});
   records_.insert_or_assign(aid, std::move(r));
 }
 
@@ -535,9 +578,33 @@ std::string AllocState::id_key(const std::vector<std::string>& sorted_ids) {
   return k;
 }
 
+void AllocState::linger(const Held& h, double until) {
+  if (h.dev < 0 || h.units <= 0) return;
+  linger_.push_back(Linger{h.dev, h.units, until});
+  linger_units_[h.dev] += h.units;
+  linger_n_[h.dev]++;
+}
+
+int64_t AllocState::lingering(int64_t dev) const {
+  auto it = linger_units_.find(dev);
+  return it == linger_units_.end() ? 0 : it->second;
+}
+
 void AllocState::hold(const std::string& ids, Held h) {
   auto prev = held_.find(ids);
-  if (prev != held_.end()) unhold(prev);  // kubelet re-used the IDs of a finished container
+  if (prev != held_.end()) {
+    // kubelet re-used the IDs: their container finished -- or its pod was force-deleted (kubelet frees the IDs at
+    // once) and this view has not seen the delete yet: its container may still be stopping
+    const Held& ph = prev->second;
+    auto o = ph.owner.empty() ? pods_.end() : pods_.find(ph.owner);
+    if (o != pods_.end() && o->first != h.uid) {
+      linger(ph, h.t + std::min(std::max(o->second.term_grace_s, 0.0), 600.0) + kLingerSlackS);
+    } else {
+      const double until = ghost_until(ph);
+      if (until > h.t) linger(ph, until);
+    }
+    unhold(prev);
+  }
   if (h.dev >= 0) phys_[h.dev] += h.units;
   if (!h.on_gpu) off_gpu_count(h.dev, +1);
   held_.emplace(ids, std::move(h));
@@ -556,7 +623,7 @@ void AllocState::unhold(std::unordered_map<std::string, Held>::iterator it) {
 
 int64_t AllocState::physical_used(int64_t dev) const {
   auto it = phys_.find(dev);
-  return it == phys_.end() ? 0 : it->second;
+  return (it == phys_.end() ? 0 : it->second) + lingering(dev);
 }
 
 void AllocState::mark_on_gpu(const std::string& aid, bool on) {
@@ -577,8 +644,10 @@ void AllocState::off_gpu_count(int64_t dev, int d) {
 }
 
 size_t AllocState::off_gpu_records_on(int64_t dev) const {
+  // a lingering container holds no ID kubelet still counts: kubelet's per-ID accounting no longer bounds `dev`
   auto it = off_gpu_dev_.find(dev);
-  return it == off_gpu_dev_.end() ? 0 : it->second;
+  auto ln = linger_n_.find(dev);
+  return (it == off_gpu_dev_.end() ? 0 : it->second) + (ln == linger_n_.end() ? 0 : ln->second);
 }
 
 bool AllocState::held_for(std::vector<std::string> ids, int64_t* dev, int64_t* units, double* t,
@@ -603,9 +672,32 @@ size_t AllocState::prune_held(const std::vector<std::vector<std::string>>& liste
   for (auto it = held_.begin(); it != held_.end();) {
     auto cur = it++;
     if (!listed.count(cur->first) && asked - cur->second.t > grace) {
+      const Held& h = cur->second;
+      if (!h.owner.empty() && pods_.count(h.owner)) continue;  // live here: see the header
+      // held by a force-deleted pod (kubelet stopped listing it at the delete, perhaps before this view knew the
+      // pod was gone -- one deleted between its binding and its admission): counted until its kill deadline
+      const double until = ghost_until(h);
+      if (until > asked) linger(h, until);
       unhold(cur);
       n++;
     }
+  }
+  for (auto it = forced_.begin(); it != forced_.end();) {
+    if (it->second <= asked) {
+      it = forced_.erase(it);
+    } else {
+      ++it;
+    }
+  }
+  for (auto it = linger_.begin(); it != linger_.end();) {
+    if (it->until > asked) {
+      ++it;
+      continue;
+    }
+    if ((linger_units_[it->dev] -= it->units) <= 0) linger_units_.erase(it->dev);
+    if (--linger_n_[it->dev] == 0) linger_n_.erase(it->dev);
+    it = linger_.erase(it);
+    n++;
   }
   return n;
 }
@@ -636,7 +728,11 @@ AllocRecord* AllocState::record_by_aid(const std::string& aid) {
 
 void AllocState::set_owner(const std::string& aid, const std::string& owner) {
   auto it = records_.find(aid);
-  if (it != records_.end()) it->second.owner = owner;
+  if (it == records_.end()) return;
+  it->second.owner = owner;
+  if (it->second.ids.empty()) return;
+  auto h = held_.find(id_key(it->second.ids));
+  if (h != held_.end()) h->second.owner = owner;
 }
 
 void AllocState::move_records(const std::string& p_uid, const std::string& q_uid, const std::string& aid) {

@@ -87,6 +87,9 @@ struct AllocPod {
   // (controller.cc sync), so the annotated account below keeps it too
   bool terminating = false;
   double grace_s = -1;        // metadata.deletionGracePeriodSeconds (-1 absent)
+  // spec.terminationGracePeriodSeconds: the apiserver's defaulting writes 30 into every pod it stores; absent only
+  // from the fakes' pods, which they delete at once (tests/fixtures/fakeapi.py delete) -- 0
+  double term_grace_s = 0;
   int cu_count = 0;           // gpushare.amd.com/cu-count
   std::string cu_mask;        // gpushare.amd.com/cu-mask
   int64_t hold_idx = -1;      // gpushare.amd.com/hold-idx
@@ -132,12 +135,20 @@ class AllocState {
   // flight (a second feed that lags, a PATCH response read after the delete) cannot bring it back with its CU
   // partition.  UIDs are never reused; a complete pod is remembered the same way (terminal phases and deletion
   // timestamps are never undone).  Kept for kTombstoneS seconds.
-  void deleted(const std::string& uid);
+  //
+  // A pod deleted while live here (never seen terminating, not terminal: a force delete) with kubelet reporting
+  // owners: kubelet drops it from PodResources and frees its device IDs at once, but its containers get their
+  // termination grace to exit.  What they hold lingers on its GPUs (physical_used, and no per-ID bound there) until
+  // `now` (wall seconds; <0: the clock) + spec.terminationGracePeriodSeconds + kLingerSlackS.
+  void deleted(const std::string& uid, double now = -1.0);
+  static constexpr double kLingerSlackS = 2.0;
+  int64_t lingering(int64_t dev) const;  // units of force-deleted pods' containers still counted on `dev`
+  size_t linger_count() const { return linger_.size(); }
   void tombstone(const std::string& uid);
   bool is_tombstoned(const std::string& uid) const { return gone_.count(uid) != 0; }
   static constexpr double kTombstoneS = 600.0;
   // A complete LIST of this node's pods (already observed): anything held that is not in `live` is gone.
-  void resync(const std::unordered_set<std::string>& live);
+  void resync(const std::unordered_set<std::string>& live, double now = -1.0);
   std::vector<std::string> holders() const;
   // ---- terminating pods (AllocPod::terminating): what the extender still charges for them, per GPU
   int64_t terminating_used(int64_t dev) const;
@@ -196,7 +207,11 @@ class AllocState {
   // runs on `dev` (every unit there holds one of its IDs)
   size_t off_gpu_records_on(int64_t dev) const;
   // kubelet's PodResources answer, requested at `asked` (wall seconds): entries made more than `grace` before it whose
-  // IDs it does not list are gone (their containers stopped).  Returns how many left.
+  // IDs it does not list are gone (their containers stopped) -- unless the pod kubelet last reported holding them is
+  // live here (kubelet stops listing a force-deleted pod at once; the delete reaches this view a moment later and
+  // makes the entry linger).  An entry held by a force-deleted pod -- or never reported while a force-deleted pod's
+  // containers may still run (kubelet gave the IDs to a pod deleted before its admission) -- lingers until that pod's
+  // kill deadline.  Lingering entries past their time go.  Returns how many left.
   size_t prune_held(const std::vector<std::vector<std::string>>& listed, double asked, double grace);
   size_t held_count() const { return held_.size(); }
   // what was handed out with these IDs: false if nothing this plugin knows of
@@ -239,7 +254,21 @@ class AllocState {
     std::string uid;  // the pod the allocation was built for (pruned with it when nobody reports owners)
     bool on_gpu = false;
     std::string cu_mask;  // the CU partition handed out with it
+    std::string owner;    // the pod kubelet last reported holding the IDs (set_owner)
   };
+  struct Linger {
+    int64_t dev = -1, units = 0;
+    double until = 0;
+  };
+  std::vector<Linger> linger_;                     // held entries of force-deleted pods' containers
+  std::unordered_map<int64_t, int64_t> linger_units_;  // dev -> their units
+  std::unordered_map<int64_t, size_t> linger_n_;       // dev -> their count
+  // force-deleted pods, by UID and by "~ns/name" -> when kubelet has killed their containers (wall seconds)
+  std::unordered_map<std::string, double> forced_;
+  void linger(const Held& h, double until);
+  void force_gone(const std::string& uid, double now);  // deleted() / resync(): a live pod gone outright
+  // a held entry kubelet stopped listing: when the force-deleted pod that may still run it is dead by (0: none)
+  double ghost_until(const Held& h) const;
 
   std::unordered_map<std::string, Held> held_;  // id_key(sorted kubelet IDs) -> what was handed out with them
   std::unordered_map<int64_t, int64_t> phys_;     // dev -> sum of held_ units (kept in step)

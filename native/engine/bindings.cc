@@ -298,6 +298,50 @@ class Engine {
     return l_.node_unaccounted(node);
   }
 
+  // The ledger halves of the device plugin's endpoints (server.cc do_move / do_physical run the same calls around
+  // their apiserver write), for in-process protocol harnesses (tests/test_interleavings.py): (rc, to, why) -- rc as
+  // Ledger::begin_move.
+  py::tuple begin_move(const std::string& uid, const std::string& node, int64_t from, int64_t to,
+                       const std::string& partner, bool physical_on_to, int64_t req_hold,
+                       const std::string& req_hold_partner) {
+    MoveRequest m;
+    m.uid = uid;
+    m.node = node;
+    m.from = from;
+    m.to = to;
+    m.partner = partner;
+    m.physical_on_to = physical_on_to;
+    m.req_hold = req_hold;
+    m.req_hold_partner = req_hold_partner;
+    std::string why;
+    int rc;
+    {
+      std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
+      rc = l_.begin_move(&m, &why);
+    }
+    return py::make_tuple(rc, m.to, why);
+  }
+
+  void end_move(const std::string& uid, bool ok) {
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
+    l_.end_move(uid, ok);
+  }
+
+  bool set_unaccounted(const std::string& node, const std::vector<int64_t>& extra, double ttl_s) {
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
+    return l_.set_unaccounted(node, extra, ttl_s);
+  }
+
+  void begin_epoch(double hold_s) {
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
+    l_.begin_epoch(hold_s);
+  }
+
+  double publication_wait(const std::string& node) {
+    std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
+    return l_.publication_wait(node);
+  }
+
   std::vector<std::string> node_names() {
     std::lock_guard<introspect::ProfiledMutex> g(l_.mu());
     return l_.node_names();
@@ -735,8 +779,9 @@ class PyBatchClient {
 // bench.py --open-loop: constant-rate arrivals, every pod's stage times (tracker.h OpenLoop)
 py::dict open_loop_run(const py::dict& api, const std::string& run, const std::string& pod_tmpl, double rate,
                        double duration_s, double warm_s, double hold_s, double drain_s, int creators, int deleters,
-                       const std::string& ns) {
+                       const std::string& ns, int grace) {
   OpenLoopConfig c;
+  c.grace = grace;
   c.run = run;
   c.pod_tmpl = pod_tmpl;
   c.rate = rate;
@@ -1682,6 +1727,13 @@ PYBIND11_MODULE(_engine, m) {
            py::arg("api") = py::dict(), py::arg("update_mode") = false, py::arg("qps") = 0.0, py::arg("burst") = 10,
            py::arg("plugin_auth") = "none", py::arg("plugin_users") = std::vector<std::string>())
       .def("node_unaccounted", [](Engine& e, const std::string& node) { return e.node_unaccounted(node); })
+      .def("begin_move", &Engine::begin_move, py::arg("uid"), py::arg("node"), py::arg("from_dev"), py::arg("to") = -1,
+           py::arg("partner") = std::string(), py::arg("physical_on_to") = false, py::arg("req_hold") = -1,
+           py::arg("req_hold_partner") = std::string())
+      .def("end_move", &Engine::end_move)
+      .def("set_unaccounted", &Engine::set_unaccounted, py::arg("node"), py::arg("extra"), py::arg("ttl") = 60.0)
+      .def("begin_epoch", &Engine::begin_epoch)
+      .def("publication_wait", &Engine::publication_wait)
       .def("stop_server", &Engine::stop_server)
       .def("start_controller", &Engine::start_controller, py::arg("api"), py::arg("resync") = 30.0,
            py::arg("sync_timeout") = 60.0, py::arg("watch_timeout") = 300)
@@ -1710,6 +1762,7 @@ PYBIND11_MODULE(_engine, m) {
   m.attr("TRACK_BOUND") = static_cast<int>(PodTracker::Bound);
   m.attr("TRACK_RUNNING") = static_cast<int>(PodTracker::Running);
   m.attr("TRACK_GONE") = static_cast<int>(PodTracker::Gone);
+  m.attr("TRACK_STOPPED") = static_cast<int>(PodTracker::Stopped);
   py::class_<PyReflectorProbe>(m, "ReflectorProbe")
       .def(py::init<const py::dict&, const std::string&, const std::string&, int>(), py::arg("api"),
            py::arg("path") = "/api/v1/pods", py::arg("field_selector") = "", py::arg("page") = 500)
@@ -1722,7 +1775,7 @@ PYBIND11_MODULE(_engine, m) {
 
   m.def("open_loop_run", &open_loop_run, py::arg("api"), py::arg("run"), py::arg("pod_tmpl"), py::arg("rate"),
         py::arg("duration_s") = 2.0, py::arg("warm_s") = 0.5, py::arg("hold_s") = 0.0, py::arg("drain_s") = 20.0,
-        py::arg("creators") = 16, py::arg("deleters") = 16, py::arg("ns") = "default");
+        py::arg("creators") = 16, py::arg("deleters") = 16, py::arg("ns") = "default", py::arg("grace") = -1);
   py::class_<PyBatchClient>(m, "BatchClient")
       .def(py::init<const py::dict&>())
       .def("run", &PyBatchClient::run, py::arg("requests"), py::arg("concurrency") = 8);
@@ -1791,6 +1844,7 @@ PYBIND11_MODULE(_engine, m) {
       .def_readwrite("assigned", &AllocPod::assigned)
       .def_readwrite("complete", &AllocPod::complete)
       .def_readwrite("terminating", &AllocPod::terminating)
+      .def_readwrite("term_grace_s", &AllocPod::term_grace_s)
       .def_readwrite("cu_count", &AllocPod::cu_count)
       .def_readwrite("cu_mask", &AllocPod::cu_mask)
       .def_readwrite("hold_idx", &AllocPod::hold_idx)
@@ -1821,11 +1875,13 @@ PYBIND11_MODULE(_engine, m) {
            py::arg("node"), py::arg("devices"))
       .def("observe", &AllocState::observe, py::call_guard<AllocLock>())
       .def("release", &AllocState::release, py::call_guard<AllocLock>())
-      .def("deleted", &AllocState::deleted, py::call_guard<AllocLock>())
+      .def("deleted", &AllocState::deleted, py::arg("uid"), py::arg("now") = -1.0, py::call_guard<AllocLock>())
+      .def("lingering", &AllocState::lingering, py::call_guard<AllocLock>())
+      .def("linger_count", &AllocState::linger_count, py::call_guard<AllocLock>())
       .def("is_tombstoned", &AllocState::is_tombstoned, py::call_guard<AllocLock>())
-      .def("resync", [](AllocState& s, const std::vector<std::string>& live) {
-        s.resync(std::unordered_set<std::string>(live.begin(), live.end()));
-      }, py::call_guard<AllocLock>())
+      .def("resync", [](AllocState& s, const std::vector<std::string>& live, double now) {
+        s.resync(std::unordered_set<std::string>(live.begin(), live.end()), now);
+      }, py::arg("live"), py::arg("now") = -1.0, py::call_guard<AllocLock>())
       .def("holders", &AllocState::holders, py::call_guard<AllocLock>())
       .def("has_pod", [](const AllocState& s, const std::string& uid) { return s.pod(uid) != nullptr; }, py::call_guard<AllocLock>())
       // ns/name -> uid through the state's key index (the reconciliation looks up every pod kubelet reports)

@@ -81,6 +81,8 @@ bool PodTracker::ok_locked(const std::string& key, int cond, std::string* err) c
     case Running:
       if (it != pods_.end() && it->second.phase == "Failed") *err = "pod " + key + " Failed";
       return it != pods_.end() && it->second.phase == "Running";
+    case Stopped:
+      return it == pods_.end() || it->second.phase == "Succeeded" || it->second.phase == "Failed";
     default:
       return it == pods_.end();
   }
@@ -99,7 +101,7 @@ std::string PodTracker::wait(const std::vector<std::string>& keys, int cond, dou
       while (i < keys.size() && ok_locked(keys[i], cond, &err)) ++i;
       if (i == keys.size()) return std::string();
       return "timeout: " + std::to_string(keys.size() - i) + " pods not " +
-             (cond == Bound ? "bound" : cond == Running ? "Running" : "gone") + ", e.g. " + keys[i];
+             (cond == Bound ? "bound" : cond == Running ? "Running" : cond == Stopped ? "stopped" : "gone") + ", e.g. " + keys[i];
     }
   }
 }
@@ -277,7 +279,9 @@ bool OpenLoop::run(const OpenLoopConfig& c, std::vector<OpenLoopPod>* pods, std:
     th.emplace_back([&] {
       ApiClient api(cfg_);
       std::string resp, e;
-      const std::string opts = "{\"kind\":\"DeleteOptions\",\"apiVersion\":\"v1\",\"gracePeriodSeconds\":0}";
+      const std::string opts = c.grace < 0 ? std::string("{\"kind\":\"DeleteOptions\",\"apiVersion\":\"v1\"}")
+                                           : "{\"kind\":\"DeleteOptions\",\"apiVersion\":\"v1\",\"gracePeriodSeconds\":" +
+                                                 std::to_string(c.grace) + "}";
       while (true) {
         size_t i;
         {

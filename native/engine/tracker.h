@@ -29,7 +29,9 @@ namespace gsx {
 
 class PodTracker {
  public:
-  enum Cond : int { Bound = 0, Running = 1, Gone = 2 };
+  // Stopped: gone, or in a terminal phase (its kubelet stopped the containers of a gracefully deleted pod and
+  // reported it; the object goes a moment later)
+  enum Cond : int { Bound = 0, Running = 1, Gone = 2, Stopped = 3 };
   PodTracker(const ApiConfig& cfg, const std::string& ns, const std::string& label_selector);
   ~PodTracker();
   bool start(double timeout_s, std::string* err);
@@ -62,6 +64,9 @@ struct OpenLoopConfig {
   double hold_s = 0.0;       // a pod runs this long before it is deleted
   double drain_s = 20.0;     // after the last arrival: wait this long for the pods to run and go
   int creators = 16, deleters = 16;
+  // DELETE's gracePeriodSeconds: < 0 sends none (the pod's spec.terminationGracePeriodSeconds: a graceful deletion
+  // its kubelet ends once the containers stopped), 0 deletes outright (a force delete)
+  int grace = -1;
 };
 
 struct OpenLoopPod {

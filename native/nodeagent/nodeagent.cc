@@ -298,7 +298,8 @@ class Agent {
       std::sort(lat.begin(), lat.end());
       double p50 = lat.empty() ? 0 : lat[lat.size() / 2];
       const double n = admitted_ ? static_cast<double>(admitted_) : 1.0;
-      char b[2048];
+      const double fn = finals_done_ ? static_cast<double>(finals_done_) : 1.0;
+      char b[2560];
       std::snprintf(b, sizeof(b),
                     "{\"admitted\":%llu,\"failed\":%llu,\"bad_stamps\":%llu,\"conflicts\":%llu,\"running\":%zu,"
                     "\"admit_p50_ms\":%.3f,\"admit_max_ms\":%.3f,\"max_ms\":{\"queue\":%.3f,\"assign_patch\":%.3f,"
@@ -308,6 +309,7 @@ class Agent {
                     "\"encode_preferred\":%.4f,\"gap\":%.4f,\"n_gap\":%llu,\"gap_loop\":%.4f,\"gap_list\":%.4f,"
                     "\"gap_handoff\":%.4f,\"relock\":%.4f,\"gap_kept\":%.4f,\"n_gap_kept\":%llu},"
                     "\"mismatch\":%llu,\"podresources_calls\":%llu,\"plugin_debug\":\"%s\",\"finalized\":%llu,"
+                    "\"finalize_mean_ms\":{\"wake\":%.4f,\"stop\":%.4f,\"status\":%.4f,\"delete\":%.4f},"
                     "\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
                     (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
@@ -326,7 +328,8 @@ class Agent {
                     sum_gap_kept_ / std::max<double>(1.0, n_gap_kept_) * 1e3, (unsigned long long)n_gap_kept_,
                     (unsigned long long)mismatch_,
                     (unsigned long long)pr_calls_.load(), plugin_debug_url().c_str(),
-                    (unsigned long long)finals_done_);
+                    (unsigned long long)finals_done_, sum_fin_wake_ / fn * 1e3, sum_fin_release_ / fn * 1e3,
+                    sum_fin_status_ / fn * 1e3, sum_fin_delete_ / fn * 1e3);
       rep.body = b;
       return rep;
     }
@@ -1159,6 +1162,8 @@ class Agent {
   // terminal phase is reported, and the object is deleted with grace 0 under a UID precondition (a pod re-created
   // under the same name is not touched).  mu_ held on entry and exit, dropped around the API calls.
   void finalize_locked(const Final& f, std::unique_lock<std::mutex>& lk) {
+    const double t0 = now_s();
+    sum_fin_wake_ += std::max(0.0, t0 - f.due);
     stop_pod_locked(f.uid);
     for (auto it = releases_.begin(); it != releases_.end(); ++it) {
       if (it->first != f.uid) continue;
@@ -1168,9 +1173,12 @@ class Agent {
       break;
     }
     finals_done_++;
+    const double t1 = now_s();
+    sum_fin_release_ += t1 - t0;
     lk.unlock();
     const std::string path = "/api/v1/namespaces/" + f.ns + "/pods/" + f.name;
     if (f.ran) patch_status(path, "{\"status\":{\"phase\":\"Succeeded\"}}");
+    const double t2 = now_s();
     std::string body = "{\"kind\":\"DeleteOptions\",\"apiVersion\":\"v1\",\"gracePeriodSeconds\":0,"
                        "\"preconditions\":{\"uid\":";
     json::append_quoted(&body, f.uid);
@@ -1186,6 +1194,8 @@ class Agent {
       std::this_thread::sleep_for(std::chrono::microseconds(std::min(100000, 500 << std::min(attempt, 8))));
     }
     lk.lock();
+    sum_fin_status_ += t2 - t1;
+    sum_fin_delete_ += now_s() - t2;
   }
 
   // DELETE a pod's slice on its runtime; mu_ held on entry and exit, dropped around the call.
@@ -1276,6 +1286,9 @@ class Agent {
   std::vector<Final> finals_;                 // graceful deletions to end (finalize_locked)
   std::unordered_set<std::string> finals_set_;
   uint64_t finals_done_ = 0;
+  // where a graceful deletion's end goes (seconds summed over finals_done_): the event to a worker, the container
+  // stop (runtime release), the terminal-phase report, the grace-0 delete
+  double sum_fin_wake_ = 0, sum_fin_release_ = 0, sum_fin_status_ = 0, sum_fin_delete_ = 0;
   double stop_delay_ = 0;
   std::map<int, int> releasing_;  // per GPU: DELETEs in flight on some worker
   std::unordered_map<std::string, int> assign_retries_;  // per pod: ASSIGNED patch attempts (backoff)

@@ -554,3 +554,90 @@ def test_plugin_republishes_on_a_new_extender_epoch_and_counts_terminating_holde
             await c.close()
             await api.stop()
     asyncio.run(go())
+
+
+def test_a_force_deleted_pods_share_lingers_until_its_containers_are_killed():
+    """AllocState::deleted / prune_held (VERDICT r5 #1, force deletes): kubelet stops listing a pod deleted outright
+    and frees its device IDs at once, but its containers get their termination grace.  Their share stays counted on
+    its GPU -- physical_used, no per-ID bound there, published as unaccounted -- until the kill deadline; a graceful
+    deletion (seen terminating first) ends with the containers and lingers nothing; an entry kubelet never reported
+    lingers while a force-deleted pod could be running it; so does one whose IDs kubelet re-used while its reported
+    holder was still live here."""
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
+    from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+
+    def make(gpus="2x16GiB"):
+        plugin = GpuSharePlugin(None, "n", fake_devices(gpus), SHARED_GPU, socket_dir="/tmp/gsx-linger-test",
+                                checkpoint="")
+        plugin.state.core.expect_owner_reports(True)
+        return plugin, plugin.state
+
+    def pod(st, name, dev, grace=5, deleting=False, rv="1"):
+        p = make_pod(name, 8, node="n", uid=f"u{name}", annotations={SHARED_GPU.annotation_idx: str(dev),
+                                                                     SHARED_GPU.annotation_assigned: "true"})
+        p["metadata"]["resourceVersion"] = rv
+        p["spec"]["terminationGracePeriodSeconds"] = grace
+        if deleting:
+            p["metadata"]["deletionTimestamp"] = "2026-01-01T00:00:00Z"
+        st.observe(p)
+        return p
+
+    plugin, st = make()
+    core = st.core
+    a = pod(st, "A", 0)
+    st.record(st.pods["uA"], [f"g0-_-{i}" for i in range(8)], 8, "", "aA", 100.0, on_gpu=True)
+    core.set_owner("aA", "uA")
+    assert core.physical_used(0) == 8 and core.off_gpu_records_on(0) == 0
+    core.deleted("uA", 101.0)  # force delete: kill deadline 101 + 5 + 2
+    assert core.linger_count() == 1 and core.lingering(0) == 8 and core.physical_used(0) == 8
+    assert core.off_gpu_records_on(0) == 1  # kubelet's per-ID count no longer bounds GPU 0
+    assert plugin.unaccounted() == [8, 0]  # the extender charges it too
+    core.prune_held([], 107.5, 0.5)
+    assert core.lingering(0) == 8
+    core.prune_held([], 108.5, 0.5)
+    assert core.linger_count() == 0 and core.physical_used(0) == 0 and plugin.unaccounted() is None
+    del a
+    # graceful: seen terminating, then deleted once kubelet finalised it -- nothing lingers
+    pod(st, "B", 1)
+    st.record(st.pods["uB"], [f"g1-_-{i}" for i in range(8)], 8, "", "aB", 200.0, on_gpu=True)
+    core.set_owner("aB", "uB")
+    pod(st, "B", 1, deleting=True, rv="2")
+    core.deleted("uB", 201.0)
+    core.prune_held([], 201.5, 0.1)
+    assert core.linger_count() == 0 and core.physical_used(1) == 0
+    # an entry kubelet never reported while a force-deleted pod may still run it (kubelet gave it the IDs before
+    # its view had the delete): it lingers until that pod's deadline, then goes
+    pod(st, "C", 0, grace=10)
+    pod(st, "D", 0)
+    core.deleted("uC", 300.0)  # C had no container yet: deadline 312
+    st.record(st.pods["uD"], [f"g0-_-{i}" for i in range(8)], 8, "", "aD", 300.5, on_gpu=True)
+    core.prune_held([], 301.5, 0.5)  # kubelet lists nothing: the ghost may be running D's allocation
+    assert core.lingering(0) == 8
+    core.prune_held([], 312.5, 0.5)
+    assert core.lingering(0) == 0
+    # kubelet re-used IDs whose reported holder this view still has live (its delete not seen yet)
+    pod(st, "E", 1)
+    ids = [f"g1-_-{i}" for i in range(8)]
+    st.record(st.pods["uE"], ids, 8, "", "aE", 400.0, on_gpu=True)
+    core.set_owner("aE", "uE")
+    pod(st, "F", 1)
+    st.record(st.pods["uF"], ids, 8, "", "aF", 401.0, on_gpu=True)
+    assert core.lingering(1) == 8 and core.physical_used(1) == 16
+    # a LIST without a pod that was live here: deleted outright
+    st.resync([p for p in []])
+    assert core.linger_count() >= 2
+    # one GPU: lingering is the only unaccounted use, and it is published
+    one, st1 = make("1x16GiB")
+    pod(st1, "G", 0)
+    st1.record(st1.pods["uG"], [f"g0-_-{i}" for i in range(8)], 8, "", "aG", 500.0, on_gpu=True)
+    st1.core.set_owner("aG", "uG")
+    st1.core.deleted("uG", 501.0)
+    assert one.unaccounted() == [8]
+    # nobody reports owners (no PodResources reconciliation): a pod's going ends its allocations, as before
+    bare = GpuSharePlugin(None, "n", fake_devices("2x16GiB"), SHARED_GPU, socket_dir="/tmp/gsx-linger-test2",
+                          checkpoint="")
+    pod(bare.state, "H", 0)
+    bare.state.record(bare.state.pods["uH"], [f"g0-_-{i}" for i in range(8)], 8, "", "aH", 600.0, on_gpu=True)
+    bare.state.core.deleted("uH", 601.0)
+    assert bare.state.core.linger_count() == 0 and bare.state.core.physical_used(0) == 0
