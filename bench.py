@@ -382,10 +382,6 @@ def latency_sweep(a, children, api_url, api_batch, runner: WaveRunner, inspect_u
 
 
 OPEN_LOOP_LATENCIES_MS = (1, 2, 5)
-# the pods' spec.terminationGracePeriodSeconds, as the apiserver's defaulting writes it into every pod: deleting one
-# is a graceful deletion its kubelet (the node agent) ends once the containers stopped.  (Deleted outright, a pod's
-# containers could outlive the object by their grace -- the device plugin keeps such a pod's share counted that long.)
-TERM_GRACE_S = 30
 OPEN_LOOP_RATES = (500, 1000, 2000, 4000, 8000, 16000, 32000)
 
 
@@ -479,13 +475,15 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats, agen
             run = f"r{k}"
             tmpl = make_pod("__NAME__", a.open_loop_gib, profile=profile, labels={"gsx-ol": run})
             del tmpl["metadata"]["uid"]
-            tmpl["spec"]["terminationGracePeriodSeconds"] = TERM_GRACE_S
+            if a.term_grace >= 0:
+                tmpl["spec"]["terminationGracePeriodSeconds"] = a.term_grace
             u0 = sched_stats().get("unschedulable", 0)
             na0 = agent_stats() if agent_stats else None
             pg0 = _plugin_debug(E, (na0 or {}).get("plugin_debug"))
             res = E.open_loop_run({"server": api_url}, run, json.dumps(tmpl, separators=(",", ":")), float(rate),
                                   duration_s=a.open_loop_s, warm_s=0.3, drain_s=10.0,
-                                  creators=a.open_loop_creators, deleters=a.open_loop_creators)
+                                  creators=a.open_loop_creators, deleters=a.open_loop_creators,
+                                  grace=-1 if a.term_grace >= 0 else 0)
             room_waits = sched_stats().get("unschedulable", 0) - u0
             na1 = agent_stats() if agent_stats else None
             pg1 = _plugin_debug(E, (na1 or {}).get("plugin_debug"))
@@ -688,6 +686,12 @@ def parse():
                          "rates, or 0 (off)")
     ap.add_argument("--open-loop-gib", type=int, default=1, help="pod size of the open-loop rows")
     ap.add_argument("--open-loop-s", type=float, default=1.5, help="seconds of arrivals per open-loop rate")
+    ap.add_argument("--term-grace", type=int, default=-1,
+                    help="the pods' spec.terminationGracePeriodSeconds: >= 0 makes every deletion graceful (the node "
+                         "agent stops the containers, reports the terminal phase, then deletes the object, as kubelet "
+                         "does); -1 (default) leaves it unset, and the fake apiserver deletes at once (a force delete: "
+                         "the node agent's PodResources lists a container until its runtime slice is released, and "
+                         "the plugin runs GSX_PLUGIN_FORCE_DELETE=report)")
     ap.add_argument("--open-loop-creators", type=int, default=64,
                     help="open-loop driver threads creating (and as many deleting) pods: at apiserver latency L they "
                          "offer at most creators / L pods/s (16 made the 2 ms row's knee the driver's own)")
@@ -800,6 +804,9 @@ def main():
     # torchrun stops the other ranks with SIGTERM when one fails: exit through atexit so child servers stop too
     signal.signal(signal.SIGTERM, lambda *_: sys.exit(143))
     a = parse()
+    # pods deleted outright (no --term-grace): the node agent's PodResources lists a container until its runtime slice
+    # is released, so the plugin may take that report as the truth instead of waiting out a kill deadline
+    os.environ.setdefault("GSX_PLUGIN_FORCE_DELETE", "report" if a.term_grace < 0 else "grace")
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         # `python bench.py --gpus N` without a launcher: start torchrun as a CHILD process (this process has not
         # touched the GPU, and is never replaced by exec) and exit with its code
@@ -1010,7 +1017,8 @@ def main():
                 except TimeoutError:
                     pass
         pod_tmpl = make_pod("__NAME__", a.pod_gib, profile=profile, labels={"gsx-wave": "__STEP__"})
-        pod_tmpl["spec"]["terminationGracePeriodSeconds"] = TERM_GRACE_S
+        if a.term_grace >= 0:
+            pod_tmpl["spec"]["terminationGracePeriodSeconds"] = a.term_grace
         del pod_tmpl["metadata"]["uid"]  # the apiserver assigns one per pod
         pod_tmpl = json.dumps(pod_tmpl, separators=(",", ":"))
     from gpushare_scheduler_extender_amd.utils.gctune import tune
@@ -1274,22 +1282,8 @@ def main():
         apiserver_stats = json.loads(body) if st == 200 else {"error": st}
         apiserver_stats.pop("counts", None)
 
-    sweep = ref_client = plugin_row = plugin_row_native = None
-    if rank == 0 and a.sweep:
-        runner = WaveRunner(wave, fetch_timings, lt, n_pods, a.warmup + a.steps, extender_counters)
-        try:
-            sweep, ref_client = latency_sweep(a, children, api_url, api_batch, runner, inspect_used)
-        except Exception as e:  # noqa: BLE001 - the sweep never costs the headline line
-            sweep = {"error": f"{type(e).__name__}: {e}"}
-        if a.agent == "node" and a.node_agent == "native-plugin":
-            try:
-                plugin_row = plugin_path(a, children, api_url, runner, E)
-            except Exception as e:  # noqa: BLE001
-                plugin_row = {"error": f"{type(e).__name__}: {e}"}
-            try:
-                plugin_row_native = inprocess_matcher_path(a, children, api_url, runner, E)
-            except Exception as e:  # noqa: BLE001
-                plugin_row_native = {"error": f"{type(e).__name__}: {e}"}
+    # the open-loop rows first: they need the shipped plugin path the timed region ran on (the sweep's comparison
+    # rows below restart the node agent with other kubelet / plugin set-ups)
     ol = None
     if rank == 0 and a.open_loop not in ("", "0"):
         try:
@@ -1304,12 +1298,19 @@ def main():
                 st_, body_ = na_client.run([("GET", "/v1/stats", b"")], 1)[0]
                 return json.loads(body_) if st_ == 200 else None
 
+            na_workers = []
+
             def na_verify(on: bool):
                 if na_client is not None:
                     # and 64 pod workers for the open loop: each blocks on the runtime call and the Running patch
-                    # (one apiserver round trip), and kubelet's status manager does not hold a pod worker for it
-                    cfg = {"verify": on, **({} if on else {"workers": 64})}
-                    na_client.run([("POST", "/v1/config", json.dumps(cfg).encode())], 1)
+                    # (one apiserver round trip), and kubelet's status manager does not hold a pod worker for it;
+                    # the agent's own number again afterwards (the sweep's wave rows below)
+                    st_, body_ = na_client.run([("POST", "/v1/config", json.dumps({"verify": on}).encode())], 1)[0]
+                    if not on and st_ == 200:
+                        na_workers.append(json.loads(body_).get("workers", 16))
+                    n = 64 if not on else (na_workers[0] if na_workers else None)
+                    if n:
+                        na_client.run([("POST", "/v1/config", json.dumps({"workers": n}).encode())], 1)
 
             # the open-loop driver (its creators, deleters and watch are threads of this process) is a load
             # generator, not the cluster: it gets every allowed CPU no other process of the run is pinned to, not
@@ -1334,6 +1335,22 @@ def main():
                 os.sched_setaffinity(0, own)
         except Exception as e:  # noqa: BLE001 - never costs the headline line
             ol = {"error": f"{type(e).__name__}: {e}"}
+    sweep = ref_client = plugin_row = plugin_row_native = None
+    if rank == 0 and a.sweep:
+        runner = WaveRunner(wave, fetch_timings, lt, n_pods, a.warmup + a.steps, extender_counters)
+        try:
+            sweep, ref_client = latency_sweep(a, children, api_url, api_batch, runner, inspect_used)
+        except Exception as e:  # noqa: BLE001 - the sweep never costs the headline line
+            sweep = {"error": f"{type(e).__name__}: {e}"}
+        if a.agent == "node" and a.node_agent == "native-plugin":
+            try:
+                plugin_row = plugin_path(a, children, api_url, runner, E)
+            except Exception as e:  # noqa: BLE001
+                plugin_row = {"error": f"{type(e).__name__}: {e}"}
+            try:
+                plugin_row_native = inprocess_matcher_path(a, children, api_url, runner, E)
+            except Exception as e:  # noqa: BLE001
+                plugin_row_native = {"error": f"{type(e).__name__}: {e}"}
     if world > 1:
         dist.barrier(group=ctl)  # every rank's runtime endpoint stays up until rank 0's sweep is done
 

@@ -105,6 +105,12 @@ GUARD_WAIT_S = float(os.environ.get("GSX_PLUGIN_GUARD_WAIT_S", "5.0"))
 # admission of every other pod of the node waits behind this call (30 s, the default termination grace, let the
 # kubelet-restart chaos rows time out with admissions queued: 1 of 1900 seeds)
 GUARD_GONE_WAIT_S = float(os.environ.get("GSX_PLUGIN_GUARD_GONE_WAIT_S", "10.0"))
+# A pod deleted outright (a force delete) vanishes from kubelet's PodResources at once while its containers get their
+# termination grace.  "grace" (default, for kubelet): what they hold stays counted -- and published to the extender --
+# until spec.terminationGracePeriodSeconds + 2 s have passed (AllocState::deleted).  "report": kubelet's report is
+# taken as the truth, for a kubelet that lists a container until it has stopped (the node agent stand-in): it stays
+# counted, and published, while listed, and goes when it is not
+FORCE_DELETE = os.environ.get("GSX_PLUGIN_FORCE_DELETE", "grace")
 POD_ANNOTATION = "gpushare.amd.com/pod"  # container annotation: the pod this Allocate was matched to
 
 
@@ -288,6 +294,7 @@ class GpuSharePlugin:
         self.ids = {d.index: fake_ids(d, self.units[d.index], tags[d.index]) for d in devices}
         self.id_owner = {i: d for d, ids in self.ids.items() for i in ids}
         self.state = AllocationState(self.node, self.devices, self.profile)
+        self.state.core.set_linger(FORCE_DELETE != "report")
         self.state.on_drop.append(self._record_dropped)
         self.health_info: dict[int, dict] = {}
         native = getattr(self, "_native", None)
@@ -859,6 +866,7 @@ class GpuSharePlugin:
         t0 = time.monotonic()
         deadline, gone_deadline = t0 + GUARD_WAIT_S, t0 + GUARD_GONE_WAIT_S
         delay = 0.02
+        refused = None
         while True:
             await self._reconcile_now(urgent=True)
             rec = self.state.fresh(self.state.pods.get(rec.uid))
@@ -868,42 +876,48 @@ class GpuSharePlugin:
             if used + units <= self.units.get(rec.dev, 0):
                 return rec
             now = time.monotonic()
+            stopping = used - self._gone_used(rec.dev) + units <= self.units.get(rec.dev, 0)
             if now >= deadline:
-                # past the short wait, keep waiting only for containers that will stop -- deleted pods' (kubelet's
-                # view of a deletion can lag the plugin's by seconds behind a dropped watch) -- and only while no
-                # other GPU has room to move the pod to
-                if (now >= gone_deadline or used - self._gone_used(rec.dev) + units > self.units.get(rec.dev, 0)
-                        or self.room_for(rec, units) >= 0):
+                # past the short wait: move the pod if another GPU has room; else keep waiting only for containers
+                # that will stop -- deleted pods' (kubelet's view of a deletion can lag the plugin's by seconds
+                # behind a dropped watch; a force-deleted pod's containers linger for their grace)
+                best = self.room_for(rec, units) if rec.uid not in self.reconciler.busy() else -1
+                if best >= 0:
+                    log.warning("moving %s from GPU %d (physically full) to GPU %d before it starts", rec.key,
+                                rec.dev, best)
+                    try:
+                        return await self.move_unstarted(rec, best)
+                    except ApiError as e:
+                        # the extender's ledger disagrees (a bind or publication this view has not seen): look again
+                        refused = e
+                        if not e.conflict or now >= gone_deadline:
+                            raise AllocateError(f"moving {rec.key} off a physically full GPU failed: {e}") from e
+                elif now >= gone_deadline or not stopping:
                     break
                 self.stats["physical_guard_gone_waits"] = self.stats.get("physical_guard_gone_waits", 0) + 1
             await asyncio.sleep(delay)
             delay = min(0.2, delay * 2)
+        self.stats["physical_guard_failed"] = self.stats.get("physical_guard_failed", 0) + 1
         if rec.uid in self.reconciler.busy():
-            self.stats["physical_guard_failed"] = self.stats.get("physical_guard_failed", 0) + 1
             raise AllocateError(f"GPU {rec.dev} of {self.node} is physically full and {rec.key} is in an unfinished "
                                 f"reconciliation exchange")
-        best = self.room_for(rec, units)
-        if best < 0:
-            self.stats["physical_guard_failed"] = self.stats.get("physical_guard_failed", 0) + 1
-            keys = {p.uid: p.key for p in self.state.pods.values()}
-            held = [f"{keys.get(r.holder, r.holder)}:{r.units}" for r in self.state.records.values() if r.dev == rec.dev]
-            raise AllocateError(f"GPU {rec.dev} of {self.node} is physically full ({self._physical_used(rec.dev)} of "
-                                f"{self.units.get(rec.dev)} {self.unit} handed out: {', '.join(held)}) and no other "
-                                f"GPU has room for {rec.key}")
-        log.warning("moving %s from GPU %d (physically full) to GPU %d before it starts", rec.key, rec.dev, best)
-        try:
-            return await self.move_unstarted(rec, best)
-        except ApiError as e:
-            raise AllocateError(f"moving {rec.key} off a physically full GPU failed: {e}") from e
+        keys = {p.uid: p.key for p in self.state.pods.values()}
+        held = [f"{keys.get(r.holder, r.holder)}:{r.units}" for r in self.state.records.values() if r.dev == rec.dev]
+        raise AllocateError(f"GPU {rec.dev} of {self.node} is physically full ({self._physical_used(rec.dev)} of "
+                            f"{self.units.get(rec.dev)} {self.unit} handed out: {', '.join(held)}) and no other "
+                            f"GPU has room for {rec.key}" + (f" (last move refused: {refused})" if refused else ""))
 
     def room_for(self, rec: PodRec, units: int, exclude: int = -1) -> int:
-        """Best-fit healthy GPU other than ``rec``'s (and ``exclude``) with room for ``rec`` by both counts: the
-        annotations (the extender's ledger) and the Allocate records (what really runs).  -1 if none."""
+        """Best-fit healthy GPU other than ``rec``'s (and ``exclude``) with room for ``rec`` by both counts: what the
+        extender's ledger holds there -- the annotations plus the unaccounted use this plugin publishes (containers
+        the annotations do not charge there, lingering ones included) -- and the Allocate records (what really
+        runs).  -1 if none."""
+        extra = self.unaccounted() or []
         best, best_free = -1, None
         for d, cap_d in self.units.items():
             if d in (rec.dev, exclude) or not self.devices[d].healthy:
                 continue
-            free_ann = cap_d - self._annotated_used(d, skip=rec.uid)
+            free_ann = cap_d - self._annotated_used(d, skip=rec.uid) - (extra[d] if d < len(extra) else 0)
             if free_ann >= rec.request and cap_d - self._physical_used(d) >= units and (best < 0 or free_ann < best_free):
                 best, best_free = d, free_ann
         return best
@@ -1030,10 +1044,10 @@ class GpuSharePlugin:
     def unaccounted(self) -> list[int] | None:
         """Per GPU, the units kubelet's containers hold there that the annotations do not charge there: a record
         kubelet reports held by another, live pod than the one it was built for, and that pod is annotated with
-        another GPU (a swap the exchange has not repaired); and what the containers of force-deleted pods hold
-        while they linger.  None when every container is charged where it runs (the extender then uses the
-        annotations alone).  On a one-GPU node only lingering counts: whoever holds an allocation there is annotated
-        with that GPU too."""
+        another GPU (a swap the exchange has not repaired); and what the containers of deleted pods still hold
+        (listed by kubelet, or lingering for their grace).  None when every container is charged where it runs (the
+        extender then uses the annotations alone).  On a one-GPU node only deleted pods' containers count: whoever
+        holds an allocation there is annotated with that GPU too."""
         if not self.units:
             return None
         pods = self.state.pods
@@ -1047,16 +1061,17 @@ class GpuSharePlugin:
                 # re-annotation refused -- double-charged both GPUs of every exchange in flight: kubelet-restart
                 # chaos seeds then stalled with binds refused, 4 of 380 failing vs 0-2)
                 continue
-            p = None if r.owner.startswith("~") else pods.get(r.owner)
-            # a holder that is gone: its container has stopped (kubelet removes a gracefully deleted pod's object only
-            # then) or is stopping (a force delete: counted below while it lingers)
+            if r.owner.startswith("~"):
+                continue  # a holder whose object is gone: counted below (gone_held)
+            p = pods.get(r.owner)
             if p is not None and not p.complete and p.dev != r.dev:
                 out[r.dev] += r.units
                 found = True
-        # force-deleted pods' containers, given their termination grace: the extender freed their share when the
-        # objects went, kubelet no longer lists them, but they may still hold the GPU (AllocState::deleted)
+        # deleted pods' containers: those kubelet still lists, and (force deletes) those given their termination
+        # grace although kubelet no longer lists them -- the extender freed their share when the objects went
+        # (AllocState::gone_held / deleted)
         for d in range(len(out)):
-            n = self.state.core.lingering(d)
+            n = self.state.core.gone_held(d) + self.state.core.lingering(d)
             if n:
                 out[d] += n
                 found = True

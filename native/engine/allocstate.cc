@@ -349,6 +349,8 @@ void AllocState::tombstone(const std::string& uid) {
 }
 
 void AllocState::deleted(const std::string& uid, double now) {
+  if (now < 0) now = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
+  deleted_[uid] = now;
   force_gone(uid, now);
   tombstone(uid);
   release(uid);
@@ -357,13 +359,15 @@ void AllocState::deleted(const std::string& uid, double now) {
 
 void AllocState::force_gone(const std::string& uid, double now) {
   auto p = pods_.find(uid);
-  if (p != pods_.end() && owners_known()) {
+  // (with kubelet's report as the truth -- set_linger(false) -- the entries simply stay held until kubelet stops
+  // listing them: prune_held, gone_held)
+  if (linger_on_ && p != pods_.end() && owners_known()) {
     // live until now: a force delete.  Its containers (the entries it holds, or was built for and nobody else was
     // reported holding) keep their GPU share until kubelet has killed them: their termination grace from now
     if (now < 0) now = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count();
     const double until = now + std::min(std::max(p->second.term_grace_s, 0.0), 600.0) + kLingerSlackS;
     forced_[uid] = until;
-    forced_["~" + p->second.key] = until;  // the reconciler's name for a holder it no longer knows (reconcile.py GONE)
+    forced_["~" + p->second.key] = until;  // the reconciler's name for a holder it no longer knows (GONE)
     std::vector<std::string> keys;
     for (const auto& kv : records_) {
       const AllocRecord& r = kv.second;
@@ -585,6 +589,23 @@ void AllocState::linger(const Held& h, double until) {
   linger_n_[h.dev]++;
 }
 
+bool AllocState::holder_gone(const Held& h) const {
+  const std::string& who = h.owner.empty() ? h.uid : h.owner;
+  // a holder kubelet lists but this view does not know ("~ns/name"), one deleted, or one never seen (a restart);
+  // not a complete pod (a finished Job's object stays, and some kubelets keep listing it)
+  if (!who.empty() && who[0] == '~') return true;
+  return !pods_.count(who) && !terminating_.count(who) && (deleted_.count(who) || !gone_.count(who));
+}
+
+int64_t AllocState::gone_held(int64_t dev) const {
+  int64_t n = 0;
+  for (const auto& kv : held_) {
+    const Held& h = kv.second;
+    if (h.dev == dev && h.listed && h.gone_reports >= 2) n += h.units;
+  }
+  return n;
+}
+
 int64_t AllocState::lingering(int64_t dev) const {
   auto it = linger_units_.find(dev);
   return it == linger_units_.end() ? 0 : it->second;
@@ -596,10 +617,10 @@ void AllocState::hold(const std::string& ids, Held h) {
     // kubelet re-used the IDs: their container finished -- or its pod was force-deleted (kubelet frees the IDs at
     // once) and this view has not seen the delete yet: its container may still be stopping
     const Held& ph = prev->second;
-    auto o = ph.owner.empty() ? pods_.end() : pods_.find(ph.owner);
+    auto o = ph.owner.empty() || !linger_on_ ? pods_.end() : pods_.find(ph.owner);
     if (o != pods_.end() && o->first != h.uid) {
       linger(ph, h.t + std::min(std::max(o->second.term_grace_s, 0.0), 600.0) + kLingerSlackS);
-    } else {
+    } else if (linger_on_) {
       const double until = ghost_until(ph);
       if (until > h.t) linger(ph, until);
     }
@@ -671,15 +692,24 @@ size_t AllocState::prune_held(const std::vector<std::vector<std::string>>& liste
   size_t n = 0;
   for (auto it = held_.begin(); it != held_.end();) {
     auto cur = it++;
-    if (!listed.count(cur->first) && asked - cur->second.t > grace) {
+    cur->second.listed = listed.count(cur->first) != 0;
+    cur->second.gone_reports = cur->second.listed && holder_gone(cur->second) ? cur->second.gone_reports + 1 : 0;
+    if (!cur->second.listed && asked - cur->second.t > grace) {
       const Held& h = cur->second;
       if (!h.owner.empty() && pods_.count(h.owner)) continue;  // live here: see the header
       // held by a force-deleted pod (kubelet stopped listing it at the delete, perhaps before this view knew the
       // pod was gone -- one deleted between its binding and its admission): counted until its kill deadline
-      const double until = ghost_until(h);
+      const double until = linger_on_ ? ghost_until(h) : 0.0;
       if (until > asked) linger(h, until);
       unhold(cur);
       n++;
+    }
+  }
+  for (auto it = deleted_.begin(); it != deleted_.end();) {
+    if (it->second < asked - kTombstoneS) {
+      it = deleted_.erase(it);
+    } else {
+      ++it;
     }
   }
   for (auto it = forced_.begin(); it != forced_.end();) {
@@ -694,12 +724,16 @@ size_t AllocState::prune_held(const std::vector<std::vector<std::string>>& liste
       ++it;
       continue;
     }
-    if ((linger_units_[it->dev] -= it->units) <= 0) linger_units_.erase(it->dev);
-    if (--linger_n_[it->dev] == 0) linger_n_.erase(it->dev);
+    unlinger(*it);
     it = linger_.erase(it);
     n++;
   }
   return n;
+}
+
+void AllocState::unlinger(const Linger& l) {
+  if ((linger_units_[l.dev] -= l.units) <= 0) linger_units_.erase(l.dev);
+  if (--linger_n_[l.dev] == 0) linger_n_.erase(l.dev);
 }
 
 bool AllocState::drop_record(const std::string& aid) {

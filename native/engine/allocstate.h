@@ -142,7 +142,16 @@ class AllocState {
   // `now` (wall seconds; <0: the clock) + spec.terminationGracePeriodSeconds + kLingerSlackS.
   void deleted(const std::string& uid, double now = -1.0);
   static constexpr double kLingerSlackS = 2.0;
+  // off: kubelet's PodResources report is taken as the truth about a force-deleted pod's containers (a kubelet that
+  // lists them until they have stopped, like the node agent stand-in): what they hold stays held until kubelet no
+  // longer lists it (prune_held), and is published as unaccounted use meanwhile (gone_held)
+  void set_linger(bool on) { linger_on_ = on; }
+  bool linger_enabled() const { return linger_on_; }
   int64_t lingering(int64_t dev) const;  // units of force-deleted pods' containers still counted on `dev`
+  // units kubelet still lists on `dev` for pods this view no longer has -- deleted pods' containers that have not
+  // stopped yet, the extender freed their share with the objects -- once two reports in a row have listed them
+  // after the pod went (a container that stops at once is never published: the physical guard still counts it)
+  int64_t gone_held(int64_t dev) const;
   size_t linger_count() const { return linger_.size(); }
   void tombstone(const std::string& uid);
   bool is_tombstoned(const std::string& uid) const { return gone_.count(uid) != 0; }
@@ -255,7 +264,10 @@ class AllocState {
     bool on_gpu = false;
     std::string cu_mask;  // the CU partition handed out with it
     std::string owner;    // the pod kubelet last reported holding the IDs (set_owner)
+    bool listed = false;  // kubelet's last report listed the IDs (prune_held)
+    int gone_reports = 0; // reports in a row that listed them after their holder had gone (holder_gone)
   };
+  bool holder_gone(const Held& h) const;
   struct Linger {
     int64_t dev = -1, units = 0;
     double until = 0;
@@ -265,7 +277,10 @@ class AllocState {
   std::unordered_map<int64_t, size_t> linger_n_;       // dev -> their count
   // force-deleted pods, by UID and by "~ns/name" -> when kubelet has killed their containers (wall seconds)
   std::unordered_map<std::string, double> forced_;
+  std::unordered_map<std::string, double> deleted_;  // uid -> when deleted() saw it go (gone_held; kept kTombstoneS)
+  bool linger_on_ = true;
   void linger(const Held& h, double until);
+  void unlinger(const Linger& l);
   void force_gone(const std::string& uid, double now);  // deleted() / resync(): a live pod gone outright
   // a held entry kubelet stopped listing: when the force-deleted pod that may still run it is dead by (0: none)
   double ghost_until(const Held& h) const;

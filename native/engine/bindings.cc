@@ -1877,6 +1877,9 @@ PYBIND11_MODULE(_engine, m) {
       .def("release", &AllocState::release, py::call_guard<AllocLock>())
       .def("deleted", &AllocState::deleted, py::arg("uid"), py::arg("now") = -1.0, py::call_guard<AllocLock>())
       .def("lingering", &AllocState::lingering, py::call_guard<AllocLock>())
+      .def("gone_held", &AllocState::gone_held, py::call_guard<AllocLock>())
+      .def("set_linger", &AllocState::set_linger, py::call_guard<AllocLock>())
+      .def("linger_enabled", &AllocState::linger_enabled, py::call_guard<AllocLock>())
       .def("linger_count", &AllocState::linger_count, py::call_guard<AllocLock>())
       .def("is_tombstoned", &AllocState::is_tombstoned, py::call_guard<AllocLock>())
       .def("resync", [](AllocState& s, const std::vector<std::string>& live, double now) {

@@ -255,10 +255,11 @@ class Agent {
       *err = "pod informer did not sync: " + pods_r_->last_error();
       return false;
     }
+    target_workers_ = static_cast<size_t>(std::max(nworkers_, 1));
     for (int i = 0; i < nworkers_; ++i) {
-      workers_.emplace_back([this] {
+      workers_.emplace_back([this, i] {
         introspect::name_thread("na-worker");
-        worker();
+        worker(static_cast<size_t>(i));
       });
     }
     ready_.store(true);
@@ -272,6 +273,7 @@ class Agent {
     }
     stop_flag_.store(true);
     cv_.notify_all();
+    park_cv_.notify_all();
     for (auto& t : workers_) t.join();
     if (pods_r_) pods_r_->stop();
     pr_stop();
@@ -346,17 +348,20 @@ class Agent {
         int64_t w = d.find(0, "workers");
         int64_t nw = 0;
         if (w >= 0 && d.as_int(static_cast<uint32_t>(w), &nw)) {
-          nw = std::min<int64_t>(nw, 256);
-          while (static_cast<int64_t>(workers_.size()) < nw && !stop_) {
-            workers_.emplace_back([this] {
+          nw = std::max<int64_t>(1, std::min<int64_t>(nw, 256));
+          target_workers_ = static_cast<size_t>(nw);
+          while (workers_.size() < target_workers_ && !stop_) {
+            const size_t me = workers_.size();
+            workers_.emplace_back([this, me] {
               introspect::name_thread("na-worker");
-              worker();
+              worker(me);
             });
           }
+          park_cv_.notify_all();
         }
       }
       rep.body = std::string("{\"verify\":") + (verify_ ? "true" : "false") + ",\"workers\":" +
-                 std::to_string(workers_.size()) + "}";
+                 std::to_string(target_workers_) + "}";
       return rep;
     }
     const std::string_view pre = "/v1/allocations/";
@@ -497,7 +502,18 @@ class Agent {
     int dev = r->second;
     running_.erase(r);
     running_bytes_.erase(uid);
-    forget_ids_locked(uid);
+    // the container's device IDs stay taken, and PodResources keeps listing it, until the runtime has stopped it
+    // (release_one): this kubelet's report is the truth about what still runs (the plugin's
+    // GSX_PLUGIN_FORCE_DELETE=report).  (kubelet frees a force-deleted pod's devices, and stops listing it, at once)
+    auto ui = used_ids_.find(uid);
+    auto uk = uid_key_.find(uid);
+    if (ui != used_ids_.end() && uk != uid_key_.end()) {
+      stopping_[uid] = {uk->second, ui->second};
+      used_ids_.erase(ui);
+      uid_key_.erase(uk);
+    } else {
+      forget_ids_locked(uid);
+    }
     for (auto& kv : devices_) {
       if (CuPartitioner* cp = state_->cus(kv.first)) cp->release(uid);
     }
@@ -512,10 +528,13 @@ class Agent {
   }
 
   // ---------------------------------------------------------------- admission (agent.py _admit)
-  void worker() {
+  void worker(size_t me) {
     std::unique_lock<std::mutex> lk(mu_);
     std::unique_lock<std::mutex> slot(dp_mu_, std::defer_lock);  // the admission slot, when this worker holds it
     while (true) {
+      // past the configured number of workers (POST /v1/config lowered it): parked apart, so that a wake-up meant
+      // for a working one never lands here
+      while (me >= target_workers_ && !stop_) park_cv_.wait(lk);
       double now = now_s();
       if (!batch_.empty() && now >= batch_deadline_) {
         std::stable_sort(batch_.begin(), batch_.end());
@@ -716,6 +735,15 @@ class Agent {
           break;
         }
       }
+    }
+    if (static_cast<int64_t>(n_free) < units && !stopping_.empty()) {
+      // IDs of containers still stopping: finish those releases here, then look again
+      std::vector<int> devs;
+      for (const auto& kv : devices_) devs.push_back(kv.first);
+      for (int d : devs) drain_releases_locked(d, lk);
+      queued_.insert(my_uid);
+      queue_.push_front(key);
+      return;
     }
     if (static_cast<int64_t>(n_free) < units) {
       std::fprintf(stderr, "[gsx-nodeagent] %s: %lld units requested, %zu IDs free\n", key.c_str(),
@@ -932,6 +960,15 @@ class Agent {
         e.container = "main";
         e.resource = p_.resource;
         e.ids = kv.second;
+        out.push_back(std::move(e));
+      }
+      for (const auto& kv : stopping_) {  // containers of deleted pods the runtime has not stopped yet
+        dp::PodDevicesMsg e;
+        e.ns = mine_ns(kv.second.first);
+        e.name = mine_name(kv.second.first);
+        e.container = "main";
+        e.resource = p_.resource;
+        e.ids = kv.second.second;
         out.push_back(std::move(e));
       }
     }
@@ -1204,6 +1241,11 @@ class Agent {
     lk.unlock();
     runtime_call(rel.second, "DELETE", "/v1/pods/" + rel.first, std::string(), nullptr);
     lk.lock();
+    auto st = stopping_.find(rel.first);
+    if (st != stopping_.end()) {
+      mark_used_locked(st->second.second, 0);
+      stopping_.erase(st);
+    }
     if (--releasing_[rel.second] == 0) cv_.notify_all();
   }
 
@@ -1274,6 +1316,8 @@ class Agent {
   std::unique_ptr<Reflector> pods_r_;
   std::mutex mu_;
   std::condition_variable cv_;
+  std::condition_variable park_cv_;  // workers past target_workers_ wait here
+  size_t target_workers_ = 1;
   bool stop_ = false;
   std::unordered_map<std::string, int> running_;
   std::unordered_set<std::string> queued_;
@@ -1284,6 +1328,8 @@ class Agent {
   std::vector<std::pair<double, std::string>> delayed_;
   std::deque<std::pair<std::string, int>> releases_;
   std::vector<Final> finals_;                 // graceful deletions to end (finalize_locked)
+  // uid -> (ns/name, device IDs) of stopped pods whose runtime slice is still being released
+  std::unordered_map<std::string, std::pair<std::string, std::vector<std::string>>> stopping_;
   std::unordered_set<std::string> finals_set_;
   uint64_t finals_done_ = 0;
   // where a graceful deletion's end goes (seconds summed over finals_done_): the event to a worker, the container

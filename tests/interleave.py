@@ -79,6 +79,9 @@ class Scenario:
     passes: int = 10                 # reconciliation passes the scheduler may start before the drain
     restarts: int = 0                # extender restarts
     stop_after: int = 0              # steps before kubelet may stop a deleted pod's container (a slow runtime)
+    # kubelet lists a force-deleted pod's container until it has stopped (the node agent stand-in), and the plugin
+    # runs GSX_PLUGIN_FORCE_DELETE=report; False: real kubelet (drops it at once) and the default "grace" policy
+    truthful: bool = False
     max_steps: int = 4000
 
 
@@ -94,6 +97,9 @@ SCENARIOS = {s.name: s for s in (
     # force deletes whose containers run out their whole termination grace, new pods bound meanwhile
     Scenario("force-grace", sizes=(8, 8, 8, 8), extra=(8, 8), deletes=2, grace="force", passes=14,
              stop_after=10 ** 9),
+    # the same against a kubelet whose report is the truth, with the plugin taking it as such (bench.py's setting)
+    Scenario("force-report", sizes=(8, 8, 8, 8), extra=(8, 8), deletes=2, grace="force", passes=14,
+             stop_after=10 ** 9, truthful=True),
 )}
 
 
@@ -193,9 +199,10 @@ class _PodResources:
 
     async def device_ids(self, resource, timeout=2.0):
         await self.h.point("podresources List")
-        # a pod kubelet saw deleted outright is out of its pod manager: not listed, though its container may still stop
+        # a pod kubelet saw deleted outright is out of its pod manager: not listed, though its container may still
+        # stop (a truthful kubelet lists it until it has)
         return {tuple(c.key.split("/", 1)): [tuple(sorted(c.ids))] for uid, c in self.h.active.items()
-                if uid not in self.h.kgone}
+                if self.h.sc.truthful or uid not in self.h.kgone}
 
     async def close(self):
         pass
@@ -338,6 +345,7 @@ class Harness:
                                        PROFILE, socket_dir=tmpdir, checkpoint="", extender="http://harness")
         pl.reconciler = reconcile_mod.Reconciler(pl, _PodResources(self))
         pl.state.core.expect_owner_reports(True)
+        pl.state.core.set_linger(not self.sc.truthful)
         pl._extender_request = self.ext_request
 
         async def informer_wait(found, timeout=0.0):  # the pod event may still be on its way: a gate, then look
@@ -481,10 +489,13 @@ class Harness:
             p = self.kview[uid]
             key = f"{p['metadata']['namespace']}/{p['metadata']['name']}"
             units = _request(p)
-            # kubelet frees a force-deleted pod's device IDs as soon as it sees the delete (its container may still run)
-            taken = ({i for u, c in self.active.items() if u not in self.kgone for i in c.ids}
+            # kubelet frees a force-deleted pod's device IDs as soon as it sees the delete (its container may still
+            # run); a truthful one when the container has stopped
+            taken = ({i for u, c in self.active.items() if self.sc.truthful or u not in self.kgone for i in c.ids}
                      | {i for ids in self.reserved.values() for i in ids})
             avail = [i for i in self.all_ids if i not in taken]
+            if len(avail) < units and self.sc.truthful:
+                return  # the node agent stand-in re-queues the pod until the stopping containers' IDs are free
             self.admitted.add(uid)
             if len(avail) < units:
                 self.failed[uid] = "kubelet: not enough device IDs"
@@ -667,8 +678,15 @@ class Harness:
                                         f"{a.get(PROFILE.annotation_assigned)}")
                 elif not md.get("deletionTimestamp") and uid not in self.failed and uid not in self.refused:
                     raise Violation(f"{md['name']} is bound to the node and was never admitted")
-        if self.failed or self.refused:
-            raise Violation(f"Allocate failed: {self.failed or ''} refused by the physical guard: {self.refused or ''}")
+        # an Allocate for a pod being deleted (kubelet admitted it before its view had the delete) may fail: the pod
+        # goes anyway
+        def live(uid):
+            p = _by_uid(self.api, uid)
+            return p is not None and not p["metadata"].get("deletionTimestamp")
+        failed = {u: w for u, w in self.failed.items() if live(u)}
+        refused = {u: w for u, w in self.refused.items() if live(u)}
+        if failed or refused:
+            raise Violation(f"Allocate failed: {failed or ''} refused by the physical guard: {refused or ''}")
         ledger = [used for _, used in self.eng.node_devices(NODE)]
         if ledger != ann_used:
             raise Violation(f"extender ledger {ledger} != annotations {ann_used}")
@@ -727,7 +745,10 @@ class Harness:
             for _ in range(self.sc.max_steps):
                 if not (self.tasks or self.gates) or not await self._step(users=False, passes=False):
                     break
-            settled = not self.enabled(False, passes=False) and self.plugin._phys_published is None
+            # (a deleting pod's container kubelet has yet to stop: the drain waits for it)
+            stopping = any(u in self.k_deleted_at or u in self.stop_due for u in self.active)
+            settled = (not self.enabled(False, passes=False) and self.plugin._phys_published is None
+                       and not stopping)
             quiet = quiet + 1 if self.api.rv == rv and settled else 0
             if quiet >= 3:
                 break

@@ -317,8 +317,9 @@ def test_a_bind_into_an_unrepaired_drift_trades_gpus_with_the_drifted_pod():
 
 def test_unaccounted_use_is_a_live_holder_on_another_gpu_and_reaches_the_extender():
     """plugin.py unaccounted / publish_physical: a record kubelet reports held by another live pod annotated with
-    another GPU is charged where the container runs; nothing while the record is unreported, held by its own pod,
-    or held by a pod that is gone; withdrawn once the annotations agree.  The extender charges what is published."""
+    another GPU is charged where the container runs; nothing while the record is unreported or held by its own pod;
+    one held by a pod that is gone is charged while kubelet lists it; withdrawn once the annotations agree.  The
+    extender charges what is published."""
     import asyncio
     import json as _json
 
@@ -366,7 +367,11 @@ def test_unaccounted_use_is_a_live_holder_on_another_gpu_and_reaches_the_extende
             assert await plugin.publish_physical()
             assert ext.server.engine.node_unaccounted("n") == []
             pod("P", 0)
-            st.set_owner("aQ", "~gone")  # held by a pod that is gone: its container is stopping
+            st.set_owner("aQ", "~default/gone")  # kubelet lists it for a pod that is gone: its container is stopping
+            st.core.prune_held([["g1-_-0"]], 0.0, 0.0)
+            st.core.prune_held([["g1-_-0"]], 0.0, 0.0)
+            assert plugin.unaccounted() == [0, 4]  # charged until kubelet stops listing it (the extender freed it)
+            st.core.prune_held([], 1e12, 0.0)
             assert plugin.unaccounted() is None
             one = GpuSharePlugin(c, "n", fake_devices("1x16GiB"), SHARED_GPU, socket_dir="/tmp/gsx-unacc-test1")
             assert one.unaccounted() is None  # one GPU: whoever holds it is annotated with it
@@ -641,3 +646,49 @@ def test_a_force_deleted_pods_share_lingers_until_its_containers_are_killed():
     bare.state.record(bare.state.pods["uH"], [f"g0-_-{i}" for i in range(8)], 8, "", "aH", 600.0, on_gpu=True)
     bare.state.core.deleted("uH", 601.0)
     assert bare.state.core.linger_count() == 0 and bare.state.core.physical_used(0) == 0
+
+
+def test_with_kubelets_report_as_the_truth_a_deleted_pods_container_counts_while_listed():
+    """GSX_PLUGIN_FORCE_DELETE=report (a kubelet that lists a container until it has stopped, like the node agent):
+    a pod deleted outright keeps its held entry while kubelet lists its IDs -- counted on its GPU and published as
+    unaccounted use (the extender freed the share with the object) -- and it goes with the first report that no
+    longer lists it.  A completed pod's entry is not published (a finished Job's object stays)."""
+    from gpushare_scheduler_extender_amd.deviceplugin.devices import fake_devices
+    from gpushare_scheduler_extender_amd.deviceplugin.plugin import GpuSharePlugin
+    from gpushare_scheduler_extender_amd.models.profile import SHARED_GPU
+
+    plugin = GpuSharePlugin(None, "n", fake_devices("2x16GiB"), SHARED_GPU, socket_dir="/tmp/gsx-report-test",
+                            checkpoint="")
+    st, core = plugin.state, plugin.state.core
+    core.expect_owner_reports(True)
+    core.set_linger(False)
+
+    def pod(name, dev, phase="Running"):
+        p = make_pod(name, 8, node="n", uid=f"u{name}", annotations={SHARED_GPU.annotation_idx: str(dev),
+                                                                     SHARED_GPU.annotation_assigned: "true"})
+        p["metadata"]["resourceVersion"] = "1"
+        p["status"]["phase"] = phase
+        st.observe(p)
+        return p
+
+    pod("A", 0)
+    ids = [f"g0-_-{i}" for i in range(8)]
+    st.record(st.pods["uA"], ids, 8, "", "aA", 100.0, on_gpu=True)
+    core.set_owner("aA", "uA")
+    core.deleted("uA", 101.0)
+    assert core.linger_count() == 0 and core.physical_used(0) == 8
+    assert core.gone_held(0) == 0  # kubelet has not reported it yet: nothing to publish
+    core.prune_held([ids], 102.0, 0.5)  # kubelet lists it: counted; published once a second report still does
+    assert core.physical_used(0) == 8 and core.gone_held(0) == 0
+    core.prune_held([ids], 102.5, 0.5)
+    assert core.gone_held(0) == 8
+    assert plugin.unaccounted() == [8, 0]
+    core.prune_held([], 103.0, 0.5)  # kubelet stopped listing it: its container has stopped
+    assert core.physical_used(0) == 0 and plugin.unaccounted() is None
+    # a completed pod kubelet keeps listing is not published
+    pod("B", 1)
+    ids_b = [f"g1-_-{i}" for i in range(8)]
+    st.record(st.pods["uB"], ids_b, 8, "", "aB", 200.0, on_gpu=True)
+    core.set_owner("aB", "uB")
+    pod("B", 1, phase="Succeeded")
+    assert core.gone_held(1) == 0
