@@ -864,17 +864,26 @@ def main():
                                         cpus=cpu_plan.get("scheduler")))
         if a.agent == "node":
             # the node's device plugin / kubelet stand-in: one process for all GPUs of the node, like a DaemonSet
-            children.append(start_node_agent(api.url, NODE, profile=a.profile,
-                                             native=a.node_agent in ("native", "native-plugin"),
-                                             plugin={"inproc": "inproc", "native-plugin": "spawn"}.get(a.node_agent,
-                                                                                                        "grpc"),
-                                             workers=min(16, max(8, 2 * a.pods_per_gpu * world)),
-                                             cpus=cpu_plan.get("node-agent"),
-                                             # the compiled stand-in is kubelet-faithful in plugin mode already
-                                             extra=["--faithful"] if a.kubelet == "faithful" and a.node_agent in (
-                                                 "plugin", "inproc") else [],
-                                             plugin_cpus=a.plugin_cpus, serial_admission=a.admission == "serial",
-                                             extender=ext.url))
+            def start_agent(cpus, api_url=api.url, ext_url=ext.url):
+                return start_node_agent(api_url, NODE, profile=a.profile,
+                                        native=a.node_agent in ("native", "native-plugin"),
+                                        plugin={"inproc": "inproc", "native-plugin": "spawn"}.get(a.node_agent, "grpc"),
+                                        workers=min(16, max(8, 2 * a.pods_per_gpu * world)), cpus=cpus,
+                                        # the compiled stand-in is kubelet-faithful in plugin mode already
+                                        extra=["--faithful"] if a.kubelet == "faithful" and a.node_agent in (
+                                            "plugin", "inproc") else [],
+                                        plugin_cpus=a.plugin_cpus, serial_admission=a.admission == "serial",
+                                        extender=ext_url)
+
+            def restore_node_agent():
+                na = restart_child(children, "node-agent", lambda old: start_agent(old.cpus))
+                client = E.BatchClient({"server": na.url})
+                wait_until(lambda: client.run([("GET", "/v1/stats", b"")], 1)[0][0] == 200, 120,
+                           "node agent never ready")
+                wait_until(lambda: bool(json.loads(client.run([("GET", "/v1/stats", b"")], 1)[0][1]).get(
+                    "plugin_debug")), 30, "plugin debug endpoint")
+
+            children.append(start_agent(cpu_plan.get("node-agent")))
         api_url, ext_url = api.url, ext.url
 
     import torch
@@ -1282,11 +1291,30 @@ def main():
         apiserver_stats = json.loads(body) if st == 200 else {"error": st}
         apiserver_stats.pop("counts", None)
 
-    # the open-loop rows first: they need the shipped plugin path the timed region ran on (the sweep's comparison
-    # rows below restart the node agent with other kubelet / plugin set-ups)
+    sweep = ref_client = plugin_row = plugin_row_native = None
+    if rank == 0 and a.sweep:
+        runner = WaveRunner(wave, fetch_timings, lt, n_pods, a.warmup + a.steps, extender_counters)
+        try:
+            sweep, ref_client = latency_sweep(a, children, api_url, api_batch, runner, inspect_used)
+        except Exception as e:  # noqa: BLE001 - the sweep never costs the headline line
+            sweep = {"error": f"{type(e).__name__}: {e}"}
+        if a.agent == "node" and a.node_agent == "native-plugin":
+            try:
+                plugin_row = plugin_path(a, children, api_url, runner, E)
+            except Exception as e:  # noqa: BLE001
+                plugin_row = {"error": f"{type(e).__name__}: {e}"}
+            try:
+                plugin_row_native = inprocess_matcher_path(a, children, api_url, runner, E)
+            except Exception as e:  # noqa: BLE001
+                plugin_row_native = {"error": f"{type(e).__name__}: {e}"}
+    # the open-loop rows run on the shipped plugin path the timed region ran on: the sweep's comparison rows above
+    # restarted the node agent with other kubelet / plugin set-ups, so it is started again as the timed region had it
+    # (after the sweep: open-loop churn left behind slowed the sweep's waves 2-4x, profiles/r06_final/README.md)
     ol = None
     if rank == 0 and a.open_loop not in ("", "0"):
         try:
+            if a.sweep and a.agent == "node" and a.node_agent == "native-plugin":
+                restore_node_agent()
             def sched_stats():
                 return json.loads(lt.run(sched_http.request("GET", "/v1/stats"), 30).body)
 
@@ -1335,22 +1363,6 @@ def main():
                 os.sched_setaffinity(0, own)
         except Exception as e:  # noqa: BLE001 - never costs the headline line
             ol = {"error": f"{type(e).__name__}: {e}"}
-    sweep = ref_client = plugin_row = plugin_row_native = None
-    if rank == 0 and a.sweep:
-        runner = WaveRunner(wave, fetch_timings, lt, n_pods, a.warmup + a.steps, extender_counters)
-        try:
-            sweep, ref_client = latency_sweep(a, children, api_url, api_batch, runner, inspect_used)
-        except Exception as e:  # noqa: BLE001 - the sweep never costs the headline line
-            sweep = {"error": f"{type(e).__name__}: {e}"}
-        if a.agent == "node" and a.node_agent == "native-plugin":
-            try:
-                plugin_row = plugin_path(a, children, api_url, runner, E)
-            except Exception as e:  # noqa: BLE001
-                plugin_row = {"error": f"{type(e).__name__}: {e}"}
-            try:
-                plugin_row_native = inprocess_matcher_path(a, children, api_url, runner, E)
-            except Exception as e:  # noqa: BLE001
-                plugin_row_native = {"error": f"{type(e).__name__}: {e}"}
     if world > 1:
         dist.barrier(group=ctl)  # every rank's runtime endpoint stays up until rank 0's sweep is done
 

@@ -304,6 +304,7 @@ class Agent {
       char b[2560];
       std::snprintf(b, sizeof(b),
                     "{\"admitted\":%llu,\"failed\":%llu,\"bad_stamps\":%llu,\"conflicts\":%llu,\"running\":%zu,"
+                    "\"stopping\":%zu,\"releases_queued\":%zu,"
                     "\"admit_p50_ms\":%.3f,\"admit_max_ms\":%.3f,\"max_ms\":{\"queue\":%.3f,\"assign_patch\":%.3f,"
                     "\"runtime\":%.3f,\"running_patch\":%.3f},\"mean_ms\":{\"queue\":%.4f,\"assign_patch\":%.4f,"
                     "\"runtime\":%.4f,\"running_patch\":%.4f},\"status_retries\":%llu,\"api_connects\":%llu,"
@@ -314,7 +315,7 @@ class Agent {
                     "\"finalize_mean_ms\":{\"wake\":%.4f,\"stop\":%.4f,\"status\":%.4f,\"delete\":%.4f},"
                     "\"native\":true}",
                     (unsigned long long)admitted_, (unsigned long long)failed_, (unsigned long long)bad_,
-                    (unsigned long long)conflicts_, running_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
+                    (unsigned long long)conflicts_, running_.size(), stopping_.size(), releases_.size(), p50 * 1e3, lat.empty() ? 0.0 : lat.back() * 1e3,
                     max_queue_ * 1e3, max_patch_ * 1e3, max_runtime_ * 1e3, max_status_ * 1e3, sum_queue_ / n * 1e3,
                     sum_patch_ / n * 1e3, sum_runtime_ / n * 1e3, sum_status_ / n * 1e3,
                     (unsigned long long)status_retries_.load(), (unsigned long long)api_.reconnects(),
