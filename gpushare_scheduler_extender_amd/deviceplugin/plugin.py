@@ -876,7 +876,9 @@ class GpuSharePlugin:
             if used + units <= self.units.get(rec.dev, 0):
                 return rec
             now = time.monotonic()
-            stopping = used - self._gone_used(rec.dev) + units <= self.units.get(rec.dev, 0)
+            # room will come, here or on another GPU, once containers of deleted pods have stopped
+            stopping = (used - self._gone_used(rec.dev) + units <= self.units.get(rec.dev, 0)
+                        or self.room_for(rec, units, soon=True) >= 0)
             if now >= deadline:
                 # past the short wait: move the pod if another GPU has room; else keep waiting only for containers
                 # that will stop -- deleted pods' (kubelet's view of a deletion can lag the plugin's by seconds
@@ -907,18 +909,24 @@ class GpuSharePlugin:
                             f"{self.units.get(rec.dev)} {self.unit} handed out: {', '.join(held)}) and no other "
                             f"GPU has room for {rec.key}" + (f" (last move refused: {refused})" if refused else ""))
 
-    def room_for(self, rec: PodRec, units: int, exclude: int = -1) -> int:
+    def room_for(self, rec: PodRec, units: int, exclude: int = -1, soon: bool = False) -> int:
         """Best-fit healthy GPU other than ``rec``'s (and ``exclude``) with room for ``rec`` by both counts: what the
         extender's ledger holds there -- the annotations plus the unaccounted use this plugin publishes (containers
-        the annotations do not charge there, lingering ones included) -- and the Allocate records (what really
-        runs).  -1 if none."""
+        the annotations do not charge there, deleted pods' stopping ones included) -- and the Allocate records (what
+        really runs).  ``soon``: as it will be once deleted pods' containers have stopped.  -1 if none."""
         extra = self.unaccounted() or []
+        core = self.state.core
         best, best_free = -1, None
         for d, cap_d in self.units.items():
             if d in (rec.dev, exclude) or not self.devices[d].healthy:
                 continue
-            free_ann = cap_d - self._annotated_used(d, skip=rec.uid) - (extra[d] if d < len(extra) else 0)
-            if free_ann >= rec.request and cap_d - self._physical_used(d) >= units and (best < 0 or free_ann < best_free):
+            ex = extra[d] if d < len(extra) else 0
+            phys = self._physical_used(d)
+            if soon:
+                ex = max(0, ex - core.gone_held(d) - core.lingering(d))
+                phys -= self._gone_used(d)
+            free_ann = cap_d - self._annotated_used(d, skip=rec.uid) - ex
+            if free_ann >= rec.request and cap_d - phys >= units and (best < 0 or free_ann < best_free):
                 best, best_free = d, free_ann
         return best
 

@@ -453,13 +453,9 @@ class Reconciler:
                 want = json.loads(p.hold_partner) if p.hold_partner else {}
             except ValueError:
                 want = {}
+            # (Q cannot have been served an Allocate with its old fields meanwhile: the matcher skips the partner of an
+            # unfinished exchange, AllocState::candidates -- tests/interleave.py swap-graceful seed 25)
             q = self.state.pods.get(want.get("uid", ""))
-            if q is not None and q.assigned == "true" and want.get("assigned") != "true":
-                # Q was served an Allocate since step 1 was planned (its ASSIGNED is that Allocate's commit now):
-                # the payload's "not served" is stale, and re-applying it would make a running pod an Allocate
-                # candidate again (tests/interleave.py found it: swap-graceful seed 25).  Whatever GPU Q's
-                # container got, the next pass compares it with Q's annotation (a drift repair)
-                q = None
             if q is not None and fields(q) != {k: want.get(k) for k in ("idx", "assigned", "cu_mask")}:
                 if not await self._patch(q, self._ann(want), partner=p.uid):
                     continue

@@ -131,6 +131,7 @@ class NodeAgent:
         self.all_ids: list[str] = []
         self.used_ids: dict[str, list[str]] = {}
         self.id_keys: dict[str, str] = {}  # uid -> ns/name of the pod holding used_ids[uid]
+        self.stopping: dict[str, tuple[str, list]] = {}  # uid -> (ns/name, IDs) of a container still stopping
         self.plugin_stats_url: str | None = None  # the plugin's /debug/state when it runs as its own process
         self.prserver = None
         if podresources_socket:
@@ -168,19 +169,23 @@ class NodeAgent:
         self._stop(podutil.meta(pod).get("uid", ""))
 
     def _pod_resources(self):
-        """kubelet's podresources view: every pod holding device IDs, one container each."""
+        """kubelet's podresources view: every pod holding device IDs, one container each -- a stopped pod's until
+        its runtime slice is released (the container has stopped): this kubelet's report is the truth about what
+        runs (the plugin's GSX_PLUGIN_FORCE_DELETE=report)."""
         out = []
-        for uid, ids in self.used_ids.items():
-            key = self.id_keys.get(uid, "")
+        for uid, ids in list(self.used_ids.items()) + [(u, ids) for u, (_, ids) in self.stopping.items()]:
+            key = self.id_keys.get(uid, "") or self.stopping.get(uid, ("", None))[0]
             ns, _, name = key.partition("/")
             out.append((ns, name, [("main", self.profile.resource, ids)]))
         return out
 
     def _stop(self, uid: str):
         self.claimed.discard(uid)
-        self.used_ids.pop(uid, None)
-        self.id_keys.pop(uid, None)
+        ids = self.used_ids.pop(uid, None)
+        key = self.id_keys.pop(uid, None)
         if self.running.pop(uid, None) is not None:
+            if ids:
+                self.stopping[uid] = (key or "", ids)  # listed, and its IDs taken, until the release completes
             self._release(uid)
 
     def _terminate(self, pod: dict):
@@ -233,10 +238,12 @@ class NodeAgent:
         self._releasing.add(t)
         t.add_done_callback(self._bg.discard)
         t.add_done_callback(self._releasing.discard)
+        t.add_done_callback(lambda _t, uid=uid: self.stopping.pop(uid, None))
 
     # ------------------------------------------------------------ device plugin calls (kubelet's device manager)
     async def _allocate_grpc(self, uid: str, units: int) -> _Alloc:
-        free = sorted(set(self.all_ids) - {i for ids in self.used_ids.values() for i in ids})
+        free = sorted(set(self.all_ids) - {i for ids in self.used_ids.values() for i in ids}
+                      - {i for _, ids in self.stopping.values() for i in ids})
         if len(free) < units:
             raise AllocateError(f"kubelet: {units} {self.profile.resource} requested, {len(free)} IDs free")
         t0 = time.perf_counter()
@@ -445,7 +452,10 @@ class NodeAgent:
             return
         if uid not in self.claimed or not self._alive(uid, key):  # deleted while starting: tear it down
             self.claimed.discard(uid)
-            self.used_ids.pop(uid, None)
+            ids = self.used_ids.pop(uid, None)
+            ikey = self.id_keys.pop(uid, None)
+            if ids:
+                self.stopping[uid] = (ikey or key, ids)
             self._release(uid)
             return
         self.running[uid] = key

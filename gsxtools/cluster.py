@@ -170,6 +170,10 @@ def start_node_agent(apiserver: str, node: str, profile: str = "shared-gpu", wor
     env = {"GSX_PLUGIN_CPUS": ",".join(map(str, plugin_cpus))} if plugin_cpus else {}
     if extender:
         env["GSX_EXTENDER_URL"] = extender
+    # both stand-ins list a container in PodResources, and keep its device IDs taken, until it has stopped: the
+    # plugin may take their report as the truth about force-deleted pods' containers (deviceplugin/plugin.py
+    # FORCE_DELETE; a real kubelet drops them at once, and the default "grace" policy is for that)
+    env["GSX_PLUGIN_FORCE_DELETE"] = os.environ.get("GSX_PLUGIN_FORCE_DELETE", "report")
     env = env or None
     if native:
         exe = Path(os.environ.get("GSX_NODEAGENT_BIN") or tool_path("gsx-nodeagent"))  # an A/B build of the stand-in

@@ -437,10 +437,27 @@ void AllocState::resync(const std::unordered_set<std::string>& live, double now)
 }
 
 std::vector<const AllocPod*> AllocState::candidates() const {
+  // the partner Q an unfinished reconciliation exchange names (P's hold-partner): its fields are about to be
+  // rewritten (step 2), so no Allocate may be served to it with the old ones meanwhile -- served on the GPU it is
+  // leaving, it would stay there while the extender has already credited that room to P (tests/interleave.py,
+  // reconcile.py _finish_holds).  Holds are rare and short: a scan, no index
+  std::unordered_set<std::string> partners;
+  for (const auto& kv : pods_) {
+    if (!skip_partners_) break;
+    const std::string& hp = kv.second.hold_partner;
+    if (hp.empty()) continue;
+    const size_t k = hp.find("\"uid\"");
+    const size_t q1 = k == std::string::npos ? k : hp.find('"', hp.find(':', k) + 1);
+    const size_t q2 = q1 == std::string::npos ? q1 : hp.find('"', q1 + 1);
+    if (q2 != std::string::npos) partners.insert(hp.substr(q1 + 1, q2 - q1 - 1));
+  }
   std::vector<const AllocPod*> out;
   for (const auto& kv : pods_) {
     const AllocPod& r = kv.second;
-    if (r.pending() && r.assigned == "false" && has_device(r.dev) && !inflight_.count(r.uid)) out.push_back(&r);
+    if (r.pending() && r.assigned == "false" && has_device(r.dev) && !inflight_.count(r.uid) &&
+        (partners.empty() || !partners.count(r.uid))) {
+      out.push_back(&r);
+    }
   }
   std::sort(out.begin(), out.end(), [](const AllocPod* a, const AllocPod* b) { return order_key(*a) < order_key(*b); });
   return out;

@@ -146,6 +146,8 @@ class AllocState {
   // lists them until they have stopped, like the node agent stand-in): what they hold stays held until kubelet no
   // longer lists it (prune_held), and is published as unaccounted use meanwhile (gone_held)
   void set_linger(bool on) { linger_on_ = on; }
+  // the matcher skips the partner of an unfinished exchange (candidates); off only to show what that prevents
+  void set_skip_partners(bool on) { skip_partners_ = on; }
   bool linger_enabled() const { return linger_on_; }
   int64_t lingering(int64_t dev) const;  // units of force-deleted pods' containers still counted on `dev`
   // units kubelet still lists on `dev` for pods this view no longer has -- deleted pods' containers that have not
@@ -279,6 +281,7 @@ class AllocState {
   std::unordered_map<std::string, double> forced_;
   std::unordered_map<std::string, double> deleted_;  // uid -> when deleted() saw it go (gone_held; kept kTombstoneS)
   bool linger_on_ = true;
+  bool skip_partners_ = true;
   void linger(const Held& h, double until);
   void unlinger(const Linger& l);
   void force_gone(const std::string& uid, double now);  // deleted() / resync(): a live pod gone outright

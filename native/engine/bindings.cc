@@ -1879,6 +1879,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("lingering", &AllocState::lingering, py::call_guard<AllocLock>())
       .def("gone_held", &AllocState::gone_held, py::call_guard<AllocLock>())
       .def("set_linger", &AllocState::set_linger, py::call_guard<AllocLock>())
+      .def("set_skip_partners", &AllocState::set_skip_partners, py::call_guard<AllocLock>())
       .def("linger_enabled", &AllocState::linger_enabled, py::call_guard<AllocLock>())
       .def("linger_count", &AllocState::linger_count, py::call_guard<AllocLock>())
       .def("is_tombstoned", &AllocState::is_tombstoned, py::call_guard<AllocLock>())

@@ -23,7 +23,9 @@ reconciliation pass; the plugin's epoch poll; a user deleting a pod (graceful or
 extender restarting (a new ledger from a LIST, a new epoch, binds held until the plugin republishes).
 
 Checked after EVERY step (safety): no GPU runs more than its capacity -- the sum of the units of the containers
-kubelet runs on a GPU (the GPU the Allocate answer told the container to use) never exceeds the GPU.  Checked once
+kubelet runs on a GPU (the GPU the Allocate answer told the container to use) never exceeds the GPU -- and the
+annotations never promise a GPU past it (an exchange in flight read as its protocol defines it, as
+tests/test_chaos.py reads it).  Checked once
 the schedule is drained with only fair system actions left (convergence): every running pod is annotated with the
 GPU its container runs on, no exchange hold is left, the extender's ledger equals the annotations with nothing
 unaccounted, no Allocate failed, and every pod bound to the node was admitted.
@@ -44,7 +46,6 @@ import logging
 import random
 import sys
 import time as _time
-import types
 
 from gpushare_scheduler_extender_amd.core.engine import new_engine
 from gpushare_scheduler_extender_amd.deviceplugin import api as dpapi
@@ -208,29 +209,14 @@ class _PodResources:
         pass
 
 
-async def _finish_holds_r5(self):
-    """reconcile.py _finish_holds before this harness found seed 25 of swap-graceful: step 2 of an interrupted
-    exchange re-applied from the hold's payload whatever the partner's fields are now -- a partner served an Allocate
-    since then got ASSIGNED=false again (mutation ``stale_hold``)."""
-    for p in [p for p in self.state.pods.values() if p.hold_idx >= 0 or p.hold_partner]:
-        try:
-            want = json.loads(p.hold_partner) if p.hold_partner else {}
-        except ValueError:
-            want = {}
-        q = self.state.pods.get(want.get("uid", ""))
-        if q is not None and reconcile_mod.fields(q) != {k: want.get(k) for k in ("idx", "assigned", "cu_mask")}:
-            if not await self._patch(q, self._ann(want), partner=p.uid):
-                continue
-        await self._clear_hold(self.state.pods.get(p.uid, p))
-
-
 # Known bug classes, re-introduced on demand so the tests can show the harness finds each:
 MUTATIONS = {
     "free_on_deleting": "the extender frees a pod's share at its deletionTimestamp (round 5's controller)",
     "no_guard": "the device plugin starts containers without its physical guard",
     "no_publication": "the device plugin never tells the extender its unaccounted use",
     "no_linger": "a force-deleted pod's share is freed as soon as kubelet stops listing it",
-    "stale_hold": "an interrupted exchange's step 2 re-applies a stale payload (fixed in round 6)",
+    "no_stand_in": "no unstarted pod stands in for a swapped partner that is gone (round 5's fix)",
+    "serve_partner": "the matcher serves the partner of an unfinished exchange its old fields (fixed in round 6)",
     "fail_on_gone": "an Allocate whose matched pod was deleted meanwhile fails kubelet's pod (fixed in round 6)",
 }
 
@@ -371,8 +357,10 @@ class Harness:
                 st._recs.pop(uid, None)
                 st._flush()
             st.forget = _forget
-        if "stale_hold" in self.muts:
-            pl.reconciler._finish_holds = types.MethodType(_finish_holds_r5, pl.reconciler)
+        if "no_stand_in" in self.muts:
+            pl.reconciler._stand_in_partner = lambda dev, p, started: None
+        if "serve_partner" in self.muts:
+            pl.state.core.set_skip_partners(False)
         self.plugin = pl
         self.all_ids = [i for d in sorted(pl.ids) for i in pl.ids[d]]
         for s in self.sc.sizes:
@@ -650,7 +638,32 @@ class Harness:
         self.restart_extender()
 
     # ------------------------------------------------------------ invariants
+    def committed(self) -> list[int]:
+        """Per-GPU units the annotations promise (bound, non-terminal pods), an exchange in flight read as its
+        protocol defines it: until the partner has taken P's old fields P's committed GPU is its hold-idx."""
+        pods = [p for p in self.api.list("pods") if (p.get("spec") or {}).get("nodeName") == NODE and not _terminal(p)]
+        by_uid = {p["metadata"]["uid"]: p for p in pods}
+        used = [0] * self.sc.gpus
+        for p in pods:
+            a = p["metadata"].get("annotations") or {}
+            try:
+                dev = int(a.get(PROFILE.annotation_idx, "-1"))
+            except ValueError:
+                dev = -1
+            if POD_HOLD_IDX_ANNOTATION in a:
+                want = json.loads(a.get(POD_HOLD_PARTNER_ANNOTATION) or "{}")
+                q = by_uid.get(want.get("uid", ""))
+                qa = (q or {}).get("metadata", {}).get("annotations") or {}
+                if q is not None and qa.get(PROFILE.annotation_idx) != str(want.get("idx")):
+                    dev = int(a[POD_HOLD_IDX_ANNOTATION])
+            if 0 <= dev < self.sc.gpus:
+                used[dev] += _request(p)
+        return used
+
     def check_safety(self):
+        for d, u in enumerate(self.committed()):
+            if u > self.sc.gpu_units:
+                raise Violation(f"the annotations promise GPU {d} {u} > {self.sc.gpu_units} units")
         used = [0] * self.sc.gpus
         for c in self.active.values():
             used[c.dev] += c.units

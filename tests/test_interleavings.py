@@ -45,11 +45,11 @@ def test_the_physical_guard_and_lingering_are_exercised():
 
 
 @pytest.mark.parametrize("mutation,scenario,what", [
-    ("stale_hold", "swap-graceful", "annotated"),
+    ("serve_partner", "swap-graceful", "annotated"),
     ("fail_on_gone", "swap-force", "Allocate failed"),
     ("no_linger", "force-grace", "runs"),
     ("no_guard", "force-grace", "runs"),
-    ("free_on_deleting", "slow-stop", "Allocate failed"),
+    ("free_on_deleting", "slow-stop", "promise"),
 ])
 def test_the_harness_finds_each_known_bug_class(mutation, scenario, what):
     found = None
