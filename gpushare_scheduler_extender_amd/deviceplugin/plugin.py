@@ -870,7 +870,9 @@ class GpuSharePlugin:
         while True:
             await self._reconcile_now(urgent=True)
             rec = self.state.fresh(self.state.pods.get(rec.uid))
-            if rec is None or rec.assigned != "false" or not rec.pending or rec.uid in self.state.inflight:
+            if (rec is None or rec.assigned != "false" or not rec.pending or rec.uid in self.state.inflight
+                    or self.reconciler.exchange_pending(rec)):
+                # served meanwhile, or an exchange the pass began is about to give it other fields: re-match
                 return None
             used = self._physical_used(rec.dev)
             if used + units <= self.units.get(rec.dev, 0):
@@ -890,9 +892,10 @@ class GpuSharePlugin:
                     try:
                         return await self.move_unstarted(rec, best)
                     except ApiError as e:
-                        # the extender's ledger disagrees (a bind or publication this view has not seen): look again
+                        # the extender's ledger disagrees (a bind or publication this view has not seen), or its
+                        # apiserver write failed: look again
                         refused = e
-                        if not e.conflict or now >= gone_deadline:
+                        if not e.transient or now >= gone_deadline:
                             raise AllocateError(f"moving {rec.key} off a physically full GPU failed: {e}") from e
                 elif now >= gone_deadline or not stopping:
                     break

@@ -55,6 +55,16 @@ def fields(p: PodRec) -> dict:
     return {"idx": p.dev, "assigned": p.assigned, "cu_mask": p.cu_mask}
 
 
+def _took(q: PodRec, want: dict) -> bool:
+    """Q carries the fields an exchange's step 2 gives it (``want``, the hold's partner payload), or was served an
+    Allocate on them since (ASSIGNED=true where the payload said false)."""
+    f = fields(q)
+    if f == {k: want.get(k) for k in ("idx", "assigned", "cu_mask")}:
+        return True
+    return (f["idx"] == want.get("idx") and (f["cu_mask"] or "") == (want.get("cu_mask") or "")
+            and f["assigned"] == "true" and want.get("assigned") == "false")
+
+
 class _Held:
     """What kubelet's container of a pod physically got (the plugin's physical account, keyed by kubelet's IDs)."""
 
@@ -454,12 +464,28 @@ class Reconciler:
             except ValueError:
                 want = {}
             # (Q cannot have been served an Allocate with its old fields meanwhile: the matcher skips the partner of an
-            # unfinished exchange, AllocState::candidates -- tests/interleave.py swap-graceful seed 25)
+            # unfinished exchange, AllocState::candidates -- tests/interleave.py swap-graceful seed 25 -- and so does
+            # the physical guard for a pod it matched before the exchange began.  It may have been served with the
+            # fields step 2 gave it: the guard's own pass ran both steps -- batch-faults seed 1914 -- and the
+            # container runs where they say)
             q = self.state.pods.get(want.get("uid", ""))
-            if q is not None and fields(q) != {k: want.get(k) for k in ("idx", "assigned", "cu_mask")}:
+            if q is not None and not _took(q, want):
                 if not await self._patch(q, self._ann(want), partner=p.uid):
                     continue
             await self._clear_hold(self.state.pods.get(p.uid, p))
+
+    def exchange_pending(self, q: PodRec) -> bool:
+        """Q is the partner of an unfinished exchange whose step 2 has not landed: its fields are about to change."""
+        for p in self.state.pods.values():
+            if not p.hold_partner:
+                continue
+            try:
+                want = json.loads(p.hold_partner)
+            except ValueError:
+                continue
+            if want.get("uid") == q.uid and not _took(q, want):
+                return True
+        return False
 
     # ------------------------------------------------------------ loop
     async def run(self):

@@ -83,6 +83,9 @@ class Scenario:
     # kubelet lists a force-deleted pod's container until it has stopped (the node agent stand-in), and the plugin
     # runs GSX_PLUGIN_FORCE_DELETE=report; False: real kubelet (drops it at once) and the default "grace" policy
     truthful: bool = False
+    # share of apiserver writes (the plugin's PATCHes, the extender's move PATCH) answered 409 or 500 (the chaos rows'
+    # injected faults), decided by the schedule's seed
+    faults: float = 0.0
     max_steps: int = 4000
 
 
@@ -101,6 +104,11 @@ SCENARIOS = {s.name: s for s in (
     # the same against a kubelet whose report is the truth, with the plugin taking it as such (bench.py's setting)
     Scenario("force-report", sizes=(8, 8, 8, 8), extra=(8, 8), deletes=2, grace="force", passes=14,
              stop_after=10 ** 9, truthful=True),
+    # the chaos rows' apiserver: writes refused (409) or failing (500) at random, sizes mixed, deletes of both kinds
+    Scenario("faults", sizes=(8, 8, 4, 4, 8), extra=(8, 4), deletes=2, grace="mixed", passes=16, faults=0.2),
+    # a chaos row's node in small: four GPUs, three sizes, a full first batch, deletes and new pods racing it
+    Scenario("batch-faults", sizes=(8, 16, 8, 16, 8, 8, 16, 8, 4, 4), extra=(8, 16, 4), deletes=3, grace="mixed",
+             gpus=4, gpu_units=24, passes=20, faults=0.15, max_steps=8000),
 )}
 
 
@@ -171,6 +179,9 @@ class _Client:
 
     async def patch(self, kind, name, patch, ns=None, sub=None, **_):
         await self.h.point(f"api PATCH {name}")
+        f = self.h.fault()
+        if f:
+            raise ApiError(f, "Conflict" if f == 409 else "InternalError", "injected")
         try:
             return self.h.api.patch(kind, ns or "default", name, patch, sub or "")
         except HTTPError as e:
@@ -216,7 +227,9 @@ MUTATIONS = {
     "no_publication": "the device plugin never tells the extender its unaccounted use",
     "no_linger": "a force-deleted pod's share is freed as soon as kubelet stops listing it",
     "no_stand_in": "no unstarted pod stands in for a swapped partner that is gone (round 5's fix)",
-    "serve_partner": "the matcher serves the partner of an unfinished exchange its old fields (fixed in round 6)",
+    "serve_partner": "the matcher serves the partner of an unfinished exchange (fixed in round 6)",
+    "strict_finish": "finishing an exchange re-applies step 2 over a partner served on the fields it gave it since "
+                     "(fixed in round 6; with serve_partner, the bug the harness first found)",
     "fail_on_gone": "an Allocate whose matched pod was deleted meanwhile fails kubelet's pod (fixed in round 6)",
 }
 
@@ -272,6 +285,14 @@ class Harness:
         self.n_pods = 0
         self.steps = 0
         self.max_used = [0] * scenario.gpus
+        self.faults = 0
+
+    def fault(self) -> int:
+        """An injected apiserver answer for this write (409 or 500), or 0."""
+        if self.sc.faults and self.rng.random() < self.sc.faults:
+            self.faults += 1
+            return 409 if self.rng.random() < 0.6 else 500
+        return 0
 
     # ------------------------------------------------------------ gates
     async def point(self, label: str, wake: float | None = None):
@@ -361,6 +382,9 @@ class Harness:
             pl.reconciler._stand_in_partner = lambda dev, p, started: None
         if "serve_partner" in self.muts:
             pl.state.core.set_skip_partners(False)
+        if "strict_finish" in self.muts:
+            reconcile_mod._took = lambda q, want: reconcile_mod.fields(q) == {
+                k: want.get(k) for k in ("idx", "assigned", "cu_mask")}
         self.plugin = pl
         self.all_ids = [i for d in sorted(pl.ids) for i in pl.ids[d]]
         for s in self.sc.sizes:
@@ -390,6 +414,10 @@ class Harness:
         if rc != 0:
             return Resp(404 if rc == 1 else 409, {"Error": why})
         await self.point(f"ext move PATCH {body['name']}")
+        f = self.fault()
+        if f:
+            eng.end_move(body["uid"], False)
+            return Resp(f, {"Error": f"apiserver {f} (injected)"})
         patch = {"metadata": {"resourceVersion": body["resourceVersion"],
                               "annotations": {PROFILE.annotation_idx: str(to), **ann}}}
         try:
@@ -539,6 +567,8 @@ class Harness:
     async def pass_task(self):
         try:
             await self.plugin.reconciler.run_once()
+        except ApiError:
+            pass  # the reconciler's loop outlives a pass an apiserver error cut short (Reconciler.run)
         finally:
             self.pass_running = False
 
@@ -793,7 +823,8 @@ def run_one(scenario: str | Scenario, seed: int, mutation: str = "", tmpdir: str
     """One schedule.  Raises Violation (with the trace attached) if an invariant breaks."""
     sc = SCENARIOS[scenario] if isinstance(scenario, str) else scenario
     h = Harness(sc, seed, mutation)
-    saved = (plugin_mod.time, reconcile_mod.time, state_mod.time, asyncio.sleep, ApiError.not_found)
+    saved = (plugin_mod.time, reconcile_mod.time, state_mod.time, asyncio.sleep, ApiError.not_found,
+             reconcile_mod._took)
     plugin_mod.time = reconcile_mod.time = state_mod.time = h.clock
     if "fail_on_gone" in h.muts:
         ApiError.not_found = property(lambda self: False)
@@ -819,14 +850,15 @@ def run_one(scenario: str | Scenario, seed: int, mutation: str = "", tmpdir: str
             loop.run_until_complete(_cancel())
             loop.close()
     finally:
-        plugin_mod.time, reconcile_mod.time, state_mod.time, asyncio.sleep, ApiError.not_found = saved
+        (plugin_mod.time, reconcile_mod.time, state_mod.time, asyncio.sleep, ApiError.not_found,
+         reconcile_mod._took) = saved
         lg.setLevel(level)
     return h
 
 
 def sweep(scenario: str, seeds, mutation: str = "") -> dict:
     out = {"scenario": scenario, "mutation": mutation, "runs": 0, "violations": [], "steps": 0, "swaps": 0,
-           "guards": 0, "holds": 0, "moves": 0, "guard_refusals": 0, "lingered": 0}
+           "guards": 0, "holds": 0, "moves": 0, "guard_refusals": 0, "lingered": 0, "faults": 0}
     for s in seeds:
         out["runs"] += 1
         try:
@@ -842,6 +874,7 @@ def sweep(scenario: str, seeds, mutation: str = "") -> dict:
         out["moves"] += h.plugin.stats.get("moves", 0)
         out["guard_refusals"] += len(h.refused)
         out["lingered"] += h.lingered
+        out["faults"] += h.faults
     return out
 
 

@@ -7,9 +7,11 @@ is checked step by step (no GPU runs past its capacity) and once drained (annota
 ledger = the annotations, nothing unaccounted, no Allocate failed, every bound pod admitted).
 
 The mutation tests re-introduce known bug classes -- round 5's controller freeing a terminating pod's share, no
-physical guard, no lingering of force-deleted pods' shares, and the two bugs this harness found in round 6 (a stale
-exchange payload re-applied to a pod served since; an Allocate failing kubelet's pod because the pod it matched was
-deleted meanwhile) -- and require the harness to find each within a few hundred schedules.
+physical guard, no lingering of force-deleted pods' shares, and bugs this harness found in round 6 (an exchange's
+step 2 re-applied over a partner served since -- two defences now, the matcher skipping partners and the finish
+accepting a partner served on the fields step 2 gave it, removed together; an Allocate failing kubelet's pod because
+the pod it matched was deleted meanwhile) -- and require the harness to find each within a few hundred schedules.
+The schedules that found bugs are replayed as regressions.
 
 ``GSX_INTERLEAVE_SEEDS`` (default 300) sets schedules per scenario; the sweep logged under profiles/r06_interleave
 ran 10000 per scenario.
@@ -38,6 +40,15 @@ def test_a_schedule_replays_from_its_seed():
     assert a.trace == b.trace and a.steps == b.steps > 50
 
 
+@pytest.mark.parametrize("scenario,seed", [
+    ("batch-faults", 1914),   # a partner served on the fields step 2 gave it, then step 2 re-applied (ASSIGNED=false)
+    ("batch-faults", 15378),  # the guard's move failing kubelet's pod on an apiserver 500
+    ("swap-graceful", 25),    # the first bug the harness found: a stale exchange payload over a served pod
+])
+def test_the_schedules_that_found_bugs_stay_clean(scenario, seed):
+    il.run_one(scenario, seed)
+
+
 def test_the_physical_guard_and_lingering_are_exercised():
     r = il.sweep("force-grace", range(200))
     assert not r["violations"], r["violations"][:2]
@@ -45,7 +56,7 @@ def test_the_physical_guard_and_lingering_are_exercised():
 
 
 @pytest.mark.parametrize("mutation,scenario,what", [
-    ("serve_partner", "swap-graceful", "annotated"),
+    ("serve_partner,strict_finish", "swap-graceful", "annotated"),
     ("fail_on_gone", "swap-force", "Allocate failed"),
     ("no_linger", "force-grace", "runs"),
     ("no_guard", "force-grace", "runs"),

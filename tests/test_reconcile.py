@@ -445,6 +445,9 @@ def test_physical_guard_waits_for_a_deleted_pods_container_when_no_gpu_has_room(
             def busy(self):
                 return set()
 
+            def exchange_pending(self, q):
+                return False
+
         async def _no_pass(urgent=False):
             return None
 
