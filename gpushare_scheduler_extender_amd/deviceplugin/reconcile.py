@@ -317,7 +317,11 @@ class Reconciler:
             # its deletion freed r.dev in the extender's ledger although P's container runs there.  An unstarted
             # pod of P's size the extender has since placed on r.dev is the natural partner: exchanging with it
             # keeps the annotations' per-GPU sums exactly as they are (it starts on P's old GPU instead)
-            q = self._stand_in_partner(r.dev, p, started)
+            # (P's own allocation served to another container -- a chain -- relabels that record to Q: only a Q of
+            # P's size keeps every record's size its pod's, else the holder is left unreconcilable and Q, marked
+            # ASSIGNED for it, never an Allocate candidate -- box chaos seed 4723)
+            chain = any(o.uid == p.uid and o.aid != r.aid for o in self.state.records.values())
+            q = self._stand_in_partner(r.dev, p, started, same_size=chain)
             if q is None:
                 await self._make_room(r.dev, p, started)
             else:
@@ -376,11 +380,12 @@ class Reconciler:
             cands.append(q)
         return min(cands, key=lambda q: q.order) if cands else None
 
-    def _stand_in_partner(self, dev: int, p: PodRec, started: set) -> PodRec | None:
+    def _stand_in_partner(self, dev: int, p: PodRec, started: set, same_size: bool = False) -> PodRec | None:
         """An unstarted pod Q the extender has placed on ``dev`` (where P's container runs) to exchange GPUs with P:
         Q takes P's annotated GPU, which P's container never used.  Equal-size first (the exchange keeps every
         GPU's sum); else the largest Q with which both GPUs fit after the exchange -- P's phantom share on its
-        annotated GPU is exactly the room Q needs there, and the extender checks the same final state."""
+        annotated GPU is exactly the room Q needs there, and the extender checks the same final state.  ``same_size``: only
+        an equal-size Q."""
         recs = self.state.records.values()
         taken = {r.holder for r in recs} | {r.uid for r in recs} | self.busy()
         cands = [q for q in self.state.pods.values()
@@ -389,7 +394,7 @@ class Reconciler:
         same = [q for q in cands if q.request == p.request]
         if same:
             return min(same, key=lambda q: q.order)
-        if p.dev < 0 or p.dev == dev:
+        if same_size or p.dev < 0 or p.dev == dev:
             return None
         plugin = self.plugin
         cap_to, cap_from = plugin.units.get(dev, 0), plugin.units.get(p.dev, 0)

@@ -858,7 +858,8 @@ def run_one(scenario: str | Scenario, seed: int, mutation: str = "", tmpdir: str
 
 def sweep(scenario: str, seeds, mutation: str = "") -> dict:
     out = {"scenario": scenario, "mutation": mutation, "runs": 0, "violations": [], "steps": 0, "swaps": 0,
-           "guards": 0, "holds": 0, "moves": 0, "guard_refusals": 0, "lingered": 0, "faults": 0}
+           "guards": 0, "holds": 0, "moves": 0, "guard_refusals": 0, "lingered": 0, "faults": 0,
+           "unequal_partners": 0, "unreconcilable": 0}
     for s in seeds:
         out["runs"] += 1
         try:
@@ -875,6 +876,8 @@ def sweep(scenario: str, seeds, mutation: str = "") -> dict:
         out["guard_refusals"] += len(h.refused)
         out["lingered"] += h.lingered
         out["faults"] += h.faults
+        out["unequal_partners"] += rs.get("unequal_partners", 0)
+        out["unreconcilable"] += rs.get("unreconcilable", 0)
     return out
 
 

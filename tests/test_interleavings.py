@@ -27,11 +27,14 @@ SEEDS = int(os.environ.get("GSX_INTERLEAVE_SEEDS", "300"))
 
 @pytest.mark.parametrize("scenario", sorted(il.SCENARIOS))
 def test_every_schedule_keeps_the_gpus_within_capacity_and_converges(scenario):
-    r = il.sweep(scenario, range(SEEDS))
+    n = SEEDS // 3 if scenario == "batch-faults" else SEEDS  # (four times the steps of the others)
+    r = il.sweep(scenario, range(n))
     assert not r["violations"], "\n".join(r["violations"][:3])
-    assert r["runs"] == SEEDS
+    assert r["runs"] == n
     # the schedules exercise the protocol, not an idle node
-    assert r["swaps"] > SEEDS // 4 and r["holds"] > 0 and r["moves"] > 0, r
+    assert r["swaps"] > n // 4 and r["holds"] > 0 and r["moves"] > 0, r
+    if il.SCENARIOS[scenario].faults:
+        assert r["faults"] > n, r
 
 
 def test_a_schedule_replays_from_its_seed():
