@@ -145,8 +145,11 @@ def test_chaos_whole_stack_converges_without_overcommit(seed, agent, bind_mode, 
                 if settled and ledger == used:
                     assert all(u <= 96 for u in used), used
                     break
-                assert time.monotonic() < deadline, {"used": used, "ledger": ledger, "pending": pending,
-                                                     "running": len(running), "bound": len(bound)}
+                if time.monotonic() >= deadline:  # (a string: pytest shortens a dict message)
+                    raise AssertionError(json.dumps({"used": used, "ledger": ledger, "pending": pending,
+                                                     "running": len(running), "bound": len(bound), "holds": holds,
+                                                     "node": insp["nodes"][0], "plugin": await _plugin_state(cl)},
+                                                    default=str))
                 await asyncio.sleep(0.05)
             # every running container is on the GPU its annotation names (physical == *_IDX), holds cleared
             drift, drifted = await cl.physical_drift(sorted(live), timeout=15)
