@@ -463,7 +463,12 @@ def open_loop(a, api_url, api_batch, E, profile, inspect_used, sched_stats, agen
         deadline = time.perf_counter() + 60
         while sum(n["usedGPU"] for n in inspect_used()["nodes"]) != 0:
             if time.perf_counter() > deadline:
-                raise TimeoutError("open loop: ledger did not drain")
+                # what the ledger still charges (pods, and the unaccounted use the plugin published), and what the
+                # node agent and the plugin hold
+                na = agent_stats() if agent_stats else {}
+                pg = _plugin_debug(E, (na or {}).get("plugin_debug"))
+                raise TimeoutError("open loop: ledger did not drain: " + json.dumps(
+                    {"inspect": inspect_used(), "node_agent": na, "plugin": pg}, default=str)[:6000])
             time.sleep(0.005)
 
     k = 0
@@ -612,6 +617,7 @@ def _plugin_debug(E, url: str | None) -> dict | None:
                                            "last_slow_reason", "handler_us", "allocate_phases_us", "lock_wait",
                                            "wait_ms", "commits_gone")},
             "stats": d.get("stats"), "reconcile": d.get("reconcile"),
+            "physical": d.get("physical"), "held": d.get("held"), "records": d.get("records"),
             # mean seconds per native fast-path Allocate: match, isolation files, record + answer (handler)
             "timing": {k: (v / max(1, (d.get("timing") or {}).get("n", 0)) if k != "n" else v)
                        for k, v in (d.get("timing") or {}).items() if not k.startswith("preferred")}}

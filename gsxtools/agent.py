@@ -241,9 +241,21 @@ class NodeAgent:
         t.add_done_callback(lambda _t, uid=uid: self.stopping.pop(uid, None))
 
     # ------------------------------------------------------------ device plugin calls (kubelet's device manager)
-    async def _allocate_grpc(self, uid: str, units: int) -> _Alloc:
-        free = sorted(set(self.all_ids) - {i for ids in self.used_ids.values() for i in ids}
+    def _free_ids(self) -> list[str]:
+        return sorted(set(self.all_ids) - {i for ids in self.used_ids.values() for i in ids}
                       - {i for _, ids in self.stopping.values() for i in ids})
+
+    async def _allocate_grpc(self, uid: str, units: int) -> _Alloc:
+        free = self._free_ids()
+        # containers of deleted pods still stopping hold the IDs this pod needs: the admission waits for their
+        # release (as the node agent does: nodeagent.cc, stopping_), bounded
+        deadline = time.monotonic() + 30.0
+        while len(free) < units and self.stopping and time.monotonic() < deadline:
+            self.stats["waited_for_stopping"] = self.stats.get("waited_for_stopping", 0) + 1
+            if self._releasing:
+                await asyncio.wait(list(self._releasing), timeout=0.05)
+            await asyncio.sleep(0.001)  # (the release's done callbacks drop its stopping entry)
+            free = self._free_ids()
         if len(free) < units:
             raise AllocateError(f"kubelet: {units} {self.profile.resource} requested, {len(free)} IDs free")
         t0 = time.perf_counter()

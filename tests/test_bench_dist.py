@@ -69,7 +69,9 @@ def test_bench_two_ranks_gloo(agent, extra):
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "3",
            "--warmup", "1", "--devices", "fake", "--agent", agent, "--sweep", "0", *extra]
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    # (the ranks' own errors come before torchrun's summary at the end of stderr)
+    assert r.returncode == 0, (r.stdout[-2000:], [ln for ln in r.stderr.splitlines() if "rror" in ln][-30:],
+                               r.stderr[-3000:])
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 8
     # 4 x 64 GiB on each of the two devices: binpack fills GPU0 before GPU1 ... and both end full
