@@ -227,6 +227,8 @@ class _ServerProtocol(asyncio.Protocol):
                 t = asyncio.get_running_loop().create_task(self._finish(res, req, keep))
                 self.server.tasks.add(t)
                 t.add_done_callback(self.server.tasks.discard)
+                # a task cancelled before its first step (the server closing) never awaits the handler's coroutine
+                t.add_done_callback(lambda _t, c=res: c.close())
                 return
             self._write(res, keep)
 

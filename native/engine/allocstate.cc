@@ -618,7 +618,7 @@ int64_t AllocState::gone_held(int64_t dev) const {
   int64_t n = 0;
   for (const auto& kv : held_) {
     const Held& h = kv.second;
-    if (h.dev == dev && h.listed && h.gone_reports >= 2) n += h.units;
+    if (h.dev == dev && h.listed && h.gone_reports >= 2 && last_prune_ - h.gone_since >= kGoneHeldMinS) n += h.units;
   }
   return n;
 }
@@ -707,10 +707,12 @@ size_t AllocState::prune_held(const std::vector<std::vector<std::string>>& liste
     listed.insert(id_key(ids));
   }
   size_t n = 0;
+  last_prune_ = asked;
   for (auto it = held_.begin(); it != held_.end();) {
     auto cur = it++;
     cur->second.listed = listed.count(cur->first) != 0;
     cur->second.gone_reports = cur->second.listed && holder_gone(cur->second) ? cur->second.gone_reports + 1 : 0;
+    if (cur->second.gone_reports == 1) cur->second.gone_since = asked;
     if (!cur->second.listed && asked - cur->second.t > grace) {
       const Held& h = cur->second;
       if (!h.owner.empty() && pods_.count(h.owner)) continue;  // live here: see the header

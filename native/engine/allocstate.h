@@ -151,9 +151,12 @@ class AllocState {
   bool linger_enabled() const { return linger_on_; }
   int64_t lingering(int64_t dev) const;  // units of force-deleted pods' containers still counted on `dev`
   // units kubelet still lists on `dev` for pods this view no longer has -- deleted pods' containers that have not
-  // stopped yet, the extender freed their share with the objects -- once two reports in a row have listed them
-  // after the pod went (a container that stops at once is never published: the physical guard still counts it)
+  // stopped yet, the extender freed their share with the objects -- once two reports in a row, kGoneHeldMinS apart
+  // at least, have listed them after the pod went (a container that stops within that is never published: the
+  // physical guard still counts it.  Published and withdrawn a pass later, a fast stop held the extender's room for
+  // a poll interval -- a 10 ms wave in the headline bench on MI355X)
   int64_t gone_held(int64_t dev) const;
+  static constexpr double kGoneHeldMinS = 0.05;
   size_t linger_count() const { return linger_.size(); }
   void tombstone(const std::string& uid);
   bool is_tombstoned(const std::string& uid) const { return gone_.count(uid) != 0; }
@@ -268,7 +271,9 @@ class AllocState {
     std::string owner;    // the pod kubelet last reported holding the IDs (set_owner)
     bool listed = false;  // kubelet's last report listed the IDs (prune_held)
     int gone_reports = 0; // reports in a row that listed them after their holder had gone (holder_gone)
+    double gone_since = 0;  // when the first of those reports was asked for
   };
+  double last_prune_ = 0;  // when the last report prune_held saw was asked for
   bool holder_gone(const Held& h) const;
   struct Linger {
     int64_t dev = -1, units = 0;

@@ -491,7 +491,9 @@ class FakeApiServer:
         """Request accounting + injected latency (what an aiohttp middleware did)."""
         async def slow(request):
             await asyncio.sleep(self.faults.latency_ms / 1000.0)
-            return await handler(request) if asyncio.iscoroutinefunction(handler) else handler(request)
+            res = handler(request)
+            # (a plain handler may hand back a coroutine too: the list handler's watch stream)
+            return await res if asyncio.iscoroutine(res) else res
 
         def h(request):
             self.counts[request.method] += 1

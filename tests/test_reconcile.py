@@ -369,7 +369,7 @@ def test_unaccounted_use_is_a_live_holder_on_another_gpu_and_reaches_the_extende
             pod("P", 0)
             st.set_owner("aQ", "~default/gone")  # kubelet lists it for a pod that is gone: its container is stopping
             st.core.prune_held([["g1-_-0"]], 0.0, 0.0)
-            st.core.prune_held([["g1-_-0"]], 0.0, 0.0)
+            st.core.prune_held([["g1-_-0"]], 1.0, 0.0)
             assert plugin.unaccounted() == [0, 4]  # charged until kubelet stops listing it (the extender freed it)
             st.core.prune_held([], 1e12, 0.0)
             assert plugin.unaccounted() is None
