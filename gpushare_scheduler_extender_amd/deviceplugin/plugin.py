@@ -105,6 +105,8 @@ GUARD_WAIT_S = float(os.environ.get("GSX_PLUGIN_GUARD_WAIT_S", "5.0"))
 # admission of every other pod of the node waits behind this call (30 s, the default termination grace, let the
 # kubelet-restart chaos rows time out with admissions queued: 1 of 1900 seeds)
 GUARD_GONE_WAIT_S = float(os.environ.get("GSX_PLUGIN_GUARD_GONE_WAIT_S", "10.0"))
+# how long an Allocate that found no candidate waits for an exchange that is about to make one (allocate_container)
+MISS_EXCHANGE_WAIT_S = float(os.environ.get("GSX_PLUGIN_MISS_EXCHANGE_WAIT_S", "10.0"))
 # A pod deleted outright (a force delete) vanishes from kubelet's PodResources at once while its containers get their
 # termination grace.  "grace" (default, for kubelet): what they hold stays counted -- and published to the extender --
 # until spec.terminationGracePeriodSeconds + 2 s have passed (AllocState::deleted).  "report": kubelet's report is
@@ -747,6 +749,16 @@ class GpuSharePlugin:
                     if rec is not None:
                         break
                     await asyncio.sleep(0.02 * (k + 1))
+                # a pod of this size an exchange is about to make a candidate again: its hold is cleared once the
+                # extender's informer has seen the exchange land, and a loaded extender's informer lags by seconds
+                # (kubelet-restart chaos rows on MI355X: the 0.7 s above ran out).  Waiting fails no pod; bounded,
+                # since kubelet admits serially
+                deadline = time.monotonic() + MISS_EXCHANGE_WAIT_S
+                while rec is None and time.monotonic() < deadline and self._exchange_due(units):
+                    self.stats["miss_exchange_waits"] = self.stats.get("miss_exchange_waits", 0) + 1
+                    await asyncio.sleep(0.1)
+                    await self._reconcile_now(urgent=True)
+                    rec, whole = self.state.match(units)
             if rec is None:
                 keys = {p.uid: p.key for p in self.state.pods.values()}
                 recs = self.state.records.values()
@@ -817,6 +829,16 @@ class GpuSharePlugin:
             self._record(rec, ids, units, alloc)
             return rec, alloc
         raise AllocateError("unreachable")
+
+    def _exchange_due(self, units: int) -> bool:
+        """Some unstarted pod requesting ``units`` is in an unfinished exchange, or another pod's container holds the
+        allocation built for it (an exchange the next pass makes): it will be an Allocate candidate again."""
+        busy = self.reconciler.busy() if self.reconciler is not None else set()
+        pods = [p for p in self.state.pods.values() if p.request == units and p.pending and not p.complete]
+        if any(p.uid in busy for p in pods):
+            return True
+        held_for = {r.uid for r in self.state.records.values() if r.holder and r.holder != r.uid}
+        return any(p.uid in held_for and p.assigned == "true" for p in pods)
 
     async def _reconcile_now(self, urgent: bool = False):
         try:

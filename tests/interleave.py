@@ -243,8 +243,12 @@ class Container:
 
 
 class Harness:
-    def __init__(self, scenario: Scenario, seed: int, mutation: str = ""):
+    def __init__(self, scenario: Scenario, seed: int, mutation: str = "", script: dict | None = None):
         self.sc, self.seed, self.mutation = scenario, seed, mutation
+        # systematic mode (``script``, see systematic()): the first enabled action at every step but the steps the
+        # script names, where it takes the one at that index; ``widths`` records how many were enabled at each step
+        self.script = script
+        self.widths: list[int] = []
         self.muts = set(filter(None, mutation.split(",")))
         unknown = self.muts - set(MUTATIONS)
         if unknown:
@@ -761,7 +765,16 @@ class Harness:
                                                           if fr else "?"))
                 raise Violation(f"stuck: actors blocked outside any gate: {where}")
             return False
-        name, fn = acts[self.rng.randrange(len(acts))]
+        self.widths.append(len(acts))
+        if self.script is None:
+            k = self.rng.randrange(len(acts))
+        else:
+            # the default order is a fair one: a sleep ends after the work already due (a delivery, a call's
+            # answer), so an actor sleeping in a loop cannot starve the others but by the script's departures
+            acts.sort(key=lambda a: a[0] == "resume sleep")
+            k = self.script.get(self.steps, 0)
+            k = k if k < len(acts) else 0
+        name, fn = acts[k]
         self.trace.append(name)
         self.steps += 1
         self.clock.t += 0.001
@@ -819,10 +832,11 @@ def _by_uid(api, uid):
     return None
 
 
-def run_one(scenario: str | Scenario, seed: int, mutation: str = "", tmpdir: str = "/tmp/gsx-interleave") -> Harness:
+def run_one(scenario: str | Scenario, seed: int, mutation: str = "", tmpdir: str = "/tmp/gsx-interleave",
+            script: dict | None = None) -> Harness:
     """One schedule.  Raises Violation (with the trace attached) if an invariant breaks."""
     sc = SCENARIOS[scenario] if isinstance(scenario, str) else scenario
-    h = Harness(sc, seed, mutation)
+    h = Harness(sc, seed, mutation, script)
     saved = (plugin_mod.time, reconcile_mod.time, state_mod.time, asyncio.sleep, ApiError.not_found,
              reconcile_mod._took)
     plugin_mod.time = reconcile_mod.time = state_mod.time = h.clock
@@ -837,7 +851,8 @@ def run_one(scenario: str | Scenario, seed: int, mutation: str = "", tmpdir: str
         try:
             loop.run_until_complete(h.run(tmpdir))
         except Violation as e:
-            e.args = (f"[{sc.name} seed {seed}{' ' + mutation if mutation else ''}] {e.args[0]}\n  trace: "
+            e.args = (f"[{sc.name} seed {seed}{' ' + mutation if mutation else ''}"
+                      f"{' script ' + json.dumps(script) if script is not None else ''}] {e.args[0]}\n  trace: "
                       + " | ".join(h.trace[-60:]),)
             raise
         finally:
@@ -881,6 +896,44 @@ def sweep(scenario: str, seeds, mutation: str = "") -> dict:
     return out
 
 
+def systematic(scenario: str, bound: int = 1, window: int = 60, seed: int = 0, mutation: str = "",
+               limit: int | None = None) -> dict:
+    """Every schedule that departs from the default order -- the first enabled action at each step -- at no more than
+    ``bound`` steps (1 or 2) among the first ``window`` (a preemption bound, as CHESS does): small bugs of ordering
+    need few departures, and the bound makes the search exhaustive instead of sampled.  ``seed`` only fixes the
+    other choices (which deletes are force deletes, injected faults)."""
+    out = {"scenario": scenario, "bound": bound, "window": window, "runs": 0, "violations": [], "steps": 0}
+
+    def one(script):
+        out["runs"] += 1
+        try:
+            h = run_one(scenario, seed, mutation, script=script)
+        except Violation as e:
+            out["violations"].append(str(e))
+            return None
+        out["steps"] += h.steps
+        return h
+
+    base = one({})
+    if base is None:
+        return out
+    firsts = [(i, j) for i, n in enumerate(base.widths[:window]) for j in range(1, n)]
+    for i, j in firsts:
+        if limit is not None and out["runs"] >= limit:
+            break
+        h = one({i: j})
+        if bound < 2 or h is None:
+            continue
+        for i2, n2 in enumerate(h.widths[:window]):
+            if i2 <= i:
+                continue
+            for j2 in range(1, n2):
+                if limit is not None and out["runs"] >= limit:
+                    break
+                one({i: j, i2: j2})
+    return out
+
+
 def _seeds(spec: str):
     out = []
     for part in spec.split(","):
@@ -894,7 +947,24 @@ def main(argv=None) -> int:
     ap.add_argument("--scenario", default="all", help=f"one of {sorted(SCENARIOS)} or all")
     ap.add_argument("--seeds", default="0-99")
     ap.add_argument("--mutation", default="", help=f"comma-separated, of {sorted(MUTATIONS)}")
+    ap.add_argument("--systematic", type=int, default=0, metavar="BOUND",
+                    help="instead of seeded random schedules: every schedule departing from the default order at <= "
+                         "BOUND (1 or 2) of the first --window steps")
+    ap.add_argument("--window", type=int, default=60)
     a = ap.parse_args(argv)
+    if a.systematic:
+        bad = 0
+        for n in (sorted(SCENARIOS) if a.scenario == "all" else [a.scenario]):
+            t0 = _time.perf_counter()
+            r = systematic(n, a.systematic, a.window, mutation=a.mutation)
+            r["seconds"] = round(_time.perf_counter() - t0, 1)
+            viol = r.pop("violations")
+            r["violations"] = len(viol)
+            print(json.dumps(r), flush=True)
+            for v in viol[:3]:
+                print("  " + v, flush=True)
+            bad += len(viol)
+        return 1 if bad and not a.mutation else 0
     names = sorted(SCENARIOS) if a.scenario == "all" else [a.scenario]
     bad = 0
     for n in names:
