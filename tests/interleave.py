@@ -31,9 +31,11 @@ GPU its container runs on, no exchange hold is left, the extender's ledger equal
 unaccounted, no Allocate failed, and every pod bound to the node was admitted.
 
 A schedule is a function of (scenario, seed): ``python -m tests.interleave --scenario swap-graceful --seeds 0-999``
-replays or sweeps; a failure prints the step trace.  The ``mutation`` argument re-introduces a known bug class
-(round-5: the extender freeing a terminating pod's share at deletionTimestamp; no physical publication; no physical
-guard) so the tests can show the harness finds it.
+replays or sweeps; a failure prints the step trace.  ``--systematic 1|2`` enumerates instead of sampling: every
+schedule that departs from a fair default order at no more than that many of the first ``--window`` steps (a
+preemption bound, as CHESS does), each replayable from its script of departures.  Scenarios with ``faults`` answer a
+share of the apiserver writes with an injected 409 or 500, as the chaos rows' fake apiserver does.  The ``mutation``
+argument re-introduces a known bug class (MUTATIONS) so the tests can show the harness finds it.
 """
 from __future__ import annotations
 
