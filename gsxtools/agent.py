@@ -617,7 +617,8 @@ async def serve_stats(box: dict, host: str = "127.0.0.1", port: int = 0):
                 "admit_max_ms": round(1e3 * lat[-1], 3) if lat else 0.0, **agent.stats, "native": False,
                 "finalized": agent.finalized,
                 "plugin": ("process" if getattr(agent, "plugin_stats_url", None) else "grpc")
-                if agent.pclient is not None else "inproc"}
+                if agent.pclient is not None else "inproc",
+                "plugin_debug": getattr(agent, "plugin_stats_url", None)}
         n = max(1, agent.timing["n"])
         body["breakdown_ms"] = {k: round(1e3 * v / n, 4) for k, v in agent.timing.items() if k != "n"}
         pstats = pt = prec = None

@@ -148,6 +148,11 @@ def test_chaos_whole_stack_converges_without_overcommit(seed, agent, bind_mode, 
                 if time.monotonic() >= deadline:  # (a string: pytest shortens a dict message)
                     raise AssertionError(json.dumps({"used": used, "ledger": ledger, "pending": pending,
                                                      "running": len(running), "bound": len(bound), "holds": holds,
+                                                     "hold_pods": {n: {k: v for k, v in (p["metadata"].get(
+                                                         "annotations") or {}).items() if "hold" in k or k in (
+                                                         ALIYUN.annotation_idx, ALIYUN.annotation_assigned)}
+                                                         for n, p in bound.items() if POD_HOLD_IDX_ANNOTATION in (
+                                                             p["metadata"].get("annotations") or {})},
                                                      "node": insp["nodes"][0], "plugin": await _plugin_state(cl)},
                                                     default=str))
                 await asyncio.sleep(0.05)
@@ -183,7 +188,7 @@ async def _plugin_state(cl) -> dict:
             d = json.loads(r.body)
         finally:
             await h.close()
-        return {k: d.get(k) for k in ("physical", "held", "records", "cu_free", "reconcile", "grpc")}
+        return {k: d.get(k) for k in ("physical", "held", "records", "cu_free", "reconcile", "grpc", "stats")}
     except Exception as e:  # noqa: BLE001 - diagnostics only
         return {"error": repr(e)}
 
