@@ -105,8 +105,9 @@ GUARD_WAIT_S = float(os.environ.get("GSX_PLUGIN_GUARD_WAIT_S", "5.0"))
 # admission of every other pod of the node waits behind this call (30 s, the default termination grace, let the
 # kubelet-restart chaos rows time out with admissions queued: 1 of 1900 seeds)
 GUARD_GONE_WAIT_S = float(os.environ.get("GSX_PLUGIN_GUARD_GONE_WAIT_S", "10.0"))
-# how long an Allocate that found no candidate waits for an exchange that is about to make one (allocate_container)
-MISS_EXCHANGE_WAIT_S = float(os.environ.get("GSX_PLUGIN_MISS_EXCHANGE_WAIT_S", "10.0"))
+# how long an Allocate that found no candidate waits for an exchange that is about to make one (allocate_container):
+# the whole call stays within the node agent stand-in's 10 s gRPC deadline (past it the pod fails all the same)
+MISS_EXCHANGE_WAIT_S = float(os.environ.get("GSX_PLUGIN_MISS_EXCHANGE_WAIT_S", "5.0"))
 # A pod deleted outright (a force delete) vanishes from kubelet's PodResources at once while its containers get their
 # termination grace.  "grace" (default, for kubelet): what they hold stays counted -- and published to the extender --
 # until spec.terminationGracePeriodSeconds + 2 s have passed (AllocState::deleted).  "report": kubelet's report is
